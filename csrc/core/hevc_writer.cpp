@@ -1,0 +1,614 @@
+// hevc_writer.cpp — HEVC parameter sets and CABAC slice-data writer.
+//
+// Consumes the per-frame decision arrays (FrameData) produced by the analysis stage and
+// emits a Main-profile Annex-B bitstream.  Skip / merge / AMVP syntax is chosen here from
+// the final motion field (the GPU only decides motion vectors and residuals), which keeps
+// the GPU analysis fully parallel while the serial CABAC runs on CPU threads — the
+// MI355X-native split of the reference's single ffmpeg call (reference
+// worker/tasks.py:1532-1586).
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+#include "tv/bitstream.h"
+#include "tv/cabac.h"
+#include "tv/hevc_codec.h"
+
+namespace tv {
+
+const uint8_t kRangeTabLps[64][4] = {
+    {128, 176, 208, 240}, {128, 167, 197, 227}, {128, 158, 187, 216}, {123, 150, 178, 205},
+    {116, 142, 169, 195}, {111, 135, 160, 185}, {105, 128, 152, 175}, {100, 122, 144, 166},
+    {95, 116, 137, 158},  {90, 110, 130, 150},  {85, 104, 123, 142},  {81, 99, 117, 135},
+    {77, 94, 111, 128},   {73, 89, 105, 122},   {69, 85, 100, 116},   {66, 80, 95, 110},
+    {62, 76, 90, 104},    {59, 72, 86, 99},     {56, 69, 81, 94},     {53, 65, 77, 89},
+    {51, 62, 73, 85},     {48, 59, 69, 80},     {46, 56, 66, 76},     {43, 53, 63, 72},
+    {41, 50, 59, 69},     {39, 48, 56, 65},     {37, 45, 54, 62},     {35, 43, 51, 59},
+    {33, 41, 48, 56},     {32, 39, 46, 53},     {30, 37, 43, 50},     {29, 35, 41, 48},
+    {27, 33, 39, 45},     {26, 31, 37, 43},     {24, 30, 35, 41},     {23, 28, 33, 39},
+    {22, 27, 32, 37},     {21, 26, 30, 35},     {20, 24, 29, 33},     {19, 23, 27, 31},
+    {18, 22, 26, 30},     {17, 21, 25, 28},     {16, 20, 23, 27},     {15, 19, 22, 25},
+    {14, 18, 21, 24},     {14, 17, 20, 23},     {13, 16, 19, 22},     {12, 15, 18, 21},
+    {12, 14, 17, 20},     {11, 14, 16, 19},     {11, 13, 15, 18},     {10, 12, 15, 17},
+    {10, 12, 14, 16},     {9, 11, 13, 15},      {9, 11, 12, 14},      {8, 10, 12, 14},
+    {8, 9, 11, 13},       {7, 9, 11, 12},       {7, 9, 10, 12},       {7, 8, 10, 11},
+    {6, 8, 9, 11},        {6, 7, 9, 10},        {6, 7, 8, 9},         {2, 2, 2, 2}};
+const uint8_t kTransIdxLps[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12,
+                                  13, 13, 15, 15, 16, 16, 18, 18, 19, 19, 21, 21, 22, 22, 23, 24,
+                                  24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30, 31, 32, 32, 33,
+                                  33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
+
+int SeqConfig::level_idc() const {
+  const long long ps = (long long)coded_w * coded_h;
+  if (ps <= 2228224) return 123;  // 4.1
+  if (ps <= 8912896) return 153;  // 5.1
+  return 186;                     // 6.2
+}
+
+static void write_ptl(BitWriter& bw, int level) {
+  bw.put(0, 2);  // general_profile_space
+  bw.put(0, 1);  // general_tier_flag
+  bw.put(1, 5);  // general_profile_idc = Main
+  bw.put((1u << 30) | (1u << 29), 32);  // compatibility flags [1] and [2]
+  bw.put(1, 1);  // progressive_source
+  bw.put(0, 1);  // interlaced_source
+  bw.put(0, 1);  // non_packed_constraint
+  bw.put(1, 1);  // frame_only_constraint
+  bw.put(0, 32);
+  bw.put(0, 11);  // 43 reserved zero bits
+  bw.put(0, 1);   // general_inbld_flag (reserved)
+  bw.put((uint32_t)level, 8);
+}
+
+void write_parameter_sets(const SeqConfig& cfg, std::vector<uint8_t>& out) {
+  if ((cfg.width & 1) || (cfg.height & 1)) throw std::runtime_error("odd picture size");
+  {  // VPS
+    BitWriter bw;
+    bw.put(0, 4);       // vps_video_parameter_set_id
+    bw.put(1, 1);       // vps_base_layer_internal_flag
+    bw.put(1, 1);       // vps_base_layer_available_flag
+    bw.put(0, 6);       // vps_max_layers_minus1
+    bw.put(0, 3);       // vps_max_sub_layers_minus1
+    bw.put(1, 1);       // vps_temporal_id_nesting_flag
+    bw.put(0xffff, 16); // reserved
+    write_ptl(bw, cfg.level_idc());
+    bw.put(1, 1);  // vps_sub_layer_ordering_info_present_flag
+    bw.ue(1);      // vps_max_dec_pic_buffering_minus1
+    bw.ue(0);      // vps_max_num_reorder_pics
+    bw.ue(0);      // vps_max_latency_increase_plus1
+    bw.put(0, 6);  // vps_max_layer_id
+    bw.ue(0);      // vps_num_layer_sets_minus1
+    bw.put(0, 1);  // vps_timing_info_present_flag
+    bw.put(0, 1);  // vps_extension_flag
+    bw.trailing_bits();
+    append_nal(out, NAL_VPS, bw.bytes());
+  }
+  {  // SPS
+    BitWriter bw;
+    bw.put(0, 4);  // sps_video_parameter_set_id
+    bw.put(0, 3);  // sps_max_sub_layers_minus1
+    bw.put(1, 1);  // sps_temporal_id_nesting_flag
+    write_ptl(bw, cfg.level_idc());
+    bw.ue(0);  // sps_seq_parameter_set_id
+    bw.ue(1);  // chroma_format_idc 4:2:0
+    bw.ue((uint32_t)cfg.coded_w);
+    bw.ue((uint32_t)cfg.coded_h);
+    const bool crop = cfg.coded_w != cfg.width || cfg.coded_h != cfg.height;
+    bw.put(crop ? 1 : 0, 1);
+    if (crop) {
+      bw.ue(0);
+      bw.ue((uint32_t)(cfg.coded_w - cfg.width) / 2);
+      bw.ue(0);
+      bw.ue((uint32_t)(cfg.coded_h - cfg.height) / 2);
+    }
+    bw.ue(0);  // bit_depth_luma_minus8
+    bw.ue(0);  // bit_depth_chroma_minus8
+    bw.ue(4);  // log2_max_pic_order_cnt_lsb_minus4 -> 8 bits
+    bw.put(1, 1);  // sps_sub_layer_ordering_info_present_flag
+    bw.ue(1);      // sps_max_dec_pic_buffering_minus1
+    bw.ue(0);      // sps_max_num_reorder_pics
+    bw.ue(0);      // sps_max_latency_increase_plus1
+    bw.ue(kMinCbLog2 - 3);           // log2_min_luma_coding_block_size_minus3
+    bw.ue(kCtbLog2 - kMinCbLog2);    // log2_diff_max_min_luma_coding_block_size
+    bw.ue(kMinTbLog2 - 2);           // log2_min_luma_transform_block_size_minus2
+    bw.ue(kMaxTbLog2 - kMinTbLog2);  // log2_diff_max_min_luma_transform_block_size
+    bw.ue(0);      // max_transform_hierarchy_depth_inter
+    bw.ue(0);      // max_transform_hierarchy_depth_intra
+    bw.put(0, 1);  // scaling_list_enabled_flag
+    bw.put(0, 1);  // amp_enabled_flag
+    bw.put(cfg.sao ? 1 : 0, 1);  // sample_adaptive_offset_enabled_flag
+    bw.put(0, 1);  // pcm_enabled_flag
+    bw.ue(1);      // num_short_term_ref_pic_sets
+    // st_ref_pic_set(0): one negative picture at delta -1, used by current
+    bw.ue(1);      // num_negative_pics
+    bw.ue(0);      // num_positive_pics
+    bw.ue(0);      // delta_poc_s0_minus1
+    bw.put(1, 1);  // used_by_curr_pic_s0_flag
+    bw.put(0, 1);  // long_term_ref_pics_present_flag
+    bw.put(0, 1);  // sps_temporal_mvp_enabled_flag
+    bw.put(0, 1);  // strong_intra_smoothing_enabled_flag
+    bw.put(0, 1);  // vui_parameters_present_flag
+    bw.put(0, 1);  // sps_extension_present_flag
+    bw.trailing_bits();
+    append_nal(out, NAL_SPS, bw.bytes());
+  }
+  {  // PPS
+    BitWriter bw;
+    bw.ue(0);      // pps_pic_parameter_set_id
+    bw.ue(0);      // pps_seq_parameter_set_id
+    bw.put(0, 1);  // dependent_slice_segments_enabled_flag
+    bw.put(0, 1);  // output_flag_present_flag
+    bw.put(0, 3);  // num_extra_slice_header_bits
+    bw.put(0, 1);  // sign_data_hiding_enabled_flag
+    bw.put(0, 1);  // cabac_init_present_flag
+    bw.ue(0);      // num_ref_idx_l0_default_active_minus1
+    bw.ue(0);      // num_ref_idx_l1_default_active_minus1
+    bw.se(cfg.qp - 26);  // init_qp_minus26
+    bw.put(0, 1);  // constrained_intra_pred_flag
+    bw.put(0, 1);  // transform_skip_enabled_flag
+    bw.put(0, 1);  // cu_qp_delta_enabled_flag
+    bw.se(0);      // pps_cb_qp_offset
+    bw.se(0);      // pps_cr_qp_offset
+    bw.put(0, 1);  // pps_slice_chroma_qp_offsets_present_flag
+    bw.put(0, 1);  // weighted_pred_flag
+    bw.put(0, 1);  // weighted_bipred_flag
+    bw.put(0, 1);  // transquant_bypass_enabled_flag
+    bw.put(0, 1);  // tiles_enabled_flag
+    bw.put(0, 1);  // entropy_coding_sync_enabled_flag
+    bw.put(0, 1);  // pps_loop_filter_across_slices_enabled_flag
+    bw.put(1, 1);  // deblocking_filter_control_present_flag
+    bw.put(0, 1);  //   deblocking_filter_override_enabled_flag
+    bw.put(cfg.deblock ? 0 : 1, 1);  // pps_deblocking_filter_disabled_flag
+    if (cfg.deblock) {
+      bw.se(0);  // pps_beta_offset_div2
+      bw.se(0);  // pps_tc_offset_div2
+    }
+    bw.put(0, 1);  // pps_scaling_list_data_present_flag
+    bw.put(0, 1);  // lists_modification_present_flag
+    bw.ue(0);      // log2_parallel_merge_level_minus2
+    bw.put(0, 1);  // slice_segment_header_extension_present_flag
+    bw.put(0, 1);  // pps_extension_present_flag
+    bw.trailing_bits();
+    append_nal(out, NAL_PPS, bw.bytes());
+  }
+}
+
+// ------------------------------------ slice data ----------------------------------------
+namespace {
+
+constexpr uint8_t kCtxIdxMap4x4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+constexpr uint8_t kGroupIdx[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+                                   8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
+constexpr uint8_t kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
+
+class SliceWriter {
+ public:
+  SliceWriter(const SeqConfig& cfg, const FrameData& fd, bool islice, BitWriter* bw)
+      : cfg_(cfg), fd_(fd), islice_(islice), enc_(bw) {
+    skip_.assign((size_t)fd.w8 * fd.h8, 0);
+    ctx_.init(islice ? 0 : 1, cfg.qp);
+    enc_.start();
+  }
+
+  void write_all() {
+    const int wc = cfg_.coded_w >> kCtbLog2, hc = cfg_.coded_h >> kCtbLog2;
+    for (int cy = 0; cy < hc; ++cy)
+      for (int cx = 0; cx < wc; ++cx) {
+        if (cfg_.sao) write_sao_off(cx, cy);
+        quadtree(cx << kCtbLog2, cy << kCtbLog2, kCtbLog2, 0);
+        const bool last = (cy == hc - 1) && (cx == wc - 1);
+        enc_.encode_terminate(last ? 1 : 0);
+      }
+    enc_.finish();
+  }
+
+ private:
+  int unit(int x, int y) const { return (y >> 3) * fd_.w8 + (x >> 3); }
+  bool avail(int xc, int yc, int xn, int yn) const {
+    return zscan_available(xc, yc, xn, yn, cfg_.coded_w, cfg_.coded_h);
+  }
+  void bin(int b, int ctx) { enc_.encode_bin(b, ctx_.c[ctx]); }
+
+  void write_sao_off(int cx, int cy) {
+    // sao(): merge flags (when neighbours exist) = 0, sao_type_idx luma = chroma = 0
+    if (cx > 0) bin(0, CTX_SAO_MERGE);
+    if (cy > 0) bin(0, CTX_SAO_MERGE);
+    bin(0, CTX_SAO_TYPE);  // luma: not applied (TR bin 0)
+    bin(0, CTX_SAO_TYPE);  // chroma
+  }
+
+  void quadtree(int x0, int y0, int log2, int depth) {
+    const int u = unit(x0, y0);
+    const bool split = fd_.cu_log2[u] < log2;
+    if (log2 > kMinCbLog2) {
+      int inc = 0;
+      if (avail(x0, y0, x0 - 1, y0) && (kCtbLog2 - fd_.cu_log2[unit(x0 - 1, y0)]) > depth) ++inc;
+      if (avail(x0, y0, x0, y0 - 1) && (kCtbLog2 - fd_.cu_log2[unit(x0, y0 - 1)]) > depth) ++inc;
+      bin(split ? 1 : 0, CTX_SPLIT_CU + inc);
+    }
+    if (split) {
+      const int h = 1 << (log2 - 1);
+      quadtree(x0, y0, log2 - 1, depth + 1);
+      quadtree(x0 + h, y0, log2 - 1, depth + 1);
+      quadtree(x0, y0 + h, log2 - 1, depth + 1);
+      quadtree(x0 + h, y0 + h, log2 - 1, depth + 1);
+    } else {
+      coding_unit(x0, y0, log2);
+    }
+  }
+
+  void set_skip(int x0, int y0, int log2, uint8_t v) {
+    const int n = 1 << (log2 - 3);
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) skip_[unit(x0 + 8 * i, y0 + 8 * j)] = v;
+  }
+
+  bool inter_at(int xc, int yc, int xn, int yn, Mv& mv) const {
+    if (!avail(xc, yc, xn, yn)) return false;
+    const int u = unit(xn, yn);
+    if (fd_.intra[u]) return false;
+    mv.x = fd_.mv[2 * u];
+    mv.y = fd_.mv[2 * u + 1];
+    return true;
+  }
+
+  void coding_unit(int x0, int y0, int log2) {
+    const int u = unit(x0, y0);
+    const int N = 1 << log2;
+    const bool intra = fd_.intra[u] != 0;
+    const int cbf = fd_.cbf[u];
+    if (!islice_) {
+      // decide skip / merge / amvp from the motion field
+      int merge_idx = -1;
+      Mv mv{fd_.mv[2 * u], fd_.mv[2 * u + 1]};
+      if (!intra) {
+        Mv cand[5];
+        auto f = [&](int xn, int yn, Mv& m) { return inter_at(x0, y0, xn, yn, m); };
+        const int nc = merge_candidates(x0, y0, N, N, cfg_.max_merge_cand, f, cand);
+        for (int i = 0; i < nc; ++i)
+          if (cand[i] == mv) {
+            merge_idx = i;
+            break;
+          }
+      }
+      const bool skip = !intra && merge_idx >= 0 && cbf == 0;
+      int inc = 0;
+      if (avail(x0, y0, x0 - 1, y0) && skip_[unit(x0 - 1, y0)]) ++inc;
+      if (avail(x0, y0, x0, y0 - 1) && skip_[unit(x0, y0 - 1)]) ++inc;
+      bin(skip ? 1 : 0, CTX_CU_SKIP + inc);
+      set_skip(x0, y0, log2, skip ? 1 : 0);
+      if (skip) {
+        write_merge_idx(merge_idx);
+        return;
+      }
+      bin(intra ? 1 : 0, CTX_PRED_MODE);  // pred_mode_flag
+      if (!intra) {
+        bin(1, CTX_PART_MODE);  // part_mode 2Nx2N
+        const bool merge = merge_idx >= 0;
+        bin(merge ? 1 : 0, CTX_MERGE_FLAG);
+        if (merge) {
+          write_merge_idx(merge_idx);
+        } else {
+          Mv mvp[2];
+          auto f = [&](int xn, int yn, Mv& m) { return inter_at(x0, y0, xn, yn, m); };
+          amvp_candidates(x0, y0, N, N, f, mvp);
+          const int c0 = mvd_cost(mv.x - mvp[0].x) + mvd_cost(mv.y - mvp[0].y);
+          const int c1 = mvd_cost(mv.x - mvp[1].x) + mvd_cost(mv.y - mvp[1].y);
+          const int sel = c1 < c0 ? 1 : 0;
+          write_mvd(mv.x - mvp[sel].x, mv.y - mvp[sel].y);
+          bin(sel, CTX_MVP_FLAG);
+          bin(cbf ? 1 : 0, CTX_RQT_ROOT_CBF);
+          if (!cbf) return;
+        }
+        transform_tree(x0, y0, log2, false, 0);
+        return;
+      }
+    }
+    // intra CU
+    if (log2 == kMinCbLog2) bin(1, CTX_PART_MODE);  // 2Nx2N
+    const int mode = fd_.ipm[u];
+    int candA = 1, candB = 1;
+    if (avail(x0, y0, x0 - 1, y0) && fd_.intra[unit(x0 - 1, y0)]) candA = fd_.ipm[unit(x0 - 1, y0)];
+    if (avail(x0, y0, x0, y0 - 1) && fd_.intra[unit(x0, y0 - 1)] &&
+        (y0 - 1) >= ((y0 >> kCtbLog2) << kCtbLog2))
+      candB = fd_.ipm[unit(x0, y0 - 1)];
+    int mpm[3];
+    intra_mpm_list(candA, candB, mpm);
+    int idx = -1;
+    for (int i = 0; i < 3; ++i)
+      if (mpm[i] == mode) idx = i;
+    bin(idx >= 0 ? 1 : 0, CTX_PREV_INTRA);
+    if (idx >= 0) {
+      enc_.encode_bypass(idx > 0);
+      if (idx > 0) enc_.encode_bypass(idx > 1);
+    } else {
+      int s[3] = {mpm[0], mpm[1], mpm[2]};
+      std::sort(s, s + 3);
+      int rem = mode;
+      for (int i = 2; i >= 0; --i)
+        if (mode > s[i]) --rem;
+      enc_.encode_bypass_bins((uint32_t)rem, 5);
+    }
+    bin(0, CTX_CHROMA_PRED);  // intra_chroma_pred_mode = 4 (DM)
+    transform_tree(x0, y0, log2, true, mode);
+  }
+
+  static int mvd_cost(int d) {  // bins of one mvd component (approx)
+    int a = d < 0 ? -d : d;
+    if (a == 0) return 1;
+    if (a == 1) return 3;
+    int v = a - 2, k = 1, n = 0;
+    while (v >= (1 << k)) {
+      v -= 1 << k;
+      ++k;
+      ++n;
+    }
+    return 3 + n + 1 + k;
+  }
+
+  void write_merge_idx(int idx) {
+    if (cfg_.max_merge_cand <= 1) return;
+    bin(idx > 0 ? 1 : 0, CTX_MERGE_IDX);
+    for (int i = 1; i < cfg_.max_merge_cand - 1 && idx >= i; ++i) enc_.encode_bypass(idx > i);
+  }
+
+  void write_eg1(uint32_t v) {  // k-th order Exp-Golomb, k = 1, bypass
+    int k = 1;
+    while (v >= (1u << k)) {
+      enc_.encode_bypass(1);
+      v -= 1u << k;
+      ++k;
+    }
+    enc_.encode_bypass(0);
+    enc_.encode_bypass_bins(v, k);
+  }
+
+  void write_mvd(int dx, int dy) {
+    const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
+    bin(ax > 0, CTX_MVD_G0);
+    bin(ay > 0, CTX_MVD_G0);
+    if (ax > 0) bin(ax > 1, CTX_MVD_G1);
+    if (ay > 0) bin(ay > 1, CTX_MVD_G1);
+    if (ax > 0) {
+      if (ax > 1) write_eg1((uint32_t)(ax - 2));
+      enc_.encode_bypass(dx < 0);
+    }
+    if (ay > 0) {
+      if (ay > 1) write_eg1((uint32_t)(ay - 2));
+      enc_.encode_bypass(dy < 0);
+    }
+  }
+
+  void transform_tree(int x0, int y0, int log2, bool intra, int mode) {
+    const int cbf = fd_.cbf[unit(x0, y0)];
+    const int cl = cbf & 1, cb = (cbf >> 1) & 1, cr = (cbf >> 2) & 1;
+    // log2 >= 3 here, so chroma cbfs are coded at depth 0
+    bin(cb, CTX_CBF_CHROMA + 0);
+    bin(cr, CTX_CBF_CHROMA + 0);
+    if (intra || cb || cr) bin(cl, CTX_CBF_LUMA + 1);
+    else if (!cl) throw std::runtime_error("inter CU with rqt_root_cbf=1 but no residual");
+    const int cmode = intra ? chroma_intra_mode(4, mode) : 0;
+    if (cl)
+      residual(fd_.coef[0] + (size_t)y0 * cfg_.coded_w + x0, cfg_.coded_w, log2, 0,
+               scan_idx_for(intra, log2, 0, mode));
+    const int cs = cfg_.coded_w >> 1;
+    if (cb)
+      residual(fd_.coef[1] + (size_t)(y0 >> 1) * cs + (x0 >> 1), cs, log2 - 1, 1,
+               scan_idx_for(intra, log2 - 1, 1, cmode));
+    if (cr)
+      residual(fd_.coef[2] + (size_t)(y0 >> 1) * cs + (x0 >> 1), cs, log2 - 1, 2,
+               scan_idx_for(intra, log2 - 1, 2, cmode));
+  }
+
+  void write_last_prefix(int pos, int log2N, int cIdx, int base) {
+    const int prefix = kGroupIdx[pos];
+    int off, shift;
+    if (cIdx == 0) {
+      off = 3 * (log2N - 2) + ((log2N - 1) >> 2);
+      shift = (log2N + 1) >> 2;
+    } else {
+      off = 15;
+      shift = log2N - 2;
+    }
+    const int cmax = (log2N << 1) - 1;
+    for (int i = 0; i < prefix; ++i) bin(1, base + off + (i >> shift));
+    if (prefix < cmax) bin(0, base + off + (prefix >> shift));
+  }
+  void write_last_suffix(int pos) {
+    const int prefix = kGroupIdx[pos];
+    if (prefix > 3) {
+      const int nb = (prefix >> 1) - 1;
+      enc_.encode_bypass_bins((uint32_t)(pos - kMinInGroup[prefix]), nb);
+    }
+  }
+
+  void write_remaining(int v, int rice) {
+    if (v < (4 << rice)) {
+      const int p = v >> rice;
+      for (int i = 0; i < p; ++i) enc_.encode_bypass(1);
+      enc_.encode_bypass(0);
+      if (rice) enc_.encode_bypass_bins((uint32_t)(v & ((1 << rice) - 1)), rice);
+    } else {
+      enc_.encode_bypass_bins(0xf, 4);
+      int k = rice + 1;
+      uint32_t s = (uint32_t)(v - (4 << rice));
+      while (s >= (1u << k)) {
+        enc_.encode_bypass(1);
+        s -= 1u << k;
+        ++k;
+      }
+      enc_.encode_bypass(0);
+      enc_.encode_bypass_bins(s, k);
+    }
+  }
+
+  void residual(const int16_t* blk, int stride, int log2N, int cIdx, int scanIdx) {
+    const int nsb = 1 << (log2N - 2);  // sub-blocks per side
+    const int numSb = nsb * nsb;
+    auto coef_at = [&](int xs, int ys, int n) -> int {
+      int xc, yc;
+      coef_pos_in_sb(scanIdx, n, xc, yc);
+      return blk[(size_t)((ys << 2) + yc) * stride + (xs << 2) + xc];
+    };
+    // last significant coefficient in scan order
+    int lastSb = -1, lastN = -1;
+    for (int i = numSb - 1; i >= 0 && lastSb < 0; --i) {
+      int xs, ys;
+      subblock_pos(log2N, scanIdx, i, xs, ys);
+      for (int n = 15; n >= 0; --n)
+        if (coef_at(xs, ys, n) != 0) {
+          lastSb = i;
+          lastN = n;
+          break;
+        }
+    }
+    if (lastSb < 0) throw std::runtime_error("residual_coding of an all-zero block");
+    {
+      int xs, ys, xc, yc;
+      subblock_pos(log2N, scanIdx, lastSb, xs, ys);
+      coef_pos_in_sb(scanIdx, lastN, xc, yc);
+      int lx = (xs << 2) + xc, ly = (ys << 2) + yc;
+      if (scanIdx == 2) std::swap(lx, ly);
+      write_last_prefix(lx, log2N, cIdx, CTX_LAST_X);
+      write_last_prefix(ly, log2N, cIdx, CTX_LAST_Y);
+      write_last_suffix(lx);
+      write_last_suffix(ly);
+    }
+    uint8_t csbf[8][8];
+    std::memset(csbf, 0, sizeof(csbf));
+    int c1 = 1;
+    for (int i = lastSb; i >= 0; --i) {
+      int xs, ys;
+      subblock_pos(log2N, scanIdx, i, xs, ys);
+      int vals[16];
+      bool any = false;
+      for (int n = 0; n < 16; ++n) {
+        vals[n] = coef_at(xs, ys, n);
+        any |= vals[n] != 0;
+      }
+      bool inferDc = false;
+      if (i < lastSb && i > 0) {
+        int ctx = 0;
+        if (xs < nsb - 1) ctx += csbf[xs + 1][ys];
+        if (ys < nsb - 1) ctx += csbf[xs][ys + 1];
+        ctx = ctx > 1 ? 1 : ctx;
+        bin(any ? 1 : 0, CTX_CSBF + ctx + (cIdx ? 2 : 0));
+        csbf[xs][ys] = any ? 1 : 0;
+        inferDc = true;
+      } else {
+        csbf[xs][ys] = 1;
+      }
+      if (!csbf[xs][ys]) continue;
+      // significance
+      int prevCsbf = 0;
+      if (xs < nsb - 1) prevCsbf += csbf[xs + 1][ys];
+      if (ys < nsb - 1) prevCsbf += csbf[xs][ys + 1] << 1;
+      const int nStart = (i == lastSb) ? lastN - 1 : 15;
+      for (int n = nStart; n >= 0; --n) {
+        if (n == 0 && inferDc) break;  // DC inferred significant
+        int xc, yc;
+        coef_pos_in_sb(scanIdx, n, xc, yc);
+        const int sig = vals[n] != 0;
+        bin(sig, CTX_SIG + sig_ctx(log2N, cIdx, scanIdx, xs, ys, xc, yc, prevCsbf));
+        if (sig) inferDc = false;
+      }
+      // levels
+      int absv[16], signs[16], cnt = 0;
+      for (int n = 15; n >= 0; --n)
+        if (vals[n]) {
+          absv[cnt] = vals[n] < 0 ? -vals[n] : vals[n];
+          signs[cnt] = vals[n] < 0;
+          ++cnt;
+        }
+      int ctxSet = (i > 0 && cIdx == 0) ? 2 : 0;
+      if (c1 == 0) ++ctxSet;
+      c1 = 1;
+      const int g1base = CTX_G1 + 4 * ctxSet + (cIdx ? 16 : 0);
+      const int nG1 = cnt < 8 ? cnt : 8;
+      int firstG2 = -1;
+      for (int k = 0; k < nG1; ++k) {
+        const int g1 = absv[k] > 1;
+        bin(g1, g1base + c1);
+        if (g1) {
+          c1 = 0;
+          if (firstG2 < 0) firstG2 = k;
+        } else if (c1 > 0 && c1 < 3) {
+          ++c1;
+        }
+      }
+      if (firstG2 >= 0) bin(absv[firstG2] > 2, CTX_G2 + ctxSet + (cIdx ? 4 : 0));
+      for (int k = 0; k < cnt; ++k) enc_.encode_bypass(signs[k]);
+      int rice = 0;
+      bool firstC2 = true;
+      for (int k = 0; k < cnt; ++k) {
+        const int base = (k < 8) ? (firstC2 ? 3 : 2) : 1;
+        if (absv[k] >= base) {
+          write_remaining(absv[k] - base, rice);
+          if (absv[k] > 3 * (1 << rice)) rice = tv_min(rice + 1, 4);
+        }
+        if (absv[k] >= 2) firstC2 = false;
+      }
+    }
+  }
+
+  static int sig_ctx(int log2N, int cIdx, int scanIdx, int xs, int ys, int xp, int yp, int prevCsbf) {
+    int sigCtx;
+    if (log2N == 2) {
+      sigCtx = kCtxIdxMap4x4[(yp << 2) + xp];
+    } else if (xs == 0 && ys == 0 && xp == 0 && yp == 0) {
+      sigCtx = 0;
+    } else {
+      if (prevCsbf == 0) sigCtx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+      else if (prevCsbf == 1) sigCtx = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
+      else if (prevCsbf == 2) sigCtx = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
+      else sigCtx = 2;
+      if (cIdx == 0 && (xs > 0 || ys > 0)) sigCtx += 3;
+      if (log2N == 3) sigCtx += (scanIdx == 0) ? 9 : 15;
+      else sigCtx += (cIdx == 0) ? 21 : 12;
+    }
+    return cIdx == 0 ? sigCtx : 27 + sigCtx;
+  }
+
+  const SeqConfig& cfg_;
+  const FrameData& fd_;
+  bool islice_;
+  CabacEncoder enc_;
+  ContextSet ctx_;
+  std::vector<uint8_t> skip_;
+};
+
+}  // namespace
+
+size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
+                   std::vector<uint8_t>& out) {
+  BitWriter bw;
+  const int nal = idr ? NAL_IDR_N_LP : NAL_TRAIL_R;
+  bw.put(1, 1);  // first_slice_segment_in_pic_flag
+  if (idr) bw.put(0, 1);  // no_output_of_prior_pics_flag
+  bw.ue(0);               // slice_pic_parameter_set_id
+  bw.ue(idr ? 2 : 1);     // slice_type: I = 2, P = 1
+  if (!idr) {
+    bw.put((uint32_t)(poc & 0xff), 8);  // slice_pic_order_cnt_lsb
+    bw.put(1, 1);                       // short_term_ref_pic_set_sps_flag (idx 0 implied)
+  }
+  if (cfg.sao) {
+    bw.put(1, 1);  // slice_sao_luma_flag
+    bw.put(1, 1);  // slice_sao_chroma_flag
+  }
+  if (!idr) {
+    bw.put(0, 1);  // num_ref_idx_active_override_flag
+    bw.ue((uint32_t)(5 - cfg.max_merge_cand));  // five_minus_max_num_merge_cand
+  }
+  bw.se(0);  // slice_qp_delta
+  // byte_alignment()
+  bw.put_bit(1);
+  bw.align_zero();
+  SliceWriter sw(cfg, fd, idr, &bw);
+  sw.write_all();
+  bw.trailing_bits();
+  const size_t before = out.size();
+  append_nal(out, nal, bw.bytes());
+  return out.size() - before;
+}
+
+}  // namespace tv

@@ -1,0 +1,220 @@
+// hevc_codec.h — host-side HEVC codec API: sequence configuration, the per-frame
+// "decision" layout produced by the analysis stage (GPU kernels or the CPU reference
+// encoder), the CABAC syntax writer, the decoder oracle and picture reconstruction helpers.
+//
+// Decision layout (all arrays indexed by 8x8 unit u = y8 * w8 + x8 of the coded picture;
+// every unit of a CU carries the CU's values, so neighbour lookups are O(1)):
+//   cu_log2[u]  log2 size of the covering CU (3..5)
+//   intra[u]    1 = MODE_INTRA, 0 = MODE_INTER
+//   ipm[u]      luma intra prediction mode (intra CUs)
+//   mv[2u+0/1]  quarter-pel motion vector (inter CUs; reference = previous picture)
+//   cbf[u]      bit0 = cbf_luma, bit1 = cbf_cb, bit2 = cbf_cr
+//   coef[c]     quantised levels, each TB stored at its picture position (int16 planes,
+//               luma stride = coded_w, chroma stride = coded_w/2)
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "hevc_defs.h"
+
+namespace tv {
+
+struct SeqConfig {
+  int width = 0, height = 0;      // display size (conformance window)
+  int coded_w = 0, coded_h = 0;   // multiples of the CTB size
+  int qp = 27;
+  int max_merge_cand = 5;
+  bool deblock = true;
+  bool sao = false;
+  int fps_num = 30, fps_den = 1;
+  void finalize() {
+    coded_w = (width + kCtb - 1) / kCtb * kCtb;
+    coded_h = (height + kCtb - 1) / kCtb * kCtb;
+  }
+  int w8() const { return coded_w >> 3; }
+  int h8() const { return coded_h >> 3; }
+  int level_idc() const;
+};
+
+struct FrameData {
+  int w8 = 0, h8 = 0;
+  const uint8_t* cu_log2 = nullptr;
+  const uint8_t* intra = nullptr;
+  const uint8_t* ipm = nullptr;
+  const int16_t* mv = nullptr;
+  const uint8_t* cbf = nullptr;
+  const int16_t* coef[3] = {nullptr, nullptr, nullptr};
+};
+
+// Owning storage for one frame's decisions (CPU side).
+struct FrameDecisions {
+  int w8 = 0, h8 = 0, cw = 0, ch = 0;
+  std::vector<uint8_t> cu_log2, intra, ipm, cbf;
+  std::vector<int16_t> mv, coef_y, coef_u, coef_v;
+  void alloc(int coded_w, int coded_h) {
+    cw = coded_w;
+    ch = coded_h;
+    w8 = coded_w >> 3;
+    h8 = coded_h >> 3;
+    const size_t n = (size_t)w8 * h8;
+    cu_log2.assign(n, 3);
+    intra.assign(n, 0);
+    ipm.assign(n, 1);
+    cbf.assign(n, 0);
+    mv.assign(2 * n, 0);
+    coef_y.assign((size_t)coded_w * coded_h, 0);
+    coef_u.assign((size_t)coded_w * coded_h / 4, 0);
+    coef_v.assign((size_t)coded_w * coded_h / 4, 0);
+  }
+  FrameData view() const {
+    FrameData f;
+    f.w8 = w8;
+    f.h8 = h8;
+    f.cu_log2 = cu_log2.data();
+    f.intra = intra.data();
+    f.ipm = ipm.data();
+    f.mv = mv.data();
+    f.cbf = cbf.data();
+    f.coef[0] = coef_y.data();
+    f.coef[1] = coef_u.data();
+    f.coef[2] = coef_v.data();
+    return f;
+  }
+};
+
+// A planar 8-bit 4:2:0 picture buffer
+struct Picture {
+  int w = 0, h = 0;  // luma size
+  std::vector<uint8_t> y, u, v;
+  void alloc(int W, int H) {
+    w = W;
+    h = H;
+    y.assign((size_t)W * H, 0);
+    u.assign((size_t)W * H / 4, 128);
+    v.assign((size_t)W * H / 4, 128);
+  }
+  uint8_t* plane(int c) { return c == 0 ? y.data() : (c == 1 ? u.data() : v.data()); }
+  const uint8_t* plane(int c) const { return c == 0 ? y.data() : (c == 1 ? u.data() : v.data()); }
+  int pw(int c) const { return c ? w / 2 : w; }
+  int ph(int c) const { return c ? h / 2 : h; }
+};
+
+// ----------------------------- bitstream generation -------------------------------------
+void write_parameter_sets(const SeqConfig& cfg, std::vector<uint8_t>& out);
+// Encode one picture as a single slice NAL; returns bytes appended.
+size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
+                   std::vector<uint8_t>& out);
+
+// ------------------------------ reconstruction helpers ----------------------------------
+// Intra prediction of a TB in component cIdx at component position (x,y).
+void predict_intra_tb(const Picture& rec, int cIdx, int x, int y, int log2N, int mode, int* pred);
+// Inter prediction (uni, L0) of a w x h block of component cIdx at component position (x,y).
+void predict_inter_block(const Picture& ref, int cIdx, int x, int y, int w, int h, int mvx,
+                         int mvy, int* pred);
+// Dequantise + inverse transform the levels of a TB (plane stride `ls`) and add to `pred`,
+// writing the clipped reconstruction into `dst` (stride ds).  cbf=false -> copy pred.
+void recon_tb(const int16_t* levels, int ls, bool cbf, int log2N, int qp, const int* pred,
+              uint8_t* dst, int ds);
+// In-loop deblocking of a reconstructed picture given the frame decisions.
+void deblock_picture(Picture& pic, const FrameData& fd, int qp);
+
+// derived chroma intra mode for intra_chroma_pred_mode idx (4 = DM)
+inline int chroma_intra_mode(int chroma_idx, int luma_mode) {
+  if (chroma_idx == 4) return luma_mode;
+  static const int m[4] = {0, 26, 10, 1};
+  return m[chroma_idx] == luma_mode ? 34 : m[chroma_idx];
+}
+
+// ------------------------------------ MV prediction -------------------------------------
+struct Mv {
+  int x = 0, y = 0;
+  bool operator==(const Mv& o) const { return x == o.x && y == o.y; }
+  bool operator!=(const Mv& o) const { return !(*this == o); }
+};
+// Merge candidate list for a 2Nx2N PU (P slice, one reference).  `inter_at(xN,yN,mv)` must
+// return true iff the location is available (z-scan, decoded, in picture) and inter coded.
+template <class F>
+int merge_candidates(int xPb, int yPb, int nW, int nH, int maxCand, F&& inter_at, Mv* out) {
+  Mv a1, b1, b0, a0, b2;
+  const bool avA1 = inter_at(xPb - 1, yPb + nH - 1, a1);
+  const bool avB1 = inter_at(xPb + nW - 1, yPb - 1, b1);
+  const bool avB0 = inter_at(xPb + nW, yPb - 1, b0);
+  const bool avA0 = inter_at(xPb - 1, yPb + nH, a0);
+  const bool avB2 = inter_at(xPb - 1, yPb - 1, b2);
+  const bool fA1 = avA1;
+  const bool fB1 = avB1 && !(avA1 && a1 == b1);
+  const bool fB0 = avB0 && !(avB1 && b1 == b0);
+  const bool fA0 = avA0 && !(avA1 && a1 == a0);
+  bool fB2 = avB2 && !(avA1 && a1 == b2) && !(avB1 && b1 == b2);
+  if ((int)fA0 + (int)fA1 + (int)fB0 + (int)fB1 == 4) fB2 = false;
+  int n = 0;
+  if (fA1 && n < maxCand) out[n++] = a1;
+  if (fB1 && n < maxCand) out[n++] = b1;
+  if (fB0 && n < maxCand) out[n++] = b0;
+  if (fA0 && n < maxCand) out[n++] = a0;
+  if (fB2 && n < maxCand) out[n++] = b2;
+  while (n < maxCand) out[n++] = Mv{0, 0};
+  return n;
+}
+
+// AMVP candidate list (2 entries) for a 2Nx2N PU, P slice, single reference picture.
+template <class F>
+void amvp_candidates(int xPb, int yPb, int nW, int nH, F&& inter_at, Mv* out) {
+  Mv a0, a1, b0, b1, b2;
+  const bool avA0 = inter_at(xPb - 1, yPb + nH, a0);
+  const bool avA1 = inter_at(xPb - 1, yPb + nH - 1, a1);
+  const bool isScaled = avA0 || avA1;
+  bool fA = false, fB = false;
+  Mv A, B;
+  if (avA0) { fA = true; A = a0; }
+  else if (avA1) { fA = true; A = a1; }
+  const bool avB0 = inter_at(xPb + nW, yPb - 1, b0);
+  const bool avB1 = inter_at(xPb + nW - 1, yPb - 1, b1);
+  const bool avB2 = inter_at(xPb - 1, yPb - 1, b2);
+  if (avB0) { fB = true; B = b0; }
+  else if (avB1) { fB = true; B = b1; }
+  else if (avB2) { fB = true; B = b2; }
+  if (!isScaled && fB) { fA = true; A = B; }
+  // (!isScaled): B re-derived by the scaled pass -> same first available B candidate
+  Mv list[3];
+  int n = 0;
+  if (fA) list[n++] = A;
+  if (fB) list[n++] = B;
+  if (n == 2 && list[0] == list[1]) n = 1;
+  while (n < 2) list[n++] = Mv{0, 0};
+  out[0] = list[0];
+  out[1] = list[1];
+}
+
+// ------------------------------------- decoder ------------------------------------------
+struct DecodedPicture {
+  int poc = 0;
+  bool idr = false;
+  Picture pic;  // coded size (includes padding rows/cols)
+};
+
+class HevcDecoder {
+ public:
+  // Decode a complete Annex-B elementary stream.  Throws std::runtime_error on syntax
+  // violations of the supported subset.
+  void decode(const uint8_t* data, size_t n);
+  std::vector<DecodedPicture> pictures;
+  int width = 0, height = 0;          // conformance-cropped size
+  int coded_w = 0, coded_h = 0;
+  // decisions parsed from the last decoded picture (for tests)
+  FrameDecisions last_decisions;
+
+ private:
+  struct Impl;
+};
+
+// ------------------------------------- containers ---------------------------------------
+// Build an ISO-BMFF (.mp4, 'hvc1') file from an Annex-B HEVC stream.  Returns bytes.
+std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int height,
+                             int fps_num, int fps_den);
+// Parse an mp4 produced by mux_mp4 back to Annex-B (probe / round trip).
+std::vector<uint8_t> demux_mp4(const uint8_t* mp4, size_t n, int* width, int* height,
+                               int* nframes, int* timescale, int* sample_delta);
+
+}  // namespace tv

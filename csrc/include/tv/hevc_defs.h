@@ -1,0 +1,501 @@
+// hevc_defs.h — HEVC (H.265) constants, tables and bit-exact scalar primitives shared by
+// the C++ host code (syntax writer, decoder oracle, CPU reference encoder) and the HIP
+// kernels for gfx950.  Everything here is `TV_HD` (host+device) and header-only so the GPU
+// and CPU paths compute byte-identical reconstructions.
+//
+// Reference parity: thinvids encodes with ffmpeg h264_vaapi CQP 27 (reference
+// worker/tasks.py:66-67, :1573-1586); this engine replaces that hot path with its own
+// HEVC encoder (SURVEY.md §2.3 K5a–K5h).  Tables are transcribed from ITU-T H.265.
+#pragma once
+#include <cstdint>
+#include <cstdlib>
+
+#if defined(__HIPCC__)
+#define TV_HD __host__ __device__ __forceinline__
+#else
+#define TV_HD inline
+#endif
+
+namespace tv {
+
+template <typename T> TV_HD T clip3(T lo, T hi, T v) { return v < lo ? lo : (v > hi ? hi : v); }
+TV_HD int clip_pixel(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+TV_HD int tv_abs(int v) { return v < 0 ? -v : v; }
+TV_HD int tv_min(int a, int b) { return a < b ? a : b; }
+TV_HD int tv_max(int a, int b) { return a > b ? a : b; }
+
+// ---------------------------------------------------------------------------------------
+// Fixed coding-structure configuration of this engine (GPU-friendly subset of Main profile)
+//   CTB 32x32, min CB 8x8, TB = CB (no residual quadtree), min TB 4 (chroma of 8x8 CB),
+//   2Nx2N partitions only, one slice per picture, 1 reference picture (previous frame).
+// ---------------------------------------------------------------------------------------
+constexpr int kCtbLog2 = 5;
+constexpr int kCtb = 1 << kCtbLog2;
+constexpr int kMinCbLog2 = 3;
+constexpr int kMinTbLog2 = 2;
+constexpr int kMaxTbLog2 = 5;
+
+// --------------------------------- transform matrix -------------------------------------
+// HEVC 32-point integer DCT.  T32[k][n]; smaller sizes use rows k*(32/N).
+// The 33 distinct magnitudes indexed by m = ((2n+1)k mod 128) folded to [0,32].
+constexpr int8_t kDctMag[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                                61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9,  4,  0};
+
+struct DctMat32 {
+  int8_t m[32][32];
+};
+constexpr DctMat32 make_dct32() {
+  DctMat32 d{};
+  for (int k = 0; k < 32; ++k)
+    for (int n = 0; n < 32; ++n) {
+      int mm = ((2 * n + 1) * k) % 128;
+      int v = 0;
+      if (mm <= 32) v = kDctMag[mm];
+      else if (mm < 64) v = -kDctMag[64 - mm];
+      else if (mm <= 96) v = -kDctMag[mm - 64];
+      else v = kDctMag[128 - mm];
+      d.m[k][n] = (int8_t)v;
+    }
+  return d;
+}
+constexpr DctMat32 kDct32 = make_dct32();
+
+// coefficient of the N-point DCT (N = 1<<log2N): row k (frequency), column n (sample)
+TV_HD int dct_coef(int log2N, int k, int n) { return kDct32.m[k << (5 - log2N)][n]; }
+
+// ------------------------------------ quantisation --------------------------------------
+constexpr int kQuantScale[6] = {26214, 23302, 20560, 18396, 16384, 14564};
+constexpr int kLevelScale[6] = {40, 45, 51, 57, 64, 72};
+
+// chroma QP mapping for 4:2:0 (H.265 Table 8-10)
+TV_HD int chroma_qp(int qpy, int offset) {
+  int qpi = clip3(-0, 57, qpy + offset);
+  if (qpi < 30) return qpi;
+  if (qpi >= 43) return qpi - 6;
+  constexpr int tab[13] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37};
+  return tab[qpi - 30];
+}
+
+// Decoder-exact scaling (dequantisation) of one level, flat scaling matrix (m = 16).
+TV_HD int dequant_level(int level, int qp, int log2N) {
+  const int bdShift = 8 + log2N - 5;  // BitDepth + log2(nTbS) + 10 - 15
+  long long v = (long long)level * 16 * kLevelScale[qp % 6];
+  v = (v << (qp / 6)) + (1LL << (bdShift - 1));
+  v >>= bdShift;
+  return (int)clip3<long long>(-32768, 32767, v);
+}
+
+// Encoder deadzone quantiser (not normative).  `coef` is the forward-transform output.
+TV_HD int quant_level(int coef, int qp, int log2N, bool intra) {
+  const int qbits = 14 + qp / 6 + (15 - 8 - log2N);
+  const int add = (intra ? 171 : 85) << (qbits - 9);
+  int a = tv_abs(coef);
+  int l = (int)(((long long)a * kQuantScale[qp % 6] + add) >> qbits);
+  if (l > 32767) l = 32767;
+  return coef < 0 ? -l : l;
+}
+
+// Exact scalar inverse 2-D transform (H.265 8.6.4.2) — `coef` and `res` are N*N row-major
+// (row = y, column = x).  Output residual is what the decoder adds to the prediction.
+TV_HD void inverse_transform(const int* coef, int log2N, int* res) {
+  const int N = 1 << log2N;
+  int tmp[32 * 32];
+  // stage 1: columns (vertical 1-D inverse), clip to 16 bit after >>7
+  for (int x = 0; x < N; ++x)
+    for (int y = 0; y < N; ++y) {
+      int s = 0;
+      for (int k = 0; k < N; ++k) s += dct_coef(log2N, k, y) * coef[k * N + x];
+      tmp[y * N + x] = clip3(-32768, 32767, (s + 64) >> 7);
+    }
+  // stage 2: rows, bdShift = 20 - BitDepth = 12
+  for (int y = 0; y < N; ++y)
+    for (int x = 0; x < N; ++x) {
+      long long s = 0;
+      for (int k = 0; k < N; ++k) s += (long long)dct_coef(log2N, k, x) * tmp[y * N + k];
+      res[y * N + x] = (int)((s + 2048) >> 12);
+    }
+}
+
+// Forward 2-D transform (encoder side; HM scaling convention).  residual -> coefficients.
+TV_HD void forward_transform(const int* res, int log2N, int* coef) {
+  const int N = 1 << log2N;
+  const int sh1 = log2N - 1, sh2 = log2N + 6;
+  int tmp[32 * 32];
+  for (int k = 0; k < N; ++k)  // vertical: tmp[k][x] = sum_y T[k][y] * r[y][x]
+    for (int x = 0; x < N; ++x) {
+      int s = 0;
+      for (int y = 0; y < N; ++y) s += dct_coef(log2N, k, y) * res[y * N + x];
+      tmp[k * N + x] = (s + (1 << (sh1 - 1))) >> sh1;
+    }
+  for (int k = 0; k < N; ++k)
+    for (int j = 0; j < N; ++j) {  // horizontal: coef[k][j] = sum_x T[j][x] * tmp[k][x]
+      long long s = 0;
+      for (int x = 0; x < N; ++x) s += (long long)dct_coef(log2N, j, x) * tmp[k * N + x];
+      coef[k * N + j] = (int)((s + (1LL << (sh2 - 1))) >> sh2);
+    }
+}
+
+// ---------------------------------- intra prediction ------------------------------------
+constexpr int8_t kIntraPredAngle[35] = {0,   0,   32,  26,  21,  17,  13,  9,  5,  2,  0,  -2,
+                                        -5,  -9,  -13, -17, -21, -26, -32, -26, -21, -17, -13, -9,
+                                        -5,  -2,  0,   2,   5,   9,   13,  17,  21,  26,  32};
+// invAngle for modes 11..25
+constexpr int16_t kInvAngle[15] = {-4096, -1638, -910, -630, -482, -390, -315, -256,
+                                   -315,  -390,  -482, -630, -910, -1638, -4096};
+
+// Intra prediction of an N x N block from its (already substituted) reference samples.
+//   left[i]  = p[-1][i-1] for i = 0..2N   (left[0] = corner p[-1][-1])
+//   top[i]   = p[i-1][-1] for i = 0..2N   (top[0]  = corner)
+// `filter_edges` enables the DC/H/V boundary smoothing (luma, N < 32).
+// Output pred[y*N+x].
+TV_HD void intra_pred_from_refs(const int* left, const int* top, int log2N, int mode,
+                                bool filter_edges, int* pred) {
+  const int N = 1 << log2N;
+  if (mode == 0) {  // planar
+    for (int y = 0; y < N; ++y)
+      for (int x = 0; x < N; ++x)
+        pred[y * N + x] = ((N - 1 - x) * left[y + 1] + (x + 1) * top[N + 1] +
+                           (N - 1 - y) * top[x + 1] + (y + 1) * left[N + 1] + N) >>
+                          (log2N + 1);
+    return;
+  }
+  if (mode == 1) {  // DC
+    int s = N;
+    for (int i = 0; i < N; ++i) s += top[i + 1] + left[i + 1];
+    const int dc = s >> (log2N + 1);
+    for (int i = 0; i < N * N; ++i) pred[i] = dc;
+    if (filter_edges) {
+      pred[0] = (left[1] + 2 * dc + top[1] + 2) >> 2;
+      for (int x = 1; x < N; ++x) pred[x] = (top[x + 1] + 3 * dc + 2) >> 2;
+      for (int y = 1; y < N; ++y) pred[y * N] = (left[y + 1] + 3 * dc + 2) >> 2;
+    }
+    return;
+  }
+  const int angle = kIntraPredAngle[mode];
+  int refbuf[3 * 32 + 2];
+  int* ref = refbuf + 32;  // ref[-N..2N]
+  const bool vert = mode >= 18;
+  const int* mainr = vert ? top : left;
+  const int* side = vert ? left : top;
+  for (int x = 0; x <= N; ++x) ref[x] = mainr[x];
+  if (angle < 0) {
+    const int inv = kInvAngle[mode - 11];
+    const int lastx = (N * angle) >> 5;
+    if (lastx < -1)
+      for (int x = lastx; x <= -1; ++x) ref[x] = side[((x * inv + 128) >> 8)];
+  } else {
+    for (int x = N + 1; x <= 2 * N; ++x) ref[x] = mainr[x];
+  }
+  for (int j = 0; j < N; ++j) {  // j = distance along the prediction direction
+    const int pos = (j + 1) * angle;
+    const int idx = pos >> 5, fact = pos & 31;
+    for (int i = 0; i < N; ++i) {
+      int v = fact ? ((32 - fact) * ref[i + idx + 1] + fact * ref[i + idx + 2] + 16) >> 5
+                   : ref[i + idx + 1];
+      if (vert) pred[j * N + i] = v;
+      else pred[i * N + j] = v;
+    }
+  }
+  if (filter_edges) {
+    if (mode == 26)
+      for (int y = 0; y < N; ++y) pred[y * N] = clip_pixel(top[1] + ((left[y + 1] - left[0]) >> 1));
+    else if (mode == 10)
+      for (int x = 0; x < N; ++x) pred[x] = clip_pixel(left[1] + ((top[x + 1] - top[0]) >> 1));
+  }
+}
+
+// [1 2 1] reference smoothing decision (H.265 8.4.4.2.3), luma only, no strong smoothing.
+TV_HD bool intra_filter_refs(int log2N, int mode) {
+  if (mode == 1 || log2N == 2) return false;
+  const int d = tv_min(tv_abs(mode - 26), tv_abs(mode - 10));
+  const int thr = log2N == 3 ? 7 : (log2N == 4 ? 1 : 0);
+  return d > thr;
+}
+
+// Apply [1 2 1] filtering in place to left/top arrays (length 2N+1 each, index 0 = corner).
+TV_HD void intra_smooth_refs(int* left, int* top, int N) {
+  int l[65], t[65];
+  const int c = (left[1] + 2 * left[0] + top[1] + 2) >> 2;
+  for (int i = 1; i < 2 * N; ++i) {
+    l[i] = (left[i + 1] + 2 * left[i] + left[i - 1] + 2) >> 2;
+    t[i] = (top[i + 1] + 2 * top[i] + top[i - 1] + 2) >> 2;
+  }
+  for (int i = 1; i < 2 * N; ++i) {
+    left[i] = l[i];
+    top[i] = t[i];
+  }
+  left[0] = top[0] = c;
+}
+
+// Reference-sample substitution (H.265 8.4.4.2.2) given availability flags.
+//   Canonical order: left[2N] (bottom) ... left[1], corner, top[1] ... top[2N].
+TV_HD void intra_substitute(int* left, int* top, const bool* lavail, const bool* tavail, int N) {
+  const int total = 4 * N + 1;
+  auto get = [&](int i) -> int& { return i < 2 * N ? left[2 * N - i] : top[i - 2 * N]; };
+  auto av = [&](int i) -> bool { return i < 2 * N ? lavail[2 * N - i] : tavail[i - 2 * N]; };
+  int first = -1;
+  for (int i = 0; i < total; ++i)
+    if (av(i)) {
+      first = i;
+      break;
+    }
+  if (first < 0) {
+    for (int i = 0; i < total; ++i) get(i) = 128;
+    left[0] = 128;
+    return;
+  }
+  if (first > 0) get(0) = get(first);
+  for (int i = 1; i < total; ++i)
+    if (!av(i)) get(i) = get(i - 1);
+  left[0] = top[0];  // the corner is stored in both arrays; index 2N maps to top[0]
+}
+
+// MPM candidate list (H.265 8.4.2)
+TV_HD void intra_mpm_list(int candA, int candB, int* list) {
+  if (candA == candB) {
+    if (candA < 2) {
+      list[0] = 0;
+      list[1] = 1;
+      list[2] = 26;
+    } else {
+      list[0] = candA;
+      list[1] = 2 + ((candA + 29) % 32);
+      list[2] = 2 + ((candA - 2 + 1) % 32);
+    }
+  } else {
+    list[0] = candA;
+    list[1] = candB;
+    if (candA != 0 && candB != 0) list[2] = 0;
+    else if (candA != 1 && candB != 1) list[2] = 1;
+    else list[2] = 26;
+  }
+}
+
+// ------------------------------- inter interpolation ------------------------------------
+constexpr int8_t kLumaFilter[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
+                                      {-1, 4, -10, 58, 17, -5, 1, 0},
+                                      {-1, 4, -11, 40, 40, -11, 4, -1},
+                                      {0, 1, -5, 17, 58, -10, 4, -1}};
+constexpr int8_t kChromaFilter[8][4] = {{0, 64, 0, 0},     {-2, 58, 10, -2}, {-4, 54, 16, -2},
+                                        {-6, 46, 28, -4},  {-4, 36, 36, -4}, {-4, 28, 46, -6},
+                                        {-2, 16, 54, -4},  {-2, 10, 58, -2}};
+
+// One luma prediction sample at integer position (xi, yi) with fraction (fx, fy) in quarter
+// pel, reference plane clamped at its borders (w x h).  Returns the final 8-bit sample
+// (uni-prediction, default weighting).
+TV_HD int mc_luma_sample(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx,
+                         int fy) {
+  auto px = [&](int x, int y) -> int {
+    x = clip3(0, w - 1, x);
+    y = clip3(0, h - 1, y);
+    return ref[y * stride + x];
+  };
+  int v;
+  if (fx == 0 && fy == 0) {
+    v = px(xi, yi) << 6;
+  } else if (fy == 0) {
+    v = 0;
+    for (int i = 0; i < 8; ++i) v += kLumaFilter[fx][i] * px(xi + i - 3, yi);
+  } else if (fx == 0) {
+    v = 0;
+    for (int i = 0; i < 8; ++i) v += kLumaFilter[fy][i] * px(xi, yi + i - 3);
+  } else {
+    v = 0;
+    for (int j = 0; j < 8; ++j) {
+      int t = 0;
+      for (int i = 0; i < 8; ++i) t += kLumaFilter[fx][i] * px(xi + i - 3, yi + j - 3);
+      v += kLumaFilter[fy][j] * t;
+    }
+    v >>= 6;
+  }
+  return clip_pixel((v + 32) >> 6);
+}
+
+TV_HD int mc_chroma_sample(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx,
+                           int fy) {
+  auto px = [&](int x, int y) -> int {
+    x = clip3(0, w - 1, x);
+    y = clip3(0, h - 1, y);
+    return ref[y * stride + x];
+  };
+  int v;
+  if (fx == 0 && fy == 0) {
+    v = px(xi, yi) << 6;
+  } else if (fy == 0) {
+    v = 0;
+    for (int i = 0; i < 4; ++i) v += kChromaFilter[fx][i] * px(xi + i - 1, yi);
+  } else if (fx == 0) {
+    v = 0;
+    for (int i = 0; i < 4; ++i) v += kChromaFilter[fy][i] * px(xi, yi + i - 1);
+  } else {
+    v = 0;
+    for (int j = 0; j < 4; ++j) {
+      int t = 0;
+      for (int i = 0; i < 4; ++i) t += kChromaFilter[fx][i] * px(xi + i - 1, yi + j - 1);
+      v += kChromaFilter[fy][j] * t;
+    }
+    v >>= 6;
+  }
+  return clip_pixel((v + 32) >> 6);
+}
+
+// ------------------------------------ deblocking ----------------------------------------
+constexpr uint8_t kBetaTable[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,
+                                    0,  0,  0,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
+                                    16, 17, 18, 20, 22, 24, 26, 28, 30, 32, 34, 36, 38,
+                                    40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
+constexpr uint8_t kTcTable[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  0,
+                                  1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2,  2,  3,  3,  3,  3,  4,
+                                  4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
+
+// Luma deblocking of one 4-sample edge segment.  `p` points at sample p0 of line 0,
+// `step` is the distance p0->q0 direction (across the edge), `lstep` between lines.
+// Returns nothing; modifies samples in place.  bs in {1,2}, qp = (QpP+QpQ+1)>>1.
+TV_HD void deblock_luma_edge4(uint8_t* q0ptr, int xstep, int lstep, int bs, int qp) {
+  // q0ptr points at q0 of line 0; p_i = q0ptr[-(i+1)*xstep], q_i = q0ptr[i*xstep]
+  const int beta = kBetaTable[clip3(0, 51, qp)];
+  const int tc = kTcTable[clip3(0, 53, qp + 2 * (bs - 1))];
+  if (tc == 0) return;
+  auto P = [&](int line, int i) -> uint8_t& { return q0ptr[line * lstep - (i + 1) * xstep]; };
+  auto Q = [&](int line, int i) -> uint8_t& { return q0ptr[line * lstep + i * xstep]; };
+  const int dp0 = tv_abs(P(0, 2) - 2 * P(0, 1) + P(0, 0));
+  const int dp3 = tv_abs(P(3, 2) - 2 * P(3, 1) + P(3, 0));
+  const int dq0 = tv_abs(Q(0, 2) - 2 * Q(0, 1) + Q(0, 0));
+  const int dq3 = tv_abs(Q(3, 2) - 2 * Q(3, 1) + Q(3, 0));
+  const int dpq0 = dp0 + dq0, dpq3 = dp3 + dq3;
+  const int dp = dp0 + dp3, dq = dq0 + dq3;
+  const int d = dpq0 + dpq3;
+  if (d >= beta) return;
+  auto dsam = [&](int line, int dpq) -> bool {
+    return 2 * dpq < (beta >> 2) &&
+           tv_abs(P(line, 3) - P(line, 0)) + tv_abs(Q(line, 0) - Q(line, 3)) < (beta >> 3) &&
+           tv_abs(P(line, 0) - Q(line, 0)) < ((5 * tc + 1) >> 1);
+  };
+  const bool strong = dsam(0, dpq0) && dsam(3, dpq3);
+  const bool dEp = dp < ((beta + (beta >> 1)) >> 3);
+  const bool dEq = dq < ((beta + (beta >> 1)) >> 3);
+  for (int k = 0; k < 4; ++k) {
+    const int p0 = P(k, 0), p1 = P(k, 1), p2 = P(k, 2), p3 = P(k, 3);
+    const int q0 = Q(k, 0), q1 = Q(k, 1), q2 = Q(k, 2), q3 = Q(k, 3);
+    if (strong) {
+      P(k, 0) = (uint8_t)clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+      P(k, 1) = (uint8_t)clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2);
+      P(k, 2) = (uint8_t)clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+      Q(k, 0) = (uint8_t)clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+      Q(k, 1) = (uint8_t)clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2);
+      Q(k, 2) = (uint8_t)clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3);
+    } else {
+      int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
+      if (tv_abs(delta) < tc * 10) {
+        delta = clip3(-tc, tc, delta);
+        P(k, 0) = (uint8_t)clip_pixel(p0 + delta);
+        Q(k, 0) = (uint8_t)clip_pixel(q0 - delta);
+        if (dEp) {
+          int dP = clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1);
+          P(k, 1) = (uint8_t)clip_pixel(p1 + dP);
+        }
+        if (dEq) {
+          int dQ = clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1);
+          Q(k, 1) = (uint8_t)clip_pixel(q1 + dQ);
+        }
+      }
+    }
+  }
+}
+
+// Chroma deblocking of one edge segment of `len` lines (only for bs == 2).
+TV_HD void deblock_chroma_edge(uint8_t* q0ptr, int xstep, int lstep, int len, int qpc) {
+  const int tc = kTcTable[clip3(0, 53, qpc + 2)];
+  if (tc == 0) return;
+  for (int k = 0; k < len; ++k) {
+    uint8_t* q0p = q0ptr + k * lstep;
+    const int p0 = q0p[-xstep], p1 = q0p[-2 * xstep], q0 = q0p[0], q1 = q0p[xstep];
+    const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
+    q0p[-xstep] = (uint8_t)clip_pixel(p0 + delta);
+    q0p[0] = (uint8_t)clip_pixel(q0 - delta);
+  }
+}
+
+// ------------------------------------ scan orders ---------------------------------------
+// 4x4 up-right diagonal scan: position i -> (x, y) packed as x | y<<2
+constexpr uint8_t kScanDiag4x4[16] = {0, 4, 1, 8, 5, 2, 12, 9, 6, 3, 13, 10, 7, 14, 11, 15};
+constexpr uint8_t kScanHor4x4[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+constexpr uint8_t kScanVer4x4[16] = {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15};
+// 2x2 sub-block scans (for 8x8 TBs): packed x | y<<2
+constexpr uint8_t kScanDiag2x2[4] = {0, 4, 1, 5};
+constexpr uint8_t kScanHor2x2[4] = {0, 1, 4, 5};
+constexpr uint8_t kScanVer2x2[4] = {0, 4, 1, 5};
+// 8x8 diagonal sub-block scan (for 32x32 TBs): packed x | y<<3
+struct Scan8 {
+  uint8_t s[64];
+};
+constexpr Scan8 make_diag8() {
+  Scan8 r{};
+  int i = 0, x = 0, y = 0;
+  while (i < 64) {
+    while (y >= 0) {
+      if (x < 8 && y < 8) r.s[i++] = (uint8_t)(x | (y << 3));
+      --y;
+      ++x;
+    }
+    y = x;
+    x = 0;
+  }
+  return r;
+}
+constexpr Scan8 kScanDiag8x8 = make_diag8();
+// 4x4 diagonal sub-block scan for 16x16 TBs: packed x | y<<2 (same as kScanDiag4x4)
+
+// sub-block (xS,yS) of scan position i for a TB with log2 size L and scanIdx s
+TV_HD void subblock_pos(int log2N, int scanIdx, int i, int& xs, int& ys) {
+  if (log2N == 2) {
+    xs = ys = 0;
+  } else if (log2N == 3) {
+    const uint8_t v = scanIdx == 0 ? kScanDiag2x2[i] : (scanIdx == 1 ? kScanHor2x2[i] : kScanVer2x2[i]);
+    xs = v & 3;
+    ys = v >> 2;
+  } else if (log2N == 4) {
+    xs = kScanDiag4x4[i] & 3;
+    ys = kScanDiag4x4[i] >> 2;
+  } else {
+    xs = kScanDiag8x8.s[i] & 7;
+    ys = kScanDiag8x8.s[i] >> 3;
+  }
+}
+TV_HD void coef_pos_in_sb(int scanIdx, int n, int& x, int& y) {
+  const uint8_t v = scanIdx == 0 ? kScanDiag4x4[n] : (scanIdx == 1 ? kScanHor4x4[n] : kScanVer4x4[n]);
+  x = v & 3;
+  y = v >> 2;
+}
+
+// scanIdx (H.265 7.4.9.11): mode dependent for intra 4x4/8x8 luma, 4x4 chroma (4:2:0)
+TV_HD int scan_idx_for(bool intra, int log2TrafoSize, int cIdx, int predMode) {
+  if (!intra) return 0;
+  if (log2TrafoSize == 2 || (log2TrafoSize == 3 && cIdx == 0)) {
+    if (predMode >= 6 && predMode <= 14) return 2;
+    if (predMode >= 22 && predMode <= 30) return 1;
+  }
+  return 0;
+}
+
+// z-order index of a 4x4 unit inside a 32x32 CTB (x4,y4 in 0..7)
+TV_HD int zorder4(int x4, int y4) {
+  int z = 0;
+  for (int b = 0; b < 3; ++b) z |= (((x4 >> b) & 1) << (2 * b)) | (((y4 >> b) & 1) << (2 * b + 1));
+  return z;
+}
+
+// Availability of luma location (xN,yN) for the block at (xC,yC) (H.265 6.4.1), for a
+// picture with a single slice and no tiles.
+TV_HD bool zscan_available(int xC, int yC, int xN, int yN, int picW, int picH) {
+  if (xN < 0 || yN < 0 || xN >= picW || yN >= picH) return false;
+  const int wCtb = (picW + kCtb - 1) >> kCtbLog2;
+  const int aN = (yN >> kCtbLog2) * wCtb + (xN >> kCtbLog2);
+  const int aC = (yC >> kCtbLog2) * wCtb + (xC >> kCtbLog2);
+  if (aN != aC) return aN < aC;
+  const int zN = zorder4((xN & (kCtb - 1)) >> 2, (yN & (kCtb - 1)) >> 2);
+  const int zC = zorder4((xC & (kCtb - 1)) >> 2, (yC & (kCtb - 1)) >> 2);
+  return zN <= zC;
+}
+
+}  // namespace tv

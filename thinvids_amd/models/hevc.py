@@ -1,0 +1,188 @@
+"""HEVC codec "model" API: synthetic source, CPU reference encoder, decoder oracle,
+MP4 mux/demux — thin numpy wrappers over ``libtvcore.so``.
+
+Frames are ``(Y, U, V)`` tuples of uint8 numpy arrays (4:2:0, Y shape ``(H, W)``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from .._native import Bytes, check, core_lib, i16p, ptr
+
+Frame = tuple  # (Y, U, V)
+
+
+def coded_size(width: int, height: int, ctb: int = 32) -> tuple[int, int]:
+    return (width + ctb - 1) // ctb * ctb, (height + ctb - 1) // ctb * ctb
+
+
+def synth_frame(seed: int, t: int, width: int, height: int) -> Frame:
+    """Deterministic synthetic frame (same bytes as the GPU generator kernel)."""
+    y = np.empty((height, width), np.uint8)
+    u = np.empty((height // 2, width // 2), np.uint8)
+    v = np.empty_like(u)
+    core_lib().tv_synth_frame(seed & 0xFFFFFFFF, t, width, height, ptr(y), ptr(u), ptr(v))
+    return y, u, v
+
+
+def psnr(a: np.ndarray, b: np.ndarray) -> float:
+    mse = np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)
+    return float("inf") if mse == 0 else 10.0 * np.log10(255.0 ** 2 / mse)
+
+
+def psnr_yuv(ref: Frame, dec: Frame) -> dict:
+    py, pu, pv = (psnr(r, d) for r, d in zip(ref, dec))
+    return {"y": py, "u": pu, "v": pv, "yuv": (6 * py + pu + pv) / 8}
+
+
+class CpuEncoder:
+    """Scalar C++ HEVC encoder (software path; reference `software_encode`)."""
+
+    def __init__(self, width: int, height: int, qp: int = 27, deblock: bool = True,
+                 search_range: int = 8, max_merge: int = 5):
+        if width % 2 or height % 2:
+            raise ValueError("width/height must be even")
+        self.lib = core_lib()
+        self.width, self.height, self.qp = width, height, qp
+        self.cw, self.ch = coded_size(width, height)
+        self.h = self.lib.tv_cpu_encoder_new(width, height, qp, int(deblock), search_range, max_merge)
+        self.out = Bytes()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.tv_cpu_encoder_free(self.h)
+            self.h = None
+
+    def encode(self, frame: Frame, idr: bool, poc: int) -> bytes:
+        y, u, v = (np.ascontiguousarray(p) for p in frame)
+        self.out.clear()
+        check(self.lib.tv_cpu_encoder_encode(self.h, ptr(y), ptr(u), ptr(v), y.shape[1], u.shape[1],
+                                             int(idr), poc, self.out.h))
+        return self.out.tobytes()
+
+    def recon(self) -> Frame:
+        y = np.empty((self.ch, self.cw), np.uint8)
+        u = np.empty((self.ch // 2, self.cw // 2), np.uint8)
+        v = np.empty_like(u)
+        self.lib.tv_cpu_encoder_recon(self.h, ptr(y), ptr(u), ptr(v))
+        return y, u, v
+
+    def decisions(self) -> dict:
+        w8, h8 = self.cw // 8, self.ch // 8
+        d = {k: np.empty((h8, w8), np.uint8) for k in ("cu_log2", "intra", "ipm", "cbf")}
+        mv = np.empty((h8, w8, 2), np.int16)
+        self.lib.tv_cpu_encoder_decisions(self.h, ptr(d["cu_log2"]), ptr(d["intra"]), ptr(d["ipm"]),
+                                          ptr(mv, i16p), ptr(d["cbf"]))
+        d["mv"] = mv
+        return d
+
+
+def encode_sequence_cpu(frames, qp: int = 27, gop: int = 0, **kw) -> tuple[bytes, list]:
+    """Encode frames (first is IDR; IDR every `gop` frames if gop>0). Returns (annexb, recons)."""
+    frames = list(frames)
+    h, w = frames[0][0].shape
+    enc = CpuEncoder(w, h, qp=qp, **kw)
+    out, recons, poc = bytearray(), [], 0
+    for i, f in enumerate(frames):
+        idr = i == 0 or (gop > 0 and i % gop == 0)
+        poc = 0 if idr else poc + 1
+        out += enc.encode(f, idr, poc)
+        recons.append(enc.recon())
+    return bytes(out), recons
+
+
+@dataclass
+class DecodedStream:
+    width: int
+    height: int
+    coded_w: int
+    coded_h: int
+    frames: list  # cropped (Y, U, V)
+    coded_frames: list  # coded-size (Y, U, V)
+
+
+def decode(annexb: bytes, coded: bool = True) -> DecodedStream:
+    """Decode an Annex-B HEVC stream with the native decoder oracle."""
+    lib = core_lib()
+    h = lib.tv_decoder_new()
+    try:
+        buf = np.frombuffer(annexb, np.uint8)
+        check(lib.tv_decoder_decode(h, ptr(np.ascontiguousarray(buf)), len(annexb)))
+        w, hh, cw, ch, n = (C.c_int() for _ in range(5))
+        lib.tv_decoder_info(h, C.byref(w), C.byref(hh), C.byref(cw), C.byref(ch), C.byref(n))
+        frames, coded_frames = [], []
+        for i in range(n.value):
+            for crop, sink, (W, H) in ((1, frames, (w.value, hh.value)),
+                                       (0, coded_frames, (cw.value, ch.value))):
+                if crop == 0 and not coded:
+                    continue
+                y = np.empty((H, W), np.uint8)
+                u = np.empty((H // 2, W // 2), np.uint8)
+                v = np.empty_like(u)
+                check(lib.tv_decoder_frame(h, i, crop, ptr(y), ptr(u), ptr(v)))
+                sink.append((y, u, v))
+        return DecodedStream(w.value, hh.value, cw.value, ch.value, frames, coded_frames)
+    finally:
+        lib.tv_decoder_free(h)
+
+
+def write_frame(width: int, height: int, qp: int, idr: bool, poc: int, dec: dict,
+                coef: tuple, deblock: bool = True, max_merge: int = 5) -> bytes:
+    """Entropy-code one frame from decision arrays (cu_log2/intra/ipm/mv/cbf + coef planes)."""
+    lib = core_lib()
+    out = Bytes()
+    cy, cu, cv = (np.ascontiguousarray(c, dtype=np.int16) for c in coef)
+    check(lib.tv_write_frame(width, height, qp, int(deblock), max_merge, int(idr), poc,
+                             ptr(np.ascontiguousarray(dec["cu_log2"])), ptr(np.ascontiguousarray(dec["intra"])),
+                             ptr(np.ascontiguousarray(dec["ipm"])),
+                             ptr(np.ascontiguousarray(dec["mv"], dtype=np.int16), i16p),
+                             ptr(np.ascontiguousarray(dec["cbf"])), ptr(cy, i16p), ptr(cu, i16p),
+                             ptr(cv, i16p), out.h))
+    return out.tobytes()
+
+
+def reconstruct_reference(width: int, height: int, qp: int, src: Frame, ref: Frame | None,
+                          dec: dict, deblock: bool = True):
+    """Golden-model pass B: decisions -> (cbf, coef planes, recon) on the CPU."""
+    lib = core_lib()
+    cw, ch = coded_size(width, height)
+    cbf = np.zeros((ch // 8, cw // 8), np.uint8)
+    cy = np.zeros((ch, cw), np.int16)
+    cu = np.zeros((ch // 2, cw // 2), np.int16)
+    cv = np.zeros_like(cu)
+    ry = np.zeros((ch, cw), np.uint8)
+    ru = np.zeros((ch // 2, cw // 2), np.uint8)
+    rv = np.zeros_like(ru)
+    s = [np.ascontiguousarray(p) for p in src]
+    r = [np.ascontiguousarray(p) for p in ref] if ref is not None else None
+    null = C.cast(None, C.POINTER(C.c_uint8))
+    check(lib.tv_reconstruct_frame(
+        width, height, qp, int(deblock), ptr(s[0]), ptr(s[1]), ptr(s[2]),
+        ptr(r[0]) if r else null, ptr(r[1]) if r else null, ptr(r[2]) if r else null,
+        ptr(np.ascontiguousarray(dec["cu_log2"])), ptr(np.ascontiguousarray(dec["intra"])),
+        ptr(np.ascontiguousarray(dec["ipm"])), ptr(np.ascontiguousarray(dec["mv"], dtype=np.int16), i16p),
+        ptr(cbf), ptr(cy, i16p), ptr(cu, i16p), ptr(cv, i16p), ptr(ry), ptr(ru), ptr(rv)))
+    return cbf, (cy, cu, cv), (ry, ru, rv)
+
+
+def mux_mp4(annexb: bytes, width: int, height: int, fps_num: int = 30, fps_den: int = 1) -> bytes:
+    lib = core_lib()
+    out = Bytes()
+    buf = np.frombuffer(annexb, np.uint8).copy()
+    check(lib.tv_mux_mp4(ptr(buf), len(annexb), width, height, fps_num, fps_den, out.h))
+    return out.tobytes()
+
+
+def demux_mp4(data: bytes) -> dict:
+    lib = core_lib()
+    out = Bytes()
+    buf = np.frombuffer(data, np.uint8).copy()
+    w, h, n, ts, d = (C.c_int() for _ in range(5))
+    check(lib.tv_demux_mp4(ptr(buf), len(data), C.byref(w), C.byref(h), C.byref(n), C.byref(ts),
+                           C.byref(d), out.h))
+    return {"annexb": out.tobytes(), "width": w.value, "height": h.value, "frames": n.value,
+            "timescale": ts.value, "sample_delta": d.value,
+            "fps": ts.value / d.value if d.value else 0.0}
