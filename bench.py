@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: encoded frames/s (whole node) of the MI355X HEVC engine at fixed QP,
+reporting the resulting PSNR — BASELINE.json metric, configs #2 (1080p30 HEVC on one
+MI355X) and #3 (4K30 HEVC GOP-aligned segments data-parallel across GPUs).
+
+One step = every rank encodes `batch` GOP-aligned segments of `gop` synthetic frames
+(weak scaling: per-GPU work is fixed as N grows), then the encoded bitstreams are gathered
+to the stitch rank (rank 0) with RCCL point-to-point over xGMI and the rate/quality
+statistics are all-reduced — the intra-node data plane that replaces the reference's HTTP
+part upload to the stitcher (reference worker/tasks.py:1655-1674).
+
+    python bench.py --gpus N --steps K --warmup W [--res 1080p|4k] [--batch B] [--gop G]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "encoded frames/sec (whole node) at fixed PSNR, 1080p & 4K HEVC, 1/2/4/8 MI355X"
+RES = {"1080p": (1920, 1080), "4k": (3840, 2160), "720p": (1280, 720), "360p": (640, 360)}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--res", default="1080p", choices=sorted(RES))
+    ap.add_argument("--batch", type=int, default=0, help="segments per GPU per step (0 = auto)")
+    ap.add_argument("--gop", type=int, default=16, help="frames per GOP-aligned segment")
+    ap.add_argument("--qp", type=int, default=27)
+    ap.add_argument("--range", type=int, default=16)
+    ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=1)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from thinvids_amd.models.gpu_engine import GpuEngine
+    from thinvids_amd.parallel.comm import gather_bytes_to_root
+
+    w, h = RES[args.res]
+    batch = args.batch or (8 if args.res in ("1080p", "720p", "360p") else 4)
+    eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range,
+                    seed=args.seed, threads=args.threads or None, device=local)
+
+    def step(s: int):
+        base = (s * world + rank) * batch
+        segs = eng.encode_synthetic([(base + b) * args.gop for b in range(batch)])
+        sse = np.array([eng.sse(b) for b in range(batch)]).sum(0)
+        nbytes = sum(len(x) for x in segs)
+        stats = torch.tensor([batch * args.gop, nbytes, *sse], dtype=torch.float64, device=dev)
+        gathered = None
+        if world > 1:
+            dist.all_reduce(stats)  # rate-control / quality statistics
+            gathered = gather_bytes_to_root(b"".join(segs), dev)  # bitstreams -> stitch rank
+        return stats, gathered
+
+    for s in range(args.warmup):
+        step(-1 - s)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tot = None
+    for s in range(args.steps):
+        stats, _ = step(s)
+        tot = stats if tot is None else tot + stats
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    tot = tot.cpu().numpy()
+    frames = tot[0]
+    npx = frames * w * h
+    psnr = lambda s, n: float(10 * np.log10(255.0 ** 2 * n / s)) if s > 0 else float("inf")
+    py, pu, pv = psnr(tot[2], npx), psnr(tot[3], npx / 4), psnr(tot[4], npx / 4)
+    fps = frames / el
+    kbps = tot[1] * 8 / (frames / 30.0) / 1000.0 / world  # per 30 fps stream
+    if rank == 0:
+        gpu_ms, wall_ms = eng.timing()
+        print(json.dumps({
+            "metric": METRIC,
+            "value": round(fps, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * el / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8 video / int32 integer transforms (bit-exact HEVC)",
+            "data": "synthetic (seeded procedural YUV 4:2:0 source generated on GPU)",
+            "config": {
+                "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic",
+                "global_batch": world * batch,
+                "seq_len": args.gop,
+                "parallelism": f"dp{world}",
+                "resolution": f"{w}x{h}",
+                "segments_per_gpu": batch,
+                "frames_per_segment": args.gop,
+                "psnr_y_db": round(py, 3),
+                "psnr_yuv_db": round((6 * py + pu + pv) / 8, 3),
+                "kbps_per_30fps_stream": round(kbps, 1),
+                "last_step_gpu_ms": round(gpu_ms, 2),
+                "last_step_wall_ms": round(wall_ms, 2),
+            },
+        }), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -59,19 +59,7 @@ int block_satd(const uint8_t* src, int ss, const int* pred, int N) {
   return s;
 }
 
-int mv_bits(int dx, int dy) {  // rough bin count of an mvd pair
-  auto c = [](int d) {
-    int a = d < 0 ? -d : d;
-    if (a == 0) return 1;
-    int v = a + 1, n = 0;
-    while (v > 1) {
-      v >>= 1;
-      ++n;
-    }
-    return 2 * n + 1;
-  };
-  return c(dx) + c(dy);
-}
+int mv_bits(int dx, int dy) { return mv_bits_est(dx, dy); }
 
 }  // namespace
 

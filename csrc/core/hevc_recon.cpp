@@ -70,21 +70,8 @@ void recon_tb(const int16_t* levels, int ls, bool cbf, int log2N, int qp, const 
 }
 
 namespace {
-inline bool same_cu(const FrameData& fd, int xa, int ya, int xb, int yb) {
-  const int ua = (ya >> 3) * fd.w8 + (xa >> 3), ub = (yb >> 3) * fd.w8 + (xb >> 3);
-  const int sa = fd.cu_log2[ua], sb = fd.cu_log2[ub];
-  if (sa != sb) return false;
-  const int m = ~((1 << sa) - 1);
-  return (xa & m) == (xb & m) && (ya & m) == (yb & m);
-}
 inline int edge_bs(const FrameData& fd, int xp, int yp, int xq, int yq) {
-  if (same_cu(fd, xp, yp, xq, yq)) return 0;
-  const int up = (yp >> 3) * fd.w8 + (xp >> 3), uq = (yq >> 3) * fd.w8 + (xq >> 3);
-  if (fd.intra[up] || fd.intra[uq]) return 2;
-  if ((fd.cbf[up] & 1) || (fd.cbf[uq] & 1)) return 1;
-  if (tv_abs(fd.mv[2 * up] - fd.mv[2 * uq]) >= 4 || tv_abs(fd.mv[2 * up + 1] - fd.mv[2 * uq + 1]) >= 4)
-    return 1;
-  return 0;
+  return deblock_edge_bs(fd.cu_log2, fd.intra, fd.cbf, fd.mv, fd.w8, xp, yp, xq, yq);
 }
 }  // namespace
 

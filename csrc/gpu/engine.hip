@@ -1,0 +1,384 @@
+// engine.hip — native GPU encode engine for one MI355X (one process per GPU).
+//
+// Encodes a BATCH of B independent GOP-aligned segments in lock-step: frame f of every
+// segment is processed by the same kernel launches (B x CTUs workgroups per launch).
+// Per frame: synth/upload -> analysis -> reconstruction -> deblock -> SSE on one HIP
+// stream; the decision/level planes are copied into a ring of pinned host slots and a
+// CPU thread pool entropy-codes (CABAC) every (segment, frame) slice while the GPU moves
+// on — the serial entropy stage overlaps the parallel GPU stages.
+//
+// Replaces the per-part `encode` task's ffmpeg invocation (reference
+// worker/tasks.py:1532-1651); the control plane (worker/encode.py) drives this engine.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "k_encode.h"
+#include "tv/cpu_encoder.h"
+#include "tv/hevc_codec.h"
+
+#define HIP_OK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess)                                                                \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));               \
+  } while (0)
+
+namespace tv {
+namespace gpu {
+
+class ThreadPool {
+ public:
+  ThreadPool(int n, int device) {
+    for (int i = 0; i < n; ++i)
+      workers_.emplace_back([this, device] {
+        (void)hipSetDevice(device);
+        for (;;) {
+          std::function<void()> job;
+          {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+            if (stop_ && q_.empty()) return;
+            job = std::move(q_.front());
+            q_.pop_front();
+          }
+          job();
+        }
+      });
+  }
+  ~ThreadPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+  int size() const { return (int)workers_.size(); }
+
+ private:
+  std::vector<std::thread> workers_;
+  std::deque<std::function<void()>> q_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
+struct EngineCfg {
+  int width, height, qp, batch, gop, range, deblock, threads, device, max_merge;
+  uint32_t seed;
+};
+
+class Engine {
+ public:
+  explicit Engine(const EngineCfg& c) : cfg_(c), g_(make_geo(c.width, c.height)) {
+    if (c.batch < 1 || c.batch > kMaxBatch) throw std::runtime_error("batch must be 1..64");
+    if (c.range < 1 || c.range > 16) throw std::runtime_error("search range must be 1..16");
+    if ((c.width & 1) || (c.height & 1)) throw std::runtime_error("odd frame size");
+    HIP_OK(hipSetDevice(c.device));
+    HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    const long B = c.batch;
+    auto alloc_set = [&](FrameSet& f) {
+      HIP_OK(hipMalloc(&f.y, B * g_.ysz));
+      HIP_OK(hipMalloc(&f.u, B * g_.csz));
+      HIP_OK(hipMalloc(&f.v, B * g_.csz));
+    };
+    alloc_set(src_);
+    alloc_set(rec_[0]);
+    alloc_set(rec_[1]);
+    HIP_OK(hipMalloc(&dec_.cu_log2, B * g_.usz));
+    HIP_OK(hipMalloc(&dec_.intra, B * g_.usz));
+    HIP_OK(hipMalloc(&dec_.ipm, B * g_.usz));
+    HIP_OK(hipMalloc(&dec_.cbf, B * g_.usz));
+    HIP_OK(hipMalloc(&dec_.mv, B * g_.usz * 2 * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&dec_.coef_y, B * g_.ysz * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&dec_.coef_u, B * g_.csz * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&dec_.coef_v, B * g_.csz * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&d_sse_, B * 3 * sizeof(unsigned long long)));
+    slot_bytes_ = B * (4 * g_.usz + 2 * g_.usz * 2 + (g_.ysz + 2 * g_.csz) * 2);
+    for (int k = 0; k < kSlots; ++k) {
+      HIP_OK(hipHostMalloc(&slots_[k].host, slot_bytes_, hipHostMallocDefault));
+      HIP_OK(hipEventCreateWithFlags(&slots_[k].ev, hipEventDisableTiming));
+      slots_[k].pending = 0;
+    }
+    HIP_OK(hipEventCreate(&t0_));
+    HIP_OK(hipEventCreate(&t1_));
+    // penalties: identical integer rounding to the CPU reference encoder
+    const double lam = lambda_sad(c.qp);
+    pen_.mode_dcpl = (int)(lam * 2);
+    pen_.mode_ang = (int)(lam * 5);
+    pen_.split_intra = (int)(lam * 3);
+    pen_.split_inter = (int)(lam * 4);
+    for (int i = 0; i < 64; ++i) pen_.mv[i] = (int)(lam * i);
+    seq_.width = c.width;
+    seq_.height = c.height;
+    seq_.qp = c.qp;
+    seq_.deblock = c.deblock != 0;
+    seq_.max_merge_cand = c.max_merge;
+    seq_.finalize();
+    pool_ = std::make_unique<ThreadPool>(c.threads, c.device);
+  }
+
+  ~Engine() {
+    pool_.reset();
+    (void)hipStreamSynchronize(stream_);
+    for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u,
+                    rec_[1].v, dec_.cu_log2, dec_.intra, dec_.ipm, dec_.cbf})
+      (void)hipFree(p);
+    (void)hipFree(dec_.mv);
+    (void)hipFree(dec_.coef_y);
+    (void)hipFree(dec_.coef_u);
+    (void)hipFree(dec_.coef_v);
+    (void)hipFree(d_sse_);
+    for (auto& s : slots_) {
+      (void)hipHostFree(s.host);
+      (void)hipEventDestroy(s.ev);
+    }
+    (void)hipEventDestroy(t0_);
+    (void)hipEventDestroy(t1_);
+    (void)hipStreamDestroy(stream_);
+  }
+
+  // Encode nseg segments of the synthetic source: segment b = frames [starts[b], +gop).
+  void encode_synth(const int* starts, int nseg) {
+    run(nseg, [&](int f, int B) {
+      FrameIdx fi{};
+      for (int b = 0; b < B; ++b) fi.t[b] = starts[b] + f;
+      launch_synth(src_, g_, cfg_.seed, fi, B, stream_);
+    });
+  }
+
+  // Encode nseg segments from host frames, coded-size planar I420 laid out
+  // [segment][frame][Y | U | V] (planes padded to the coded size by the caller).
+  void encode_host(const uint8_t* frames, int nseg) {
+    const long fsz = g_.ysz + 2 * g_.csz;
+    run(nseg, [&](int f, int B) {
+      for (int b = 0; b < B; ++b) {
+        const uint8_t* p = frames + ((long)b * cfg_.gop + f) * fsz;
+        HIP_OK(hipMemcpyAsync(src_.y + b * g_.ysz, p, g_.ysz, hipMemcpyHostToDevice, stream_));
+        HIP_OK(hipMemcpyAsync(src_.u + b * g_.csz, p + g_.ysz, g_.csz, hipMemcpyHostToDevice, stream_));
+        HIP_OK(hipMemcpyAsync(src_.v + b * g_.csz, p + g_.ysz + g_.csz, g_.csz, hipMemcpyHostToDevice,
+                              stream_));
+      }
+    });
+  }
+
+  const std::vector<uint8_t>& segment(int b) const { return out_.at(b); }
+  double sse(int b, int c) const { return sse_host_[b * 3 + c]; }
+  double gpu_ms() const { return gpu_ms_; }
+  double wall_ms() const { return wall_ms_; }
+  const Geo& geo() const { return g_; }
+  // device pointers of the current reconstruction (last frame) for tests
+  FrameSet last_recon() const { return rec_[(cfg_.gop - 1) & 1]; }
+  DecisionSet decisions() const { return dec_; }
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  static constexpr int kSlots = 4;
+  struct Slot {
+    uint8_t* host = nullptr;
+    hipEvent_t ev{};
+    std::atomic<int> pending{0};
+  };
+
+  // host view of segment b's decisions in a slot
+  FrameData slot_view(const Slot& s, int b, int B) const {
+    const long U = g_.usz;
+    uint8_t* p = s.host;
+    FrameData f;
+    f.w8 = g_.w8;
+    f.h8 = g_.h8;
+    f.cu_log2 = p + b * U;
+    p += B * U;
+    f.intra = p + b * U;
+    p += B * U;
+    f.ipm = p + b * U;
+    p += B * U;
+    f.cbf = p + b * U;
+    p += B * U;
+    f.mv = reinterpret_cast<const int16_t*>(p) + b * U * 2;
+    p += B * U * 4;
+    f.coef[0] = reinterpret_cast<const int16_t*>(p) + b * g_.ysz;
+    p += B * g_.ysz * 2;
+    f.coef[1] = reinterpret_cast<const int16_t*>(p) + b * g_.csz;
+    p += B * g_.csz * 2;
+    f.coef[2] = reinterpret_cast<const int16_t*>(p) + b * g_.csz;
+    return f;
+  }
+
+  void copy_out(Slot& s, int B) {
+    const long U = g_.usz;
+    uint8_t* p = s.host;
+    auto cp = [&](void* d, long n) {
+      HIP_OK(hipMemcpyAsync(p, d, n, hipMemcpyDeviceToHost, stream_));
+      p += n;
+    };
+    cp(dec_.cu_log2, B * U);
+    cp(dec_.intra, B * U);
+    cp(dec_.ipm, B * U);
+    cp(dec_.cbf, B * U);
+    cp(dec_.mv, B * U * 4);
+    cp(dec_.coef_y, B * g_.ysz * 2);
+    cp(dec_.coef_u, B * g_.csz * 2);
+    cp(dec_.coef_v, B * g_.csz * 2);
+    HIP_OK(hipEventRecord(s.ev, stream_));
+  }
+
+  template <class Upload> void run(int nseg, Upload&& upload) {
+    if (nseg < 1 || nseg > cfg_.batch) throw std::runtime_error("nseg out of range");
+    const int B = nseg, F = cfg_.gop;
+    const auto w0 = std::chrono::steady_clock::now();
+    out_.assign(B, {});
+    std::vector<std::vector<std::vector<uint8_t>>> slices(B, std::vector<std::vector<uint8_t>>(F));
+    std::atomic<int> failed{0};
+    std::string err;
+    std::mutex err_mu;
+    HIP_OK(hipMemsetAsync(d_sse_, 0, B * 3 * sizeof(unsigned long long), stream_));
+    HIP_OK(hipEventRecord(t0_, stream_));
+    for (int f = 0; f < F; ++f) {
+      upload(f, B);
+      FrameSet cur = rec_[f & 1], prev = rec_[(f + 1) & 1];
+      if (f == 0) launch_intra_frame(src_, cur, dec_, g_, cfg_.qp, pen_, B, stream_);
+      else launch_inter_frame(src_, prev, cur, dec_, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
+      if (cfg_.deblock) launch_deblock(cur, dec_, g_, cfg_.qp, B, stream_);
+      launch_sse(src_, cur, g_, d_sse_, B, stream_);
+      HIP_OK(hipGetLastError());
+      Slot& s = slots_[f % kSlots];
+      while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+      copy_out(s, B);
+      s.pending.store(B, std::memory_order_release);
+      for (int b = 0; b < B; ++b) {
+        pool_->submit([this, &s, b, B, f, &slices, &failed, &err, &err_mu] {
+          try {
+            HIP_OK(hipEventSynchronize(s.ev));
+            write_slice(seq_, slot_view(s, b, B), f, f == 0, slices[b][f]);
+          } catch (const std::exception& e) {
+            std::lock_guard<std::mutex> lk(err_mu);
+            err = e.what();
+            failed = 1;
+          }
+          s.pending.fetch_sub(1, std::memory_order_acq_rel);
+        });
+      }
+    }
+    HIP_OK(hipEventRecord(t1_, stream_));
+    for (auto& s : slots_)
+      while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    HIP_OK(hipStreamSynchronize(stream_));
+    if (failed) throw std::runtime_error("entropy coding failed: " + err);
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, t0_, t1_));
+    gpu_ms_ = ms;
+    std::vector<unsigned long long> sse(B * 3);
+    HIP_OK(hipMemcpy(sse.data(), d_sse_, B * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    sse_host_.assign(sse.begin(), sse.end());
+    for (int b = 0; b < B; ++b) {
+      write_parameter_sets(seq_, out_[b]);
+      for (int f = 0; f < F; ++f) out_[b].insert(out_[b].end(), slices[b][f].begin(), slices[b][f].end());
+    }
+    wall_ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+  }
+
+  EngineCfg cfg_;
+  Geo g_;
+  SeqConfig seq_;
+  Penalties pen_{};
+  hipStream_t stream_{};
+  FrameSet src_{}, rec_[2]{};
+  DecisionSet dec_{};
+  unsigned long long* d_sse_ = nullptr;
+  Slot slots_[kSlots];
+  long slot_bytes_ = 0;
+  hipEvent_t t0_{}, t1_{};
+  std::unique_ptr<ThreadPool> pool_;
+  std::vector<std::vector<uint8_t>> out_;
+  std::vector<double> sse_host_;
+  double gpu_ms_ = 0, wall_ms_ = 0;
+};
+
+}  // namespace gpu
+}  // namespace tv
+
+// ------------------------------------- C API --------------------------------------------
+namespace {
+thread_local std::string g_gpu_err;
+template <class F> int gguard(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_gpu_err = e.what();
+    return -1;
+  }
+}
+}  // namespace
+
+extern "C" {
+const char* tv_gpu_last_error() { return g_gpu_err.c_str(); }
+
+int tv_gpu_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void* tv_engine_new(int width, int height, int qp, int batch, int gop, int range, int deblock,
+                    uint32_t seed, int threads, int device, int max_merge) {
+  void* r = nullptr;
+  gguard([&] {
+    tv::gpu::EngineCfg c{width, height, qp, batch, gop, range, deblock, threads, device, max_merge, seed};
+    r = new tv::gpu::Engine(c);
+  });
+  return r;
+}
+void tv_engine_free(void* e) { delete static_cast<tv::gpu::Engine*>(e); }
+int tv_engine_encode_synth(void* e, const int* starts, int nseg) {
+  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_synth(starts, nseg); });
+}
+int tv_engine_encode_host(void* e, const uint8_t* frames, int nseg) {
+  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_host(frames, nseg); });
+}
+size_t tv_engine_segment_size(void* e, int b) { return static_cast<tv::gpu::Engine*>(e)->segment(b).size(); }
+void tv_engine_segment_copy(void* e, int b, uint8_t* dst) {
+  const auto& v = static_cast<tv::gpu::Engine*>(e)->segment(b);
+  std::memcpy(dst, v.data(), v.size());
+}
+void tv_engine_sse(void* e, int b, double* out3) {
+  for (int c = 0; c < 3; ++c) out3[c] = static_cast<tv::gpu::Engine*>(e)->sse(b, c);
+}
+void tv_engine_timing(void* e, double* gpu_ms, double* wall_ms) {
+  *gpu_ms = static_cast<tv::gpu::Engine*>(e)->gpu_ms();
+  *wall_ms = static_cast<tv::gpu::Engine*>(e)->wall_ms();
+}
+// copy the last frame's coded-size reconstruction of segment b (tests)
+int tv_engine_last_recon(void* e, int b, uint8_t* y, uint8_t* u, uint8_t* v) {
+  return gguard([&] {
+    auto* E = static_cast<tv::gpu::Engine*>(e);
+    const auto& g = E->geo();
+    auto r = E->last_recon();
+    HIP_OK(hipMemcpy(y, r.y + b * g.ysz, g.ysz, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(u, r.u + b * g.csz, g.csz, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(v, r.v + b * g.csz, g.csz, hipMemcpyDeviceToHost));
+  });
+}
+}

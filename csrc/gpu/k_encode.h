@@ -1,0 +1,32 @@
+// k_encode.h — host-visible declarations of the encode-pipeline kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gpu_common.h"
+
+namespace tv {
+namespace gpu {
+
+constexpr int kMaxBatch = 64;
+
+struct FrameIdx {
+  int t[kMaxBatch];  // source frame index per segment
+};
+
+// Integer rate penalties (lambda * bits) precomputed on the host exactly like the CPU
+// reference encoder computes them, so GPU and CPU decisions agree.
+struct Penalties {
+  int mode_dcpl, mode_ang, split_intra, split_inter;
+  int mv[64];
+};
+
+void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi, int B, hipStream_t s);
+void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s);
+void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, int qp,
+                        const Penalties& pen, int B, hipStream_t s);
+void launch_inter_frame(FrameSet src, FrameSet ref, FrameSet rec, DecisionSet dec, const Geo& g,
+                        int qp, const Penalties& pen, int range, int B, hipStream_t s);
+void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s);
+
+}  // namespace gpu
+}  // namespace tv

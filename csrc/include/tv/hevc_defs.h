@@ -143,65 +143,59 @@ constexpr int8_t kIntraPredAngle[35] = {0,   0,   32,  26,  21,  17,  13,  9,  5
 constexpr int16_t kInvAngle[15] = {-4096, -1638, -910, -630, -482, -390, -315, -256,
                                    -315,  -390,  -482, -630, -910, -1638, -4096};
 
-// Intra prediction of an N x N block from its (already substituted) reference samples.
-//   left[i]  = p[-1][i-1] for i = 0..2N   (left[0] = corner p[-1][-1])
-//   top[i]   = p[i-1][-1] for i = 0..2N   (top[0]  = corner)
-// `filter_edges` enables the DC/H/V boundary smoothing (luma, N < 32).
-// Output pred[y*N+x].
+// One intra-predicted sample at (x, y) of an N x N block from its (already substituted,
+// optionally smoothed) reference samples:
+//   left[i] = p[-1][i-1] for i = 0..2N   (left[0] = corner p[-1][-1])
+//   top[i]  = p[i-1][-1] for i = 0..2N   (top[0]  = corner)
+// `dc` is the DC value of the block (only used by mode 1), `fe` enables the DC/H/V boundary
+// smoothing (luma, N < 32).  Used per lane by the HIP kernels and per block on the CPU.
+template <typename R>
+TV_HD int intra_pred_pixel(const R* left, const R* top, int log2N, int mode, bool fe, int dc, int x,
+                           int y) {
+  const int N = 1 << log2N;
+  if (mode == 0)
+    return ((N - 1 - x) * left[y + 1] + (x + 1) * top[N + 1] + (N - 1 - y) * top[x + 1] +
+            (y + 1) * left[N + 1] + N) >> (log2N + 1);
+  if (mode == 1) {
+    if (fe) {
+      if (x == 0 && y == 0) return (left[1] + 2 * dc + top[1] + 2) >> 2;
+      if (y == 0) return (top[x + 1] + 3 * dc + 2) >> 2;
+      if (x == 0) return (left[y + 1] + 3 * dc + 2) >> 2;
+    }
+    return dc;
+  }
+  const int angle = kIntraPredAngle[mode];
+  const bool vert = mode >= 18;
+  const R* mainr = vert ? top : left;
+  const R* side = vert ? left : top;
+  const int i = vert ? x : y, j = vert ? y : x;
+  const int pos = (j + 1) * angle;
+  const int idx = pos >> 5, fact = pos & 31;
+  const int inv = angle < 0 ? kInvAngle[mode - 11] : 0;
+  auto ref = [&](int k) -> int { return k >= 0 ? (int)mainr[k] : (int)side[(k * inv + 128) >> 8]; };
+  int v = fact ? ((32 - fact) * ref(i + idx + 1) + fact * ref(i + idx + 2) + 16) >> 5 : ref(i + idx + 1);
+  if (fe) {
+    if (mode == 26 && x == 0) v = clip_pixel(top[1] + ((left[y + 1] - left[0]) >> 1));
+    else if (mode == 10 && y == 0) v = clip_pixel(left[1] + ((top[x + 1] - top[0]) >> 1));
+  }
+  return v;
+}
+
+template <typename R> TV_HD int intra_dc_value(const R* left, const R* top, int log2N) {
+  const int N = 1 << log2N;
+  int s = N;
+  for (int i = 0; i < N; ++i) s += top[i + 1] + left[i + 1];
+  return s >> (log2N + 1);
+}
+
+// Whole-block intra prediction (CPU path), pred[y*N+x].
 TV_HD void intra_pred_from_refs(const int* left, const int* top, int log2N, int mode,
                                 bool filter_edges, int* pred) {
   const int N = 1 << log2N;
-  if (mode == 0) {  // planar
-    for (int y = 0; y < N; ++y)
-      for (int x = 0; x < N; ++x)
-        pred[y * N + x] = ((N - 1 - x) * left[y + 1] + (x + 1) * top[N + 1] +
-                           (N - 1 - y) * top[x + 1] + (y + 1) * left[N + 1] + N) >>
-                          (log2N + 1);
-    return;
-  }
-  if (mode == 1) {  // DC
-    int s = N;
-    for (int i = 0; i < N; ++i) s += top[i + 1] + left[i + 1];
-    const int dc = s >> (log2N + 1);
-    for (int i = 0; i < N * N; ++i) pred[i] = dc;
-    if (filter_edges) {
-      pred[0] = (left[1] + 2 * dc + top[1] + 2) >> 2;
-      for (int x = 1; x < N; ++x) pred[x] = (top[x + 1] + 3 * dc + 2) >> 2;
-      for (int y = 1; y < N; ++y) pred[y * N] = (left[y + 1] + 3 * dc + 2) >> 2;
-    }
-    return;
-  }
-  const int angle = kIntraPredAngle[mode];
-  int refbuf[3 * 32 + 2];
-  int* ref = refbuf + 32;  // ref[-N..2N]
-  const bool vert = mode >= 18;
-  const int* mainr = vert ? top : left;
-  const int* side = vert ? left : top;
-  for (int x = 0; x <= N; ++x) ref[x] = mainr[x];
-  if (angle < 0) {
-    const int inv = kInvAngle[mode - 11];
-    const int lastx = (N * angle) >> 5;
-    if (lastx < -1)
-      for (int x = lastx; x <= -1; ++x) ref[x] = side[((x * inv + 128) >> 8)];
-  } else {
-    for (int x = N + 1; x <= 2 * N; ++x) ref[x] = mainr[x];
-  }
-  for (int j = 0; j < N; ++j) {  // j = distance along the prediction direction
-    const int pos = (j + 1) * angle;
-    const int idx = pos >> 5, fact = pos & 31;
-    for (int i = 0; i < N; ++i) {
-      int v = fact ? ((32 - fact) * ref[i + idx + 1] + fact * ref[i + idx + 2] + 16) >> 5
-                   : ref[i + idx + 1];
-      if (vert) pred[j * N + i] = v;
-      else pred[i * N + j] = v;
-    }
-  }
-  if (filter_edges) {
-    if (mode == 26)
-      for (int y = 0; y < N; ++y) pred[y * N] = clip_pixel(top[1] + ((left[y + 1] - left[0]) >> 1));
-    else if (mode == 10)
-      for (int x = 0; x < N; ++x) pred[x] = clip_pixel(left[1] + ((top[x + 1] - top[0]) >> 1));
-  }
+  const int dc = mode == 1 ? intra_dc_value(left, top, log2N) : 0;
+  for (int y = 0; y < N; ++y)
+    for (int x = 0; x < N; ++x)
+      pred[y * N + x] = intra_pred_pixel(left, top, log2N, mode, filter_edges, dc, x, y);
 }
 
 // [1 2 1] reference smoothing decision (H.265 8.4.4.2.3), luma only, no strong smoothing.
@@ -414,6 +408,42 @@ TV_HD void deblock_chroma_edge(uint8_t* q0ptr, int xstep, int lstep, int len, in
     q0p[-xstep] = (uint8_t)clip_pixel(p0 + delta);
     q0p[0] = (uint8_t)clip_pixel(q0 - delta);
   }
+}
+
+// Boundary strength of the deblocking edge between luma positions P and Q (H.265 8.7.2.4)
+// for this engine's structure (TB = PU = CU, one reference picture).  Arrays are the
+// per-8x8-unit decision planes (see hevc_codec.h).  Returns 0 for edges inside a CU.
+TV_HD int deblock_edge_bs(const uint8_t* cu_log2, const uint8_t* intra, const uint8_t* cbf,
+                          const int16_t* mv, int w8, int xp, int yp, int xq, int yq) {
+  const int up = (yp >> 3) * w8 + (xp >> 3), uq = (yq >> 3) * w8 + (xq >> 3);
+  const int sp = cu_log2[up], sq = cu_log2[uq];
+  if (sp == sq) {
+    const int m = ~((1 << sp) - 1);
+    if ((xp & m) == (xq & m) && (yp & m) == (yq & m)) return 0;
+  }
+  if (intra[up] || intra[uq]) return 2;
+  if ((cbf[up] & 1) || (cbf[uq] & 1)) return 1;
+  if (tv_abs(mv[2 * up] - mv[2 * uq]) >= 4 || tv_abs(mv[2 * up + 1] - mv[2 * uq + 1]) >= 4) return 1;
+  return 0;
+}
+
+// Rough bin count of an mvd pair (encoder cost model; CPU and GPU use the same).
+TV_HD int mv_bits_est(int dx, int dy) {
+  int bits = 0;
+  for (int c = 0; c < 2; ++c) {
+    int a = tv_abs(c ? dy : dx);
+    if (a == 0) {
+      bits += 1;
+      continue;
+    }
+    int v = a + 1, n = 0;
+    while (v > 1) {
+      v >>= 1;
+      ++n;
+    }
+    bits += 2 * n + 1;
+  }
+  return bits;
 }
 
 // ------------------------------------ scan orders ---------------------------------------

@@ -1,0 +1,136 @@
+"""GPU encode engine (libtvgpu.so): batched HEVC encoding of GOP-aligned segments on one
+MI355X.  One instance per process/GPU; see csrc/gpu/engine.hip.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .._native import gpu_lib, ptr
+from .hevc import coded_size
+
+_sigs_done = False
+
+
+def _lib():
+    global _sigs_done
+    lib = gpu_lib()
+    if not _sigs_done:
+        vp = C.c_void_p
+        lib.tv_gpu_last_error.restype = C.c_char_p
+        lib.tv_gpu_device_count.restype = C.c_int
+        lib.tv_engine_new.restype = vp
+        lib.tv_engine_new.argtypes = [C.c_int] * 7 + [C.c_uint32, C.c_int, C.c_int, C.c_int]
+        lib.tv_engine_free.argtypes = [vp]
+        lib.tv_engine_encode_synth.restype = C.c_int
+        lib.tv_engine_encode_synth.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
+        lib.tv_engine_encode_host.restype = C.c_int
+        lib.tv_engine_encode_host.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int]
+        lib.tv_engine_segment_size.restype = C.c_size_t
+        lib.tv_engine_segment_size.argtypes = [vp, C.c_int]
+        lib.tv_engine_segment_copy.argtypes = [vp, C.c_int, C.POINTER(C.c_uint8)]
+        lib.tv_engine_sse.argtypes = [vp, C.c_int, C.POINTER(C.c_double)]
+        lib.tv_engine_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        lib.tv_engine_last_recon.restype = C.c_int
+        lib.tv_engine_last_recon.argtypes = [vp, C.c_int] + [C.POINTER(C.c_uint8)] * 3
+        _sigs_done = True
+    return lib
+
+
+def device_count() -> int:
+    return _lib().tv_gpu_device_count()
+
+
+def default_threads() -> int:
+    env = os.environ.get("TV_THREADS")
+    if env:
+        return max(1, int(env))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 4
+    return max(2, min(16, n))
+
+
+class GpuEngine:
+    def __init__(self, width: int, height: int, qp: int = 27, batch: int = 8, gop: int = 16,
+                 search_range: int = 16, deblock: bool = True, seed: int = 1, threads: int | None = None,
+                 device: int = 0, max_merge: int = 5):
+        self.lib = _lib()
+        self.width, self.height, self.qp = width, height, qp
+        self.batch, self.gop = batch, gop
+        self.cw, self.ch = coded_size(width, height)
+        self.h = self.lib.tv_engine_new(width, height, qp, batch, gop, search_range, int(deblock),
+                                        seed & 0xFFFFFFFF, threads or default_threads(), device, max_merge)
+        if not self.h:
+            raise RuntimeError("GPU engine init failed: " + self.lib.tv_gpu_last_error().decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tv_engine_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RuntimeError(self.lib.tv_gpu_last_error().decode())
+
+    def encode_synthetic(self, starts) -> list[bytes]:
+        """Encode len(starts) segments; segment b = synthetic frames [starts[b], starts[b]+gop)."""
+        arr = (C.c_int * len(starts))(*[int(s) for s in starts])
+        self._check(self.lib.tv_engine_encode_synth(self.h, arr, len(starts)))
+        return [self.segment(b) for b in range(len(starts))]
+
+    def encode_frames(self, segments) -> list[bytes]:
+        """segments: list (<= batch) of lists of gop frames (Y, U, V) at display size."""
+        fsz = self.cw * self.ch * 3 // 2
+        buf = np.empty((len(segments), self.gop, fsz), np.uint8)
+        for b, seg in enumerate(segments):
+            if len(seg) != self.gop:
+                raise ValueError("every segment must have exactly `gop` frames")
+            for f, (y, u, v) in enumerate(seg):
+                buf[b, f] = pad_frame(y, u, v, self.cw, self.ch)
+        self._check(self.lib.tv_engine_encode_host(self.h, ptr(buf), len(segments)))
+        return [self.segment(b) for b in range(len(segments))]
+
+    def segment(self, b: int) -> bytes:
+        n = self.lib.tv_engine_segment_size(self.h, b)
+        out = np.empty(n, np.uint8)
+        self.lib.tv_engine_segment_copy(self.h, b, ptr(out))
+        return out.tobytes()
+
+    def sse(self, b: int) -> tuple[float, float, float]:
+        a = (C.c_double * 3)()
+        self.lib.tv_engine_sse(self.h, b, a)
+        return a[0], a[1], a[2]
+
+    def psnr(self, b: int) -> dict:
+        y, u, v = self.sse(b)
+        npx = self.width * self.height * self.gop
+        f = lambda s, n: float("inf") if s == 0 else 10 * np.log10(255.0 ** 2 * n / s)
+        py, pu, pv = f(y, npx), f(u, npx / 4), f(v, npx / 4)
+        return {"y": py, "u": pu, "v": pv, "yuv": (6 * py + pu + pv) / 8}
+
+    def timing(self) -> tuple[float, float]:
+        g, w = C.c_double(), C.c_double()
+        self.lib.tv_engine_timing(self.h, C.byref(g), C.byref(w))
+        return g.value, w.value
+
+    def last_recon(self, b: int):
+        y = np.empty((self.ch, self.cw), np.uint8)
+        u = np.empty((self.ch // 2, self.cw // 2), np.uint8)
+        v = np.empty_like(u)
+        self._check(self.lib.tv_engine_last_recon(self.h, b, ptr(y), ptr(u), ptr(v)))
+        return y, u, v
+
+
+def pad_frame(y, u, v, cw, ch) -> np.ndarray:
+    """Edge-replicate a display-size I420 frame to the coded size; returns flat Y|U|V."""
+    h, w = y.shape
+    Y = np.pad(y, ((0, ch - h), (0, cw - w)), mode="edge")
+    U = np.pad(u, ((0, ch // 2 - h // 2), (0, cw // 2 - w // 2)), mode="edge")
+    V = np.pad(v, ((0, ch // 2 - h // 2), (0, cw // 2 - w // 2)), mode="edge")
+    return np.concatenate([Y.ravel(), U.ravel(), V.ravel()])

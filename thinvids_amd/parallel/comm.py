@@ -1,0 +1,89 @@
+"""Intra-node communication for the encode data plane (SURVEY.md §2.2 COMM, §5.8).
+
+The reference moves segment bytes with HTTP GET/PUT between worker hosts
+(reference worker/tasks.py:663-806, :1497-1525, :1655-1674).  Inside one MI355X node
+the same transfers are RCCL collectives over xGMI (`torch.distributed` backend "nccl" is
+RCCL on ROCm), one process per GPU:
+
+* ``gather_bytes_to_root`` — variable-length bitstream gather to the stitch rank:
+  all_gather of int64 sizes, then grouped point-to-point send/recv (one hop per peer on
+  the fully connected xGMI mesh; no ring).
+* ``scatter_frames_from_root`` — GOP scatter from the ingest rank with grouped sends.
+* ``allreduce_stats`` — small latency-bound all-reduce of rate-control statistics.
+
+The same functions run on the ``gloo`` backend with CPU tensors (tests, world_size > 1).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _world():
+    if not dist.is_available() or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(), dist.get_rank()
+
+
+def gather_bytes_to_root(payload: bytes, device: torch.device, root: int = 0):
+    """Gather one byte string from every rank to `root`.  Returns list[bytes] on root, None
+    elsewhere."""
+    world, rank = _world()
+    if world == 1:
+        return [payload]
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=device)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    if rank == root:
+        bufs = [torch.empty(max(1, sizes[r]), dtype=torch.uint8, device=device) for r in range(world)]
+        ops = [dist.P2POp(dist.irecv, bufs[r], r) for r in range(world) if r != root and sizes[r] > 0]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        out = []
+        for r in range(world):
+            if r == root:
+                out.append(payload)
+            else:
+                out.append(bytes(bufs[r][: sizes[r]].cpu().numpy().tobytes()) if sizes[r] else b"")
+        return out
+    if len(payload):
+        t = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
+        for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, root)]):
+            req.wait()
+    return None
+
+
+def scatter_frames_from_root(frames: list | None, shape: tuple, device: torch.device, root: int = 0):
+    """Scatter one uint8 tensor of `shape` per rank from `root` (GOP frames of a segment).
+    `frames` (root only) is a list of world tensors/arrays."""
+    world, rank = _world()
+    out = torch.empty(shape, dtype=torch.uint8, device=device)
+    if world == 1:
+        out.copy_(torch.as_tensor(np.asarray(frames[0])))
+        return out
+    if rank == root:
+        ops = []
+        for r in range(world):
+            t = torch.as_tensor(np.asarray(frames[r])).to(device)
+            if r == root:
+                out.copy_(t)
+            else:
+                ops.append(dist.P2POp(dist.isend, t.contiguous(), r))
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    else:
+        for req in dist.batch_isend_irecv([dist.P2POp(dist.irecv, out, root)]):
+            req.wait()
+    return out
+
+
+def allreduce_stats(values, device: torch.device, op: str = "sum") -> np.ndarray:
+    """All-reduce a small float64 vector (e.g. per-segment complexity for 2-pass RC)."""
+    t = torch.as_tensor(np.asarray(values, dtype=np.float64), device=device)
+    world, _ = _world()
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
+    return t.cpu().numpy()
