@@ -41,11 +41,13 @@ void tv_bytes_clear(void* b) { static_cast<Bytes*>(b)->v.clear(); }
 
 // ------------------------------------ synthetic source ----------------------------------
 void tv_synth_frame(uint32_t seed, int t, int W, int H, uint8_t* y, uint8_t* u, uint8_t* v) {
+  SynthFrameCtx ctx;
+  synth_frame_ctx(seed, t, W, H, ctx);
   for (int c = 0; c < 3; ++c) {
     uint8_t* P = c == 0 ? y : (c == 1 ? u : v);
     const int w = c ? W / 2 : W, h = c ? H / 2 : H;
     for (int j = 0; j < h; ++j)
-      for (int i = 0; i < w; ++i) P[(size_t)j * w + i] = (uint8_t)synth_sample(seed, t, c, i, j, W, H);
+      for (int i = 0; i < w; ++i) P[(size_t)j * w + i] = (uint8_t)synth_sample_ctx(ctx, c, i, j);
   }
 }
 

@@ -93,7 +93,8 @@ class Engine {
  public:
   explicit Engine(const EngineCfg& c) : cfg_(c), g_(make_geo(c.width, c.height)) {
     if (c.batch < 1 || c.batch > kMaxBatch) throw std::runtime_error("batch must be 1..64");
-    if (c.range < 1 || c.range > 16) throw std::runtime_error("search range must be 1..16");
+    if (c.range < 4 || c.range > 16 || (c.range & 3))
+      throw std::runtime_error("search range must be 4, 8, 12 or 16");
     if ((c.width & 1) || (c.height & 1)) throw std::runtime_error("odd frame size");
     HIP_OK(hipSetDevice(c.device));
     HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -115,6 +116,7 @@ class Engine {
     HIP_OK(hipMalloc(&dec_.coef_u, B * g_.csz * sizeof(int16_t)));
     HIP_OK(hipMalloc(&dec_.coef_v, B * g_.csz * sizeof(int16_t)));
     HIP_OK(hipMalloc(&d_sse_, B * 3 * sizeof(unsigned long long)));
+    HIP_OK(hipMalloc(&phase_, B * 16 * g_.psz));
     slot_bytes_ = B * (4 * g_.usz + 2 * g_.usz * 2 + (g_.ysz + 2 * g_.csz) * 2);
     for (int k = 0; k < kSlots; ++k) {
       HIP_OK(hipHostMalloc(&slots_[k].host, slot_bytes_, hipHostMallocDefault));
@@ -150,6 +152,7 @@ class Engine {
     (void)hipFree(dec_.coef_u);
     (void)hipFree(dec_.coef_v);
     (void)hipFree(d_sse_);
+    (void)hipFree(phase_);
     for (auto& s : slots_) {
       (void)hipHostFree(s.host);
       (void)hipEventDestroy(s.ev);
@@ -259,8 +262,9 @@ class Engine {
       upload(f, B);
       FrameSet cur = rec_[f & 1], prev = rec_[(f + 1) & 1];
       if (f == 0) launch_intra_frame(src_, cur, dec_, g_, cfg_.qp, pen_, B, stream_);
-      else launch_inter_frame(src_, prev, cur, dec_, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
+      else launch_inter_frame(src_, prev, phase_, cur, dec_, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
       if (cfg_.deblock) launch_deblock(cur, dec_, g_, cfg_.qp, B, stream_);
+      if (f + 1 < F) launch_phase_planes(cur, phase_, g_, B, stream_);  // reference of f+1
       launch_sse(src_, cur, g_, d_sse_, B, stream_);
       HIP_OK(hipGetLastError());
       Slot& s = slots_[f % kSlots];
@@ -307,6 +311,7 @@ class Engine {
   FrameSet src_{}, rec_[2]{};
   DecisionSet dec_{};
   unsigned long long* d_sse_ = nullptr;
+  uint8_t* phase_ = nullptr;
   Slot slots_[kSlots];
   long slot_bytes_ = 0;
   hipEvent_t t0_{}, t1_{};

@@ -19,6 +19,8 @@ struct Geo {
   int wc, hc;      // CTBs
   long ysz, csz;   // plane sizes (bytes / elements)
   long usz;        // units
+  int pw16;        // phase-plane pitch (W + 16: 8-sample pad each side)
+  long psz;        // phase-plane size ((W + 16) * (H + 16))
 };
 
 inline Geo make_geo(int dw, int dh) {
@@ -34,6 +36,8 @@ inline Geo make_geo(int dw, int dh) {
   g.ysz = (long)g.W * g.H;
   g.csz = g.ysz / 4;
   g.usz = (long)g.w8 * g.h8;
+  g.pw16 = g.W + 16;
+  g.psz = (long)(g.W + 16) * (g.H + 16);
   return g;
 }
 

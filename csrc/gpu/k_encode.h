@@ -24,8 +24,10 @@ void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi,
 void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s);
 void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, int qp,
                         const Penalties& pen, int B, hipStream_t s);
-void launch_inter_frame(FrameSet src, FrameSet ref, FrameSet rec, DecisionSet dec, const Geo& g,
-                        int qp, const Penalties& pen, int range, int B, hipStream_t s);
+void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
+                        const Geo& g, int qp, const Penalties& pen, int range, int B, hipStream_t s);
+// 16 quarter-pel phase planes (B x 16 x psz bytes) of the luma reference
+void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipStream_t s);
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s);
 
 }  // namespace gpu

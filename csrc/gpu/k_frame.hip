@@ -1,0 +1,177 @@
+// k_frame.hip — frame-level kernels: synthetic source, PSNR SSE, quarter-pel phase planes,
+// in-loop deblocking.  Batched: blockIdx.z (or .y) selects the segment.
+#include "gpu_common.h"
+#include "k_encode.h"
+#include "tv/synth.h"
+
+namespace tv {
+namespace gpu {
+
+// ---------------------------------- synthetic source ------------------------------------
+// One workgroup row-tile; the per-frame object trajectories are evaluated once per
+// workgroup into LDS (they were 18 hashes per pixel before).
+__global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t seed, FrameIdx fi) {
+  const int c = blockIdx.y, b = blockIdx.z;
+  const int pw = c ? g.W / 2 : g.W, ph = c ? g.H / 2 : g.H;
+  const int dw = c ? g.dw / 2 : g.dw, dh = c ? g.dh / 2 : g.dh;
+  __shared__ SynthFrameCtx ctx;
+  if (threadIdx.x == 0) synth_frame_ctx(seed, fi.t[b], g.dw, g.dh, ctx);
+  __syncthreads();
+  uint8_t* P = src.plane(c, b, g);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < pw * ph; i += gridDim.x * blockDim.x) {
+    const int x = i % pw, y = i / pw;
+    P[i] = (uint8_t)synth_sample_ctx(ctx, c, tv_min(x, dw - 1), tv_min(y, dh - 1));
+  }
+}
+
+// ------------------------------------------ SSE -----------------------------------------
+// One workgroup per (row block, plane, segment); 4-byte vector loads along rows.
+__global__ void __launch_bounds__(256) k_sse(FrameSet a, FrameSet r, Geo g, unsigned long long* sse) {
+  const int c = blockIdx.y, b = blockIdx.z;
+  const int pw = c ? g.W / 2 : g.W;
+  const int dw = c ? g.dw / 2 : g.dw, dh = c ? g.dh / 2 : g.dh;
+  const uint8_t* A = a.plane(c, b, g);
+  const uint8_t* R = r.plane(c, b, g);
+  const int wq = (dw + 3) >> 2;  // 4-pixel groups per row (pw is a multiple of 16)
+  unsigned s = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < wq * dh; i += gridDim.x * blockDim.x) {
+    const int y = i / wq, x = (i - y * wq) * 4;
+    const uint32_t va = *reinterpret_cast<const uint32_t*>(A + (long)y * pw + x);
+    const uint32_t vr = *reinterpret_cast<const uint32_t*>(R + (long)y * pw + x);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int d = (int)((va >> (8 * k)) & 255) - (int)((vr >> (8 * k)) & 255);
+      s += (x + k < dw) ? (unsigned)(d * d) : 0u;
+    }
+  }
+  unsigned long long t = s;
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  __shared__ unsigned long long part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(sse + b * 3 + c, part[0] + part[1] + part[2] + part[3]);
+}
+
+// --------------------------------- quarter-pel phase planes -----------------------------
+// Plane p = fx + 4*fy holds the exact HEVC 8-tap interpolated luma sample at every integer
+// position of the padded domain [-8, W+8) x [-8, H+8) (beyond 4 samples outside the
+// picture the clamped interpolation is constant, so clamping the query to the pad is
+// exact).  Separable: the 3 horizontal phases are filtered once into LDS (int16), then the
+// 4 vertical phases of each.  Motion search and luma motion compensation then become
+// plain byte loads.
+__global__ void __launch_bounds__(256) k_phase_planes(FrameSet ref, uint8_t* phase, Geo g) {
+  const int b = blockIdx.z, tid = threadIdx.x;
+  const int tx0 = blockIdx.x * 32 - 8, ty0 = blockIdx.y * 32 - 8;
+  const uint8_t* R = ref.plane(0, b, g);
+  __shared__ uint8_t raw[39][40];
+  __shared__ int16_t hf[3][39][32];
+  for (int i = tid; i < 39 * 39; i += 256) {
+    const int rr = i / 39, cc = i % 39;
+    const int X = clip3(0, g.W - 1, tx0 - 3 + cc), Y = clip3(0, g.H - 1, ty0 - 3 + rr);
+    raw[rr][cc] = R[(long)Y * g.W + X];
+  }
+  __syncthreads();
+  for (int i = tid; i < 3 * 39 * 32; i += 256) {
+    const int fx = 1 + i / (39 * 32), rem = i % (39 * 32), rr = rem / 32, c = rem % 32;
+    int v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += kLumaFilter[fx][k] * raw[rr][c + k];
+    hf[fx - 1][rr][c] = (int16_t)v;
+  }
+  __syncthreads();
+  uint8_t* base = phase + (long)b * 16 * g.psz;
+  for (int i = tid; i < 32 * 32; i += 256) {
+    const int r = i >> 5, c = i & 31;
+    const int X = tx0 + c, Y = ty0 + r;
+    if (X >= g.W + 8 || Y >= g.H + 8) continue;
+    const long off = (long)(Y + 8) * g.pw16 + (X + 8);
+#pragma unroll
+    for (int fy = 0; fy < 4; ++fy)
+#pragma unroll
+      for (int fx = 0; fx < 4; ++fx) {
+        int v;
+        if (fy == 0) {
+          v = fx == 0 ? (raw[r + 3][c + 3] << 6) : hf[fx - 1][r + 3][c];
+        } else if (fx == 0) {
+          v = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v += kLumaFilter[fy][k] * raw[r + k][c + 3];
+        } else {
+          v = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v += kLumaFilter[fy][k] * hf[fx - 1][r + k][c];
+          v >>= 6;
+        }
+        base[(long)(fx + 4 * fy) * g.psz + off] = (uint8_t)clip_pixel((v + 32) >> 6);
+      }
+  }
+}
+
+// ------------------------------------ deblocking ----------------------------------------
+__global__ void __launch_bounds__(256) k_deblock(FrameSet rec, DecisionSet dec, Geo g, int qp, int horizontal) {
+  const int b = blockIdx.y;
+  const long ub = b * g.usz;
+  const uint8_t* cl = dec.cu_log2 + ub;
+  const uint8_t* in = dec.intra + ub;
+  const uint8_t* cb = dec.cbf + ub;
+  const int16_t* mv = dec.mv + 2 * ub;
+  uint8_t* Y = rec.plane(0, b, g);
+  uint8_t* U = rec.plane(1, b, g);
+  uint8_t* V = rec.plane(2, b, g);
+  const int W = g.W, H = g.H, Wc = W / 2;
+  const int qpc = chroma_qp(qp, 0);
+  const int nl = horizontal ? (H / 8 - 1) * (W / 4) : (W / 8 - 1) * (H / 4);
+  const int nc = horizontal ? (H / 16 - 1) * (Wc / 4) : (W / 16 - 1) * (H / 8);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nl + nc; i += gridDim.x * blockDim.x) {
+    if (i < nl) {
+      if (!horizontal) {
+        const int x = 8 * (1 + i % (W / 8 - 1)), y = 4 * (i / (W / 8 - 1));
+        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, x - 1, y, x, y);
+        if (bs) deblock_luma_edge4(Y + (long)y * W + x, 1, W, bs, qp);
+      } else {
+        const int y = 8 * (1 + i % (H / 8 - 1)), x = 4 * (i / (H / 8 - 1));
+        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, x, y - 1, x, y);
+        if (bs) deblock_luma_edge4(Y + (long)y * W + x, W, 1, bs, qp);
+      }
+    } else {
+      const int j = i - nl;
+      if (!horizontal) {
+        const int xc = 8 * (1 + j % (W / 16 - 1)), yc = 4 * (j / (W / 16 - 1));
+        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, 2 * xc - 1, 2 * yc, 2 * xc, 2 * yc);
+        if (bs == 2) {
+          deblock_chroma_edge(U + (long)yc * Wc + xc, 1, Wc, 4, qpc);
+          deblock_chroma_edge(V + (long)yc * Wc + xc, 1, Wc, 4, qpc);
+        }
+      } else {
+        const int yc = 8 * (1 + j % (H / 16 - 1)), xc = 4 * (j / (H / 16 - 1));
+        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, 2 * xc, 2 * yc - 1, 2 * xc, 2 * yc);
+        if (bs == 2) {
+          deblock_chroma_edge(U + (long)yc * Wc + xc, Wc, 1, 4, qpc);
+          deblock_chroma_edge(V + (long)yc * Wc + xc, Wc, 1, 4, qpc);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------ launchers -----------------------------------------
+void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi, int B, hipStream_t s) {
+  dim3 grid((unsigned)tv_min(512, (int)((g.ysz + 1023) / 1024)), 3, B);
+  k_synth<<<grid, 256, 0, s>>>(src, g, seed, fi);
+}
+void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s) {
+  dim3 grid((unsigned)tv_min(256, (int)((g.ysz / 4 + 4095) / 4096)), 3, B);
+  k_sse<<<grid, 256, 0, s>>>(a, r, g, sse);
+}
+void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipStream_t s) {
+  dim3 grid((g.W + 16 + 31) / 32, (g.H + 16 + 31) / 32, B);
+  k_phase_planes<<<grid, 256, 0, s>>>(ref, phase, g);
+}
+void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s) {
+  dim3 grid((unsigned)tv_min(1024, (int)(g.ysz / 32 / 256 + 1)), B);
+  k_deblock<<<grid, 256, 0, s>>>(rec, dec, g, qp, 0);
+  k_deblock<<<grid, 256, 0, s>>>(rec, dec, g, qp, 1);
+}
+
+}  // namespace gpu
+}  // namespace tv

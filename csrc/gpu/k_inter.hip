@@ -1,0 +1,310 @@
+// k_inter.hip — P-frame kernels.
+//
+//  k_inter_me     pass A per CTB (320 threads = 5 waves):
+//                   * the source CTB and a 72x72 reference window are staged in LDS as
+//                     32-bit words;
+//                   * integer full search over [-R, R]^2: each thread owns 4 horizontally
+//                     adjacent candidates, loads 3 window words per row and derives the 4
+//                     shifted rows with v_alignbyte, accumulating 16 8x8 SADs per candidate
+//                     with v_sad_u8 (4 pixels / instruction); 16x16 and 32x32 costs are sums
+//                     of 8x8 SADs (SAD reuse);
+//                   * half- then quarter-pel refinement of all 21 blocks at once, reading
+//                     the precomputed phase planes (no per-block barriers);
+//                   * bottom-up CU split decision.
+//  k_inter_recon  pass B per CTB: luma prediction = phase-plane loads, chroma 4-tap MC,
+//                 residual, MFMA transform/quant, exact inverse, reconstruction.
+#include "gpu_common.h"
+#include "k_encode.h"
+#include "tb_coder.h"
+
+namespace tv {
+namespace gpu {
+
+constexpr int kMeThreads = 320;
+constexpr int kWin = 72;       // window side: 32 + 2*16 + 8
+constexpr int kWinOff = 20;    // window origin = CTB origin - 20 (multiple of 4)
+constexpr int kWinW = kWin / 4;  // 32-bit words per window row
+
+__device__ __forceinline__ void me_blk_geom(int bi, int& bx, int& by, int& l2) {
+  if (bi < 16) {
+    bx = (bi & 3) * 8;
+    by = (bi >> 2) * 8;
+    l2 = 3;
+  } else if (bi < 20) {
+    bx = ((bi - 16) & 1) * 16;
+    by = ((bi - 16) >> 1) * 16;
+    l2 = 4;
+  } else {
+    bx = by = 0;
+    l2 = 5;
+  }
+}
+__device__ __forceinline__ int me_blk8_of(int q, int r) {
+  return (((q >> 1) * 2 + (r >> 1)) << 2) + (q & 1) * 2 + (r & 1);
+}
+__device__ __forceinline__ void cand_offset(int k, int& ox, int& oy) {
+  ox = (k == 0 || k == 3 || k == 5) ? -1 : ((k == 1 || k == 6) ? 0 : 1);
+  oy = k < 3 ? -1 : (k < 5 ? 0 : 1);
+}
+__device__ __forceinline__ int phase_at(const uint8_t* P, const Geo& g, int x, int y) {
+  x = clip3(-8, g.W + 7, x);
+  y = clip3(-8, g.H + 7, y);
+  return P[(long)(y + 8) * g.pw16 + x + 8];
+}
+
+__global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
+                                                         DecisionSet dec, Geo g, Penalties pen, int range) {
+  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
+  const uint8_t* S = src.plane(0, b, g);
+  const uint8_t* R = ref.plane(0, b, g);
+  __shared__ uint32_t s32[256];
+  __shared__ uint32_t win[kWin * kWinW];
+  __shared__ unsigned best[21];
+  __shared__ int bcost[21], bmv[21][2];
+  __shared__ int subsad[21][8];
+  if (tid < 256) s32[tid] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (tid >> 3)) * g.W + cx + 4 * (tid & 7));
+  for (int w = tid; w < kWin * kWinW; w += kMeThreads) {
+    const int row = w / kWinW, wc = w % kWinW;
+    const int gy = clip3(0, g.H - 1, cy - kWinOff + row);
+    const int gx0 = cx - kWinOff + 4 * wc;
+    uint32_t v;
+    if (gx0 >= 0 && gx0 + 3 < g.W) {
+      v = *reinterpret_cast<const uint32_t*>(R + (long)gy * g.W + gx0);
+    } else {
+      v = 0;
+      for (int k = 0; k < 4; ++k) v |= (uint32_t)R[(long)gy * g.W + clip3(0, g.W - 1, gx0 + k)] << (8 * k);
+    }
+    win[w] = v;
+  }
+  if (tid < 21) best[tid] = 0xffffffffu;
+  __syncthreads();
+
+  // ------------------------------- integer full search ---------------------------------
+  const int side = 2 * range + 1, groups = range / 2 + 1, items = groups * side;
+  unsigned lb[21];
+#pragma unroll
+  for (int k = 0; k < 21; ++k) lb[k] = 0xffffffffu;
+  for (int item = tid; item < items; item += kMeThreads) {
+    const int dyi = item / groups, gi = item - dyi * groups;
+    const int dy = dyi - range, dx0 = 4 * gi - range;
+    // per-shift rate term and packed candidate index; shifts beyond +R are excluded with a
+    // penalty larger than any SAD (keeps the update branch-free)
+    unsigned mvc[4], cid[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int dx = dx0 + s;
+      mvc[s] = dx > range ? 0x3ffffu : (unsigned)pen.mv[mv_bits_est(4 * dx, 4 * dy)];
+      cid[s] = (unsigned)(dyi * side + tv_min(dx, range) + range);
+    }
+    unsigned q16[4][4], t32[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      t32[s] = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) q16[q][s] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int bx = (k & 3) * 8, by = (k >> 2) * 8;
+      const int q = ((k >> 3) << 1) | ((k >> 1) & 1);
+      unsigned acc[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int srow = (by + j) * 8 + (bx >> 2);
+        const uint32_t s0 = s32[srow], s1 = s32[srow + 1];
+        const int wrow = (kWinOff + dy + by + j) * kWinW + ((kWinOff + dx0 + bx) >> 2);
+        const uint32_t w0 = win[wrow], w1 = win[wrow + 1], w2 = win[wrow + 2];
+        acc[0] = __builtin_amdgcn_sad_u8(w1, s1, __builtin_amdgcn_sad_u8(w0, s0, acc[0]));
+#pragma unroll
+        for (int s = 1; s < 4; ++s) {
+          const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, s);
+          const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, s);
+          acc[s] = __builtin_amdgcn_sad_u8(hi, s1, __builtin_amdgcn_sad_u8(lo, s0, acc[s]));
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const unsigned v = ((acc[s] + mvc[s]) << 11) | cid[s];
+        lb[k] = v < lb[k] ? v : lb[k];
+        q16[q][s] += acc[s];
+        t32[s] += acc[s];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // bound live ranges: no hoisting across 8x8 blocks
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned v = ((q16[q][s] + mvc[s]) << 11) | cid[s];
+        lb[16 + q] = v < lb[16 + q] ? v : lb[16 + q];
+      }
+      const unsigned v = ((t32[s] + mvc[s]) << 11) | cid[s];
+      lb[20] = v < lb[20] ? v : lb[20];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 21; ++k) {
+    const unsigned m = wave_min_u32(lb[k]);
+    if ((tid & 63) == 0) atomicMin(&best[k], m);
+  }
+  __syncthreads();
+  if (tid < 21) {
+    const int c = (int)(best[tid] & 2047);
+    bcost[tid] = (int)(best[tid] >> 11);
+    bmv[tid][0] = 4 * (c % side - range);
+    bmv[tid][1] = 4 * (c / side - range);
+  }
+
+  // ------------------------ half- then quarter-pel refinement ---------------------------
+  const uint8_t* sb = reinterpret_cast<const uint8_t*>(s32);
+  const uint8_t* ph = phase + (long)b * 16 * g.psz;
+  for (int step = 2; step >= 1; step >>= 1) {
+    if (tid < 168) subsad[tid >> 3][tid & 7] = 0;
+    __syncthreads();
+    for (int ci = tid; ci < 8 * 384; ci += kMeThreads) {
+      const int k = ci / 384, r = ci - k * 384;
+      int bi, cr, l2;
+      if (r < 128) {
+        bi = r >> 3;
+        cr = r & 7;
+        l2 = 3;
+      } else if (r < 256) {
+        bi = 16 + ((r - 128) >> 5);
+        cr = (r - 128) & 31;
+        l2 = 4;
+      } else {
+        bi = 20;
+        cr = r - 256;
+        l2 = 5;
+      }
+      int bx, by, l2b;
+      me_blk_geom(bi, bx, by, l2b);
+      const int cpr = (1 << l2) >> 3;
+      const int row = cr / cpr, col0 = (cr - row * cpr) * 8;
+      int ox, oy;
+      cand_offset(k, ox, oy);
+      const int mx = bmv[bi][0] + ox * step, my = bmv[bi][1] + oy * step;
+      const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
+      const int gy = clip3(-8, g.H + 7, cy + by + row + (my >> 2));
+      const uint8_t* Prow = P + (long)(gy + 8) * g.pw16 + 8;
+      const int gx = cx + bx + col0 + (mx >> 2);
+      const uint8_t* srow = sb + (by + row) * 32 + bx + col0;
+      int s = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += tv_abs((int)srow[i] - (int)Prow[clip3(-8, g.W + 7, gx + i)]);
+      atomicAdd(&subsad[bi][k], s);
+    }
+    __syncthreads();
+    if (tid < 21) {
+      unsigned bestv = (unsigned)bcost[tid] << 4;
+      for (int k = 0; k < 8; ++k) {
+        int ox, oy;
+        cand_offset(k, ox, oy);
+        const int mx = bmv[tid][0] + ox * step, my = bmv[tid][1] + oy * step;
+        const unsigned v = ((unsigned)(subsad[tid][k] + pen.mv[mv_bits_est(mx, my)]) << 4) | (unsigned)(k + 1);
+        bestv = v < bestv ? v : bestv;
+      }
+      const int kk = (int)(bestv & 15);
+      bcost[tid] = (int)(bestv >> 4);
+      if (kk) {
+        int ox, oy;
+        cand_offset(kk - 1, ox, oy);
+        bmv[tid][0] += ox * step;
+        bmv[tid][1] += oy * step;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ------------------------------- CU split decision ------------------------------------
+  if (tid == 0) {
+    const int ps = pen.split_inter;
+    int sum16 = 0;
+    uint8_t l2u[16];
+    int mvu[16][2];
+    for (int q = 0; q < 4; ++q) {
+      int sum8 = 0;
+      for (int r = 0; r < 4; ++r) sum8 += bcost[me_blk8_of(q, r)] + ps;
+      const bool split = sum8 < bcost[16 + q] + ps;
+      sum16 += split ? sum8 : bcost[16 + q] + ps;
+      for (int r = 0; r < 4; ++r) {
+        const int ux = (q & 1) * 2 + (r & 1), uy = (q >> 1) * 2 + (r >> 1);
+        const int sbi = split ? me_blk8_of(q, r) : 16 + q;
+        l2u[uy * 4 + ux] = split ? 3 : 4;
+        mvu[uy * 4 + ux][0] = bmv[sbi][0];
+        mvu[uy * 4 + ux][1] = bmv[sbi][1];
+      }
+    }
+    const bool whole = bcost[20] + ps <= sum16;
+    for (int k = 0; k < 16; ++k) {
+      const long u = b * g.usz + (long)((cy >> 3) + (k >> 2)) * g.w8 + (cx >> 3) + (k & 3);
+      dec.cu_log2[u] = whole ? 5 : l2u[k];
+      dec.mv[2 * u] = (int16_t)(whole ? bmv[20][0] : mvu[k][0]);
+      dec.mv[2 * u + 1] = (int16_t)(whole ? bmv[20][1] : mvu[k][1]);
+      dec.intra[u] = 0;
+      dec.ipm[u] = 1;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
+                                                     FrameSet rec, DecisionSet dec, Geo g, int qp) {
+  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
+  __shared__ int pred[1024], resid[1024];
+  __shared__ TbScratch scr;
+  const long ub = b * g.usz;
+  const int qpc = chroma_qp(qp, 0);
+  const uint8_t* ph = phase + (long)b * 16 * g.psz;
+  tb_init(scr);
+  __syncthreads();
+  for (int k8 = 0; k8 < 16; ++k8) {
+    const int x0 = cx + (k8 & 3) * 8, y0 = cy + (k8 >> 2) * 8;
+    const long u = ub + (y0 >> 3) * g.w8 + (x0 >> 3);
+    const int log2 = dec.cu_log2[u];
+    if ((x0 & ((1 << log2) - 1)) || (y0 & ((1 << log2) - 1))) continue;  // not a CU origin
+    const int mvx = dec.mv[2 * u], mvy = dec.mv[2 * u + 1];
+    int cbf = 0;
+    for (int c = 0; c < 3; ++c) {
+      const int l2 = c ? log2 - 1 : log2, N = 1 << l2;
+      const int x = c ? x0 >> 1 : x0, y = c ? y0 >> 1 : y0;
+      const int pw = c ? g.W / 2 : g.W, phh = c ? g.H / 2 : g.H;
+      const uint8_t* S = src.plane(c, b, g);
+      if (c == 0) {
+        const uint8_t* P = ph + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
+        for (int i = tid; i < N * N; i += 256) {
+          const int px = i & (N - 1), py = i >> l2;
+          const int p = phase_at(P, g, x + px + (mvx >> 2), y + py + (mvy >> 2));
+          pred[i] = p;
+          resid[i] = (int)S[(y + py) * pw + x + px] - p;
+        }
+      } else {
+        const uint8_t* Rf = ref.plane(c, b, g);
+        for (int i = tid; i < N * N; i += 256) {
+          const int px = i & (N - 1), py = i >> l2;
+          const int p = mc_chroma_sample(Rf, pw, pw, phh, x + px + (mvx >> 3), y + py + (mvy >> 3), mvx & 7, mvy & 7);
+          pred[i] = p;
+          resid[i] = (int)S[(y + py) * pw + x + px] - p;
+        }
+      }
+      __syncthreads();
+      int16_t* lev = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz) +
+                     (long)y * pw + x;
+      const int cb = wg_code_tb(resid, pred, l2, c ? qpc : qp, false, lev, pw,
+                                rec.plane(c, b, g) + (long)y * pw + x, pw, scr);
+      cbf |= cb << c;
+    }
+    const int n8 = 1 << (log2 - 3);
+    if (tid < n8 * n8) dec.cbf[u + (tid / n8) * g.w8 + (tid % n8)] = (uint8_t)cbf;
+  }
+}
+
+void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
+                        const Geo& g, int qp, const Penalties& pen, int range, int B, hipStream_t s) {
+  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, g, pen, range);
+  k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, qp);
+}
+
+}  // namespace gpu
+}  // namespace tv

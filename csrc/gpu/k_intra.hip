@@ -1,0 +1,290 @@
+// k_intra.hip — I-frame kernels.
+//
+//  k_intra_analysis  pass A, fully parallel over CTUs: for all 21 blocks of a CTB
+//                    (16 x 8x8, 4 x 16x16, 1 x 32x32) and all 35 HEVC intra modes, predict
+//                    from SOURCE neighbours and compute the 8x8-Hadamard SATD with one wave
+//                    per (block, mode): lane = pixel, butterflies via cross-lane shuffles.
+//                    Then the bottom-up CU split decision.
+//  k_intra_recon     pass B, CTB anti-diagonal wavefront (cx + 2*cy = d per launch): the
+//                    normative prediction from reconstructed neighbours + MFMA TB coding.
+#include "gpu_common.h"
+#include "k_encode.h"
+#include "tb_coder.h"
+
+namespace tv {
+namespace gpu {
+
+__device__ __forceinline__ void blk_geom(int bi, int& bx, int& by, int& l2) {
+  if (bi < 16) {
+    bx = (bi & 3) * 8;
+    by = (bi >> 2) * 8;
+    l2 = 3;
+  } else if (bi < 20) {
+    bx = ((bi - 16) & 1) * 16;
+    by = ((bi - 16) >> 1) * 16;
+    l2 = 4;
+  } else {
+    bx = by = 0;
+    l2 = 5;
+  }
+}
+__device__ __forceinline__ int blk8_of(int q, int r) {
+  return (((q >> 1) * 2 + (r >> 1)) << 2) + (q & 1) * 2 + (r & 1);
+}
+// flattened reference-sample entry e (0..468) -> (block, index within 2N+1)
+__device__ __forceinline__ void ref_entry(int e, int& bi, int& i) {
+  if (e < 272) {
+    bi = e / 17;
+    i = e % 17;
+  } else if (e < 404) {
+    bi = 16 + (e - 272) / 33;
+    i = (e - 272) % 33;
+  } else {
+    bi = 20;
+    i = e - 404;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSet dec, Geo g, Penalties pen) {
+  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
+  const uint8_t* S = src.plane(0, b, g);
+  __shared__ uint8_t sblk[32 * 32];
+  __shared__ int16_t refs[21][4][65];  // left, top, smoothed left, smoothed top
+  __shared__ bool avl[21][2][65];
+  __shared__ int dcv[21];
+  __shared__ unsigned best[21];
+  for (int i = tid; i < 1024; i += 256) sblk[i] = S[(cy + (i >> 5)) * g.W + cx + (i & 31)];
+  if (tid < 21) best[tid] = 0xffffffffu;
+  for (int e = tid; e < 469; e += 256) {
+    int bi, i, bx, by, l2;
+    ref_entry(e, bi, i);
+    blk_geom(bi, bx, by, l2);
+    const int x = cx + bx, y = cy + by;
+    if (i == 0) {
+      const bool a = zscan_available(x, y, x - 1, y - 1, g.W, g.H);
+      avl[bi][0][0] = avl[bi][1][0] = a;
+      refs[bi][0][0] = refs[bi][1][0] = a ? S[(y - 1) * g.W + x - 1] : 0;
+    } else {
+      const bool al = zscan_available(x, y, x - 1, y + i - 1, g.W, g.H);
+      avl[bi][0][i] = al;
+      refs[bi][0][i] = al ? S[(y + i - 1) * g.W + x - 1] : 0;
+      const bool at = zscan_available(x, y, x + i - 1, y - 1, g.W, g.H);
+      avl[bi][1][i] = at;
+      refs[bi][1][i] = at ? S[(y - 1) * g.W + x + i - 1] : 0;
+    }
+  }
+  __syncthreads();
+  if (tid < 21) {
+    int bx, by, l2;
+    blk_geom(tid, bx, by, l2);
+    intra_substitute(refs[tid][0], refs[tid][1], avl[tid][0], avl[tid][1], 1 << l2);
+    dcv[tid] = intra_dc_value(refs[tid][0], refs[tid][1], l2);
+  }
+  __syncthreads();
+  for (int e = tid; e < 469; e += 256) {  // [1 2 1] smoothed copies
+    int bi, i, bx, by, l2;
+    ref_entry(e, bi, i);
+    blk_geom(bi, bx, by, l2);
+    const int N2 = 2 << l2;
+    const int16_t* L = refs[bi][0];
+    const int16_t* T = refs[bi][1];
+    if (i == 0) {
+      refs[bi][2][0] = refs[bi][3][0] = (int16_t)((L[1] + 2 * L[0] + T[1] + 2) >> 2);
+    } else if (i == N2) {
+      refs[bi][2][i] = L[i];
+      refs[bi][3][i] = T[i];
+    } else {
+      refs[bi][2][i] = (int16_t)((L[i + 1] + 2 * L[i] + L[i - 1] + 2) >> 2);
+      refs[bi][3][i] = (int16_t)((T[i + 1] + 2 * T[i] + T[i - 1] + 2) >> 2);
+    }
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int t = wave; t < 735; t += 4) {
+    int bi, mode;
+    if (t < 560) {
+      bi = t / 35;
+      mode = t % 35;
+    } else if (t < 700) {
+      bi = 16 + (t - 560) / 35;
+      mode = (t - 560) % 35;
+    } else {
+      bi = 20;
+      mode = t - 700;
+    }
+    int bx, by, l2;
+    blk_geom(bi, bx, by, l2);
+    const int N = 1 << l2, nq = N >> 3;
+    const bool filt = intra_filter_refs(l2, mode);
+    const int16_t* L = refs[bi][filt ? 2 : 0];
+    const int16_t* T = refs[bi][filt ? 3 : 1];
+    int sum = 0;
+    for (int q = 0; q < nq * nq; ++q) {
+      const int qx = (q % nq) * 8 + (lane & 7), qy = (q / nq) * 8 + (lane >> 3);
+      const int p = intra_pred_pixel(L, T, l2, mode, N < 32, dcv[bi], qx, qy);
+      sum += wave_satd8x8((int)sblk[(by + qy) * 32 + bx + qx] - p);
+    }
+    const unsigned cost = (unsigned)(sum + (mode <= 1 ? pen.mode_dcpl : pen.mode_ang));
+    if (lane == 0) atomicMin(&best[bi], (cost << 6) | (unsigned)mode);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int ps = pen.split_intra;
+    const int c32 = (int)(best[20] >> 6);
+    int sum16 = 0;
+    uint8_t l2u[16], mu[16];
+    for (int q = 0; q < 4; ++q) {
+      const int c16 = (int)(best[16 + q] >> 6);
+      int sum8 = 0;
+      for (int r = 0; r < 4; ++r) sum8 += (int)(best[blk8_of(q, r)] >> 6) + ps;
+      const bool split = sum8 < c16 + ps;
+      sum16 += split ? sum8 : c16 + ps;
+      for (int r = 0; r < 4; ++r) {
+        const int ux = (q & 1) * 2 + (r & 1), uy = (q >> 1) * 2 + (r >> 1);
+        l2u[uy * 4 + ux] = split ? 3 : 4;
+        mu[uy * 4 + ux] = (uint8_t)(split ? (best[blk8_of(q, r)] & 63) : (best[16 + q] & 63));
+      }
+    }
+    const bool whole = c32 + ps <= sum16;
+    for (int k = 0; k < 16; ++k) {
+      const long u = b * g.usz + (long)((cy >> 3) + (k >> 2)) * g.w8 + (cx >> 3) + (k & 3);
+      dec.cu_log2[u] = whole ? 5 : l2u[k];
+      dec.ipm[u] = whole ? (uint8_t)(best[20] & 63) : mu[k];
+      dec.intra[u] = 1;
+      dec.mv[2 * u] = dec.mv[2 * u + 1] = 0;
+    }
+  }
+}
+
+// Gather + substitute (+ smooth) the intra references of one TB from the reconstruction.
+struct RefBuf {
+  int L[65], T[65], FL[65], FT[65];
+  bool la[65], ta[65];
+};
+
+__device__ void wg_build_refs(const uint8_t* P, int pw, int cIdx, int x, int y, int log2N, bool filt,
+                              const Geo& g, RefBuf& r) {
+  const int N = 1 << log2N, s = cIdx ? 1 : 0, tid = threadIdx.x;
+  const int xL = x << s, yL = y << s;
+  for (int i = tid; i <= 2 * N; i += blockDim.x) {
+    if (i == 0) {
+      const bool a = zscan_available(xL, yL, (x - 1) << s, (y - 1) << s, g.W, g.H);
+      r.la[0] = r.ta[0] = a;
+      r.L[0] = r.T[0] = a ? P[(y - 1) * pw + (x - 1)] : 0;
+    } else {
+      const bool al = zscan_available(xL, yL, (x - 1) << s, (y + i - 1) << s, g.W, g.H);
+      r.la[i] = al;
+      r.L[i] = al ? P[(y + i - 1) * pw + (x - 1)] : 0;
+      const bool at = zscan_available(xL, yL, (x + i - 1) << s, (y - 1) << s, g.W, g.H);
+      r.ta[i] = at;
+      r.T[i] = at ? P[(y - 1) * pw + (x + i - 1)] : 0;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) intra_substitute(r.L, r.T, r.la, r.ta, N);
+  __syncthreads();
+  if (filt) {
+    for (int i = tid; i <= 2 * N; i += blockDim.x) {
+      if (i == 0) {
+        r.FL[0] = r.FT[0] = (r.L[1] + 2 * r.L[0] + r.T[1] + 2) >> 2;
+      } else if (i == 2 * N) {
+        r.FL[i] = r.L[i];
+        r.FT[i] = r.T[i];
+      } else {
+        r.FL[i] = (r.L[i + 1] + 2 * r.L[i] + r.L[i - 1] + 2) >> 2;
+        r.FT[i] = (r.T[i + 1] + 2 * r.T[i] + r.T[i - 1] + 2) >> 2;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) k_intra_recon(FrameSet src, FrameSet rec, DecisionSet dec, Geo g,
+                                                     int qp, int diag, int cy0) {
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int cyi = cy0 + blockIdx.x, cxi = diag - 2 * cyi;
+  const int cx = cxi * 32, cy = cyi * 32;
+  __shared__ int pred[1024], resid[1024];
+  __shared__ RefBuf rb;
+  __shared__ TbScratch scr;
+  __shared__ int cus[16][3];
+  __shared__ int ncu;
+  const long ub = b * g.usz;
+  const int qpc = chroma_qp(qp, 0);
+  tb_init(scr);
+  if (tid == 0) {  // CUs of this CTB in z-order
+    int n = 0;
+    if (dec.cu_log2[ub + (cy >> 3) * g.w8 + (cx >> 3)] == 5) {
+      cus[0][0] = cx;
+      cus[0][1] = cy;
+      cus[0][2] = 5;
+      n = 1;
+    } else {
+      for (int q = 0; q < 4; ++q) {
+        const int x16 = cx + (q & 1) * 16, y16 = cy + (q >> 1) * 16;
+        if (dec.cu_log2[ub + (y16 >> 3) * g.w8 + (x16 >> 3)] == 4) {
+          cus[n][0] = x16;
+          cus[n][1] = y16;
+          cus[n][2] = 4;
+          ++n;
+        } else {
+          for (int r = 0; r < 4; ++r) {
+            cus[n][0] = x16 + (r & 1) * 8;
+            cus[n][1] = y16 + (r >> 1) * 8;
+            cus[n][2] = 3;
+            ++n;
+          }
+        }
+      }
+    }
+    ncu = n;
+  }
+  __syncthreads();
+  for (int k = 0; k < ncu; ++k) {
+    const int x0 = cus[k][0], y0 = cus[k][1], log2 = cus[k][2];
+    const long u = ub + (y0 >> 3) * g.w8 + (x0 >> 3);
+    const int mode = dec.ipm[u];
+    int cbf = 0;
+    for (int c = 0; c < 3; ++c) {
+      const int l2 = c ? log2 - 1 : log2, N = 1 << l2;
+      const int x = c ? x0 >> 1 : x0, y = c ? y0 >> 1 : y0;
+      const int pw = c ? g.W / 2 : g.W;
+      uint8_t* R = rec.plane(c, b, g);
+      const uint8_t* S = src.plane(c, b, g);
+      const bool filt = c == 0 && intra_filter_refs(l2, mode);
+      wg_build_refs(R, pw, c, x, y, l2, filt, g, rb);
+      const int* L = filt ? rb.FL : rb.L;
+      const int* T = filt ? rb.FT : rb.T;
+      const int dc = mode == 1 ? intra_dc_value(L, T, l2) : 0;
+      for (int i = tid; i < N * N; i += 256) {
+        const int px = i & (N - 1), py = i >> l2;
+        const int p = intra_pred_pixel(L, T, l2, mode, c == 0 && N < 32, dc, px, py);
+        pred[i] = p;
+        resid[i] = (int)S[(y + py) * pw + x + px] - p;
+      }
+      __syncthreads();
+      int16_t* lev = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz) +
+                     (long)y * pw + x;
+      const int cb = wg_code_tb(resid, pred, l2, c ? qpc : qp, true, lev, pw, R + (long)y * pw + x, pw, scr);
+      cbf |= cb << c;
+    }
+    const int n8 = 1 << (log2 - 3);
+    if (tid < n8 * n8) dec.cbf[u + (tid / n8) * g.w8 + (tid % n8)] = (uint8_t)cbf;
+  }
+}
+
+void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, int qp,
+                        const Penalties& pen, int B, hipStream_t s) {
+  k_intra_analysis<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, dec, g, pen);
+  const int ndiag = (g.wc - 1) + 2 * (g.hc - 1) + 1;
+  for (int d = 0; d < ndiag; ++d) {
+    const int cy0 = tv_max(0, (d - (g.wc - 1) + 1) / 2);
+    const int cy1 = tv_min(g.hc - 1, d / 2);
+    if (cy1 < cy0) continue;
+    k_intra_recon<<<dim3(cy1 - cy0 + 1, B), 256, 0, s>>>(src, rec, dec, g, qp, d, cy0);
+  }
+}
+
+}  // namespace gpu
+}  // namespace tv

@@ -1,0 +1,141 @@
+// tb_coder.h — workgroup-cooperative transform-block coding on gfx950 matrix cores.
+//
+// Forward DCT, deadzone quantisation, dequantisation and the normative inverse DCT of one
+// N x N TB.  The 16- and 32-point 2-D transforms run as 16x16 output tiles of
+// v_mfma_f32_16x16x4_f32 (exact f32 MFMA, one wave per tile).  Every MFMA product stays an
+// exact integer: operands that can exceed 8 bits (intermediate rows, dequantised levels)
+// are split as v = 256*hi + lo and accumulated in two chains, so each chain's partial sums
+// are < 2^24 and the int32 recombination is bit-identical to the scalar golden model
+// (tv::forward_transform / tv::inverse_transform).  4- and 8-point TBs use the VALU.
+#pragma once
+#include "gpu_common.h"
+
+namespace tv {
+namespace gpu {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct TbScratch {
+  int T[32][33];     // DCT matrix (padded rows)
+  int tmp[32 * 33];  // stage intermediate (padded rows)
+  int coef[1024];
+  int red[4];
+};
+
+__device__ inline void tb_init(TbScratch& s) {
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) s.T[i >> 5][i & 31] = kDct32.m[i >> 5][i & 31];
+}
+
+__device__ __forceinline__ int tbT(const TbScratch& s, int log2N, int k, int n) {
+  return s.T[k << (5 - log2N)][n];
+}
+
+// One 16x16 output tile P = X * Y (K = 16 or 32) on the calling wave.  X(i,k), Y(k,j) are
+// callables returning ints (exactly representable in f32).  When `split`, the operand
+// selected by `split_x` is decomposed into 8-bit halves and the tile recombined in int32.
+template <class FX, class FY>
+__device__ __forceinline__ void mfma_tile(FX X, FY Y, int ti, int tj, int K, bool split, bool split_x,
+                                          int out[4]) {
+  const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+  f32x4 hi = {0.f, 0.f, 0.f, 0.f}, lo = {0.f, 0.f, 0.f, 0.f};
+  for (int kk = 0; kk < K; kk += 4) {
+    const int xv = X(16 * ti + i, kk + kq), yv = Y(kk + kq, 16 * tj + i);
+    if (!split) {
+      hi = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv, (float)yv, hi, 0, 0, 0);
+    } else if (split_x) {
+      hi = __builtin_amdgcn_mfma_f32_16x16x4f32((float)(xv >> 8), (float)yv, hi, 0, 0, 0);
+      lo = __builtin_amdgcn_mfma_f32_16x16x4f32((float)(xv & 255), (float)yv, lo, 0, 0, 0);
+    } else {
+      hi = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv, (float)(yv >> 8), hi, 0, 0, 0);
+      lo = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv, (float)(yv & 255), lo, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) out[r] = split ? (int)hi[r] * 256 + (int)lo[r] : (int)hi[r];
+}
+
+// Run a stage over the whole N x N output: each wave owns 16x16 tiles; N <= 8 uses VALU.
+// `emit(row, col, value)` stores the stage output.  All threads must call (no barrier here).
+template <class FX, class FY, class EMIT>
+__device__ __forceinline__ void tb_stage(int log2N, FX X, FY Y, bool split, bool split_x, EMIT emit) {
+  const int N = 1 << log2N;
+  if (N >= 16) {
+    const int tiles = (N >> 4) * (N >> 4);
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int t = wave; t < tiles; t += nw) {
+      const int ti = t / (N >> 4), tj = t % (N >> 4);
+      int o[4];
+      mfma_tile(X, Y, ti, tj, N, split, split_x, o);
+      const int lane = threadIdx.x & 63;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) emit(16 * ti + (lane >> 4) * 4 + r, 16 * tj + (lane & 15), o[r]);
+    }
+  } else {
+    for (int e = threadIdx.x; e < N * N; e += blockDim.x) {
+      const int r = e >> log2N, c = e & (N - 1);
+      int acc = 0;
+      for (int k = 0; k < N; ++k) acc += X(r, k) * Y(k, c);
+      emit(r, c, acc);
+    }
+  }
+}
+
+// Code one TB.  resid/pred are LDS arrays (N*N row-major).  Writes levels to `lev`
+// (stride ls) and reconstructed pixels to `rec` (stride rs).  Returns cbf (uniform).
+__device__ int wg_code_tb(const int* resid, const int* pred, int log2N, int qp, bool intra,
+                          int16_t* lev, int ls, uint8_t* rec, int rs, TbScratch& s) {
+  const int N = 1 << log2N, n2 = N * N, tid = threadIdx.x, nt = blockDim.x;
+  const int sh1 = log2N - 1, sh2 = log2N + 6;
+  if (tid < 4) s.red[tid] = 0;
+  // forward stage 1: tmp[k][x] = (sum_y T[k][y] r[y][x] + rnd) >> sh1     (operands <= 8 bit)
+  tb_stage(
+      log2N, [&](int k, int y) { return tbT(s, log2N, k, y); }, [&](int y, int x) { return resid[y * N + x]; },
+      false, false, [&](int r, int c, int v) { s.tmp[r * 33 + c] = (v + (1 << (sh1 - 1))) >> sh1; });
+  __syncthreads();
+  // forward stage 2 + quantisation: coef[k][j] = (sum_x tmp[k][x] T[j][x] + rnd) >> sh2
+  tb_stage(
+      log2N, [&](int k, int x) { return s.tmp[k * 33 + x]; }, [&](int x, int j) { return tbT(s, log2N, j, x); },
+      true, true, [&](int r, int c, int v) {
+        s.coef[r * N + c] = quant_level((v + (1 << (sh2 - 1))) >> sh2, qp, log2N, intra);
+      });
+  __syncthreads();
+  int nz = 0, sa = 0;
+  for (int i = tid; i < n2; i += nt) {
+    nz += s.coef[i] != 0;
+    sa += tv_abs(s.coef[i]);
+  }
+  nz = wave_sum(nz);
+  sa = wave_sum(sa);
+  if ((tid & 63) == 0) {
+    atomicAdd(&s.red[0], nz);
+    atomicAdd(&s.red[1], sa);
+  }
+  __syncthreads();
+  if (tid == 0) s.red[2] = (!intra && s.red[0] == 1 && s.red[1] == 1 && s.coef[0] == 0) ? 0 : s.red[0];
+  __syncthreads();
+  const int NZ = s.red[2];
+  for (int i = tid; i < n2; i += nt) {
+    const int l = NZ ? s.coef[i] : 0;
+    lev[(i >> log2N) * ls + (i & (N - 1))] = (int16_t)l;
+    if (!NZ) rec[(i >> log2N) * rs + (i & (N - 1))] = (uint8_t)clip_pixel(pred[i]);
+    else s.coef[i] = dequant_level(l, qp, log2N);
+  }
+  __syncthreads();
+  if (!NZ) return 0;
+  // inverse stage 1: tmp[y][x] = clip16((sum_k T[k][y] d[k][x] + 64) >> 7)   (split d)
+  tb_stage(
+      log2N, [&](int y, int k) { return tbT(s, log2N, k, y); }, [&](int k, int x) { return s.coef[k * N + x]; },
+      true, false, [&](int r, int c, int v) { s.tmp[r * 33 + c] = clip3(-32768, 32767, (v + 64) >> 7); });
+  __syncthreads();
+  // inverse stage 2: res[y][x] = (sum_k g[y][k] T[k][x] + 2048) >> 12            (split g)
+  tb_stage(
+      log2N, [&](int y, int k) { return s.tmp[y * 33 + k]; }, [&](int k, int x) { return tbT(s, log2N, k, x); },
+      true, true, [&](int r, int c, int v) {
+        rec[r * rs + c] = (uint8_t)clip_pixel(pred[r * N + c] + ((v + 2048) >> 12));
+      });
+  __syncthreads();
+  return 1;
+}
+
+}  // namespace gpu
+}  // namespace tv

@@ -223,9 +223,10 @@ TV_HD void intra_smooth_refs(int* left, int* top, int N) {
 
 // Reference-sample substitution (H.265 8.4.4.2.2) given availability flags.
 //   Canonical order: left[2N] (bottom) ... left[1], corner, top[1] ... top[2N].
-TV_HD void intra_substitute(int* left, int* top, const bool* lavail, const bool* tavail, int N) {
+template <typename R>
+TV_HD void intra_substitute(R* left, R* top, const bool* lavail, const bool* tavail, int N) {
   const int total = 4 * N + 1;
-  auto get = [&](int i) -> int& { return i < 2 * N ? left[2 * N - i] : top[i - 2 * N]; };
+  auto get = [&](int i) -> R& { return i < 2 * N ? left[2 * N - i] : top[i - 2 * N]; };
   auto av = [&](int i) -> bool { return i < 2 * N ? lavail[2 * N - i] : tavail[i - 2 * N]; };
   int first = -1;
   for (int i = 0; i < total; ++i)

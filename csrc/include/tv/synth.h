@@ -58,22 +58,22 @@ TV_HD SynthObject synth_object(uint32_t seed, int k, int W, int H) {
 
 constexpr int kSynthObjects = 6;
 
-// Sample of plane c (0=Y,1=U,2=V) at component coordinates (x, y) of frame t.
-TV_HD int synth_sample(uint32_t seed, int t, int c, int x, int y, int W, int H) {
-  const int s = c ? 1 : 0;
-  const int xl = x << s, yl = y << s;  // luma-grid position
-  // background pan: (2.25, 0.75) px/frame
-  const int32_t bx16 = xl * 16 + t * 36, by16 = yl * 16 + t * 12;
-  int v;
-  if (c == 0) {
-    v = (synth_vnoise(bx16, by16, 7, seed) * 5 + synth_vnoise(bx16, by16, 5, seed + 1) * 2 +
-         synth_vnoise(bx16, by16, 3, seed + 2)) >> 3;
-  } else {
-    v = 96 + (synth_vnoise(bx16, by16, 8, seed + 10 * c) >> 1);
-  }
-  // objects (later ones on top)
+// Per-frame state: object positions after bouncing (computed once per frame).
+struct SynthFrameCtx {
+  uint32_t seed;
+  int t, W, H;
+  SynthObject obj[kSynthObjects];
+  int32_t ox[kSynthObjects], oy[kSynthObjects];
+};
+
+TV_HD void synth_frame_ctx(uint32_t seed, int t, int W, int H, SynthFrameCtx& f) {
+  f.seed = seed;
+  f.t = t;
+  f.W = W;
+  f.H = H;
   for (int k = 0; k < kSynthObjects; ++k) {
     const SynthObject o = synth_object(seed, k, W, H);
+    f.obj[k] = o;
     // bounce inside the frame: triangle wave of the trajectory
     const int32_t spanx = (W - o.w) * 16, spany = (H - o.h) * 16;
     int32_t ox = o.x16 + o.vx16 * t, oy = o.y16 + o.vy16 * t;
@@ -87,7 +87,28 @@ TV_HD int synth_sample(uint32_t seed, int t, int c, int x, int y, int W, int H) 
       if (m < 0) m += 2 * spany;
       oy = m < spany ? m : 2 * spany - m;
     }
-    const int32_t rx16 = xl * 16 - ox, ry16 = yl * 16 - oy;
+    f.ox[k] = ox;
+    f.oy[k] = oy;
+  }
+}
+
+// Sample of plane c (0=Y,1=U,2=V) at component coordinates (x, y).
+TV_HD int synth_sample_ctx(const SynthFrameCtx& f, int c, int x, int y) {
+  const int s = c ? 1 : 0;
+  const int xl = x << s, yl = y << s;  // luma-grid position
+  // background pan: (2.25, 0.75) px/frame
+  const int32_t bx16 = xl * 16 + f.t * 36, by16 = yl * 16 + f.t * 12;
+  const uint32_t seed = f.seed;
+  int v;
+  if (c == 0) {
+    v = (synth_vnoise(bx16, by16, 7, seed) * 5 + synth_vnoise(bx16, by16, 5, seed + 1) * 2 +
+         synth_vnoise(bx16, by16, 3, seed + 2)) >> 3;
+  } else {
+    v = 96 + (synth_vnoise(bx16, by16, 8, seed + 10 * c) >> 1);
+  }
+  for (int k = 0; k < kSynthObjects; ++k) {  // later objects on top
+    const SynthObject& o = f.obj[k];
+    const int32_t rx16 = xl * 16 - f.ox[k], ry16 = yl * 16 - f.oy[k];
     if (rx16 < 0 || ry16 < 0 || rx16 >= o.w * 16 || ry16 >= o.h * 16) continue;
     if (o.shape == 1) {
       const int64_t dx = 2 * (int64_t)rx16 - o.w * 16, dy = 2 * (int64_t)ry16 - o.h * 16;
@@ -101,6 +122,12 @@ TV_HD int synth_sample(uint32_t seed, int t, int c, int x, int y, int W, int H) 
     }
   }
   return clip_pixel(v);
+}
+
+TV_HD int synth_sample(uint32_t seed, int t, int c, int x, int y, int W, int H) {
+  SynthFrameCtx f;
+  synth_frame_ctx(seed, t, W, H, f);
+  return synth_sample_ctx(f, c, x, y);
 }
 
 }  // namespace tv
