@@ -26,8 +26,12 @@ __device__ inline void tb_init(TbScratch& s) {
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) s.T[i >> 5][i & 31] = kDct32.m[i >> 5][i & 31];
 }
 
-__device__ __forceinline__ int tbT(const TbScratch& s, int log2N, int k, int n) {
-  return s.T[k << (5 - log2N)][n];
+__device__ __forceinline__ int tbT(const int (*T)[33], int log2N, int k, int n) {
+  return T[k << (5 - log2N)][n];
+}
+__device__ __forceinline__ int tbT(const TbScratch& s, int log2N, int k, int n) { return tbT(s.T, log2N, k, n); }
+__device__ inline void tb_load_matrix(int (*T)[33]) {
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) T[i >> 5][i & 31] = kDct32.m[i >> 5][i & 31];
 }
 
 // One 16x16 output tile P = X * Y (K = 16 or 32) on the calling wave.  X(i,k), Y(k,j) are
