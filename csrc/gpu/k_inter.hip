@@ -16,6 +16,7 @@
 #include "gpu_common.h"
 #include "k_encode.h"
 #include "tb_coder.h"
+#include "wave_tb.h"
 
 namespace tv {
 namespace gpu {
@@ -248,22 +249,33 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   }
 }
 
+// P-frame pass B: CUs of a P-frame are independent (inter-only), so each wavefront of the
+// workgroup codes its own CUs wave-synchronously; no workgroup barrier per TB.
+struct CuLds {
+  uint8_t pred[1024];
+  int16_t resid[1024];
+  WaveTbScratch tb;
+};
+
 __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                      FrameSet rec, DecisionSet dec, Geo g, int qp) {
-  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int ctu = blockIdx.x, b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
-  __shared__ int pred[1024], resid[1024];
-  __shared__ TbScratch scr;
+  __shared__ int Tm[32][33];
+  __shared__ CuLds W[4];
   const long ub = b * g.usz;
   const int qpc = chroma_qp(qp, 0);
   const uint8_t* ph = phase + (long)b * 16 * g.psz;
-  tb_init(scr);
+  tb_load_matrix(Tm);
   __syncthreads();
+  CuLds& Ld = W[wave];
+  int nth = 0;  // CU ordinal within the CTB; CU k goes to wave k % 4
   for (int k8 = 0; k8 < 16; ++k8) {
     const int x0 = cx + (k8 & 3) * 8, y0 = cy + (k8 >> 2) * 8;
     const long u = ub + (y0 >> 3) * g.w8 + (x0 >> 3);
     const int log2 = dec.cu_log2[u];
     if ((x0 & ((1 << log2) - 1)) || (y0 & ((1 << log2) - 1))) continue;  // not a CU origin
+    if ((nth++ & 3) != wave) continue;
     const int mvx = dec.mv[2 * u], mvy = dec.mv[2 * u + 1];
     int cbf = 0;
     for (int c = 0; c < 3; ++c) {
@@ -273,30 +285,30 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
       const uint8_t* S = src.plane(c, b, g);
       if (c == 0) {
         const uint8_t* P = ph + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
-        for (int i = tid; i < N * N; i += 256) {
+        for (int i = lane; i < N * N; i += 64) {
           const int px = i & (N - 1), py = i >> l2;
           const int p = phase_at(P, g, x + px + (mvx >> 2), y + py + (mvy >> 2));
-          pred[i] = p;
-          resid[i] = (int)S[(y + py) * pw + x + px] - p;
+          Ld.pred[i] = (uint8_t)p;
+          Ld.resid[i] = (int16_t)((int)S[(y + py) * pw + x + px] - p);
         }
       } else {
         const uint8_t* Rf = ref.plane(c, b, g);
-        for (int i = tid; i < N * N; i += 256) {
+        for (int i = lane; i < N * N; i += 64) {
           const int px = i & (N - 1), py = i >> l2;
           const int p = mc_chroma_sample(Rf, pw, pw, phh, x + px + (mvx >> 3), y + py + (mvy >> 3), mvx & 7, mvy & 7);
-          pred[i] = p;
-          resid[i] = (int)S[(y + py) * pw + x + px] - p;
+          Ld.pred[i] = (uint8_t)p;
+          Ld.resid[i] = (int16_t)((int)S[(y + py) * pw + x + px] - p);
         }
       }
-      __syncthreads();
+      wave_sync();
       int16_t* lev = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz) +
                      (long)y * pw + x;
-      const int cb = wg_code_tb(resid, pred, l2, c ? qpc : qp, false, lev, pw,
-                                rec.plane(c, b, g) + (long)y * pw + x, pw, scr);
+      const int cb = wave_code_tb(Ld.resid, Ld.pred, l2, c ? qpc : qp, false, lev, pw,
+                                  rec.plane(c, b, g) + (long)y * pw + x, pw, Tm, Ld.tb);
       cbf |= cb << c;
     }
     const int n8 = 1 << (log2 - 3);
-    if (tid < n8 * n8) dec.cbf[u + (tid / n8) * g.w8 + (tid % n8)] = (uint8_t)cbf;
+    if (lane < n8 * n8) dec.cbf[u + (lane / n8) * g.w8 + (lane % n8)] = (uint8_t)cbf;
   }
 }
 

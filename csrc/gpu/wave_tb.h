@@ -11,10 +11,12 @@
 namespace tv {
 namespace gpu {
 
-// Order LDS accesses of this wave (all lanes execute it): waits for outstanding LDS/VMEM ops
-// and stops the compiler from moving memory operations across.
+// Order LDS accesses between the lanes of this wave.  A wave's DS instructions execute in
+// issue order, so only the compiler has to be stopped from moving memory operations across;
+// a wavefront-scope fence emits no wait at all (a workgroup-scope fence would also wait for
+// every outstanding global store, vmcnt(0), which dominated the wavefront latency).
 __device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
