@@ -249,9 +249,9 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   }
 }
 
-// P-frame pass B: CUs of a P-frame are independent (inter-only), so each wavefront of the
-// workgroup codes its own CUs wave-synchronously; no workgroup barrier per TB.
-struct CuLds {
+// P-frame pass B: all TBs of a P-frame are independent (inter-only), so the (CU, component)
+// TBs of a CTB are dealt round-robin to the 4 waves and coded wave-synchronously.
+struct TbLds {
   uint8_t pred[1024];
   int16_t resid[1024];
   WaveTbScratch tb;
@@ -262,53 +262,68 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
   const int ctu = blockIdx.x, b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
   __shared__ int Tm[32][33];
-  __shared__ CuLds W[4];
+  __shared__ TbLds W[4];
+  __shared__ int cus[16][4];  // x0, y0, log2, unit
+  __shared__ int ncu;
+  __shared__ unsigned cbfs[16];
   const long ub = b * g.usz;
-  const int qpc = chroma_qp(qp, 0);
   const uint8_t* ph = phase + (long)b * 16 * g.psz;
   tb_load_matrix(Tm);
-  __syncthreads();
-  CuLds& Ld = W[wave];
-  int nth = 0;  // CU ordinal within the CTB; CU k goes to wave k % 4
-  for (int k8 = 0; k8 < 16; ++k8) {
-    const int x0 = cx + (k8 & 3) * 8, y0 = cy + (k8 >> 2) * 8;
-    const long u = ub + (y0 >> 3) * g.w8 + (x0 >> 3);
-    const int log2 = dec.cu_log2[u];
-    if ((x0 & ((1 << log2) - 1)) || (y0 & ((1 << log2) - 1))) continue;  // not a CU origin
-    if ((nth++ & 3) != wave) continue;
-    const int mvx = dec.mv[2 * u], mvy = dec.mv[2 * u + 1];
-    int cbf = 0;
-    for (int c = 0; c < 3; ++c) {
-      const int l2 = c ? log2 - 1 : log2, N = 1 << l2;
-      const int x = c ? x0 >> 1 : x0, y = c ? y0 >> 1 : y0;
-      const int pw = c ? g.W / 2 : g.W, phh = c ? g.H / 2 : g.H;
-      const uint8_t* S = src.plane(c, b, g);
-      if (c == 0) {
-        const uint8_t* P = ph + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
-        for (int i = lane; i < N * N; i += 64) {
-          const int px = i & (N - 1), py = i >> l2;
-          const int p = phase_at(P, g, x + px + (mvx >> 2), y + py + (mvy >> 2));
-          Ld.pred[i] = (uint8_t)p;
-          Ld.resid[i] = (int16_t)((int)S[(y + py) * pw + x + px] - p);
-        }
-      } else {
-        const uint8_t* Rf = ref.plane(c, b, g);
-        for (int i = lane; i < N * N; i += 64) {
-          const int px = i & (N - 1), py = i >> l2;
-          const int p = mc_chroma_sample(Rf, pw, pw, phh, x + px + (mvx >> 3), y + py + (mvy >> 3), mvx & 7, mvy & 7);
-          Ld.pred[i] = (uint8_t)p;
-          Ld.resid[i] = (int16_t)((int)S[(y + py) * pw + x + px] - p);
-        }
-      }
-      wave_sync();
-      int16_t* lev = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz) +
-                     (long)y * pw + x;
-      const int cb = wave_code_tb(Ld.resid, Ld.pred, l2, c ? qpc : qp, false, lev, pw,
-                                  rec.plane(c, b, g) + (long)y * pw + x, pw, Tm, Ld.tb);
-      cbf |= cb << c;
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int k8 = 0; k8 < 16; ++k8) {
+      const int x0 = cx + (k8 & 3) * 8, y0 = cy + (k8 >> 2) * 8;
+      const int u = (y0 >> 3) * g.w8 + (x0 >> 3);
+      const int log2 = dec.cu_log2[ub + u];
+      if ((x0 & ((1 << log2) - 1)) || (y0 & ((1 << log2) - 1))) continue;  // not a CU origin
+      cus[n][0] = x0;
+      cus[n][1] = y0;
+      cus[n][2] = log2;
+      cus[n][3] = u;
+      ++n;
     }
-    const int n8 = 1 << (log2 - 3);
-    if (lane < n8 * n8) dec.cbf[u + (lane / n8) * g.w8 + (lane % n8)] = (uint8_t)cbf;
+    ncu = n;
+  }
+  if (threadIdx.x < 16) cbfs[threadIdx.x] = 0;
+  __syncthreads();
+  TbLds& Ld = W[wave];
+  for (int t = wave; t < 3 * ncu; t += 4) {
+    const int k = t / 3, c = t - 3 * k;
+    const int x0 = cus[k][0], y0 = cus[k][1], log2 = cus[k][2];
+    const long u = ub + cus[k][3];
+    const int mvx = dec.mv[2 * u], mvy = dec.mv[2 * u + 1];
+    const int l2 = c ? log2 - 1 : log2, N = 1 << l2;
+    const int x = c ? x0 >> 1 : x0, y = c ? y0 >> 1 : y0;
+    const int pw = c ? g.W / 2 : g.W, phh = c ? g.H / 2 : g.H;
+    const uint8_t* S = src.plane(c, b, g);
+    if (c == 0) {
+      const uint8_t* P = ph + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
+      for (int i = lane; i < N * N; i += 64) {
+        const int px = i & (N - 1), py = i >> l2;
+        const int p = phase_at(P, g, x + px + (mvx >> 2), y + py + (mvy >> 2));
+        Ld.pred[i] = (uint8_t)p;
+        Ld.resid[i] = (int16_t)((int)S[(y + py) * pw + x + px] - p);
+      }
+    } else {
+      const uint8_t* Rf = ref.plane(c, b, g);
+      for (int i = lane; i < N * N; i += 64) {
+        const int px = i & (N - 1), py = i >> l2;
+        const int p = mc_chroma_sample(Rf, pw, pw, phh, x + px + (mvx >> 3), y + py + (mvy >> 3), mvx & 7, mvy & 7);
+        Ld.pred[i] = (uint8_t)p;
+        Ld.resid[i] = (int16_t)((int)S[(y + py) * pw + x + px] - p);
+      }
+    }
+    wave_sync();
+    int16_t* lev = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz) +
+                   (long)y * pw + x;
+    const int cb = wave_code_tb(Ld.resid, Ld.pred, l2, c ? chroma_qp(qp, 0) : qp, false, lev, pw,
+                                rec.plane(c, b, g) + (long)y * pw + x, pw, Tm, Ld.tb);
+    if (lane == 0 && cb) atomicOr(&cbfs[k], 1u << c);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < ncu * 16; k += blockDim.x) {
+    const int cu = k >> 4, j = k & 15, n8 = 1 << (cus[cu][2] - 3);
+    if (j < n8 * n8) dec.cbf[ub + cus[cu][3] + (j / n8) * g.w8 + j % n8] = (uint8_t)cbfs[cu];
   }
 }
 

@@ -158,175 +158,166 @@ __global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSe
   }
 }
 
-// ------------------------- I-frame pass B: wave-per-CTU wavefront -----------------------
-// Each wavefront owns one CTB of the current anti-diagonal: its source, its own
-// reconstruction and the reconstructed borders of its left / above / above-right
-// neighbours are staged in LDS once, so every TB of the CTB is predicted, transformed and
-// reconstructed from LDS with wave-synchronous code (no workgroup barrier per TB).
-struct CtuLds {
-  uint8_t src[3][1024];
-  uint8_t rec[3][1024];
-  uint8_t top[3][72];   // row y = cy-1, x = cx-1 .. cx+2S-1  (index 0 = corner)
-  uint8_t left[3][32];  // column x = cx-1, y = cy .. cy+S-1
+// ------------------- I-frame pass B: CTB wavefront, one wave per component ----------------
+// Each workgroup (3 waves) owns one CTB of the current anti-diagonal.  Intra prediction of a
+// component only reads that component's reconstruction, so Y, Cb and Cr are three
+// independent chains: wave c codes every TB of component c in z-order.  The component's
+// source, own reconstruction and the reconstructed borders of the left / above /
+// above-right neighbours are staged in LDS once; each TB is then predicted, transformed and
+// reconstructed wave-synchronously from LDS (no workgroup barrier per TB).
+struct CompLds {
+  uint8_t src[1024];
+  uint8_t rec[1024];
+  uint8_t top[72];   // row y = cy-1, x = cx-1 .. cx+2S-1  (index 0 = corner)
+  uint8_t left[32];  // column x = cx-1, y = cy .. cy+S-1
   uint8_t pred[1024];
   int16_t resid[1024];
   int V[132];
   int L[65], T[65], FL[65], FT[65];
-  int cus[16][3];
-  int ncu;
   WaveTbScratch tb;
 };
 
-__global__ void __launch_bounds__(256) k_intra_recon(FrameSet src, FrameSet rec, DecisionSet dec, Geo g, int qp,
-                                                     int diag, int cy0, int cy1) {
-  const int b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec, DecisionSet dec, Geo g, int qp,
+                                                     int diag, int cy0) {
+  const int b = blockIdx.y, c = threadIdx.x >> 6, lane = threadIdx.x & 63;
   __shared__ int Tm[32][33];
-  __shared__ CtuLds W[4];
-  tb_load_matrix(Tm);
-  __syncthreads();
-  const int cyi = cy0 + blockIdx.x * 4 + wave;
-  if (cyi > cy1) return;  // wave-uniform; no barriers below
-  CtuLds& L = W[wave];
-  const int cxi = diag - 2 * cyi;
+  __shared__ CompLds W[3];
+  __shared__ int cus[16][3];
+  __shared__ int ncu;
+  __shared__ unsigned cbfs[16];
+  const int cyi = cy0 + blockIdx.x, cxi = diag - 2 * cyi;
   const int cx = cxi * 32, cy = cyi * 32;
   const long ub = b * g.usz;
-  const int qpc = chroma_qp(qp, 0);
-  // stage source + neighbour borders
-  for (int c = 0; c < 3; ++c) {
-    const int S = c ? 16 : 32, sh = c ? 1 : 0;
-    const int pw = g.W >> sh, ph = g.H >> sh, x0 = cx >> sh, y0 = cy >> sh;
-    const uint8_t* Sp = src.plane(c, b, g);
-    const uint8_t* Rp = rec.plane(c, b, g);
-    for (int i = lane; i < S * S; i += 64) L.src[c][i] = Sp[(long)(y0 + i / S) * pw + x0 + i % S];
-    for (int i = lane; i <= 2 * S; i += 64) {
-      const int x = tv_min(pw - 1, tv_max(0, x0 - 1 + i)), y = tv_max(0, y0 - 1);
-      L.top[c][i] = Rp[(long)y * pw + x];
-    }
-    for (int i = lane; i < S; i += 64) L.left[c][i] = Rp[(long)tv_min(ph - 1, y0 + i) * pw + tv_max(0, x0 - 1)];
-  }
-  if (lane == 0) {  // CUs of this CTB in z-order
+  tb_load_matrix(Tm);
+  if (threadIdx.x == 0) {  // CUs of this CTB in z-order
     int n = 0;
     if (dec.cu_log2[ub + (cy >> 3) * g.w8 + (cx >> 3)] == 5) {
-      L.cus[0][0] = cx;
-      L.cus[0][1] = cy;
-      L.cus[0][2] = 5;
+      cus[0][0] = cx;
+      cus[0][1] = cy;
+      cus[0][2] = 5;
       n = 1;
     } else {
       for (int q = 0; q < 4; ++q) {
         const int x16 = cx + (q & 1) * 16, y16 = cy + (q >> 1) * 16;
         if (dec.cu_log2[ub + (y16 >> 3) * g.w8 + (x16 >> 3)] == 4) {
-          L.cus[n][0] = x16;
-          L.cus[n][1] = y16;
-          L.cus[n][2] = 4;
+          cus[n][0] = x16;
+          cus[n][1] = y16;
+          cus[n][2] = 4;
           ++n;
         } else {
           for (int r = 0; r < 4; ++r) {
-            L.cus[n][0] = x16 + (r & 1) * 8;
-            L.cus[n][1] = y16 + (r >> 1) * 8;
-            L.cus[n][2] = 3;
+            cus[n][0] = x16 + (r & 1) * 8;
+            cus[n][1] = y16 + (r >> 1) * 8;
+            cus[n][2] = 3;
             ++n;
           }
         }
       }
     }
-    L.ncu = n;
+    ncu = n;
   }
-  wave_sync();
-  const int ncu = L.ncu;
+  if (threadIdx.x < 16) cbfs[threadIdx.x] = 0;
+  CompLds& L = W[c];
+  const int sh = c ? 1 : 0, S = c ? 16 : 32;
+  const int pw = g.W >> sh, ph = g.H >> sh, bx = cx >> sh, by = cy >> sh;
+  {  // stage source + neighbour borders of this component
+    const uint8_t* Sp = src.plane(c, b, g);
+    const uint8_t* Rp = rec.plane(c, b, g);
+    for (int i = lane; i < S * S; i += 64) L.src[i] = Sp[(long)(by + i / S) * pw + bx + i % S];
+    for (int i = lane; i <= 2 * S; i += 64)
+      L.top[i] = Rp[(long)tv_max(0, by - 1) * pw + tv_min(pw - 1, tv_max(0, bx - 1 + i))];
+    for (int i = lane; i < S; i += 64) L.left[i] = Rp[(long)tv_min(ph - 1, by + i) * pw + tv_max(0, bx - 1)];
+  }
+  __syncthreads();
+  const int qpx = c ? chroma_qp(qp, 0) : qp;
+  int16_t* coefp = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz);
   for (int k = 0; k < ncu; ++k) {
-    const int x0 = L.cus[k][0], y0 = L.cus[k][1], log2 = L.cus[k][2];
-    const long u = ub + (y0 >> 3) * g.w8 + (x0 >> 3);
-    const int mode = dec.ipm[u];
-    int cbf = 0;
-    for (int c = 0; c < 3; ++c) {
-      const int sh = c ? 1 : 0, S = c ? 16 : 32;
-      const int l2 = log2 - sh, N = 1 << l2;
-      const int x = x0 >> sh, y = y0 >> sh;     // TB position (component samples)
-      const int bx = cx >> sh, by = cy >> sh;   // CTB origin (component samples)
-      // --- reference samples in canonical order (bottom-left .. corner .. top-right)
-      const int total = 4 * N + 1;
-      unsigned long long m[3] = {0, 0, 0};
+    const int x0 = cus[k][0], y0 = cus[k][1], log2 = cus[k][2];
+    const int mode = dec.ipm[ub + (y0 >> 3) * g.w8 + (x0 >> 3)];
+    const int l2 = log2 - sh, N = 1 << l2;
+    const int x = x0 >> sh, y = y0 >> sh;  // TB position (component samples)
+    // --- reference samples in canonical order (bottom-left .. corner .. top-right)
+    const int total = 4 * N + 1;
+    unsigned long long m[3] = {0, 0, 0};
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int i = lane + 64 * r;
-        bool av = false;
+    for (int r = 0; r < 3; ++r) {
+      const int i = lane + 64 * r;
+      bool av = false;
+      if (i < total) {
+        int xn, yn;
+        if (i < 2 * N) {
+          xn = x - 1;
+          yn = y + 2 * N - 1 - i;
+        } else {
+          xn = x - 1 + (i - 2 * N);
+          yn = y - 1;
+        }
+        av = zscan_available(x0, y0, xn << sh, yn << sh, g.W, g.H);
         int val = 0;
-        if (i < total) {
-          int xn, yn;
-          if (i < 2 * N) {
-            xn = x - 1;
-            yn = y + 2 * N - 1 - i;
-          } else {
-            xn = x - 1 + (i - 2 * N);
-            yn = y - 1;
-          }
-          av = zscan_available(x0, y0, xn << sh, yn << sh, g.W, g.H);
-          if (av) {
-            if (xn >= bx && yn >= by) val = L.rec[c][(yn - by) * S + (xn - bx)];
-            else if (yn == by - 1) val = L.top[c][xn - (bx - 1)];
-            else val = L.left[c][yn - by];
-          }
-          L.V[i] = val;
+        if (av) {
+          if (xn >= bx && yn >= by) val = L.rec[(yn - by) * S + (xn - bx)];
+          else if (yn == by - 1) val = L.top[xn - (bx - 1)];
+          else val = L.left[yn - by];
         }
-        m[r] = __ballot(av);
+        L.V[i] = val;
       }
-      wave_sync();
-      // --- substitution (H.265 8.4.4.2.2) as a parallel nearest-available search
-      for (int i = lane; i < total; i += 64) {
-        int j = -1;
-        for (int w = i >> 6; w >= 0 && j < 0; --w) {
-          const unsigned long long mm = (w == (i >> 6)) ? (m[w] & (((i & 63) == 63) ? ~0ull : ((2ull << (i & 63)) - 1))) : m[w];
-          if (mm) j = w * 64 + 63 - __clzll(mm);
-        }
-        if (j < 0)
-          for (int w = 0; w < 3 && j < 0; ++w)
-            if (m[w]) j = w * 64 + __ffsll(m[w]) - 1;
-        const int v = j < 0 ? 128 : L.V[j];
-        if (i < 2 * N) L.L[2 * N - i] = v;
-        else if (i == 2 * N) L.L[0] = L.T[0] = v;
-        else L.T[i - 2 * N] = v;
-      }
-      wave_sync();
-      const bool filt = c == 0 && intra_filter_refs(l2, mode);
-      if (filt) {
-        for (int i = lane; i <= 2 * N; i += 64) {
-          if (i == 0) {
-            L.FL[0] = L.FT[0] = (L.L[1] + 2 * L.L[0] + L.T[1] + 2) >> 2;
-          } else if (i == 2 * N) {
-            L.FL[i] = L.L[i];
-            L.FT[i] = L.T[i];
-          } else {
-            L.FL[i] = (L.L[i + 1] + 2 * L.L[i] + L.L[i - 1] + 2) >> 2;
-            L.FT[i] = (L.T[i + 1] + 2 * L.T[i] + L.T[i - 1] + 2) >> 2;
-          }
-        }
-        wave_sync();
-      }
-      const int* RL = filt ? L.FL : L.L;
-      const int* RT = filt ? L.FT : L.T;
-      const int dc = mode == 1 ? intra_dc_value(RL, RT, l2) : 0;
-      for (int i = lane; i < N * N; i += 64) {
-        const int px = i & (N - 1), py = i >> l2;
-        const int p = intra_pred_pixel(RL, RT, l2, mode, c == 0 && N < 32, dc, px, py);
-        L.pred[i] = (uint8_t)p;
-        L.resid[i] = (int16_t)((int)L.src[c][(y - by + py) * S + (x - bx + px)] - p);
-      }
-      wave_sync();
-      const int pw = g.W >> sh;
-      int16_t* lev = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz) +
-                     (long)y * pw + x;
-      const int cb = wave_code_tb(L.resid, L.pred, l2, c ? qpc : qp, true, lev, pw,
-                                  &L.rec[c][(y - by) * S + (x - bx)], S, Tm, L.tb);
-      cbf |= cb << c;
+      m[r] = __ballot(av);
     }
-    const int n8 = 1 << (log2 - 3);
-    if (lane < n8 * n8) dec.cbf[u + (lane / n8) * g.w8 + (lane % n8)] = (uint8_t)cbf;
+    wave_sync();
+    // --- substitution (H.265 8.4.4.2.2) as a parallel nearest-available search
+    for (int i = lane; i < total; i += 64) {
+      int j = -1;
+      for (int w = i >> 6; w >= 0 && j < 0; --w) {
+        const unsigned long long mm =
+            (w == (i >> 6)) ? (m[w] & (((i & 63) == 63) ? ~0ull : ((2ull << (i & 63)) - 1))) : m[w];
+        if (mm) j = w * 64 + 63 - __clzll(mm);
+      }
+      if (j < 0)
+        for (int w = 0; w < 3 && j < 0; ++w)
+          if (m[w]) j = w * 64 + __ffsll(m[w]) - 1;
+      const int v = j < 0 ? 128 : L.V[j];
+      if (i < 2 * N) L.L[2 * N - i] = v;
+      else if (i == 2 * N) L.L[0] = L.T[0] = v;
+      else L.T[i - 2 * N] = v;
+    }
+    wave_sync();
+    const bool filt = c == 0 && intra_filter_refs(l2, mode);
+    if (filt) {
+      for (int i = lane; i <= 2 * N; i += 64) {
+        if (i == 0) {
+          L.FL[0] = L.FT[0] = (L.L[1] + 2 * L.L[0] + L.T[1] + 2) >> 2;
+        } else if (i == 2 * N) {
+          L.FL[i] = L.L[i];
+          L.FT[i] = L.T[i];
+        } else {
+          L.FL[i] = (L.L[i + 1] + 2 * L.L[i] + L.L[i - 1] + 2) >> 2;
+          L.FT[i] = (L.T[i + 1] + 2 * L.T[i] + L.T[i - 1] + 2) >> 2;
+        }
+      }
+      wave_sync();
+    }
+    const int* RL = filt ? L.FL : L.L;
+    const int* RT = filt ? L.FT : L.T;
+    const int dc = mode == 1 ? intra_dc_value(RL, RT, l2) : 0;
+    for (int i = lane; i < N * N; i += 64) {
+      const int px = i & (N - 1), py = i >> l2;
+      const int p = intra_pred_pixel(RL, RT, l2, mode, c == 0 && N < 32, dc, px, py);
+      L.pred[i] = (uint8_t)p;
+      L.resid[i] = (int16_t)((int)L.src[(y - by + py) * S + (x - bx + px)] - p);
+    }
+    wave_sync();
+    const int cb = wave_code_tb(L.resid, L.pred, l2, qpx, true, coefp + (long)y * pw + x, pw,
+                                &L.rec[(y - by) * S + (x - bx)], S, Tm, L.tb);
+    if (lane == 0 && cb) atomicOr(&cbfs[k], 1u << c);
   }
-  // write the CTB reconstruction back
-  for (int c = 0; c < 3; ++c) {
-    const int S = c ? 16 : 32, sh = c ? 1 : 0, pw = g.W >> sh;
-    uint8_t* Rp = rec.plane(c, b, g) + (long)(cy >> sh) * pw + (cx >> sh);
-    for (int i = lane; i < S * S; i += 64) Rp[(long)(i / S) * pw + i % S] = L.rec[c][i];
+  __syncthreads();
+  // write the CTB reconstruction and the per-CU cbf flags back
+  uint8_t* Rp = rec.plane(c, b, g) + (long)by * pw + bx;
+  for (int i = lane; i < S * S; i += 64) Rp[(long)(i / S) * pw + i % S] = L.rec[i];
+  for (int k = threadIdx.x; k < ncu * 16; k += blockDim.x) {
+    const int cu = k >> 4, j = k & 15, log2 = cus[cu][2], n8 = 1 << (log2 - 3);
+    if (j < n8 * n8)
+      dec.cbf[ub + ((cus[cu][1] >> 3) + j / n8) * g.w8 + (cus[cu][0] >> 3) + j % n8] = (uint8_t)cbfs[cu];
   }
 }
 
@@ -338,8 +329,7 @@ void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& 
     const int cy0 = tv_max(0, (d - (g.wc - 1) + 1) / 2);
     const int cy1 = tv_min(g.hc - 1, d / 2);
     if (cy1 < cy0) continue;
-    const int n = cy1 - cy0 + 1;
-    k_intra_recon<<<dim3((n + 3) / 4, B), 256, 0, s>>>(src, rec, dec, g, qp, d, cy0, cy1);
+    k_intra_recon<<<dim3(cy1 - cy0 + 1, B), 192, 0, s>>>(src, rec, dec, g, qp, d, cy0);
   }
 }
 
