@@ -388,17 +388,59 @@ class SliceWriter {
     if (intra || cb || cr) bin(cl, CTX_CBF_LUMA + 1);
     else if (!cl) throw std::runtime_error("inter CU with rqt_root_cbf=1 but no residual");
     const int cmode = intra ? chroma_intra_mode(4, mode) : 0;
-    if (cl)
-      residual(fd_.coef[0] + (size_t)y0 * cfg_.coded_w + x0, cfg_.coded_w, log2, 0,
-               scan_idx_for(intra, log2, 0, mode));
-    const int cs = cfg_.coded_w >> 1;
-    if (cb)
-      residual(fd_.coef[1] + (size_t)(y0 >> 1) * cs + (x0 >> 1), cs, log2 - 1, 1,
-               scan_idx_for(intra, log2 - 1, 1, cmode));
-    if (cr)
-      residual(fd_.coef[2] + (size_t)(y0 >> 1) * cs + (x0 >> 1), cs, log2 - 1, 2,
-               scan_idx_for(intra, log2 - 1, 2, cmode));
+    int stride;
+    if (cl) {
+      const int16_t* p = tb_levels(0, x0, y0, log2, stride);
+      residual(p, stride, log2, 0, scan_idx_for(intra, log2, 0, mode));
+    }
+    if (cb) {
+      const int16_t* p = tb_levels(1, x0 >> 1, y0 >> 1, log2 - 1, stride);
+      residual(p, stride, log2 - 1, 1, scan_idx_for(intra, log2 - 1, 1, cmode));
+    }
+    if (cr) {
+      const int16_t* p = tb_levels(2, x0 >> 1, y0 >> 1, log2 - 1, stride);
+      residual(p, stride, log2 - 1, 2, scan_idx_for(intra, log2 - 1, 2, cmode));
+    }
   }
+
+  // Levels of the TB of component c at component position (x, y): a pointer into the dense
+  // plane, or (compact GPU form) a gather of its non-zero 4x4 groups into tbbuf_.
+  const int16_t* tb_levels(int c, int x, int y, int log2N, int& stride) {
+    if (!fd_.sb_packed) {
+      stride = c ? cfg_.coded_w >> 1 : cfg_.coded_w;
+      return fd_.coef[c] + (size_t)y * stride + x;
+    }
+    const int N = 1 << log2N, ng = N >> 2;
+    stride = N;
+    std::memset(tbbuf_, 0, sizeof(int16_t) * N * N);
+    for (int gy = 0; gy < ng; ++gy)
+      for (int gx = 0; gx < ng; ++gx) {
+        const int X = x + 4 * gx, Y = y + 4 * gy;
+        int ctb, bit;
+        if (c == 0) {
+          ctb = (Y >> 5) * fd_.wc + (X >> 5);
+          bit = ((Y & 31) >> 2) * 8 + ((X & 31) >> 2);
+        } else {
+          ctb = (Y >> 4) * fd_.wc + (X >> 4);
+          bit = ((Y & 15) >> 2) * 4 + ((X & 15) >> 2) + (c == 2 ? 16 : 0);
+        }
+        const uint64_t my = fd_.sb_mask_y[ctb];
+        const uint32_t mc = fd_.sb_mask_c[ctb];
+        int rank;
+        if (c == 0) {
+          if (!((my >> bit) & 1)) continue;
+          rank = __builtin_popcountll(my & ((1ull << bit) - 1));
+        } else {
+          if (!((mc >> bit) & 1)) continue;
+          rank = __builtin_popcountll(my) + __builtin_popcount(mc & ((1u << bit) - 1));
+        }
+        const int16_t* src = fd_.sb_packed + ((size_t)fd_.sb_offset[ctb] + rank) * 16;
+        for (int r = 0; r < 4; ++r)
+          std::memcpy(tbbuf_ + (4 * gy + r) * N + 4 * gx, src + 4 * r, 4 * sizeof(int16_t));
+      }
+    return tbbuf_;
+  }
+  int16_t tbbuf_[32 * 32];
 
   void write_last_prefix(int pos, int log2N, int cIdx, int base) {
     const int prefix = kGroupIdx[pos];

@@ -96,9 +96,11 @@ class Engine {
     if (c.range < 4 || c.range > 16 || (c.range & 3))
       throw std::runtime_error("search range must be 4, 8, 12 or 16");
     if ((c.width & 1) || (c.height & 1)) throw std::runtime_error("odd frame size");
+    if (c.width < 64 || c.height < 64) throw std::runtime_error("frame must be at least 64x64");
     HIP_OK(hipSetDevice(c.device));
     HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     const long B = c.batch;
+    nctu_ = g_.wc * g_.hc;
     auto alloc_set = [&](FrameSet& f) {
       HIP_OK(hipMalloc(&f.y, B * g_.ysz));
       HIP_OK(hipMalloc(&f.u, B * g_.csz));
@@ -107,21 +109,22 @@ class Engine {
     alloc_set(src_);
     alloc_set(rec_[0]);
     alloc_set(rec_[1]);
-    HIP_OK(hipMalloc(&dec_.cu_log2, B * g_.usz));
-    HIP_OK(hipMalloc(&dec_.intra, B * g_.usz));
-    HIP_OK(hipMalloc(&dec_.ipm, B * g_.usz));
-    HIP_OK(hipMalloc(&dec_.cbf, B * g_.usz));
-    HIP_OK(hipMalloc(&dec_.mv, B * g_.usz * 2 * sizeof(int16_t)));
-    HIP_OK(hipMalloc(&dec_.coef_y, B * g_.ysz * sizeof(int16_t)));
-    HIP_OK(hipMalloc(&dec_.coef_u, B * g_.csz * sizeof(int16_t)));
-    HIP_OK(hipMalloc(&dec_.coef_v, B * g_.csz * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&coef_y_, B * g_.ysz * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&coef_u_, B * g_.csz * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&coef_v_, B * g_.csz * sizeof(int16_t)));
     HIP_OK(hipMalloc(&d_sse_, B * 3 * sizeof(unsigned long long)));
     HIP_OK(hipMalloc(&phase_, B * 16 * g_.psz));
-    slot_bytes_ = B * (4 * g_.usz + 2 * g_.usz * 2 + (g_.ysz + 2 * g_.csz) * 2);
+    HIP_OK(hipMalloc(&count_scratch_, B * nctu_ * sizeof(int)));
+    cap_ = g_.ysz + 2 * g_.csz;
+    // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
+    slot_bytes_ = align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * nctu_ * 8) +
+                  align(B * nctu_ * 4) + align(B * nctu_ * 4) + align(B * 4) + align(B * cap_ * 2);
     for (int k = 0; k < kSlots; ++k) {
-      HIP_OK(hipHostMalloc(&slots_[k].host, slot_bytes_, hipHostMallocDefault));
-      HIP_OK(hipEventCreateWithFlags(&slots_[k].ev, hipEventDisableTiming));
-      slots_[k].pending = 0;
+      Slot& s = slots_[k];
+      HIP_OK(hipMalloc(&s.dev, slot_bytes_));
+      HIP_OK(hipHostMalloc(&s.host, slot_bytes_, hipHostMallocDefault));
+      HIP_OK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+      s.pending = 0;
     }
     HIP_OK(hipEventCreate(&t0_));
     HIP_OK(hipEventCreate(&t1_));
@@ -144,16 +147,16 @@ class Engine {
   ~Engine() {
     pool_.reset();
     (void)hipStreamSynchronize(stream_);
-    for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u,
-                    rec_[1].v, dec_.cu_log2, dec_.intra, dec_.ipm, dec_.cbf})
+    for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u, rec_[1].v})
       (void)hipFree(p);
-    (void)hipFree(dec_.mv);
-    (void)hipFree(dec_.coef_y);
-    (void)hipFree(dec_.coef_u);
-    (void)hipFree(dec_.coef_v);
+    (void)hipFree(coef_y_);
+    (void)hipFree(coef_u_);
+    (void)hipFree(coef_v_);
     (void)hipFree(d_sse_);
     (void)hipFree(phase_);
+    (void)hipFree(count_scratch_);
     for (auto& s : slots_) {
+      (void)hipFree(s.dev);
       (void)hipHostFree(s.host);
       (void)hipEventDestroy(s.ev);
     }
@@ -190,61 +193,122 @@ class Engine {
   double sse(int b, int c) const { return sse_host_[b * 3 + c]; }
   double gpu_ms() const { return gpu_ms_; }
   double wall_ms() const { return wall_ms_; }
+  long coef_bytes() const { return coef_bytes_; }
   const Geo& geo() const { return g_; }
-  // device pointers of the current reconstruction (last frame) for tests
   FrameSet last_recon() const { return rec_[(cfg_.gop - 1) & 1]; }
-  DecisionSet decisions() const { return dec_; }
   hipStream_t stream() const { return stream_; }
 
  private:
   static constexpr int kSlots = 4;
+  static long align(long n) { return (n + 255) & ~255L; }
   struct Slot {
+    uint8_t* dev = nullptr;
     uint8_t* host = nullptr;
     hipEvent_t ev{};
     std::atomic<int> pending{0};
   };
+  // carve one slot buffer (device or host) into its arrays
+  struct Parts {
+    uint8_t *cu_log2, *intra, *ipm, *cbf;
+    int16_t* mv;
+    unsigned long long* mask_y;
+    unsigned* mask_c;
+    int *count, *offset, *total;
+    int16_t* packed;
+  };
+  Parts carve(uint8_t* base) const {
+    const long B = cfg_.batch, U = g_.usz;
+    Parts p;
+    uint8_t* q = base;
+    p.cu_log2 = q;
+    p.intra = q + B * U;
+    p.ipm = q + 2 * B * U;
+    p.cbf = q + 3 * B * U;
+    q += align(B * U * 4);
+    p.mv = reinterpret_cast<int16_t*>(q);
+    q += align(B * U * 4);
+    p.mask_y = reinterpret_cast<unsigned long long*>(q);
+    q += align(B * nctu_ * 8);
+    p.mask_c = reinterpret_cast<unsigned*>(q);
+    q += align(B * nctu_ * 4);
+    p.offset = reinterpret_cast<int*>(q);
+    q += align(B * nctu_ * 4);
+    p.total = reinterpret_cast<int*>(q);
+    q += align(B * 4);
+    p.packed = reinterpret_cast<int16_t*>(q);
+    p.count = nullptr;  // device count array lives in the scratch below
+    return p;
+  }
+  DecisionSet slot_dec(const Slot& s) const {
+    const Parts p = carve(s.dev);
+    DecisionSet d;
+    d.cu_log2 = p.cu_log2;
+    d.intra = p.intra;
+    d.ipm = p.ipm;
+    d.cbf = p.cbf;
+    d.mv = p.mv;
+    d.coef_y = coef_y_;
+    d.coef_u = coef_u_;
+    d.coef_v = coef_v_;
+    return d;
+  }
+  CompactSet slot_compact(const Slot& s) const {
+    const Parts p = carve(s.dev);
+    CompactSet c;
+    c.mask_y = p.mask_y;
+    c.mask_c = p.mask_c;
+    c.count = reinterpret_cast<int*>(coef_count_scratch());
+    c.offset = p.offset;
+    c.total = p.total;
+    c.packed = p.packed;
+    c.cap = cap_;
+    return c;
+  }
+  // per-CTB counts are consumed by the scan within the same frame: one scratch suffices
+  void* coef_count_scratch() const { return count_scratch_; }
 
-  // host view of segment b's decisions in a slot
-  FrameData slot_view(const Slot& s, int b, int B) const {
+  // host view of segment b in a slot (compact levels)
+  FrameData host_view(const Slot& s, int b) const {
+    const Parts p = carve(s.host);
     const long U = g_.usz;
-    uint8_t* p = s.host;
     FrameData f;
     f.w8 = g_.w8;
     f.h8 = g_.h8;
-    f.cu_log2 = p + b * U;
-    p += B * U;
-    f.intra = p + b * U;
-    p += B * U;
-    f.ipm = p + b * U;
-    p += B * U;
-    f.cbf = p + b * U;
-    p += B * U;
-    f.mv = reinterpret_cast<const int16_t*>(p) + b * U * 2;
-    p += B * U * 4;
-    f.coef[0] = reinterpret_cast<const int16_t*>(p) + b * g_.ysz;
-    p += B * g_.ysz * 2;
-    f.coef[1] = reinterpret_cast<const int16_t*>(p) + b * g_.csz;
-    p += B * g_.csz * 2;
-    f.coef[2] = reinterpret_cast<const int16_t*>(p) + b * g_.csz;
+    f.cu_log2 = p.cu_log2 + b * U;
+    f.intra = p.intra + b * U;
+    f.ipm = p.ipm + b * U;
+    f.cbf = p.cbf + b * U;
+    f.mv = p.mv + b * U * 2;
+    f.sb_mask_y = reinterpret_cast<const uint64_t*>(p.mask_y + (long)b * nctu_);
+    f.sb_mask_c = p.mask_c + (long)b * nctu_;
+    f.sb_offset = p.offset + (long)b * nctu_;
+    f.sb_packed = p.packed + (long)b * cap_;
+    f.wc = g_.wc;
     return f;
   }
 
-  void copy_out(Slot& s, int B) {
+  // worker: fetch exactly the used bytes of slot s from the device on a private stream
+  void fetch_slot(Slot& s, int B) {
+    thread_local hipStream_t ws = nullptr;
+    if (!ws) HIP_OK(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
+    HIP_OK(hipEventSynchronize(s.ev));
+    const Parts d = carve(s.dev), h = carve(s.host);
     const long U = g_.usz;
-    uint8_t* p = s.host;
-    auto cp = [&](void* d, long n) {
-      HIP_OK(hipMemcpyAsync(p, d, n, hipMemcpyDeviceToHost, stream_));
-      p += n;
-    };
-    cp(dec_.cu_log2, B * U);
-    cp(dec_.intra, B * U);
-    cp(dec_.ipm, B * U);
-    cp(dec_.cbf, B * U);
-    cp(dec_.mv, B * U * 4);
-    cp(dec_.coef_y, B * g_.ysz * 2);
-    cp(dec_.coef_u, B * g_.csz * 2);
-    cp(dec_.coef_v, B * g_.csz * 2);
-    HIP_OK(hipEventRecord(s.ev, stream_));
+    HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
+    HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, align(B * U * 4), hipMemcpyDeviceToHost, ws));  // 4 u8 planes
+    HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
+    HIP_OK(hipMemcpyAsync(h.mask_y, d.mask_y, align(B * nctu_ * 8) + align(B * nctu_ * 4) + B * nctu_ * 4,
+                          hipMemcpyDeviceToHost, ws));  // mask_y | mask_c | offset
+    HIP_OK(hipStreamSynchronize(ws));
+    long bytes = 0;
+    for (int b = 0; b < B; ++b) {
+      const long n = (long)h.total[b] * 16 * 2;
+      if (n > cap_ * 2) throw std::runtime_error("compact level overflow");
+      if (n) HIP_OK(hipMemcpyAsync(h.packed + b * cap_, d.packed + b * cap_, n, hipMemcpyDeviceToHost, ws));
+      bytes += n;
+    }
+    HIP_OK(hipStreamSynchronize(ws));
+    coef_bytes_ += bytes;
   }
 
   template <class Upload> void run(int nseg, Upload&& upload) {
@@ -252,44 +316,58 @@ class Engine {
     const int B = nseg, F = cfg_.gop;
     const auto w0 = std::chrono::steady_clock::now();
     out_.assign(B, {});
+    coef_bytes_ = 0;
     std::vector<std::vector<std::vector<uint8_t>>> slices(B, std::vector<std::vector<uint8_t>>(F));
     std::atomic<int> failed{0};
     std::string err;
     std::mutex err_mu;
+    auto fail = [&](const std::exception& e) {
+      std::lock_guard<std::mutex> lk(err_mu);
+      err = e.what();
+      failed = 1;
+    };
     HIP_OK(hipMemsetAsync(d_sse_, 0, B * 3 * sizeof(unsigned long long), stream_));
     HIP_OK(hipEventRecord(t0_, stream_));
     for (int f = 0; f < F; ++f) {
+      Slot& s = slots_[f % kSlots];
+      while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+      const DecisionSet dec = slot_dec(s);
       upload(f, B);
       FrameSet cur = rec_[f & 1], prev = rec_[(f + 1) & 1];
-      if (f == 0) launch_intra_frame(src_, cur, dec_, g_, cfg_.qp, pen_, B, stream_);
-      else launch_inter_frame(src_, prev, phase_, cur, dec_, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
-      if (cfg_.deblock) launch_deblock(cur, dec_, g_, cfg_.qp, B, stream_);
+      if (f == 0) launch_intra_frame(src_, cur, dec, g_, cfg_.qp, pen_, B, stream_);
+      else launch_inter_frame(src_, prev, phase_, cur, dec, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
+      launch_compact(dec, g_, slot_compact(s), B, stream_);
+      if (cfg_.deblock) launch_deblock(cur, dec, g_, cfg_.qp, B, stream_);
       if (f + 1 < F) launch_phase_planes(cur, phase_, g_, B, stream_);  // reference of f+1
       launch_sse(src_, cur, g_, d_sse_, B, stream_);
       HIP_OK(hipGetLastError());
-      Slot& s = slots_[f % kSlots];
-      while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-      copy_out(s, B);
-      s.pending.store(B, std::memory_order_release);
-      for (int b = 0; b < B; ++b) {
-        pool_->submit([this, &s, b, B, f, &slices, &failed, &err, &err_mu] {
-          try {
-            HIP_OK(hipEventSynchronize(s.ev));
-            write_slice(seq_, slot_view(s, b, B), f, f == 0, slices[b][f]);
-          } catch (const std::exception& e) {
-            std::lock_guard<std::mutex> lk(err_mu);
-            err = e.what();
-            failed = 1;
-          }
-          s.pending.fetch_sub(1, std::memory_order_acq_rel);
-        });
-      }
+      HIP_OK(hipEventRecord(s.ev, stream_));
+      s.pending.store(B + 1, std::memory_order_release);
+      pool_->submit([this, &s, B, f, &slices, &fail] {
+        try {
+          fetch_slot(s, B);
+        } catch (const std::exception& e) {
+          fail(e);
+          s.pending.fetch_sub(B + 1, std::memory_order_acq_rel);
+          return;
+        }
+        s.pending.fetch_sub(1, std::memory_order_acq_rel);
+        for (int b = 0; b < B; ++b)
+          pool_->submit([this, &s, b, f, &slices, &fail] {
+            try {
+              write_slice(seq_, host_view(s, b), f, f == 0, slices[b][f]);
+            } catch (const std::exception& e) {
+              fail(e);
+            }
+            s.pending.fetch_sub(1, std::memory_order_acq_rel);
+          });
+      });
     }
     HIP_OK(hipEventRecord(t1_, stream_));
     for (auto& s : slots_)
       while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
     HIP_OK(hipStreamSynchronize(stream_));
-    if (failed) throw std::runtime_error("entropy coding failed: " + err);
+    if (failed) throw std::runtime_error("encode failed: " + err);
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, t0_, t1_));
     gpu_ms_ = ms;
@@ -309,9 +387,12 @@ class Engine {
   Penalties pen_{};
   hipStream_t stream_{};
   FrameSet src_{}, rec_[2]{};
-  DecisionSet dec_{};
+  int16_t *coef_y_ = nullptr, *coef_u_ = nullptr, *coef_v_ = nullptr;
   unsigned long long* d_sse_ = nullptr;
   uint8_t* phase_ = nullptr;
+  void* count_scratch_ = nullptr;
+  int nctu_ = 0;
+  long cap_ = 0;
   Slot slots_[kSlots];
   long slot_bytes_ = 0;
   hipEvent_t t0_{}, t1_{};
@@ -319,6 +400,7 @@ class Engine {
   std::vector<std::vector<uint8_t>> out_;
   std::vector<double> sse_host_;
   double gpu_ms_ = 0, wall_ms_ = 0;
+  std::atomic<long> coef_bytes_{0};
 };
 
 }  // namespace gpu

@@ -30,5 +30,17 @@ void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameS
 void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipStream_t s);
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s);
 
+// Compact (non-zero 4x4 groups only) level representation for the D2H transfer.
+struct CompactSet {
+  unsigned long long* mask_y;  // [B][nctu] luma groups (bit = sy*8 + sx within the CTB)
+  unsigned* mask_c;            // [B][nctu] chroma groups (Cb bits 0..15, Cr bits 16..31)
+  int* count;                  // [B][nctu]
+  int* offset;                 // [B][nctu] exclusive scan of count (in groups)
+  int* total;                  // [B]
+  int16_t* packed;             // [B][cap] 16 levels per group
+  long cap;                    // int16 capacity per segment
+};
+void launch_compact(DecisionSet dec, const Geo& g, CompactSet cs, int B, hipStream_t s);
+
 }  // namespace gpu
 }  // namespace tv

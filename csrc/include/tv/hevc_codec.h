@@ -45,6 +45,14 @@ struct FrameData {
   const int16_t* mv = nullptr;
   const uint8_t* cbf = nullptr;
   const int16_t* coef[3] = {nullptr, nullptr, nullptr};
+  // compact levels (GPU path; used when sb_packed != nullptr): per-CTB masks of non-zero
+  // 4x4 groups (luma bit = sy*8+sx; chroma Cb bits 0..15 / Cr 16..31), exclusive group
+  // offsets, and 16 levels per group packed in CTB order (Y, Cb, Cr raster).
+  const uint64_t* sb_mask_y = nullptr;
+  const uint32_t* sb_mask_c = nullptr;
+  const int32_t* sb_offset = nullptr;
+  const int16_t* sb_packed = nullptr;
+  int wc = 0;  // CTBs per row
 };
 
 // Owning storage for one frame's decisions (CPU side).
