@@ -62,9 +62,14 @@ def main() -> None:
     eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range,
                     seed=args.seed, threads=args.threads or None, device=local)
 
+    prof = {"encode": 0.0, "post": 0.0}
+
     def step(s: int):
         base = (s * world + rank) * batch
+        t_a = time.perf_counter()
         segs = eng.encode_synthetic([(base + b) * args.gop for b in range(batch)])
+        t_b = time.perf_counter()
+        prof["encode"] += t_b - t_a
         sse = np.array([eng.sse(b) for b in range(batch)]).sum(0)
         nbytes = sum(len(x) for x in segs)
         stats = torch.tensor([batch * args.gop, nbytes, *sse], dtype=torch.float64, device=dev)
@@ -72,10 +77,12 @@ def main() -> None:
         if world > 1:
             dist.all_reduce(stats)  # rate-control / quality statistics
             gathered = gather_bytes_to_root(b"".join(segs), dev)  # bitstreams -> stitch rank
+        prof["post"] += time.perf_counter() - t_b
         return stats, gathered
 
     for s in range(args.warmup):
         step(-1 - s)
+    prof["encode"] = prof["post"] = 0.0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -100,7 +107,7 @@ def main() -> None:
     fps = frames / el
     kbps = tot[1] * 8 / (frames / 30.0) / 1000.0 / world  # per 30 fps stream
     if rank == 0:
-        gpu_ms, wall_ms = eng.timing()
+        tm = eng.timing()
         print(json.dumps({
             "metric": METRIC,
             "value": round(fps, 2),
@@ -125,8 +132,13 @@ def main() -> None:
                 "psnr_y_db": round(py, 3),
                 "psnr_yuv_db": round((6 * py + pu + pv) / 8, 3),
                 "kbps_per_30fps_stream": round(kbps, 1),
-                "last_step_gpu_ms": round(gpu_ms, 2),
-                "last_step_wall_ms": round(wall_ms, 2),
+                "last_step_gpu_ms": round(tm["gpu_ms"], 2),
+                "last_step_engine_wall_ms": round(tm["wall_ms"], 2),
+                "last_step_entropy_cpu_ms": round(tm["entropy_cpu_ms"], 2),
+                "last_step_coef_mb_d2h": round(tm["coef_mb"], 2),
+                "encode_s": round(prof["encode"], 3),
+                "post_s": round(prof["post"], 3),
+                "cpu_threads": eng.threads,
             },
         }), flush=True)
     eng.close()

@@ -194,6 +194,7 @@ class Engine {
   double gpu_ms() const { return gpu_ms_; }
   double wall_ms() const { return wall_ms_; }
   long coef_bytes() const { return coef_bytes_; }
+  double entropy_ms() const { return entropy_ns_ / 1e6; }
   const Geo& geo() const { return g_; }
   FrameSet last_recon() const { return rec_[(cfg_.gop - 1) & 1]; }
   hipStream_t stream() const { return stream_; }
@@ -317,6 +318,7 @@ class Engine {
     const auto w0 = std::chrono::steady_clock::now();
     out_.assign(B, {});
     coef_bytes_ = 0;
+    entropy_ns_ = 0;
     std::vector<std::vector<std::vector<uint8_t>>> slices(B, std::vector<std::vector<uint8_t>>(F));
     std::atomic<int> failed{0};
     std::string err;
@@ -355,7 +357,10 @@ class Engine {
         for (int b = 0; b < B; ++b)
           pool_->submit([this, &s, b, f, &slices, &fail] {
             try {
+              const auto c0 = std::chrono::steady_clock::now();
               write_slice(seq_, host_view(s, b), f, f == 0, slices[b][f]);
+              entropy_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 std::chrono::steady_clock::now() - c0).count();
             } catch (const std::exception& e) {
               fail(e);
             }
@@ -401,6 +406,7 @@ class Engine {
   std::vector<double> sse_host_;
   double gpu_ms_ = 0, wall_ms_ = 0;
   std::atomic<long> coef_bytes_{0};
+  std::atomic<long> entropy_ns_{0};
 };
 
 }  // namespace gpu
@@ -453,9 +459,12 @@ void tv_engine_segment_copy(void* e, int b, uint8_t* dst) {
 void tv_engine_sse(void* e, int b, double* out3) {
   for (int c = 0; c < 3; ++c) out3[c] = static_cast<tv::gpu::Engine*>(e)->sse(b, c);
 }
-void tv_engine_timing(void* e, double* gpu_ms, double* wall_ms) {
-  *gpu_ms = static_cast<tv::gpu::Engine*>(e)->gpu_ms();
-  *wall_ms = static_cast<tv::gpu::Engine*>(e)->wall_ms();
+void tv_engine_timing(void* e, double* gpu_ms, double* wall_ms, double* entropy_ms, double* coef_mb) {
+  auto* E = static_cast<tv::gpu::Engine*>(e);
+  *gpu_ms = E->gpu_ms();
+  *wall_ms = E->wall_ms();
+  *entropy_ms = E->entropy_ms();
+  *coef_mb = E->coef_bytes() / 1e6;
 }
 // copy the last frame's coded-size reconstruction of segment b (tests)
 int tv_engine_last_recon(void* e, int b, uint8_t* y, uint8_t* u, uint8_t* v) {

@@ -32,7 +32,7 @@ def _lib():
         lib.tv_engine_segment_size.argtypes = [vp, C.c_int]
         lib.tv_engine_segment_copy.argtypes = [vp, C.c_int, C.POINTER(C.c_uint8)]
         lib.tv_engine_sse.argtypes = [vp, C.c_int, C.POINTER(C.c_double)]
-        lib.tv_engine_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        lib.tv_engine_timing.argtypes = [vp] + [C.POINTER(C.c_double)] * 4
         lib.tv_engine_last_recon.restype = C.c_int
         lib.tv_engine_last_recon.argtypes = [vp, C.c_int] + [C.POINTER(C.c_uint8)] * 3
         _sigs_done = True
@@ -62,8 +62,9 @@ class GpuEngine:
         self.width, self.height, self.qp = width, height, qp
         self.batch, self.gop = batch, gop
         self.cw, self.ch = coded_size(width, height)
+        self.threads = threads or default_threads()
         self.h = self.lib.tv_engine_new(width, height, qp, batch, gop, search_range, int(deblock),
-                                        seed & 0xFFFFFFFF, threads or default_threads(), device, max_merge)
+                                        seed & 0xFFFFFFFF, self.threads, device, max_merge)
         if not self.h:
             raise RuntimeError("GPU engine init failed: " + self.lib.tv_gpu_last_error().decode())
 
@@ -114,10 +115,12 @@ class GpuEngine:
         py, pu, pv = f(y, npx), f(u, npx / 4), f(v, npx / 4)
         return {"y": py, "u": pu, "v": pv, "yuv": (6 * py + pu + pv) / 8}
 
-    def timing(self) -> tuple[float, float]:
-        g, w = C.c_double(), C.c_double()
-        self.lib.tv_engine_timing(self.h, C.byref(g), C.byref(w))
-        return g.value, w.value
+    def timing(self) -> dict:
+        """Last encode call: GPU stream time, engine wall time, summed CPU entropy-coding
+        time (all threads), and compact level bytes transferred device->host."""
+        g, w, e, m = C.c_double(), C.c_double(), C.c_double(), C.c_double()
+        self.lib.tv_engine_timing(self.h, C.byref(g), C.byref(w), C.byref(e), C.byref(m))
+        return {"gpu_ms": g.value, "wall_ms": w.value, "entropy_cpu_ms": e.value, "coef_mb": m.value}
 
     def last_recon(self, b: int):
         y = np.empty((self.ch, self.cw), np.uint8)
