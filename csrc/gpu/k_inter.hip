@@ -163,38 +163,39 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   for (int step = 2; step >= 1; step >>= 1) {
     if (tid < 168) subsad[tid >> 3][tid & 7] = 0;
     __syncthreads();
-    for (int ci = tid; ci < 8 * 384; ci += kMeThreads) {
-      const int k = ci / 384, r = ci - k * 384;
-      int bi, cr, l2;
-      if (r < 128) {
-        bi = r >> 3;
-        cr = r & 7;
+    // work unit = 64 contiguous pixels of one (block, candidate): lane = pixel, so every
+    // phase-plane load instruction touches 1-8 cache lines (not 64), then one wave reduction.
+    // Per candidate: 16 units (8x8 blocks), 16 (4 per 16x16), 16 (32x32) = 48 units.
+    const int wave = tid >> 6, lane = tid & 63;
+    for (int unit = wave; unit < 8 * 48; unit += kMeThreads / 64) {
+      const int k = unit / 48, r = unit - k * 48;
+      int bi, part, l2;
+      if (r < 16) {
+        bi = r;
+        part = 0;
         l2 = 3;
-      } else if (r < 256) {
-        bi = 16 + ((r - 128) >> 5);
-        cr = (r - 128) & 31;
+      } else if (r < 32) {
+        bi = 16 + ((r - 16) >> 2);
+        part = (r - 16) & 3;
         l2 = 4;
       } else {
         bi = 20;
-        cr = r - 256;
+        part = r - 32;
         l2 = 5;
       }
       int bx, by, l2b;
       me_blk_geom(bi, bx, by, l2b);
-      const int cpr = (1 << l2) >> 3;
-      const int row = cr / cpr, col0 = (cr - row * cpr) * 8;
+      const int p = part * 64 + lane;  // pixel index inside the block
+      const int px = p & ((1 << l2) - 1), py = p >> l2;
       int ox, oy;
       cand_offset(k, ox, oy);
       const int mx = bmv[bi][0] + ox * step, my = bmv[bi][1] + oy * step;
       const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
-      const int gy = clip3(-8, g.H + 7, cy + by + row + (my >> 2));
-      const uint8_t* Prow = P + (long)(gy + 8) * g.pw16 + 8;
-      const int gx = cx + bx + col0 + (mx >> 2);
-      const uint8_t* srow = sb + (by + row) * 32 + bx + col0;
-      int s = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s += tv_abs((int)srow[i] - (int)Prow[clip3(-8, g.W + 7, gx + i)]);
-      atomicAdd(&subsad[bi][k], s);
+      const int gy = clip3(-8, g.H + 7, cy + by + py + (my >> 2));
+      const int gx = clip3(-8, g.W + 7, cx + bx + px + (mx >> 2));
+      const int d = tv_abs((int)sb[(by + py) * 32 + bx + px] - (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
+      const int s = wave_sum(d);
+      if (lane == 0) atomicAdd(&subsad[bi][k], s);  // a (block, cand) may span several waves
     }
     __syncthreads();
     if (tid < 21) {
