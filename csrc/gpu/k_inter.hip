@@ -166,36 +166,53 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
     // work unit = 64 contiguous pixels of one (block, candidate): lane = pixel, so every
     // phase-plane load instruction touches 1-8 cache lines (not 64), then one wave reduction.
     // Per candidate: 16 units (8x8 blocks), 16 (4 per 16x16), 16 (32x32) = 48 units.
+    // Each wave takes 8 units per batch and issues all 8 loads before consuming any, so
+    // 8 phase-plane loads per lane are in flight (latency, not bandwidth, bounds this loop).
     const int wave = tid >> 6, lane = tid & 63;
-    for (int unit = wave; unit < 8 * 48; unit += kMeThreads / 64) {
-      const int k = unit / 48, r = unit - k * 48;
-      int bi, part, l2;
-      if (r < 16) {
-        bi = r;
-        part = 0;
-        l2 = 3;
-      } else if (r < 32) {
-        bi = 16 + ((r - 16) >> 2);
-        part = (r - 16) & 3;
-        l2 = 4;
-      } else {
-        bi = 20;
-        part = r - 32;
-        l2 = 5;
+    constexpr int kNW = kMeThreads / 64, kUB = 8;
+    for (int base = wave; base < 8 * 48; base += kNW * kUB) {
+      int sv[kUB], pv[kUB], tgt[kUB];
+#pragma unroll
+      for (int j = 0; j < kUB; ++j) {
+        const int unit = base + kNW * j;
+        tgt[j] = -1;
+        sv[j] = pv[j] = 0;
+        if (unit < 8 * 48) {
+          const int k = unit / 48, r = unit - k * 48;
+          int bi, part, l2;
+          if (r < 16) {
+            bi = r;
+            part = 0;
+            l2 = 3;
+          } else if (r < 32) {
+            bi = 16 + ((r - 16) >> 2);
+            part = (r - 16) & 3;
+            l2 = 4;
+          } else {
+            bi = 20;
+            part = r - 32;
+            l2 = 5;
+          }
+          int bx, by, l2b;
+          me_blk_geom(bi, bx, by, l2b);
+          const int p = part * 64 + lane;  // pixel index inside the block
+          const int px = p & ((1 << l2) - 1), py = p >> l2;
+          int ox, oy;
+          cand_offset(k, ox, oy);
+          const int mx = bmv[bi][0] + ox * step, my = bmv[bi][1] + oy * step;
+          const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
+          const int gy = clip3(-8, g.H + 7, cy + by + py + (my >> 2));
+          const int gx = clip3(-8, g.W + 7, cx + bx + px + (mx >> 2));
+          pv[j] = P[(long)(gy + 8) * g.pw16 + gx + 8];
+          sv[j] = sb[(by + py) * 32 + bx + px];
+          tgt[j] = bi * 8 + k;
+        }
       }
-      int bx, by, l2b;
-      me_blk_geom(bi, bx, by, l2b);
-      const int p = part * 64 + lane;  // pixel index inside the block
-      const int px = p & ((1 << l2) - 1), py = p >> l2;
-      int ox, oy;
-      cand_offset(k, ox, oy);
-      const int mx = bmv[bi][0] + ox * step, my = bmv[bi][1] + oy * step;
-      const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
-      const int gy = clip3(-8, g.H + 7, cy + by + py + (my >> 2));
-      const int gx = clip3(-8, g.W + 7, cx + bx + px + (mx >> 2));
-      const int d = tv_abs((int)sb[(by + py) * 32 + bx + px] - (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
-      const int s = wave_sum(d);
-      if (lane == 0) atomicAdd(&subsad[bi][k], s);  // a (block, cand) may span several waves
+#pragma unroll
+      for (int j = 0; j < kUB; ++j) {
+        const int s = wave_sum(tv_abs(sv[j] - pv[j]));
+        if (lane == 0 && tgt[j] >= 0) atomicAdd(&subsad[tgt[j] >> 3][tgt[j] & 7], s);
+      }
     }
     __syncthreads();
     if (tid < 21) {
