@@ -166,53 +166,59 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
     // work unit = 64 contiguous pixels of one (block, candidate): lane = pixel, so every
     // phase-plane load instruction touches 1-8 cache lines (not 64), then one wave reduction.
     // Per candidate: 16 units (8x8 blocks), 16 (4 per 16x16), 16 (32x32) = 48 units.
-    // Each wave takes 8 units per batch and issues all 8 loads before consuming any, so
-    // 8 phase-plane loads per lane are in flight (latency, not bandwidth, bounds this loop).
-    const int wave = tid >> 6, lane = tid & 63;
-    constexpr int kNW = kMeThreads / 64, kUB = 8;
-    for (int base = wave; base < 8 * 48; base += kNW * kUB) {
-      int sv[kUB], pv[kUB], tgt[kUB];
+    // A thread owns a group of 8 rows x 8 pixels of one (block, candidate): per row it loads
+    // 3 aligned dwords of the phase plane, forms the 2 shifted dwords with v_alignbyte and
+    // accumulates with v_sad_u8 — the same 4-pixels-per-instruction form as the integer
+    // search (per-pixel address math made this stage VALU-issue-bound before).
+    // Groups per candidate: 16 (8x8 blocks) + 16 (4 per 16x16) + 16 (16 for the 32x32).
+    for (int grp = tid; grp < 8 * 48; grp += kMeThreads) {
+      const int k = grp / 48, r = grp - k * 48;
+      int bi, row0, col0;
+      if (r < 16) {
+        bi = r;
+        row0 = col0 = 0;
+      } else if (r < 32) {
+        const int q = (r - 16) & 3;
+        bi = 16 + ((r - 16) >> 2);
+        row0 = 8 * (q >> 1);
+        col0 = 8 * (q & 1);
+      } else {
+        const int q = r - 32;
+        bi = 20;
+        row0 = 8 * (q >> 2);
+        col0 = 8 * (q & 3);
+      }
+      int bx, by, l2b;
+      me_blk_geom(bi, bx, by, l2b);
+      int ox, oy;
+      cand_offset(k, ox, oy);
+      const int mx = bmv[bi][0] + ox * step, my = bmv[bi][1] + oy * step;
+      const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
+      const int gx0 = cx + bx + col0 + (mx >> 2);
+      const int gy0 = cy + by + row0 + (my >> 2);
+      const int sw = ((by + row0) * 32 + bx + col0) >> 2;  // source word index of row 0
+      unsigned s = 0;
+      if (gx0 >= -8 && gx0 + 11 <= g.W + 7 && gy0 >= -8 && gy0 + 7 <= g.H + 7) {
+        const int a = gx0 & ~3, sh = gx0 & 3;
+        const uint8_t* rowp = P + (long)(gy0 + 8) * g.pw16 + a + 8;
 #pragma unroll
-      for (int j = 0; j < kUB; ++j) {
-        const int unit = base + kNW * j;
-        tgt[j] = -1;
-        sv[j] = pv[j] = 0;
-        if (unit < 8 * 48) {
-          const int k = unit / 48, r = unit - k * 48;
-          int bi, part, l2;
-          if (r < 16) {
-            bi = r;
-            part = 0;
-            l2 = 3;
-          } else if (r < 32) {
-            bi = 16 + ((r - 16) >> 2);
-            part = (r - 16) & 3;
-            l2 = 4;
-          } else {
-            bi = 20;
-            part = r - 32;
-            l2 = 5;
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(rowp + (long)j * g.pw16);
+          const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
+          const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+          const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+          s = __builtin_amdgcn_sad_u8(hi, s32[sw + 8 * j + 1], __builtin_amdgcn_sad_u8(lo, s32[sw + 8 * j], s));
+        }
+      } else {  // touches the clamped border: per-pixel path
+        for (int j = 0; j < 8; ++j) {
+          const int gy = clip3(-8, g.H + 7, gy0 + j);
+          for (int i = 0; i < 8; ++i) {
+            const int gx = clip3(-8, g.W + 7, gx0 + i);
+            s += tv_abs((int)sb[(by + row0 + j) * 32 + bx + col0 + i] - (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
           }
-          int bx, by, l2b;
-          me_blk_geom(bi, bx, by, l2b);
-          const int p = part * 64 + lane;  // pixel index inside the block
-          const int px = p & ((1 << l2) - 1), py = p >> l2;
-          int ox, oy;
-          cand_offset(k, ox, oy);
-          const int mx = bmv[bi][0] + ox * step, my = bmv[bi][1] + oy * step;
-          const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
-          const int gy = clip3(-8, g.H + 7, cy + by + py + (my >> 2));
-          const int gx = clip3(-8, g.W + 7, cx + bx + px + (mx >> 2));
-          pv[j] = P[(long)(gy + 8) * g.pw16 + gx + 8];
-          sv[j] = sb[(by + py) * 32 + bx + px];
-          tgt[j] = bi * 8 + k;
         }
       }
-#pragma unroll
-      for (int j = 0; j < kUB; ++j) {
-        const int s = wave_sum(tv_abs(sv[j] - pv[j]));
-        if (lane == 0 && tgt[j] >= 0) atomicAdd(&subsad[tgt[j] >> 3][tgt[j] & 7], s);
-      }
+      atomicAdd(&subsad[bi][k], (int)s);
     }
     __syncthreads();
     if (tid < 21) {

@@ -1,0 +1,192 @@
+"""Media sources, sinks and probing (replaces the reference's ffprobe / ffmpeg demux role,
+SURVEY.md §2.3 K1/K11).
+
+Readable inputs (no ffmpeg in this image, so only formats we can decode ourselves):
+
+* ``.y4m``   — YUV4MPEG2, 8-bit 4:2:0 (raw frames; the realistic ingest format here);
+* ``.synth`` — JSON ``{"width", "height", "frames", "fps", "seed"}``: the procedural source
+  of :mod:`thinvids_amd.models.hevc` (P5 "direct source" with zero I/O);
+* ``.hevc`` / ``.265`` / ``.mp4`` produced by this engine (decoded with the oracle decoder).
+
+Every source exposes ``width, height, fps_num, fps_den, nframes`` and
+``read(start, n) -> list[(Y, U, V)]``.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass
+from fractions import Fraction
+
+import numpy as np
+
+from . import hevc
+
+VIDEO_EXTS = (".y4m", ".synth", ".hevc", ".265", ".mp4")
+
+
+# ------------------------------------------------------------------------------ Y4M
+@dataclass
+class Y4MInfo:
+    width: int
+    height: int
+    fps_num: int
+    fps_den: int
+    header_len: int
+    frame_bytes: int
+    nframes: int
+
+
+def _y4m_info(path: str) -> Y4MInfo:
+    with open(path, "rb") as f:
+        header = f.readline()
+        if not header.startswith(b"YUV4MPEG2"):
+            raise ValueError(f"{path}: not a YUV4MPEG2 file")
+        w = h = 0
+        fn, fd = 30, 1
+        for tok in header.decode().split()[1:]:
+            if tok[0] == "W":
+                w = int(tok[1:])
+            elif tok[0] == "H":
+                h = int(tok[1:])
+            elif tok[0] == "F":
+                a, b = tok[1:].split(":")
+                fn, fd = int(a), int(b)
+            elif tok[0] == "C" and not tok[1:].startswith("420"):
+                raise ValueError(f"{path}: only 4:2:0 8-bit Y4M is supported (got {tok})")
+        frame_hdr = f.readline()
+        if frame_hdr and not frame_hdr.startswith(b"FRAME"):
+            raise ValueError(f"{path}: malformed frame header")
+        fhl = len(frame_hdr) if frame_hdr else 6
+    plane = w * h * 3 // 2
+    size = os.path.getsize(path)
+    n = max(0, (size - len(header)) // (fhl + plane))
+    return Y4MInfo(w, h, fn, fd, len(header), fhl + plane, n)
+
+
+def write_y4m(path: str, frames, fps_num: int = 30, fps_den: int = 1) -> None:
+    frames = list(frames)
+    h, w = frames[0][0].shape
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(f"YUV4MPEG2 W{w} H{h} F{fps_num}:{fps_den} Ip A1:1 C420jpeg\n".encode())
+        for y, u, v in frames:
+            f.write(b"FRAME\n")
+            f.write(np.ascontiguousarray(y, np.uint8).tobytes())
+            f.write(np.ascontiguousarray(u, np.uint8).tobytes())
+            f.write(np.ascontiguousarray(v, np.uint8).tobytes())
+    os.replace(tmp, path)
+
+
+class Y4MSource:
+    kind = "rawvideo"
+
+    def __init__(self, path: str):
+        self.path = path
+        self.info = _y4m_info(path)
+        self.width, self.height = self.info.width, self.info.height
+        self.fps_num, self.fps_den = self.info.fps_num, self.info.fps_den
+        self.nframes = self.info.nframes
+
+    def read(self, start: int, n: int):
+        out = []
+        i = self.info
+        n = max(0, min(n, self.nframes - start))
+        ysz, csz = i.width * i.height, i.width * i.height // 4
+        with open(self.path, "rb") as f:
+            f.seek(i.header_len + start * i.frame_bytes)
+            for _ in range(n):
+                raw = f.read(i.frame_bytes)
+                hdr = raw.index(b"\n") + 1
+                buf = np.frombuffer(raw, np.uint8, offset=hdr)
+                y = buf[:ysz].reshape(i.height, i.width)
+                u = buf[ysz:ysz + csz].reshape(i.height // 2, i.width // 2)
+                v = buf[ysz + csz:ysz + 2 * csz].reshape(i.height // 2, i.width // 2)
+                out.append((y, u, v))
+        return out
+
+
+# ---------------------------------------------------------------------------- synth
+class SynthSource:
+    kind = "synthetic"
+
+    def __init__(self, path: str | None = None, spec: dict | None = None):
+        if spec is None:
+            with open(path) as f:
+                spec = json.load(f)
+        self.path = path
+        self.spec = spec
+        self.width, self.height = int(spec["width"]), int(spec["height"])
+        fps = Fraction(str(spec.get("fps", 30))).limit_denominator(1001)
+        self.fps_num, self.fps_den = fps.numerator, fps.denominator
+        self.nframes = int(spec["frames"])
+        self.seed = int(spec.get("seed", 1))
+        self.start = int(spec.get("start_frame", 0))
+
+    def read(self, start: int, n: int):
+        n = max(0, min(n, self.nframes - start))
+        return [hevc.synth_frame(self.seed, self.start + start + k, self.width, self.height) for k in range(n)]
+
+
+def write_synth_spec(path: str, width: int, height: int, frames: int, fps=30, seed: int = 1) -> None:
+    with open(path, "w") as f:
+        json.dump({"width": width, "height": height, "frames": frames, "fps": fps, "seed": seed}, f)
+
+
+# ----------------------------------------------------------------------------- HEVC
+class HevcSource:
+    kind = "hevc"
+
+    def __init__(self, path: str):
+        self.path = path
+        with open(path, "rb") as f:
+            data = f.read()
+        self.fps_num, self.fps_den = 30, 1
+        if path.endswith(".mp4"):
+            dm = hevc.demux_mp4(data)
+            data = dm["annexb"]
+            ts, d = dm["timescale"], dm["sample_delta"]
+            if ts and d:
+                fr = Fraction(ts, d).limit_denominator(1001)
+                self.fps_num, self.fps_den = fr.numerator, fr.denominator
+        self._dec = hevc.decode(data, coded=False)
+        self.width, self.height = self._dec.width, self._dec.height
+        self.nframes = len(self._dec.frames)
+
+    def read(self, start: int, n: int):
+        return list(self._dec.frames[start:start + n])
+
+
+def open_source(path: str):
+    ext = os.path.splitext(path)[1].lower()
+    if ext == ".y4m":
+        return Y4MSource(path)
+    if ext == ".synth":
+        return SynthSource(path)
+    if ext in (".hevc", ".265", ".mp4"):
+        return HevcSource(path)
+    raise ValueError(f"unsupported input format: {path}")
+
+
+def probe(path: str) -> dict:
+    """ffprobe-like summary used for the job hash `source_*` / `dest_*` fields."""
+    src = open_source(path)
+    size = os.path.getsize(path) if os.path.exists(path) else 0
+    fps = src.fps_num / src.fps_den
+    dur = src.nframes / fps if fps else 0.0
+    codec = {"rawvideo": "rawvideo", "synthetic": "synthetic", "hevc": "hevc"}[src.kind]
+    return {
+        "codec": codec,
+        "width": src.width,
+        "height": src.height,
+        "resolution": f"{src.width}x{src.height}",
+        "fps": round(fps, 3),
+        "fps_num": src.fps_num,
+        "fps_den": src.fps_den,
+        "frames": src.nframes,
+        "duration": round(dur, 3),
+        "size": size,
+        "bitrate_kbps": round(size * 8 / dur / 1000.0, 1) if dur else 0.0,
+        "streams": [{"index": 0, "codec_type": "video", "codec_name": codec, "width": src.width,
+                     "height": src.height}],
+    }
