@@ -88,8 +88,11 @@ def main() -> None:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tot = None
+    step_ms = []
     for s in range(args.steps):
+        ts = time.perf_counter()
         stats, _ = step(s)
+        step_ms.append(round(1000 * (time.perf_counter() - ts), 2))
         tot = stats if tot is None else tot + stats
     if world > 1:
         dist.barrier()
@@ -139,6 +142,7 @@ def main() -> None:
                 "encode_s": round(prof["encode"], 3),
                 "post_s": round(prof["post"], 3),
                 "cpu_threads": eng.threads,
+                "step_ms": step_ms,
             },
         }), flush=True)
     eng.close()

@@ -18,6 +18,8 @@
 #include "tb_coder.h"
 #include "wave_tb.h"
 
+#include <cstdlib>
+
 namespace tv {
 namespace gpu {
 
@@ -54,7 +56,8 @@ __device__ __forceinline__ int phase_at(const uint8_t* P, const Geo& g, int x, i
 }
 
 __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
-                                                         DecisionSet dec, Geo g, Penalties pen, int range) {
+                                                         DecisionSet dec, Geo g, Penalties pen, int range,
+                                                         int ablate) {
   const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
   const uint8_t* S = src.plane(0, b, g);
@@ -86,7 +89,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   unsigned lb[21];
 #pragma unroll
   for (int k = 0; k < 21; ++k) lb[k] = 0xffffffffu;
-  for (int item = tid; item < items; item += kMeThreads) {
+  for (int item = tid; item < ((ablate & 1) ? 0 : items); item += kMeThreads) {
     const int dyi = item / groups, gi = item - dyi * groups;
     const int dy = dyi - range, dx0 = 4 * gi - range;
     // per-shift rate term and packed candidate index; shifts beyond +R are excluded with a
@@ -160,12 +163,9 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   // ------------------------ half- then quarter-pel refinement ---------------------------
   const uint8_t* sb = reinterpret_cast<const uint8_t*>(s32);
   const uint8_t* ph = phase + (long)b * 16 * g.psz;
-  for (int step = 2; step >= 1; step >>= 1) {
+  for (int step = 2; step >= 1 && !(ablate & 2); step >>= 1) {
     if (tid < 168) subsad[tid >> 3][tid & 7] = 0;
     __syncthreads();
-    // work unit = 64 contiguous pixels of one (block, candidate): lane = pixel, so every
-    // phase-plane load instruction touches 1-8 cache lines (not 64), then one wave reduction.
-    // Per candidate: 16 units (8x8 blocks), 16 (4 per 16x16), 16 (32x32) = 48 units.
     // A thread owns a group of 8 rows x 8 pixels of one (block, candidate): per row it loads
     // 3 aligned dwords of the phase plane, forms the 2 shifted dwords with v_alignbyte and
     // accumulates with v_sad_u8 — the same 4-pixels-per-instruction form as the integer
@@ -353,7 +353,13 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
 
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
                         const Geo& g, int qp, const Penalties& pen, int range, int B, hipStream_t s) {
-  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, g, pen, range);
+  // TV_ME_ABLATE (timing experiments only; output is invalid): bit0 skip integer search,
+  // bit1 skip sub-pel refinement
+  static const int ablate = [] {
+    const char* e = getenv("TV_ME_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, g, pen, range, ablate);
   k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, qp);
 }
 
