@@ -72,10 +72,12 @@ def main() -> None:
         prof["encode"] += t_b - t_a
         sse = np.array([eng.sse(b) for b in range(batch)]).sum(0)
         nbytes = sum(len(x) for x in segs)
-        stats = torch.tensor([batch * args.gop, nbytes, *sse], dtype=torch.float64, device=dev)
+        stats = np.array([batch * args.gop, nbytes, *sse], dtype=np.float64)
         gathered = None
         if world > 1:
-            dist.all_reduce(stats)  # rate-control / quality statistics
+            t = torch.from_numpy(stats).to(dev)
+            dist.all_reduce(t)  # rate-control / quality statistics
+            stats = t.cpu().numpy()
             gathered = gather_bytes_to_root(b"".join(segs), dev)  # bitstreams -> stitch rank
         prof["post"] += time.perf_counter() - t_b
         return stats, gathered
@@ -102,7 +104,6 @@ def main() -> None:
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
-    tot = tot.cpu().numpy()
     frames = tot[0]
     npx = frames * w * h
     psnr = lambda s, n: float(10 * np.log10(255.0 ** 2 * n / s)) if s > 0 else float("inf")
