@@ -167,20 +167,20 @@ class Engine {
 
   // Encode nseg segments of the synthetic source: segment b = frames [starts[b], +gop).
   void encode_synth(const int* starts, int nseg) {
-    run(nseg, [&](int f, int B) {
+    run(nseg, cfg_.gop, [&](int f, int B) {
       FrameIdx fi{};
       for (int b = 0; b < B; ++b) fi.t[b] = starts[b] + f;
       launch_synth(src_, g_, cfg_.seed, fi, B, stream_);
     });
   }
 
-  // Encode nseg segments from host frames, coded-size planar I420 laid out
-  // [segment][frame][Y | U | V] (planes padded to the coded size by the caller).
-  void encode_host(const uint8_t* frames, int nseg) {
+  // Encode nseg segments of nframes (1..gop) host frames each, coded-size planar I420 laid
+  // out [segment][frame][Y | U | V] (planes padded to the coded size by the caller).
+  void encode_host(const uint8_t* frames, int nseg, int nframes) {
     const long fsz = g_.ysz + 2 * g_.csz;
-    run(nseg, [&](int f, int B) {
+    run(nseg, nframes, [&](int f, int B) {
       for (int b = 0; b < B; ++b) {
-        const uint8_t* p = frames + ((long)b * cfg_.gop + f) * fsz;
+        const uint8_t* p = frames + ((long)b * nframes + f) * fsz;
         HIP_OK(hipMemcpyAsync(src_.y + b * g_.ysz, p, g_.ysz, hipMemcpyHostToDevice, stream_));
         HIP_OK(hipMemcpyAsync(src_.u + b * g_.csz, p + g_.ysz, g_.csz, hipMemcpyHostToDevice, stream_));
         HIP_OK(hipMemcpyAsync(src_.v + b * g_.csz, p + g_.ysz + g_.csz, g_.csz, hipMemcpyHostToDevice,
@@ -196,7 +196,7 @@ class Engine {
   long coef_bytes() const { return coef_bytes_; }
   double entropy_ms() const { return entropy_ns_ / 1e6; }
   const Geo& geo() const { return g_; }
-  FrameSet last_recon() const { return rec_[(cfg_.gop - 1) & 1]; }
+  FrameSet last_recon() const { return rec_[(last_frames_ - 1) & 1]; }
   hipStream_t stream() const { return stream_; }
 
  private:
@@ -312,9 +312,11 @@ class Engine {
     coef_bytes_ += bytes;
   }
 
-  template <class Upload> void run(int nseg, Upload&& upload) {
+  template <class Upload> void run(int nseg, int nframes, Upload&& upload) {
     if (nseg < 1 || nseg > cfg_.batch) throw std::runtime_error("nseg out of range");
-    const int B = nseg, F = cfg_.gop;
+    if (nframes < 1 || nframes > cfg_.gop) throw std::runtime_error("nframes out of range");
+    const int B = nseg, F = nframes;
+    last_frames_ = F;
     const auto w0 = std::chrono::steady_clock::now();
     out_.assign(B, {});
     coef_bytes_ = 0;
@@ -397,6 +399,7 @@ class Engine {
   uint8_t* phase_ = nullptr;
   void* count_scratch_ = nullptr;
   int nctu_ = 0;
+  int last_frames_ = 1;
   long cap_ = 0;
   Slot slots_[kSlots];
   long slot_bytes_ = 0;
@@ -448,8 +451,8 @@ void tv_engine_free(void* e) { delete static_cast<tv::gpu::Engine*>(e); }
 int tv_engine_encode_synth(void* e, const int* starts, int nseg) {
   return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_synth(starts, nseg); });
 }
-int tv_engine_encode_host(void* e, const uint8_t* frames, int nseg) {
-  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_host(frames, nseg); });
+int tv_engine_encode_host(void* e, const uint8_t* frames, int nseg, int nframes) {
+  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_host(frames, nseg, nframes); });
 }
 size_t tv_engine_segment_size(void* e, int b) { return static_cast<tv::gpu::Engine*>(e)->segment(b).size(); }
 void tv_engine_segment_copy(void* e, int b, uint8_t* dst) {

@@ -27,7 +27,7 @@ def _lib():
         lib.tv_engine_encode_synth.restype = C.c_int
         lib.tv_engine_encode_synth.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
         lib.tv_engine_encode_host.restype = C.c_int
-        lib.tv_engine_encode_host.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int]
+        lib.tv_engine_encode_host.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int]
         lib.tv_engine_segment_size.restype = C.c_size_t
         lib.tv_engine_segment_size.argtypes = [vp, C.c_int]
         lib.tv_engine_segment_copy.argtypes = [vp, C.c_int, C.POINTER(C.c_uint8)]
@@ -83,18 +83,24 @@ class GpuEngine:
         """Encode len(starts) segments; segment b = synthetic frames [starts[b], starts[b]+gop)."""
         arr = (C.c_int * len(starts))(*[int(s) for s in starts])
         self._check(self.lib.tv_engine_encode_synth(self.h, arr, len(starts)))
+        self.last_frames = self.gop
         return [self.segment(b) for b in range(len(starts))]
 
     def encode_frames(self, segments) -> list[bytes]:
-        """segments: list (<= batch) of lists of gop frames (Y, U, V) at display size."""
+        """segments: list (<= batch) of equally long lists (1..gop) of display-size (Y, U, V)
+        frames; each segment becomes one closed GOP (IDR + P frames)."""
+        n = len(segments[0]) if segments else 0
+        if not segments or len(segments) > self.batch:
+            raise ValueError(f"need 1..{self.batch} segments")
+        if not 1 <= n <= self.gop or any(len(s) != n for s in segments):
+            raise ValueError(f"segments must all have the same length in 1..{self.gop}")
         fsz = self.cw * self.ch * 3 // 2
-        buf = np.empty((len(segments), self.gop, fsz), np.uint8)
+        buf = np.empty((len(segments), n, fsz), np.uint8)
         for b, seg in enumerate(segments):
-            if len(seg) != self.gop:
-                raise ValueError("every segment must have exactly `gop` frames")
             for f, (y, u, v) in enumerate(seg):
                 buf[b, f] = pad_frame(y, u, v, self.cw, self.ch)
-        self._check(self.lib.tv_engine_encode_host(self.h, ptr(buf), len(segments)))
+        self._check(self.lib.tv_engine_encode_host(self.h, ptr(buf), len(segments), n))
+        self.last_frames = n
         return [self.segment(b) for b in range(len(segments))]
 
     def segment(self, b: int) -> bytes:
@@ -110,7 +116,7 @@ class GpuEngine:
 
     def psnr(self, b: int) -> dict:
         y, u, v = self.sse(b)
-        npx = self.width * self.height * self.gop
+        npx = self.width * self.height * getattr(self, "last_frames", self.gop)
         f = lambda s, n: float("inf") if s == 0 else 10 * np.log10(255.0 ** 2 * n / s)
         py, pu, pv = f(y, npx), f(u, npx / 4), f(v, npx / 4)
         return {"y": py, "u": pu, "v": pv, "yuv": (6 * py + pu + pv) / 8}
