@@ -1,0 +1,282 @@
+// k_ops.hip — pre-processing kernels of the transcode pipeline:
+//
+//  k_resize_h / k_resize_v   separable windowed-sinc (Lanczos-a) resampling of one plane.
+//                            Filter tables (start index + Q14 taps per output coordinate,
+//                            widened by the scale ratio when down-scaling, i.e. ffmpeg
+//                            `scale=-2:H:flags=lanczos` semantics) are built on the host.
+//                            H pass: a 256-wide row tile of the source is staged in LDS and
+//                            every lane reads its taps from LDS; V pass reads the int16
+//                            intermediate column-coalesced.
+//  k_rgb_to_i420             packed RGB24 -> I420, BT.601/BT.709, limited range; one thread
+//                            per 2x2 block (chroma = mean of the 4 converted pixels).
+//  k_p010_to_i420            10-bit P010 (semi-planar, MSB aligned) -> 8-bit I420 (rounding).
+//  k_tonemap_pq              HDR10 (P010, BT.2020 PQ) -> SDR I420 BT.709: PQ EOTF, BT.2390
+//                            EETF roll-off (knee on max-RGB), BT.2020->709 gamut matrix,
+//                            BT.709 OETF; one thread per 2x2 block.
+//  k_overlay_mask            burn a host-rasterised label mask (0 keep / 1 border / 2 glyph)
+//                            into a batch of frames (reference `drawtext text=%{n}`,
+//                            worker/tasks.py:2377-2395).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace tv {
+namespace ops {
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ uint8_t sat8(int v) { return (uint8_t)clampi(v, 0, 255); }
+
+constexpr int kTile = 256;
+
+// ---------------------------------------------------------------- resize (H pass)
+// tmp[y][x] = sum_k w[x][k] * src[y][ix[x]+k]  (Q14 weights, result kept at Q6 in int16)
+__global__ void __launch_bounds__(kTile) k_resize_h(const uint8_t* __restrict__ src, int sw, int sstride,
+                                                    int16_t* __restrict__ tmp, int dw, const int* __restrict__ ix,
+                                                    const int16_t* __restrict__ wx, int taps) {
+  __shared__ uint8_t row[kTile * 8 + 64];
+  const int y = blockIdx.y, x0 = blockIdx.x * kTile, x = x0 + threadIdx.x;
+  const uint8_t* s = src + (long)y * sstride;
+  // source span touched by this tile of outputs
+  const int lo = ix[x0];
+  const int hi = ix[min(x0 + kTile, dw) - 1] + taps;  // exclusive
+  const int span = hi - lo;
+  const bool staged = span <= (int)sizeof(row);
+  if (staged)
+    for (int i = threadIdx.x; i < span; i += kTile) row[i] = s[clampi(lo + i, 0, sw - 1)];
+  __syncthreads();
+  if (x >= dw) return;
+  const int b = ix[x];
+  const int16_t* w = wx + (long)x * taps;
+  int acc = 0;
+  if (staged) {
+    for (int k = 0; k < taps; ++k) acc += w[k] * row[b + k - lo];
+  } else {
+    for (int k = 0; k < taps; ++k) acc += w[k] * s[clampi(b + k, 0, sw - 1)];
+  }
+  tmp[(long)y * dw + x] = (int16_t)clampi((acc + (1 << 7)) >> 8, -32768, 32767);  // Q14 -> Q6
+}
+
+// ---------------------------------------------------------------- resize (V pass)
+__global__ void __launch_bounds__(kTile) k_resize_v(const int16_t* __restrict__ tmp, int sh, int dw,
+                                                    uint8_t* __restrict__ dst, int dstride, int dh,
+                                                    const int* __restrict__ iy, const int16_t* __restrict__ wy,
+                                                    int taps) {
+  const int x = blockIdx.x * kTile + threadIdx.x, y = blockIdx.y;
+  if (x >= dw || y >= dh) return;
+  const int b = iy[y];
+  const int16_t* w = wy + (long)y * taps;
+  int acc = 0;
+  for (int k = 0; k < taps; ++k) acc += w[k] * tmp[(long)clampi(b + k, 0, sh - 1) * dw + x];
+  dst[(long)y * dstride + x] = sat8((acc + (1 << 19)) >> 20);  // Q14 * Q6 -> Q0
+}
+
+// ------------------------------------------------------------------- RGB -> I420
+struct YuvMat {
+  float ry, gy, by, ru, gu, bu, rv, gv, bv;
+};
+__device__ __forceinline__ YuvMat yuv_mat(int bt709) {
+  // limited range: Y = 16 + 219*Y', C = 128 + 224*C'
+  if (bt709) return {0.2126f, 0.7152f, 0.0722f, -0.1146f, -0.3854f, 0.5f, 0.5f, -0.4542f, -0.0458f};
+  return {0.299f, 0.587f, 0.114f, -0.168736f, -0.331264f, 0.5f, 0.5f, -0.418688f, -0.081312f};
+}
+
+__global__ void k_rgb_to_i420(const uint8_t* __restrict__ rgb, int w, int h, int stride, uint8_t* __restrict__ Y,
+                              uint8_t* __restrict__ U, uint8_t* __restrict__ V, int bt709) {
+  const int cx = blockIdx.x * blockDim.x + threadIdx.x, cy = blockIdx.y;
+  if (cx >= w / 2 || cy >= h / 2) return;
+  const YuvMat m = yuv_mat(bt709);
+  float su = 0.f, sv = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int x = 2 * cx + i, y = 2 * cy + j;
+      const uint8_t* p = rgb + (long)y * stride + 3 * x;
+      const float r = p[0] / 255.f, g = p[1] / 255.f, b = p[2] / 255.f;
+      Y[(long)y * w + x] = sat8(__float2int_rn(16.f + 219.f * (m.ry * r + m.gy * g + m.by * b)));
+      su += m.ru * r + m.gu * g + m.bu * b;
+      sv += m.rv * r + m.gv * g + m.bv * b;
+    }
+  U[(long)cy * (w / 2) + cx] = sat8(__float2int_rn(128.f + 224.f * su * 0.25f));
+  V[(long)cy * (w / 2) + cx] = sat8(__float2int_rn(128.f + 224.f * sv * 0.25f));
+}
+
+// ------------------------------------------------------------------ P010 -> I420
+__global__ void k_p010_to_i420(const uint16_t* __restrict__ y16, const uint16_t* __restrict__ uv16, int w, int h,
+                               uint8_t* __restrict__ Y, uint8_t* __restrict__ U, uint8_t* __restrict__ V) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  Y[(long)y * w + x] = (uint8_t)min(255, ((y16[(long)y * w + x] >> 6) + 2) >> 2);
+  if (!(x & 1) && !(y & 1)) {
+    const long c = (long)(y >> 1) * w + x;  // interleaved UV row of w samples
+    const long o = (long)(y >> 1) * (w >> 1) + (x >> 1);
+    U[o] = (uint8_t)min(255, ((uv16[c] >> 6) + 2) >> 2);
+    V[o] = (uint8_t)min(255, ((uv16[c + 1] >> 6) + 2) >> 2);
+  }
+}
+
+// --------------------------------------------------------------- HDR10 tone-map
+__device__ __forceinline__ float pq_eotf(float e) {  // -> linear, 1.0 = 10000 nits
+  const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
+  const float p = __powf(fmaxf(e, 0.f), 1.f / m2);
+  return __powf(fmaxf(p - c1, 0.f) / (c2 - c3 * p), 1.f / m1);
+}
+__device__ __forceinline__ float pq_oetf(float l) {
+  const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
+  const float p = __powf(fmaxf(l, 0.f), m1);
+  return __powf((c1 + c2 * p) / (1.f + c3 * p), m2);
+}
+__device__ __forceinline__ float bt709_oetf(float l) {
+  l = fminf(fmaxf(l, 0.f), 1.f);
+  return l < 0.018f ? 4.5f * l : 1.099f * __powf(l, 0.45f) - 0.099f;
+}
+// BT.2390 EETF on PQ-encoded luminance: source peak src_pq, target peak dst_pq
+__device__ __forceinline__ float eetf(float e, float src_pq, float dst_pq) {
+  const float en = e / src_pq, maxl = dst_pq / src_pq;
+  const float ks = 1.5f * maxl - 0.5f;
+  float o = en;
+  if (en > ks) {
+    const float t = (en - ks) / (1.f - ks), t2 = t * t, t3 = t2 * t;
+    o = (2 * t3 - 3 * t2 + 1) * ks + (t3 - 2 * t2 + t) * (1.f - ks) + (-2 * t3 + 3 * t2) * maxl;
+  }
+  return o * src_pq;
+}
+
+__global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* __restrict__ uv16, int w, int h,
+                             uint8_t* __restrict__ Y, uint8_t* __restrict__ U, uint8_t* __restrict__ V,
+                             float src_peak_nits, float dst_peak_nits) {
+  const int cx = blockIdx.x * blockDim.x + threadIdx.x, cy = blockIdx.y;
+  if (cx >= w / 2 || cy >= h / 2) return;
+  const long c = (long)cy * w + 2 * cx;
+  // limited-range 10-bit chroma
+  const float cb = ((uv16[c] >> 6) - 512.f) / 896.f, cr = ((uv16[c + 1] >> 6) - 512.f) / 896.f;
+  const float src_pq = pq_oetf(src_peak_nits / 10000.f), dst_pq = pq_oetf(dst_peak_nits / 10000.f);
+  const YuvMat m = yuv_mat(1);
+  float su = 0.f, sv = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int x = 2 * cx + i, y = 2 * cy + j;
+      const float yp = ((y16[(long)y * w + x] >> 6) - 64.f) / 876.f;
+      // BT.2020 NCL Y'CbCr -> R'G'B' (PQ)
+      float r = yp + 1.4746f * cr, g = yp - 0.16455f * cb - 0.57135f * cr, b = yp + 1.8814f * cb;
+      // tone-map on max(R,G,B) in the PQ domain, scale linear RGB by the luminance ratio
+      const float mx = fmaxf(fmaxf(r, g), fmaxf(b, 1e-6f));
+      const float lm = pq_eotf(mx), lt = pq_eotf(eetf(mx, src_pq, dst_pq));
+      const float sc = lm > 0.f ? lt / lm : 0.f;
+      const float norm = 10000.f / dst_peak_nits;  // target peak -> 1.0
+      const float R = pq_eotf(r) * sc * norm, G = pq_eotf(g) * sc * norm, B = pq_eotf(b) * sc * norm;
+      // BT.2020 -> BT.709 primaries (linear)
+      const float r7 = 1.6605f * R - 0.5876f * G - 0.0728f * B;
+      const float g7 = -0.1246f * R + 1.1329f * G - 0.0083f * B;
+      const float b7 = -0.0182f * R - 0.1006f * G + 1.1187f * B;
+      const float rr = bt709_oetf(r7), gg = bt709_oetf(g7), bb = bt709_oetf(b7);
+      Y[(long)y * w + x] = sat8(__float2int_rn(16.f + 219.f * (m.ry * rr + m.gy * gg + m.by * bb)));
+      su += m.ru * rr + m.gu * gg + m.bu * bb;
+      sv += m.rv * rr + m.gv * gg + m.bv * bb;
+    }
+  U[(long)cy * (w / 2) + cx] = sat8(__float2int_rn(128.f + 224.f * su * 0.25f));
+  V[(long)cy * (w / 2) + cx] = sat8(__float2int_rn(128.f + 224.f * sv * 0.25f));
+}
+
+// ---------------------------------------------------------------- label overlay
+// frames: n x (Y | U | V) I420 at w x h; masks: n x (mh x mw), placed at (x0, y0) (even).
+__global__ void k_overlay_mask(uint8_t* __restrict__ frames, int w, int h, const uint8_t* __restrict__ masks,
+                               int mw, int mh, int x0, int y0) {
+  const int mx = blockIdx.x * blockDim.x + threadIdx.x, my = blockIdx.y, f = blockIdx.z;
+  if (mx >= mw || my >= mh) return;
+  const int x = x0 + mx, y = y0 + my;
+  if (x < 0 || y < 0 || x >= w || y >= h) return;
+  const uint8_t m = masks[((long)f * mh + my) * mw + mx];
+  if (!m) return;
+  uint8_t* Y = frames + (long)f * (w * h * 3 / 2);
+  Y[(long)y * w + x] = m == 2 ? 235 : 16;
+  if (!(x & 1) && !(y & 1)) {
+    uint8_t* U = Y + (long)w * h;
+    uint8_t* V = U + (long)(w / 2) * (h / 2);
+    U[(long)(y / 2) * (w / 2) + x / 2] = 128;
+    V[(long)(y / 2) * (w / 2) + x / 2] = 128;
+  }
+}
+
+}  // namespace ops
+}  // namespace tv
+
+// ------------------------------------------------------------------- C API
+// Every entry point takes device pointers and the caller's stream; returns 0 / -1.
+namespace {
+thread_local std::string g_ops_err;
+int ops_status() {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return 0;
+  g_ops_err = hipGetErrorString(e);
+  return -1;
+}
+inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+}  // namespace
+
+extern "C" {
+const char* tv_ops_last_error() { return g_ops_err.c_str(); }
+
+int tv_resize_plane(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh, int dstride,
+                    const int* ix, const int16_t* wx, int tx, const int* iy, const int16_t* wy, int ty,
+                    int16_t* tmp, void* stream) {
+  if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 || tx <= 0 || ty <= 0 || tx > 64 || ty > 64) {
+    g_ops_err = "tv_resize_plane: bad geometry";
+    return -1;
+  }
+  auto s = static_cast<hipStream_t>(stream);
+  tv::ops::k_resize_h<<<dim3(cdiv(dw, tv::ops::kTile), sh), tv::ops::kTile, 0, s>>>(src, sw, sstride, tmp, dw, ix,
+                                                                                     wx, tx);
+  tv::ops::k_resize_v<<<dim3(cdiv(dw, tv::ops::kTile), dh), tv::ops::kTile, 0, s>>>(tmp, sh, dw, dst, dstride, dh,
+                                                                                     iy, wy, ty);
+  return ops_status();
+}
+
+int tv_rgb_to_i420(const uint8_t* rgb, int w, int h, int stride, uint8_t* y, uint8_t* u, uint8_t* v, int bt709,
+                   void* stream) {
+  if ((w | h) & 1) {
+    g_ops_err = "tv_rgb_to_i420: odd size";
+    return -1;
+  }
+  tv::ops::k_rgb_to_i420<<<dim3(cdiv(w / 2, 128), h / 2), 128, 0, static_cast<hipStream_t>(stream)>>>(
+      rgb, w, h, stride, y, u, v, bt709);
+  return ops_status();
+}
+
+int tv_p010_to_i420(const uint16_t* y16, const uint16_t* uv16, int w, int h, uint8_t* y, uint8_t* u, uint8_t* v,
+                    void* stream) {
+  if ((w | h) & 1) {
+    g_ops_err = "tv_p010_to_i420: odd size";
+    return -1;
+  }
+  tv::ops::k_p010_to_i420<<<dim3(cdiv(w, 256), h), 256, 0, static_cast<hipStream_t>(stream)>>>(y16, uv16, w, h, y,
+                                                                                                u, v);
+  return ops_status();
+}
+
+int tv_tonemap_pq(const uint16_t* y16, const uint16_t* uv16, int w, int h, uint8_t* y, uint8_t* u, uint8_t* v,
+                  float src_peak, float dst_peak, void* stream) {
+  if ((w | h) & 1 || src_peak <= dst_peak) {
+    g_ops_err = "tv_tonemap_pq: odd size or src_peak <= dst_peak";
+    return -1;
+  }
+  tv::ops::k_tonemap_pq<<<dim3(cdiv(w / 2, 128), h / 2), 128, 0, static_cast<hipStream_t>(stream)>>>(
+      y16, uv16, w, h, y, u, v, src_peak, dst_peak);
+  return ops_status();
+}
+
+int tv_overlay_mask(uint8_t* frames, int n, int w, int h, const uint8_t* masks, int mw, int mh, int x0, int y0,
+                    void* stream) {
+  if (n <= 0 || mw <= 0 || mh <= 0 || (x0 & 1) || (y0 & 1)) {
+    g_ops_err = "tv_overlay_mask: bad arguments";
+    return -1;
+  }
+  tv::ops::k_overlay_mask<<<dim3(cdiv(mw, 128), mh, n), 128, 0, static_cast<hipStream_t>(stream)>>>(
+      frames, w, h, masks, mw, mh, x0, y0);
+  return ops_status();
+}
+}

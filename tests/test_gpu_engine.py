@@ -38,3 +38,21 @@ def test_gpu_host_frames_path():
     seg = eng.encode_frames([frames])[0]
     cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, search_range=4)
     assert seg == cpu_bs
+
+
+@pytest.mark.gpu
+def test_encode_parts_variable_chunks():
+    """Worker path: parts of different lengths cut into closed-GOP chunks, batched on the
+    GPU engine, each part decodes to the right number of frames."""
+    from thinvids_amd.worker.encoder import EncodeSpec, EngineCache, encode_parts
+
+    frames = [hevc.synth_frame(5, t, 192, 128) for t in range(21)]
+    spec = EncodeSpec(192, 128, qp=30, gop=8)
+    cache = EngineCache(device=0, batch=4)
+    bits = encode_parts([frames[:21], frames[:13]], spec, cache)
+    cache.close()
+    for b, n in zip(bits, (21, 13)):
+        dec = hevc.decode(b, coded=False)
+        assert len(dec.frames) == n
+        for a, d in zip(frames, dec.frames):
+            assert hevc.psnr(a[0], d[0]) > 30

@@ -1,0 +1,114 @@
+"""Pre-processing ops: numpy float64 references (CPU) and the HIP kernels against them
+(GPU).  Numerics tests follow the rule "HIP kernel vs plain fp32/fp64 reference of the
+same op"."""
+import numpy as np
+import pytest
+
+from thinvids_amd.ops import color, overlay, resize
+
+
+def _img(h, w, seed=0):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = 128 + 60 * np.sin(x / 7.0) * np.cos(y / 11.0)
+    return np.clip(base + rng.normal(0, 8, (h, w)), 0, 255).astype(np.uint8)
+
+
+def test_filter_tables_normalised():
+    for n_in, n_out in ((1920, 1280), (1280, 1920), (1080, 720), (64, 64), (3840, 640)):
+        s, w, wq = resize.filter_table(n_in, n_out)
+        assert np.allclose(w.sum(1), 1.0)
+        assert (wq.astype(np.int64).sum(1) == 1 << resize.Q).all()
+        assert np.all(np.diff(s) >= 0)
+
+
+def test_resize_ref_properties():
+    flat = np.full((90, 160), 77, np.uint8)
+    assert (resize.resize_plane_ref(flat, 60, 106) == 77).all()
+    img = _img(96, 128)
+    same = resize.resize_plane_ref(img, 96, 128)
+    assert np.abs(same.astype(int) - img).max() <= 1  # identity scale ~ identity
+    down = resize.resize_plane_ref(img, 48, 64)
+    assert down.shape == (48, 64)
+    # down-scale of a smooth field tracks 2x2 box average within a few levels
+    box = img.reshape(48, 2, 64, 2).mean((1, 3))
+    assert np.abs(down.astype(float) - box).mean() < 6
+
+
+def test_colour_refs():
+    white = np.full((4, 4, 3), 255, np.uint8)
+    y, u, v = color.rgb_to_i420_ref(white)
+    assert (y == 235).all() and (u == 128).all() and (v == 128).all()
+    black = np.zeros((4, 4, 3), np.uint8)
+    y, _, _ = color.rgb_to_i420_ref(black)
+    assert (y == 16).all()
+    y16 = np.full((4, 4), 940 << 6, np.uint16)
+    uv = np.full((2, 4), 512 << 6, np.uint16)
+    y8, u8, v8 = color.p010_to_i420_ref(y16, uv)
+    assert (y8 == 235).all() and (u8 == 128).all() and (v8 == 128).all()
+    # PQ round trip and monotone tone curve
+    l = np.linspace(0, 1, 50)
+    assert np.allclose(color.pq_eotf(color.pq_oetf(l)), l, atol=1e-9)
+    ramp = np.tile(((np.linspace(64, 940, 64).astype(np.int64)) << 6).astype(np.uint16), (2, 1))
+    ty, tu, tv = color.tonemap_pq_ref(ramp, np.full((1, 64), 512 << 6, np.uint16))
+    assert np.all(np.diff(ty[0].astype(int)) >= 0) and ty[0, 0] == 16 and ty[0, -1] <= 235
+
+
+def test_stamp_ref_draws_label():
+    f = tuple(np.full(s, 100, np.uint8) for s in ((240, 320), (120, 160), (120, 160)))
+    y, u, v = overlay.stamp_ref(f, "123")
+    assert (y == 235).sum() > 500 and (y == 16).sum() > 500
+    assert (f[0] == 100).all()  # input untouched
+    m = overlay.label_mask("7")
+    assert m.shape[0] % 2 == 0 and m.shape[1] % 2 == 0 and set(np.unique(m)) == {0, 1, 2}
+
+
+# ------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,out", [((1080, 1920), (720, 1280)), ((96, 128), (150, 200)),
+                                       ((2160, 3840), (360, 640))])
+def test_resize_hip_matches_reference(shape, out):
+    import torch
+
+    img = _img(*shape, seed=3)
+    got = resize.resize_plane(torch.from_numpy(img).cuda(), *out).cpu().numpy()
+    ref = resize.resize_plane_ref(img, *out)
+    assert got.shape == ref.shape
+    assert np.abs(got.astype(int) - ref).max() <= 1
+
+
+@pytest.mark.gpu
+def test_colour_hip_matches_reference():
+    import torch
+
+    rng = np.random.default_rng(1)
+    rgb = rng.integers(0, 256, (64, 96, 3), dtype=np.uint8)
+    for bt709 in (True, False):
+        got = color.rgb_to_i420(torch.from_numpy(rgb).cuda(), bt709)
+        ref = color.rgb_to_i420_ref(rgb, bt709)
+        for g, r in zip(got, ref):
+            assert np.abs(g.cpu().numpy().astype(int) - r).max() <= 1
+    y16 = (rng.integers(64, 941, (64, 96)) << 6).astype(np.uint16)
+    uv16 = (rng.integers(64, 961, (32, 96)) << 6).astype(np.uint16)
+    t = lambda a: torch.from_numpy(a.view(np.int16)).cuda()
+    for g, r in zip(color.p010_to_i420(t(y16), t(uv16)), color.p010_to_i420_ref(y16, uv16)):
+        assert (g.cpu().numpy() == r).all()
+    for g, r in zip(color.tonemap_pq(t(y16), t(uv16)), color.tonemap_pq_ref(y16, uv16)):
+        assert np.abs(g.cpu().numpy().astype(int) - r).max() <= 2
+
+
+@pytest.mark.gpu
+def test_overlay_hip_matches_reference():
+    import torch
+
+    w, h = 320, 240
+    frames = [tuple(np.full(s, 60 + 10 * k, np.uint8) for s in ((h, w), (h // 2, w // 2), (h // 2, w // 2)))
+              for k in range(3)]
+    flat = np.stack([np.concatenate([p.ravel() for p in f]) for f in frames])
+    dev = torch.from_numpy(flat).cuda()
+    overlay.stamp_frames_gpu(dev, w, h, [11, 12, 13])
+    host = dev.cpu().numpy()
+    for k, f in enumerate(frames):
+        ry, ru, rv = overlay.stamp_ref(f, str(11 + k))
+        assert (host[k, :w * h].reshape(h, w) == ry).all()
+        assert (host[k, w * h:w * h + w * h // 4].reshape(h // 2, w // 2) == ru).all()

@@ -1,0 +1,123 @@
+"""End-to-end worker pipeline on CPU: transcode -> split -> encode -> stitch through the
+real queues with threaded consumers (reference test strategy: SURVEY.md §4 — the reference
+exercises these paths only on a live cluster; here they run in-process with the local
+store, the HTTP data plane on 127.0.0.1 and the software encoder)."""
+import os
+import time
+import uuid
+
+import numpy as np
+import pytest
+
+from thinvids_amd.models import hevc, media
+
+
+@pytest.fixture(scope="module")
+def env(tmp_path_factory):
+    root = tmp_path_factory.mktemp("tv")
+    old = dict(os.environ)
+    os.environ.update({
+        "PROJECT_ROOT": str(root / "projects"), "LIBRARY_ROOT": str(root / "library"),
+        "WATCH_ROOT": str(root / "watch"), "MASTER_HTTP_PORT": "0", "MASTER_HTTP_BIND": "127.0.0.1",
+        "HOSTNAME": "127.0.0.1", "STITCH_STABLE_SEC": "0.05", "STITCH_POLL_SEC": "0.05",
+        "TV_FORCE_CPU": "1", "JOB_HEARTBEAT_INTERVAL_SEC": "2",
+    })
+    from thinvids_amd.common import invalidate_settings_cache, save_settings
+    from thinvids_amd.store import LocalStore, set_store
+    from thinvids_amd.worker.config import get_config
+
+    store = LocalStore()
+    set_store(store)
+    get_config(reload=True)
+    invalidate_settings_cache()
+    save_settings({"tv_gop": "8", "tv_segment_frames": "8"}, store)
+    from thinvids_amd.queue import Consumer
+    from thinvids_amd.worker import tasks
+
+    tasks.pipeline_q.flush()
+    tasks.encode_q.flush()
+    cons = [Consumer(tasks.pipeline_q, workers=3).start(),
+            Consumer(tasks.encode_q, workers=1, handler=lambda q: tasks.encode_batch_handler(timeout=0.1)).start()]
+    yield {"root": root, "store": store, "tasks": tasks}
+    for c in cons:
+        c.stop()
+    os.environ.clear()
+    os.environ.update(old)
+
+
+def _source(root, name, n=20, w=128, h=96):
+    watch = root / "watch"
+    watch.mkdir(exist_ok=True)
+    frames = [hevc.synth_frame(3, t, w, h) for t in range(n)]
+    path = watch / name
+    media.write_y4m(str(path), frames, 25, 1)
+    return path, frames
+
+
+def _wait_status(store, job_id, want, timeout=90):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        s = store.hget(f"job:{job_id}", "status")
+        if s in want:
+            return s
+        time.sleep(0.05)
+    raise AssertionError(f"job stuck in {store.hget(f'job:{job_id}', 'status')}: {store.hgetall(f'job:{job_id}')}")
+
+
+@pytest.mark.parametrize("mode", ["split", "direct"])
+def test_transcode_end_to_end(env, mode):
+    store, tasks = env["store"], env["tasks"]
+    path, frames = _source(env["root"], f"clip_{mode}.y4m")
+    job_id, tok = str(uuid.uuid4()), uuid.uuid4().hex
+    store.hset(f"job:{job_id}", mapping={
+        "job_id": job_id, "filename": f"clip_{mode}.y4m", "input_path": str(path), "status": "STARTING",
+        "pipeline_run_token": tok, "software_encode": "1", "target_height": "1080", "processing_mode": mode})
+    tasks.transcode(job_id, tok)
+    assert _wait_status(store, job_id, {"DONE", "FAILED"}) == "DONE", store.hgetall(f"job:{job_id}")
+    job = store.hgetall(f"job:{job_id}")
+    assert job["processing_mode_effective"] == mode
+    assert int(job["parts_total"]) >= 2 and int(job["parts_done"]) == int(job["parts_total"])
+    assert int(job["encode_progress"]) == 100 and int(job["combine_progress"]) == 100
+    out = job["output_path"]
+    assert out.endswith(f"clip_{mode}.mp4") and os.path.isfile(out)
+    assert job["dest_codec"] == "hevc" and job["dest_resolution"] == "128x96"
+    with open(out, "rb") as f:
+        dm = hevc.demux_mp4(f.read())
+    dec = hevc.decode(dm["annexb"], coded=False)
+    assert len(dec.frames) == len(frames)
+    for a, b in zip(frames, dec.frames):
+        assert hevc.psnr(a[0], b[0]) > 30
+    # scratch cleaned, activity recorded
+    assert not os.path.exists(os.path.join(str(env["root"] / "projects"), job_id))
+    log = store.lrange(f"joblog:{job_id}", 0, -1)
+    assert any("[FINISH]" in line for line in log) and any("[ENCODE]" in line for line in log)
+
+
+def test_stale_token_is_ignored(env):
+    store, tasks = env["store"], env["tasks"]
+    job_id = str(uuid.uuid4())
+    store.hset(f"job:{job_id}", mapping={"status": "STARTING", "pipeline_run_token": "new"})
+    assert tasks.transcode.call_local(job_id, "old") is None
+    assert store.hget(f"job:{job_id}", "status") == "STARTING"
+
+
+def test_dataplane_roundtrip(env, tmp_path):
+    from thinvids_amd.worker import dataplane
+    from thinvids_amd.worker.helpers import part_paths
+
+    srv = dataplane.start_http_once()
+    ep = f"127.0.0.1:{srv.port}"
+    job_id = str(uuid.uuid4())
+    part, enc = part_paths(job_id, 7)
+    os.makedirs(os.path.dirname(part), exist_ok=True)
+    payload = np.random.default_rng(0).integers(0, 255, 3 * 1024 * 1024 + 17, dtype=np.uint8).tobytes()
+    with open(part, "wb") as f:
+        f.write(payload)
+    n = dataplane.fetch_part(ep, job_id, 7, str(tmp_path / "got.y4m"))
+    assert n == len(payload) and (tmp_path / "got.y4m").read_bytes() == payload
+    dataplane.upload_result(ep, job_id, 7, payload[:1000])
+    assert open(enc, "rb").read() == payload[:1000]
+    import urllib.error
+
+    with pytest.raises(urllib.error.HTTPError):
+        dataplane.fetch_part(ep, job_id, 0, str(tmp_path / "bad"))
