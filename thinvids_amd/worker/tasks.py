@@ -158,7 +158,8 @@ def split(job_id: str, run_token: str | None = None):
                                size_b=int(info["size"] or 0),
                                target_segment_mb=as_float(settings.get("target_segment_mb"), 10),
                                est_bytes_per_frame=spec.width * spec.height * 0.02)
-    if job.get("number_parts") and str(job["number_parts"]).isdigit() and int(job["number_parts"]) > 0:
+    if str(job.get("number_parts_override")) == "1" and str(job.get("number_parts") or "").isdigit() \
+            and int(job["number_parts"]) > 0:
         # per-job override (stored but unused by the reference pipeline; honoured here)
         plan = planning.plan_parts(int(info["frames"]), 0, gop=spec.gop,
                                    segment_frames=-(-int(info["frames"]) // int(job["number_parts"])))
