@@ -296,10 +296,20 @@ class Engine {
     const Parts d = carve(s.dev), h = carve(s.host);
     const long U = g_.usz;
     HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
-    HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, align(B * U * 4), hipMemcpyDeviceToHost, ws));  // 4 u8 planes
     HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
-    HIP_OK(hipMemcpyAsync(h.mask_y, d.mask_y, align(B * nctu_ * 8) + align(B * nctu_ * 4) + B * nctu_ * 4,
-                          hipMemcpyDeviceToHost, ws));  // mask_y | mask_c | offset
+    if (B == cfg_.batch) {  // full batch: the planes are contiguous, 2 copies cover them
+      HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, B * U * 4, hipMemcpyDeviceToHost, ws));  // 4 u8 planes
+      HIP_OK(hipMemcpyAsync(h.mask_y, d.mask_y, align(B * nctu_ * 8) + align(B * nctu_ * 4) + B * nctu_ * 4,
+                            hipMemcpyDeviceToHost, ws));  // mask_y | mask_c | offset
+    } else {  // partial batch: each plane is laid out for cfg_.batch segments
+      for (uint8_t* const* pl : {&h.cu_log2, &h.intra, &h.ipm, &h.cbf}) {
+        const long off = *pl - h.cu_log2;
+        HIP_OK(hipMemcpyAsync(*pl, d.cu_log2 + off, B * U, hipMemcpyDeviceToHost, ws));
+      }
+      HIP_OK(hipMemcpyAsync(h.mask_y, d.mask_y, B * nctu_ * 8, hipMemcpyDeviceToHost, ws));
+      HIP_OK(hipMemcpyAsync(h.mask_c, d.mask_c, B * nctu_ * 4, hipMemcpyDeviceToHost, ws));
+      HIP_OK(hipMemcpyAsync(h.offset, d.offset, B * nctu_ * 4, hipMemcpyDeviceToHost, ws));
+    }
     HIP_OK(hipStreamSynchronize(ws));
     long bytes = 0;
     for (int b = 0; b < B; ++b) {
