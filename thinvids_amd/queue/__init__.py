@@ -154,9 +154,12 @@ class TaskQueue:
 
     def drain(self, max_tasks: int = 10_000) -> int:
         """Run queued tasks inline until the queue is empty (tests / single-process mode)."""
-        n = 0
-        while n < max_tasks and self.run_one(timeout=0.01):
-            n += 1
+        n = idle = 0
+        while n < max_tasks and len(self) > 0 and idle <= len(self):
+            if self.run_one(timeout=0.01):
+                n, idle = n + 1, 0
+            else:  # revoked (dropped) or not yet due (requeued)
+                idle += 1
         return n
 
 
