@@ -50,7 +50,7 @@ class AgentConfig:
         self.gc_interval_sec = max(60, as_int(e.get("GC_INTERVAL_SEC"), 900))
         self.gc_min_age_sec = max(300, as_int(e.get("GC_MIN_AGE_SEC"), 21600))
         self.role_sync_interval_sec = max(5, as_int(e.get("ROLE_SYNC_INTERVAL_SEC"), 10))
-        self.encode_service = e.get("ENCODE_SERVICE", "thinvids-worker-encode.service")
+        self.encode_service = e.get("ENCODE_SERVICE", "thinvids-worker-encode.target")
         self.pipeline_service = e.get("PIPELINE_SERVICE", "thinvids-worker-pipeline.service")
         self.manage_services = as_bool(e.get("AGENT_MANAGE_SERVICES", "1"), True) and bool(shutil.which("systemctl"))
 
