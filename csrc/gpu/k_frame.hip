@@ -59,51 +59,93 @@ __global__ void __launch_bounds__(256) k_sse(FrameSet a, FrameSet r, Geo g, unsi
 // exact).  Separable: the 3 horizontal phases are filtered once into LDS (int16), then the
 // 4 vertical phases of each.  Motion search and luma motion compensation then become
 // plain byte loads.
+// 16 quarter-sample phase planes of a reference frame (padded by 8 on every side), one
+// 32x32 output tile per block.  Each thread produces 4 horizontally adjacent samples of all
+// 16 planes: the 8 vertical taps of every source row set (integer samples + the three
+// horizontal half/quarter filters) are read once as dwords / 4 x int16 from LDS and reused
+// for the three vertical phases, and every plane is written with one dword store.
 __global__ void __launch_bounds__(256) k_phase_planes(FrameSet ref, uint8_t* phase, Geo g) {
   const int b = blockIdx.z, tid = threadIdx.x;
   const int tx0 = blockIdx.x * 32 - 8, ty0 = blockIdx.y * 32 - 8;
   const uint8_t* R = ref.plane(0, b, g);
-  __shared__ uint8_t raw[39][40];
-  __shared__ int16_t hf[3][39][32];
-  for (int i = tid; i < 39 * 39; i += 256) {
-    const int rr = i / 39, cc = i % 39;
-    const int X = clip3(0, g.W - 1, tx0 - 3 + cc), Y = clip3(0, g.H - 1, ty0 - 3 + rr);
-    raw[rr][cc] = R[(long)Y * g.W + X];
+  // raw[rr][k] = sample (tx0 - 4 + k, ty0 - 3 + rr): column c of the tile sits at k = c + 4
+  __shared__ __align__(16) uint8_t raw[39][40];
+  __shared__ __align__(16) int16_t hf[3][39][32];
+  for (int i = tid; i < 39 * 40; i += 256) {
+    const int rr = i / 40, k = i % 40;
+    const int X = clip3(0, g.W - 1, tx0 - 4 + k), Y = clip3(0, g.H - 1, ty0 - 3 + rr);
+    raw[rr][k] = R[(long)Y * g.W + X];
   }
   __syncthreads();
   for (int i = tid; i < 3 * 39 * 32; i += 256) {
     const int fx = 1 + i / (39 * 32), rem = i % (39 * 32), rr = rem / 32, c = rem % 32;
     int v = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v += kLumaFilter[fx][k] * raw[rr][c + k];
+    for (int k = 0; k < 8; ++k) v += kLumaFilter[fx][k] * raw[rr][c + k + 1];
     hf[fx - 1][rr][c] = (int16_t)v;
   }
   __syncthreads();
-  uint8_t* base = phase + (long)b * 16 * g.psz;
-  for (int i = tid; i < 32 * 32; i += 256) {
-    const int r = i >> 5, c = i & 31;
-    const int X = tx0 + c, Y = ty0 + r;
-    if (X >= g.W + 8 || Y >= g.H + 8) continue;
-    const long off = (long)(Y + 8) * g.pw16 + (X + 8);
+  const int r = tid >> 3, c0 = (tid & 7) * 4;
+  const int X = tx0 + c0, Y = ty0 + r;
+  if (X + 8 >= g.pw16 || Y >= g.H + 8) return;
+  uint8_t* base = phase + (long)b * 16 * g.psz + (long)(Y + 8) * g.pw16 + (X + 8);
+  auto put = [&](int plane, const int (&v)[4]) {
+    uint32_t w = 0;
 #pragma unroll
-    for (int fy = 0; fy < 4; ++fy)
+    for (int j = 0; j < 4; ++j) w |= (uint32_t)clip_pixel((v[j] + 32) >> 6) << (8 * j);
+    *reinterpret_cast<uint32_t*>(base + (long)plane * g.psz) = w;
+  };
+  // integer column source: 8 rows x 4 samples
+  {
+    int col[8][4];
 #pragma unroll
-      for (int fx = 0; fx < 4; ++fx) {
-        int v;
-        if (fy == 0) {
-          v = fx == 0 ? (raw[r + 3][c + 3] << 6) : hf[fx - 1][r + 3][c];
-        } else if (fx == 0) {
-          v = 0;
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(&raw[r + k][c0 + 4]);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v += kLumaFilter[fy][k] * raw[r + k][c + 3];
-        } else {
-          v = 0;
+      for (int j = 0; j < 4; ++j) col[k][j] = (w >> (8 * j)) & 255;
+    }
+    int v[4];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v += kLumaFilter[fy][k] * hf[fx - 1][r + k][c];
-          v >>= 6;
-        }
-        base[(long)(fx + 4 * fy) * g.psz + off] = (uint8_t)clip_pixel((v + 32) >> 6);
+    for (int j = 0; j < 4; ++j) v[j] = col[3][j] << 6;
+    put(0, v);
+#pragma unroll
+    for (int fy = 1; fy < 4; ++fy) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int a = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a += kLumaFilter[fy][k] * col[k][j];
+        v[j] = a;
       }
+      put(4 * fy, v);
+    }
+  }
+#pragma unroll
+  for (int fx = 1; fx < 4; ++fx) {
+    int col[8][4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint2 w = *reinterpret_cast<const uint2*>(&hf[fx - 1][r + k][c0]);
+      col[k][0] = (int16_t)(w.x & 0xffff);
+      col[k][1] = (int16_t)(w.x >> 16);
+      col[k][2] = (int16_t)(w.y & 0xffff);
+      col[k][3] = (int16_t)(w.y >> 16);
+    }
+    int v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = col[3][j];
+    put(fx, v);
+#pragma unroll
+    for (int fy = 1; fy < 4; ++fy) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int a = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a += kLumaFilter[fy][k] * col[k][j];
+        v[j] = a >> 6;
+      }
+      put(fx + 4 * fy, v);
+    }
   }
 }
 

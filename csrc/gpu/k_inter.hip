@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   __shared__ int bcost[21], bmv[21][2];
   __shared__ int subsad[21][8];
   if (tid < 256) s32[tid] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (tid >> 3)) * g.W + cx + 4 * (tid & 7));
-  for (int w = tid; w < kWin * kWinW; w += kMeThreads) {
+  for (int w = tid; w < ((ablate & 4) ? 0 : kWin * kWinW); w += kMeThreads) {
     const int row = w / kWinW, wc = w % kWinW;
     const int gy = clip3(0, g.H - 1, cy - kWinOff + row);
     const int gx0 = cx - kWinOff + 4 * wc;
@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   }
 
   // ------------------------------- CU split decision ------------------------------------
-  if (tid == 0) {
+  if (tid == 0 && !(ablate & 8)) {
     const int ps = pen.split_inter;
     int sum16 = 0;
     uint8_t l2u[16];
@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
                         const Geo& g, int qp, const Penalties& pen, int range, int B, hipStream_t s) {
   // TV_ME_ABLATE (timing experiments only; output is invalid): bit0 skip integer search,
-  // bit1 skip sub-pel refinement
+  // bit1 skip sub-pel refinement, bit2 skip the window fill, bit3 skip the decision write
   static const int ablate = [] {
     const char* e = getenv("TV_ME_ABLATE");
     return e ? atoi(e) : 0;
