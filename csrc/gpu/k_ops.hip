@@ -202,6 +202,62 @@ __global__ void k_overlay_mask(uint8_t* __restrict__ frames, int w, int h, const
   }
 }
 
+
+// ---------------------------------------------------------------- bwdif deinterlace
+// Bob-Weaver deinterlacing of one plane, one output frame per input frame (reference
+// `bwdif=mode=send_frame`, worker/tasks.py:62-63): lines of the kept field are copied, each
+// missing line is predicted temporally from the same-parity lines of the two frames around
+// it (prev2/next2), refined by an edge-aware spatial interpolator (4-tap, or a 5-line
+// low/high-frequency blend when the vertical edge is strong) and clamped to the temporal
+// uncertainty `diff` widened by the spatial check.
+__global__ void k_bwdif(const uint8_t* __restrict__ prev, const uint8_t* __restrict__ cur,
+                        const uint8_t* __restrict__ next, uint8_t* __restrict__ out, int w, int h, int keep) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  const long o = (long)y * w + x;
+  if ((y & 1) == keep || y < 2 || y >= h - 2) {  // kept field (and border lines: bob)
+    if ((y & 1) == keep) {
+      out[o] = cur[o];
+    } else {
+      const int up = y > 0 ? cur[o - w] : cur[o + w], dn = y < h - 1 ? cur[o + w] : cur[o - w];
+      out[o] = (uint8_t)((up + dn + 1) >> 1);
+    }
+    return;
+  }
+  // same-parity temporal neighbours: the missing line lies between prev's and cur's field
+  const uint8_t* p2 = prev;
+  const uint8_t* n2 = cur;
+  auto at = [&](const uint8_t* f, int dy) { return (int)f[(long)clampi(y + dy, 0, h - 1) * w + x]; };
+  const int c = at(cur, -1), e = at(cur, 1);
+  const int d = (at(p2, 0) + at(n2, 0)) >> 1;
+  const int td0 = abs(at(p2, 0) - at(n2, 0));
+  const int td1 = (abs(at(prev, -1) - c) + abs(at(prev, 1) - e)) >> 1;
+  const int td2 = (abs(at(next, -1) - c) + abs(at(next, 1) - e)) >> 1;
+  int diff = max(td0 >> 1, max(td1, td2));
+  int v;
+  if (!diff) {
+    v = d;
+  } else {
+    const int b = ((at(p2, -2) + at(n2, -2)) >> 1) - c;
+    const int f = ((at(p2, 2) + at(n2, 2)) >> 1) - e;
+    const int dc = d - c, de = d - e;
+    const int mx = max(max(de, dc), min(b, f));
+    const int mn = min(min(de, dc), max(b, f));
+    diff = max(max(diff, mn), -mx);
+    int interp;
+    if (abs(c - e) > td0) {
+      interp = ((5570 * (at(p2, 0) + at(n2, 0)) - 3801 * (at(p2, -2) + at(n2, -2) + at(p2, 2) + at(n2, 2)) +
+                 1016 * (at(p2, -4) + at(n2, -4) + at(p2, 4) + at(n2, 4))) >> 2) +
+               4309 * (c + e) - 213 * (at(cur, -3) + at(cur, 3));
+    } else {
+      interp = 5077 * (c + e) - 981 * (at(cur, -3) + at(cur, 3));
+    }
+    interp >>= 13;
+    v = clampi(interp, d - diff, d + diff);
+  }
+  out[o] = sat8(v);
+}
+
 }  // namespace ops
 }  // namespace tv
 
@@ -277,6 +333,16 @@ int tv_overlay_mask(uint8_t* frames, int n, int w, int h, const uint8_t* masks, 
   }
   tv::ops::k_overlay_mask<<<dim3(cdiv(mw, 128), mh, n), 128, 0, static_cast<hipStream_t>(stream)>>>(
       frames, w, h, masks, mw, mh, x0, y0);
+  return ops_status();
+}
+int tv_bwdif_plane(const uint8_t* prev, const uint8_t* cur, const uint8_t* next, uint8_t* out, int w, int h,
+                   int tff, void* stream) {
+  if (w <= 0 || h < 4) {
+    g_ops_err = "tv_bwdif_plane: bad geometry";
+    return -1;
+  }
+  tv::ops::k_bwdif<<<dim3(cdiv(w, 256), h), 256, 0, static_cast<hipStream_t>(stream)>>>(prev, cur, next, out, w, h,
+                                                                                          tff ? 0 : 1);
   return ops_status();
 }
 }

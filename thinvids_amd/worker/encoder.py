@@ -131,24 +131,37 @@ def encode_parts(parts: list[list], spec: EncodeSpec, cache: EngineCache | None 
     return [b"".join(x) for x in out]
 
 
-def prepare_frames(frames: list, out_w: int, out_h: int, device: str | None = None) -> list:
-    """Resize (Lanczos) a list of I420 frames to out_w x out_h; identity if already there.
-    On a GPU host the HIP resampler runs on the device."""
+def prepare_frames(frames: list, out_w: int, out_h: int, device: str | None = None,
+                   deinterlace: bool = False) -> list:
+    """Optional bwdif deinterlace, then Lanczos resize of a list of I420 frames to
+    out_w x out_h (identity when already there).  On a GPU host both HIP kernels run on the
+    device and each frame crosses PCIe once each way."""
     if not frames:
         return frames
     h, w = frames[0][0].shape
-    if (w, h) == (out_w, out_h):
+    if (w, h) == (out_w, out_h) and not deinterlace:
         return frames
+    from ..ops.deint import bwdif_frame
     from ..ops.resize import resize_frame
 
+    n = len(frames)
     if device is None and gpu_available():
         import torch
 
-        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", os.environ.get("TV_DEVICE", "0"))))
+        up = [tuple(torch.from_numpy(np.ascontiguousarray(p)).to(dev, non_blocking=True) for p in f) for f in frames]
         out = []
-        for y, u, v in frames:
-            t = tuple(torch.from_numpy(np.ascontiguousarray(p)).to(dev, non_blocking=True) for p in (y, u, v))
-            r = resize_frame(t, out_w, out_h)
-            out.append(tuple(p.cpu().numpy() for p in r))
+        for i in range(n):
+            f = up[i]
+            if deinterlace:
+                f = bwdif_frame(up[max(0, i - 1)], f, up[min(n - 1, i + 1)])
+            if (w, h) != (out_w, out_h):
+                f = resize_frame(f, out_w, out_h)
+            out.append(tuple(p.cpu().numpy() for p in f))
         return out
-    return [resize_frame((np.asarray(y), np.asarray(u), np.asarray(v)), out_w, out_h) for y, u, v in frames]
+    frames = [tuple(np.asarray(p) for p in f) for f in frames]
+    if deinterlace:
+        frames = [bwdif_frame(frames[max(0, i - 1)], frames[i], frames[min(n - 1, i + 1)]) for i in range(n)]
+    if (w, h) == (out_w, out_h):
+        return frames
+    return [resize_frame(f, out_w, out_h) for f in frames]

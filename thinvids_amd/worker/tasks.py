@@ -309,7 +309,8 @@ def encode_batch(tasks: list[dict]) -> list[dict | None]:
         job_heartbeat(job_id, "encode", note=f"part {idx}")
         try:
             spec = encode_spec_for_job(job)
-            frames = prepare_frames(_load_part(job_id, job, t), spec.width, spec.height)
+            _, deint = effective_target_height(job)  # DVD-native SD keeps its lines + bwdif
+            frames = prepare_frames(_load_part(job_id, job, t), spec.width, spec.height, deinterlace=deint)
             if not frames:
                 raise RuntimeError("part has no frames")
             live.append((i, t, job, spec, frames, t0))
