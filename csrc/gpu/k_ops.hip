@@ -258,6 +258,37 @@ __global__ void k_bwdif(const uint8_t* __restrict__ prev, const uint8_t* __restr
   out[o] = sat8(v);
 }
 
+// ------------------------------------------------------------------------ SSIM
+// Mean SSIM over 8x8 windows on a 4-sample grid (x264/libvpx convention): one thread per
+// window computes the five moments, a wave reduction + one atomic per wave accumulates
+// (sum of SSIM, window count) in double.
+__global__ void __launch_bounds__(256) k_ssim(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int w,
+                                              int h, int stride_a, int stride_b, double* __restrict__ acc) {
+  const int nx = (w - 8) / 4 + 1, ny = (h - 8) / 4 + 1;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  double v = 0.0;
+  if (i < nx * ny) {
+    const int x0 = (i % nx) * 4, y0 = (i / nx) * 4;
+    int sa = 0, sb = 0, saa = 0, sbb = 0, sab = 0;
+    for (int y = 0; y < 8; ++y)
+      for (int x = 0; x < 8; ++x) {
+        const int p = a[(long)(y0 + y) * stride_a + x0 + x], q = b[(long)(y0 + y) * stride_b + x0 + x];
+        sa += p;
+        sb += q;
+        saa += p * p;
+        sbb += q * q;
+        sab += p * q;
+      }
+    const double n = 64.0, c1 = 6.5025, c2 = 58.5225;  // (0.01*255)^2, (0.03*255)^2
+    const double ma = sa / n, mb = sb / n;
+    const double va = saa / n - ma * ma, vb = sbb / n - mb * mb, cov = sab / n - ma * mb;
+    v = ((2 * ma * mb + c1) * (2 * cov + c2)) / ((ma * ma + mb * mb + c1) * (va + vb + c2));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(acc, v);
+}
+
 }  // namespace ops
 }  // namespace tv
 
@@ -345,4 +376,15 @@ int tv_bwdif_plane(const uint8_t* prev, const uint8_t* cur, const uint8_t* next,
                                                                                           tff ? 0 : 1);
   return ops_status();
 }
+}
+
+extern "C" int tv_ssim_plane(const uint8_t* a, const uint8_t* b, int w, int h, int stride_a, int stride_b, double* acc,
+                             void* stream) {
+  if (w < 8 || h < 8) {
+    g_ops_err = "tv_ssim_plane: plane smaller than 8x8";
+    return -1;
+  }
+  const long n = (long)((w - 8) / 4 + 1) * ((h - 8) / 4 + 1);
+  tv::ops::k_ssim<<<cdiv(n, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(a, b, w, h, stride_a, stride_b, acc);
+  return ops_status();
 }

@@ -141,3 +141,24 @@ def test_bwdif_hip_matches_reference():
     fr = [_img(72, 96, seed=s) for s in (1, 2, 3)]
     got = deint.bwdif_plane(*[torch.from_numpy(f).cuda() for f in fr]).cpu().numpy()
     assert (got == deint.bwdif_plane_ref(*fr)).all()
+
+
+def test_ssim_ref():
+    from thinvids_amd.ops import quality
+
+    a = _img(64, 80, seed=1)
+    assert abs(quality.ssim_ref(a, a) - 1.0) < 1e-12
+    noisy = np.clip(a.astype(int) + np.random.default_rng(0).normal(0, 10, a.shape), 0, 255).astype(np.uint8)
+    worse = np.clip(a.astype(int) + np.random.default_rng(0).normal(0, 30, a.shape), 0, 255).astype(np.uint8)
+    assert 1.0 > quality.ssim_ref(a, noisy) > quality.ssim_ref(a, worse) > 0
+
+
+@pytest.mark.gpu
+def test_ssim_hip_matches_reference():
+    import torch
+
+    from thinvids_amd.ops import quality
+
+    a, b = _img(120, 200, seed=1), _img(120, 200, seed=2)
+    got = quality.ssim(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda())
+    assert abs(got - quality.ssim_ref(a, b)) < 1e-9
