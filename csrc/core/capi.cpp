@@ -57,7 +57,8 @@ void* tv_cpu_encoder_new(int width, int height, int qp, int deblock, int range, 
   cfg.width = width;
   cfg.height = height;
   cfg.qp = qp;
-  cfg.deblock = deblock != 0;
+  cfg.deblock = (deblock & 1) != 0;  // bit 0: deblocking, bit 1: SAO
+  cfg.sao = (deblock & 2) != 0;
   cfg.max_merge_cand = max_merge;
   cfg.finalize();
   return new CpuEncoder(cfg, range);

@@ -289,6 +289,10 @@ void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* 
       }
     }
   if (cfg.deblock) deblock_picture(rec, fd.view(), qp);
+  if (cfg.sao) {  // SAO decisions on the deblocked picture, then the in-loop filter itself
+    sao_decide_picture(src, rec, qp, fd.sao.data());
+    sao_picture(rec, fd.sao.data());
+  }
 }
 
 // ------------------------------------ driver --------------------------------------------

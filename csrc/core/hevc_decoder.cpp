@@ -159,12 +159,40 @@ class SliceDecoder {
   int bin(int ctx) { return dec_.decode_bin(ctx_.c[ctx]); }
 
   void parse_sao(int cx, int cy) {
-    bool merge = false;
-    if (cx > 0) merge = bin(CTX_SAO_MERGE);
-    if (!merge && cy > 0) merge = bin(CTX_SAO_MERGE);
-    if (merge) return;
-    for (int c = 0; c < 2; ++c) {  // luma, chroma types
-      if (bin(CTX_SAO_TYPE)) fail("SAO offsets unsupported");
+    const int wc = sps_.coded_w >> kCtbLog2;
+    uint32_t* p = fd_->sao.data() + 3 * (size_t)(cy * wc + cx);
+    if (cx > 0 && bin(CTX_SAO_MERGE)) {
+      for (int c = 0; c < 3; ++c) p[c] = p[c - 3];
+      return;
+    }
+    if (cy > 0 && bin(CTX_SAO_MERGE)) {
+      for (int c = 0; c < 3; ++c) p[c] = p[c - 3 * wc];
+      return;
+    }
+    int type = 0, eo = 0;
+    for (int c = 0; c < 3; ++c) {
+      if (c < 2) {
+        type = bin(CTX_SAO_TYPE) ? (dec_.decode_bypass() ? 2 : 1) : 0;
+      }
+      int off[4] = {0, 0, 0, 0}, cls = 0;
+      if (type) {
+        for (int i = 0; i < 4; ++i) {
+          int a = 0;
+          while (a < kSaoMaxOff && dec_.decode_bypass()) ++a;
+          off[i] = a;
+        }
+        if (type == 1) {
+          for (int i = 0; i < 4; ++i)
+            if (off[i] && dec_.decode_bypass()) off[i] = -off[i];
+          cls = (int)dec_.decode_bypass_bins(5);
+        } else {
+          if (c < 2) eo = (int)dec_.decode_bypass_bins(2);
+          cls = eo;
+          off[2] = -off[2];
+          off[3] = -off[3];
+        }
+      }
+      p[c] = sao_pack(type, cls, off);
     }
   }
 
@@ -610,6 +638,7 @@ void HevcDecoder::decode(const uint8_t* data, size_t n) {
     SliceDecoder sd(sps, pps, islice, qp, max_merge, &br, &dp.pic, ref, &last_decisions, sao);
     sd.run();
     if (pps.deblock) deblock_picture(dp.pic, last_decisions.view(), qp);
+    if (sao) sao_picture(dp.pic, last_decisions.sao.data());
     pictures.push_back(std::move(dp));
   }
 }

@@ -111,4 +111,52 @@ void deblock_picture(Picture& pic, const FrameData& fd, int qp) {
     }
 }
 
+// ------------------------------------------------------------------------------ SAO
+void sao_ctb_stats(const Picture& src, const Picture& deb, int c, int cx, int cy, SaoStats& st) {
+  std::memset(&st, 0, sizeof(st));
+  const int w = deb.pw(c), h = deb.ph(c), n = c ? kCtb / 2 : kCtb;
+  const uint8_t* S = src.plane(c);
+  const uint8_t* D = deb.plane(c);
+  for (int y = cy * n; y < (cy + 1) * n && y < h; ++y)
+    for (int x = cx * n; x < (cx + 1) * n && x < w; ++x) {
+      const int v = D[y * w + x], diff = (int)S[y * w + x] - v;
+      st.bo_n[v >> 3] += 1;
+      st.bo_s[v >> 3] += diff;
+      for (int k = 0; k < 4; ++k) {
+        int dx, dy;
+        sao_eo_dir(k, dx, dy);
+        const int ax = x + dx, ay = y + dy, bx = x - dx, by = y - dy;
+        if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= w || ay >= h || bx >= w || by >= h) continue;
+        const int cat = sao_eo_category(v, D[ay * w + ax], D[by * w + bx]);
+        st.eo_n[k][cat] += 1;
+        st.eo_s[k][cat] += diff;
+      }
+    }
+}
+
+void sao_decide_picture(const Picture& src, const Picture& deb, int qp, uint32_t* params) {
+  const int wc = deb.w >> kCtbLog2, hc = deb.h >> kCtbLog2;
+  const long long lam16 = sao_lambda16(qp);
+  for (int cy = 0; cy < hc; ++cy)
+    for (int cx = 0; cx < wc; ++cx) {
+      SaoStats st[3];
+      for (int c = 0; c < 3; ++c) sao_ctb_stats(src, deb, c, cx, cy, st[c]);
+      sao_decide(st, lam16, params + 3 * (size_t)(cy * wc + cx));
+    }
+}
+
+void sao_picture(Picture& pic, const uint32_t* params) {
+  const int wc = pic.w >> kCtbLog2;
+  for (int c = 0; c < 3; ++c) {
+    const int w = pic.pw(c), h = pic.ph(c), n = c ? kCtb / 2 : kCtb;
+    std::vector<uint8_t> deb(pic.plane(c), pic.plane(c) + (size_t)w * h);
+    uint8_t* out = pic.plane(c);
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        const uint32_t p = params[3 * (size_t)((y / n) * wc + x / n) + c];
+        if (sao_type(p)) out[y * w + x] = (uint8_t)sao_sample(deb.data(), w, h, x, y, p);
+      }
+  }
+}
+
 }  // namespace tv

@@ -194,7 +194,7 @@ class SliceWriter {
     const int wc = cfg_.coded_w >> kCtbLog2, hc = cfg_.coded_h >> kCtbLog2;
     for (int cy = 0; cy < hc; ++cy)
       for (int cx = 0; cx < wc; ++cx) {
-        if (cfg_.sao) write_sao_off(cx, cy);
+        if (cfg_.sao) write_sao(cx, cy, wc);
         quadtree(cx << kCtbLog2, cy << kCtbLog2, kCtbLog2, 0);
         const bool last = (cy == hc - 1) && (cx == wc - 1);
         enc_.encode_terminate(last ? 1 : 0);
@@ -209,12 +209,42 @@ class SliceWriter {
   }
   void bin(int b, int ctx) { enc_.encode_bin(b, ctx_.c[ctx]); }
 
-  void write_sao_off(int cx, int cy) {
-    // sao(): merge flags (when neighbours exist) = 0, sao_type_idx luma = chroma = 0
-    if (cx > 0) bin(0, CTX_SAO_MERGE);
-    if (cy > 0) bin(0, CTX_SAO_MERGE);
-    bin(0, CTX_SAO_TYPE);  // luma: not applied (TR bin 0)
-    bin(0, CTX_SAO_TYPE);  // chroma
+  // sao() (7.3.8.3).  Merges are chosen by exact parameter equality with the left / upper
+  // CTB, so they never change the reconstruction.
+  void write_sao(int cx, int cy, int wc) {
+    const uint32_t none[3] = {sao_off_param(), sao_off_param(), sao_off_param()};
+    const uint32_t* p = fd_.sao ? fd_.sao + 3 * (size_t)(cy * wc + cx) : none;
+    auto same = [&](const uint32_t* q) { return q[0] == p[0] && q[1] == p[1] && q[2] == p[2]; };
+    if (cx > 0) {
+      const bool m = fd_.sao && same(p - 3);
+      bin(m, CTX_SAO_MERGE);
+      if (m) return;
+    }
+    if (cy > 0) {
+      const bool m = fd_.sao && same(p - 3 * (size_t)wc);
+      bin(m, CTX_SAO_MERGE);
+      if (m) return;
+    }
+    for (int c = 0; c < 3; ++c) {
+      const int t = sao_type(p[c]);
+      if (c < 2) {  // sao_type_idx_luma / _chroma: TR cMax 2, first bin context coded
+        bin(t != 0, CTX_SAO_TYPE);
+        if (t) enc_.encode_bypass(t == 2);
+      }
+      if (!t) continue;
+      for (int i = 0; i < 4; ++i) {  // sao_offset_abs: TR bypass, cMax 7
+        const int a = tv_abs(sao_offset(p[c], i));
+        for (int k = 0; k < a; ++k) enc_.encode_bypass(1);
+        if (a < kSaoMaxOff) enc_.encode_bypass(0);
+      }
+      if (t == 1) {
+        for (int i = 0; i < 4; ++i)
+          if (sao_offset(p[c], i)) enc_.encode_bypass(sao_offset(p[c], i) < 0);
+        enc_.encode_bypass_bins((uint32_t)sao_class(p[c]), 5);  // sao_band_position
+      } else if (c < 2) {
+        enc_.encode_bypass_bins((uint32_t)sao_class(p[c]), 2);  // sao_eo_class_luma / _chroma
+      }
+    }
   }
 
   void quadtree(int x0, int y0, int log2, int depth) {

@@ -117,7 +117,12 @@ class Engine {
     HIP_OK(hipMalloc(&count_scratch_, B * nctu_ * sizeof(int)));
     cap_ = g_.ysz + 2 * g_.csz;
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
-    slot_bytes_ = align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * nctu_ * 8) +
+    if (c.deblock & 2) {  // SAO reads the deblocked picture from a copy
+      HIP_OK(hipMalloc(&deb_.y, B * g_.ysz));
+      HIP_OK(hipMalloc(&deb_.u, B * g_.csz));
+      HIP_OK(hipMalloc(&deb_.v, B * g_.csz));
+    }
+    slot_bytes_ = align(B * nctu_ * 12) + align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * nctu_ * 8) +
                   align(B * nctu_ * 4) + align(B * nctu_ * 4) + align(B * 4) + align(B * cap_ * 2);
     for (int k = 0; k < kSlots; ++k) {
       Slot& s = slots_[k];
@@ -138,7 +143,8 @@ class Engine {
     seq_.width = c.width;
     seq_.height = c.height;
     seq_.qp = c.qp;
-    seq_.deblock = c.deblock != 0;
+    seq_.deblock = (c.deblock & 1) != 0;  // bit 0: deblocking, bit 1: SAO
+    seq_.sao = (c.deblock & 2) != 0;
     seq_.max_merge_cand = c.max_merge;
     seq_.finalize();
     pool_ = std::make_unique<ThreadPool>(c.threads, c.device);
@@ -147,7 +153,8 @@ class Engine {
   ~Engine() {
     pool_.reset();
     (void)hipStreamSynchronize(stream_);
-    for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u, rec_[1].v})
+    for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u, rec_[1].v,
+                    deb_.y, deb_.u, deb_.v})
       (void)hipFree(p);
     (void)hipFree(coef_y_);
     (void)hipFree(coef_u_);
@@ -216,6 +223,7 @@ class Engine {
     unsigned* mask_c;
     int *count, *offset, *total;
     int16_t* packed;
+    uint32_t* sao;
   };
   Parts carve(uint8_t* base) const {
     const long B = cfg_.batch, U = g_.usz;
@@ -236,6 +244,8 @@ class Engine {
     q += align(B * nctu_ * 4);
     p.total = reinterpret_cast<int*>(q);
     q += align(B * 4);
+    p.sao = reinterpret_cast<uint32_t*>(q);
+    q += align(B * nctu_ * 12);
     p.packed = reinterpret_cast<int16_t*>(q);
     p.count = nullptr;  // device count array lives in the scratch below
     return p;
@@ -251,6 +261,7 @@ class Engine {
     d.coef_y = coef_y_;
     d.coef_u = coef_u_;
     d.coef_v = coef_v_;
+    d.sao = p.sao;
     return d;
   }
   CompactSet slot_compact(const Slot& s) const {
@@ -285,6 +296,7 @@ class Engine {
     f.sb_offset = p.offset + (long)b * nctu_;
     f.sb_packed = p.packed + (long)b * cap_;
     f.wc = g_.wc;
+    f.sao = seq_.sao ? p.sao + (long)b * nctu_ * 3 : nullptr;
     return f;
   }
 
@@ -297,6 +309,7 @@ class Engine {
     const long U = g_.usz;
     HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
     HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
+    if (seq_.sao) HIP_OK(hipMemcpyAsync(h.sao, d.sao, B * nctu_ * 12, hipMemcpyDeviceToHost, ws));
     if (B == cfg_.batch) {  // full batch: the planes are contiguous, 2 copies cover them
       HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, B * U * 4, hipMemcpyDeviceToHost, ws));  // 4 u8 planes
       HIP_OK(hipMemcpyAsync(h.mask_y, d.mask_y, align(B * nctu_ * 8) + align(B * nctu_ * 4) + B * nctu_ * 4,
@@ -351,7 +364,8 @@ class Engine {
       if (f == 0) launch_intra_frame(src_, cur, dec, g_, cfg_.qp, pen_, B, stream_);
       else launch_inter_frame(src_, prev, phase_, cur, dec, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
       launch_compact(dec, g_, slot_compact(s), B, stream_);
-      if (cfg_.deblock) launch_deblock(cur, dec, g_, cfg_.qp, B, stream_);
+      if (seq_.deblock) launch_deblock(cur, dec, g_, cfg_.qp, B, stream_);
+      if (seq_.sao) launch_sao(src_, cur, deb_, dec, g_, cfg_.qp, B, stream_);
       if (f + 1 < F) launch_phase_planes(cur, phase_, g_, B, stream_);  // reference of f+1
       launch_sse(src_, cur, g_, d_sse_, B, stream_);
       HIP_OK(hipGetLastError());
@@ -403,7 +417,7 @@ class Engine {
   SeqConfig seq_;
   Penalties pen_{};
   hipStream_t stream_{};
-  FrameSet src_{}, rec_[2]{};
+  FrameSet src_{}, rec_[2]{}, deb_{};
   int16_t *coef_y_ = nullptr, *coef_u_ = nullptr, *coef_v_ = nullptr;
   unsigned long long* d_sse_ = nullptr;
   uint8_t* phase_ = nullptr;

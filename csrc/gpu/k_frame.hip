@@ -209,6 +209,64 @@ void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipS
   dim3 grid((g.W + 16 + 31) / 32, (g.H + 16 + 31) / 32, B);
   k_phase_planes<<<grid, 256, 0, s>>>(ref, phase, g);
 }
+// ---------------------------------------- SAO ------------------------------------------
+// One block per CTB: the three components' statistics are accumulated with LDS atomics
+// (band + 4 EO classes per sample), then one lane runs the shared integer RD decision
+// (tv::sao_decide, identical to the CPU golden model).
+__global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, DecisionSet dec, Geo g,
+                                                    long long lam16) {
+  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int cx = ctu % g.wc, cy = ctu / g.wc;
+  __shared__ SaoStats st[3];
+  for (int i = tid; i < 3 * (int)(sizeof(SaoStats) / 4); i += 256) reinterpret_cast<int*>(st)[i] = 0;
+  __syncthreads();
+  // 1024 luma + 2 x 256 chroma samples: 6 per thread
+  for (int i = tid; i < 1536; i += 256) {
+    const int c = i < 1024 ? 0 : (i < 1280 ? 1 : 2);
+    const int j = c == 0 ? i : (i - 1024 - (c - 1) * 256);
+    const int n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
+    const int x = cx * n + j % n, y = cy * n + j / n;
+    const uint8_t* D = deb.plane(c, b, g);
+    const int v = D[y * w + x], diff = (int)src.plane(c, b, g)[y * w + x] - v;
+    atomicAdd(&st[c].bo_n[v >> 3], 1);
+    atomicAdd(&st[c].bo_s[v >> 3], diff);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      int dx, dy;
+      sao_eo_dir(k, dx, dy);
+      const int ax = x + dx, ay = y + dy, bx = x - dx, by = y - dy;
+      if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= w || ay >= h || bx >= w || by >= h) continue;
+      const int cat = sao_eo_category(v, D[ay * w + ax], D[by * w + bx]);
+      atomicAdd(&st[c].eo_n[k][cat], 1);
+      atomicAdd(&st[c].eo_s[k][cat], diff);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) sao_decide(st, lam16, dec.sao + 3 * ((long)b * g.wc * g.hc + ctu));
+}
+
+__global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet rec, DecisionSet dec, Geo g) {
+  const int b = blockIdx.y;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long ny = g.ysz, nc = g.csz;
+  if (i >= ny + 2 * nc) return;
+  const int c = i < ny ? 0 : (i < ny + nc ? 1 : 2);
+  const long j = c == 0 ? i : i - ny - (c - 1) * nc;
+  const int w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H, n = c ? 16 : 32;
+  const int x = (int)(j % w), y = (int)(j / w);
+  const uint32_t p = dec.sao[3 * ((long)b * g.wc * g.hc + (y / n) * g.wc + x / n) + c];
+  if (sao_type(p)) rec.plane(c, b, g)[j] = (uint8_t)sao_sample(deb.plane(c, b, g), w, h, x, y, p);
+}
+
+void launch_sao(FrameSet src, FrameSet rec, FrameSet deb, DecisionSet dec, const Geo& g, int qp, int B,
+                hipStream_t s) {
+  (void)hipMemcpyAsync(deb.y, rec.y, B * g.ysz, hipMemcpyDeviceToDevice, s);
+  (void)hipMemcpyAsync(deb.u, rec.u, B * g.csz, hipMemcpyDeviceToDevice, s);
+  (void)hipMemcpyAsync(deb.v, rec.v, B * g.csz, hipMemcpyDeviceToDevice, s);
+  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, dec, g, sao_lambda16(qp));
+  k_sao_apply<<<dim3((unsigned)((g.ysz + 2 * g.csz + 255) / 256), B), 256, 0, s>>>(deb, rec, dec, g);
+}
+
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s) {
   dim3 grid((unsigned)tv_min(1024, (int)(g.ysz / 32 / 256 + 1)), B);
   k_deblock<<<grid, 256, 0, s>>>(rec, dec, g, qp, 0);

@@ -53,6 +53,8 @@ struct FrameData {
   const int32_t* sb_offset = nullptr;
   const int16_t* sb_packed = nullptr;
   int wc = 0;  // CTBs per row
+  // SAO parameters, 3 packed words (Y, Cb, Cr) per CTB in raster order (nullptr: SAO off)
+  const uint32_t* sao = nullptr;
 };
 
 // Owning storage for one frame's decisions (CPU side).
@@ -60,7 +62,9 @@ struct FrameDecisions {
   int w8 = 0, h8 = 0, cw = 0, ch = 0;
   std::vector<uint8_t> cu_log2, intra, ipm, cbf;
   std::vector<int16_t> mv, coef_y, coef_u, coef_v;
+  std::vector<uint32_t> sao;  // 3 per CTB
   void alloc(int coded_w, int coded_h) {
+    sao.assign(3 * (size_t)(coded_w >> kCtbLog2) * (coded_h >> kCtbLog2), sao_off_param());
     cw = coded_w;
     ch = coded_h;
     w8 = coded_w >> 3;
@@ -87,6 +91,8 @@ struct FrameDecisions {
     f.coef[0] = coef_y.data();
     f.coef[1] = coef_u.data();
     f.coef[2] = coef_v.data();
+    f.sao = sao.data();
+    f.wc = cw >> kCtbLog2;
     return f;
   }
 };
@@ -126,6 +132,12 @@ void recon_tb(const int16_t* levels, int ls, bool cbf, int log2N, int qp, const 
               uint8_t* dst, int ds);
 // In-loop deblocking of a reconstructed picture given the frame decisions.
 void deblock_picture(Picture& pic, const FrameData& fd, int qp);
+// SAO statistics of CTB (cx, cy), component c: source vs deblocked picture.
+void sao_ctb_stats(const Picture& src, const Picture& deb, int c, int cx, int cy, SaoStats& st);
+// Encoder: decide per-CTB SAO parameters (3 per CTB) for a deblocked picture.
+void sao_decide_picture(const Picture& src, const Picture& deb, int qp, uint32_t* params);
+// Apply SAO in place (uses an internal copy of the deblocked samples).
+void sao_picture(Picture& pic, const uint32_t* params);
 
 // derived chroma intra mode for intra_chroma_pred_mode idx (4 = DM)
 inline int chroma_intra_mode(int chroma_idx, int luma_mode) {

@@ -8,6 +8,7 @@
 // HEVC encoder (SURVEY.md §2.3 K5a–K5h).  Tables are transcribed from ITU-T H.265.
 #pragma once
 #include <cstdint>
+#include <cmath>
 #include <cstdlib>
 
 #if defined(__HIPCC__)
@@ -527,6 +528,154 @@ TV_HD bool zscan_available(int xC, int yC, int xN, int yN, int picW, int picH) {
   const int zN = zorder4((xN & (kCtb - 1)) >> 2, (yN & (kCtb - 1)) >> 2);
   const int zC = zorder4((xC & (kCtb - 1)) >> 2, (yC & (kCtb - 1)) >> 2);
   return zN <= zC;
+}
+
+// ------------------------------------------------------------------------------ SAO
+// Sample adaptive offset (H.265 7.3.8.3 / 8.7.3), 8-bit.  One CTB/component parameter set
+// is packed in 32 bits: type (0 off, 1 band, 2 edge) | class (EO class or band position)
+// << 2 | (offset[i] + 8) << (7 + 4 i), offsets in [-7, 7] with the EO sign convention
+// (categories 1, 2 >= 0; 3, 4 <= 0) already applied.  Encoder decisions are integer RD so
+// the CPU golden model and the GPU kernels choose identical parameters.
+constexpr int kSaoMaxOff = 7;  // (1 << (Min(bitDepth, 10) - 5)) - 1
+TV_HD uint32_t sao_pack(int type, int cls, const int* off) {
+  uint32_t p = (uint32_t)type | ((uint32_t)cls << 2);
+  for (int i = 0; i < 4; ++i) p |= (uint32_t)(off[i] + 8) << (7 + 4 * i);
+  return p;
+}
+TV_HD int sao_type(uint32_t p) { return (int)(p & 3); }
+TV_HD int sao_class(uint32_t p) { return (int)((p >> 2) & 31); }
+TV_HD int sao_offset(uint32_t p, int i) { return (int)((p >> (7 + 4 * i)) & 15) - 8; }
+TV_HD uint32_t sao_off_param() {
+  const int z[4] = {0, 0, 0, 0};
+  return sao_pack(0, 0, z);
+}
+// neighbour displacement of EO class c: (dx, dy) of sample a; sample b is the mirror
+TV_HD void sao_eo_dir(int c, int& dx, int& dy) {
+  dx = c == 1 ? 0 : (c == 3 ? 1 : -1);
+  dy = c == 0 ? 0 : -1;
+}
+// EO category (0 = none, 1 local min .. 4 local max) of p against neighbours a, b
+TV_HD int sao_eo_category(int p, int a, int b) {
+  const int e = 2 + (p > a) - (p < a) + (p > b) - (p < b);
+  return e == 2 ? 0 : (e < 2 ? e + 1 : e);
+}
+// one SAO'd sample.  x, y: component coordinates; src: deblocked plane (w x h).
+TV_HD int sao_sample(const uint8_t* src, int w, int h, int x, int y, uint32_t p) {
+  const int v = src[y * w + x];
+  const int t = sao_type(p);
+  if (t == 1) {
+    const int k = ((v >> 3) - sao_class(p)) & 31;
+    return k < 4 ? clip_pixel(v + sao_offset(p, k)) : v;
+  }
+  if (t == 2) {
+    int dx, dy;
+    sao_eo_dir(sao_class(p), dx, dy);
+    const int ax = x + dx, ay = y + dy, bx = x - dx, by = y - dy;
+    if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= w || ay >= h || bx >= w || by >= h) return v;
+    const int c = sao_eo_category(v, src[ay * w + ax], src[by * w + bx]);
+    return c ? clip_pixel(v + sao_offset(p, c - 1)) : v;
+  }
+  return v;
+}
+
+// Statistics of one CTB component: count and sum(orig - deblocked) per EO class/category
+// and per band.
+struct SaoStats {
+  int eo_n[4][5], eo_s[4][5];
+  int bo_n[32], bo_s[32];
+};
+TV_HD int sao_tr_bits(int a) { return a < kSaoMaxOff ? a + 1 : kSaoMaxOff; }
+// best offset for one category given (n, s): minimises 16*dSSE + lam16*bits; sign_lo/hi
+// bound the allowed range; `sign_bit` adds one bit for non-zero values (band offsets).
+TV_HD long long sao_best_offset(int n, int s, int lo, int hi, long long lam16, bool sign_bit, int& best) {
+  best = 0;
+  long long bj = lam16 * sao_tr_bits(0);
+  if (n == 0) return bj;
+  int o = (2 * s + (s >= 0 ? n : -n)) / (2 * n);  // round(s / n)
+  o = o < lo ? lo : (o > hi ? hi : o);
+  const int step = o > 0 ? -1 : 1;
+  for (int v = o; v != 0; v += step) {
+    const long long dd = (long long)n * v * v - 2LL * v * s;
+    const long long j = 16 * dd + lam16 * (sao_tr_bits(v < 0 ? -v : v) + (sign_bit ? 1 : 0));
+    if (j < bj) {
+      bj = j;
+      best = v;
+    }
+  }
+  return bj;
+}
+// EO cost of class c for one component; fills off[4]
+TV_HD long long sao_eo_cost(const SaoStats& st, int c, long long lam16, int* off) {
+  long long j = 0;
+  for (int k = 0; k < 4; ++k) {
+    const bool pos = k < 2;
+    j += sao_best_offset(st.eo_n[c][k + 1], st.eo_s[c][k + 1], pos ? 0 : -kSaoMaxOff, pos ? kSaoMaxOff : 0, lam16,
+                         false, off[k]);
+  }
+  return j;
+}
+// BO cost (best band position) for one component; fills pos, off[4]
+TV_HD long long sao_bo_cost(const SaoStats& st, long long lam16, int& pos, int* off) {
+  long long cj[32];
+  int co[32];
+  for (int b = 0; b < 32; ++b)
+    cj[b] = sao_best_offset(st.bo_n[b], st.bo_s[b], -kSaoMaxOff, kSaoMaxOff, lam16, true, co[b]);
+  long long best = 0;
+  pos = 0;
+  for (int p = 0; p < 32; ++p) {
+    long long j = 0;
+    for (int k = 0; k < 4; ++k) j += cj[(p + k) & 31];
+    if (p == 0 || j < best) {
+      best = j;
+      pos = p;
+    }
+  }
+  for (int k = 0; k < 4; ++k) off[k] = co[(pos + k) & 31];
+  return best + lam16 * 5;  // sao_band_position
+}
+// Decide luma (st[0]) and chroma (st[1], st[2]: shared type and EO class) parameters.
+// Rate in bits: type TR bins (off 1, band 2, edge 2), EO class 2, band position 5, offsets.
+TV_HD void sao_decide(const SaoStats* st, long long lam16, uint32_t* out) {
+  int off[4], bo[4], pos;
+  // luma
+  {
+    long long best = lam16 * 1;
+    out[0] = sao_off_param();
+    for (int c = 0; c < 4; ++c) {
+      const long long j = sao_eo_cost(st[0], c, lam16, off) + lam16 * 4;
+      if (j < best) {
+        best = j;
+        out[0] = sao_pack(2, c, off);
+      }
+    }
+    const long long jb = sao_bo_cost(st[0], lam16, pos, bo) + lam16 * 2;
+    if (jb < best) out[0] = sao_pack(1, pos, bo);
+  }
+  // chroma: one type (and EO class) for Cb and Cr
+  {
+    long long best = lam16 * 1;
+    out[1] = out[2] = sao_off_param();
+    for (int c = 0; c < 4; ++c) {
+      int o1[4], o2[4];
+      const long long j = sao_eo_cost(st[1], c, lam16, o1) + sao_eo_cost(st[2], c, lam16, o2) + lam16 * 4;
+      if (j < best) {
+        best = j;
+        out[1] = sao_pack(2, c, o1);
+        out[2] = sao_pack(2, c, o2);
+      }
+    }
+    int p1, p2, b1[4], b2[4];
+    const long long jb = sao_bo_cost(st[1], lam16, p1, b1) + sao_bo_cost(st[2], lam16, p2, b2) + lam16 * 2;
+    if (jb < best) {
+      out[1] = sao_pack(1, p1, b1);
+      out[2] = sao_pack(1, p2, b2);
+    }
+  }
+}
+// lambda for SSE-domain decisions in 1/16 units (lam_sse = lam_sad^2)
+inline long long sao_lambda16(int qp) {
+  const double l = 0.57 * std::pow(2.0, (qp - 12) / 3.0);
+  return (long long)(l * 16.0);
 }
 
 }  // namespace tv

@@ -68,3 +68,23 @@ def test_write_frame_from_decisions_matches_encoder():
     np.testing.assert_array_equal(cbf, dec["cbf"])
     out2 = hevc.write_frame(96, 64, 27, True, 0, dec, coef)
     assert out2 == out
+
+
+@pytest.mark.parametrize("qp,deblock", [(32, True), (22, True), (27, False)])
+def test_sao_roundtrip_and_gain(qp, deblock):
+    """SAO (edge/band offsets, merges, chroma-shared type): the oracle decoder reproduces the
+    encoder's in-loop reconstruction exactly, and SAO does not lower PSNR."""
+    frames = _frames(4, 6, 192, 128)
+    res = {}
+    for sao in (False, True):
+        enc = hevc.CpuEncoder(192, 128, qp=qp, deblock=deblock, sao=sao, search_range=8)
+        bs, recons = b"", []
+        for i, f in enumerate(frames):
+            bs += enc.encode(f, i == 0, i)
+            recons.append(enc.recon())
+        d = hevc.decode(bs)
+        for r, c in zip(recons, d.coded_frames):
+            for p in range(3):
+                np.testing.assert_array_equal(r[p], c[p])
+        res[sao] = np.mean([hevc.psnr(a[0], b[0]) for a, b in zip(frames, d.frames)])
+    assert res[True] >= res[False] - 0.01

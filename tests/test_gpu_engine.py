@@ -13,14 +13,16 @@ def _engine(**kw):
     return GpuEngine(**kw)
 
 
-@pytest.mark.parametrize("w,h,qp,deblock", [(192, 128, 27, True), (160, 90, 32, True), (128, 64, 22, False)])
-def test_gpu_bitstream_equals_cpu_reference(w, h, qp, deblock):
+@pytest.mark.parametrize("w,h,qp,deblock,sao", [(192, 128, 27, True, False), (160, 90, 32, True, False),
+                                                (128, 64, 22, False, False), (192, 128, 30, True, True),
+                                                (160, 90, 24, False, True)])
+def test_gpu_bitstream_equals_cpu_reference(w, h, qp, deblock, sao):
     gop, rng = 4, 8
-    eng = _engine(width=w, height=h, qp=qp, batch=2, gop=gop, search_range=rng, deblock=deblock, seed=5)
+    eng = _engine(width=w, height=h, qp=qp, batch=2, gop=gop, search_range=rng, deblock=deblock, sao=sao, seed=5)
     segs = eng.encode_synthetic([0, 10])
     for b, start in enumerate([0, 10]):
         frames = [hevc.synth_frame(5, start + f, w, h) for f in range(gop)]
-        cpu_bs, recons = hevc.encode_sequence_cpu(frames, qp=qp, deblock=deblock, search_range=rng)
+        cpu_bs, recons = hevc.encode_sequence_cpu(frames, qp=qp, deblock=deblock, sao=sao, search_range=rng)
         assert segs[b] == cpu_bs, f"segment {b}: GPU bitstream differs from CPU golden model"
         d = hevc.decode(segs[b])
         gy, gu, gv = eng.last_recon(b)

@@ -56,14 +56,16 @@ def default_threads() -> int:
 
 class GpuEngine:
     def __init__(self, width: int, height: int, qp: int = 27, batch: int = 8, gop: int = 16,
-                 search_range: int = 16, deblock: bool = True, seed: int = 1, threads: int | None = None,
+                 search_range: int = 16, deblock: bool = True, sao: bool = False, seed: int = 1,
+                 threads: int | None = None,
                  device: int = 0, max_merge: int = 5):
         self.lib = _lib()
         self.width, self.height, self.qp = width, height, qp
         self.batch, self.gop = batch, gop
         self.cw, self.ch = coded_size(width, height)
         self.threads = threads or default_threads()
-        self.h = self.lib.tv_engine_new(width, height, qp, batch, gop, search_range, int(deblock),
+        self.sao = sao
+        self.h = self.lib.tv_engine_new(width, height, qp, batch, gop, search_range, int(deblock) | (2 if sao else 0),
                                         seed & 0xFFFFFFFF, self.threads, device, max_merge)
         if not self.h:
             raise RuntimeError("GPU engine init failed: " + self.lib.tv_gpu_last_error().decode())

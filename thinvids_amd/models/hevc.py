@@ -42,13 +42,14 @@ class CpuEncoder:
     """Scalar C++ HEVC encoder (software path; reference `software_encode`)."""
 
     def __init__(self, width: int, height: int, qp: int = 27, deblock: bool = True,
-                 search_range: int = 8, max_merge: int = 5):
+                 search_range: int = 8, max_merge: int = 5, sao: bool = False):
         if width % 2 or height % 2:
             raise ValueError("width/height must be even")
         self.lib = core_lib()
         self.width, self.height, self.qp = width, height, qp
         self.cw, self.ch = coded_size(width, height)
-        self.h = self.lib.tv_cpu_encoder_new(width, height, qp, int(deblock), search_range, max_merge)
+        self.h = self.lib.tv_cpu_encoder_new(width, height, qp, int(deblock) | (2 if sao else 0), search_range,
+                                             max_merge)
         self.out = Bytes()
 
     def __del__(self):

@@ -33,10 +33,11 @@ class EncodeSpec:
     gop: int = 64
     search_range: int = 16
     deblock: bool = True
+    sao: bool = False
     software: bool = False
 
     def engine_key(self):
-        return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock)
+        return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao)
 
 
 class EngineCache:
@@ -61,7 +62,8 @@ class EngineCache:
                     old = self._order.pop(0)
                     self._engines.pop(old).close()
                 eng = GpuEngine(spec.width, spec.height, qp=spec.qp, batch=self.batch, gop=spec.gop,
-                                search_range=spec.search_range, deblock=spec.deblock, device=self.device)
+                                search_range=spec.search_range, deblock=spec.deblock, sao=spec.sao,
+                                device=self.device)
                 eng.lock = threading.Lock()
                 self._engines[key] = eng
                 self._order.append(key)
@@ -110,7 +112,8 @@ def encode_parts(parts: list[list], spec: EncodeSpec, cache: EngineCache | None 
     if spec.software or not gpu_available():
         if not spec.software:
             raise RuntimeError("no GPU available for a hardware encode (set software_encode for the CPU path)")
-        return [hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock)[0]
+        return [hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock,
+                                           sao=spec.sao)[0]
                 for frames in parts]
     eng = (cache or default_cache()).get(spec)
     # (part, chunk index, frames) grouped by chunk length
