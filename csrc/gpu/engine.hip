@@ -361,13 +361,28 @@ class Engine {
       const DecisionSet dec = slot_dec(s);
       upload(f, B);
       FrameSet cur = rec_[f & 1], prev = rec_[(f + 1) & 1];
+      // TV_SYNC_DEBUG=1: synchronise and check after every stage (fault isolation)
+      auto stage = [&](const char* name) {
+        if (!sync_debug_) return;
+        const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(stream_);
+        if (e1 != hipSuccess || e2 != hipSuccess)
+          throw std::runtime_error(std::string("stage ") + name + " failed: " +
+                                   hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+      };
+      stage("upload");
       if (f == 0) launch_intra_frame(src_, cur, dec, g_, cfg_.qp, pen_, B, stream_);
       else launch_inter_frame(src_, prev, phase_, cur, dec, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
+      stage(f == 0 ? "intra" : "inter");
       launch_compact(dec, g_, slot_compact(s), B, stream_);
+      stage("compact");
       if (seq_.deblock) launch_deblock(cur, dec, g_, cfg_.qp, B, stream_);
+      stage("deblock");
       if (seq_.sao) launch_sao(src_, cur, deb_, dec, g_, cfg_.qp, B, stream_);
+      stage("sao");
       if (f + 1 < F) launch_phase_planes(cur, phase_, g_, B, stream_);  // reference of f+1
+      stage("phase_planes");
       launch_sse(src_, cur, g_, d_sse_, B, stream_);
+      stage("sse");
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(s.ev, stream_));
       s.pending.store(B + 1, std::memory_order_release);
@@ -424,6 +439,10 @@ class Engine {
   void* count_scratch_ = nullptr;
   int nctu_ = 0;
   int last_frames_ = 1;
+  const bool sync_debug_ = [] {
+    const char* e = getenv("TV_SYNC_DEBUG");
+    return e && *e == '1';
+  }();
   long cap_ = 0;
   Slot slots_[kSlots];
   long slot_bytes_ = 0;

@@ -1,9 +1,8 @@
 """Debug: per-chunk PSNR of the batched worker encode path."""
-import numpy as np
 from thinvids_amd.models import hevc
 from thinvids_amd.models.gpu_engine import GpuEngine
 
-frames = [hevc.synth_frame(5, t, 192, 128) for t in range(21)]
+frames = [hevc.synth_frame(5, t, 192, 128) for t in range(40)]
 for batch, nseg, n in ((4, 3, 8), (4, 1, 8), (1, 1, 8), (4, 2, 5), (2, 2, 8)):
     eng = GpuEngine(192, 128, qp=30, batch=batch, gop=8, search_range=16)
     segs = [frames[8 * i:8 * i + n] for i in range(nseg)]
