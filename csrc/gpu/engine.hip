@@ -261,7 +261,6 @@ class Engine {
     d.coef_y = coef_y_;
     d.coef_u = coef_u_;
     d.coef_v = coef_v_;
-    d.sao = p.sao;
     return d;
   }
   CompactSet slot_compact(const Slot& s) const {
@@ -377,7 +376,7 @@ class Engine {
       stage("compact");
       if (seq_.deblock) launch_deblock(cur, dec, g_, cfg_.qp, B, stream_);
       stage("deblock");
-      if (seq_.sao) launch_sao(src_, cur, deb_, dec, g_, cfg_.qp, B, stream_);
+      if (seq_.sao) launch_sao(src_, cur, deb_, carve(s.dev).sao, g_, cfg_.qp, B, stream_);
       stage("sao");
       if (f + 1 < F) launch_phase_planes(cur, phase_, g_, B, stream_);  // reference of f+1
       stage("phase_planes");

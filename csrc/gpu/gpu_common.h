@@ -60,7 +60,6 @@ struct DecisionSet {
   int16_t* coef_y;
   int16_t* coef_u;
   int16_t* coef_v;
-  uint32_t* sao;  // 3 packed SAO parameter words per CTB (B x nctu x 3)
 };
 
 __device__ __forceinline__ int wave_sum(int v) {

@@ -29,9 +29,9 @@ void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameS
 // 16 quarter-pel phase planes (B x 16 x psz bytes) of the luma reference
 void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipStream_t s);
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s);
-// SAO: per-CTB statistics (source vs deblocked) + RD decision into dec.sao, then the
-// filter from the deblocked copy `deb` into `rec`.
-void launch_sao(FrameSet src, FrameSet rec, FrameSet deb, DecisionSet dec, const Geo& g, int qp, int B,
+// SAO: per-CTB statistics (source vs deblocked) + RD decision into `sao` (3 packed words per
+// CTB, B x nctu x 3), then the filter from the deblocked copy `deb` into `rec`.
+void launch_sao(FrameSet src, FrameSet rec, FrameSet deb, uint32_t* sao, const Geo& g, int qp, int B,
                 hipStream_t s);
 
 // Compact (non-zero 4x4 groups only) level representation for the D2H transfer.

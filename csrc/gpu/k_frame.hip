@@ -213,7 +213,7 @@ void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipS
 // One block per CTB: the three components' statistics are accumulated with LDS atomics
 // (band + 4 EO classes per sample), then one lane runs the shared integer RD decision
 // (tv::sao_decide, identical to the CPU golden model).
-__global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, DecisionSet dec, Geo g,
+__global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, uint32_t* sao, Geo g,
                                                     long long lam16) {
   const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int cx = ctu % g.wc, cy = ctu / g.wc;
@@ -242,10 +242,10 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
     }
   }
   __syncthreads();
-  if (tid == 0) sao_decide(st, lam16, dec.sao + 3 * ((long)b * g.wc * g.hc + ctu));
+  if (tid == 0) sao_decide(st, lam16, sao + 3 * ((long)b * g.wc * g.hc + ctu));
 }
 
-__global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet rec, DecisionSet dec, Geo g) {
+__global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet rec, const uint32_t* sao, Geo g) {
   const int b = blockIdx.y;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   const long ny = g.ysz, nc = g.csz;
@@ -254,17 +254,17 @@ __global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet rec, D
   const long j = c == 0 ? i : i - ny - (c - 1) * nc;
   const int w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H, n = c ? 16 : 32;
   const int x = (int)(j % w), y = (int)(j / w);
-  const uint32_t p = dec.sao[3 * ((long)b * g.wc * g.hc + (y / n) * g.wc + x / n) + c];
+  const uint32_t p = sao[3 * ((long)b * g.wc * g.hc + (y / n) * g.wc + x / n) + c];
   if (sao_type(p)) rec.plane(c, b, g)[j] = (uint8_t)sao_sample(deb.plane(c, b, g), w, h, x, y, p);
 }
 
-void launch_sao(FrameSet src, FrameSet rec, FrameSet deb, DecisionSet dec, const Geo& g, int qp, int B,
+void launch_sao(FrameSet src, FrameSet rec, FrameSet deb, uint32_t* sao, const Geo& g, int qp, int B,
                 hipStream_t s) {
   (void)hipMemcpyAsync(deb.y, rec.y, B * g.ysz, hipMemcpyDeviceToDevice, s);
   (void)hipMemcpyAsync(deb.u, rec.u, B * g.csz, hipMemcpyDeviceToDevice, s);
   (void)hipMemcpyAsync(deb.v, rec.v, B * g.csz, hipMemcpyDeviceToDevice, s);
-  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, dec, g, sao_lambda16(qp));
-  k_sao_apply<<<dim3((unsigned)((g.ysz + 2 * g.csz + 255) / 256), B), 256, 0, s>>>(deb, rec, dec, g);
+  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, sao, g, sao_lambda16(qp));
+  k_sao_apply<<<dim3((unsigned)((g.ysz + 2 * g.csz + 255) / 256), B), 256, 0, s>>>(deb, rec, sao, g);
 }
 
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s) {
