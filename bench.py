@@ -35,6 +35,7 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=0, help="segments per GPU per step (0 = auto)")
     ap.add_argument("--gop", type=int, default=16, help="frames per GOP-aligned segment")
     ap.add_argument("--qp", type=int, default=27)
+    ap.add_argument("--sao", action="store_true", help="enable SAO (in-loop sample adaptive offset)")
     ap.add_argument("--range", type=int, default=16)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)
@@ -59,7 +60,7 @@ def main() -> None:
 
     w, h = RES[args.res]
     batch = args.batch or (8 if args.res in ("1080p", "720p", "360p") else 4)
-    eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range,
+    eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=args.sao,
                     seed=args.seed, threads=args.threads or None, device=local)
 
     prof = {"encode": 0.0, "post": 0.0}
@@ -126,7 +127,7 @@ def main() -> None:
             "dtype": "uint8 video / int32 integer transforms (bit-exact HEVC)",
             "data": "synthetic (seeded procedural YUV 4:2:0 source generated on GPU)",
             "config": {
-                "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic",
+                "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else ""),
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",

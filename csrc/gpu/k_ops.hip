@@ -120,17 +120,17 @@ __global__ void k_p010_to_i420(const uint16_t* __restrict__ y16, const uint16_t*
 // --------------------------------------------------------------- HDR10 tone-map
 __device__ __forceinline__ float pq_eotf(float e) {  // -> linear, 1.0 = 10000 nits
   const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
-  const float p = __powf(fmaxf(e, 0.f), 1.f / m2);
-  return __powf(fmaxf(p - c1, 0.f) / (c2 - c3 * p), 1.f / m1);
+  const float p = powf(fmaxf(e, 0.f), 1.f / m2);
+  return powf(fmaxf(p - c1, 0.f) / (c2 - c3 * p), 1.f / m1);
 }
 __device__ __forceinline__ float pq_oetf(float l) {
   const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
-  const float p = __powf(fmaxf(l, 0.f), m1);
-  return __powf((c1 + c2 * p) / (1.f + c3 * p), m2);
+  const float p = powf(fmaxf(l, 0.f), m1);
+  return powf((c1 + c2 * p) / (1.f + c3 * p), m2);
 }
 __device__ __forceinline__ float bt709_oetf(float l) {
   l = fminf(fmaxf(l, 0.f), 1.f);
-  return l < 0.018f ? 4.5f * l : 1.099f * __powf(l, 0.45f) - 0.099f;
+  return l < 0.018f ? 4.5f * l : 1.099f * powf(l, 0.45f) - 0.099f;
 }
 // BT.2390 EETF on PQ-encoded luminance: source peak src_pq, target peak dst_pq
 __device__ __forceinline__ float eetf(float e, float src_pq, float dst_pq) {
@@ -166,7 +166,7 @@ __global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* _
       // tone-map on max(R,G,B) in the PQ domain, scale linear RGB by the luminance ratio
       const float mx = fmaxf(fmaxf(r, g), fmaxf(b, 1e-6f));
       const float lm = pq_eotf(mx), lt = pq_eotf(eetf(mx, src_pq, dst_pq));
-      const float sc = lm > 0.f ? lt / lm : 0.f;
+      const float sc = lm > 1e-6f ? lt / lm : 0.f;  // near-black: no ratio blow-up
       const float norm = 10000.f / dst_peak_nits;  // target peak -> 1.0
       const float R = pq_eotf(r) * sc * norm, G = pq_eotf(g) * sc * norm, B = pq_eotf(b) * sc * norm;
       // BT.2020 -> BT.709 primaries (linear)

@@ -78,7 +78,7 @@ def tonemap_pq_ref(y16: np.ndarray, uv16: np.ndarray, src_peak: float = 1000.0, 
     src_pq, dst_pq = pq_oetf(src_peak / 10000.0), pq_oetf(dst_peak / 10000.0)
     mx = np.maximum(np.maximum(r, g), np.maximum(b, 1e-6))
     lm, lt = pq_eotf(mx), pq_eotf(_eetf(mx, src_pq, dst_pq))
-    sc = np.where(lm > 0, lt / np.where(lm > 0, lm, 1), 0.0) * (10000.0 / dst_peak)
+    sc = np.where(lm > 1e-6, lt / np.where(lm > 1e-6, lm, 1), 0.0) * (10000.0 / dst_peak)
     R, G, B = pq_eotf(r) * sc, pq_eotf(g) * sc, pq_eotf(b) * sc
     r7 = 1.6605 * R - 0.5876 * G - 0.0728 * B
     g7 = -0.1246 * R + 1.1329 * G - 0.0083 * B
