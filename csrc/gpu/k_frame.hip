@@ -241,8 +241,13 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       atomicAdd(&st[c].eo_s[k][cat], diff);
     }
   }
+  __shared__ SaoTables tab;
   __syncthreads();
-  if (tid == 0) sao_decide(st, lam16, sao + 3 * ((long)b * g.wc * g.hc + ctu));
+  if (tid < kSaoItems) sao_item(st, lam16, tid, tab);  // 144 offset/cost items in parallel
+  __syncthreads();
+  if (tid < 96) sao_window(tid, tab);  // 3 x 32 band windows
+  __syncthreads();
+  if (tid == 0) sao_finish(tab, lam16, sao + 3 * ((long)b * g.wc * g.hc + ctu));
 }
 
 __global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet rec, const uint32_t* sao, Geo g) {

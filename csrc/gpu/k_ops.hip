@@ -120,7 +120,7 @@ __global__ void k_p010_to_i420(const uint16_t* __restrict__ y16, const uint16_t*
 // --------------------------------------------------------------- HDR10 tone-map
 __device__ __forceinline__ float pq_eotf(float e) {  // -> linear, 1.0 = 10000 nits
   const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
-  const float p = powf(fmaxf(e, 0.f), 1.f / m2);
+  const float p = powf(fminf(fmaxf(e, 0.f), 1.f), 1.f / m2);  // PQ signal is in [0, 1]
   return powf(fmaxf(p - c1, 0.f) / (c2 - c3 * p), 1.f / m1);
 }
 __device__ __forceinline__ float pq_oetf(float l) {

@@ -604,73 +604,99 @@ TV_HD long long sao_best_offset(int n, int s, int lo, int hi, long long lam16, b
   }
   return bj;
 }
-// EO cost of class c for one component; fills off[4]
-TV_HD long long sao_eo_cost(const SaoStats& st, int c, long long lam16, int* off) {
+// The decision runs in three data-parallel phases so a GPU block can spread it over its
+// lanes while the CPU golden model runs the same steps in loops:
+//   1. 144 independent items: the best offset + cost of every (component, EO class,
+//      category) [3 x 16] and every (component, band) [3 x 32];
+//   2. for every component and band position, the cost of the 4-band window [3 x 32];
+//   3. the final choice per component (luma) / jointly for Cb+Cr (shared type + EO class).
+struct SaoTables {
+  long long eo_j[3][4][4];
+  long long bo_j[3][32];
+  long long win_j[3][32];
+  int8_t eo_o[3][4][4];
+  int8_t bo_o[3][32];
+};
+constexpr int kSaoItems = 3 * 48;
+TV_HD void sao_item(const SaoStats* st, long long lam16, int idx, SaoTables& t) {
+  const int c = idx / 48, r = idx % 48;
+  int o;
+  if (r < 16) {
+    const int cls = r >> 2, k = r & 3;
+    const bool pos = k < 2;  // categories 1, 2 >= 0; 3, 4 <= 0
+    t.eo_j[c][cls][k] = sao_best_offset(st[c].eo_n[cls][k + 1], st[c].eo_s[cls][k + 1], pos ? 0 : -kSaoMaxOff,
+                                        pos ? kSaoMaxOff : 0, lam16, false, o);
+    t.eo_o[c][cls][k] = (int8_t)o;
+  } else {
+    const int b = r - 16;
+    t.bo_j[c][b] = sao_best_offset(st[c].bo_n[b], st[c].bo_s[b], -kSaoMaxOff, kSaoMaxOff, lam16, true, o);
+    t.bo_o[c][b] = (int8_t)o;
+  }
+}
+TV_HD void sao_window(int idx, SaoTables& t) {  // idx in [0, 96)
+  const int c = idx / 32, p = idx % 32;
   long long j = 0;
-  for (int k = 0; k < 4; ++k) {
-    const bool pos = k < 2;
-    j += sao_best_offset(st.eo_n[c][k + 1], st.eo_s[c][k + 1], pos ? 0 : -kSaoMaxOff, pos ? kSaoMaxOff : 0, lam16,
-                         false, off[k]);
-  }
-  return j;
+  for (int k = 0; k < 4; ++k) j += t.bo_j[c][(p + k) & 31];
+  t.win_j[c][p] = j;
 }
-// BO cost (best band position) for one component; fills pos, off[4]
-TV_HD long long sao_bo_cost(const SaoStats& st, long long lam16, int& pos, int* off) {
-  long long cj[32];
-  int co[32];
-  for (int b = 0; b < 32; ++b)
-    cj[b] = sao_best_offset(st.bo_n[b], st.bo_s[b], -kSaoMaxOff, kSaoMaxOff, lam16, true, co[b]);
-  long long best = 0;
-  pos = 0;
-  for (int p = 0; p < 32; ++p) {
-    long long j = 0;
-    for (int k = 0; k < 4; ++k) j += cj[(p + k) & 31];
-    if (p == 0 || j < best) {
-      best = j;
-      pos = p;
-    }
-  }
-  for (int k = 0; k < 4; ++k) off[k] = co[(pos + k) & 31];
-  return best + lam16 * 5;  // sao_band_position
+TV_HD int sao_best_band(const SaoTables& t, int c) {
+  int best = 0;
+  for (int p = 1; p < 32; ++p)
+    if (t.win_j[c][p] < t.win_j[c][best]) best = p;
+  return best;
 }
-// Decide luma (st[0]) and chroma (st[1], st[2]: shared type and EO class) parameters.
+TV_HD uint32_t sao_pack_eo(const SaoTables& t, int c, int cls) {
+  int off[4];
+  for (int k = 0; k < 4; ++k) off[k] = t.eo_o[c][cls][k];
+  return sao_pack(2, cls, off);
+}
+TV_HD uint32_t sao_pack_bo(const SaoTables& t, int c, int pos) {
+  int off[4];
+  for (int k = 0; k < 4; ++k) off[k] = t.bo_o[c][(pos + k) & 31];
+  return sao_pack(1, pos, off);
+}
+TV_HD long long sao_eo_j(const SaoTables& t, int c, int cls) {
+  return t.eo_j[c][cls][0] + t.eo_j[c][cls][1] + t.eo_j[c][cls][2] + t.eo_j[c][cls][3];
+}
 // Rate in bits: type TR bins (off 1, band 2, edge 2), EO class 2, band position 5, offsets.
-TV_HD void sao_decide(const SaoStats* st, long long lam16, uint32_t* out) {
-  int off[4], bo[4], pos;
-  // luma
-  {
+TV_HD void sao_finish(const SaoTables& t, long long lam16, uint32_t* out) {
+  int pos[3];
+  for (int c = 0; c < 3; ++c) pos[c] = sao_best_band(t, c);
+  {  // luma
     long long best = lam16 * 1;
     out[0] = sao_off_param();
-    for (int c = 0; c < 4; ++c) {
-      const long long j = sao_eo_cost(st[0], c, lam16, off) + lam16 * 4;
+    for (int cls = 0; cls < 4; ++cls) {
+      const long long j = sao_eo_j(t, 0, cls) + lam16 * 4;
       if (j < best) {
         best = j;
-        out[0] = sao_pack(2, c, off);
+        out[0] = sao_pack_eo(t, 0, cls);
       }
     }
-    const long long jb = sao_bo_cost(st[0], lam16, pos, bo) + lam16 * 2;
-    if (jb < best) out[0] = sao_pack(1, pos, bo);
+    if (t.win_j[0][pos[0]] + lam16 * 7 < best) out[0] = sao_pack_bo(t, 0, pos[0]);
   }
-  // chroma: one type (and EO class) for Cb and Cr
-  {
+  {  // chroma: one type (and EO class) for Cb and Cr
     long long best = lam16 * 1;
     out[1] = out[2] = sao_off_param();
-    for (int c = 0; c < 4; ++c) {
-      int o1[4], o2[4];
-      const long long j = sao_eo_cost(st[1], c, lam16, o1) + sao_eo_cost(st[2], c, lam16, o2) + lam16 * 4;
+    for (int cls = 0; cls < 4; ++cls) {
+      const long long j = sao_eo_j(t, 1, cls) + sao_eo_j(t, 2, cls) + lam16 * 4;
       if (j < best) {
         best = j;
-        out[1] = sao_pack(2, c, o1);
-        out[2] = sao_pack(2, c, o2);
+        out[1] = sao_pack_eo(t, 1, cls);
+        out[2] = sao_pack_eo(t, 2, cls);
       }
     }
-    int p1, p2, b1[4], b2[4];
-    const long long jb = sao_bo_cost(st[1], lam16, p1, b1) + sao_bo_cost(st[2], lam16, p2, b2) + lam16 * 2;
-    if (jb < best) {
-      out[1] = sao_pack(1, p1, b1);
-      out[2] = sao_pack(1, p2, b2);
+    if (t.win_j[1][pos[1]] + t.win_j[2][pos[2]] + lam16 * 12 < best) {
+      out[1] = sao_pack_bo(t, 1, pos[1]);
+      out[2] = sao_pack_bo(t, 2, pos[2]);
     }
   }
+}
+// Sequential form of the three phases (CPU golden model).
+inline void sao_decide(const SaoStats* st, long long lam16, uint32_t* out) {
+  SaoTables t;
+  for (int i = 0; i < kSaoItems; ++i) sao_item(st, lam16, i, t);
+  for (int i = 0; i < 96; ++i) sao_window(i, t);
+  sao_finish(t, lam16, out);
 }
 // lambda for SSE-domain decisions in 1/16 units (lam_sse = lam_sad^2)
 inline long long sao_lambda16(int qp) {

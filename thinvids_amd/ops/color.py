@@ -44,7 +44,7 @@ _M1, _M2, _C1, _C2, _C3 = 0.1593017578125, 78.84375, 0.8359375, 18.8515625, 18.6
 
 
 def pq_eotf(e):
-    p = np.power(np.maximum(e, 0.0), 1.0 / _M2)
+    p = np.power(np.clip(e, 0.0, 1.0), 1.0 / _M2)
     return np.power(np.maximum(p - _C1, 0.0) / (_C2 - _C3 * p), 1.0 / _M1)
 
 
