@@ -62,18 +62,38 @@ struct DecisionSet {
   int16_t* coef_v;
 };
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// ---- wave-level data movement on the VALU (DPP) instead of LDS (ds_bpermute) ----------
+// A __shfl_xor is a ds_bpermute: an LDS round trip (~100+ cycles) per step, and reduction
+// chains of them serialise.  Within a 16-lane row DPP permutes are free operand modifiers;
+// the four row results are then combined with v_readlane (scalar).  Requires a full wave.
+namespace dpp {
+constexpr int kQuadXor1 = 0xB1;       // quad_perm [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;       // quad_perm [2,3,0,1]
+constexpr int kRowShl4 = 0x104, kRowShr4 = 0x114, kRowShl8 = 0x108, kRowShr8 = 0x118;
+constexpr int kRowHalfMirror = 0x141;  // lane i <- 7 - i within 8
+constexpr int kRowMirror = 0x140;      // lane i <- 15 - i within 16
+template <int CTRL> __device__ __forceinline__ int mov(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
 }
+}  // namespace dpp
+
+__device__ __forceinline__ int wave_sum(int v) {
+  v += dpp::mov<dpp::kQuadXor1>(v);
+  v += dpp::mov<dpp::kQuadXor2>(v);
+  v += dpp::mov<dpp::kRowHalfMirror>(v);
+  v += dpp::mov<dpp::kRowMirror>(v);  // every lane: its 16-lane row sum
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+__device__ __forceinline__ unsigned umin2(unsigned a, unsigned b) { return a < b ? a : b; }
 __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    unsigned w = __shfl_xor(v, o, 64);
-    v = w < v ? w : v;
-  }
-  return v;
+  v = umin2(v, (unsigned)dpp::mov<dpp::kQuadXor1>((int)v));
+  v = umin2(v, (unsigned)dpp::mov<dpp::kQuadXor2>((int)v));
+  v = umin2(v, (unsigned)dpp::mov<dpp::kRowHalfMirror>((int)v));
+  v = umin2(v, (unsigned)dpp::mov<dpp::kRowMirror>((int)v));
+  const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0), b = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
+  const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 32), d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+  return umin2(umin2(a, b), umin2(c, d));
 }
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll
@@ -88,9 +108,19 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 // Matches tv satd8x8 on the CPU: (sum |H d H| + 2) >> 2.
 __device__ __forceinline__ int wave_satd8x8(int d) {
   const int lane = threadIdx.x & 63;
+  // butterflies over x (lane bits 0..2) and the first y bit (lane bit 3) stay inside a
+  // 16-lane row: DPP.  Only the two cross-row stages (y bits 1, 2) use ds_bpermute.
+  int p = dpp::mov<dpp::kQuadXor1>(d);
+  d = (lane & 1) ? (p - d) : (d + p);
+  p = dpp::mov<dpp::kQuadXor2>(d);
+  d = (lane & 2) ? (p - d) : (d + p);
+  p = (lane & 4) ? dpp::mov<dpp::kRowShr4>(d) : dpp::mov<dpp::kRowShl4>(d);
+  d = (lane & 4) ? (p - d) : (d + p);
+  p = (lane & 8) ? dpp::mov<dpp::kRowShr8>(d) : dpp::mov<dpp::kRowShl8>(d);
+  d = (lane & 8) ? (p - d) : (d + p);
 #pragma unroll
-  for (int s = 1; s < 64; s <<= 1) {
-    const int p = __shfl_xor(d, s, 64);
+  for (int s = 16; s < 64; s <<= 1) {
+    p = __shfl_xor(d, s, 64);
     d = (lane & s) ? (p - d) : (d + p);
   }
   return (wave_sum(tv_abs(d)) + 2) >> 2;

@@ -237,8 +237,10 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       const int ax = x + dx, ay = y + dy, bx = x - dx, by = y - dy;
       if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= w || ay >= h || bx >= w || by >= h) continue;
       const int cat = sao_eo_category(v, D[ay * w + ax], D[by * w + bx]);
-      atomicAdd(&st[c].eo_n[k][cat], 1);
-      atomicAdd(&st[c].eo_s[k][cat], diff);
+      if (cat) {  // category 0 is never offset: skip its (heavily contended) counters
+        atomicAdd(&st[c].eo_n[k][cat], 1);
+        atomicAdd(&st[c].eo_s[k][cat], diff);
+      }
     }
   }
   __shared__ SaoTables tab;
