@@ -293,7 +293,9 @@ class Engine {
     f.sb_mask_y = reinterpret_cast<const uint64_t*>(p.mask_y + (long)b * nctu_);
     f.sb_mask_c = p.mask_c + (long)b * nctu_;
     f.sb_offset = p.offset + (long)b * nctu_;
-    f.sb_packed = p.packed + (long)b * cap_;
+    long base = 0;  // segments' packed levels are back to back
+    for (int k = 0; k < b; ++k) base += p.total[k];
+    f.sb_packed = p.packed + base * 16;
     f.wc = g_.wc;
     f.sao = seq_.sao ? p.sao + (long)b * nctu_ * 3 : nullptr;
     return f;
@@ -306,14 +308,16 @@ class Engine {
     HIP_OK(hipEventSynchronize(s.ev));
     const Parts d = carve(s.dev), h = carve(s.host);
     const long U = g_.usz;
-    HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
-    HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
-    if (seq_.sao) HIP_OK(hipMemcpyAsync(h.sao, d.sao, B * nctu_ * 12, hipMemcpyDeviceToHost, ws));
-    if (B == cfg_.batch) {  // full batch: the planes are contiguous, 2 copies cover them
-      HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, B * U * 4, hipMemcpyDeviceToHost, ws));  // 4 u8 planes
-      HIP_OK(hipMemcpyAsync(h.mask_y, d.mask_y, align(B * nctu_ * 8) + align(B * nctu_ * 4) + B * nctu_ * 4,
-                            hipMemcpyDeviceToHost, ws));  // mask_y | mask_c | offset
+    // Every D2H copy is a blit-kernel launch (~10 us of CU time each): the full-batch case
+    // moves the whole contiguous header (decision planes .. SAO params) in one copy and all
+    // segments' packed levels (back to back) in a second one.
+    if (B == cfg_.batch) {
+      const long head = reinterpret_cast<uint8_t*>(d.packed) - d.cu_log2;
+      HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, head, hipMemcpyDeviceToHost, ws));
     } else {  // partial batch: each plane is laid out for cfg_.batch segments
+      HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
+      HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
+      if (seq_.sao) HIP_OK(hipMemcpyAsync(h.sao, d.sao, B * nctu_ * 12, hipMemcpyDeviceToHost, ws));
       for (uint8_t* const* pl : {&h.cu_log2, &h.intra, &h.ipm, &h.cbf}) {
         const long off = *pl - h.cu_log2;
         HIP_OK(hipMemcpyAsync(*pl, d.cu_log2 + off, B * U, hipMemcpyDeviceToHost, ws));
@@ -323,13 +327,11 @@ class Engine {
       HIP_OK(hipMemcpyAsync(h.offset, d.offset, B * nctu_ * 4, hipMemcpyDeviceToHost, ws));
     }
     HIP_OK(hipStreamSynchronize(ws));
-    long bytes = 0;
-    for (int b = 0; b < B; ++b) {
-      const long n = (long)h.total[b] * 16 * 2;
-      if (n > cap_ * 2) throw std::runtime_error("compact level overflow");
-      if (n) HIP_OK(hipMemcpyAsync(h.packed + b * cap_, d.packed + b * cap_, n, hipMemcpyDeviceToHost, ws));
-      bytes += n;
-    }
+    long groups = 0;
+    for (int b = 0; b < B; ++b) groups += h.total[b];
+    const long bytes = groups * 16 * 2;
+    if (groups > (long)B * cap_ / 16) throw std::runtime_error("compact level overflow");
+    if (bytes) HIP_OK(hipMemcpyAsync(h.packed, d.packed, bytes, hipMemcpyDeviceToHost, ws));
     HIP_OK(hipStreamSynchronize(ws));
     coef_bytes_ += bytes;
   }

@@ -88,7 +88,10 @@ __global__ void __launch_bounds__(256) k_sb_pack(DecisionSet dec, Geo g, Compact
   const unsigned mc = cs.mask_c[i];
   const int ny = __popcll(my);
   const int n = ny + __popc(mc);
-  int16_t* out = cs.packed + (long)b * cs.cap + (long)cs.offset[i] * 16;
+  // segments are packed back to back (one device->host copy per frame for all of them)
+  long base = 0;
+  for (int k = 0; k < b; ++k) base += cs.total[k];
+  int16_t* out = cs.packed + (base + cs.offset[i]) * 16;
   for (int t = lane; t < n * 4; t += 64) {
     const int gidx = t >> 2, row = t & 3;
     const int16_t* src;
