@@ -77,6 +77,21 @@ template <int CTRL> __device__ __forceinline__ int mov(int v) {
 }
 }  // namespace dpp
 
+#ifdef TV_NO_DPP  // ds_bpermute reference implementations (debug builds)
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+#else
 __device__ __forceinline__ int wave_sum(int v) {
   v += dpp::mov<dpp::kQuadXor1>(v);
   v += dpp::mov<dpp::kQuadXor2>(v);
@@ -95,6 +110,7 @@ __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
   const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 32), d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
   return umin2(umin2(a, b), umin2(c, d));
 }
+#endif
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -108,16 +124,27 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 // Matches tv satd8x8 on the CPU: (sum |H d H| + 2) >> 2.
 __device__ __forceinline__ int wave_satd8x8(int d) {
   const int lane = threadIdx.x & 63;
+#ifdef TV_NO_DPP
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const int p = __shfl_xor(d, s, 64);
+    d = (lane & s) ? (p - d) : (d + p);
+  }
+  return (wave_sum(tv_abs(d)) + 2) >> 2;
+#endif
   // butterflies over x (lane bits 0..2) and the first y bit (lane bit 3) stay inside a
   // 16-lane row: DPP.  Only the two cross-row stages (y bits 1, 2) use ds_bpermute.
   int p = dpp::mov<dpp::kQuadXor1>(d);
   d = (lane & 1) ? (p - d) : (d + p);
   p = dpp::mov<dpp::kQuadXor2>(d);
   d = (lane & 2) ? (p - d) : (d + p);
-  p = (lane & 4) ? dpp::mov<dpp::kRowShr4>(d) : dpp::mov<dpp::kRowShl4>(d);
-  d = (lane & 4) ? (p - d) : (d + p);
-  p = (lane & 8) ? dpp::mov<dpp::kRowShr8>(d) : dpp::mov<dpp::kRowShl8>(d);
-  d = (lane & 8) ? (p - d) : (d + p);
+  // Both shifts are evaluated by the whole wave: a DPP op inside a divergent branch (which
+  // `c ? dpp_a : dpp_b` is, since the intrinsic is convergent) reads disabled lanes.
+  int pr = dpp::mov<dpp::kRowShr4>(d), pl = dpp::mov<dpp::kRowShl4>(d);
+  d = (lane & 4) ? (pr - d) : (d + pl);
+  pr = dpp::mov<dpp::kRowShr8>(d);
+  pl = dpp::mov<dpp::kRowShl8>(d);
+  d = (lane & 8) ? (pr - d) : (d + pl);
 #pragma unroll
   for (int s = 16; s < 64; s <<= 1) {
     p = __shfl_xor(d, s, 64);

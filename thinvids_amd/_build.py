@@ -26,7 +26,7 @@ ARCH = os.environ.get("TV_OFFLOAD_ARCH", "gfx950")
 
 CXXFLAGS = ["-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wno-unused-function", f"-I{INC}"]
 HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INC}",
-            "-Wno-unused-result", "-munsafe-fp-atomics"]
+            "-Wno-unused-result", "-munsafe-fp-atomics", *os.environ.get("TV_HIPFLAGS_EXTRA", "").split()]
 
 
 def _hipcc() -> str:
@@ -37,7 +37,7 @@ def _hipcc() -> str:
 
 
 def _headers() -> list[Path]:
-    return sorted(INC.rglob("*.h"))
+    return sorted(INC.rglob("*.h")) + sorted((CSRC / "gpu").glob("*.h"))
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:
