@@ -119,3 +119,99 @@ def test_node_job_ladder_single_process(tmp_path, source):
     with open(res["outputs"][1]["path"], "rb") as f:
         dec = hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False)
     assert len(dec.frames) == 24 and dec.frames[0][0].shape == (48, 64)
+
+
+def _job_worker_env(rank, world, port, src, out, kw, res_path, env):
+    os.environ.update(env)
+    from thinvids_amd.parallel.node_job import run_job
+
+    dist = _init(rank, world, port)
+    try:
+        res = run_job(src, out, software=True, **kw)
+    except RuntimeError as e:
+        res = {"error": str(e)}
+    with open(f"{res_path}.{rank}", "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def _spawn_job(tmp_path, source, kw, env, world=2):
+    src, frames = source
+    out = str(tmp_path / "out.mp4")
+    res_path = str(tmp_path / "res.json")
+    kw = dict(gop=8, segment_frames=8, batch_segments=1, **kw)
+    mp.spawn(_job_worker_env, args=(world, _free_port(), src, out, kw, res_path, env), nprocs=world, join=True)
+    return [json.load(open(f"{res_path}.{r}")) for r in range(world)], out
+
+
+def test_node_job_segment_failure_is_retried_by_any_rank(tmp_path, source):
+    """A segment that fails twice goes back on the shared retry list (the reference's part
+    re-enqueue, worker/tasks.py:1385-1464) and the job completes."""
+    from thinvids_amd.models import hevc
+
+    res, out = _spawn_job(tmp_path, source, {}, {"TV_FAULT": "segment:1:fail:2",
+                                                 "TV_FAULT_STATE": str(tmp_path / "fs")})
+    r0 = res[0]
+    assert "error" not in r0, r0
+    assert sum(p["retried"] for p in r0["per_rank"]) == 2
+    assert sum(p["encoded"] for p in r0["per_rank"]) == 3
+    with open(out, "rb") as f:
+        assert len(hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False).frames) == 24
+
+
+def test_node_job_abort_after_retry_budget(tmp_path, source):
+    res, _ = _spawn_job(tmp_path, source, {"max_retries": 1}, {"TV_FAULT": "segment:2:fail"})
+    # the rank that sees the abort flag first raises; ranks whose store host (rank 0) exits
+    # first fail on the store connection — either way no rank stitches a partial output
+    assert any("segment (0, 2) failed 2 times" in r.get("error", "") for r in res), res
+    assert all(r.get("error") for r in res), res
+
+
+def test_node_job_hung_rank_work_is_stolen(tmp_path, source):
+    """Rank 1 stalls before its first claim: dynamic stealing lets rank 0 take the work."""
+    res, _ = _spawn_job(tmp_path, source, {}, {"TV_FAULT": "rank:1:hang:3"})
+    per = res[0]["per_rank"]
+    assert per[0]["encoded"] >= 2 and per[0]["encoded"] + per[1]["encoded"] == 3
+
+
+def test_node_job_segment_resume(tmp_path, source):
+    ck = str(tmp_path / "ck")
+    res1, out = _spawn_job(tmp_path, source, {"resume_dir": ck}, {})
+    first = open(out, "rb").read()
+    res2, out = _spawn_job(tmp_path, source, {"resume_dir": ck}, {})
+    per = res2[0]["per_rank"]
+    assert sum(p["resumed"] for p in per) == 3 and sum(p["encoded"] for p in per) == 0
+    assert open(out, "rb").read() == first
+    # a corrupted checkpoint is re-encoded, not trusted
+    seg = sorted(p for p in os.listdir(ck) if p.endswith(".hevc"))[0]
+    with open(os.path.join(ck, seg), "r+b") as f:
+        f.seek(40)
+        f.write(b"\xff\xff")
+    res3, out = _spawn_job(tmp_path, source, {"resume_dir": ck}, {})
+    per = res3[0]["per_rank"]
+    assert sum(p["resumed"] for p in per) == 2 and sum(p["encoded"] for p in per) == 1
+    assert open(out, "rb").read() == first
+
+
+def test_node_job_elastic_restart_torchrun(tmp_path, source):
+    """Rank 1 dies on the first attempt; torchrun restarts the group (--max-restarts 1) and
+    the job resumes from the segment checkpoints of the failed attempt."""
+    import subprocess
+    import sys
+
+    src, frames = source
+    out = tmp_path / "el.mp4"
+    env = dict(os.environ, TV_FAULT="rank:1:die:1", TV_FAULT_STATE=str(tmp_path / "fs"), TV_FORCE_CPU="1",
+               PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--max-restarts", "1", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "thinvids_amd.parallel.node_job", "--input", src, "--output", str(out), "--software",
+           "--gop", "8", "--segment-frames", "8", "--resume-dir", str(tmp_path / "ck"), "--timeout-sec", "60"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["world"] == 2 and len(os.listdir(tmp_path / "fs")) == 1  # the fault fired once
+    from thinvids_amd.models import hevc
+
+    with open(out, "rb") as f:
+        assert len(hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False).frames) == 24

@@ -121,3 +121,83 @@ def test_dataplane_roundtrip(env, tmp_path):
 
     with pytest.raises(urllib.error.HTTPError):
         dataplane.fetch_part(ep, job_id, 0, str(tmp_path / "bad"))
+
+
+def _run_job(env, name, mode="split", n=20):
+    store, tasks = env["store"], env["tasks"]
+    path, frames = _source(env["root"], name, n=n)
+    job_id, tok = str(uuid.uuid4()), uuid.uuid4().hex
+    store.hset(f"job:{job_id}", mapping={
+        "job_id": job_id, "filename": name, "input_path": str(path), "status": "STARTING",
+        "pipeline_run_token": tok, "software_encode": "1", "target_height": "1080", "processing_mode": mode})
+    tasks.transcode(job_id, tok)
+    return job_id, frames
+
+
+@pytest.fixture
+def fault_env(env, monkeypatch, tmp_path):
+    monkeypatch.setenv("TV_FAULT_STATE", str(tmp_path / "faults"))
+    return env
+
+
+def test_injected_part_failure_is_retried(fault_env, monkeypatch):
+    """Part 2 fails twice in encode and once in upload: the part is re-enqueued (reference
+    `_fail` -> re-enqueue, worker/tasks.py:1385-1464) and the job still finishes."""
+    monkeypatch.setenv("TV_FAULT", "part:2:fail:2,upload:1:fail:1")
+    store = fault_env["store"]
+    job_id, frames = _run_job(fault_env, "fault_retry.y4m")
+    assert _wait_status(store, job_id, {"DONE", "FAILED"}) == "DONE", store.hgetall(f"job:{job_id}")
+    counts = store.hgetall(f"job_retry_counts:{job_id}") or {}
+    job = store.hgetall(f"job:{job_id}")
+    assert job["last_retry_part"] in ("1", "2")
+    with open(job["output_path"], "rb") as f:
+        dec = hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False)
+    assert len(dec.frames) == len(frames)
+    assert not counts  # cleaned at finalize
+    log = store.lrange(f"joblog:{job_id}", 0, -1)
+    assert sum("Retrying" in line or "retry" in line.lower() for line in log) >= 1 or job["last_retry_stage"]
+
+
+def test_injected_part_failure_exhausts_budget(fault_env, monkeypatch):
+    monkeypatch.setenv("TV_FAULT", "part:1:fail")
+    monkeypatch.setenv("PART_FAILURE_MAX_RETRIES", "2")
+    from thinvids_amd.worker.config import get_config
+
+    get_config(reload=True)
+    try:
+        store = fault_env["store"]
+        job_id, _ = _run_job(fault_env, "fault_budget.y4m", mode="direct")
+        assert _wait_status(store, job_id, {"DONE", "FAILED"}) == "FAILED"
+        job = store.hgetall(f"job:{job_id}")
+        assert job["failed_stage"] == "encode" and job["failed_part"] == "1"
+        assert "retry budget exhausted (3/2)" in job["error"]
+    finally:
+        monkeypatch.delenv("PART_FAILURE_MAX_RETRIES")
+        get_config(reload=True)
+
+
+def test_injected_stitch_failure_fails_job(fault_env, monkeypatch):
+    monkeypatch.setenv("TV_FAULT", "stitch:*:fail")
+    store = fault_env["store"]
+    job_id, _ = _run_job(fault_env, "fault_stitch.y4m")
+    assert _wait_status(store, job_id, {"DONE", "FAILED"}) == "FAILED"
+    job = store.hgetall(f"job:{job_id}")
+    assert job["failed_stage"] == "stitch" and "injected fault" in job["error"]
+
+
+def test_fault_spec_parsing(tmp_path, monkeypatch):
+    from thinvids_amd.utils import fault
+
+    specs = fault.parse("part:3:fail:2, rank:*:hang:0.01,segment:1:die")
+    assert [(s.kind, s.key, s.action, s.arg) for s in specs] == [
+        ("part", "3", "fail", 2.0), ("rank", "*", "hang", 0.01), ("segment", "1", "die", None)]
+    with pytest.raises(ValueError):
+        fault.parse("part:3:explode")
+    monkeypatch.setenv("TV_FAULT", "part:3:fail:2")
+    monkeypatch.setenv("TV_FAULT_STATE", str(tmp_path))
+    fault.check("part", 4)  # other key: no-op
+    for _ in range(2):
+        with pytest.raises(fault.InjectedFault):
+            fault.check("part", 3)
+    fault.check("part", 3)  # budget of 2 spent (persisted in TV_FAULT_STATE)
+    assert len(os.listdir(tmp_path)) == 2

@@ -23,6 +23,7 @@ Flow (the reference's split -> encode -> stitch, without HTTP or disk in between
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -30,6 +31,8 @@ import sys
 import time
 
 import numpy as np
+
+from ..utils import fault
 
 
 def _dist():
@@ -71,13 +74,157 @@ class _Counter:
     def __init__(self, key: str):
         dist = _dist()
         self.store = dist.distributed_c10d._get_default_store() if dist else None
-        self.key, self.local = key, 0
+        self.key, self.local = _ns(key), 0
 
     def next(self) -> int:
         if self.store is None:
             self.local += 1
             return self.local - 1
         return int(self.store.add(self.key, 1)) - 1
+
+
+def _ns(key: str) -> str:
+    """Store keys are namespaced by the elastic restart count, so a torchrun restart of the
+    process group (``--max-restarts``) starts with fresh counters."""
+    return f"tv{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}_{key}"
+
+
+class _LocalStore:
+    """Single-process stand-in for the c10d store (add/set/get)."""
+
+    def __init__(self):
+        self.kv: dict = {}
+
+    def add(self, k, n):
+        self.kv[k] = int(self.kv.get(k, 0)) + n
+        return self.kv[k]
+
+    def set(self, k, v):
+        self.kv[k] = v if isinstance(v, bytes) else str(v).encode()
+
+    def get(self, k):
+        return self.kv[k]
+
+
+class WorkQueue:
+    """Segment work queue shared by all ranks through the rendezvous store — the reference's
+    Huey pull model (any encoder takes the next part, worker/tasks.py:1276, :1322) plus its
+    failure path (a failed part is re-enqueued for *any* node, :1385-1464):
+
+    * ``claim(n)``: up to n fresh items from an atomic counter (a fast GPU takes more);
+    * ``fail(item)``: count the failure; re-publish the item on the retry list, or raise
+      the job-wide abort flag when it has failed ``max_retries`` + 1 times;
+    * ``claim_retry()``: claim one unclaimed retry item (one ``add`` per item: exactly one
+      rank wins it);
+    * ``finished()``: True once every rank has drained the fresh items, no retry is in
+      flight and every retry item is claimed — the termination check re-reads the retry
+      count around the in-flight read so an item published meanwhile keeps ranks looping.
+    """
+
+    def __init__(self, name: str, items: list, world: int, max_retries: int = 3):
+        dist = _dist()
+        self.store = dist.distributed_c10d._get_default_store() if dist else _LocalStore()
+        self.name, self.items, self.world, self.max_retries = name, items, world, max_retries
+        self.ctr = _Counter(f"{name}_next") if dist else None
+        self._local_next = 0
+        self._scan = 0
+
+    def _k(self, s: str) -> str:
+        return _ns(f"{self.name}_{s}")
+
+    def _add(self, s: str, n: int = 1) -> int:
+        return int(self.store.add(self._k(s), n))
+
+    def claim(self, n: int) -> list:
+        out = []
+        for _ in range(max(1, n)):
+            if self.ctr is not None:
+                k = self.ctr.next()
+            else:
+                k, self._local_next = self._local_next, self._local_next + 1
+            if k >= len(self.items):
+                break
+            out.append(self.items[k])
+        return out
+
+    def fresh_done(self) -> None:
+        self._add("done")
+
+    def aborted(self) -> str | None:
+        if self._add("abort", 0):
+            return self.store.get(self._k("abort_msg")).decode()
+        return None
+
+    def fail(self, item, why: str) -> None:
+        key = json.dumps(list(item))
+        n = self._add(f"fail_{key}")
+        if n > self.max_retries:
+            self.store.set(self._k("abort_msg"), f"segment {item} failed {n} times: {why}")
+            self._add("abort")
+            return
+        idx = self._add("rq_n") - 1
+        self.store.set(self._k(f"rq_{idx}"), key)
+
+    def claim_retry(self):
+        n = self._add("rq_n", 0)
+        while self._scan < n:
+            i = self._scan
+            self._scan += 1
+            if self._add(f"rq_c_{i}") == 1:
+                self._add("inflight")
+                return tuple(json.loads(self.store.get(self._k(f"rq_{i}")).decode()))
+        return None
+
+    def retry_done(self) -> None:
+        self._add("inflight", -1)
+
+    def finished(self) -> bool:
+        if self._add("done", 0) < self.world:
+            return False
+        n1 = self._add("rq_n", 0)
+        busy = self._add("inflight", 0)
+        n2 = self._add("rq_n", 0)
+        if busy or n1 != n2:
+            return False
+        return all(self._add(f"rq_c_{i}", 0) >= 1 for i in range(n2))
+
+
+class Checkpoint:
+    """Segment-level resume: every encoded segment is published atomically
+    as ``<dir>/r<rung>_s<idx>_q<qp>.hevc`` with a ``.sha256`` sidecar written last; a rerun
+    (or an elastic restart) reuses every segment whose checksum verifies.  Keyed by QP, so
+    first-pass segments double as the 2-pass statistics checkpoint."""
+
+    def __init__(self, root: str | None):
+        self.root = root
+        if root:
+            os.makedirs(root, exist_ok=True)
+
+    def _path(self, r: int, i: int, qp: int) -> str:
+        return os.path.join(self.root, f"r{r}_s{i}_q{qp}.hevc")
+
+    def load(self, r: int, i: int, qp: int) -> bytes | None:
+        if not self.root:
+            return None
+        p = self._path(r, i, qp)
+        try:
+            with open(p, "rb") as f:
+                data = f.read()
+            with open(p + ".sha256") as f:
+                want = f.read().strip()
+        except OSError:
+            return None
+        return data if hashlib.sha256(data).hexdigest() == want else None
+
+    def save(self, r: int, i: int, qp: int, data: bytes) -> None:
+        if not self.root:
+            return
+        p = self._path(r, i, qp)
+        for path, payload, mode in ((p, data, "wb"), (p + ".sha256", hashlib.sha256(data).hexdigest(), "w")):
+            tmp = f"{path}.{os.getpid()}.tmp"
+            with open(tmp, mode) as f:
+                f.write(payload)
+            os.replace(tmp, path)
 
 
 def _encode_many(items: list, spec_for, cache) -> dict:
@@ -95,7 +242,8 @@ def _encode_many(items: list, spec_for, cache) -> dict:
 
 def run_job(input_path: str, output: str, height: int | None = None, qp: int = 27, gop: int = 64,
             segment_frames: int = 256, mode: str = "direct", bitrate_kbps: float = 0.0, ladder=None,
-            search_range: int = 16, software: bool = False, batch_segments: int = 8) -> dict:
+            search_range: int = 16, software: bool = False, batch_segments: int = 8,
+            resume_dir: str | None = None, max_retries: int = 3) -> dict:
     import torch
 
     from ..models import hevc, media
@@ -116,6 +264,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     software = software or not gpu_available()
     cache = None if software else EngineCache(device=dev.index or 0, batch=batch_segments)
     jobs = [(r, i) for r in range(len(rungs)) for i in range(len(segs))]  # ladder fan-out (P10)
+    ckpt = Checkpoint(resume_dir)
+    stats = {"encoded": 0, "resumed": 0, "retried": 0}
 
     def spec(r, q):
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=int(q), gop=gop, search_range=search_range,
@@ -152,20 +302,63 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     fr = prepare_frames(frames, *rungs[r])
                     mine.update(_encode_many([((r, i), fr, spec(r, qps[r][i]))], None, cache))
         else:
-            ctr = _Counter(f"tv_seg_pass{encode_pass.calls}")  # same key on every rank
+            wq = WorkQueue(f"pass{encode_pass.calls}", jobs, world, max_retries)
+            fault.check("rank", rank)  # TV_FAULT=rank:<r>:hang|die|fail (tests)
+
+            def run(batch):
+                todo = []
+                for r, i in batch:
+                    b = ckpt.load(r, i, int(qps[r][i]))
+                    if b is not None:
+                        mine[(r, i)] = b
+                        stats["resumed"] += 1
+                        continue
+                    try:
+                        fault.check("segment", i)
+                        todo.append((r, i))
+                    except fault.InjectedFault as e:
+                        wq.fail((r, i), str(e))
+                if not todo:
+                    return
+                try:
+                    items = [((r, i), prepare_frames(load(i), *rungs[r]), spec(r, qps[r][i])) for r, i in todo]
+                    got = _encode_many(items, None, cache)
+                except Exception as e:  # a real engine/IO failure: every item goes back
+                    for it in todo:
+                        wq.fail(it, repr(e))
+                    return
+                for (r, i), b in got.items():
+                    ckpt.save(r, i, int(qps[r][i]), b)
+                    mine[(r, i)] = b
+                    stats["encoded"] += 1
+
             while True:
-                claimed = []
-                for _ in range(max(1, batch_segments)):  # claim a batch -> one batched launch
-                    k = ctr.next()
-                    if k >= len(jobs):
-                        break
-                    claimed.append(jobs[k])
+                msg = wq.aborted()
+                if msg:
+                    raise RuntimeError(msg)
+                claimed = wq.claim(batch_segments)  # a batch -> one batched launch
                 if not claimed:
                     break
-                items = [((r, i), prepare_frames(load(i), *rungs[r]), spec(r, qps[r][i])) for r, i in claimed]
-                mine.update(_encode_many(items, None, cache))
+                run(claimed)
                 if len(claimed) < batch_segments:
                     break
+            wq.fresh_done()
+            while not wq.finished():  # failed segments, re-published for any rank
+                msg = wq.aborted()
+                if msg:
+                    raise RuntimeError(msg)
+                it = wq.claim_retry()
+                if it is None:
+                    time.sleep(0.01)
+                    continue
+                try:
+                    stats["retried"] += 1
+                    run([it])
+                finally:
+                    wq.retry_done()
+            msg = wq.aborted()
+            if msg:
+                raise RuntimeError(msg)
         encode_pass.calls += 1
         return mine
 
@@ -191,19 +384,25 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     mine = encode_pass(qps)
     # gather bitstreams to rank 0 (one message per rank: json index + concatenated bytes)
     keys = sorted(mine)
-    header = json.dumps([[r, i, len(mine[(r, i)])] for r, i in keys]).encode()
+    header = json.dumps({"seg": [[r, i, len(mine[(r, i)])] for r, i in keys], "stats": stats}).encode()
     blob = len(header).to_bytes(8, "little") + header + b"".join(mine[k] for k in keys)
     parts = gather_bytes_to_root(blob, dev) if world > 1 else [blob]
     result = {"world": world, "segments": len(segs), "rungs": [list(x) for x in rungs], "passes": passes}
     if rank == 0:
         streams: dict = {}
+        per_rank = []
         for p in parts:
             hl = int.from_bytes(p[:8], "little")
-            idx = json.loads(p[8:8 + hl])
+            hdr = json.loads(p[8:8 + hl])
+            idx = hdr["seg"]
+            per_rank.append(hdr["stats"])
             off = 8 + hl
             for r, i, n in idx:
                 streams[(r, i)] = p[off:off + n]
                 off += n
+        missing = [k for k in jobs if k not in streams]
+        if missing:
+            raise RuntimeError(f"segments missing at stitch: {missing}")
         outs = []
         for r, (ow, oh) in enumerate(rungs):
             annexb = b"".join(streams[(r, i)] for i in range(len(segs)))
@@ -215,7 +414,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             os.replace(tmp, path)
             outs.append({"path": path, "bytes": len(data), "width": ow, "height": oh,
                          "kbps": len(annexb) * 8 / (nfr * src.fps_den / src.fps_num) / 1000})
-        result.update(outputs=outs, qp_plan=[[int(q) for q in row] for row in qps],
+        result.update(per_rank=per_rank, outputs=outs, qp_plan=[[int(q) for q in row] for row in qps],
                       seconds=round(time.time() - t0, 3), fps=round(nfr * len(rungs) / (time.time() - t0), 2))
     if cache:
         cache.close()
@@ -235,6 +434,9 @@ def main(argv=None) -> int:
     ap.add_argument("--ladder", default="")
     ap.add_argument("--software", action="store_true")
     ap.add_argument("--backend", default=None)
+    ap.add_argument("--resume-dir", default=None, help="segment checkpoint directory (resume / elastic restart)")
+    ap.add_argument("--max-retries", type=int, default=3, help="per-segment retry budget before the job aborts")
+    ap.add_argument("--timeout-sec", type=float, default=600.0, help="collective timeout (a hung rank surfaces)")
     a = ap.parse_args(argv)
     import torch
     import torch.distributed as dist
@@ -243,10 +445,12 @@ def main(argv=None) -> int:
         backend = a.backend or ("nccl" if torch.cuda.is_available() and not a.software else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group(backend)
+        import datetime
+
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=a.timeout_sec))
     ladder = [int(x) for x in a.ladder.split(",") if x.strip()] or None
     res = run_job(a.input, a.output, a.height, a.qp, a.gop, a.segment_frames, a.mode, a.bitrate_kbps, ladder,
-                  software=a.software)
+                  software=a.software, resume_dir=a.resume_dir, max_retries=a.max_retries)
     if int(os.environ.get("RANK", "0")) == 0:
         print(json.dumps(res), flush=True)
     if dist.is_initialized():

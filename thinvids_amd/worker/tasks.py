@@ -31,6 +31,7 @@ from ..common import Status, emit_activity
 from ..models import hevc, media
 from ..queue import get_encode_queue, get_pipeline_queue
 from ..store import get_store
+from ..utils import fault
 from . import dataplane, planning
 from .config import get_config
 from .encoder import EncodeSpec, encode_parts, prepare_frames
@@ -309,6 +310,7 @@ def encode_batch(tasks: list[dict]) -> list[dict | None]:
                           stage="encode_start", source="worker")
         job_heartbeat(job_id, "encode", note=f"part {idx}")
         try:
+            fault.check("download", idx)
             spec = encode_spec_for_job(job)
             _, deint = effective_target_height(job)  # DVD-native SD keeps its lines + bwdif
             frames = prepare_frames(_load_part(job_id, job, t), spec.width, spec.height, deinterlace=deint)
@@ -322,6 +324,16 @@ def encode_batch(tasks: list[dict]) -> list[dict | None]:
     for item in live:
         by_spec.setdefault(item[3], []).append(item)
     for spec, items in by_spec.items():
+        ok = []
+        for it in items:
+            try:
+                fault.check("part", int(it[1]["idx"]))
+                ok.append(it)
+            except fault.InjectedFault as e:
+                results[it[0]] = _part_failed(it[1]["job_id"], it[2], it[1], str(e), "encode")
+        items = ok
+        if not items:
+            continue
         try:
             bits = encode_parts([it[4] for it in items], spec)
         except Exception as e:
@@ -332,6 +344,7 @@ def encode_batch(tasks: list[dict]) -> list[dict | None]:
         for (i, t, job, spec_, frames, t0), annexb in zip(items, bits):
             job_id, idx = t["job_id"], int(t["idx"])
             try:
+                fault.check("upload", idx)
                 fn, fd = _fps(job)
                 _deliver(job_id, job, idx, hevc.mux_mp4(annexb, spec.width, spec.height, fn, fd))
                 _commit(job_id, job, idx, t0)
@@ -460,6 +473,7 @@ def stitch(job_id: str, run_token: str | None = None):
     out_local = os.path.join(base, f"job_{job_id}_output.mp4")
     paths = [os.path.join(enc_dir, f"enc_{i:03d}.mp4") for i in range(1, total + 1)]
     try:
+        fault.check("stitch", "*")
         concat_parts(paths, out_local, spec.width, spec.height, fn, fd)
         final = final_output_path(str(job.get("filename") or f"{job_id}.mp4"))
         ensure_dirs(os.path.dirname(final))
