@@ -10,6 +10,7 @@
 // Replaces the per-part `encode` task's ffmpeg invocation (reference
 // worker/tasks.py:1532-1651); the control plane (worker/encode.py) drives this engine.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <atomic>
 #include <chrono>
@@ -39,6 +40,25 @@
 
 namespace tv {
 namespace gpu {
+
+// ROCTx ranges (TV_ROCTX=1): host-side frame / D2H / entropy stages appear next to the
+// kernels in `rocprofv3 --marker-trace --kernel-trace` timelines.
+inline bool roctx_on() {
+  static const bool on = [] {
+    const char* e = getenv("TV_ROCTX");
+    return e && *e == '1';
+  }();
+  return on;
+}
+struct Range {
+  explicit Range(const char* name) : on(roctx_on()) {
+    if (on) roctxRangePushA(name);
+  }
+  ~Range() {
+    if (on) roctxRangePop();
+  }
+  bool on;
+};
 
 class ThreadPool {
  public:
@@ -357,6 +377,7 @@ class Engine {
     HIP_OK(hipMemsetAsync(d_sse_, 0, B * 3 * sizeof(unsigned long long), stream_));
     HIP_OK(hipEventRecord(t0_, stream_));
     for (int f = 0; f < F; ++f) {
+      Range frame_range(f == 0 ? "engine.frame.intra" : "engine.frame.inter");
       Slot& s = slots_[f % kSlots];
       while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
       const DecisionSet dec = slot_dec(s);
@@ -389,6 +410,7 @@ class Engine {
       s.pending.store(B + 1, std::memory_order_release);
       pool_->submit([this, &s, B, f, &slices, &fail] {
         try {
+          Range r("engine.d2h");
           fetch_slot(s, B);
         } catch (const std::exception& e) {
           fail(e);
@@ -399,6 +421,7 @@ class Engine {
         for (int b = 0; b < B; ++b)
           pool_->submit([this, &s, b, f, &slices, &fail] {
             try {
+              Range r("engine.cabac_slice");
               const auto c0 = std::chrono::steady_clock::now();
               write_slice(seq_, host_view(s, b), f, f == 0, slices[b][f]);
               entropy_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(

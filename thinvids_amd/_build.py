@@ -80,7 +80,8 @@ def build_gpu(force: bool = False, jobs: int = 8) -> Path:
         objs = list(ex.map(lambda s: _compile(s, OBJDIR / "gpu" / (s.stem + ".o"), hipcc, HIPFLAGS, force), srcs))
     if force or _stale(out, objs + [core]):
         _run([hipcc, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", str(out), *map(str, objs),
-              f"-L{LIBDIR}", "-ltvcore", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+              f"-L{LIBDIR}", "-ltvcore", "-Wl,-rpath,$ORIGIN", "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx",
+              "-Wl,-rpath,/opt/rocm/lib", "-lpthread"])
     return out
 
 

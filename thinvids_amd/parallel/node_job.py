@@ -32,7 +32,7 @@ import time
 
 import numpy as np
 
-from ..utils import fault
+from ..utils import fault, trace
 
 
 def _dist():
@@ -321,8 +321,10 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 if not todo:
                     return
                 try:
-                    items = [((r, i), prepare_frames(load(i), *rungs[r]), spec(r, qps[r][i])) for r, i in todo]
-                    got = _encode_many(items, None, cache)
+                    with trace.span("node_job.load"):
+                        items = [((r, i), prepare_frames(load(i), *rungs[r]), spec(r, qps[r][i])) for r, i in todo]
+                    with trace.span("node_job.encode", segments=len(items)):
+                        got = _encode_many(items, None, cache)
                 except Exception as e:  # a real engine/IO failure: every item goes back
                     for it in todo:
                         wq.fail(it, repr(e))
@@ -386,7 +388,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     keys = sorted(mine)
     header = json.dumps({"seg": [[r, i, len(mine[(r, i)])] for r, i in keys], "stats": stats}).encode()
     blob = len(header).to_bytes(8, "little") + header + b"".join(mine[k] for k in keys)
-    parts = gather_bytes_to_root(blob, dev) if world > 1 else [blob]
+    with trace.span("node_job.gather"):
+        parts = gather_bytes_to_root(blob, dev) if world > 1 else [blob]
     result = {"world": world, "segments": len(segs), "rungs": [list(x) for x in rungs], "passes": passes}
     if rank == 0:
         streams: dict = {}
@@ -407,14 +410,15 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         for r, (ow, oh) in enumerate(rungs):
             annexb = b"".join(streams[(r, i)] for i in range(len(segs)))
             path = output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4"
-            data = hevc.mux_mp4(annexb, ow, oh, src.fps_num, src.fps_den)
+            with trace.span("node_job.mux"):
+                data = hevc.mux_mp4(annexb, ow, oh, src.fps_num, src.fps_den)
             tmp = path + ".tmp"
             with open(tmp, "wb") as f:
                 f.write(data)
             os.replace(tmp, path)
             outs.append({"path": path, "bytes": len(data), "width": ow, "height": oh,
                          "kbps": len(annexb) * 8 / (nfr * src.fps_den / src.fps_num) / 1000})
-        result.update(per_rank=per_rank, outputs=outs, qp_plan=[[int(q) for q in row] for row in qps],
+        result.update(trace=trace.summary(), per_rank=per_rank, outputs=outs, qp_plan=[[int(q) for q in row] for row in qps],
                       seconds=round(time.time() - t0, 3), fps=round(nfr * len(rungs) / (time.time() - t0), 2))
     if cache:
         cache.close()

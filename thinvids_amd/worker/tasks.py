@@ -31,7 +31,7 @@ from ..common import Status, emit_activity
 from ..models import hevc, media
 from ..queue import get_encode_queue, get_pipeline_queue
 from ..store import get_store
-from ..utils import fault
+from ..utils import fault, trace
 from . import dataplane, planning
 from .config import get_config
 from .encoder import EncodeSpec, encode_parts, prepare_frames
@@ -313,7 +313,10 @@ def encode_batch(tasks: list[dict]) -> list[dict | None]:
             fault.check("download", idx)
             spec = encode_spec_for_job(job)
             _, deint = effective_target_height(job)  # DVD-native SD keeps its lines + bwdif
-            frames = prepare_frames(_load_part(job_id, job, t), spec.width, spec.height, deinterlace=deint)
+            with trace.span("worker.download"):
+                raw = _load_part(job_id, job, t)
+            with trace.span("worker.prepare"):
+                frames = prepare_frames(raw, spec.width, spec.height, deinterlace=deint)
             if not frames:
                 raise RuntimeError("part has no frames")
             live.append((i, t, job, spec, frames, t0))
@@ -335,7 +338,8 @@ def encode_batch(tasks: list[dict]) -> list[dict | None]:
         if not items:
             continue
         try:
-            bits = encode_parts([it[4] for it in items], spec)
+            with trace.span("worker.encode", parts=len(items)):
+                bits = encode_parts([it[4] for it in items], spec)
         except Exception as e:
             log.error("encode failed:\n%s", traceback.format_exc())
             for i, t, job, *_ in items:
@@ -346,7 +350,8 @@ def encode_batch(tasks: list[dict]) -> list[dict | None]:
             try:
                 fault.check("upload", idx)
                 fn, fd = _fps(job)
-                _deliver(job_id, job, idx, hevc.mux_mp4(annexb, spec.width, spec.height, fn, fd))
+                with trace.span("worker.upload"):
+                    _deliver(job_id, job, idx, hevc.mux_mp4(annexb, spec.width, spec.height, fn, fd))
                 _commit(job_id, job, idx, t0)
                 results[i] = {"status": "COMPLETED", "idx": idx, "bytes": len(annexb), "frames": len(frames)}
             except Exception as e:
@@ -474,7 +479,8 @@ def stitch(job_id: str, run_token: str | None = None):
     paths = [os.path.join(enc_dir, f"enc_{i:03d}.mp4") for i in range(1, total + 1)]
     try:
         fault.check("stitch", "*")
-        concat_parts(paths, out_local, spec.width, spec.height, fn, fd)
+        with trace.span("stitch.concat"):
+            concat_parts(paths, out_local, spec.width, spec.height, fn, fd)
         final = final_output_path(str(job.get("filename") or f"{job_id}.mp4"))
         ensure_dirs(os.path.dirname(final))
         tmp = final + ".tmp"
