@@ -1,0 +1,420 @@
+// k_av1.hip — AV1 in-loop filter kernels for gfx950 (BASELINE config #4):
+//
+//   k_cdef_dir     one wavefront per 8x8 luma block (lane = pixel): partial sums of the 8
+//                  directions with LDS atomics, lanes 0..7 score one direction each;
+//   k_cdef_search  one workgroup per 64x64 (chroma 32x32) filter block: the block + 2-pixel
+//                  halo is staged in LDS once and every thread sweeps one of the 64
+//                  (primary, secondary) strength presets over a quarter of the pixels —
+//                  the encoder's CDEF strength search as one launch per plane batch;
+//   k_cdef_apply   the filter with the chosen per-block preset (LDS tile, pixel per thread);
+//   k_wiener_*     64x64 restoration units: LDS tile with a 3-pixel halo, horizontal 7-tap
+//                  pass into an LDS intermediate, vertical pass to the output; the
+//                  least-squares statistics of the separable tap estimation reduce per unit
+//                  (wave DPP sums, int64 LDS atomics);
+//   k_sgr_*        self-guided restoration: box sums from the LDS tile, (A, B) planes in LDS
+//                  per radius, 3x3 weighted guide, projection / statistics per unit.
+//
+// All planes are batched (B planes of w x h, pitch w, back to back; grid.y = plane) and
+// every per-pixel formula comes from tv/av1_defs.h, shared with the C++ golden model
+// (csrc/core/av1_tools.cpp): GPU == CPU bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "gpu_common.h"
+#include "tv/av1_defs.h"
+
+namespace tv {
+namespace gpu {
+namespace {
+
+using namespace tv::av1;
+constexpr int kRu = 64;
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// 64-bit wave sum (DPP-free: 64-bit values are rare here, per-unit reductions only)
+__device__ __forceinline__ long long wave_sum64(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------------------ CDEF ----
+__global__ void __launch_bounds__(256) k_cdef_dir(const uint8_t* __restrict__ Y, int w, int h, uint8_t* dir,
+                                                  int* var) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.y;
+  const int w8 = w >> 3, n8 = w8 * (h >> 3);
+  const int blk = blockIdx.x * 4 + wave;
+  __shared__ int part[4][8][16];
+  __shared__ int cost[4][8];
+  for (int i = lane; i < 128; i += 64) part[wave][i >> 4][i & 15] = 0;
+  __syncthreads();
+  if (blk < n8) {
+    const int by = blk / w8, bx = blk - by * w8, i = lane >> 3, j = lane & 7;
+    const int x = (int)Y[(long)b * w * h + (long)(by * 8 + i) * w + bx * 8 + j] - 128;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) atomicAdd(&part[wave][d][cdef_bin(d, i, j)], x);
+  }
+  __syncthreads();
+  if (blk < n8 && lane < 8) cost[wave][lane] = cdef_cost(part[wave][lane], lane);
+  __syncthreads();
+  if (blk < n8 && lane == 0) {
+    int v;
+    dir[(long)b * n8 + blk] = (uint8_t)cdef_pick(cost[wave], &v);
+    var[(long)b * n8 + blk] = v;
+  }
+}
+
+constexpr int kFbMax = 64, kHalo = 2, kTile = kFbMax + 2 * kHalo;
+
+// Stage filter block `fb` (+halo) of plane b in LDS as int16 (-1 = outside the frame).
+__device__ __forceinline__ void cdef_stage(const uint8_t* P, int w, int h, int x0, int y0, int fbw, int fbh,
+                                           int16_t (*T)[kTile]) {
+  const int tw = fbw + 2 * kHalo, th = fbh + 2 * kHalo;
+  for (int i = threadIdx.x; i < tw * th; i += blockDim.x) {
+    const int ty = i / tw, tx = i - ty * tw, y = y0 + ty - kHalo, x = x0 + tx - kHalo;
+    T[ty][tx] = (x >= 0 && x < w && y >= 0 && y < h) ? (int16_t)P[(long)y * w + x] : (int16_t)-1;
+  }
+}
+
+__device__ __forceinline__ int cdef_tile_filter(const int16_t (*T)[kTile], int ty, int tx, int pri, int sec, int dmp,
+                                                int d) {
+  auto get = [&](int dy, int dx) -> int { return T[ty + dy][tx + dx]; };
+  return cdef_filter(get, T[ty][tx], pri, sec, dmp, d);
+}
+
+__global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__ src, const uint8_t* __restrict__ rec,
+                                                     int w, int h, int chroma, const uint8_t* __restrict__ dir,
+                                                     const int* __restrict__ var, int luma_w8, int luma_n8,
+                                                     int damping, unsigned long long* sse) {
+  const int b = blockIdx.y, fb = blockIdx.x;
+  const int bs_l2 = chroma ? 2 : 3, fbs = chroma ? 32 : 64, nfx = (w + fbs - 1) / fbs;
+  const int x0 = (fb % nfx) * fbs, y0 = (fb / nfx) * fbs;
+  const int fbw = min(fbs, w - x0), fbh = min(fbs, h - y0);
+  const int dmp = chroma ? damping - 1 : damping;
+  __shared__ int16_t T[kTile][kTile];
+  __shared__ unsigned long long acc[kCdefPresets];
+  const long po = (long)b * w * h;
+  cdef_stage(rec + po, w, h, x0, y0, fbw, fbh, T);
+  if (threadIdx.x < kCdefPresets) acc[threadIdx.x] = 0;
+  __syncthreads();
+  const int p = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int psec = cdef_sec_value(p & 3), ppri = p >> 2;
+  unsigned s = 0;  // <= 1024 pixels x 255^2 fits in 32 bits
+  for (int q = g; q < fbw * fbh; q += 4) {
+    const int i = q / fbw, j = q - i * fbw, x = x0 + j, y = y0 + i;
+    const long k = (long)b * luma_n8 + (y >> bs_l2) * luma_w8 + (x >> bs_l2);
+    const int pri = chroma ? ppri : cdef_adjust_strength(ppri, var[k]);
+    const int f = (pri | psec) ? cdef_tile_filter(T, i + kHalo, j + kHalo, pri, psec, dmp, dir[k]) : T[i + kHalo][j + kHalo];
+    const int e = f - (int)src[po + (long)y * w + x];
+    s += (unsigned)(e * e);
+  }
+  atomicAdd(&acc[p], (unsigned long long)s);
+  __syncthreads();
+  const int nfb = nfx * ((h + fbs - 1) / fbs);
+  if (threadIdx.x < kCdefPresets) sse[((long)b * nfb + fb) * kCdefPresets + threadIdx.x] = acc[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) k_cdef_apply(const uint8_t* __restrict__ rec, int w, int h, int chroma,
+                                                    const uint8_t* __restrict__ dir, const int* __restrict__ var,
+                                                    int luma_w8, int luma_n8, int damping,
+                                                    const int8_t* __restrict__ fb_preset, uint8_t* out) {
+  const int b = blockIdx.y, fb = blockIdx.x;
+  const int bs_l2 = chroma ? 2 : 3, fbs = chroma ? 32 : 64, nfx = (w + fbs - 1) / fbs;
+  const int nfb = nfx * ((h + fbs - 1) / fbs);
+  const int x0 = (fb % nfx) * fbs, y0 = (fb / nfx) * fbs;
+  const int fbw = min(fbs, w - x0), fbh = min(fbs, h - y0);
+  const int dmp = chroma ? damping - 1 : damping;
+  const int p = fb_preset[(long)b * nfb + fb];
+  const long po = (long)b * w * h;
+  __shared__ int16_t T[kTile][kTile];
+  cdef_stage(rec + po, w, h, x0, y0, fbw, fbh, T);
+  __syncthreads();
+  for (int q = threadIdx.x; q < fbw * fbh; q += blockDim.x) {
+    const int i = q / fbw, j = q - i * fbw, x = x0 + j, y = y0 + i;
+    const long k = (long)b * luma_n8 + (y >> bs_l2) * luma_w8 + (x >> bs_l2);
+    int pri = 0, sec = 0;
+    if (p >= 0) {
+      sec = cdef_sec_value(p & 3);
+      pri = chroma ? (p >> 2) : cdef_adjust_strength(p >> 2, var[k]);
+    }
+    out[po + (long)y * w + x] =
+        (uint8_t)((pri | sec) ? cdef_tile_filter(T, i + kHalo, j + kHalo, pri, sec, dmp, dir[k]) : T[i + kHalo][j + kHalo]);
+  }
+}
+
+// ---------------------------------------------------------------------- Wiener ----------
+constexpr int kLrHalo = 3, kLrTile = kRu + 2 * kLrHalo;  // 70
+
+// rec tile of unit (ux, uy) with edge-replicated 3-pixel halo
+__device__ __forceinline__ void lr_stage(const uint8_t* P, int w, int h, int ux, int uy, int uw, int uh,
+                                         uint8_t (*T)[kLrTile]) {
+  const int tw = uw + 2 * kLrHalo, th = uh + 2 * kLrHalo;
+  for (int i = threadIdx.x; i < tw * th; i += blockDim.x) {
+    const int ty = i / tw, tx = i - ty * tw;
+    T[ty][tx] = P[(long)clampi(uy + ty - kLrHalo, 0, h - 1) * w + clampi(ux + tx - kLrHalo, 0, w - 1)];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_wiener_apply(const uint8_t* __restrict__ rec, int w, int h,
+                                                      const int* __restrict__ coef, uint8_t* out) {
+  const int b = blockIdx.y, u = blockIdx.x, nux = (w + kRu - 1) / kRu, nu = nux * ((h + kRu - 1) / kRu);
+  const int ux = (u % nux) * kRu, uy = (u / nux) * kRu, uw = min(kRu, w - ux), uh = min(kRu, h - uy);
+  const long po = (long)b * w * h;
+  __shared__ uint8_t T[kLrTile][kLrTile];
+  __shared__ int mid[kLrTile][kRu];
+  __shared__ int c[6];
+  if (threadIdx.x < 6) c[threadIdx.x] = coef[((long)b * nu + u) * 6 + threadIdx.x];
+  lr_stage(rec + po, w, h, ux, uy, uw, uh, T);
+  __syncthreads();
+  const bool id = !(c[0] | c[1] | c[2] | c[3] | c[4] | c[5]);
+  if (id) {
+    for (int q = threadIdx.x; q < uw * uh; q += blockDim.x) {
+      const int i = q / uw, j = q - i * uw;
+      out[po + (long)(uy + i) * w + ux + j] = T[i + kLrHalo][j + kLrHalo];
+    }
+    return;
+  }
+  for (int q = threadIdx.x; q < (uh + 6) * uw; q += blockDim.x) {
+    const int r = q / uw, j = q - r * uw;
+    mid[r][j] = wiener_h([&](int t) -> int { return T[r][j + t]; }, c);
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x) {
+    const int i = q / uw, j = q - i * uw;
+    out[po + (long)(uy + i) * w + ux + j] = (uint8_t)wiener_v(&mid[i][j], kRu, c + 3);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_wiener_stats(const uint8_t* __restrict__ src, const uint8_t* __restrict__ rec,
+                                                      int w, int h, int dirn, const int* __restrict__ other,
+                                                      long long* stats) {
+  const int b = blockIdx.y, u = blockIdx.x, nux = (w + kRu - 1) / kRu, nu = nux * ((h + kRu - 1) / kRu);
+  const int ux = (u % nux) * kRu, uy = (u / nux) * kRu, uw = min(kRu, w - ux), uh = min(kRu, h - uy);
+  const long po = (long)b * w * h;
+  __shared__ uint8_t T[kLrTile][kLrTile];
+  __shared__ int Z[kLrTile][kLrTile];  // z on the unit extended by 3 along the estimation direction
+  __shared__ int c[3];
+  __shared__ unsigned long long red[9];
+  if (threadIdx.x < 3) c[threadIdx.x] = other[((long)b * nu + u) * 3 + threadIdx.x];
+  if (threadIdx.x < 9) red[threadIdx.x] = 0;
+  lr_stage(rec + po, w, h, ux, uy, uw, uh, T);
+  __syncthreads();
+  // z at tile position (r, s): plane coordinate clamp(uy + r - 3), clamp(ux + s - 3)
+  const int zw = dirn == 0 ? uw + 6 : uw, zh = dirn == 0 ? uh : uh + 6;
+  for (int q = threadIdx.x; q < zw * zh; q += blockDim.x) {
+    const int r = q / zw, s = q - r * zw;
+    const int ty = dirn == 0 ? r + kLrHalo : r, tx = dirn == 0 ? s : s + kLrHalo;  // tile coords of the sample
+    // the tile halo is edge-replicated, so tile neighbours == clamped plane neighbours
+    Z[ty][tx] = dirn == 0 ? lr_tap_filter([&](int t) -> int { return T[ty + t - 3][tx]; }, c)
+                          : lr_tap_filter([&](int t) -> int { return T[ty][tx + t - 3]; }, c);
+  }
+  __syncthreads();
+  long long a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x) {
+    const int i = q / uw, j = q - i * uw, ty = i + kLrHalo, tx = j + kLrHalo;
+    // neighbour along the estimation direction, clamped at the frame border
+    auto at = [&](int d) -> int {
+      if (dirn == 0) {
+        const int x = clampi(ux + j + d, 0, w - 1);
+        return Z[ty][x - ux + kLrHalo];
+      }
+      const int y = clampi(uy + i + d, 0, h - 1);
+      return Z[y - uy + kLrHalo][tx];
+    };
+    const int zc = at(0);
+    const int f0 = at(-3) + at(3) - 2 * zc, f1 = at(-2) + at(2) - 2 * zc, f2 = at(-1) + at(1) - 2 * zc;
+    const long long e = 128LL * ((int)src[po + (long)(uy + i) * w + ux + j] - zc);
+    a[0] += f0 * f0;
+    a[1] += f0 * f1;
+    a[2] += f0 * f2;
+    a[3] += f1 * f1;
+    a[4] += f1 * f2;
+    a[5] += f2 * f2;
+    a[6] += f0 * e;
+    a[7] += f1 * e;
+    a[8] += f2 * e;
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const long long v = wave_sum64(a[k]);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&red[k], (unsigned long long)v);
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) stats[((long)b * nu + u) * 9 + threadIdx.x] = (long long)red[threadIdx.x];
+}
+
+// ----------------------------------------------------------------- self-guided ----------
+constexpr int kAb = kRu + 2;  // A/B planes cover the unit + 1
+
+// guided output (RST domain) for the unit's pixels, radius r, into F (registers, 16/thread)
+__device__ void sgr_guided(const uint8_t (*T)[kLrTile], int w, int h, int ux, int uy, int uw, int uh, int r, int eps,
+                           int (*A)[kAb], int (*Bv)[kAb], int* F) {
+  // A/B at plane positions clamp(uy - 1 + i), clamp(ux - 1 + j): box sums around the clamped
+  // position over clamped coordinates (tile halo covers +-3 around the unit)
+  for (int q = threadIdx.x; q < (uw + 2) * (uh + 2); q += blockDim.x) {
+    const int i = q / (uw + 2), j = q - i * (uw + 2);
+    const int cy = clampi(uy - 1 + i, 0, h - 1), cx = clampi(ux - 1 + j, 0, w - 1);
+    int s = 0, sq = 0;
+    for (int dy = -r; dy <= r; ++dy)
+      for (int dx = -r; dx <= r; ++dx) {
+        const int yy = clampi(cy + dy, 0, h - 1), xx = clampi(cx + dx, 0, w - 1);
+        const int v = T[yy - uy + kLrHalo][xx - ux + kLrHalo];
+        s += v;
+        sq += v * v;
+      }
+    sgr_ab(s, sq, r, eps, &A[i][j], &Bv[i][j]);
+  }
+  __syncthreads();
+  int n = 0;
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+    const int i = q / uw, j = q - i * uw;
+    int a = 0, bb = 0;
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int wt = (dx && dy) ? 3 : 4;
+        // neighbour (clamped in the plane) -> A/B index
+        const int yy = clampi(uy + i + dy, 0, h - 1) - uy + 1, xx = clampi(ux + j + dx, 0, w - 1) - ux + 1;
+        a += wt * A[yy][xx];
+        bb += wt * Bv[yy][xx];
+      }
+    const int sh = kSgrSgrBits + 5 - kSgrRstBits;
+    F[n] = (a * (int)T[i + kLrHalo][j + kLrHalo] + bb + (1 << (sh - 1))) >> sh;
+  }
+  __syncthreads();
+}
+
+template <bool kStats>
+__global__ void __launch_bounds__(256) k_sgr(const uint8_t* __restrict__ src, const uint8_t* __restrict__ rec, int w,
+                                             int h, int set_all, const int* __restrict__ params, long long* stats,
+                                             uint8_t* out) {
+  const int b = blockIdx.y, u = blockIdx.x, nux = (w + kRu - 1) / kRu, nu = nux * ((h + kRu - 1) / kRu);
+  const int ux = (u % nux) * kRu, uy = (u / nux) * kRu, uw = min(kRu, w - ux), uh = min(kRu, h - uy);
+  const long po = (long)b * w * h;
+  __shared__ uint8_t T[kLrTile][kLrTile];
+  __shared__ int A[kAb][kAb], Bv[kAb][kAb];
+  __shared__ unsigned long long red[5];
+  const int* pr = kStats ? nullptr : params + ((long)b * nu + u) * 3;
+  const int set = kStats ? set_all : pr[0];
+  if (!kStats && set < 0) {  // unit off: copy
+    for (int q = threadIdx.x; q < uw * uh; q += blockDim.x) {
+      const int i = q / uw, j = q - i * uw;
+      out[po + (long)(uy + i) * w + ux + j] = rec[po + (long)(uy + i) * w + ux + j];
+    }
+    return;
+  }
+  lr_stage(rec + po, w, h, ux, uy, uw, uh, T);
+  if (kStats && threadIdx.x < 5) red[threadIdx.x] = 0;
+  __syncthreads();
+  const int r0 = sgr_param(set, 0), r1 = sgr_param(set, 2);
+  int f0[16], f1[16];
+  int n = 0;
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+    const int i = q / uw, j = q - i * uw;
+    f0[n] = f1[n] = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
+  }
+  if (r0) sgr_guided(T, w, h, ux, uy, uw, uh, r0, sgr_param(set, 1), A, Bv, f0);
+  if (r1) sgr_guided(T, w, h, ux, uy, uw, uh, r1, sgr_param(set, 3), A, Bv, f1);
+  long long a[5] = {0, 0, 0, 0, 0};
+  n = 0;
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+    const int i = q / uw, j = q - i * uw;
+    const int x = (int)T[i + kLrHalo][j + kLrHalo];
+    if (kStats) {
+      const int uu = x << kSgrRstBits;
+      const long long da = f0[n] - uu, db = f1[n] - uu;
+      const long long e = ((long long)(((int)src[po + (long)(uy + i) * w + ux + j]) << kSgrRstBits) - uu)
+                          << kSgrPrjBits;
+      a[0] += da * da;
+      a[1] += da * db;
+      a[2] += db * db;
+      a[3] += da * e;
+      a[4] += db * e;
+    } else {
+      out[po + (long)(uy + i) * w + ux + j] = (uint8_t)sgr_project(x, f0[n], f1[n], r0, r1, pr[1], pr[2]);
+    }
+  }
+  if (kStats) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const long long v = wave_sum64(a[k]);
+      if ((threadIdx.x & 63) == 0) atomicAdd(&red[k], (unsigned long long)v);
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) stats[((long)b * nu + u) * 5 + threadIdx.x] = (long long)red[threadIdx.x];
+  }
+}
+
+thread_local std::string g_av1_gpu_err;
+int av1_status(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return 0;
+  g_av1_gpu_err = std::string(what) + ": " + hipGetErrorString(e);
+  return -1;
+}
+bool bad_geo(int w, int h, int B, int mult, const char* what) {
+  if (w < mult || h < mult || (w % mult) || (h % mult) || B < 1 || B > 65535) {
+    g_av1_gpu_err = std::string(what) + ": bad geometry";
+    return true;
+  }
+  return false;
+}
+inline unsigned nunits(int w, int h) { return (unsigned)(((w + kRu - 1) / kRu) * ((h + kRu - 1) / kRu)); }
+
+}  // namespace
+}  // namespace gpu
+}  // namespace tv
+
+using namespace tv::gpu;
+
+extern "C" {
+const char* tv_av1_gpu_last_error() { return g_av1_gpu_err.c_str(); }
+
+// B luma planes (w, h multiples of 8) -> dir/var [B][w/8 * h/8]
+int tv_gpu_cdef_dirs(const uint8_t* Y, int w, int h, int B, uint8_t* dir, int* var, void* stream) {
+  if (bad_geo(w, h, B, 8, "cdef_dirs")) return -1;
+  const int n8 = (w / 8) * (h / 8);
+  k_cdef_dir<<<dim3((n8 + 3) / 4, B), 256, 0, (hipStream_t)stream>>>(Y, w, h, dir, var);
+  return av1_status("cdef_dirs");
+}
+// sse: [B][nfb][64] (uint64)
+int tv_gpu_cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, int B, int chroma, const uint8_t* dir,
+                       const int* var, int luma_w8, int luma_n8, int damping, unsigned long long* sse, void* stream) {
+  if (bad_geo(w, h, B, chroma ? 4 : 8, "cdef_search") || damping < 3 || damping > 6) return -1;
+  const int fbs = chroma ? 32 : 64, nfb = ((w + fbs - 1) / fbs) * ((h + fbs - 1) / fbs);
+  k_cdef_search<<<dim3(nfb, B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, chroma, dir, var, luma_w8, luma_n8,
+                                                               damping, sse);
+  return av1_status("cdef_search");
+}
+int tv_gpu_cdef_apply(const uint8_t* rec, int w, int h, int B, int chroma, const uint8_t* dir, const int* var,
+                      int luma_w8, int luma_n8, int damping, const int8_t* fb_preset, uint8_t* out, void* stream) {
+  if (bad_geo(w, h, B, chroma ? 4 : 8, "cdef_apply") || damping < 3 || damping > 6) return -1;
+  const int fbs = chroma ? 32 : 64, nfb = ((w + fbs - 1) / fbs) * ((h + fbs - 1) / fbs);
+  k_cdef_apply<<<dim3(nfb, B), 256, 0, (hipStream_t)stream>>>(rec, w, h, chroma, dir, var, luma_w8, luma_n8, damping,
+                                                              fb_preset, out);
+  return av1_status("cdef_apply");
+}
+int tv_gpu_wiener_apply(const uint8_t* rec, int w, int h, int B, const int* coef, uint8_t* out, void* stream) {
+  if (bad_geo(w, h, B, 2, "wiener_apply")) return -1;
+  k_wiener_apply<<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(rec, w, h, coef, out);
+  return av1_status("wiener_apply");
+}
+int tv_gpu_wiener_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int B, int dir, const int* other,
+                        long long* stats, void* stream) {
+  if (bad_geo(w, h, B, 2, "wiener_stats")) return -1;
+  k_wiener_stats<<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, dir, other, stats);
+  return av1_status("wiener_stats");
+}
+int tv_gpu_sgr_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int B, int set, long long* stats,
+                     void* stream) {
+  if (bad_geo(w, h, B, 2, "sgr_stats") || set < 0 || set > 15) return -1;
+  k_sgr<true><<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, set, nullptr, stats, nullptr);
+  return av1_status("sgr_stats");
+}
+int tv_gpu_sgr_apply(const uint8_t* rec, int w, int h, int B, const int* params, uint8_t* out, void* stream) {
+  if (bad_geo(w, h, B, 2, "sgr_apply")) return -1;
+  k_sgr<false><<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(nullptr, rec, w, h, 0, params, nullptr, out);
+  return av1_status("sgr_apply");
+}
+}

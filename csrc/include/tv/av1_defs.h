@@ -1,0 +1,207 @@
+// av1_defs.h — AV1 in-loop filter arithmetic shared by the C++ golden model (av1_tools.cpp)
+// and the gfx950 kernels (k_av1.hip): CDEF direction search + filter, Wiener and
+// self-guided loop restoration (BASELINE config #4).
+//
+// Everything is integer and written once as TV_HD functions, so GPU == CPU bit for bit.
+// 8-bit video only (BitDepth 8: coeff_shift 0, InterRound0 3 / InterRound1 11).
+#pragma once
+#include <cstdint>
+
+#include "tv/hevc_defs.h"  // TV_HD, clip3, tv_abs
+
+namespace tv {
+namespace av1 {
+
+// ------------------------------------------------------------------------------ CDEF ----
+// Direction offsets (dy, dx) of the primary taps k = 0, 1 for the 8 directions.
+TV_HD int cdef_dir_dy(int d, int k) {
+  constexpr int8_t t[8][2] = {{-1, -2}, {0, -1}, {0, 0}, {0, 1}, {1, 2}, {1, 2}, {1, 2}, {1, 2}};
+  return t[d & 7][k];
+}
+TV_HD int cdef_dir_dx(int d, int k) {
+  constexpr int8_t t[8][2] = {{1, 2}, {1, 2}, {1, 2}, {1, 2}, {1, 2}, {0, 1}, {0, 0}, {0, -1}};
+  return t[d & 7][k];
+}
+TV_HD int floor_log2(unsigned v) { return v ? 31 - __builtin_clz(v) : -1; }
+
+// Partial-sum bin of pixel (i = row, j = col) of an 8x8 block for direction d.
+TV_HD int cdef_bin(int d, int i, int j) {
+  switch (d) {
+    case 0: return i + j;
+    case 1: return i + (j >> 1);
+    case 2: return i;
+    case 3: return 3 + i - (j >> 1);
+    case 4: return 7 + i - j;
+    case 5: return 3 - (i >> 1) + j;
+    case 6: return j;
+    default: return (i >> 1) + j;
+  }
+}
+
+// Direction cost from the 15 partial sums (of pixel - 128) of direction d.
+TV_HD int cdef_cost(const int* partial /* [15] */, int d) {
+  constexpr int div[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
+  int cost = 0;
+  if (d == 2 || d == 6) {
+    for (int i = 0; i < 8; ++i) cost += partial[i] * partial[i];
+    return cost * div[8];
+  }
+  if (d == 0 || d == 4) {
+    for (int i = 0; i < 7; ++i) cost += (partial[i] * partial[i] + partial[14 - i] * partial[14 - i]) * div[i + 1];
+    return cost + partial[7] * partial[7] * div[8];
+  }
+  for (int j = 0; j < 5; ++j) cost += partial[3 + j] * partial[3 + j];
+  cost *= div[8];
+  for (int j = 0; j < 3; ++j) cost += (partial[j] * partial[j] + partial[10 - j] * partial[10 - j]) * div[2 * j + 2];
+  return cost;
+}
+
+// best direction (first maximum) and variance from the 8 costs
+TV_HD int cdef_pick(const int* cost, int* var) {
+  int best = 0, bc = cost[0];
+  for (int d = 1; d < 8; ++d)
+    if (cost[d] > bc) {
+      bc = cost[d];
+      best = d;
+    }
+  *var = (bc - cost[(best + 4) & 7]) >> 10;
+  return best;
+}
+
+TV_HD int cdef_constrain(int diff, int threshold, int damping) {
+  if (!threshold) return 0;
+  const int adj = damping - floor_log2((unsigned)threshold);
+  const int a = tv_abs(diff);
+  int lim = threshold - (a >> (adj > 0 ? adj : 0));
+  lim = lim > 0 ? lim : 0;
+  const int v = a < lim ? a : lim;
+  return diff < 0 ? -v : v;
+}
+
+// luma primary strength adjusted by the block variance
+TV_HD int cdef_adjust_strength(int strength, int var) {
+  if (!var) return 0;
+  int i = (var >> 6) ? floor_log2((unsigned)(var >> 6)) : 0;
+  i = i < 12 ? i : 12;
+  return (strength * (4 + i) + 8) >> 4;
+}
+
+// Filter one pixel with value c.  get(dy, dx) returns the neighbour sample or -1 when it
+// is unavailable (outside the frame).  `pri`/`sec` are final strengths (sec in {0,1,2,4}).
+template <class G>
+TV_HD int cdef_filter(G get, int c, int pri, int sec, int damping, int dir) {
+  int sum = 0, mx = c, mn = c;
+  const int pt = pri & 1;
+  for (int k = 0; k < 2; ++k) {
+    const int ptap = pt ? 3 : (k ? 2 : 4);
+    const int stap = k ? 1 : 2;
+    for (int sg = -1; sg <= 1; sg += 2) {
+      if (pri) {
+        const int v = get(sg * cdef_dir_dy(dir, k), sg * cdef_dir_dx(dir, k));
+        if (v >= 0) {
+          sum += ptap * cdef_constrain(v - c, pri, damping);
+          mx = v > mx ? v : mx;
+          mn = v < mn ? v : mn;
+        }
+      }
+      if (!sec) continue;
+      for (int off = -2; off <= 2; off += 4) {
+        const int d2 = (dir + off) & 7;
+        const int v = get(sg * cdef_dir_dy(d2, k), sg * cdef_dir_dx(d2, k));
+        if (v >= 0) {
+          sum += stap * cdef_constrain(v - c, sec, damping);
+          mx = v > mx ? v : mx;
+          mn = v < mn ? v : mn;
+        }
+      }
+    }
+  }
+  const int y0 = c + ((8 + sum - (sum < 0)) >> 4);
+  return clip3(mn, mx, y0);
+}
+
+// plane form: pixel (x, y) of a w x h plane with pitch p
+TV_HD int cdef_filter_pixel(const uint8_t* P, int p, int w, int h, int x, int y, int pri, int sec, int damping,
+                            int dir) {
+  auto get = [=](int dy, int dx) -> int {
+    const int yy = y + dy, xx = x + dx;
+    return (xx >= 0 && xx < w && yy >= 0 && yy < h) ? (int)P[(long)yy * p + xx] : -1;
+  };
+  return cdef_filter(get, (int)P[(long)y * p + x], pri, sec, damping, dir);
+}
+
+// CDEF strength preset: index = pri * 4 + sec_idx; sec_idx 3 means strength 4.
+TV_HD int cdef_sec_value(int sec_idx) { return sec_idx == 3 ? 4 : sec_idx; }
+constexpr int kCdefPresets = 64;  // 16 primary x 4 secondary
+
+// ------------------------------------------------------------------ loop restoration ----
+constexpr int kWienerTaps = 7;
+constexpr int kRound0 = 3, kRound1 = 11;  // 8-bit: InterRound0 / InterRound1 (sum = 2 * FILTER_BITS)
+TV_HD int wiener_min(int k) { return k == 0 ? -5 : (k == 1 ? -23 : -17); }
+TV_HD int wiener_max(int k) { return k == 0 ? 10 : (k == 1 ? 8 : 46); }
+TV_HD int wiener_tap(const int* c3 /* c0, c1, c2 */, int t) {
+  if (t == 3) return 128 - 2 * (c3[0] + c3[1] + c3[2]);
+  return c3[t < 3 ? t : 6 - t];
+}
+// horizontal stage: value stored in the 16-bit intermediate; get(t) = sample at x + t - 3
+template <class G>
+TV_HD int wiener_h(G get, const int* hc) {
+  int s = 0;
+  for (int t = 0; t < kWienerTaps; ++t) s += wiener_tap(hc, t) * get(t);
+  const int off = 1 << (8 + 7 - kRound0 - 1), lim = (1 << (8 + 1 + 7 - kRound0)) - 1;
+  return clip3(-off, lim - off, (s + (1 << (kRound0 - 1))) >> kRound0);
+}
+// 1-D 7-tap filter of 8-bit samples back to the 8-bit scale (/128, no clipping): the fixed
+// direction of the separable Wiener least-squares passes
+template <class G>
+TV_HD int lr_tap_filter(G get, const int* c3) {
+  int s = 0;
+  for (int t = 0; t < kWienerTaps; ++t) s += wiener_tap(c3, t) * get(t);
+  return (s + 64) >> 7;
+}
+TV_HD int wiener_v(const int* col /* 7 intermediates, stride cs */, int cs, const int* vc) {
+  int s = 0;
+  for (int t = 0; t < kWienerTaps; ++t) s += wiener_tap(vc, t) * col[t * cs];
+  return clip3(0, 255, (s + (1 << (kRound1 - 1))) >> kRound1);
+}
+
+// Self-guided restoration: parameter sets {r0, e0, r1, e1}.
+TV_HD int sgr_param(int set, int k) {
+  constexpr int16_t t[16][4] = {{2, 140, 1, 3236}, {2, 112, 1, 2158}, {2, 93, 1, 1618}, {2, 80, 1, 1438},
+                                {2, 70, 1, 1295},  {2, 58, 1, 1177},  {2, 47, 1, 1079}, {2, 37, 1, 996},
+                                {2, 30, 1, 925},   {2, 25, 1, 863},   {0, -1, 1, 2589}, {0, -1, 1, 1618},
+                                {0, -1, 1, 1177},  {0, -1, 1, 925},   {2, 56, 0, -1},   {2, 22, 0, -1}};
+  return t[set & 15][k];
+}
+constexpr int kSgrMtableBits = 20, kSgrSgrBits = 8, kSgrRecipBits = 12, kSgrRstBits = 4, kSgrPrjBits = 7;
+
+// (a, b) guide coefficients of one pixel from its (2r+1)^2 box sum / square sum
+TV_HD void sgr_ab(int sum, int sq, int r, int eps, int* A, int* B) {
+  const int n = (2 * r + 1) * (2 * r + 1);
+  const int n2e = n * n * eps;
+  const unsigned s = ((1u << kSgrMtableBits) + (unsigned)(n2e / 2)) / (unsigned)n2e;
+  const long long p0 = (long long)sq * n - (long long)sum * sum;
+  const unsigned p = p0 > 0 ? (unsigned)p0 : 0u;
+  const unsigned z = (unsigned)(((unsigned long long)p * s + (1u << (kSgrMtableBits - 1))) >> kSgrMtableBits);
+  int a2;
+  if (z >= 255) a2 = 256;
+  else if (z == 0) a2 = 1;
+  else a2 = (int)(((z << kSgrSgrBits) + (z / 2)) / (z + 1));
+  const int one_over_n = ((1 << kSgrRecipBits) + n / 2) / n;
+  const long long b2 = (long long)((1 << kSgrSgrBits) - a2) * sum * one_over_n;
+  *A = a2;
+  *B = (int)((b2 + (1 << (kSgrRecipBits - 1))) >> kSgrRecipBits);
+}
+
+// projection of the two guided outputs (flt = filtered << RST_BITS domain) onto the pixel
+TV_HD int sgr_project(int x, int f0, int f1, int r0, int r1, int w0, int w1) {
+  const int u = x << kSgrRstBits;
+  int v = u << kSgrPrjBits;
+  if (r0) v += w0 * (f0 - u);
+  if (r1) v += w1 * (f1 - u);
+  const int s = kSgrRstBits + kSgrPrjBits;
+  return clip3(0, 255, (v + (1 << (s - 1))) >> s);
+}
+
+}  // namespace av1
+}  // namespace tv
