@@ -514,25 +514,52 @@ class SliceWriter {
     }
   }
 
+  // In-sub-block scan positions (packed x | y << 2) of scanIdx 0/1/2.
+  static const uint8_t* in_sb_scan(int scanIdx) {
+    return scanIdx == 0 ? kScanDiag4x4 : (scanIdx == 1 ? kScanHor4x4 : kScanVer4x4);
+  }
+  // sigCtx pattern (0..2) of the 16 scan positions for each prevCsbf (H.265 9.3.4.2.5),
+  // precomputed per scanIdx so the per-coefficient context is one table lookup.
+  struct SigPattern {
+    uint8_t p[3][4][16];
+    SigPattern() {
+      for (int sc = 0; sc < 3; ++sc)
+        for (int pc = 0; pc < 4; ++pc)
+          for (int n = 0; n < 16; ++n) {
+            const int xp = in_sb_scan(sc)[n] & 3, yp = in_sb_scan(sc)[n] >> 2;
+            int v;
+            if (pc == 0) v = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+            else if (pc == 1) v = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
+            else if (pc == 2) v = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
+            else v = 2;
+            p[sc][pc][n] = (uint8_t)v;
+          }
+    }
+  };
+
   void residual(const int16_t* blk, int stride, int log2N, int cIdx, int scanIdx) {
+    static const SigPattern kPat;
     const int nsb = 1 << (log2N - 2);  // sub-blocks per side
     const int numSb = nsb * nsb;
-    auto coef_at = [&](int xs, int ys, int n) -> int {
-      int xc, yc;
-      coef_pos_in_sb(scanIdx, n, xc, yc);
-      return blk[(size_t)((ys << 2) + yc) * stride + (xs << 2) + xc];
+    const uint8_t* ps = in_sb_scan(scanIdx);
+    int off[16];
+    for (int n = 0; n < 16; ++n) off[n] = (ps[n] >> 2) * stride + (ps[n] & 3);
+    auto sb_ptr = [&](int i, int& xs, int& ys) {
+      subblock_pos(log2N, scanIdx, i, xs, ys);
+      return blk + (size_t)(ys << 2) * stride + (xs << 2);
     };
     // last significant coefficient in scan order
     int lastSb = -1, lastN = -1;
-    for (int i = numSb - 1; i >= 0 && lastSb < 0; --i) {
+    for (int i = numSb - 1; i >= 0; --i) {
       int xs, ys;
-      subblock_pos(log2N, scanIdx, i, xs, ys);
-      for (int n = 15; n >= 0; --n)
-        if (coef_at(xs, ys, n) != 0) {
-          lastSb = i;
-          lastN = n;
-          break;
-        }
+      const int16_t* b = sb_ptr(i, xs, ys);
+      unsigned m = 0;
+      for (int n = 0; n < 16; ++n) m |= (unsigned)(b[off[n]] != 0) << n;
+      if (m) {
+        lastSb = i;
+        lastN = 31 - __builtin_clz(m);
+        break;
+      }
     }
     if (lastSb < 0) throw std::runtime_error("residual_coding of an all-zero block");
     {
@@ -546,16 +573,19 @@ class SliceWriter {
       write_last_suffix(lx);
       write_last_suffix(ly);
     }
+    // context offset added to the 0..2 pattern (H.265 9.3.4.2.5), per sub-block class
+    const int sizeOff = log2N == 3 ? (scanIdx == 0 ? 9 : 15) : (cIdx == 0 ? 21 : 12);
+    const int compOff = CTX_SIG + (cIdx ? 27 : 0);
     uint8_t csbf[8][8];
     std::memset(csbf, 0, sizeof(csbf));
     int c1 = 1;
     for (int i = lastSb; i >= 0; --i) {
       int xs, ys;
-      subblock_pos(log2N, scanIdx, i, xs, ys);
+      const int16_t* b = sb_ptr(i, xs, ys);
       int vals[16];
       bool any = false;
       for (int n = 0; n < 16; ++n) {
-        vals[n] = coef_at(xs, ys, n);
+        vals[n] = b[off[n]];
         any |= vals[n] != 0;
       }
       bool inferDc = false;
@@ -575,13 +605,20 @@ class SliceWriter {
       int prevCsbf = 0;
       if (xs < nsb - 1) prevCsbf += csbf[xs + 1][ys];
       if (ys < nsb - 1) prevCsbf += csbf[xs][ys + 1] << 1;
+      int ctxs[16];
+      if (log2N == 2) {
+        for (int n = 0; n < 16; ++n) ctxs[n] = compOff + kCtxIdxMap4x4[ps[n]];
+      } else {
+        const uint8_t* pat = kPat.p[scanIdx][prevCsbf];
+        const int add = compOff + sizeOff + ((cIdx == 0 && i > 0) ? 3 : 0);
+        for (int n = 0; n < 16; ++n) ctxs[n] = add + pat[n];
+        if (i == 0) ctxs[0] = compOff;  // DC of the TB
+      }
       const int nStart = (i == lastSb) ? lastN - 1 : 15;
       for (int n = nStart; n >= 0; --n) {
         if (n == 0 && inferDc) break;  // DC inferred significant
-        int xc, yc;
-        coef_pos_in_sb(scanIdx, n, xc, yc);
         const int sig = vals[n] != 0;
-        bin(sig, CTX_SIG + sig_ctx(log2N, cIdx, scanIdx, xs, ys, xc, yc, prevCsbf));
+        bin(sig, ctxs[n]);
         if (sig) inferDc = false;
       }
       // levels
@@ -609,7 +646,9 @@ class SliceWriter {
         }
       }
       if (firstG2 >= 0) bin(absv[firstG2] > 2, CTX_G2 + ctxSet + (cIdx ? 4 : 0));
-      for (int k = 0; k < cnt; ++k) enc_.encode_bypass(signs[k]);
+      uint32_t sbits = 0;
+      for (int k = 0; k < cnt; ++k) sbits = (sbits << 1) | (uint32_t)signs[k];
+      enc_.encode_bypass_bins(sbits, cnt);
       int rice = 0;
       bool firstC2 = true;
       for (int k = 0; k < cnt; ++k) {
@@ -621,24 +660,6 @@ class SliceWriter {
         if (absv[k] >= 2) firstC2 = false;
       }
     }
-  }
-
-  static int sig_ctx(int log2N, int cIdx, int scanIdx, int xs, int ys, int xp, int yp, int prevCsbf) {
-    int sigCtx;
-    if (log2N == 2) {
-      sigCtx = kCtxIdxMap4x4[(yp << 2) + xp];
-    } else if (xs == 0 && ys == 0 && xp == 0 && yp == 0) {
-      sigCtx = 0;
-    } else {
-      if (prevCsbf == 0) sigCtx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
-      else if (prevCsbf == 1) sigCtx = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
-      else if (prevCsbf == 2) sigCtx = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
-      else sigCtx = 2;
-      if (cIdx == 0 && (xs > 0 || ys > 0)) sigCtx += 3;
-      if (log2N == 3) sigCtx += (scanIdx == 0) ? 9 : 15;
-      else sigCtx += (cIdx == 0) ? 21 : 12;
-    }
-    return cIdx == 0 ? sigCtx : 27 + sigCtx;
   }
 
   const SeqConfig& cfg_;

@@ -37,11 +37,53 @@ __device__ inline void tb_load_matrix(int (*T)[33]) {
 // One 16x16 output tile P = X * Y (K = 16 or 32) on the calling wave.  X(i,k), Y(k,j) are
 // callables returning ints (exactly representable in f32).  When `split`, the operand
 // selected by `split_x` is decomposed into 8-bit halves and the tile recombined in int32.
+//
+// gfx950 path: the whole K = 32 (16) reduction is ONE v_mfma_f32_16x16x32_f16
+// (16x16x16f16) per split half.  Every operand is an integer of at most 9 bits (DCT basis
+// <= 90, residual / split halves within +-256), so it is exact in f16, every product is
+// exact in f32 and all partial sums stay below 2^24: bit-identical to the scalar model,
+// with 4-8x fewer matrix instructions than the f32 16x16x4 chain (TV_MFMA_F32 keeps that).
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
 template <class FX, class FY>
 __device__ __forceinline__ void mfma_tile(FX X, FY Y, int ti, int tj, int K, bool split, bool split_x,
                                           int out[4]) {
   const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
   f32x4 hi = {0.f, 0.f, 0.f, 0.f}, lo = {0.f, 0.f, 0.f, 0.f};
+#ifndef TV_MFMA_F32
+  if (K == 32) {
+    h8 a, b, a2, b2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * kq + e;
+      const int xv = X(16 * ti + i, k), yv = Y(k, 16 * tj + i);
+      const bool sx = split && split_x, sy = split && !split_x;
+      a[e] = (_Float16)(sx ? (xv >> 8) : xv);
+      a2[e] = (_Float16)(xv & 255);
+      b[e] = (_Float16)(sy ? (yv >> 8) : yv);
+      b2[e] = (_Float16)(yv & 255);
+    }
+    hi = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, hi, 0, 0, 0);
+    if (split) lo = split_x ? __builtin_amdgcn_mfma_f32_16x16x32_f16(a2, b, lo, 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b2, lo, 0, 0, 0);
+  } else {
+    h4 a, b, a2, b2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * kq + e;
+      const int xv = X(16 * ti + i, k), yv = Y(k, 16 * tj + i);
+      const bool sx = split && split_x, sy = split && !split_x;
+      a[e] = (_Float16)(sx ? (xv >> 8) : xv);
+      a2[e] = (_Float16)(xv & 255);
+      b[e] = (_Float16)(sy ? (yv >> 8) : yv);
+      b2[e] = (_Float16)(yv & 255);
+    }
+    hi = __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, hi, 0, 0, 0);
+    if (split) lo = split_x ? __builtin_amdgcn_mfma_f32_16x16x16f16(a2, b, lo, 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x16f16(a, b2, lo, 0, 0, 0);
+  }
+#else
   for (int kk = 0; kk < K; kk += 4) {
     const int xv = X(16 * ti + i, kk + kq), yv = Y(kk + kq, 16 * tj + i);
     if (!split) {
@@ -54,6 +96,7 @@ __device__ __forceinline__ void mfma_tile(FX X, FY Y, int ti, int tj, int K, boo
       lo = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv, (float)(yv & 255), lo, 0, 0, 0);
     }
   }
+#endif
 #pragma unroll
   for (int r = 0; r < 4; ++r) out[r] = split ? (int)hi[r] * 256 + (int)lo[r] : (int)hi[r];
 }
