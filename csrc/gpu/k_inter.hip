@@ -310,8 +310,31 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
   }
   if (threadIdx.x < 16) cbfs[threadIdx.x] = 0;
   __syncthreads();
+  // A CTB coded as one 32x32 CU: its luma TB would keep one wave busy for the whole
+  // kernel while the others idle after chroma, so all four waves code it together (one
+  // 16x16 MFMA tile each per stage), then two waves take the chroma TBs.
+  const bool whole = ncu == 1 && cus[0][2] == 5;
+  if (whole) {
+    const long u = ub + cus[0][3];
+    const int mvx = dec.mv[2 * u], mvy = dec.mv[2 * u + 1];
+    const uint8_t* P = ph + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
+    const uint8_t* S = src.plane(0, b, g);
+    uint8_t* pred = W[0].pred;
+    int16_t* resid = W[0].resid;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+      const int px = i & 31, py = i >> 5;
+      const int p = phase_at(P, g, cx + px + (mvx >> 2), cy + py + (mvy >> 2));
+      pred[i] = (uint8_t)p;
+      resid[i] = (int16_t)((int)S[(cy + py) * g.W + cx + px] - p);
+    }
+    __syncthreads();
+    const int cb = wg_code_tb(resid, pred, 5, qp, false, dec.coef_y + b * g.ysz + (long)cy * g.W + cx, g.W,
+                              rec.plane(0, b, g) + (long)cy * g.W + cx, g.W, Tm, W[1].tb.tmp, W[1].tb.coef,
+                              reinterpret_cast<int*>(W[2].resid));
+    if (threadIdx.x == 0 && cb) atomicOr(&cbfs[0], 1u);
+  }
   TbLds& Ld = W[wave];
-  for (int t = wave; t < 3 * ncu; t += 4) {
+  for (int t = whole ? wave + 1 : wave; t < 3 * ncu; t += whole ? 8 : 4) {
     const int k = t / 3, c = t - 3 * k;
     const int x0 = cus[k][0], y0 = cus[k][1], log2 = cus[k][2];
     const long u = ub + cus[k][3];

@@ -15,21 +15,9 @@ namespace gpu {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-struct TbScratch {
-  int T[32][33];     // DCT matrix (padded rows)
-  int tmp[32 * 33];  // stage intermediate (padded rows)
-  int coef[1024];
-  int red[4];
-};
-
-__device__ inline void tb_init(TbScratch& s) {
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) s.T[i >> 5][i & 31] = kDct32.m[i >> 5][i & 31];
-}
-
 __device__ __forceinline__ int tbT(const int (*T)[33], int log2N, int k, int n) {
   return T[k << (5 - log2N)][n];
 }
-__device__ __forceinline__ int tbT(const TbScratch& s, int log2N, int k, int n) { return tbT(s.T, log2N, k, n); }
 __device__ inline void tb_load_matrix(int (*T)[33]) {
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) T[i >> 5][i & 31] = kDct32.m[i >> 5][i & 31];
 }
@@ -127,58 +115,60 @@ __device__ __forceinline__ void tb_stage(int log2N, FX X, FY Y, bool split, bool
   }
 }
 
-// Code one TB.  resid/pred are LDS arrays (N*N row-major).  Writes levels to `lev`
+// Code one TB with the whole workgroup (each wave owns 16x16 output tiles of a stage;
+// workgroup barriers between stages).  resid/pred are LDS arrays (N*N row-major), tbm the
+// DCT matrix in LDS, `tmp`/`coef` LDS scratch, `red` 4 LDS ints.  Writes levels to `lev`
 // (stride ls) and reconstructed pixels to `rec` (stride rs).  Returns cbf (uniform).
-__device__ int wg_code_tb(const int* resid, const int* pred, int log2N, int qp, bool intra,
-                          int16_t* lev, int ls, uint8_t* rec, int rs, TbScratch& s) {
+// Same arithmetic as wave_code_tb (wave_tb.h) and tv::forward/inverse_transform.
+template <class PredT, class RecT>
+__device__ int wg_code_tb(const int16_t* resid, const PredT* pred, int log2N, int qp, bool intra, int16_t* lev,
+                          int ls, RecT* rec, int rs, const int (*tbm)[33], int* tmp, int* coef, int* red) {
   const int N = 1 << log2N, n2 = N * N, tid = threadIdx.x, nt = blockDim.x;
   const int sh1 = log2N - 1, sh2 = log2N + 6;
-  if (tid < 4) s.red[tid] = 0;
-  // forward stage 1: tmp[k][x] = (sum_y T[k][y] r[y][x] + rnd) >> sh1     (operands <= 8 bit)
+  if (tid < 4) red[tid] = 0;
+  // forward stage 1: tmp[k][x] = (sum_y T[k][y] r[y][x] + rnd) >> sh1     (operands <= 9 bit)
   tb_stage(
-      log2N, [&](int k, int y) { return tbT(s, log2N, k, y); }, [&](int y, int x) { return resid[y * N + x]; },
-      false, false, [&](int r, int c, int v) { s.tmp[r * 33 + c] = (v + (1 << (sh1 - 1))) >> sh1; });
+      log2N, [&](int k, int y) { return tbT(tbm, log2N, k, y); }, [&](int y, int x) { return (int)resid[y * N + x]; },
+      false, false, [&](int r, int c, int v) { tmp[r * 33 + c] = (v + (1 << (sh1 - 1))) >> sh1; });
   __syncthreads();
   // forward stage 2 + quantisation: coef[k][j] = (sum_x tmp[k][x] T[j][x] + rnd) >> sh2
   tb_stage(
-      log2N, [&](int k, int x) { return s.tmp[k * 33 + x]; }, [&](int x, int j) { return tbT(s, log2N, j, x); },
+      log2N, [&](int k, int x) { return tmp[k * 33 + x]; }, [&](int x, int j) { return tbT(tbm, log2N, j, x); },
       true, true, [&](int r, int c, int v) {
-        s.coef[r * N + c] = quant_level((v + (1 << (sh2 - 1))) >> sh2, qp, log2N, intra);
+        coef[r * N + c] = quant_level((v + (1 << (sh2 - 1))) >> sh2, qp, log2N, intra);
       });
   __syncthreads();
   int nz = 0, sa = 0;
   for (int i = tid; i < n2; i += nt) {
-    nz += s.coef[i] != 0;
-    sa += tv_abs(s.coef[i]);
+    nz += coef[i] != 0;
+    sa += tv_abs(coef[i]);
   }
   nz = wave_sum(nz);
   sa = wave_sum(sa);
   if ((tid & 63) == 0) {
-    atomicAdd(&s.red[0], nz);
-    atomicAdd(&s.red[1], sa);
+    atomicAdd(&red[0], nz);
+    atomicAdd(&red[1], sa);
   }
   __syncthreads();
-  if (tid == 0) s.red[2] = (!intra && s.red[0] == 1 && s.red[1] == 1 && s.coef[0] == 0) ? 0 : s.red[0];
-  __syncthreads();
-  const int NZ = s.red[2];
+  const int NZ = (!intra && red[0] == 1 && red[1] == 1 && coef[0] == 0) ? 0 : red[0];
   for (int i = tid; i < n2; i += nt) {
-    const int l = NZ ? s.coef[i] : 0;
+    const int l = NZ ? coef[i] : 0;
     lev[(i >> log2N) * ls + (i & (N - 1))] = (int16_t)l;
-    if (!NZ) rec[(i >> log2N) * rs + (i & (N - 1))] = (uint8_t)clip_pixel(pred[i]);
-    else s.coef[i] = dequant_level(l, qp, log2N);
+    if (!NZ) rec[(i >> log2N) * rs + (i & (N - 1))] = (RecT)clip_pixel((int)pred[i]);
+    else coef[i] = dequant_level(l, qp, log2N);
   }
   __syncthreads();
   if (!NZ) return 0;
   // inverse stage 1: tmp[y][x] = clip16((sum_k T[k][y] d[k][x] + 64) >> 7)   (split d)
   tb_stage(
-      log2N, [&](int y, int k) { return tbT(s, log2N, k, y); }, [&](int k, int x) { return s.coef[k * N + x]; },
-      true, false, [&](int r, int c, int v) { s.tmp[r * 33 + c] = clip3(-32768, 32767, (v + 64) >> 7); });
+      log2N, [&](int y, int k) { return tbT(tbm, log2N, k, y); }, [&](int k, int x) { return coef[k * N + x]; },
+      true, false, [&](int r, int c, int v) { tmp[r * 33 + c] = clip3(-32768, 32767, (v + 64) >> 7); });
   __syncthreads();
   // inverse stage 2: res[y][x] = (sum_k g[y][k] T[k][x] + 2048) >> 12            (split g)
   tb_stage(
-      log2N, [&](int y, int k) { return s.tmp[y * 33 + k]; }, [&](int k, int x) { return tbT(s, log2N, k, x); },
+      log2N, [&](int y, int k) { return tmp[y * 33 + k]; }, [&](int k, int x) { return tbT(tbm, log2N, k, x); },
       true, true, [&](int r, int c, int v) {
-        rec[r * rs + c] = (uint8_t)clip_pixel(pred[r * N + c] + ((v + 2048) >> 12));
+        rec[r * rs + c] = (RecT)clip_pixel((int)pred[r * N + c] + ((v + 2048) >> 12));
       });
   __syncthreads();
   return 1;
