@@ -474,3 +474,63 @@ int tv_av1_rc_roundtrip(const int* sym, const int* alpha, const int* ctx, int n,
   });
 }
 }
+
+// ================================================================ AV1 transforms ======
+#include "tv/av1_txfm.h"
+
+namespace tv {
+namespace av1 {
+namespace {
+inline int32_t rshift_round(int64_t v, int s) { return (int32_t)((v + (1LL << (s - 1))) >> s); }
+inline int32_t clamp16(int32_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+}  // namespace
+
+// Golden 2-D transform of nblk N x N blocks (row-major int16): forward (columns then rows)
+// or inverse (rows then columns), same integer stages as k_av1_txfm.hip.
+void txfm2d_ref(const int16_t* in, int16_t* out, int nblk, int log2N, int tcol, int trow, bool inverse) {
+  const int N = 1 << log2N;
+  if (!txfm_valid(tcol, N) || !txfm_valid(trow, N)) throw std::runtime_error("av1 txfm: bad type/size");
+  std::vector<int32_t> Bc(N * N), Br(N * N), t(N * N);
+  for (int k = 0; k < N; ++k)
+    for (int n = 0; n < N; ++n) {
+      Bc[k * N + n] = txfm_basis(tcol, N, k, n);
+      Br[k * N + n] = txfm_basis(trow, N, k, n);
+    }
+  int f1, f2, i1, i2;
+  txfm_shifts(log2N, f1, f2, i1, i2);
+  for (int b = 0; b < nblk; ++b) {
+    const int16_t* X = in + (size_t)b * N * N;
+    int16_t* Y = out + (size_t)b * N * N;
+    for (int r = 0; r < N; ++r)
+      for (int c = 0; c < N; ++c) {
+        int64_t s = 0;
+        for (int k = 0; k < N; ++k)
+          s += inverse ? (int64_t)X[r * N + k] * Br[k * N + c]    // g[r][c] = sum_j C[r][j] Br[j][c]
+                       : (int64_t)Bc[r * N + k] * X[k * N + c];   // tmp[r][c] = sum_y Bc[r][y] X[y][c]
+        t[r * N + c] = clamp16(rshift_round(s, inverse ? i1 : f1));
+      }
+    for (int r = 0; r < N; ++r)
+      for (int c = 0; c < N; ++c) {
+        int64_t s = 0;
+        for (int k = 0; k < N; ++k)
+          s += inverse ? (int64_t)Bc[k * N + r] * t[k * N + c]    // X[r][c] = sum_k Bc[k][r] g[k][c]
+                       : (int64_t)t[r * N + k] * Br[c * N + k];   // C[r][c] = sum_x tmp[r][x] Br[c][x]
+        Y[r * N + c] = (int16_t)clamp16(rshift_round(s, inverse ? i2 : f2));
+      }
+  }
+}
+
+}  // namespace av1
+}  // namespace tv
+
+extern "C" {
+int tv_av1_txfm_ref(const int16_t* in, int16_t* out, int nblk, int log2N, int tcol, int trow, int inverse) {
+  return av1_guard([&] { tv::av1::txfm2d_ref(in, out, nblk, log2N, tcol, trow, inverse != 0); });
+}
+int tv_av1_txfm_basis(int type, int N, int32_t* out) {
+  if (!tv::av1::txfm_valid(type, N)) return -1;
+  for (int k = 0; k < N; ++k)
+    for (int n = 0; n < N; ++n) out[k * N + n] = tv::av1::txfm_basis(type, N, k, n);
+  return 0;
+}
+}

@@ -266,3 +266,50 @@ def test_gpu_postfilter_equals_cpu():
     for a, b in zip(og, oc):
         np.testing.assert_array_equal(a[0].cpu().numpy(), b)
     assert rg["psnr_lr"] == pytest.approx(rc["psnr_lr"])
+
+
+# -------------------------------------------------------------------- transforms -------
+_TX = [(n, c, r) for n in (4, 8, 16, 32, 64) for c in ("dct", "adst", "flipadst", "idtx")
+       for r in ("dct", "adst", "idtx") if not ((c in ("adst", "flipadst") or r == "adst") and n > 16)
+       and not ((c == "idtx" or r == "idtx") and n > 32)]
+
+
+def test_txfm_basis_matches_av1_constants():
+    assert list(av1.txfm_basis("adst", 4)[0]) == [1321, 2482, 3344, 3803]  # AV1 sinpi(1..4)
+    d8 = av1.txfm_basis("dct", 8)
+    assert d8[0, 0] == 2896 and d8[1, 0] == 4017 and d8[2, 0] == 3784  # cospi 32, 4(56), 8(48)
+    assert av1.txfm_basis("idtx", 4)[0, 0] == 5793  # NewSqrt2
+    for n in (4, 8, 16, 32, 64):  # rows are orthogonal with norm 4096 sqrt(n/2)
+        b = av1.txfm_basis("dct", n).astype(np.float64)
+        g = b @ b.T / (4096.0 ** 2 * n / 2)
+        assert np.abs(g - np.eye(n)).max() < 2e-3
+
+
+@pytest.mark.parametrize("n,col,row", [t for t in _TX if t[0] <= 32])
+def test_txfm_roundtrip(n, col, row):
+    rng = np.random.default_rng(n)
+    x = rng.integers(-255, 256, (6, n, n)).astype(np.int16)
+    c = av1.txfm2d(x, col, row)
+    y = av1.txfm2d(c, col, row, inverse=True)
+    assert np.abs(y.astype(int) - x).max() <= 1
+    # energy compaction: a smooth ramp puts (nearly) everything into few DCT coefficients
+    if col == row == "dct":
+        ramp = np.add.outer(np.arange(n), np.arange(n)).astype(np.int16)[None] * (200 // (2 * n))
+        cc = np.abs(av1.txfm2d(ramp, col, row)[0].astype(np.int64)) ** 2
+        assert cc[:2, :2].sum() > 0.95 * cc.sum()
+
+
+@pytest.mark.gpu
+def test_gpu_txfm_bit_exact():
+    import torch
+
+    rng = np.random.default_rng(5)
+    for n, col, row in _TX:
+        x = rng.integers(-255, 256, (9, n, n)).astype(np.int16)
+        xg = torch.from_numpy(x).cuda()
+        cg = av1.txfm2d(xg, col, row)
+        cc = av1.txfm2d(x, col, row)
+        np.testing.assert_array_equal(cg.cpu().numpy(), cc, err_msg=f"fwd {n} {col} {row}")
+        ig = av1.txfm2d(cg, col, row, inverse=True)
+        np.testing.assert_array_equal(ig.cpu().numpy(), av1.txfm2d(cc, col, row, inverse=True),
+                                      err_msg=f"inv {n} {col} {row}")

@@ -439,3 +439,54 @@ def range_coder_roundtrip(symbols, alphabet, contexts, adapt: bool = True):
     if rc != 0:
         raise RuntimeError(lib.tv_av1_last_error().decode())
     return buf.tobytes(), dec
+
+
+# ------------------------------------------------------------------- transforms ----
+TX_TYPES = {"dct": 0, "adst": 1, "flipadst": 2, "idtx": 3}
+_basis_cache: dict = {}
+
+
+def txfm_basis(kind: str | int, n: int) -> np.ndarray:
+    """(n, n) int32 basis of a 1-D AV1 transform (row k = basis function k)."""
+    t = TX_TYPES.get(kind, kind)
+    out = np.zeros((n, n), np.int32)
+    lib = _core()
+    lib.tv_av1_txfm_basis.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_int32)]
+    if lib.tv_av1_txfm_basis(int(t), n, _p(out, C.c_int32)) != 0:
+        raise ValueError(f"unsupported transform {kind} x {n}")
+    return out
+
+
+def txfm2d(blocks, col: str = "dct", row: str = "dct", inverse: bool = False):
+    """Forward (columns then rows) or inverse AV1 2-D transform of N x N int16 blocks:
+    numpy (nblk, N, N) -> C++ golden model; torch cuda -> MFMA kernels (bit-identical)."""
+    tc, tr = TX_TYPES.get(col, col), TX_TYPES.get(row, row)
+    nblk, n, n2 = blocks.shape
+    if n != n2 or n not in (4, 8, 16, 32, 64):
+        raise ValueError("blocks must be (nblk, N, N) with N in 4..64")
+    log2n = n.bit_length() - 1
+    if _is_np(blocks):
+        x = np.ascontiguousarray(blocks, np.int16)
+        out = np.empty_like(x)
+        lib = _core()
+        lib.tv_av1_txfm_ref.argtypes = [C.POINTER(C.c_int16), C.POINTER(C.c_int16)] + [C.c_int] * 5
+        lib.tv_av1_txfm_ref.restype = C.c_int
+        if lib.tv_av1_txfm_ref(_p(x, C.c_int16), _p(out, C.c_int16), nblk, log2n, tc, tr, int(inverse)) != 0:
+            raise ValueError(lib.tv_av1_last_error().decode())
+        return out
+    import torch
+
+    key = (tc, tr, n, blocks.device)
+    if key not in _basis_cache:
+        _basis_cache[key] = (torch.from_numpy(txfm_basis(tc, n)).to(blocks.device),
+                             torch.from_numpy(txfm_basis(tr, n)).to(blocks.device))
+    bc, br = _basis_cache[key]
+    x = blocks.to(torch.int16).contiguous()
+    out = torch.empty_like(x)
+    lib = _gpu()
+    lib.tv_gpu_av1_txfm.restype = C.c_int
+    lib.tv_av1_txfm_last_error.restype = C.c_char_p
+    rc = lib.tv_gpu_av1_txfm(_t(x), _t(out), nblk, log2n, int(inverse), _t(bc), _t(br), _stream(x))
+    if rc != 0:
+        raise RuntimeError(lib.tv_av1_txfm_last_error().decode())
+    return out
