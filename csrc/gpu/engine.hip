@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -107,11 +108,13 @@ class ThreadPool {
 struct EngineCfg {
   int width, height, qp, batch, gop, range, deblock, threads, device, max_merge;
   uint32_t seed;
+  int groups;
 };
 
-class Engine {
+// One group of segments on its own HIP stream (buffers, pinned slot ring, events).
+class Core {
  public:
-  explicit Engine(const EngineCfg& c) : cfg_(c), g_(make_geo(c.width, c.height)) {
+  Core(const EngineCfg& c, ThreadPool* pool) : cfg_(c), g_(make_geo(c.width, c.height)), pool_(pool) {
     if (c.batch < 1 || c.batch > kMaxBatch) throw std::runtime_error("batch must be 1..64");
     if (c.range < 4 || c.range > 16 || (c.range & 3))
       throw std::runtime_error("search range must be 4, 8, 12 or 16");
@@ -167,11 +170,9 @@ class Engine {
     seq_.sao = (c.deblock & 2) != 0;
     seq_.max_merge_cand = c.max_merge;
     seq_.finalize();
-    pool_ = std::make_unique<ThreadPool>(c.threads, c.device);
   }
 
-  ~Engine() {
-    pool_.reset();
+  ~Core() {
     (void)hipStreamSynchronize(stream_);
     for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u, rec_[1].v,
                     deb_.y, deb_.u, deb_.v})
@@ -192,34 +193,8 @@ class Engine {
     (void)hipStreamDestroy(stream_);
   }
 
-  // Encode nseg segments of the synthetic source: segment b = frames [starts[b], +gop).
-  void encode_synth(const int* starts, int nseg) {
-    run(nseg, cfg_.gop, [&](int f, int B) {
-      FrameIdx fi{};
-      for (int b = 0; b < B; ++b) fi.t[b] = starts[b] + f;
-      launch_synth(src_, g_, cfg_.seed, fi, B, stream_);
-    });
-  }
-
-  // Encode nseg segments of nframes (1..gop) host frames each, coded-size planar I420 laid
-  // out [segment][frame][Y | U | V] (planes padded to the coded size by the caller).
-  void encode_host(const uint8_t* frames, int nseg, int nframes) {
-    const long fsz = g_.ysz + 2 * g_.csz;
-    run(nseg, nframes, [&](int f, int B) {
-      for (int b = 0; b < B; ++b) {
-        const uint8_t* p = frames + ((long)b * nframes + f) * fsz;
-        HIP_OK(hipMemcpyAsync(src_.y + b * g_.ysz, p, g_.ysz, hipMemcpyHostToDevice, stream_));
-        HIP_OK(hipMemcpyAsync(src_.u + b * g_.csz, p + g_.ysz, g_.csz, hipMemcpyHostToDevice, stream_));
-        HIP_OK(hipMemcpyAsync(src_.v + b * g_.csz, p + g_.ysz + g_.csz, g_.csz, hipMemcpyHostToDevice,
-                              stream_));
-      }
-    });
-  }
-
   const std::vector<uint8_t>& segment(int b) const { return out_.at(b); }
   double sse(int b, int c) const { return sse_host_[b * 3 + c]; }
-  double gpu_ms() const { return gpu_ms_; }
-  double wall_ms() const { return wall_ms_; }
   long coef_bytes() const { return coef_bytes_; }
   double entropy_ms() const { return entropy_ns_ / 1e6; }
   const Geo& geo() const { return g_; }
@@ -356,99 +331,120 @@ class Engine {
     coef_bytes_ += bytes;
   }
 
-  template <class Upload> void run(int nseg, int nframes, Upload&& upload) {
+
+ public:
+  // ---- one encode call, split so the Engine can interleave several cores' frames ----
+  void begin(int nseg, int nframes) {
     if (nseg < 1 || nseg > cfg_.batch) throw std::runtime_error("nseg out of range");
     if (nframes < 1 || nframes > cfg_.gop) throw std::runtime_error("nframes out of range");
-    const int B = nseg, F = nframes;
-    last_frames_ = F;
-    const auto w0 = std::chrono::steady_clock::now();
-    out_.assign(B, {});
+    B_ = nseg;
+    F_ = nframes;
+    last_frames_ = nframes;
+    out_.assign(B_, {});
     coef_bytes_ = 0;
     entropy_ns_ = 0;
-    std::vector<std::vector<std::vector<uint8_t>>> slices(B, std::vector<std::vector<uint8_t>>(F));
-    std::atomic<int> failed{0};
-    std::string err;
-    std::mutex err_mu;
-    auto fail = [&](const std::exception& e) {
-      std::lock_guard<std::mutex> lk(err_mu);
-      err = e.what();
-      failed = 1;
-    };
-    HIP_OK(hipMemsetAsync(d_sse_, 0, B * 3 * sizeof(unsigned long long), stream_));
+    slices_.assign(B_, std::vector<std::vector<uint8_t>>(F_));
+    failed_ = 0;
+    err_.clear();
+    HIP_OK(hipMemsetAsync(d_sse_, 0, B_ * 3 * sizeof(unsigned long long), stream_));
     HIP_OK(hipEventRecord(t0_, stream_));
-    for (int f = 0; f < F; ++f) {
-      Range frame_range(f == 0 ? "engine.frame.intra" : "engine.frame.inter");
-      Slot& s = slots_[f % kSlots];
-      while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
-      const DecisionSet dec = slot_dec(s);
-      upload(f, B);
-      FrameSet cur = rec_[f & 1], prev = rec_[(f + 1) & 1];
-      // TV_SYNC_DEBUG=1: synchronise and check after every stage (fault isolation)
-      auto stage = [&](const char* name) {
-        if (!sync_debug_) return;
-        const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(stream_);
-        if (e1 != hipSuccess || e2 != hipSuccess)
-          throw std::runtime_error(std::string("stage ") + name + " failed: " +
-                                   hipGetErrorString(e1 != hipSuccess ? e1 : e2));
-      };
-      stage("upload");
-      if (f == 0) launch_intra_frame(src_, cur, dec, g_, cfg_.qp, pen_, B, stream_);
-      else launch_inter_frame(src_, prev, phase_, cur, dec, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
-      stage(f == 0 ? "intra" : "inter");
-      launch_compact(dec, g_, slot_compact(s), B, stream_);
-      stage("compact");
-      if (seq_.deblock) launch_deblock(cur, dec, g_, cfg_.qp, B, stream_);
-      stage("deblock");
-      if (seq_.sao) launch_sao(src_, cur, deb_, carve(s.dev).sao, g_, cfg_.qp, B, stream_);
-      stage("sao");
-      if (f + 1 < F) launch_phase_planes(cur, phase_, g_, B, stream_);  // reference of f+1
-      stage("phase_planes");
-      launch_sse(src_, cur, g_, d_sse_, B, stream_);
-      stage("sse");
-      HIP_OK(hipGetLastError());
-      HIP_OK(hipEventRecord(s.ev, stream_));
-      s.pending.store(B + 1, std::memory_order_release);
-      pool_->submit([this, &s, B, f, &slices, &fail] {
-        try {
-          Range r("engine.d2h");
-          fetch_slot(s, B);
-        } catch (const std::exception& e) {
-          fail(e);
-          s.pending.fetch_sub(B + 1, std::memory_order_acq_rel);
-          return;
-        }
-        s.pending.fetch_sub(1, std::memory_order_acq_rel);
-        for (int b = 0; b < B; ++b)
-          pool_->submit([this, &s, b, f, &slices, &fail] {
-            try {
-              Range r("engine.cabac_slice");
-              const auto c0 = std::chrono::steady_clock::now();
-              write_slice(seq_, host_view(s, b), f, f == 0, slices[b][f]);
-              entropy_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                 std::chrono::steady_clock::now() - c0).count();
-            } catch (const std::exception& e) {
-              fail(e);
-            }
-            s.pending.fetch_sub(1, std::memory_order_acq_rel);
-          });
-      });
-    }
-    HIP_OK(hipEventRecord(t1_, stream_));
+  }
+
+  // Enqueue frame f of every segment (upload(f, B) fills src_ on stream()), then hand its
+  // decisions to the CABAC pool.  Blocks only when the slot ring is full.
+  template <class Upload> void issue(int f, Upload&& upload) {
+    const int B = B_, F = F_;
+    Range frame_range(f == 0 ? "engine.frame.intra" : "engine.frame.inter");
+    Slot& s = slots_[f % kSlots];
+    while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    const DecisionSet dec = slot_dec(s);
+    upload(f, B);
+    FrameSet cur = rec_[f & 1], prev = rec_[(f + 1) & 1];
+    // TV_SYNC_DEBUG=1: synchronise and check after every stage (fault isolation)
+    auto stage = [&](const char* name) {
+      if (!sync_debug_) return;
+      const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(stream_);
+      if (e1 != hipSuccess || e2 != hipSuccess)
+        throw std::runtime_error(std::string("stage ") + name + " failed: " +
+                                 hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+    };
+    stage("upload");
+    if (f == 0) launch_intra_frame(src_, cur, dec, g_, cfg_.qp, pen_, B, stream_);
+    else launch_inter_frame(src_, prev, phase_, cur, dec, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
+    stage(f == 0 ? "intra" : "inter");
+    launch_compact(dec, g_, slot_compact(s), B, stream_);
+    stage("compact");
+    if (seq_.deblock) launch_deblock(cur, dec, g_, cfg_.qp, B, stream_);
+    stage("deblock");
+    if (seq_.sao) launch_sao(src_, cur, deb_, carve(s.dev).sao, g_, cfg_.qp, B, stream_);
+    stage("sao");
+    if (f + 1 < F) launch_phase_planes(cur, phase_, g_, B, stream_);  // reference of f+1
+    stage("phase_planes");
+    launch_sse(src_, cur, g_, d_sse_, B, stream_);
+    stage("sse");
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(s.ev, stream_));
+    s.pending.store(B + 1, std::memory_order_release);
+    pool_->submit([this, &s, B, f] {
+      try {
+        Range r("engine.d2h");
+        fetch_slot(s, B);
+      } catch (const std::exception& e) {
+        fail(e);
+        s.pending.fetch_sub(B + 1, std::memory_order_acq_rel);
+        return;
+      }
+      s.pending.fetch_sub(1, std::memory_order_acq_rel);
+      for (int b = 0; b < B; ++b)
+        pool_->submit([this, &s, b, f] {
+          try {
+            Range r("engine.cabac_slice");
+            const auto c0 = std::chrono::steady_clock::now();
+            write_slice(seq_, host_view(s, b), f, f == 0, slices_[b][f]);
+            entropy_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now() - c0).count();
+          } catch (const std::exception& e) {
+            fail(e);
+          }
+          s.pending.fetch_sub(1, std::memory_order_acq_rel);
+        });
+    });
+  }
+
+  void end_record() { HIP_OK(hipEventRecord(t1_, stream_)); }
+
+  void finish() {
     for (auto& s : slots_)
       while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
     HIP_OK(hipStreamSynchronize(stream_));
-    if (failed) throw std::runtime_error("encode failed: " + err);
-    float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, t0_, t1_));
-    gpu_ms_ = ms;
-    std::vector<unsigned long long> sse(B * 3);
-    HIP_OK(hipMemcpy(sse.data(), d_sse_, B * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (failed_) throw std::runtime_error("encode failed: " + err_);
+    std::vector<unsigned long long> sse(B_ * 3);
+    HIP_OK(hipMemcpy(sse.data(), d_sse_, B_ * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     sse_host_.assign(sse.begin(), sse.end());
-    for (int b = 0; b < B; ++b) {
+    for (int b = 0; b < B_; ++b) {
       write_parameter_sets(seq_, out_[b]);
-      for (int f = 0; f < F; ++f) out_[b].insert(out_[b].end(), slices[b][f].begin(), slices[b][f].end());
+      for (int f = 0; f < F_; ++f) out_[b].insert(out_[b].end(), slices_[b][f].begin(), slices_[b][f].end());
     }
-    wall_ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+  }
+
+  // Single-core encode (groups == 1)
+  template <class Upload> void run(int nseg, int nframes, Upload&& upload) {
+    begin(nseg, nframes);
+    for (int f = 0; f < nframes; ++f) issue(f, upload);
+    end_record();
+    finish();
+  }
+
+  FrameSet src() const { return src_; }
+  hipEvent_t t0() const { return t0_; }
+  hipEvent_t t1() const { return t1_; }
+  long entropy_ns() const { return entropy_ns_; }
+
+ private:
+  void fail(const std::exception& e) {
+    std::lock_guard<std::mutex> lk(err_mu_);
+    err_ = e.what();
+    failed_ = 1;
   }
 
   EngineCfg cfg_;
@@ -471,12 +467,127 @@ class Engine {
   Slot slots_[kSlots];
   long slot_bytes_ = 0;
   hipEvent_t t0_{}, t1_{};
-  std::unique_ptr<ThreadPool> pool_;
+  ThreadPool* pool_;
+  int B_ = 0, F_ = 0;
+  std::vector<std::vector<std::vector<uint8_t>>> slices_;
+  std::atomic<int> failed_{0};
+  std::string err_;
+  std::mutex err_mu_;
   std::vector<std::vector<uint8_t>> out_;
   std::vector<double> sse_host_;
-  double gpu_ms_ = 0, wall_ms_ = 0;
   std::atomic<long> coef_bytes_{0};
   std::atomic<long> entropy_ns_{0};
+};
+
+// The engine: `groups` cores, each owning batch/groups segments on its own stream.  Frame f
+// of core g is issued in host step f + g, so the cores run one frame apart: while one
+// core's I-frame CTB wavefront (latency-bound, ~1 wave per CU) runs, the other cores'
+// motion search / reconstruction kernels fill the rest of the GPU.
+class Engine {
+ public:
+  explicit Engine(const EngineCfg& c) : cfg_(c) {
+    if (c.batch < 1 || c.batch > kMaxBatch) throw std::runtime_error("batch must be 1..64");
+    HIP_OK(hipSetDevice(c.device));
+    int G = c.groups < 1 ? 1 : c.groups;
+    if (G > c.batch) G = c.batch;
+    per_ = (c.batch + G - 1) / G;
+    G = (c.batch + per_ - 1) / per_;
+    pool_ = std::make_unique<ThreadPool>(c.threads, c.device);
+    for (int g = 0; g < G; ++g) {
+      EngineCfg cc = c;
+      cc.batch = std::min(per_, c.batch - g * per_);
+      cores_.push_back(std::make_unique<Core>(cc, pool_.get()));
+    }
+  }
+  ~Engine() {
+    cores_.clear();
+    pool_.reset();
+  }
+
+  // Encode nseg segments of the synthetic source: segment b = frames [starts[b], +gop).
+  void encode_synth(const int* starts, int nseg) {
+    run(nseg, cfg_.gop, [&](Core& core, int b0, int f, int B) {
+      FrameIdx fi{};
+      for (int b = 0; b < B; ++b) fi.t[b] = starts[b0 + b] + f;
+      launch_synth(core.src(), core.geo(), cfg_.seed, fi, B, core.stream());
+    });
+  }
+
+  // Encode nseg segments of nframes (1..gop) host frames each, coded-size planar I420 laid
+  // out [segment][frame][Y | U | V] (planes padded to the coded size by the caller).
+  void encode_host(const uint8_t* frames, int nseg, int nframes) {
+    run(nseg, nframes, [&](Core& core, int b0, int f, int B) {
+      const Geo& g = core.geo();
+      const long fsz = g.ysz + 2 * g.csz;
+      const FrameSet src = core.src();
+      for (int b = 0; b < B; ++b) {
+        const uint8_t* p = frames + ((long)(b0 + b) * nframes + f) * fsz;
+        HIP_OK(hipMemcpyAsync(src.y + b * g.ysz, p, g.ysz, hipMemcpyHostToDevice, core.stream()));
+        HIP_OK(hipMemcpyAsync(src.u + b * g.csz, p + g.ysz, g.csz, hipMemcpyHostToDevice, core.stream()));
+        HIP_OK(hipMemcpyAsync(src.v + b * g.csz, p + g.ysz + g.csz, g.csz, hipMemcpyHostToDevice,
+                              core.stream()));
+      }
+    });
+  }
+
+  const std::vector<uint8_t>& segment(int b) const { return core_of(b).segment(b % per_); }
+  double sse(int b, int c) const { return core_of(b).sse(b % per_, c); }
+  double gpu_ms() const { return gpu_ms_; }
+  double wall_ms() const { return wall_ms_; }
+  long coef_bytes() const {
+    long n = 0;
+    for (int g = 0; g < used_; ++g) n += cores_[g]->coef_bytes();
+    return n;
+  }
+  double entropy_ms() const {
+    double n = 0;
+    for (int g = 0; g < used_; ++g) n += cores_[g]->entropy_ms();
+    return n;
+  }
+  const Geo& geo() const { return cores_[0]->geo(); }
+  FrameSet last_recon(int b, int& local) const {
+    local = b % per_;
+    return core_of(b).last_recon();
+  }
+
+ private:
+  const Core& core_of(int b) const {
+    if (b < 0 || b / per_ >= used_) throw std::runtime_error("segment index out of range");
+    return *cores_[b / per_];
+  }
+  template <class Upload> void run(int nseg, int nframes, Upload&& upload) {
+    if (nseg < 1 || nseg > cfg_.batch) throw std::runtime_error("nseg out of range");
+    const auto w0 = std::chrono::steady_clock::now();
+    used_ = (nseg + per_ - 1) / per_;
+    for (int g = 0; g < used_; ++g) cores_[g]->begin(std::min(per_, nseg - g * per_), nframes);
+    for (int t = 0; t < nframes + used_ - 1; ++t)
+      for (int g = 0; g < used_; ++g) {
+        const int f = t - g;
+        if (f < 0 || f >= nframes) continue;
+        Core& core = *cores_[g];
+        core.issue(f, [&](int ff, int B) { upload(core, g * per_, ff, B); });
+        if (f == nframes - 1) core.end_record();
+      }
+    std::string err;
+    for (int g = 0; g < used_; ++g) {
+      try {
+        cores_[g]->finish();
+      } catch (const std::exception& e) {
+        if (err.empty()) err = e.what();
+      }
+    }
+    if (!err.empty()) throw std::runtime_error(err);
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, cores_[0]->t0(), cores_[used_ - 1]->t1()));
+    gpu_ms_ = ms;
+    wall_ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+  }
+
+  EngineCfg cfg_;
+  int per_ = 1, used_ = 0;
+  std::unique_ptr<ThreadPool> pool_;
+  std::vector<std::unique_ptr<Core>> cores_;
+  double gpu_ms_ = 0, wall_ms_ = 0;
 };
 
 }  // namespace gpu
@@ -509,7 +620,10 @@ void* tv_engine_new(int width, int height, int qp, int batch, int gop, int range
                     uint32_t seed, int threads, int device, int max_merge) {
   void* r = nullptr;
   gguard([&] {
-    tv::gpu::EngineCfg c{width, height, qp, batch, gop, range, deblock, threads, device, max_merge, seed};
+    // TV_ENGINE_GROUPS: segment groups on separate streams, one frame apart (default 2)
+    const char* ge = getenv("TV_ENGINE_GROUPS");
+    const int groups = ge ? std::max(1, atoi(ge)) : (batch >= 2 ? 2 : 1);
+    tv::gpu::EngineCfg c{width, height, qp, batch, gop, range, deblock, threads, device, max_merge, seed, groups};
     r = new tv::gpu::Engine(c);
   });
   return r;
@@ -541,10 +655,11 @@ int tv_engine_last_recon(void* e, int b, uint8_t* y, uint8_t* u, uint8_t* v) {
   return gguard([&] {
     auto* E = static_cast<tv::gpu::Engine*>(e);
     const auto& g = E->geo();
-    auto r = E->last_recon();
-    HIP_OK(hipMemcpy(y, r.y + b * g.ysz, g.ysz, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(u, r.u + b * g.csz, g.csz, hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(v, r.v + b * g.csz, g.csz, hipMemcpyDeviceToHost));
+    int lb = 0;
+    auto r = E->last_recon(b, lb);
+    HIP_OK(hipMemcpy(y, r.y + lb * g.ysz, g.ysz, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(u, r.u + lb * g.csz, g.csz, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(v, r.v + lb * g.csz, g.csz, hipMemcpyDeviceToHost));
   });
 }
 }
