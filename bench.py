@@ -60,8 +60,10 @@ def main() -> None:
 
     w, h = RES[args.res]
     # segments per GPU: enough CTBs per wavefront diagonal of the I-frame recon and per
-    # motion-search launch to fill 256 CUs (measured: 1080p 8 -> 32 segments = +47 %)
-    batch = args.batch or (32 if args.res in ("1080p", "720p", "360p") else 16)
+    # motion-search launch to fill 256 CUs (measured: 1080p 8 -> 32 segments = +47 %); the
+    # engine splits them into two stream groups one frame apart (measured on MI355X:
+    # 1080p 32 -> 48 segments +3 %, 4K 16 -> 24 segments +9 %; profiles/README.md)
+    batch = args.batch or (48 if args.res in ("1080p", "720p", "360p") else 24)
     eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=args.sao,
                     seed=args.seed, threads=args.threads or None, device=local)
 
