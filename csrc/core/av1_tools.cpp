@@ -239,6 +239,31 @@ void sgr_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int set, in
 }
 
 // ================================================================== range coder ======
+
+// ---------------------------------------------------------------- deblocking loop filter ----
+// AV1 7.14: every vertical edge of the plane (pass 0), then every horizontal edge (pass 1).
+// Edges of one pass never share a tap (a size-n filter needs tx >= n on both sides), so the
+// raster order inside a pass does not matter; the GPU kernel relies on the same property.
+void deblock(const uint8_t* in, int w, int h, bool chroma, const uint32_t* info, int sharp, uint8_t* out) {
+  if (w % 4 || h % 4) throw std::invalid_argument("deblock: plane dims must be multiples of 4");
+  std::memcpy(out, in, (size_t)w * h);
+  const int w4 = w / 4;
+  for (int y = 0; y < h; ++y)
+    for (int x = 4; x < w; x += 4) {
+      const uint32_t* row = info + (size_t)(y / 4) * w4;
+      int lvl = 0;
+      const int size = lf_edge(row[x / 4 - 1], row[x / 4], x, w, 0, chroma, &lvl);
+      if (size) lf_filter(out + (size_t)y * w + x, 1, size, lvl, sharp);
+    }
+  for (int y = 4; y < h; y += 4)
+    for (int x = 0; x < w; ++x) {
+      int lvl = 0;
+      const int size = lf_edge(info[(size_t)(y / 4 - 1) * w4 + x / 4], info[(size_t)(y / 4) * w4 + x / 4], y, h, 1,
+                               chroma, &lvl);
+      if (size) lf_filter(out + (size_t)y * w + x, w, size, lvl, sharp);
+    }
+}
+
 void cdf_init_uniform(uint16_t* icdf, int n) {
   if (n < 2 || n > 16) throw std::runtime_error("cdf: 2..16 symbols");
   for (int i = 0; i < n; ++i) icdf[i] = (uint16_t)(32768 - ((i + 1) * 32768 + n / 2) / n);
@@ -437,6 +462,9 @@ void tv_av1_sgr_apply(const uint8_t* rec, int w, int h, const int* params, uint8
 }
 void tv_av1_sgr_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int set, int64_t* stats) {
   sgr_stats(src, rec, w, h, set, stats);
+}
+int tv_av1_deblock(const uint8_t* in, int w, int h, int chroma, const uint32_t* info, int sharp, uint8_t* out) {
+  return av1_guard([&] { deblock(in, w, h, chroma != 0, info, sharp, out); });
 }
 void tv_av1_sgr_filter_planes(const uint8_t* rec, int w, int h, int set, int32_t* f0, int32_t* f1) {
   sgr_filter_planes(rec, w, h, set, f0, f1);

@@ -346,6 +346,55 @@ __global__ void __launch_bounds__(256) k_sgr(const uint8_t* __restrict__ src, co
   }
 }
 
+// ----------------------------------------------------------------- deblocking filter ----
+// k_deblock: one workgroup per 64x64 output tile.  The tile plus an 8-pixel ring is staged
+// in LDS once (dword loads); the vertical edges x0..x0+64 are filtered on all 80 rows (the
+// ring rows feed the horizontal taps), then the horizontal edges y0..y0+64 on the tile's
+// 64 columns, and the 64x64 interior is written back — both passes of AV1 7.14 in one
+// launch with one HBM read and one write per pixel.  Edges of a pass never share taps
+// (av1_defs.h lf_edge), so every (line, edge) item of a pass is independent.
+constexpr int kLfT = 64, kLfR = 8, kLfP = kLfT + 2 * kLfR;  // tile, ring, LDS pitch (80)
+
+__global__ void __launch_bounds__(256) k_deblock(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int w,
+                                                 int h, int chroma, const uint32_t* __restrict__ info, int sharp) {
+  __shared__ __attribute__((aligned(16))) uint8_t T[kLfP * kLfP];
+  const int x0 = blockIdx.x * kLfT, y0 = blockIdx.y * kLfT, b = blockIdx.z, w4 = w >> 2;
+  const uint8_t* P = in + (long)b * w * h;
+  const uint32_t* I = info + (long)b * w4 * (h >> 2);
+  for (int i = threadIdx.x; i < kLfP * (kLfP / 4); i += blockDim.x) {
+    const int r = i / (kLfP / 4), c4 = i - r * (kLfP / 4), y = y0 - kLfR + r, x = x0 - kLfR + c4 * 4;
+    uint32_t v = 0;
+    if (y >= 0 && y < h && x >= 0 && x < w) v = *(const uint32_t*)(P + (long)y * w + x);
+    *(uint32_t*)(T + r * kLfP + c4 * 4) = v;
+  }
+  __syncthreads();
+  // pass 0: 17 vertical edges (x0 .. x0+64) x 80 rows; item = edge * 80 + row
+  for (int i = threadIdx.x; i < (kLfT / 4 + 1) * kLfP; i += blockDim.x) {
+    const int e = i / kLfP, r = i - e * kLfP, y = y0 - kLfR + r, x = x0 + e * 4;
+    if (y < 0 || y >= h || x >= w) continue;
+    const uint32_t* row = I + (long)(y >> 2) * w4;
+    int lvl = 0;
+    const int size = lf_edge(x > 0 ? row[(x >> 2) - 1] : 0u, row[x >> 2], x, w, 0, chroma, &lvl);
+    if (size) lf_filter(T + r * kLfP + kLfR + e * 4, 1, size, lvl, sharp);
+  }
+  __syncthreads();
+  // pass 1: 17 horizontal edges (y0 .. y0+64) x 64 columns; item = edge * 64 + column
+  for (int i = threadIdx.x; i < (kLfT / 4 + 1) * kLfT; i += blockDim.x) {
+    const int e = i / kLfT, c = i - e * kLfT, y = y0 + e * 4, x = x0 + c;
+    if (y >= h || x >= w) continue;
+    int lvl = 0;
+    const int size = lf_edge(y > 0 ? I[(long)((y >> 2) - 1) * w4 + (x >> 2)] : 0u, I[(long)(y >> 2) * w4 + (x >> 2)],
+                             y, h, 1, chroma, &lvl);
+    if (size) lf_filter(T + (kLfR + e * 4) * kLfP + kLfR + c, kLfP, size, lvl, sharp);
+  }
+  __syncthreads();
+  uint8_t* O = out + (long)b * w * h;
+  for (int i = threadIdx.x; i < kLfT * (kLfT / 4); i += blockDim.x) {
+    const int r = i / (kLfT / 4), c4 = i - r * (kLfT / 4), y = y0 + r, x = x0 + c4 * 4;
+    if (y < h && x < w) *(uint32_t*)(O + (long)y * w + x) = *(const uint32_t*)(T + (kLfR + r) * kLfP + kLfR + c4 * 4);
+  }
+}
+
 thread_local std::string g_av1_gpu_err;
 int av1_status(const char* what) {
   const hipError_t e = hipGetLastError();
@@ -411,6 +460,14 @@ int tv_gpu_sgr_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int B
   if (bad_geo(w, h, B, 2, "sgr_stats") || set < 0 || set > 15) return -1;
   k_sgr<true><<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, set, nullptr, stats, nullptr);
   return av1_status("sgr_stats");
+}
+// B planes (w, h multiples of 4), info [B][h/4][w/4] (av1_defs.h layout), sharp 0..7
+int tv_gpu_av1_deblock(const uint8_t* in, uint8_t* out, int w, int h, int B, int chroma, const uint32_t* info,
+                       int sharp, void* stream) {
+  if (bad_geo(w, h, B, 4, "av1_deblock") || sharp < 0 || sharp > 7) return -1;
+  k_deblock<<<dim3((w + kLfT - 1) / kLfT, (h + kLfT - 1) / kLfT, B), 256, 0, (hipStream_t)stream>>>(in, out, w, h,
+                                                                                                  chroma, info, sharp);
+  return av1_status("av1_deblock");
 }
 int tv_gpu_sgr_apply(const uint8_t* rec, int w, int h, int B, const int* params, uint8_t* out, void* stream) {
   if (bad_geo(w, h, B, 2, "sgr_apply")) return -1;

@@ -39,6 +39,11 @@ void sgr_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int set, in
 // The two guided-filter outputs (RST domain) of one plane, for tests / the GPU check.
 void sgr_filter_planes(const uint8_t* rec, int w, int h, int set, int32_t* f0, int32_t* f1);
 
+// ---- deblocking loop filter (AV1 7.14) -------------------------------------------------
+// Filter every tx edge of a plane: `info` holds one word per 4x4 unit (layout in
+// av1_defs.h: tx / block log2 sizes, per-direction levels, skip && inter); sharp 0..7.
+void deblock(const uint8_t* in, int w, int h, bool chroma, const uint32_t* info, int sharp, uint8_t* out);
+
 // ---- multi-symbol range coder -------------------------------------------------------------
 // Probabilities are AV1 inverse CDFs: icdf[i] = 32768 * P(X > i), icdf[n-1] = 0, plus one
 // adaptation counter at icdf[n] (n <= 16).

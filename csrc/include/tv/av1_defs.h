@@ -203,5 +203,98 @@ TV_HD int sgr_project(int x, int f0, int f1, int r0, int r1, int w0, int w1) {
   return clip3(0, 255, (v + (1 << (s - 1))) >> s);
 }
 
+
+// ------------------------------------------------------------ deblocking loop filter ----
+// One 32-bit info word per 4x4 unit of a plane (row-major, w/4 per row):
+//   bits 0-2  log2(tx width) - 2      bits 3-5   log2(tx height) - 2
+//   bits 6-8  log2(block width) - 2   bits 9-11  log2(block height) - 2
+//   bits 12-17 filter level for vertical edges, 18-23 for horizontal edges (0..63)
+//   bit 24    skip && is_inter (internal tx edges of such blocks are not filtered)
+// Transform and coding blocks are aligned to their size (true for every AV1 partition), so
+// "x is a tx / block edge" is x % size == 0.
+TV_HD int lf_tx(uint32_t i, int pass) { return 4 << ((i >> (pass ? 3 : 0)) & 7); }
+TV_HD int lf_bs(uint32_t i, int pass) { return 4 << ((i >> (pass ? 9 : 6)) & 7); }
+TV_HD int lf_lvl(uint32_t i, int pass) { return (int)((i >> (pass ? 18 : 12)) & 63); }
+
+// Filter length of the edge between 4x4 units `prev` (p side) and `cur` (q side) whose q
+// side starts at `pos` (x for pass 0 = vertical edges, y for pass 1) in a plane of extent
+// `dim` along the filter: 0 = not filtered, else 4 / 6 (chroma) / 8 / 16 (luma 13-tap).
+// AV1 7.14.2 / 7.14.3: tx edge, block edge or not (skip && inter), level fallback to the
+// p side, size = min of both tx sizes capped at 16 (luma) / 6 (chroma).  Sizes are also
+// capped so the taps stay inside the plane (only reachable with a tx map crossing the
+// frame edge).
+TV_HD int lf_edge(uint32_t prev, uint32_t cur, int pos, int dim, int pass, int chroma, int* lvl) {
+  const int ts = lf_tx(cur, pass);
+  if (pos <= 0 || pos % ts) return 0;
+  if ((cur >> 24 & 1) && pos % lf_bs(cur, pass)) return 0;
+  int l = lf_lvl(cur, pass);
+  if (!l) l = lf_lvl(prev, pass);
+  if (!l) return 0;
+  *lvl = l;
+  const int ps = lf_tx(prev, pass);
+  int fs = ts < ps ? ts : ps;
+  if (chroma) return fs >= 8 && pos >= 3 && pos + 3 <= dim ? 6 : 4;
+  if (fs >= 16 && pos >= 7 && pos + 7 <= dim) return 16;
+  if (fs >= 8 && pos >= 4 && pos + 4 <= dim) return 8;
+  return 4;
+}
+
+TV_HD int lf_s8(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+
+// AV1 7.14.6: filter one line of an edge.  q0 points at the first q-side pixel, `step` is
+// the distance between taps (1 for a vertical edge, the pitch for a horizontal one).
+TV_HD void lf_filter(uint8_t* q0, int step, int size, int lvl, int sharp) {
+  const int shift = sharp > 4 ? 2 : (sharp > 0 ? 1 : 0);
+  int limit = lvl >> shift;
+  limit = sharp > 0 ? clip3(1, 9 - sharp, limit) : (limit < 1 ? 1 : limit);
+  const int blimit = 2 * (lvl + 2) + limit, thresh = lvl >> 4;
+  const int nr = size == 16 ? 7 : (size == 8 ? 4 : (size == 6 ? 3 : 2));  // taps read per side
+  int p[7], q[7];
+  for (int k = 0; k < nr; ++k) {
+    q[k] = q0[k * step];
+    p[k] = q0[-(k + 1) * step];
+  }
+  const int lm = size == 4 ? 2 : (size == 6 ? 3 : 4);
+  bool mask = tv_abs(p[0] - q[0]) * 2 + (tv_abs(p[1] - q[1]) >> 1) <= blimit;
+  for (int k = 1; k < lm; ++k) mask = mask && tv_abs(p[k] - p[k - 1]) <= limit && tv_abs(q[k] - q[k - 1]) <= limit;
+  if (!mask) return;
+  bool flat = size >= 6;
+  for (int k = 1; k < lm && flat; ++k) flat = tv_abs(p[k] - p[0]) <= 1 && tv_abs(q[k] - q[0]) <= 1;
+  if (!flat) {  // narrow filter (7.14.6.3)
+    const bool hev = tv_abs(p[1] - p[0]) > thresh || tv_abs(q[1] - q[0]) > thresh;
+    const int ps1 = p[1] - 128, ps0 = p[0] - 128, qs0 = q[0] - 128, qs1 = q[1] - 128;
+    int f = hev ? lf_s8(ps1 - qs1) : 0;
+    f = lf_s8(f + 3 * (qs0 - ps0));
+    const int f1 = lf_s8(f + 4) >> 3, f2 = lf_s8(f + 3) >> 3;
+    q0[0] = (uint8_t)(lf_s8(qs0 - f1) + 128);
+    q0[-step] = (uint8_t)(lf_s8(ps0 + f2) + 128);
+    if (!hev) {
+      const int f3 = (f1 + 1) >> 1;
+      q0[step] = (uint8_t)(lf_s8(qs1 - f3) + 128);
+      q0[-2 * step] = (uint8_t)(lf_s8(ps1 + f3) + 128);
+    }
+    return;
+  }
+  bool flat2 = size == 16;
+  for (int k = 4; k < 7 && flat2; ++k) flat2 = tv_abs(p[k] - p[0]) <= 1 && tv_abs(q[k] - q[0]) <= 1;
+  // wide filter (7.14.6.4): n taps modified per side, weight 2 within |j| <= n2
+  const int log2 = flat2 ? 4 : 3, n = flat2 ? 6 : (size == 6 ? 2 : 3), n2 = (log2 == 3 && size != 6) ? 0 : 1;
+  int F[14];  // F[7 + k]: k >= 0 -> q[k], k < 0 -> p[-k-1]
+  for (int k = 0; k <= n; ++k) {
+    F[7 + k] = q[k];
+    F[6 - k] = p[k];
+  }
+  int o[12];
+  for (int i = -n; i < n; ++i) {
+    int t = 0;
+    for (int j = -n; j <= n; ++j) {
+      const int k = clip3(-(n + 1), n, i + j);
+      t += F[7 + k] * ((j <= n2 && j >= -n2) ? 2 : 1);
+    }
+    o[i + n] = (t + (1 << (log2 - 1))) >> log2;
+  }
+  for (int i = -n; i < n; ++i) q0[i * step] = (uint8_t)o[i + n];
+}
+
 }  // namespace av1
 }  // namespace tv

@@ -52,6 +52,9 @@ def _core():
         lib.tv_av1_sgr_apply.argtypes = [u8, i, i, i32, u8]
         lib.tv_av1_sgr_stats.argtypes = [u8, u8, i, i, i, i64]
         lib.tv_av1_sgr_filter_planes.argtypes = [u8, i, i, i, i32, i32]
+        lib.tv_av1_deblock.argtypes = [u8, i, i, i, C.POINTER(C.c_uint32), i, u8]
+        lib.tv_av1_deblock.restype = C.c_int
+        lib.tv_av1_last_error.restype = C.c_char_p
         lib.tv_av1_rc_roundtrip.argtypes = [_vp, _vp, _vp, i, i, i, _vp, _vp]
         lib.tv_av1_rc_roundtrip.restype = C.c_int
         lib._av1_sigs = True
@@ -64,7 +67,7 @@ def _gpu():
     lib = gpu_lib()
     if not getattr(lib, "_av1_sigs", False):
         for name in ("tv_gpu_cdef_dirs", "tv_gpu_cdef_search", "tv_gpu_cdef_apply", "tv_gpu_wiener_apply",
-                     "tv_gpu_wiener_stats", "tv_gpu_sgr_stats", "tv_gpu_sgr_apply"):
+                     "tv_gpu_wiener_stats", "tv_gpu_sgr_stats", "tv_gpu_sgr_apply", "tv_gpu_av1_deblock"):
             getattr(lib, name).restype = C.c_int
         lib.tv_av1_gpu_last_error.restype = C.c_char_p
         lib._av1_sigs = True
@@ -372,6 +375,83 @@ def loop_restoration_apply(rec, dec: LrDecision):
 
 
 # ------------------------------------------------------------------ whole-frame tool ----
+# ------------------------------------------------------------------ deblocking ----
+def lf_info(tx_w, tx_h, bs_w, bs_h, lvl_v, lvl_h, skip_inter=None) -> np.ndarray:
+    """Pack per-4x4 loop-filter info words (layout: csrc/include/tv/av1_defs.h).  Sizes are
+    in pixels (4..64), levels 0..63; all arrays share one (h/4, w/4) shape."""
+    lg = lambda a: (np.log2(np.asarray(a)).astype(np.uint32) - 2) & 7  # noqa: E731
+    word = (lg(tx_w) | lg(tx_h) << 3 | lg(bs_w) << 6 | lg(bs_h) << 9
+            | (np.asarray(lvl_v, np.uint32) & 63) << 12 | (np.asarray(lvl_h, np.uint32) & 63) << 18)
+    if skip_inter is not None:
+        word |= (np.asarray(skip_inter, np.uint32) & 1) << 24
+    return np.ascontiguousarray(word, np.uint32)
+
+
+def random_lf_info(w: int, h: int, rng: np.random.Generator, chroma: bool = False, lvl_max: int = 63,
+                   skip_p: float = 0.3) -> np.ndarray:
+    """A random but valid partition of a plane for tests / benches: superblocks (64, or 32 in
+    a 4:2:0 chroma plane) split recursively into square / half blocks, each block carrying a
+    uniform tx grid of a size <= the block, one level pair and a skip && inter flag."""
+    h4, w4 = h // 4, w // 4
+    f = {k: np.zeros((h4, w4), np.int64) for k in ("txw", "txh", "bw", "bh", "lv", "lh", "sk")}
+
+    def block(x, y, bw, bh):
+        if x >= w or y >= h:
+            return
+        r = rng.random()
+        if bw > 8 and bh > 8 and r < 0.35:
+            hw, hh = bw // 2, bh // 2
+            for dy in (0, hh):
+                for dx in (0, hw):
+                    block(x + dx, y + dy, hw, hh)
+            return
+        if bw == bh and bw > 4 and r < 0.5:
+            if rng.random() < 0.5:
+                block(x, y, bw, bh // 2), block(x, y + bh // 2, bw, bh // 2)
+            else:
+                block(x, y, bw // 2, bh), block(x + bw // 2, y, bw // 2, bh)
+            return
+        tw = min(bw, 64) >> int(rng.integers(0, 3))
+        th = min(bh, 64) >> int(rng.integers(0, 3))
+        tw, th = max(tw, 4), max(th, 4)
+        if tw > 4 * th or th > 4 * tw:  # AV1 tx aspect <= 4:1
+            tw = th = min(tw, th)
+        sl = np.s_[y // 4:(y + bh) // 4, x // 4:(x + bw) // 4]
+        f["txw"][sl], f["txh"][sl], f["bw"][sl], f["bh"][sl] = tw, th, bw, bh
+        f["lv"][sl], f["lh"][sl] = rng.integers(0, lvl_max + 1), rng.integers(0, lvl_max + 1)
+        f["sk"][sl] = rng.random() < skip_p
+
+    sb = 32 if chroma else 64
+    for y in range(0, h, sb):
+        for x in range(0, w, sb):
+            block(x, y, sb, sb)
+    return lf_info(f["txw"], f["txh"], f["bw"], f["bh"], f["lv"], f["lh"], f["sk"])
+
+
+def deblock(rec, info, chroma: bool = False, sharpness: int = 0):
+    """AV1 deblocking loop filter (7.14) of a plane: numpy (h, w) + info (h/4, w/4) -> the
+    C++ golden model; torch (B, h, w) cuda + info (B, h/4, w/4) -> one fused HIP launch
+    (k_deblock, both passes per 64x64 LDS tile)."""
+    if _is_np(rec):
+        h, w = rec.shape
+        out = np.empty_like(rec)
+        rc = _core().tv_av1_deblock(_p(np.ascontiguousarray(rec)), w, h, int(chroma),
+                                    _p(np.ascontiguousarray(info, np.uint32), C.c_uint32), sharpness, _p(out))
+        if rc != 0:
+            raise RuntimeError(_core().tv_av1_last_error().decode())
+        return out
+    import torch
+
+    B, h, w = rec.shape
+    if _is_np(info):
+        info = torch.from_numpy(np.ascontiguousarray(info, np.uint32).view(np.int32))
+    inf = info.to(device=rec.device, dtype=torch.int32).reshape(B, h // 4, w // 4).contiguous()
+    out = torch.empty_like(rec)
+    _check(_gpu().tv_gpu_av1_deblock(_t(rec.contiguous()), _t(out), w, h, B, int(chroma), _t(inf), sharpness,
+                                     _stream(rec)))
+    return out
+
+
 def psnr(a, b) -> float:
     if not _is_np(a):
         a, b = a.cpu().numpy(), b.cpu().numpy()
@@ -379,10 +459,16 @@ def psnr(a, b) -> float:
     return float("inf") if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse))
 
 
-def postfilter_frames(src: tuple, rec: tuple, damping: int = 5, restore: bool = True, sgr_sets=(0, 4, 8, 10, 14)):
-    """CDEF (strength search + filter) then loop restoration on a batch of decoded I420
-    frames: src/rec = (Y, U, V) torch uint8 stacks (B, h, w) on the GPU (or numpy (h, w)
-    planes on the CPU golden path).  Returns (filtered planes, report dict)."""
+def postfilter_frames(src: tuple, rec: tuple, damping: int = 5, restore: bool = True, sgr_sets=(0, 4, 8, 10, 14),
+                      lf: tuple | None = None, sharpness: int = 0):
+    """AV1 in-loop filter chain on a batch of decoded I420 frames: deblocking (when `lf` =
+    per-plane info maps is given), CDEF (strength search + filter), then loop restoration.
+    src/rec = (Y, U, V) torch uint8 stacks (B, h, w) on the GPU (or numpy (h, w) planes on
+    the CPU golden path).  Returns (filtered planes, report dict)."""
+    psnr_rec = None
+    if lf is not None:
+        psnr_rec = [psnr(s, r) for s, r in zip(src, rec)]
+        rec = tuple(deblock(r, i, c > 0, sharpness) for c, (r, i) in enumerate(zip(rec, lf)))
     Ys, Us, Vs = src
     Yr, Ur, Vr = rec
     dirs, var = cdef_dirs(Yr)
@@ -410,6 +496,8 @@ def postfilter_frames(src: tuple, rec: tuple, damping: int = 5, restore: bool = 
         out = [cdef_apply(Yr, dirs, var, PY, False, damping), cdef_apply(Ur, dirs, var, PUV, True, damping),
                cdef_apply(Vr, dirs, var, PUV, True, damping)]
     rep = {"psnr_in": [psnr(s, r) for s, r in zip(src, rec)], "cdef_tables": tables}
+    if psnr_rec is not None:
+        rep["psnr_in"], rep["psnr_deblock"] = psnr_rec, rep["psnr_in"]
     rep["psnr_cdef"] = [psnr(s, o) for s, o in zip(src, out)]
     if restore:
         lr = [loop_restoration_search(s, o, sgr_sets=sgr_sets) for s, o in zip(src, out)]

@@ -77,6 +77,13 @@ def main():
     prm = np.tile(np.array([0, -20, 40], np.int32), (a.batch, nu, 1))
     t = timed(lambda: av1.sgr_apply(Yr, prm), a.iters)
     res["sgr_apply_luma_fps"] = round(a.batch / t, 1)
+    rng = np.random.default_rng(0)
+    lf = [np.stack([av1.random_lf_info(pw, ph, rng, chroma=c > 0, lvl_max=40) for _ in range(a.batch)])
+          for c, (pw, ph) in enumerate(((w, h), (w // 2, h // 2), (w // 2, h // 2)))]
+    lf = [torch.as_tensor(x.view(np.int32)).to(dev) for x in lf]
+    t = timed(lambda: [av1.deblock(r, i, c > 0) for c, (r, i) in enumerate(zip((Yr, Ur, Vr), lf))], a.iters)
+    res["deblock_yuv_fps"] = round(a.batch / t, 1)
+    res["deblock_yuv_gbps"] = round(a.batch * w * h * 1.5 * 2 / t / 1e9, 1)
     if a.lr:
         t = timed(lambda: av1.loop_restoration_search(Ys, Yr, sgr_sets=(0, 10, 14)), max(1, a.iters // 2))
         res["lr_search_luma_fps"] = round(a.batch / t, 1)
