@@ -515,20 +515,31 @@ class Engine {
 
   // Encode nseg segments of nframes (1..gop) host frames each, coded-size planar I420 laid
   // out [segment][frame][Y | U | V] (planes padded to the coded size by the caller).
-  void encode_host(const uint8_t* frames, int nseg, int nframes) {
+  void encode_host(const uint8_t* frames, int nseg, int nframes) { encode_mem(frames, nseg, nframes); }
+
+  // Same layout, but the frames already live in device memory on this GPU (produced by
+  // the caller's pre-processing kernels, e.g. the ABR ladder's tone-map + Lanczos rungs):
+  // device-to-device copies into each group's source planes, no PCIe crossing.  The
+  // caller must have finished writing them (its stream synchronised) before the call.
+  void encode_device(const uint8_t* frames, int nseg, int nframes) { encode_mem(frames, nseg, nframes); }
+
+ private:
+  // hipMemcpyDefault: the runtime resolves host (pageable / pinned) vs device pointers.
+  void encode_mem(const uint8_t* frames, int nseg, int nframes) {
     run(nseg, nframes, [&](Core& core, int b0, int f, int B) {
       const Geo& g = core.geo();
       const long fsz = g.ysz + 2 * g.csz;
       const FrameSet src = core.src();
       for (int b = 0; b < B; ++b) {
         const uint8_t* p = frames + ((long)(b0 + b) * nframes + f) * fsz;
-        HIP_OK(hipMemcpyAsync(src.y + b * g.ysz, p, g.ysz, hipMemcpyHostToDevice, core.stream()));
-        HIP_OK(hipMemcpyAsync(src.u + b * g.csz, p + g.ysz, g.csz, hipMemcpyHostToDevice, core.stream()));
-        HIP_OK(hipMemcpyAsync(src.v + b * g.csz, p + g.ysz + g.csz, g.csz, hipMemcpyHostToDevice,
-                              core.stream()));
+        HIP_OK(hipMemcpyAsync(src.y + b * g.ysz, p, g.ysz, hipMemcpyDefault, core.stream()));
+        HIP_OK(hipMemcpyAsync(src.u + b * g.csz, p + g.ysz, g.csz, hipMemcpyDefault, core.stream()));
+        HIP_OK(hipMemcpyAsync(src.v + b * g.csz, p + g.ysz + g.csz, g.csz, hipMemcpyDefault, core.stream()));
       }
     });
   }
+
+ public:
 
   const std::vector<uint8_t>& segment(int b) const { return core_of(b).segment(b % per_); }
   double sse(int b, int c) const { return core_of(b).sse(b % per_, c); }
@@ -651,6 +662,9 @@ void tv_engine_timing(void* e, double* gpu_ms, double* wall_ms, double* entropy_
   *coef_mb = E->coef_bytes() / 1e6;
 }
 // copy the last frame's coded-size reconstruction of segment b (tests)
+int tv_engine_encode_device(void* e, const uint8_t* dframes, int nseg, int nframes) {
+  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_device(dframes, nseg, nframes); });
+}
 int tv_engine_last_recon(void* e, int b, uint8_t* y, uint8_t* u, uint8_t* v) {
   return gguard([&] {
     auto* E = static_cast<tv::gpu::Engine*>(e);

@@ -32,12 +32,15 @@ constexpr int kTile = 256;
 
 // ---------------------------------------------------------------- resize (H pass)
 // tmp[y][x] = sum_k w[x][k] * src[y][ix[x]+k]  (Q14 weights, result kept at Q6 in int16)
-__global__ void __launch_bounds__(kTile) k_resize_h(const uint8_t* __restrict__ src, int sw, int sstride,
-                                                    int16_t* __restrict__ tmp, int dw, const int* __restrict__ ix,
-                                                    const int16_t* __restrict__ wx, int taps) {
+// blockIdx.z = frame of a batch (source frame stride sfs, tmp frame stride tfs).
+__global__ void __launch_bounds__(kTile) k_resize_h(const uint8_t* __restrict__ src, int sw, int sstride, long sfs,
+                                                    int16_t* __restrict__ tmp, long tfs, int dw,
+                                                    const int* __restrict__ ix, const int16_t* __restrict__ wx,
+                                                    int taps) {
   __shared__ uint8_t row[kTile * 8 + 64];
   const int y = blockIdx.y, x0 = blockIdx.x * kTile, x = x0 + threadIdx.x;
-  const uint8_t* s = src + (long)y * sstride;
+  const uint8_t* s = src + blockIdx.z * sfs + (long)y * sstride;
+  tmp += blockIdx.z * tfs;
   // source span touched by this tile of outputs
   const int lo = ix[x0];
   const int hi = ix[min(x0 + kTile, dw) - 1] + taps;  // exclusive
@@ -59,17 +62,21 @@ __global__ void __launch_bounds__(kTile) k_resize_h(const uint8_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------- resize (V pass)
-__global__ void __launch_bounds__(kTile) k_resize_v(const int16_t* __restrict__ tmp, int sh, int dw,
-                                                    uint8_t* __restrict__ dst, int dstride, int dh,
-                                                    const int* __restrict__ iy, const int16_t* __restrict__ wy,
-                                                    int taps) {
+// Writes a pw x ph (>= dw x dh) output: columns/rows past the picture replicate its last
+// column/row, i.e. the edge padding an encoder wants up to its coded size comes for free.
+__global__ void __launch_bounds__(kTile) k_resize_v(const int16_t* __restrict__ tmp, long tfs, int sh, int dw,
+                                                    uint8_t* __restrict__ dst, long dfs, int dstride, int dh, int pw,
+                                                    int ph, const int* __restrict__ iy,
+                                                    const int16_t* __restrict__ wy, int taps) {
   const int x = blockIdx.x * kTile + threadIdx.x, y = blockIdx.y;
-  if (x >= dw || y >= dh) return;
-  const int b = iy[y];
-  const int16_t* w = wy + (long)y * taps;
+  if (x >= pw || y >= ph) return;
+  const int xs = min(x, dw - 1), ys = min(y, dh - 1);
+  tmp += blockIdx.z * tfs;
+  const int b = iy[ys];
+  const int16_t* w = wy + (long)ys * taps;
   int acc = 0;
-  for (int k = 0; k < taps; ++k) acc += w[k] * tmp[(long)clampi(b + k, 0, sh - 1) * dw + x];
-  dst[(long)y * dstride + x] = sat8((acc + (1 << 19)) >> 20);  // Q14 * Q6 -> Q0
+  for (int k = 0; k < taps; ++k) acc += w[k] * tmp[(long)clampi(b + k, 0, sh - 1) * dw + xs];
+  dst[blockIdx.z * dfs + (long)y * dstride + x] = sat8((acc + (1 << 19)) >> 20);  // Q14 * Q6 -> Q0
 }
 
 // ------------------------------------------------------------------- RGB -> I420
@@ -144,11 +151,19 @@ __device__ __forceinline__ float eetf(float e, float src_pq, float dst_pq) {
   return o * src_pq;
 }
 
+// blockIdx.z = frame of a batch: P010 frames back to back (luma w*h, chroma w*h/2 samples),
+// output planes advance by ofs bytes per frame.
 __global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* __restrict__ uv16, int w, int h,
-                             uint8_t* __restrict__ Y, uint8_t* __restrict__ U, uint8_t* __restrict__ V,
+                             uint8_t* __restrict__ Y, uint8_t* __restrict__ U, uint8_t* __restrict__ V, long ofs,
                              float src_peak_nits, float dst_peak_nits) {
   const int cx = blockIdx.x * blockDim.x + threadIdx.x, cy = blockIdx.y;
   if (cx >= w / 2 || cy >= h / 2) return;
+  const long z = blockIdx.z;
+  y16 += z * w * h;
+  uv16 += z * w * h / 2;
+  Y += z * ofs;
+  U += z * ofs;
+  V += z * ofs;
   const long c = (long)cy * w + 2 * cx;
   // limited-range 10-bit chroma
   const float cb = ((uv16[c] >> 6) - 512.f) / 896.f, cr = ((uv16[c + 1] >> 6) - 512.f) / 896.f;
@@ -180,6 +195,48 @@ __global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* _
     }
   U[(long)cy * (w / 2) + cx] = sat8(__float2int_rn(128.f + 224.f * su * 0.25f));
   V[(long)cy * (w / 2) + cx] = sat8(__float2int_rn(128.f + 224.f * sv * 0.25f));
+}
+
+// ------------------------------------------------------- synthetic HDR10 source
+// Seeded procedural P010 (BT.2020 PQ, limited range) frames for the ABR-ladder benchmark:
+// smooth gradients, coarse + fine texture and sparse ~1000-nit highlights, translated by
+// (3, 1) pixels per frame so motion search has real work.  One thread per 2x2 block,
+// blockIdx.z = frame (t = t0 + z).
+__device__ __forceinline__ uint32_t hash3(uint32_t x, uint32_t y, uint32_t s) {
+  uint32_t h = x * 0x8da6b343u ^ y * 0xd8163841u ^ s * 0xcb1ab31fu;
+  h ^= h >> 15;
+  h *= 0x2c1b3c6du;
+  h ^= h >> 12;
+  h *= 0x297a2d39u;
+  return h ^ (h >> 15);
+}
+
+__global__ void k_synth_p010(uint16_t* __restrict__ y16, uint16_t* __restrict__ uv16, int w, int h, int t0,
+                             uint32_t seed) {
+  const int cx = blockIdx.x * blockDim.x + threadIdx.x, cy = blockIdx.y;
+  if (cx >= w / 2 || cy >= h / 2) return;
+  const long z = blockIdx.z;
+  const int t = t0 + (int)z;
+  y16 += z * w * h;
+  uv16 += z * w * h / 2;
+  const int px = 2 * cx + 3 * t, py = 2 * cy + t;  // pattern coordinates (global motion)
+  const float base = 0.36f + 0.2f * __sinf(px * 0.0041f + py * 0.0023f) + 0.1f * __sinf(py * 0.0107f - px * 0.0031f);
+  const uint32_t cell = hash3((uint32_t)px >> 6, (uint32_t)py >> 6, seed);
+  const float hi = (cell & 15u) == 0u ? 0.34f : 0.f;  // sparse highlight tiles (~1000 nits)
+  const float coarse = ((hash3((uint32_t)px >> 3, (uint32_t)py >> 3, seed + 1u) & 255u) / 255.f - 0.5f) * 0.07f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float fine = ((hash3((uint32_t)(px + i), (uint32_t)(py + j), seed + 2u) & 15u) / 15.f - 0.5f) * 0.012f;
+      const float yv = fminf(fmaxf(base + hi + coarse + fine, 0.f), 1.f);
+      y16[(long)(2 * cy + j) * w + 2 * cx + i] = (uint16_t)((64 + __float2int_rn(yv * 876.f)) << 6);
+    }
+  const float cb = 0.09f * __sinf(px * 0.0019f + t * 0.01f) + ((cell >> 4) & 7u) * 0.004f;
+  const float cr = 0.07f * __cosf(py * 0.0027f) - ((cell >> 8) & 7u) * 0.003f;
+  const long c = (long)cy * w + 2 * cx;
+  uv16[c] = (uint16_t)((512 + __float2int_rn(cb * 896.f)) << 6);
+  uv16[c + 1] = (uint16_t)((512 + __float2int_rn(cr * 896.f)) << 6);
 }
 
 // ---------------------------------------------------------------- label overlay
@@ -316,10 +373,10 @@ int tv_resize_plane(const uint8_t* src, int sw, int sh, int sstride, uint8_t* ds
     return -1;
   }
   auto s = static_cast<hipStream_t>(stream);
-  tv::ops::k_resize_h<<<dim3(cdiv(dw, tv::ops::kTile), sh), tv::ops::kTile, 0, s>>>(src, sw, sstride, tmp, dw, ix,
-                                                                                     wx, tx);
-  tv::ops::k_resize_v<<<dim3(cdiv(dw, tv::ops::kTile), dh), tv::ops::kTile, 0, s>>>(tmp, sh, dw, dst, dstride, dh,
-                                                                                     iy, wy, ty);
+  tv::ops::k_resize_h<<<dim3(cdiv(dw, tv::ops::kTile), sh), tv::ops::kTile, 0, s>>>(src, sw, sstride, 0, tmp, 0, dw,
+                                                                                     ix, wx, tx);
+  tv::ops::k_resize_v<<<dim3(cdiv(dw, tv::ops::kTile), dh), tv::ops::kTile, 0, s>>>(tmp, 0, sh, dw, dst, 0, dstride,
+                                                                                     dh, dw, dh, iy, wy, ty);
   return ops_status();
 }
 
@@ -352,7 +409,49 @@ int tv_tonemap_pq(const uint16_t* y16, const uint16_t* uv16, int w, int h, uint8
     return -1;
   }
   tv::ops::k_tonemap_pq<<<dim3(cdiv(w / 2, 128), h / 2), 128, 0, static_cast<hipStream_t>(stream)>>>(
-      y16, uv16, w, h, y, u, v, src_peak, dst_peak);
+      y16, uv16, w, h, y, u, v, 0, src_peak, dst_peak);
+  return ops_status();
+}
+
+// n frames: P010 in (y16: n x w*h, uv16: n x w*h/2), I420 out n x (Y | U | V) back to back.
+int tv_tonemap_pq_batch(const uint16_t* y16, const uint16_t* uv16, int w, int h, int n, uint8_t* out,
+                        float src_peak, float dst_peak, void* stream) {
+  if ((w | h) & 1 || w <= 0 || h <= 0 || n <= 0 || n > 65535 || src_peak <= dst_peak) {
+    g_ops_err = "tv_tonemap_pq_batch: bad geometry or src_peak <= dst_peak";
+    return -1;
+  }
+  const long ysz = (long)w * h, csz = ysz / 4;
+  tv::ops::k_tonemap_pq<<<dim3(cdiv(w / 2, 128), h / 2, n), 128, 0, static_cast<hipStream_t>(stream)>>>(
+      y16, uv16, w, h, out, out + ysz, out + ysz + csz, ysz + 2 * csz, src_peak, dst_peak);
+  return ops_status();
+}
+
+int tv_synth_p010(uint16_t* y16, uint16_t* uv16, int w, int h, int n, int t0, uint32_t seed, void* stream) {
+  if ((w | h) & 1 || w <= 0 || h <= 0 || n <= 0 || n > 65535) {
+    g_ops_err = "tv_synth_p010: bad geometry";
+    return -1;
+  }
+  tv::ops::k_synth_p010<<<dim3(cdiv(w / 2, 128), h / 2, n), 128, 0, static_cast<hipStream_t>(stream)>>>(
+      y16, uv16, w, h, t0, seed);
+  return ops_status();
+}
+
+// Batched Lanczos resample of one plane of n frames (frame strides sfs / dfs bytes) into a
+// pw x ph edge-padded destination; tmp holds n x sh x dw int16.
+int tv_resize_batch(const uint8_t* src, int sw, int sh, int sstride, long sfs, uint8_t* dst, int dw, int dh,
+                    int dstride, long dfs, int pw, int ph, int n, const int* ix, const int16_t* wx, int tx,
+                    const int* iy, const int16_t* wy, int ty, int16_t* tmp, void* stream) {
+  if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 || pw < dw || ph < dh || dstride < pw || n <= 0 || n > 65535 ||
+      tx <= 0 || ty <= 0 || tx > 64 || ty > 64 || sh > 65535 || ph > 65535) {
+    g_ops_err = "tv_resize_batch: bad geometry";
+    return -1;
+  }
+  auto s = static_cast<hipStream_t>(stream);
+  const long tfs = (long)sh * dw;
+  tv::ops::k_resize_h<<<dim3(cdiv(dw, tv::ops::kTile), sh, n), tv::ops::kTile, 0, s>>>(src, sw, sstride, sfs, tmp,
+                                                                                        tfs, dw, ix, wx, tx);
+  tv::ops::k_resize_v<<<dim3(cdiv(pw, tv::ops::kTile), ph, n), tv::ops::kTile, 0, s>>>(
+      tmp, tfs, sh, dw, dst, dfs, dstride, dh, pw, ph, iy, wy, ty);
   return ops_status();
 }
 

@@ -1,0 +1,77 @@
+"""ABR ladder (BASELINE config #5): rung planning on CPU; on the GPU the batched
+tone-map / Lanczos kernels against the single-frame HIP ops + numpy edge padding (exact),
+and a small ladder end to end through the oracle decoder."""
+import numpy as np
+import pytest
+
+from thinvids_amd.models import abr
+
+
+def test_plan_rungs_8k():
+    r = abr.plan_rungs(7680, 4320)
+    assert r == [(3840, 2160), (2560, 1440), (1920, 1080), (1280, 720), (854, 480)]
+    # never upscales, duplicates collapse
+    assert abr.plan_rungs(1920, 1080, (2160, 1080, 720)) == [(1920, 1080), (1280, 720)]
+
+
+def test_split_threads_proportional():
+    t = abr.split_threads(abr.plan_rungs(7680, 4320), 16)
+    assert t[0] >= t[1] >= t[2] >= 2 and t[-1] == 2
+    assert sum(t) <= 16 + 2 * len(t)
+
+
+def test_staging_layout_coded_size():
+    L = abr.staging_layout(854, 480)
+    assert (L["cw"], L["ch"]) == (864, 480)
+    assert L["fsz"] == 864 * 480 * 3 // 2
+    y, u, v = L["planes"]
+    assert y == (0, 854, 480, 864, 864, 480)
+    assert u[0] == 864 * 480 and v[0] == 864 * 480 + 432 * 240
+
+
+@pytest.mark.gpu
+def test_ladder_chunk_matches_single_frame_ops():
+    import torch
+
+    from thinvids_amd.models.gpu_engine import pad_frame
+    from thinvids_amd.ops import color, resize
+
+    lad = abr.AbrLadder(src_w=640, src_h=360, heights=(240, 180), segments=1, gop=3)
+    try:
+        lad.synth_p010(5, 3)
+        y16, uv16 = lad.y16.clone(), lad.uv16.clone()
+        lad.ladder_chunk(0, 3)
+        torch.cuda.synchronize()
+        assert int(y16.to(torch.int32).min()) >= 64 << 6 and int(y16.to(torch.int32).max()) <= 940 << 6
+        for f in range(3):
+            sdr = color.tonemap_pq(y16[f], uv16[f])
+            got_sdr = lad.sdr[f].cpu().numpy()
+            want_sdr = np.concatenate([p.cpu().numpy().ravel() for p in sdr])
+            assert np.array_equal(got_sdr, want_sdr)
+            for (w, h), L, st in zip(lad.rungs, lad.layouts, lad.staging):
+                planes = resize.resize_frame(sdr, w, h)
+                want = pad_frame(*[p.cpu().numpy() for p in planes], L["cw"], L["ch"])
+                assert np.array_equal(st[f].cpu().numpy(), want), (w, h, f)
+    finally:
+        lad.close()
+
+
+@pytest.mark.gpu
+def test_ladder_encode_decodes():
+    from thinvids_amd.models import hevc
+
+    lad = abr.AbrLadder(src_w=640, src_h=360, heights=(360, 240, 180), segments=2, gop=4)
+    try:
+        segs = lad.encode_synthetic([0, 4])
+        assert len(segs) == 3 and all(len(s) == 2 for s in segs)
+        for r, (eng, rung) in enumerate(zip(lad.engines, segs)):
+            for b, bs in enumerate(rung):
+                d = hevc.decode(bs)
+                assert len(d.frames) == 4
+                gy, _, _ = eng.last_recon(b)
+                assert np.array_equal(d.coded_frames[-1][0], gy)
+        q = lad.psnr()
+        assert [(x["w"], x["h"]) for x in q] == lad.rungs
+        assert all(x["y"] > 30 for x in q), q
+    finally:
+        lad.close()

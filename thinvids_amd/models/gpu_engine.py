@@ -28,6 +28,8 @@ def _lib():
         lib.tv_engine_encode_synth.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
         lib.tv_engine_encode_host.restype = C.c_int
         lib.tv_engine_encode_host.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int]
+        lib.tv_engine_encode_device.restype = C.c_int
+        lib.tv_engine_encode_device.argtypes = [vp, vp, C.c_int, C.c_int]
         lib.tv_engine_segment_size.restype = C.c_size_t
         lib.tv_engine_segment_size.argtypes = [vp, C.c_int]
         lib.tv_engine_segment_copy.argtypes = [vp, C.c_int, C.POINTER(C.c_uint8)]
@@ -104,6 +106,19 @@ class GpuEngine:
         self._check(self.lib.tv_engine_encode_host(self.h, ptr(buf), len(segments), n))
         self.last_frames = n
         return [self.segment(b) for b in range(len(segments))]
+
+    def encode_device(self, frames, nseg: int, nframes: int) -> list[bytes]:
+        """frames: a contiguous uint8 CUDA tensor on this engine's GPU laid out
+        [segment][frame][Y | U | V] at the coded size (edge-padded), already written (the
+        producing stream synchronised).  Copied device-to-device into the engine."""
+        fsz = self.cw * self.ch * 3 // 2
+        if not 1 <= nseg <= self.batch or not 1 <= nframes <= self.gop:
+            raise ValueError(f"need 1..{self.batch} segments of 1..{self.gop} frames")
+        if not frames.is_cuda or not frames.is_contiguous() or frames.numel() < nseg * nframes * fsz:
+            raise ValueError("frames must be a contiguous CUDA tensor of nseg*nframes coded-size I420 frames")
+        self._check(self.lib.tv_engine_encode_device(self.h, C.c_void_p(frames.data_ptr()), nseg, nframes))
+        self.last_frames = nframes
+        return [self.segment(b) for b in range(nseg)]
 
     def segment(self, b: int) -> bytes:
         n = self.lib.tv_engine_segment_size(self.h, b)
