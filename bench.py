@@ -64,9 +64,20 @@ def ladder_main(args) -> None:
     lad = AbrLadder(sw, sh, heights, qp=args.qp, segments=batch, gop=args.gop, device=local,
                     threads=args.threads or None, seed=args.seed, search_range=args.range, sao=args.sao)
 
-    def step(s: int):
-        base = (s * world + rank) * batch
-        segs = lad.encode_synthetic([(base + b) * args.gop for b in range(batch)])
+    def prep(i: int):  # step i's source -> tone-map -> rungs into staging slot i % 2
+        base = (i * world + rank) * batch
+        lad.prepare_synthetic([(base + b) * args.gop for b in range(batch)], slot=i % 2)
+        torch.cuda.current_stream(dev).synchronize()
+
+    # step i encodes staging slot i % 2 while this thread prepares step i + 1 into the other
+    # slot (every step = one full prep + one full encode; prep(0) runs before warm-up)
+    prep(0)
+    counter = [0]
+
+    def step(_s: int):
+        i = counter[0]
+        counter[0] += 1
+        segs = lad.encode_overlapped(batch, i % 2, prepare_next=lambda: prep(i + 1))
         nbytes = sum(len(x) for r in segs for x in r)
         stats = np.array([batch * args.gop, nbytes], dtype=np.float64)
         if world > 1:

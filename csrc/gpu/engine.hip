@@ -568,6 +568,7 @@ class Engine {
   }
   template <class Upload> void run(int nseg, int nframes, Upload&& upload) {
     if (nseg < 1 || nseg > cfg_.batch) throw std::runtime_error("nseg out of range");
+    HIP_OK(hipSetDevice(cfg_.device));  // the calling host thread may be new (ABR rung threads)
     const auto w0 = std::chrono::steady_clock::now();
     used_ = (nseg + per_ - 1) / per_;
     for (int g = 0; g < used_; ++g) cores_[g]->begin(std::min(per_, nseg - g * per_), nframes);

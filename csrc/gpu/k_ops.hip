@@ -125,10 +125,16 @@ __global__ void k_p010_to_i420(const uint16_t* __restrict__ y16, const uint16_t*
 }
 
 // --------------------------------------------------------------- HDR10 tone-map
+// x^y for x >= 0, y > 0 on the transcendental unit: v_log_f32 + v_exp_f32 (~1 ulp each)
+// instead of the ~40-instruction libm powf; the tone-map does 12 per pixel and was the
+// ladder's top pre-processing kernel (27 ms / 16 8K frames with powf).
+__device__ __forceinline__ float fpow(float x, float y) {
+  return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+}
 __device__ __forceinline__ float pq_eotf(float e) {  // -> linear, 1.0 = 10000 nits
   const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
-  const float p = powf(fminf(fmaxf(e, 0.f), 1.f), 1.f / m2);  // PQ signal is in [0, 1]
-  return powf(fmaxf(p - c1, 0.f) / (c2 - c3 * p), 1.f / m1);
+  const float p = fpow(fminf(fmaxf(e, 0.f), 1.f), 1.f / m2);  // PQ signal is in [0, 1]
+  return fpow(fmaxf(p - c1, 0.f) / (c2 - c3 * p), 1.f / m1);
 }
 __device__ __forceinline__ float pq_oetf(float l) {
   const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
@@ -137,7 +143,7 @@ __device__ __forceinline__ float pq_oetf(float l) {
 }
 __device__ __forceinline__ float bt709_oetf(float l) {
   l = fminf(fmaxf(l, 0.f), 1.f);
-  return l < 0.018f ? 4.5f * l : 1.099f * powf(l, 0.45f) - 0.099f;
+  return l < 0.018f ? 4.5f * l : 1.099f * fpow(l, 0.45f) - 0.099f;
 }
 // BT.2390 EETF on PQ-encoded luminance: source peak src_pq, target peak dst_pq
 __device__ __forceinline__ float eetf(float e, float src_pq, float dst_pq) {
@@ -168,6 +174,7 @@ __global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* _
   // limited-range 10-bit chroma
   const float cb = ((uv16[c] >> 6) - 512.f) / 896.f, cr = ((uv16[c + 1] >> 6) - 512.f) / 896.f;
   const float src_pq = pq_oetf(src_peak_nits / 10000.f), dst_pq = pq_oetf(dst_peak_nits / 10000.f);
+  const float lm_floor = pq_eotf(1e-6f);
   const YuvMat m = yuv_mat(1);
   float su = 0.f, sv = 0.f;
 #pragma unroll
@@ -180,10 +187,12 @@ __global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* _
       float r = yp + 1.4746f * cr, g = yp - 0.16455f * cb - 0.57135f * cr, b = yp + 1.8814f * cb;
       // tone-map on max(R,G,B) in the PQ domain, scale linear RGB by the luminance ratio
       const float mx = fmaxf(fmaxf(r, g), fmaxf(b, 1e-6f));
-      const float lm = pq_eotf(mx), lt = pq_eotf(eetf(mx, src_pq, dst_pq));
+      const float lt = pq_eotf(eetf(mx, src_pq, dst_pq));
+      const float r0 = pq_eotf(r), g0 = pq_eotf(g), b0 = pq_eotf(b);
+      const float lm = fmaxf(fmaxf(r0, g0), fmaxf(b0, lm_floor));  // == pq_eotf(mx): monotonic
       const float sc = lm > 1e-6f ? lt / lm : 0.f;  // near-black: no ratio blow-up
       const float norm = 10000.f / dst_peak_nits;  // target peak -> 1.0
-      const float R = pq_eotf(r) * sc * norm, G = pq_eotf(g) * sc * norm, B = pq_eotf(b) * sc * norm;
+      const float R = r0 * sc * norm, G = g0 * sc * norm, B = b0 * sc * norm;
       // BT.2020 -> BT.709 primaries (linear)
       const float r7 = 1.6605f * R - 0.5876f * G - 0.0728f * B;
       const float g7 = -0.1246f * R + 1.1329f * G - 0.0083f * B;

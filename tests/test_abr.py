@@ -30,17 +30,19 @@ def test_staging_layout_coded_size():
 
 
 @pytest.mark.gpu
-def test_ladder_chunk_matches_single_frame_ops():
+@pytest.mark.parametrize("cascade", [False, True])
+def test_ladder_chunk_matches_single_frame_ops(cascade):
     import torch
 
     from thinvids_amd.models.gpu_engine import pad_frame
     from thinvids_amd.ops import color, resize
 
-    lad = abr.AbrLadder(src_w=640, src_h=360, heights=(240, 180), segments=1, gop=3)
+    lad = abr.AbrLadder(src_w=640, src_h=360, heights=(240, 180, 120), segments=2, gop=3, cascade=cascade)
     try:
         lad.synth_p010(5, 3)
         y16, uv16 = lad.y16.clone(), lad.uv16.clone()
-        lad.ladder_chunk(0, 3)
+        lad.ladder_chunk(3, 3, slot=1)
+        lad.staging = lad.staging_slots[1]
         torch.cuda.synchronize()
         assert int(y16.to(torch.int32).min()) >= 64 << 6 and int(y16.to(torch.int32).max()) <= 940 << 6
         for f in range(3):
@@ -48,10 +50,12 @@ def test_ladder_chunk_matches_single_frame_ops():
             got_sdr = lad.sdr[f].cpu().numpy()
             want_sdr = np.concatenate([p.cpu().numpy().ravel() for p in sdr])
             assert np.array_equal(got_sdr, want_sdr)
+            first = None
             for (w, h), L, st in zip(lad.rungs, lad.layouts, lad.staging):
-                planes = resize.resize_frame(sdr, w, h)
+                planes = resize.resize_frame(first if (cascade and first is not None) else sdr, w, h)
+                first = first or planes
                 want = pad_frame(*[p.cpu().numpy() for p in planes], L["cw"], L["ch"])
-                assert np.array_equal(st[f].cpu().numpy(), want), (w, h, f)
+                assert np.array_equal(st[3 + f].cpu().numpy(), want), (w, h, f)
     finally:
         lad.close()
 
@@ -73,5 +77,22 @@ def test_ladder_encode_decodes():
         q = lad.psnr()
         assert [(x["w"], x["h"]) for x in q] == lad.rungs
         assert all(x["y"] > 30 for x in q), q
+    finally:
+        lad.close()
+
+
+@pytest.mark.gpu
+def test_ladder_overlapped_equals_serial():
+    lad = abr.AbrLadder(src_w=640, src_h=360, heights=(240, 180), segments=2, gop=4)
+    try:
+        serial = [lad.encode_synthetic([0, 4]), lad.encode_synthetic([8, 12])]
+        lad.prepare_synthetic([0, 4], slot=0)
+        import torch
+
+        torch.cuda.synchronize()
+        a = lad.encode_overlapped(2, 0, prepare_next=lambda: (lad.prepare_synthetic([8, 12], slot=1),
+                                                               torch.cuda.synchronize()))
+        b = lad.encode_overlapped(2, 1)
+        assert [a, b] == serial
     finally:
         lad.close()

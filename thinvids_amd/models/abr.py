@@ -100,7 +100,7 @@ class AbrLadder:
     def __init__(self, src_w: int = SRC_8K[0], src_h: int = SRC_8K[1], heights=LADDER, qp: int = 27,
                  segments: int = 16, gop: int = 16, device: int = 0, threads: int | None = None, seed: int = 1,
                  src_peak: float = 1000.0, dst_peak: float = 100.0, search_range: int = 16,
-                 concurrent: bool = True, sao: bool = False):
+                 concurrent: bool = True, sao: bool = False, cascade: bool = True, slots: int = 2):
         import torch
 
         if (src_w | src_h) & 1:
@@ -108,7 +108,7 @@ class AbrLadder:
         self.src_w, self.src_h = src_w, src_h
         self.segments, self.gop, self.seed = segments, gop, seed
         self.src_peak, self.dst_peak = src_peak, dst_peak
-        self.concurrent = concurrent
+        self.concurrent, self.cascade = concurrent, cascade
         self.dev = torch.device("cuda", device)
         self.rungs = plan_rungs(src_w, src_h, heights)
         self.layouts = [staging_layout(w, h) for w, h in self.rungs]
@@ -117,7 +117,11 @@ class AbrLadder:
                                   seed=seed, threads=t, device=device, sao=sao)
                         for (w, h), t in zip(self.rungs, split_threads(self.rungs, total))]
         u8, i16, u16 = torch.uint8, torch.int16, torch.uint16
-        self.staging = [torch.empty((segments * gop, L["fsz"]), dtype=u8, device=self.dev) for L in self.layouts]
+        # slots: staging sets, so the pre-processing of call k+1 can fill one while the
+        # engines read the other (prepare_synthetic(..., slot) / encode_prepared(n, slot))
+        self.staging_slots = [[torch.empty((segments * gop, L["fsz"]), dtype=u8, device=self.dev)
+                               for L in self.layouts] for _ in range(max(1, slots))]
+        self.staging = self.staging_slots[0]
         self.src_fsz = src_w * src_h * 3 // 2
         self.y16 = torch.empty((gop, src_h, src_w), dtype=u16, device=self.dev)
         self.uv16 = torch.empty((gop, src_h // 2, src_w), dtype=u16, device=self.dev)
@@ -141,49 +145,65 @@ class AbrLadder:
         _ok(self.lib, self.lib.tv_synth_p010(self.y16.data_ptr(), self.uv16.data_ptr(), self.src_w, self.src_h, n,
                                              t0, self.seed & 0xFFFFFFFF, self._stream()))
 
-    def ladder_chunk(self, slot0: int, n: int) -> None:
+    def ladder_chunk(self, slot0: int, n: int, slot: int = 0) -> None:
         """Tone-map the n chunk frames (in y16/uv16) and resample them into every rung's
-        staging slots slot0..slot0+n-1."""
+        staging frames slot0..slot0+n-1 of staging set `slot`.  With `cascade` the lower
+        rungs are resampled from the first (largest) rung instead of the full source: the
+        first rung is already band-limited above every lower rung's Nyquist, and the H pass
+        then reads a 4x smaller picture (8K -> 4K -> 1440p/1080p/720p/480p)."""
         lib, st = self.lib, self._stream()
+        staging = self.staging_slots[slot]
         _ok(lib, lib.tv_tonemap_pq_batch(self.y16.data_ptr(), self.uv16.data_ptr(), self.src_w, self.src_h, n,
                                          self.sdr.data_ptr(), C.c_float(self.src_peak), C.c_float(self.dst_peak), st))
         sw, sh = self.src_w, self.src_h
-        src_planes = [(0, sw, sh), (sw * sh, sw // 2, sh // 2), (sw * sh * 5 // 4, sw // 2, sh // 2)]
-        for L, buf in zip(self.layouts, self.staging):
+        full = (self.sdr.data_ptr(), self.src_fsz,
+                [(0, sw, sh, sw), (sw * sh, sw // 2, sh // 2, sw // 2), (sw * sh * 5 // 4, sw // 2, sh // 2, sw // 2)])
+        L0 = self.layouts[0]
+        first = (staging[0].data_ptr() + slot0 * L0["fsz"], L0["fsz"],
+                 [(off, w, h, stride) for off, w, h, stride, _, _ in L0["planes"]])
+        for r, (L, buf) in enumerate(zip(self.layouts, staging)):
+            src_ptr, sfs, src_planes = first if (self.cascade and r > 0) else full
             base = buf.data_ptr() + slot0 * L["fsz"]
-            for (soff, pw_, ph_), (doff, dw, dh, dstride, pw, ph) in zip(src_planes, L["planes"]):
+            for (soff, pw_, ph_, sstride), (doff, dw, dh, dstride, pw, ph) in zip(src_planes, L["planes"]):
                 ix, wx, tx = _tables(pw_, dw, 3, self.dev.index)
                 iy, wy, ty = _tables(ph_, dh, 3, self.dev.index)
-                _ok(lib, lib.tv_resize_batch(self.sdr.data_ptr() + soff, pw_, ph_, pw_, self.src_fsz, base + doff, dw,
-                                             dh, dstride, L["fsz"], pw, ph, n, ix.data_ptr(), wx.data_ptr(), tx,
-                                             iy.data_ptr(), wy.data_ptr(), ty, self.tmp.data_ptr(), st))
+                _ok(lib, lib.tv_resize_batch(src_ptr + soff, pw_, ph_, sstride, sfs, base + doff, dw, dh, dstride,
+                                             L["fsz"], pw, ph, n, ix.data_ptr(), wx.data_ptr(), tx, iy.data_ptr(),
+                                             wy.data_ptr(), ty, self.tmp.data_ptr(), st))
 
-    def prepare_synthetic(self, starts) -> None:
+    def prepare_synthetic(self, starts, slot: int = 0) -> None:
         """Segment b = synthetic frames [starts[b], starts[b] + gop)."""
+        if not 1 <= len(starts) <= self.segments:
+            raise ValueError(f"need 1..{self.segments} segments")
         for b, t0 in enumerate(starts):
             self.synth_p010(int(t0), self.gop)
-            self.ladder_chunk(b * self.gop, self.gop)
+            self.ladder_chunk(b * self.gop, self.gop, slot)
 
-    def prepare_p010(self, segments) -> None:
+    def prepare_p010(self, segments, slot: int = 0) -> None:
         """segments: list of (y16, uv16) CUDA uint16 tensors shaped (gop, h, w) / (gop, h/2, w)."""
         for b, (y16, uv16) in enumerate(segments):
             self.y16.copy_(y16)
             self.uv16.copy_(uv16)
-            self.ladder_chunk(b * self.gop, self.gop)
+            self.ladder_chunk(b * self.gop, self.gop, slot)
 
     # -------------------------------------------------------------------- encode
-    def encode_prepared(self, nseg: int) -> list[list[bytes]]:
-        """Encode the staged segments on every rung; returns bitstreams [rung][segment]."""
+    def encode_prepared(self, nseg: int, slot: int = 0, synced: bool = False) -> list[list[bytes]]:
+        """Encode the staged segments of staging set `slot` on every rung; returns
+        bitstreams [rung][segment].  `synced`: the caller already synchronised the
+        pre-processing stream (e.g. it runs this on another thread while it prepares the
+        next slot on the same stream)."""
         import torch
 
-        torch.cuda.current_stream(self.dev).synchronize()
+        if not synced:
+            torch.cuda.current_stream(self.dev).synchronize()
+        staging = self.staging_slots[slot]
         self._nseg = nseg
         out: list = [None] * len(self.engines)
         errs: list = []
 
         def run(r):
             try:
-                out[r] = self.engines[r].encode_device(self.staging[r], nseg, self.gop)
+                out[r] = self.engines[r].encode_device(staging[r], nseg, self.gop)
             except Exception as e:  # surfaced after the join
                 errs.append(e)
 
@@ -201,10 +221,32 @@ class AbrLadder:
         return out
 
     def encode_synthetic(self, starts) -> list[list[bytes]]:
-        if not 1 <= len(starts) <= self.segments:
-            raise ValueError(f"need 1..{self.segments} segments")
         self.prepare_synthetic(starts)
         return self.encode_prepared(len(starts))
+
+    def encode_overlapped(self, nseg: int, slot: int, prepare_next=None) -> list[list[bytes]]:
+        """Encode staging set `slot` (already prepared and synchronised) on a helper thread
+        while this thread runs `prepare_next()` (which should fill the other slot and end
+        with a stream synchronise): the next call's tone-map / Lanczos kernels overlap this
+        call's encode kernels and CABAC."""
+        res: dict = {}
+
+        def enc():
+            try:
+                res["out"] = self.encode_prepared(nseg, slot, synced=True)
+            except Exception as e:  # re-raised on the caller's thread
+                res["err"] = e
+
+        t = threading.Thread(target=enc, daemon=True)
+        t.start()
+        try:
+            if prepare_next is not None:
+                prepare_next()
+        finally:
+            t.join()
+        if "err" in res:
+            raise res["err"]
+        return res["out"]
 
     def psnr(self) -> list[dict]:
         """Per rung: PSNR of the last call's reconstruction vs the rung's own (tone-mapped,
