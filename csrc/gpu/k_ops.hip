@@ -79,6 +79,71 @@ __global__ void __launch_bounds__(kTile) k_resize_v(const int16_t* __restrict__ 
   dst[blockIdx.z * dfs + (long)y * dstride + x] = sat8((acc + (1 << 19)) >> 20);  // Q14 * Q6 -> Q0
 }
 
+// ------------------------------------------------------- fused 2-D resize (batched)
+// One workgroup = a 64 x TH output tile of one frame (blockIdx.z): the clamped source window
+// it needs is staged in LDS once, the H pass writes its rows x 64 int16 intermediate to LDS,
+// the V pass reads it from there — no global int16 round trip (the two-pass kernels above
+// write + re-read sh x dw x 2 bytes per plane).  Same arithmetic and clamping as
+// k_resize_h/k_resize_v, so the result is bit-identical; output columns/rows past dw/dh
+// replicate the last ones (edge padding to pw x ph).  LDS: R x Wp source bytes + R x 64 x 2
+// intermediate, R/Wp chosen by the host from the tables (resize2d_plan in models/abr.py).
+constexpr int kR2W = 64;
+template <int MAXT>
+__global__ void __launch_bounds__(256) k_resize2d(const uint8_t* __restrict__ src, int sw, int sh, int sstride,
+                                                  long sfs, uint8_t* __restrict__ dst, int dw, int dh, int dstride,
+                                                  long dfs, int pw, int ph, int th, int wp,
+                                                  const int* __restrict__ ix, const int16_t* __restrict__ wx, int tx,
+                                                  const int* __restrict__ iy, const int16_t* __restrict__ wy,
+                                                  int ty) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int x0 = blockIdx.x * kR2W, y0 = blockIdx.y * th;
+  src += blockIdx.z * sfs;
+  dst += blockIdx.z * dfs;
+  const int xa = min(x0, dw - 1), xb = min(x0 + kR2W - 1, dw - 1);
+  const int ya = min(y0, dh - 1), yb = min(y0 + th - 1, dh - 1);
+  const int clo = ix[xa], W = ix[xb] + tx - clo;
+  const int rlo = iy[ya], R = iy[yb] + ty - rlo;
+  uint8_t* ssrc = smem;                                                   // R x wp
+  int16_t* stmp = reinterpret_cast<int16_t*>(smem + ((R * wp + 15) & ~15));  // R x 64
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int r = wv; r < R; r += 4) {
+    const uint8_t* s = src + (long)clampi(rlo + r, 0, sh - 1) * sstride;
+    for (int c = lane; c < W; c += 64) ssrc[r * wp + c] = s[clampi(clo + c, 0, sw - 1)];
+  }
+  __syncthreads();
+  {
+    // a lane's output column is fixed for every row: its taps live in registers
+    const int x = min(x0 + lane, dw - 1);
+    const int b = ix[x] - clo;
+    int wr[MAXT];
+#pragma unroll
+    for (int k = 0; k < MAXT; ++k) wr[k] = k < tx ? wx[(long)x * tx + k] : 0;
+    for (int r = wv; r < R; r += 4) {
+      const uint8_t* s = ssrc + r * wp + b;
+      int acc = 0;
+#pragma unroll
+      for (int k = 0; k < MAXT; ++k)
+        if (k < tx) acc += wr[k] * s[k];
+      stmp[r * kR2W + lane] = (int16_t)clampi((acc + (1 << 7)) >> 8, -32768, 32767);  // Q14 -> Q6
+    }
+  }
+  __syncthreads();
+  const int x = x0 + lane;
+  if (x >= pw) return;
+  // one output row per wave per iteration: row index, filter start and taps are wave-uniform
+  // (scalar loads)
+  for (int yl = __builtin_amdgcn_readfirstlane(wv); yl < th; yl += 4) {
+    const int y = y0 + yl;
+    if (y >= ph) break;
+    const int ys = min(y, dh - 1);
+    const int b = iy[ys] - rlo;
+    const int16_t* w = wy + (long)ys * ty;
+    int acc = 0;
+    for (int k = 0; k < ty; ++k) acc += w[k] * stmp[(b + k) * kR2W + lane];
+    dst[(long)y * dstride + x] = sat8((acc + (1 << 19)) >> 20);  // Q14 * Q6 -> Q0
+  }
+}
+
 // ------------------------------------------------------------------- RGB -> I420
 struct YuvMat {
   float ry, gy, by, ru, gu, bu, rv, gv, bv;
@@ -134,7 +199,7 @@ __device__ __forceinline__ float fpow(float x, float y) {
 __device__ __forceinline__ float pq_eotf(float e) {  // -> linear, 1.0 = 10000 nits
   const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
   const float p = fpow(fminf(fmaxf(e, 0.f), 1.f), 1.f / m2);  // PQ signal is in [0, 1]
-  return fpow(fmaxf(p - c1, 0.f) / (c2 - c3 * p), 1.f / m1);
+  return fpow(fmaxf(p - c1, 0.f) * __builtin_amdgcn_rcpf(c2 - c3 * p), 1.f / m1);
 }
 __device__ __forceinline__ float pq_oetf(float l) {
   const float m1 = 0.1593017578125f, m2 = 78.84375f, c1 = 0.8359375f, c2 = 18.8515625f, c3 = 18.6875f;
@@ -147,11 +212,12 @@ __device__ __forceinline__ float bt709_oetf(float l) {
 }
 // BT.2390 EETF on PQ-encoded luminance: source peak src_pq, target peak dst_pq
 __device__ __forceinline__ float eetf(float e, float src_pq, float dst_pq) {
-  const float en = e / src_pq, maxl = dst_pq / src_pq;
+  const float inv = __builtin_amdgcn_rcpf(src_pq);
+  const float en = e * inv, maxl = dst_pq * inv;
   const float ks = 1.5f * maxl - 0.5f;
   float o = en;
   if (en > ks) {
-    const float t = (en - ks) / (1.f - ks), t2 = t * t, t3 = t2 * t;
+    const float t = (en - ks) * __builtin_amdgcn_rcpf(1.f - ks), t2 = t * t, t3 = t2 * t;
     o = (2 * t3 - 3 * t2 + 1) * ks + (t3 - 2 * t2 + t) * (1.f - ks) + (-2 * t3 + 3 * t2) * maxl;
   }
   return o * src_pq;
@@ -172,7 +238,7 @@ __global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* _
   V += z * ofs;
   const long c = (long)cy * w + 2 * cx;
   // limited-range 10-bit chroma
-  const float cb = ((uv16[c] >> 6) - 512.f) / 896.f, cr = ((uv16[c + 1] >> 6) - 512.f) / 896.f;
+  const float cb = ((uv16[c] >> 6) - 512.f) * (1.f / 896.f), cr = ((uv16[c + 1] >> 6) - 512.f) * (1.f / 896.f);
   const float src_pq = pq_oetf(src_peak_nits / 10000.f), dst_pq = pq_oetf(dst_peak_nits / 10000.f);
   const float lm_floor = pq_eotf(1e-6f);
   const YuvMat m = yuv_mat(1);
@@ -182,7 +248,7 @@ __global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* _
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int x = 2 * cx + i, y = 2 * cy + j;
-      const float yp = ((y16[(long)y * w + x] >> 6) - 64.f) / 876.f;
+      const float yp = ((y16[(long)y * w + x] >> 6) - 64.f) * (1.f / 876.f);
       // BT.2020 NCL Y'CbCr -> R'G'B' (PQ)
       float r = yp + 1.4746f * cr, g = yp - 0.16455f * cb - 0.57135f * cr, b = yp + 1.8814f * cb;
       // tone-map on max(R,G,B) in the PQ domain, scale linear RGB by the luminance ratio
@@ -190,7 +256,7 @@ __global__ void k_tonemap_pq(const uint16_t* __restrict__ y16, const uint16_t* _
       const float lt = pq_eotf(eetf(mx, src_pq, dst_pq));
       const float r0 = pq_eotf(r), g0 = pq_eotf(g), b0 = pq_eotf(b);
       const float lm = fmaxf(fmaxf(r0, g0), fmaxf(b0, lm_floor));  // == pq_eotf(mx): monotonic
-      const float sc = lm > 1e-6f ? lt / lm : 0.f;  // near-black: no ratio blow-up
+      const float sc = lm > 1e-6f ? lt * __builtin_amdgcn_rcpf(lm) : 0.f;  // near-black: no ratio blow-up
       const float norm = 10000.f / dst_peak_nits;  // target peak -> 1.0
       const float R = r0 * sc * norm, G = g0 * sc * norm, B = b0 * sc * norm;
       // BT.2020 -> BT.709 primaries (linear)
@@ -446,16 +512,33 @@ int tv_synth_p010(uint16_t* y16, uint16_t* uv16, int w, int h, int n, int t0, ui
 }
 
 // Batched Lanczos resample of one plane of n frames (frame strides sfs / dfs bytes) into a
-// pw x ph edge-padded destination; tmp holds n x sh x dw int16.
+// pw x ph edge-padded destination.  th > 0: fused 2-D kernel with th-row output tiles,
+// source rows staged at wp bytes pitch, smem bytes of LDS (host-planned); th == 0: the
+// two-pass kernels through tmp (n x sh x dw int16).
 int tv_resize_batch(const uint8_t* src, int sw, int sh, int sstride, long sfs, uint8_t* dst, int dw, int dh,
                     int dstride, long dfs, int pw, int ph, int n, const int* ix, const int16_t* wx, int tx,
-                    const int* iy, const int16_t* wy, int ty, int16_t* tmp, void* stream) {
+                    const int* iy, const int16_t* wy, int ty, int16_t* tmp, int th, int wp, int smem,
+                    void* stream) {
   if (sw <= 0 || sh <= 0 || dw <= 0 || dh <= 0 || pw < dw || ph < dh || dstride < pw || n <= 0 || n > 65535 ||
-      tx <= 0 || ty <= 0 || tx > 64 || ty > 64 || sh > 65535 || ph > 65535) {
+      tx <= 0 || ty <= 0 || tx > 64 || ty > 64 || sh > 65535 || ph > 65535 || th < 0 || smem < 0 ||
+      smem > 64 * 1024 || (th > 0 && wp < tx)) {
     g_ops_err = "tv_resize_batch: bad geometry";
     return -1;
   }
   auto s = static_cast<hipStream_t>(stream);
+  if (th > 0) {
+    const dim3 grid(cdiv(pw, tv::ops::kR2W), cdiv(ph, th), n);
+    if (tx <= 16)
+      tv::ops::k_resize2d<16><<<grid, 256, smem, s>>>(src, sw, sh, sstride, sfs, dst, dw, dh, dstride, dfs, pw, ph,
+                                                       th, wp, ix, wx, tx, iy, wy, ty);
+    else if (tx <= 32)
+      tv::ops::k_resize2d<32><<<grid, 256, smem, s>>>(src, sw, sh, sstride, sfs, dst, dw, dh, dstride, dfs, pw, ph,
+                                                       th, wp, ix, wx, tx, iy, wy, ty);
+    else
+      tv::ops::k_resize2d<64><<<grid, 256, smem, s>>>(src, sw, sh, sstride, sfs, dst, dw, dh, dstride, dfs, pw, ph,
+                                                       th, wp, ix, wx, tx, iy, wy, ty);
+    return ops_status();
+  }
   const long tfs = (long)sh * dw;
   tv::ops::k_resize_h<<<dim3(cdiv(dw, tv::ops::kTile), sh, n), tv::ops::kTile, 0, s>>>(src, sw, sstride, sfs, tmp,
                                                                                         tfs, dw, ix, wx, tx);

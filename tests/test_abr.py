@@ -20,6 +20,13 @@ def test_split_threads_proportional():
     assert sum(t) <= 16 + 2 * len(t)
 
 
+def test_resize2d_plan_fits_lds():
+    for geo in ((7680, 4320, 3840, 2160, 3840, 2176), (3840, 2160, 854, 480, 864, 480),
+                (640, 360, 426, 240, 448, 256)):
+        th, wp, smem = abr.resize2d_plan(*geo)
+        assert th >= 8 and wp % 4 == 0 and 0 < smem <= 40 * 1024
+
+
 def test_staging_layout_coded_size():
     L = abr.staging_layout(854, 480)
     assert (L["cw"], L["ch"]) == (864, 480)
@@ -30,14 +37,15 @@ def test_staging_layout_coded_size():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cascade", [False, True])
-def test_ladder_chunk_matches_single_frame_ops(cascade):
+@pytest.mark.parametrize("cascade,fused", [(False, True), (True, True), (True, False)])
+def test_ladder_chunk_matches_single_frame_ops(cascade, fused):
     import torch
 
     from thinvids_amd.models.gpu_engine import pad_frame
     from thinvids_amd.ops import color, resize
 
-    lad = abr.AbrLadder(src_w=640, src_h=360, heights=(240, 180, 120), segments=2, gop=3, cascade=cascade)
+    lad = abr.AbrLadder(src_w=640, src_h=360, heights=(240, 180, 120), segments=2, gop=3, cascade=cascade,
+                        fused=fused)
     try:
         lad.synth_p010(5, 3)
         y16, uv16 = lad.y16.clone(), lad.uv16.clone()

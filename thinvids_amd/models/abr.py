@@ -72,6 +72,32 @@ def _tables(n_in: int, n_out: int, a: int, dev_index: int):
     return torch.from_numpy(s.copy()).to(dev), torch.from_numpy(wq.copy()).to(dev), int(wq.shape[1])
 
 
+@lru_cache(maxsize=64)
+def resize2d_plan(sw: int, sh: int, dw: int, dh: int, pw: int, ph: int, a: int = 3,
+                  budget: int = 40 * 1024) -> tuple[int, int, int]:
+    """(th, wp, smem) for the fused k_resize2d: the tallest output tile (64 wide, th rows)
+    whose staged source window (R rows x wp bytes) + int16 intermediate (R x 64) fits the
+    LDS budget, over every tile of the plane (exact, from the filter tables).  40 KB keeps 4
+    workgroups (16 waves) per CU.  (0, 0, 0) -> the two-pass kernels."""
+    import numpy as np
+
+    from ..ops.resize import filter_table
+
+    ix, _, wxq = filter_table(sw, dw, a)
+    iy, _, wyq = filter_table(sh, dh, a)
+    tx, ty = wxq.shape[1], wyq.shape[1]
+    x0 = np.arange(0, pw, 64)
+    wmax = int((ix[np.minimum(x0 + 63, dw - 1)] + tx - ix[np.minimum(x0, dw - 1)]).max())
+    wp = (wmax + 3) & ~3
+    for th in (64, 48, 32, 24, 16, 12, 8, 4, 2, 1):
+        y0 = np.arange(0, ph, th)
+        rmax = int((iy[np.minimum(y0 + th - 1, dh - 1)] + ty - iy[np.minimum(y0, dh - 1)]).max())
+        smem = ((rmax * wp + 15) & ~15) + rmax * 64 * 2
+        if smem <= budget:
+            return th, wp, smem
+    return 0, 0, 0
+
+
 def _ops():
     from .._native import gpu_lib
 
@@ -81,7 +107,7 @@ def _ops():
         lib.tv_synth_p010.argtypes = [vp, vp, ci, ci, ci, ci, C.c_uint32, vp]
         lib.tv_tonemap_pq_batch.argtypes = [vp, vp, ci, ci, ci, vp, C.c_float, C.c_float, vp]
         lib.tv_resize_batch.argtypes = [vp, ci, ci, ci, cl, vp, ci, ci, ci, cl, ci, ci, ci,
-                                        vp, vp, ci, vp, vp, ci, vp, vp]
+                                        vp, vp, ci, vp, vp, ci, vp, ci, ci, ci, vp]
         lib.tv_ops_last_error.restype = C.c_char_p
         lib._abr_sigs = True
     return lib
@@ -100,7 +126,8 @@ class AbrLadder:
     def __init__(self, src_w: int = SRC_8K[0], src_h: int = SRC_8K[1], heights=LADDER, qp: int = 27,
                  segments: int = 16, gop: int = 16, device: int = 0, threads: int | None = None, seed: int = 1,
                  src_peak: float = 1000.0, dst_peak: float = 100.0, search_range: int = 16,
-                 concurrent: bool = True, sao: bool = False, cascade: bool = True, slots: int = 2):
+                 concurrent: bool = True, sao: bool = False, cascade: bool = True, slots: int = 2,
+                 fused: bool = True):
         import torch
 
         if (src_w | src_h) & 1:
@@ -108,7 +135,7 @@ class AbrLadder:
         self.src_w, self.src_h = src_w, src_h
         self.segments, self.gop, self.seed = segments, gop, seed
         self.src_peak, self.dst_peak = src_peak, dst_peak
-        self.concurrent, self.cascade = concurrent, cascade
+        self.concurrent, self.cascade, self.fused = concurrent, cascade, fused
         self.dev = torch.device("cuda", device)
         self.rungs = plan_rungs(src_w, src_h, heights)
         self.layouts = [staging_layout(w, h) for w, h in self.rungs]
@@ -126,7 +153,8 @@ class AbrLadder:
         self.y16 = torch.empty((gop, src_h, src_w), dtype=u16, device=self.dev)
         self.uv16 = torch.empty((gop, src_h // 2, src_w), dtype=u16, device=self.dev)
         self.sdr = torch.empty((gop, self.src_fsz), dtype=u8, device=self.dev)
-        self.tmp = torch.empty(gop * src_h * max(w for w, _ in self.rungs), dtype=i16, device=self.dev)
+        self.tmp = torch.empty(gop * src_h * max(w for w, _ in self.rungs) if not fused else 1, dtype=i16,
+                               device=self.dev)
         self.lib = _ops()
 
     def close(self) -> None:
@@ -167,9 +195,10 @@ class AbrLadder:
             for (soff, pw_, ph_, sstride), (doff, dw, dh, dstride, pw, ph) in zip(src_planes, L["planes"]):
                 ix, wx, tx = _tables(pw_, dw, 3, self.dev.index)
                 iy, wy, ty = _tables(ph_, dh, 3, self.dev.index)
+                th, wp, smem = resize2d_plan(pw_, ph_, dw, dh, pw, ph) if self.fused else (0, 0, 0)
                 _ok(lib, lib.tv_resize_batch(src_ptr + soff, pw_, ph_, sstride, sfs, base + doff, dw, dh, dstride,
                                              L["fsz"], pw, ph, n, ix.data_ptr(), wx.data_ptr(), tx, iy.data_ptr(),
-                                             wy.data_ptr(), ty, self.tmp.data_ptr(), st))
+                                             wy.data_ptr(), ty, self.tmp.data_ptr(), th, wp, smem, st))
 
     def prepare_synthetic(self, starts, slot: int = 0) -> None:
         """Segment b = synthetic frames [starts[b], starts[b] + gop)."""
