@@ -27,6 +27,15 @@ constexpr int kMeThreads = 320;
 constexpr int kWin = 72;       // window side: 32 + 2*16 + 8
 constexpr int kWinOff = 20;    // window origin = CTB origin - 20 (multiple of 4)
 constexpr int kWinW = kWin / 4;  // 32-bit words per window row
+// LDS pitch of a window row: odd, so the 32 lanes of a ds_read_b32 group — which walk the
+// candidate rows dy (item mapping below) — land on 32 distinct banks (19*d mod 32 is a
+// permutation); the old pitch 18 with dx-group-fast lanes was 2-way conflicted.
+constexpr int kWinP = kWinW + 1;
+// LDS pitch (words) of a source-CTB row.  Measured on MI355X: pitch 9 removes the sub-pel
+// stage's 4-way conflicts but costs 32 VGPRs (127, 4 waves/SIMD, -9 % end to end); pitch 10
+// (+ amdgpu_waves_per_eu(5)) cuts k_inter_me bank conflicts 16 -> 13.6 % at equal speed.
+// Kept at 8: the integer search's uniform s0/s1 pair stays one aligned 8-byte read.
+constexpr int kSrcP = 8;
 
 __device__ __forceinline__ void me_blk_geom(int bi, int& bx, int& by, int& l2) {
   if (bi < 16) {
@@ -62,12 +71,14 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
   const uint8_t* S = src.plane(0, b, g);
   const uint8_t* R = ref.plane(0, b, g);
-  __shared__ uint32_t s32[256];
-  __shared__ uint32_t win[kWin * kWinW];
+  __shared__ uint32_t s32[32 * kSrcP];
+  __shared__ uint32_t win[kWin * kWinP];
   __shared__ unsigned best[21];
   __shared__ int bcost[21], bmv[21][2];
   __shared__ int subsad[21][8];
-  if (tid < 256) s32[tid] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (tid >> 3)) * g.W + cx + 4 * (tid & 7));
+  if (tid < 256)
+    s32[(tid >> 3) * kSrcP + (tid & 7)] =
+        *reinterpret_cast<const uint32_t*>(S + (long)(cy + (tid >> 3)) * g.W + cx + 4 * (tid & 7));
   for (int w = tid; w < ((ablate & 4) ? 0 : kWin * kWinW); w += kMeThreads) {
     const int row = w / kWinW, wc = w % kWinW;
     const int gy = clip3(0, g.H - 1, cy - kWinOff + row);
@@ -79,7 +90,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       v = 0;
       for (int k = 0; k < 4; ++k) v |= (uint32_t)R[(long)gy * g.W + clip3(0, g.W - 1, gx0 + k)] << (8 * k);
     }
-    win[w] = v;
+    win[row * kWinP + wc] = v;
   }
   if (tid < 21) best[tid] = 0xffffffffu;
   __syncthreads();
@@ -90,7 +101,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
 #pragma unroll
   for (int k = 0; k < 21; ++k) lb[k] = 0xffffffffu;
   for (int item = tid; item < ((ablate & 1) ? 0 : items); item += kMeThreads) {
-    const int dyi = item / groups, gi = item - dyi * groups;
+    const int gi = item / side, dyi = item - gi * side;  // dy fastest across lanes (banks)
     const int dy = dyi - range, dx0 = 4 * gi - range;
     // per-shift rate term and packed candidate index; shifts beyond +R are excluded with a
     // penalty larger than any SAD (keeps the update branch-free)
@@ -115,9 +126,9 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       unsigned acc[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int srow = (by + j) * 8 + (bx >> 2);
+        const int srow = (by + j) * kSrcP + (bx >> 2);
         const uint32_t s0 = s32[srow], s1 = s32[srow + 1];
-        const int wrow = (kWinOff + dy + by + j) * kWinW + ((kWinOff + dx0 + bx) >> 2);
+        const int wrow = (kWinOff + dy + by + j) * kWinP + ((kWinOff + dx0 + bx) >> 2);
         const uint32_t w0 = win[wrow], w1 = win[wrow + 1], w2 = win[wrow + 2];
         acc[0] = __builtin_amdgcn_sad_u8(w1, s1, __builtin_amdgcn_sad_u8(w0, s0, acc[0]));
 #pragma unroll
@@ -196,7 +207,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
       const int gx0 = cx + bx + col0 + (mx >> 2);
       const int gy0 = cy + by + row0 + (my >> 2);
-      const int sw = ((by + row0) * 32 + bx + col0) >> 2;  // source word index of row 0
+      const int sw = (by + row0) * kSrcP + ((bx + col0) >> 2);  // source word index of row 0
       unsigned s = 0;
       if (gx0 >= -8 && gx0 + 11 <= g.W + 7 && gy0 >= -8 && gy0 + 7 <= g.H + 7) {
         const int a = gx0 & ~3, sh = gx0 & 3;
@@ -207,14 +218,16 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
           const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
           const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
           const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-          s = __builtin_amdgcn_sad_u8(hi, s32[sw + 8 * j + 1], __builtin_amdgcn_sad_u8(lo, s32[sw + 8 * j], s));
+          s = __builtin_amdgcn_sad_u8(hi, s32[sw + kSrcP * j + 1],
+                                      __builtin_amdgcn_sad_u8(lo, s32[sw + kSrcP * j], s));
         }
       } else {  // touches the clamped border: per-pixel path
         for (int j = 0; j < 8; ++j) {
           const int gy = clip3(-8, g.H + 7, gy0 + j);
           for (int i = 0; i < 8; ++i) {
             const int gx = clip3(-8, g.W + 7, gx0 + i);
-            s += tv_abs((int)sb[(by + row0 + j) * 32 + bx + col0 + i] - (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
+            s += tv_abs((int)sb[(by + row0 + j) * 4 * kSrcP + bx + col0 + i] -
+                        (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
           }
         }
       }
