@@ -9,7 +9,66 @@ namespace gpu {
 
 // ---------------------------------- synthetic source ------------------------------------
 // One workgroup row-tile; the per-frame object trajectories are evaluated once per
-// workgroup into LDS (they were 18 hashes per pixel before).
+// workgroup into LDS (they were 18 hashes per pixel before).  Each thread produces 4
+// horizontally adjacent samples (one dword store): the value-noise octaves keep their
+// lattice-corner hashes across the 4 samples (a cell is >= 4 px wide, so the cell changes at
+// most once: 2 new hashes instead of 4 per octave per sample), and the row terms (cell row,
+// vertical smoothstep) are computed once.  Bit-identical to synth_sample_ctx (tv/synth.h),
+// which the CPU golden encoder uses.
+struct VNoiseRow {
+  int sh, sy;
+  int32_t cy, cx;
+  uint32_t seed;
+  int a, b, c, d;
+  __device__ void init(int32_t py16, int lp, uint32_t sd) {
+    sh = lp + 4;
+    seed = sd;
+    cy = py16 >> sh;
+    const int fy = (int)((py16 - (cy << sh)) << 8 >> sh);
+    sy = (fy * fy * (768 - 2 * fy)) >> 16;
+    cx = INT32_MIN;
+  }
+  __device__ int eval(int32_t px16) {
+    const int32_t nx = px16 >> sh;
+    if (nx != cx) {
+      if (nx == cx + 1) {
+        a = b;
+        c = d;
+      } else {
+        a = synth_hash(nx, cy, seed) & 255;
+        c = synth_hash(nx, cy + 1, seed) & 255;
+      }
+      b = synth_hash(nx + 1, cy, seed) & 255;
+      d = synth_hash(nx + 1, cy + 1, seed) & 255;
+      cx = nx;
+    }
+    const int fx = (int)((px16 - (cx << sh)) << 8 >> sh);
+    const int sx = (fx * fx * (768 - 2 * fx)) >> 16;
+    const int top = a * 256 + (b - a) * sx;
+    const int bot = c * 256 + (d - c) * sx;
+    return (top * 256 + (bot - top) * sy) >> 16;
+  }
+};
+
+__device__ __forceinline__ int synth_objects(const SynthFrameCtx& f, int c, int xl, int yl, int v) {
+  for (int k = 0; k < kSynthObjects; ++k) {  // later objects on top
+    const SynthObject& o = f.obj[k];
+    const int32_t rx16 = xl * 16 - f.ox[k], ry16 = yl * 16 - f.oy[k];
+    if (rx16 < 0 || ry16 < 0 || rx16 >= o.w * 16 || ry16 >= o.h * 16) continue;
+    if (o.shape == 1) {
+      const int64_t dx = 2 * (int64_t)rx16 - o.w * 16, dy = 2 * (int64_t)ry16 - o.h * 16;
+      const int64_t ww = (int64_t)o.w * 16, hh = (int64_t)o.h * 16;
+      if (dx * dx * hh * hh + dy * dy * ww * ww > ww * ww * hh * hh) continue;
+    }
+    if (c == 0) {
+      v = 40 + ((synth_vnoise(rx16, ry16, 4, o.seed) * 3 + synth_vnoise(rx16, ry16, 2, o.seed + 5)) >> 2) * 3 / 4;
+    } else {
+      v = 64 + (int)(synth_hash(k, c, f.seed) & 127) + (synth_vnoise(rx16, ry16, 5, o.seed + c) >> 3);
+    }
+  }
+  return v;
+}
+
 __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t seed, FrameIdx fi) {
   const int c = blockIdx.y, b = blockIdx.z;
   const int pw = c ? g.W / 2 : g.W, ph = c ? g.H / 2 : g.H;
@@ -18,9 +77,32 @@ __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t see
   if (threadIdx.x == 0) synth_frame_ctx(seed, fi.t[b], g.dw, g.dh, ctx);
   __syncthreads();
   uint8_t* P = src.plane(c, b, g);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < pw * ph; i += gridDim.x * blockDim.x) {
-    const int x = i % pw, y = i / pw;
-    P[i] = (uint8_t)synth_sample_ctx(ctx, c, tv_min(x, dw - 1), tv_min(y, dh - 1));
+  const int s = c ? 1 : 0, pq = pw >> 2;  // pw is a multiple of 16
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < pq * ph; i += gridDim.x * blockDim.x) {
+    const int y = i / pq, x0 = (i - y * pq) * 4;
+    const int yl = tv_min(y, dh - 1) << s;
+    const int32_t by16 = yl * 16 + ctx.t * 12;
+    VNoiseRow n0, n1, n2;
+    if (c == 0) {
+      n0.init(by16, 7, ctx.seed);
+      n1.init(by16, 5, ctx.seed + 1);
+      n2.init(by16, 3, ctx.seed + 2);
+    } else {
+      n0.init(by16, 8, ctx.seed + 10 * c);
+    }
+    uint32_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int xl = tv_min(x0 + j, dw - 1) << s;
+      const int32_t bx16 = xl * 16 + ctx.t * 36;
+      int v;
+      if (c == 0)
+        v = (n0.eval(bx16) * 5 + n1.eval(bx16) * 2 + n2.eval(bx16)) >> 3;
+      else
+        v = 96 + (n0.eval(bx16) >> 1);
+      word |= (uint32_t)clip_pixel(synth_objects(ctx, c, xl, yl, v)) << (8 * j);
+    }
+    *reinterpret_cast<uint32_t*>(P + (long)y * pw + x0) = word;
   }
 }
 
