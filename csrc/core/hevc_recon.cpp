@@ -18,15 +18,15 @@ void predict_intra_tb(const Picture& rec, int cIdx, int x, int y, int log2N, int
   bool la[65], ta[65];
   // corner
   {
-    const bool a = zscan_available(xL, yL, (x - 1) << s, (y - 1) << s, W, H);
+    const bool a = zscan_available(xL, yL, (x - 1) * (1 << s), (y - 1) * (1 << s), W, H);
     la[0] = ta[0] = a;
     left[0] = top[0] = a ? P[(y - 1) * pw + (x - 1)] : 0;
   }
   for (int i = 0; i < 2 * N; ++i) {
-    const bool al = zscan_available(xL, yL, (x - 1) << s, (y + i) << s, W, H);
+    const bool al = zscan_available(xL, yL, (x - 1) * (1 << s), (y + i) * (1 << s), W, H);
     la[i + 1] = al;
     left[i + 1] = al ? P[(y + i) * pw + (x - 1)] : 0;
-    const bool at = zscan_available(xL, yL, (x + i) << s, (y - 1) << s, W, H);
+    const bool at = zscan_available(xL, yL, (x + i) * (1 << s), (y - 1) * (1 << s), W, H);
     ta[i + 1] = at;
     top[i + 1] = at ? P[(y - 1) * pw + (x + i)] : 0;
   }

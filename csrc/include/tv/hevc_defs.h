@@ -81,7 +81,7 @@ TV_HD int chroma_qp(int qpy, int offset) {
 TV_HD int dequant_level(int level, int qp, int log2N) {
   const int bdShift = 8 + log2N - 5;  // BitDepth + log2(nTbS) + 10 - 15
   long long v = (long long)level * 16 * kLevelScale[qp % 6];
-  v = (v << (qp / 6)) + (1LL << (bdShift - 1));
+  v = v * (1LL << (qp / 6)) + (1LL << (bdShift - 1));  // multiply: v may be negative
   v >>= bdShift;
   return (int)clip3<long long>(-32768, 32767, v);
 }
