@@ -262,7 +262,10 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     rungs = [output_geometry(w0, h0, th) for th in heights]
     segs = plan_segments(nfr, segment_frames, gop)
     software = software or not gpu_available()
-    cache = None if software else EngineCache(device=dev.index or 0, batch=batch_segments)
+    # one engine per rung stays resident (a 5-rung ladder thrashed the default 4-engine cache:
+    # every eviction re-allocates an engine's HBM and streams)
+    cache = None if software else EngineCache(device=dev.index or 0, batch=batch_segments,
+                                              max_engines=max(4, len(rungs)))
     jobs = [(r, i) for r in range(len(rungs)) for i in range(len(segs))]  # ladder fan-out (P10)
     ckpt = Checkpoint(resume_dir)
     stats = {"encoded": 0, "resumed": 0, "retried": 0}
@@ -322,7 +325,10 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     return
                 try:
                     with trace.span("node_job.load"):
-                        items = [((r, i), prepare_frames(load(i), *rungs[r]), spec(r, qps[r][i])) for r, i in todo]
+                        src_frames: dict = {}  # a segment is read once for all of its rungs
+                        items = [((r, i), prepare_frames(src_frames[i] if i in src_frames
+                                                         else src_frames.setdefault(i, load(i)), *rungs[r]),
+                                  spec(r, qps[r][i])) for r, i in todo]
                     with trace.span("node_job.encode", segments=len(items)):
                         got = _encode_many(items, None, cache)
                 except Exception as e:  # a real engine/IO failure: every item goes back
