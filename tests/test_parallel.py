@@ -207,13 +207,29 @@ def test_node_job_elastic_restart_torchrun(tmp_path, source):
            "--max-restarts", "1", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            "-m", "thinvids_amd.parallel.node_job", "--input", src, "--output", str(out), "--software",
            "--gop", "8", "--segment-frames", "8", "--resume-dir", str(tmp_path / "ck"), "--timeout-sec", "60"]
-    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
-    if p.returncode != 0 and "connectFullMesh" in p.stderr:
+    import signal
+
+    def run_once():
+        # own session so a hung attempt's torchrun *and* its workers can be killed as one group
+        proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                start_new_session=True)
+        try:
+            so, se = proc.communicate(timeout=150)
+            return proc.returncode, so, se
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
+            so, se = proc.communicate()
+            return -9, so, se + "\n[test] attempt timed out"
+
+    rc, so, se = run_once()
+    if rc != 0 and ("connectFullMesh" in se or rc == -9):
         # gloo's post-restart mesh setup can race the restarted peer's listener on a loaded
-        # host (connection refused); that is the transport, not the resume logic under test —
-        # run the job once more on a fresh port (the fault already fired, checkpoints remain).
+        # host (connection refused, or a rendezvous that never completes); that is the transport,
+        # not the resume logic under test — run the job once more on a fresh port (the fault
+        # already fired, checkpoints remain).
         cmd[cmd.index("--master-port") + 1] = str(_free_port())
-        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        rc, so, se = run_once()
+    p = subprocess.CompletedProcess(cmd, rc, so, se)
     assert p.returncode == 0, p.stderr[-3000:]
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["world"] == 2 and len(os.listdir(tmp_path / "fs")) == 1  # the fault fired once
