@@ -121,6 +121,23 @@ def test_node_job_ladder_single_process(tmp_path, source):
     assert len(dec.frames) == 24 and dec.frames[0][0].shape == (48, 64)
 
 
+@pytest.mark.gpu
+def test_node_job_ladder_gpu_engine(tmp_path, source, monkeypatch):
+    """Same ladder fan-out on the HIP engine: one resident engine per rung, each segment read
+    once for both rungs (node_job.run), every rung decodes to the full clip."""
+    from thinvids_amd.models import hevc
+    from thinvids_amd.parallel.node_job import run_job
+
+    monkeypatch.delenv("TV_FORCE_CPU", raising=False)
+    src, frames = source
+    res = run_job(src, str(tmp_path / "lad.mp4"), gop=8, segment_frames=16, ladder=[96, 72], software=False)  # engine needs >= 64x64
+    assert [o["height"] for o in res["outputs"]] == [96, 72]
+    for o in res["outputs"]:
+        with open(o["path"], "rb") as f:
+            dec = hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False)
+        assert len(dec.frames) == 24 and dec.frames[0][0].shape == (o["height"], o["width"])
+
+
 def _job_worker_env(rank, world, port, src, out, kw, res_path, env):
     os.environ.update(env)
     from thinvids_amd.parallel.node_job import run_job
