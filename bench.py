@@ -29,19 +29,111 @@ LADDER_METRIC = "HDR10 source frames/sec (whole node) through a tone-map + Lancz
 
 
 def _dist_setup(args):
+    """One rank per GPU, always inside a live RCCL (`nccl`) process group — also at N=1, so
+    the same all_reduce / all_gather code runs on the GPU whatever N is.  The rank's CPU set
+    (CABAC pool) is pinned NUMA-local before the engine spawns its threads."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    from thinvids_amd.parallel.launch import free_port, pin_rank
+
+    if "WORLD_SIZE" not in os.environ:  # N=1 without a launcher: a one-rank group
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", LOCAL_WORLD_SIZE="1",
+                          MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    cpus = pin_rank(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    return world, rank, local, dev
+    dist.init_process_group("nccl", device_id=dev)
+    assert dist.get_world_size() == args.gpus, "live group size != --gpus"
+    return dist.get_world_size(), dist.get_rank(), local, dev, cpus
+
+
+class _CpuMeter:
+    """Process CPU seconds (all threads: CABAC pool + Python) over the timed region."""
+
+    def start(self):
+        import resource
+
+        r = resource.getrusage(resource.RUSAGE_SELF)
+        self.c0, self.t0 = r.ru_utime + r.ru_stime, time.perf_counter()
+
+    def cores(self) -> float:
+        import resource
+
+        r = resource.getrusage(resource.RUSAGE_SELF)
+        return (r.ru_utime + r.ru_stime - self.c0) / max(1e-9, time.perf_counter() - self.t0)
+
+
+def _per_rank(values, dev):
+    """all_gather a small float vector from every rank -> list of lists (rank order)."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(values, dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[round(float(x), 3) for x in o.cpu()] for o in out]
+
+
+class _PostQueue:
+    """Per-step communication (RC/quality stats all-reduce + bitstream gather to the stitch
+    rank) on one background thread, so step s's collectives overlap step s+1's encode.  Only
+    this thread issues collectives between start and drain, so every rank issues them in the
+    same order."""
+
+    def __init__(self, local: int):
+        import concurrent.futures as cf
+
+        import torch
+
+        self.ex = cf.ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(local))
+        self.futs = []
+
+    def submit(self, fn, *a):
+        self.futs.append(self.ex.submit(fn, *a))
+
+    def drain(self):
+        out = [f.result() for f in self.futs]
+        self.futs = []
+        return out
+
+    def close(self):
+        self.ex.shutdown(wait=True)
+
+
+def _timed(args, step, dev, world, post, extra_ranks=None):
+    """W untimed warm-up steps, then exactly K timed steps bracketed by barrier + device
+    synchronise on both sides; returns (elapsed = MAX over ranks, per-step ms, post results,
+    per-rank [cpu cores busy, cpus pinned])."""
+    import torch
+    import torch.distributed as dist
+
+    for s in range(args.warmup):
+        step(-1 - s)
+    post.drain()
+    dist.barrier()
+    torch.cuda.synchronize()
+    meter = _CpuMeter()
+    meter.start()
+    t0 = time.perf_counter()
+    step_ms = []
+    for s in range(args.steps):
+        ts = time.perf_counter()
+        step(s)
+        step_ms.append(round(1000 * (time.perf_counter() - ts), 2))
+    res = post.drain()  # the last step's collectives complete inside the timed region
+    dist.barrier()
+    torch.cuda.synchronize()
+    el_t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    cores = meter.cores()
+    dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    ranks = _per_rank([cores] + list(extra_ranks or []), dev)
+    return float(el_t.item()), step_ms, res, ranks
 
 
 def ladder_main(args) -> None:
@@ -57,17 +149,25 @@ def ladder_main(args) -> None:
     from thinvids_amd.models.abr import AbrLadder
     from thinvids_amd.parallel.comm import gather_bytes_to_root
 
-    world, rank, local, dev = _dist_setup(args)
+    world, rank, local, dev, cpus = _dist_setup(args)
     sw, sh = SRC[args.src]
     heights = [int(x) for x in args.ladder.split(",") if x.strip()]
     batch = args.batch or 24  # measured 8K ladder: b8 183, b16 360, b24 373, b32 365 source frames/s
     lad = AbrLadder(sw, sh, heights, qp=args.qp, segments=batch, gop=args.gop, device=local,
                     threads=args.threads or None, seed=args.seed, search_range=args.range, sao=args.sao)
+    post = _PostQueue(local)
 
     def prep(i: int):  # step i's source -> tone-map -> rungs into staging slot i % 2
         base = (i * world + rank) * batch
         lad.prepare_synthetic([(base + b) * args.gop for b in range(batch)], slot=i % 2)
         torch.cuda.current_stream(dev).synchronize()
+
+    def comm(segs):
+        nbytes = sum(len(x) for r in segs for x in r)
+        t = torch.tensor([batch * args.gop, nbytes], dtype=torch.float64, device=dev)
+        dist.all_reduce(t)
+        gather_bytes_to_root(b"".join(x for r in segs for x in r), dev)
+        return t.cpu().numpy()
 
     # step i encodes staging slot i % 2 while this thread prepares step i + 1 into the other
     # slot (every step = one full prep + one full encode; prep(0) runs before warm-up)
@@ -78,35 +178,10 @@ def ladder_main(args) -> None:
         i = counter[0]
         counter[0] += 1
         segs = lad.encode_overlapped(batch, i % 2, prepare_next=lambda: prep(i + 1))
-        nbytes = sum(len(x) for r in segs for x in r)
-        stats = np.array([batch * args.gop, nbytes], dtype=np.float64)
-        if world > 1:
-            t = torch.from_numpy(stats).to(dev)
-            dist.all_reduce(t)
-            stats = t.cpu().numpy()
-            gather_bytes_to_root(b"".join(x for r in segs for x in r), dev)
-        return stats
+        post.submit(comm, segs)
 
-    for s in range(args.warmup):
-        step(-1 - s)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    tot = None
-    step_ms = []
-    for s in range(args.steps):
-        ts = time.perf_counter()
-        st = step(s)
-        step_ms.append(round(1000 * (time.perf_counter() - ts), 2))
-        tot = st if tot is None else tot + st
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el_t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = float(el_t.item())
+    el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), lad.engines[0].threads])
+    tot = np.sum(res, axis=0)
     q = lad.psnr()
     if rank == 0:
         tm = [e.timing() for e in lad.engines]
@@ -135,12 +210,14 @@ def ladder_main(args) -> None:
                 "mbit_per_step": round(tot[1] * 8 / 1e6 / args.steps, 2),
                 "last_step_gpu_ms_per_rung": [round(t["gpu_ms"], 2) for t in tm],
                 "last_step_entropy_cpu_ms_per_rung": [round(t["entropy_cpu_ms"], 2) for t in tm],
+                "per_rank_cpu": [{"busy_cores": r[0], "pinned_cpus": int(r[1]), "cabac_threads": int(r[2])}
+                                 for r in ranks],
                 "step_ms": step_ms,
             },
         }), flush=True)
+    post.close()
     lad.close()
-    if world > 1:
-        dist.destroy_process_group()
+    dist.destroy_process_group()
 
 
 def main() -> None:
@@ -159,6 +236,11 @@ def main() -> None:
     ap.add_argument("--ladder", default="", help="ABR mode (config #5): rung heights, e.g. 2160,1440,1080,720,480")
     ap.add_argument("--src", default="8k", choices=sorted(SRC), help="ABR mode: HDR10 source resolution")
     args = ap.parse_args()
+    from thinvids_amd.parallel.launch import launched_by_torchrun, spawn_ranks
+
+    if args.gpus > 1 and not launched_by_torchrun():
+        # self-launch: N ranks (one per GPU) started before this parent touches the GPU
+        sys.exit(spawn_ranks(args.gpus, [os.path.abspath(__file__), *sys.argv[1:]]))
     if args.ladder:
         return ladder_main(args)
 
@@ -166,15 +248,7 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    world, rank, local, dev, cpus = _dist_setup(args)
 
     from thinvids_amd.models.gpu_engine import GpuEngine
     from thinvids_amd.parallel.comm import gather_bytes_to_root
@@ -187,55 +261,29 @@ def main() -> None:
     batch = args.batch or (48 if args.res in ("1080p", "720p", "360p") else 24)
     eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=args.sao,
                     seed=args.seed, threads=args.threads or None, device=local)
+    post = _PostQueue(local)
 
-    prof = {"encode": 0.0, "post": 0.0}
+    def comm(segs, sse):
+        # rate-control / quality statistics all-reduce + bitstreams -> stitch rank (rank 0)
+        stats = torch.tensor([batch * args.gop, sum(len(x) for x in segs), *sse], dtype=torch.float64, device=dev)
+        dist.all_reduce(stats)
+        gathered = gather_bytes_to_root(b"".join(segs), dev)
+        return stats.cpu().numpy(), (sum(len(x) for x in gathered) if gathered else 0)
 
     def step(s: int):
         base = (s * world + rank) * batch
-        t_a = time.perf_counter()
         segs = eng.encode_synthetic([(base + b) * args.gop for b in range(batch)])
-        t_b = time.perf_counter()
-        prof["encode"] += t_b - t_a
-        sse = np.array([eng.sse(b) for b in range(batch)]).sum(0)
-        nbytes = sum(len(x) for x in segs)
-        stats = np.array([batch * args.gop, nbytes, *sse], dtype=np.float64)
-        gathered = None
-        if world > 1:
-            t = torch.from_numpy(stats).to(dev)
-            dist.all_reduce(t)  # rate-control / quality statistics
-            stats = t.cpu().numpy()
-            gathered = gather_bytes_to_root(b"".join(segs), dev)  # bitstreams -> stitch rank
-        prof["post"] += time.perf_counter() - t_b
-        return stats, gathered
+        post.submit(comm, segs, np.array([eng.sse(b) for b in range(batch)]).sum(0))
 
-    for s in range(args.warmup):
-        step(-1 - s)
-    prof["encode"] = prof["post"] = 0.0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    tot = None
-    step_ms = []
-    for s in range(args.steps):
-        ts = time.perf_counter()
-        stats, _ = step(s)
-        step_ms.append(round(1000 * (time.perf_counter() - ts), 2))
-        tot = stats if tot is None else tot + stats
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = float(el_t.item())
+    el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), eng.threads])
+    tot = np.sum([r[0] for r in res], axis=0)
+    gathered_bytes = sum(r[1] for r in res)
     frames = tot[0]
     npx = frames * w * h
     psnr = lambda s, n: float(10 * np.log10(255.0 ** 2 * n / s)) if s > 0 else float("inf")
     py, pu, pv = psnr(tot[2], npx), psnr(tot[3], npx / 4), psnr(tot[4], npx / 4)
     fps = frames / el
-    kbps = tot[1] * 8 / (frames / 30.0) / 1000.0 / world  # per 30 fps stream
+    kbps = tot[1] * 8 / (frames / 30.0) / 1000.0  # per 30 fps stream
     if rank == 0:
         tm = eng.timing()
         print(json.dumps({
@@ -256,25 +304,26 @@ def main() -> None:
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",
+                "comm": f"rccl world={world}: stats all_reduce + bitstream gather to rank 0 (overlapped)",
                 "resolution": f"{w}x{h}",
                 "segments_per_gpu": batch,
                 "frames_per_segment": args.gop,
                 "psnr_y_db": round(py, 3),
                 "psnr_yuv_db": round((6 * py + pu + pv) / 8, 3),
                 "kbps_per_30fps_stream": round(kbps, 1),
+                "gathered_mb_at_root": round(gathered_bytes / 1e6, 3),
                 "last_step_gpu_ms": round(tm["gpu_ms"], 2),
                 "last_step_engine_wall_ms": round(tm["wall_ms"], 2),
                 "last_step_entropy_cpu_ms": round(tm["entropy_cpu_ms"], 2),
                 "last_step_coef_mb_d2h": round(tm["coef_mb"], 2),
-                "encode_s": round(prof["encode"], 3),
-                "post_s": round(prof["post"], 3),
-                "cpu_threads": eng.threads,
+                "per_rank_cpu": [{"busy_cores": r[0], "pinned_cpus": int(r[1]), "cabac_threads": int(r[2])}
+                                 for r in ranks],
                 "step_ms": step_ms,
             },
         }), flush=True)
+    post.close()
     eng.close()
-    if world > 1:
-        dist.destroy_process_group()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

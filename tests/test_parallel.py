@@ -114,8 +114,11 @@ def test_node_job_ladder_single_process(tmp_path, source):
 
     os.environ["TV_FORCE_CPU"] = "1"
     src, frames = source
-    res = run_job(src, str(tmp_path / "lad.mp4"), gop=8, segment_frames=16, ladder=[96, 48], software=True)
+    res = run_job(src, str(tmp_path / "lad.mp4"), gop=8, segment_frames=8, ladder=[96, 48], software=True,
+                  batch_segments=2)
     assert [o["height"] for o in res["outputs"]] == [96, 48] and res["outputs"][1]["width"] == 64
+    # 3 segments (more than one claimed batch), 2 rungs: each segment read exactly once
+    assert res["per_rank"][0]["reads"] == 3 and res["per_rank"][0]["encoded"] == 6
     with open(res["outputs"][1]["path"], "rb") as f:
         dec = hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False)
     assert len(dec.frames) == 24 and dec.frames[0][0].shape == (48, 64)
@@ -128,10 +131,24 @@ def test_node_job_ladder_gpu_engine(tmp_path, source, monkeypatch):
     from thinvids_amd.models import hevc
     from thinvids_amd.parallel.node_job import run_job
 
+    from thinvids_amd.models import gpu_engine
+
     monkeypatch.delenv("TV_FORCE_CPU", raising=False)
+    built = []
+    orig = gpu_engine.GpuEngine.__init__
+
+    def counting_init(self, *a, **k):
+        built.append((a, k))
+        orig(self, *a, **k)
+
+    monkeypatch.setattr(gpu_engine.GpuEngine, "__init__", counting_init)
     src, frames = source
-    res = run_job(src, str(tmp_path / "lad.mp4"), gop=8, segment_frames=16, ladder=[96, 72], software=False)  # engine needs >= 64x64
+    # 3 segments of 8 frames in claims of 2: more segments than one batch
+    res = run_job(src, str(tmp_path / "lad.mp4"), gop=8, segment_frames=8, ladder=[96, 72], software=False,
+                  batch_segments=2)  # engine needs >= 64x64
     assert [o["height"] for o in res["outputs"]] == [96, 72]
+    assert res["per_rank"][0]["reads"] == 3  # each segment read once for both rungs
+    assert len(built) == 2  # one resident engine per rung
     for o in res["outputs"]:
         with open(o["path"], "rb") as f:
             dec = hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False)
@@ -156,7 +173,7 @@ def _spawn_job(tmp_path, source, kw, env, world=2):
     src, frames = source
     out = str(tmp_path / "out.mp4")
     res_path = str(tmp_path / "res.json")
-    kw = dict(gop=8, segment_frames=8, batch_segments=1, **kw)
+    kw = {"gop": 8, "segment_frames": 8, "batch_segments": 1, **kw}
     mp.spawn(_job_worker_env, args=(world, _free_port(), src, out, kw, res_path, env), nprocs=world, join=True)
     return [json.load(open(f"{res_path}.{r}")) for r in range(world)], out
 
@@ -180,7 +197,7 @@ def test_node_job_abort_after_retry_budget(tmp_path, source):
     res, _ = _spawn_job(tmp_path, source, {"max_retries": 1}, {"TV_FAULT": "segment:2:fail"})
     # the rank that sees the abort flag first raises; ranks whose store host (rank 0) exits
     # first fail on the store connection — either way no rank stitches a partial output
-    assert any("segment (0, 2) failed 2 times" in r.get("error", "") for r in res), res
+    assert any("segment (2,) failed 2 times" in r.get("error", "") for r in res), res
     assert all(r.get("error") for r in res), res
 
 
@@ -200,14 +217,19 @@ def test_node_job_segment_resume(tmp_path, source):
     assert sum(p["resumed"] for p in per) == 3 and sum(p["encoded"] for p in per) == 0
     assert open(out, "rb").read() == first
     # a corrupted checkpoint is re-encoded, not trusted
-    seg = sorted(p for p in os.listdir(ck) if p.endswith(".hevc"))[0]
-    with open(os.path.join(ck, seg), "r+b") as f:
+    (fp,) = os.listdir(ck)  # one job fingerprint directory
+    seg = sorted(p for p in os.listdir(os.path.join(ck, fp)) if p.endswith(".hevc"))[0]
+    with open(os.path.join(ck, fp, seg), "r+b") as f:
         f.seek(40)
         f.write(b"\xff\xff")
     res3, out = _spawn_job(tmp_path, source, {"resume_dir": ck}, {})
     per = res3[0]["per_rank"]
     assert sum(p["resumed"] for p in per) == 2 and sum(p["encoded"] for p in per) == 1
     assert open(out, "rb").read() == first
+    # a different job (other GOP) in the same resume dir never reuses these segments
+    res4, _ = _spawn_job(tmp_path, source, {"resume_dir": ck, "gop": 4}, {})
+    assert sum(p["resumed"] for p in res4[0]["per_rank"]) == 0
+    assert len(os.listdir(ck)) == 2
 
 
 def test_node_job_elastic_restart_torchrun(tmp_path, source):

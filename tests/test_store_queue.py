@@ -126,3 +126,31 @@ def test_redispatch_policy():
     assert newly == [] and retry == [3, 4] and not give  # oldest misses, capped at 2
     newly, retry, give = plan_redispatch({1, 2, 5}, 10, 10, now, now - 60, seen, {3: 2}, {3: now - 100}, 10, t)
     assert 3 not in retry and give  # retry budget exhausted long ago -> give up
+
+
+def test_batch_refuses_private_nested_and_blocking_ops():
+    import json
+    import socket
+
+    srv = StoreServer("127.0.0.1", 0)
+    srv.start_background()
+    try:
+        srv.store.set("keep", "1")
+        s = socket.create_connection(srv.server_address)
+        f = s.makefile("rwb")
+        for bad in (["__init__", [], {}], ["blpop", [["q"], 0], {}], ["execute_batch", [[]], {}],
+                    ["_new", ["x", "string"], {}]):
+            f.write((json.dumps({"batch": [["set", ["a", "1"], {}], bad]}) + "\n").encode())
+            f.flush()
+            resp = json.loads(f.readline())
+            assert "err" in resp and "not allowed" in resp["err"], resp
+        f.write((json.dumps({"op": "__init__", "args": []}) + "\n").encode())
+        f.flush()
+        assert "err" in json.loads(f.readline())
+        assert srv.store.get("keep") == "1" and srv.store.get("a") is None  # nothing ran
+        with pytest.raises(ValueError):
+            LocalStore().execute_batch([("blpop", [["q"], 0], {})])
+        s.close()
+    finally:
+        srv.shutdown()
+        srv.server_close()

@@ -23,18 +23,46 @@ i16p = C.POINTER(C.c_int16)
 vp = C.c_void_p
 
 
-def _ensure_built(name: str) -> Path:
-    path = LIBDIR / name
-    if not path.exists() and os.environ.get("TV_NO_AUTOBUILD") != "1":
-        from . import _build
+def _which(name: str) -> str:
+    return "core" if name == "libtvcore.so" else "gpu"
 
+
+def _embedded_ok(path: Path, digest: str) -> bool:
+    """The library's exported build hash (a string literal in .rodata) equals `digest`."""
+    try:
+        return digest.encode() in path.read_bytes()
+    except OSError:
+        return False
+
+
+def _ensure_built(name: str) -> Path:
+    """Return the library path, guaranteeing it was built from the CURRENT sources: the
+    content hash embedded at link time must match the hash of csrc/ now.  A missing or
+    stale library is rebuilt (TV_NO_AUTOBUILD=1: refused loudly instead)."""
+    from . import _build
+
+    path = LIBDIR / name
+    have_src = (_build.CSRC / "core").is_dir()
+    want = _build.expected_hash(_which(name)) if have_src else None
+    if want is not None and not _embedded_ok(path, want):
+        if os.environ.get("TV_NO_AUTOBUILD") == "1":
+            state = "stale (built from other sources)" if path.exists() else "missing"
+            raise RuntimeError(f"native library {path} is {state}; run `python -m thinvids_amd._build`")
         if name == "libtvcore.so":
             _build.build_core()
         else:
             _build.build_gpu()
+        if not _embedded_ok(path, want):
+            raise RuntimeError(f"native library {path} does not match the sources after a rebuild")
     if not path.exists():
         raise RuntimeError(f"native library {path} is missing; run `python -m thinvids_amd._build`")
     return path
+
+
+def build_hash(lib, which: str) -> str:
+    f = getattr(lib, f"tv_{which}_build_hash")
+    f.restype = C.c_char_p
+    return f().decode()
 
 
 def _sig(lib, name, res, args):

@@ -26,11 +26,17 @@ def _world():
     return dist.get_world_size(), dist.get_rank()
 
 
+def _live() -> bool:
+    """A process group exists: collectives run even at world size 1 (a one-rank RCCL
+    communicator still executes on the GPU, so the N=1 bench exercises the same code)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def gather_bytes_to_root(payload: bytes, device: torch.device, root: int = 0):
     """Gather one byte string from every rank to `root`.  Returns list[bytes] on root, None
     elsewhere."""
     world, rank = _world()
-    if world == 1:
+    if not _live():
         return [payload]
     n = torch.tensor([len(payload)], dtype=torch.int64, device=device)
     sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
@@ -50,7 +56,9 @@ def gather_bytes_to_root(payload: bytes, device: torch.device, root: int = 0):
                 out.append(bytes(bufs[r][: sizes[r]].cpu().numpy().tobytes()) if sizes[r] else b"")
         return out
     if len(payload):
-        t = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
+        t = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+        if device.type == "cuda":
+            t = t.pin_memory().to(device, non_blocking=True)
         for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, root)]):
             req.wait()
     return None
@@ -83,7 +91,6 @@ def scatter_frames_from_root(frames: list | None, shape: tuple, device: torch.de
 def allreduce_stats(values, device: torch.device, op: str = "sum") -> np.ndarray:
     """All-reduce a small float64 vector (e.g. per-segment complexity for 2-pass RC)."""
     t = torch.as_tensor(np.asarray(values, dtype=np.float64), device=device)
-    world, _ = _world()
-    if world > 1:
+    if _live():
         dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
     return t.cpu().numpy()

@@ -191,14 +191,20 @@ class WorkQueue:
 
 class Checkpoint:
     """Segment-level resume: every encoded segment is published atomically
-    as ``<dir>/r<rung>_s<idx>_q<qp>.hevc`` with a ``.sha256`` sidecar written last; a rerun
-    (or an elastic restart) reuses every segment whose checksum verifies.  Keyed by QP, so
-    first-pass segments double as the 2-pass statistics checkpoint."""
+    as ``<dir>/<fingerprint>/r<rung>_s<idx>_q<qp>.hevc`` with a ``.sha256`` sidecar written
+    last; a rerun (or an elastic restart) reuses every segment whose checksum verifies.
+    Keyed by QP, so first-pass segments double as the 2-pass statistics checkpoint.  The
+    fingerprint covers everything that changes a segment's bytes (source identity, ladder
+    geometry, GOP, segmentation, search range), so a reused directory never mixes jobs."""
 
-    def __init__(self, root: str | None):
-        self.root = root
-        if root:
-            os.makedirs(root, exist_ok=True)
+    def __init__(self, root: str | None, fingerprint: str = ""):
+        self.root = os.path.join(root, fingerprint) if root and fingerprint else root
+        if self.root:
+            os.makedirs(self.root, exist_ok=True)
+
+    @staticmethod
+    def fingerprint(**fields) -> str:
+        return hashlib.sha256(json.dumps(fields, sort_keys=True, default=str).encode()).hexdigest()[:20]
 
     def _path(self, r: int, i: int, qp: int) -> str:
         return os.path.join(self.root, f"r{r}_s{i}_q{qp}.hevc")
@@ -267,8 +273,11 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     cache = None if software else EngineCache(device=dev.index or 0, batch=batch_segments,
                                               max_engines=max(4, len(rungs)))
     jobs = [(r, i) for r in range(len(rungs)) for i in range(len(segs))]  # ladder fan-out (P10)
-    ckpt = Checkpoint(resume_dir)
-    stats = {"encoded": 0, "resumed": 0, "retried": 0}
+    st = os.stat(input_path) if os.path.exists(input_path) else None
+    ckpt = Checkpoint(resume_dir, Checkpoint.fingerprint(
+        src=os.path.abspath(input_path), size=st.st_size if st else 0, mtime=st.st_mtime_ns if st else 0,
+        rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software))
+    stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
 
     def spec(r, q):
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=int(q), gop=gop, search_range=search_range,
@@ -276,16 +285,45 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
 
     def load(i):
         s, n = segs[i]
+        stats["reads"] += 1
         return src.read(s, n)
+
+    def encode_segments(seg_ids, qps, source_of) -> dict:
+        """Work item = one segment with ALL its rungs: the source range is read (or received)
+        once, every rung is prepared from it, the source is dropped, and each rung engine then
+        encodes the claimed segments in one batched launch."""
+        out, todo = {}, []
+        for i in seg_ids:
+            need = []
+            for r in range(len(rungs)):
+                b = ckpt.load(r, i, int(qps[r][i]))
+                if b is not None:
+                    out[(r, i)] = b
+                    stats["resumed"] += 1
+                else:
+                    need.append(r)
+            if need:
+                with trace.span("node_job.load"):
+                    raw = source_of(i)
+                    todo.extend(((r, i), prepare_frames(raw, *rungs[r]), spec(r, qps[r][i])) for r in need)
+                    del raw  # peak host memory: one source segment at a time
+        if todo:
+            with trace.span("node_job.encode", segments=len(todo)):
+                got = _encode_many(todo, None, cache)
+            for (r, i), b in got.items():
+                ckpt.save(r, i, int(qps[r][i]), b)
+                out[(r, i)] = b
+                stats["encoded"] += 1
+        return out
 
     def encode_pass(qps) -> dict:
         mine = {}
         if mode == "scatter" and world > 1:
             # round-robin rounds: rank 0 reads `world` segments and sends one to each rank
             fsz = w0 * h0 * 3 // 2
-            for base in range(0, len(jobs), world):
-                rnd = jobs[base:base + world]
-                n_max = max(segs[i][1] for _, i in rnd)
+            for base in range(0, len(segs), world):
+                rnd = list(range(base, min(len(segs), base + world)))
+                n_max = max(segs[i][1] for i in rnd)
                 shape = (n_max, fsz)
                 payload = None
                 if rank == 0:
@@ -293,58 +331,41 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     for k in range(world):
                         buf = np.zeros(shape, np.uint8)
                         if k < len(rnd):
-                            for f, (y, u, v) in enumerate(load(rnd[k][1])):
+                            for f, (y, u, v) in enumerate(load(rnd[k])):
                                 buf[f] = np.concatenate([y.ravel(), u.ravel(), v.ravel()])
                         payload.append(buf)
                 got = scatter_frames_from_root(payload, shape, dev).cpu().numpy()
                 if rank < len(rnd):
-                    r, i = rnd[rank]
+                    i = rnd[rank]
                     ysz, csz = w0 * h0, w0 * h0 // 4
                     frames = [(x[:ysz].reshape(h0, w0), x[ysz:ysz + csz].reshape(h0 // 2, w0 // 2),
                                x[ysz + csz:].reshape(h0 // 2, w0 // 2)) for x in got[:segs[i][1]]]
-                    fr = prepare_frames(frames, *rungs[r])
-                    mine.update(_encode_many([((r, i), fr, spec(r, qps[r][i]))], None, cache))
+                    mine.update(encode_segments([i], qps, lambda _i: frames))
         else:
-            wq = WorkQueue(f"pass{encode_pass.calls}", jobs, world, max_retries)
+            wq = WorkQueue(f"pass{encode_pass.calls}", list(range(len(segs))), world, max_retries)
             fault.check("rank", rank)  # TV_FAULT=rank:<r>:hang|die|fail (tests)
 
             def run(batch):
                 todo = []
-                for r, i in batch:
-                    b = ckpt.load(r, i, int(qps[r][i]))
-                    if b is not None:
-                        mine[(r, i)] = b
-                        stats["resumed"] += 1
-                        continue
+                for i in batch:
                     try:
                         fault.check("segment", i)
-                        todo.append((r, i))
+                        todo.append(i)
                     except fault.InjectedFault as e:
-                        wq.fail((r, i), str(e))
+                        wq.fail((i,), str(e))
                 if not todo:
                     return
                 try:
-                    with trace.span("node_job.load"):
-                        src_frames: dict = {}  # a segment is read once for all of its rungs
-                        items = [((r, i), prepare_frames(src_frames[i] if i in src_frames
-                                                         else src_frames.setdefault(i, load(i)), *rungs[r]),
-                                  spec(r, qps[r][i])) for r, i in todo]
-                    with trace.span("node_job.encode", segments=len(items)):
-                        got = _encode_many(items, None, cache)
+                    mine.update(encode_segments(todo, qps, load))
                 except Exception as e:  # a real engine/IO failure: every item goes back
-                    for it in todo:
-                        wq.fail(it, repr(e))
-                    return
-                for (r, i), b in got.items():
-                    ckpt.save(r, i, int(qps[r][i]), b)
-                    mine[(r, i)] = b
-                    stats["encoded"] += 1
+                    for i in todo:
+                        wq.fail((i,), repr(e))
 
             while True:
                 msg = wq.aborted()
                 if msg:
                     raise RuntimeError(msg)
-                claimed = wq.claim(batch_segments)  # a batch -> one batched launch
+                claimed = wq.claim(batch_segments)  # a batch -> one batched launch per rung
                 if not claimed:
                     break
                 run(claimed)
@@ -361,7 +382,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     continue
                 try:
                     stats["retried"] += 1
-                    run([it])
+                    run([it[0]])
                 finally:
                     wq.retry_done()
             msg = wq.aborted()

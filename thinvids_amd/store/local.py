@@ -388,6 +388,12 @@ class LocalStore:
 
     # apply a batch of (name, args, kwargs) atomically; used by pipelines and the server
     def execute_batch(self, cmds: list) -> list:
+        """Run buffered commands atomically.  Only public data ops are callable: no private
+        methods, no nested pipelines/batches and no blocking ``blpop`` (its condition wait
+        would release the lock mid-batch and could park the calling thread forever)."""
+        bad = [c[0] for c in cmds if c[0] not in Pipeline._ALLOWED]
+        if bad:
+            raise ValueError(f"op not allowed in a batch: {bad[0]}")
         with self._lock:
             out = []
             for name, args, kwargs in cmds:

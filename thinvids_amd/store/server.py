@@ -17,7 +17,14 @@ import threading
 
 from .local import LocalStore
 
-_READ_ONLY_OPS = None  # every public LocalStore method is allowed except private ones
+
+def _check_op(op: str) -> str:
+    """The allow-list of remotely callable ops (shared with batches and pipelines)."""
+    from .local import Pipeline
+
+    if not isinstance(op, str) or op not in Pipeline._ALLOWED and op != "blpop":
+        raise ValueError(f"op not allowed: {op}")
+    return op
 
 
 def _enc(v):
@@ -39,12 +46,10 @@ class _Handler(socketserver.StreamRequestHandler):
             try:
                 msg = json.loads(line)
                 if "batch" in msg:
-                    res = store.execute_batch([(n, a, k) for n, a, k in msg["batch"]])
+                    res = store.execute_batch([(_check_op(n), a, k) for n, a, k in msg["batch"]])
                     out = {"ok": [_enc(r) for r in res]}
                 else:
-                    op = msg["op"]
-                    if op.startswith("_") or op in ("pipeline", "execute_batch"):
-                        raise ValueError(f"op not allowed: {op}")
+                    op = _check_op(msg["op"])
                     res = getattr(store, op)(*msg.get("args", []), **msg.get("kwargs", {}))
                     out = {"ok": _enc(res)}
             except Exception as e:  # report to the client, keep serving

@@ -152,7 +152,9 @@ def prepare_frames(frames: list, out_w: int, out_h: int, device: str | None = No
         import torch
 
         dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", os.environ.get("TV_DEVICE", "0"))))
-        up = [tuple(torch.from_numpy(np.ascontiguousarray(p)).to(dev, non_blocking=True) for p in f) for f in frames]
+        # np.require(W) copies read-only views (y4m frombuffer) so torch gets a writable array
+        up = [tuple(torch.from_numpy(np.require(p, np.uint8, ["C", "W"])).to(dev, non_blocking=True) for p in f)
+              for f in frames]
         out = []
         for i in range(n):
             f = up[i]
