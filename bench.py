@@ -230,7 +230,7 @@ def main() -> None:
     ap.add_argument("--gop", type=int, default=16, help="frames per GOP-aligned segment")
     ap.add_argument("--qp", type=int, default=27)
     ap.add_argument("--sao", action="store_true", help="enable SAO (in-loop sample adaptive offset)")
-    ap.add_argument("--range", type=int, default=16)
+    ap.add_argument("--range", type=int, default=64, help="motion search range (full-res pels, multiple of 16)")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--ladder", default="", help="ABR mode (config #5): rung heights, e.g. 2160,1440,1080,720,480")

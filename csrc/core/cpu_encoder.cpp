@@ -15,8 +15,10 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <stdexcept>
 
 #include "tv/cpu_encoder.h"
+#include "tv/me_model.h"
 
 namespace tv {
 
@@ -58,8 +60,6 @@ int block_satd(const uint8_t* src, int ss, const int* pred, int N) {
     for (int bx = 0; bx < N; bx += 8) s += satd8x8(diff + by * N + bx, N);
   return s;
 }
-
-int mv_bits(int dx, int dy) { return mv_bits_est(dx, dy); }
 
 }  // namespace
 
@@ -135,20 +135,60 @@ void analyze_intra(const SeqConfig& cfg, const Picture& src, FrameDecisions& fd)
     }
 }
 
-void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, int range,
-                   FrameDecisions& fd) {
+void quarter_luma(const Picture& src, std::vector<uint8_t>& q) {
+  const int W = src.w, H = src.h, qw = W / 4, qh = H / 4;
+  q.assign((size_t)qw * qh, 0);
+  for (int y = 0; y < qh; ++y)
+    for (int x = 0; x < qw; ++x) {
+      int s = 0;
+      for (int j = 0; j < 4; ++j)
+        for (int i = 0; i < 4; ++i) s += src.y[(size_t)(4 * y + j) * W + 4 * x + i];
+      q[(size_t)y * qw + x] = (uint8_t)((s + 8) >> 4);
+    }
+}
+
+void coarse_search(const uint8_t* qcur, const uint8_t* qprev, int W, int H, int range, const int* penmv,
+                   int16_t* cmv, int* ccost) {
+  const int qw = W / 4, qh = H / 4, wc = W / kCtb, hc = H / kCtb, rq = range / 4;
+  for (int cyi = 0; cyi < hc; ++cyi)
+    for (int cxi = 0; cxi < wc; ++cxi) {
+      const int x0 = 8 * cxi, y0 = 8 * cyi;
+      unsigned best = 0xffffffffu;
+      for (int dy = -rq; dy <= rq; ++dy)
+        for (int dx = -rq; dx <= rq; ++dx) {
+          int sad = 0;
+          for (int j = 0; j < 8; ++j) {
+            const int ry = clip3(0, qh - 1, y0 + j + dy);
+            for (int i = 0; i < 8; ++i)
+              sad += tv_abs(qcur[(size_t)(y0 + j) * qw + x0 + i] - qprev[(size_t)ry * qw + clip3(0, qw - 1, x0 + i + dx)]);
+          }
+          const unsigned idx = (unsigned)((dy + rq) * (2 * rq + 1) + dx + rq);
+          const unsigned v = ((unsigned)(sad + me_coarse_pen(penmv, dx, dy)) << 13) | idx;
+          best = v < best ? v : best;
+        }
+      const int idx = (int)(best & 8191), side = 2 * rq + 1;
+      const int o = cyi * wc + cxi;
+      cmv[2 * o] = (int16_t)(4 * (idx % side - rq));
+      cmv[2 * o + 1] = (int16_t)(4 * (idx / side - rq));
+      ccost[o] = (int)(best >> 13);
+    }
+}
+
+void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, const int16_t* cmv,
+                   const int16_t* prev_mv, int range, FrameDecisions& fd) {
   const double lam = lambda_sad(cfg.qp);
-  const int W = cfg.coded_w, H = cfg.coded_h;
+  const int W = cfg.coded_w, H = cfg.coded_h, wc = W / kCtb, hc = H / kCtb;
+  int penmv[64];
+  for (int i = 0; i < 64; ++i) penmv[i] = (int)(lam * i);
+  const int pen_split = (int)(lam * 4);
   const uint8_t* S = src.y.data();
   const uint8_t* R = ref.y.data();
-  auto sad_int = [&](int x, int y, int N, int dx, int dy) {
+  auto sad8 = [&](int x, int y, int dx, int dy) {  // one 8x8 block, integer displacement
     int s = 0;
-    for (int j = 0; j < N; ++j) {
+    for (int j = 0; j < 8; ++j) {
       const int ry = clip3(0, H - 1, y + j + dy);
-      for (int i = 0; i < N; ++i) {
-        const int rx = clip3(0, W - 1, x + i + dx);
-        s += tv_abs(S[(size_t)(y + j) * W + x + i] - R[(size_t)ry * W + rx]);
-      }
+      for (int i = 0; i < 8; ++i)
+        s += tv_abs(S[(size_t)(y + j) * W + x + i] - R[(size_t)ry * W + clip3(0, W - 1, x + i + dx)]);
     }
     return s;
   };
@@ -160,62 +200,98 @@ void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref,
         s += tv_abs(S[(size_t)(y + j) * W + x + i] - mc_luma_sample(R, W, W, H, bx + i, by + j, fx, fy));
     return s;
   };
-  struct Res {
-    int cost;
-    int mvx, mvy;
-  };
-  auto search = [&](int x, int y, int N) -> Res {
-    Res best{INT_MAX, 0, 0};
-    for (int dy = -range; dy <= range; ++dy)
-      for (int dx = -range; dx <= range; ++dx) {
-        const int c = sad_int(x, y, N, dx, dy) + (int)(lam * mv_bits(4 * dx, 4 * dy));
-        if (c < best.cost) best = Res{c, 4 * dx, 4 * dy};
-      }
-    // half then quarter pel refinement
-    for (int step = 2; step >= 1; step >>= 1) {
-      Res cen = best;
-      for (int k = 0; k < 8; ++k) {
-        static const int ox[8] = {-1, 0, 1, -1, 1, -1, 0, 1}, oy[8] = {-1, -1, -1, 0, 0, 1, 1, 1};
-        const int mx = cen.mvx + ox[k] * step, my = cen.mvy + oy[k] * step;
-        const int c = sad_qpel(x, y, N, mx, my) + (int)(lam * mv_bits(mx, my));
-        if (c < best.cost) best = Res{c, mx, my};
-      }
+  // block geometry of the 21 ME blocks: 16 x 8x8 (raster), 4 x 16x16, 1 x 32x32
+  auto blk = [](int bi, int& bx, int& by, int& n) {
+    if (bi < 16) {
+      bx = (bi & 3) * 8, by = (bi >> 2) * 8, n = 8;
+    } else if (bi < 20) {
+      bx = ((bi - 16) & 1) * 16, by = ((bi - 16) >> 1) * 16, n = 16;
+    } else {
+      bx = by = 0, n = 32;
     }
-    return best;
   };
-  for (int cy = 0; cy < H; cy += 32)
-    for (int cx = 0; cx < W; cx += 32) {
-      const Res r32 = search(cx, cy, 32);
+  auto blk8_of = [](int q, int r) { return (((q >> 1) * 2 + (r >> 1)) << 2) + (q & 1) * 2 + (r & 1); };
+  const int lim = range - 4;
+  for (int cyi = 0; cyi < hc; ++cyi)
+    for (int cxi = 0; cxi < wc; ++cxi) {
+      const int cx = cxi * kCtb, cy = cyi * kCtb;
+      const int u0 = (cy >> 3) * fd.w8 + (cx >> 3);
+      int cand[kMeMaxCand][2], pmv[2];
+      const int nc = me_candidates(cmv, wc, hc, cxi, cyi, prev_mv[2 * u0], prev_mv[2 * u0 + 1], lim, cand, pmv);
+      // integer refinement: the 21 block costs at every window position (8x8 SADs reused)
+      unsigned best[21];
+      for (int k = 0; k < 21; ++k) best[k] = 0xffffffffu;
+      for (int pos = 0; pos < nc * kMePosPerCand; ++pos) {
+        int mx, my;
+        me_pos_to_mv(pos, cand, mx, my);
+        const unsigned pen = (unsigned)penmv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])];
+        int s8[16], s16[4] = {0, 0, 0, 0}, s32 = 0;
+        for (int k = 0; k < 16; ++k) {
+          s8[k] = sad8(cx + (k & 3) * 8, cy + (k >> 2) * 8, mx, my);
+          s16[((k >> 3) << 1) | ((k >> 1) & 1)] += s8[k];
+          s32 += s8[k];
+        }
+        auto upd = [&](int bi, int sad) {
+          const unsigned v = ((unsigned)sad + pen) << 11 | (unsigned)pos;
+          best[bi] = v < best[bi] ? v : best[bi];
+        };
+        for (int k = 0; k < 16; ++k) upd(k, s8[k]);
+        for (int q = 0; q < 4; ++q) upd(16 + q, s16[q]);
+        upd(20, s32);
+      }
+      int bcost[21], bmv[21][2];
+      for (int bi = 0; bi < 21; ++bi) {
+        int mx, my;
+        me_pos_to_mv((int)(best[bi] & 2047), cand, mx, my);
+        bmv[bi][0] = 4 * mx;
+        bmv[bi][1] = 4 * my;
+        bcost[bi] = (int)(best[bi] >> 11);
+        int bx, by, n;
+        blk(bi, bx, by, n);
+        // half then quarter pel refinement (centre wins ties, then the lowest neighbour)
+        for (int step = 2; step >= 1; step >>= 1) {
+          const int c0x = bmv[bi][0], c0y = bmv[bi][1];
+          for (int k = 0; k < 8; ++k) {
+            int ox, oy;
+            me_cand_offset(k, ox, oy);
+            const int qx = c0x + ox * step, qy = c0y + oy * step;
+            const int c = sad_qpel(cx + bx, cy + by, n, qx, qy) + penmv[me_pen_index(qx - pmv[0], qy - pmv[1])];
+            if (c < bcost[bi]) {
+              bcost[bi] = c;
+              bmv[bi][0] = qx;
+              bmv[bi][1] = qy;
+            }
+          }
+        }
+      }
+      // bottom-up CU split decision
       int sum16 = 0;
       for (int q = 0; q < 4; ++q) {
-        const int x = cx + (q & 1) * 16, y = cy + (q >> 1) * 16;
-        const Res r16 = search(x, y, 16);
-        Res r8[4];
         int sum8 = 0;
-        for (int k = 0; k < 4; ++k) {
-          r8[k] = search(x + (k & 1) * 8, y + (k >> 1) * 8, 8);
-          sum8 += r8[k].cost + (int)(lam * 4);
-        }
-        const bool split = sum8 < r16.cost + (int)(lam * 4);
-        sum16 += split ? sum8 : r16.cost + (int)(lam * 4);
-        for (int k = 0; k < 4; ++k) {
-          const int u = ((y >> 3) + (k >> 1)) * fd.w8 + (x >> 3) + (k & 1);
+        for (int r = 0; r < 4; ++r) sum8 += bcost[blk8_of(q, r)] + pen_split;
+        const bool split = sum8 < bcost[16 + q] + pen_split;
+        sum16 += split ? sum8 : bcost[16 + q] + pen_split;
+        for (int r = 0; r < 4; ++r) {
+          const int ux = (q & 1) * 2 + (r & 1), uy = (q >> 1) * 2 + (r >> 1);
+          const int u = u0 + uy * fd.w8 + ux;
+          const int sbi = split ? blk8_of(q, r) : 16 + q;
           fd.cu_log2[u] = split ? 3 : 4;
-          fd.mv[2 * u] = (int16_t)(split ? r8[k].mvx : r16.mvx);
-          fd.mv[2 * u + 1] = (int16_t)(split ? r8[k].mvy : r16.mvy);
+          fd.mv[2 * u] = (int16_t)bmv[sbi][0];
+          fd.mv[2 * u + 1] = (int16_t)bmv[sbi][1];
         }
       }
-      if (r32.cost + (int)(lam * 4) <= sum16) {
-        for (int j = 0; j < 4; ++j)
-          for (int i = 0; i < 4; ++i) {
-            const int u = ((cy >> 3) + j) * fd.w8 + (cx >> 3) + i;
-            fd.cu_log2[u] = 5;
-            fd.mv[2 * u] = (int16_t)r32.mvx;
-            fd.mv[2 * u + 1] = (int16_t)r32.mvy;
-          }
-      }
+      const bool whole = bcost[20] + pen_split <= sum16;
       for (int j = 0; j < 4; ++j)
-        for (int i = 0; i < 4; ++i) fd.intra[((cy >> 3) + j) * fd.w8 + (cx >> 3) + i] = 0;
+        for (int i = 0; i < 4; ++i) {
+          const int u = u0 + j * fd.w8 + i;
+          if (whole) {
+            fd.cu_log2[u] = 5;
+            fd.mv[2 * u] = (int16_t)bmv[20][0];
+            fd.mv[2 * u + 1] = (int16_t)bmv[20][1];
+          }
+          fd.intra[u] = 0;
+          fd.ipm[u] = 1;
+        }
     }
 }
 
@@ -297,6 +373,8 @@ void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* 
 
 // ------------------------------------ driver --------------------------------------------
 CpuEncoder::CpuEncoder(const SeqConfig& cfg, int search_range) : cfg_(cfg), range_(search_range) {
+  if (search_range < 16 || search_range > 128 || (search_range & 15))
+    throw std::runtime_error("search range must be a multiple of 16 in 16..128");
   cfg_.finalize();
   src_.alloc(cfg_.coded_w, cfg_.coded_h);
   rec_.alloc(cfg_.coded_w, cfg_.coded_h);
@@ -314,9 +392,19 @@ void CpuEncoder::encode_frame(const uint8_t* const planes[3], const int strides[
     reconstruct_frame(cfg_, src_, nullptr, dec, rec_);
   } else {
     std::swap(ref_, rec_);
-    analyze_inter(cfg_, src_, ref_, range_, dec);
+    quarter_luma(src_, qcur_);
+    const int wc = cfg_.coded_w / kCtb, hc = cfg_.coded_h / kCtb;
+    std::vector<int16_t> cmv(2 * (size_t)wc * hc);
+    std::vector<int> ccost((size_t)wc * hc);
+    int penmv[64];
+    for (int i = 0; i < 64; ++i) penmv[i] = (int)(lambda_sad(cfg_.qp) * i);
+    coarse_search(qcur_.data(), qprev_.data(), cfg_.coded_w, cfg_.coded_h, range_, penmv, cmv.data(), ccost.data());
+    analyze_inter(cfg_, src_, ref_, cmv.data(), prev_mv_.data(), range_, dec);
     reconstruct_frame(cfg_, src_, &ref_, dec, rec_);
   }
+  if (idr) quarter_luma(src_, qcur_);
+  std::swap(qcur_, qprev_);
+  prev_mv_ = dec.mv;
   write_slice(cfg_, dec.view(), poc, idr, out);
 }
 

@@ -116,8 +116,8 @@ class Core {
  public:
   Core(const EngineCfg& c, ThreadPool* pool) : cfg_(c), g_(make_geo(c.width, c.height)), pool_(pool) {
     if (c.batch < 1 || c.batch > kMaxBatch) throw std::runtime_error("batch must be 1..64");
-    if (c.range < 4 || c.range > 16 || (c.range & 3))
-      throw std::runtime_error("search range must be 4, 8, 12 or 16");
+    if (c.range < 16 || c.range > 128 || (c.range & 15))
+      throw std::runtime_error("search range must be a multiple of 16 in 16..128");
     if ((c.width & 1) || (c.height & 1)) throw std::runtime_error("odd frame size");
     if (c.width < 64 || c.height < 64) throw std::runtime_error("frame must be at least 64x64");
     HIP_OK(hipSetDevice(c.device));
@@ -138,6 +138,12 @@ class Core {
     HIP_OK(hipMalloc(&d_sse_, B * 3 * sizeof(unsigned long long)));
     HIP_OK(hipMalloc(&phase_, B * 16 * g_.psz));
     HIP_OK(hipMalloc(&count_scratch_, B * nctu_ * sizeof(int)));
+    // hierarchical motion search: quarter-res source luma (this / previous frame), coarse field
+    qsz_ = (long)(g_.W / 4) * (g_.H / 4);
+    HIP_OK(hipMalloc(&q_[0], B * qsz_));
+    HIP_OK(hipMalloc(&q_[1], B * qsz_));
+    HIP_OK(hipMalloc(&cmv_, B * nctu_ * 2 * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&ccost_, B * nctu_ * sizeof(int)));
     cap_ = g_.ysz + 2 * g_.csz;
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
     if (c.deblock & 2) {  // SAO reads the deblocked picture from a copy
@@ -183,6 +189,10 @@ class Core {
     (void)hipFree(d_sse_);
     (void)hipFree(phase_);
     (void)hipFree(count_scratch_);
+    (void)hipFree(q_[0]);
+    (void)hipFree(q_[1]);
+    (void)hipFree(cmv_);
+    (void)hipFree(ccost_);
     for (auto& s : slots_) {
       (void)hipFree(s.dev);
       (void)hipHostFree(s.host);
@@ -369,8 +379,14 @@ class Core {
                                  hipGetErrorString(e1 != hipSuccess ? e1 : e2));
     };
     stage("upload");
-    if (f == 0) launch_intra_frame(src_, cur, dec, g_, cfg_.qp, pen_, B, stream_);
-    else launch_inter_frame(src_, prev, phase_, cur, dec, g_, cfg_.qp, pen_, cfg_.range, B, stream_);
+    launch_quarter(src_, q_[f & 1], g_, B, stream_);  // lookahead plane (next frame's coarse ref)
+    if (f == 0) {
+      launch_intra_frame(src_, cur, dec, g_, cfg_.qp, pen_, B, stream_);
+    } else {
+      // the previous frame's decisions still sit in its slot (reused only kSlots frames later)
+      const MeBuffers me{q_[f & 1], q_[(f + 1) & 1], slot_dec(slots_[(f - 1) % kSlots]).mv, cmv_, ccost_};
+      launch_inter_frame(src_, prev, phase_, cur, dec, g_, cfg_.qp, pen_, cfg_.range, me, B, stream_);
+    }
     stage(f == 0 ? "intra" : "inter");
     launch_compact(dec, g_, slot_compact(s), B, stream_);
     stage("compact");
@@ -457,6 +473,10 @@ class Core {
   unsigned long long* d_sse_ = nullptr;
   uint8_t* phase_ = nullptr;
   void* count_scratch_ = nullptr;
+  uint8_t* q_[2]{};
+  int16_t* cmv_ = nullptr;
+  int* ccost_ = nullptr;
+  long qsz_ = 0;
   int nctu_ = 0;
   int last_frames_ = 1;
   const bool sync_debug_ = [] {

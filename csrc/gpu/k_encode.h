@@ -24,8 +24,20 @@ void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi,
 void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s);
 void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, int qp,
                         const Penalties& pen, int B, hipStream_t s);
+// Hierarchical motion-search state of one P frame (tv/me_model.h): quarter-res source luma
+// of this and the previous frame, the previous frame's MV field (temporal candidate) and the
+// per-CTB coarse field (B x nctu x 2 int16 / B x nctu int).
+struct MeBuffers {
+  const uint8_t* qcur;
+  const uint8_t* qprev;
+  const int16_t* prev_mv;
+  int16_t* cmv;
+  int* ccost;
+};
+void launch_quarter(FrameSet src, uint8_t* q, const Geo& g, int B, hipStream_t s);
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
-                        const Geo& g, int qp, const Penalties& pen, int range, int B, hipStream_t s);
+                        const Geo& g, int qp, const Penalties& pen, int range, const MeBuffers& me, int B,
+                        hipStream_t s);
 // 16 quarter-pel phase planes (B x 16 x psz bytes) of the luma reference
 void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipStream_t s);
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s);

@@ -17,24 +17,33 @@
 #include "k_encode.h"
 #include "tb_coder.h"
 #include "wave_tb.h"
-
-#include <cstdlib>
+#include "tv/me_model.h"
 
 namespace tv {
 namespace gpu {
 
-constexpr int kMeThreads = 320;
-constexpr int kWin = 72;       // window side: 32 + 2*16 + 8
-constexpr int kWinOff = 20;    // window origin = CTB origin - 20 (multiple of 4)
-constexpr int kWinW = kWin / 4;  // 32-bit words per window row
-// LDS pitch of a window row: odd, so the 32 lanes of a ds_read_b32 group — which walk the
-// candidate rows dy (item mapping below) — land on 32 distinct banks (19*d mod 32 is a
-// permutation); the old pitch 18 with dx-group-fast lanes was 2-way conflicted.
-constexpr int kWinP = kWinW + 1;
-// LDS pitch (words) of a source-CTB row.  Measured on MI355X: pitch 9 removes the sub-pel
-// stage's 4-way conflicts but costs 32 VGPRs (127, 4 waves/SIMD, -9 % end to end); pitch 10
-// (+ amdgpu_waves_per_eu(5)) cuts k_inter_me bank conflicts 16 -> 13.6 % at equal speed.
-// Kept at 8: the integer search's uniform s0/s1 pair stays one aligned 8-byte read.
+// ---------------------------------------------------------------------------------------
+// Hierarchical motion search (tv/me_model.h; the CPU golden model is tv::analyze_inter).
+//
+//  k_quarter     quarter-resolution luma of the source: (sum of a 4x4 block + 8) >> 4,
+//                one v_sad_u8 against zero per source row word.
+//  k_coarse_me   one wave per CTB: the 8x8 quarter-res block vs the previous quarter-res
+//                SOURCE frame, full search over [-Rq, Rq]^2 (Rq = range/4) from an LDS
+//                window, 4 horizontally adjacent candidates per lane via v_alignbyte +
+//                v_sad_u8.  No recon dependency: the coarse field is a lookahead.
+//  k_inter_me    two waves per CTB: up to 7 candidate centres (zero, coarse, 4 coarse
+//                neighbours, temporal), an [-4,+3] x [-3,+3] integer window each staged in
+//                LDS pre-aligned to the window origin; every lane owns 4 adjacent positions
+//                of one (candidate, row) and accumulates all 16 8x8 SADs (16x16 / 32x32 are
+//                sums: SAD reuse); then half/quarter-pel refinement of the 21 blocks from
+//                the phase planes and the bottom-up CU split decision.  Rate = MVD bits
+//                against the CTB predictor.
+// ---------------------------------------------------------------------------------------
+constexpr int kMeThreads = 128;
+constexpr int kFRows = kCtb + kMeWinH - 1;  // 38 window rows per candidate
+constexpr int kFWords = 10;                 // 40 bytes: 32 + 7 offsets + 1 spare word
+constexpr int kFPitch = kFWords + 1;        // odd pitch: lanes walking rows hit distinct banks
+// LDS pitch (words) of a source-CTB row (uniform s0/s1 reads stay one aligned 8-byte read)
 constexpr int kSrcP = 8;
 
 __device__ __forceinline__ void me_blk_geom(int bi, int& bx, int& by, int& l2) {
@@ -54,107 +63,187 @@ __device__ __forceinline__ void me_blk_geom(int bi, int& bx, int& by, int& l2) {
 __device__ __forceinline__ int me_blk8_of(int q, int r) {
   return (((q >> 1) * 2 + (r >> 1)) << 2) + (q & 1) * 2 + (r & 1);
 }
-__device__ __forceinline__ void cand_offset(int k, int& ox, int& oy) {
-  ox = (k == 0 || k == 3 || k == 5) ? -1 : ((k == 1 || k == 6) ? 0 : 1);
-  oy = k < 3 ? -1 : (k < 5 ? 0 : 1);
-}
 __device__ __forceinline__ int phase_at(const uint8_t* P, const Geo& g, int x, int y) {
   x = clip3(-8, g.W + 7, x);
   y = clip3(-8, g.H + 7, y);
   return P[(long)(y + 8) * g.pw16 + x + 8];
 }
+// 4 bytes of row `row` starting at byte x (any alignment), clamped horizontally to [0, w-1]
+__device__ __forceinline__ uint32_t load4_clamped(const uint8_t* row, int x, int w) {
+  const int a = x & ~3, sh = x & 3;
+  if (x >= 0 && a + 7 < w) {
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + a);
+    if (!sh) return w0;
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + a + 4);
+    return __builtin_amdgcn_alignbyte(w1, w0, sh);
+  }
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v |= (uint32_t)row[clip3(0, w - 1, x + k)] << (8 * k);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) k_quarter(FrameSet src, uint8_t* q, Geo g) {
+  const int b = blockIdx.y, qw = g.W >> 2, qh = g.H >> 2;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= qw * qh) return;
+  const int x = i % qw, y = i / qw;
+  const uint8_t* S = src.plane(0, b, g) + (long)(4 * y) * g.W + 4 * x;
+  unsigned s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s = __builtin_amdgcn_sad_u8(*reinterpret_cast<const uint32_t*>(S + (long)j * g.W), 0u, s);
+  q[(long)b * qw * qh + i] = (uint8_t)((s + 8) >> 4);
+}
+
+constexpr int kCoarseMaxRq = 32;
+constexpr int kCoarseRows = 8 + 2 * kCoarseMaxRq;
+constexpr int kCoarseWords = kCoarseMaxRq / 2 + 3;
+
+__global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uint8_t* qprev, Geo g, Penalties pen,
+                                                  int rq, int16_t* cmv, int* ccost) {
+  const int ctu = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+  const int qw = g.W >> 2, qh = g.H >> 2;
+  const int x0 = 8 * (ctu % g.wc), y0 = 8 * (ctu / g.wc);
+  const uint8_t* C = qcur + (long)b * qw * qh;
+  const uint8_t* P = qprev + (long)b * qw * qh;
+  __shared__ uint32_t s32[16];
+  __shared__ uint32_t win[kCoarseRows * (kCoarseWords | 1)];
+  const int side = 2 * rq + 1, rows = 8 + 2 * rq, wpr = rq / 2 + 3, pitch = wpr | 1;
+  if (lane < 16) s32[lane] = *reinterpret_cast<const uint32_t*>(C + (long)(y0 + (lane >> 1)) * qw + x0 + 4 * (lane & 1));
+  for (int w = lane; w < rows * wpr; w += 64) {
+    const int r = w / wpr, c = w - r * wpr;
+    const uint8_t* row = P + (long)clip3(0, qh - 1, y0 - rq + r) * qw;
+    win[r * pitch + c] = load4_clamped(row, x0 - rq + 4 * c, qw);
+  }
+  __syncthreads();
+  unsigned best = 0xffffffffu;
+  const int groups = rq / 2 + 1;
+  for (int item = lane; item < groups * side; item += 64) {
+    const int gi = item / side, dyi = item - gi * side;
+    const int dy = dyi - rq, dx0 = 4 * gi - rq;
+    unsigned acc[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t s0 = s32[2 * j], s1 = s32[2 * j + 1];
+      const int wr = (dyi + j) * pitch + gi;
+      const uint32_t w0 = win[wr], w1 = win[wr + 1], w2 = win[wr + 2];
+      acc[0] = __builtin_amdgcn_sad_u8(w1, s1, __builtin_amdgcn_sad_u8(w0, s0, acc[0]));
+#pragma unroll
+      for (int sft = 1; sft < 4; ++sft) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sft);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sft);
+        acc[sft] = __builtin_amdgcn_sad_u8(hi, s1, __builtin_amdgcn_sad_u8(lo, s0, acc[sft]));
+      }
+    }
+#pragma unroll
+    for (int sft = 0; sft < 4; ++sft) {
+      const int dx = dx0 + sft;
+      if (dx > rq) continue;
+      const unsigned v = ((acc[sft] + (unsigned)me_coarse_pen(pen.mv, dx, dy)) << 13) | (unsigned)(dyi * side + dx + rq);
+      best = v < best ? v : best;
+    }
+  }
+  best = wave_min_u32(best);
+  if (lane == 0) {
+    const int idx = (int)(best & 8191), o = b * g.wc * g.hc + ctu;
+    cmv[2 * o] = (int16_t)(4 * (idx % side - rq));
+    cmv[2 * o + 1] = (int16_t)(4 * (idx / side - rq));
+    ccost[o] = (int)(best >> 13);
+  }
+}
 
 __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
-                                                         DecisionSet dec, Geo g, Penalties pen, int range,
-                                                         int ablate) {
+                                                         DecisionSet dec, const int16_t* prev_mv, const int16_t* cmv,
+                                                         Geo g, Penalties pen, int range) {
   const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
+  const int cxi = ctu % g.wc, cyi = ctu / g.wc, cx = cxi * 32, cy = cyi * 32;
   const uint8_t* S = src.plane(0, b, g);
   const uint8_t* R = ref.plane(0, b, g);
   __shared__ uint32_t s32[32 * kSrcP];
-  __shared__ uint32_t win[kWin * kWinP];
+  __shared__ uint32_t win[kMeMaxCand * kFRows * kFPitch];
+  __shared__ int cand[kMeMaxCand][2];
+  __shared__ int pmv[2], ncand;
   __shared__ unsigned best[21];
   __shared__ int bcost[21], bmv[21][2];
   __shared__ int subsad[21][8];
-  if (tid < 256)
-    s32[(tid >> 3) * kSrcP + (tid & 7)] =
-        *reinterpret_cast<const uint32_t*>(S + (long)(cy + (tid >> 3)) * g.W + cx + 4 * (tid & 7));
-  for (int w = tid; w < ((ablate & 4) ? 0 : kWin * kWinW); w += kMeThreads) {
-    const int row = w / kWinW, wc = w % kWinW;
-    const int gy = clip3(0, g.H - 1, cy - kWinOff + row);
-    const int gx0 = cx - kWinOff + 4 * wc;
-    uint32_t v;
-    if (gx0 >= 0 && gx0 + 3 < g.W) {
-      v = *reinterpret_cast<const uint32_t*>(R + (long)gy * g.W + gx0);
-    } else {
-      v = 0;
-      for (int k = 0; k < 4; ++k) v |= (uint32_t)R[(long)gy * g.W + clip3(0, g.W - 1, gx0 + k)] << (8 * k);
-    }
-    win[row * kWinP + wc] = v;
+  for (int t = tid; t < 256; t += kMeThreads)
+    s32[(t >> 3) * kSrcP + (t & 7)] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (t >> 3)) * g.W + cx + 4 * (t & 7));
+  if (tid == 0) {
+    const long u0 = b * g.usz + (long)(cy >> 3) * g.w8 + (cx >> 3);
+    ncand = me_candidates(cmv + (long)b * g.wc * g.hc * 2, g.wc, g.hc, cxi, cyi, prev_mv[2 * u0], prev_mv[2 * u0 + 1],
+                          range - 4, cand, pmv);
   }
   if (tid < 21) best[tid] = 0xffffffffu;
   __syncthreads();
+  const int nc = ncand;
+  // candidate windows, each pre-aligned so byte 0 of a row is x = cx + cand_x + kMeWinX0
+  for (int e = tid; e < nc * kFRows * kFWords; e += kMeThreads) {
+    const int k = e / (kFRows * kFWords), rem = e - k * (kFRows * kFWords);
+    const int r = rem / kFWords, w = rem - r * kFWords;
+    const uint8_t* row = R + (long)clip3(0, g.H - 1, cy + cand[k][1] + kMeWinY0 + r) * g.W;
+    win[(k * kFRows + r) * kFPitch + w] = load4_clamped(row, cx + cand[k][0] + kMeWinX0 + 4 * w, g.W);
+  }
+  __syncthreads();
 
-  // ------------------------------- integer full search ---------------------------------
-  const int side = 2 * range + 1, groups = range / 2 + 1, items = groups * side;
+  // ------------------------------- integer refinement -----------------------------------
   unsigned lb[21];
 #pragma unroll
   for (int k = 0; k < 21; ++k) lb[k] = 0xffffffffu;
-  for (int item = tid; item < ((ablate & 1) ? 0 : items); item += kMeThreads) {
-    const int gi = item / side, dyi = item - gi * side;  // dy fastest across lanes (banks)
-    const int dy = dyi - range, dx0 = 4 * gi - range;
-    // per-shift rate term and packed candidate index; shifts beyond +R are excluded with a
-    // penalty larger than any SAD (keeps the update branch-free)
-    unsigned mvc[4], cid[4];
+  for (int item = tid; item < nc * kMeWinH * 2; item += kMeThreads) {
+    const int k = item / (kMeWinH * 2), rr = item - k * (kMeWinH * 2);
+    const int dyi = rr >> 1, gs = rr & 1;
+    const int pos0 = k * kMePosPerCand + dyi * kMeWinW + 4 * gs;
+    const int my = cand[k][1] + kMeWinY0 + dyi;
+    unsigned mvc[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int dx = dx0 + s;
-      mvc[s] = dx > range ? 0x3ffffu : (unsigned)pen.mv[mv_bits_est(4 * dx, 4 * dy)];
-      cid[s] = (unsigned)(dyi * side + tv_min(dx, range) + range);
+    for (int sft = 0; sft < 4; ++sft) {
+      const int mx = cand[k][0] + kMeWinX0 + 4 * gs + sft;
+      mvc[sft] = (unsigned)pen.mv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])];
     }
+    const uint32_t* W0 = win + (k * kFRows + dyi) * kFPitch + gs;
     unsigned q16[4][4], t32[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      t32[s] = 0;
+    for (int sft = 0; sft < 4; ++sft) {
+      t32[sft] = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) q16[q][s] = 0;
+      for (int q = 0; q < 4; ++q) q16[q][sft] = 0;
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int bx = (k & 3) * 8, by = (k >> 2) * 8;
-      const int q = ((k >> 3) << 1) | ((k >> 1) & 1);
+    for (int kb = 0; kb < 16; ++kb) {
+      const int bx = (kb & 3) * 8, by = (kb >> 2) * 8;
+      const int q = ((kb >> 3) << 1) | ((kb >> 1) & 1);
       unsigned acc[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int srow = (by + j) * kSrcP + (bx >> 2);
         const uint32_t s0 = s32[srow], s1 = s32[srow + 1];
-        const int wrow = (kWinOff + dy + by + j) * kWinP + ((kWinOff + dx0 + bx) >> 2);
-        const uint32_t w0 = win[wrow], w1 = win[wrow + 1], w2 = win[wrow + 2];
+        const uint32_t* wp = W0 + (by + j) * kFPitch + (bx >> 2);
+        const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
         acc[0] = __builtin_amdgcn_sad_u8(w1, s1, __builtin_amdgcn_sad_u8(w0, s0, acc[0]));
 #pragma unroll
-        for (int s = 1; s < 4; ++s) {
-          const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, s);
-          const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, s);
-          acc[s] = __builtin_amdgcn_sad_u8(hi, s1, __builtin_amdgcn_sad_u8(lo, s0, acc[s]));
+        for (int sft = 1; sft < 4; ++sft) {
+          const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sft);
+          const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sft);
+          acc[sft] = __builtin_amdgcn_sad_u8(hi, s1, __builtin_amdgcn_sad_u8(lo, s0, acc[sft]));
         }
       }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const unsigned v = ((acc[s] + mvc[s]) << 11) | cid[s];
-        lb[k] = v < lb[k] ? v : lb[k];
-        q16[q][s] += acc[s];
-        t32[s] += acc[s];
+      for (int sft = 0; sft < 4; ++sft) {
+        const unsigned v = ((acc[sft] + mvc[sft]) << 11) | (unsigned)(pos0 + sft);
+        lb[kb] = v < lb[kb] ? v : lb[kb];
+        q16[q][sft] += acc[sft];
+        t32[sft] += acc[sft];
       }
       __builtin_amdgcn_sched_barrier(0);  // bound live ranges: no hoisting across 8x8 blocks
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int sft = 0; sft < 4; ++sft) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const unsigned v = ((q16[q][s] + mvc[s]) << 11) | cid[s];
+        const unsigned v = ((q16[q][sft] + mvc[sft]) << 11) | (unsigned)(pos0 + sft);
         lb[16 + q] = v < lb[16 + q] ? v : lb[16 + q];
       }
-      const unsigned v = ((t32[s] + mvc[s]) << 11) | cid[s];
+      const unsigned v = ((t32[sft] + mvc[sft]) << 11) | (unsigned)(pos0 + sft);
       lb[20] = v < lb[20] ? v : lb[20];
     }
   }
@@ -165,23 +254,22 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   }
   __syncthreads();
   if (tid < 21) {
-    const int c = (int)(best[tid] & 2047);
+    int mx, my;
+    me_pos_to_mv((int)(best[tid] & 2047), cand, mx, my);
     bcost[tid] = (int)(best[tid] >> 11);
-    bmv[tid][0] = 4 * (c % side - range);
-    bmv[tid][1] = 4 * (c / side - range);
+    bmv[tid][0] = 4 * mx;
+    bmv[tid][1] = 4 * my;
   }
 
   // ------------------------ half- then quarter-pel refinement ---------------------------
   const uint8_t* sb = reinterpret_cast<const uint8_t*>(s32);
   const uint8_t* ph = phase + (long)b * 16 * g.psz;
-  for (int step = 2; step >= 1 && !(ablate & 2); step >>= 1) {
-    if (tid < 168) subsad[tid >> 3][tid & 7] = 0;
+  for (int step = 2; step >= 1; step >>= 1) {
+    for (int t = tid; t < 168; t += kMeThreads) subsad[t >> 3][t & 7] = 0;
     __syncthreads();
     // A thread owns a group of 8 rows x 8 pixels of one (block, candidate): per row it loads
     // 3 aligned dwords of the phase plane, forms the 2 shifted dwords with v_alignbyte and
-    // accumulates with v_sad_u8 — the same 4-pixels-per-instruction form as the integer
-    // search (per-pixel address math made this stage VALU-issue-bound before).
-    // Groups per candidate: 16 (8x8 blocks) + 16 (4 per 16x16) + 16 (16 for the 32x32).
+    // accumulates with v_sad_u8.  Groups per candidate: 16 (8x8) + 16 (16x16) + 16 (32x32).
     for (int grp = tid; grp < 8 * 48; grp += kMeThreads) {
       const int k = grp / 48, r = grp - k * 48;
       int bi, row0, col0;
@@ -202,13 +290,13 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       int bx, by, l2b;
       me_blk_geom(bi, bx, by, l2b);
       int ox, oy;
-      cand_offset(k, ox, oy);
+      me_cand_offset(k, ox, oy);
       const int mx = bmv[bi][0] + ox * step, my = bmv[bi][1] + oy * step;
       const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
       const int gx0 = cx + bx + col0 + (mx >> 2);
       const int gy0 = cy + by + row0 + (my >> 2);
       const int sw = (by + row0) * kSrcP + ((bx + col0) >> 2);  // source word index of row 0
-      unsigned s = 0;
+      unsigned sad = 0;
       if (gx0 >= -8 && gx0 + 11 <= g.W + 7 && gy0 >= -8 && gy0 + 7 <= g.H + 7) {
         const int a = gx0 & ~3, sh = gx0 & 3;
         const uint8_t* rowp = P + (long)(gy0 + 8) * g.pw16 + a + 8;
@@ -218,36 +306,35 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
           const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
           const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
           const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-          s = __builtin_amdgcn_sad_u8(hi, s32[sw + kSrcP * j + 1],
-                                      __builtin_amdgcn_sad_u8(lo, s32[sw + kSrcP * j], s));
+          sad = __builtin_amdgcn_sad_u8(hi, s32[sw + kSrcP * j + 1], __builtin_amdgcn_sad_u8(lo, s32[sw + kSrcP * j], sad));
         }
       } else {  // touches the clamped border: per-pixel path
         for (int j = 0; j < 8; ++j) {
           const int gy = clip3(-8, g.H + 7, gy0 + j);
           for (int i = 0; i < 8; ++i) {
             const int gx = clip3(-8, g.W + 7, gx0 + i);
-            s += tv_abs((int)sb[(by + row0 + j) * 4 * kSrcP + bx + col0 + i] -
-                        (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
+            sad += tv_abs((int)sb[(by + row0 + j) * 4 * kSrcP + bx + col0 + i] - (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
           }
         }
       }
-      atomicAdd(&subsad[bi][k], (int)s);
+      atomicAdd(&subsad[bi][k], (int)sad);
     }
     __syncthreads();
     if (tid < 21) {
       unsigned bestv = (unsigned)bcost[tid] << 4;
       for (int k = 0; k < 8; ++k) {
         int ox, oy;
-        cand_offset(k, ox, oy);
+        me_cand_offset(k, ox, oy);
         const int mx = bmv[tid][0] + ox * step, my = bmv[tid][1] + oy * step;
-        const unsigned v = ((unsigned)(subsad[tid][k] + pen.mv[mv_bits_est(mx, my)]) << 4) | (unsigned)(k + 1);
+        const unsigned v =
+            ((unsigned)(subsad[tid][k] + pen.mv[me_pen_index(mx - pmv[0], my - pmv[1])]) << 4) | (unsigned)(k + 1);
         bestv = v < bestv ? v : bestv;
       }
       const int kk = (int)(bestv & 15);
       bcost[tid] = (int)(bestv >> 4);
       if (kk) {
         int ox, oy;
-        cand_offset(kk - 1, ox, oy);
+        me_cand_offset(kk - 1, ox, oy);
         bmv[tid][0] += ox * step;
         bmv[tid][1] += oy * step;
       }
@@ -256,7 +343,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   }
 
   // ------------------------------- CU split decision ------------------------------------
-  if (tid == 0 && !(ablate & 8)) {
+  if (tid == 0) {
     const int ps = pen.split_inter;
     int sum16 = 0;
     uint8_t l2u[16];
@@ -387,15 +474,16 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
   }
 }
 
+void launch_quarter(FrameSet src, uint8_t* q, const Geo& g, int B, hipStream_t s) {
+  const int n = (g.W >> 2) * (g.H >> 2);
+  k_quarter<<<dim3((n + 255) / 256, B), 256, 0, s>>>(src, q, g);
+}
+
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
-                        const Geo& g, int qp, const Penalties& pen, int range, int B, hipStream_t s) {
-  // TV_ME_ABLATE (timing experiments only; output is invalid): bit0 skip integer search,
-  // bit1 skip sub-pel refinement, bit2 skip the window fill, bit3 skip the decision write
-  static const int ablate = [] {
-    const char* e = getenv("TV_ME_ABLATE");
-    return e ? atoi(e) : 0;
-  }();
-  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, g, pen, range, ablate);
+                        const Geo& g, int qp, const Penalties& pen, int range, const MeBuffers& me, int B,
+                        hipStream_t s) {
+  k_coarse_me<<<dim3(g.wc * g.hc, B), 64, 0, s>>>(me.qcur, me.qprev, g, pen, range / 4, me.cmv, me.ccost);
+  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, pen, range);
   k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, qp);
 }
 

@@ -11,15 +11,20 @@ double lambda_sad(int qp);
 void pad_source(const uint8_t* const planes[3], const int strides[3], int width, int height,
                 Picture& dst);
 void analyze_intra(const SeqConfig& cfg, const Picture& src, FrameDecisions& fd);
-void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, int range,
-                   FrameDecisions& fd);
+// Hierarchical motion search (tv/me_model.h): quarter-res luma of a source picture, the
+// per-CTB coarse field of qcur vs qprev, and the full-res refinement + CU split decision.
+void quarter_luma(const Picture& src, std::vector<uint8_t>& q);
+void coarse_search(const uint8_t* qcur, const uint8_t* qprev, int W, int H, int range, const int* penmv,
+                   int16_t* cmv, int* ccost);
+void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, const int16_t* cmv,
+                   const int16_t* prev_mv, int range, FrameDecisions& fd);
 // Pass B: prediction + transform/quant + reconstruction (+ deblocking) from decisions.
 void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* ref,
                        FrameDecisions& fd, Picture& rec);
 
 class CpuEncoder {
  public:
-  explicit CpuEncoder(const SeqConfig& cfg, int search_range = 8);
+  explicit CpuEncoder(const SeqConfig& cfg, int search_range = 64);
   // Appends VPS/SPS/PPS (for IDR) and one slice NAL to `out`.
   void encode_frame(const uint8_t* const planes[3], const int strides[3], bool idr, int poc,
                     std::vector<uint8_t>& out);
@@ -31,6 +36,8 @@ class CpuEncoder {
   SeqConfig cfg_;
   int range_;
   Picture src_, rec_, ref_;
+  std::vector<uint8_t> qcur_, qprev_;  // quarter-res source luma (current / previous frame)
+  std::vector<int16_t> prev_mv_;       // previous frame's MV field (temporal candidate)
 };
 
 }  // namespace tv

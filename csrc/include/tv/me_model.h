@@ -1,0 +1,106 @@
+// me_model.h — the hierarchical motion-search model shared by the CPU golden encoder and
+// the gfx950 kernels (TV_HD: host + device), so both make bit-identical decisions.
+//
+//   1. quarter-resolution luma of every SOURCE frame: q = (sum of a 4x4 block + 8) >> 4;
+//   2. coarse search per 32x32 CTB (an 8x8 block at quarter resolution) of the current
+//      quarter frame against the previous quarter SOURCE frame, full search over
+//      [-Rq, Rq]^2 with Rq = range / 4 (range = +-64 full-res pels by default): the
+//      coarse field is fully parallel (no recon dependency) and doubles as lookahead;
+//   3. full-resolution refinement per CTB around a small candidate set — zero, the CTB's
+//      coarse vector, its four coarse neighbours and the co-located vector of the previous
+//      frame — with a [-4, +3] x [-3, +3] integer window per candidate and the SAD of all
+//      21 blocks (16 x 8x8, 4 x 16x16, 1 x 32x32) at every position;
+//   4. half- then quarter-pel refinement per block;
+//   5. the rate term charges the MVD against a CTB predictor (median of the left / top /
+//      top-right coarse vectors), not |MV|: coherent fields are cheap, as AMVP/merge make
+//      them in the bitstream.
+#pragma once
+#include "hevc_defs.h"
+
+namespace tv {
+
+constexpr int kMeMaxCand = 7;
+constexpr int kMeWinX0 = -4, kMeWinX1 = 3;  // integer window around a candidate
+constexpr int kMeWinY0 = -3, kMeWinY1 = 3;
+constexpr int kMeWinW = kMeWinX1 - kMeWinX0 + 1;  // 8
+constexpr int kMeWinH = kMeWinY1 - kMeWinY0 + 1;  // 7
+constexpr int kMePosPerCand = kMeWinW * kMeWinH;  // 56
+
+TV_HD int me_pen_index(int dx, int dy) { return tv_min(63, mv_bits_est(dx, dy)); }
+
+// coarse rate term for a quarter-res displacement (dxq, dyq): the full-res penalty / 16
+// (a quarter-res SAD sums 16x fewer, 16x averaged samples)
+TV_HD int me_coarse_pen(const int* penmv, int dxq, int dyq) {
+  return (penmv[me_pen_index(16 * dxq, 16 * dyq)] + 8) >> 4;
+}
+
+TV_HD int me_median3(int a, int b, int c) { return tv_max(tv_min(a, b), tv_min(tv_max(a, b), c)); }
+
+// floor division of a quarter-pel component to integer pels
+TV_HD int me_qpel_to_int(int v) { return (v + 2) >> 2; }
+
+// Candidate centres (integer full-res pels) of CTB (cxi, cyi) and its MVD predictor pmv
+// (quarter pels).  cmv: coarse field [hc][wc][2] in integer full-res pels.  (tmx, tmy):
+// co-located quarter-pel MV of the previous frame.  Centres are clamped to [-lim, lim] so
+// every integer position stays inside +-range.  Exact duplicates are dropped (first kept).
+TV_HD int me_candidates(const int16_t* cmv, int wc, int hc, int cxi, int cyi, int tmx, int tmy, int lim,
+                        int cand[kMeMaxCand][2], int pmv[2]) {
+  const int self = cyi * wc + cxi;
+  int raw[kMeMaxCand][2];
+  int n = 0;
+  raw[n][0] = 0;
+  raw[n][1] = 0;
+  ++n;
+  raw[n][0] = cmv[2 * self];
+  raw[n][1] = cmv[2 * self + 1];
+  ++n;
+  const int nx[4] = {cxi - 1, cxi, cxi + 1, cxi};
+  const int ny[4] = {cyi, cyi - 1, cyi, cyi + 1};
+  for (int k = 0; k < 4; ++k) {
+    if (nx[k] < 0 || ny[k] < 0 || nx[k] >= wc || ny[k] >= hc) continue;
+    const int o = ny[k] * wc + nx[k];
+    raw[n][0] = cmv[2 * o];
+    raw[n][1] = cmv[2 * o + 1];
+    ++n;
+  }
+  raw[n][0] = me_qpel_to_int(tmx);
+  raw[n][1] = me_qpel_to_int(tmy);
+  ++n;
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    const int x = clip3(-lim, lim, raw[i][0]), y = clip3(-lim, lim, raw[i][1]);
+    bool dup = false;
+    for (int j = 0; j < m; ++j) dup = dup || (cand[j][0] == x && cand[j][1] == y);
+    if (dup) continue;
+    cand[m][0] = x;
+    cand[m][1] = y;
+    ++m;
+  }
+  // predictor: median of left / top / top-right coarse vectors (missing -> own coarse)
+  int px[3], py[3];
+  const int ax[3] = {cxi - 1, cxi, cxi + 1}, ay[3] = {cyi, cyi - 1, cyi - 1};
+  for (int k = 0; k < 3; ++k) {
+    const bool ok = ax[k] >= 0 && ay[k] >= 0 && ax[k] < wc && ay[k] < hc;
+    const int o = ok ? ay[k] * wc + ax[k] : self;
+    px[k] = cmv[2 * o];
+    py[k] = cmv[2 * o + 1];
+  }
+  pmv[0] = 4 * me_median3(px[0], px[1], px[2]);
+  pmv[1] = 4 * me_median3(py[0], py[1], py[2]);
+  return m;
+}
+
+// position index within the candidate windows -> integer MV (full-res pels)
+TV_HD void me_pos_to_mv(int pos, const int cand[kMeMaxCand][2], int& mx, int& my) {
+  const int k = pos / kMePosPerCand, r = pos - k * kMePosPerCand;
+  mx = cand[k][0] + (r % kMeWinW) + kMeWinX0;
+  my = cand[k][1] + (r / kMeWinW) + kMeWinY0;
+}
+
+// sub-pel neighbour k (0..7) of a centre
+TV_HD void me_cand_offset(int k, int& ox, int& oy) {
+  ox = (k == 0 || k == 3 || k == 5) ? -1 : ((k == 1 || k == 6) ? 0 : 1);
+  oy = k < 3 ? -1 : (k < 5 ? 0 : 1);
+}
+
+}  // namespace tv

@@ -14,7 +14,7 @@ def _frames(seed, n, w, h):
                                              (64, 64, 12, True)])
 def test_decode_equals_encoder_recon(w, h, qp, deblock):
     frames = _frames(3, 4, w, h)
-    bs, recons = hevc.encode_sequence_cpu(frames, qp=qp, deblock=deblock, search_range=4)
+    bs, recons = hevc.encode_sequence_cpu(frames, qp=qp, deblock=deblock, search_range=16)
     d = hevc.decode(bs)
     assert (d.width, d.height) == (w, h)
     assert len(d.frames) == len(frames)
@@ -27,7 +27,7 @@ def test_decode_equals_encoder_recon(w, h, qp, deblock):
 
 def test_multiple_idr_segments_concatenate():
     frames = _frames(5, 6, 96, 64)
-    bs, recons = hevc.encode_sequence_cpu(frames, qp=30, gop=3, search_range=4)
+    bs, recons = hevc.encode_sequence_cpu(frames, qp=30, gop=3, search_range=16)
     d = hevc.decode(bs)
     assert len(d.frames) == 6
     for r, dd in zip(recons, d.coded_frames):
@@ -46,7 +46,7 @@ def test_synth_deterministic_and_moving():
 
 def test_mp4_roundtrip():
     frames = _frames(2, 3, 96, 64)
-    bs, _ = hevc.encode_sequence_cpu(frames, qp=27, search_range=4)
+    bs, _ = hevc.encode_sequence_cpu(frames, qp=27, search_range=16)
     mp4 = hevc.mux_mp4(bs, 96, 64, 30, 1)
     assert mp4[4:8] == b"ftyp"
     assert mp4.index(b"moov") < mp4.index(b"mdat")  # faststart layout
@@ -60,7 +60,7 @@ def test_mp4_roundtrip():
 
 def test_write_frame_from_decisions_matches_encoder():
     frames = _frames(4, 2, 96, 64)
-    enc = hevc.CpuEncoder(96, 64, qp=27, search_range=4)
+    enc = hevc.CpuEncoder(96, 64, qp=27, search_range=16)
     out = enc.encode(frames[0], True, 0)
     dec = enc.decisions()
     # re-run golden pass B from the decisions and entropy-code it separately
@@ -77,7 +77,7 @@ def test_sao_roundtrip_and_gain(qp, deblock):
     frames = _frames(4, 6, 192, 128)
     res = {}
     for sao in (False, True):
-        enc = hevc.CpuEncoder(192, 128, qp=qp, deblock=deblock, sao=sao, search_range=8)
+        enc = hevc.CpuEncoder(192, 128, qp=qp, deblock=deblock, sao=sao, search_range=16)
         bs, recons = b"", []
         for i, f in enumerate(frames):
             bs += enc.encode(f, i == 0, i)

@@ -17,7 +17,7 @@ def _engine(**kw):
                                                 (128, 64, 22, False, False), (192, 128, 30, True, True),
                                                 (160, 90, 24, False, True)])
 def test_gpu_bitstream_equals_cpu_reference(w, h, qp, deblock, sao):
-    gop, rng = 4, 8
+    gop, rng = 4, 16
     eng = _engine(width=w, height=h, qp=qp, batch=2, gop=gop, search_range=rng, deblock=deblock, sao=sao, seed=5)
     segs = eng.encode_synthetic([0, 10])
     for b, start in enumerate([0, 10]):
@@ -35,10 +35,10 @@ def test_gpu_bitstream_equals_cpu_reference(w, h, qp, deblock, sao):
 
 def test_gpu_host_frames_path():
     w, h, gop = 96, 64, 3
-    eng = _engine(width=w, height=h, qp=27, batch=1, gop=gop, search_range=4)
+    eng = _engine(width=w, height=h, qp=27, batch=1, gop=gop, search_range=16)
     frames = [hevc.synth_frame(8, t, w, h) for t in range(gop)]
     seg = eng.encode_frames([frames])[0]
-    cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, search_range=4)
+    cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, search_range=16)
     assert seg == cpu_bs
 
 
@@ -58,3 +58,20 @@ def test_encode_parts_variable_chunks():
         assert len(dec.frames) == n
         for a, d in zip(frames, dec.frames):
             assert hevc.psnr(a[0], d[0]) > 30
+
+
+@pytest.mark.parametrize("w,h,batch,gop,sao,check", [(1920, 1080, 8, 3, False, (0, 7)), (1920, 1080, 8, 3, True, (5,)),
+                                                     (3840, 2160, 2, 2, False, (1,))])
+def test_gpu_bit_exact_at_benchmark_geometry(w, h, batch, gop, sao, check):
+    """The benchmarked geometry (full-HD / 4K, search range 64, a batch split over two
+    stream groups, SAO on and off) is bit-exact with the CPU golden model: frame edges, the
+    coarse lookahead field, candidate windows and multi-group scheduling at real size."""
+    rng = 64
+    eng = _engine(width=w, height=h, qp=27, batch=batch, gop=gop, search_range=rng, sao=sao, seed=3)
+    starts = [100 * b for b in range(batch)]
+    segs = eng.encode_synthetic(starts)
+    for b in check:
+        frames = [hevc.synth_frame(3, starts[b] + f, w, h) for f in range(gop)]
+        cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, sao=sao, search_range=rng)
+        assert segs[b] == cpu_bs, f"segment {b}: GPU bitstream differs from CPU golden model"
+    eng.close()

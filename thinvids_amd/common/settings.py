@@ -38,7 +38,7 @@ DEFAULT_SETTINGS: dict[str, str] = {
     "tv_qp": "27",
     "tv_rc": "cqp",
     "tv_gop": "64",
-    "tv_search_range": "16",
+    "tv_search_range": "64",
     "tv_deblock": "1",
     "tv_sao": "1",
     "tv_segment_frames": "0",  # 0 = derive from target_segment_mb

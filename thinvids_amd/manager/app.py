@@ -310,7 +310,7 @@ def settings_from_payload(p: dict, cur: dict) -> dict:
         "pipeline_min_idle_workers_to_start_next": str(max(1, int(p.get(
             "pipeline_min_idle_workers_to_start_next", cur.get("pipeline_min_idle_workers_to_start_next", 4))))),
     }
-    for k, lo, hi in (("tv_qp", 0, 51), ("tv_gop", 1, 600), ("tv_search_range", 4, 16), ("tv_segment_frames", 0, 100000)):
+    for k, lo, hi in (("tv_qp", 0, 51), ("tv_gop", 1, 600), ("tv_search_range", 16, 128), ("tv_segment_frames", 0, 100000)):
         if k in p:
             m[k] = str(min(hi, max(lo, int(p[k]))))
     if "tv_deblock" in p:

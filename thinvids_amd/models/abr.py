@@ -125,7 +125,7 @@ class AbrLadder:
 
     def __init__(self, src_w: int = SRC_8K[0], src_h: int = SRC_8K[1], heights=LADDER, qp: int = 27,
                  segments: int = 16, gop: int = 16, device: int = 0, threads: int | None = None, seed: int = 1,
-                 src_peak: float = 1000.0, dst_peak: float = 100.0, search_range: int = 16,
+                 src_peak: float = 1000.0, dst_peak: float = 100.0, search_range: int = 64,
                  concurrent: bool = True, sao: bool = False, cascade: bool = True, slots: int = 2,
                  fused: bool = True):
         import torch

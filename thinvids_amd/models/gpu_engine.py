@@ -58,7 +58,7 @@ def default_threads() -> int:
 
 class GpuEngine:
     def __init__(self, width: int, height: int, qp: int = 27, batch: int = 8, gop: int = 16,
-                 search_range: int = 16, deblock: bool = True, sao: bool = False, seed: int = 1,
+                 search_range: int = 64, deblock: bool = True, sao: bool = False, seed: int = 1,
                  threads: int | None = None,
                  device: int = 0, max_merge: int = 5):
         self.lib = _lib()

@@ -42,7 +42,7 @@ class CpuEncoder:
     """Scalar C++ HEVC encoder (software path; reference `software_encode`)."""
 
     def __init__(self, width: int, height: int, qp: int = 27, deblock: bool = True,
-                 search_range: int = 8, max_merge: int = 5, sao: bool = False):
+                 search_range: int = 64, max_merge: int = 5, sao: bool = False):
         if width % 2 or height % 2:
             raise ValueError("width/height must be even")
         self.lib = core_lib()

@@ -248,7 +248,7 @@ def _encode_many(items: list, spec_for, cache) -> dict:
 
 def run_job(input_path: str, output: str, height: int | None = None, qp: int = 27, gop: int = 64,
             segment_frames: int = 256, mode: str = "direct", bitrate_kbps: float = 0.0, ladder=None,
-            search_range: int = 16, software: bool = False, batch_segments: int = 8,
+            search_range: int = 64, software: bool = False, batch_segments: int = 8,
             resume_dir: str | None = None, max_retries: int = 3) -> dict:
     import torch
 

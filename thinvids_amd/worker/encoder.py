@@ -31,7 +31,7 @@ class EncodeSpec:
     height: int
     qp: int = 27
     gop: int = 64
-    search_range: int = 16
+    search_range: int = 64
     deblock: bool = True
     sao: bool = False
     software: bool = False

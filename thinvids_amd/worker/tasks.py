@@ -97,7 +97,7 @@ def encode_spec_for_job(job: dict, settings: dict | None = None) -> EncodeSpec:
     th, _ = effective_target_height(job)
     ow, oh = output_geometry(w, h, th)
     return EncodeSpec(width=ow, height=oh, qp=as_int(job.get("qp") or s.get("tv_qp"), get_config().qp),
-                      gop=max(1, as_int(s.get("tv_gop"), 64)), search_range=as_int(s.get("tv_search_range"), 16),
+                      gop=max(1, as_int(s.get("tv_gop"), 64)), search_range=max(16, min(128, as_int(s.get("tv_search_range"), 64) // 16 * 16)),
                       deblock=as_bool(s.get("tv_deblock"), True), sao=as_bool(s.get("tv_sao"), True),
                       software=as_bool(job.get("software_encode")))
 

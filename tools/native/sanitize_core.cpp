@@ -53,7 +53,7 @@ int main() {
   for (int sao = 0; sao < 2; ++sao) {
     const int W = 136, H = 72, N = 4;
     const int CW = (W + 31) / 32 * 32, CH = (H + 31) / 32 * 32;
-    void* enc = tv_cpu_encoder_new(W, H, 27, 1 | (sao << 1), 8, 5);
+    void* enc = tv_cpu_encoder_new(W, H, 27, 1 | (sao << 1), 16, 5);
     if (!enc) return fail("encoder_new");
     void* frame = tv_bytes_new();
     std::vector<uint8_t> stream, y(W * H), u(W * H / 4), v(W * H / 4);
