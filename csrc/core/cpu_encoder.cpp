@@ -86,15 +86,25 @@ void analyze_intra(const SeqConfig& cfg, const Picture& src, FrameDecisions& fd)
   struct Best {
     int cost, mode;
   };
+  // two-stage mode search (tv/me_model.h kIntraCoarseModes): planar, DC and every 4th
+  // angular mode, then the +-1/+-2 neighbours of the best coarse angular mode
   auto best_mode = [&](int x, int y, int log2) -> Best {
-    Best b{INT_MAX, 1};
-    for (int m = 0; m < 35; ++m) {
+    unsigned best = 0xffffffffu, best_ang = 0xffffffffu;
+    auto eval = [&](int m) {
       predict_intra_tb(src, 0, x, y, log2, m, pred);
       int c = block_satd(src.y.data() + (size_t)y * W + x, W, pred, 1 << log2);
       c += (int)(lam * (m <= 1 ? 2 : 5));
-      if (c < b.cost) b = Best{c, m};
+      const unsigned v = ((unsigned)c << 6) | (unsigned)m;
+      best = v < best ? v : best;
+      if (m >= 2) best_ang = v < best_ang ? v : best_ang;
+    };
+    for (int i = 0; i < kIntraCoarseModes; ++i) eval(intra_coarse_mode(i));
+    const int ma = (int)(best_ang & 63);
+    for (int i = 0; i < 4; ++i) {
+      const int m = intra_refine_mode(ma, i);
+      if (m >= 2) eval(m);
     }
-    return b;
+    return Best{(int)(best >> 6), (int)(best & 63)};
   };
   for (int cy = 0; cy < H; cy += 32)
     for (int cx = 0; cx < W; cx += 32) {

@@ -366,7 +366,7 @@ class Core {
     const int B = B_, F = F_;
     Range frame_range(f == 0 ? "engine.frame.intra" : "engine.frame.inter");
     Slot& s = slots_[f % kSlots];
-    while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    wait_slot(s);
     const DecisionSet dec = slot_dec(s);
     upload(f, B);
     FrameSet cur = rec_[f & 1], prev = rec_[(f + 1) & 1];
@@ -407,10 +407,10 @@ class Core {
         fetch_slot(s, B);
       } catch (const std::exception& e) {
         fail(e);
-        s.pending.fetch_sub(B + 1, std::memory_order_acq_rel);
+        release(s, B + 1);
         return;
       }
-      s.pending.fetch_sub(1, std::memory_order_acq_rel);
+      release(s, 1);
       for (int b = 0; b < B; ++b)
         pool_->submit([this, &s, b, f] {
           try {
@@ -422,7 +422,7 @@ class Core {
           } catch (const std::exception& e) {
             fail(e);
           }
-          s.pending.fetch_sub(1, std::memory_order_acq_rel);
+          release(s, 1);
         });
     });
   }
@@ -431,7 +431,7 @@ class Core {
 
   void finish() {
     for (auto& s : slots_)
-      while (s.pending.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+      wait_slot(s);
     HIP_OK(hipStreamSynchronize(stream_));
     if (failed_) throw std::runtime_error("encode failed: " + err_);
     std::vector<unsigned long long> sse(B_ * 3);
@@ -457,6 +457,18 @@ class Core {
   long entropy_ns() const { return entropy_ns_; }
 
  private:
+  // Slot hand-back: the host thread sleeps on a condition variable instead of spinning, so
+  // eight ranks on one node do not burn cores the CABAC pools need.
+  void release(Slot& s, int n) {
+    if (s.pending.fetch_sub(n, std::memory_order_acq_rel) == n) {
+      std::lock_guard<std::mutex> lk(slot_mu_);
+      slot_cv_.notify_all();
+    }
+  }
+  void wait_slot(Slot& s) {
+    std::unique_lock<std::mutex> lk(slot_mu_);
+    slot_cv_.wait(lk, [&] { return s.pending.load(std::memory_order_acquire) == 0; });
+  }
   void fail(const std::exception& e) {
     std::lock_guard<std::mutex> lk(err_mu_);
     err_ = e.what();
@@ -490,6 +502,8 @@ class Core {
   ThreadPool* pool_;
   int B_ = 0, F_ = 0;
   std::vector<std::vector<std::vector<uint8_t>>> slices_;
+  std::mutex slot_mu_;
+  std::condition_variable slot_cv_;
   std::atomic<int> failed_{0};
   std::string err_;
   std::mutex err_mu_;

@@ -373,104 +373,304 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   }
 }
 
-// P-frame pass B: all TBs of a P-frame are independent (inter-only), so the (CU, component)
-// TBs of a CTB are dealt round-robin to the 4 waves and coded wave-synchronously.
-struct TbLds {
-  uint8_t pred[1024];
-  int16_t resid[1024];
-  WaveTbScratch tb;
+// ---------------------------------------------------------------------------------------
+// P-frame pass B on matrix cores: every TB of the CTB is coded by 16x16 MFMA tiles.
+//
+// A P frame has only inter CUs, so all predictions and residuals of the CTB exist up front
+// and every transform stage is a batch of small GEMMs.  TBs smaller than 16 are packed
+// block-diagonally into one v_mfma 16x16x16 tile: a 16x16 luma quadrant of four 8x8 TBs is
+// diag(T8, T8) * R (stage 1) / A * diag(T8, T8)^T (stage 2) — the shared DCT matrix makes the
+// four products one MFMA; the Cb and Cr 8x8 regions of a quadrant (one 8x8 TB each, or four
+// 4x4 TBs each) form the two diagonal blocks of one tile, diag(Rcb, Rcr).  So a CTB is 8
+// tiles per stage (4 luma quadrants + 4 chroma pairs; a single 32x32 CU: 4 K=32 luma tiles +
+// 2 chroma tiles) with no VALU dot products at all.  Every operand is an integer of <= 9
+// bits (8-bit split halves where needed) so every product and partial sum is exact in f32:
+// bit-identical to tv::forward_transform / tv::inverse_transform (see tb_coder.h).
+// ---------------------------------------------------------------------------------------
+struct PReconLds {
+  int16_t T[32][32];          // DCT-32 (every smaller DCT is a row subsample)
+  int tmpY[32 * 33];          // stage 1 / stage 3 outputs (luma)
+  int tmpC[2][16 * 16];       // stage 1 / stage 3 outputs (Cb, Cr)
+  int16_t resY[32 * 32];      // residual, later levels (luma)
+  int16_t resC[2][16 * 16];   // residual, later levels (chroma)
+  uint8_t predY[32 * 32];
+  uint8_t predC[2][16 * 16];
+  int mv[16][2];              // per 8x8 unit (raster within the CTB)
+  int nz[48], sa[48], dc[48];  // per-TB statistics: luma 0..15, Cb 16..31, Cr 32..47
+  int qtype[4];               // luma quadrant: 0 part of a 32x32 CU, 1 16x16 CU, 2 four 8x8 CUs
 };
+
+// block size (log2) of the TB owning luma sample (x, y) / chroma sample (x, y) of the CTB
+__device__ __forceinline__ int pr_l2_luma(const PReconLds& L, int x, int y) {
+  const int t = L.qtype[(y >> 4) * 2 + (x >> 4)];
+  return t == 0 ? 5 : (t == 1 ? 4 : 3);
+}
+__device__ __forceinline__ int pr_tb_luma(const PReconLds& L, int x, int y) {
+  const int q = (y >> 4) * 2 + (x >> 4), t = L.qtype[q];
+  return t == 0 ? 0 : (t == 1 ? 4 * q : 4 * q + ((y >> 3) & 1) * 2 + ((x >> 3) & 1));
+}
+__device__ __forceinline__ int pr_tb_chroma(const PReconLds& L, int p, int x, int y) {
+  const int q = (y >> 3) * 2 + (x >> 3), t = L.qtype[q];
+  const int base = 16 + 16 * p;
+  return t == 0 ? base : (t == 1 ? base + 4 * q : base + 4 * q + ((y >> 2) & 1) * 2 + ((x >> 2) & 1));
+}
+// block-diagonal composite of DCT blocks of size 2^l2 inside a 16x16 tile: C(r, k)
+__device__ __forceinline__ int pr_comp(const PReconLds& L, int l2, int r, int k) {
+  return (r >> l2) == (k >> l2) ? (int)L.T[(r & ((1 << l2) - 1)) << (5 - l2)][k & ((1 << l2) - 1)] : 0;
+}
+// a TB whose only non-zero level is a lone +-1 outside DC is dropped (tv code_tb, inter)
+__device__ __forceinline__ bool pr_zeroed(const PReconLds& L, int id) {
+  return L.nz[id] == 0 || (L.nz[id] == 1 && L.sa[id] == 1 && L.dc[id] == 0);
+}
 
 __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                      FrameSet rec, DecisionSet dec, Geo g, int qp) {
-  const int ctu = blockIdx.x, b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
-  __shared__ int Tm[32][33];
-  __shared__ TbLds W[4];
-  __shared__ int cus[16][4];  // x0, y0, log2, unit
-  __shared__ int ncu;
-  __shared__ unsigned cbfs[16];
   const long ub = b * g.usz;
-  const uint8_t* ph = phase + (long)b * 16 * g.psz;
-  tb_load_matrix(Tm);
-  if (threadIdx.x == 0) {
-    int n = 0;
-    for (int k8 = 0; k8 < 16; ++k8) {
-      const int x0 = cx + (k8 & 3) * 8, y0 = cy + (k8 >> 2) * 8;
-      const int u = (y0 >> 3) * g.w8 + (x0 >> 3);
-      const int log2 = dec.cu_log2[ub + u];
-      if ((x0 & ((1 << log2) - 1)) || (y0 & ((1 << log2) - 1))) continue;  // not a CU origin
-      cus[n][0] = x0;
-      cus[n][1] = y0;
-      cus[n][2] = log2;
-      cus[n][3] = u;
-      ++n;
-    }
-    ncu = n;
+  const int qpc = chroma_qp(qp, 0), Wc = g.W >> 1, Hc = g.H >> 1;
+  __shared__ PReconLds L;
+  for (int i = tid; i < 1024; i += 256) L.T[i >> 5][i & 31] = (int16_t)kDct32.m[i >> 5][i & 31];
+  if (tid < 16) {
+    const long u = ub + (long)((cy >> 3) + (tid >> 2)) * g.w8 + (cx >> 3) + (tid & 3);
+    L.mv[tid][0] = dec.mv[2 * u];
+    L.mv[tid][1] = dec.mv[2 * u + 1];
   }
-  if (threadIdx.x < 16) cbfs[threadIdx.x] = 0;
+  if (tid < 48) L.nz[tid] = L.sa[tid] = L.dc[tid] = 0;
+  if (tid < 4) {
+    const int l2 = dec.cu_log2[ub + (long)((cy >> 3) + (tid >> 1) * 2) * g.w8 + (cx >> 3) + (tid & 1) * 2];
+    L.qtype[tid] = l2 == 5 ? 0 : (l2 == 4 ? 1 : 2);
+  }
   __syncthreads();
-  // A CTB coded as one 32x32 CU: its luma TB would keep one wave busy for the whole
-  // kernel while the others idle after chroma, so all four waves code it together (one
-  // 16x16 MFMA tile each per stage), then two waves take the chroma TBs.
-  const bool whole = ncu == 1 && cus[0][2] == 5;
-  if (whole) {
-    const long u = ub + cus[0][3];
-    const int mvx = dec.mv[2 * u], mvy = dec.mv[2 * u + 1];
-    const uint8_t* P = ph + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
+  // ---- prediction + residual of all three planes
+  {
     const uint8_t* S = src.plane(0, b, g);
-    uint8_t* pred = W[0].pred;
-    int16_t* resid = W[0].resid;
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-      const int px = i & 31, py = i >> 5;
-      const int p = phase_at(P, g, cx + px + (mvx >> 2), cy + py + (mvy >> 2));
-      pred[i] = (uint8_t)p;
-      resid[i] = (int16_t)((int)S[(cy + py) * g.W + cx + px] - p);
-    }
-    __syncthreads();
-    const int cb = wg_code_tb(resid, pred, 5, qp, false, dec.coef_y + b * g.ysz + (long)cy * g.W + cx, g.W,
-                              rec.plane(0, b, g) + (long)cy * g.W + cx, g.W, Tm, W[1].tb.tmp, W[1].tb.coef,
-                              reinterpret_cast<int*>(W[2].resid));
-    if (threadIdx.x == 0 && cb) atomicOr(&cbfs[0], 1u);
-  }
-  TbLds& Ld = W[wave];
-  for (int t = whole ? wave + 1 : wave; t < 3 * ncu; t += whole ? 8 : 4) {
-    const int k = t / 3, c = t - 3 * k;
-    const int x0 = cus[k][0], y0 = cus[k][1], log2 = cus[k][2];
-    const long u = ub + cus[k][3];
-    const int mvx = dec.mv[2 * u], mvy = dec.mv[2 * u + 1];
-    const int l2 = c ? log2 - 1 : log2, N = 1 << l2;
-    const int x = c ? x0 >> 1 : x0, y = c ? y0 >> 1 : y0;
-    const int pw = c ? g.W / 2 : g.W, phh = c ? g.H / 2 : g.H;
-    const uint8_t* S = src.plane(c, b, g);
-    if (c == 0) {
+    const uint8_t* ph = phase + (long)b * 16 * g.psz;
+    for (int i = tid; i < 1024; i += 256) {
+      const int x = i & 31, y = i >> 5, un = (y >> 3) * 4 + (x >> 3);
+      const int mvx = L.mv[un][0], mvy = L.mv[un][1];
       const uint8_t* P = ph + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
-      for (int i = lane; i < N * N; i += 64) {
-        const int px = i & (N - 1), py = i >> l2;
-        const int p = phase_at(P, g, x + px + (mvx >> 2), y + py + (mvy >> 2));
-        Ld.pred[i] = (uint8_t)p;
-        Ld.resid[i] = (int16_t)((int)S[(y + py) * pw + x + px] - p);
+      const int p = phase_at(P, g, cx + x + (mvx >> 2), cy + y + (mvy >> 2));
+      L.predY[i] = (uint8_t)p;
+      L.resY[i] = (int16_t)((int)S[(long)(cy + y) * g.W + cx + x] - p);
+    }
+    for (int i = tid; i < 512; i += 256) {
+      const int pl = i >> 8, x = i & 15, y = (i >> 4) & 15, un = (y >> 2) * 4 + (x >> 2);
+      const int mvx = L.mv[un][0], mvy = L.mv[un][1];
+      const uint8_t* Rf = ref.plane(1 + pl, b, g);
+      const int gx = (cx >> 1) + x, gy = (cy >> 1) + y;
+      const int p = mc_chroma_sample(Rf, Wc, Wc, Hc, gx + (mvx >> 3), gy + (mvy >> 3), mvx & 7, mvy & 7);
+      L.predC[pl][y * 16 + x] = (uint8_t)p;
+      L.resC[pl][y * 16 + x] = (int16_t)((int)src.plane(1 + pl, b, g)[(long)gy * Wc + gx] - p);
+    }
+  }
+  __syncthreads();
+  const bool whole = L.qtype[0] == 0;
+  const int ntiles = whole ? 6 : 8;
+  // tile t: luma (whole: 32x32 tile ti,tj = t>>1, t&1; else quadrant t) for t < 4, chroma
+  // (whole: plane t-4 as one 16x16 TB; else the Cb|Cr pair of quadrant t-4) for t >= 4.
+  // ---------------------------------------------------------------- stage 1: T * R
+  for (int t = wave; t < ntiles; t += 4) {
+    int o[4];
+    if (t < 4) {
+      if (whole) {
+        mfma_tile([&](int r, int k) { return (int)L.T[r][k]; }, [&](int k, int c) { return (int)L.resY[k * 32 + c]; },
+                  t >> 1, t & 1, 32, false, false, o);
+      } else {
+        const int ox = (t & 1) * 16, oy = (t >> 1) * 16, l2 = L.qtype[t] == 1 ? 4 : 3;
+        mfma_tile([&](int r, int k) { return pr_comp(L, l2, r, k); },
+                  [&](int k, int c) { return (int)L.resY[(oy + k) * 32 + ox + c]; }, 0, 0, 16, false, false, o);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
+        const int y = whole ? 16 * (t >> 1) + rr : (t >> 1) * 16 + rr, x = whole ? 16 * (t & 1) + cc : (t & 1) * 16 + cc;
+        const int sh1 = pr_l2_luma(L, x, y) - 1;
+        L.tmpY[y * 33 + x] = (o[r] + (1 << (sh1 - 1))) >> sh1;
+      }
+    } else if (whole) {
+      const int pl = t - 4;
+      mfma_tile([&](int r, int k) { return pr_comp(L, 4, r, k); }, [&](int k, int c) { return (int)L.resC[pl][k * 16 + c]; },
+                0, 0, 16, false, false, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
+        L.tmpC[pl][rr * 16 + cc] = (o[r] + 4) >> 3;  // 16-point: sh1 = 3
       }
     } else {
-      const uint8_t* Rf = ref.plane(c, b, g);
-      for (int i = lane; i < N * N; i += 64) {
-        const int px = i & (N - 1), py = i >> l2;
-        const int p = mc_chroma_sample(Rf, pw, pw, phh, x + px + (mvx >> 3), y + py + (mvy >> 3), mvx & 7, mvy & 7);
-        Ld.pred[i] = (uint8_t)p;
-        Ld.resid[i] = (int16_t)((int)S[(y + py) * pw + x + px] - p);
+      const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
+      mfma_tile([&](int r, int k) { return pr_comp(L, l2, r, k); },
+                [&](int k, int c) {
+                  return (k >> 3) == (c >> 3) ? (int)L.resC[k >> 3][(oy + (k & 7)) * 16 + ox + (c & 7)] : 0;
+                },
+                0, 0, 16, false, false, o);
+      const int sh1 = l2 - 1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
+        if ((rr >> 3) == (cc >> 3)) L.tmpC[rr >> 3][(oy + (rr & 7)) * 16 + ox + (cc & 7)] = (o[r] + (1 << (sh1 - 1))) >> sh1;
       }
     }
-    wave_sync();
-    int16_t* lev = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz) +
-                   (long)y * pw + x;
-    const int cb = wave_code_tb(Ld.resid, Ld.pred, l2, c ? chroma_qp(qp, 0) : qp, false, lev, pw,
-                                rec.plane(c, b, g) + (long)y * pw + x, pw, Tm, Ld.tb);
-    if (lane == 0 && cb) atomicOr(&cbfs[k], 1u << c);
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < ncu * 16; k += blockDim.x) {
-    const int cu = k >> 4, j = k & 15, n8 = 1 << (cus[cu][2] - 3);
-    if (j < n8 * n8) dec.cbf[ub + cus[cu][3] + (j / n8) * g.w8 + j % n8] = (uint8_t)cbfs[cu];
+  // ------------------------------------------------- stage 2: A * T^T + quantisation
+  auto emit_level = [&](int16_t* dst, int id, int l2, int q, int v, bool origin) {
+    const int sh2 = l2 + 6;
+    const int lev = quant_level((v + (1 << (sh2 - 1))) >> sh2, q, l2, false);
+    *dst = (int16_t)lev;
+    if (lev) {
+      atomicAdd(&L.nz[id], 1);
+      atomicAdd(&L.sa[id], tv_abs(lev));
+    }
+    if (origin) L.dc[id] = lev;
+  };
+  for (int t = wave; t < ntiles; t += 4) {
+    int o[4];
+    if (t < 4) {
+      if (whole) {
+        mfma_tile([&](int r, int k) { return L.tmpY[r * 33 + k]; }, [&](int k, int c) { return (int)L.T[c][k]; },
+                  t >> 1, t & 1, 32, true, true, o);
+      } else {
+        const int ox = (t & 1) * 16, oy = (t >> 1) * 16, l2 = L.qtype[t] == 1 ? 4 : 3;
+        mfma_tile([&](int r, int k) { return L.tmpY[(oy + r) * 33 + ox + k]; },
+                  [&](int k, int c) { return pr_comp(L, l2, c, k); }, 0, 0, 16, true, true, o);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
+        const int y = (t >> 1) * 16 + rr, x = (t & 1) * 16 + cc;
+        const int l2 = pr_l2_luma(L, x, y), m = (1 << l2) - 1;
+        emit_level(&L.resY[y * 32 + x], pr_tb_luma(L, x, y), l2, qp, o[r], (x & m) == 0 && (y & m) == 0);
+      }
+    } else if (whole) {
+      const int pl = t - 4;
+      mfma_tile([&](int r, int k) { return L.tmpC[pl][r * 16 + k]; }, [&](int k, int c) { return pr_comp(L, 4, c, k); },
+                0, 0, 16, true, true, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
+        emit_level(&L.resC[pl][rr * 16 + cc], 16 + 16 * pl, 4, qpc, o[r], rr == 0 && cc == 0);
+      }
+    } else {
+      const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
+      mfma_tile([&](int r, int k) {
+                  return (r >> 3) == (k >> 3) ? L.tmpC[r >> 3][(oy + (r & 7)) * 16 + ox + (k & 7)] : 0;
+                },
+                [&](int k, int c) { return pr_comp(L, l2, c, k); }, 0, 0, 16, true, true, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
+        if ((rr >> 3) != (cc >> 3)) continue;
+        const int pl = rr >> 3, x = ox + (cc & 7), y = oy + (rr & 7), m = (1 << l2) - 1;
+        emit_level(&L.resC[pl][y * 16 + x], pr_tb_chroma(L, pl, x, y), l2, qpc, o[r], (x & m) == 0 && (y & m) == 0);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- final levels (dropped TBs zeroed) -> the level planes; cbf per CU
+  {
+    int16_t* LY = dec.coef_y + b * g.ysz + (long)cy * g.W + cx;
+    for (int i = tid; i < 1024; i += 256) {
+      const int x = i & 31, y = i >> 5;
+      if (pr_zeroed(L, pr_tb_luma(L, x, y))) L.resY[i] = 0;
+      LY[(long)y * g.W + x] = L.resY[i];
+    }
+    for (int i = tid; i < 512; i += 256) {
+      const int pl = i >> 8, x = i & 15, y = (i >> 4) & 15;
+      if (pr_zeroed(L, pr_tb_chroma(L, pl, x, y))) L.resC[pl][y * 16 + x] = 0;
+      (pl ? dec.coef_v : dec.coef_u)[b * g.csz + (long)((cy >> 1) + y) * Wc + (cx >> 1) + x] = L.resC[pl][y * 16 + x];
+    }
+    if (tid < 16) {
+      const int x = (tid & 3) * 8, y = (tid >> 2) * 8;  // this unit's CU = its TBs
+      const int cb = (pr_zeroed(L, pr_tb_luma(L, x, y)) ? 0 : 1) | (pr_zeroed(L, pr_tb_chroma(L, 0, x >> 1, y >> 1)) ? 0 : 2) |
+                     (pr_zeroed(L, pr_tb_chroma(L, 1, x >> 1, y >> 1)) ? 0 : 4);
+      dec.cbf[ub + (long)((cy >> 3) + (tid >> 2)) * g.w8 + (cx >> 3) + (tid & 3)] = (uint8_t)cb;
+    }
+  }
+  __syncthreads();
+  // --------------------------------------- stage 3: T^T * dequant(levels)  (split d)
+  for (int t = wave; t < ntiles; t += 4) {
+    int o[4];
+    if (t < 4) {
+      if (whole) {
+        mfma_tile([&](int r, int k) { return (int)L.T[k][r]; },
+                  [&](int k, int c) { return dequant_level(L.resY[k * 32 + c], qp, 5); }, t >> 1, t & 1, 32, true, false, o);
+      } else {
+        const int ox = (t & 1) * 16, oy = (t >> 1) * 16, l2 = L.qtype[t] == 1 ? 4 : 3;
+        mfma_tile([&](int r, int k) { return pr_comp(L, l2, k, r); },
+                  [&](int k, int c) { return dequant_level(L.resY[(oy + k) * 32 + ox + c], qp, l2); }, 0, 0, 16, true, false, o);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int y = (t >> 1) * 16 + (lane >> 4) * 4 + r, x = (t & 1) * 16 + (lane & 15);
+        L.tmpY[y * 33 + x] = clip3(-32768, 32767, (o[r] + 64) >> 7);
+      }
+    } else if (whole) {
+      const int pl = t - 4;
+      mfma_tile([&](int r, int k) { return pr_comp(L, 4, k, r); },
+                [&](int k, int c) { return dequant_level(L.resC[pl][k * 16 + c], qpc, 4); }, 0, 0, 16, true, false, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        L.tmpC[pl][((lane >> 4) * 4 + r) * 16 + (lane & 15)] = clip3(-32768, 32767, (o[r] + 64) >> 7);
+    } else {
+      const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
+      mfma_tile([&](int r, int k) { return pr_comp(L, l2, k, r); },
+                [&](int k, int c) {
+                  return (k >> 3) == (c >> 3) ? dequant_level(L.resC[k >> 3][(oy + (k & 7)) * 16 + ox + (c & 7)], qpc, l2) : 0;
+                },
+                0, 0, 16, true, false, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
+        if ((rr >> 3) == (cc >> 3))
+          L.tmpC[rr >> 3][(oy + (rr & 7)) * 16 + ox + (cc & 7)] = clip3(-32768, 32767, (o[r] + 64) >> 7);
+      }
+    }
+  }
+  __syncthreads();
+  // ------------------------------------- stage 4: G * T + prediction -> reconstruction
+  for (int t = wave; t < ntiles; t += 4) {
+    int o[4];
+    if (t < 4) {
+      if (whole) {
+        mfma_tile([&](int r, int k) { return L.tmpY[r * 33 + k]; }, [&](int k, int c) { return (int)L.T[k][c]; },
+                  t >> 1, t & 1, 32, true, true, o);
+      } else {
+        const int ox = (t & 1) * 16, oy = (t >> 1) * 16, l2 = L.qtype[t] == 1 ? 4 : 3;
+        mfma_tile([&](int r, int k) { return L.tmpY[(oy + r) * 33 + ox + k]; },
+                  [&](int k, int c) { return pr_comp(L, l2, k, c); }, 0, 0, 16, true, true, o);
+      }
+      uint8_t* R = rec.plane(0, b, g) + (long)cy * g.W + cx;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int y = (t >> 1) * 16 + (lane >> 4) * 4 + r, x = (t & 1) * 16 + (lane & 15);
+        R[(long)y * g.W + x] = (uint8_t)clip_pixel((int)L.predY[y * 32 + x] + ((o[r] + 2048) >> 12));
+      }
+    } else if (whole) {
+      const int pl = t - 4;
+      mfma_tile([&](int r, int k) { return L.tmpC[pl][r * 16 + k]; }, [&](int k, int c) { return pr_comp(L, 4, k, c); },
+                0, 0, 16, true, true, o);
+      uint8_t* R = rec.plane(1 + pl, b, g) + (long)(cy >> 1) * Wc + (cx >> 1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int y = (lane >> 4) * 4 + r, x = lane & 15;
+        R[(long)y * Wc + x] = (uint8_t)clip_pixel((int)L.predC[pl][y * 16 + x] + ((o[r] + 2048) >> 12));
+      }
+    } else {
+      const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
+      mfma_tile([&](int r, int k) {
+                  return (r >> 3) == (k >> 3) ? L.tmpC[r >> 3][(oy + (r & 7)) * 16 + ox + (k & 7)] : 0;
+                },
+                [&](int k, int c) { return pr_comp(L, l2, k, c); }, 0, 0, 16, true, true, o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
+        if ((rr >> 3) != (cc >> 3)) continue;
+        const int pl = rr >> 3, x = ox + (cc & 7), y = oy + (rr & 7);
+        rec.plane(1 + pl, b, g)[(long)((cy >> 1) + y) * Wc + (cx >> 1) + x] =
+            (uint8_t)clip_pixel((int)L.predC[pl][y * 16 + x] + ((o[r] + 2048) >> 12));
+      }
+    }
   }
 }
 

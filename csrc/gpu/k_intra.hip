@@ -11,6 +11,7 @@
 #include "k_encode.h"
 #include "tb_coder.h"
 #include "wave_tb.h"
+#include "tv/me_model.h"
 
 namespace tv {
 namespace gpu {
@@ -54,9 +55,9 @@ __global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSe
   __shared__ int16_t refs[21][4][65];  // left, top, smoothed left, smoothed top
   __shared__ bool avl[21][2][65];
   __shared__ int dcv[21];
-  __shared__ unsigned best[21];
+  __shared__ unsigned best[21], best_ang[21];
   for (int i = tid; i < 1024; i += 256) sblk[i] = S[(cy + (i >> 5)) * g.W + cx + (i & 31)];
-  if (tid < 21) best[tid] = 0xffffffffu;
+  if (tid < 21) best[tid] = best_ang[tid] = 0xffffffffu;
   for (int e = tid; e < 469; e += 256) {
     int bi, i, bx, by, l2;
     ref_entry(e, bi, i);
@@ -102,18 +103,9 @@ __global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSe
   }
   __syncthreads();
   const int wave = tid >> 6, lane = tid & 63;
-  for (int t = wave; t < 735; t += 4) {
-    int bi, mode;
-    if (t < 560) {
-      bi = t / 35;
-      mode = t % 35;
-    } else if (t < 700) {
-      bi = 16 + (t - 560) / 35;
-      mode = (t - 560) % 35;
-    } else {
-      bi = 20;
-      mode = t - 700;
-    }
+  // one wave per (block, mode); stage 1 = the 11 coarse modes of every block, stage 2 = the
+  // +-1 / +-2 neighbours of each block's best stage-1 angular mode (tv/me_model.h)
+  auto eval = [&](int bi, int mode, bool coarse) {
     int bx, by, l2;
     blk_geom(bi, bx, by, l2);
     const int N = 1 << l2, nq = N >> 3;
@@ -126,8 +118,18 @@ __global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSe
       const int p = intra_pred_pixel(L, T, l2, mode, N < 32, dcv[bi], qx, qy);
       sum += wave_satd8x8((int)sblk[(by + qy) * 32 + bx + qx] - p);
     }
-    const unsigned cost = (unsigned)(sum + (mode <= 1 ? pen.mode_dcpl : pen.mode_ang));
-    if (lane == 0) atomicMin(&best[bi], (cost << 6) | (unsigned)mode);
+    const unsigned v = ((unsigned)(sum + (mode <= 1 ? pen.mode_dcpl : pen.mode_ang)) << 6) | (unsigned)mode;
+    if (lane == 0) {
+      atomicMin(&best[bi], v);
+      // only stage 1 moves the refinement centre: stage-2 waves read it concurrently
+      if (coarse && mode >= 2) atomicMin(&best_ang[bi], v);
+    }
+  };
+  for (int t = wave; t < 21 * kIntraCoarseModes; t += 4) eval(t / kIntraCoarseModes, intra_coarse_mode(t % kIntraCoarseModes), true);
+  __syncthreads();
+  for (int t = wave; t < 21 * 4; t += 4) {
+    const int bi = t >> 2, m = intra_refine_mode((int)(best_ang[bi] & 63), t & 3);
+    if (m >= 2) eval(bi, m, false);
   }
   __syncthreads();
   if (tid == 0) {
