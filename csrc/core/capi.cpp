@@ -171,6 +171,19 @@ void tv_decoder_free(void* d) { delete static_cast<HevcDecoder*>(d); }
 int tv_decoder_decode(void* d, const uint8_t* data, size_t n) {
   return guard([&] { static_cast<HevcDecoder*>(d)->decode(data, n); });
 }
+int tv_decoder_decode_range(void* d, const uint8_t* data, size_t n, int first, int count) {
+  return guard([&] { static_cast<HevcDecoder*>(d)->decode_range(data, n, first, count); });
+}
+// header-only probe: geometry + picture count, no slice decoding
+int tv_hevc_probe(const uint8_t* data, size_t n, int* w, int* h, int* pictures, int* idrs) {
+  return guard([&] {
+    const StreamInfo s = probe_annexb(data, n);
+    *w = s.width;
+    *h = s.height;
+    *pictures = s.pictures;
+    *idrs = s.idrs;
+  });
+}
 void tv_decoder_info(void* d, int* w, int* h, int* cw, int* ch, int* nframes) {
   auto* D = static_cast<HevcDecoder*>(d);
   *w = D->width;

@@ -5,6 +5,7 @@
 // encoder is checked by decoding every produced stream with this independent parser and
 // requiring decoded == encoder reconstruction, bit for bit.  It is also the probe used by
 // the stitch stage for the `dest_*` job fields (reference worker/tasks.py:2225-2274).
+#include <climits>
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -573,13 +574,59 @@ class SliceDecoder {
 
 }  // namespace
 
-void HevcDecoder::decode(const uint8_t* data, size_t n) {
+StreamInfo probe_annexb(const uint8_t* data, size_t n) {
+  StreamInfo info;
+  for (const auto& nal : split_annexb(data, n)) {
+    if (nal.size < 3) continue;
+    const int type = nal.type();
+    if (type == NAL_SPS) {
+      std::vector<uint8_t> rbsp = unescape_rbsp(nal.data + 2, nal.size - 2);
+      BitReader br(rbsp.data(), rbsp.size());
+      const Sps sps = parse_sps(br);
+      info.width = sps.width;
+      info.height = sps.height;
+      info.coded_w = sps.coded_w;
+      info.coded_h = sps.coded_h;
+    } else if (type <= 21 && (nal.data[2] & 0x80)) {  // first_slice_segment_in_pic_flag
+      ++info.pictures;
+      if (type == NAL_IDR_W_RADL || type == NAL_IDR_N_LP) ++info.idrs;
+    }
+  }
+  return info;
+}
+
+void HevcDecoder::decode(const uint8_t* data, size_t n) { decode_range(data, n, 0, -1); }
+
+void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int count) {
   Sps sps;
   Pps pps;
   const auto nals = split_annexb(data, n);
+  // picture index of every slice NAL and the last IDR at or before `first`
+  int start_pic = 0;
+  {
+    int k = 0;
+    for (const auto& nal : nals) {
+      if (nal.size < 3) continue;
+      const int t = nal.type();
+      if (t > 21 || !(nal.data[2] & 0x80)) continue;
+      if ((t == NAL_IDR_W_RADL || t == NAL_IDR_N_LP) && k <= first) start_pic = k;
+      ++k;
+    }
+  }
+  const int end_pic = count < 0 ? INT_MAX : first + count;
+  Picture ref_pic;
+  bool have_ref = false;
+  int pic = -1;
   for (const auto& nal : nals) {
     if (nal.size < 2) continue;
     const int type = nal.type();
+    if (type <= 21 && nal.size >= 3 && (nal.data[2] & 0x80)) {
+      ++pic;
+      if (pic < start_pic) continue;
+      if (pic >= end_pic) break;
+    } else if (type <= 21 && (pic < start_pic || pic >= end_pic)) {
+      continue;
+    }
     std::vector<uint8_t> rbsp = unescape_rbsp(nal.data + 2, nal.size - 2);
     BitReader br(rbsp.data(), rbsp.size());
     if (type == NAL_VPS || type == NAL_AUD || type >= 36) continue;
@@ -631,15 +678,17 @@ void HevcDecoder::decode(const uint8_t* data, size_t n) {
     dp.pic.alloc(sps.coded_w, sps.coded_h);
     const Picture* ref = nullptr;
     if (!islice) {
-      if (pictures.empty()) fail("P slice without a decoded reference");
-      ref = &pictures.back().pic;
+      if (!have_ref) fail("P slice without a decoded reference");
+      ref = &ref_pic;
     }
     last_decisions.alloc(sps.coded_w, sps.coded_h);
     SliceDecoder sd(sps, pps, islice, qp, max_merge, &br, &dp.pic, ref, &last_decisions, sao);
     sd.run();
     if (pps.deblock) deblock_picture(dp.pic, last_decisions.view(), qp);
     if (sao) sao_picture(dp.pic, last_decisions.sao.data());
-    pictures.push_back(std::move(dp));
+    ref_pic = dp.pic;
+    have_ref = true;
+    if (pic >= first) pictures.push_back(std::move(dp));
   }
 }
 

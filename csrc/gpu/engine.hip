@@ -539,8 +539,8 @@ class Engine {
   }
 
   // Encode nseg segments of the synthetic source: segment b = frames [starts[b], +gop).
-  void encode_synth(const int* starts, int nseg) {
-    run(nseg, cfg_.gop, [&](Core& core, int b0, int f, int B) {
+  void encode_synth(const int* starts, int nseg, int nframes) {
+    run(nseg, nframes, [&](Core& core, int b0, int f, int B) {
       FrameIdx fi{};
       for (int b = 0; b < B; ++b) fi.t[b] = starts[b0 + b] + f;
       launch_synth(core.src(), core.geo(), cfg_.seed, fi, B, core.stream());
@@ -675,8 +675,8 @@ void* tv_engine_new(int width, int height, int qp, int batch, int gop, int range
   return r;
 }
 void tv_engine_free(void* e) { delete static_cast<tv::gpu::Engine*>(e); }
-int tv_engine_encode_synth(void* e, const int* starts, int nseg) {
-  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_synth(starts, nseg); });
+int tv_engine_encode_synth(void* e, const int* starts, int nseg, int nframes) {
+  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_synth(starts, nseg, nframes); });
 }
 int tv_engine_encode_host(void* e, const uint8_t* frames, int nseg, int nframes) {
   return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_host(frames, nseg, nframes); });

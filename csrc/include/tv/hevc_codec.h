@@ -219,6 +219,10 @@ class HevcDecoder {
   // Decode a complete Annex-B elementary stream.  Throws std::runtime_error on syntax
   // violations of the supported subset.
   void decode(const uint8_t* data, size_t n);
+  // Decode only pictures [first, first + count) (decode order == output order here): parsing
+  // starts at the last IDR at or before `first`, earlier pictures are skipped without
+  // decoding and only the requested ones are kept (random access into a long stream).
+  void decode_range(const uint8_t* data, size_t n, int first, int count);
   std::vector<DecodedPicture> pictures;
   int width = 0, height = 0;          // conformance-cropped size
   int coded_w = 0, coded_h = 0;
@@ -228,6 +232,13 @@ class HevcDecoder {
  private:
   struct Impl;
 };
+
+// Header-only probe of an Annex-B stream: SPS geometry and the picture count (one slice
+// per picture), no slice data decoded.
+struct StreamInfo {
+  int width = 0, height = 0, coded_w = 0, coded_h = 0, pictures = 0, idrs = 0;
+};
+StreamInfo probe_annexb(const uint8_t* data, size_t n);
 
 // ------------------------------------- containers ---------------------------------------
 // Build an ISO-BMFF (.mp4, 'hvc1') file from an Annex-B HEVC stream.  Returns bytes.

@@ -88,3 +88,26 @@ def test_sao_roundtrip_and_gain(qp, deblock):
                 np.testing.assert_array_equal(r[p], c[p])
         res[sao] = np.mean([hevc.psnr(a[0], b[0]) for a, b in zip(frames, d.frames)])
     assert res[True] >= res[False] - 0.01
+
+
+def test_range_decode_and_header_probe_stream_long_inputs(tmp_path):
+    """A source HEVC/MP4 is probed from headers only and read by range from the preceding
+    IDR (verdict r1: HevcSource decoded whole files into RAM)."""
+    from thinvids_amd.models import media
+
+    frames = [hevc.synth_frame(2, t, 96, 64) for t in range(12)]
+    bs, _ = hevc.encode_sequence_cpu(frames, qp=30, gop=4, search_range=16)
+    info = hevc.probe_annexb(bs)
+    assert info == {"width": 96, "height": 64, "frames": 12, "idrs": 3}
+    full = hevc.decode(bs, coded=False).frames
+    part = hevc.decode(bs, coded=False, first=5, count=4).frames
+    assert len(part) == 4
+    for a, b in zip(full[5:9], part):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    p = tmp_path / "s.mp4"
+    p.write_bytes(hevc.mux_mp4(bs, 96, 64, 25, 1))
+    src = media.HevcSource(str(p))
+    assert (src.width, src.height, src.nframes) == (96, 64, 12)
+    got = src.read(10, 5)
+    assert len(got) == 2 and np.array_equal(got[1][0], full[11][0])

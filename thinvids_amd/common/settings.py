@@ -42,6 +42,13 @@ DEFAULT_SETTINGS: dict[str, str] = {
     "tv_deblock": "1",
     "tv_sao": "1",
     "tv_segment_frames": "0",  # 0 = derive from target_segment_mb
+    "tv_bitrate_kbps": "0",  # tv_rc=2pass|abr target
+    "tv_ladder": "",  # e.g. "2160,1440,1080,720,480": one MP4 per rung (ABR fan-out)
+    # node executor (one rank per GPU, RCCL data plane) — used when one is alive
+    "tv_node_executor": "1",
+    "tv_node_segment_frames": "256",
+    "tv_node_mode": "direct",  # direct (each rank reads its range) | scatter (rank 0 -> xGMI)
+    "tv_node_batch": "8",  # segments claimed per rank per batched launch
 }
 
 _cache = {"ts": 0.0, "data": {}}

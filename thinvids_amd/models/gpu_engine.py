@@ -25,7 +25,7 @@ def _lib():
         lib.tv_engine_new.argtypes = [C.c_int] * 7 + [C.c_uint32, C.c_int, C.c_int, C.c_int]
         lib.tv_engine_free.argtypes = [vp]
         lib.tv_engine_encode_synth.restype = C.c_int
-        lib.tv_engine_encode_synth.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
+        lib.tv_engine_encode_synth.argtypes = [vp, C.POINTER(C.c_int), C.c_int, C.c_int]
         lib.tv_engine_encode_host.restype = C.c_int
         lib.tv_engine_encode_host.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int]
         lib.tv_engine_encode_device.restype = C.c_int
@@ -67,6 +67,7 @@ class GpuEngine:
         self.cw, self.ch = coded_size(width, height)
         self.threads = threads or default_threads()
         self.sao = sao
+        self.device = device
         self.h = self.lib.tv_engine_new(width, height, qp, batch, gop, search_range, int(deblock) | (2 if sao else 0),
                                         seed & 0xFFFFFFFF, self.threads, device, max_merge)
         if not self.h:
@@ -83,11 +84,15 @@ class GpuEngine:
         if rc != 0:
             raise RuntimeError(self.lib.tv_gpu_last_error().decode())
 
-    def encode_synthetic(self, starts) -> list[bytes]:
-        """Encode len(starts) segments; segment b = synthetic frames [starts[b], starts[b]+gop)."""
+    def encode_synthetic(self, starts, nframes: int | None = None) -> list[bytes]:
+        """Encode len(starts) segments generated on the GPU; segment b = synthetic frames
+        [starts[b], starts[b] + nframes) (nframes defaults to the GOP)."""
+        n = self.gop if nframes is None else int(nframes)
+        if not 1 <= n <= self.gop or not 1 <= len(starts) <= self.batch:
+            raise ValueError(f"need 1..{self.batch} segments of 1..{self.gop} frames")
         arr = (C.c_int * len(starts))(*[int(s) for s in starts])
-        self._check(self.lib.tv_engine_encode_synth(self.h, arr, len(starts)))
-        self.last_frames = self.gop
+        self._check(self.lib.tv_engine_encode_synth(self.h, arr, len(starts), n))
+        self.last_frames = n
         return [self.segment(b) for b in range(len(starts))]
 
     def encode_frames(self, segments) -> list[bytes]:
@@ -98,14 +103,18 @@ class GpuEngine:
             raise ValueError(f"need 1..{self.batch} segments")
         if not 1 <= n <= self.gop or any(len(s) != n for s in segments):
             raise ValueError(f"segments must all have the same length in 1..{self.gop}")
+        # one pinned upload per segment, edge padding to the coded size on the GPU
+        import torch
+
+        from ..ops import stage
+
+        dev = torch.device("cuda", self.device)
         fsz = self.cw * self.ch * 3 // 2
-        buf = np.empty((len(segments), n, fsz), np.uint8)
+        staging = torch.empty(len(segments) * n * fsz, dtype=torch.uint8, device=dev)
         for b, seg in enumerate(segments):
-            for f, (y, u, v) in enumerate(seg):
-                buf[b, f] = pad_frame(y, u, v, self.cw, self.ch)
-        self._check(self.lib.tv_engine_encode_host(self.h, ptr(buf), len(segments), n))
-        self.last_frames = n
-        return [self.segment(b) for b in range(len(segments))]
+            stage.to_staging(stage.upload_frames(seg, dev), self.width, self.height, staging, b * n)
+        torch.cuda.current_stream(dev).synchronize()
+        return self.encode_device(staging, len(segments), n)
 
     def encode_device(self, frames, nseg: int, nframes: int) -> list[bytes]:
         """frames: a contiguous uint8 CUDA tensor on this engine's GPU laid out
@@ -114,7 +123,7 @@ class GpuEngine:
         fsz = self.cw * self.ch * 3 // 2
         if not 1 <= nseg <= self.batch or not 1 <= nframes <= self.gop:
             raise ValueError(f"need 1..{self.batch} segments of 1..{self.gop} frames")
-        if not frames.is_cuda or not frames.is_contiguous() or frames.numel() < nseg * nframes * fsz:
+        if not frames.is_cuda or not frames.is_contiguous() or frames.numel() * frames.element_size() < nseg * nframes * fsz:
             raise ValueError("frames must be a contiguous CUDA tensor of nseg*nframes coded-size I420 frames")
         self._check(self.lib.tv_engine_encode_device(self.h, C.c_void_p(frames.data_ptr()), nseg, nframes))
         self.last_frames = nframes

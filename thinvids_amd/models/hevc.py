@@ -105,13 +105,30 @@ class DecodedStream:
     coded_frames: list  # coded-size (Y, U, V)
 
 
-def decode(annexb: bytes, coded: bool = True) -> DecodedStream:
-    """Decode an Annex-B HEVC stream with the native decoder oracle."""
+def probe_annexb(annexb: bytes) -> dict:
+    """Header-only probe (SPS geometry, picture and IDR counts): nothing is decoded."""
     lib = core_lib()
+    if not getattr(lib, "_probe_sig", False):
+        lib.tv_hevc_probe.argtypes = [C.POINTER(C.c_uint8), C.c_size_t] + [C.POINTER(C.c_int)] * 4
+        lib.tv_hevc_probe.restype = C.c_int
+        lib.tv_decoder_decode_range.argtypes = [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t, C.c_int, C.c_int]
+        lib.tv_decoder_decode_range.restype = C.c_int
+        lib._probe_sig = True
+    buf = np.frombuffer(annexb, np.uint8)
+    w, h, n, k = (C.c_int() for _ in range(4))
+    check(lib.tv_hevc_probe(ptr(buf), len(annexb), C.byref(w), C.byref(h), C.byref(n), C.byref(k)))
+    return {"width": w.value, "height": h.value, "frames": n.value, "idrs": k.value}
+
+
+def decode(annexb: bytes, coded: bool = True, first: int = 0, count: int = -1) -> DecodedStream:
+    """Decode an Annex-B HEVC stream with the native decoder oracle; `first`/`count` decode
+    only that picture range (from the nearest preceding IDR)."""
+    lib = core_lib()
+    probe_annexb(b"")  # signatures
     h = lib.tv_decoder_new()
     try:
         buf = np.frombuffer(annexb, np.uint8)
-        check(lib.tv_decoder_decode(h, ptr(np.ascontiguousarray(buf)), len(annexb)))
+        check(lib.tv_decoder_decode_range(h, ptr(buf), len(annexb), int(first), int(count)))
         w, hh, cw, ch, n = (C.c_int() for _ in range(5))
         lib.tv_decoder_info(h, C.byref(w), C.byref(hh), C.byref(cw), C.byref(ch), C.byref(n))
         frames, coded_frames = [], []

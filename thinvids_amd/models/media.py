@@ -3,7 +3,8 @@ SURVEY.md §2.3 K1/K11).
 
 Readable inputs (no ffmpeg in this image, so only formats we can decode ourselves):
 
-* ``.y4m``   — YUV4MPEG2, 8-bit 4:2:0 (raw frames; the realistic ingest format here);
+* ``.y4m``   — YUV4MPEG2 4:2:0, 8-bit or 10-bit (``C420p10``: HDR10 PQ masters; frames
+  come back as uint16 planes and are tone-mapped on the GPU before encoding);
 * ``.synth`` — JSON ``{"width", "height", "frames", "fps", "seed"}``: the procedural source
   of :mod:`thinvids_amd.models.hevc` (P5 "direct source" with zero I/O);
 * ``.hevc`` / ``.265`` / ``.mp4`` produced by this engine (decoded with the oracle decoder).
@@ -35,6 +36,7 @@ class Y4MInfo:
     header_len: int
     frame_bytes: int
     nframes: int
+    bits: int = 8
 
 
 def _y4m_info(path: str) -> Y4MInfo:
@@ -44,6 +46,7 @@ def _y4m_info(path: str) -> Y4MInfo:
             raise ValueError(f"{path}: not a YUV4MPEG2 file")
         w = h = 0
         fn, fd = 30, 1
+        bits = 8
         for tok in header.decode().split()[1:]:
             if tok[0] == "W":
                 w = int(tok[1:])
@@ -52,29 +55,36 @@ def _y4m_info(path: str) -> Y4MInfo:
             elif tok[0] == "F":
                 a, b = tok[1:].split(":")
                 fn, fd = int(a), int(b)
-            elif tok[0] == "C" and not tok[1:].startswith("420"):
-                raise ValueError(f"{path}: only 4:2:0 8-bit Y4M is supported (got {tok})")
+            elif tok[0] == "C":
+                if tok[1:] in ("420p10",):
+                    bits = 10
+                elif not tok[1:].startswith("420") or tok[1:].startswith("420p1"):
+                    raise ValueError(f"{path}: only 4:2:0 8-bit or 10-bit Y4M is supported (got {tok})")
         frame_hdr = f.readline()
         if frame_hdr and not frame_hdr.startswith(b"FRAME"):
             raise ValueError(f"{path}: malformed frame header")
         fhl = len(frame_hdr) if frame_hdr else 6
-    plane = w * h * 3 // 2
+    plane = w * h * 3 // 2 * (2 if bits > 8 else 1)
     size = os.path.getsize(path)
     n = max(0, (size - len(header)) // (fhl + plane))
-    return Y4MInfo(w, h, fn, fd, len(header), fhl + plane, n)
+    return Y4MInfo(w, h, fn, fd, len(header), fhl + plane, n, bits)
 
 
 def write_y4m(path: str, frames, fps_num: int = 30, fps_den: int = 1) -> None:
+    """Write 8-bit (uint8 planes) or 10-bit (uint16 planes, ``C420p10`` little-endian) Y4M."""
     frames = list(frames)
     h, w = frames[0][0].shape
+    ten = frames[0][0].dtype == np.uint16
+    dt = np.dtype("<u2") if ten else np.uint8
     tmp = path + ".tmp"
     with open(tmp, "wb") as f:
-        f.write(f"YUV4MPEG2 W{w} H{h} F{fps_num}:{fps_den} Ip A1:1 C420jpeg\n".encode())
+        f.write(f"YUV4MPEG2 W{w} H{h} F{fps_num}:{fps_den} Ip A1:1 {'C420p10 XYSCSS=420P10' if ten else 'C420jpeg'}\n"
+                .encode())
         for y, u, v in frames:
             f.write(b"FRAME\n")
-            f.write(np.ascontiguousarray(y, np.uint8).tobytes())
-            f.write(np.ascontiguousarray(u, np.uint8).tobytes())
-            f.write(np.ascontiguousarray(v, np.uint8).tobytes())
+            f.write(np.ascontiguousarray(y, dt).tobytes())
+            f.write(np.ascontiguousarray(u, dt).tobytes())
+            f.write(np.ascontiguousarray(v, dt).tobytes())
     os.replace(tmp, path)
 
 
@@ -87,18 +97,22 @@ class Y4MSource:
         self.width, self.height = self.info.width, self.info.height
         self.fps_num, self.fps_den = self.info.fps_num, self.info.fps_den
         self.nframes = self.info.nframes
+        self.bits = self.info.bits
 
     def read(self, start: int, n: int):
+        """Frames [start, start + n) read straight from their byte range (random access:
+        nothing before `start` is touched, so a long file streams segment by segment)."""
         out = []
         i = self.info
         n = max(0, min(n, self.nframes - start))
         ysz, csz = i.width * i.height, i.width * i.height // 4
+        dt = np.dtype("<u2") if i.bits > 8 else np.uint8
         with open(self.path, "rb") as f:
             f.seek(i.header_len + start * i.frame_bytes)
             for _ in range(n):
                 raw = f.read(i.frame_bytes)
                 hdr = raw.index(b"\n") + 1
-                buf = np.frombuffer(raw, np.uint8, offset=hdr)
+                buf = np.frombuffer(raw, dt, offset=hdr)
                 y = buf[:ysz].reshape(i.height, i.width)
                 u = buf[ysz:ysz + csz].reshape(i.height // 2, i.width // 2)
                 v = buf[ysz + csz:ysz + 2 * csz].reshape(i.height // 2, i.width // 2)
@@ -135,6 +149,9 @@ def write_synth_spec(path: str, width: int, height: int, frames: int, fps=30, se
 
 # ----------------------------------------------------------------------------- HEVC
 class HevcSource:
+    """Our own HEVC elementary stream / MP4 output as a source.  Only the header is parsed
+    up front (geometry, picture count); ``read`` decodes just the requested range from the
+    preceding IDR, so a long file is never decoded (or held decoded) as a whole."""
     kind = "hevc"
 
     def __init__(self, path: str):
@@ -149,12 +166,16 @@ class HevcSource:
             if ts and d:
                 fr = Fraction(ts, d).limit_denominator(1001)
                 self.fps_num, self.fps_den = fr.numerator, fr.denominator
-        self._dec = hevc.decode(data, coded=False)
-        self.width, self.height = self._dec.width, self._dec.height
-        self.nframes = len(self._dec.frames)
+        self._annexb = data
+        info = hevc.probe_annexb(data)
+        self.width, self.height = info["width"], info["height"]
+        self.nframes = info["frames"]
 
     def read(self, start: int, n: int):
-        return list(self._dec.frames[start:start + n])
+        n = max(0, min(n, self.nframes - start))
+        if n == 0:
+            return []
+        return list(hevc.decode(self._annexb, coded=False, first=start, count=n).frames)
 
 
 def open_source(path: str):
@@ -186,6 +207,7 @@ def probe(path: str) -> dict:
         "frames": src.nframes,
         "duration": round(dur, 3),
         "size": size,
+        "bits": int(getattr(src, "bits", 8)),
         "bitrate_kbps": round(size * 8 / dur / 1000.0, 1) if dur else 0.0,
         "streams": [{"index": 0, "codec_type": "video", "codec_name": codec, "width": src.width,
                      "height": src.height}],

@@ -178,6 +178,11 @@ class WorkQueue:
     def retry_done(self) -> None:
         self._add("inflight", -1)
 
+    def fail_all(self, why: str) -> None:
+        """Raise the job-wide abort flag (cooperative halt: every rank stops claiming)."""
+        self.store.set(self._k("abort_msg"), why)
+        self._add("abort")
+
     def finished(self) -> bool:
         if self._add("done", 0) < self.world:
             return False
@@ -233,30 +238,47 @@ class Checkpoint:
             os.replace(tmp, path)
 
 
-def _encode_many(items: list, spec_for, cache) -> dict:
-    """items: [(key, frames, spec)] -> {key: annexb}; batched per spec on the engine."""
-    from ..worker.encoder import encode_parts
+class JobHooks:
+    """Callbacks a node job reports through (the node executor binds them to the job hash:
+    progress counters, heartbeat, cooperative halt — reference worker/tasks.py:1694-1733,
+    :392-394).  The default does nothing."""
 
-    out, groups = {}, {}
-    for key, frames, spec in items:
-        groups.setdefault(spec, []).append((key, frames))
+    def segment_done(self, frames: int) -> None:
+        pass
+
+    def halted(self) -> bool:
+        return False
+
+
+def _encode_many(items: list, cache) -> tuple[dict, dict]:
+    """items: [(key, part, spec)] -> ({key: annexb}, {key: PartStats}); batched per spec on
+    the engine (a part may be host frames, device frames or a synthetic range)."""
+    from ..worker.encoder import PartStats, encode_parts
+
+    out, st, groups = {}, {}, {}
+    for key, part, spec in items:
+        groups.setdefault(spec, []).append((key, part))
     for spec, grp in groups.items():
-        for k, b in zip([g[0] for g in grp], encode_parts([g[1] for g in grp], spec, cache)):
+        stats = [PartStats() for _ in grp]
+        for (k, _), b, ps in zip(grp, encode_parts([g[1] for g in grp], spec, cache, stats), stats):
             out[k] = b
-    return out
+            st[k] = ps
+    return out, st
 
 
 def run_job(input_path: str, output: str, height: int | None = None, qp: int = 27, gop: int = 64,
             segment_frames: int = 256, mode: str = "direct", bitrate_kbps: float = 0.0, ladder=None,
             search_range: int = 64, software: bool = False, batch_segments: int = 8,
-            resume_dir: str | None = None, max_retries: int = 3) -> dict:
+            resume_dir: str | None = None, max_retries: int = 3, hooks: JobHooks | None = None,
+            deblock: bool = True, sao: bool = False, cache=None) -> dict:
     import torch
 
     from ..models import hevc, media
-    from ..worker.encoder import EncodeSpec, EngineCache, gpu_available, prepare_frames
+    from ..worker.encoder import EncodeSpec, EngineCache, PartStats, SynthRange, gpu_available, psnr_from_sse
     from ..worker.helpers import output_geometry
     from .comm import allreduce_stats, gather_bytes_to_root, scatter_frames_from_root
 
+    hooks = hooks or JobHooks()
     dist = _dist()
     world = dist.get_world_size() if dist else 1
     rank = dist.get_rank() if dist else 0
@@ -268,31 +290,47 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     rungs = [output_geometry(w0, h0, th) for th in heights]
     segs = plan_segments(nfr, segment_frames, gop)
     software = software or not gpu_available()
+    synthetic = isinstance(src, media.SynthSource)
+    if getattr(src, "bits", 8) != 8 and mode == "scatter":
+        mode = "direct"  # 10-bit sources: every rank reads its own range
     # one engine per rung stays resident (a 5-rung ladder thrashed the default 4-engine cache:
     # every eviction re-allocates an engine's HBM and streams)
-    cache = None if software else EngineCache(device=dev.index or 0, batch=batch_segments,
-                                              max_engines=max(4, len(rungs)))
+    own_cache = cache is None and not software
+    if own_cache:
+        cache = EngineCache(device=dev.index or 0, batch=min(64, batch_segments * max(1, -(-segment_frames // gop))),
+                            max_engines=max(4, len(rungs)))
     jobs = [(r, i) for r in range(len(rungs)) for i in range(len(segs))]  # ladder fan-out (P10)
     st = os.stat(input_path) if os.path.exists(input_path) else None
     ckpt = Checkpoint(resume_dir, Checkpoint.fingerprint(
         src=os.path.abspath(input_path), size=st.st_size if st else 0, mtime=st.st_mtime_ns if st else 0,
-        rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software))
+        rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software,
+        deblock=deblock, sao=sao))
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
+    quality: dict = {}  # (r, i) -> PartStats of segments encoded here
 
     def spec(r, q):
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=int(q), gop=gop, search_range=search_range,
-                          software=software)
+                          software=software, deblock=deblock, sao=sao, seed=getattr(src, "seed", 1))
 
     def load(i):
+        """Segment i's source: a synthetic range (generated where it is encoded), or host
+        frames uploaded to this GPU once for all rungs."""
         s, n = segs[i]
         stats["reads"] += 1
-        return src.read(s, n)
+        if synthetic:
+            return SynthRange(src.seed, w0, h0, src.start + s, n)
+        frames = src.read(s, n)
+        if software:
+            return frames
+        from ..ops import stage
+
+        return stage.upload_frames(frames, dev)
 
     def encode_segments(seg_ids, qps, source_of) -> dict:
         """Work item = one segment with ALL its rungs: the source range is read (or received)
-        once, every rung is prepared from it, the source is dropped, and each rung engine then
-        encodes the claimed segments in one batched launch."""
-        out, todo = {}, []
+        once, every rung is staged from it on the device, and each rung engine then encodes
+        the claimed segments in one batched launch."""
+        out, todo, keep = {}, [], []
         for i in seg_ids:
             need = []
             for r in range(len(rungs)):
@@ -304,24 +342,31 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     need.append(r)
             if need:
                 with trace.span("node_job.load"):
-                    raw = source_of(i)
-                    todo.extend(((r, i), prepare_frames(raw, *rungs[r]), spec(r, qps[r][i])) for r in need)
-                    del raw  # peak host memory: one source segment at a time
+                    part = source_of(i)
+                todo.extend(((r, i), part, spec(r, qps[r][i])) for r in need)
+                keep.append(part)
         if todo:
             with trace.span("node_job.encode", segments=len(todo)):
-                got = _encode_many(todo, None, cache)
+                got, qual = _encode_many(todo, cache)
             for (r, i), b in got.items():
                 ckpt.save(r, i, int(qps[r][i]), b)
                 out[(r, i)] = b
+                quality[(r, i)] = qual[(r, i)]
                 stats["encoded"] += 1
+        del keep  # device / host source copies of this claim are released here
+        for i in seg_ids:
+            hooks.segment_done(segs[i][1])
         return out
 
     def encode_pass(qps) -> dict:
         mine = {}
         if mode == "scatter" and world > 1:
-            # round-robin rounds: rank 0 reads `world` segments and sends one to each rank
+            # rounds: rank 0 reads `world` segments and sends each rank its segment over one
+            # xGMI hop; the received tensor stays on the device (no host bounce)
             fsz = w0 * h0 * 3 // 2
             for base in range(0, len(segs), world):
+                if hooks.halted():
+                    raise RuntimeError("job halted")
                 rnd = list(range(base, min(len(segs), base + world)))
                 n_max = max(segs[i][1] for i in rnd)
                 shape = (n_max, fsz)
@@ -331,16 +376,24 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     for k in range(world):
                         buf = np.zeros(shape, np.uint8)
                         if k < len(rnd):
-                            for f, (y, u, v) in enumerate(load(rnd[k])):
+                            for f, (y, u, v) in enumerate(src.read(*segs[rnd[k]])):
                                 buf[f] = np.concatenate([y.ravel(), u.ravel(), v.ravel()])
+                            stats["reads"] += 1
                         payload.append(buf)
-                got = scatter_frames_from_root(payload, shape, dev).cpu().numpy()
+                got = scatter_frames_from_root(payload, shape, dev)
                 if rank < len(rnd):
                     i = rnd[rank]
-                    ysz, csz = w0 * h0, w0 * h0 // 4
-                    frames = [(x[:ysz].reshape(h0, w0), x[ysz:ysz + csz].reshape(h0 // 2, w0 // 2),
-                               x[ysz + csz:].reshape(h0 // 2, w0 // 2)) for x in got[:segs[i][1]]]
-                    mine.update(encode_segments([i], qps, lambda _i: frames))
+                    n = segs[i][1]
+                    if got.is_cuda and not software:
+                        from ..ops import stage
+
+                        part = stage.from_flat(got, w0, h0, n)
+                    else:
+                        g = got.cpu().numpy()
+                        ysz, csz = w0 * h0, w0 * h0 // 4
+                        part = [(x[:ysz].reshape(h0, w0), x[ysz:ysz + csz].reshape(h0 // 2, w0 // 2),
+                                 x[ysz + csz:].reshape(h0 // 2, w0 // 2)) for x in g[:n]]
+                    mine.update(encode_segments([i], qps, lambda _i, p=part: p))
         else:
             wq = WorkQueue(f"pass{encode_pass.calls}", list(range(len(segs))), world, max_retries)
             fault.check("rank", rank)  # TV_FAULT=rank:<r>:hang|die|fail (tests)
@@ -365,6 +418,9 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 msg = wq.aborted()
                 if msg:
                     raise RuntimeError(msg)
+                if hooks.halted():
+                    wq.fail_all("job halted")
+                    raise RuntimeError("job halted")
                 claimed = wq.claim(batch_segments)  # a batch -> one batched launch per rung
                 if not claimed:
                     break
@@ -392,14 +448,29 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         return mine
 
     encode_pass.calls = 0
+    cdev = dev if dev.type == "cuda" else torch.device("cpu")
+
+    def agreed_pass(q):
+        """encode_pass + a collective verdict: a rank that failed (halt, abort, engine
+        error) never strands its peers inside the next collective."""
+        err, got = None, {}
+        try:
+            got = encode_pass(q)
+        except Exception as e:  # noqa: BLE001 - re-raised below on every rank
+            err = e
+        failed = allreduce_stats([1.0 if err else 0.0], cdev, op="max")[0]
+        if failed:
+            raise err if err is not None else RuntimeError("a peer rank failed this job")
+        return got
+
     base = [[qp] * len(segs) for _ in rungs]
     passes = 1
     if bitrate_kbps > 0:
-        first = encode_pass(base)
+        first = agreed_pass(base)
         sizes = np.zeros(len(jobs))
         for (r, i), b in first.items():
             sizes[jobs.index((r, i))] = len(b) * 8
-        sizes = allreduce_stats(sizes, dev if dev.type == "cuda" else torch.device("cpu"))  # RC stats all-reduce
+        sizes = allreduce_stats(sizes, cdev)  # RC stats all-reduce
         fps = src.fps_num / src.fps_den
         qps = []
         for r in range(len(rungs)):
@@ -408,15 +479,22 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             target = bitrate_kbps * 1000 * nfr / fps * scale
             qps.append(list(qp_plan_two_pass(sizes[idx], [n for _, n in segs], qp, target)))
         passes = 2
+        quality.clear()
     else:
         qps = base
-    mine = encode_pass(qps)
+    mine = agreed_pass(qps)
+    t_enc = time.time() - t0
+    # quality: per-rung frames + SSE of the segments encoded on this rank, all-reduced
+    qv = np.zeros((len(rungs), 4))
+    for (r, i), ps in quality.items():
+        qv[r] += [ps.frames, *ps.sse]
+    qv = allreduce_stats(qv.reshape(-1), cdev).reshape(len(rungs), 4)
     # gather bitstreams to rank 0 (one message per rank: json index + concatenated bytes)
     keys = sorted(mine)
     header = json.dumps({"seg": [[r, i, len(mine[(r, i)])] for r, i in keys], "stats": stats}).encode()
     blob = len(header).to_bytes(8, "little") + header + b"".join(mine[k] for k in keys)
     with trace.span("node_job.gather"):
-        parts = gather_bytes_to_root(blob, dev) if world > 1 else [blob]
+        parts = gather_bytes_to_root(blob, cdev) if world > 1 else [blob]
     result = {"world": world, "segments": len(segs), "rungs": [list(x) for x in rungs], "passes": passes}
     if rank == 0:
         streams: dict = {}
@@ -443,11 +521,16 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             with open(tmp, "wb") as f:
                 f.write(data)
             os.replace(tmp, path)
+            q = psnr_from_sse(qv[r, 1:], ow * oh * qv[r, 0]) if qv[r, 0] else {}
             outs.append({"path": path, "bytes": len(data), "width": ow, "height": oh,
-                         "kbps": len(annexb) * 8 / (nfr * src.fps_den / src.fps_num) / 1000})
+                         "kbps": len(annexb) * 8 / (nfr * src.fps_den / src.fps_num) / 1000,
+                         "psnr_y": round(q["y"], 3) if q else None, "psnr_yuv": round(q["yuv"], 3) if q else None,
+                         "quality_frames": int(qv[r, 0])})
+        el = time.time() - t0
         result.update(trace=trace.summary(), per_rank=per_rank, outputs=outs, qp_plan=[[int(q) for q in row] for row in qps],
-                      seconds=round(time.time() - t0, 3), fps=round(nfr * len(rungs) / (time.time() - t0), 2))
-    if cache:
+                      seconds=round(el, 3), encode_seconds=round(t_enc, 3),
+                      fps=round(nfr * len(rungs) / el, 2), encode_fps=round(nfr * len(rungs) * passes / max(t_enc, 1e-9), 2))
+    if own_cache:
         cache.close()
     return result
 

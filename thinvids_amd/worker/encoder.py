@@ -1,12 +1,18 @@
-"""Segment encoder used by the worker's ``encode`` task (replaces the reference's ffmpeg
-VA-API / libx264 invocation, worker/tasks.py:1532-1651).
+"""Segment encoder used by the worker's ``encode`` task and the node executor (replaces the
+reference's ffmpeg VA-API / libx264 invocation, worker/tasks.py:1532-1651).
 
 MI355X-first shape: a *part* (a run of frames, possibly many GOPs) is cut into closed GOP
-chunks; the chunks of every part handed to one call — typically several parts pulled as
-one batch by the per-GPU encode consumer — are packed into batched engine launches of up
-to ``engine_batch`` chunks of equal length, so the GPU always sees B segments at once.
-Every chunk starts with an IDR + parameter sets, so a part's bitstream is the plain
-concatenation of its chunks.
+chunks; the chunks of every part handed to one call — several parts pulled as one batch
+by the per-GPU encode consumer, or a node rank's claimed segments — are packed into
+batched engine launches of up to ``engine_batch`` chunks of equal length, so the GPU
+always sees B segments at once.  Every chunk starts with an IDR + parameter sets, so a
+part's bitstream is the plain concatenation of its chunks.
+
+GPU path (no host bounce): a part's frames reach the device once (pinned upload, an RCCL
+receive or on-device synthesis) and are tone-mapped / resized / edge-padded by HIP kernels
+straight into the engine's staging buffer (:mod:`thinvids_amd.ops.stage`), then encoded
+with ``GpuEngine.encode_device``.  A synthetic part at the engine's own size is generated
+inside the engine (``encode_synthetic``: zero copies).
 
 ``software=True`` selects the C++ reference encoder on the CPU (the reference's per-job
 ``software_encode`` path, libx264 there).
@@ -35,21 +41,60 @@ class EncodeSpec:
     deblock: bool = True
     sao: bool = False
     software: bool = False
+    seed: int = 1  # synthetic sources generated inside the engine
 
     def engine_key(self):
-        return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao)
+        return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed)
+
+
+@dataclass(frozen=True)
+class SynthRange:
+    """Frames [t0, t0 + n) of the seeded synthetic source (w x h): generated on the GPU
+    where they are encoded (no scatter, no I/O)."""
+    seed: int
+    width: int
+    height: int
+    t0: int
+    n: int
+
+    def __len__(self):
+        return self.n
+
+    def host_frames(self) -> list:
+        return [hevc.synth_frame(self.seed, self.t0 + k, self.width, self.height) for k in range(self.n)]
+
+
+@dataclass
+class PartStats:
+    """Per part: frames encoded and summed SSE (Y, U, V) of the reconstruction vs the
+    encoder input (the job's per-part PSNR)."""
+    frames: int = 0
+    sse: tuple = (0.0, 0.0, 0.0)
+
+    def add(self, frames: int, sse) -> None:
+        self.frames += frames
+        self.sse = tuple(a + float(b) for a, b in zip(self.sse, sse))
+
+
+def psnr_from_sse(sse, npx_luma: float) -> dict:
+    f = lambda s, n: float("inf") if s <= 0 else float(10 * np.log10(255.0 ** 2 * n / s))
+    y, u, v = f(sse[0], npx_luma), f(sse[1], npx_luma / 4), f(sse[2], npx_luma / 4)
+    return {"y": y, "u": u, "v": v, "yuv": (6 * y + u + v) / 8}
 
 
 class EngineCache:
     """Per-process GPU engines keyed by stream geometry/QP (allocation is HBM-heavy, so an
     engine lives for the life of the consumer).  Thread-safe; one engine serialises its
-    own calls."""
+    own calls.  Each engine owns a device staging buffer (batch x GOP coded frames).
+    ``batch=0`` sizes each engine for its resolution (segments in flight that fill 256 CUs,
+    measured: 48 at <= 1080p, 24 at 4K; profiles/README.md)."""
 
     def __init__(self, device: int = 0, batch: int = 8, max_engines: int = 4):
         self.device, self.batch, self.max_engines = device, batch, max_engines
         self._engines: dict = {}
         self._order: list = []
         self._lock = threading.Lock()
+        self.constructed = 0
 
     def get(self, spec: EncodeSpec):
         from ..models.gpu_engine import GpuEngine
@@ -61,12 +106,14 @@ class EngineCache:
                 while len(self._order) >= self.max_engines:
                     old = self._order.pop(0)
                     self._engines.pop(old).close()
-                eng = GpuEngine(spec.width, spec.height, qp=spec.qp, batch=self.batch, gop=spec.gop,
+                eng = GpuEngine(spec.width, spec.height, qp=spec.qp, batch=self.batch or auto_batch(spec), gop=spec.gop,
                                 search_range=spec.search_range, deblock=spec.deblock, sao=spec.sao,
-                                device=self.device)
+                                seed=spec.seed, device=self.device)
                 eng.lock = threading.Lock()
+                eng.staging = None
                 self._engines[key] = eng
                 self._order.append(key)
+                self.constructed += 1
             return eng
 
     def close(self):
@@ -75,6 +122,11 @@ class EngineCache:
                 e.close()
             self._engines.clear()
             self._order.clear()
+
+
+def auto_batch(spec: EncodeSpec) -> int:
+    px = spec.width * spec.height
+    return 48 if px <= 1920 * 1088 else (24 if px <= 3840 * 2176 else 8)
 
 
 _default_cache: EngineCache | None = None
@@ -106,42 +158,128 @@ def chunk_plan(nframes: int, gop: int) -> list[tuple[int, int]]:
     return [(s, min(gop, nframes - s)) for s in range(0, nframes, gop)]
 
 
-def encode_parts(parts: list[list], spec: EncodeSpec, cache: EngineCache | None = None) -> list[bytes]:
-    """Encode several parts (lists of (Y, U, V) frames at spec size); returns one Annex-B
-    bitstream per part."""
+def _nframes(part) -> int:
+    return part.n if hasattr(part, "n") else len(part)
+
+
+def _slice(part, s: int, n: int):
+    if isinstance(part, SynthRange):
+        return SynthRange(part.seed, part.width, part.height, part.t0 + s, n)
+    if hasattr(part, "select"):  # DevFrames
+        return part.select(s, n)
+    return part[s:s + n]
+
+
+def _host_frames(part) -> list:
+    if isinstance(part, SynthRange):
+        return part.host_frames()
+    if hasattr(part, "select"):  # DevFrames -> host (software path only)
+        flat = part.buf.reshape(-1).cpu().numpy()
+        out = []
+        for k in range(part.n):
+            pl = []
+            for off, pw, ph, st, fs in part.planes:
+                o = off + k * fs
+                pl.append(np.lib.stride_tricks.as_strided(flat[o:], (ph, pw), (st * flat.itemsize, flat.itemsize)).copy())
+            out.append(tuple(pl))
+        return out
+    return part
+
+
+def encode_parts(parts: list, spec: EncodeSpec, cache: EngineCache | None = None,
+                 stats: list | None = None) -> list[bytes]:
+    """Encode several parts into one Annex-B bitstream each.  A part is a list of host
+    (Y, U, V) frames (any size: resized to the spec), a :class:`~thinvids_amd.ops.stage.DevFrames`
+    already on this GPU, or a :class:`SynthRange`.  `stats` (optional list of
+    :class:`PartStats`, one per part) receives frames and reconstruction SSE."""
     if spec.software or not gpu_available():
         if not spec.software:
             raise RuntimeError("no GPU available for a hardware encode (set software_encode for the CPU path)")
-        return [hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock,
-                                           sao=spec.sao)[0]
-                for frames in parts]
-    eng = (cache or default_cache()).get(spec)
-    # (part, chunk index, frames) grouped by chunk length
+        return [_encode_cpu(_host_frames(p), spec, stats[i] if stats else None) for i, p in enumerate(parts)]
+    return _encode_gpu(parts, spec, cache or default_cache(), stats)
+
+
+def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None) -> bytes:
+    h, w = frames[0][0].shape
+    if (w, h) != (spec.width, spec.height) or frames[0][0].dtype != np.uint8:
+        frames = prepare_frames(frames, spec.width, spec.height)
+    bs, recons = hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock, sao=spec.sao,
+                                          search_range=spec.search_range)
+    if st is not None:
+        sse = np.zeros(3)
+        for f, r in zip(frames, recons):
+            for c in range(3):
+                hh, ww = f[c].shape
+                d = f[c].astype(np.int64) - r[c][:hh, :ww].astype(np.int64)
+                sse[c] += float((d * d).sum())
+        st.add(len(frames), sse)
+    return bs
+
+
+def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats) -> list[bytes]:
+    import torch
+
+    from ..ops import stage
+
+    eng = cache.get(spec)
+    dev = torch.device("cuda", cache.device)
+    # host parts go to the device once (one pinned H2D each)
+    dparts = [p if (isinstance(p, SynthRange) or hasattr(p, "select")) else stage.upload_frames(p, dev)
+              for p in parts]
     chunks: dict[int, list] = {}
     out: list[list] = []
-    for p, frames in enumerate(parts):
-        plan = chunk_plan(len(frames), spec.gop)
+    for pi, p in enumerate(dparts):
+        plan = chunk_plan(_nframes(p), spec.gop)
         out.append([b""] * len(plan))
         for c, (s, n) in enumerate(plan):
-            chunks.setdefault(n, []).append((p, c, frames[s:s + n]))
+            chunks.setdefault(n, []).append((pi, c, _slice(p, s, n)))
+    fsz, _ = stage.staging_planes(spec.width, spec.height)
+    own_size = (spec.width, spec.height)
     with eng.lock:
         for n, items in chunks.items():
             for i in range(0, len(items), eng.batch):
                 grp = items[i:i + eng.batch]
-                bits = eng.encode_frames([fr for _, _, fr in grp])
-                for (p, c, _), b in zip(grp, bits):
-                    out[p][c] = b
+                srcs = [x[2] for x in grp]
+                if all(isinstance(s, SynthRange) and s.seed == spec.seed and (s.width, s.height) == own_size
+                       for s in srcs):
+                    bits = eng.encode_synthetic([s.t0 for s in srcs], nframes=n)
+                else:
+                    need = eng.batch * spec.gop * fsz
+                    if eng.staging is None or eng.staging.numel() < need:
+                        eng.staging = torch.empty(need, dtype=torch.uint8, device=dev)
+                    for j, s in enumerate(srcs):
+                        if isinstance(s, SynthRange):
+                            s = stage.synth_frames(s.seed, s.width, s.height, range(s.t0, s.t0 + s.n), dev)
+                        stage.to_staging(s, spec.width, spec.height, eng.staging, j * n)
+                    torch.cuda.current_stream(dev).synchronize()
+                    bits = eng.encode_device(eng.staging, len(grp), n)
+                for j, ((pi, c, _), b) in enumerate(zip(grp, bits)):
+                    out[pi][c] = b
+                    if stats is not None:
+                        stats[pi].add(n, eng.sse(j))
     return [b"".join(x) for x in out]
+
+
+def _tonemap_planar_ref(y, u, v):
+    """Host tone-map of a 10-bit planar PQ frame (values 0..1023) via the P010 reference."""
+    from ..ops.color import tonemap_pq_ref
+
+    y16 = (y.astype(np.uint16) << 6)
+    uv16 = np.stack([u.astype(np.uint16) << 6, v.astype(np.uint16) << 6], -1).reshape(u.shape[0], -1)
+    return tonemap_pq_ref(y16, uv16)
 
 
 def prepare_frames(frames: list, out_w: int, out_h: int, device: str | None = None,
                    deinterlace: bool = False) -> list:
     """Optional bwdif deinterlace, then Lanczos resize of a list of I420 frames to
-    out_w x out_h (identity when already there).  On a GPU host both HIP kernels run on the
-    device and each frame crosses PCIe once each way."""
+    out_w x out_h (identity when already there); 10-bit PQ frames are tone-mapped first.
+    The worker's deinterlace path and the software encoder use this; the GPU job path
+    stages on the device instead (:mod:`thinvids_amd.ops.stage`)."""
     if not frames:
         return frames
     h, w = frames[0][0].shape
+    if frames[0][0].dtype == np.uint16:
+        frames = [_tonemap_planar_ref(*f) for f in frames]
     if (w, h) == (out_w, out_h) and not deinterlace:
         return frames
     from ..ops.deint import bwdif_frame

@@ -110,6 +110,15 @@ def transcode(job_id: str, run_token: str | None = None):
     if not task_token_is_current(job_id, run_token, "transcode") or is_job_halted(job_id):
         return None
     job = _job(job_id)
+    host = _node_executor_for(job)
+    if host:
+        # one node, N GPU ranks, RCCL data plane: the node executor runs the whole job
+        from .node_executor import submit
+
+        _set(job_id, processing_mode_effective="node", node_executor_host=host, waiting_node_at=now())
+        job_heartbeat(job_id, "transcode", force=True)
+        submit(job_id, run_token, host)
+        return {"status": "QUEUED_NODE", "host": host}
     reset_job_run_state(job_id, job)
     _set(job_id, status=Status.RUNNING.value, started_at=job.get("started_at") or now())
     job_heartbeat(job_id, "transcode", force=True)
@@ -118,6 +127,20 @@ def transcode(job_id: str, run_token: str | None = None):
     stitch(job_id, run_token)
     split(job_id, run_token)
     return {"status": "DISPATCHED"}
+
+
+def _node_executor_for(job: dict) -> str | None:
+    """A live node executor takes the job unless the job / policy pins the classic
+    split|direct pipeline or the setting `tv_node_executor` is off."""
+    from ..common import as_bool, get_settings
+
+    if not as_bool(get_settings().get("tv_node_executor"), True):
+        return None
+    if str(job.get("processing_mode") or "").lower() in ("split", "direct"):
+        return None
+    from .node_executor import live_executor
+
+    return live_executor(prefer=get_config().worker_name)
 
 
 # =========================================================================  split
