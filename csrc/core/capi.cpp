@@ -210,6 +210,10 @@ int tv_decoder_frame(void* d, int idx, int cropped, uint8_t* y, uint8_t* u, uint
 int tv_mux_mp4(const uint8_t* annexb, size_t n, int w, int h, int fps_num, int fps_den, void* out) {
   return guard([&] { static_cast<Bytes*>(out)->v = mux_mp4(annexb, n, w, h, fps_num, fps_den); });
 }
+int tv_mux_mp4_file(const uint8_t* const* segs, const size_t* sizes, int nseg, int w, int h, int fps_num, int fps_den,
+                    const char* path, unsigned long long* out_size) {
+  return guard([&] { *out_size = mux_mp4_file(segs, sizes, nseg, w, h, fps_num, fps_den, path); });
+}
 int tv_demux_mp4(const uint8_t* mp4, size_t n, int* w, int* h, int* nframes, int* timescale,
                  int* delta, void* out) {
   return guard([&] { static_cast<Bytes*>(out)->v = demux_mp4(mp4, n, w, h, nframes, timescale, delta); });

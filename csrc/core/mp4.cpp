@@ -4,6 +4,7 @@
 // (reference worker/tasks.py:2047-2069): the concatenated Annex-B segments become 'hvc1'
 // samples (length-prefixed NAL units, parameter sets hoisted into hvcC), moov placed
 // before mdat (faststart layout).
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -62,56 +63,65 @@ void matrix(Box& o) {
   for (uint32_t v : m) o.u32(v);
 }
 
+// One sample = references to its NAL units (in-band parameter sets first when they change
+// between segments) — the payload is never copied until it is written.
 struct Sample {
-  std::vector<uint8_t> data;  // length-prefixed NALs
+  std::vector<NalView> nals;
+  uint32_t size = 0;  // length-prefixed bytes
   bool sync = false;
 };
 
-}  // namespace
-
-std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int height, int fps_num,
-                             int fps_den) {
-  const auto nals = split_annexb(annexb, n);
+struct MuxPlan {
   std::vector<uint8_t> vps, sps, pps;
   bool ps_consistent = true;
   std::vector<Sample> samples;
+  uint64_t mdat_payload = 0;
+};
+
+// Scan the Annex-B segments (in order) into samples; no payload bytes are copied.
+MuxPlan plan_mux(const uint8_t* const* segs, const size_t* sizes, int nseg) {
+  MuxPlan P;
   std::vector<NalView> pending_ps;
-  for (const auto& nal : nals) {
-    const int t = nal.type();
-    std::vector<uint8_t> bytes(nal.data, nal.data + nal.size);
-    if (t == NAL_VPS || t == NAL_SPS || t == NAL_PPS) {
-      auto& slot = t == NAL_VPS ? vps : (t == NAL_SPS ? sps : pps);
-      if (slot.empty()) slot = bytes;
-      else if (slot != bytes) ps_consistent = false;
-      pending_ps.push_back(nal);
-      continue;
-    }
-    if (t > 31) continue;  // AUD / SEI etc. dropped
-    Sample s;
-    s.sync = (t >= 16 && t <= 23);
-    if (!ps_consistent) {  // keep parameter sets in-band ('hev1')
-      for (const auto& p : pending_ps) {
-        Box o;
-        o.u32((uint32_t)p.size);
-        o.bytes(p.data, p.size);
-        s.data.insert(s.data.end(), o.b.begin(), o.b.end());
+  for (int k = 0; k < nseg; ++k) {
+    for (const auto& nal : split_annexb(segs[k], sizes[k])) {
+      const int t = nal.type();
+      if (t == NAL_VPS || t == NAL_SPS || t == NAL_PPS) {
+        auto& slot = t == NAL_VPS ? P.vps : (t == NAL_SPS ? P.sps : P.pps);
+        const std::vector<uint8_t> bytes(nal.data, nal.data + nal.size);
+        if (slot.empty()) slot = bytes;
+        else if (slot != bytes) P.ps_consistent = false;
+        pending_ps.push_back(nal);
+        continue;
       }
+      if (t > 31) continue;  // AUD / SEI etc. dropped
+      Sample s;
+      s.sync = (t >= 16 && t <= 23);
+      s.nals = pending_ps;  // kept only if the parameter sets turn out inconsistent
+      s.nals.push_back(nal);
+      pending_ps.clear();
+      P.samples.push_back(std::move(s));
     }
-    pending_ps.clear();
-    Box o;
-    o.u32((uint32_t)nal.size);
-    o.bytes(nal.data, nal.size);
-    s.data.insert(s.data.end(), o.b.begin(), o.b.end());
-    samples.push_back(std::move(s));
   }
-  if (sps.empty() || pps.empty() || vps.empty()) throw std::runtime_error("mux_mp4: missing parameter sets");
+  if (P.sps.empty() || P.pps.empty() || P.vps.empty()) throw std::runtime_error("mux_mp4: missing parameter sets");
+  for (auto& s : P.samples) {
+    if (P.ps_consistent) s.nals.erase(s.nals.begin(), s.nals.end() - 1);  // parameter sets live in hvcC
+    s.size = 0;
+    for (const auto& n : s.nals) s.size += 4 + (uint32_t)n.size;
+    P.mdat_payload += s.size;
+  }
+  return P;
+}
+
+// ftyp + moov (faststart) + the mdat header, for a plan whose payload follows directly
+std::vector<uint8_t> mp4_header(const MuxPlan& P, int width, int height, int fps_num, int fps_den) {
+  const auto& samples = P.samples;
   const uint32_t timescale = (uint32_t)fps_num * 1000u;
   const uint32_t delta = (uint32_t)fps_den * 1000u;
   const uint64_t dur_media = (uint64_t)samples.size() * delta;
   const uint64_t dur_ms = dur_media * 1000 / timescale;
 
   // hvcC from the SPS profile_tier_level
-  std::vector<uint8_t> sps_rbsp = unescape_rbsp(sps.data() + 2, sps.size() - 2);
+  std::vector<uint8_t> sps_rbsp = unescape_rbsp(P.sps.data() + 2, P.sps.size() - 2);
   if (sps_rbsp.size() < 13) throw std::runtime_error("mux_mp4: short SPS");
   Box hv;
   hv.u8(1);
@@ -124,7 +134,7 @@ std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int hei
   hv.u16(0);
   hv.u8((0u << 6) | (1u << 3) | (1u << 2) | 3u);
   hv.u8(3);
-  for (const auto* ps : {&vps, &sps, &pps}) {
+  for (const auto* ps : {&P.vps, &P.sps, &P.pps}) {
     hv.u8(0x80 | (((*ps)[0] >> 1) & 0x3f));
     hv.u16(1);
     hv.u16((uint32_t)ps->size());
@@ -150,7 +160,7 @@ std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int hei
   se.u16(0x0018);
   se.u16(0xffff);
   se.bytes(box("hvcC", hv.b));
-  const auto entry = box(ps_consistent ? "hvc1" : "hev1", se.b);
+  const auto entry = box(P.ps_consistent ? "hvc1" : "hev1", se.b);
   Box stsd;
   stsd.u32(1);
   stsd.bytes(entry);
@@ -174,11 +184,8 @@ std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int hei
   Box stsz;
   stsz.u32(0);
   stsz.u32((uint32_t)samples.size());
-  uint64_t mdat_payload = 0;
-  for (const auto& s : samples) {
-    stsz.u32((uint32_t)s.data.size());
-    mdat_payload += s.data.size();
-  }
+  for (const auto& s : samples) stsz.u32(s.size);
+  const uint64_t mdat_payload = P.mdat_payload;
   const bool large = mdat_payload + (1 << 20) > 0xffffffffull;
   auto build_moov = [&](uint64_t chunk_off) {
     Box co;
@@ -191,7 +198,6 @@ std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int hei
                                        fullbox(large ? "co64" : "stco", 0, 0, co.b)}));
     Box vmhd;
     vmhd.zeros(8);
-    Box urlb;
     Box dref;
     dref.u32(1);
     dref.bytes(fullbox("url ", 0, 1, {}));
@@ -259,8 +265,59 @@ std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int hei
     mh.str("mdat", 4);
   }
   out.insert(out.end(), mh.b.begin(), mh.b.end());
-  for (const auto& s : samples) out.insert(out.end(), s.data.begin(), s.data.end());
   return out;
+}
+
+void put_len(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 24);
+  p[1] = (uint8_t)(v >> 16);
+  p[2] = (uint8_t)(v >> 8);
+  p[3] = (uint8_t)v;
+}
+
+}  // namespace
+
+std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int height, int fps_num,
+                             int fps_den) {
+  const MuxPlan P = plan_mux(&annexb, &n, 1);
+  std::vector<uint8_t> out = mp4_header(P, width, height, fps_num, fps_den);
+  size_t o = out.size();
+  out.resize(o + P.mdat_payload);
+  for (const auto& s : P.samples)
+    for (const auto& nal : s.nals) {
+      put_len(out.data() + o, (uint32_t)nal.size);
+      std::memcpy(out.data() + o + 4, nal.data, nal.size);
+      o += 4 + nal.size;
+    }
+  return out;
+}
+
+uint64_t mux_mp4_file(const uint8_t* const* segs, const size_t* sizes, int nseg, int width, int height, int fps_num,
+                      int fps_den, const char* path) {
+  const MuxPlan P = plan_mux(segs, sizes, nseg);
+  const std::vector<uint8_t> head = mp4_header(P, width, height, fps_num, fps_den);
+  FILE* f = std::fopen(path, "wb");
+  if (!f) throw std::runtime_error(std::string("mux_mp4_file: cannot open ") + path);
+  std::vector<uint8_t> buf;
+  buf.reserve(8 << 20);
+  bool ok = std::fwrite(head.data(), 1, head.size(), f) == head.size();
+  auto flush = [&] {
+    ok = ok && std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+    buf.clear();
+  };
+  for (const auto& s : P.samples) {
+    for (const auto& nal : s.nals) {
+      uint8_t len[4];
+      put_len(len, (uint32_t)nal.size);
+      buf.insert(buf.end(), len, len + 4);
+      buf.insert(buf.end(), nal.data, nal.data + nal.size);
+    }
+    if (buf.size() >= (8u << 20)) flush();
+  }
+  flush();
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok) throw std::runtime_error(std::string("mux_mp4_file: write failed: ") + path);
+  return head.size() + P.mdat_payload;
 }
 
 // ------------------------------------- demux --------------------------------------------

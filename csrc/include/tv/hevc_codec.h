@@ -244,6 +244,11 @@ StreamInfo probe_annexb(const uint8_t* data, size_t n);
 // Build an ISO-BMFF (.mp4, 'hvc1') file from an Annex-B HEVC stream.  Returns bytes.
 std::vector<uint8_t> mux_mp4(const uint8_t* annexb, size_t n, int width, int height,
                              int fps_num, int fps_den);
+// Stream the concatenation of Annex-B segments straight into a faststart MP4 file (the
+// sample tables come from a scan of the segments; payload is written once, never copied
+// into one big buffer).  Returns the file size.
+uint64_t mux_mp4_file(const uint8_t* const* segs, const size_t* sizes, int nseg, int width, int height, int fps_num,
+                      int fps_den, const char* path);
 // Parse an mp4 produced by mux_mp4 back to Annex-B (probe / round trip).
 std::vector<uint8_t> demux_mp4(const uint8_t* mp4, size_t n, int* width, int* height,
                                int* nframes, int* timescale, int* sample_delta);

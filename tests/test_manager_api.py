@@ -224,3 +224,15 @@ def test_policy_and_wol(mgr):
     assert len(pkt) == 102 and pkt[:6] == b"\xff" * 6 and pkt[6:12] == bytes.fromhex("aabbccddeeff")
     ok, msg = core.reboot_one_node("localhost")
     assert not ok and "manager" in msg
+
+
+def test_unreadable_container_is_rejected_up_front(mgr):
+    """A container the engine cannot demux (.mkv: no ffmpeg here) is REJECTED at add_job
+    with the probe reason, never dispatched to fail later."""
+    c, st, root = mgr["c"], mgr["st"], mgr["root"]
+    (root / "watch" / "film.mkv").write_bytes(b"\x1aE\xdf\xa3" + b"\0" * 64)
+    r = c.post("/add_job", json={"filename": "film.mkv"})
+    assert r.status_code in (200, 201), r.get_data(as_text=True)
+    job = st.hgetall(f"job:{r.get_json()['job_id']}")
+    assert job["status"] == "REJECTED" and job["rejected_reason"] == "probe_failed"
+    assert "unsupported" in job["error"]

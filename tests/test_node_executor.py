@@ -120,7 +120,8 @@ def test_transcode_without_executor_uses_split_pipeline(node_env):
     node_env["store"].set("node:executor:other", "{}", ex=15)
     node_env["store"].sadd("node:executors", "other")
     assert _node_executor_for({"processing_mode": "auto"}) == "other"
-    assert _node_executor_for({"processing_mode": "split"}) is None
+    assert _node_executor_for({"processing_mode": "split"}) == "other"  # the policy default
+    assert _node_executor_for({"node_executor": "0"}) is None
 
 
 @pytest.mark.gpu
@@ -205,3 +206,32 @@ def test_add_job_end_to_end_on_gpu_node_executor(node_env, monkeypatch):
     assert len(dec.frames) == 96
     ps = np.mean([hevc.psnr_yuv(a, b)["y"] for a, b in zip(frames, dec.frames)])
     assert abs(ps - float(job["psnr_y"])) < 0.6
+
+
+def test_run_job_twice_in_one_process_group(tmp_path, monkeypatch):
+    """A long-lived executor runs many jobs in one process group: work-queue keys in the
+    rendezvous store must not leak from one job into the next."""
+    import torch.multiprocessing as mp
+
+    from thinvids_amd.parallel.launch import free_port
+
+    frames = [hevc.synth_frame(4, t, 96, 64) for t in range(24)]
+    src = tmp_path / "a.y4m"
+    media.write_y4m(str(src), frames, 25, 1)
+    mp.spawn(_twice_worker, args=(2, free_port(), str(src), str(tmp_path)), nprocs=2, join=True)
+    for k in (0, 1):
+        with open(tmp_path / f"o{k}.mp4", "rb") as f:
+            assert len(hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False).frames) == 24
+
+
+def _twice_worker(rank, world, port, src, out_dir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), TV_FORCE_CPU="1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from thinvids_amd.parallel.node_job import run_job
+
+    for k in (0, 1):
+        run_job(src, os.path.join(out_dir, f"o{k}.mp4"), gop=8, segment_frames=8, software=True, batch_segments=1)
+    dist.destroy_process_group()

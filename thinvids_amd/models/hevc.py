@@ -194,6 +194,24 @@ def mux_mp4(annexb: bytes, width: int, height: int, fps_num: int = 30, fps_den: 
     return out.tobytes()
 
 
+def mux_mp4_file(segments, width: int, height: int, fps_num: int, fps_den: int, path: str) -> int:
+    """Write the concatenation of Annex-B segments as a faststart MP4 at `path`, streaming
+    the payload from the segment buffers (no joined copy).  Returns the file size."""
+    lib = core_lib()
+    if not getattr(lib, "_muxf_sig", False):
+        lib.tv_mux_mp4_file.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_int, C.c_int, C.c_int,
+                                        C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_ulonglong)]
+        lib.tv_mux_mp4_file.restype = C.c_int
+        lib._muxf_sig = True
+    segs = [s for s in segments if len(s)]
+    keep = [np.frombuffer(s, np.uint8) for s in segs]
+    ptrs = (C.c_void_p * len(keep))(*[k.ctypes.data for k in keep])
+    sizes = (C.c_size_t * len(keep))(*[len(k) for k in keep])
+    out = C.c_ulonglong()
+    check(lib.tv_mux_mp4_file(ptrs, sizes, len(keep), width, height, fps_num, fps_den, path.encode(), C.byref(out)))
+    return int(out.value)
+
+
 def demux_mp4(data: bytes) -> dict:
     lib = core_lib()
     out = Bytes()

@@ -238,6 +238,9 @@ class Checkpoint:
             os.replace(tmp, path)
 
 
+_job_seq = [0]  # run_job calls in this process (identical on every rank: SPMD)
+
+
 class JobHooks:
     """Callbacks a node job reports through (the node executor binds them to the job hash:
     progress counters, heartbeat, cooperative halt — reference worker/tasks.py:1694-1733,
@@ -279,6 +282,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     from .comm import allreduce_stats, gather_bytes_to_root, scatter_frames_from_root
 
     hooks = hooks or JobHooks()
+    _job_seq[0] += 1
+    job_tag = f"j{_job_seq[0]}"  # rendezvous-store keys of this job (a long-lived executor runs many)
     dist = _dist()
     world = dist.get_world_size() if dist else 1
     rank = dist.get_rank() if dist else 0
@@ -395,7 +400,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                                  x[ysz + csz:].reshape(h0 // 2, w0 // 2)) for x in g[:n]]
                     mine.update(encode_segments([i], qps, lambda _i, p=part: p))
         else:
-            wq = WorkQueue(f"pass{encode_pass.calls}", list(range(len(segs))), world, max_retries)
+            wq = WorkQueue(f"{job_tag}_pass{encode_pass.calls}", list(range(len(segs))), world, max_retries)
             fault.check("rank", rank)  # TV_FAULT=rank:<r>:hang|die|fail (tests)
 
             def run(batch):
@@ -500,8 +505,9 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         streams: dict = {}
         per_rank = []
         for p in parts:
+            p = memoryview(p)
             hl = int.from_bytes(p[:8], "little")
-            hdr = json.loads(p[8:8 + hl])
+            hdr = json.loads(bytes(p[8:8 + hl]))
             idx = hdr["seg"]
             per_rank.append(hdr["stats"])
             off = 8 + hl
@@ -513,17 +519,16 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             raise RuntimeError(f"segments missing at stitch: {missing}")
         outs = []
         for r, (ow, oh) in enumerate(rungs):
-            annexb = b"".join(streams[(r, i)] for i in range(len(segs)))
+            seg_bits = [streams[(r, i)] for i in range(len(segs))]
             path = output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4"
-            with trace.span("node_job.mux"):
-                data = hevc.mux_mp4(annexb, ow, oh, src.fps_num, src.fps_den)
             tmp = path + ".tmp"
-            with open(tmp, "wb") as f:
-                f.write(data)
+            with trace.span("node_job.mux"):  # streamed from the gathered buffers, no joined copy
+                nbytes = hevc.mux_mp4_file(seg_bits, ow, oh, src.fps_num, src.fps_den, tmp)
             os.replace(tmp, path)
             q = psnr_from_sse(qv[r, 1:], ow * oh * qv[r, 0]) if qv[r, 0] else {}
-            outs.append({"path": path, "bytes": len(data), "width": ow, "height": oh,
-                         "kbps": len(annexb) * 8 / (nfr * src.fps_den / src.fps_num) / 1000,
+            outs.append({"path": path, "bytes": nbytes, "width": ow, "height": oh, "frames": nfr,
+                         "fps_num": src.fps_num, "fps_den": src.fps_den,
+                         "kbps": sum(len(b) for b in seg_bits) * 8 / (nfr * src.fps_den / src.fps_num) / 1000,
                          "psnr_y": round(q["y"], 3) if q else None, "psnr_yuv": round(q["yuv"], 3) if q else None,
                          "quality_frames": int(qv[r, 0])})
         el = time.time() - t0

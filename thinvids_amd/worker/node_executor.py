@@ -189,8 +189,6 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
 def _publish(job_id: str, spec: dict, res: dict) -> None:
     """Stitch rank: move the muxed output(s) into the library, probe them, write dest_* and
     the per-job throughput / quality fields, mark DONE (reference stitch :2225-2307)."""
-    from ..models import media
-
     st = get_store()
     job = spec["job"]
     t_comb = now()
@@ -212,14 +210,15 @@ def _publish(job_id: str, spec: dict, res: dict) -> None:
               "qp_plan_json": json.dumps(res.get("qp_plan", [])[:1]), "ladder_outputs_json": json.dumps(
                   [{"path": f, "width": o["width"], "height": o["height"], "kbps": round(o["kbps"], 1),
                     "psnr_y": o.get("psnr_y")} for f, o in zip(finals, outs)]) if len(outs) > 1 else ""}
-    try:
-        d = media.probe(finals[0])
-        fields.update(dest_file_size=d["size"], dest_duration=f"{d['duration']:.2f}", dest_codec=d["codec"],
-                      dest_resolution=d["resolution"], dest_fps=f"{d['fps']:.2f}",
-                      dest_bitrate_kbps=f"{d['bitrate_kbps']:.0f}", english_subtitles_found=0,
-                      english_subtitles_supported=0, english_subtitles_kept=0, subtitle_warning="")
-    except Exception:  # noqa: BLE001 - the output exists; a probe failure is not fatal
-        pass
+    # dest_* from the muxer's own accounting (re-probing a multi-GB output would read it back)
+    o = outs[0]
+    fps = o["fps_num"] / o["fps_den"]
+    dur = o["frames"] / fps if fps else 0.0
+    fields.update(dest_file_size=os.path.getsize(finals[0]), dest_duration=f"{dur:.2f}", dest_codec="hevc",
+                  dest_resolution=f"{o['width']}x{o['height']}", dest_fps=f"{fps:.2f}",
+                  dest_bitrate_kbps=f"{os.path.getsize(finals[0]) * 8 / dur / 1000 if dur else 0:.0f}",
+                  english_subtitles_found=0, english_subtitles_supported=0, english_subtitles_kept=0,
+                  subtitle_warning="")
     st.hset(job_key(job_id), mapping={k: ("" if v is None else v) for k, v in fields.items()})
     st.srem(ACTIVE_JOBS_KEY, job_id)
     shutil.rmtree(spec["base"], ignore_errors=True)

@@ -130,13 +130,12 @@ def transcode(job_id: str, run_token: str | None = None):
 
 
 def _node_executor_for(job: dict) -> str | None:
-    """A live node executor takes the job unless the job / policy pins the classic
-    split|direct pipeline or the setting `tv_node_executor` is off."""
+    """A live node executor takes the job (it subsumes the split and direct modes: every
+    rank reads its own segment range) unless the setting `tv_node_executor` or the job's
+    own `node_executor` field is off."""
     from ..common import as_bool, get_settings
 
-    if not as_bool(get_settings().get("tv_node_executor"), True):
-        return None
-    if str(job.get("processing_mode") or "").lower() in ("split", "direct"):
+    if not as_bool(get_settings().get("tv_node_executor"), True) or not as_bool(job.get("node_executor"), True):
         return None
     from .node_executor import live_executor
 
@@ -424,17 +423,15 @@ def _ready_set(enc_dir: str, total: int, stable_sec: float) -> set:
 def concat_parts(paths: list[str], out_path: str, width: int, height: int, fps_num: int, fps_den: int) -> int:
     """Concatenate encoded MP4 parts (each a run of closed GOPs) into one faststart MP4
     (reference `ffmpeg -f concat -c copy +faststart`, :2047-2120)."""
-    stream = bytearray()
-    for p in paths:
+    segs = []
+    for p in paths:  # each part's elementary stream; the MP4 is streamed from these buffers
         with open(p, "rb") as f:
-            stream += hevc.demux_mp4(f.read())["annexb"]
-    data = hevc.mux_mp4(bytes(stream), width, height, fps_num, fps_den)
+            segs.append(hevc.demux_mp4(f.read())["annexb"])
     tmp = out_path + ".tmp"
     ensure_dirs(os.path.dirname(out_path) or ".")
-    with open(tmp, "wb") as f:
-        f.write(data)
+    n = hevc.mux_mp4_file(segs, width, height, fps_num, fps_den, tmp)
     os.replace(tmp, out_path)
-    return len(data)
+    return n
 
 
 @pipeline_q.task(retries=0)
