@@ -63,6 +63,18 @@ void* tv_cpu_encoder_new(int width, int height, int qp, int deblock, int range, 
   cfg.finalize();
   return new CpuEncoder(cfg, range);
 }
+void* tv_cpu_encoder_new_crf(int width, int height, int qp, int deblock, int range, int max_merge, int crf) {
+  SeqConfig cfg;
+  cfg.width = width;
+  cfg.height = height;
+  cfg.qp = qp;
+  cfg.deblock = (deblock & 1) != 0;
+  cfg.sao = (deblock & 2) != 0;
+  cfg.max_merge_cand = max_merge;
+  cfg.crf = crf;
+  cfg.finalize();
+  return new CpuEncoder(cfg, range);
+}
 void tv_cpu_encoder_free(void* e) { delete static_cast<CpuEncoder*>(e); }
 int tv_cpu_encoder_encode(void* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, int sy,
                           int sc, int idr, int poc, void* out) {
@@ -70,6 +82,15 @@ int tv_cpu_encoder_encode(void* e, const uint8_t* y, const uint8_t* u, const uin
     const uint8_t* planes[3] = {y, u, v};
     const int strides[3] = {sy, sc, sc};
     static_cast<CpuEncoder*>(e)->encode_frame(planes, strides, idr != 0, poc, static_cast<Bytes*>(out)->v);
+  });
+}
+// same with an explicit slice QP for this frame (rate control)
+int tv_cpu_encoder_encode_qp(void* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, int sy, int sc, int idr,
+                             int poc, int qp, void* out) {
+  return guard([&] {
+    const uint8_t* planes[3] = {y, u, v};
+    const int strides[3] = {sy, sc, sc};
+    static_cast<CpuEncoder*>(e)->encode_frame(planes, strides, idr != 0, poc, static_cast<Bytes*>(out)->v, qp);
   });
 }
 // copy the coded-size reconstruction

@@ -19,6 +19,7 @@
 
 #include "tv/cpu_encoder.h"
 #include "tv/me_model.h"
+#include "tv/rc_model.h"
 
 namespace tv {
 
@@ -393,28 +394,42 @@ CpuEncoder::CpuEncoder(const SeqConfig& cfg, int search_range) : cfg_(cfg), rang
 }
 
 void CpuEncoder::encode_frame(const uint8_t* const planes[3], const int strides[3], bool idr,
-                              int poc, std::vector<uint8_t>& out) {
+                              int poc, std::vector<uint8_t>& out, int qp) {
   pad_source(planes, strides, cfg_.width, cfg_.height, src_);
   dec.alloc(cfg_.coded_w, cfg_.coded_h);
-  if (idr) {
-    write_parameter_sets(cfg_, out);
-    analyze_intra(cfg_, src_, dec);
-    reconstruct_frame(cfg_, src_, nullptr, dec, rec_);
-  } else {
-    std::swap(ref_, rec_);
-    quarter_luma(src_, qcur_);
-    const int wc = cfg_.coded_w / kCtb, hc = cfg_.coded_h / kCtb;
-    std::vector<int16_t> cmv(2 * (size_t)wc * hc);
-    std::vector<int> ccost((size_t)wc * hc);
+  const int wc = cfg_.coded_w / kCtb, hc = cfg_.coded_h / kCtb, qw = cfg_.coded_w / 4;
+  quarter_luma(src_, qcur_);
+  // coarse lookahead: penalties at the sequence QP (the frame QP may depend on its result)
+  std::vector<int16_t> cmv(2 * (size_t)wc * hc);
+  std::vector<int> ccost((size_t)wc * hc);
+  if (!idr) {
     int penmv[64];
     for (int i = 0; i < 64; ++i) penmv[i] = (int)(lambda_sad(cfg_.qp) * i);
     coarse_search(qcur_.data(), qprev_.data(), cfg_.coded_w, cfg_.coded_h, range_, penmv, cmv.data(), ccost.data());
-    analyze_inter(cfg_, src_, ref_, cmv.data(), prev_mv_.data(), range_, dec);
-    reconstruct_frame(cfg_, src_, &ref_, dec, rec_);
   }
-  if (idr) quarter_luma(src_, qcur_);
+  SeqConfig fc = cfg_;  // this frame's QP drives lambda, quantisation, deblocking and SAO
+  if (qp >= 0) {
+    fc.qp = qp;
+  } else if (cfg_.crf > 0) {  // CRF: QP from the lookahead complexity of this frame
+    uint64_t sum = 0;
+    for (int cy = 0; cy < hc; ++cy)
+      for (int cx = 0; cx < wc; ++cx)
+        sum += idr ? rc_block_activity(qcur_.data() + (size_t)(8 * cy) * qw + 8 * cx, qw)
+                   : (uint64_t)ccost[(size_t)cy * wc + cx];
+    fc.qp = rc_crf_qp(cfg_.crf, idr, sum, wc * hc);
+  }
+  if (idr) {
+    write_parameter_sets(cfg_, out);
+    analyze_intra(fc, src_, dec);
+    reconstruct_frame(fc, src_, nullptr, dec, rec_);
+  } else {
+    std::swap(ref_, rec_);
+    analyze_inter(fc, src_, ref_, cmv.data(), prev_mv_.data(), range_, dec);
+    reconstruct_frame(fc, src_, &ref_, dec, rec_);
+  }
   std::swap(qcur_, qprev_);
   prev_mv_ = dec.mv;
+  dec.qp = fc.qp;
   write_slice(cfg_, dec.view(), poc, idr, out);
 }
 

@@ -186,7 +186,7 @@ class SliceWriter {
   SliceWriter(const SeqConfig& cfg, const FrameData& fd, bool islice, BitWriter* bw)
       : cfg_(cfg), fd_(fd), islice_(islice), enc_(bw) {
     skip_.assign((size_t)fd.w8 * fd.h8, 0);
-    ctx_.init(islice ? 0 : 1, cfg.qp);
+    ctx_.init(islice ? 0 : 1, fd.qp >= 0 ? fd.qp : cfg.qp);  // contexts start from SliceQpY
     enc_.start();
   }
 
@@ -692,7 +692,7 @@ size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
     bw.put(0, 1);  // num_ref_idx_active_override_flag
     bw.ue((uint32_t)(5 - cfg.max_merge_cand));  // five_minus_max_num_merge_cand
   }
-  bw.se(0);  // slice_qp_delta
+  bw.se(fd.qp >= 0 ? fd.qp - cfg.qp : 0);  // slice_qp_delta (per-frame rate control)
   // byte_alignment()
   bw.put_bit(1);
   bw.align_zero();

@@ -109,6 +109,7 @@ struct EngineCfg {
   int width, height, qp, batch, gop, range, deblock, threads, device, max_merge;
   uint32_t seed;
   int groups;
+  int crf;  // > 0: in-engine CRF (per-frame QP from the lookahead, tv/rc_model.h)
 };
 
 // One group of segments on its own HIP stream (buffers, pinned slot ring, events).
@@ -130,8 +131,11 @@ class Core {
       HIP_OK(hipMalloc(&f.v, B * g_.csz));
     };
     alloc_set(src_);
-    alloc_set(rec_[0]);
-    alloc_set(rec_[1]);
+    // recon ring: final recon of the previous frame (reference), the frame being
+    // reconstructed, and with SAO a third buffer the in-loop filter writes into (no copy of
+    // the deblocked picture: the three rotate by index)
+    nrec_ = (c.deblock & 2) ? 3 : 2;
+    for (int k = 0; k < nrec_; ++k) alloc_set(rec_[k]);
     HIP_OK(hipMalloc(&coef_y_, B * g_.ysz * sizeof(int16_t)));
     HIP_OK(hipMalloc(&coef_u_, B * g_.csz * sizeof(int16_t)));
     HIP_OK(hipMalloc(&coef_v_, B * g_.csz * sizeof(int16_t)));
@@ -146,13 +150,9 @@ class Core {
     HIP_OK(hipMalloc(&ccost_, B * nctu_ * sizeof(int)));
     cap_ = g_.ysz + 2 * g_.csz;
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
-    if (c.deblock & 2) {  // SAO reads the deblocked picture from a copy
-      HIP_OK(hipMalloc(&deb_.y, B * g_.ysz));
-      HIP_OK(hipMalloc(&deb_.u, B * g_.csz));
-      HIP_OK(hipMalloc(&deb_.v, B * g_.csz));
-    }
     slot_bytes_ = align(B * nctu_ * 12) + align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * nctu_ * 8) +
-                  align(B * nctu_ * 4) + align(B * nctu_ * 4) + align(B * 4) + align(B * cap_ * 2);
+                  align(B * nctu_ * 4) + align(B * nctu_ * 4) + align(B * 4) + align(B) + align(B * cap_ * 2);
+    HIP_OK(hipHostMalloc(&qhost_, (size_t)c.gop * B, hipHostMallocDefault));
     for (int k = 0; k < kSlots; ++k) {
       Slot& s = slots_[k];
       HIP_OK(hipMalloc(&s.dev, slot_bytes_));
@@ -162,13 +162,23 @@ class Core {
     }
     HIP_OK(hipEventCreate(&t0_));
     HIP_OK(hipEventCreate(&t1_));
-    // penalties: identical integer rounding to the CPU reference encoder
-    const double lam = lambda_sad(c.qp);
-    pen_.mode_dcpl = (int)(lam * 2);
-    pen_.mode_ang = (int)(lam * 5);
-    pen_.split_intra = (int)(lam * 3);
-    pen_.split_inter = (int)(lam * 4);
-    for (int i = 0; i < 64; ++i) pen_.mv[i] = (int)(lam * i);
+    // decision constants of every QP (rate control picks the QP per segment and frame on the
+    // device): identical integer rounding to the CPU reference encoder
+    {
+      RcTables t{};
+      for (int q = 0; q < 52; ++q) {
+        const double lam = lambda_sad(q);
+        Penalties& p = t.pen[q];
+        p.mode_dcpl = (int)(lam * 2);
+        p.mode_ang = (int)(lam * 5);
+        p.split_intra = (int)(lam * 3);
+        p.split_inter = (int)(lam * 4);
+        for (int i = 0; i < 64; ++i) p.mv[i] = (int)(lam * i);
+        t.sao_lam16[q] = sao_lambda16(q);
+      }
+      HIP_OK(hipMalloc(&rc_, sizeof(RcTables)));
+      HIP_OK(hipMemcpy(rc_, &t, sizeof(RcTables), hipMemcpyHostToDevice));
+    }
     seq_.width = c.width;
     seq_.height = c.height;
     seq_.qp = c.qp;
@@ -181,7 +191,7 @@ class Core {
   ~Core() {
     (void)hipStreamSynchronize(stream_);
     for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u, rec_[1].v,
-                    deb_.y, deb_.u, deb_.v})
+                    rec_[2].y, rec_[2].u, rec_[2].v})
       (void)hipFree(p);
     (void)hipFree(coef_y_);
     (void)hipFree(coef_u_);
@@ -193,6 +203,8 @@ class Core {
     (void)hipFree(q_[1]);
     (void)hipFree(cmv_);
     (void)hipFree(ccost_);
+    (void)hipFree(rc_);
+    (void)hipHostFree(qhost_);
     for (auto& s : slots_) {
       (void)hipFree(s.dev);
       (void)hipHostFree(s.host);
@@ -208,7 +220,7 @@ class Core {
   long coef_bytes() const { return coef_bytes_; }
   double entropy_ms() const { return entropy_ns_ / 1e6; }
   const Geo& geo() const { return g_; }
-  FrameSet last_recon() const { return rec_[(last_frames_ - 1) & 1]; }
+  FrameSet last_recon() const { return rec_[fin_]; }
   hipStream_t stream() const { return stream_; }
 
  private:
@@ -229,6 +241,7 @@ class Core {
     int *count, *offset, *total;
     int16_t* packed;
     uint32_t* sao;
+    int8_t* qp;
   };
   Parts carve(uint8_t* base) const {
     const long B = cfg_.batch, U = g_.usz;
@@ -251,6 +264,8 @@ class Core {
     q += align(B * 4);
     p.sao = reinterpret_cast<uint32_t*>(q);
     q += align(B * nctu_ * 12);
+    p.qp = reinterpret_cast<int8_t*>(q);
+    q += align(B);
     p.packed = reinterpret_cast<int16_t*>(q);
     p.count = nullptr;  // device count array lives in the scratch below
     return p;
@@ -258,6 +273,7 @@ class Core {
   DecisionSet slot_dec(const Slot& s) const {
     const Parts p = carve(s.dev);
     DecisionSet d;
+    d.qp = p.qp;
     d.cu_log2 = p.cu_log2;
     d.intra = p.intra;
     d.ipm = p.ipm;
@@ -303,6 +319,7 @@ class Core {
     f.sb_packed = p.packed + base * 16;
     f.wc = g_.wc;
     f.sao = seq_.sao ? p.sao + (long)b * nctu_ * 3 : nullptr;
+    f.qp = p.qp[b];
     return f;
   }
 
@@ -321,6 +338,7 @@ class Core {
       HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, head, hipMemcpyDeviceToHost, ws));
     } else {  // partial batch: each plane is laid out for cfg_.batch segments
       HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
+      HIP_OK(hipMemcpyAsync(h.qp, d.qp, B, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
       if (seq_.sao) HIP_OK(hipMemcpyAsync(h.sao, d.sao, B * nctu_ * 12, hipMemcpyDeviceToHost, ws));
       for (uint8_t* const* pl : {&h.cu_log2, &h.intra, &h.ipm, &h.cbf}) {
@@ -344,11 +362,19 @@ class Core {
 
  public:
   // ---- one encode call, split so the Engine can interleave several cores' frames ----
-  void begin(int nseg, int nframes) {
+  // qmap: this core's [nseg][nframes] slice QPs (nullptr: the sequence QP everywhere)
+  void begin(int nseg, int nframes, const int8_t* qmap) {
     if (nseg < 1 || nseg > cfg_.batch) throw std::runtime_error("nseg out of range");
     if (nframes < 1 || nframes > cfg_.gop) throw std::runtime_error("nframes out of range");
     B_ = nseg;
     F_ = nframes;
+    qmap_given_ = qmap != nullptr;
+    for (int f = 0; f < nframes; ++f)
+      for (int b = 0; b < nseg; ++b) {
+        const int q = qmap ? qmap[b * nframes + f] : cfg_.qp;
+        if (q < 0 || q > 51) throw std::runtime_error("slice QP out of range");
+        qhost_[f * nseg + b] = (int8_t)q;
+      }
     last_frames_ = nframes;
     out_.assign(B_, {});
     coef_bytes_ = 0;
@@ -368,8 +394,10 @@ class Core {
     Slot& s = slots_[f % kSlots];
     wait_slot(s);
     const DecisionSet dec = slot_dec(s);
+    HIP_OK(hipMemcpyAsync(dec.qp, qhost_ + f * B, B, hipMemcpyHostToDevice, stream_));  // this frame's QPs
     upload(f, B);
-    FrameSet cur = rec_[f & 1], prev = rec_[(f + 1) & 1];
+    const int cur_i = f == 0 ? 0 : (fin_ + 1) % nrec_;
+    FrameSet cur = rec_[cur_i], prev = rec_[fin_];
     // TV_SYNC_DEBUG=1: synchronise and check after every stage (fault isolation)
     auto stage = [&](const char* name) {
       if (!sync_debug_) return;
@@ -380,23 +408,28 @@ class Core {
     };
     stage("upload");
     launch_quarter(src_, q_[f & 1], g_, B, stream_);  // lookahead plane (next frame's coarse ref)
-    if (f == 0) {
-      launch_intra_frame(src_, cur, dec, g_, cfg_.qp, pen_, B, stream_);
-    } else {
-      // the previous frame's decisions still sit in its slot (reused only kSlots frames later)
-      const MeBuffers me{q_[f & 1], q_[(f + 1) & 1], slot_dec(slots_[(f - 1) % kSlots]).mv, cmv_, ccost_};
-      launch_inter_frame(src_, prev, phase_, cur, dec, g_, cfg_.qp, pen_, cfg_.range, me, B, stream_);
-    }
+    // the previous frame's decisions still sit in its slot (reused only kSlots frames later)
+    const MeBuffers me{q_[f & 1], q_[(f + 1) & 1], f ? slot_dec(slots_[(f - 1) % kSlots]).mv : nullptr, cmv_,
+                       ccost_};
+    if (f > 0) launch_coarse_me(me, g_, rc_, cfg_.qp, cfg_.range, B, stream_);
+    if (cfg_.crf > 0 && !qmap_given_) launch_rc_crf(q_[f & 1], ccost_, dec.qp, g_, cfg_.crf, f == 0, B, stream_);
+    if (f == 0) launch_intra_frame(src_, cur, dec, g_, rc_, B, stream_);
+    else launch_inter_frame(src_, prev, phase_, cur, dec, g_, rc_, cfg_.range, me, B, stream_);
     stage(f == 0 ? "intra" : "inter");
     launch_compact(dec, g_, slot_compact(s), B, stream_);
     stage("compact");
-    if (seq_.deblock) launch_deblock(cur, dec, g_, cfg_.qp, B, stream_);
+    if (seq_.deblock) launch_deblock(cur, dec, g_, B, stream_);
     stage("deblock");
-    if (seq_.sao) launch_sao(src_, cur, deb_, carve(s.dev).sao, g_, cfg_.qp, B, stream_);
+    int fin = cur_i;
+    if (seq_.sao) {  // deblocked `cur` -> SAO output in the ring's third buffer
+      fin = f == 0 ? 1 : 3 - cur_i - fin_;  // the ring index neither reference nor current
+      launch_sao(src_, cur, rec_[fin], carve(s.dev).sao, dec.qp, rc_, g_, B, stream_);
+    }
     stage("sao");
-    if (f + 1 < F) launch_phase_planes(cur, phase_, g_, B, stream_);  // reference of f+1
+    fin_ = fin;
+    if (f + 1 < F) launch_phase_planes(rec_[fin], phase_, g_, B, stream_);  // reference of f+1
     stage("phase_planes");
-    launch_sse(src_, cur, g_, d_sse_, B, stream_);
+    launch_sse(src_, rec_[fin], g_, d_sse_, B, stream_);
     stage("sse");
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(s.ev, stream_));
@@ -445,7 +478,7 @@ class Core {
 
   // Single-core encode (groups == 1)
   template <class Upload> void run(int nseg, int nframes, Upload&& upload) {
-    begin(nseg, nframes);
+    begin(nseg, nframes, nullptr);
     for (int f = 0; f < nframes; ++f) issue(f, upload);
     end_record();
     finish();
@@ -478,9 +511,12 @@ class Core {
   EngineCfg cfg_;
   Geo g_;
   SeqConfig seq_;
-  Penalties pen_{};
+  RcTables* rc_ = nullptr;
+  bool qmap_given_ = false;  // an explicit QP map (2-pass plan) overrides in-engine CRF
+  int8_t* qhost_ = nullptr;  // pinned [frame][segment] slice QPs of the current call
   hipStream_t stream_{};
-  FrameSet src_{}, rec_[2]{}, deb_{};
+  FrameSet src_{}, rec_[3]{};
+  int nrec_ = 2, fin_ = 0;  // recon ring size; index of the last finished (reference) picture
   int16_t *coef_y_ = nullptr, *coef_u_ = nullptr, *coef_v_ = nullptr;
   unsigned long long* d_sse_ = nullptr;
   uint8_t* phase_ = nullptr;
@@ -539,8 +575,8 @@ class Engine {
   }
 
   // Encode nseg segments of the synthetic source: segment b = frames [starts[b], +gop).
-  void encode_synth(const int* starts, int nseg, int nframes) {
-    run(nseg, nframes, [&](Core& core, int b0, int f, int B) {
+  void encode_synth(const int* starts, int nseg, int nframes, const int8_t* qmap) {
+    run(nseg, nframes, qmap, [&](Core& core, int b0, int f, int B) {
       FrameIdx fi{};
       for (int b = 0; b < B; ++b) fi.t[b] = starts[b0 + b] + f;
       launch_synth(core.src(), core.geo(), cfg_.seed, fi, B, core.stream());
@@ -549,18 +585,22 @@ class Engine {
 
   // Encode nseg segments of nframes (1..gop) host frames each, coded-size planar I420 laid
   // out [segment][frame][Y | U | V] (planes padded to the coded size by the caller).
-  void encode_host(const uint8_t* frames, int nseg, int nframes) { encode_mem(frames, nseg, nframes); }
+  void encode_host(const uint8_t* frames, int nseg, int nframes, const int8_t* qmap) {
+    encode_mem(frames, nseg, nframes, qmap);
+  }
 
   // Same layout, but the frames already live in device memory on this GPU (produced by
   // the caller's pre-processing kernels, e.g. the ABR ladder's tone-map + Lanczos rungs):
   // device-to-device copies into each group's source planes, no PCIe crossing.  The
   // caller must have finished writing them (its stream synchronised) before the call.
-  void encode_device(const uint8_t* frames, int nseg, int nframes) { encode_mem(frames, nseg, nframes); }
+  void encode_device(const uint8_t* frames, int nseg, int nframes, const int8_t* qmap) {
+    encode_mem(frames, nseg, nframes, qmap);
+  }
 
  private:
   // hipMemcpyDefault: the runtime resolves host (pageable / pinned) vs device pointers.
-  void encode_mem(const uint8_t* frames, int nseg, int nframes) {
-    run(nseg, nframes, [&](Core& core, int b0, int f, int B) {
+  void encode_mem(const uint8_t* frames, int nseg, int nframes, const int8_t* qmap) {
+    run(nseg, nframes, qmap, [&](Core& core, int b0, int f, int B) {
       const Geo& g = core.geo();
       const long fsz = g.ysz + 2 * g.csz;
       const FrameSet src = core.src();
@@ -600,12 +640,14 @@ class Engine {
     if (b < 0 || b / per_ >= used_) throw std::runtime_error("segment index out of range");
     return *cores_[b / per_];
   }
-  template <class Upload> void run(int nseg, int nframes, Upload&& upload) {
+  // qmap: [nseg][nframes] slice QPs (nullptr: the sequence QP)
+  template <class Upload> void run(int nseg, int nframes, const int8_t* qmap, Upload&& upload) {
     if (nseg < 1 || nseg > cfg_.batch) throw std::runtime_error("nseg out of range");
     HIP_OK(hipSetDevice(cfg_.device));  // the calling host thread may be new (ABR rung threads)
     const auto w0 = std::chrono::steady_clock::now();
     used_ = (nseg + per_ - 1) / per_;
-    for (int g = 0; g < used_; ++g) cores_[g]->begin(std::min(per_, nseg - g * per_), nframes);
+    for (int g = 0; g < used_; ++g)
+      cores_[g]->begin(std::min(per_, nseg - g * per_), nframes, qmap ? qmap + (long)g * per_ * nframes : nullptr);
     for (int t = 0; t < nframes + used_ - 1; ++t)
       for (int g = 0; g < used_; ++g) {
         const int f = t - g;
@@ -663,23 +705,25 @@ int tv_gpu_device_count() {
 }
 
 void* tv_engine_new(int width, int height, int qp, int batch, int gop, int range, int deblock,
-                    uint32_t seed, int threads, int device, int max_merge) {
+                    uint32_t seed, int threads, int device, int max_merge, int crf) {
   void* r = nullptr;
   gguard([&] {
     // TV_ENGINE_GROUPS: segment groups on separate streams, one frame apart (default 2)
     const char* ge = getenv("TV_ENGINE_GROUPS");
     const int groups = ge ? std::max(1, atoi(ge)) : (batch >= 2 ? 2 : 1);
-    tv::gpu::EngineCfg c{width, height, qp, batch, gop, range, deblock, threads, device, max_merge, seed, groups};
+    if (crf < 0 || crf > 51) throw std::runtime_error("crf must be 0 (off) or 1..51");
+    tv::gpu::EngineCfg c{width, height, qp, batch, gop, range, deblock, threads, device, max_merge, seed, groups, crf};
     r = new tv::gpu::Engine(c);
   });
   return r;
 }
 void tv_engine_free(void* e) { delete static_cast<tv::gpu::Engine*>(e); }
-int tv_engine_encode_synth(void* e, const int* starts, int nseg, int nframes) {
-  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_synth(starts, nseg, nframes); });
+// qmap (nullable): [nseg][nframes] slice QPs chosen by the caller's rate control
+int tv_engine_encode_synth(void* e, const int* starts, int nseg, int nframes, const int8_t* qmap) {
+  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_synth(starts, nseg, nframes, qmap); });
 }
-int tv_engine_encode_host(void* e, const uint8_t* frames, int nseg, int nframes) {
-  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_host(frames, nseg, nframes); });
+int tv_engine_encode_host(void* e, const uint8_t* frames, int nseg, int nframes, const int8_t* qmap) {
+  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_host(frames, nseg, nframes, qmap); });
 }
 size_t tv_engine_segment_size(void* e, int b) { return static_cast<tv::gpu::Engine*>(e)->segment(b).size(); }
 void tv_engine_segment_copy(void* e, int b, uint8_t* dst) {
@@ -697,8 +741,8 @@ void tv_engine_timing(void* e, double* gpu_ms, double* wall_ms, double* entropy_
   *coef_mb = E->coef_bytes() / 1e6;
 }
 // copy the last frame's coded-size reconstruction of segment b (tests)
-int tv_engine_encode_device(void* e, const uint8_t* dframes, int nseg, int nframes) {
-  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_device(dframes, nseg, nframes); });
+int tv_engine_encode_device(void* e, const uint8_t* dframes, int nseg, int nframes, const int8_t* qmap) {
+  return gguard([&] { static_cast<tv::gpu::Engine*>(e)->encode_device(dframes, nseg, nframes, qmap); });
 }
 int tv_engine_last_recon(void* e, int b, uint8_t* y, uint8_t* u, uint8_t* v) {
   return gguard([&] {

@@ -52,6 +52,7 @@ struct FrameSet {
 };
 
 struct DecisionSet {
+  int8_t* qp;  // [B] slice QP of this frame per segment (rate control)
   uint8_t* cu_log2;
   uint8_t* intra;
   uint8_t* ipm;

@@ -19,11 +19,17 @@ struct Penalties {
   int mode_dcpl, mode_ang, split_intra, split_inter;
   int mv[64];
 };
+// Every QP's decision constants (device-resident, indexed by the per-segment slice QP of
+// the frame being coded: rate control changes QP per segment and frame).
+struct RcTables {
+  Penalties pen[52];
+  long long sao_lam16[52];
+};
 
 void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi, int B, hipStream_t s);
 void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s);
-void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, int qp,
-                        const Penalties& pen, int B, hipStream_t s);
+void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, int B,
+                        hipStream_t s);
 // Hierarchical motion-search state of one P frame (tv/me_model.h): quarter-res source luma
 // of this and the previous frame, the previous frame's MV field (temporal candidate) and the
 // per-CTB coarse field (B x nctu x 2 int16 / B x nctu int).
@@ -35,16 +41,22 @@ struct MeBuffers {
   int* ccost;
 };
 void launch_quarter(FrameSet src, uint8_t* q, const Geo& g, int B, hipStream_t s);
+// quarter-res coarse search of this frame vs the previous (penalties at the sequence QP)
+void launch_coarse_me(const MeBuffers& me, const Geo& g, const RcTables* rc, int seq_qp, int range, int B,
+                      hipStream_t s);
+// CRF: per-segment frame QP from the lookahead complexity into qp[B]
+void launch_rc_crf(const uint8_t* q, const int* ccost, int8_t* qp, const Geo& g, int crf, bool intra, int B,
+                   hipStream_t s);
+// fine motion search + P-frame reconstruction (after launch_coarse_me)
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
-                        const Geo& g, int qp, const Penalties& pen, int range, const MeBuffers& me, int B,
-                        hipStream_t s);
+                        const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s);
 // 16 quarter-pel phase planes (B x 16 x psz bytes) of the luma reference
 void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipStream_t s);
-void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s);
-// SAO: per-CTB statistics (source vs deblocked) + RD decision into `sao` (3 packed words per
-// CTB, B x nctu x 3), then the filter from the deblocked copy `deb` into `rec`.
-void launch_sao(FrameSet src, FrameSet rec, FrameSet deb, uint32_t* sao, const Geo& g, int qp, int B,
-                hipStream_t s);
+void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int B, hipStream_t s);
+// SAO: per-CTB statistics (source vs deblocked `deb`) + RD decision into `sao` (3 packed
+// words per CTB, B x nctu x 3), then the filter from `deb` into `out` (every sample written).
+void launch_sao(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, const int8_t* qp, const RcTables* rc,
+                const Geo& g, int B, hipStream_t s);
 
 // Compact (non-zero 4x4 groups only) level representation for the D2H transfer.
 struct CompactSet {

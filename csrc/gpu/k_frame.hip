@@ -232,8 +232,9 @@ __global__ void __launch_bounds__(256) k_phase_planes(FrameSet ref, uint8_t* pha
 }
 
 // ------------------------------------ deblocking ----------------------------------------
-__global__ void __launch_bounds__(256) k_deblock(FrameSet rec, DecisionSet dec, Geo g, int qp, int horizontal) {
+__global__ void __launch_bounds__(256) k_deblock(FrameSet rec, DecisionSet dec, Geo g, int horizontal) {
   const int b = blockIdx.y;
+  const int qp = dec.qp[b];
   const long ub = b * g.usz;
   const uint8_t* cl = dec.cu_log2 + ub;
   const uint8_t* in = dec.intra + ub;
@@ -292,39 +293,89 @@ void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipS
   k_phase_planes<<<grid, 256, 0, s>>>(ref, phase, g);
 }
 // ---------------------------------------- SAO ------------------------------------------
-// One block per CTB: the three components' statistics are accumulated with LDS atomics
-// (band + 4 EO classes per sample), then one lane runs the shared integer RD decision
-// (tv::sao_decide, identical to the CPU golden model).
+// One block per CTB.  The deblocked CTB of every component plus a one-sample border is
+// staged in LDS (-1 marks samples outside the picture), so the EO neighbour reads never touch
+// global memory.  Statistics without LDS-atomic storms:
+//   * EO: each thread accumulates its samples' 4 classes x 4 categories (count, sum) in
+//     registers; one DPP wave reduction per counter, one LDS add per wave;
+//   * band: per wave, loop over the distinct bands present (ballot + readlane): one wave
+//     reduction and one LDS add per distinct band.
+// Then the shared integer RD decision (tv::sao_decide: identical to the CPU golden model).
+constexpr int kSaoT = 34;   // luma tile side with border
+constexpr int kSaoTc = 18;  // chroma
 __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, uint32_t* sao, Geo g,
-                                                    long long lam16) {
-  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+                                                    const int8_t* qp, const RcTables* rc) {
+  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const long long lam16 = rc->sao_lam16[qp[b]];
   const int cx = ctu % g.wc, cy = ctu / g.wc;
   __shared__ SaoStats st[3];
+  __shared__ int16_t tl[kSaoT * kSaoT];
+  __shared__ int16_t tc[2][kSaoTc * kSaoTc];
   for (int i = tid; i < 3 * (int)(sizeof(SaoStats) / 4); i += 256) reinterpret_cast<int*>(st)[i] = 0;
+  for (int i = tid; i < kSaoT * kSaoT + 2 * kSaoTc * kSaoTc; i += 256) {
+    const int c = i < kSaoT * kSaoT ? 0 : (i < kSaoT * kSaoT + kSaoTc * kSaoTc ? 1 : 2);
+    const int j = c == 0 ? i : i - kSaoT * kSaoT - (c - 1) * kSaoTc * kSaoTc;
+    const int T = c ? kSaoTc : kSaoT, n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
+    const int x = cx * n + j % T - 1, y = cy * n + j / T - 1;
+    const int16_t v = (x < 0 || y < 0 || x >= w || y >= h) ? (int16_t)-1 : (int16_t)deb.plane(c, b, g)[y * w + x];
+    if (c == 0) tl[j] = v;
+    else tc[c - 1][j] = v;
+  }
   __syncthreads();
-  // 1024 luma + 2 x 256 chroma samples: 6 per thread
-  for (int i = tid; i < 1536; i += 256) {
-    const int c = i < 1024 ? 0 : (i < 1280 ? 1 : 2);
-    const int j = c == 0 ? i : (i - 1024 - (c - 1) * 256);
-    const int n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
-    const int x = cx * n + j % n, y = cy * n + j / n;
-    const uint8_t* D = deb.plane(c, b, g);
-    const int v = D[y * w + x], diff = (int)src.plane(c, b, g)[y * w + x] - v;
-    atomicAdd(&st[c].bo_n[v >> 3], 1);
-    atomicAdd(&st[c].bo_s[v >> 3], diff);
+  // one region per wave: waves 0/1 = luma rows 0-15 / 16-31 (8 samples per lane), wave 2 =
+  // Cb, wave 3 = Cr (4 per lane).  Counts and sums travel packed as sum * 2048 + count
+  // (count <= 1024, |sum| <= 255 * 1024): one wave reduction per EO counter, not two.
+  const int wave = tid >> 6;
+  const int c = wave < 2 ? 0 : wave - 1;
+  const int n = c ? 16 : 32, T = c ? kSaoTc : kSaoT, w = c ? g.W / 2 : g.W;
+  const int16_t* t = c == 0 ? tl : tc[c - 1];
+  const int iters = c ? 4 : 8;
+  int eo[4][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) eo[d][q] = 0;
+  for (int k = 0; k < iters; ++k) {
+    const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
+    const int lx = i % n, ly = i / n;
+    const int v = t[(ly + 1) * T + lx + 1];
+    const int diff = (int)src.plane(c, b, g)[(cy * n + ly) * w + cx * n + lx] - v;
+    const int packed = diff * 2048 + 1;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
       int dx, dy;
-      sao_eo_dir(k, dx, dy);
-      const int ax = x + dx, ay = y + dy, bx = x - dx, by = y - dy;
-      if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= w || ay >= h || bx >= w || by >= h) continue;
-      const int cat = sao_eo_category(v, D[ay * w + ax], D[by * w + bx]);
-      if (cat) {  // category 0 is never offset: skip its (heavily contended) counters
-        atomicAdd(&st[c].eo_n[k][cat], 1);
-        atomicAdd(&st[c].eo_s[k][cat], diff);
+      sao_eo_dir(d, dx, dy);
+      const int a = t[(ly + 1 + dy) * T + lx + 1 + dx], bb = t[(ly + 1 - dy) * T + lx + 1 - dx];
+      const int cat = (a < 0 || bb < 0) ? 0 : sao_eo_category(v, a, bb);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) eo[d][q] += cat == q + 1 ? packed : 0;
+    }
+    // band statistics: one reduction per distinct band in the wave (ballot + readlane)
+    const int band = v >> 3;
+    bool pending = true;
+    for (;;) {
+      const unsigned long long m = __ballot(pending);
+      if (m == 0) break;
+      const int bsel = __builtin_amdgcn_readlane(band, __ffsll((long long)m) - 1);
+      const bool mine = pending && band == bsel;
+      const int tot = wave_sum(mine ? packed : 0);
+      if (lane == 0) {
+        atomicAdd(&st[c].bo_n[bsel], tot & 2047);
+        atomicAdd(&st[c].bo_s[bsel], (tot - (tot & 2047)) / 2048);
       }
+      pending = pending && !mine;
     }
   }
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int tot = wave_sum(eo[d][q]);
+      if (lane == 0 && (tot & 2047)) {
+        atomicAdd(&st[c].eo_n[d][q + 1], tot & 2047);
+        atomicAdd(&st[c].eo_s[d][q + 1], (tot - (tot & 2047)) / 2048);
+      }
+    }
   __shared__ SaoTables tab;
   __syncthreads();
   if (tid < kSaoItems) sao_item(st, lam16, tid, tab);  // 144 offset/cost items in parallel
@@ -334,7 +385,8 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   if (tid == 0) sao_finish(tab, lam16, sao + 3 * ((long)b * g.wc * g.hc + ctu));
 }
 
-__global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet rec, const uint32_t* sao, Geo g) {
+// every sample of `out`: the SAO'd deblocked sample (or the deblocked sample itself)
+__global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet out, const uint32_t* sao, Geo g) {
   const int b = blockIdx.y;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   const long ny = g.ysz, nc = g.csz;
@@ -344,22 +396,20 @@ __global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet rec, c
   const int w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H, n = c ? 16 : 32;
   const int x = (int)(j % w), y = (int)(j / w);
   const uint32_t p = sao[3 * ((long)b * g.wc * g.hc + (y / n) * g.wc + x / n) + c];
-  if (sao_type(p)) rec.plane(c, b, g)[j] = (uint8_t)sao_sample(deb.plane(c, b, g), w, h, x, y, p);
+  const uint8_t* D = deb.plane(c, b, g);
+  out.plane(c, b, g)[j] = sao_type(p) ? (uint8_t)sao_sample(D, w, h, x, y, p) : D[j];
 }
 
-void launch_sao(FrameSet src, FrameSet rec, FrameSet deb, uint32_t* sao, const Geo& g, int qp, int B,
-                hipStream_t s) {
-  (void)hipMemcpyAsync(deb.y, rec.y, B * g.ysz, hipMemcpyDeviceToDevice, s);
-  (void)hipMemcpyAsync(deb.u, rec.u, B * g.csz, hipMemcpyDeviceToDevice, s);
-  (void)hipMemcpyAsync(deb.v, rec.v, B * g.csz, hipMemcpyDeviceToDevice, s);
-  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, sao, g, sao_lambda16(qp));
-  k_sao_apply<<<dim3((unsigned)((g.ysz + 2 * g.csz + 255) / 256), B), 256, 0, s>>>(deb, rec, sao, g);
+void launch_sao(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, const int8_t* qp, const RcTables* rc,
+                const Geo& g, int B, hipStream_t s) {
+  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, sao, g, qp, rc);
+  k_sao_apply<<<dim3((unsigned)((g.ysz + 2 * g.csz + 255) / 256), B), 256, 0, s>>>(deb, out, sao, g);
 }
 
-void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int qp, int B, hipStream_t s) {
+void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int B, hipStream_t s) {
   dim3 grid((unsigned)tv_min(1024, (int)(g.ysz / 32 / 256 + 1)), B);
-  k_deblock<<<grid, 256, 0, s>>>(rec, dec, g, qp, 0);
-  k_deblock<<<grid, 256, 0, s>>>(rec, dec, g, qp, 1);
+  k_deblock<<<grid, 256, 0, s>>>(rec, dec, g, 0);
+  k_deblock<<<grid, 256, 0, s>>>(rec, dec, g, 1);
 }
 
 }  // namespace gpu

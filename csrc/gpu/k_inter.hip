@@ -18,6 +18,7 @@
 #include "tb_coder.h"
 #include "wave_tb.h"
 #include "tv/me_model.h"
+#include "tv/rc_model.h"
 
 namespace tv {
 namespace gpu {
@@ -99,9 +100,10 @@ constexpr int kCoarseMaxRq = 32;
 constexpr int kCoarseRows = 8 + 2 * kCoarseMaxRq;
 constexpr int kCoarseWords = kCoarseMaxRq / 2 + 3;
 
-__global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uint8_t* qprev, Geo g, Penalties pen,
-                                                  int rq, int16_t* cmv, int* ccost) {
+__global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uint8_t* qprev, Geo g, const RcTables* rc,
+                                                  int seq_qp, int rq, int16_t* cmv, int* ccost) {
   const int ctu = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+  const Penalties& pen = rc->pen[seq_qp];  // lookahead: the frame QP may depend on its result
   const int qw = g.W >> 2, qh = g.H >> 2;
   const int x0 = 8 * (ctu % g.wc), y0 = 8 * (ctu / g.wc);
   const uint8_t* C = qcur + (long)b * qw * qh;
@@ -154,8 +156,9 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
 
 __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                          DecisionSet dec, const int16_t* prev_mv, const int16_t* cmv,
-                                                         Geo g, Penalties pen, int range) {
+                                                         Geo g, const RcTables* rc, int range) {
   const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const Penalties& pen = rc->pen[dec.qp[b]];
   const int cxi = ctu % g.wc, cyi = ctu / g.wc, cx = cxi * 32, cy = cyi * 32;
   const uint8_t* S = src.plane(0, b, g);
   const uint8_t* R = ref.plane(0, b, g);
@@ -424,8 +427,9 @@ __device__ __forceinline__ bool pr_zeroed(const PReconLds& L, int id) {
 }
 
 __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
-                                                     FrameSet rec, DecisionSet dec, Geo g, int qp) {
+                                                     FrameSet rec, DecisionSet dec, Geo g) {
   const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int qp = dec.qp[b];
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
   const long ub = b * g.usz;
   const int qpc = chroma_qp(qp, 0), Wc = g.W >> 1, Hc = g.H >> 1;
@@ -679,12 +683,42 @@ void launch_quarter(FrameSet src, uint8_t* q, const Geo& g, int B, hipStream_t s
   k_quarter<<<dim3((n + 255) / 256, B), 256, 0, s>>>(src, q, g);
 }
 
+void launch_coarse_me(const MeBuffers& me, const Geo& g, const RcTables* rc, int seq_qp, int range, int B,
+                      hipStream_t s) {
+  k_coarse_me<<<dim3(g.wc * g.hc, B), 64, 0, s>>>(me.qcur, me.qprev, g, rc, seq_qp, range / 4, me.cmv, me.ccost);
+}
+
+// CRF (tv/rc_model.h): the frame QP of every segment from its lookahead complexity — the
+// summed coarse-search cost (P) or the quarter-res activity (IDR) — written into dec.qp
+__global__ void __launch_bounds__(256) k_rc_crf(const uint8_t* q, const int* ccost, int8_t* qp, Geo g, int crf,
+                                                int intra) {
+  const int b = blockIdx.x, nctu = g.wc * g.hc, qw = g.W >> 2;
+  __shared__ unsigned long long sum;
+  if (threadIdx.x == 0) sum = 0;
+  __syncthreads();
+  unsigned long long acc = 0;
+  for (int c = threadIdx.x; c < nctu; c += 256) {
+    if (intra) {
+      const uint8_t* Q = q + (long)b * qw * (g.H >> 2) + (long)(8 * (c / g.wc)) * qw + 8 * (c % g.wc);
+      acc += rc_block_activity(Q, qw);
+    } else {
+      acc += (unsigned long long)ccost[(long)b * nctu + c];
+    }
+  }
+  atomicAdd(&sum, acc);
+  __syncthreads();
+  if (threadIdx.x == 0) qp[b] = (int8_t)rc_crf_qp(crf, intra != 0, sum, nctu);
+}
+
+void launch_rc_crf(const uint8_t* q, const int* ccost, int8_t* qp, const Geo& g, int crf, bool intra, int B,
+                   hipStream_t s) {
+  k_rc_crf<<<B, 256, 0, s>>>(q, ccost, qp, g, crf, intra ? 1 : 0);
+}
+
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
-                        const Geo& g, int qp, const Penalties& pen, int range, const MeBuffers& me, int B,
-                        hipStream_t s) {
-  k_coarse_me<<<dim3(g.wc * g.hc, B), 64, 0, s>>>(me.qcur, me.qprev, g, pen, range / 4, me.cmv, me.ccost);
-  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, pen, range);
-  k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, qp);
+                        const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s) {
+  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range);
+  k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g);
 }
 
 }  // namespace gpu

@@ -47,8 +47,9 @@ __device__ __forceinline__ void ref_entry(int e, int& bi, int& i) {
   }
 }
 
-__global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSet dec, Geo g, Penalties pen) {
+__global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSet dec, Geo g, const RcTables* rc) {
   const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const Penalties& pen = rc->pen[dec.qp[b]];
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
   const uint8_t* S = src.plane(0, b, g);
   __shared__ uint8_t sblk[32 * 32];
@@ -179,9 +180,10 @@ struct CompLds {
   WaveTbScratch tb;
 };
 
-__global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec, DecisionSet dec, Geo g, int qp,
-                                                     int diag, int cy0) {
+__global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec, DecisionSet dec, Geo g, int diag,
+                                                     int cy0) {
   const int b = blockIdx.y, c = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qp = dec.qp[b];
   __shared__ int Tm[32][33];
   __shared__ CompLds W[3];
   __shared__ int cus[16][3];
@@ -323,15 +325,15 @@ __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec,
   }
 }
 
-void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, int qp,
-                        const Penalties& pen, int B, hipStream_t s) {
-  k_intra_analysis<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, dec, g, pen);
+void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, int B,
+                        hipStream_t s) {
+  k_intra_analysis<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, dec, g, rc);
   const int ndiag = (g.wc - 1) + 2 * (g.hc - 1) + 1;
   for (int d = 0; d < ndiag; ++d) {
     const int cy0 = tv_max(0, (d - (g.wc - 1) + 1) / 2);
     const int cy1 = tv_min(g.hc - 1, d / 2);
     if (cy1 < cy0) continue;
-    k_intra_recon<<<dim3(cy1 - cy0 + 1, B), 192, 0, s>>>(src, rec, dec, g, qp, d, cy0);
+    k_intra_recon<<<dim3(cy1 - cy0 + 1, B), 192, 0, s>>>(src, rec, dec, g, d, cy0);
   }
 }
 

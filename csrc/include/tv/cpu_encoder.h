@@ -25,9 +25,10 @@ void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* 
 class CpuEncoder {
  public:
   explicit CpuEncoder(const SeqConfig& cfg, int search_range = 64);
-  // Appends VPS/SPS/PPS (for IDR) and one slice NAL to `out`.
+  // Appends VPS/SPS/PPS (for IDR) and one slice NAL to `out`.  qp >= 0: this frame's slice
+  // QP (rate control), else the sequence QP.
   void encode_frame(const uint8_t* const planes[3], const int strides[3], bool idr, int poc,
-                    std::vector<uint8_t>& out);
+                    std::vector<uint8_t>& out, int qp = -1);
   const Picture& recon() const { return rec_; }
   const SeqConfig& config() const { return cfg_; }
   FrameDecisions dec;

@@ -25,6 +25,7 @@ struct SeqConfig {
   int coded_w = 0, coded_h = 0;   // multiples of the CTB size
   int qp = 27;
   int max_merge_cand = 5;
+  int crf = 0;  // > 0: per-frame QP from the lookahead complexity (tv/rc_model.h)
   bool deblock = true;
   bool sao = false;
   int fps_num = 30, fps_den = 1;
@@ -55,6 +56,7 @@ struct FrameData {
   int wc = 0;  // CTBs per row
   // SAO parameters, 3 packed words (Y, Cb, Cr) per CTB in raster order (nullptr: SAO off)
   const uint32_t* sao = nullptr;
+  int qp = -1;  // slice QP (rate control); -1: the sequence QP (PPS init_qp)
 };
 
 // Owning storage for one frame's decisions (CPU side).
@@ -63,8 +65,10 @@ struct FrameDecisions {
   std::vector<uint8_t> cu_log2, intra, ipm, cbf;
   std::vector<int16_t> mv, coef_y, coef_u, coef_v;
   std::vector<uint32_t> sao;  // 3 per CTB
+  int qp = -1;                // slice QP of this frame (-1: sequence QP)
   void alloc(int coded_w, int coded_h) {
     sao.assign(3 * (size_t)(coded_w >> kCtbLog2) * (coded_h >> kCtbLog2), sao_off_param());
+    qp = -1;
     cw = coded_w;
     ch = coded_h;
     w8 = coded_w >> 3;
@@ -93,6 +97,7 @@ struct FrameDecisions {
     f.coef[2] = coef_v.data();
     f.sao = sao.data();
     f.wc = cw >> kCtbLog2;
+    f.qp = qp;
     return f;
   }
 };

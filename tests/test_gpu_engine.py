@@ -75,3 +75,15 @@ def test_gpu_bit_exact_at_benchmark_geometry(w, h, batch, gop, sao, check):
         cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, sao=sao, search_range=rng)
         assert segs[b] == cpu_bs, f"segment {b}: GPU bitstream differs from CPU golden model"
     eng.close()
+
+
+def test_gpu_crf_bit_exact():
+    """In-engine CRF: the per-frame QP decided on the GPU from the lookahead complexity is the
+    CPU golden model's, and the bitstreams are identical."""
+    w, h, gop = 192, 128, 5
+    eng = _engine(width=w, height=h, qp=27, batch=2, gop=gop, search_range=16, seed=5, crf=30)
+    segs = eng.encode_synthetic([0, 10])
+    for b, start in enumerate([0, 10]):
+        frames = [hevc.synth_frame(5, start + f, w, h) for f in range(gop)]
+        cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, crf=30, search_range=16)
+        assert segs[b] == cpu_bs

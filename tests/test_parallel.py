@@ -276,3 +276,69 @@ def test_node_job_elastic_restart_torchrun(tmp_path, source):
 
     with open(out, "rb") as f:
         assert len(hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False).frames) == 24
+
+
+def _rc_worker(rank, world, port, src, out, kbps, res_path):
+    from thinvids_amd.parallel.node_job import run_job
+
+    dist = _init(rank, world, port)
+    res = run_job(src, out, software=True, gop=8, segment_frames=8, bitrate_kbps=kbps, batch_segments=1)
+    if rank == 0:
+        with open(res_path, "w") as f:
+            json.dump(res, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("frac", [0.55, 1.5])
+def test_two_pass_rate_control_hits_target_on_two_ranks(tmp_path, frac):
+    """Frame-level 2-pass: pass-1 per-frame bits all-reduced over the group, a global
+    per-frame QP plan, rank-local feedback in pass 2: achieved bitrate within +-5 %."""
+    from thinvids_amd.models import hevc, media
+
+    frames = [hevc.synth_frame(11, t, 160, 96) for t in range(48)]
+    src = str(tmp_path / "rc.y4m")
+    media.write_y4m(src, frames, 30, 1)
+    base, _ = hevc.encode_sequence_cpu(frames, qp=27, gop=8, search_range=64)
+    target = len(base) * 8 / (48 / 30) / 1000 * frac
+    res_path = str(tmp_path / "res.json")
+    mp.spawn(_rc_worker, args=(2, _free_port(), src, str(tmp_path / "o.mp4"), target, res_path), nprocs=2, join=True)
+    res = json.load(open(res_path))
+    assert res["passes"] == 2
+    got = res["outputs"][0]["kbps"]
+    assert abs(got / target - 1) < 0.05, (got, target)
+    with open(tmp_path / "o.mp4", "rb") as f:
+        assert len(hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False).frames) == 48
+
+
+@pytest.mark.gpu
+def test_two_pass_rate_control_gpu_engine(tmp_path, monkeypatch):
+    """Same 2-pass on the HIP engine (per-segment, per-frame QP maps on the device)."""
+    from thinvids_amd.models import hevc, media
+    from thinvids_amd.parallel.node_job import run_job
+
+    monkeypatch.delenv("TV_FORCE_CPU", raising=False)
+    frames = [hevc.synth_frame(12, t, 256, 160) for t in range(64)]
+    src = str(tmp_path / "rc.y4m")
+    media.write_y4m(src, frames, 30, 1)
+    r1 = run_job(src, str(tmp_path / "a.mp4"), gop=16, segment_frames=16)
+    target = r1["outputs"][0]["kbps"] * 0.6
+    r2 = run_job(src, str(tmp_path / "b.mp4"), gop=16, segment_frames=16, bitrate_kbps=target)
+    assert r2["passes"] == 2 and abs(r2["outputs"][0]["kbps"] / target - 1) < 0.05, (r2["outputs"], target)
+
+
+@pytest.mark.gpu
+def test_gpu_per_frame_qp_map_bit_exact():
+    """A per-segment, per-frame QP map on the GPU engine is bit-exact with the CPU golden
+    model's per-frame slice QPs."""
+    from thinvids_amd.models import hevc
+    from thinvids_amd.models.gpu_engine import GpuEngine
+
+    w, h, gop = 192, 128, 5
+    qmap = np.array([[22, 30, 26, 34, 27], [40, 24, 31, 27, 19]])
+    eng = GpuEngine(width=w, height=h, qp=27, batch=2, gop=gop, search_range=16, sao=True, seed=5)
+    segs = eng.encode_synthetic([0, 10], qp=qmap)
+    for b, start in enumerate([0, 10]):
+        frames = [hevc.synth_frame(5, start + f, w, h) for f in range(gop)]
+        cpu, _ = hevc.encode_sequence_cpu(frames, qp=27, sao=True, search_range=16, frame_qps=qmap[b])
+        assert segs[b] == cpu, f"segment {b}"
+    eng.close()

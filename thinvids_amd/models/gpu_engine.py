@@ -22,14 +22,14 @@ def _lib():
         lib.tv_gpu_last_error.restype = C.c_char_p
         lib.tv_gpu_device_count.restype = C.c_int
         lib.tv_engine_new.restype = vp
-        lib.tv_engine_new.argtypes = [C.c_int] * 7 + [C.c_uint32, C.c_int, C.c_int, C.c_int]
+        lib.tv_engine_new.argtypes = [C.c_int] * 7 + [C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int]
         lib.tv_engine_free.argtypes = [vp]
         lib.tv_engine_encode_synth.restype = C.c_int
-        lib.tv_engine_encode_synth.argtypes = [vp, C.POINTER(C.c_int), C.c_int, C.c_int]
+        lib.tv_engine_encode_synth.argtypes = [vp, C.POINTER(C.c_int), C.c_int, C.c_int, vp]
         lib.tv_engine_encode_host.restype = C.c_int
-        lib.tv_engine_encode_host.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int]
+        lib.tv_engine_encode_host.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int, vp]
         lib.tv_engine_encode_device.restype = C.c_int
-        lib.tv_engine_encode_device.argtypes = [vp, vp, C.c_int, C.c_int]
+        lib.tv_engine_encode_device.argtypes = [vp, vp, C.c_int, C.c_int, vp]
         lib.tv_engine_segment_size.restype = C.c_size_t
         lib.tv_engine_segment_size.argtypes = [vp, C.c_int]
         lib.tv_engine_segment_copy.argtypes = [vp, C.c_int, C.POINTER(C.c_uint8)]
@@ -60,7 +60,7 @@ class GpuEngine:
     def __init__(self, width: int, height: int, qp: int = 27, batch: int = 8, gop: int = 16,
                  search_range: int = 64, deblock: bool = True, sao: bool = False, seed: int = 1,
                  threads: int | None = None,
-                 device: int = 0, max_merge: int = 5):
+                 device: int = 0, max_merge: int = 5, crf: int = 0):
         self.lib = _lib()
         self.width, self.height, self.qp = width, height, qp
         self.batch, self.gop = batch, gop
@@ -69,7 +69,7 @@ class GpuEngine:
         self.sao = sao
         self.device = device
         self.h = self.lib.tv_engine_new(width, height, qp, batch, gop, search_range, int(deblock) | (2 if sao else 0),
-                                        seed & 0xFFFFFFFF, self.threads, device, max_merge)
+                                        seed & 0xFFFFFFFF, self.threads, device, max_merge, int(crf))
         if not self.h:
             raise RuntimeError("GPU engine init failed: " + self.lib.tv_gpu_last_error().decode())
 
@@ -80,22 +80,36 @@ class GpuEngine:
 
     __del__ = close
 
+    def _qmap(self, qp, nseg: int, nframes: int):
+        """None -> sequence QP; int -> that QP everywhere; array -> [nseg][nframes] slice QPs."""
+        if qp is None:
+            self._qbuf = None
+            return None
+        q = np.asarray(qp)
+        q = np.broadcast_to(q, (nseg, nframes)) if q.ndim < 2 else q
+        if q.shape != (nseg, nframes) or (q < 0).any() or (q > 51).any():
+            raise ValueError(f"qp map must be [{nseg}][{nframes}] in 0..51")
+        self._qbuf = np.ascontiguousarray(q, dtype=np.int8)
+        self.last_qp = self._qbuf
+        return C.c_void_p(self._qbuf.ctypes.data)
+
     def _check(self, rc):
         if rc != 0:
             raise RuntimeError(self.lib.tv_gpu_last_error().decode())
 
-    def encode_synthetic(self, starts, nframes: int | None = None) -> list[bytes]:
+    def encode_synthetic(self, starts, nframes: int | None = None, qp=None) -> list[bytes]:
         """Encode len(starts) segments generated on the GPU; segment b = synthetic frames
-        [starts[b], starts[b] + nframes) (nframes defaults to the GOP)."""
+        [starts[b], starts[b] + nframes) (nframes defaults to the GOP).  `qp`: rate-control
+        slice QPs (int or [nseg][nframes])."""
         n = self.gop if nframes is None else int(nframes)
         if not 1 <= n <= self.gop or not 1 <= len(starts) <= self.batch:
             raise ValueError(f"need 1..{self.batch} segments of 1..{self.gop} frames")
         arr = (C.c_int * len(starts))(*[int(s) for s in starts])
-        self._check(self.lib.tv_engine_encode_synth(self.h, arr, len(starts), n))
+        self._check(self.lib.tv_engine_encode_synth(self.h, arr, len(starts), n, self._qmap(qp, len(starts), n)))
         self.last_frames = n
         return [self.segment(b) for b in range(len(starts))]
 
-    def encode_frames(self, segments) -> list[bytes]:
+    def encode_frames(self, segments, qp=None) -> list[bytes]:
         """segments: list (<= batch) of equally long lists (1..gop) of display-size (Y, U, V)
         frames; each segment becomes one closed GOP (IDR + P frames)."""
         n = len(segments[0]) if segments else 0
@@ -114,9 +128,9 @@ class GpuEngine:
         for b, seg in enumerate(segments):
             stage.to_staging(stage.upload_frames(seg, dev), self.width, self.height, staging, b * n)
         torch.cuda.current_stream(dev).synchronize()
-        return self.encode_device(staging, len(segments), n)
+        return self.encode_device(staging, len(segments), n, qp=qp)
 
-    def encode_device(self, frames, nseg: int, nframes: int) -> list[bytes]:
+    def encode_device(self, frames, nseg: int, nframes: int, qp=None) -> list[bytes]:
         """frames: a contiguous uint8 CUDA tensor on this engine's GPU laid out
         [segment][frame][Y | U | V] at the coded size (edge-padded), already written (the
         producing stream synchronised).  Copied device-to-device into the engine."""
@@ -125,7 +139,8 @@ class GpuEngine:
             raise ValueError(f"need 1..{self.batch} segments of 1..{self.gop} frames")
         if not frames.is_cuda or not frames.is_contiguous() or frames.numel() * frames.element_size() < nseg * nframes * fsz:
             raise ValueError("frames must be a contiguous CUDA tensor of nseg*nframes coded-size I420 frames")
-        self._check(self.lib.tv_engine_encode_device(self.h, C.c_void_p(frames.data_ptr()), nseg, nframes))
+        self._check(self.lib.tv_engine_encode_device(self.h, C.c_void_p(frames.data_ptr()), nseg, nframes,
+                                                     self._qmap(qp, nseg, nframes)))
         self.last_frames = nframes
         return [self.segment(b) for b in range(nseg)]
 

@@ -10,7 +10,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .._native import Bytes, check, core_lib, i16p, ptr
+from .._native import u8p, Bytes, check, core_lib, i16p, ptr
 
 Frame = tuple  # (Y, U, V)
 
@@ -42,14 +42,20 @@ class CpuEncoder:
     """Scalar C++ HEVC encoder (software path; reference `software_encode`)."""
 
     def __init__(self, width: int, height: int, qp: int = 27, deblock: bool = True,
-                 search_range: int = 64, max_merge: int = 5, sao: bool = False):
+                 search_range: int = 64, max_merge: int = 5, sao: bool = False, crf: int = 0):
         if width % 2 or height % 2:
             raise ValueError("width/height must be even")
         self.lib = core_lib()
         self.width, self.height, self.qp = width, height, qp
         self.cw, self.ch = coded_size(width, height)
-        self.h = self.lib.tv_cpu_encoder_new(width, height, qp, int(deblock) | (2 if sao else 0), search_range,
-                                             max_merge)
+        if crf:
+            f = self.lib.tv_cpu_encoder_new_crf
+            f.restype = C.c_void_p
+            f.argtypes = [C.c_int] * 7
+            self.h = f(width, height, qp, int(deblock) | (2 if sao else 0), search_range, max_merge, int(crf))
+        else:
+            self.h = self.lib.tv_cpu_encoder_new(width, height, qp, int(deblock) | (2 if sao else 0), search_range,
+                                                 max_merge)
         self.out = Bytes()
 
     def __del__(self):
@@ -57,11 +63,18 @@ class CpuEncoder:
             self.lib.tv_cpu_encoder_free(self.h)
             self.h = None
 
-    def encode(self, frame: Frame, idr: bool, poc: int) -> bytes:
+    def encode(self, frame: Frame, idr: bool, poc: int, qp: int | None = None) -> bytes:
+        """One frame; `qp` overrides the slice QP of this frame (rate control)."""
         y, u, v = (np.ascontiguousarray(p) for p in frame)
         self.out.clear()
-        check(self.lib.tv_cpu_encoder_encode(self.h, ptr(y), ptr(u), ptr(v), y.shape[1], u.shape[1],
-                                             int(idr), poc, self.out.h))
+        if qp is None:
+            check(self.lib.tv_cpu_encoder_encode(self.h, ptr(y), ptr(u), ptr(v), y.shape[1], u.shape[1],
+                                                 int(idr), poc, self.out.h))
+        else:
+            f = self.lib.tv_cpu_encoder_encode_qp
+            f.restype = C.c_int
+            f.argtypes = [C.c_void_p, u8p, u8p, u8p] + [C.c_int] * 5 + [C.c_void_p]
+            check(f(self.h, ptr(y), ptr(u), ptr(v), y.shape[1], u.shape[1], int(idr), poc, int(qp), self.out.h))
         return self.out.tobytes()
 
     def recon(self) -> Frame:
@@ -81,8 +94,9 @@ class CpuEncoder:
         return d
 
 
-def encode_sequence_cpu(frames, qp: int = 27, gop: int = 0, **kw) -> tuple[bytes, list]:
-    """Encode frames (first is IDR; IDR every `gop` frames if gop>0). Returns (annexb, recons)."""
+def encode_sequence_cpu(frames, qp: int = 27, gop: int = 0, frame_qps=None, **kw) -> tuple[bytes, list]:
+    """Encode frames (first is IDR; IDR every `gop` frames if gop>0). Returns (annexb, recons).
+    `frame_qps`: optional per-frame slice QP (rate control); `qp` stays the PPS init QP."""
     frames = list(frames)
     h, w = frames[0][0].shape
     enc = CpuEncoder(w, h, qp=qp, **kw)
@@ -90,7 +104,7 @@ def encode_sequence_cpu(frames, qp: int = 27, gop: int = 0, **kw) -> tuple[bytes
     for i, f in enumerate(frames):
         idr = i == 0 or (gop > 0 and i % gop == 0)
         poc = 0 if idr else poc + 1
-        out += enc.encode(f, idr, poc)
+        out += enc.encode(f, idr, poc, None if frame_qps is None else int(frame_qps[i]))
         recons.append(enc.recon())
     return bytes(out), recons
 

@@ -32,6 +32,7 @@ import time
 
 import numpy as np
 
+from ..models.ratecontrol import RateFeedback, frame_sizes, plan_frame_qps, predict_bits, round_qps
 from ..utils import fault, trace
 
 
@@ -254,16 +255,18 @@ class JobHooks:
 
 
 def _encode_many(items: list, cache) -> tuple[dict, dict]:
-    """items: [(key, part, spec)] -> ({key: annexb}, {key: PartStats}); batched per spec on
-    the engine (a part may be host frames, device frames or a synthetic range)."""
+    """items: [(key, part, spec, per-frame QPs or None)] -> ({key: annexb}, {key: PartStats});
+    batched per spec on the engine (a part may be host frames, device frames or a synthetic
+    range)."""
     from ..worker.encoder import PartStats, encode_parts
 
     out, st, groups = {}, {}, {}
-    for key, part, spec in items:
-        groups.setdefault(spec, []).append((key, part))
+    for key, part, spec, q in items:
+        groups.setdefault(spec, []).append((key, part, q))
     for spec, grp in groups.items():
         stats = [PartStats() for _ in grp]
-        for (k, _), b, ps in zip(grp, encode_parts([g[1] for g in grp], spec, cache, stats), stats):
+        bits = encode_parts([g[1] for g in grp], spec, cache, stats, [g[2] for g in grp])
+        for (k, _, _), b, ps in zip(grp, bits, stats):
             out[k] = b
             st[k] = ps
     return out, st
@@ -273,7 +276,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             segment_frames: int = 256, mode: str = "direct", bitrate_kbps: float = 0.0, ladder=None,
             search_range: int = 64, software: bool = False, batch_segments: int = 8,
             resume_dir: str | None = None, max_retries: int = 3, hooks: JobHooks | None = None,
-            deblock: bool = True, sao: bool = False, cache=None) -> dict:
+            deblock: bool = True, sao: bool = False, cache=None, crf: int = 0) -> dict:
     import torch
 
     from ..models import hevc, media
@@ -313,9 +316,19 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
     quality: dict = {}  # (r, i) -> PartStats of segments encoded here
 
-    def spec(r, q):
-        return EncodeSpec(rungs[r][0], rungs[r][1], qp=int(q), gop=gop, search_range=search_range,
-                          software=software, deblock=deblock, sao=sao, seed=getattr(src, "seed", 1))
+    def spec(r):  # the QP is a per-frame input now: one resident engine per rung, whatever the plan
+        return EncodeSpec(rungs[r][0], rungs[r][1], qp=qp, gop=gop, search_range=search_range,
+                          software=software, deblock=deblock, sao=sao, seed=getattr(src, "seed", 1),
+                          crf=0 if bitrate_kbps > 0 else crf)
+
+    rc = {"plan": None, "fb": RateFeedback(), "bits": {}}  # pass-2 plan, feedback, per-frame bits
+
+    def seg_qps(r, i, offset):
+        """(integer per-frame QPs or None, checkpoint key) of segment i on rung r."""
+        if rc["plan"] is None:
+            return None, qp
+        q = round_qps(rc["plan"][r][i], offset)
+        return q, "p" + hashlib.sha1(q.astype(np.int8).tobytes()).hexdigest()[:12]
 
     def load(i):
         """Segment i's source: a synthetic range (generated where it is encoded), or host
@@ -331,15 +344,19 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
 
         return stage.upload_frames(frames, dev)
 
-    def encode_segments(seg_ids, qps, source_of) -> dict:
+    def encode_segments(seg_ids, source_of) -> dict:
         """Work item = one segment with ALL its rungs: the source range is read (or received)
         once, every rung is staged from it on the device, and each rung engine then encodes
-        the claimed segments in one batched launch."""
-        out, todo, keep = {}, [], []
+        the claimed segments in one batched launch.  In pass 2 the per-frame QP plan of
+        every segment is offset by this rank's rate feedback so far."""
+        out, todo, keep, plans = {}, [], [], {}
+        offset = rc["fb"].offset()
         for i in seg_ids:
             need = []
             for r in range(len(rungs)):
-                b = ckpt.load(r, i, int(qps[r][i]))
+                q, key = seg_qps(r, i, offset)
+                plans[(r, i)] = (q, key)
+                b = ckpt.load(r, i, key)
                 if b is not None:
                     out[(r, i)] = b
                     stats["resumed"] += 1
@@ -348,22 +365,28 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             if need:
                 with trace.span("node_job.load"):
                     part = source_of(i)
-                todo.extend(((r, i), part, spec(r, qps[r][i])) for r in need)
+                todo.extend(((r, i), part, spec(r), plans[(r, i)][0]) for r in need)
                 keep.append(part)
         if todo:
             with trace.span("node_job.encode", segments=len(todo)):
                 got, qual = _encode_many(todo, cache)
             for (r, i), b in got.items():
-                ckpt.save(r, i, int(qps[r][i]), b)
+                ckpt.save(r, i, plans[(r, i)][1], b)
                 out[(r, i)] = b
                 quality[(r, i)] = qual[(r, i)]
                 stats["encoded"] += 1
         del keep  # device / host source copies of this claim are released here
+        for (r, i), b in out.items():
+            fb = frame_sizes(b)
+            rc["bits"][(r, i)] = fb
+            q = plans[(r, i)][0]
+            if q is not None:  # rate feedback: actual vs the model's prediction at these QPs
+                rc["fb"].record(8.0 * sum(fb), float(predict_bits(rc["b1"][(r, i)], qp, q).sum()))
         for i in seg_ids:
             hooks.segment_done(segs[i][1])
         return out
 
-    def encode_pass(qps) -> dict:
+    def encode_pass() -> dict:
         mine = {}
         if mode == "scatter" and world > 1:
             # rounds: rank 0 reads `world` segments and sends each rank its segment over one
@@ -398,7 +421,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                         ysz, csz = w0 * h0, w0 * h0 // 4
                         part = [(x[:ysz].reshape(h0, w0), x[ysz:ysz + csz].reshape(h0 // 2, w0 // 2),
                                  x[ysz + csz:].reshape(h0 // 2, w0 // 2)) for x in g[:n]]
-                    mine.update(encode_segments([i], qps, lambda _i, p=part: p))
+                    mine.update(encode_segments([i], lambda _i, p=part: p))
         else:
             wq = WorkQueue(f"{job_tag}_pass{encode_pass.calls}", list(range(len(segs))), world, max_retries)
             fault.check("rank", rank)  # TV_FAULT=rank:<r>:hang|die|fail (tests)
@@ -414,7 +437,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 if not todo:
                     return
                 try:
-                    mine.update(encode_segments(todo, qps, load))
+                    mine.update(encode_segments(todo, load))
                 except Exception as e:  # a real engine/IO failure: every item goes back
                     for i in todo:
                         wq.fail((i,), repr(e))
@@ -455,12 +478,12 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     encode_pass.calls = 0
     cdev = dev if dev.type == "cuda" else torch.device("cpu")
 
-    def agreed_pass(q):
+    def agreed_pass():
         """encode_pass + a collective verdict: a rank that failed (halt, abort, engine
         error) never strands its peers inside the next collective."""
         err, got = None, {}
         try:
-            got = encode_pass(q)
+            got = encode_pass()
         except Exception as e:  # noqa: BLE001 - re-raised below on every rank
             err = e
         failed = allreduce_stats([1.0 if err else 0.0], cdev, op="max")[0]
@@ -468,26 +491,30 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             raise err if err is not None else RuntimeError("a peer rank failed this job")
         return got
 
-    base = [[qp] * len(segs) for _ in rungs]
     passes = 1
     if bitrate_kbps > 0:
-        first = agreed_pass(base)
-        sizes = np.zeros(len(jobs))
-        for (r, i), b in first.items():
-            sizes[jobs.index((r, i))] = len(b) * 8
-        sizes = allreduce_stats(sizes, cdev)  # RC stats all-reduce
+        # pass 1 at the base QP -> every frame's bits, all-reduced over the node (RCCL) ->
+        # one global per-frame QP plan -> pass 2 with rank-local rate feedback
+        agreed_pass()
+        starts = np.cumsum([0] + [n for _, n in segs])
+        flat = np.zeros(len(rungs) * nfr)
+        for (r, i), fb in rc["bits"].items():
+            flat[r * nfr + starts[i]:r * nfr + starts[i] + len(fb)] = 8.0 * np.asarray(fb, np.float64)
+        flat = allreduce_stats(flat, cdev)  # RC statistics all-reduce
         fps = src.fps_num / src.fps_den
-        qps = []
+        rc["b1"] = {(r, i): flat[r * nfr + starts[i]:r * nfr + starts[i] + n] for r in range(len(rungs))
+                    for i, (_, n) in enumerate(segs)}
+        plan = []
         for r in range(len(rungs)):
-            idx = [jobs.index((r, i)) for i in range(len(segs))]
             scale = (rungs[r][0] * rungs[r][1]) / (rungs[0][0] * rungs[0][1])  # per-rung budget ~ pixels
             target = bitrate_kbps * 1000 * nfr / fps * scale
-            qps.append(list(qp_plan_two_pass(sizes[idx], [n for _, n in segs], qp, target)))
+            per_seg, _ = plan_frame_qps([rc["b1"][(r, i)] for i in range(len(segs))], qp, target)
+            plan.append(per_seg)
+        rc["plan"] = plan
+        rc["bits"] = {}
         passes = 2
         quality.clear()
-    else:
-        qps = base
-    mine = agreed_pass(qps)
+    mine = agreed_pass()
     t_enc = time.time() - t0
     # quality: per-rung frames + SSE of the segments encoded on this rank, all-reduced
     qv = np.zeros((len(rungs), 4))
@@ -532,7 +559,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                          "psnr_y": round(q["y"], 3) if q else None, "psnr_yuv": round(q["yuv"], 3) if q else None,
                          "quality_frames": int(qv[r, 0])})
         el = time.time() - t0
-        result.update(trace=trace.summary(), per_rank=per_rank, outputs=outs, qp_plan=[[int(q) for q in row] for row in qps],
+        result.update(trace=trace.summary(), per_rank=per_rank, outputs=outs, qp_plan=[[round(float(np.mean(q)), 2) for q in row] for row in rc["plan"]] if rc["plan"] else
+                      [[qp] * len(segs) for _ in rungs], rc_offset=round(rc["fb"].offset(), 3),
                       seconds=round(el, 3), encode_seconds=round(t_enc, 3),
                       fps=round(nfr * len(rungs) / el, 2), encode_fps=round(nfr * len(rungs) * passes / max(t_enc, 1e-9), 2))
     if own_cache:

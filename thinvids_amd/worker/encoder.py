@@ -42,9 +42,11 @@ class EncodeSpec:
     sao: bool = False
     software: bool = False
     seed: int = 1  # synthetic sources generated inside the engine
+    crf: int = 0  # > 0: in-engine CRF (per-frame QP from the lookahead)
 
     def engine_key(self):
-        return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed)
+        return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed,
+                self.crf)
 
 
 @dataclass(frozen=True)
@@ -108,7 +110,7 @@ class EngineCache:
                     self._engines.pop(old).close()
                 eng = GpuEngine(spec.width, spec.height, qp=spec.qp, batch=self.batch or auto_batch(spec), gop=spec.gop,
                                 search_range=spec.search_range, deblock=spec.deblock, sao=spec.sao,
-                                seed=spec.seed, device=self.device)
+                                seed=spec.seed, device=self.device, crf=spec.crf)
                 eng.lock = threading.Lock()
                 eng.staging = None
                 self._engines[key] = eng
@@ -187,24 +189,26 @@ def _host_frames(part) -> list:
 
 
 def encode_parts(parts: list, spec: EncodeSpec, cache: EngineCache | None = None,
-                 stats: list | None = None) -> list[bytes]:
+                 stats: list | None = None, qps: list | None = None) -> list[bytes]:
     """Encode several parts into one Annex-B bitstream each.  A part is a list of host
     (Y, U, V) frames (any size: resized to the spec), a :class:`~thinvids_amd.ops.stage.DevFrames`
     already on this GPU, or a :class:`SynthRange`.  `stats` (optional list of
-    :class:`PartStats`, one per part) receives frames and reconstruction SSE."""
+    :class:`PartStats`, one per part) receives frames and reconstruction SSE.  `qps`
+    (optional, one per part): per-frame slice QPs from rate control (None = spec.qp)."""
+    qps = qps or [None] * len(parts)
     if spec.software or not gpu_available():
         if not spec.software:
             raise RuntimeError("no GPU available for a hardware encode (set software_encode for the CPU path)")
-        return [_encode_cpu(_host_frames(p), spec, stats[i] if stats else None) for i, p in enumerate(parts)]
-    return _encode_gpu(parts, spec, cache or default_cache(), stats)
+        return [_encode_cpu(_host_frames(p), spec, stats[i] if stats else None, qps[i]) for i, p in enumerate(parts)]
+    return _encode_gpu(parts, spec, cache or default_cache(), stats, qps)
 
 
-def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None) -> bytes:
+def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None, fq=None) -> bytes:
     h, w = frames[0][0].shape
     if (w, h) != (spec.width, spec.height) or frames[0][0].dtype != np.uint8:
         frames = prepare_frames(frames, spec.width, spec.height)
     bs, recons = hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock, sao=spec.sao,
-                                          search_range=spec.search_range)
+                                          search_range=spec.search_range, frame_qps=fq, crf=spec.crf)
     if st is not None:
         sse = np.zeros(3)
         for f, r in zip(frames, recons):
@@ -216,7 +220,7 @@ def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None) -> bytes:
     return bs
 
 
-def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats) -> list[bytes]:
+def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats, qps) -> list[bytes]:
     import torch
 
     from ..ops import stage
@@ -232,7 +236,8 @@ def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats) -> list[byte
         plan = chunk_plan(_nframes(p), spec.gop)
         out.append([b""] * len(plan))
         for c, (s, n) in enumerate(plan):
-            chunks.setdefault(n, []).append((pi, c, _slice(p, s, n)))
+            q = None if qps[pi] is None else np.asarray(qps[pi][s:s + n], np.int64)
+            chunks.setdefault(n, []).append((pi, c, _slice(p, s, n), q))
     fsz, _ = stage.staging_planes(spec.width, spec.height)
     own_size = (spec.width, spec.height)
     with eng.lock:
@@ -240,9 +245,11 @@ def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats) -> list[byte
             for i in range(0, len(items), eng.batch):
                 grp = items[i:i + eng.batch]
                 srcs = [x[2] for x in grp]
+                qmap = None if all(x[3] is None for x in grp) else \
+                    np.stack([x[3] if x[3] is not None else np.full(n, spec.qp) for x in grp])
                 if all(isinstance(s, SynthRange) and s.seed == spec.seed and (s.width, s.height) == own_size
                        for s in srcs):
-                    bits = eng.encode_synthetic([s.t0 for s in srcs], nframes=n)
+                    bits = eng.encode_synthetic([s.t0 for s in srcs], nframes=n, qp=qmap)
                 else:
                     need = eng.batch * spec.gop * fsz
                     if eng.staging is None or eng.staging.numel() < need:
@@ -252,8 +259,8 @@ def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats) -> list[byte
                             s = stage.synth_frames(s.seed, s.width, s.height, range(s.t0, s.t0 + s.n), dev)
                         stage.to_staging(s, spec.width, spec.height, eng.staging, j * n)
                     torch.cuda.current_stream(dev).synchronize()
-                    bits = eng.encode_device(eng.staging, len(grp), n)
-                for j, ((pi, c, _), b) in enumerate(zip(grp, bits)):
+                    bits = eng.encode_device(eng.staging, len(grp), n, qp=qmap)
+                for j, ((pi, c, _, _), b) in enumerate(zip(grp, bits)):
                     out[pi][c] = b
                     if stats is not None:
                         stats[pi].add(n, eng.sse(j))

@@ -110,11 +110,12 @@ def _job_params(job: dict) -> dict:
     ladder = [int(x) for x in str(job.get("ladder") or s.get("tv_ladder") or "").split(",") if x.strip()]
     rc = str(job.get("rc_mode") or s.get("tv_rc") or "cqp").lower()
     kbps = as_float(job.get("bitrate_kbps") or s.get("tv_bitrate_kbps"), 0.0) if rc in ("2pass", "abr") else 0.0
+    crf = as_int(job.get("crf") or s.get("tv_crf"), 27) if rc == "crf" else 0
     return {"height": th, "qp": spec.qp, "gop": spec.gop, "search_range": spec.search_range, "deblock": spec.deblock,
             "sao": spec.sao, "software": spec.software, "ladder": ladder or None, "bitrate_kbps": kbps,
             "segment_frames": max(spec.gop, as_int(s.get("tv_node_segment_frames"), 256)),
             "mode": str(s.get("tv_node_mode") or "direct"), "batch_segments": as_int(s.get("tv_node_batch"), 8),
-            "settings_ok": as_bool(s.get("tv_node_executor"), True)}
+            "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc}
 
 
 def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, log) -> None:
@@ -174,7 +175,7 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                       segment_frames=p["segment_frames"], mode=p["mode"], bitrate_kbps=p["bitrate_kbps"],
                       ladder=p["ladder"], search_range=p["search_range"], software=p["software"],
                       batch_segments=p["batch_segments"], hooks=hooks, deblock=p["deblock"], sao=p["sao"],
-                      cache=None if p["software"] else cache)
+                      cache=None if p["software"] else cache, crf=p["crf"])
     except Exception as e:
         if rank == 0:
             log.error("[%s] node job failed:\n%s", job_id, traceback.format_exc())

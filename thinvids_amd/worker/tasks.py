@@ -99,7 +99,9 @@ def encode_spec_for_job(job: dict, settings: dict | None = None) -> EncodeSpec:
     return EncodeSpec(width=ow, height=oh, qp=as_int(job.get("qp") or s.get("tv_qp"), get_config().qp),
                       gop=max(1, as_int(s.get("tv_gop"), 64)), search_range=max(16, min(128, as_int(s.get("tv_search_range"), 64) // 16 * 16)),
                       deblock=as_bool(s.get("tv_deblock"), True), sao=as_bool(s.get("tv_sao"), True),
-                      software=as_bool(job.get("software_encode")))
+                      software=as_bool(job.get("software_encode")),
+                      crf=as_int(job.get("crf") or s.get("tv_crf"), 27)
+                      if str(job.get("rc_mode") or s.get("tv_rc") or "cqp").lower() == "crf" else 0)
 
 
 # =====================================================================  transcode
