@@ -104,7 +104,7 @@ def test_node_job_world2(tmp_path, source, kw):
     assert len(dec.frames) == 24
     assert min(hevc.psnr(a[0], b[0]) for a, b in zip(frames, dec.frames)) > 28
     if kw.get("bitrate_kbps"):
-        assert res["passes"] == 2 and len(res["qp_plan"][0]) == 3
+        assert res["passes"] in (2, 3) and len(res["qp_plan"][0]) == 3
 
 
 def test_node_job_ladder_single_process(tmp_path, source):
@@ -303,7 +303,7 @@ def test_two_pass_rate_control_hits_target_on_two_ranks(tmp_path, frac):
     res_path = str(tmp_path / "res.json")
     mp.spawn(_rc_worker, args=(2, _free_port(), src, str(tmp_path / "o.mp4"), target, res_path), nprocs=2, join=True)
     res = json.load(open(res_path))
-    assert res["passes"] == 2
+    assert res["passes"] in (2, 3)
     got = res["outputs"][0]["kbps"]
     assert abs(got / target - 1) < 0.05, (got, target)
     with open(tmp_path / "o.mp4", "rb") as f:
@@ -323,7 +323,7 @@ def test_two_pass_rate_control_gpu_engine(tmp_path, monkeypatch):
     r1 = run_job(src, str(tmp_path / "a.mp4"), gop=16, segment_frames=16)
     target = r1["outputs"][0]["kbps"] * 0.6
     r2 = run_job(src, str(tmp_path / "b.mp4"), gop=16, segment_frames=16, bitrate_kbps=target)
-    assert r2["passes"] == 2 and abs(r2["outputs"][0]["kbps"] / target - 1) < 0.05, (r2["outputs"], target)
+    assert r2["passes"] in (2, 3) and abs(r2["outputs"][0]["kbps"] / target - 1) < 0.05, (r2["outputs"], target)
 
 
 @pytest.mark.gpu

@@ -32,7 +32,7 @@ import time
 
 import numpy as np
 
-from ..models.ratecontrol import RateFeedback, frame_sizes, plan_frame_qps, predict_bits, round_qps
+from ..models.ratecontrol import SLOPE, RateFeedback, frame_sizes, plan_frame_qps, predict_bits, round_qps
 from ..utils import fault, trace
 
 
@@ -511,10 +511,31 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             per_seg, _ = plan_frame_qps([rc["b1"][(r, i)] for i in range(len(segs))], qp, target)
             plan.append(per_seg)
         rc["plan"] = plan
-        rc["bits"] = {}
-        passes = 2
-        quality.clear()
-    mine = agreed_pass()
+        targets = [bitrate_kbps * 1000 * nfr / fps * (rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]
+        passes = 1
+        for _ in range(2):  # pass 2, plus a secant-corrected pass 3 only when pass 2 misses by > 2.5 %
+            rc["bits"] = {}
+            rc["fb"] = RateFeedback()
+            quality.clear()
+            mine = agreed_pass()
+            passes += 1
+            got = np.zeros(len(rungs))
+            for (r, i), fb in rc["bits"].items():
+                if (r, i) in mine:
+                    got[r] += 8.0 * sum(fb)
+            got = allreduce_stats(got, cdev)
+            err = got / np.asarray(targets) - 1.0
+            if np.all(np.abs(err) <= 0.025):
+                break
+            # the response to a uniform QP shift around the pass-2 operating point: move
+            # every frame's plan by the rung's residual (the model slope only scales it)
+            for r in range(len(rungs)):
+                d = SLOPE * math.log2(max(got[r], 1.0) / targets[r])
+                plan[r] = [q + d for q in plan[r]]
+                for i in range(len(segs)):  # feedback baseline = pass-2 bits at the pass-2 QPs
+                    rc["b1"][(r, i)] = predict_bits(rc["b1"][(r, i)], 0, -d)
+    else:
+        mine = agreed_pass()
     t_enc = time.time() - t0
     # quality: per-rung frames + SSE of the segments encoded on this rank, all-reduced
     qv = np.zeros((len(rungs), 4))
