@@ -153,6 +153,8 @@ class Core {
     slot_bytes_ = align(B * nctu_ * 12) + align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * nctu_ * 8) +
                   align(B * nctu_ * 4) + align(B * nctu_ * 4) + align(B * 4) + align(B) + align(B * cap_ * 2);
     HIP_OK(hipHostMalloc(&qhost_, (size_t)c.gop * B, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc(&quni_, (size_t)B, hipHostMallocDefault));
+    std::memset(quni_, c.qp, (size_t)B);
     for (int k = 0; k < kSlots; ++k) {
       Slot& s = slots_[k];
       HIP_OK(hipMalloc(&s.dev, slot_bytes_));
@@ -205,6 +207,7 @@ class Core {
     (void)hipFree(ccost_);
     (void)hipFree(rc_);
     (void)hipHostFree(qhost_);
+    (void)hipHostFree(quni_);
     for (auto& s : slots_) {
       (void)hipFree(s.dev);
       (void)hipHostFree(s.host);
@@ -231,6 +234,7 @@ class Core {
     uint8_t* host = nullptr;
     hipEvent_t ev{};
     std::atomic<int> pending{0};
+    bool qp_dirty = true;  // the slot's device QP array may not hold the sequence QP
   };
   // carve one slot buffer (device or host) into its arrays
   struct Parts {
@@ -394,7 +398,16 @@ class Core {
     Slot& s = slots_[f % kSlots];
     wait_slot(s);
     const DecisionSet dec = slot_dec(s);
-    HIP_OK(hipMemcpyAsync(dec.qp, qhost_ + f * B, B, hipMemcpyHostToDevice, stream_));  // this frame's QPs
+    // this frame's QPs: copied only when they differ from what the slot already holds (a
+    // constant-QP stream pays nothing per frame; a QP map or CRF rewrites them every frame)
+    if (qmap_given_) {
+      HIP_OK(hipMemcpyAsync(dec.qp, qhost_ + f * B, B, hipMemcpyHostToDevice, stream_));
+      s.qp_dirty = true;
+    } else if (s.qp_dirty) {  // back to the sequence QP for every segment slot
+      HIP_OK(hipMemcpyAsync(dec.qp, quni_, cfg_.batch, hipMemcpyHostToDevice, stream_));
+      s.qp_dirty = false;
+    }
+    if (cfg_.crf > 0 && !qmap_given_) s.qp_dirty = true;  // k_rc_crf overwrites them
     upload(f, B);
     const int cur_i = f == 0 ? 0 : (fin_ + 1) % nrec_;
     FrameSet cur = rec_[cur_i], prev = rec_[fin_];
@@ -514,6 +527,7 @@ class Core {
   RcTables* rc_ = nullptr;
   bool qmap_given_ = false;  // an explicit QP map (2-pass plan) overrides in-engine CRF
   int8_t* qhost_ = nullptr;  // pinned [frame][segment] slice QPs of the current call
+  int8_t* quni_ = nullptr;   // pinned: the sequence QP for every segment slot
   hipStream_t stream_{};
   FrameSet src_{}, rec_[3]{};
   int nrec_ = 2, fin_ = 0;  // recon ring size; index of the last finished (reference) picture
