@@ -236,3 +236,43 @@ def test_unreadable_container_is_rejected_up_front(mgr):
     job = st.hgetall(f"job:{r.get_json()['job_id']}")
     assert job["status"] == "REJECTED" and job["rejected_reason"] == "probe_failed"
     assert "unsupported" in job["error"]
+
+
+def test_job_settings_encoder_overrides(mgr):
+    """Per-job encoder knobs from the settings modal reach the node/worker encode spec."""
+    c, st = mgr["c"], mgr["st"]
+    jid = c.post("/add_job", json={"filename": "movie.y4m", "force_paused": True}).json["job_id"]
+    r = c.post(f"/job_settings/{jid}", json={"rc_mode": "2pass", "qp": 30, "bitrate_kbps": "1500",
+                                              "ladder": "1080, 720", "node_executor": "0"})
+    assert r.status_code == 200
+    g = c.get(f"/job_settings/{jid}").json
+    assert g["rc_mode"] == "2pass" and g["qp"] == "30" and g["ladder"] == "1080,720" and g["node_executor"] == "0"
+    assert float(g["bitrate_kbps"]) == 1500.0
+    for bad in ({"rc_mode": "vbr"}, {"qp": 60}, {"crf": 0}, {"bitrate_kbps": -3}, {"ladder": "10"}):
+        assert c.post(f"/job_settings/{jid}", json=bad).status_code == 500, bad
+    assert st.hget(f"job:{jid}", "rc_mode") == "2pass"  # rejected payloads change nothing
+    assert c.post(f"/job_settings/{jid}", json={"qp": "", "rc_mode": ""}).status_code == 200
+    assert st.hget(f"job:{jid}", "qp") == "" and st.hget(f"job:{jid}", "rc_mode") == ""
+    from thinvids_amd.worker.node_executor import _job_params
+
+    job = {**st.hgetall(f"job:{jid}"), "source_width": 1920, "source_height": 1080, "rc_mode": "crf", "crf": "24"}
+    p = _job_params(job)
+    assert p["rc"] == "crf" and p["crf"] == 24 and p["ladder"] == [1080, 720]
+
+
+def test_nodes_detail_fields(mgr):
+    c, st = mgr["c"], mgr["st"]
+    _heartbeat(st, "node1")
+    st.hset("metrics:node:node1", mapping={"hbm_used": str(3 << 30), "hbm_total": str(288 << 30),
+                                           "gpus_json": json.dumps([{"util": 50.0, "hbm_used": 1, "hbm_total": 2}])})
+    st.set("node:executor:node1", json.dumps({"world": 8, "pid": 42, "ts": time.time()}))
+    n = c.get("/nodes_data").json["nodes"][0]
+    assert n["executor"]["world"] == 8 and n["gpus"][0]["util"] == 50.0 and n["hbm_total"] == 288 << 30
+    st.hset("metrics:node:node1", "gpus_json", "{bad")
+    n = c.get("/nodes_data").json["nodes"][0]
+    assert n["gpus"] == []
+    # the pages carry the modal / chart hooks the scripts drive
+    html = c.get("/").get_data(as_text=True)
+    assert 'id="jobset"' in html and 'id="video"' in html and "function step(" in html
+    assert "TVHIST" in c.get("/metrics").get_data(as_text=True)
+    assert "function detail(" in c.get("/nodes").get_data(as_text=True)

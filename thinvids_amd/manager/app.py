@@ -319,6 +319,43 @@ def settings_from_payload(p: dict, cur: dict) -> dict:
 
 
 # ------------------------------------------------------------------------- app
+RC_MODES = ("", "cqp", "crf", "2pass", "abr")
+
+
+def encoder_overrides(d: dict) -> dict:
+    """Validated per-job encoder overrides from a job-settings payload (only the keys
+    present; "" clears an override so the global tv_* setting applies).  Raises ValueError
+    on out-of-range values."""
+    out = {}
+    if "rc_mode" in d:
+        rc = str(d["rc_mode"] or "").lower()
+        if rc not in RC_MODES:
+            raise ValueError(f"rc_mode must be one of {RC_MODES[1:]}")
+        out["rc_mode"] = rc
+    for k, lo, hi in (("qp", 0, 51), ("crf", 1, 51)):
+        if k in d:
+            v = d[k]
+            if v in ("", None):
+                out[k] = ""
+            elif not lo <= int(v) <= hi:
+                raise ValueError(f"{k} out of range")
+            else:
+                out[k] = int(v)
+    if "bitrate_kbps" in d:
+        v = d["bitrate_kbps"]
+        out["bitrate_kbps"] = "" if v in ("", None) else float(v)
+        if out["bitrate_kbps"] != "" and out["bitrate_kbps"] <= 0:
+            raise ValueError("bitrate_kbps must be positive")
+    if "ladder" in d:
+        rungs = [int(x) for x in str(d["ladder"] or "").replace(" ", "").split(",") if x]
+        if any(not 64 <= r <= 4320 for r in rungs):
+            raise ValueError("ladder rungs must be heights in 64..4320")
+        out["ladder"] = ",".join(str(r) for r in rungs)
+    if "node_executor" in d:
+        out["node_executor"] = "" if d["node_executor"] in ("", None) else ("1" if as_bool(d["node_executor"]) else "0")
+    return out
+
+
 def create_app(store=None, housekeeping: bool = False) -> Flask:
     here = os.path.dirname(os.path.abspath(__file__))
     app = Flask("thinvids_manager", template_folder=os.path.join(here, "templates"),
@@ -421,6 +458,23 @@ def create_app(store=None, housekeeping: bool = False) -> Flask:
         return jsonify({"status": "ok", **root, "path": rel, "parent": parent, "dirs": dirs, "files": files})
 
     # ------------------------------------------------------ nodes/metrics
+    def _json_list(v):
+        try:
+            d = json.loads(v or "[]")
+        except ValueError:
+            return []
+        return d if isinstance(d, list) else []
+
+    def _executor_info(host):
+        raw = st().get(f"node:executor:{host}")
+        if not raw:
+            return None
+        try:
+            d = json.loads(raw)
+        except ValueError:
+            return None
+        return {"world": as_int(d.get("world"), 0), "pid": as_int(d.get("pid"), 0), "ts": as_float(d.get("ts"))}
+
     @app.get("/nodes_data")
     def nodes_data():
         nodes = core.get_all_nodes(st())
@@ -440,7 +494,12 @@ def create_app(store=None, housekeeping: bool = False) -> Flask:
                           "worker_role": roles.get(h, "disabled" if n["disabled"] else "encode"),
                           "gpu_count": as_int(md.get("gpu_count"), 0), "gpu_name": md.get("gpu_name", ""),
                           "quarantine_reason": q.get("reason") or "",
-                          "quarantined_at": as_float(q.get("quarantined_at"))})
+                          "quarantined_at": as_float(q.get("quarantined_at")),
+                          # detail panel: live utilisation and the node executor's rank group
+                          "cpu": as_float(md.get("cpu")), "mem": as_float(md.get("mem")),
+                          "gpu": as_float(md.get("gpu"), -1.0), "hbm_used": as_int(md.get("hbm_used")),
+                          "hbm_total": as_int(md.get("hbm_total")), "disk": as_int(md.get("disk")),
+                          "gpus": _json_list(md.get("gpus_json")), "executor": _executor_info(h)})
         items.sort(key=lambda x: natural_host_key(x["hostname"]))
         return jsonify({"nodes": items})
 
@@ -822,7 +881,12 @@ def create_app(store=None, housekeeping: bool = False) -> Flask:
                             "target_height": normalize_target_height(job.get("target_height")),
                             "streams": job.get("streams_json") or "[]",
                             "selected_v_stream": job.get("selected_v_stream", "0"),
-                            "selected_a_stream": job.get("selected_a_stream", "0")})
+                            "selected_a_stream": job.get("selected_a_stream", "0"),
+                            # encoder knobs of this framework (per-job overrides of tv_*)
+                            "rc_mode": job.get("rc_mode", ""), "qp": job.get("qp", ""), "crf": job.get("crf", ""),
+                            "bitrate_kbps": job.get("bitrate_kbps", ""), "ladder": job.get("ladder", ""),
+                            "node_executor": job.get("node_executor", ""),
+                            "source_fps": job.get("source_fps", "")})
         if core.job_status(job) == Status.RUNNING:
             return jsonify({"error": "Job is RUNNING; stop it or copy/restart to change settings."}), 400
         d = request.get_json(silent=True) or {}
@@ -838,8 +902,9 @@ def create_app(store=None, housekeeping: bool = False) -> Flask:
                        "target_height": normalize_target_height(d.get("target_height", job.get("target_height")))}
             if "number_parts" in d:
                 mapping["number_parts_override"] = "1"
-        except (TypeError, ValueError):
-            return jsonify({"error": "Failed to update settings"}), 500
+            mapping.update(encoder_overrides(d))
+        except (TypeError, ValueError) as e:
+            return jsonify({"error": f"Failed to update settings: {e}"}), 500
         st().hset(key, mapping=mapping)
         caches["jobs"] = (0.0, None)
         return jsonify({"status": "ok"}), 200
