@@ -286,29 +286,94 @@ def build_final_path(watch_root: Path, title: str, year: str | None, height: int
     return unique_path(Path(watch_root) / subdir / name / f"{name} {int(height)}p {codec}{suffix}")
 
 
+def stream_language(stream: dict) -> str:
+    """ffprobe tags.language, else MakeMKV's lang_code / lang_name."""
+    for v in ((stream.get("tags") or {}).get("language"), stream.get("language"), stream.get("lang_code"),
+              stream.get("lang_name")):
+        if str(v or "").strip():
+            return str(v).strip().lower()
+    return ""
+
+
 def is_english(stream: dict) -> bool:
-    return str(stream.get("lang_code") or stream.get("language") or "").strip().lower()[:3] in ENGLISH | {"eng"}
+    lang = stream_language(stream)
+    return lang in ENGLISH or lang == "english"
+
+
+def canonical_stream_type(stream: dict) -> str:
+    """"video" / "audio" / "subtitle" from ffprobe codec_type or MakeMKV's type field
+    ("Video", "Audio", "Subtitles")."""
+    k = str(stream.get("codec_type") or stream.get("type") or "").strip().lower()
+    return "video" if k.startswith("video") else "audio" if k.startswith("audio") else \
+        "subtitle" if k.startswith("sub") else k
+
+
+def stream_codec(stream: dict) -> str:
+    return str(stream.get("codec_name") or stream.get("codec_short") or stream.get("codec_long") or "").strip().lower()
+
+
+def choose_default_audio(audio: list[dict]) -> dict | None:
+    """English AC-3 first (the DVD main mix), then any English track, then the first."""
+    return (next((s for s in audio if is_english(s) and stream_codec(s) == "ac3"), None)
+            or next((s for s in audio if is_english(s)), None) or (audio[0] if audio else None))
+
+
+def choose_default_subtitle(subs: list[dict]) -> dict | None:
+    return next((s for s in subs if is_english(s)), None)
 
 
 def remux_plan(streams: list[dict]) -> dict:
-    """Stream selection for the remux: all video, the default (English-first) audio, every
-    English subtitle."""
-    kind = lambda s: str(s.get("type") or s.get("codec_type") or "").lower()
-    video = [s for s in streams if kind(s).startswith("video")]
-    audio = [s for s in streams if kind(s).startswith("audio")]
-    subs = [s for s in streams if kind(s).startswith("subtitle")]
-    a = next((s for s in audio if is_english(s)), audio[0] if audio else None)
-    return {"video": [s["index"] for s in video], "audio": [a["index"]] if a else [],
-            "subtitles": [s["index"] for s in subs if is_english(s)]}
+    """Stream selection for the remux: all video, the default audio, every English
+    subtitle."""
+    by = lambda k: [s for s in streams if canonical_stream_type(s) == k]
+    a = choose_default_audio(by("audio"))
+    return {"video": [s["index"] for s in by("video")], "audio": [a["index"]] if a else [],
+            "subtitles": [s["index"] for s in by("subtitle") if is_english(s)]}
 
 
 def stage_for_manual_review(mkv: Path, staging: Path, meta: dict) -> Path:
-    staging.mkdir(parents=True, exist_ok=True)
-    dest = unique_path(staging / mkv.name)
-    shutil.move(str(mkv), dest)
-    with open(dest.with_suffix(".json"), "w") as f:
-        json.dump({**meta, "staged_path": str(dest)}, f, indent=2)
-    return dest
+    """Move a low-confidence rip into a new staging bundle (see :mod:`.bundle`)."""
+    from .bundle import stage
+
+    return stage(mkv, meta, staging, str(meta.get("disc_label") or ""), str(meta.get("title") or "")).mkv
+
+
+# ------------------------------------------------------------- configuration
+def load_env_file(path) -> dict:
+    """KEY=value lines of a shell-style defaults file (``export`` and quotes allowed)."""
+    import shlex
+
+    p = Path(path).expanduser()
+    if not p.is_file():
+        return {}
+    out = {}
+    for line in p.read_text(encoding="utf-8").splitlines():
+        line = line.strip()
+        if not line or line.startswith("#"):
+            continue
+        if line.startswith("export "):
+            line = line[7:].strip()
+        m = re.match(r"^([A-Za-z_][A-Za-z0-9_]*)=(.*)$", line)
+        if not m:
+            continue
+        try:
+            v = " ".join(shlex.split(m.group(2))) if m.group(2).strip() else ""
+        except ValueError:
+            v = m.group(2).strip()
+        out[m.group(1)] = v
+    return out
+
+
+def configured(file_cfg: dict, *names: str, fallback=None, cast=str):
+    """First non-empty of the environment variables `names`, then the defaults file's
+    entry for names[0], else `fallback` (also when the value does not parse)."""
+    for v in [os.environ.get(n) for n in names] + [file_cfg.get(names[0])]:
+        if v not in (None, ""):
+            try:
+                return cast(v)
+            except ValueError:
+                return fallback
+    return fallback
 
 
 def submit_add_job(manager_url: str, rel_filename: str, input_path: str | None = None, post=None) -> dict:
@@ -317,53 +382,14 @@ def submit_add_job(manager_url: str, rel_filename: str, input_path: str | None =
     payload = {"filename": rel_filename, "mark_watcher_processed": True}
     if input_path:
         payload["input_path"] = input_path
-    r = (post or requests.post)(manager_url.rstrip("/") + "/add_job", json=payload, timeout=20)
+    url = manager_url.rstrip("/")
+    url = url if url.endswith("/add_job") else url + "/add_job"
+    r = (post or requests.post)(url, json=payload, timeout=20)
     return r.json()
 
 
 # ---------------------------------------------------------------------- CLI
-def _run(cmd: list[str], timeout: int = 7200) -> subprocess.CompletedProcess:
-    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+def main(argv=None) -> int:  # pragma: no cover - thin wrapper, see cli.run
+    from .cli import main as _main
 
-
-def main(argv=None) -> int:  # pragma: no cover - needs a drive + makemkvcon
-    import argparse
-
-    ap = argparse.ArgumentParser(description="Rip the main title of a DVD and queue it for transcoding")
-    ap.add_argument("--source", default="disc:0")
-    ap.add_argument("--watch-root", default=os.environ.get("WATCH_ROOT", "/watch"))
-    ap.add_argument("--staging", default=os.environ.get("THINVIDS_DVD_STAGING", "/watch/.staging"))
-    ap.add_argument("--manager", default=os.environ.get("THINVIDS_MANAGER_URL", "http://127.0.0.1:5005"))
-    ap.add_argument("--disc-label", default="")
-    ap.add_argument("--min-seconds", type=int, default=int(os.environ.get("THINVIDS_DVD_MIN_SECONDS", "2400")))
-    ap.add_argument("--min-score", type=float, default=float(os.environ.get("THINVIDS_DVD_AUTO_TITLE_MIN_SCORE", "70")))
-    ap.add_argument("--dry-run", action="store_true")
-    a = ap.parse_args(argv)
-    if not shutil.which("makemkvcon"):
-        print("makemkvcon not installed", file=sys.stderr)
-        return 2
-    info = _run(["makemkvcon", "--robot", "--noscan", "info", a.source])
-    parsed = parse_makemkv_robot_output(info.stdout)
-    title = choose_main_title(parsed, a.min_seconds)
-    key = os.environ.get("TMDB_API_KEY")
-    meta = auto_detect_movie_metadata(parsed, title, a.disc_label, tmdb=Tmdb(key) if key else None,
-                                      min_score=a.min_score)
-    print(json.dumps({"title_index": title["index"], "meta": meta}))
-    if a.dry_run:
-        return 0
-    tmp = Path(a.staging) / "rip"
-    tmp.mkdir(parents=True, exist_ok=True)
-    _run(["makemkvcon", "--robot", "mkv", a.source, str(title["index"]), str(tmp)])
-    mkvs = sorted(tmp.glob("*.mkv"))
-    if len(mkvs) != 1:
-        print(f"expected one MKV, found {len(mkvs)}", file=sys.stderr)
-        return 1
-    if meta["needs_manual_review"]:
-        print("staged for review:", stage_for_manual_review(mkvs[0], Path(a.staging), meta))
-        return 0
-    height = int(str(title.get("video_size") or "720x480").split("x")[-1] or 480)
-    final = build_final_path(Path(a.watch_root), meta["title"], meta.get("year"), height, codec="mpeg2")
-    final.parent.mkdir(parents=True, exist_ok=True)
-    shutil.move(str(mkvs[0]), final)
-    print(json.dumps(submit_add_job(a.manager, str(final.relative_to(a.watch_root)), str(final))))
-    return 0
+    return _main(argv)
