@@ -235,3 +235,77 @@ def _twice_worker(rank, world, port, src, out_dir):
     for k in (0, 1):
         run_job(src, os.path.join(out_dir, f"o{k}.mp4"), gop=8, segment_frames=8, software=True, batch_segments=1)
     dist.destroy_process_group()
+
+
+def _start_supervised(n, max_jobs=1):
+    from thinvids_amd.worker import node_executor
+
+    res = {}
+
+    def run():
+        res["rc"] = node_executor.main(["--gpus", str(n), "--max-jobs", str(max_jobs), "--idle-exit", "120"])
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    return t, res
+
+
+@pytest.mark.parametrize("fault", ["rank:1:die:1", "rank:1:hang:600"])
+def test_supervisor_recovers_from_dead_or_hung_rank_on_smaller_world(node_env, monkeypatch, fault):
+    """A rank that dies (or hangs mid-job) takes the communicator down: the supervisor kills
+    the group, quarantines that GPU, requeues the job and restarts on the remaining GPU; the
+    job resumes and completes on the smaller world."""
+    from thinvids_amd.common import save_settings
+    from thinvids_amd.parallel.elastic import quarantine_key
+    from thinvids_amd.worker.node_executor import live_executor
+
+    store, tmp = node_env["store"], node_env["tmp"]
+    save_settings({"tv_gop": "8", "tv_node_segment_frames": "8", "tv_node_batch": "1", "tv_sao": "0"}, store)
+    monkeypatch.setenv("TV_FORCE_CPU", "1")
+    monkeypatch.setenv("TV_FAULT", fault)
+    monkeypatch.setenv("TV_FAULT_STATE", str(tmp / "faults"))
+    monkeypatch.setenv("TV_NODE_STALL_SEC", "4")
+    th, res = _start_supervised(2)
+    t0 = time.time()
+    while live_executor(store) is None:
+        assert time.time() - t0 < 120, "executor did not come up"
+        time.sleep(0.1)
+    frames = [hevc.synth_frame(4, t, 128, 96) for t in range(32)]
+    job_id, tok, tasks = _submit(store, tmp, "clip.y4m", frames, software=True)
+    assert tasks.transcode.call_local(job_id, tok)["status"] == "QUEUED_NODE"
+    assert _wait(store, job_id, {"DONE", "FAILED"}, timeout=240) == "DONE", store.hgetall(f"job:{job_id}")
+    th.join(120)
+    assert res.get("rc") == 0
+    job = store.hgetall(f"job:{job_id}")
+    assert int(job["node_restarts"]) == 1 and int(job["node_world"]) == 1
+    assert ("exited with 86" if "die" in fault else "no progress") in job["node_last_failure"]
+    assert list(store.hgetall(quarantine_key("node-test"))) == ["1"]
+    with open(job["output_path"], "rb") as f:
+        dec = hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False)
+    assert len(dec.frames) == 32
+
+
+def test_supervisor_stall_culprit_and_requeue_budget(node_env, monkeypatch):
+    from thinvids_amd.parallel.elastic import RankBeat, Supervisor, rank_key
+    from thinvids_amd.worker.node_executor import _requeue, queue_key
+
+    store = node_env["store"]
+    sup = Supervisor([], [0, 1, 2], "h", store, stall_sec=5)
+    now = time.time()
+    beats = {0: {"job": {"job_id": "a"}, "progress_ts": now - 2}, 1: {"job": {"job_id": "a"}, "progress_ts": now - 9},
+             2: {"job": None, "progress_ts": now - 100}}
+    assert sup._stalled(beats, 3) == 1  # oldest progress among ranks in the job
+    beats[1]["progress_ts"] = now - 1
+    assert sup._stalled(beats, 3) is None  # idle rank 2 never counts
+    b = RankBeat(store, "h", 0, gen=3, gpu=5, interval=0.05).start()
+    b.set_job({"job_id": "a", "run_token": "t"})
+    assert sup._beats(1, 3)[0]["gpu"] == 5 and sup._beats(1, 4) == {}
+    b.stop()
+    assert store.get(rank_key("h", 0)) is None
+    monkeypatch.setenv("TV_NODE_JOB_RESTARTS", "1")
+    store.hset("job:a", mapping={"job_id": "a", "filename": "x.y4m", "status": "RUNNING"})
+    rq = _requeue("h", lambda m: None)
+    assert rq({"job_id": "a", "run_token": "t"}, "rank 1 died") is True
+    assert json.loads(store.lpop(queue_key("h")))["run_token"] == "t"
+    assert rq({"job_id": "a", "run_token": "t"}, "rank 1 died") is False
+    assert store.hget("job:a", "status") == "FAILED" and "2 times" in store.hget("job:a", "error")

@@ -160,7 +160,12 @@ def pin_rank(local_rank: int, local_world: int) -> list[int]:
     which are created later).  No-op when TV_NO_PIN=1 or the platform lacks affinity."""
     if os.environ.get("TV_NO_PIN") == "1" or not hasattr(os, "sched_setaffinity"):
         return sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
-    cpus = plan_affinity(local_rank, local_world)
+    gpu_nodes = None
+    phys = [int(x) for x in os.environ.get("TV_PHYS_GPUS", "").split(",") if x.strip()]
+    if phys:  # a supervisor restarted this node on a subset of its GPUs (HIP_VISIBLE_DEVICES)
+        allg = gpu_numa_nodes()
+        gpu_nodes = [allg[g] if g < len(allg) else 0 for g in phys]
+    cpus = plan_affinity(local_rank, local_world, gpu_nodes=gpu_nodes)
     try:
         os.sched_setaffinity(0, cpus)
     except OSError:

@@ -22,6 +22,11 @@ start-up or HBM allocation.  Progress, heartbeats and cooperative halt go throug
 job-hash fields and keys as the split/encode/stitch path.
 
     python -m thinvids_amd.worker.node_executor --gpus 8        (self-launches 8 ranks)
+
+The launching process is a :class:`parallel.elastic.Supervisor`: when a rank dies or stops
+making progress mid-job, it kills the rank group (communicator abort), quarantines that
+GPU, requeues the job at the front of the node queue (it resumes from its per-segment
+checkpoints under ``<job dir>/ckpt``) and restarts on the remaining GPUs.
 """
 from __future__ import annotations
 
@@ -71,13 +76,16 @@ def submit(job_id: str, run_token: str | None, host: str, store=None) -> None:
 
 
 class _StoreHooks:
-    """node_job.JobHooks bound to the job hash (every rank reports its own segments)."""
+    """node_job.JobHooks bound to the job hash (every rank reports its own segments) and to
+    the rank heartbeat (per-segment progress, which the supervisor's stall detection reads)."""
 
-    def __init__(self, job_id: str, total: int, stage_t0: float):
-        self.job_id, self.total, self.t0 = job_id, total, stage_t0
+    def __init__(self, job_id: str, total: int, stage_t0: float, beat=None):
+        self.job_id, self.total, self.t0, self.beat = job_id, total, stage_t0, beat
         self._halt_checked, self._halted = 0.0, False
 
     def segment_done(self, frames: int) -> None:
+        if self.beat is not None:
+            self.beat.progress("segment")
         st = get_store()
         k = job_key(self.job_id)
         p = st.pipeline()
@@ -118,11 +126,16 @@ def _job_params(job: dict) -> dict:
             "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc}
 
 
-def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, log) -> None:
+class CommFailure(RuntimeError):
+    """The rank group's communicator failed: the supervisor re-initialises it."""
+
+
+def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, log, beat=None) -> None:
     """Run one job on every rank (called collectively)."""
     import torch.distributed as dist
 
     from ..models import media
+    from ..parallel.elastic import is_comm_failure
     from ..parallel.node_job import plan_segments, run_job
 
     st = get_store()
@@ -140,7 +153,7 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                 job.update(source_width=info["width"], source_height=info["height"])
                 params = _job_params(job)
                 segs = plan_segments(int(info["frames"]), params["segment_frames"], params["gop"])
-                reset_job_run_state(job_id, job)
+                reset_job_run_state(job_id, job)  # keeps <base>/ckpt: a requeued job resumes
                 t0 = now()
                 base = job_base_dir(job_id, job)
                 ensure_dirs(base)
@@ -160,7 +173,8 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                 job_heartbeat(job_id, "transcode", force=True)
                 emit_activity(f'Starting "{job_title(job)}" on {world} GPU rank(s)', job_id=job_id,
                               filename=job.get("filename"), stage="start", source="worker")
-                box[0] = {"job": job, "path": path, "params": params, "segs": len(segs), "t0": t0, "base": base}
+                box[0] = {"job": job, "path": path, "params": params, "segs": len(segs), "t0": t0, "base": base,
+                          "ckpt": os.path.join(base, "ckpt")}
             except Exception as e:  # probe / planning failure
                 _fail(job_id, f"node plan failed: {e}", "split")
     dist.broadcast_object_list(box, src=0, group=_gloo())
@@ -168,15 +182,22 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
     if spec is None:
         return
     p = spec["params"]
-    hooks = _StoreHooks(job_id, spec["segs"], spec["t0"])
+    if beat is not None:
+        beat.set_job({"job_id": job_id, "run_token": run_token})
+    hooks = _StoreHooks(job_id, spec["segs"], spec["t0"], beat)
     out_local = os.path.join(spec["base"], f"job_{job_id}_output.mp4")
     try:
         res = run_job(spec["path"], out_local, height=p["height"], qp=p["qp"], gop=p["gop"],
                       segment_frames=p["segment_frames"], mode=p["mode"], bitrate_kbps=p["bitrate_kbps"],
                       ladder=p["ladder"], search_range=p["search_range"], software=p["software"],
                       batch_segments=p["batch_segments"], hooks=hooks, deblock=p["deblock"], sao=p["sao"],
-                      cache=None if p["software"] else cache, crf=p["crf"])
+                      cache=None if p["software"] else cache, crf=p["crf"], resume_dir=spec["ckpt"])
     except Exception as e:
+        if is_comm_failure(e):  # the job is fine, the communicator is not: requeue + re-init
+            log.error("[%s] communicator failure on rank %d: %s", job_id, rank, e)
+            raise CommFailure(str(e)) from e
+        if beat is not None:
+            beat.set_job(None)
         if rank == 0:
             log.error("[%s] node job failed:\n%s", job_id, traceback.format_exc())
             if is_job_halted(job_id):
@@ -185,6 +206,8 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
         return
     if rank == 0:
         _publish(job_id, spec, res)
+    if beat is not None:
+        beat.set_job(None)
 
 
 def _publish(job_id: str, spec: dict, res: dict) -> None:
@@ -260,6 +283,7 @@ def serve(host: str | None = None, max_jobs: int | None = None, idle_exit: float
     import torch
     import torch.distributed as dist
 
+    from ..parallel.elastic import EXIT_COMM, RankBeat
     from ..parallel.launch import pin_rank
     from .encoder import EngineCache, gpu_available
 
@@ -280,17 +304,22 @@ def serve(host: str | None = None, max_jobs: int | None = None, idle_exit: float
     cache = EngineCache(device=local, batch=int(os.environ.get("TV_NODE_ENGINE_BATCH", "0")), max_engines=6) if gpu else None
     st = get_store()
     stop = threading.Event()
+    gen = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+    phys = [int(x) for x in os.environ.get("TV_PHYS_GPUS", "").split(",") if x.strip()] or list(range(world))
+    rbeat = RankBeat(st, host, rank, gen, phys[local] if local < len(phys) else local).start()
     if rank == 0:
         st.sadd(EXECUTORS_KEY, host)
 
         def beat():
             while not stop.is_set():
-                st.set(alive_key(host), json.dumps({"world": world, "pid": os.getpid(), "ts": now()}), ex=ALIVE_TTL)
+                st.set(alive_key(host), json.dumps({"world": world, "pid": os.getpid(), "ts": now(), "gen": gen,
+                                                    "gpus": phys}), ex=ALIVE_TTL)
                 stop.wait(2.0)
 
         threading.Thread(target=beat, daemon=True, name="node-executor-beat").start()
         log.info("node executor on %s: %d rank(s), %s", host, world, "RCCL" if gpu else "gloo")
     done, idle_since = 0, time.monotonic()
+    code = 0
     try:
         while True:
             box = [None]
@@ -307,18 +336,51 @@ def serve(host: str | None = None, max_jobs: int | None = None, idle_exit: float
                 continue
             if msg.get("stop"):
                 break
-            execute(msg["job_id"], msg.get("run_token"), rank, world, cache, log)
+            try:
+                execute(msg["job_id"], msg.get("run_token"), rank, world, cache, log, rbeat)
+            except CommFailure:
+                code = EXIT_COMM  # leave the broken communicator to the supervisor
+                break
             done += 1
             if max_jobs is not None and done >= max_jobs:
                 break
     finally:
         stop.set()
-        if rank == 0:
+        if code == 0:  # a failing rank leaves its last beat (and job) for the supervisor
+            rbeat.stop()
+        if rank == 0 and code == 0:
             st.delete(alive_key(host))
-        if cache is not None:
+        if cache is not None and code == 0:
             cache.close()
-        dist.destroy_process_group()
+        if code == 0:
+            dist.destroy_process_group()
+    if code:
+        sys.stdout.flush()
+        os._exit(code)  # no teardown collectives on a dead communicator
     return 0
+
+
+def _requeue(host: str, log):
+    """Supervisor callback: put a failed generation's in-flight job back at the front of this
+    node's queue (it resumes from its segment checkpoints), or fail it once its restart
+    budget (TV_NODE_JOB_RESTARTS, default 3) is spent."""
+    def requeue(job: dict, reason: str) -> bool:
+        st = get_store()
+        jid = job.get("job_id")
+        if not jid:
+            return False
+        n = int(st.hincrby(job_key(jid), "node_restarts", 1))
+        if n > int(os.environ.get("TV_NODE_JOB_RESTARTS", "3")):
+            _fail(jid, f"node executor failed {n} times: {reason}", "encode")
+            return False
+        st.hset(job_key(jid), mapping={"node_last_failure": reason[:500]})
+        rec = st.hgetall(job_key(jid)) or {}
+        emit_activity(f'Requeueing "{job_title(rec)}" after {reason} (restart {n})', job_id=jid,
+                      filename=rec.get("filename"), stage="retry", source="worker")
+        st.lpush(queue_key(host), json.dumps({"job_id": jid, "run_token": job.get("run_token")}))
+        log(f"requeued {jid}: {reason}")
+        return True
+    return requeue
 
 
 def main(argv=None) -> int:
@@ -327,16 +389,29 @@ def main(argv=None) -> int:
     ap.add_argument("--host", default=None)
     ap.add_argument("--max-jobs", type=int, default=None)
     ap.add_argument("--idle-exit", type=float, default=None, help="exit after this many idle seconds")
+    ap.add_argument("--no-supervise", action="store_true", help="plain launch: no rank restart / GPU fallback")
     a = ap.parse_args(argv)
     from ..parallel.launch import launched_by_torchrun, spawn_ranks
 
     if not launched_by_torchrun():
         n = a.gpus
+        cpu = os.environ.get("TV_FORCE_CPU") == "1"
         if n is None:  # count devices without initialising HIP in this (launcher) process
             import torch
 
-            n = 1 if os.environ.get("TV_FORCE_CPU") == "1" else max(1, torch.cuda.device_count())
-        return spawn_ranks(n, ["-m", "thinvids_amd.worker.node_executor", *(argv if argv is not None else sys.argv[1:])])
+            n = 1 if cpu else max(1, torch.cuda.device_count())
+        rank_argv = ["-m", "thinvids_amd.worker.node_executor", *(argv if argv is not None else sys.argv[1:])]
+        if a.no_supervise:
+            return spawn_ranks(n, rank_argv)
+        from ..parallel.elastic import Supervisor
+
+        host = a.host or os.environ.get("TV_NODE_HOST") or os.environ.get("HOSTNAME") or "localhost"
+        log = get_logging("node-supervisor")
+        sup = Supervisor(rank_argv, list(range(n)), host, get_store(),
+                         stall_sec=float(os.environ.get("TV_NODE_STALL_SEC", "600")),
+                         max_restarts=int(os.environ.get("TV_NODE_MAX_RESTARTS", "8")),
+                         requeue=_requeue(host, log.warning), log=log.warning, cpu_mode=cpu)
+        return sup.run()
     return serve(a.host, a.max_jobs, a.idle_exit)
 
 
