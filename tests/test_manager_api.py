@@ -268,6 +268,8 @@ def test_nodes_detail_fields(mgr):
     st.set("node:executor:node1", json.dumps({"world": 8, "pid": 42, "ts": time.time()}))
     n = c.get("/nodes_data").json["nodes"][0]
     assert n["executor"]["world"] == 8 and n["gpus"][0]["util"] == 50.0 and n["hbm_total"] == 288 << 30
+    st.hset("node:gpu_quarantine:node1", "3", json.dumps({"reason": "rank 3 (GPU 3) exited with 86", "ts": 1}))
+    assert "exited" in c.get("/nodes_data").json["nodes"][0]["gpu_quarantine"]["3"]["reason"]
     st.hset("metrics:node:node1", "gpus_json", "{bad")
     n = c.get("/nodes_data").json["nodes"][0]
     assert n["gpus"] == []

@@ -499,7 +499,9 @@ def create_app(store=None, housekeeping: bool = False) -> Flask:
                           "cpu": as_float(md.get("cpu")), "mem": as_float(md.get("mem")),
                           "gpu": as_float(md.get("gpu"), -1.0), "hbm_used": as_int(md.get("hbm_used")),
                           "hbm_total": as_int(md.get("hbm_total")), "disk": as_int(md.get("disk")),
-                          "gpus": _json_list(md.get("gpus_json")), "executor": _executor_info(h)})
+                          "gpus": _json_list(md.get("gpus_json")), "executor": _executor_info(h),
+                          "gpu_quarantine": {g: (json.loads(v) if v.startswith("{") else {"reason": v})
+                                             for g, v in (st().hgetall(f"node:gpu_quarantine:{h}") or {}).items()}})
         items.sort(key=lambda x: natural_host_key(x["hostname"]))
         return jsonify({"nodes": items})
 
