@@ -78,6 +78,24 @@ template <int CTRL> __device__ __forceinline__ int mov(int v) {
 }
 }  // namespace dpp
 
+// ---- XCD-aware workgroup placement (guide T1) -------------------------------------------
+// Workgroups are dealt round-robin to the 8 XCDs, each with a private 4 MB L2.  Neighbouring
+// CTBs read overlapping reference windows / phase-plane rows (four CTBs share a 128-byte
+// line), so the default placement makes every XCD fetch the same lines.  Remap the linear
+// workgroup id so each XCD walks one contiguous run of the logical grid.  Bijective for any
+// grid size; placement only changes speed, never results.
+__device__ __forceinline__ int xcd_remap(int id, int n) {
+  const int per = (n + 7) >> 3, r = n & 7;  // r == 0: every XCD owns `per` workgroups
+  const int x = id & 7, s = id >> 3;
+  return x * per - (r && x > r ? x - r : 0) + s;
+}
+// (CTB, segment) of this workgroup in a gridDim = (CTBs, segments) launch
+__device__ __forceinline__ void xcd_ctb(int& ctu, int& b) {
+  const int L = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+  ctu = L % gridDim.x;
+  b = L / gridDim.x;
+}
+
 #ifdef TV_NO_DPP  // ds_bpermute reference implementations (debug builds)
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll

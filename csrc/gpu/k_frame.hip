@@ -147,8 +147,11 @@ __global__ void __launch_bounds__(256) k_sse(FrameSet a, FrameSet r, Geo g, unsi
 // horizontal half/quarter filters) are read once as dwords / 4 x int16 from LDS and reused
 // for the three vertical phases, and every plane is written with one dword store.
 __global__ void __launch_bounds__(256) k_phase_planes(FrameSet ref, uint8_t* phase, Geo g) {
-  const int b = blockIdx.z, tid = threadIdx.x;
-  const int tx0 = blockIdx.x * 32 - 8, ty0 = blockIdx.y * 32 - 8;
+  const int tid = threadIdx.x;
+  const int L = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                          gridDim.x * gridDim.y * gridDim.z);
+  const int tpf = gridDim.x * gridDim.y, b = L / tpf, tyi = (L - b * tpf) / gridDim.x;
+  const int tx0 = (L - b * tpf - tyi * gridDim.x) * 32 - 8, ty0 = tyi * 32 - 8;
   const uint8_t* R = ref.plane(0, b, g);
   // raw[rr][k] = sample (tx0 - 4 + k, ty0 - 3 + rr): column c of the tile sits at k = c + 4
   __shared__ __align__(16) uint8_t raw[39][40];
@@ -305,7 +308,9 @@ constexpr int kSaoT = 34;   // luma tile side with border
 constexpr int kSaoTc = 18;  // chroma
 __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, uint32_t* sao, Geo g,
                                                     const int8_t* qp, const RcTables* rc) {
-  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
+  int ctu, b;
+  xcd_ctb(ctu, b);
   const long long lam16 = rc->sao_lam16[qp[b]];
   const int cx = ctu % g.wc, cy = ctu / g.wc;
   __shared__ SaoStats st[3];

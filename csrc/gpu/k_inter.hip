@@ -102,7 +102,9 @@ constexpr int kCoarseWords = kCoarseMaxRq / 2 + 3;
 
 __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uint8_t* qprev, Geo g, const RcTables* rc,
                                                   int seq_qp, int rq, int16_t* cmv, int* ccost) {
-  const int ctu = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+  const int lane = threadIdx.x;
+  int ctu, b;
+  xcd_ctb(ctu, b);
   const Penalties& pen = rc->pen[seq_qp];  // lookahead: the frame QP may depend on its result
   const int qw = g.W >> 2, qh = g.H >> 2;
   const int x0 = 8 * (ctu % g.wc), y0 = 8 * (ctu / g.wc);
@@ -157,7 +159,9 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
 __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                          DecisionSet dec, const int16_t* prev_mv, const int16_t* cmv,
                                                          Geo g, const RcTables* rc, int range) {
-  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int tid = threadIdx.x;
+  int ctu, b;
+  xcd_ctb(ctu, b);
   const Penalties& pen = rc->pen[dec.qp[b]];
   const int cxi = ctu % g.wc, cyi = ctu / g.wc, cx = cxi * 32, cy = cyi * 32;
   const uint8_t* S = src.plane(0, b, g);
@@ -428,7 +432,9 @@ __device__ __forceinline__ bool pr_zeroed(const PReconLds& L, int id) {
 
 __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                      FrameSet rec, DecisionSet dec, Geo g) {
-  const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int ctu, b;
+  xcd_ctb(ctu, b);
   const int qp = dec.qp[b];
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
   const long ub = b * g.usz;
