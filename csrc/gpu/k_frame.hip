@@ -138,14 +138,41 @@ __global__ void __launch_bounds__(256) k_sse(FrameSet a, FrameSet r, Geo g, unsi
 // Plane p = fx + 4*fy holds the exact HEVC 8-tap interpolated luma sample at every integer
 // position of the padded domain [-8, W+8) x [-8, H+8) (beyond 4 samples outside the
 // picture the clamped interpolation is constant, so clamping the query to the pad is
-// exact).  Separable: the 3 horizontal phases are filtered once into LDS (int16), then the
-// 4 vertical phases of each.  Motion search and luma motion compensation then become
-// plain byte loads.
-// 16 quarter-sample phase planes of a reference frame (padded by 8 on every side), one
-// 32x32 output tile per block.  Each thread produces 4 horizontally adjacent samples of all
-// 16 planes: the 8 vertical taps of every source row set (integer samples + the three
-// horizontal half/quarter filters) are read once as dwords / 4 x int16 from LDS and reused
-// for the three vertical phases, and every plane is written with one dword store.
+// exact).  Motion search and luma motion compensation then become plain byte loads.
+//
+// One 32x32 output tile per workgroup, all 16 planes.  The 8-tap filters run on the packed
+// integer dot-product units instead of scalar multiply-adds:
+//  * horizontal (int8 samples): a sample window of 8 bytes is two dwords (v_alignbyte from
+//    the tile row held as dwords in LDS); samples are biased to signed bytes (x ^ 0x80) so
+//    each half is one v_dot4_i32_i8 against the packed taps, the bias is 128 * sum(taps) =
+//    8192 added back — 2 dot4 per output instead of 8 MACs;
+//  * vertical over integer rows: the 4x4 byte blocks of 8 rows are transposed with 16
+//    v_perm_b32, then 2 dot4 per output;
+//  * vertical over the 16-bit horizontal intermediates: row pairs are packed with v_perm and
+//    reduced with v_dot2_i32_i16 (4 per output).
+// Every product and sum is exact (|intermediate| < 2^15, |2-D sum| < 2^21): bit-identical
+// to tv::mc_luma_sample.
+typedef short tv_short2 __attribute__((ext_vector_type(2)));
+
+__device__ constexpr uint32_t pack_taps4(int f, int k0) {
+  return (uint32_t)(uint8_t)kLumaFilter[f][k0] | (uint32_t)(uint8_t)kLumaFilter[f][k0 + 1] << 8 |
+         (uint32_t)(uint8_t)kLumaFilter[f][k0 + 2] << 16 | (uint32_t)(uint8_t)kLumaFilter[f][k0 + 3] << 24;
+}
+__device__ constexpr uint32_t pack_taps2(int f, int k0) {
+  return (uint32_t)(uint16_t)kLumaFilter[f][k0] | (uint32_t)(uint16_t)kLumaFilter[f][k0 + 1] << 16;
+}
+__device__ __forceinline__ int dot4(uint32_t a, uint32_t b, int c) {
+  return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(tv_short2, a), __builtin_bit_cast(tv_short2, b), c, false);
+}
+__device__ __forceinline__ uint32_t pack4_pixels(int v0, int v1, int v2, int v3) {
+  return (uint32_t)clip_pixel(v0) | (uint32_t)clip_pixel(v1) << 8 | (uint32_t)clip_pixel(v2) << 16 |
+         (uint32_t)clip_pixel(v3) << 24;
+}
+
+constexpr int kPhW = 10;  // dwords per staged source row: 40 bytes = tile 32 + 8 tap reach
 __global__ void __launch_bounds__(256) k_phase_planes(FrameSet ref, uint8_t* phase, Geo g) {
   const int tid = threadIdx.x;
   const int L = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
@@ -153,83 +180,111 @@ __global__ void __launch_bounds__(256) k_phase_planes(FrameSet ref, uint8_t* pha
   const int tpf = gridDim.x * gridDim.y, b = L / tpf, tyi = (L - b * tpf) / gridDim.x;
   const int tx0 = (L - b * tpf - tyi * gridDim.x) * 32 - 8, ty0 = tyi * 32 - 8;
   const uint8_t* R = ref.plane(0, b, g);
-  // raw[rr][k] = sample (tx0 - 4 + k, ty0 - 3 + rr): column c of the tile sits at k = c + 4
-  __shared__ __align__(16) uint8_t raw[39][40];
+  // raw[rr] dword w = samples (tx0 - 4 + 4w .. +3, ty0 - 3 + rr), clamped, biased to int8
+  __shared__ uint32_t raw[39][kPhW];
+  // hf[fx-1][rr][c]: horizontal filter fx at (tx0 + c, ty0 - 3 + rr)
   __shared__ __align__(16) int16_t hf[3][39][32];
-  for (int i = tid; i < 39 * 40; i += 256) {
-    const int rr = i / 40, k = i % 40;
-    const int X = clip3(0, g.W - 1, tx0 - 4 + k), Y = clip3(0, g.H - 1, ty0 - 3 + rr);
-    raw[rr][k] = R[(long)Y * g.W + X];
+  for (int i = tid; i < 39 * kPhW; i += 256) {
+    const int rr = i / kPhW, w = i - rr * kPhW;
+    const uint8_t* row = R + (long)clip3(0, g.H - 1, ty0 - 3 + rr) * g.W;
+    const int x = tx0 - 4 + 4 * w;
+    uint32_t v;
+    if (x >= 0 && x + 3 < g.W) {
+      v = *reinterpret_cast<const uint32_t*>(row + x);  // x is 4-aligned (tx0 = 32k - 8)
+    } else {
+      v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v |= (uint32_t)row[clip3(0, g.W - 1, x + k)] << (8 * k);
+    }
+    raw[rr][w] = v ^ 0x80808080u;
   }
   __syncthreads();
-  for (int i = tid; i < 3 * 39 * 32; i += 256) {
-    const int fx = 1 + i / (39 * 32), rem = i % (39 * 32), rr = rem / 32, c = rem % 32;
-    int v = 0;
+  // horizontal pass: item = (row, 4 output columns), the 3 fractional filters at once
+  for (int i = tid; i < 39 * 8; i += 256) {
+    const int rr = i >> 3, c4 = i & 7;
+    // column c = 4*c4 + j takes bytes c+1 .. c+8 of the row (taps at x-3 .. x+4)
+    const uint32_t w0 = raw[rr][c4], w1 = raw[rr][c4 + 1], w2 = raw[rr][c4 + 2];
+    int out[3][4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v += kLumaFilter[fx][k] * raw[rr][c + k + 1];
-    hf[fx - 1][rr][c] = (int16_t)v;
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = j == 3 ? w1 : __builtin_amdgcn_alignbyte(w1, w0, j + 1);
+      const uint32_t hi = j == 3 ? w2 : __builtin_amdgcn_alignbyte(w2, w1, j + 1);
+#pragma unroll
+      for (int f = 1; f < 4; ++f) out[f - 1][j] = dot4(lo, pack_taps4(f, 0), dot4(hi, pack_taps4(f, 4), 8192));
+    }
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      uint2 v;
+      v.x = (uint32_t)(uint16_t)out[f][0] | (uint32_t)out[f][1] << 16;
+      v.y = (uint32_t)(uint16_t)out[f][2] | (uint32_t)out[f][3] << 16;
+      *reinterpret_cast<uint2*>(&hf[f][rr][4 * c4]) = v;
+    }
   }
   __syncthreads();
   const int r = tid >> 3, c0 = (tid & 7) * 4;
   const int X = tx0 + c0, Y = ty0 + r;
   if (X + 8 >= g.pw16 || Y >= g.H + 8) return;
   uint8_t* base = phase + (long)b * 16 * g.psz + (long)(Y + 8) * g.pw16 + (X + 8);
-  auto put = [&](int plane, const int (&v)[4]) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w |= (uint32_t)clip_pixel((v[j] + 32) >> 6) << (8 * j);
-    *reinterpret_cast<uint32_t*>(base + (long)plane * g.psz) = w;
-  };
-  // integer column source: 8 rows x 4 samples
+  auto store = [&](int plane, uint32_t w) { *reinterpret_cast<uint32_t*>(base + (long)plane * g.psz) = w; };
+  // ---- fx = 0: integer column, rows Y-3 .. Y+4 = raw rows r .. r+7, word c0/4 + 1
   {
-    int col[8][4];
+    uint32_t R8[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(&raw[r + k][c0 + 4]);
+    for (int k = 0; k < 8; ++k) R8[k] = raw[r + k][(c0 >> 2) + 1];
+    store(0, R8[3] ^ 0x80808080u);
+    uint32_t C[2][4];  // C[h][j]: column j, rows 4h .. 4h+3 (one byte each)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) col[k][j] = (w >> (8 * j)) & 255;
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t* q = R8 + 4 * h;
+      const uint32_t t01l = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u);
+      const uint32_t t01h = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);
+      const uint32_t t23l = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u);
+      const uint32_t t23h = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
+      C[h][0] = __builtin_amdgcn_perm(t23l, t01l, 0x05040100u);
+      C[h][1] = __builtin_amdgcn_perm(t23l, t01l, 0x07060302u);
+      C[h][2] = __builtin_amdgcn_perm(t23h, t01h, 0x05040100u);
+      C[h][3] = __builtin_amdgcn_perm(t23h, t01h, 0x07060302u);
     }
-    int v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = col[3][j] << 6;
-    put(0, v);
 #pragma unroll
     for (int fy = 1; fy < 4; ++fy) {
+      int v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        int a = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) a += kLumaFilter[fy][k] * col[k][j];
-        v[j] = a;
-      }
-      put(4 * fy, v);
+      for (int j = 0; j < 4; ++j)
+        v[j] = (dot4(C[0][j], pack_taps4(fy, 0), dot4(C[1][j], pack_taps4(fy, 4), 8192)) + 32) >> 6;
+      store(4 * fy, pack4_pixels(v[0], v[1], v[2], v[3]));
     }
   }
+  // ---- fx = 1..3: vertical over the int16 intermediates, row pairs packed for v_dot2
 #pragma unroll
   for (int fx = 1; fx < 4; ++fx) {
-    int col[8][4];
+    uint2 H8[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint2 w = *reinterpret_cast<const uint2*>(&hf[fx - 1][r + k][c0]);
-      col[k][0] = (int16_t)(w.x & 0xffff);
-      col[k][1] = (int16_t)(w.x >> 16);
-      col[k][2] = (int16_t)(w.y & 0xffff);
-      col[k][3] = (int16_t)(w.y >> 16);
+    for (int k = 0; k < 8; ++k) H8[k] = *reinterpret_cast<const uint2*>(&hf[fx - 1][r + k][c0]);
+    {
+      const int h0 = (int16_t)(H8[3].x & 0xffff), h1 = (int16_t)(H8[3].x >> 16);
+      const int h2 = (int16_t)(H8[3].y & 0xffff), h3 = (int16_t)(H8[3].y >> 16);
+      store(fx, pack4_pixels((h0 + 32) >> 6, (h1 + 32) >> 6, (h2 + 32) >> 6, (h3 + 32) >> 6));
     }
-    int v[4];
+    uint32_t P[4][4];  // P[m][j]: column j, rows 2m (low half) and 2m + 1 (high half)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = col[3][j];
-    put(fx, v);
+    for (int m = 0; m < 4; ++m) {
+      P[m][0] = __builtin_amdgcn_perm(H8[2 * m + 1].x, H8[2 * m].x, 0x05040100u);
+      P[m][1] = __builtin_amdgcn_perm(H8[2 * m + 1].x, H8[2 * m].x, 0x07060302u);
+      P[m][2] = __builtin_amdgcn_perm(H8[2 * m + 1].y, H8[2 * m].y, 0x05040100u);
+      P[m][3] = __builtin_amdgcn_perm(H8[2 * m + 1].y, H8[2 * m].y, 0x07060302u);
+    }
 #pragma unroll
     for (int fy = 1; fy < 4; ++fy) {
+      int v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        int a = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) a += kLumaFilter[fy][k] * col[k][j];
-        v[j] = a >> 6;
+        int a = dot2(P[0][j], pack_taps2(fy, 0), 0);
+        a = dot2(P[1][j], pack_taps2(fy, 2), a);
+        a = dot2(P[2][j], pack_taps2(fy, 4), a);
+        a = dot2(P[3][j], pack_taps2(fy, 6), a);
+        v[j] = ((a >> 6) + 32) >> 6;
       }
-      put(fx + 4 * fy, v);
+      store(fx + 4 * fy, pack4_pixels(v[0], v[1], v[2], v[3]));
     }
   }
 }
