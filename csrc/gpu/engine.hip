@@ -123,6 +123,14 @@ class Core {
     if (c.width < 64 || c.height < 64) throw std::runtime_error("frame must be at least 64x64");
     HIP_OK(hipSetDevice(c.device));
     HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    {  // I-frame wavefront stream: highest priority, so its 100+ short dependent launches are
+       // dispatched ahead of the other stream group's queued P-frame workgroups
+      int lo = 0, hi = 0;
+      HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_OK(hipStreamCreateWithPriority(&istream_, hipStreamNonBlocking, hi));
+      HIP_OK(hipEventCreateWithFlags(&iev_[0], hipEventDisableTiming));
+      HIP_OK(hipEventCreateWithFlags(&iev_[1], hipEventDisableTiming));
+    }
     const long B = c.batch;
     nctu_ = g_.wc * g_.hc;
     auto alloc_set = [&](FrameSet& f) {
@@ -216,6 +224,9 @@ class Core {
     (void)hipEventDestroy(t0_);
     (void)hipEventDestroy(t1_);
     (void)hipStreamDestroy(stream_);
+    (void)hipEventDestroy(iev_[0]);
+    (void)hipEventDestroy(iev_[1]);
+    (void)hipStreamDestroy(istream_);
   }
 
   const std::vector<uint8_t>& segment(int b) const { return out_.at(b); }
@@ -426,8 +437,13 @@ class Core {
                        ccost_};
     if (f > 0) launch_coarse_me(me, g_, rc_, cfg_.qp, cfg_.range, B, stream_);
     if (cfg_.crf > 0 && !qmap_given_) launch_rc_crf(q_[f & 1], ccost_, dec.qp, g_, cfg_.crf, f == 0, B, stream_);
-    if (f == 0) launch_intra_frame(src_, cur, dec, g_, rc_, B, stream_);
-    else launch_inter_frame(src_, prev, phase_, cur, dec, g_, rc_, cfg_.range, me, B, stream_);
+    if (f == 0) {  // fork onto the priority stream and join back
+      HIP_OK(hipEventRecord(iev_[0], stream_));
+      HIP_OK(hipStreamWaitEvent(istream_, iev_[0], 0));
+      launch_intra_frame(src_, cur, dec, g_, rc_, B, istream_);
+      HIP_OK(hipEventRecord(iev_[1], istream_));
+      HIP_OK(hipStreamWaitEvent(stream_, iev_[1], 0));
+    } else launch_inter_frame(src_, prev, phase_, cur, dec, g_, rc_, cfg_.range, me, B, stream_);
     stage(f == 0 ? "intra" : "inter");
     launch_compact(dec, g_, slot_compact(s), B, stream_);
     stage("compact");
@@ -528,7 +544,8 @@ class Core {
   bool qmap_given_ = false;  // an explicit QP map (2-pass plan) overrides in-engine CRF
   int8_t* qhost_ = nullptr;  // pinned [frame][segment] slice QPs of the current call
   int8_t* quni_ = nullptr;   // pinned: the sequence QP for every segment slot
-  hipStream_t stream_{};
+  hipStream_t stream_{}, istream_{};
+  hipEvent_t iev_[2]{};
   FrameSet src_{}, rec_[3]{};
   int nrec_ = 2, fin_ = 0;  // recon ring size; index of the last finished (reference) picture
   int16_t *coef_y_ = nullptr, *coef_u_ = nullptr, *coef_v_ = nullptr;
