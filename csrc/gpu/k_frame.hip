@@ -9,8 +9,7 @@ namespace gpu {
 
 // ---------------------------------- synthetic source ------------------------------------
 // One workgroup row-tile; the per-frame object trajectories are evaluated once per
-// workgroup into LDS (they were 18 hashes per pixel before).  A sample covered by an object
-// evaluates only the topmost object's texture (no hidden layers).  Each thread produces 4
+// workgroup into LDS (they were 18 hashes per pixel before).  Each thread produces 4
 // horizontally adjacent samples (one dword store): the value-noise octaves keep their
 // lattice-corner hashes across the 4 samples (a cell is >= 4 px wide, so the cell changes at
 // most once: 2 new hashes instead of 4 per octave per sample), and the row terms (cell row,
@@ -51,30 +50,23 @@ struct VNoiseRow {
   }
 };
 
-// Topmost object covering luma-grid sample (xl, yl), or -1.  Objects are drawn in index
-// order (later on top), so the search runs top-down and stops at the first hit: covered
-// samples evaluate one object's texture (tv::synth_sample_ctx evaluates every layer and
-// keeps the last: same value).
-__device__ __forceinline__ int synth_top_object(const SynthFrameCtx& f, int xl, int yl, int32_t& rx16, int32_t& ry16) {
-  for (int k = kSynthObjects - 1; k >= 0; --k) {
+__device__ __forceinline__ int synth_objects(const SynthFrameCtx& f, int c, int xl, int yl, int v) {
+  for (int k = 0; k < kSynthObjects; ++k) {  // later objects on top
     const SynthObject& o = f.obj[k];
-    rx16 = xl * 16 - f.ox[k];
-    ry16 = yl * 16 - f.oy[k];
+    const int32_t rx16 = xl * 16 - f.ox[k], ry16 = yl * 16 - f.oy[k];
     if (rx16 < 0 || ry16 < 0 || rx16 >= o.w * 16 || ry16 >= o.h * 16) continue;
     if (o.shape == 1) {
       const int64_t dx = 2 * (int64_t)rx16 - o.w * 16, dy = 2 * (int64_t)ry16 - o.h * 16;
       const int64_t ww = (int64_t)o.w * 16, hh = (int64_t)o.h * 16;
       if (dx * dx * hh * hh + dy * dy * ww * ww > ww * ww * hh * hh) continue;
     }
-    return k;
+    if (c == 0) {
+      v = 40 + ((synth_vnoise(rx16, ry16, 4, o.seed) * 3 + synth_vnoise(rx16, ry16, 2, o.seed + 5)) >> 2) * 3 / 4;
+    } else {
+      v = 64 + (int)(synth_hash(k, c, f.seed) & 127) + (synth_vnoise(rx16, ry16, 5, o.seed + c) >> 3);
+    }
   }
-  return -1;
-}
-__device__ __forceinline__ int synth_object_value(const SynthFrameCtx& f, int c, int k, int32_t rx16, int32_t ry16) {
-  const SynthObject& o = f.obj[k];
-  if (c == 0)
-    return 40 + ((synth_vnoise(rx16, ry16, 4, o.seed) * 3 + synth_vnoise(rx16, ry16, 2, o.seed + 5)) >> 2) * 3 / 4;
-  return 64 + (int)(synth_hash(k, c, f.seed) & 127) + (synth_vnoise(rx16, ry16, 5, o.seed + c) >> 3);
+  return v;
 }
 
 __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t seed, FrameIdx fi) {
@@ -102,18 +94,13 @@ __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t see
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int xl = tv_min(x0 + j, dw - 1) << s;
-      // background on every lane (uniform control flow keeps the shared lattice state cheap),
-      // then only the topmost covering object's texture
       const int32_t bx16 = xl * 16 + ctx.t * 36;
       int v;
       if (c == 0)
         v = (n0.eval(bx16) * 5 + n1.eval(bx16) * 2 + n2.eval(bx16)) >> 3;
       else
         v = 96 + (n0.eval(bx16) >> 1);
-      int32_t rx16, ry16;
-      const int k = synth_top_object(ctx, xl, yl, rx16, ry16);
-      if (k >= 0) v = synth_object_value(ctx, c, k, rx16, ry16);
-      word |= (uint32_t)clip_pixel(v) << (8 * j);
+      word |= (uint32_t)clip_pixel(synth_objects(ctx, c, xl, yl, v)) << (8 * j);
     }
     *reinterpret_cast<uint32_t*>(P + (long)y * pw + x0) = word;
   }

@@ -13,6 +13,8 @@
 //                   * bottom-up CU split decision.
 //  k_inter_recon  pass B per CTB: luma prediction = phase-plane loads, chroma 4-tap MC,
 //                 residual, MFMA transform/quant, exact inverse, reconstruction.
+#include <cstdlib>
+
 #include "gpu_common.h"
 #include "k_encode.h"
 #include "tb_coder.h"
@@ -40,9 +42,10 @@ namespace gpu {
 //                the phase planes and the bottom-up CU split decision.  Rate = MVD bits
 //                against the CTB predictor.
 // ---------------------------------------------------------------------------------------
-constexpr int kMeThreads = 128;
+constexpr int kMeThreads = 256;
 constexpr int kFRows = kCtb + kMeWinH - 1;  // 38 window rows per candidate
-constexpr int kFWords = 10;                 // 40 bytes: 32 + 7 offsets + 1 spare word
+constexpr int kFWords = 12;                 // 48 bytes staged (40 used: 32 + 7 offsets + 1)
+constexpr int kFChunks = kFWords / 4;       // 16-byte chunks per staged row
 constexpr int kFPitch = kFWords + 1;        // odd pitch: lanes walking rows hit distinct banks
 // LDS pitch (words) of a source-CTB row (uniform s0/s1 reads stay one aligned 8-byte read)
 constexpr int kSrcP = 8;
@@ -158,7 +161,7 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
 
 __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                          DecisionSet dec, const int16_t* prev_mv, const int16_t* cmv,
-                                                         Geo g, const RcTables* rc, int range) {
+                                                         Geo g, const RcTables* rc, int range, int diag_stop) {
   const int tid = threadIdx.x;
   int ctu, b;
   xcd_ctb(ctu, b);
@@ -173,6 +176,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   __shared__ unsigned best[21];
   __shared__ int bcost[21], bmv[21][2];
   __shared__ int subsad[21][8];
+  __shared__ int sad16[kMeMaxCand * kMePosPerCand][4];  // per position: the 4 quadrant 16x16 SADs
   for (int t = tid; t < 256; t += kMeThreads)
     s32[(t >> 3) * kSrcP + (t & 7)] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (t >> 3)) * g.W + cx + 4 * (t & 7));
   if (tid == 0) {
@@ -184,20 +188,44 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   __syncthreads();
   const int nc = ncand;
   // candidate windows, each pre-aligned so byte 0 of a row is x = cx + cand_x + kMeWinX0
-  for (int e = tid; e < nc * kFRows * kFWords; e += kMeThreads) {
-    const int k = e / (kFRows * kFWords), rem = e - k * (kFRows * kFWords);
-    const int r = rem / kFWords, w = rem - r * kFWords;
+  // one lane per 16-byte chunk: a dwordx4 + dword load from the dword-aligned address, then
+  // v_alignbyte to the candidate's byte offset (the clamped per-byte path only at the edges)
+  for (int e = tid; e < nc * kFRows * kFChunks; e += kMeThreads) {
+    const int k = e / (kFRows * kFChunks), rem = e - k * (kFRows * kFChunks);
+    const int r = rem / kFChunks, ch = rem - r * kFChunks;
     const uint8_t* row = R + (long)clip3(0, g.H - 1, cy + cand[k][1] + kMeWinY0 + r) * g.W;
-    win[(k * kFRows + r) * kFPitch + w] = load4_clamped(row, cx + cand[k][0] + kMeWinX0 + 4 * w, g.W);
+    const int x = cx + cand[k][0] + kMeWinX0 + 16 * ch, a = x & ~3, sh = x & 3;
+    uint32_t* dst = win + (k * kFRows + r) * kFPitch + 4 * ch;
+    if (x >= 0 && a + 20 <= g.W) {
+      const uint4 u = *reinterpret_cast<const uint4*>(row + a);
+      const uint32_t u4 = *reinterpret_cast<const uint32_t*>(row + a + 16);
+      dst[0] = __builtin_amdgcn_alignbyte(u.y, u.x, sh);
+      dst[1] = __builtin_amdgcn_alignbyte(u.z, u.y, sh);
+      dst[2] = __builtin_amdgcn_alignbyte(u.w, u.z, sh);
+      dst[3] = __builtin_amdgcn_alignbyte(u4, u.w, sh);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = load4_clamped(row, x + 4 * j, g.W);
+    }
   }
   __syncthreads();
+  // timing diagnostics only (TV_DIAG_ME_STOP=1/2/3): later search phases are skipped and the
+  // decisions degrade (still well-formed); never set in production
+  const bool skip_int = diag_stop == 1, skip_sub = diag_stop == 1 || diag_stop == 2;
 
   // ------------------------------- integer refinement -----------------------------------
-  unsigned lb[21];
+  // item = (candidate, window row, 4-position group, 16x16 quadrant): a lane accumulates
+  // the 4 8x8 SADs of its quadrant for 4 adjacent positions (their sum is the quadrant's
+  // 16x16 SAD); the 32x32 SADs are the sums of the 4 quadrants, formed after a barrier.
+  // Splitting by quadrant keeps every lane busy when few distinct candidates remain.
+  unsigned lb[5];  // 4 8x8 blocks of my quadrant, then its 16x16
 #pragma unroll
-  for (int k = 0; k < 21; ++k) lb[k] = 0xffffffffu;
-  for (int item = tid; item < nc * kMeWinH * 2; item += kMeThreads) {
-    const int k = item / (kMeWinH * 2), rr = item - k * (kMeWinH * 2);
+  for (int k = 0; k < 5; ++k) lb[k] = 0xffffffffu;
+  int qd = 0;
+  for (int item = skip_int ? kMeThreads * 64 : tid; item < nc * kMeWinH * 2 * 4; item += kMeThreads) {
+    qd = item & 3;
+    const int it = item >> 2;
+    const int k = it / (kMeWinH * 2), rr = it - k * (kMeWinH * 2);
     const int dyi = rr >> 1, gs = rr & 1;
     const int pos0 = k * kMePosPerCand + dyi * kMeWinW + 4 * gs;
     const int my = cand[k][1] + kMeWinY0 + dyi;
@@ -207,18 +235,12 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       const int mx = cand[k][0] + kMeWinX0 + 4 * gs + sft;
       mvc[sft] = (unsigned)pen.mv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])];
     }
+    const int qx = (qd & 1) * 16, qy = (qd >> 1) * 16;
     const uint32_t* W0 = win + (k * kFRows + dyi) * kFPitch + gs;
-    unsigned q16[4][4], t32[4];
+    unsigned q16[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int sft = 0; sft < 4; ++sft) {
-      t32[sft] = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) q16[q][sft] = 0;
-    }
-#pragma unroll
-    for (int kb = 0; kb < 16; ++kb) {
-      const int bx = (kb & 3) * 8, by = (kb >> 2) * 8;
-      const int q = ((kb >> 3) << 1) | ((kb >> 1) & 1);
+    for (int j8 = 0; j8 < 4; ++j8) {
+      const int bx = qx + (j8 & 1) * 8, by = qy + (j8 >> 1) * 8;
       unsigned acc[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -237,33 +259,44 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
 #pragma unroll
       for (int sft = 0; sft < 4; ++sft) {
         const unsigned v = ((acc[sft] + mvc[sft]) << 11) | (unsigned)(pos0 + sft);
-        lb[kb] = v < lb[kb] ? v : lb[kb];
-        q16[q][sft] += acc[sft];
-        t32[sft] += acc[sft];
+        lb[j8] = v < lb[j8] ? v : lb[j8];
+        q16[sft] += acc[sft];
       }
       __builtin_amdgcn_sched_barrier(0);  // bound live ranges: no hoisting across 8x8 blocks
     }
 #pragma unroll
     for (int sft = 0; sft < 4; ++sft) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const unsigned v = ((q16[q][sft] + mvc[sft]) << 11) | (unsigned)(pos0 + sft);
-        lb[16 + q] = v < lb[16 + q] ? v : lb[16 + q];
-      }
-      const unsigned v = ((t32[sft] + mvc[sft]) << 11) | (unsigned)(pos0 + sft);
-      lb[20] = v < lb[20] ? v : lb[20];
+      const unsigned v = ((q16[sft] + mvc[sft]) << 11) | (unsigned)(pos0 + sft);
+      lb[4] = v < lb[4] ? v : lb[4];
+      sad16[pos0 + sft][qd] = (int)q16[sft];
     }
   }
+  // a lane's quadrant is fixed (item stride is a multiple of 4), so lb[] maps to static slots
 #pragma unroll
-  for (int k = 0; k < 21; ++k) {
-    const unsigned m = wave_min_u32(lb[k]);
+  for (int k = 0; k < 20; ++k) {
+    const int kq = k < 16 ? ((k >> 3) << 1) | ((k >> 1) & 1) : k - 16;  // quadrant of 8x8 raster block k
+    const int kj = k < 16 ? ((k >> 2) & 1) * 2 + (k & 1) : 4;           // its slot in lb[]
+    const unsigned m = wave_min_u32(qd == kq ? lb[kj] : 0xffffffffu);
     if ((tid & 63) == 0) atomicMin(&best[k], m);
   }
   __syncthreads();
+  {  // 32x32 = the 4 quadrant SADs of a position
+    unsigned b32 = 0xffffffffu;
+    for (int p = skip_int ? kMeThreads * 64 : tid; p < nc * kMePosPerCand; p += kMeThreads) {
+      const int k = p / kMePosPerCand, r = p - k * kMePosPerCand;
+      const int mx = cand[k][0] + kMeWinX0 + (r % kMeWinW), my = cand[k][1] + kMeWinY0 + r / kMeWinW;
+      const unsigned t = (unsigned)(sad16[p][0] + sad16[p][1] + sad16[p][2] + sad16[p][3]);
+      const unsigned v = ((t + (unsigned)pen.mv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])]) << 11) | (unsigned)p;
+      b32 = v < b32 ? v : b32;
+    }
+    const unsigned m = wave_min_u32(b32);
+    if ((tid & 63) == 0) atomicMin(&best[20], m);
+  }
+  __syncthreads();
   if (tid < 21) {
-    int mx, my;
-    me_pos_to_mv((int)(best[tid] & 2047), cand, mx, my);
-    bcost[tid] = (int)(best[tid] >> 11);
+    int mx = 0, my = 0;
+    if (!skip_int) me_pos_to_mv((int)(best[tid] & 2047), cand, mx, my);
+    bcost[tid] = skip_int ? 0 : (int)(best[tid] >> 11);
     bmv[tid][0] = 4 * mx;
     bmv[tid][1] = 4 * my;
   }
@@ -271,7 +304,8 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   // ------------------------ half- then quarter-pel refinement ---------------------------
   const uint8_t* sb = reinterpret_cast<const uint8_t*>(s32);
   const uint8_t* ph = phase + (long)b * 16 * g.psz;
-  for (int step = 2; step >= 1; step >>= 1) {
+  const int last_step = skip_sub ? 4 : (diag_stop == 3 ? 2 : 1);
+  for (int step = 2; step >= last_step; step >>= 1) {
     for (int t = tid; t < 168; t += kMeThreads) subsad[t >> 3][t & 7] = 0;
     __syncthreads();
     // A thread owns a group of 8 rows x 8 pixels of one (block, candidate): per row it loads
@@ -723,7 +757,12 @@ void launch_rc_crf(const uint8_t* q, const int* ccost, int8_t* qp, const Geo& g,
 
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
                         const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s) {
-  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range);
+  static const int diag_stop = [] {
+    const char* e = std::getenv("TV_DIAG_ME_STOP");
+    return e ? std::atoi(e) : 0;
+  }();
+  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range,
+                                                         diag_stop);
   k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g);
 }
 
