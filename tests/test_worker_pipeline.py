@@ -201,3 +201,41 @@ def test_fault_spec_parsing(tmp_path, monkeypatch):
             fault.check("part", 3)
     fault.check("part", 3)  # budget of 2 spent (persisted in TV_FAULT_STATE)
     assert len(os.listdir(tmp_path)) == 2
+
+
+def test_stamp_streams_in_gop_chunks(env, monkeypatch):
+    """Stamp (verification encode) reads, stamps and encodes in closed-GOP chunks and muxes
+    the segment bitstreams straight to disk: the output has every frame, each carrying its
+    burned-in number, and a new READY job points at it."""
+    from thinvids_amd.ops.overlay import stamp_ref
+
+    store, tasks = env["store"], env["tasks"]
+    monkeypatch.setattr(tasks, "STAMP_GOP", 8)
+    monkeypatch.setattr(tasks, "STAMP_BATCH", 2)
+    path, frames = _source(env["root"], "stampme.y4m", n=37, w=96, h=64)
+    reads = []
+    real_open = media.open_source
+
+    def counting_open(p):
+        s = real_open(p)
+        real_read = s.read
+        s.read = lambda a, n: (reads.append((a, n)), real_read(a, n))[1]
+        return s
+
+    monkeypatch.setattr(tasks.media, "open_source", counting_open)
+    job_id, tok = str(uuid.uuid4()), uuid.uuid4().hex
+    store.hset(f"job:{job_id}", mapping={"job_id": job_id, "filename": "stampme.y4m", "input_path": str(path),
+                                         "status": "STAMPING", "pipeline_run_token": tok, "stamp_run_token": tok})
+    monkeypatch.setattr(tasks, "task_token_is_current", lambda *a, **k: True)
+    res = tasks.stamp.call_local(job_id, tok)
+    assert res["status"] == "STAMPED", store.hgetall(f"job:{job_id}")
+    assert reads == [(s, 8) for s in range(0, 37, 8)]  # one bounded read per chunk
+    with open(res["output"], "rb") as f:
+        dec = hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False)
+    assert len(dec.frames) == 37
+    for t in (0, 9, 36):  # the label of frame t is burned in (QP 18: close to the stamped reference)
+        ref = stamp_ref(frames[t], str(t))
+        assert np.mean(np.abs(dec.frames[t][0].astype(int) - ref[0].astype(int))) < 3.0
+        assert np.mean(np.abs(ref[0].astype(int) - frames[t][0].astype(int))) > 0.1
+    new = store.hgetall(f"job:{res['new_job_id']}")
+    assert new["status"] == "READY" and new["input_path"] == res["output"]

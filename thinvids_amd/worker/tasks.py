@@ -547,6 +547,10 @@ def _redispatch(job_id: str, idx: int, run_token: str | None) -> None:
 
 
 # ==========================================================================  stamp
+STAMP_GOP = 64    # frames per stamped segment (closed GOP)
+STAMP_BATCH = 4   # segments per engine launch (bounds host memory)
+
+
 @pipeline_q.task(retries=0)
 def stamp(job_id: str, run_token: str | None = None):
     """Verification encode (reference :2314-2613): burn the frame number into every frame,
@@ -566,16 +570,21 @@ def stamp(job_id: str, run_token: str | None = None):
         base, _ = os.path.splitext(src_path)
         out = base + ".stamped.mp4"
         _set(job_id, stamp_source=src_path, stamp_tmp=out + ".tmp", stamp_output=out)
-        frames = []
-        for start in range(0, src.nframes, 64):
-            chunk = src.read(start, 64)
-            frames.extend(_stamp_chunk(chunk, start, stamp_ref))
-            job_heartbeat(job_id, "stamp", note=f"{start + len(chunk)}/{src.nframes}")
-        spec = EncodeSpec(width=src.width, height=src.height, qp=18, gop=64,
-                          software=not _gpu_ok())
-        annexb = encode_parts([frames], spec)[0]
-        with open(out + ".tmp", "wb") as f:
-            f.write(hevc.mux_mp4(annexb, src.width, src.height, src.fps_num, src.fps_den))
+        # streamed in closed-GOP chunks (reference :2424-2437 pipes ffmpeg frame by frame): a
+        # chunk of STAMP_GOP frames is read, stamped and becomes one IDR-first segment; a few
+        # chunks are encoded per engine launch and only their bitstreams are kept, so host
+        # memory is bounded by STAMP_BATCH chunks whatever the source length
+        spec = EncodeSpec(width=src.width, height=src.height, qp=18, gop=STAMP_GOP, software=not _gpu_ok())
+        bits, pending = [], []
+        for start in range(0, src.nframes, STAMP_GOP):
+            chunk = src.read(start, STAMP_GOP)
+            pending.append(_stamp_chunk(chunk, start, stamp_ref))
+            del chunk
+            if len(pending) == STAMP_BATCH or start + STAMP_GOP >= src.nframes:
+                bits.extend(encode_parts(pending, spec))
+                pending = []
+            job_heartbeat(job_id, "stamp", note=f"{min(src.nframes, start + STAMP_GOP)}/{src.nframes}")
+        hevc.mux_mp4_file(bits, src.width, src.height, src.fps_num, src.fps_den, out + ".tmp")
         os.replace(out + ".tmp", out)
     except Exception as e:
         log.error("[%s] stamp failed:\n%s", job_id, traceback.format_exc())
