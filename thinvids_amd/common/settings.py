@@ -44,6 +44,7 @@ DEFAULT_SETTINGS: dict[str, str] = {
     "tv_segment_frames": "0",  # 0 = derive from target_segment_mb
     "tv_bitrate_kbps": "0",  # tv_rc=2pass target
     "tv_crf": "27",  # tv_rc=crf quality level
+    "tv_scenecut": "1",  # IDR (closed-GOP restart) at detected scene cuts
     "tv_ladder": "",  # e.g. "2160,1440,1080,720,480": one MP4 per rung (ABR fan-out)
     # node executor (one rank per GPU, RCCL data plane) — used when one is alive
     "tv_node_executor": "1",

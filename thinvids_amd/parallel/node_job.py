@@ -276,7 +276,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             segment_frames: int = 256, mode: str = "direct", bitrate_kbps: float = 0.0, ladder=None,
             search_range: int = 64, software: bool = False, batch_segments: int = 8,
             resume_dir: str | None = None, max_retries: int = 3, hooks: JobHooks | None = None,
-            deblock: bool = True, sao: bool = False, cache=None, crf: int = 0) -> dict:
+            deblock: bool = True, sao: bool = False, cache=None, crf: int = 0, scenecut: bool = False) -> dict:
     import torch
 
     from ..models import hevc, media
@@ -312,14 +312,14 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     ckpt = Checkpoint(resume_dir, Checkpoint.fingerprint(
         src=os.path.abspath(input_path), size=st.st_size if st else 0, mtime=st.st_mtime_ns if st else 0,
         rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software,
-        deblock=deblock, sao=sao))
+        deblock=deblock, sao=sao, scenecut=scenecut))
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
     quality: dict = {}  # (r, i) -> PartStats of segments encoded here
 
     def spec(r):  # the QP is a per-frame input now: one resident engine per rung, whatever the plan
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=qp, gop=gop, search_range=search_range,
                           software=software, deblock=deblock, sao=sao, seed=getattr(src, "seed", 1),
-                          crf=0 if bitrate_kbps > 0 else crf)
+                          crf=0 if bitrate_kbps > 0 else crf, scenecut=scenecut)
 
     rc = {"plan": None, "fb": RateFeedback(), "bits": {}}  # pass-2 plan, feedback, per-frame bits
 

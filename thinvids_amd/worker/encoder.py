@@ -43,6 +43,7 @@ class EncodeSpec:
     software: bool = False
     seed: int = 1  # synthetic sources generated inside the engine
     crf: int = 0  # > 0: in-engine CRF (per-frame QP from the lookahead)
+    scenecut: bool = False  # restart the closed GOP (IDR) at detected scene cuts
 
     def engine_key(self):
         return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed,
@@ -155,9 +156,25 @@ def gpu_available() -> bool:
         return False
 
 
-def chunk_plan(nframes: int, gop: int) -> list[tuple[int, int]]:
-    """Closed-GOP chunks [(start, n)] covering a part."""
-    return [(s, min(gop, nframes - s)) for s in range(0, nframes, gop)]
+def chunk_plan(nframes: int, gop: int, cuts=()) -> list[tuple[int, int]]:
+    """Closed-GOP chunks [(start, n)] covering a part: every `gop` frames, and a new GOP
+    at each scene cut (the cadence restarts there)."""
+    out, s, cuts = [], 0, sorted(c for c in cuts if 0 < c < nframes)
+    while s < nframes:
+        e = min(s + gop, nframes)
+        nxt = next((c for c in cuts if s < c < e), None)
+        e = nxt if nxt is not None else e
+        out.append((s, e - s))
+        s = e
+    return out
+
+
+def _cuts(part, spec: EncodeSpec) -> list[int]:
+    if not spec.scenecut or isinstance(part, SynthRange):
+        return []
+    from ..models.scenecut import part_cuts
+
+    return part_cuts(part)
 
 
 def _nframes(part) -> int:
@@ -199,7 +216,13 @@ def encode_parts(parts: list, spec: EncodeSpec, cache: EngineCache | None = None
     if spec.software or not gpu_available():
         if not spec.software:
             raise RuntimeError("no GPU available for a hardware encode (set software_encode for the CPU path)")
-        return [_encode_cpu(_host_frames(p), spec, stats[i] if stats else None, qps[i]) for i, p in enumerate(parts)]
+        out = []
+        for i, p in enumerate(parts):
+            frames = _host_frames(p)
+            plan = chunk_plan(len(frames), max(len(frames), 1), _cuts(frames, spec))  # split at cuts only
+            out.append(b"".join(_encode_cpu(frames[a:a + n], spec, stats[i] if stats else None,
+                                            None if qps[i] is None else qps[i][a:a + n]) for a, n in plan))
+        return out
     return _encode_gpu(parts, spec, cache or default_cache(), stats, qps)
 
 
@@ -233,7 +256,7 @@ def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats, qps) -> list
     chunks: dict[int, list] = {}
     out: list[list] = []
     for pi, p in enumerate(dparts):
-        plan = chunk_plan(_nframes(p), spec.gop)
+        plan = chunk_plan(_nframes(p), spec.gop, _cuts(p, spec))
         out.append([b""] * len(plan))
         for c, (s, n) in enumerate(plan):
             q = None if qps[pi] is None else np.asarray(qps[pi][s:s + n], np.int64)

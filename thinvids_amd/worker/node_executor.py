@@ -123,7 +123,8 @@ def _job_params(job: dict) -> dict:
             "sao": spec.sao, "software": spec.software, "ladder": ladder or None, "bitrate_kbps": kbps,
             "segment_frames": max(spec.gop, as_int(s.get("tv_node_segment_frames"), 256)),
             "mode": str(s.get("tv_node_mode") or "direct"), "batch_segments": as_int(s.get("tv_node_batch"), 8),
-            "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc}
+            "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc,
+            "scenecut": spec.scenecut}
 
 
 class CommFailure(RuntimeError):
@@ -191,7 +192,8 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                       segment_frames=p["segment_frames"], mode=p["mode"], bitrate_kbps=p["bitrate_kbps"],
                       ladder=p["ladder"], search_range=p["search_range"], software=p["software"],
                       batch_segments=p["batch_segments"], hooks=hooks, deblock=p["deblock"], sao=p["sao"],
-                      cache=None if p["software"] else cache, crf=p["crf"], resume_dir=spec["ckpt"])
+                      cache=None if p["software"] else cache, crf=p["crf"], resume_dir=spec["ckpt"],
+                      scenecut=p.get("scenecut", False))
     except Exception as e:
         if is_comm_failure(e):  # the job is fine, the communicator is not: requeue + re-init
             log.error("[%s] communicator failure on rank %d: %s", job_id, rank, e)

@@ -101,7 +101,8 @@ def encode_spec_for_job(job: dict, settings: dict | None = None) -> EncodeSpec:
                       deblock=as_bool(s.get("tv_deblock"), True), sao=as_bool(s.get("tv_sao"), True),
                       software=as_bool(job.get("software_encode")),
                       crf=as_int(job.get("crf") or s.get("tv_crf"), 27)
-                      if str(job.get("rc_mode") or s.get("tv_rc") or "cqp").lower() == "crf" else 0)
+                      if str(job.get("rc_mode") or s.get("tv_rc") or "cqp").lower() == "crf" else 0,
+                      scenecut=as_bool(s.get("tv_scenecut"), True))
 
 
 # =====================================================================  transcode
