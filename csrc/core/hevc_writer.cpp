@@ -418,34 +418,55 @@ class SliceWriter {
     if (intra || cb || cr) bin(cl, CTX_CBF_LUMA + 1);
     else if (!cl) throw std::runtime_error("inter CU with rqt_root_cbf=1 but no residual");
     const int cmode = intra ? chroma_intra_mode(4, mode) : 0;
-    int stride;
+    TbView v;
     if (cl) {
-      const int16_t* p = tb_levels(0, x0, y0, log2, stride);
-      residual(p, stride, log2, 0, scan_idx_for(intra, log2, 0, mode));
+      tb_view(0, x0, y0, log2, v);
+      residual(v, log2, 0, scan_idx_for(intra, log2, 0, mode));
     }
     if (cb) {
-      const int16_t* p = tb_levels(1, x0 >> 1, y0 >> 1, log2 - 1, stride);
-      residual(p, stride, log2 - 1, 1, scan_idx_for(intra, log2 - 1, 1, cmode));
+      tb_view(1, x0 >> 1, y0 >> 1, log2 - 1, v);
+      residual(v, log2 - 1, 1, scan_idx_for(intra, log2 - 1, 1, cmode));
     }
     if (cr) {
-      const int16_t* p = tb_levels(2, x0 >> 1, y0 >> 1, log2 - 1, stride);
-      residual(p, stride, log2 - 1, 2, scan_idx_for(intra, log2 - 1, 2, cmode));
+      tb_view(2, x0 >> 1, y0 >> 1, log2 - 1, v);
+      residual(v, log2 - 1, 2, scan_idx_for(intra, log2 - 1, 2, cmode));
     }
   }
 
-  // Levels of the TB of component c at component position (x, y): a pointer into the dense
-  // plane, or (compact GPU form) a gather of its non-zero 4x4 groups into tbbuf_.
-  const int16_t* tb_levels(int c, int x, int y, int log2N, int& stride) {
+  // Levels of the TB of component c at component position (x, y), as its 4x4 sub-blocks:
+  // sb[ys * nsb + xs] points at the sub-block's top-left level (row stride `stride`) and bit
+  // ys * nsb + xs of `nz` is set iff it holds a non-zero level.  Dense planes (CPU path) are
+  // scanned once; the compact GPU form reads the CTB group masks and points straight into the
+  // packed groups (stride 4) — no gather, and zero sub-blocks are never touched.
+  struct TbView {
+    const int16_t* sb[64];
+    int stride;
+    uint64_t nz;
+  };
+  void tb_view(int c, int x, int y, int log2N, TbView& v) const {
+    const int nsb = 1 << (log2N - 2);
+    v.nz = 0;
     if (!fd_.sb_packed) {
-      stride = c ? cfg_.coded_w >> 1 : cfg_.coded_w;
-      return fd_.coef[c] + (size_t)y * stride + x;
+      v.stride = c ? cfg_.coded_w >> 1 : cfg_.coded_w;
+      const int16_t* base = fd_.coef[c] + (size_t)y * v.stride + x;
+      for (int ys = 0; ys < nsb; ++ys)
+        for (int xs = 0; xs < nsb; ++xs) {
+          const int16_t* p = base + (size_t)(4 * ys) * v.stride + 4 * xs;
+          v.sb[ys * nsb + xs] = p;
+          uint64_t any = 0;
+          for (int r = 0; r < 4; ++r) {
+            uint64_t w;
+            std::memcpy(&w, p + (size_t)r * v.stride, 8);
+            any |= w;
+          }
+          if (any) v.nz |= 1ull << (ys * nsb + xs);
+        }
+      return;
     }
-    const int N = 1 << log2N, ng = N >> 2;
-    stride = N;
-    std::memset(tbbuf_, 0, sizeof(int16_t) * N * N);
-    for (int gy = 0; gy < ng; ++gy)
-      for (int gx = 0; gx < ng; ++gx) {
-        const int X = x + 4 * gx, Y = y + 4 * gy;
+    v.stride = 4;
+    for (int ys = 0; ys < nsb; ++ys)
+      for (int xs = 0; xs < nsb; ++xs) {
+        const int X = x + 4 * xs, Y = y + 4 * ys;
         int ctb, bit;
         if (c == 0) {
           ctb = (Y >> 5) * fd_.wc + (X >> 5);
@@ -464,13 +485,10 @@ class SliceWriter {
           if (!((mc >> bit) & 1)) continue;
           rank = __builtin_popcountll(my) + __builtin_popcount(mc & ((1u << bit) - 1));
         }
-        const int16_t* src = fd_.sb_packed + ((size_t)fd_.sb_offset[ctb] + rank) * 16;
-        for (int r = 0; r < 4; ++r)
-          std::memcpy(tbbuf_ + (4 * gy + r) * N + 4 * gx, src + 4 * r, 4 * sizeof(int16_t));
+        v.sb[ys * nsb + xs] = fd_.sb_packed + ((size_t)fd_.sb_offset[ctb] + rank) * 16;
+        v.nz |= 1ull << (ys * nsb + xs);
       }
-    return tbbuf_;
   }
-  int16_t tbbuf_[32 * 32];
 
   void write_last_prefix(int pos, int log2N, int cIdx, int base) {
     const int prefix = kGroupIdx[pos];
@@ -537,31 +555,28 @@ class SliceWriter {
     }
   };
 
-  void residual(const int16_t* blk, int stride, int log2N, int cIdx, int scanIdx) {
+  void residual(const TbView& v, int log2N, int cIdx, int scanIdx) {
     static const SigPattern kPat;
     const int nsb = 1 << (log2N - 2);  // sub-blocks per side
     const int numSb = nsb * nsb;
     const uint8_t* ps = in_sb_scan(scanIdx);
     int off[16];
-    for (int n = 0; n < 16; ++n) off[n] = (ps[n] >> 2) * stride + (ps[n] & 3);
-    auto sb_ptr = [&](int i, int& xs, int& ys) {
-      subblock_pos(log2N, scanIdx, i, xs, ys);
-      return blk + (size_t)(ys << 2) * stride + (xs << 2);
-    };
-    // last significant coefficient in scan order
+    for (int n = 0; n < 16; ++n) off[n] = (ps[n] >> 2) * v.stride + (ps[n] & 3);
+    // last significant coefficient in scan order: the last non-zero sub-block, then its last
+    // non-zero scan position
+    if (!v.nz) throw std::runtime_error("residual_coding of an all-zero block");
     int lastSb = -1, lastN = -1;
     for (int i = numSb - 1; i >= 0; --i) {
       int xs, ys;
-      const int16_t* b = sb_ptr(i, xs, ys);
+      subblock_pos(log2N, scanIdx, i, xs, ys);
+      if (!((v.nz >> (ys * nsb + xs)) & 1)) continue;
+      const int16_t* b = v.sb[ys * nsb + xs];
       unsigned m = 0;
       for (int n = 0; n < 16; ++n) m |= (unsigned)(b[off[n]] != 0) << n;
-      if (m) {
-        lastSb = i;
-        lastN = 31 - __builtin_clz(m);
-        break;
-      }
+      lastSb = i;
+      lastN = 31 - __builtin_clz(m);
+      break;
     }
-    if (lastSb < 0) throw std::runtime_error("residual_coding of an all-zero block");
     {
       int xs, ys, xc, yc;
       subblock_pos(log2N, scanIdx, lastSb, xs, ys);
@@ -581,12 +596,14 @@ class SliceWriter {
     int c1 = 1;
     for (int i = lastSb; i >= 0; --i) {
       int xs, ys;
-      const int16_t* b = sb_ptr(i, xs, ys);
+      subblock_pos(log2N, scanIdx, i, xs, ys);
+      const bool any = (v.nz >> (ys * nsb + xs)) & 1;
       int vals[16];
-      bool any = false;
-      for (int n = 0; n < 16; ++n) {
-        vals[n] = b[off[n]];
-        any |= vals[n] != 0;
+      if (any) {
+        const int16_t* b = v.sb[ys * nsb + xs];
+        for (int n = 0; n < 16; ++n) vals[n] = b[off[n]];
+      } else {
+        std::memset(vals, 0, sizeof(vals));  // DC sub-block: coded (inferred) even when empty
       }
       bool inferDc = false;
       if (i < lastSb && i > 0) {

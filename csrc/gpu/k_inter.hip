@@ -439,6 +439,7 @@ struct PReconLds {
   int mv[16][2];              // per 8x8 unit (raster within the CTB)
   int nz[48], sa[48], dc[48];  // per-TB statistics: luma 0..15, Cb 16..31, Cr 32..47
   int qtype[4];               // luma quadrant: 0 part of a 32x32 CU, 1 16x16 CU, 2 four 8x8 CUs
+  int tzero[8];               // stage-3/4 tile t has no surviving level: reconstruction = prediction
 };
 
 // block size (log2) of the TB owning luma sample (x, y) / chroma sample (x, y) of the CTB
@@ -465,7 +466,7 @@ __device__ __forceinline__ bool pr_zeroed(const PReconLds& L, int id) {
 }
 
 __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
-                                                     FrameSet rec, DecisionSet dec, Geo g) {
+                                                     FrameSet rec, DecisionSet dec, Geo g, int tile_skip) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   int ctu, b;
   xcd_ctb(ctu, b);
@@ -624,6 +625,20 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
       if (pr_zeroed(L, pr_tb_chroma(L, pl, x, y))) L.resC[pl][y * 16 + x] = 0;
       (pl ? dec.coef_v : dec.coef_u)[b * g.csz + (long)((cy >> 1) + y) * Wc + (cx >> 1) + x] = L.resC[pl][y * 16 + x];
     }
+    if (tid < 8) {  // tiles whose TBs all dropped out skip the inverse transform
+      bool z = true;
+      if (tid < 4) {
+        if (L.qtype[0] == 0) z = pr_zeroed(L, 0);
+        else for (int k = 0; k < 4; ++k) z = z && pr_zeroed(L, pr_tb_luma(L, (tid & 1) * 16 + (k & 1) * 8, (tid >> 1) * 16 + (k >> 1) * 8));
+      } else if (L.qtype[0] == 0) {
+        z = pr_zeroed(L, 16 + 16 * (tid - 4));
+      } else {
+        const int q = tid - 4;  // Cb | Cr pair of quadrant q (Cb and Cr 8x8 regions)
+        for (int pl = 0; pl < 2; ++pl)
+          for (int k = 0; k < 4; ++k) z = z && pr_zeroed(L, pr_tb_chroma(L, pl, (q & 1) * 8 + (k & 1) * 4, (q >> 1) * 8 + (k >> 1) * 4));
+      }
+      L.tzero[tid] = z && tile_skip;
+    }
     if (tid < 16) {
       const int x = (tid & 3) * 8, y = (tid >> 2) * 8;  // this unit's CU = its TBs
       const int cb = (pr_zeroed(L, pr_tb_luma(L, x, y)) ? 0 : 1) | (pr_zeroed(L, pr_tb_chroma(L, 0, x >> 1, y >> 1)) ? 0 : 2) |
@@ -634,6 +649,7 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
   __syncthreads();
   // --------------------------------------- stage 3: T^T * dequant(levels)  (split d)
   for (int t = wave; t < ntiles; t += 4) {
+    if (L.tzero[t]) continue;  // wave-uniform: an all-zero tile reconstructs to the prediction
     int o[4];
     if (t < 4) {
       if (whole) {
@@ -675,13 +691,17 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
   // ------------------------------------- stage 4: G * T + prediction -> reconstruction
   for (int t = wave; t < ntiles; t += 4) {
     int o[4];
+    const bool tz = L.tzero[t];
+    if (tz) {  // copy the prediction (what clip(pred + 0) gives)
+      o[0] = o[1] = o[2] = o[3] = 0;
+    }
     if (t < 4) {
       if (whole) {
-        mfma_tile([&](int r, int k) { return L.tmpY[r * 33 + k]; }, [&](int k, int c) { return (int)L.T[k][c]; },
+        if (!tz) mfma_tile([&](int r, int k) { return L.tmpY[r * 33 + k]; }, [&](int k, int c) { return (int)L.T[k][c]; },
                   t >> 1, t & 1, 32, true, true, o);
       } else {
         const int ox = (t & 1) * 16, oy = (t >> 1) * 16, l2 = L.qtype[t] == 1 ? 4 : 3;
-        mfma_tile([&](int r, int k) { return L.tmpY[(oy + r) * 33 + ox + k]; },
+        if (!tz) mfma_tile([&](int r, int k) { return L.tmpY[(oy + r) * 33 + ox + k]; },
                   [&](int k, int c) { return pr_comp(L, l2, k, c); }, 0, 0, 16, true, true, o);
       }
       uint8_t* R = rec.plane(0, b, g) + (long)cy * g.W + cx;
@@ -692,7 +712,7 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
       }
     } else if (whole) {
       const int pl = t - 4;
-      mfma_tile([&](int r, int k) { return L.tmpC[pl][r * 16 + k]; }, [&](int k, int c) { return pr_comp(L, 4, k, c); },
+      if (!tz) mfma_tile([&](int r, int k) { return L.tmpC[pl][r * 16 + k]; }, [&](int k, int c) { return pr_comp(L, 4, k, c); },
                 0, 0, 16, true, true, o);
       uint8_t* R = rec.plane(1 + pl, b, g) + (long)(cy >> 1) * Wc + (cx >> 1);
 #pragma unroll
@@ -702,7 +722,7 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
       }
     } else {
       const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
-      mfma_tile([&](int r, int k) {
+      if (!tz) mfma_tile([&](int r, int k) {
                   return (r >> 3) == (k >> 3) ? L.tmpC[r >> 3][(oy + (r & 7)) * 16 + ox + (k & 7)] : 0;
                 },
                 [&](int k, int c) { return pr_comp(L, l2, k, c); }, 0, 0, 16, true, true, o);
@@ -763,7 +783,13 @@ void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameS
   }();
   k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range,
                                                          diag_stop);
-  k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g);
+  // TV_RECON_TILE_SKIP=0 runs the inverse transform on all-zero tiles too (same output;
+  // kept as a same-box A/B switch for the skip)
+  static const int tile_skip = [] {
+    const char* e = std::getenv("TV_RECON_TILE_SKIP");
+    return e ? std::atoi(e) : 1;
+  }();
+  k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, tile_skip);
 }
 
 }  // namespace gpu

@@ -11,6 +11,10 @@ namespace tv {
 class BitWriter {
  public:
   void put(uint32_t v, int n) {  // n <= 32, MSB first
+    if (nbits_ == 0 && n == 8) {  // byte-aligned byte: the CABAC output path
+      buf_.push_back((uint8_t)v);
+      return;
+    }
     for (int i = n - 1; i >= 0; --i) put_bit((v >> i) & 1);
   }
   void put_bit(int b) {

@@ -235,10 +235,8 @@ class CabacEncoder {
   }
   // fractional-bit estimate is not needed by the engine; count of bins for stats
  private:
-  static int renorm_bits(uint32_t lps) {
-    int n = 0;
-    while ((lps << n) < 256) ++n;
-    return n;
+  static int renorm_bits(uint32_t lps) {  // shifts bringing lps (6..255) to >= 256
+    return __builtin_clz(lps) - 23;
   }
   void test_write_out() {
     if (bits_left_ < 12) write_out();

@@ -45,7 +45,29 @@ def device_count() -> int:
     return _lib().tv_gpu_device_count()
 
 
+def cgroup_cpu_quota() -> float | None:
+    """CPUs this process may use per the cgroup (v2 cpu.max, v1 cfs quota), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def default_threads() -> int:
+    """CABAC pool size: 1.5 x the CPUs this rank may use (affinity, capped by the cgroup
+    quota), at most 32.  Slices block briefly on the slot ring and the D2H fetch, so a pool
+    the size of the quota leaves it idle (measured on a 16-CPU-quota MI355X box: 8 threads
+    3880 frames/s, 16 threads ~6050, 24 threads 6250-6660 with all 16 CPUs busy)."""
     env = os.environ.get("TV_THREADS")
     if env:
         return max(1, int(env))
@@ -53,7 +75,9 @@ def default_threads() -> int:
         n = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         n = os.cpu_count() or 4
-    return max(2, min(16, n))
+    q = cgroup_cpu_quota()
+    cpus = min(n, q) if q else n
+    return max(2, min(32, int(cpus * 1.5)))
 
 
 class GpuEngine:
