@@ -512,22 +512,27 @@ class SliceWriter {
     }
   }
 
+  // coeff_abs_level_remaining: TR prefix (p ones, a zero) + rice bits, or the escape
+  // (4 ones, exp-Golomb order rice+1); prefixes go out as one bypass run.
   void write_remaining(int v, int rice) {
     if (v < (4 << rice)) {
-      const int p = v >> rice;
-      for (int i = 0; i < p; ++i) enc_.encode_bypass(1);
-      enc_.encode_bypass(0);
-      if (rice) enc_.encode_bypass_bins((uint32_t)(v & ((1 << rice) - 1)), rice);
+      const int p = v >> rice;  // <= 3
+      enc_.encode_bypass_bins(((1u << (p + 1)) - 2) << rice | (uint32_t)(v & ((1 << rice) - 1)), p + 1 + rice);
     } else {
-      enc_.encode_bypass_bins(0xf, 4);
-      int k = rice + 1;
+      int k = rice + 1, ones = 0;
       uint32_t s = (uint32_t)(v - (4 << rice));
       while (s >= (1u << k)) {
-        enc_.encode_bypass(1);
         s -= 1u << k;
         ++k;
+        ++ones;
       }
-      enc_.encode_bypass(0);
+      // 4 + ones prefix ones, a zero, then k suffix bits (k <= 15 + ..: split the long runs)
+      const int np = 4 + ones + 1;
+      if (np <= 24) enc_.encode_bypass_bins((1u << np) - 2, np);
+      else {
+        for (int i = 0; i < 4 + ones; ++i) enc_.encode_bypass(1);
+        enc_.encode_bypass(0);
+      }
       enc_.encode_bypass_bins(s, k);
     }
   }

@@ -120,6 +120,15 @@ inline const CtxInitTable& ctx_init_table() {
 
 extern const uint8_t kRangeTabLps[64][4];
 extern const uint8_t kTransIdxLps[64];
+// MPS transition: state + 1, saturating at 62 (state 63 is the terminate state)
+struct TransMps {
+  uint8_t t[64];
+  constexpr TransMps() : t() {
+    for (int i = 0; i < 64; ++i) t[i] = (uint8_t)(i < 62 ? i + 1 : i);
+  }
+};
+constexpr TransMps kTransMpsTab{};
+constexpr const uint8_t* kTransIdxMps = kTransMpsTab.t;
 
 struct CtxState {
   uint8_t state;  // pStateIdx
@@ -159,23 +168,20 @@ class CabacEncoder {
     num_buffered_ = 0;
     buffered_ = 0xff;
   }
+  // Branch-free on the coded value (significance / greater-1 bins are unpredictable): both
+  // outcomes are formed and selected, renormalisation is one clz.
   void encode_bin(int bin, CtxState& ctx) {
-    uint32_t lps = kRangeTabLps[ctx.state][(range_ >> 6) & 3];
-    range_ -= lps;
-    if (bin != ctx.mps) {
-      int nb = renorm_bits(lps);
-      low_ = (low_ + range_) << nb;
-      range_ = lps << nb;
-      if (ctx.state == 0) ctx.mps = (uint8_t)(1 - ctx.mps);
-      ctx.state = kTransIdxLps[ctx.state];
-      bits_left_ -= nb;
-    } else {
-      if (ctx.state < 62) ++ctx.state;
-      if (range_ >= 256) return;
-      low_ <<= 1;
-      range_ <<= 1;
-      bits_left_--;
-    }
+    const uint32_t lps = kRangeTabLps[ctx.state][(range_ >> 6) & 3];
+    const uint32_t rmps = range_ - lps;
+    const bool is_lps = bin != ctx.mps;
+    const uint32_t r = is_lps ? lps : rmps;
+    const uint32_t l = is_lps ? low_ + rmps : low_;
+    const int nb = __builtin_clz(r) - 23;  // shifts bringing r (>= 6) to >= 256; 0 if already
+    low_ = l << nb;
+    range_ = r << nb;
+    bits_left_ -= nb;
+    ctx.mps = (uint8_t)(ctx.mps ^ (is_lps & (ctx.state == 0)));
+    ctx.state = is_lps ? kTransIdxLps[ctx.state] : kTransIdxMps[ctx.state];
     test_write_out();
   }
   void encode_bypass(int bin) {
