@@ -167,7 +167,8 @@ class Core {
       Slot& s = slots_[k];
       HIP_OK(hipMalloc(&s.dev, slot_bytes_));
       HIP_OK(hipHostMalloc(&s.host, slot_bytes_, hipHostMallocDefault));
-      HIP_OK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+      // waited on by the fetch thread: see sync_mode()
+      HIP_OK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming | (sync_mode() == 2 ? hipEventBlockingSync : 0)));
       s.pending = 0;
     }
     HIP_OK(hipEventCreate(&t0_));
@@ -339,10 +340,44 @@ class Core {
   }
 
   // worker: fetch exactly the used bytes of slot s from the device on a private stream
+  // wait for everything queued on `st` without spinning a CPU core
+  // Host waits for GPU work: TV_SYNC_MODE=spin (default: hipStreamSynchronize /
+  // hipEventSynchronize spin — lowest wake-up latency), poll (query + 40 us sleeps) or block
+  // (blocking-sync events).  Same-box A/B on the 1080p bench (profiles/README.md): spin 7510-7632
+  // frames/s; poll 6399-6663 and block 6522-6932 although they free 5-6 of the 16 CPUs — the
+  // slot turnaround latency, not the CPU, sets the pace once CABAC keeps up.
+  static int sync_mode() {
+    static const int m = [] {
+      const char* e = getenv("TV_SYNC_MODE");
+      if (e && std::string(e) == "poll") return 0;
+      if (e && std::string(e) == "block") return 2;
+      return 1;
+    }();
+    return m;
+  }
+  static void wait_event(hipEvent_t ev) {
+    if (sync_mode() == 0) {
+      hipError_t e;
+      while ((e = hipEventQuery(ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(40));
+      HIP_OK(e);
+    } else {
+      HIP_OK(hipEventSynchronize(ev));
+    }
+  }
+  static void sleep_sync(hipStream_t st) {
+    if (sync_mode() == 1) {
+      HIP_OK(hipStreamSynchronize(st));
+      return;
+    }
+    thread_local hipEvent_t ev = nullptr;
+    if (!ev) HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming | (sync_mode() == 2 ? hipEventBlockingSync : 0)));
+    HIP_OK(hipEventRecord(ev, st));
+    wait_event(ev);
+  }
   void fetch_slot(Slot& s, int B) {
     thread_local hipStream_t ws = nullptr;
     if (!ws) HIP_OK(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
-    HIP_OK(hipEventSynchronize(s.ev));
+    wait_event(s.ev);
     const Parts d = carve(s.dev), h = carve(s.host);
     const long U = g_.usz;
     // Every D2H copy is a blit-kernel launch (~10 us of CU time each): the full-batch case
@@ -364,13 +399,13 @@ class Core {
       HIP_OK(hipMemcpyAsync(h.mask_c, d.mask_c, B * nctu_ * 4, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.offset, d.offset, B * nctu_ * 4, hipMemcpyDeviceToHost, ws));
     }
-    HIP_OK(hipStreamSynchronize(ws));
+    sleep_sync(ws);
     long groups = 0;
     for (int b = 0; b < B; ++b) groups += h.total[b];
     const long bytes = groups * 16 * 2;
     if (groups > (long)B * cap_ / 16) throw std::runtime_error("compact level overflow");
     if (bytes) HIP_OK(hipMemcpyAsync(h.packed, d.packed, bytes, hipMemcpyDeviceToHost, ws));
-    HIP_OK(hipStreamSynchronize(ws));
+    sleep_sync(ws);
     coef_bytes_ += bytes;
   }
 
@@ -494,7 +529,7 @@ class Core {
   void finish() {
     for (auto& s : slots_)
       wait_slot(s);
-    HIP_OK(hipStreamSynchronize(stream_));
+    sleep_sync(stream_);
     if (failed_) throw std::runtime_error("encode failed: " + err_);
     std::vector<unsigned long long> sse(B_ * 3);
     HIP_OK(hipMemcpy(sse.data(), d_sse_, B_ * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
