@@ -163,7 +163,9 @@ class Core {
     HIP_OK(hipHostMalloc(&qhost_, (size_t)c.gop * B, hipHostMallocDefault));
     HIP_OK(hipHostMalloc(&quni_, (size_t)B, hipHostMallocDefault));
     std::memset(quni_, c.qp, (size_t)B);
-    for (int k = 0; k < kSlots; ++k) {
+    nslots_ = slot_count();
+    slots_.reset(new Slot[nslots_]);
+    for (int k = 0; k < nslots_; ++k) {
       Slot& s = slots_[k];
       HIP_OK(hipMalloc(&s.dev, slot_bytes_));
       HIP_OK(hipHostMalloc(&s.host, slot_bytes_, hipHostMallocDefault));
@@ -217,7 +219,8 @@ class Core {
     (void)hipFree(rc_);
     (void)hipHostFree(qhost_);
     (void)hipHostFree(quni_);
-    for (auto& s : slots_) {
+    for (int k = 0; k < nslots_; ++k) {
+      Slot& s = slots_[k];
       (void)hipFree(s.dev);
       (void)hipHostFree(s.host);
       (void)hipEventDestroy(s.ev);
@@ -239,7 +242,15 @@ class Core {
   hipStream_t stream() const { return stream_; }
 
  private:
-  static constexpr int kSlots = 4;
+  // frames in flight per core (host issue runs this far ahead of CABAC): TV_SLOTS, default 4
+  static int slot_count() {
+    static const int n = [] {
+      const char* e = getenv("TV_SLOTS");
+      const int v = e ? atoi(e) : 4;
+      return v < 2 ? 2 : (v > 16 ? 16 : v);
+    }();
+    return n;
+  }
   static long align(long n) { return (n + 255) & ~255L; }
   struct Slot {
     uint8_t* dev = nullptr;
@@ -441,7 +452,7 @@ class Core {
   template <class Upload> void issue(int f, Upload&& upload) {
     const int B = B_, F = F_;
     Range frame_range(f == 0 ? "engine.frame.intra" : "engine.frame.inter");
-    Slot& s = slots_[f % kSlots];
+    Slot& s = slots_[f % nslots_];
     wait_slot(s);
     const DecisionSet dec = slot_dec(s);
     // this frame's QPs: copied only when they differ from what the slot already holds (a
@@ -467,8 +478,8 @@ class Core {
     };
     stage("upload");
     launch_quarter(src_, q_[f & 1], g_, B, stream_);  // lookahead plane (next frame's coarse ref)
-    // the previous frame's decisions still sit in its slot (reused only kSlots frames later)
-    const MeBuffers me{q_[f & 1], q_[(f + 1) & 1], f ? slot_dec(slots_[(f - 1) % kSlots]).mv : nullptr, cmv_,
+    // the previous frame's decisions still sit in its slot (reused only nslots_ frames later)
+    const MeBuffers me{q_[f & 1], q_[(f + 1) & 1], f ? slot_dec(slots_[(f - 1) % nslots_]).mv : nullptr, cmv_,
                        ccost_};
     if (f > 0) launch_coarse_me(me, g_, rc_, cfg_.qp, cfg_.range, B, stream_);
     if (cfg_.crf > 0 && !qmap_given_) launch_rc_crf(q_[f & 1], ccost_, dec.qp, g_, cfg_.crf, f == 0, B, stream_);
@@ -527,8 +538,7 @@ class Core {
   void end_record() { HIP_OK(hipEventRecord(t1_, stream_)); }
 
   void finish() {
-    for (auto& s : slots_)
-      wait_slot(s);
+    for (int k = 0; k < nslots_; ++k) wait_slot(slots_[k]);
     sleep_sync(stream_);
     if (failed_) throw std::runtime_error("encode failed: " + err_);
     std::vector<unsigned long long> sse(B_ * 3);
@@ -598,7 +608,8 @@ class Core {
     return e && *e == '1';
   }();
   long cap_ = 0;
-  Slot slots_[kSlots];
+  std::unique_ptr<Slot[]> slots_;
+  int nslots_ = 0;
   long slot_bytes_ = 0;
   hipEvent_t t0_{}, t1_{};
   ThreadPool* pool_;
