@@ -647,6 +647,7 @@ class Engine {
     }
   }
   ~Engine() {
+    intra_timing_report();
     cores_.clear();
     pool_.reset();
   }

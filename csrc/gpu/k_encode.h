@@ -28,6 +28,8 @@ struct RcTables {
 
 void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi, int B, hipStream_t s);
 void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s);
+bool intra_timing();
+void intra_timing_report();
 void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, int B,
                         hipStream_t s);
 // Hierarchical motion-search state of one P frame (tv/me_model.h): quarter-res source luma

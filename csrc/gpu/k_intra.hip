@@ -7,6 +7,9 @@
 //                    Then the bottom-up CU split decision.
 //  k_intra_recon     pass B, CTB anti-diagonal wavefront (cx + 2*cy = d per launch): the
 //                    normative prediction from reconstructed neighbours + MFMA TB coding.
+#include <cstdio>
+#include <cstdlib>
+
 #include "gpu_common.h"
 #include "k_encode.h"
 #include "tb_coder.h"
@@ -47,6 +50,18 @@ __device__ __forceinline__ void ref_entry(int e, int& bi, int& i) {
   }
 }
 
+// the angular-mode tables in LDS (indexed constexpr tables become global loads on the GPU)
+struct AngleLds {
+  int8_t angle[35];
+  int16_t inv[35];
+  __device__ void load(int tid, int nthreads) {
+    for (int m = tid; m < 35; m += nthreads) {
+      angle[m] = m >= 2 ? (int8_t)intra_angle(m) : 0;
+      inv[m] = m >= 2 ? (int16_t)intra_inv_angle(m) : 0;
+    }
+  }
+};
+
 __global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSet dec, Geo g, const RcTables* rc) {
   const int ctu = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const Penalties& pen = rc->pen[dec.qp[b]];
@@ -57,6 +72,8 @@ __global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSe
   __shared__ bool avl[21][2][65];
   __shared__ int dcv[21];
   __shared__ unsigned best[21], best_ang[21];
+  __shared__ AngleLds ang;
+  ang.load(tid, 256);
   for (int i = tid; i < 1024; i += 256) sblk[i] = S[(cy + (i >> 5)) * g.W + cx + (i & 31)];
   if (tid < 21) best[tid] = best_ang[tid] = 0xffffffffu;
   for (int e = tid; e < 469; e += 256) {
@@ -116,7 +133,7 @@ __global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSe
     int sum = 0;
     for (int q = 0; q < nq * nq; ++q) {
       const int qx = (q % nq) * 8 + (lane & 7), qy = (q / nq) * 8 + (lane >> 3);
-      const int p = intra_pred_pixel(L, T, l2, mode, N < 32, dcv[bi], qx, qy);
+      const int p = intra_pred_pixel_ai(L, T, l2, mode, ang.angle[mode], ang.inv[mode], N < 32, dcv[bi], qx, qy);
       sum += wave_satd8x8((int)sblk[(by + qy) * 32 + bx + qx] - p);
     }
     const unsigned v = ((unsigned)(sum + (mode <= 1 ? pen.mode_dcpl : pen.mode_ang)) << 6) | (unsigned)mode;
@@ -180,41 +197,59 @@ struct CompLds {
   WaveTbScratch tb;
 };
 
+// TV_DIAG_INTRA=1: lane 0 of every wave adds the clock cycles of each phase to
+// g_intra_phase[c][phase] (c = component wave): timing only, printed at engine teardown.
+__device__ unsigned long long g_intra_phase[3][8];
+
 __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec, DecisionSet dec, Geo g, int diag,
-                                                     int cy0) {
+                                                     int cy0, int timing) {
   const int b = blockIdx.y, c = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qp = dec.qp[b];
   __shared__ int Tm[32][33];
   __shared__ CompLds W[3];
-  __shared__ int cus[16][3];
+  __shared__ int cus[16][4];
+  __shared__ AngleLds ang;
+  ang.load(threadIdx.x, 192);
   __shared__ int ncu;
   __shared__ unsigned cbfs[16];
+  long long tph = timing ? (long long)clock64() : 0;
+  auto mark = [&](int ph) {
+    if (!timing) return;
+    const long long t = (long long)clock64();
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_intra_phase[threadIdx.x >> 6][ph], (unsigned long long)(t - tph));
+    tph = t;
+  };
   const int cyi = cy0 + blockIdx.x, cxi = diag - 2 * cyi;
   const int cx = cxi * 32, cy = cyi * 32;
   const long ub = b * g.usz;
   tb_load_matrix(Tm);
-  if (threadIdx.x == 0) {  // CUs of this CTB in z-order
+  // the CTB's 16 8x8-unit sizes and modes, loaded in parallel (one global round trip instead
+  // of a dependent load per CU inside the sequential CU loop)
+  __shared__ uint8_t ul2[16], uipm[16];
+  if (threadIdx.x < 16) {
+    const long u = ub + (long)((cy >> 3) + (threadIdx.x >> 2)) * g.w8 + (cx >> 3) + (threadIdx.x & 3);
+    ul2[threadIdx.x] = dec.cu_log2[u];
+    uipm[threadIdx.x] = dec.ipm[u];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // CUs of this CTB in z-order: x, y, log2, mode
     int n = 0;
-    if (dec.cu_log2[ub + (cy >> 3) * g.w8 + (cx >> 3)] == 5) {
-      cus[0][0] = cx;
-      cus[0][1] = cy;
-      cus[0][2] = 5;
-      n = 1;
+    auto add = [&](int ux, int uy, int l2) {
+      cus[n][0] = cx + 8 * ux;
+      cus[n][1] = cy + 8 * uy;
+      cus[n][2] = l2;
+      cus[n][3] = uipm[uy * 4 + ux];
+      ++n;
+    };
+    if (ul2[0] == 5) {
+      add(0, 0, 5);
     } else {
       for (int q = 0; q < 4; ++q) {
-        const int x16 = cx + (q & 1) * 16, y16 = cy + (q >> 1) * 16;
-        if (dec.cu_log2[ub + (y16 >> 3) * g.w8 + (x16 >> 3)] == 4) {
-          cus[n][0] = x16;
-          cus[n][1] = y16;
-          cus[n][2] = 4;
-          ++n;
+        const int qx = (q & 1) * 2, qy = (q >> 1) * 2;
+        if (ul2[qy * 4 + qx] == 4) {
+          add(qx, qy, 4);
         } else {
-          for (int r = 0; r < 4; ++r) {
-            cus[n][0] = x16 + (r & 1) * 8;
-            cus[n][1] = y16 + (r >> 1) * 8;
-            cus[n][2] = 3;
-            ++n;
-          }
+          for (int r = 0; r < 4; ++r) add(qx + (r & 1), qy + (r >> 1), 3);
         }
       }
     }
@@ -233,18 +268,18 @@ __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec,
     for (int i = lane; i < S; i += 64) L.left[i] = Rp[(long)tv_min(ph - 1, by + i) * pw + tv_max(0, bx - 1)];
   }
   __syncthreads();
+  mark(0);  // matrix + CU list + staging
   const int qpx = c ? chroma_qp(qp, 0) : qp;
   int16_t* coefp = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz);
   for (int k = 0; k < ncu; ++k) {
     const int x0 = cus[k][0], y0 = cus[k][1], log2 = cus[k][2];
-    const int mode = dec.ipm[ub + (y0 >> 3) * g.w8 + (x0 >> 3)];
+    const int mode = cus[k][3];
     const int l2 = log2 - sh, N = 1 << l2;
     const int x = x0 >> sh, y = y0 >> sh;  // TB position (component samples)
     // --- reference samples in canonical order (bottom-left .. corner .. top-right)
     const int total = 4 * N + 1;
-    unsigned long long m[3] = {0, 0, 0};
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
+    // one round = 64 reference positions; the common 8x8 / 4x4 TBs (4N+1 <= 64) need one
+    auto round = [&](int r) -> unsigned long long {
       const int i = lane + 64 * r;
       bool av = false;
       if (i < total) {
@@ -265,9 +300,13 @@ __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec,
         }
         L.V[i] = val;
       }
-      m[r] = __ballot(av);
-    }
+      return __ballot(av);
+    };
+    unsigned long long m[3] = {round(0), 0, 0};
+    if (total > 64) m[1] = round(1);
+    if (total > 128) m[2] = round(2);
     wave_sync();
+    mark(1);  // reference samples + availability
     // --- substitution (H.265 8.4.4.2.2) as a parallel nearest-available search
     for (int i = lane; i < total; i += 64) {
       int j = -1;
@@ -285,6 +324,7 @@ __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec,
       else L.T[i - 2 * N] = v;
     }
     wave_sync();
+    mark(2);  // substitution
     const bool filt = c == 0 && intra_filter_refs(l2, mode);
     if (filt) {
       for (int i = lane; i <= 2 * N; i += 64) {
@@ -303,18 +343,22 @@ __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec,
     const int* RL = filt ? L.FL : L.L;
     const int* RT = filt ? L.FT : L.T;
     const int dc = mode == 1 ? intra_dc_value(RL, RT, l2) : 0;
+    const int ang_a = ang.angle[mode], ang_i = ang.inv[mode];
     for (int i = lane; i < N * N; i += 64) {
       const int px = i & (N - 1), py = i >> l2;
-      const int p = intra_pred_pixel(RL, RT, l2, mode, c == 0 && N < 32, dc, px, py);
+      const int p = intra_pred_pixel_ai(RL, RT, l2, mode, ang_a, ang_i, c == 0 && N < 32, dc, px, py);
       L.pred[i] = (uint8_t)p;
       L.resid[i] = (int16_t)((int)L.src[(y - by + py) * S + (x - bx + px)] - p);
     }
     wave_sync();
+    mark(3);  // filter + prediction + residual
     const int cb = wave_code_tb(L.resid, L.pred, l2, qpx, true, coefp + (long)y * pw + x, pw,
                                 &L.rec[(y - by) * S + (x - bx)], S, Tm, L.tb);
     if (lane == 0 && cb) atomicOr(&cbfs[k], 1u << c);
+    mark(4);  // transform / quant / inverse / recon
   }
   __syncthreads();
+  mark(5);  // waiting for the other component waves
   // write the CTB reconstruction and the per-CU cbf flags back
   uint8_t* Rp = rec.plane(c, b, g) + (long)by * pw + bx;
   for (int i = lane; i < S * S; i += 64) Rp[(long)(i / S) * pw + i % S] = L.rec[i];
@@ -333,7 +377,27 @@ void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& 
     const int cy0 = tv_max(0, (d - (g.wc - 1) + 1) / 2);
     const int cy1 = tv_min(g.hc - 1, d / 2);
     if (cy1 < cy0) continue;
-    k_intra_recon<<<dim3(cy1 - cy0 + 1, B), 192, 0, s>>>(src, rec, dec, g, d, cy0);
+    k_intra_recon<<<dim3(cy1 - cy0 + 1, B), 192, 0, s>>>(src, rec, dec, g, d, cy0, intra_timing() ? 1 : 0);
+  }
+}
+
+bool intra_timing() {
+  static const bool on = [] {
+    const char* e = std::getenv("TV_DIAG_INTRA");
+    return e && *e == '1';
+  }();
+  return on;
+}
+
+void intra_timing_report() {
+  if (!intra_timing()) return;
+  unsigned long long h[3][8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_intra_phase), sizeof(h)) != hipSuccess) return;
+  const char* names[6] = {"staging", "refs", "substitution", "pred+resid", "tb coding", "join"};
+  for (int c = 0; c < 3; ++c) {
+    std::fprintf(stderr, "[TV_DIAG_INTRA] wave %d:", c);
+    for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %s %.1fM", names[k], h[c][k] / 1e6);
+    std::fprintf(stderr, "\n");
   }
 }
 

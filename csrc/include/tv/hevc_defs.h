@@ -67,6 +67,17 @@ TV_HD int dct_coef(int log2N, int k, int n) { return kDct32.m[k << (5 - log2N)][
 // ------------------------------------ quantisation --------------------------------------
 constexpr int kQuantScale[6] = {26214, 23302, 20560, 18396, 16384, 14564};
 constexpr int kLevelScale[6] = {40, 45, 51, 57, 64, 72};
+// Table reads as select chains: indexing the constexpr arrays from device code becomes a
+// global-memory load per coefficient (a ~1 us round trip inside the I-frame wavefront's
+// serial TB chain); the selects are a handful of ALU ops.
+TV_HD int quant_scale(int qp) {
+  const int r = qp % 6;
+  return r == 0 ? 26214 : r == 1 ? 23302 : r == 2 ? 20560 : r == 3 ? 18396 : r == 4 ? 16384 : 14564;
+}
+TV_HD int level_scale(int qp) {
+  const int r = qp % 6;
+  return r == 0 ? 40 : r == 1 ? 45 : r == 2 ? 51 : r == 3 ? 57 : r == 4 ? 64 : 72;
+}
 
 // chroma QP mapping for 4:2:0 (H.265 Table 8-10)
 TV_HD int chroma_qp(int qpy, int offset) {
@@ -80,7 +91,7 @@ TV_HD int chroma_qp(int qpy, int offset) {
 // Decoder-exact scaling (dequantisation) of one level, flat scaling matrix (m = 16).
 TV_HD int dequant_level(int level, int qp, int log2N) {
   const int bdShift = 8 + log2N - 5;  // BitDepth + log2(nTbS) + 10 - 15
-  long long v = (long long)level * 16 * kLevelScale[qp % 6];
+  long long v = (long long)level * 16 * level_scale(qp);
   v = v * (1LL << (qp / 6)) + (1LL << (bdShift - 1));  // multiply: v may be negative
   v >>= bdShift;
   return (int)clip3<long long>(-32768, 32767, v);
@@ -91,7 +102,7 @@ TV_HD int quant_level(int coef, int qp, int log2N, bool intra) {
   const int qbits = 14 + qp / 6 + (15 - 8 - log2N);
   const int add = (intra ? 171 : 85) << (qbits - 9);
   int a = tv_abs(coef);
-  int l = (int)(((long long)a * kQuantScale[qp % 6] + add) >> qbits);
+  int l = (int)(((long long)a * quant_scale(qp) + add) >> qbits);
   if (l > 32767) l = 32767;
   return coef < 0 ? -l : l;
 }
@@ -151,8 +162,21 @@ constexpr int16_t kInvAngle[15] = {-4096, -1638, -910, -630, -482, -390, -315, -
 // `dc` is the DC value of the block (only used by mode 1), `fe` enables the DC/H/V boundary
 // smoothing (luma, N < 32).  Used per lane by the HIP kernels and per block on the CPU.
 template <typename R>
+TV_HD int intra_pred_pixel_ai(const R* left, const R* top, int log2N, int mode, int angle, int inv, bool fe,
+                              int dc, int x, int y);
+// angle / inverse angle of an angular mode (device callers hoist these table reads out of
+// their per-sample loops: an indexed constexpr table is a global-memory load on the GPU)
+TV_HD int intra_angle(int mode) { return kIntraPredAngle[mode]; }
+TV_HD int intra_inv_angle(int mode) { return mode >= 11 && mode <= 25 ? kInvAngle[mode - 11] : 0; }
+template <typename R>
 TV_HD int intra_pred_pixel(const R* left, const R* top, int log2N, int mode, bool fe, int dc, int x,
                            int y) {
+  return intra_pred_pixel_ai(left, top, log2N, mode, mode >= 2 ? intra_angle(mode) : 0,
+                             mode >= 2 ? intra_inv_angle(mode) : 0, fe, dc, x, y);
+}
+template <typename R>
+TV_HD int intra_pred_pixel_ai(const R* left, const R* top, int log2N, int mode, int angle, int inv, bool fe,
+                              int dc, int x, int y) {
   const int N = 1 << log2N;
   if (mode == 0)
     return ((N - 1 - x) * left[y + 1] + (x + 1) * top[N + 1] + (N - 1 - y) * top[x + 1] +
@@ -165,14 +189,12 @@ TV_HD int intra_pred_pixel(const R* left, const R* top, int log2N, int mode, boo
     }
     return dc;
   }
-  const int angle = kIntraPredAngle[mode];
   const bool vert = mode >= 18;
   const R* mainr = vert ? top : left;
   const R* side = vert ? left : top;
   const int i = vert ? x : y, j = vert ? y : x;
   const int pos = (j + 1) * angle;
   const int idx = pos >> 5, fact = pos & 31;
-  const int inv = angle < 0 ? kInvAngle[mode - 11] : 0;
   auto ref = [&](int k) -> int { return k >= 0 ? (int)mainr[k] : (int)side[(k * inv + 128) >> 8]; };
   int v = fact ? ((32 - fact) * ref(i + idx + 1) + fact * ref(i + idx + 2) + 16) >> 5 : ref(i + idx + 1);
   if (fe) {
