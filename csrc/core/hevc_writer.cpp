@@ -207,6 +207,10 @@ class SliceWriter {
   bool avail(int xc, int yc, int xn, int yn) const {
     return zscan_available(xc, yc, xn, yn, cfg_.coded_w, cfg_.coded_h);
   }
+  // the left / upper neighbour of a CU always precedes it in z-scan order (one slice, no
+  // tiles): only the picture edge makes them unavailable
+  static bool has_left(int x0) { return x0 > 0; }
+  static bool has_up(int y0) { return y0 > 0; }
   void bin(int b, int ctx) { enc_.encode_bin(b, ctx_.c[ctx]); }
 
   // sao() (7.3.8.3).  Merges are chosen by exact parameter equality with the left / upper
@@ -252,8 +256,8 @@ class SliceWriter {
     const bool split = fd_.cu_log2[u] < log2;
     if (log2 > kMinCbLog2) {
       int inc = 0;
-      if (avail(x0, y0, x0 - 1, y0) && (kCtbLog2 - fd_.cu_log2[unit(x0 - 1, y0)]) > depth) ++inc;
-      if (avail(x0, y0, x0, y0 - 1) && (kCtbLog2 - fd_.cu_log2[unit(x0, y0 - 1)]) > depth) ++inc;
+      if (has_left(x0) && (kCtbLog2 - fd_.cu_log2[unit(x0 - 1, y0)]) > depth) ++inc;
+      if (has_up(y0) && (kCtbLog2 - fd_.cu_log2[unit(x0, y0 - 1)]) > depth) ++inc;
       bin(split ? 1 : 0, CTX_SPLIT_CU + inc);
     }
     if (split) {
@@ -303,8 +307,8 @@ class SliceWriter {
       }
       const bool skip = !intra && merge_idx >= 0 && cbf == 0;
       int inc = 0;
-      if (avail(x0, y0, x0 - 1, y0) && skip_[unit(x0 - 1, y0)]) ++inc;
-      if (avail(x0, y0, x0, y0 - 1) && skip_[unit(x0, y0 - 1)]) ++inc;
+      if (has_left(x0) && skip_[unit(x0 - 1, y0)]) ++inc;
+      if (has_up(y0) && skip_[unit(x0, y0 - 1)]) ++inc;
       bin(skip ? 1 : 0, CTX_CU_SKIP + inc);
       set_skip(x0, y0, log2, skip ? 1 : 0);
       if (skip) {
@@ -338,9 +342,8 @@ class SliceWriter {
     if (log2 == kMinCbLog2) bin(1, CTX_PART_MODE);  // 2Nx2N
     const int mode = fd_.ipm[u];
     int candA = 1, candB = 1;
-    if (avail(x0, y0, x0 - 1, y0) && fd_.intra[unit(x0 - 1, y0)]) candA = fd_.ipm[unit(x0 - 1, y0)];
-    if (avail(x0, y0, x0, y0 - 1) && fd_.intra[unit(x0, y0 - 1)] &&
-        (y0 - 1) >= ((y0 >> kCtbLog2) << kCtbLog2))
+    if (has_left(x0) && fd_.intra[unit(x0 - 1, y0)]) candA = fd_.ipm[unit(x0 - 1, y0)];
+    if (has_up(y0) && fd_.intra[unit(x0, y0 - 1)] && (y0 - 1) >= ((y0 >> kCtbLog2) << kCtbLog2))
       candB = fd_.ipm[unit(x0, y0 - 1)];
     int mpm[3];
     intra_mpm_list(candA, candB, mpm);
@@ -352,11 +355,8 @@ class SliceWriter {
       enc_.encode_bypass(idx > 0);
       if (idx > 0) enc_.encode_bypass(idx > 1);
     } else {
-      int s[3] = {mpm[0], mpm[1], mpm[2]};
-      std::sort(s, s + 3);
-      int rem = mode;
-      for (int i = 2; i >= 0; --i)
-        if (mode > s[i]) --rem;
+      // rem_intra_luma_pred_mode: the mode minus the MPMs below it (order-free count)
+      const int rem = mode - (mode > mpm[0]) - (mode > mpm[1]) - (mode > mpm[2]);
       enc_.encode_bypass_bins((uint32_t)rem, 5);
     }
     bin(0, CTX_CHROMA_PRED);  // intra_chroma_pred_mode = 4 (DM)
