@@ -5,6 +5,7 @@
 #include <string>
 #include <vector>
 
+#include "tv/container.h"
 #include "tv/cpu_encoder.h"
 #include "tv/hevc_codec.h"
 #include "tv/synth.h"
@@ -61,7 +62,9 @@ void* tv_cpu_encoder_new(int width, int height, int qp, int deblock, int range, 
   cfg.sao = (deblock & 2) != 0;
   cfg.max_merge_cand = max_merge;
   cfg.finalize();
-  return new CpuEncoder(cfg, range);
+  CpuEncoder* e = nullptr;  // a bad config becomes tv_last_error, not an abort across the FFI
+  guard([&] { e = new CpuEncoder(cfg, range); });
+  return e;
 }
 void* tv_cpu_encoder_new_crf(int width, int height, int qp, int deblock, int range, int max_merge, int crf) {
   SeqConfig cfg;
@@ -73,7 +76,9 @@ void* tv_cpu_encoder_new_crf(int width, int height, int qp, int deblock, int ran
   cfg.max_merge_cand = max_merge;
   cfg.crf = crf;
   cfg.finalize();
-  return new CpuEncoder(cfg, range);
+  CpuEncoder* e = nullptr;  // a bad config becomes tv_last_error, not an abort across the FFI
+  guard([&] { e = new CpuEncoder(cfg, range); });
+  return e;
 }
 void tv_cpu_encoder_free(void* e) { delete static_cast<CpuEncoder*>(e); }
 int tv_cpu_encoder_encode(void* e, const uint8_t* y, const uint8_t* u, const uint8_t* v, int sy,
@@ -235,6 +240,13 @@ int tv_mux_mp4_file(const uint8_t* const* segs, const size_t* sizes, int nseg, i
                     const char* path, unsigned long long* out_size) {
   return guard([&] { *out_size = mux_mp4_file(segs, sizes, nseg, w, h, fps_num, fps_den, path); });
 }
+int tv_mux_file(const uint8_t* const* segs, const size_t* sizes, int nseg, int w, int h, int fps_num, int fps_den,
+                const SideTrack* tracks, int ntracks, int container, const char* path, unsigned long long* out_size) {
+  return guard([&] {
+    *out_size = mux_file(segs, sizes, nseg, w, h, fps_num, fps_den, tracks, ntracks, container, path);
+  });
+}
+size_t tv_side_track_size() { return sizeof(SideTrack); }
 int tv_demux_mp4(const uint8_t* mp4, size_t n, int* w, int* h, int* nframes, int* timescale,
                  int* delta, void* out) {
   return guard([&] { static_cast<Bytes*>(out)->v = demux_mp4(mp4, n, w, h, nframes, timescale, delta); });

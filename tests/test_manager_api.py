@@ -227,15 +227,24 @@ def test_policy_and_wol(mgr):
 
 
 def test_unreadable_container_is_rejected_up_front(mgr):
-    """A container the engine cannot demux (.mkv: no ffmpeg here) is REJECTED at add_job
-    with the probe reason, never dispatched to fail later."""
+    """A container the engine cannot demux (a broken .mkv, or Matroska whose video is not
+    HEVC: no H.264 decoder here) is REJECTED at add_job with the probe reason, never
+    dispatched to fail later."""
+    from thinvids_amd.models import hevc, streams
+
     c, st, root = mgr["c"], mgr["st"], mgr["root"]
     (root / "watch" / "film.mkv").write_bytes(b"\x1aE\xdf\xa3" + b"\0" * 64)
-    r = c.post("/add_job", json={"filename": "film.mkv"})
-    assert r.status_code in (200, 201), r.get_data(as_text=True)
-    job = st.hgetall(f"job:{r.get_json()['job_id']}")
-    assert job["status"] == "REJECTED" and job["rejected_reason"] == "probe_failed"
-    assert "unsupported" in job["error"]
+    bs, _ = hevc.encode_sequence_cpu([hevc.synth_frame(1, 0, 32, 32)], qp=30, search_range=16)
+    avc = str(root / "watch" / "avc.mkv")
+    streams.mux([bs], 32, 32, 25, 1, avc, [], streams.CONTAINER_MKV)
+    raw = open(avc, "rb").read()
+    open(avc, "wb").write(raw.replace(b"V_MPEGH/ISO/HEVC", b"V_MPEG4/ISO/AVC\0"))
+    for name, why in (("film.mkv", "mkv"), ("avc.mkv", "HEVC only")):
+        r = c.post("/add_job", json={"filename": name})
+        assert r.status_code in (200, 201), r.get_data(as_text=True)
+        job = st.hgetall(f"job:{r.get_json()['job_id']}")
+        assert job["status"] == "REJECTED" and job["rejected_reason"] == "probe_failed"
+        assert why in job["error"], job["error"]
 
 
 def test_job_settings_encoder_overrides(mgr):

@@ -239,3 +239,48 @@ def test_stamp_streams_in_gop_chunks(env, monkeypatch):
         assert np.mean(np.abs(ref[0].astype(int) - frames[t][0].astype(int))) > 0.1
     new = store.hgetall(f"job:{res['new_job_id']}")
     assert new["status"] == "READY" and new["input_path"] == res["output"]
+
+
+def test_transcode_carries_audio_and_english_subtitles(env):
+    """Sidecar audio + English SubRip next to the source: the stitcher carries both and the
+    output becomes Matroska (reference rule, worker/tasks.py:2126-2223), with the
+    english_subtitles_* job fields set; the HEVC video inside decodes to every frame."""
+    import struct
+
+    from thinvids_amd.models import streams
+
+    store, tasks = env["store"], env["tasks"]
+    path, frames = _source(env["root"], "withsubs.y4m", n=16)
+    base = os.path.splitext(str(path))[0]
+    rate, pcm = 8000, (np.arange(8000, dtype=np.int64) % 200 * 50 - 5000).astype("<i2").tobytes()
+    with open(base + ".wav", "wb") as f:
+        f.write(b"RIFF" + struct.pack("<I", 36 + len(pcm)) + b"WAVE")
+        f.write(b"fmt " + struct.pack("<IHHIIHH", 16, 1, 1, rate, rate * 2, 2, 16))
+        f.write(b"data" + struct.pack("<I", len(pcm)) + pcm)
+    with open(base + ".en.srt", "w") as f:
+        f.write("1\n00:00:00,040 --> 00:00:00,300\nfirst cue\n\n2\n00:00:00,320 --> 00:00:00,600\nsecond cue\n")
+    job_id, tok = str(uuid.uuid4()), uuid.uuid4().hex
+    store.hset(f"job:{job_id}", mapping={
+        "job_id": job_id, "filename": "withsubs.y4m", "input_path": str(path), "status": "STARTING",
+        "pipeline_run_token": tok, "software_encode": "1", "processing_mode": "split"})
+    tasks.transcode(job_id, tok)
+    assert _wait_status(store, job_id, {"DONE", "FAILED"}) == "DONE", store.hgetall(f"job:{job_id}")
+    job = store.hgetall(f"job:{job_id}")
+    out = job["output_path"]
+    assert out.endswith("withsubs.mkv") and os.path.isfile(out)
+    assert (int(job["english_subtitles_found"]), int(job["english_subtitles_kept"])) == (1, 1)
+    assert int(job["audio_streams_kept"]) == 1 and int(job["dest_streams"]) == 3
+    assert job["dest_codec"] == "hevc" and job["dest_resolution"] == "128x96"
+    annexb, _, _ = streams.mkv_hevc_annexb(out)
+    dec = hevc.decode(annexb, coded=False)
+    assert len(dec.frames) == len(frames)
+    side, _ = streams.mkv_streams(out)
+    audio = [s for s in side if s.kind == streams.SIDE_AUDIO][0]
+    subs = [s for s in side if s.kind == streams.SIDE_SUBTITLE][0]
+    with open(out, "rb") as f:
+        got = b""
+        for o, n in zip(audio.offsets, audio.sizes):
+            f.seek(int(o))
+            got += f.read(int(n))
+    assert got == pcm
+    assert subs.language == "eng" and list(subs.pts) == [40, 320]

@@ -45,7 +45,7 @@ def _hipcc() -> str:
 
 
 def _headers() -> list[Path]:
-    return sorted(INC.rglob("*.h")) + sorted((CSRC / "gpu").glob("*.h"))
+    return sorted(INC.rglob("*.h")) + sorted((CSRC / "core").glob("*.h")) + sorted((CSRC / "gpu").glob("*.h"))
 
 
 def core_sources() -> list[Path]:

@@ -56,6 +56,8 @@ class CpuEncoder:
         else:
             self.h = self.lib.tv_cpu_encoder_new(width, height, qp, int(deblock) | (2 if sao else 0), search_range,
                                                  max_merge)
+        if not self.h:
+            raise ValueError(self.lib.tv_last_error().decode())
         self.out = Bytes()
 
     def __del__(self):

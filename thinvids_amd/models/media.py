@@ -7,7 +7,10 @@ Readable inputs (no ffmpeg in this image, so only formats we can decode ourselve
   come back as uint16 planes and are tone-mapped on the GPU before encoding);
 * ``.synth`` — JSON ``{"width", "height", "frames", "fps", "seed"}``: the procedural source
   of :mod:`thinvids_amd.models.hevc` (P5 "direct source" with zero I/O);
-* ``.hevc`` / ``.265`` / ``.mp4`` produced by this engine (decoded with the oracle decoder).
+* ``.hevc`` / ``.265`` / ``.mp4`` / ``.mkv`` whose video is HEVC (decoded with the oracle
+  decoder; Matroska is indexed by :mod:`thinvids_amd.models.streams`).  Audio and subtitle
+  streams of a source (and sidecar ``.wav`` / ``.srt`` files) are listed by :func:`probe`
+  and carried into the output by the stitcher.
 
 Every source exposes ``width, height, fps_num, fps_den, nframes`` and
 ``read(start, n) -> list[(Y, U, V)]``.
@@ -23,7 +26,7 @@ import numpy as np
 
 from . import hevc
 
-VIDEO_EXTS = (".y4m", ".synth", ".hevc", ".265", ".mp4")
+VIDEO_EXTS = (".y4m", ".synth", ".hevc", ".265", ".mp4", ".mkv")
 
 
 # ------------------------------------------------------------------------------ Y4M
@@ -156,10 +159,18 @@ class HevcSource:
 
     def __init__(self, path: str):
         self.path = path
-        with open(path, "rb") as f:
-            data = f.read()
         self.fps_num, self.fps_den = 30, 1
-        if path.endswith(".mp4"):
+        if path.lower().endswith(".mkv"):
+            from .streams import mkv_hevc_annexb
+
+            data, vt, _ = mkv_hevc_annexb(path)
+            if vt.default_duration_ns:
+                fr = Fraction(10 ** 9, vt.default_duration_ns).limit_denominator(1001)
+                self.fps_num, self.fps_den = fr.numerator, fr.denominator
+        else:
+            with open(path, "rb") as f:
+                data = f.read()
+        if path.lower().endswith(".mp4"):
             dm = hevc.demux_mp4(data)
             data = dm["annexb"]
             ts, d = dm["timescale"], dm["sample_delta"]
@@ -184,7 +195,7 @@ def open_source(path: str):
         return Y4MSource(path)
     if ext == ".synth":
         return SynthSource(path)
-    if ext in (".hevc", ".265", ".mp4"):
+    if ext in (".hevc", ".265", ".mp4", ".mkv"):
         return HevcSource(path)
     raise ValueError(f"unsupported input format: {path}")
 
@@ -209,6 +220,21 @@ def probe(path: str) -> dict:
         "size": size,
         "bits": int(getattr(src, "bits", 8)),
         "bitrate_kbps": round(size * 8 / dur / 1000.0, 1) if dur else 0.0,
-        "streams": [{"index": 0, "codec_type": "video", "codec_name": codec, "width": src.width,
-                     "height": src.height}],
+        "streams": _stream_list(path, codec, src),
     }
+
+
+def _stream_list(path: str, codec: str, src) -> list[dict]:
+    """ffprobe-like stream list: the video stream, then the source's audio / subtitle streams
+    (container tracks and sidecar files, :func:`thinvids_amd.models.streams.source_streams`)."""
+    from .streams import source_streams
+
+    out = [{"index": 0, "codec_type": "video", "codec_name": codec, "width": src.width, "height": src.height}]
+    try:
+        side, desc = source_streams(path)
+    except ValueError:
+        return out
+    for d in desc:
+        if d.get("codec_type") in ("audio", "subtitle"):
+            out.append({"index": len(out), **d})
+    return out

@@ -272,6 +272,19 @@ def _encode_many(items: list, cache) -> tuple[dict, dict]:
     return out, st
 
 
+def _side_plan(input_path: str):
+    """Audio / English-subtitle streams of the source for the output container (None when
+    the source cannot be indexed: the video output is kept, as the reference keeps its MP4
+    when the subtitle remux fails, worker/tasks.py:2202-2219)."""
+    from ..models.streams import plan_output
+
+    try:
+        return plan_output(input_path)
+    except Exception as e:  # noqa: BLE001
+        print(f"[node_job] side streams skipped: {e}", file=sys.stderr, flush=True)
+        return None
+
+
 def run_job(input_path: str, output: str, height: int | None = None, qp: int = 27, gop: int = 64,
             segment_frames: int = 256, mode: str = "direct", bitrate_kbps: float = 0.0, ladder=None,
             search_range: int = 64, software: bool = False, batch_segments: int = 8,
@@ -280,6 +293,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     import torch
 
     from ..models import hevc, media
+    from ..models.streams import write_output
     from ..worker.encoder import EncodeSpec, EngineCache, PartStats, SynthRange, gpu_available, psnr_from_sse
     from ..worker.helpers import output_geometry
     from .comm import allreduce_stats, gather_bytes_to_root, scatter_frames_from_root
@@ -566,13 +580,12 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         if missing:
             raise RuntimeError(f"segments missing at stitch: {missing}")
         outs = []
+        side = _side_plan(input_path)
         for r, (ow, oh) in enumerate(rungs):
             seg_bits = [streams[(r, i)] for i in range(len(segs))]
             path = output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4"
-            tmp = path + ".tmp"
             with trace.span("node_job.mux"):  # streamed from the gathered buffers, no joined copy
-                nbytes = hevc.mux_mp4_file(seg_bits, ow, oh, src.fps_num, src.fps_den, tmp)
-            os.replace(tmp, path)
+                path, nbytes = write_output(seg_bits, ow, oh, src.fps_num, src.fps_den, path, side)
             q = psnr_from_sse(qv[r, 1:], ow * oh * qv[r, 0]) if qv[r, 0] else {}
             outs.append({"path": path, "bytes": nbytes, "width": ow, "height": oh, "frames": nfr,
                          "fps_num": src.fps_num, "fps_den": src.fps_den,
@@ -580,6 +593,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                          "psnr_y": round(q["y"], 3) if q else None, "psnr_yuv": round(q["yuv"], 3) if q else None,
                          "quality_frames": int(qv[r, 0])})
         el = time.time() - t0
+        result.update(side_fields=side.fields if side else {}, side_warnings=side.warnings if side else [])
         result.update(trace=trace.summary(), per_rank=per_rank, outputs=outs, qp_plan=[[round(float(np.mean(q)), 2) for q in row] for row in rc["plan"]] if rc["plan"] else
                       [[qp] * len(segs) for _ in rungs], rc_offset=round(rc["fb"].offset(), 3),
                       seconds=round(el, 3), encode_seconds=round(t_enc, 3),

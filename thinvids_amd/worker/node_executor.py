@@ -218,12 +218,13 @@ def _publish(job_id: str, spec: dict, res: dict) -> None:
     st = get_store()
     job = spec["job"]
     t_comb = now()
-    final = final_output_path(str(job.get("filename") or f"{job_id}.mp4"))
-    ensure_dirs(os.path.dirname(final))
     outs = res["outputs"]
+    ext = os.path.splitext(outs[0]["path"])[1] or ".mp4"  # .mkv when English subtitles are carried
+    final = final_output_path(str(job.get("filename") or f"{job_id}.mp4"), ext)
+    ensure_dirs(os.path.dirname(final))
     finals = []
     for k, o in enumerate(outs):
-        dst = final if k == 0 else f"{os.path.splitext(final)[0]}_{o['height']}p.mp4"
+        dst = final if k == 0 else f"{os.path.splitext(final)[0]}_{o['height']}p{os.path.splitext(o['path'])[1]}"
         tmp = dst + ".tmp"
         shutil.move(o["path"], tmp)
         os.replace(tmp, dst)
@@ -245,6 +246,7 @@ def _publish(job_id: str, spec: dict, res: dict) -> None:
                   dest_bitrate_kbps=f"{os.path.getsize(finals[0]) * 8 / dur / 1000 if dur else 0:.0f}",
                   english_subtitles_found=0, english_subtitles_supported=0, english_subtitles_kept=0,
                   subtitle_warning="")
+    fields.update(res.get("side_fields") or {})
     st.hset(job_key(job_id), mapping={k: ("" if v is None else v) for k, v in fields.items()})
     st.srem(ACTIVE_JOBS_KEY, job_id)
     shutil.rmtree(spec["base"], ignore_errors=True)

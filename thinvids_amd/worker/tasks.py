@@ -423,18 +423,21 @@ def _ready_set(enc_dir: str, total: int, stable_sec: float) -> set:
     return ready
 
 
-def concat_parts(paths: list[str], out_path: str, width: int, height: int, fps_num: int, fps_den: int) -> int:
-    """Concatenate encoded MP4 parts (each a run of closed GOPs) into one faststart MP4
-    (reference `ffmpeg -f concat -c copy +faststart`, :2047-2120)."""
+def concat_parts(paths: list[str], out_path: str, width: int, height: int, fps_num: int, fps_den: int,
+                 plan=None) -> tuple[str, int]:
+    """Concatenate encoded MP4 parts (each a run of closed GOPs) into one faststart file
+    (reference `ffmpeg -f concat -c copy +faststart`, :2047-2120) together with the source's
+    side streams of `plan` (:func:`thinvids_amd.models.streams.plan_output`; the reference's
+    subtitle remux pass :2126-2223 folds into this one write).  Returns (path, bytes): the
+    extension is the plan's (.mkv when English subtitles are carried)."""
+    from ..models import streams
+
     segs = []
-    for p in paths:  # each part's elementary stream; the MP4 is streamed from these buffers
+    for p in paths:  # each part's elementary stream; the output is streamed from these buffers
         with open(p, "rb") as f:
             segs.append(hevc.demux_mp4(f.read())["annexb"])
-    tmp = out_path + ".tmp"
     ensure_dirs(os.path.dirname(out_path) or ".")
-    n = hevc.mux_mp4_file(segs, width, height, fps_num, fps_den, tmp)
-    os.replace(tmp, out_path)
-    return n
+    return streams.write_output(segs, width, height, fps_num, fps_den, out_path, plan)
 
 
 @pipeline_q.task(retries=0)
@@ -500,11 +503,12 @@ def stitch(job_id: str, run_token: str | None = None):
     fn, fd = _fps(job)
     out_local = os.path.join(base, f"job_{job_id}_output.mp4")
     paths = [os.path.join(enc_dir, f"enc_{i:03d}.mp4") for i in range(1, total + 1)]
+    plan = _side_plan(job_id, job)
     try:
         fault.check("stitch", "*")
         with trace.span("stitch.concat"):
-            concat_parts(paths, out_local, spec.width, spec.height, fn, fd)
-        final = final_output_path(str(job.get("filename") or f"{job_id}.mp4"))
+            out_local, _ = concat_parts(paths, out_local, spec.width, spec.height, fn, fd, plan)
+        final = final_output_path(str(job.get("filename") or f"{job_id}.mp4"), plan.ext if plan else ".mp4")
         ensure_dirs(os.path.dirname(final))
         tmp = final + ".tmp"
         shutil.move(out_local, tmp)
@@ -517,8 +521,9 @@ def stitch(job_id: str, run_token: str | None = None):
         d = media.probe(final)
         _set(job_id, dest_file_size=d["size"], dest_duration=f"{d['duration']:.2f}", dest_codec=d["codec"],
              dest_resolution=d["resolution"], dest_fps=f"{d['fps']:.2f}",
-             dest_bitrate_kbps=f"{d['bitrate_kbps']:.0f}", english_subtitles_found=0,
-             english_subtitles_supported=0, english_subtitles_kept=0, subtitle_warning="")
+             dest_bitrate_kbps=f"{d['bitrate_kbps']:.0f}", dest_streams=len(d["streams"]),
+             **(plan.fields if plan else {"english_subtitles_found": 0, "english_subtitles_supported": 0,
+                                          "english_subtitles_kept": 0, "subtitle_warning": ""}))
     except Exception:
         log.warning("[%s] dest probe failed", job_id)
     shutil.rmtree(base, ignore_errors=True)
@@ -532,6 +537,26 @@ def stitch(job_id: str, run_token: str | None = None):
     st.delete(f"job_done_parts:{job_id}", f"job_retry_counts:{job_id}", f"job_retry_ts:{job_id}",
               f"job_missing_first_seen:{job_id}", f"job_retry_inflight:{job_id}")
     return {"status": "COMPLETED", "output": final}
+
+
+def _side_plan(job_id: str, job: dict):
+    """Side streams of the job's source for the output (audio copy, English subtitles);
+    None (video-only MP4) when the source cannot be indexed — the video is never lost over
+    a side-stream problem (the reference likewise keeps the MP4 when its remux fails,
+    :2202-2219)."""
+    from ..models import streams
+
+    src = resolve_input_path(job)
+    try:
+        plan = streams.plan_output(src)
+    except Exception as e:  # noqa: BLE001
+        log.warning("[%s] side streams skipped: %s", job_id, e)
+        _set(job_id, subtitle_warning=f"side streams skipped: {e}"[:500])
+        return None
+    for w in plan.warnings:
+        emit_activity(f'{w} for "{job_title(job)}"', job_id=job_id, filename=job.get("filename"),
+                      stage="subtitle_warning", source="worker")
+    return plan
 
 
 def _redispatch(job_id: str, idx: int, run_token: str | None) -> None:

@@ -4,13 +4,17 @@
 // Built together with csrc/core/*.cpp under -fsanitize=address,undefined by
 // tools/sanitize_core.sh (tests/test_sanitize.py runs it on the CPU): a golden-encoder
 // round trip (IDR + P frames with deblocking and SAO) through the oracle decoder, MP4
-// mux/demux, the AV1 multi-symbol range coder and the CDEF direction search.  Any
+// mux/demux, MP4 and Matroska muxing with audio + subtitle side streams, the AV1 multi-symbol range coder and the CDEF direction search.  Any
 // out-of-bounds access, use-after-free, leak or undefined behaviour aborts with a report;
 // a functional mismatch exits 1.
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <unistd.h>
 #include <vector>
+
+#include "tv/container.h"
 
 extern "C" {
 const char* tv_last_error();
@@ -32,6 +36,8 @@ void tv_decoder_info(void*, int*, int*, int*, int*, int*);
 int tv_decoder_frame(void*, int idx, int cropped, uint8_t*, uint8_t*, uint8_t*);
 int tv_mux_mp4(const uint8_t*, size_t, int w, int h, int fps_num, int fps_den, void* out);
 int tv_demux_mp4(const uint8_t*, size_t, int* w, int* h, int* nframes, int* timescale, int* delta, void* out);
+int tv_mux_file(const uint8_t* const* segs, const size_t* sizes, int nseg, int w, int h, int fps_num, int fps_den,
+                const tv::SideTrack* tracks, int ntracks, int container, const char* path, unsigned long long* out);
 int tv_av1_rc_roundtrip(const int* sym, const int* alpha, const int* ctx, int n, int nctx, int adapt, void* out,
                         int* dec);
 void tv_av1_cdef_find_dirs(const uint8_t* Y, int w, int h, uint8_t* dir, int* var);
@@ -80,6 +86,46 @@ int main() {
     int mw, mh, mn, ts, dl;
     if (tv_demux_mp4(tv_bytes_data(mp4), tv_bytes_size(mp4), &mw, &mh, &mn, &ts, &dl, es)) return fail("demux");
     if (mw != W || mh != H || mn != N) return fail("demux geometry");
+    // 2b) the same stream with an in-memory audio track and a subtitle track with a gap and
+    //     an overlap, as interleaved MP4 and as Matroska, then the MP4 video back out
+    {
+      std::vector<uint8_t> pay(4000);
+      for (auto& b : pay) b = (uint8_t)rnd();
+      const int na = 20;
+      std::vector<uint64_t> ao(na);
+      std::vector<uint32_t> as(na), ad(na, 1024);
+      std::vector<int64_t> ap(na);
+      for (int i = 0; i < na; ++i) ao[i] = (uint64_t)i * 150, as[i] = 100 + (uint32_t)(rnd() % 50), ap[i] = 1024 * i;
+      const uint8_t asc[2] = {0x11, 0x90};
+      const char text[] = "firstsecond";
+      const uint64_t so[2] = {0, 5};
+      const uint32_t ss[2] = {5, 6}, sd[2] = {900, 300};
+      const int64_t sp[2] = {40, 500};
+      tv::SideTrack tr[2] = {};
+      tr[0] = {tv::SIDE_AUDIO, tv::SIDE_AAC, 48000, 2, 48000, 16, 1, 0, {'e', 'n', 'g', 0}, nullptr, asc, 2,
+               nullptr, pay.data(), na, ao.data(), as.data(), ap.data(), ad.data()};
+      tr[1] = {tv::SIDE_SUBTITLE, tv::SIDE_SUBRIP, 1000, 0, 0, 0, 0, 0, {'e', 'n', 'g', 0}, nullptr, nullptr, 0,
+               nullptr, (const uint8_t*)text, 2, so, ss, sp, sd};
+      const uint8_t* segs[1] = {stream.data()};
+      const size_t sizes[1] = {stream.size()};
+      unsigned long long bytes = 0;
+      char mp4p[] = "/tmp/tv_sanitize_XXXXXX";
+      const int fd = mkstemp(mp4p);
+      if (fd < 0) return fail("mkstemp");
+      close(fd);
+      if (tv_mux_file(segs, sizes, 1, W, H, 25, 1, tr, 2, tv::CONTAINER_MKV, mp4p, &bytes) || bytes < stream.size())
+        return fail("mkv mux");
+      if (tv_mux_file(segs, sizes, 1, W, H, 25, 1, tr, 2, tv::CONTAINER_MP4, mp4p, &bytes)) return fail("mp4 mux");
+      std::vector<uint8_t> file(bytes);
+      FILE* f = std::fopen(mp4p, "rb");
+      const bool rd = f && std::fread(file.data(), 1, file.size(), f) == file.size();
+      if (f) std::fclose(f);
+      std::remove(mp4p);
+      if (!rd) return fail("mp4 read back");
+      void* es2 = tv_bytes_new();
+      if (tv_demux_mp4(file.data(), file.size(), &mw, &mh, &mn, &ts, &dl, es2) || mn != N) return fail("side demux");
+      tv_bytes_free(es2);
+    }
     tv_bytes_free(mp4);
     tv_bytes_free(es);
     tv_decoder_free(dec);
