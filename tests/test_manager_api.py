@@ -287,3 +287,32 @@ def test_nodes_detail_fields(mgr):
     assert 'id="jobset"' in html and 'id="video"' in html and "function step(" in html
     assert "TVHIST" in c.get("/metrics").get_data(as_text=True)
     assert "function detail(" in c.get("/nodes").get_data(as_text=True)
+
+
+def test_probe_lists_streams_and_prefers_english_audio(mgr):
+    """Source probe (reference get_video_details :2120-2220): streams_json groups video /
+    audio / subtitle streams with codec + language, and the first English audio stream is
+    selected; the stitcher later maps exactly that one (`-map 0:a:{sel}`)."""
+    import numpy as np
+
+    from thinvids_amd.models import streams
+
+    c, st, root = mgr["c"], mgr["st"], mgr["root"]
+    bs, _ = hevc.encode_sequence_cpu([hevc.synth_frame(1, t, 32, 32) for t in range(3)], qp=30, search_range=16)
+
+    def pcm(lang, fill):
+        return streams.SideStream(streams.SIDE_AUDIO, streams.SIDE_PCM_S16LE, "pcm_s16le", lang, 8000, 1, 8000, 16,
+                                  data=bytes([fill]) * 1600, offsets=np.zeros(1, np.uint64),
+                                  sizes=np.asarray([1600], np.uint32), pts=np.zeros(1, np.int64),
+                                  durs=np.asarray([800], np.uint32))
+    sub = streams._text_stream([(0, 90, "hi")], "eng", "subrip", "srt")
+    src = str(root / "watch" / "multi.mkv")
+    streams.mux([bs], 32, 32, 25, 1, src, [pcm("fra", 1), pcm("eng", 2), sub], streams.CONTAINER_MKV)
+    jid = c.post("/add_job", json={"filename": "multi.mkv", "force_paused": True}).json["job_id"]
+    job = st.hgetall(f"job:{jid}")
+    sj = json.loads(job["streams_json"])
+    assert [a["language"] for a in sj["audio"]] == ["fra", "eng"] and sj["video"][0]["codec"] == "hevc"
+    assert sj["subtitle"][0]["codec"] == "subrip" and int(job["selected_a_stream"]) == 1
+    plan = streams.plan_output(src, int(job["selected_a_stream"]))
+    assert plan.ext == ".mkv" and [t.language for t in plan.tracks] == ["eng", "eng"]
+    assert plan.tracks[0].kind == streams.SIDE_AUDIO and plan.fields["audio_streams_kept"] == 1

@@ -247,12 +247,34 @@ def get_video_details(path: str) -> dict:
         size = os.path.getsize(path) if os.path.exists(path) else 0
         return {"source_codec": "unknown", "source_resolution": "", "source_duration": "0", "source_fps": "0",
                 "source_file_size": size, "total_frames": 0, "streams_json": "[]", "probe_error": str(e)[:500]}
+    groups = {"video": [], "audio": [], "subtitle": []}
+    for s in info["streams"]:
+        kind = s.get("codec_type")
+        if kind not in groups:
+            continue
+        tags = s.get("tags") or {}
+        e = {"index": int(s.get("index", 0)), "codec": s.get("codec_name") or "", "title": tags.get("title") or "",
+             "language": tags.get("language") or "", "disposition_default": len(groups[kind]) == 0}
+        if kind == "video":
+            e.update(width=int(s.get("width") or 0), height=int(s.get("height") or 0), fps=info["fps"],
+                     nb_frames=info["frames"])
+        elif kind == "audio":
+            e.update(channels=int(s.get("channels") or 0), sample_rate=int(s.get("sample_rate") or 0))
+        groups[kind].append(e)
+    # first English audio stream, else the first (reference :2193-2198)
+    a_sel = next((i for i, a in enumerate(groups["audio"]) if _is_english(a["language"])), 0)
     return {"source_codec": info["codec"], "source_resolution": info["resolution"],
             "source_width": info["width"], "source_height": info["height"],
             "source_duration": f"{info['duration']:.3f}", "source_fps": f"{info['fps']:.3f}",
             "source_fps_num": info["fps_num"], "source_fps_den": info["fps_den"],
             "source_file_size": info["size"], "source_bitrate_kbps": info["bitrate_kbps"],
-            "total_frames": info["frames"], "streams_json": json.dumps(info["streams"])}
+            "total_frames": info["frames"], "streams_json": json.dumps(groups), "selected_v_stream": 0,
+            "selected_a_stream": a_sel}
+
+
+def _is_english(lang: str) -> bool:
+    lang = (lang or "").strip().lower()
+    return lang in ("eng", "en", "english") or lang.startswith("en-")
 
 
 # ------------------------------------------------------------- scheduler (C24)

@@ -683,11 +683,16 @@ class OutputPlan:
     warnings: list
 
 
-def plan_output(src_path: str | None) -> OutputPlan:
+def plan_output(src_path: str | None, audio_index: int | None = 0) -> OutputPlan:
     """Which side streams go into the output and in which container (reference rule,
-    worker/tasks.py:2126-2164: Matroska iff copy-safe English subtitles exist)."""
+    worker/tasks.py:2126-2164: Matroska iff copy-safe English subtitles exist).  Like the
+    reference's ``-map 0:a:{selected_a_stream}?`` (:1151, :1553) one audio stream is kept —
+    the job's selected one (out of range: the first); ``audio_index=None`` keeps them all."""
     streams = source_streams(src_path)[0] if src_path and os.path.exists(src_path) else []
-    audio = [s for s in streams if s.kind == SIDE_AUDIO and s.nsamples]
+    audio = [s for s in streams if s.kind == SIDE_AUDIO]
+    if audio_index is not None and audio:
+        audio = [audio[audio_index if 0 <= audio_index < len(audio) else 0]]
+    audio = [s for s in audio if s.nsamples]
     subs_en = [s for s in streams if s.kind == SIDE_SUBTITLE and s.language in ENGLISH]
     ok = [s for s in subs_en if s.codec_name in COPY_SAFE_SUBS and s.nsamples and s.codec != SIDE_MP4_ENTRY]
     bad = [s for s in subs_en if s not in ok]

@@ -272,14 +272,14 @@ def _encode_many(items: list, cache) -> tuple[dict, dict]:
     return out, st
 
 
-def _side_plan(input_path: str):
+def _side_plan(input_path: str, audio_stream: int = 0):
     """Audio / English-subtitle streams of the source for the output container (None when
     the source cannot be indexed: the video output is kept, as the reference keeps its MP4
     when the subtitle remux fails, worker/tasks.py:2202-2219)."""
     from ..models.streams import plan_output
 
     try:
-        return plan_output(input_path)
+        return plan_output(input_path, audio_stream)
     except Exception as e:  # noqa: BLE001
         print(f"[node_job] side streams skipped: {e}", file=sys.stderr, flush=True)
         return None
@@ -289,7 +289,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             segment_frames: int = 256, mode: str = "direct", bitrate_kbps: float = 0.0, ladder=None,
             search_range: int = 64, software: bool = False, batch_segments: int = 8,
             resume_dir: str | None = None, max_retries: int = 3, hooks: JobHooks | None = None,
-            deblock: bool = True, sao: bool = False, cache=None, crf: int = 0, scenecut: bool = False) -> dict:
+            deblock: bool = True, sao: bool = False, cache=None, crf: int = 0, scenecut: bool = False,
+            audio_stream: int = 0) -> dict:
     import torch
 
     from ..models import hevc, media
@@ -580,7 +581,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         if missing:
             raise RuntimeError(f"segments missing at stitch: {missing}")
         outs = []
-        side = _side_plan(input_path)
+        side = _side_plan(input_path, audio_stream)
         for r, (ow, oh) in enumerate(rungs):
             seg_bits = [streams[(r, i)] for i in range(len(segs))]
             path = output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4"

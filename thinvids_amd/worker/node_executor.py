@@ -193,7 +193,8 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                       ladder=p["ladder"], search_range=p["search_range"], software=p["software"],
                       batch_segments=p["batch_segments"], hooks=hooks, deblock=p["deblock"], sao=p["sao"],
                       cache=None if p["software"] else cache, crf=p["crf"], resume_dir=spec["ckpt"],
-                      scenecut=p.get("scenecut", False))
+                      scenecut=p.get("scenecut", False),
+                      audio_stream=int(spec["job"].get("selected_a_stream") or 0))
     except Exception as e:
         if is_comm_failure(e):  # the job is fine, the communicator is not: requeue + re-init
             log.error("[%s] communicator failure on rank %d: %s", job_id, rank, e)

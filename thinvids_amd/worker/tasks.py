@@ -548,7 +548,7 @@ def _side_plan(job_id: str, job: dict):
 
     src = resolve_input_path(job)
     try:
-        plan = streams.plan_output(src)
+        plan = streams.plan_output(src, int(job.get("selected_a_stream") or 0))
     except Exception as e:  # noqa: BLE001
         log.warning("[%s] side streams skipped: %s", job_id, e)
         _set(job_id, subtitle_warning=f"side streams skipped: {e}"[:500])
