@@ -1,0 +1,1669 @@
+// av1_codec.cpp — AV1 encode path of the C++ golden model (BASELINE
+// config #4): OBU / sequence header / uncompressed frame header / tile syntax, the decoder
+// oracle, shared reconstruction (intra / inter prediction, dequantisation, inverse
+// transform, deblocking, CDEF) and the golden encoder the gfx950 engine reproduces.
+//
+// The partition / mode-info / motion-vector / coefficient syntax is written ONCE as a
+// template over the symbol direction (SymW encodes the given values, SymR decodes them),
+// so writer and oracle parse the same grammar; the oracle's reconstruction then has to
+// match the encoder's (golden or GPU) bit for bit.  The symbol contexts follow the AV1
+// specification's derivations (partition, skip, is_inter, y/uv modes, single_ref_p*,
+// new/zero/ref mv + drl from the spatial MV stack of 7.10.2, mv joints/classes, all_zero,
+// eob_pt / eob_extra, coeff_base(_eob) / coeff_br with the 2-D context offsets, dc_sign,
+// Golomb remainders).  SUBSTITUTE: every CDF starts uniform (the specification's default
+// CDF tables are not available offline) and adapts with the AV1 counter-based rate.
+//
+// Reference parity: thinvids rejects AV1 sources (/root/reference/worker/tasks.py:929-939)
+// and encodes H.264 (:1532-1586); this is the north-star AV1 encoder of BASELINE.json.
+#include "tv/av1_codec.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "tv/av1.h"
+#include "tv/av1_defs.h"
+#include "tv/av1_txfm.h"
+#include "tv/bitstream.h"
+
+namespace tv {
+namespace av1 {
+
+void txfm2d_ref(const int16_t* in, int16_t* out, int nblk, int log2N, int tcol, int trow, bool inverse);
+
+SeqGeo make_seq_geo(int dw, int dh) {
+  if (dw < 16 || dh < 16 || dw > 8192 || dh > 8192 || (dw & 1) || (dh & 1))
+    throw std::runtime_error("av1: unsupported frame size");
+  SeqGeo g;
+  g.dw = dw;
+  g.dh = dh;
+  g.W = (dw + 15) & ~15;
+  g.H = (dh + 15) & ~15;
+  g.bw = g.W / 16;
+  g.bh = g.H / 16;
+  g.sbw = (g.W + 63) / 64;
+  g.sbh = (g.H + 63) / 64;
+  return g;
+}
+
+FrameDecisions FrameData::view() const {
+  FrameDecisions d;
+  d.fp = fp;
+  d.mode = mode.data();
+  d.mv = mv.data();
+  d.ly = ly.data();
+  d.lu = lu.data();
+  d.lv = lv.data();
+  d.cdef_idx = cdef_idx.data();
+  d.packed = false;
+  return d;
+}
+
+namespace {
+
+// ------------------------------------------------------------------ scans / tables ------
+struct Scans {
+  int16_t s8[64], s16[256];
+};
+void zigzag(int N, int16_t* out) {
+  int k = 0;
+  for (int s = 0; s <= 2 * N - 2; ++s) {
+    const int lo = std::max(0, s - N + 1), hi = std::min(s, N - 1);
+    if (s & 1)
+      for (int r = lo; r <= hi; ++r) out[k++] = (int16_t)(r * N + (s - r));
+    else
+      for (int r = hi; r >= lo; --r) out[k++] = (int16_t)(r * N + (s - r));
+  }
+}
+const Scans& scans() {
+  static const Scans s = [] {
+    Scans t;
+    zigzag(8, t.s8);
+    zigzag(16, t.s16);
+    return t;
+  }();
+  return s;
+}
+constexpr int kCoeffBaseOffset[5][5] = {
+    {0, 1, 6, 6, 21}, {1, 6, 6, 21, 21}, {6, 6, 21, 21, 21}, {6, 21, 21, 21, 21}, {21, 21, 21, 21, 21}};
+constexpr int kIntraModeCtx[13] = {0, 1, 2, 3, 4, 4, 4, 4, 3, 0, 1, 2, 0};
+inline bool directional(int m) { return m >= V_PRED && m <= 8; }
+
+// ------------------------------------------------------------------------ CDFs ----------
+typedef uint16_t C17[17];  // up to 16 symbols + adaptation counter
+struct Cdfs {
+  C17 partition[4][4];          // [bsl - 1][ctx]: 8x8 (4 syms), 16 / 32 / 64 (10 syms)
+  C17 kf_y[5][5], y_mode[4], uv[2][13], angle[8];
+  C17 skip[3], is_inter[4], single_ref[3][6];
+  C17 new_mv[6], zero_mv[2], ref_mv[6], drl[3];
+  C17 mv_joint, mv_sign[2], mv_class[2], class0_bit[2], class0_fr[2][2], mv_fr[2], mv_bits[2][10];
+  C17 intra_tx[4][13], inter_tx[4];
+  C17 txb_skip[5][13], eob_pt[7][2][2], eob_extra[5][2][9], base_eob[5][2][4], base[5][2][42], br[4][2][21];
+  C17 dc_sign[2][3];
+};
+template <size_t K> void init_all(C17 (&a)[K], int n) {
+  for (auto& c : a) cdf_init_uniform(c, n);
+}
+template <size_t K, size_t L> void init_all(C17 (&a)[K][L], int n) {
+  for (auto& r : a) init_all(r, n);
+}
+template <size_t K, size_t L, size_t M> void init_all(C17 (&a)[K][L][M], int n) {
+  for (auto& r : a) init_all(r, n);
+}
+void init_cdfs(Cdfs& c) {
+  cdf_init_uniform(c.partition[0][0], 4);
+  for (int i = 1; i < 4; ++i) cdf_init_uniform(c.partition[0][i], 4);
+  for (int b = 1; b < 4; ++b) init_all(c.partition[b], 10);
+  init_all(c.kf_y, 13);
+  init_all(c.y_mode, 13);
+  init_all(c.uv[0], 13);
+  init_all(c.uv[1], 14);
+  init_all(c.angle, 7);
+  init_all(c.skip, 2);
+  init_all(c.is_inter, 2);
+  init_all(c.single_ref, 2);
+  init_all(c.new_mv, 2);
+  init_all(c.zero_mv, 2);
+  init_all(c.ref_mv, 2);
+  init_all(c.drl, 2);
+  cdf_init_uniform(c.mv_joint, 4);
+  init_all(c.mv_sign, 2);
+  init_all(c.mv_class, 11);
+  init_all(c.class0_bit, 2);
+  init_all(c.class0_fr, 4);
+  init_all(c.mv_fr, 4);
+  init_all(c.mv_bits, 2);
+  init_all(c.intra_tx, 5);
+  init_all(c.inter_tx, 2);
+  init_all(c.txb_skip, 2);
+  for (int s = 0; s < 7; ++s) init_all(c.eob_pt[s], s + 5);
+  init_all(c.eob_extra, 2);
+  init_all(c.base_eob, 3);
+  init_all(c.base, 4);
+  init_all(c.br, 4);
+  init_all(c.dc_sign, 2);
+}
+// P(symbol s) of an inverse CDF (15-bit)
+inline int sym_prob(const uint16_t* icdf, int s) { return (s ? icdf[s - 1] : 32768) - icdf[s]; }
+
+// ------------------------------------------------------------------ symbol I/O ----------
+struct SymW {
+  static constexpr bool kW = true;
+  RangeEncoder rc;
+  void sym(int& v, uint16_t* c, int n) { rc.encode(v, c, n); }
+  void boolp(int& v, int p0) { rc.encode_bool(v, p0); }
+  void lit(int& v, int bits) { rc.encode_literal((uint32_t)v, bits); }
+};
+struct SymR {
+  static constexpr bool kW = false;
+  RangeDecoder rd;
+  SymR(const uint8_t* p, size_t n) : rd(p, n) {}
+  void sym(int& v, uint16_t* c, int n) { v = rd.decode(c, n); }
+  void boolp(int& v, int p0) { v = rd.decode_bool(p0); }
+  void lit(int& v, int bits) { v = (int)rd.decode_literal(bits); }
+};
+
+struct MvStack {
+  int n = 0;
+  int mv[8][2] = {};
+  int w[8] = {};
+  int newctx = 0, refctx = 0, zeroctx = 0;
+};
+
+// ------------------------------------------------------------------ tile syntax ---------
+// Block-level state of one frame (one tile).  For the writer `mode`, `mv`, levels and
+// cdef_idx are inputs; for the reader they are outputs.
+template <class IO>
+struct Tile {
+  IO& io;
+  const SeqGeo& g;
+  FrameParams& fp;
+  int MiRows, MiCols;
+  Cdfs cdf;
+  std::vector<uint32_t>& mode;
+  std::vector<uint32_t>& mv;
+  std::vector<int8_t>& cdef_idx;
+  std::vector<uint8_t> ymode, coded;      // inter mode (NEARESTMV..NEWMV) or intra y mode
+  std::vector<int8_t> cdef_seen;
+  std::vector<uint8_t> aLvl[3], aDc[3], lLvl[3], lDc[3];
+  // level access: writer reads, reader writes (full layout [nblk][N*N])
+  std::function<const int16_t*(int, int)> lev_in;
+  int16_t* lev_out[3] = {nullptr, nullptr, nullptr};
+
+  Tile(IO& io_, const SeqGeo& g_, FrameParams& fp_, std::vector<uint32_t>& mode_, std::vector<uint32_t>& mv_,
+       std::vector<int8_t>& cdef_)
+      : io(io_), g(g_), fp(fp_), MiRows(g_.H / 4), MiCols(g_.W / 4), mode(mode_), mv(mv_), cdef_idx(cdef_) {
+    init_cdfs(cdf);
+    ymode.assign(g.nblk(), 0);
+    coded.assign(g.nblk(), 0);
+    cdef_seen.assign(g.nsb(), -1);
+    for (int p = 0; p < 3; ++p) {
+      const int ss = p ? 1 : 0;
+      aLvl[p].assign(MiCols >> ss, 0);
+      aDc[p].assign(MiCols >> ss, 0);
+      lLvl[p].assign(MiRows >> ss, 0);
+      lDc[p].assign(MiRows >> ss, 0);
+    }
+  }
+
+  int blk(int mir, int mic) const { return (mir >> 2) * g.bw + (mic >> 2); }
+  bool inside(int r, int c) const { return r >= 0 && c >= 0 && r < MiRows && c < MiCols; }
+
+  // ---- coefficients (5.11.39) ----
+  int base_ctx(const int* q, int pos, int lg) const {
+    const int N = 1 << lg, row = pos >> lg, col = pos & (N - 1);
+    if (!row && !col) return 0;
+    constexpr int off[5][2] = {{0, 1}, {1, 0}, {1, 1}, {0, 2}, {2, 0}};
+    int mag = 0;
+    for (auto& o : off) {
+      const int rr = row + o[0], cc = col + o[1];
+      if (rr < N && cc < N) mag += std::min(q[(rr << lg) + cc], 3);
+    }
+    return std::min((mag + 1) >> 1, 4) + kCoeffBaseOffset[std::min(row, 4)][std::min(col, 4)];
+  }
+  int br_ctx(const int* q, int pos, int lg) const {
+    const int N = 1 << lg, row = pos >> lg, col = pos & (N - 1);
+    constexpr int off[3][2] = {{0, 1}, {1, 0}, {1, 1}};
+    int mag = 0;
+    for (auto& o : off) {
+      const int rr = row + o[0], cc = col + o[1];
+      if (rr < N && cc < N) mag += std::min(q[(rr << lg) + cc], 15);
+    }
+    mag = std::min((mag + 1) >> 1, 6);
+    if (!pos) return mag;
+    return (row < 2 && col < 2) ? mag + 7 : mag + 14;
+  }
+
+  // one transform block; L = raster levels (writer: input, reader: output)
+  void coeffs(int plane, int lg, int x4, int y4, int16_t* L, bool is_inter, int intra_dir) {
+    const int N = 1 << lg, area = N * N, w4 = N >> 2, ptype = plane > 0, txc = lg - 2;
+    const int16_t* scan = lg == 4 ? scans().s16 : scans().s8;
+    auto& AL = aLvl[plane];
+    auto& AD = aDc[plane];
+    auto& LL = lLvl[plane];
+    auto& LD = lDc[plane];
+    int ctx = 0;
+    if (plane) {
+      int above = 0, left = 0;
+      for (int i = 0; i < w4; ++i) {
+        if (x4 + i < (int)AL.size()) above |= AL[x4 + i] | AD[x4 + i];
+        if (y4 + i < (int)LL.size()) left |= LL[y4 + i] | LD[y4 + i];
+      }
+      ctx = 7 + (above != 0) + (left != 0);
+    }
+    int eob = 0;
+    if (IO::kW)
+      for (int c = area - 1; c >= 0; --c)
+        if (L[scan[c]]) {
+          eob = c + 1;
+          break;
+        }
+    int all_zero = eob == 0;
+    io.sym(all_zero, cdf.txb_skip[txc][ctx], 2);
+    auto set_ctx = [&](int lvl, int dc) {
+      for (int i = 0; i < w4; ++i) {
+        if (x4 + i < (int)AL.size()) AL[x4 + i] = (uint8_t)lvl, AD[x4 + i] = (uint8_t)dc;
+        if (y4 + i < (int)LL.size()) LL[y4 + i] = (uint8_t)lvl, LD[y4 + i] = (uint8_t)dc;
+      }
+    };
+    if (all_zero) {
+      if (!IO::kW) std::memset(L, 0, sizeof(int16_t) * area);
+      set_ctx(0, 0);
+      return;
+    }
+    if (plane == 0) {  // transform_type: DCT_DCT is symbol 1 of both reduced sets
+      int s = 1;
+      if (is_inter) io.sym(s, cdf.inter_tx[txc], 2);
+      else io.sym(s, cdf.intra_tx[txc][intra_dir], 5);
+      if (s != 1) throw std::runtime_error("av1 oracle: transform type outside the encoder subset");
+    }
+    const int ems = 2 * lg - 4;  // eobMultisize: 8x8 -> 2 (eob_pt_64), 16x16 -> 4 (eob_pt_256)
+    int eobPt = 0;
+    if (IO::kW) eobPt = eob <= 2 ? eob : floor_log2((unsigned)(eob - 1)) + 2;
+    int s = eobPt - 1;
+    io.sym(s, cdf.eob_pt[ems][ptype][0], ems + 5);
+    eobPt = s + 1;
+    const int rem = IO::kW && eobPt >= 3 ? eob - ((1 << (eobPt - 2)) + 1) : 0;
+    int e = eobPt < 2 ? eobPt : (1 << (eobPt - 2)) + 1;
+    if (eobPt - 3 >= 0) {
+      int bit = (rem >> (eobPt - 3)) & 1;
+      io.sym(bit, cdf.eob_extra[txc][ptype][eobPt - 3], 2);
+      if (bit) e += 1 << (eobPt - 3);
+      for (int i = 1; i < std::max(1, eobPt - 2); ++i) {
+        const int sh = std::max(1, eobPt - 2) - 1 - i;
+        bit = (rem >> sh) & 1;
+        io.lit(bit, 1);
+        if (bit) e += 1 << sh;
+      }
+    }
+    if (IO::kW && e != eob) throw std::runtime_error("av1 writer: eob coding mismatch");
+    eob = e;
+    if (eob > area) throw std::runtime_error("av1 oracle: eob out of range");
+    int q[256];
+    std::memset(q, 0, sizeof(int) * area);
+    for (int c = eob - 1; c >= 0; --c) {
+      const int pos = scan[c];
+      const int a = IO::kW ? std::abs((int)L[pos]) : 0;
+      int level;
+      if (c == eob - 1) {
+        const int bctx = c == 0 ? 0 : (c <= area / 8 ? 1 : (c <= area / 4 ? 2 : 3));
+        int v = std::min(a, 3) - 1;
+        io.sym(v, cdf.base_eob[txc][ptype][bctx], 3);
+        level = v + 1;
+      } else {
+        int v = std::min(a, 3);
+        io.sym(v, cdf.base[txc][ptype][base_ctx(q, pos, lg)], 4);
+        level = v;
+      }
+      if (level > 2) {
+        for (int k = 0; k < 4; ++k) {
+          int v = IO::kW ? std::min(a - level, 3) : 0;
+          io.sym(v, cdf.br[std::min(txc, 3)][ptype][br_ctx(q, pos, lg)], 4);
+          level += v;
+          if (v < 3) break;
+        }
+      }
+      q[pos] = level;
+    }
+    // dc_sign context from the neighbours' dc categories
+    int dcs = 0;
+    for (int i = 0; i < w4; ++i) {
+      if (x4 + i < (int)AD.size()) dcs += AD[x4 + i] == 1 ? -1 : (AD[x4 + i] == 2 ? 1 : 0);
+      if (y4 + i < (int)LD.size()) dcs += LD[y4 + i] == 1 ? -1 : (LD[y4 + i] == 2 ? 1 : 0);
+    }
+    const int dctx = dcs < 0 ? 1 : (dcs > 0 ? 2 : 0);
+    int cul = 0, dcCat = 0;
+    for (int c = 0; c < eob; ++c) {
+      const int pos = scan[c];
+      int sign = 0;
+      if (q[pos]) {
+        sign = IO::kW ? (L[pos] < 0) : 0;
+        if (c == 0) io.sym(sign, cdf.dc_sign[ptype][dctx], 2);
+        else io.lit(sign, 1);
+      }
+      if (q[pos] > 14) {
+        const int x = IO::kW ? std::abs((int)L[pos]) - 14 : 0;
+        int length = 0;
+        if (IO::kW) {
+          length = floor_log2((unsigned)x) + 1;
+          for (int i = 0; i < length; ++i) {
+            int b = i == length - 1;
+            io.lit(b, 1);
+          }
+          for (int i = length - 2; i >= 0; --i) {
+            int b = (x >> i) & 1;
+            io.lit(b, 1);
+          }
+        } else {
+          int b = 0;
+          do {
+            ++length;
+            io.lit(b, 1);
+            if (length > 20) throw std::runtime_error("av1 oracle: bad golomb length");
+          } while (!b);
+          int xx = 1;
+          for (int i = length - 2; i >= 0; --i) {
+            io.lit(b, 1);
+            xx = (xx << 1) | b;
+          }
+          q[pos] = xx + 14;
+        }
+      }
+      if (pos == 0 && q[pos] > 0) dcCat = sign ? 1 : 2;
+      q[pos] &= 0xFFFFF;
+      cul += q[pos];
+      if (!IO::kW) L[pos] = (int16_t)(sign ? -q[pos] : q[pos]);
+    }
+    if (!IO::kW)
+      for (int i = 0; i < area; ++i)
+        if (!q[i]) L[i] = 0;
+    set_ctx(std::min(63, cul), dcCat);
+  }
+
+  // ---- MV stack (7.10.2, single reference, no temporal candidates) ----
+  MvStack S;
+  int found = 0, newcount = 0;
+  void search_stack(int b, int weight) {
+    int m[2] = {mv_row(mv[b]), mv_col(mv[b])};
+    for (int& v : m)
+      if (v & 1) v += v > 0 ? -1 : 1;  // lower_mv_precision (allow_high_precision_mv = 0)
+    if (ymode[b] == NEWMV) ++newcount;
+    found = 1;
+    for (int i = 0; i < S.n; ++i)
+      if (S.mv[i][0] == m[0] && S.mv[i][1] == m[1]) {
+        S.w[i] += weight;
+        return;
+      }
+    if (S.n < 8) {
+      S.mv[S.n][0] = m[0];
+      S.mv[S.n][1] = m[1];
+      S.w[S.n] = weight;
+      ++S.n;
+    }
+  }
+  void add_cand(int r, int c, int weight) {
+    const int b = blk(r, c);
+    if (!mode_inter(mode[b])) return;
+    search_stack(b, weight);
+  }
+  void scan_row(int mir, int mic, int dr) {
+    const int bw4 = 4, end4 = std::min(std::min(bw4, MiCols - mic), 16);
+    int dc = 0;
+    if (std::abs(dr) > 1) {
+      dr += mir & 1;
+      dc = 1 - (mic & 1);
+    }
+    for (int i = 0; i < end4;) {
+      const int r = mir + dr, c = mic + dc + i;
+      if (!inside(r, c)) break;
+      int len = std::min(bw4, 4);
+      if (std::abs(dr) > 1) len = std::max(2, len);
+      add_cand(r, c, 2 * len);
+      i += len;
+    }
+  }
+  void scan_col(int mir, int mic, int dc) {
+    const int bh4 = 4, end4 = std::min(std::min(bh4, MiRows - mir), 16);
+    int dr = 0;
+    if (std::abs(dc) > 1) {
+      dr = 1 - (mir & 1);
+      dc += mic & 1;
+    }
+    for (int i = 0; i < end4;) {
+      const int r = mir + dr + i, c = mic + dc;
+      if (!inside(r, c)) break;
+      int len = std::min(bh4, 4);
+      if (std::abs(dc) > 1) len = std::max(2, len);
+      add_cand(r, c, 2 * len);
+      i += len;
+    }
+  }
+  void scan_point(int mir, int mic, int dr, int dc) {
+    const int r = mir + dr, c = mic + dc;
+    if (inside(r, c) && coded[blk(r, c)]) add_cand(r, c, 4);
+  }
+  void sort_stack(int start, int end) {
+    while (end > start) {
+      int ne = start;
+      for (int i = start + 1; i < end; ++i)
+        if (S.w[i - 1] < S.w[i]) {
+          std::swap(S.w[i - 1], S.w[i]);
+          std::swap(S.mv[i - 1][0], S.mv[i][0]);
+          std::swap(S.mv[i - 1][1], S.mv[i][1]);
+          ne = i;
+        }
+      end = ne;
+    }
+  }
+  void find_mv_stack(int mir, int mic) {
+    S = MvStack();
+    newcount = 0;
+    found = 0;
+    scan_row(mir, mic, -1);
+    int fa = found;
+    found = 0;
+    scan_col(mir, mic, -1);
+    int fl = found;
+    found = 0;
+    scan_point(mir, mic, -1, 4);
+    if (found) fa = 1;
+    const int close = fa + fl, nearest = S.n, nnew = newcount;
+    for (int i = 0; i < nearest; ++i) S.w[i] += 640;
+    found = 0;
+    scan_point(mir, mic, -1, -1);
+    if (found) fa = 1;
+    found = 0;
+    scan_row(mir, mic, -3);
+    if (found) fa = 1;
+    found = 0;
+    scan_col(mir, mic, -3);
+    if (found) fl = 1;
+    found = 0;
+    scan_row(mir, mic, -5);
+    if (found) fa = 1;
+    found = 0;
+    scan_col(mir, mic, -5);
+    if (found) fl = 1;
+    const int total = fa + fl;
+    sort_stack(0, nearest);
+    sort_stack(nearest, S.n);
+    if (S.n < 2) {  // extra_search
+      const int num4 = std::min(std::min(4, MiCols - mic), std::min(4, MiRows - mir));
+      for (int pass = 0; pass < 2 && S.n < 2; ++pass) {
+        for (int idx = 0; idx < num4 && S.n < 2; idx += 4) {
+          const int r = pass ? mir + idx : mir - 1, c = pass ? mic - 1 : mic + idx;
+          if (!inside(r, c)) break;
+          const int b = blk(r, c);
+          if (!mode_inter(mode[b])) continue;
+          const int m0 = mv_row(mv[b]), m1 = mv_col(mv[b]);
+          int i = 0;
+          for (; i < S.n; ++i)
+            if (S.mv[i][0] == m0 && S.mv[i][1] == m1) break;
+          if (i == S.n) {
+            S.mv[i][0] = m0;
+            S.mv[i][1] = m1;
+            S.w[i] = 2;
+            ++S.n;
+          }
+        }
+      }
+      for (int i = S.n; i < 2; ++i) S.mv[i][0] = S.mv[i][1] = 0;  // GlobalMvs (identity)
+    }
+    for (int i = 0; i < S.n; ++i) {
+      const int top = -(mir * 4 * 8), bottom = (MiRows - 4 - mir) * 4 * 8, border = 128 + 4 * 4 * 8;
+      const int left = -(mic * 4 * 8), right = (MiCols - 4 - mic) * 4 * 8;
+      S.mv[i][0] = clip3(top - border, bottom + border, S.mv[i][0]);
+      S.mv[i][1] = clip3(left - border, right + border, S.mv[i][1]);
+    }
+    if (close == 0) {
+      S.newctx = std::min(total, 1);
+      S.refctx = total;
+    } else if (close == 1) {
+      S.newctx = 3 - std::min(nnew, 1);
+      S.refctx = 2 + total;
+    } else {
+      S.newctx = 5 - std::min(nnew, 1);
+      S.refctx = 5;
+    }
+    S.zeroctx = 0;
+  }
+  int drl_ctx(int idx) const {
+    const int a = idx < 8 ? S.w[idx] : 0, b = idx + 1 < 8 ? S.w[idx + 1] : 0;
+    if (a >= 640 && b >= 640) return 0;
+    if (a >= 640) return 1;
+    return 2;
+  }
+
+  void mv_component(int comp, int& v) {
+    int sign = v < 0, z = std::abs(v) - 1;
+    int cls = IO::kW ? (z < 16 ? 0 : floor_log2((unsigned)z) - 3) : 0;
+    io.sym(sign, cdf.mv_sign[comp], 2);
+    io.sym(cls, cdf.mv_class[comp], 11);
+    int d, fr;
+    if (cls == 0) {
+      d = (z >> 3) & 1;
+      fr = (z >> 1) & 3;
+      io.sym(d, cdf.class0_bit[comp], 2);
+      io.sym(fr, cdf.class0_fr[comp][d], 4);
+      z = (d << 3) | (fr << 1) | 1;
+    } else {
+      const int off = IO::kW ? z - (1 << (cls + 3)) : 0;
+      d = 0;
+      for (int b = 0; b < cls; ++b) {
+        int bit = (off >> (3 + b)) & 1;
+        io.sym(bit, cdf.mv_bits[comp][b], 2);
+        d |= bit << b;
+      }
+      fr = (off >> 1) & 3;
+      io.sym(fr, cdf.mv_fr[comp], 4);
+      z = (1 << (cls + 3)) + ((d << 3) | (fr << 1) | 1);
+    }
+    const int mag = z + 1;
+    if (IO::kW && mag != std::abs(v)) throw std::runtime_error("av1 writer: mv not representable (odd?)");
+    v = sign ? -mag : mag;
+  }
+  void mv_diff(int* diff) {
+    int j = (diff[0] != 0) * 2 + (diff[1] != 0);
+    io.sym(j, cdf.mv_joint, 4);
+    if (!IO::kW) diff[0] = diff[1] = 0;
+    if (j == 2 || j == 3) mv_component(0, diff[0]);
+    if (j == 1 || j == 3) mv_component(1, diff[1]);
+  }
+
+  // ---- block (decode_block for a 16x16 block) ----
+  void intra_modes(int b, bool kf, bool availU, bool availL) {
+    int y = mode_y(mode[b]), uvm = mode_uv(mode[b]);
+    if (kf) {
+      const int am = availU ? ymode[b - g.bw] : DC_PRED, lm = availL ? ymode[b - 1] : DC_PRED;
+      io.sym(y, cdf.kf_y[kIntraModeCtx[am]][kIntraModeCtx[lm]], 13);
+    } else {
+      io.sym(y, cdf.y_mode[2], 13);  // Size_Group[BLOCK_16X16] = 2
+    }
+    if (directional(y)) {
+      int ad = 3;
+      io.sym(ad, cdf.angle[y - V_PRED], 7);
+      if (ad != 3) throw std::runtime_error("av1 oracle: angle delta outside the encoder subset");
+    }
+    io.sym(uvm, cdf.uv[1][y], 14);  // CfL allowed for 16x16
+    if (uvm == 13) throw std::runtime_error("av1 oracle: CfL outside the encoder subset");
+    if (directional(uvm)) {
+      int ad = 3;
+      io.sym(ad, cdf.angle[uvm - V_PRED], 7);
+      if (ad != 3) throw std::runtime_error("av1 oracle: angle delta outside the encoder subset");
+    }
+    ymode[b] = (uint8_t)y;
+    if (!IO::kW) mode[b] = pack_mode(0, y, uvm, mode_skip(mode[b]), mode_nz(mode[b]));
+  }
+
+  void inter_modes(int b, int mir, int mic, bool availU, bool availL) {
+    int cnt = 0;  // neighbours referencing LAST
+    if (availU && mode_inter(mode[b - g.bw])) ++cnt;
+    if (availL && mode_inter(mode[b - 1])) ++cnt;
+    auto rc = [](int c0, int c1) { return c0 == c1 ? 1 : (c0 < c1 ? 0 : 2); };
+    int v = 0;
+    io.sym(v, cdf.single_ref[rc(cnt, 0)][0], 2);  // p1: LAST..GOLDEN vs BWD..ALT
+    if (v) throw std::runtime_error("av1 oracle: reference outside the encoder subset");
+    io.sym(v, cdf.single_ref[rc(cnt, 0)][2], 2);  // p3: LAST/LAST2 vs LAST3/GOLDEN
+    if (v) throw std::runtime_error("av1 oracle: reference outside the encoder subset");
+    io.sym(v, cdf.single_ref[rc(cnt, 0)][3], 2);  // p4: LAST vs LAST2
+    if (v) throw std::runtime_error("av1 oracle: reference outside the encoder subset");
+    find_mv_stack(mir, mic);
+    int m[2] = {mv_row(mv[b]), mv_col(mv[b])};
+    int ym = NEWMV, idx = 0;
+    if (IO::kW) {
+      auto eq = [&](int k) { return S.mv[k][0] == m[0] && S.mv[k][1] == m[1]; };
+      if (eq(0)) ym = NEARESTMV;
+      else if (!m[0] && !m[1]) ym = GLOBALMV;
+      else {
+        for (int k = 1; k <= 3; ++k)
+          if ((k == 1 || S.n > k) && eq(k)) {
+            ym = NEARMV;
+            idx = k;
+            break;
+          }
+        if (ym == NEWMV && S.n > 1) {  // predictor with the cheapest difference
+          int best = 1 << 30;
+          for (int k = 0; k < 3 && (k == 0 || S.n > k); ++k) {
+            const int bits = mv_comp_bits(m[0] - S.mv[k][0]) + mv_comp_bits(m[1] - S.mv[k][1]);
+            if (bits < best) best = bits, idx = k;
+          }
+        }
+      }
+    }
+    int nm = ym != NEWMV;
+    io.sym(nm, cdf.new_mv[S.newctx], 2);
+    if (!nm) ym = NEWMV;
+    else {
+      int zm = ym != GLOBALMV;
+      io.sym(zm, cdf.zero_mv[S.zeroctx], 2);
+      if (!zm) ym = GLOBALMV;
+      else {
+        int rm = ym == NEARMV;
+        io.sym(rm, cdf.ref_mv[S.refctx], 2);
+        ym = rm ? NEARMV : NEARESTMV;
+      }
+    }
+    if (ym == NEWMV) {
+      int ri = 0;
+      for (int k = 0; k < 2; ++k)
+        if (S.n > k + 1) {
+          int bit = idx != k;
+          io.sym(bit, cdf.drl[drl_ctx(k)], 2);
+          if (!bit) {
+            ri = k;
+            break;
+          }
+          ri = k + 1;
+        }
+      idx = ri;
+    } else if (ym == NEARMV) {
+      int ri = 1;
+      for (int k = 1; k < 3; ++k)
+        if (S.n > k + 1) {
+          int bit = idx != k;
+          io.sym(bit, cdf.drl[drl_ctx(k)], 2);
+          if (!bit) {
+            ri = k;
+            break;
+          }
+          ri = k + 1;
+        }
+      idx = ri;
+    }
+    if (ym == GLOBALMV) m[0] = m[1] = 0;
+    else if (ym == NEARESTMV) m[0] = S.mv[0][0], m[1] = S.mv[0][1];
+    else if (ym == NEARMV) {
+      if (idx > 7) throw std::runtime_error("av1 oracle: bad ref mv idx");
+      m[0] = S.mv[idx][0], m[1] = S.mv[idx][1];
+    } else {
+      const int pos = S.n <= 1 ? 0 : idx;
+      int diff[2] = {m[0] - S.mv[pos][0], m[1] - S.mv[pos][1]};
+      mv_diff(diff);
+      m[0] = S.mv[pos][0] + diff[0];
+      m[1] = S.mv[pos][1] + diff[1];
+    }
+    if (IO::kW && (m[0] != mv_row(mv[b]) || m[1] != mv_col(mv[b])))
+      throw std::runtime_error("av1 writer: mv mode reconstruction mismatch");
+    ymode[b] = (uint8_t)ym;
+    if (!IO::kW) {
+      mv[b] = pack_mv(m[0], m[1]);
+      mode[b] = pack_mode(1, 0, 0, mode_skip(mode[b]), mode_nz(mode[b]));
+    }
+  }
+
+  void block(int mir, int mic) {
+    const int b = blk(mir, mic);
+    const bool availU = mir > 0, availL = mic > 0, kf = fp.key != 0;
+    int skip = mode_skip(mode[b]);
+    const int sctx = (availU ? mode_skip(mode[b - g.bw]) : 0) + (availL ? mode_skip(mode[b - 1]) : 0);
+    io.sym(skip, cdf.skip[sctx], 2);
+    if (!IO::kW) mode[b] = pack_mode(0, 0, 0, skip, 0);
+    if (!skip) {  // read_cdef
+      const int sb = (mir >> 4) * g.sbw + (mic >> 4);
+      if (cdef_seen[sb] == -1) {
+        int v = IO::kW ? cdef_idx[sb] : 0;
+        if (IO::kW && (v < 0 || v >= (1 << fp.cdef_bits))) throw std::runtime_error("av1 writer: cdef_idx missing");
+        io.lit(v, fp.cdef_bits);
+        cdef_seen[sb] = (int8_t)v;
+        if (!IO::kW) cdef_idx[sb] = (int8_t)v;
+      }
+    }
+    int inter = 0;
+    if (!kf) {
+      inter = mode_inter(mode[b]);
+      const int aI = availU ? !mode_inter(mode[b - g.bw]) : 0, lI = availL ? !mode_inter(mode[b - 1]) : 0;
+      int ictx = 0;
+      if (availU && availL) ictx = (lI && aI) ? 3 : (lI || aI);
+      else if (availU || availL) ictx = 2 * (availU ? aI : lI);
+      io.sym(inter, cdf.is_inter[ictx], 2);
+    }
+    if (inter) inter_modes(b, mir, mic, availU, availL);
+    else intra_modes(b, kf, availU, availL);
+    // residual
+    int nz = 0;
+    const int x4 = mic, y4 = mir;
+    if (!skip) {
+      for (int p = 0; p < 3; ++p) {
+        const int lg = p ? 3 : 4;
+        int16_t tmp[256];
+        int16_t* L = tmp;
+        if (IO::kW) {
+          const int16_t* src = lev_in(p, b);
+          if (src) std::memcpy(tmp, src, sizeof(int16_t) << (2 * lg));
+          else std::memset(tmp, 0, sizeof(int16_t) << (2 * lg));
+        } else {
+          L = lev_out[p] + ((size_t)b << (2 * lg));
+        }
+        coeffs(p, lg, p ? x4 >> 1 : x4, p ? y4 >> 1 : y4, L, inter != 0, ymode[b]);
+        for (int i = 0; i < (1 << (2 * lg)); ++i)
+          if (L[i]) {
+            nz |= 1 << p;
+            break;
+          }
+      }
+      if (IO::kW && nz != mode_nz(mode[b])) throw std::runtime_error("av1 writer: nonzero mask mismatch");
+      if (nz == 0) throw std::runtime_error("av1: non-skip block without coefficients");
+    } else {
+      for (int p = 0; p < 3; ++p) {  // reset_block_context
+        const int ss = p ? 1 : 0, w4 = 4 >> ss;
+        for (int i = 0; i < w4; ++i) {
+          aLvl[p][(x4 >> ss) + i] = aDc[p][(x4 >> ss) + i] = 0;
+          lLvl[p][(y4 >> ss) + i] = lDc[p][(y4 >> ss) + i] = 0;
+        }
+        if (!IO::kW) std::memset(lev_out[p] + ((size_t)b << (p ? 6 : 8)), 0, sizeof(int16_t) << (p ? 6 : 8));
+      }
+    }
+    if (!IO::kW) mode[b] = (mode[b] & ~(7u << 10)) | ((uint32_t)nz << 10);
+    coded[b] = 1;
+  }
+
+  void partition(int mir, int mic, int bsl) {
+    if (mir >= MiRows || mic >= MiCols) return;
+    const bool availU = mir > 0, availL = mic > 0;
+    const int half = (1 << bsl) >> 1;
+    const bool hasRows = mir + half < MiRows, hasCols = mic + half < MiCols;
+    int part = bsl > 2 ? 3 : 0;  // PARTITION_SPLIT down to 16x16, then PARTITION_NONE
+    const int above = availU && 2 < bsl, left = availL && 2 < bsl;
+    uint16_t* c = cdf.partition[bsl - 1][left * 2 + above];
+    if (hasRows && hasCols) {
+      io.sym(part, c, 10);
+    } else if (hasCols) {  // split_or_horz
+      const int ps = sym_prob(c, 2) + sym_prob(c, 3) + sym_prob(c, 4) + sym_prob(c, 6) + sym_prob(c, 7) +
+                     sym_prob(c, 9);
+      int bit = part == 3;
+      io.boolp(bit, 32768 - ps);
+      part = bit ? 3 : 1;
+    } else if (hasRows) {  // split_or_vert
+      const int ps = sym_prob(c, 1) + sym_prob(c, 3) + sym_prob(c, 4) + sym_prob(c, 5) + sym_prob(c, 6) +
+                     sym_prob(c, 8);
+      int bit = part == 3;
+      io.boolp(bit, 32768 - ps);
+      part = bit ? 3 : 2;
+    } else {
+      part = 3;
+    }
+    if (part == 3 && bsl > 2) {
+      partition(mir, mic, bsl - 1);
+      partition(mir, mic + half, bsl - 1);
+      partition(mir + half, mic, bsl - 1);
+      partition(mir + half, mic + half, bsl - 1);
+    } else if (part == 0 && bsl == 2) {
+      block(mir, mic);
+    } else {
+      throw std::runtime_error("av1 oracle: partition outside the encoder subset");
+    }
+  }
+
+  void tile() {
+    for (int sr = 0; sr < g.sbh; ++sr) {
+      for (int p = 0; p < 3; ++p) {  // clear_left_context
+        std::fill(lLvl[p].begin(), lLvl[p].end(), 0);
+        std::fill(lDc[p].begin(), lDc[p].end(), 0);
+      }
+      for (int sc = 0; sc < g.sbw; ++sc) partition(sr * 16, sc * 16, 4);
+    }
+  }
+};
+
+// ------------------------------------------------------------------ headers -------------
+constexpr int OBU_SEQUENCE_HEADER = 1, OBU_TEMPORAL_DELIMITER = 2, OBU_FRAME = 6;
+
+int bits_for(int v) {  // bits to code values 0..v
+  int n = 1;
+  while ((1 << n) <= v) ++n;
+  return n;
+}
+int tile_log2(int blk, int target) {
+  int k = 0;
+  while ((blk << k) < target) ++k;
+  return k;
+}
+
+void write_seq_header(BitWriter& w, const SeqGeo& g) {
+  w.put(0, 3);  // seq_profile (Main)
+  w.put(0, 1);  // still_picture
+  w.put(0, 1);  // reduced_still_picture_header
+  w.put(0, 1);  // timing_info_present_flag
+  w.put(0, 1);  // initial_display_delay_present_flag
+  w.put(0, 5);  // operating_points_cnt_minus_1
+  w.put(0, 12); // operating_point_idc[0]
+  w.put(31, 5); // seq_level_idx[0] (31: unconstrained)
+  w.put(0, 1);  // seq_tier[0]
+  const int wb = bits_for(g.W - 1), hb = bits_for(g.H - 1);
+  w.put(wb - 1, 4);
+  w.put(hb - 1, 4);
+  w.put(g.W - 1, wb);
+  w.put(g.H - 1, hb);
+  w.put(0, 1);  // frame_id_numbers_present_flag
+  w.put(0, 1);  // use_128x128_superblock
+  w.put(0, 1);  // enable_filter_intra
+  w.put(0, 1);  // enable_intra_edge_filter
+  w.put(0, 1);  // enable_interintra_compound
+  w.put(0, 1);  // enable_masked_compound
+  w.put(0, 1);  // enable_warped_motion
+  w.put(0, 1);  // enable_dual_filter
+  w.put(0, 1);  // enable_order_hint
+  w.put(0, 1);  // seq_choose_screen_content_tools
+  w.put(0, 1);  // seq_force_screen_content_tools
+  w.put(0, 1);  // enable_superres
+  w.put(1, 1);  // enable_cdef
+  w.put(0, 1);  // enable_restoration
+  // color_config: 8-bit, not monochrome, no colour description, studio range, 4:2:0
+  w.put(0, 1);  // high_bitdepth
+  w.put(0, 1);  // mono_chrome
+  w.put(0, 1);  // color_description_present_flag
+  w.put(0, 1);  // color_range
+  w.put(0, 2);  // chroma_sample_position
+  w.put(0, 1);  // separate_uv_delta_q
+  w.put(0, 1);  // film_grain_params_present
+  w.trailing_bits();
+}
+
+SeqGeo read_seq_header(BitReader& r) {
+  auto expect = [&](int n, uint32_t v, const char* what) {
+    if (r.u(n) != v) throw std::runtime_error(std::string("av1 oracle: unsupported sequence header ") + what);
+  };
+  expect(3, 0, "profile");
+  expect(1, 0, "still_picture");
+  expect(1, 0, "reduced_still_picture_header");
+  expect(1, 0, "timing_info");
+  expect(1, 0, "initial_display_delay");
+  expect(5, 0, "operating points");
+  r.u(12);
+  const int lvl = (int)r.u(5);
+  if (lvl > 7) r.u(1);
+  const int wb = (int)r.u(4) + 1, hb = (int)r.u(4) + 1;
+  const int W = (int)r.u(wb) + 1, H = (int)r.u(hb) + 1;
+  const char* flags[] = {"frame ids",     "128x128 SB",      "filter intra",   "intra edge filter",
+                         "interintra",    "masked compound", "warped motion",  "dual filter",
+                         "order hint",    "choose screen content", "force screen content", "superres"};
+  for (auto f : flags) expect(1, 0, f);
+  expect(1, 1, "enable_cdef");
+  expect(1, 0, "enable_restoration");
+  expect(1, 0, "high_bitdepth");
+  expect(1, 0, "mono_chrome");
+  expect(1, 0, "color_description");
+  r.u(1);
+  r.u(2);
+  expect(1, 0, "separate_uv_delta_q");
+  expect(1, 0, "film grain");
+  SeqGeo g = make_seq_geo(W, H);  // render size arrives in the frame header
+  if (g.W != W || g.H != H) throw std::runtime_error("av1 oracle: coded size not a multiple of 16");
+  return g;
+}
+
+void write_frame_header(BitWriter& w, const SeqGeo& g, const FrameParams& fp) {
+  w.put(0, 1);  // show_existing_frame
+  w.put(fp.key ? 0 : 1, 2);  // frame_type KEY_FRAME / INTER_FRAME
+  w.put(1, 1);  // show_frame
+  if (!fp.key) w.put(0, 1);  // error_resilient_mode (key + shown: implied 1)
+  w.put(0, 1);  // disable_cdf_update
+  w.put(0, 1);  // frame_size_override_flag
+  if (!fp.key) w.put(7, 3);  // primary_ref_frame = PRIMARY_REF_NONE
+  if (!fp.key) w.put(0x01, 8);  // refresh_frame_flags: slot 0 (key frames refresh all)
+  const bool diff = g.dw != g.W || g.dh != g.H;
+  if (fp.key) {
+    w.put(diff, 1);  // render_and_frame_size_different
+    if (diff) {
+      w.put(g.dw - 1, 16);
+      w.put(g.dh - 1, 16);
+    }
+  } else {
+    for (int i = 0; i < 7; ++i) w.put(0, 3);  // ref_frame_idx: every reference is slot 0
+    w.put(diff, 1);
+    if (diff) {
+      w.put(g.dw - 1, 16);
+      w.put(g.dh - 1, 16);
+    }
+    w.put(0, 1);  // allow_high_precision_mv
+    w.put(0, 1);  // is_filter_switchable
+    w.put(0, 2);  // interpolation_filter EIGHTTAP
+    w.put(0, 1);  // is_motion_mode_switchable
+  }
+  w.put(1, 1);  // disable_frame_end_update_cdf
+  // tile_info: uniform spacing, one tile
+  const int sbc = g.sbw, sbr = g.sbh;
+  w.put(1, 1);
+  const int minc = tile_log2(64, sbc), maxc = tile_log2(1, std::min(sbc, 64));
+  if (minc > 0) throw std::runtime_error("av1: frame too wide for one tile");
+  if (minc < maxc) w.put(0, 1);
+  const int maxr = tile_log2(1, std::min(sbr, 64));
+  const int mint = std::max(minc, tile_log2(2304, sbr * sbc));
+  if (mint > 0) throw std::runtime_error("av1: frame too large for one tile");
+  if (0 < maxr) w.put(0, 1);
+  // quantization_params
+  w.put(fp.qindex, 8);
+  w.put(0, 1);  // DeltaQYDc
+  w.put(0, 1);  // DeltaQUDc
+  w.put(0, 1);  // DeltaQUAc
+  w.put(0, 1);  // using_qmatrix
+  w.put(0, 1);  // segmentation_enabled
+  if (fp.qindex > 0) w.put(0, 1);  // delta_q_present
+  // loop_filter_params
+  w.put(fp.lf[0], 6);
+  w.put(fp.lf[1], 6);
+  if (fp.lf[0] || fp.lf[1]) {
+    w.put(fp.lf[2], 6);
+    w.put(fp.lf[3], 6);
+  }
+  w.put(fp.sharp, 3);
+  w.put(0, 1);  // loop_filter_delta_enabled
+  // cdef_params
+  w.put(fp.cdef_damping - 3, 2);
+  w.put(fp.cdef_bits, 2);
+  for (int i = 0; i < (1 << fp.cdef_bits); ++i) {
+    w.put(fp.cdef_y[i] >> 2, 4);
+    w.put(fp.cdef_y[i] & 3, 2);
+    w.put(fp.cdef_uv[i] >> 2, 4);
+    w.put(fp.cdef_uv[i] & 3, 2);
+  }
+  w.put(0, 1);  // tx_mode_select (TX_MODE_LARGEST)
+  if (!fp.key) w.put(0, 1);  // reference_select
+  w.put(1, 1);  // reduced_tx_set
+  if (!fp.key)
+    for (int i = 0; i < 7; ++i) w.put(0, 1);  // is_global
+}
+
+FrameParams read_frame_header(BitReader& r, SeqGeo& g, bool& have_ref) {
+  auto expect = [&](int n, uint32_t v, const char* what) {
+    if (r.u(n) != v) throw std::runtime_error(std::string("av1 oracle: unsupported frame header ") + what);
+  };
+  FrameParams fp;
+  expect(1, 0, "show_existing_frame");
+  const int ft = (int)r.u(2);
+  if (ft > 1) throw std::runtime_error("av1 oracle: frame type outside the encoder subset");
+  fp.key = ft == 0;
+  expect(1, 1, "show_frame");
+  if (!fp.key) expect(1, 0, "error_resilient_mode");
+  expect(1, 0, "disable_cdf_update");
+  expect(1, 0, "frame_size_override_flag");
+  if (!fp.key) {
+    expect(3, 7, "primary_ref_frame");
+    r.u(8);
+    if (!have_ref) throw std::runtime_error("av1 oracle: inter frame without a reference");
+    for (int i = 0; i < 7; ++i) expect(3, 0, "ref_frame_idx");
+  }
+  if (r.u(1)) {
+    const int dw = (int)r.u(16) + 1, dh = (int)r.u(16) + 1;
+    const int W = g.W, H = g.H;
+    g = make_seq_geo(dw, dh);
+    if (g.W != W || g.H != H) throw std::runtime_error("av1 oracle: render size does not match the coded size");
+  } else {
+    g.dw = g.W;
+    g.dh = g.H;
+  }
+  if (!fp.key) {
+    expect(1, 0, "allow_high_precision_mv");
+    expect(1, 0, "is_filter_switchable");
+    expect(2, 0, "interpolation_filter");
+    expect(1, 0, "is_motion_mode_switchable");
+  }
+  expect(1, 1, "disable_frame_end_update_cdf");
+  expect(1, 1, "uniform_tile_spacing_flag");
+  const int maxc = tile_log2(1, std::min(g.sbw, 64)), maxr = tile_log2(1, std::min(g.sbh, 64));
+  if (0 < maxc) expect(1, 0, "increment_tile_cols_log2");
+  if (0 < maxr) expect(1, 0, "increment_tile_rows_log2");
+  fp.qindex = (int)r.u(8);
+  for (int i = 0; i < 4; ++i) expect(1, 0, "delta q / qmatrix");
+  expect(1, 0, "segmentation_enabled");
+  if (fp.qindex > 0) expect(1, 0, "delta_q_present");
+  fp.lf[0] = (int)r.u(6);
+  fp.lf[1] = (int)r.u(6);
+  if (fp.lf[0] || fp.lf[1]) {
+    fp.lf[2] = (int)r.u(6);
+    fp.lf[3] = (int)r.u(6);
+  }
+  fp.sharp = (int)r.u(3);
+  expect(1, 0, "loop_filter_delta_enabled");
+  fp.cdef_damping = (int)r.u(2) + 3;
+  fp.cdef_bits = (int)r.u(2);
+  for (int i = 0; i < (1 << fp.cdef_bits); ++i) {
+    const int yp = (int)r.u(4), ys = (int)r.u(2), up = (int)r.u(4), us = (int)r.u(2);
+    fp.cdef_y[i] = (uint8_t)(yp * 4 + ys);
+    fp.cdef_uv[i] = (uint8_t)(up * 4 + us);
+  }
+  expect(1, 0, "tx_mode_select");
+  if (!fp.key) expect(1, 0, "reference_select");
+  expect(1, 1, "reduced_tx_set");
+  if (!fp.key)
+    for (int i = 0; i < 7; ++i) expect(1, 0, "is_global");
+  return fp;
+}
+
+void put_leb128(std::vector<uint8_t>& out, size_t v) {
+  do {
+    uint8_t b = v & 0x7f;
+    v >>= 7;
+    if (v) b |= 0x80;
+    out.push_back(b);
+  } while (v);
+}
+void put_obu(std::vector<uint8_t>& out, int type, const std::vector<uint8_t>& payload) {
+  out.push_back((uint8_t)((type << 3) | 2));  // obu_has_size_field
+  put_leb128(out, payload.size());
+  out.insert(out.end(), payload.begin(), payload.end());
+}
+
+}  // namespace
+
+// ================================================================== writer ==============
+std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& d, bool seq_header) {
+  const int nb = g.nblk();
+  FrameParams fp = d.fp;
+  std::vector<uint32_t> mode(d.mode, d.mode + nb), mv(nb, 0);
+  if (d.mv) mv.assign(d.mv, d.mv + nb);
+  std::vector<int8_t> cdef(d.cdef_idx, d.cdef_idx + g.nsb());
+  SymW io;
+  Tile<SymW> t(io, g, fp, mode, mv, cdef);
+  // level access (packed layout: prefix offsets over the nonzero masks)
+  std::vector<int32_t> off[3];
+  const int16_t* base[3] = {d.ly, d.lu, d.lv};
+  if (d.packed)
+    for (int p = 0; p < 3; ++p) {
+      off[p].assign(nb, -1);
+      int k = 0;
+      for (int b = 0; b < nb; ++b)
+        if (mode_nz(mode[b]) >> p & 1) off[p][b] = k++;
+    }
+  t.lev_in = [&](int p, int b) -> const int16_t* {
+    const size_t sz = p ? 64 : 256;
+    if (!d.packed) return base[p] + (size_t)b * sz;
+    return off[p][b] < 0 ? nullptr : base[p] + (size_t)off[p][b] * sz;
+  };
+  t.tile();
+  const std::vector<uint8_t> tile = io.rc.finish();
+  std::vector<uint8_t> out;
+  put_obu(out, OBU_TEMPORAL_DELIMITER, {});
+  if (seq_header) {
+    BitWriter sw;
+    write_seq_header(sw, g);
+    put_obu(out, OBU_SEQUENCE_HEADER, sw.bytes());
+  }
+  BitWriter fw;
+  write_frame_header(fw, g, fp);
+  fw.align_zero();  // byte_alignment (frame_obu); tile_group: one tile, no start/end flags
+  std::vector<uint8_t> payload = fw.bytes();
+  payload.insert(payload.end(), tile.begin(), tile.end());
+  put_obu(out, OBU_FRAME, payload);
+  return out;
+}
+
+// ================================================================== reconstruction ======
+namespace {
+struct PlaneRef {
+  const uint8_t* p;
+  int w, h;
+  int operator()(int x, int y) const { return p[(size_t)clip3(0, h - 1, y) * w + clip3(0, w - 1, x)]; }
+};
+
+// dequantise + inverse transform a TB of levels into a residual (int16 raster)
+void residual_of(const int16_t* lev, int lg, int qidx, int txt, int16_t* res) {
+  const int N = 1 << lg, area = N * N;
+  int16_t dq[256];
+  bool any = false;
+  for (int i = 0; i < area; ++i) {
+    dq[i] = (int16_t)dequant(lev[i], i == 0 ? dc_q(qidx) : ac_q(qidx));
+    any |= dq[i] != 0;
+  }
+  if (!any) {
+    std::memset(res, 0, sizeof(int16_t) * area);
+    return;
+  }
+  txfm2d_ref(dq, res, 1, lg, txt & 1, (txt >> 1) & 1, true);
+}
+
+void loop_filters(const SeqGeo& g, const FrameParams& fp, const uint32_t* mode, const int8_t* cdef_idx, Planes& rec,
+                  Planes& out) {
+  const int W = g.W, H = g.H;
+  // deblocking: one info word per 4x4 unit of each plane
+  Planes db;
+  db.y.resize(rec.y.size());
+  db.u.resize(rec.u.size());
+  db.v.resize(rec.v.size());
+  for (int p = 0; p < 3; ++p) {
+    const int w = p ? W / 2 : W, h = p ? H / 2 : H, w4 = w / 4, h4 = h / 4, bs4 = p ? 2 : 4;
+    const int lv = p == 0 ? fp.lf[0] : fp.lf[p + 1], lh = p == 0 ? fp.lf[1] : fp.lf[p + 1];
+    std::vector<uint32_t> info((size_t)w4 * h4);
+    for (int y = 0; y < h4; ++y)
+      for (int x = 0; x < w4; ++x) {
+        const uint32_t m = mode[(y / bs4) * g.bw + x / bs4];
+        info[(size_t)y * w4 + x] = lf_word(p > 0, lv, lh, mode_skip(m) && mode_inter(m));
+      }
+    const std::vector<uint8_t>& in = p == 0 ? rec.y : (p == 1 ? rec.u : rec.v);
+    std::vector<uint8_t>& o = p == 0 ? db.y : (p == 1 ? db.u : db.v);
+    if ((p == 0 && !(fp.lf[0] || fp.lf[1])) || (p > 0 && !(fp.lf[0] || fp.lf[1]))) o = in;
+    else deblock(in.data(), w, h, p > 0, info.data(), fp.sharp, o.data());
+  }
+  // CDEF with the per-SB preset of cdef_idx (-1: off)
+  const int n8 = (W / 8) * (H / 8);
+  std::vector<uint8_t> dir(n8);
+  std::vector<int> var(n8);
+  cdef_find_dirs(db.y.data(), W, H, dir.data(), var.data());
+  std::vector<int8_t> py(g.nsb()), puv(g.nsb());
+  for (int s = 0; s < g.nsb(); ++s) {
+    py[s] = cdef_idx[s] < 0 ? -1 : (int8_t)fp.cdef_y[cdef_idx[s]];
+    puv[s] = cdef_idx[s] < 0 ? -1 : (int8_t)fp.cdef_uv[cdef_idx[s]];
+  }
+  out.y.resize(db.y.size());
+  out.u.resize(db.u.size());
+  out.v.resize(db.v.size());
+  cdef_apply(db.y.data(), W, H, false, dir.data(), var.data(), W / 8, fp.cdef_damping, py.data(), out.y.data());
+  cdef_apply(db.u.data(), W / 2, H / 2, true, dir.data(), var.data(), W / 8, fp.cdef_damping, puv.data(),
+             out.u.data());
+  cdef_apply(db.v.data(), W / 2, H / 2, true, dir.data(), var.data(), W / 8, fp.cdef_damping, puv.data(),
+             out.v.data());
+}
+
+// prediction of one block (luma 16x16 or chroma 8x8) into pred[]
+void predict(const SeqGeo& g, int p, int bx, int by, uint32_t m, uint32_t mvw, const Planes& rec, const Planes* ref,
+             int* pred) {
+  const int N = p ? 8 : 16, w = p ? g.W / 2 : g.W, h = p ? g.H / 2 : g.H;
+  const int x0 = bx * N, y0 = by * N;
+  if (mode_inter(m)) {
+    if (!ref) throw std::runtime_error("av1: inter block without a reference");
+    const std::vector<uint8_t>& R = p == 0 ? ref->y : (p == 1 ? ref->u : ref->v);
+    PlaneRef get{R.data(), w, h};
+    const int r = mv_row(mvw), c = mv_col(mvw);
+    const int ix = mv_int(c, p > 0), iy = mv_int(r, p > 0), fx = mv_frac(c, p > 0), fy = mv_frac(r, p > 0);
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) pred[i * N + j] = inter_pred_px(get, x0 + j + ix, y0 + i + iy, fx, fy);
+    return;
+  }
+  const std::vector<uint8_t>& C = p == 0 ? rec.y : (p == 1 ? rec.u : rec.v);
+  auto get = [&](int x, int y) { return (int)C[(size_t)y * w + x]; };
+  IntraEdge e;
+  intra_edges(get, x0, y0, N, e);
+  const int mode = p ? mode_uv(m) : mode_y(m), dc = intra_dc(e, N);
+  for (int i = 0; i < N; ++i)
+    for (int j = 0; j < N; ++j) pred[i * N + j] = intra_pred_px(mode, e, N, i, j, dc);
+}
+
+}  // namespace
+
+void reconstruct(const SeqGeo& g, const FrameDecisions& d, const Planes* ref, Planes& out) {
+  Planes rec;
+  rec.y.assign((size_t)g.W * g.H, 0);
+  rec.u.assign((size_t)g.W * g.H / 4, 0);
+  rec.v.assign((size_t)g.W * g.H / 4, 0);
+  const int nb = g.nblk();
+  std::vector<int32_t> off[3];
+  const int16_t* base[3] = {d.ly, d.lu, d.lv};
+  for (int p = 0; p < 3; ++p) {
+    off[p].assign(nb, -1);
+    int k = 0;
+    for (int b = 0; b < nb; ++b)
+      if (!d.packed || (mode_nz(d.mode[b]) >> p & 1)) off[p][b] = d.packed ? k++ : b;
+  }
+  for (int by = 0; by < g.bh; ++by)
+    for (int bx = 0; bx < g.bw; ++bx) {
+      const int b = by * g.bw + bx;
+      const uint32_t m = d.mode[b], mvw = d.mv ? d.mv[b] : 0;
+      for (int p = 0; p < 3; ++p) {
+        const int N = p ? 8 : 16, lg = p ? 3 : 4, w = p ? g.W / 2 : g.W;
+        int pred[256];
+        int16_t res[256];
+        predict(g, p, bx, by, m, mvw, rec, ref, pred);
+        const bool nz = !mode_skip(m) && (mode_nz(m) >> p & 1) && off[p][b] >= 0;
+        if (nz) {
+          const int txt = p == 0 || mode_inter(m) ? 0 : uv_txtype(mode_uv(m));
+          residual_of(base[p] + (size_t)off[p][b] * N * N, lg, d.fp.qindex, txt, res);
+        } else {
+          std::memset(res, 0, sizeof(res));
+        }
+        std::vector<uint8_t>& P = p == 0 ? rec.y : (p == 1 ? rec.u : rec.v);
+        for (int i = 0; i < N; ++i)
+          for (int j = 0; j < N; ++j)
+            P[(size_t)(by * N + i) * w + bx * N + j] = (uint8_t)clip_pixel(pred[i * N + j] + res[i * N + j]);
+      }
+    }
+  loop_filters(g, d.fp, d.mode, d.cdef_idx, rec, out);
+}
+
+// ================================================================== decoder oracle ======
+namespace {
+size_t read_leb128(const uint8_t* p, size_t n, size_t& pos) {
+  size_t v = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (pos >= n) throw std::runtime_error("av1 oracle: truncated leb128");
+    const uint8_t b = p[pos++];
+    v |= (size_t)(b & 0x7f) << (7 * i);
+    if (!(b & 0x80)) return v;
+  }
+  throw std::runtime_error("av1 oracle: bad leb128");
+}
+}  // namespace
+
+Decoded decode_stream(const uint8_t* p, size_t n) {
+  Decoded out;
+  bool have_seq = false;
+  size_t pos = 0;
+  while (pos < n) {
+    const uint8_t h = p[pos++];
+    if (h & 0x80) throw std::runtime_error("av1 oracle: forbidden bit set");
+    const int type = (h >> 3) & 15;
+    if (h & 4) throw std::runtime_error("av1 oracle: extension headers unsupported");
+    if (!(h & 2)) throw std::runtime_error("av1 oracle: OBU without size field");
+    const size_t sz = read_leb128(p, n, pos);
+    if (pos + sz > n) throw std::runtime_error("av1 oracle: truncated OBU");
+    const uint8_t* q = p + pos;
+    pos += sz;
+    if (type == OBU_TEMPORAL_DELIMITER) continue;
+    if (type == OBU_SEQUENCE_HEADER) {
+      BitReader r(q, sz);
+      out.geo = read_seq_header(r);
+      have_seq = true;
+      continue;
+    }
+    if (type != OBU_FRAME) throw std::runtime_error("av1 oracle: OBU type outside the encoder subset");
+    if (!have_seq) throw std::runtime_error("av1 oracle: frame before sequence header");
+    BitReader r(q, sz);
+    bool have_ref = !out.frames.empty();
+    SeqGeo g = out.geo;
+    FrameData fd;
+    fd.fp = read_frame_header(r, g, have_ref);
+    out.geo = g;
+    r.byte_align();
+    const size_t hdr = r.byte_pos();
+    const int nb = g.nblk();
+    fd.mode.assign(nb, 0);
+    fd.mv.assign(nb, 0);
+    fd.ly.assign((size_t)nb * 256, 0);
+    fd.lu.assign((size_t)nb * 64, 0);
+    fd.lv.assign((size_t)nb * 64, 0);
+    fd.cdef_idx.assign(g.nsb(), -1);
+    SymR io(q + hdr, sz - hdr);
+    Tile<SymR> t(io, g, fd.fp, fd.mode, fd.mv, fd.cdef_idx);
+    t.lev_out[0] = fd.ly.data();
+    t.lev_out[1] = fd.lu.data();
+    t.lev_out[2] = fd.lv.data();
+    t.tile();
+    Planes rec;
+    reconstruct(g, fd.view(), fd.fp.key ? nullptr : &out.frames.back(), rec);
+    out.frames.push_back(std::move(rec));
+    out.data.push_back(std::move(fd));
+  }
+  return out;
+}
+
+// ================================================================== golden encoder ======
+void cdef_choose(const uint64_t* sse_y, const uint64_t* sse_uv, const uint8_t* active, int nfb, uint8_t* ytab,
+                 uint8_t* uvtab, int8_t* fb_idx) {
+  std::vector<uint64_t> best(nfb, ~0ull);
+  for (int k = 0; k < kMaxPresets; ++k) {
+    int bp = 0;
+    uint64_t bt = ~0ull;
+    for (int p = 0; p < kCdefPresets; ++p) {
+      uint64_t t = 0;
+      for (int f = 0; f < nfb; ++f)
+        if (active[f]) t += std::min(best[f], sse_y[(size_t)f * kCdefPresets + p]);
+      if (t < bt) bt = t, bp = p;
+    }
+    ytab[k] = (uint8_t)bp;
+    for (int f = 0; f < nfb; ++f) best[f] = std::min(best[f], sse_y[(size_t)f * kCdefPresets + bp]);
+  }
+  std::vector<int> a(nfb, 0);
+  for (int f = 0; f < nfb; ++f) {
+    uint64_t bv = ~0ull;
+    for (int k = 0; k < kMaxPresets; ++k) {
+      const uint64_t v = sse_y[(size_t)f * kCdefPresets + ytab[k]];
+      if (v < bv) bv = v, a[f] = k;
+    }
+  }
+  for (int k = 0; k < kMaxPresets; ++k) {
+    int bp = 0;
+    uint64_t bt = ~0ull;
+    for (int p = 0; p < kCdefPresets; ++p) {
+      uint64_t t = 0;
+      for (int f = 0; f < nfb; ++f)
+        if (active[f] && a[f] == k) t += sse_uv[(size_t)f * kCdefPresets + p];
+      if (t < bt) bt = t, bp = p;
+    }
+    uvtab[k] = (uint8_t)bp;
+  }
+  for (int f = 0; f < nfb; ++f) {
+    if (!active[f]) {
+      fb_idx[f] = -1;
+      continue;
+    }
+    uint64_t bv = ~0ull;
+    int bk = 0;
+    for (int k = 0; k < kMaxPresets; ++k) {
+      const uint64_t v = sse_y[(size_t)f * kCdefPresets + ytab[k]] + sse_uv[(size_t)f * kCdefPresets + uvtab[k]];
+      if (v < bv) bv = v, bk = k;
+    }
+    fb_idx[f] = (int8_t)bk;
+  }
+}
+
+namespace {
+// run f(row) for rows [0, n) on up to hardware_concurrency threads (disjoint outputs)
+template <class F> void parallel_rows(int n, F f) {
+  const int nt = std::max(1, std::min(n, (int)std::thread::hardware_concurrency()));
+  std::atomic<int> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&] {
+      for (int r; (r = next.fetch_add(1)) < n;) f(r);
+    });
+  for (auto& x : th) x.join();
+}
+// transform + quantise + reconstruct one TB: src/pred raster N x N -> levels, recon
+int code_tb(const int* src, const int* pred, int lg, int qidx, int txt, int rnd, int16_t* lev, int* rec) {
+  const int N = 1 << lg, area = N * N;
+  int16_t r[256], c[256], res[256];
+  for (int i = 0; i < area; ++i) r[i] = (int16_t)(src[i] - pred[i]);
+  txfm2d_ref(r, c, 1, lg, txt & 1, (txt >> 1) & 1, false);
+  int nz = 0;
+  for (int i = 0; i < area; ++i) {
+    lev[i] = (int16_t)quant(c[i], i == 0 ? dc_q(qidx) : ac_q(qidx), rnd);
+    nz |= lev[i] != 0;
+  }
+  if (nz) residual_of(lev, lg, qidx, txt, res);
+  else std::memset(res, 0, sizeof(int16_t) * area);
+  for (int i = 0; i < area; ++i) rec[i] = clip_pixel(pred[i] + res[i]);
+  return nz;
+}
+int satd_block(const int* a, const int* b, int N) {
+  int s = 0;
+  for (int by = 0; by < N; by += 4)
+    for (int bx = 0; bx < N; bx += 4) {
+      int d[16];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) d[i * 4 + j] = a[(by + i) * N + bx + j] - b[(by + i) * N + bx + j];
+      s += satd4(d);
+    }
+  return s;
+}
+}  // namespace
+
+GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qidx) {
+  GoldenOut out;
+  const int nb = g.nblk(), lam = lambda16(qidx);
+  for (size_t f = 0; f < src.size(); ++f) {
+    const Planes& S = src[f];
+    const Planes* ref = f ? &out.recon.back() : nullptr;
+    FrameData fd;
+    fd.fp.key = f == 0;
+    fd.fp.qindex = qidx;
+    const int lvl = lf_level_for_q(qidx);
+    for (int i = 0; i < 4; ++i) fd.fp.lf[i] = lvl;
+    fd.fp.cdef_damping = 3 + (qidx >> 6);
+    fd.mode.assign(nb, 0);
+    fd.mv.assign(nb, 0);
+    fd.ly.assign((size_t)nb * 256, 0);
+    fd.lu.assign((size_t)nb * 64, 0);
+    fd.lv.assign((size_t)nb * 64, 0);
+    Planes rec;
+    rec.y.assign((size_t)g.W * g.H, 0);
+    rec.u.assign((size_t)g.W * g.H / 4, 0);
+    rec.v.assign((size_t)g.W * g.H / 4, 0);
+    // edge-extended luma reference for the full-pel search
+    constexpr int kPad = kMeRange + 8;
+    const int pw = g.W + 2 * kPad;
+    std::vector<uint8_t> padY;
+    if (ref) {
+      padY.resize((size_t)pw * (g.H + 2 * kPad));
+      PlaneRef ry{ref->y.data(), g.W, g.H};
+      for (int y = 0; y < g.H + 2 * kPad; ++y)
+        for (int x = 0; x < pw; ++x) padY[(size_t)y * pw + x] = (uint8_t)ry(x - kPad, y - kPad);
+    }
+    auto code_block = [&](int by, int bx) {
+        const int b = by * g.bw + bx;
+        int s[3][256], pred[3][256], rc[256];
+        for (int p = 0; p < 3; ++p) {
+          const int N = p ? 8 : 16, w = p ? g.W / 2 : g.W;
+          const std::vector<uint8_t>& P = p == 0 ? S.y : (p == 1 ? S.u : S.v);
+          for (int i = 0; i < N; ++i)
+            for (int j = 0; j < N; ++j) s[p][i * N + j] = P[(size_t)(by * N + i) * w + bx * N + j];
+        }
+        int ym = 0, uvm = 0, inter = 0;
+        uint32_t mvw = 0;
+        if (fd.fp.key) {
+          int best = 1 << 30;
+          for (int k = 0; k < kNumIntraCand; ++k) {
+            const uint32_t m = pack_mode(0, intra_cand(k), 0, 0, 0);
+            int pr[256];
+            predict(g, 0, bx, by, m, 0, rec, nullptr, pr);
+            const int cost = satd_block(s[0], pr, 16) + ((lam * intra_mode_bits16(intra_cand(k))) >> 8);
+            if (cost < best) best = cost, ym = intra_cand(k), std::memcpy(pred[0], pr, sizeof(pr));
+          }
+          best = 1 << 30;
+          for (int k = 0; k < kNumIntraCand; ++k) {
+            const uint32_t m = pack_mode(0, 0, intra_cand(k), 0, 0);
+            int pu[64], pv[64];
+            predict(g, 1, bx, by, m, 0, rec, nullptr, pu);
+            predict(g, 2, bx, by, m, 0, rec, nullptr, pv);
+            const int cost = satd_block(s[1], pu, 8) + satd_block(s[2], pv, 8) +
+                             ((lam * intra_mode_bits16(intra_cand(k))) >> 8);
+            if (cost < best) {
+              best = cost, uvm = intra_cand(k);
+              std::memcpy(pred[1], pu, sizeof(pu));
+              std::memcpy(pred[2], pv, sizeof(pv));
+            }
+          }
+        } else {
+          inter = 1;
+          // integer search on the edge-extended reference
+          int bc = 1 << 30, bk = 0;
+          for (int k = 0; k < kMeSide * kMeSide; ++k) {
+            const int dx = me_cand_dx(k), dy = me_cand_dy(k);
+            int sad = 0;
+            const uint8_t* rp = padY.data() + (size_t)(by * 16 + dy + kPad) * pw + bx * 16 + dx + kPad;
+            for (int i = 0; i < 16; ++i)
+              for (int j = 0; j < 16; ++j) sad += std::abs(s[0][i * 16 + j] - (int)rp[(size_t)i * pw + j]);
+            const int cost = sad + ((lam * (mv_comp_bits(dy * 8) + mv_comp_bits(dx * 8))) >> 4);
+            if (cost < bc) bc = cost, bk = k;
+          }
+          int mr = me_cand_dy(bk) * 8, mc = me_cand_dx(bk) * 8;
+          auto sub_cost = [&](int r, int c) {
+            int pr[256];
+            predict(g, 0, bx, by, pack_mode(1, 0, 0, 0, 0), pack_mv(r, c), rec, ref, pr);
+            return satd_block(s[0], pr, 16) + ((lam * (mv_comp_bits(r) + mv_comp_bits(c))) >> 4);
+          };
+          for (int step = 4; step >= 2; step >>= 1) {
+            int best = sub_cost(mr, mc), br = mr, bcc = mc;
+            for (int k = 0; k < 8; ++k) {
+              const int r = mr + me_ring_dy(k) * step, c = mc + me_ring_dx(k) * step;
+              const int cst = sub_cost(r, c);
+              if (cst < best) best = cst, br = r, bcc = c;
+            }
+            mr = br;
+            mc = bcc;
+          }
+          mvw = pack_mv(mr, mc);
+          for (int p = 0; p < 3; ++p) predict(g, p, bx, by, pack_mode(1, 0, 0, 0, 0), mvw, rec, ref, pred[p]);
+        }
+        int nz = 0;
+        for (int p = 0; p < 3; ++p) {
+          const int N = p ? 8 : 16, lg = p ? 3 : 4, w = p ? g.W / 2 : g.W;
+          const int txt = p == 0 || inter ? 0 : uv_txtype(uvm);
+          int16_t* lev = p == 0 ? &fd.ly[(size_t)b * 256] : (p == 1 ? &fd.lu[(size_t)b * 64] : &fd.lv[(size_t)b * 64]);
+          if (code_tb(s[p], pred[p], lg, qidx, txt, inter ? kRndInter : kRndIntra, lev, rc)) nz |= 1 << p;
+          std::vector<uint8_t>& P = p == 0 ? rec.y : (p == 1 ? rec.u : rec.v);
+          for (int i = 0; i < N; ++i)
+            for (int j = 0; j < N; ++j) P[(size_t)(by * N + i) * w + bx * N + j] = (uint8_t)rc[i * N + j];
+        }
+        fd.mode[b] = pack_mode(inter, ym, uvm, nz == 0, nz);
+        fd.mv[b] = mvw;
+    };
+    if (fd.fp.key) {  // intra: left / above dependencies (raster order)
+      for (int by = 0; by < g.bh; ++by)
+        for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx);
+    } else {  // inter blocks only read the reference: rows in parallel
+      parallel_rows(g.bh, [&](int by) {
+        for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx);
+      });
+    }
+    // loop filters with the CDEF search on the deblocked frame
+    const int W = g.W, H = g.H;
+    Planes db;
+    {
+      // deblock only (cdef off) to obtain the search input
+      std::vector<int8_t> off(g.nsb(), -1);
+      loop_filters(g, fd.fp, fd.mode.data(), off.data(), rec, db);
+    }
+    const int n8 = (W / 8) * (H / 8), nfb = g.nsb();
+    std::vector<uint8_t> dir(n8);
+    std::vector<int> var(n8);
+    cdef_find_dirs(db.y.data(), W, H, dir.data(), var.data());
+    std::vector<uint64_t> sy((size_t)nfb * kCdefPresets), su(sy.size()), sv(sy.size());
+    cdef_search(S.y.data(), db.y.data(), W, H, false, dir.data(), var.data(), W / 8, fd.fp.cdef_damping, sy.data());
+    cdef_search(S.u.data(), db.u.data(), W / 2, H / 2, true, dir.data(), var.data(), W / 8, fd.fp.cdef_damping,
+                su.data());
+    cdef_search(S.v.data(), db.v.data(), W / 2, H / 2, true, dir.data(), var.data(), W / 8, fd.fp.cdef_damping,
+                sv.data());
+    for (size_t i = 0; i < su.size(); ++i) su[i] += sv[i];
+    std::vector<uint8_t> active(nfb, 0);
+    for (int b = 0; b < nb; ++b)
+      if (!mode_skip(fd.mode[b])) active[((b / g.bw) / 4) * g.sbw + (b % g.bw) / 4] = 1;
+    fd.cdef_idx.assign(nfb, -1);
+    cdef_choose(sy.data(), su.data(), active.data(), nfb, fd.fp.cdef_y, fd.fp.cdef_uv, fd.cdef_idx.data());
+    // final recon: CDEF applied to the deblocked frame
+    Planes fin;
+    loop_filters(g, fd.fp, fd.mode.data(), fd.cdef_idx.data(), rec, fin);
+    out.recon.push_back(std::move(fin));
+    out.frames.push_back(std::move(fd));
+  }
+  return out;
+}
+
+}  // namespace av1
+}  // namespace tv
+
+// ================================================================== C API ===============
+namespace {
+thread_local std::string g_codec_err;
+template <class F> int codec_guard(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_codec_err = e.what();
+    return -1;
+  }
+}
+void split_planes(const uint8_t* yuv, const tv::av1::SeqGeo& g, tv::av1::Planes& P) {
+  const size_t ys = (size_t)g.W * g.H, cs = ys / 4;
+  P.y.assign(yuv, yuv + ys);
+  P.u.assign(yuv + ys, yuv + ys + cs);
+  P.v.assign(yuv + ys + cs, yuv + ys + 2 * cs);
+}
+// frame parameter vector of the C API: key, qindex, lf[4], sharp, damping, cdef_bits,
+// cdef_y[8], cdef_uv[8]
+void pack_fparams(const tv::av1::FrameParams& fp, int32_t* p) {
+  p[0] = fp.key;
+  p[1] = fp.qindex;
+  for (int i = 0; i < 4; ++i) p[2 + i] = fp.lf[i];
+  p[6] = fp.sharp;
+  p[7] = fp.cdef_damping;
+  p[8] = fp.cdef_bits;
+  for (int i = 0; i < 8; ++i) {
+    p[9 + i] = fp.cdef_y[i];
+    p[17 + i] = fp.cdef_uv[i];
+  }
+}
+tv::av1::FrameParams unpack_fparams(const int32_t* p) {
+  tv::av1::FrameParams fp;
+  fp.key = p[0];
+  fp.qindex = p[1];
+  for (int i = 0; i < 4; ++i) fp.lf[i] = p[2 + i];
+  fp.sharp = p[6];
+  fp.cdef_damping = p[7];
+  fp.cdef_bits = p[8];
+  for (int i = 0; i < 8; ++i) {
+    fp.cdef_y[i] = (uint8_t)p[9 + i];
+    fp.cdef_uv[i] = (uint8_t)p[17 + i];
+  }
+  return fp;
+}
+void join_planes(const tv::av1::Planes& P, uint8_t* out) {
+  std::memcpy(out, P.y.data(), P.y.size());
+  std::memcpy(out + P.y.size(), P.u.data(), P.u.size());
+  std::memcpy(out + P.y.size() + P.u.size(), P.v.data(), P.v.size());
+}
+}  // namespace
+
+extern "C" {
+using namespace tv::av1;
+const char* tv_av1c_last_error() { return g_codec_err.c_str(); }
+
+// Golden encode of n coded-size I420 frames (concatenated Y U V per frame) at `qidx`:
+// the temporal units go to `out` (one Bytes object) and their byte sizes to tu_sizes[n];
+// the post-filter reconstructions to recon (same layout); per-frame decisions to mode /
+// mv [n][nblk] and levels ly [n][nblk][256], lu / lv [n][nblk][64] (may be null).
+int tv_av1c_golden_encode(int dw, int dh, int n, const uint8_t* yuv, int qidx, void* out, int64_t* tu_sizes,
+                          uint8_t* recon, uint32_t* mode, uint32_t* mv, int16_t* ly, int16_t* lu, int16_t* lv,
+                          int32_t* fparams, int8_t* cdef) {
+  return codec_guard([&] {
+    const SeqGeo g = make_seq_geo(dw, dh);
+    const size_t fsz = (size_t)g.W * g.H * 3 / 2;
+    std::vector<Planes> src(n);
+    for (int i = 0; i < n; ++i) split_planes(yuv + i * fsz, g, src[i]);
+    GoldenOut go = golden_encode(g, src, qidx);
+    auto* bytes = static_cast<std::vector<uint8_t>*>(out);
+    bytes->clear();
+    const int nb = g.nblk();
+    for (int i = 0; i < n; ++i) {
+      const auto tu = write_temporal_unit(g, go.frames[i].view(), i == 0);
+      bytes->insert(bytes->end(), tu.begin(), tu.end());
+      tu_sizes[i] = (int64_t)tu.size();
+      if (recon) join_planes(go.recon[i], recon + i * fsz);
+      const FrameData& fd = go.frames[i];
+      if (mode) std::memcpy(mode + (size_t)i * nb, fd.mode.data(), sizeof(uint32_t) * nb);
+      if (mv) std::memcpy(mv + (size_t)i * nb, fd.mv.data(), sizeof(uint32_t) * nb);
+      if (ly) std::memcpy(ly + (size_t)i * nb * 256, fd.ly.data(), sizeof(int16_t) * nb * 256);
+      if (lu) std::memcpy(lu + (size_t)i * nb * 64, fd.lu.data(), sizeof(int16_t) * nb * 64);
+      if (lv) std::memcpy(lv + (size_t)i * nb * 64, fd.lv.data(), sizeof(int16_t) * nb * 64);
+      if (fparams) pack_fparams(fd.fp, fparams + (size_t)i * 25);
+      if (cdef) std::memcpy(cdef + (size_t)i * g.nsb(), fd.cdef_idx.data(), g.nsb());
+    }
+  });
+}
+
+// Decode a stream (concatenated temporal units) -> up to max_frames coded-size frames.
+// geo[0..3] = display w, h, coded W, H; returns the frame count in *nframes.
+int tv_av1c_decode(const uint8_t* data, size_t n, int max_frames, uint8_t* frames, int* geo, int* nframes) {
+  return codec_guard([&] {
+    Decoded d = decode_stream(data, n);
+    geo[0] = d.geo.dw;
+    geo[1] = d.geo.dh;
+    geo[2] = d.geo.W;
+    geo[3] = d.geo.H;
+    *nframes = (int)d.frames.size();
+    if (frames) {
+      const size_t fsz = (size_t)d.geo.W * d.geo.H * 3 / 2;
+      for (int i = 0; i < std::min(max_frames, (int)d.frames.size()); ++i) join_planes(d.frames[i], frames + i * fsz);
+    }
+  });
+}
+
+// Probe a stream's geometry / frame count without reconstructing (header walk).
+int tv_av1c_probe(const uint8_t* data, size_t n, int* geo, int* nframes) {
+  return tv_av1c_decode(data, n, 0, nullptr, geo, nframes);
+}
+
+// Write one frame's temporal unit from engine decisions (packed levels layout).
+int tv_av1c_write_tu(int dw, int dh, const int* fparams, const uint32_t* mode, const uint32_t* mv, const int16_t* ly,
+                     const int16_t* lu, const int16_t* lv, const int8_t* cdef_idx, int packed, int seq_header,
+                     void* out) {
+  return codec_guard([&] {
+    const SeqGeo g = make_seq_geo(dw, dh);
+    FrameDecisions d;
+    d.fp = unpack_fparams(fparams);
+    d.mode = mode;
+    d.mv = mv;
+    d.ly = ly;
+    d.lu = lu;
+    d.lv = lv;
+    d.cdef_idx = cdef_idx;
+    d.packed = packed != 0;
+    auto tu = write_temporal_unit(g, d, seq_header != 0);
+    auto* bytes = static_cast<std::vector<uint8_t>*>(out);
+    bytes->insert(bytes->end(), tu.begin(), tu.end());
+  });
+}
+}  // extern "C"

@@ -5,7 +5,10 @@
 #include "tv/av1.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
+#include <vector>
 #include <stdexcept>
 #include <string>
 
@@ -53,7 +56,12 @@ void cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, bool chro
   const int bs = chroma ? 4 : 8, fbs = fb_size(chroma), nfx = (w + fbs - 1) / fbs;
   const int dmp = chroma ? damping - 1 : damping;
   std::memset(sse, 0, sizeof(uint64_t) * nfb_of(w, h, chroma) * kCdefPresets);
-  for (int by = 0; by < h / bs; ++by)
+  // bands of filter-block rows on separate threads (each writes only its own fb rows)
+  const int nband = (h + fbs - 1) / fbs;
+  const int nt = std::max(1, std::min(nband, (int)std::thread::hardware_concurrency()));
+  std::atomic<int> next{0};
+  auto band = [&](int fr) {
+    for (int by = fr * fbs / bs; by < std::min(h / bs, (fr + 1) * fbs / bs); ++by)
     for (int bx = 0; bx < w / bs; ++bx) {
       const int d = dir[by * luma_w8 + bx], v = var[by * luma_w8 + bx];
       uint64_t* S = sse + (long)((by * bs / fbs) * nfx + bx * bs / fbs) * kCdefPresets;
@@ -71,6 +79,13 @@ void cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, bool chro
         S[p] += acc;
       }
     }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&] {
+      for (int r; (r = next.fetch_add(1)) < nband;) band(r);
+    });
+  for (auto& x : th) x.join();
 }
 
 void cdef_apply(const uint8_t* rec, int w, int h, bool chroma, const uint8_t* dir, const int* var, int luma_w8,

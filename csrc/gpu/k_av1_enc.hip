@@ -1,0 +1,616 @@
+// k_av1_enc.hip — gfx950 kernels of the AV1 encode engine (BASELINE
+// config #4).  Every decision and reconstruction equals the C++ golden encoder
+// (csrc/core/av1_codec.cpp golden_encode) bit for bit; the shared arithmetic lives in
+// tv/av1_enc.h (TV_HD) and the integer transform stages follow av1_txfm.h exactly.
+//
+//   k_av1e_inter   one wave per 16x16 block (P frames): reference window staged in LDS
+//                  (57 x 57 bytes, clamped), full-pel +-16 search on packed v_sad_u8 with
+//                  alignbyte-unaligned LDS rows, half- then quarter-pel refinement (4
+//                  candidates x 16 4x4-SATD lanes per pass, 16-lane DPP reductions),
+//                  luma / chroma prediction, forward transform, quantisation,
+//                  dequantisation, inverse transform and reconstruction.
+//   k_av1e_intra   one wave per 16x16 block of an anti-diagonal (key frames): the seven
+//                  candidate modes read no above-right samples, so the frame is a plain
+//                  (rows + cols - 1)-step wavefront; 4 luma modes x 16 lanes per pass, all
+//                  7 chroma modes x 8 lanes (U + V 4x4 SATDs) in one pass.
+//   k_av1e_lfinfo  deblocking info words (tx / block sizes, levels, skip && inter).
+//   k_av1e_cdef_choose  one workgroup per segment: greedy 8-preset CDEF table from the
+//                  k_cdef_search SSEs of the active 64x64 blocks (identical to cdef_choose).
+// Grids are (blocks, segments): one launch covers the same frame of every segment.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "gpu_common.h"
+#include "tv/av1_enc.h"
+#include "tv/av1_txfm.h"
+
+namespace tv {
+namespace gpu {
+namespace {
+
+using namespace tv::av1;
+
+__constant__ int32_t c_dct16[256];
+__constant__ int32_t c_dct8[64];
+__constant__ int32_t c_adst8[64];
+
+constexpr int R = kMeRange;
+constexpr int kWinP = 60;              // window pitch (bytes, multiple of 4)
+constexpr int kWinN = 16 + 2 * R + 9;  // 57 rows: [-R-4, R+20] around the block
+constexpr int kWinOff = R + 4;         // block origin inside the window
+
+__device__ __forceinline__ int rsr(long long v, int s) { return (int)((v + (1LL << (s - 1))) >> s); }
+__device__ __forceinline__ int c16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+
+// sum over a 16-lane row (every lane gets its row's sum)
+__device__ __forceinline__ int row16_sum(int v) {
+  v += dpp::mov<dpp::kQuadXor1>(v);
+  v += dpp::mov<dpp::kQuadXor2>(v);
+  v += dpp::mov<dpp::kRowHalfMirror>(v);
+  v += dpp::mov<dpp::kRowMirror>(v);
+  return v;
+}
+// sum over an 8-lane half row
+__device__ __forceinline__ int row8_sum(int v) {
+  v += dpp::mov<dpp::kQuadXor1>(v);
+  v += dpp::mov<dpp::kQuadXor2>(v);
+  v += dpp::mov<dpp::kRowHalfMirror>(v);
+  return v;
+}
+
+// basis of 1-D type (0 DCT, 1 ADST) for N = 8 / 16
+__device__ __forceinline__ const int32_t* basis(int lg, int type) {
+  return lg == 4 ? c_dct16 : (type ? c_adst8 : c_dct8);
+}
+
+// One N x N 2-D transform on the calling wave (LDS in -> LDS out), the stages of
+// txfm2d_ref: forward tmp = Bc X (round f1), C = tmp Br^T (round f2); inverse
+// g = X Br (round i1), out = Bc^T g (round i2); int16 clamps after each stage.
+template <int LG>
+__device__ void wave_txfm(const int16_t* in, int16_t* tmp, int16_t* out, int tcol, int trow, bool inverse) {
+  constexpr int N = 1 << LG;
+  const int lane = threadIdx.x & 63;
+  const int32_t* Bc = basis(LG, tcol);
+  const int32_t* Br = basis(LG, trow);
+  const int f1 = 12 + (LG - 1) / 2 - 2, f2 = 12 + LG / 2 - 1, i1 = 13 + LG / 2, i2 = 14 + (LG - 1) / 2;
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int r = idx >> LG, c = idx & (N - 1);
+    long long s = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      s += inverse ? (long long)in[r * N + k] * Br[k * N + c] : (long long)Bc[r * N + k] * in[k * N + c];
+    tmp[idx] = (int16_t)c16(rsr(s, inverse ? i1 : f1));
+  }
+  __syncthreads();
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int r = idx >> LG, c = idx & (N - 1);
+    long long s = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      s += inverse ? (long long)Bc[k * N + r] * tmp[k * N + c] : (long long)tmp[r * N + k] * Br[c * N + k];
+    out[idx] = (int16_t)c16(rsr(s, inverse ? i2 : f2));
+  }
+  __syncthreads();
+}
+
+// Residual coding of one TB held in LDS: res (int16, src - pred) -> levels (global),
+// reconstruction added onto pred (int, LDS) -> returns 1 if any level is nonzero.
+// Scratch a/b: LDS int16 [N*N] each.
+template <int LG>
+__device__ int code_tb(int16_t* res, int16_t* a, int16_t* b, int tcol, int trow, int qidx, int rnd,
+                       int16_t* __restrict__ lev_out) {
+  constexpr int N = 1 << LG;
+  const int lane = threadIdx.x & 63;
+  wave_txfm<LG>(res, a, b, tcol, trow, false);  // coefficients in b
+  const int qd = dc_q(qidx), qa = ac_q(qidx);
+  int nz = 0;
+  for (int i = lane; i < N * N; i += 64) {
+    const int l = quant(b[i], i ? qa : qd, rnd);
+    lev_out[i] = (int16_t)l;
+    a[i] = (int16_t)dequant(l, i ? qa : qd);
+    nz |= l != 0;
+  }
+  const bool any = __any(nz);
+  __syncthreads();
+  if (any) {
+    wave_txfm<LG>(a, b, res, tcol, trow, true);  // residual back in res
+  } else {
+    for (int i = lane; i < N * N; i += 64) res[i] = 0;
+    __syncthreads();
+  }
+  return any ? 1 : 0;
+}
+
+struct Planes3 {
+  const uint8_t *y, *u, *v;
+};
+struct Planes3W {
+  uint8_t *y, *u, *v;
+};
+
+// ================================================================= inter ================
+__global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Planes3W rec, uint32_t* __restrict__ mode,
+                                                   uint32_t* __restrict__ mvout, int16_t* __restrict__ ly,
+                                                   int16_t* __restrict__ lu, int16_t* __restrict__ lv, int W, int H,
+                                                   int qidx) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kWinN * kWinP + 8];
+  __shared__ __attribute__((aligned(16))) uint8_t sblk[256];
+  __shared__ int cost[9];
+  __shared__ int16_t res[256], ta[256], tb[256];
+  __shared__ int predc[256];
+  int blk, b;
+  xcd_ctb(blk, b);
+  const int lane = threadIdx.x;
+  const int bw = W >> 4, bx = blk % bw, by = blk / bw, x0 = bx * 16, y0 = by * 16;
+  const long ysz = (long)W * H, csz = ysz >> 2;
+  const uint8_t* S = src.y + b * ysz;
+  const uint8_t* Rf = ref.y + b * ysz;
+  const int lam = lambda16(qidx);
+  // stage the clamped reference window and the source block
+  for (int i = lane; i < kWinN * kWinN; i += 64) {
+    const int wy = i / kWinN, wx = i - wy * kWinN;
+    const int yy = clip3(0, H - 1, y0 - kWinOff + wy), xx = clip3(0, W - 1, x0 - kWinOff + wx);
+    win[wy * kWinP + wx] = Rf[(long)yy * W + xx];
+  }
+  for (int i = lane; i < 256; i += 64) sblk[i] = S[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)];
+  __syncthreads();
+  // ---- full-pel search: packed SAD, first minimum of (cost, index)
+  uint32_t sv[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) sv[i] = reinterpret_cast<const uint32_t*>(sblk)[i];
+  unsigned best = 0xFFFFFFFFu;
+  for (int k = lane; k < kMeSide * kMeSide; k += 64) {
+    const int dx = me_cand_dx(k), dy = me_cand_dy(k);
+    unsigned sad = 0;
+    const int ox = kWinOff + dx, sh = ox & 3;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(win + (kWinOff + dy + i) * kWinP + (ox & ~3));
+      const uint32_t w0 = row[0], w1 = row[1], w2 = row[2], w3 = row[3], w4 = row[4];
+      sad = __builtin_amdgcn_sad_u8(sv[i * 4 + 0], __builtin_amdgcn_alignbyte(w1, w0, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sv[i * 4 + 1], __builtin_amdgcn_alignbyte(w2, w1, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sv[i * 4 + 2], __builtin_amdgcn_alignbyte(w3, w2, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sv[i * 4 + 3], __builtin_amdgcn_alignbyte(w4, w3, sh), sad);
+    }
+    const unsigned c = sad + ((lam * (mv_comp_bits(dy * 8) + mv_comp_bits(dx * 8))) >> 4);
+    const unsigned key = (c << 12) | (unsigned)k;
+    best = key < best ? key : best;
+  }
+  best = wave_min_u32(best);
+  const int bk = best & 4095;
+  int mr = me_cand_dy(bk) * 8, mc = me_cand_dx(bk) * 8;
+  // ---- sub-pel refinement: center + 8 ring candidates at step 4 (half) then 2 (quarter)
+  auto wget = [&](int x, int y) -> int {  // window sample at block-relative (x, y)
+    return win[(kWinOff + y) * kWinP + kWinOff + x];
+  };
+  const int grp = lane >> 4, b4 = lane & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
+  for (int step = 4; step >= 2; step >>= 1) {
+    for (int pass = 0; pass < 3; ++pass) {
+      const int ci = pass * 4 + grp;  // 0 = center, 1..8 = ring
+      int r = mr, c = mc;
+      if (ci >= 1 && ci <= 8) {
+        r += me_ring_dy(ci - 1) * step;
+        c += me_ring_dx(ci - 1) * step;
+      }
+      int d[16];
+      const int ix = mv_int(c, false), iy = mv_int(r, false), fx = mv_frac(c, false), fy = mv_frac(r, false);
+      int hrow[11][4];
+#pragma unroll
+      for (int rr = 0; rr < 11; ++rr)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int s = 0;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) s += subpel_tap(fx, t) * wget(px + j + ix + t - 3, py + rr + iy - 3);
+          hrow[rr][j] = (s + (1 << (kInterRound0 - 1))) >> kInterRound0;
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int s = 0;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) s += subpel_tap(fy, t) * hrow[i + t][j];
+          const int p = clip_pixel((s + (1 << (kInterRound1 - 1))) >> kInterRound1);
+          d[i * 4 + j] = (int)sblk[(py + i) * 16 + px + j] - p;
+        }
+      const int sat = row16_sum(satd4(d));
+      if (b4 == 0 && ci <= 8) cost[ci] = sat + ((lam * (mv_comp_bits(r) + mv_comp_bits(c))) >> 4);
+    }
+    __syncthreads();
+    int bc = cost[0], bi = 0;
+    for (int k = 1; k <= 8; ++k)
+      if (cost[k] < bc) bc = cost[k], bi = k;
+    if (bi) {
+      mr += me_ring_dy(bi - 1) * step;
+      mc += me_ring_dx(bi - 1) * step;
+    }
+    __syncthreads();
+  }
+  // ---- luma prediction + residual
+  {
+    const int ix = mv_int(mc, false), iy = mv_int(mr, false), fx = mv_frac(mc, false), fy = mv_frac(mr, false);
+    for (int i = lane; i < 256; i += 64) {
+      const int yy = i >> 4, xx = i & 15;
+      const int p = inter_pred_px(wget, xx + ix, yy + iy, fx, fy);
+      predc[i] = p;
+      res[i] = (int16_t)((int)sblk[i] - p);
+    }
+  }
+  __syncthreads();
+  const int nb = bw * (H >> 4);
+  const long bo = (long)b * nb + blk;
+  int nz = code_tb<4>(res, ta, tb, 0, 0, qidx, kRndInter, ly + bo * 256);
+  for (int i = lane; i < 256; i += 64)
+    rec.y[b * ysz + (long)(y0 + (i >> 4)) * W + x0 + (i & 15)] = (uint8_t)clip_pixel(predc[i] + res[i]);
+  __syncthreads();
+  // ---- chroma (8x8 per plane), reference read through L2 with clamping
+  const int Wc = W >> 1, Hc = H >> 1, cx0 = bx * 8, cy0 = by * 8;
+  const int ix = mv_int(mc, true), iy = mv_int(mr, true), fx = mv_frac(mc, true), fy = mv_frac(mr, true);
+  for (int pl = 1; pl <= 2; ++pl) {
+    const uint8_t* Rc = (pl == 1 ? ref.u : ref.v) + b * csz;
+    const uint8_t* Sc = (pl == 1 ? src.u : src.v) + b * csz;
+    auto cget = [&](int x, int y) -> int { return Rc[(long)clip3(0, Hc - 1, y) * Wc + clip3(0, Wc - 1, x)]; };
+    {
+      const int yy = lane >> 3, xx = lane & 7;
+      const int p = inter_pred_px(cget, cx0 + xx + ix, cy0 + yy + iy, fx, fy);
+      predc[lane] = p;
+      res[lane] = (int16_t)((int)Sc[(long)(cy0 + yy) * Wc + cx0 + xx] - p);
+    }
+    __syncthreads();
+    int16_t* lo = (pl == 1 ? lu : lv) + bo * 64;
+    if (code_tb<3>(res, ta, tb, 0, 0, qidx, kRndInter, lo)) nz |= 1 << pl;
+    uint8_t* Rw = (pl == 1 ? rec.u : rec.v) + b * csz;
+    Rw[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)] = (uint8_t)clip_pixel(predc[lane] + res[lane]);
+    __syncthreads();
+  }
+  if (lane == 0) {
+    mode[bo] = pack_mode(1, 0, 0, nz == 0, nz);
+    mvout[bo] = pack_mv(mr, mc);
+  }
+}
+
+// ================================================================= intra ================
+struct EdgeLds {
+  IntraEdge e;
+  int dc;
+};
+
+// edges of an N x N block of plane P (pitch w) at (x, y) into LDS (lanes 0..2N)
+__device__ void load_edges(const uint8_t* P, int w, int x, int y, int N, EdgeLds& E) {
+  const int lane = threadIdx.x & 63;
+  auto get = [&](int xx, int yy) -> int { return P[(long)yy * w + xx]; };
+  if (lane == 0) {
+    E.e.have_a = y > 0;
+    E.e.have_l = x > 0;
+    if (E.e.have_a && E.e.have_l) E.e.tl = get(x - 1, y - 1);
+    else if (E.e.have_a) E.e.tl = get(x, y - 1);
+    else if (E.e.have_l) E.e.tl = get(x - 1, y);
+    else E.e.tl = 128;
+  }
+  if (lane < N) {
+    const int i = lane;
+    int a, l;
+    if (y > 0) a = get(x + i, y - 1);
+    else if (x > 0) a = get(x - 1, y);
+    else a = 127;
+    if (x > 0) l = get(x - 1, y + i);
+    else if (y > 0) l = get(x, y - 1);
+    else l = 129;
+    E.e.above[i] = a;
+    E.e.left[i] = l;
+  }
+  __syncthreads();
+  if (lane == 0) E.dc = intra_dc(E.e, N);
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, uint32_t* __restrict__ mode,
+                                                   uint32_t* __restrict__ mvout, int16_t* __restrict__ ly,
+                                                   int16_t* __restrict__ lu, int16_t* __restrict__ lv, int W, int H,
+                                                   int qidx, int diag, int bx_lo) {
+  __shared__ EdgeLds E[2];
+  __shared__ uint8_t sblk[256];
+  __shared__ uint8_t sc[2][64];
+  __shared__ int cost[8];
+  __shared__ int16_t res[256], ta[256], tb[256];
+  __shared__ int predc[256];
+  const int lane = threadIdx.x, b = blockIdx.y;
+  const int bw = W >> 4, bx = bx_lo + blockIdx.x, by = diag - bx, x0 = bx * 16, y0 = by * 16;
+  const long ysz = (long)W * H, csz = ysz >> 2;
+  const int lam = lambda16(qidx), Wc = W >> 1, cx0 = bx * 8, cy0 = by * 8;
+  const uint8_t* S = src.y + b * ysz;
+  uint8_t* RY = rec.y + b * ysz;
+  for (int i = lane; i < 256; i += 64) sblk[i] = S[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)];
+  sc[0][lane] = (src.u + b * csz)[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)];
+  sc[1][lane] = (src.v + b * csz)[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)];
+  load_edges(RY, W, x0, y0, 16, E[0]);
+  // ---- luma: 7 candidates, 4 per pass (16 lanes = 16 4x4 SATDs each)
+  const int grp = lane >> 4, b4 = lane & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int ci = pass * 4 + grp;
+    const int m = intra_cand(ci < kNumIntraCand ? ci : 0);
+    int d[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        d[i * 4 + j] = (int)sblk[(py + i) * 16 + px + j] - intra_pred_px(m, E[0].e, 16, py + i, px + j, E[0].dc);
+    const int sat = row16_sum(satd4(d));
+    if (b4 == 0 && ci < kNumIntraCand) cost[ci] = sat + ((lam * intra_mode_bits16(m)) >> 8);
+  }
+  __syncthreads();
+  int ym = intra_cand(0);
+  {
+    int bc = cost[0];
+    for (int k = 1; k < kNumIntraCand; ++k)
+      if (cost[k] < bc) bc = cost[k], ym = intra_cand(k);
+  }
+  __syncthreads();
+  for (int i = lane; i < 256; i += 64) {
+    const int p = intra_pred_px(ym, E[0].e, 16, i >> 4, i & 15, E[0].dc);
+    predc[i] = p;
+    res[i] = (int16_t)((int)sblk[i] - p);
+  }
+  __syncthreads();
+  const int nb = bw * (H >> 4), blk = by * bw + bx;
+  const long bo = (long)b * nb + blk;
+  int nz = code_tb<4>(res, ta, tb, 0, 0, qidx, kRndIntra, ly + bo * 256);
+  for (int i = lane; i < 256; i += 64)
+    RY[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)] = (uint8_t)clip_pixel(predc[i] + res[i]);
+  __syncthreads();
+  // ---- chroma: 7 candidates x 8 lanes (U: 4 blocks, V: 4 blocks) in one pass
+  uint8_t* RU = rec.u + b * csz;
+  uint8_t* RV = rec.v + b * csz;
+  load_edges(RU, Wc, cx0, cy0, 8, E[0]);
+  load_edges(RV, Wc, cx0, cy0, 8, E[1]);
+  {
+    const int ci = lane >> 3, q = lane & 7, pl = q >> 2, qb = q & 3, qx = (qb & 1) * 4, qy = (qb >> 1) * 4;
+    const int m = intra_cand(ci < kNumIntraCand ? ci : 0);
+    int d[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        d[i * 4 + j] = (int)sc[pl][(qy + i) * 8 + qx + j] - intra_pred_px(m, E[pl].e, 8, qy + i, qx + j, E[pl].dc);
+    const int sat = row8_sum(satd4(d));
+    if (q == 0 && ci < kNumIntraCand) cost[ci] = sat + ((lam * intra_mode_bits16(m)) >> 8);
+  }
+  __syncthreads();
+  int uvm = intra_cand(0);
+  {
+    int bc = cost[0];
+    for (int k = 1; k < kNumIntraCand; ++k)
+      if (cost[k] < bc) bc = cost[k], uvm = intra_cand(k);
+  }
+  const int txt = uv_txtype(uvm);
+  for (int pl = 0; pl < 2; ++pl) {
+    __syncthreads();
+    const int p = intra_pred_px(uvm, E[pl].e, 8, lane >> 3, lane & 7, E[pl].dc);
+    predc[lane] = p;
+    res[lane] = (int16_t)((int)sc[pl][lane] - p);
+    __syncthreads();
+    int16_t* lo = (pl == 0 ? lu : lv) + bo * 64;
+    if (code_tb<3>(res, ta, tb, txt & 1, (txt >> 1) & 1, qidx, kRndIntra, lo)) nz |= 2 << pl;
+    uint8_t* Rw = pl == 0 ? RU : RV;
+    Rw[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)] = (uint8_t)clip_pixel(predc[lane] + res[lane]);
+  }
+  if (lane == 0) {
+    mode[bo] = pack_mode(0, ym, uvm, nz == 0, nz);
+    mvout[bo] = 0;
+  }
+}
+
+// ================================================================= loop-filter info ======
+__global__ void k_av1e_lfinfo(const uint32_t* __restrict__ mode, int W, int H, int lv0, int lv1, int lv2, int lv3,
+                              uint32_t* __restrict__ iy, uint32_t* __restrict__ iu, uint32_t* __restrict__ iv) {
+  const int b = blockIdx.y, w4 = W >> 2, h4 = H >> 2, bw = W >> 4, nb = bw * (H >> 4);
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= w4 * h4) return;
+  const int x = u % w4, y = u / w4;
+  const uint32_t m = mode[(long)b * nb + (y >> 2) * bw + (x >> 2)];
+  const bool si = mode_skip(m) && mode_inter(m);
+  iy[(long)b * w4 * h4 + u] = lf_word(false, lv0, lv1, si);
+  if (!(x & 1) && !(y & 1)) {
+    const long cu = (long)b * (w4 / 2) * (h4 / 2) + (y >> 1) * (w4 / 2) + (x >> 1);
+    iu[cu] = lf_word(true, lv2, lv2, si);
+    iv[cu] = lf_word(true, lv3, lv3, si);
+  }
+}
+
+// ================================================================= CDEF preset choice ====
+constexpr int kMaxFb = 4096;
+__global__ void __launch_bounds__(256) k_av1e_cdef_choose(const unsigned long long* __restrict__ sy,
+                                                          const unsigned long long* __restrict__ su,
+                                                          const unsigned long long* __restrict__ sv,
+                                                          const uint32_t* __restrict__ mode, int W, int H,
+                                                          uint8_t* __restrict__ tabs, int8_t* __restrict__ fbidx,
+                                                          int8_t* __restrict__ py, int8_t* __restrict__ puv) {
+  __shared__ unsigned long long best[kMaxFb];
+  __shared__ uint8_t active[kMaxFb], asg[kMaxFb];
+  __shared__ unsigned long long part[4][64];
+  __shared__ uint8_t ytab[8], uvtab[8];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int bw = W >> 4, bh = H >> 4, nb = bw * bh, sbw = (W + 63) >> 6, sbh = (H + 63) >> 6, nfb = sbw * sbh;
+  const long so = (long)b * nfb * 64;
+  for (int f = t; f < nfb; f += 256) {
+    const int sx = f % sbw, sy0 = f / sbw;
+    int act = 0;
+    for (int yy = sy0 * 4; yy < min(bh, sy0 * 4 + 4); ++yy)
+      for (int xx = sx * 4; xx < min(bw, sx * 4 + 4); ++xx) act |= !mode_skip(mode[(long)b * nb + yy * bw + xx]);
+    active[f] = (uint8_t)act;
+    best[f] = ~0ull;
+  }
+  __syncthreads();
+  const int p = t & 63, pq = t >> 6;
+  for (int k = 0; k < kMaxPresets; ++k) {
+    unsigned long long acc = 0;
+    for (int f = pq; f < nfb; f += 4)
+      if (active[f]) {
+        const unsigned long long v = sy[so + f * 64 + p];
+        acc += v < best[f] ? v : best[f];
+      }
+    part[pq][p] = acc;
+    __syncthreads();
+    if (t == 0) {
+      int bp = 0;
+      unsigned long long bt = ~0ull;
+      for (int q = 0; q < 64; ++q) {
+        const unsigned long long s = part[0][q] + part[1][q] + part[2][q] + part[3][q];
+        if (s < bt) bt = s, bp = q;
+      }
+      ytab[k] = (uint8_t)bp;
+    }
+    __syncthreads();
+    for (int f = t; f < nfb; f += 256) {
+      const unsigned long long v = sy[so + f * 64 + ytab[k]];
+      if (v < best[f]) best[f] = v;
+    }
+    __syncthreads();
+  }
+  for (int f = t; f < nfb; f += 256) {
+    unsigned long long bv = ~0ull;
+    int a = 0;
+    for (int k = 0; k < kMaxPresets; ++k) {
+      const unsigned long long v = sy[so + f * 64 + ytab[k]];
+      if (v < bv) bv = v, a = k;
+    }
+    asg[f] = (uint8_t)a;
+  }
+  __syncthreads();
+  for (int k = 0; k < kMaxPresets; ++k) {
+    unsigned long long acc = 0;
+    for (int f = pq; f < nfb; f += 4)
+      if (active[f] && asg[f] == k) acc += su[so + f * 64 + p] + sv[so + f * 64 + p];
+    part[pq][p] = acc;
+    __syncthreads();
+    if (t == 0) {
+      int bp = 0;
+      unsigned long long bt = ~0ull;
+      for (int q = 0; q < 64; ++q) {
+        const unsigned long long s = part[0][q] + part[1][q] + part[2][q] + part[3][q];
+        if (s < bt) bt = s, bp = q;
+      }
+      uvtab[k] = (uint8_t)bp;
+    }
+    __syncthreads();
+  }
+  for (int f = t; f < nfb; f += 256) {
+    int bk = -1;
+    if (active[f]) {
+      unsigned long long bv = ~0ull;
+      for (int k = 0; k < kMaxPresets; ++k) {
+        const unsigned long long v = sy[so + f * 64 + ytab[k]] + su[so + f * 64 + uvtab[k]] + sv[so + f * 64 + uvtab[k]];
+        if (v < bv) bv = v, bk = k;
+      }
+    }
+    fbidx[(long)b * nfb + f] = (int8_t)bk;
+    py[(long)b * nfb + f] = bk < 0 ? (int8_t)-1 : (int8_t)ytab[bk];
+    puv[(long)b * nfb + f] = bk < 0 ? (int8_t)-1 : (int8_t)uvtab[bk];
+  }
+  if (t < 8) {
+    tabs[b * 16 + t] = ytab[t];
+    tabs[b * 16 + 8 + t] = uvtab[t];
+  }
+}
+
+// ================================================================= host helpers =========
+thread_local std::string g_err;
+int status(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return -1;
+  }
+  return 0;
+}
+int ensure_tables() {
+  static bool done[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    g_err = "av1e: no device";
+    return -1;
+  }
+  if (done[dev]) return 0;
+  int32_t d16[256], d8[64], a8[64];
+  for (int k = 0; k < 16; ++k)
+    for (int n = 0; n < 16; ++n) d16[k * 16 + n] = tv::av1::txfm_basis(tv::av1::TX_DCT, 16, k, n);
+  for (int k = 0; k < 8; ++k)
+    for (int n = 0; n < 8; ++n) {
+      d8[k * 8 + n] = tv::av1::txfm_basis(tv::av1::TX_DCT, 8, k, n);
+      a8[k * 8 + n] = tv::av1::txfm_basis(tv::av1::TX_ADST, 8, k, n);
+    }
+  if (hipMemcpyToSymbol(HIP_SYMBOL(c_dct16), d16, sizeof(d16)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(c_dct8), d8, sizeof(d8)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(c_adst8), a8, sizeof(a8)) != hipSuccess) {
+    g_err = "av1e: basis upload failed";
+    return -1;
+  }
+  done[dev] = true;
+  return 0;
+}
+bool bad(int W, int H, int B, int qidx, const char* what) {
+  if (W < 16 || H < 16 || (W & 15) || (H & 15) || B < 1 || B > 65535 || qidx < 1 || qidx > 255 || W > 8192 ||
+      H > 8192) {
+    g_err = std::string(what) + ": bad geometry / q-index";
+    return true;
+  }
+  return false;
+}
+
+}  // namespace
+}  // namespace gpu
+}  // namespace tv
+
+using namespace tv::gpu;
+
+extern "C" {
+const char* tv_av1e_last_error() { return g_err.c_str(); }
+
+// P frame of B segments: src / ref / rec planes [B][H][W] (+ chroma [B][H/2][W/2]).
+int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* ry, const uint8_t* ru,
+                  const uint8_t* rv, uint8_t* oy, uint8_t* ou, uint8_t* ov, uint32_t* mode, uint32_t* mv, int16_t* ly,
+                  int16_t* lu, int16_t* lv, int W, int H, int B, int qidx, void* stream) {
+  if (bad(W, H, B, qidx, "av1e_inter") || ensure_tables()) return -1;
+  const int nb = (W >> 4) * (H >> 4);
+  k_av1e_inter<<<dim3(nb, B), 64, 0, (hipStream_t)stream>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv},
+                                                            Planes3W{oy, ou, ov}, mode, mv, ly, lu, lv, W, H, qidx);
+  return status("av1e_inter");
+}
+
+// Key frame of B segments: one launch per anti-diagonal of the 16x16 block grid.
+int tv_av1e_intra(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, uint8_t* oy, uint8_t* ou, uint8_t* ov,
+                  uint32_t* mode, uint32_t* mv, int16_t* ly, int16_t* lu, int16_t* lv, int W, int H, int B, int qidx,
+                  void* stream) {
+  if (bad(W, H, B, qidx, "av1e_intra") || ensure_tables()) return -1;
+  const int bw = W >> 4, bh = H >> 4;
+  for (int d = 0; d < bw + bh - 1; ++d) {
+    const int lo = d - (bh - 1) > 0 ? d - (bh - 1) : 0, hi = d < bw - 1 ? d : bw - 1;
+    k_av1e_intra<<<dim3(hi - lo + 1, B), 64, 0, (hipStream_t)stream>>>(Planes3{sy, su, sv}, Planes3W{oy, ou, ov},
+                                                                       mode, mv, ly, lu, lv, W, H, qidx, d, lo);
+  }
+  return status("av1e_intra");
+}
+
+int tv_av1e_lfinfo(const uint32_t* mode, int W, int H, int B, int lv0, int lv1, int lv2, int lv3, uint32_t* iy,
+                   uint32_t* iu, uint32_t* iv, void* stream) {
+  if (bad(W, H, B, 1, "av1e_lfinfo")) return -1;
+  const int n = (W >> 2) * (H >> 2);
+  k_av1e_lfinfo<<<dim3((n + 255) / 256, B), 256, 0, (hipStream_t)stream>>>(mode, W, H, lv0, lv1, lv2, lv3, iy, iu, iv);
+  return status("av1e_lfinfo");
+}
+
+// sse_* [B][nfb][64]; tabs [B][16] (8 luma + 8 chroma presets); fbidx / py / puv [B][nfb]
+int tv_av1e_cdef_choose(const unsigned long long* sy, const unsigned long long* su, const unsigned long long* sv,
+                        const uint32_t* mode, int W, int H, int B, uint8_t* tabs, int8_t* fbidx, int8_t* py,
+                        int8_t* puv, void* stream) {
+  if (bad(W, H, B, 1, "av1e_cdef_choose")) return -1;
+  if (((W + 63) >> 6) * ((H + 63) >> 6) > kMaxFb) {
+    g_err = "av1e_cdef_choose: frame too large";
+    return -1;
+  }
+  k_av1e_cdef_choose<<<B, 256, 0, (hipStream_t)stream>>>(sy, su, sv, mode, W, H, tabs, fbidx, py, puv);
+  return status("av1e_cdef_choose");
+}
+}

@@ -1,0 +1,290 @@
+// av1_enc.h — AV1 encoder primitives shared (TV_HD) by the C++ golden encoder / decoder
+// oracle (csrc/core/av1_codec.cpp) and the gfx950 encode kernels (csrc/gpu/k_av1_enc.hip),
+// so GPU and CPU reconstructions are identical bit for bit (BASELINE
+// config #4 "4K60 AV1 with CDEF + loop-restoration HIP kernels").
+//
+// Coding structure (a GPU-friendly subset of AV1 Main, 8-bit 4:2:0):
+//   * 64x64 superblocks, coded size padded to a multiple of 16 (render_size = display size);
+//     every superblock splits to 16x16 coding blocks (PARTITION_SPLIT / split_or_* at edges);
+//   * TX_MODE_LARGEST: one 16x16 luma and two 8x8 chroma transforms per block, reduced_tx_set;
+//   * key frames: intra modes DC / V / H / SMOOTH / SMOOTH_V / SMOOTH_H / PAETH (the seven
+//     modes that read no above-right samples: the I-frame wavefront is a plain diagonal);
+//     intra edge filter / filter intra / CfL / palette off;
+//   * inter frames: one reference (LAST = previous frame), quarter-pel motion, EIGHTTAP
+//     (regular) filters; the NEWMV / NEARESTMV / NEARMV / GLOBALMV choice is made by the
+//     syntax writer from the spatial MV stack (the mode does not change the reconstruction);
+//   * deblocking with frame levels, CDEF (8 presets per frame, 64x64 cdef_idx).
+//
+// Tables the AV1 specification defines but that are not available offline (no spec text,
+// libaom or dav1d in the image) are substituted and marked "SUBSTITUTE" below: the q-index
+// lookup, default CDFs (csrc/core/av1_codec.cpp) and the transform rounding (av1_txfm.h).
+// The stream syntax follows AV1 (OBUs, uncompressed header, partition / mode / coefficient
+// symbols and contexts); parity with libaom / dav1d is unpinned.
+#pragma once
+#include <cstdint>
+
+#include "tv/hevc_defs.h"  // TV_HD, clip3, tv_abs
+
+namespace tv {
+namespace av1 {
+
+constexpr int kBlk = 16;   // coding block (luma)
+constexpr int kCBlk = 8;   // chroma block
+constexpr int kSb = 64;    // superblock
+constexpr int kMaxPresets = 8;
+
+// intra modes (AV1 numbering)
+enum : int { DC_PRED = 0, V_PRED = 1, H_PRED = 2, SMOOTH_PRED = 9, SMOOTH_V_PRED = 10, SMOOTH_H_PRED = 11,
+             PAETH_PRED = 12 };
+// inter modes (YModes of inter blocks)
+enum : int { NEARESTMV = 13, NEARMV = 14, GLOBALMV = 15, NEWMV = 16 };
+constexpr int kNumIntraCand = 7;
+TV_HD int intra_cand(int i) {
+  constexpr int8_t m[kNumIntraCand] = {DC_PRED, V_PRED, H_PRED, SMOOTH_PRED, SMOOTH_V_PRED, SMOOTH_H_PRED, PAETH_PRED};
+  return m[i];
+}
+// 1-D transform types (av1_txfm.h: 0 DCT, 1 ADST) of the chroma intra transform
+// (Mode_To_Txfm: V -> ADST_DCT, H -> DCT_ADST, SMOOTH / PAETH -> ADST_ADST, ...): vertical
+// (column) type in bit 0, horizontal (row) type in bit 1.
+TV_HD int uv_txtype(int uv_mode) {
+  switch (uv_mode) {
+    case V_PRED: case SMOOTH_V_PRED: return 1;              // ADST_DCT
+    case H_PRED: case SMOOTH_H_PRED: return 2;              // DCT_ADST
+    case SMOOTH_PRED: case PAETH_PRED: return 3;            // ADST_ADST
+    default: return 0;                                      // DCT_DCT
+  }
+}
+
+// ---------------------------------------------------------------- quantizer ------------
+// SUBSTITUTE for Dc_Qlookup / Ac_Qlookup (8-bit): same end points (4 at qindex 0, AC 1828 /
+// DC 1336 at 255), +1 per index up to 96 as in the spec's linear region, then geometric.
+TV_HD int ac_q(int q) {
+  q = clip3(0, 255, q);
+  if (q == 0) return 4;
+  if (q <= 96) return q + 7;
+  // 103 * 2^((q - 96) / 38.3): integer fixed point so host == device
+  const int e = (q - 96) * 1711;  // (q-96)/38.3 in 1/65536 units
+  const int ip = e >> 16, fp = e & 65535;
+  // 2^f ~ 1 + f (0.6565 + 0.3435 f) on [0, 1)
+  const long long two_f = 65536 + (((long long)fp * (43025 + ((22511LL * fp) >> 16))) >> 16);
+  long long v = (103LL * two_f) << ip;
+  int r = (int)((v + 32768) >> 16);
+  return r > 1828 ? 1828 : r;
+}
+TV_HD int dc_q(int q) {
+  const int a = ac_q(q);
+  return a - (int)(((long long)a * 27 * clip3(0, 255, q)) / (100 * 255));
+}
+// encoder quantisation rounding (1/128 of the step): intra 1/3, inter 1/6 (dead zone)
+constexpr int kRndIntra = 43, kRndInter = 21;
+TV_HD int quant(int c, int q, int rnd) {
+  const int a = c < 0 ? -c : c;
+  const int l = (a + ((q * rnd) >> 7)) / q;
+  return c < 0 ? -l : l;
+}
+// AV1 dequantisation (7.12.3, dqDenom 0 for <= 16x16): |l * q| & 0xFFFFFF, clamp to int16
+TV_HD int dequant(int l, int q) {
+  if (!l) return 0;
+  const long long a = ((long long)(l < 0 ? -l : l) * q) & 0xFFFFFF;
+  const int v = (int)(l < 0 ? -a : a);
+  return clip3(-32768, 32767, v);
+}
+// frame loop-filter level from the AC step (libaom-style linear guess), 0..63
+TV_HD int lf_level_for_q(int q) {
+  const long long v = ((long long)ac_q(q) * 20723 + 1015158) >> 18;
+  return (int)clip3(0LL, 63LL, v);
+}
+// lambda for SAD/SATD-domain decisions (bits -> distortion units, x16)
+TV_HD int lambda16(int q) { return tv_max(16, (ac_q(q) * 16 * 3) / 32); }
+
+// ------------------------------------------------------------------ intra prediction ----
+// Smooth weights (Sm_Weights_Tx_*)
+TV_HD int sm_weight(int N, int i) {
+  constexpr uint8_t w8[8] = {255, 197, 146, 105, 73, 50, 37, 32};
+  constexpr uint8_t w16[16] = {255, 225, 196, 170, 145, 123, 102, 84, 68, 54, 43, 33, 26, 20, 17, 16};
+  return N == 8 ? w8[i] : w16[i];
+}
+
+// Edge samples of an N x N block at (x, y) of a plane (7.11.2 without the intra edge
+// filter): above[0..N-1], left[0..N-1], top-left.  get(x, y) reads reconstructed samples.
+struct IntraEdge {
+  int above[16], left[16], tl;
+  bool have_a, have_l;
+};
+template <class G>
+TV_HD void intra_edges(G get, int x, int y, int N, IntraEdge& e) {
+  e.have_a = y > 0;
+  e.have_l = x > 0;
+  for (int i = 0; i < N; ++i) {
+    if (e.have_a) e.above[i] = get(x + i, y - 1);
+    else if (e.have_l) e.above[i] = get(x - 1, y);
+    else e.above[i] = 127;
+    if (e.have_l) e.left[i] = get(x - 1, y + i);
+    else if (e.have_a) e.left[i] = get(x, y - 1);
+    else e.left[i] = 129;
+  }
+  if (e.have_a && e.have_l) e.tl = get(x - 1, y - 1);
+  else if (e.have_a) e.tl = get(x, y - 1);
+  else if (e.have_l) e.tl = get(x - 1, y);
+  else e.tl = 128;
+}
+
+TV_HD int intra_dc(const IntraEdge& e, int N) {
+  const int lg = N == 8 ? 3 : 4;
+  int s = 0;
+  if (e.have_a && e.have_l) {
+    for (int i = 0; i < N; ++i) s += e.above[i] + e.left[i];
+    return (s + N) >> (lg + 1);
+  }
+  if (e.have_a) {
+    for (int i = 0; i < N; ++i) s += e.above[i];
+    return (s + (N >> 1)) >> lg;
+  }
+  if (e.have_l) {
+    for (int i = 0; i < N; ++i) s += e.left[i];
+    return (s + (N >> 1)) >> lg;
+  }
+  return 128;
+}
+
+// predicted sample (row i, col j); dc = intra_dc(e, N) precomputed for DC_PRED
+TV_HD int intra_pred_px(int mode, const IntraEdge& e, int N, int i, int j, int dc) {
+  switch (mode) {
+    case V_PRED: return e.above[j];
+    case H_PRED: return e.left[i];
+    case SMOOTH_PRED: {
+      const int wy = sm_weight(N, i), wx = sm_weight(N, j);
+      const int s = wy * e.above[j] + (256 - wy) * e.left[N - 1] + wx * e.left[i] + (256 - wx) * e.above[N - 1];
+      return (s + 256) >> 9;
+    }
+    case SMOOTH_V_PRED: {
+      const int wy = sm_weight(N, i);
+      return (wy * e.above[j] + (256 - wy) * e.left[N - 1] + 128) >> 8;
+    }
+    case SMOOTH_H_PRED: {
+      const int wx = sm_weight(N, j);
+      return (wx * e.left[i] + (256 - wx) * e.above[N - 1] + 128) >> 8;
+    }
+    case PAETH_PRED: {
+      const int base = e.above[j] + e.left[i] - e.tl;
+      const int pl = tv_abs(base - e.left[i]), pa = tv_abs(base - e.above[j]), pt = tv_abs(base - e.tl);
+      if (pl <= pa && pl <= pt) return e.left[i];
+      if (pa <= pt) return e.above[j];
+      return e.tl;
+    }
+    default: return dc;
+  }
+}
+
+// ------------------------------------------------------------------ inter prediction ----
+// EIGHTTAP (regular) sub-pixel filters, 1/16 positions.
+TV_HD int subpel_tap(int f, int t) {
+  constexpr int16_t k[16][8] = {
+      {0, 0, 0, 128, 0, 0, 0, 0},      {0, 2, -6, 126, 8, -2, 0, 0},    {0, 2, -10, 122, 18, -4, 0, 0},
+      {0, 2, -12, 116, 28, -8, 2, 0},  {0, 2, -14, 110, 38, -10, 2, 0}, {0, 2, -14, 102, 48, -12, 2, 0},
+      {0, 2, -16, 94, 58, -12, 2, 0},  {0, 2, -14, 84, 66, -12, 2, 0},  {0, 2, -14, 76, 76, -14, 2, 0},
+      {0, 2, -12, 66, 84, -14, 2, 0},  {0, 2, -12, 58, 94, -16, 2, 0},  {0, 2, -12, 48, 102, -14, 2, 0},
+      {0, 2, -10, 38, 110, -14, 2, 0}, {0, 2, -8, 28, 116, -12, 2, 0},  {0, 0, -4, 18, 122, -10, 2, 0},
+      {0, 0, -2, 8, 126, -6, 2, 0}};
+  return k[f][t];
+}
+constexpr int kInterRound0 = 3, kInterRound1 = 11;
+
+// Predicted sample at integer position (x, y) of a block displaced by (ix + fx/16, iy +
+// fy/16); get(x, y) reads the reference with coordinates clamped to the plane (7.11.3.3).
+template <class G>
+TV_HD int inter_pred_px(G get, int x, int y, int fx, int fy) {
+  if (!fx && !fy) return get(x, y);
+  int col[8];
+  for (int r = 0; r < 8; ++r) {
+    int s = 0;
+    for (int t = 0; t < 8; ++t) s += subpel_tap(fx, t) * get(x + t - 3, y + r - 3);
+    col[r] = (s + (1 << (kInterRound0 - 1))) >> kInterRound0;
+  }
+  int s = 0;
+  for (int t = 0; t < 8; ++t) s += subpel_tap(fy, t) * col[t];
+  return clip_pixel((s + (1 << (kInterRound1 - 1))) >> kInterRound1);
+}
+// Motion vectors are (row, col) in 1/8 luma samples, always even (quarter-pel, no hp).
+// Luma: integer mv >> 3, phase (mv & 7) * 2; chroma (4:2:0): integer mv >> 4, phase mv & 15.
+TV_HD int mv_int(int mv, bool chroma) { return chroma ? (mv >> 4) : (mv >> 3); }
+TV_HD int mv_frac(int mv, bool chroma) { return chroma ? (mv & 15) : ((mv & 7) << 1); }
+
+// ------------------------------------------------------------------------- costs --------
+// 4x4 Hadamard SATD of a difference block d[16] (row-major)
+TV_HD int satd4(const int* d) {
+  int m[16];
+  for (int i = 0; i < 4; ++i) {
+    const int a0 = d[i * 4] + d[i * 4 + 3], a1 = d[i * 4 + 1] + d[i * 4 + 2];
+    const int a2 = d[i * 4 + 1] - d[i * 4 + 2], a3 = d[i * 4] - d[i * 4 + 3];
+    m[i * 4] = a0 + a1;
+    m[i * 4 + 1] = a3 + a2;
+    m[i * 4 + 2] = a0 - a1;
+    m[i * 4 + 3] = a3 - a2;
+  }
+  int s = 0;
+  for (int j = 0; j < 4; ++j) {
+    const int a0 = m[j] + m[12 + j], a1 = m[4 + j] + m[8 + j];
+    const int a2 = m[4 + j] - m[8 + j], a3 = m[j] - m[12 + j];
+    s += tv_abs(a0 + a1) + tv_abs(a3 + a2) + tv_abs(a0 - a1) + tv_abs(a3 - a2);
+  }
+  return (s + 1) >> 1;
+}
+// approximate bits of one MV component difference (1/8 units, even)
+TV_HD int mv_comp_bits(int d) {
+  int a = (d < 0 ? -d : d) >> 1;  // quarter-pel units
+  if (!a) return 1;
+  int b = 0;
+  while (a) {
+    ++b;
+    a >>= 1;
+  }
+  return 2 * b + 2;
+}
+// approximate mode bits of the key-frame intra candidates (x16)
+TV_HD int intra_mode_bits16(int m) {
+  switch (m) {
+    case DC_PRED: return 32;
+    case V_PRED: case H_PRED: return 48;
+    case SMOOTH_PRED: return 40;
+    case PAETH_PRED: return 48;
+    default: return 56;
+  }
+}
+
+// ------------------------------------------------------------------ motion search -------
+// Full-pel window of +-kMeRange around the co-located block, then 8 half-pel and 8
+// quarter-pel refinements (SATD + lambda * mv bits, first minimum wins).
+constexpr int kMeRange = 16;
+constexpr int kMeSide = 2 * kMeRange + 1;
+TV_HD int me_cand_dx(int k) { return k % kMeSide - kMeRange; }
+TV_HD int me_cand_dy(int k) { return k / kMeSide - kMeRange; }
+TV_HD int me_ring_dx(int k) { constexpr int8_t t[8] = {-1, 0, 1, -1, 1, -1, 0, 1}; return t[k]; }
+TV_HD int me_ring_dy(int k) { constexpr int8_t t[8] = {-1, -1, -1, 0, 0, 1, 1, 1}; return t[k]; }
+
+// ------------------------------------------------------------------ per-block record ----
+// One 32-bit word per 16x16 block: bit 0 inter, 1-4 y mode, 5-8 uv mode, 9 skip (no
+// nonzero level in any plane), 10-12 nonzero mask (Y, U, V); mv word: row (low 16, signed)
+// and col (high 16).
+TV_HD uint32_t pack_mode(int inter, int ym, int uvm, int skip, int nzmask) {
+  return (uint32_t)(inter & 1) | ((uint32_t)(ym & 15) << 1) | ((uint32_t)(uvm & 15) << 5) |
+         ((uint32_t)(skip & 1) << 9) | ((uint32_t)(nzmask & 7) << 10);
+}
+TV_HD int mode_inter(uint32_t m) { return m & 1; }
+TV_HD int mode_y(uint32_t m) { return (m >> 1) & 15; }
+TV_HD int mode_uv(uint32_t m) { return (m >> 5) & 15; }
+TV_HD int mode_skip(uint32_t m) { return (m >> 9) & 1; }
+TV_HD int mode_nz(uint32_t m) { return (m >> 10) & 7; }
+TV_HD uint32_t pack_mv(int row, int col) { return (uint32_t)(row & 0xFFFF) | ((uint32_t)(col & 0xFFFF) << 16); }
+TV_HD int mv_row(uint32_t v) { return (int)(int16_t)(v & 0xFFFF); }
+TV_HD int mv_col(uint32_t v) { return (int)(int16_t)(v >> 16); }
+
+// deblocking info word for a 4x4 unit (av1_defs.h layout): tx = block = 16 luma / 8 chroma
+TV_HD uint32_t lf_word(bool chroma, int lvl_v, int lvl_h, bool skip_inter) {
+  const uint32_t l = chroma ? 1u : 2u;
+  return l | (l << 3) | (l << 6) | (l << 9) | ((uint32_t)(lvl_v & 63) << 12) | ((uint32_t)(lvl_h & 63) << 18) |
+         ((uint32_t)skip_inter << 24);
+}
+
+}  // namespace av1
+}  // namespace tv

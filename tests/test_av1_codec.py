@@ -1,0 +1,127 @@
+"""AV1 encode path (BASELINE config #4): golden encoder -> OBU stream ->
+decoder oracle round trip, the packed-decision writer used by the GPU engine, IVF, and
+(GPU) the gfx950 engine against the golden encoder bit for bit.  Decoding by libaom /
+dav1d is parity unpinned (neither exists in the image; CDF / q tables are substitutes,
+csrc/include/tv/av1_enc.h)."""
+import numpy as np
+import pytest
+
+from thinvids_amd.models import av1, hevc
+
+
+def _frames(seed, w, h, n, t0=0):
+    out = []
+    for t in range(n):
+        f = hevc.synth_frame(seed, t0 + t, w, h)
+        out.append(tuple(f))
+    return out
+
+
+def _psnr_y(res, frames, w, h):
+    W, H = av1.coded_size(w, h)
+    return [hevc.psnr(f[0], r[:W * H].reshape(H, W)[:h, :w]) for f, r in zip(frames, res.recon)]
+
+
+@pytest.mark.parametrize("w,h,q", [(72, 40, 100), (128, 96, 60), (160, 90, 160)])
+def test_golden_stream_decodes_to_golden_recon(w, h, q):
+    frames = _frames(3, w, h, 4)
+    res = av1.golden_encode(frames, w, h, q)
+    dec = av1.decode(res.stream)
+    assert (dec.width, dec.height) == (w, h)
+    assert dec.frames.shape[0] == 4
+    np.testing.assert_array_equal(dec.frames, res.recon)
+    ps = _psnr_y(res, frames, w, h)
+    assert min(ps) > {60: 40, 100: 36, 160: 30}[q]
+    # inter frames code motion (mode bit 0) and most inter blocks are cheap (skip or small)
+    assert ((res.mode[1:] & 1) == 1).all()
+    assert res.tu_sizes[0] > res.tu_sizes[1]
+
+
+def test_higher_qindex_means_fewer_bits_lower_psnr():
+    w, h = 128, 64
+    frames = _frames(9, w, h, 3)
+    lo, hi = av1.golden_encode(frames, w, h, 50), av1.golden_encode(frames, w, h, 180)
+    assert len(hi.stream) < len(lo.stream)
+    assert np.mean(_psnr_y(hi, frames, w, h)) < np.mean(_psnr_y(lo, frames, w, h))
+
+
+def test_packed_writer_matches_golden_stream():
+    """The GPU engine's entropy path (packed nonzero TBs) writes the same bytes as the
+    golden encoder's writer for the same decisions."""
+    w, h, q = 96, 64, 110
+    frames = _frames(5, w, h, 3)
+    res = av1.golden_encode(frames, w, h, q)
+    tus = av1.split_temporal_units(res.stream, res.tu_sizes)
+    for k in range(3):
+        mode = res.mode[k]
+        packed = []
+        for p, lev in enumerate((res.ly[k], res.lu[k], res.lv[k])):
+            nz = ((mode >> (10 + p)) & 1).astype(bool)
+            packed.append(np.ascontiguousarray(lev[nz]) if nz.any() else np.zeros((1, lev.shape[1]), np.int16))
+        out = av1.write_tu(w, h, res.fparams[k], np.ascontiguousarray(mode), np.ascontiguousarray(res.mv[k]),
+                           packed[0], packed[1], packed[2], np.ascontiguousarray(res.cdef_idx[k]), packed=True,
+                           seq_header=(k == 0))
+        assert out == tus[k]
+
+
+def test_ivf_round_trip():
+    w, h = 64, 48
+    frames = _frames(1, w, h, 2)
+    res = av1.golden_encode(frames, w, h, 90)
+    tus = av1.split_temporal_units(res.stream, res.tu_sizes)
+    ivf = av1.ivf_wrap(tus, w, h, 30, 1)
+    info, back = av1.ivf_unwrap(ivf)
+    assert info["fourcc"] == "AV01" and info["width"] == w and back == tus
+    assert av1.probe(b"".join(back))["frames"] == 2
+
+
+def test_qindex_mapping_monotone():
+    qs = [av1.qindex_for_hevc_qp(qp) for qp in (22, 27, 32, 37)]
+    assert qs == sorted(qs) and len(set(qs)) == 4
+    assert abs(av1.ac_q(255) - 1828) <= 8 and av1.ac_q(0) == 4
+
+
+# ---------------------------------------------------------------------------- GPU -----
+def _gpu_vs_golden(w, h, starts, nframes, q):
+    import torch
+
+    from thinvids_amd.models.av1_engine import Av1GpuEngine
+
+    W, H = av1.coded_size(w, h)
+    segs = [_frames(11, w, h, nframes, t0) for t0 in starts]
+    eng = Av1GpuEngine(w, h, batch=len(starts), qindex=q)
+    dev = eng.dev
+
+    def load(t, planes):
+        for b, fr in enumerate(segs):
+            for c, (dst, x) in enumerate(zip(planes, av1.pad_frame(fr[t], W, H))):
+                dst[b].copy_(torch.from_numpy(np.ascontiguousarray(x)).to(dev))
+
+    g = eng.encode_gop(nframes, load)
+    futs = eng.submit_entropy(g)
+    for b, fr in enumerate(segs):
+        gold = av1.golden_encode(fr, w, h, q)
+        np.testing.assert_array_equal(g.mode[:, b], gold.mode, err_msg=f"segment {b}: mode words")
+        np.testing.assert_array_equal(g.mv[:, b], gold.mv, err_msg=f"segment {b}: motion vectors")
+        np.testing.assert_array_equal(g.tabs[:, b, :8], gold.fparams[:, 9:17])
+        np.testing.assert_array_equal(g.fbidx[:, b], gold.cdef_idx)
+        tus = futs[b].result()
+        assert b"".join(tus) == gold.stream, f"segment {b}: GPU bitstream differs from the golden encoder"
+        last = gold.recon[-1]
+        fy = eng.fin[0][b].cpu().numpy().reshape(-1)
+        np.testing.assert_array_equal(fy, last[:W * H])
+    eng.close()
+    return g, eng
+
+
+@pytest.mark.gpu
+def test_gpu_av1_engine_matches_golden_small():
+    _gpu_vs_golden(200, 120, [0, 7], 4, 100)
+
+
+@pytest.mark.gpu
+def test_gpu_av1_engine_matches_golden_1080p():
+    """Benchmark geometry: 1920x1080 (coded 1088, split_or_horz SB rows), key + P frame."""
+    g, eng = _gpu_vs_golden(1920, 1080, [3], 2, 110)
+    ps = eng.psnr(g)
+    assert ps["y"] > 35

@@ -1,0 +1,231 @@
+"""AV1 codec "model" API (BASELINE config #4): golden encoder, decoder
+oracle, IVF container, and the temporal-unit writer the GPU engine's entropy stage uses.
+
+Coding-tool subset and the tables substituted for the ones the AV1 specification defines
+but this offline image does not hold (default CDFs, q-index lookup, transform rounding):
+``csrc/include/tv/av1_enc.h``.  The stream syntax is AV1's (OBUs, uncompressed header,
+partition / mode / MV / coefficient symbols with the spec's context derivations) and the
+decoder oracle here parses it back bit-exactly; decoding by libaom / dav1d is parity
+unpinned (neither exists in the image).
+
+Reference parity: thinvids rejects AV1 sources (/root/reference/worker/tasks.py:929-939)
+and only emits H.264 (:1532-1586); this is the north-star AV1 path of BASELINE.json.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+
+from .._native import Bytes, core_lib, ptr, u8p
+
+i16p = C.POINTER(C.c_int16)
+u32p = C.POINTER(C.c_uint32)
+i32p = C.POINTER(C.c_int32)
+i64p = C.POINTER(C.c_int64)
+i8p = C.POINTER(C.c_int8)
+vp = C.c_void_p
+
+# mirrored from av1_enc.h
+INTRA_CANDS = (0, 1, 2, 9, 10, 11, 12)
+
+
+def coded_size(width: int, height: int) -> tuple[int, int]:
+    return (width + 15) & ~15, (height + 15) & ~15
+
+
+def _lib():
+    lib = core_lib()
+    if not getattr(lib, "_av1c_sigs", False):
+        i = C.c_int
+        lib.tv_av1c_last_error.restype = C.c_char_p
+        lib.tv_av1c_golden_encode.argtypes = [i, i, i, u8p, i, vp, i64p, u8p, u32p, u32p, i16p, i16p, i16p, i32p,
+                                                i8p]
+        lib.tv_av1c_golden_encode.restype = i
+        lib.tv_av1c_decode.argtypes = [u8p, C.c_size_t, i, u8p, i32p, i32p]
+        lib.tv_av1c_decode.restype = i
+        lib.tv_av1c_write_tu.argtypes = [i, i, i32p, u32p, u32p, i16p, i16p, i16p, i8p, i, i, vp]
+        lib.tv_av1c_write_tu.restype = i
+        lib._av1c_sigs = True
+    return lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise RuntimeError(_lib().tv_av1c_last_error().decode())
+
+
+def ac_q(q: int) -> int:
+    """Substitute AC quantiser step (av1_enc.h ac_q), for rate-control mapping."""
+    q = min(max(q, 0), 255)
+    if q == 0:
+        return 4
+    if q <= 96:
+        return q + 7
+    e = (q - 96) * 1711
+    ip, fp = e >> 16, e & 65535
+    two_f = 65536 + ((fp * (43025 + ((22511 * fp) >> 16))) >> 16)
+    return min(1828, ((103 * two_f << ip) + 32768) >> 16)
+
+
+def qindex_for_hevc_qp(qp: int) -> int:
+    """The q-index whose AC step matches HEVC QP `qp`'s (x8 transform scale): qstep =
+    2^((qp-4)/6) in orthonormal units."""
+    target = 8.0 * 2.0 ** ((qp - 4) / 6.0)
+    return int(min(range(1, 256), key=lambda q: abs(ac_q(q) - target)))
+
+
+@dataclass
+class GoldenResult:
+    stream: bytes
+    tu_sizes: list
+    recon: np.ndarray  # (n, W*H*3/2) uint8, coded size
+    mode: np.ndarray   # (n, nblk) uint32
+    mv: np.ndarray
+    ly: np.ndarray     # (n, nblk, 256) int16
+    lu: np.ndarray
+    lv: np.ndarray
+    fparams: np.ndarray  # (n, 25) int32 (frame_params layout)
+    cdef_idx: np.ndarray  # (n, nsb) int8
+
+
+def pack_i420(frames, W: int, H: int) -> np.ndarray:
+    """[(Y, U, V)] of coded size -> (n, W*H*3/2) uint8."""
+    out = np.empty((len(frames), W * H * 3 // 2), np.uint8)
+    for k, (y, u, v) in enumerate(frames):
+        out[k, :W * H] = y.reshape(-1)
+        out[k, W * H:W * H * 5 // 4] = u.reshape(-1)
+        out[k, W * H * 5 // 4:] = v.reshape(-1)
+    return out
+
+
+def pad_frame(frame, W: int, H: int):
+    """Edge-replicate a display-size (Y, U, V) to the coded size."""
+    y, u, v = frame
+    h, w = y.shape
+    return (np.pad(y, ((0, H - h), (0, W - w)), mode="edge"),
+            np.pad(u, ((0, H // 2 - h // 2), (0, W // 2 - w // 2)), mode="edge"),
+            np.pad(v, ((0, H // 2 - h // 2), (0, W // 2 - w // 2)), mode="edge"))
+
+
+def golden_encode(frames, width: int, height: int, qindex: int) -> GoldenResult:
+    """C++ golden encoder over display-size (Y, U, V) frames (one closed GOP)."""
+    W, H = coded_size(width, height)
+    n = len(frames)
+    yuv = pack_i420([pad_frame(f, W, H) for f in frames], W, H)
+    nb = (W // 16) * (H // 16)
+    out = Bytes()
+    sizes = np.zeros(n, np.int64)
+    recon = np.empty_like(yuv)
+    mode = np.zeros((n, nb), np.uint32)
+    mv = np.zeros((n, nb), np.uint32)
+    ly = np.zeros((n, nb, 256), np.int16)
+    lu = np.zeros((n, nb, 64), np.int16)
+    lv = np.zeros((n, nb, 64), np.int16)
+    fparams = np.zeros((n, 25), np.int32)
+    cdef = np.zeros((n, ((W + 63) // 64) * ((H + 63) // 64)), np.int8)
+    _check(_lib().tv_av1c_golden_encode(width, height, n, ptr(yuv), qindex, out.h, sizes.ctypes.data_as(i64p),
+                                        ptr(recon), mode.ctypes.data_as(u32p), mv.ctypes.data_as(u32p),
+                                        ly.ctypes.data_as(i16p), lu.ctypes.data_as(i16p), lv.ctypes.data_as(i16p),
+                                        fparams.ctypes.data_as(i32p), cdef.ctypes.data_as(i8p)))
+    return GoldenResult(out.tobytes(), sizes.tolist(), recon, mode, mv, ly, lu, lv, fparams, cdef)
+
+
+@dataclass
+class Av1Decoded:
+    width: int
+    height: int
+    W: int
+    H: int
+    frames: np.ndarray  # (n, W*H*3/2) coded size
+
+    def planes(self, k: int, display: bool = True):
+        W, H = self.W, self.H
+        f = self.frames[k]
+        y = f[:W * H].reshape(H, W)
+        u = f[W * H:W * H * 5 // 4].reshape(H // 2, W // 2)
+        v = f[W * H * 5 // 4:].reshape(H // 2, W // 2)
+        if display:
+            return y[:self.height, :self.width], u[:self.height // 2, :self.width // 2], v[:self.height // 2,
+                                                                                             :self.width // 2]
+        return y, u, v
+
+
+def probe(stream: bytes) -> dict:
+    geo = np.zeros(4, np.int32)
+    n = C.c_int32(0)
+    buf = np.frombuffer(stream, np.uint8)
+    _check(_lib().tv_av1c_decode(ptr(buf), len(buf), 0, None, geo.ctypes.data_as(i32p), C.byref(n)))
+    return {"width": int(geo[0]), "height": int(geo[1]), "coded": (int(geo[2]), int(geo[3])), "frames": n.value}
+
+
+def decode(stream: bytes) -> Av1Decoded:
+    """Decoder oracle: parse + reconstruct every frame of a stream of temporal units."""
+    info = probe(stream)
+    W, H = info["coded"]
+    frames = np.empty((info["frames"], W * H * 3 // 2), np.uint8)
+    geo = np.zeros(4, np.int32)
+    n = C.c_int32(0)
+    buf = np.frombuffer(stream, np.uint8)
+    _check(_lib().tv_av1c_decode(ptr(buf), len(buf), info["frames"], ptr(frames), geo.ctypes.data_as(i32p),
+                                 C.byref(n)))
+    return Av1Decoded(info["width"], info["height"], W, H, frames)
+
+
+# cdef / frame parameter vector of tv_av1c_write_tu
+def frame_params(key: bool, qindex: int, lf, sharp: int, damping: int, cdef_y, cdef_uv, cdef_bits: int = 3):
+    p = np.zeros(25, np.int32)
+    p[0], p[1] = int(key), qindex
+    p[2:6] = lf
+    p[6], p[7], p[8] = sharp, damping, cdef_bits
+    p[9:17] = cdef_y
+    p[17:25] = cdef_uv
+    return p
+
+
+def write_tu(width: int, height: int, fparams: np.ndarray, mode: np.ndarray, mv: np.ndarray, ly: np.ndarray,
+             lu: np.ndarray, lv: np.ndarray, cdef_idx: np.ndarray, packed: bool, seq_header: bool,
+             out: Bytes | None = None) -> bytes | None:
+    """One frame's temporal unit from engine decisions (appended to `out` when given)."""
+    o = out if out is not None else Bytes()
+    _check(_lib().tv_av1c_write_tu(width, height, fparams.ctypes.data_as(i32p), mode.ctypes.data_as(u32p),
+                                   mv.ctypes.data_as(u32p), ly.ctypes.data_as(i16p), lu.ctypes.data_as(i16p),
+                                   lv.ctypes.data_as(i16p), cdef_idx.ctypes.data_as(i8p), int(packed),
+                                   int(seq_header), o.h))
+    return None if out is not None else o.tobytes()
+
+
+# ------------------------------------------------------------------------------- IVF ----
+def ivf_header(width: int, height: int, fps_num: int, fps_den: int, nframes: int) -> bytes:
+    return struct.pack("<4sHH4sHHIIII", b"DKIF", 0, 32, b"AV01", width, height, fps_num, fps_den, nframes, 0)
+
+
+def ivf_wrap(tus, width: int, height: int, fps_num: int = 30, fps_den: int = 1) -> bytes:
+    """Temporal units -> an IVF file (the AV1 elementary-stream container of aomenc)."""
+    out = [ivf_header(width, height, fps_num, fps_den, len(tus))]
+    for k, tu in enumerate(tus):
+        out.append(struct.pack("<IQ", len(tu), k))
+        out.append(tu)
+    return b"".join(out)
+
+
+def ivf_unwrap(data: bytes) -> tuple[dict, list]:
+    if data[:4] != b"DKIF":
+        raise ValueError("not an IVF file")
+    _, _, hlen, fourcc, w, h, num, den, n, _ = struct.unpack("<4sHH4sHHIIII", data[:32])
+    pos, tus = hlen, []
+    while pos + 12 <= len(data):
+        sz, _pts = struct.unpack("<IQ", data[pos:pos + 12])
+        tus.append(data[pos + 12:pos + 12 + sz])
+        pos += 12 + sz
+    return {"fourcc": fourcc.decode(), "width": w, "height": h, "fps": (num, den)}, tus
+
+
+def split_temporal_units(stream: bytes, sizes) -> list:
+    out, pos = [], 0
+    for s in sizes:
+        out.append(stream[pos:pos + s])
+        pos += s
+    return out

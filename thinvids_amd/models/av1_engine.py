@@ -1,0 +1,216 @@
+"""GPU AV1 encode engine (BASELINE config #4) for one MI355X.
+
+Encodes a BATCH of B independent GOP-aligned segments in lock-step: frame t of every
+segment is one launch of each kernel (grid = blocks x segments).  Per frame, on the
+current HIP stream:
+
+    key frame   k_av1e_intra (anti-diagonal wavefront of 16x16 blocks)
+    P frame     k_av1e_inter (full-pel +-16 LDS search, quarter-pel refine, recon)
+    both        k_av1e_lfinfo -> k_deblock (Y, U, V) -> k_cdef_dir -> k_cdef_search
+                (Y, U, V) -> k_av1e_cdef_choose -> k_cdef_apply -> next reference
+
+Decisions (mode / MV words, quantised levels, CDEF tables and indices) of the whole GOP
+stay resident in HBM; at the end of the GOP the nonzero transform blocks are compacted on
+the device and copied to the host once, and a CPU thread pool writes every segment's OBU
+temporal units (range coder) while the GPU moves on to the next GOP.
+
+Bit-exact with the C++ golden encoder (``av1.golden_encode``) and decodable by the
+decoder oracle (``av1.decode``): tests/test_av1_codec.py.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import av1 as av1m
+
+_vp = C.c_void_p
+
+
+def _gpu():
+    from .._native import gpu_lib
+
+    lib = gpu_lib()
+    if not getattr(lib, "_av1e_sigs", False):
+        for n in ("tv_av1e_inter", "tv_av1e_intra", "tv_av1e_lfinfo", "tv_av1e_cdef_choose"):
+            getattr(lib, n).restype = C.c_int
+        lib.tv_av1e_last_error.restype = C.c_char_p
+        lib._av1e_sigs = True
+    return lib
+
+
+def _ok(rc: int):
+    if rc != 0:
+        raise RuntimeError(_gpu().tv_av1e_last_error().decode())
+
+
+def _p(t):
+    return _vp(t.data_ptr())
+
+
+@dataclass
+class GopHost:
+    """Host copy of one GOP's decisions for the entropy stage."""
+    nframes: int
+    mode: np.ndarray     # (F, B, nb) uint32
+    mv: np.ndarray
+    tabs: np.ndarray     # (F, B, 16) uint8
+    fbidx: np.ndarray    # (F, B, nfb) int8
+    packed: list         # per plane: (levels (K, n) int16, offsets (F, B) int64)
+    sse: np.ndarray      # (F, B, 3) int64
+    key: list            # per frame
+
+
+class Av1GpuEngine:
+    """B segments x one GOP per call on one GPU; see module docstring."""
+
+    def __init__(self, width: int, height: int, batch: int, qindex: int = 100, device: int = 0,
+                 threads: int | None = None):
+        import torch
+
+        self.torch = torch
+        self.w, self.h, self.B, self.q = width, height, batch, int(qindex)
+        self.W, self.H = av1m.coded_size(width, height)
+        self.dev = torch.device("cuda", device)
+        self.nb = (self.W // 16) * (self.H // 16)
+        self.nfb = ((self.W + 63) // 64) * ((self.H + 63) // 64)
+        self.lvl = self._lf_level()
+        self.damping = 3 + (self.q >> 6)
+        B, H, W = batch, self.H, self.W
+        u8 = dict(dtype=torch.uint8, device=self.dev)
+        mk = lambda: (torch.zeros((B, H, W), **u8), torch.zeros((B, H // 2, W // 2), **u8),
+                      torch.zeros((B, H // 2, W // 2), **u8))
+        self.src, self.rec, self.fin = mk(), mk(), mk()
+        self.pool = cf.ThreadPoolExecutor(max_workers=threads or min(32, os.cpu_count() or 8))
+        self._gop_cap = 0
+
+    def _lf_level(self) -> int:
+        return min(63, max(0, (av1m.ac_q(self.q) * 20723 + 1015158) >> 18))
+
+    def _alloc_gop(self, F: int):
+        torch = self.torch
+        if F <= self._gop_cap:
+            return
+        B, nb, nfb = self.B, self.nb, self.nfb
+        d = self.dev
+        self.g_mode = torch.zeros((F, B, nb), dtype=torch.int32, device=d)
+        self.g_mv = torch.zeros((F, B, nb), dtype=torch.int32, device=d)
+        self.g_ly = torch.zeros((F, B, nb, 256), dtype=torch.int16, device=d)
+        self.g_lu = torch.zeros((F, B, nb, 64), dtype=torch.int16, device=d)
+        self.g_lv = torch.zeros((F, B, nb, 64), dtype=torch.int16, device=d)
+        self.g_tabs = torch.zeros((F, B, 16), dtype=torch.uint8, device=d)
+        self.g_fbidx = torch.zeros((F, B, nfb), dtype=torch.int8, device=d)
+        self.g_sse = torch.zeros((F, B, 3), dtype=torch.int64, device=d)
+        self._gop_cap = F
+
+    # ------------------------------------------------------------------ one frame ----
+    def _frame(self, t: int, key: bool):
+        from ..ops import av1 as ops
+
+        torch = self.torch
+        lib = _gpu()
+        st = _vp(torch.cuda.current_stream(self.dev).cuda_stream)
+        W, H, B, q = self.W, self.H, self.B, self.q
+        sy, su, sv = self.src
+        ry, ru, rv = self.rec
+        fy, fu, fv = self.fin
+        mode, mv = self.g_mode[t], self.g_mv[t]
+        ly, lu, lv = self.g_ly[t], self.g_lu[t], self.g_lv[t]
+        if key:
+            _ok(lib.tv_av1e_intra(_p(sy), _p(su), _p(sv), _p(ry), _p(ru), _p(rv), _p(mode), _p(mv), _p(ly), _p(lu),
+                                  _p(lv), W, H, B, q, st))
+        else:
+            _ok(lib.tv_av1e_inter(_p(sy), _p(su), _p(sv), _p(fy), _p(fu), _p(fv), _p(ry), _p(ru), _p(rv), _p(mode),
+                                  _p(mv), _p(ly), _p(lu), _p(lv), W, H, B, q, st))
+        iy = torch.empty((B, H // 4, W // 4), dtype=torch.int32, device=self.dev)
+        iu = torch.empty((B, H // 8, W // 8), dtype=torch.int32, device=self.dev)
+        iv = torch.empty_like(iu)
+        L = self.lvl
+        _ok(lib.tv_av1e_lfinfo(_p(mode), W, H, B, L, L, L, L, _p(iy), _p(iu), _p(iv), st))
+        dy = ops.deblock(ry, iy, False, 0)
+        du = ops.deblock(ru, iu, True, 0)
+        dv = ops.deblock(rv, iv, True, 0)
+        dirs, var = ops.cdef_dirs(dy)
+        se_y = ops.cdef_search(sy, dy, dirs, var, False, self.damping)
+        se_u = ops.cdef_search(su, du, dirs, var, True, self.damping, luma_w8=W // 8)
+        se_v = ops.cdef_search(sv, dv, dirs, var, True, self.damping, luma_w8=W // 8)
+        py = torch.empty((B, self.nfb), dtype=torch.int8, device=self.dev)
+        puv = torch.empty_like(py)
+        _ok(lib.tv_av1e_cdef_choose(_p(se_y), _p(se_u), _p(se_v), _p(mode), W, H, B, _p(self.g_tabs[t]),
+                                    _p(self.g_fbidx[t]), _p(py), _p(puv), st))
+        self.fin = (ops.cdef_apply(dy, dirs, var, py, False, self.damping),
+                    ops.cdef_apply(du, dirs, var, puv, True, self.damping, luma_w8=W // 8),
+                    ops.cdef_apply(dv, dirs, var, puv, True, self.damping, luma_w8=W // 8))
+        w, h = self.w, self.h
+        for c, (s, f) in enumerate(zip(self.src, self.fin)):
+            ss = (slice(None), slice(0, h >> (c > 0)), slice(0, w >> (c > 0)))
+            d = s[ss].to(torch.int32) - f[ss].to(torch.int32)
+            self.g_sse[t, :, c] = (d * d).sum(dim=(1, 2))
+
+    def encode_gop(self, nframes: int, load_frame) -> GopHost:
+        """Run the GPU part of one GOP for all B segments.  load_frame(t, (Y, U, V)) fills
+        the coded-size source planes [B, H, W] of frame t (device tensors).  Returns the
+        host copy of the decisions (one device->host transfer of compacted levels)."""
+        torch = self.torch
+        self._alloc_gop(nframes)
+        for t in range(nframes):
+            load_frame(t, self.src)
+            self._frame(t, t == 0)
+        F = nframes
+        mode = self.g_mode[:F]
+        packed = []
+        for p, lev in enumerate((self.g_ly[:F], self.g_lu[:F], self.g_lv[:F])):
+            nz = ((mode >> (10 + p)) & 1).bool()
+            counts = nz.sum(dim=2)
+            packed.append((lev[nz], counts))
+        host = GopHost(
+            nframes=F,
+            mode=mode.cpu().numpy().view(np.uint32),
+            mv=self.g_mv[:F].cpu().numpy().view(np.uint32),
+            tabs=self.g_tabs[:F].cpu().numpy(),
+            fbidx=self.g_fbidx[:F].cpu().numpy(),
+            packed=[],
+            sse=self.g_sse[:F].cpu().numpy(),
+            key=[t == 0 for t in range(F)],
+        )
+        for lev, counts in packed:
+            c = counts.cpu().numpy().astype(np.int64).reshape(-1)
+            off = np.concatenate([[0], np.cumsum(c)])[:-1].reshape(F, self.B)
+            host.packed.append((lev.cpu().numpy(), off))
+        return host
+
+    # ------------------------------------------------------------------ entropy ------
+    def write_segment(self, g: GopHost, b: int) -> list:
+        """Temporal units of segment b of a GOP (runs on a pool thread; the native writer
+        releases the GIL)."""
+        tus = []
+        for t in range(g.nframes):
+            tabs = g.tabs[t, b]
+            fp = av1m.frame_params(g.key[t], self.q, [self.lvl] * 4, 0, self.damping, tabs[:8], tabs[8:])
+            lev = [np.ascontiguousarray(pk[0][pk[1][t, b]:]) if len(pk[0]) else np.zeros((1, n), np.int16)
+                   for pk, n in zip(g.packed, (256, 64, 64))]
+            tus.append(av1m.write_tu(self.w, self.h, fp, np.ascontiguousarray(g.mode[t, b]),
+                                     np.ascontiguousarray(g.mv[t, b]), lev[0], lev[1], lev[2],
+                                     np.ascontiguousarray(g.fbidx[t, b]), packed=True, seq_header=g.key[t]))
+        return tus
+
+    def submit_entropy(self, g: GopHost) -> list:
+        return [self.pool.submit(self.write_segment, g, b) for b in range(self.B)]
+
+    def psnr(self, g: GopHost) -> dict:
+        n = g.sse.shape[0] * g.sse.shape[1]
+        px = [self.w * self.h, (self.w // 2) * (self.h // 2), (self.w // 2) * (self.h // 2)]
+        out = {}
+        for c, k in enumerate("yuv"):
+            mse = g.sse[:, :, c].sum() / (n * px[c])
+            out[k] = float("inf") if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse))
+        mse = g.sse.sum() / (n * sum(px))
+        out["yuv"] = float("inf") if mse == 0 else float(10 * np.log10(255.0 ** 2 / mse))
+        return out
+
+    def close(self):
+        self.pool.shutdown(wait=True)
