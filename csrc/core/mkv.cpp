@@ -144,8 +144,8 @@ uint64_t write_mkv(const MuxPlan& P, int width, int height, int fps_num, int fps
     e.uint(kFlagLacing, 0);
     e.uint(kDefaultDuration, (uint64_t)std::llround(1e9 * fps_den / fps_num));
     e.str(kLanguage, "und");
-    e.str(kCodecID, "V_MPEGH/ISO/HEVC");
-    const auto hv = hvcc_record(P);
+    e.str(kCodecID, P.codec == MUX_AV1 ? "V_AV1" : "V_MPEGH/ISO/HEVC");
+    const auto hv = P.codec == MUX_AV1 ? P.av1c : hvcc_record(P);
     e.bin(kCodecPrivate, hv.data(), hv.size());
     v.uint(kPixelWidth, (uint64_t)width);
     v.uint(kPixelHeight, (uint64_t)height);

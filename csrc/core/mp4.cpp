@@ -301,7 +301,75 @@ std::vector<uint8_t> trak_box(const TrakInfo& I, const TrakTables& T, bool large
 
 namespace muxi {
 
+bool is_av1_stream(const uint8_t* p, size_t n) { return n >= 2 && p[0] == 0x12 && p[1] == 0x00; }
+
+namespace {
+size_t leb128(const uint8_t* p, size_t n, size_t& pos) {
+  size_t v = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (pos >= n) throw std::runtime_error("mux: truncated AV1 OBU size");
+    const uint8_t b = p[pos++];
+    v |= (size_t)(b & 0x7f) << (7 * i);
+    if (!(b & 0x80)) return v;
+  }
+  throw std::runtime_error("mux: bad AV1 OBU size");
+}
+MuxPlan plan_mux_av1(const uint8_t* const* segs, const size_t* sizes, int nseg) {
+  MuxPlan P;
+  P.codec = MUX_AV1;
+  std::vector<uint8_t> seqhdr;
+  for (int k = 0; k < nseg; ++k) {
+    const uint8_t* p = segs[k];
+    const size_t n = sizes[k];
+    size_t pos = 0;
+    Sample* cur = nullptr;
+    bool seen_frame = false;
+    while (pos < n) {
+      const size_t start = pos;
+      const uint8_t h = p[pos++];
+      const int type = (h >> 3) & 15;
+      if (h & 4) ++pos;  // extension header
+      if (!(h & 2)) throw std::runtime_error("mux: AV1 OBU without a size field");
+      const size_t sz = leb128(p, n, pos);
+      if (pos + sz > n) throw std::runtime_error("mux: truncated AV1 OBU");
+      const size_t end = pos + sz;
+      if (type == 2) {  // temporal delimiter: a new sample starts after it
+        P.samples.emplace_back();
+        cur = &P.samples.back();
+        cur->raw = true;
+        seen_frame = false;
+        pos = end;
+        continue;
+      }
+      if (!cur) throw std::runtime_error("mux: AV1 stream does not start with a temporal delimiter");
+      if (type == 1 && seqhdr.empty()) seqhdr.assign(p + start, p + end);
+      if ((type == 6 || type == 3) && sz > 0 && !seen_frame) {  // first frame header of the TU
+        seen_frame = true;
+        cur->sync = !(p[pos] >> 7) && ((p[pos] >> 5) & 3) == 0;  // not show_existing, KEY_FRAME
+      }
+      if (!cur->nals.empty() && cur->nals.back().data + cur->nals.back().size == p + start)
+        cur->nals.back().size += end - start;  // contiguous OBUs stay one view
+      else
+        cur->nals.push_back(NalView{p + start, end - start});
+      pos = end;
+    }
+  }
+  if (seqhdr.empty()) throw std::runtime_error("mux: AV1 stream without a sequence header");
+  // AV1CodecConfigurationRecord: marker/version, profile/level, tier + colour flags (8-bit
+  // 4:2:0, chroma_sample_position 0: the encoder's sequence header), no presentation delay
+  P.av1c = {0x81, (uint8_t)((0 << 5) | 31), 0x0C, 0x00};
+  P.av1c.insert(P.av1c.end(), seqhdr.begin(), seqhdr.end());
+  for (auto& s : P.samples) {
+    s.size = 0;
+    for (const auto& v : s.nals) s.size += (uint32_t)v.size;
+    P.mdat_payload += s.size;
+  }
+  return P;
+}
+}  // namespace
+
 MuxPlan plan_mux(const uint8_t* const* segs, const size_t* sizes, int nseg) {
+  if (nseg > 0 && is_av1_stream(segs[0], sizes[0])) return plan_mux_av1(segs, sizes, nseg);
   MuxPlan P;
   std::vector<NalView> pending_ps;
   for (int k = 0; k < nseg; ++k) {
@@ -403,14 +471,19 @@ uint64_t write_mp4(const MuxPlan& P, int width, int height, int fps_num, int fps
     se.u32(0);
     se.u16(1);
     char name[32] = {0};
-    const char* nm = "thinvids-amd HEVC";
+    const char* nm = P.codec == muxi::MUX_AV1 ? "thinvids-amd AV1" : "thinvids-amd HEVC";
     name[0] = (char)std::strlen(nm);
     std::memcpy(name + 1, nm, std::strlen(nm));
     se.str(name, 32);
     se.u16(0x0018);
     se.u16(0xffff);
-    se.bytes(box("hvcC", muxi::hvcc_record(P)));
-    I[0].entry = box(P.ps_consistent ? "hvc1" : "hev1", se.b);
+    if (P.codec == muxi::MUX_AV1) {
+      se.bytes(box("av1C", P.av1c));
+      I[0].entry = box("av01", se.b);
+    } else {
+      se.bytes(box("hvcC", muxi::hvcc_record(P)));
+      I[0].entry = box(P.ps_consistent ? "hvc1" : "hev1", se.b);
+    }
   }
   // ---- side tracks
   bool first_audio = true;
@@ -511,7 +584,7 @@ uint64_t write_mp4(const MuxPlan& P, int width, int height, int fps_num, int fps
   Box ftyp;
   ftyp.str("isom", 4);
   ftyp.u32(512);
-  ftyp.str("isomiso2hvc1mp41", 16);
+  ftyp.str(P.codec == muxi::MUX_AV1 ? "isomiso2av01mp41" : "isomiso2hvc1mp41", 16);
   const auto ftyp_box = box("ftyp", ftyp.b);
   const uint64_t mdat_hdr = large ? 16 : 8;
   const size_t moov_size = build_moov(0).size();  // offsets do not change the size

@@ -18,19 +18,28 @@ namespace muxi {
 // change between segments) — the payload is never copied until it is written.
 struct Sample {
   std::vector<NalView> nals;
-  uint32_t size = 0;  // length-prefixed bytes
+  uint32_t size = 0;  // length-prefixed bytes (HEVC) / raw OBU bytes (AV1)
   bool sync = false;
+  bool raw = false;   // AV1: the single view is the temporal unit's OBUs, written as is
 };
 
+enum MuxCodec : int { MUX_HEVC = 0, MUX_AV1 = 1 };
+
 struct MuxPlan {
+  int codec = MUX_HEVC;
   std::vector<uint8_t> vps, sps, pps;
+  std::vector<uint8_t> av1c;  // AV1CodecConfigurationRecord (AV1 only)
   bool ps_consistent = true;
   std::vector<Sample> samples;
   uint64_t mdat_payload = 0;
 };
 
-// Scan the Annex-B segments (in order) into samples; no payload bytes are copied.
+// Scan the segments (in order) into samples; no payload bytes are copied.  Annex-B HEVC,
+// or AV1 low-overhead OBU streams (detected by a leading temporal delimiter OBU): one
+// sample per temporal unit without its temporal delimiter (AV1-ISOBMFF 2.4), the first
+// sequence header OBU copied into the av1C record.
 MuxPlan plan_mux(const uint8_t* const* segs, const size_t* sizes, int nseg);
+bool is_av1_stream(const uint8_t* p, size_t n);
 
 // HEVCDecoderConfigurationRecord (ISO/IEC 14496-15 8.3.3.1) from the parameter sets; the
 // payload of MP4's 'hvcC' box and Matroska's V_MPEGH/ISO/HEVC CodecPrivate.
@@ -45,6 +54,10 @@ inline void put_be32(uint8_t* p, uint32_t v) {
 
 // Append video sample `s` (4-byte length-prefixed NAL units) to `out`.
 inline void append_sample(const Sample& s, std::vector<uint8_t>& out) {
+  if (s.raw) {
+    for (const auto& v : s.nals) out.insert(out.end(), v.data, v.data + v.size);
+    return;
+  }
   for (const auto& nal : s.nals) {
     uint8_t len[4];
     put_be32(len, (uint32_t)nal.size);

@@ -133,7 +133,7 @@ struct Planes3W {
 __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Planes3W rec, uint32_t* __restrict__ mode,
                                                    uint32_t* __restrict__ mvout, int16_t* __restrict__ ly,
                                                    int16_t* __restrict__ lu, int16_t* __restrict__ lv, int W, int H,
-                                                   int qidx) {
+                                                   const int* __restrict__ qarr) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kWinN * kWinP + 8];
   __shared__ __attribute__((aligned(16))) uint8_t sblk[256];
   __shared__ int cost[9];
@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   __shared__ int predc[256];
   int blk, b;
   xcd_ctb(blk, b);
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x, qidx = qarr[b];
   const int bw = W >> 4, bx = blk % bw, by = blk / bw, x0 = bx * 16, y0 = by * 16;
   const long ysz = (long)W * H, csz = ysz >> 2;
   const uint8_t* S = src.y + b * ysz;
@@ -309,14 +309,14 @@ __device__ void load_edges(const uint8_t* P, int w, int x, int y, int N, EdgeLds
 __global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, uint32_t* __restrict__ mode,
                                                    uint32_t* __restrict__ mvout, int16_t* __restrict__ ly,
                                                    int16_t* __restrict__ lu, int16_t* __restrict__ lv, int W, int H,
-                                                   int qidx, int diag, int bx_lo) {
+                                                   const int* __restrict__ qarr, int diag, int bx_lo) {
   __shared__ EdgeLds E[2];
   __shared__ uint8_t sblk[256];
   __shared__ uint8_t sc[2][64];
   __shared__ int cost[8];
   __shared__ int16_t res[256], ta[256], tb[256];
   __shared__ int predc[256];
-  const int lane = threadIdx.x, b = blockIdx.y;
+  const int lane = threadIdx.x, b = blockIdx.y, qidx = qarr[b];
   const int bw = W >> 4, bx = bx_lo + blockIdx.x, by = diag - bx, x0 = bx * 16, y0 = by * 16;
   const long ysz = (long)W * H, csz = ysz >> 2;
   const int lam = lambda16(qidx), Wc = W >> 1, cx0 = bx * 8, cy0 = by * 8;
@@ -403,9 +403,9 @@ __global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, ui
 }
 
 // ================================================================= loop-filter info ======
-__global__ void k_av1e_lfinfo(const uint32_t* __restrict__ mode, int W, int H, int lv0, int lv1, int lv2, int lv3,
+__global__ void k_av1e_lfinfo(const uint32_t* __restrict__ mode, int W, int H, const int* __restrict__ lvl,
                               uint32_t* __restrict__ iy, uint32_t* __restrict__ iu, uint32_t* __restrict__ iv) {
-  const int b = blockIdx.y, w4 = W >> 2, h4 = H >> 2, bw = W >> 4, nb = bw * (H >> 4);
+  const int b = blockIdx.y, lv0 = lvl[4 * b], lv1 = lvl[4 * b + 1], lv2 = lvl[4 * b + 2], lv3 = lvl[4 * b + 3], w4 = W >> 2, h4 = H >> 2, bw = W >> 4, nb = bw * (H >> 4);
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= w4 * h4) return;
   const int x = u % w4, y = u / w4;
@@ -568,36 +568,38 @@ using namespace tv::gpu;
 extern "C" {
 const char* tv_av1e_last_error() { return g_err.c_str(); }
 
-// P frame of B segments: src / ref / rec planes [B][H][W] (+ chroma [B][H/2][W/2]).
+// P frame of B segments: src / ref / rec planes [B][H][W] (+ chroma [B][H/2][W/2]); qarr:
+// device q-index per segment (1..255, range-checked by the host engine).
 int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* ry, const uint8_t* ru,
                   const uint8_t* rv, uint8_t* oy, uint8_t* ou, uint8_t* ov, uint32_t* mode, uint32_t* mv, int16_t* ly,
-                  int16_t* lu, int16_t* lv, int W, int H, int B, int qidx, void* stream) {
-  if (bad(W, H, B, qidx, "av1e_inter") || ensure_tables()) return -1;
+                  int16_t* lu, int16_t* lv, int W, int H, int B, const int* qarr, void* stream) {
+  if (bad(W, H, B, 1, "av1e_inter") || ensure_tables()) return -1;
   const int nb = (W >> 4) * (H >> 4);
   k_av1e_inter<<<dim3(nb, B), 64, 0, (hipStream_t)stream>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv},
-                                                            Planes3W{oy, ou, ov}, mode, mv, ly, lu, lv, W, H, qidx);
+                                                            Planes3W{oy, ou, ov}, mode, mv, ly, lu, lv, W, H, qarr);
   return status("av1e_inter");
 }
 
 // Key frame of B segments: one launch per anti-diagonal of the 16x16 block grid.
 int tv_av1e_intra(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, uint8_t* oy, uint8_t* ou, uint8_t* ov,
-                  uint32_t* mode, uint32_t* mv, int16_t* ly, int16_t* lu, int16_t* lv, int W, int H, int B, int qidx,
-                  void* stream) {
-  if (bad(W, H, B, qidx, "av1e_intra") || ensure_tables()) return -1;
+                  uint32_t* mode, uint32_t* mv, int16_t* ly, int16_t* lu, int16_t* lv, int W, int H, int B,
+                  const int* qarr, void* stream) {
+  if (bad(W, H, B, 1, "av1e_intra") || ensure_tables()) return -1;
   const int bw = W >> 4, bh = H >> 4;
   for (int d = 0; d < bw + bh - 1; ++d) {
     const int lo = d - (bh - 1) > 0 ? d - (bh - 1) : 0, hi = d < bw - 1 ? d : bw - 1;
     k_av1e_intra<<<dim3(hi - lo + 1, B), 64, 0, (hipStream_t)stream>>>(Planes3{sy, su, sv}, Planes3W{oy, ou, ov},
-                                                                       mode, mv, ly, lu, lv, W, H, qidx, d, lo);
+                                                                       mode, mv, ly, lu, lv, W, H, qarr, d, lo);
   }
   return status("av1e_intra");
 }
 
-int tv_av1e_lfinfo(const uint32_t* mode, int W, int H, int B, int lv0, int lv1, int lv2, int lv3, uint32_t* iy,
-                   uint32_t* iu, uint32_t* iv, void* stream) {
+// lvl: [B][4] loop_filter_level[0..3] per segment
+int tv_av1e_lfinfo(const uint32_t* mode, int W, int H, int B, const int* lvl, uint32_t* iy, uint32_t* iu,
+                   uint32_t* iv, void* stream) {
   if (bad(W, H, B, 1, "av1e_lfinfo")) return -1;
   const int n = (W >> 2) * (H >> 2);
-  k_av1e_lfinfo<<<dim3((n + 255) / 256, B), 256, 0, (hipStream_t)stream>>>(mode, W, H, lv0, lv1, lv2, lv3, iy, iu, iv);
+  k_av1e_lfinfo<<<dim3((n + 255) / 256, B), 256, 0, (hipStream_t)stream>>>(mode, W, H, lvl, iy, iu, iv);
   return status("av1e_lfinfo");
 }
 

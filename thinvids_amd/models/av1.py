@@ -70,11 +70,17 @@ def ac_q(q: int) -> int:
     return min(1828, ((103 * two_f << ip) + 32768) >> 16)
 
 
+_QP_TO_QINDEX: dict = {}
+
+
 def qindex_for_hevc_qp(qp: int) -> int:
     """The q-index whose AC step matches HEVC QP `qp`'s (x8 transform scale): qstep =
     2^((qp-4)/6) in orthonormal units."""
-    target = 8.0 * 2.0 ** ((qp - 4) / 6.0)
-    return int(min(range(1, 256), key=lambda q: abs(ac_q(q) - target)))
+    qp = int(qp)
+    if qp not in _QP_TO_QINDEX:
+        target = 8.0 * 2.0 ** ((qp - 4) / 6.0)
+        _QP_TO_QINDEX[qp] = int(min(range(1, 256), key=lambda q: abs(ac_q(q) - target)))
+    return _QP_TO_QINDEX[qp]
 
 
 @dataclass
@@ -229,3 +235,101 @@ def split_temporal_units(stream: bytes, sizes) -> list:
         out.append(stream[pos:pos + s])
         pos += s
     return out
+
+
+# ------------------------------------------------------------------------------- MP4 ----
+TD_OBU = b"\x12\x00"  # temporal delimiter OBU (stripped from ISO-BMFF samples)
+
+
+def _boxes(data: bytes, start: int, end: int):
+    pos = start
+    while pos + 8 <= end:
+        size, typ = struct.unpack(">I4s", data[pos:pos + 8])
+        hdr = 8
+        if size == 1:
+            size = struct.unpack(">Q", data[pos + 8:pos + 16])[0]
+            hdr = 16
+        elif size == 0:
+            size = end - pos
+        if size < hdr:
+            raise ValueError("mp4: bad box size")
+        yield typ.decode("latin-1"), pos + hdr, pos + size
+        pos += size
+
+
+def mp4_av1_track(data: bytes) -> dict | None:
+    """The 'av01' video track of an MP4 (our muxer's output): geometry, timing and the
+    sample (offset, size, sync) table; None when the file has no AV1 track."""
+    def find(path, start, end):
+        for t, a, b in _boxes(data, start, end):
+            if t == path[0]:
+                return (a, b) if len(path) == 1 else find(path[1:], a, b)
+        return None
+
+    moov = find(["moov"], 0, len(data))
+    if not moov:
+        return None
+    for t, a, b in _boxes(data, *moov):
+        if t != "trak":
+            continue
+        stbl = find(["mdia", "minf", "stbl"], a, b)
+        mdhd = find(["mdia", "mdhd"], a, b)
+        if not stbl or not mdhd:
+            continue
+        boxes = {t2: (a2, b2) for t2, a2, b2 in _boxes(data, *stbl)}
+        sa, sb = boxes["stsd"]
+        entry = data[sa + 8:sa + 16]
+        if entry[4:8] != b"av01":
+            continue
+        ea = sa + 8
+        width, height = struct.unpack(">HH", data[ea + 8 + 24:ea + 8 + 28])
+        ver = data[mdhd[0]]
+        timescale = struct.unpack(">I", data[mdhd[0] + (20 if ver == 1 else 12):][:4])[0]
+        a2 = boxes["stts"][0]
+        delta = struct.unpack(">I", data[a2 + 12:a2 + 16])[0] if struct.unpack(">I", data[a2 + 4:a2 + 8])[0] else 0
+        a2 = boxes["stsz"][0]
+        fixed, count = struct.unpack(">II", data[a2 + 4:a2 + 12])
+        sizes = [fixed] * count if fixed else list(struct.unpack(f">{count}I", data[a2 + 12:a2 + 12 + 4 * count]))
+        if "stco" in boxes:
+            a2 = boxes["stco"][0]
+            n = struct.unpack(">I", data[a2 + 4:a2 + 8])[0]
+            chunk_off = struct.unpack(f">{n}I", data[a2 + 8:a2 + 8 + 4 * n])
+        else:
+            a2 = boxes["co64"][0]
+            n = struct.unpack(">I", data[a2 + 4:a2 + 8])[0]
+            chunk_off = struct.unpack(f">{n}Q", data[a2 + 8:a2 + 8 + 8 * n])
+        a2 = boxes["stsc"][0]
+        n = struct.unpack(">I", data[a2 + 4:a2 + 8])[0]
+        stsc = [struct.unpack(">III", data[a2 + 8 + 12 * i:a2 + 20 + 12 * i]) for i in range(n)]
+        offsets, k = [], 0
+        for ci, co in enumerate(chunk_off):
+            spc = next(e[1] for e in reversed(stsc) if e[0] <= ci + 1)
+            o = co
+            for _ in range(spc):
+                if k >= count:
+                    break
+                offsets.append(o)
+                o += sizes[k]
+                k += 1
+        sync = set(range(1, count + 1))
+        if "stss" in boxes:
+            a2 = boxes["stss"][0]
+            n = struct.unpack(">I", data[a2 + 4:a2 + 8])[0]
+            sync = set(struct.unpack(f">{n}I", data[a2 + 8:a2 + 8 + 4 * n]))
+        return {"width": width, "height": height, "timescale": timescale, "delta": delta,
+                "samples": [(o, z, (i + 1) in sync) for i, (o, z) in enumerate(zip(offsets, sizes))]}
+    return None
+
+
+def mp4_av1_stream(data: bytes, first: int = 0, count: int = -1) -> tuple[dict, bytes]:
+    """Temporal units [first, first + count) of an AV1 MP4 back as a decodable OBU stream
+    (temporal delimiters restored), starting from the preceding key frame."""
+    tr = mp4_av1_track(data)
+    if tr is None:
+        raise ValueError("mp4: no AV1 track")
+    smp = tr["samples"]
+    end = len(smp) if count < 0 else min(len(smp), first + count)
+    k = first
+    while k > 0 and not smp[k][2]:
+        k -= 1
+    return tr, b"".join(TD_OBU + data[o:o + z] for o, z, _ in smp[k:end])

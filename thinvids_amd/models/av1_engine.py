@@ -52,6 +52,11 @@ def _p(t):
     return _vp(t.data_ptr())
 
 
+def lf_level(q: int) -> int:
+    """Frame loop-filter level of a q-index (av1_enc.h lf_level_for_q)."""
+    return min(63, max(0, (av1m.ac_q(q) * 20723 + 1015158) >> 18))
+
+
 @dataclass
 class GopHost:
     """Host copy of one GOP's decisions for the entropy stage."""
@@ -63,6 +68,7 @@ class GopHost:
     packed: list         # per plane: (levels (K, n) int16, offsets (F, B) int64)
     sse: np.ndarray      # (F, B, 3) int64
     key: list            # per frame
+    qm: np.ndarray = None  # (F, B) q-index per frame and segment
 
 
 class Av1GpuEngine:
@@ -87,9 +93,11 @@ class Av1GpuEngine:
         self.src, self.rec, self.fin = mk(), mk(), mk()
         self.pool = cf.ThreadPoolExecutor(max_workers=threads or min(32, os.cpu_count() or 8))
         self._gop_cap = 0
+        self.lock = None  # set by the worker's engine cache
+        self.staging = None
 
-    def _lf_level(self) -> int:
-        return min(63, max(0, (av1m.ac_q(self.q) * 20723 + 1015158) >> 18))
+    def _lf_level(self, q: int | None = None) -> int:
+        return lf_level(self.q if q is None else q)
 
     def _alloc_gop(self, F: int):
         torch = self.torch
@@ -108,29 +116,28 @@ class Av1GpuEngine:
         self._gop_cap = F
 
     # ------------------------------------------------------------------ one frame ----
-    def _frame(self, t: int, key: bool):
+    def _frame(self, t: int, key: bool, nseg: int, qarr, lvl):
         from ..ops import av1 as ops
 
         torch = self.torch
         lib = _gpu()
         st = _vp(torch.cuda.current_stream(self.dev).cuda_stream)
-        W, H, B, q = self.W, self.H, self.B, self.q
-        sy, su, sv = self.src
-        ry, ru, rv = self.rec
-        fy, fu, fv = self.fin
-        mode, mv = self.g_mode[t], self.g_mv[t]
-        ly, lu, lv = self.g_ly[t], self.g_lu[t], self.g_lv[t]
+        W, H, B, q = self.W, self.H, nseg, self.q
+        sy, su, sv = (x[:B] for x in self.src)
+        ry, ru, rv = (x[:B] for x in self.rec)
+        fy, fu, fv = (x[:B] for x in self.fin)
+        mode, mv = self.g_mode[t, :B], self.g_mv[t, :B]
+        ly, lu, lv = self.g_ly[t, :B], self.g_lu[t, :B], self.g_lv[t, :B]
         if key:
             _ok(lib.tv_av1e_intra(_p(sy), _p(su), _p(sv), _p(ry), _p(ru), _p(rv), _p(mode), _p(mv), _p(ly), _p(lu),
-                                  _p(lv), W, H, B, q, st))
+                                  _p(lv), W, H, B, _p(qarr), st))
         else:
             _ok(lib.tv_av1e_inter(_p(sy), _p(su), _p(sv), _p(fy), _p(fu), _p(fv), _p(ry), _p(ru), _p(rv), _p(mode),
-                                  _p(mv), _p(ly), _p(lu), _p(lv), W, H, B, q, st))
+                                  _p(mv), _p(ly), _p(lu), _p(lv), W, H, B, _p(qarr), st))
         iy = torch.empty((B, H // 4, W // 4), dtype=torch.int32, device=self.dev)
         iu = torch.empty((B, H // 8, W // 8), dtype=torch.int32, device=self.dev)
         iv = torch.empty_like(iu)
-        L = self.lvl
-        _ok(lib.tv_av1e_lfinfo(_p(mode), W, H, B, L, L, L, L, _p(iy), _p(iu), _p(iv), st))
+        _ok(lib.tv_av1e_lfinfo(_p(mode), W, H, B, _p(lvl), _p(iy), _p(iu), _p(iv), st))
         dy = ops.deblock(ry, iy, False, 0)
         du = ops.deblock(ru, iu, True, 0)
         dv = ops.deblock(rv, iv, True, 0)
@@ -140,46 +147,64 @@ class Av1GpuEngine:
         se_v = ops.cdef_search(sv, dv, dirs, var, True, self.damping, luma_w8=W // 8)
         py = torch.empty((B, self.nfb), dtype=torch.int8, device=self.dev)
         puv = torch.empty_like(py)
-        _ok(lib.tv_av1e_cdef_choose(_p(se_y), _p(se_u), _p(se_v), _p(mode), W, H, B, _p(self.g_tabs[t]),
-                                    _p(self.g_fbidx[t]), _p(py), _p(puv), st))
+        _ok(lib.tv_av1e_cdef_choose(_p(se_y), _p(se_u), _p(se_v), _p(mode), W, H, B, _p(self.g_tabs[t, :B]),
+                                    _p(self.g_fbidx[t, :B]), _p(py), _p(puv), st))
         self.fin = (ops.cdef_apply(dy, dirs, var, py, False, self.damping),
                     ops.cdef_apply(du, dirs, var, puv, True, self.damping, luma_w8=W // 8),
                     ops.cdef_apply(dv, dirs, var, puv, True, self.damping, luma_w8=W // 8))
         w, h = self.w, self.h
+        if B < self.B:  # keep full-batch planes: the slice's final frames become the reference
+            fin = [torch.empty_like(x) for x in self.src]
+            for full, part in zip(fin, self.fin):
+                full[:B].copy_(part)
+            self.fin = tuple(fin)
         for c, (s, f) in enumerate(zip(self.src, self.fin)):
-            ss = (slice(None), slice(0, h >> (c > 0)), slice(0, w >> (c > 0)))
+            ss = (slice(0, B), slice(0, h >> (c > 0)), slice(0, w >> (c > 0)))
             d = s[ss].to(torch.int32) - f[ss].to(torch.int32)
-            self.g_sse[t, :, c] = (d * d).sum(dim=(1, 2))
+            self.g_sse[t, :B, c] = (d * d).sum(dim=(1, 2))
 
-    def encode_gop(self, nframes: int, load_frame) -> GopHost:
+    def encode_gop(self, nframes: int, load_frame, nseg: int | None = None, qmap=None) -> GopHost:
         """Run the GPU part of one GOP for all B segments.  load_frame(t, (Y, U, V)) fills
-        the coded-size source planes [B, H, W] of frame t (device tensors).  Returns the
-        host copy of the decisions (one device->host transfer of compacted levels)."""
+        the coded-size source planes [B, H, W] of frame t (device tensors).  `qmap`
+        (optional (nframes, nseg) ints): per-frame, per-segment q-index from rate control
+        (2-pass / CRF plans); None = the engine's constant q-index.  Returns the host copy
+        of the decisions (one device->host transfer of compacted levels)."""
         torch = self.torch
+        nseg = nseg or self.B
+        if not 1 <= nseg <= self.B:
+            raise ValueError(f"nseg {nseg} outside 1..{self.B}")
         self._alloc_gop(nframes)
+        qm = np.full((nframes, nseg), self.q, np.int32) if qmap is None else \
+            np.clip(np.asarray(qmap, np.int32).reshape(nframes, nseg), 1, 255)
+        lv = np.array([[[lf_level(int(x))] * 4 for x in row] for row in qm], np.int32)
+        qd = torch.from_numpy(qm).to(self.dev)
+        ld = torch.from_numpy(lv).to(self.dev)
         for t in range(nframes):
             load_frame(t, self.src)
-            self._frame(t, t == 0)
+            self._frame(t, t == 0, nseg, qd[t], ld[t])
+        self.qm = qm
         F = nframes
-        mode = self.g_mode[:F]
+        self.nseg = nseg
+        mode = self.g_mode[:F, :nseg]
         packed = []
-        for p, lev in enumerate((self.g_ly[:F], self.g_lu[:F], self.g_lv[:F])):
+        for p, lev in enumerate((self.g_ly[:F, :nseg], self.g_lu[:F, :nseg], self.g_lv[:F, :nseg])):
             nz = ((mode >> (10 + p)) & 1).bool()
             counts = nz.sum(dim=2)
             packed.append((lev[nz], counts))
         host = GopHost(
             nframes=F,
             mode=mode.cpu().numpy().view(np.uint32),
-            mv=self.g_mv[:F].cpu().numpy().view(np.uint32),
-            tabs=self.g_tabs[:F].cpu().numpy(),
-            fbidx=self.g_fbidx[:F].cpu().numpy(),
+            mv=self.g_mv[:F, :nseg].cpu().numpy().view(np.uint32),
+            tabs=self.g_tabs[:F, :nseg].cpu().numpy(),
+            fbidx=self.g_fbidx[:F, :nseg].cpu().numpy(),
             packed=[],
-            sse=self.g_sse[:F].cpu().numpy(),
+            sse=self.g_sse[:F, :nseg].cpu().numpy(),
             key=[t == 0 for t in range(F)],
+            qm=qm,
         )
         for lev, counts in packed:
             c = counts.cpu().numpy().astype(np.int64).reshape(-1)
-            off = np.concatenate([[0], np.cumsum(c)])[:-1].reshape(F, self.B)
+            off = np.concatenate([[0], np.cumsum(c)])[:-1].reshape(F, nseg)
             host.packed.append((lev.cpu().numpy(), off))
         return host
 
@@ -190,7 +215,8 @@ class Av1GpuEngine:
         tus = []
         for t in range(g.nframes):
             tabs = g.tabs[t, b]
-            fp = av1m.frame_params(g.key[t], self.q, [self.lvl] * 4, 0, self.damping, tabs[:8], tabs[8:])
+            q = int(g.qm[t, b])
+            fp = av1m.frame_params(g.key[t], q, [lf_level(q)] * 4, 0, self.damping, tabs[:8], tabs[8:])
             lev = [np.ascontiguousarray(pk[0][pk[1][t, b]:]) if len(pk[0]) else np.zeros((1, n), np.int16)
                    for pk, n in zip(g.packed, (256, 64, 64))]
             tus.append(av1m.write_tu(self.w, self.h, fp, np.ascontiguousarray(g.mode[t, b]),
@@ -199,7 +225,7 @@ class Av1GpuEngine:
         return tus
 
     def submit_entropy(self, g: GopHost) -> list:
-        return [self.pool.submit(self.write_segment, g, b) for b in range(self.B)]
+        return [self.pool.submit(self.write_segment, g, b) for b in range(g.mode.shape[1])]
 
     def psnr(self, g: GopHost) -> dict:
         n = g.sse.shape[0] * g.sse.shape[1]

@@ -189,12 +189,86 @@ class HevcSource:
         return list(hevc.decode(self._annexb, coded=False, first=start, count=n).frames)
 
 
+# ----------------------------------------------------------------------------- AV1
+class Av1Source:
+    """Our own AV1 output (MP4 'av01' track or IVF) as a source: the header walk gives the
+    geometry and frame count; ``read`` decodes a range with the decoder oracle from the
+    preceding key frame (models/av1.py)."""
+    kind = "av1"
+
+    def __init__(self, path: str):
+        from . import av1
+
+        self.path = path
+        with open(path, "rb") as f:
+            head = f.read(4)
+        self.fps_num, self.fps_den = 30, 1
+        if head == b"DKIF":
+            with open(path, "rb") as f:
+                info, tus = av1.ivf_unwrap(f.read())
+            self.fps_num, self.fps_den = info["fps"]
+            self._tus = tus
+            self.width, self.height, self.nframes = info["width"], info["height"], len(tus)
+        else:
+            with open(path, "rb") as f:
+                tr = av1.mp4_av1_track(f.read())
+            if tr is None:
+                raise ValueError(f"{path}: no AV1 track")
+            self._tus = None
+            if tr["timescale"] and tr["delta"]:
+                fr = Fraction(tr["timescale"], tr["delta"]).limit_denominator(1001)
+                self.fps_num, self.fps_den = fr.numerator, fr.denominator
+            self.width, self.height, self.nframes = tr["width"], tr["height"], len(tr["samples"])
+
+    def read(self, start: int, n: int):
+        from . import av1
+
+        n = max(0, min(n, self.nframes - start))
+        if n == 0:
+            return []
+        if self._tus is not None:
+            k = start
+            stream = b"".join(self._tus[:start + n])  # IVF: decode from the start (closed GOPs)
+            k = 0
+        else:
+            with open(self.path, "rb") as f:
+                data = f.read()
+            tr, stream = av1.mp4_av1_stream(data, start, n)
+            k = start
+            while k > 0 and not tr["samples"][k][2]:
+                k -= 1
+        dec = av1.decode(stream)
+        return [dec.planes(i) for i in range(start - k, start - k + n)]
+
+
+def _is_av1_file(path: str) -> bool:
+    try:
+        with open(path, "rb") as f:
+            head = f.read(1 << 16)
+    except OSError:
+        return False
+    return head[:4] == b"DKIF" or (path.lower().endswith(".mp4") and b"av01" in head[:4096] + _moov_probe(path))
+
+
+def _moov_probe(path: str) -> bytes:
+    """The bytes of the moov box's sample description area (faststart files keep it first)."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read(1 << 20)
+        i = data.find(b"stsd")
+        return data[i:i + 64] if i >= 0 else b""
+    except OSError:
+        return b""
+
+
 def open_source(path: str):
     ext = os.path.splitext(path)[1].lower()
     if ext == ".y4m":
         return Y4MSource(path)
     if ext == ".synth":
         return SynthSource(path)
+    if ext == ".ivf" or (ext == ".mp4" and _is_av1_file(path)):
+        return Av1Source(path)
     if ext in (".hevc", ".265", ".mp4", ".mkv"):
         return HevcSource(path)
     raise ValueError(f"unsupported input format: {path}")
@@ -206,7 +280,7 @@ def probe(path: str) -> dict:
     size = os.path.getsize(path) if os.path.exists(path) else 0
     fps = src.fps_num / src.fps_den
     dur = src.nframes / fps if fps else 0.0
-    codec = {"rawvideo": "rawvideo", "synthetic": "synthetic", "hevc": "hevc"}[src.kind]
+    codec = {"rawvideo": "rawvideo", "synthetic": "synthetic", "hevc": "hevc", "av1": "av1"}[src.kind]
     return {
         "codec": codec,
         "width": src.width,

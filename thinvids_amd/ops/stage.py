@@ -174,16 +174,17 @@ def tone_map(src: DevFrames, src_peak: float = 1000.0, dst_peak: float = 100.0) 
     return res
 
 
-def staging_planes(w: int, h: int) -> tuple[int, list]:
+def staging_planes(w: int, h: int, coded: tuple | None = None) -> tuple[int, list]:
     """(coded frame size, [(offset, display w, h, row stride, coded w, coded h)]) of the
-    engine staging layout."""
-    cw, ch = coded_size(w, h)
+    engine staging layout (`coded` overrides the HEVC CTB-aligned coded size, e.g. the AV1
+    engine's 16-aligned one)."""
+    cw, ch = coded or coded_size(w, h)
     ysz, csz = cw * ch, (cw // 2) * (ch // 2)
     return ysz + 2 * csz, [(0, w, h, cw, cw, ch), (ysz, w // 2, h // 2, cw // 2, cw // 2, ch // 2),
                            (ysz + csz, w // 2, h // 2, cw // 2, cw // 2, ch // 2)]
 
 
-def to_staging(src: DevFrames, out_w: int, out_h: int, dst, frame0: int = 0) -> None:
+def to_staging(src: DevFrames, out_w: int, out_h: int, dst, frame0: int = 0, coded: tuple | None = None) -> None:
     """Write src's frames (tone-mapped if 10-bit) into the engine staging tensor `dst`
     (coded-size [frame][Y|U|V] of out_w x out_h) starting at frame slot `frame0`: edge pad
     when the size is unchanged, fused Lanczos otherwise.  Runs on the current stream."""
@@ -195,7 +196,7 @@ def to_staging(src: DevFrames, out_w: int, out_h: int, dst, frame0: int = 0) -> 
     lib = _lib()
     dev = dst.device
     st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    fsz, planes = staging_planes(out_w, out_h)
+    fsz, planes = staging_planes(out_w, out_h, coded)
     base = dst.data_ptr() + frame0 * fsz
     for c, (doff, dw, dh, dstride, pw, ph) in enumerate(planes):
         _, sw, sh, sstride, sfs = src.planes[c]

@@ -290,7 +290,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             search_range: int = 64, software: bool = False, batch_segments: int = 8,
             resume_dir: str | None = None, max_retries: int = 3, hooks: JobHooks | None = None,
             deblock: bool = True, sao: bool = False, cache=None, crf: int = 0, scenecut: bool = False,
-            audio_stream: int = 0) -> dict:
+            audio_stream: int = 0, codec: str = "hevc", qindex: int = 0) -> dict:
     import torch
 
     from ..models import hevc, media
@@ -334,7 +334,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     def spec(r):  # the QP is a per-frame input now: one resident engine per rung, whatever the plan
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=qp, gop=gop, search_range=search_range,
                           software=software, deblock=deblock, sao=sao, seed=getattr(src, "seed", 1),
-                          crf=0 if bitrate_kbps > 0 else crf, scenecut=scenecut)
+                          crf=0 if bitrate_kbps > 0 else crf, scenecut=scenecut, codec=codec, qindex=qindex)
 
     rc = {"plan": None, "fb": RateFeedback(), "bits": {}}  # pass-2 plan, feedback, per-frame bits
 

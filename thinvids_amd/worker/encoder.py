@@ -44,10 +44,19 @@ class EncodeSpec:
     seed: int = 1  # synthetic sources generated inside the engine
     crf: int = 0  # > 0: in-engine CRF (per-frame QP from the lookahead)
     scenecut: bool = False  # restart the closed GOP (IDR) at detected scene cuts
+    codec: str = "hevc"  # "av1": the AV1 engine (models/av1_engine.py), BASELINE config #4
+    qindex: int = 0  # AV1 q-index (0: matched to qp)
 
     def engine_key(self):
+        if self.codec == "av1":
+            return ("av1", self.width, self.height, self.av1_qindex())
         return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed,
                 self.crf)
+
+    def av1_qindex(self) -> int:
+        from ..models.av1 import qindex_for_hevc_qp
+
+        return self.qindex or qindex_for_hevc_qp(self.qp)
 
 
 @dataclass(frozen=True)
@@ -109,9 +118,16 @@ class EngineCache:
                 while len(self._order) >= self.max_engines:
                     old = self._order.pop(0)
                     self._engines.pop(old).close()
-                eng = GpuEngine(spec.width, spec.height, qp=spec.qp, batch=self.batch or auto_batch(spec), gop=spec.gop,
-                                search_range=spec.search_range, deblock=spec.deblock, sao=spec.sao,
-                                seed=spec.seed, device=self.device, crf=spec.crf)
+                if spec.codec == "av1":
+                    from ..models.av1_engine import Av1GpuEngine
+
+                    eng = Av1GpuEngine(spec.width, spec.height, batch=min(32, self.batch or auto_batch(spec)),
+                                       qindex=spec.av1_qindex(), device=self.device)
+                    eng.batch = eng.B
+                else:
+                    eng = GpuEngine(spec.width, spec.height, qp=spec.qp, batch=self.batch or auto_batch(spec),
+                                    gop=spec.gop, search_range=spec.search_range, deblock=spec.deblock, sao=spec.sao,
+                                    seed=spec.seed, device=self.device, crf=spec.crf)
                 eng.lock = threading.Lock()
                 eng.staging = None
                 self._engines[key] = eng
@@ -230,8 +246,20 @@ def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None, fq=None) -> byte
     h, w = frames[0][0].shape
     if (w, h) != (spec.width, spec.height) or frames[0][0].dtype != np.uint8:
         frames = prepare_frames(frames, spec.width, spec.height)
-    bs, recons = hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock, sao=spec.sao,
-                                          search_range=spec.search_range, frame_qps=fq, crf=spec.crf)
+    if spec.codec == "av1":  # C++ golden AV1 encoder, one closed GOP per `gop` frames
+        from ..models import av1
+
+        bs, recons = b"", []
+        W, H = av1.coded_size(spec.width, spec.height)
+        for a in range(0, len(frames), spec.gop):
+            r = av1.golden_encode(frames[a:a + spec.gop], spec.width, spec.height, spec.av1_qindex())
+            bs += r.stream
+            for f in r.recon:
+                recons.append((f[:W * H].reshape(H, W), f[W * H:W * H * 5 // 4].reshape(H // 2, W // 2),
+                               f[W * H * 5 // 4:].reshape(H // 2, W // 2)))
+    else:
+        bs, recons = hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock, sao=spec.sao,
+                                              search_range=spec.search_range, frame_qps=fq, crf=spec.crf)
     if st is not None:
         sse = np.zeros(3)
         for f, r in zip(frames, recons):
@@ -261,6 +289,8 @@ def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats, qps) -> list
         for c, (s, n) in enumerate(plan):
             q = None if qps[pi] is None else np.asarray(qps[pi][s:s + n], np.int64)
             chunks.setdefault(n, []).append((pi, c, _slice(p, s, n), q))
+    if spec.codec == "av1":
+        return _encode_gpu_av1(eng, chunks, out, spec, dev, stats)
     fsz, _ = stage.staging_planes(spec.width, spec.height)
     own_size = (spec.width, spec.height)
     with eng.lock:
@@ -287,6 +317,49 @@ def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats, qps) -> list
                     out[pi][c] = b
                     if stats is not None:
                         stats[pi].add(n, eng.sse(j))
+    return [b"".join(x) for x in out]
+
+
+def _encode_gpu_av1(eng, chunks: dict, out: list, spec: EncodeSpec, dev, stats) -> list[bytes]:
+    """AV1 engine: equal-length chunks in groups of up to eng.B segments; sources are
+    staged (tone-map / resize / edge pad) straight into the engine's coded-size planes."""
+    import torch
+
+    from ..models import av1
+    from ..ops import stage
+
+    cw, ch = av1.coded_size(spec.width, spec.height)
+    fsz = cw * ch * 3 // 2
+    ysz, csz = cw * ch, cw * ch // 4
+    with eng.lock:
+        for n, items in chunks.items():
+            for i in range(0, len(items), eng.B):
+                grp = items[i:i + eng.B]
+                need = len(grp) * n * fsz
+                if eng.staging is None or eng.staging.numel() < need:
+                    eng.staging = torch.empty(need, dtype=torch.uint8, device=dev)
+                for j, (_, _, s, _) in enumerate(grp):
+                    if isinstance(s, SynthRange):
+                        s = stage.synth_frames(s.seed, s.width, s.height, range(s.t0, s.t0 + s.n), dev)
+                    stage.to_staging(s, spec.width, spec.height, eng.staging, j * n, coded=(cw, ch))
+                frames = eng.staging[:need].view(len(grp), n, fsz)
+
+                def load(t, planes, frames=frames):
+                    f = frames[:, t]
+                    planes[0][:len(grp)].copy_(f[:, :ysz].view(-1, ch, cw))
+                    planes[1][:len(grp)].copy_(f[:, ysz:ysz + csz].view(-1, ch // 2, cw // 2))
+                    planes[2][:len(grp)].copy_(f[:, ysz + csz:].view(-1, ch // 2, cw // 2))
+
+                qmap = None
+                if any(x[3] is not None for x in grp):  # rate-control plan: per-frame HEVC QP -> q-index
+                    qmap = np.array([[av1.qindex_for_hevc_qp(int(x[3][t])) if x[3] is not None
+                                      else spec.av1_qindex() for x in grp] for t in range(n)], np.int32)
+                g = eng.encode_gop(n, load, nseg=len(grp), qmap=qmap)
+                futs = eng.submit_entropy(g)
+                for j, ((pi, c, _, _), fu) in enumerate(zip(grp, futs)):
+                    out[pi][c] = b"".join(fu.result())
+                    if stats is not None:
+                        stats[pi].add(n, g.sse[:, j].sum(axis=0))
     return [b"".join(x) for x in out]
 
 

@@ -124,7 +124,7 @@ def _job_params(job: dict) -> dict:
             "segment_frames": max(spec.gop, as_int(s.get("tv_node_segment_frames"), 256)),
             "mode": str(s.get("tv_node_mode") or "direct"), "batch_segments": as_int(s.get("tv_node_batch"), 8),
             "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc,
-            "scenecut": spec.scenecut}
+            "scenecut": spec.scenecut, "codec": spec.codec, "qindex": spec.qindex}
 
 
 class CommFailure(RuntimeError):
@@ -193,7 +193,7 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                       ladder=p["ladder"], search_range=p["search_range"], software=p["software"],
                       batch_segments=p["batch_segments"], hooks=hooks, deblock=p["deblock"], sao=p["sao"],
                       cache=None if p["software"] else cache, crf=p["crf"], resume_dir=spec["ckpt"],
-                      scenecut=p.get("scenecut", False),
+                      scenecut=p.get("scenecut", False), codec=p.get("codec", "hevc"), qindex=p.get("qindex", 0),
                       audio_stream=int(spec["job"].get("selected_a_stream") or 0))
     except Exception as e:
         if is_comm_failure(e):  # the job is fine, the communicator is not: requeue + re-init
@@ -242,7 +242,7 @@ def _publish(job_id: str, spec: dict, res: dict) -> None:
     o = outs[0]
     fps = o["fps_num"] / o["fps_den"]
     dur = o["frames"] / fps if fps else 0.0
-    fields.update(dest_file_size=os.path.getsize(finals[0]), dest_duration=f"{dur:.2f}", dest_codec="hevc",
+    fields.update(dest_file_size=os.path.getsize(finals[0]), dest_duration=f"{dur:.2f}", dest_codec=spec["params"].get("codec", "hevc"),
                   dest_resolution=f"{o['width']}x{o['height']}", dest_fps=f"{fps:.2f}",
                   dest_bitrate_kbps=f"{os.path.getsize(finals[0]) * 8 / dur / 1000 if dur else 0:.0f}",
                   english_subtitles_found=0, english_subtitles_supported=0, english_subtitles_kept=0,

@@ -102,7 +102,9 @@ def encode_spec_for_job(job: dict, settings: dict | None = None) -> EncodeSpec:
                       software=as_bool(job.get("software_encode")),
                       crf=as_int(job.get("crf") or s.get("tv_crf"), 27)
                       if str(job.get("rc_mode") or s.get("tv_rc") or "cqp").lower() == "crf" else 0,
-                      scenecut=as_bool(s.get("tv_scenecut"), True))
+                      scenecut=as_bool(s.get("tv_scenecut"), True),
+                      codec="av1" if str(job.get("codec") or s.get("tv_codec") or "hevc").lower() == "av1" else "hevc",
+                      qindex=as_int(job.get("qindex") or s.get("tv_qindex"), 0))
 
 
 # =====================================================================  transcode
