@@ -87,7 +87,7 @@ __device__ __forceinline__ int cdef_tile_filter(const int16_t (*T)[kTile], int t
 __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__ src, const uint8_t* __restrict__ rec,
                                                      int w, int h, int chroma, const uint8_t* __restrict__ dir,
                                                      const int* __restrict__ var, int luma_w8, int luma_n8,
-                                                     int damping, unsigned long long* sse) {
+                                                     int damping, unsigned long long* sse, unsigned long long pmask) {
   const int b = blockIdx.y, fb = blockIdx.x;
   const int bs_l2 = chroma ? 2 : 3, fbs = chroma ? 32 : 64, nfx = (w + fbs - 1) / fbs;
   const int x0 = (fb % nfx) * fbs, y0 = (fb / nfx) * fbs;
@@ -99,10 +99,18 @@ __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__
   cdef_stage(rec + po, w, h, x0, y0, fbw, fbh, T);
   if (threadIdx.x < kCdefPresets) acc[threadIdx.x] = 0;
   __syncthreads();
-  const int p = threadIdx.x & 63, g = threadIdx.x >> 6;
+  // evaluated presets (pmask bits) spread over the 256 threads: thread -> (preset, pixel group)
+  const int np = __popcll(pmask), ng = 256 / np;
+  const int pi = threadIdx.x % np, g = threadIdx.x / np;
+  int p = 0;
+  for (int k = 0, seen = 0; k < kCdefPresets; ++k)
+    if (pmask >> k & 1) {
+      if (seen == pi) p = k;
+      ++seen;
+    }
   const int psec = cdef_sec_value(p & 3), ppri = p >> 2;
   unsigned s = 0;  // <= 1024 pixels x 255^2 fits in 32 bits
-  for (int q = g; q < fbw * fbh; q += 4) {
+  for (int q = g; q < fbw * fbh && g < ng; q += ng) {
     const int i = q / fbw, j = q - i * fbw, x = x0 + j, y = y0 + i;
     const long k = (long)b * luma_n8 + (y >> bs_l2) * luma_w8 + (x >> bs_l2);
     const int pri = chroma ? ppri : cdef_adjust_strength(ppri, var[k]);
@@ -110,10 +118,12 @@ __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__
     const int e = f - (int)src[po + (long)y * w + x];
     s += (unsigned)(e * e);
   }
-  atomicAdd(&acc[p], (unsigned long long)s);
+  if (g < ng) atomicAdd(&acc[p], (unsigned long long)s);
   __syncthreads();
   const int nfb = nfx * ((h + fbs - 1) / fbs);
-  if (threadIdx.x < kCdefPresets) sse[((long)b * nfb + fb) * kCdefPresets + threadIdx.x] = acc[threadIdx.x];
+  if (threadIdx.x < kCdefPresets)
+    sse[((long)b * nfb + fb) * kCdefPresets + threadIdx.x] =
+        (pmask >> threadIdx.x & 1) ? acc[threadIdx.x] : (unsigned long long)kCdefSkipped;
 }
 
 __global__ void __launch_bounds__(256) k_cdef_apply(const uint8_t* __restrict__ rec, int w, int h, int chroma,
@@ -429,11 +439,12 @@ int tv_gpu_cdef_dirs(const uint8_t* Y, int w, int h, int B, uint8_t* dir, int* v
 }
 // sse: [B][nfb][64] (uint64)
 int tv_gpu_cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, int B, int chroma, const uint8_t* dir,
-                       const int* var, int luma_w8, int luma_n8, int damping, unsigned long long* sse, void* stream) {
-  if (bad_geo(w, h, B, chroma ? 4 : 8, "cdef_search") || damping < 3 || damping > 6) return -1;
+                       const int* var, int luma_w8, int luma_n8, int damping, unsigned long long* sse, void* stream,
+                       unsigned long long pmask) {
+  if (bad_geo(w, h, B, chroma ? 4 : 8, "cdef_search") || damping < 3 || damping > 6 || !pmask) return -1;
   const int fbs = chroma ? 32 : 64, nfb = ((w + fbs - 1) / fbs) * ((h + fbs - 1) / fbs);
   k_cdef_search<<<dim3(nfb, B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, chroma, dir, var, luma_w8, luma_n8,
-                                                               damping, sse);
+                                                               damping, sse, pmask);
   return av1_status("cdef_search");
 }
 int tv_gpu_cdef_apply(const uint8_t* rec, int w, int h, int B, int chroma, const uint8_t* dir, const int* var,

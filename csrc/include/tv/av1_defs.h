@@ -133,6 +133,7 @@ TV_HD int cdef_filter_pixel(const uint8_t* P, int p, int w, int h, int x, int y,
 // CDEF strength preset: index = pri * 4 + sec_idx; sec_idx 3 means strength 4.
 TV_HD int cdef_sec_value(int sec_idx) { return sec_idx == 3 ? 4 : sec_idx; }
 constexpr int kCdefPresets = 64;  // 16 primary x 4 secondary
+constexpr uint64_t kCdefSkipped = 1ull << 40;  // SSE reported for presets a search skipped
 
 // ------------------------------------------------------------------ loop restoration ----
 constexpr int kWienerTaps = 7;

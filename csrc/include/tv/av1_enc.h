@@ -252,6 +252,19 @@ TV_HD int intra_mode_bits16(int m) {
   }
 }
 
+// CDEF presets the encoder evaluates (preset = pri * 4 + sec_idx): luma primary strengths
+// {0,1,2,3,5,7,10,13} x secondary {0, 2}; chroma {0,2,4,7} x {0, 2} (a libaom-style fast
+// strength subset: 16 / 8 of the 64 presets, 4x / 8x less CDEF search work).
+constexpr uint64_t cdef_mask(const int* pri, int npri, const int* sec, int nsec) {
+  uint64_t m = 0;
+  for (int i = 0; i < npri; ++i)
+    for (int j = 0; j < nsec; ++j) m |= 1ull << (pri[i] * 4 + sec[j]);
+  return m;
+}
+constexpr int kCdefPriY[8] = {0, 1, 2, 3, 5, 7, 10, 13}, kCdefPriUV[4] = {0, 2, 4, 7}, kCdefSec[2] = {0, 2};
+constexpr uint64_t kCdefMaskY = cdef_mask(kCdefPriY, 8, kCdefSec, 2);
+constexpr uint64_t kCdefMaskUV = cdef_mask(kCdefPriUV, 4, kCdefSec, 2);
+
 // ------------------------------------------------------------------ motion search -------
 // Full-pel window of +-kMeRange around the co-located block, then 8 half-pel and 8
 // quarter-pel refinements (SATD + lambda * mv bits, first minimum wins).

@@ -31,6 +31,15 @@ from . import av1 as av1m
 _vp = C.c_void_p
 
 
+def _cdef_mask(pri, sec) -> int:
+    return sum(1 << (p * 4 + s) for p in pri for s in sec)
+
+
+# evaluated CDEF presets: av1_enc.h kCdefMaskY / kCdefMaskUV
+CDEF_MASK_Y = _cdef_mask((0, 1, 2, 3, 5, 7, 10, 13), (0, 2))
+CDEF_MASK_UV = _cdef_mask((0, 2, 4, 7), (0, 2))
+
+
 def _gpu():
     from .._native import gpu_lib
 
@@ -142,9 +151,9 @@ class Av1GpuEngine:
         du = ops.deblock(ru, iu, True, 0)
         dv = ops.deblock(rv, iv, True, 0)
         dirs, var = ops.cdef_dirs(dy)
-        se_y = ops.cdef_search(sy, dy, dirs, var, False, self.damping)
-        se_u = ops.cdef_search(su, du, dirs, var, True, self.damping, luma_w8=W // 8)
-        se_v = ops.cdef_search(sv, dv, dirs, var, True, self.damping, luma_w8=W // 8)
+        se_y = ops.cdef_search(sy, dy, dirs, var, False, self.damping, pmask=CDEF_MASK_Y)
+        se_u = ops.cdef_search(su, du, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV)
+        se_v = ops.cdef_search(sv, dv, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV)
         py = torch.empty((B, self.nfb), dtype=torch.int8, device=self.dev)
         puv = torch.empty_like(py)
         _ok(lib.tv_av1e_cdef_choose(_p(se_y), _p(se_u), _p(se_v), _p(mode), W, H, B, _p(self.g_tabs[t, :B]),
