@@ -59,6 +59,7 @@ FrameDecisions FrameData::view() const {
   d.lu = lu.data();
   d.lv = lv.data();
   d.cdef_idx = cdef_idx.data();
+  d.lr = lr.empty() ? nullptr : lr.data();
   d.packed = false;
   return d;
 }
@@ -104,6 +105,7 @@ struct Cdfs {
   C17 intra_tx[4][13], inter_tx[4];
   C17 txb_skip[5][13], eob_pt[7][2][2], eob_extra[5][2][9], base_eob[5][2][4], base[5][2][42], br[4][2][21];
   C17 dc_sign[2][3];
+  C17 use_sgrproj;
 };
 template <size_t K> void init_all(C17 (&a)[K], int n) {
   for (auto& c : a) cdf_init_uniform(c, n);
@@ -146,6 +148,7 @@ void init_cdfs(Cdfs& c) {
   init_all(c.base, 4);
   init_all(c.br, 4);
   init_all(c.dc_sign, 2);
+  cdf_init_uniform(c.use_sgrproj, 2);
 }
 // P(symbol s) of an inverse CDF (15-bit)
 inline int sym_prob(const uint16_t* icdf, int s) { return (s ? icdf[s - 1] : 32768) - icdf[s]; }
@@ -187,6 +190,9 @@ struct Tile {
   std::vector<uint32_t>& mode;
   std::vector<uint32_t>& mv;
   std::vector<int8_t>& cdef_idx;
+  int32_t* lr = nullptr;                  // [3][nu][3]: writer input / reader output (null: no LR)
+  int lr_type[3] = {0, 0, 0};
+  int ref_xqd[3][2];
   std::vector<uint8_t> ymode, coded;      // inter mode (NEARESTMV..NEWMV) or intra y mode
   std::vector<int8_t> cdef_seen;
   std::vector<uint8_t> aLvl[3], aDc[3], lLvl[3], lDc[3];
@@ -761,6 +767,96 @@ struct Tile {
     coded[b] = 1;
   }
 
+  // ---- loop restoration unit syntax (5.11.58 read_lr_unit, SGRPROJ frame type) ----
+  void ns(int& v, int n) {  // non-symmetric unsigned literal of n values
+    const int w = floor_log2((unsigned)n) + 1, m = (1 << w) - n;
+    if (IO::kW) {
+      if (v < m) {
+        io.lit(v, w - 1);
+      } else {
+        int hi = (v + m) >> 1, ex = (v + m) & 1;
+        io.lit(hi, w - 1);
+        io.lit(ex, 1);
+      }
+      return;
+    }
+    int x = 0;
+    io.lit(x, w - 1);
+    if (x < m) {
+      v = x;
+      return;
+    }
+    int ex = 0;
+    io.lit(ex, 1);
+    v = (x << 1) - m + ex;
+  }
+  void subexp(int& v, int nsyms, int k) {
+    int i = 0, mk = 0;
+    for (;;) {
+      const int b2 = i ? k + i - 1 : k, a = 1 << b2;
+      if (nsyms <= mk + 3 * a) {
+        int x = v - mk;
+        ns(x, nsyms - mk);
+        v = x + mk;
+        return;
+      }
+      int more = IO::kW ? v >= mk + a : 0;
+      io.lit(more, 1);
+      if (!more) {
+        int x = v - mk;
+        io.lit(x, b2);
+        v = x + mk;
+        return;
+      }
+      ++i;
+      mk += a;
+    }
+  }
+  static int recenter(int r, int v) { return v > 2 * r ? v : (v >= r ? (v - r) << 1 : ((r - v) << 1) - 1); }
+  static int inv_recenter(int r, int v) { return v > 2 * r ? v : ((v & 1) ? r - ((v + 1) >> 1) : r + (v >> 1)); }
+  void signed_subexp_ref(int& v, int low, int high, int k, int r) {
+    const int mx = high - low, rr = r - low;
+    int x = 0;
+    if (IO::kW) {
+      const int u = v - low;
+      x = (rr << 1) <= mx ? recenter(rr, u) : recenter(mx - 1 - rr, mx - 1 - u);
+    }
+    subexp(x, mx, k);
+    const int u = (rr << 1) <= mx ? inv_recenter(rr, x) : mx - 1 - inv_recenter(mx - 1 - rr, x);
+    if (IO::kW && u + low != v) throw std::runtime_error("av1 writer: subexp mismatch");
+    v = u + low;
+  }
+  void lr_unit(int p, int u) {
+    int32_t* P = lr + ((size_t)p * g.lr_nu() + u) * 3;
+    int on = P[0] >= 0;
+    io.sym(on, cdf.use_sgrproj, 2);
+    if (!on) {
+      if (!IO::kW) P[0] = -1, P[1] = P[2] = 0;
+      return;
+    }
+    int set = P[0];
+    io.lit(set, 4);
+    const int r0 = sgr_param(set, 0), r1 = sgr_param(set, 2);
+    int x0 = P[1], x1 = P[2];
+    if (r0) signed_subexp_ref(x0, kXqdMin0, kXqdMax0 + 1, 4, ref_xqd[p][0]);
+    else x0 = 0;
+    ref_xqd[p][0] = x0;
+    if (r1) signed_subexp_ref(x1, kXqdMin1, kXqdMax1 + 1, 4, ref_xqd[p][1]);
+    else x1 = clip3(kXqdMin1, kXqdMax1, 128 - ref_xqd[p][0]);
+    if (IO::kW && (x0 != P[1] || x1 != P[2])) throw std::runtime_error("av1 writer: sgr weights not representable");
+    ref_xqd[p][1] = x1;
+    P[0] = set, P[1] = x0, P[2] = x1;
+  }
+  void read_lr(int sr, int sc) {
+    for (int p = 0; p < 3; ++p) {
+      if (!lr_type[p]) continue;
+      const int sbs = p ? 32 : 64, x0 = sc * sbs, y0 = sr * sbs;
+      for (int uy = 0; uy < g.lr_uy(p); ++uy)
+        for (int ux = 0; ux < g.lr_ux(p); ++ux)
+          if (ux * 64 >= x0 && ux * 64 < x0 + sbs && uy * 64 >= y0 && uy * 64 < y0 + sbs) lr_unit(p, uy * g.lr_ux(p) + ux);
+    }
+  }
+
   void partition(int mir, int mic, int bsl) {
     if (mir >= MiRows || mic >= MiCols) return;
     const bool availU = mir > 0, availL = mic > 0;
@@ -799,12 +895,16 @@ struct Tile {
   }
 
   void tile() {
+    for (int p = 0; p < 3; ++p) ref_xqd[p][0] = kXqdMid0, ref_xqd[p][1] = kXqdMid1;
     for (int sr = 0; sr < g.sbh; ++sr) {
       for (int p = 0; p < 3; ++p) {  // clear_left_context
         std::fill(lLvl[p].begin(), lLvl[p].end(), 0);
         std::fill(lDc[p].begin(), lDc[p].end(), 0);
       }
-      for (int sc = 0; sc < g.sbw; ++sc) partition(sr * 16, sc * 16, 4);
+      for (int sc = 0; sc < g.sbw; ++sc) {
+        read_lr(sr, sc);
+        partition(sr * 16, sc * 16, 4);
+      }
     }
   }
 };
@@ -851,7 +951,7 @@ void write_seq_header(BitWriter& w, const SeqGeo& g) {
   w.put(0, 1);  // seq_force_screen_content_tools
   w.put(0, 1);  // enable_superres
   w.put(1, 1);  // enable_cdef
-  w.put(0, 1);  // enable_restoration
+  w.put(1, 1);  // enable_restoration
   // color_config: 8-bit, not monochrome, no colour description, studio range, 4:2:0
   w.put(0, 1);  // high_bitdepth
   w.put(0, 1);  // mono_chrome
@@ -883,7 +983,7 @@ SeqGeo read_seq_header(BitReader& r) {
                          "order hint",    "choose screen content", "force screen content", "superres"};
   for (auto f : flags) expect(1, 0, f);
   expect(1, 1, "enable_cdef");
-  expect(1, 0, "enable_restoration");
+  expect(1, 1, "enable_restoration");
   expect(1, 0, "high_bitdepth");
   expect(1, 0, "mono_chrome");
   expect(1, 0, "color_description");
@@ -896,7 +996,7 @@ SeqGeo read_seq_header(BitReader& r) {
   return g;
 }
 
-void write_frame_header(BitWriter& w, const SeqGeo& g, const FrameParams& fp) {
+void write_frame_header(BitWriter& w, const SeqGeo& g, const FrameParams& fp, const int* lr_type) {
   w.put(0, 1);  // show_existing_frame
   w.put(fp.key ? 0 : 1, 2);  // frame_type KEY_FRAME / INTER_FRAME
   w.put(1, 1);  // show_frame
@@ -961,6 +1061,12 @@ void write_frame_header(BitWriter& w, const SeqGeo& g, const FrameParams& fp) {
     w.put(fp.cdef_uv[i] >> 2, 4);
     w.put(fp.cdef_uv[i] & 3, 2);
   }
+  // lr_params: lr_type 3 = SGRPROJ (Remap_Lr_Type), 64x64 units (lr_unit_shift 0), no uv shift
+  for (int p = 0; p < 3; ++p) w.put(lr_type[p] ? 3 : 0, 2);
+  if (lr_type[0] || lr_type[1] || lr_type[2]) {
+    w.put(0, 1);  // lr_unit_shift
+    if (lr_type[1] || lr_type[2]) w.put(0, 1);  // lr_uv_shift
+  }
   w.put(0, 1);  // tx_mode_select (TX_MODE_LARGEST)
   if (!fp.key) w.put(0, 1);  // reference_select
   w.put(1, 1);  // reduced_tx_set
@@ -968,7 +1074,7 @@ void write_frame_header(BitWriter& w, const SeqGeo& g, const FrameParams& fp) {
     for (int i = 0; i < 7; ++i) w.put(0, 1);  // is_global
 }
 
-FrameParams read_frame_header(BitReader& r, SeqGeo& g, bool& have_ref) {
+FrameParams read_frame_header(BitReader& r, SeqGeo& g, bool& have_ref, int* lr_type) {
   auto expect = [&](int n, uint32_t v, const char* what) {
     if (r.u(n) != v) throw std::runtime_error(std::string("av1 oracle: unsupported frame header ") + what);
   };
@@ -1026,6 +1132,15 @@ FrameParams read_frame_header(BitReader& r, SeqGeo& g, bool& have_ref) {
     fp.cdef_y[i] = (uint8_t)(yp * 4 + ys);
     fp.cdef_uv[i] = (uint8_t)(up * 4 + us);
   }
+  for (int p = 0; p < 3; ++p) {
+    const int t = (int)r.u(2);
+    if (t != 0 && t != 3) throw std::runtime_error("av1 oracle: restoration type outside the encoder subset");
+    lr_type[p] = t == 3;
+  }
+  if (lr_type[0] || lr_type[1] || lr_type[2]) {
+    expect(1, 0, "lr_unit_shift");
+    if (lr_type[1] || lr_type[2]) expect(1, 0, "lr_uv_shift");
+  }
   expect(1, 0, "tx_mode_select");
   if (!fp.key) expect(1, 0, "reference_select");
   expect(1, 1, "reduced_tx_set");
@@ -1059,6 +1174,13 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
   std::vector<int8_t> cdef(d.cdef_idx, d.cdef_idx + g.nsb());
   SymW io;
   Tile<SymW> t(io, g, fp, mode, mv, cdef);
+  std::vector<int32_t> lr;
+  if (d.lr) {
+    lr.assign(d.lr, d.lr + (size_t)3 * g.lr_nu() * 3);
+    t.lr = lr.data();
+    for (int p = 0; p < 3; ++p)
+      for (int u = 0; u < g.lr_ux(p) * g.lr_uy(p); ++u) t.lr_type[p] |= lr[((size_t)p * g.lr_nu() + u) * 3] >= 0;
+  }
   // level access (packed layout: prefix offsets over the nonzero masks)
   std::vector<int32_t> off[3];
   const int16_t* base[3] = {d.ly, d.lu, d.lv};
@@ -1084,7 +1206,7 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
     put_obu(out, OBU_SEQUENCE_HEADER, sw.bytes());
   }
   BitWriter fw;
-  write_frame_header(fw, g, fp);
+  write_frame_header(fw, g, fp, t.lr_type);
   fw.align_zero();  // byte_alignment (frame_obu); tile_group: one tile, no start/end flags
   std::vector<uint8_t> payload = fw.bytes();
   payload.insert(payload.end(), tile.begin(), tile.end());
@@ -1116,8 +1238,23 @@ void residual_of(const int16_t* lev, int lg, int qidx, int txt, int16_t* res) {
   txfm2d_ref(dq, res, 1, lg, txt & 1, (txt >> 1) & 1, true);
 }
 
+// self-guided restoration of the CDEF output with the per-unit (set, xqd0, xqd1)
+void apply_lr(const SeqGeo& g, const int32_t* lr, Planes& io) {
+  for (int p = 0; p < 3; ++p) {
+    const int nu = g.lr_ux(p) * g.lr_uy(p);
+    const int32_t* P = lr + (size_t)p * g.lr_nu() * 3;
+    bool any = false;
+    for (int u = 0; u < nu; ++u) any |= P[3 * u] >= 0;
+    if (!any) continue;
+    std::vector<uint8_t>& X = p == 0 ? io.y : (p == 1 ? io.u : io.v);
+    std::vector<uint8_t> o(X.size());
+    sgr_apply(X.data(), p ? g.W / 2 : g.W, p ? g.H / 2 : g.H, P, o.data());
+    X.swap(o);
+  }
+}
+
 void loop_filters(const SeqGeo& g, const FrameParams& fp, const uint32_t* mode, const int8_t* cdef_idx, Planes& rec,
-                  Planes& out) {
+                  Planes& out, const int32_t* lr = nullptr) {
   const int W = g.W, H = g.H;
   // deblocking: one info word per 4x4 unit of each plane
   Planes db;
@@ -1156,6 +1293,7 @@ void loop_filters(const SeqGeo& g, const FrameParams& fp, const uint32_t* mode, 
              out.u.data());
   cdef_apply(db.v.data(), W / 2, H / 2, true, dir.data(), var.data(), W / 8, fp.cdef_damping, puv.data(),
              out.v.data());
+  if (lr) apply_lr(g, lr, out);
 }
 
 // prediction of one block (luma 16x16 or chroma 8x8) into pred[]
@@ -1220,7 +1358,7 @@ void reconstruct(const SeqGeo& g, const FrameDecisions& d, const Planes* ref, Pl
             P[(size_t)(by * N + i) * w + bx * N + j] = (uint8_t)clip_pixel(pred[i * N + j] + res[i * N + j]);
       }
     }
-  loop_filters(g, d.fp, d.mode, d.cdef_idx, rec, out);
+  loop_filters(g, d.fp, d.mode, d.cdef_idx, rec, out, d.lr);
 }
 
 // ================================================================== decoder oracle ======
@@ -1264,7 +1402,8 @@ Decoded decode_stream(const uint8_t* p, size_t n) {
     bool have_ref = !out.frames.empty();
     SeqGeo g = out.geo;
     FrameData fd;
-    fd.fp = read_frame_header(r, g, have_ref);
+    int lr_type[3] = {0, 0, 0};
+    fd.fp = read_frame_header(r, g, have_ref, lr_type);
     out.geo = g;
     r.byte_align();
     const size_t hdr = r.byte_pos();
@@ -1280,6 +1419,10 @@ Decoded decode_stream(const uint8_t* p, size_t n) {
     t.lev_out[0] = fd.ly.data();
     t.lev_out[1] = fd.lu.data();
     t.lev_out[2] = fd.lv.data();
+    fd.lr.assign((size_t)3 * g.lr_nu() * 3, 0);
+    for (size_t i = 0; i < fd.lr.size(); i += 3) fd.lr[i] = -1;
+    t.lr = fd.lr.data();
+    for (int p = 0; p < 3; ++p) t.lr_type[p] = lr_type[p];
     t.tile();
     Planes rec;
     reconstruct(g, fd.view(), fd.fp.key ? nullptr : &out.frames.back(), rec);
@@ -1340,6 +1483,16 @@ void cdef_choose(const uint64_t* sse_y, const uint64_t* sse_uv, const uint8_t* a
 }
 
 namespace {
+// per-64x64-unit SSE of two planes (ceil unit layout)
+void unit_sse(const uint8_t* a, const uint8_t* b, int w, int h, long long* out) {
+  const int ux = (w + 63) / 64, uy = (h + 63) / 64;
+  std::fill(out, out + ux * uy, 0LL);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const int d = (int)a[(size_t)y * w + x] - (int)b[(size_t)y * w + x];
+      out[(y / 64) * ux + x / 64] += d * d;
+    }
+}
 // run f(row) for rows [0, n) on up to hardware_concurrency threads (disjoint outputs)
 template <class F> void parallel_rows(int n, F f) {
   const int nt = std::max(1, std::min(n, (int)std::thread::hardware_concurrency()));
@@ -1523,9 +1676,42 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
       if (!mode_skip(fd.mode[b])) active[((b / g.bw) / 4) * g.sbw + (b % g.bw) / 4] = 1;
     fd.cdef_idx.assign(nfb, -1);
     cdef_choose(sy.data(), su.data(), active.data(), nfb, fd.fp.cdef_y, fd.fp.cdef_uv, fd.cdef_idx.data());
-    // final recon: CDEF applied to the deblocked frame
+    // final recon: CDEF applied to the deblocked frame, then the self-guided restoration
+    // search per 64x64 unit on the CDEF output (off / candidate sets, SSE + rate)
     Planes fin;
     loop_filters(g, fd.fp, fd.mode.data(), fd.cdef_idx.data(), rec, fin);
+    fd.lr.assign((size_t)3 * g.lr_nu() * 3, 0);
+    const long long rate = lr_rate_cost(qidx);
+    for (int p = 0; p < 3; ++p) {
+      const int pw = p ? W / 2 : W, ph = p ? H / 2 : H, nu = g.lr_ux(p) * g.lr_uy(p);
+      const std::vector<uint8_t>& X = p == 0 ? fin.y : (p == 1 ? fin.u : fin.v);
+      const std::vector<uint8_t>& Sp = p == 0 ? S.y : (p == 1 ? S.u : S.v);
+      int32_t* P = fd.lr.data() + (size_t)p * g.lr_nu() * 3;
+      std::vector<long long> best(nu);
+      unit_sse(Sp.data(), X.data(), pw, ph, best.data());
+      for (int u = 0; u < nu; ++u) P[3 * u] = -1, P[3 * u + 1] = P[3 * u + 2] = 0;
+      for (int k = 0; k < kNumLrSets; ++k) {
+        const int set = lr_set(k);
+        std::vector<int64_t> st((size_t)nu * 5);
+        sgr_stats(Sp.data(), X.data(), pw, ph, set, st.data());
+        std::vector<int32_t> prm((size_t)nu * 3);
+        for (int u = 0; u < nu; ++u) {
+          prm[3 * u] = set;
+          sgr_solve((const long long*)&st[5 * u], sgr_param(set, 0), sgr_param(set, 2), &prm[3 * u + 1],
+                    &prm[3 * u + 2]);
+        }
+        std::vector<uint8_t> o(X.size());
+        sgr_apply(X.data(), pw, ph, prm.data(), o.data());
+        std::vector<long long> e(nu);
+        unit_sse(Sp.data(), o.data(), pw, ph, e.data());
+        for (int u = 0; u < nu; ++u)
+          if (e[u] + rate < best[u]) {
+            best[u] = e[u] + rate;
+            P[3 * u] = set, P[3 * u + 1] = prm[3 * u + 1], P[3 * u + 2] = prm[3 * u + 2];
+          }
+      }
+    }
+    apply_lr(g, fd.lr.data(), fin);
     out.recon.push_back(std::move(fin));
     out.frames.push_back(std::move(fd));
   }
@@ -1598,7 +1784,7 @@ const char* tv_av1c_last_error() { return g_codec_err.c_str(); }
 // mv [n][nblk] and levels ly [n][nblk][256], lu / lv [n][nblk][64] (may be null).
 int tv_av1c_golden_encode(int dw, int dh, int n, const uint8_t* yuv, int qidx, void* out, int64_t* tu_sizes,
                           uint8_t* recon, uint32_t* mode, uint32_t* mv, int16_t* ly, int16_t* lu, int16_t* lv,
-                          int32_t* fparams, int8_t* cdef) {
+                          int32_t* fparams, int8_t* cdef, int32_t* lr) {
   return codec_guard([&] {
     const SeqGeo g = make_seq_geo(dw, dh);
     const size_t fsz = (size_t)g.W * g.H * 3 / 2;
@@ -1621,6 +1807,7 @@ int tv_av1c_golden_encode(int dw, int dh, int n, const uint8_t* yuv, int qidx, v
       if (lv) std::memcpy(lv + (size_t)i * nb * 64, fd.lv.data(), sizeof(int16_t) * nb * 64);
       if (fparams) pack_fparams(fd.fp, fparams + (size_t)i * 25);
       if (cdef) std::memcpy(cdef + (size_t)i * g.nsb(), fd.cdef_idx.data(), g.nsb());
+      if (lr) std::memcpy(lr + (size_t)i * fd.lr.size(), fd.lr.data(), sizeof(int32_t) * fd.lr.size());
     }
   });
 }
@@ -1649,8 +1836,8 @@ int tv_av1c_probe(const uint8_t* data, size_t n, int* geo, int* nframes) {
 
 // Write one frame's temporal unit from engine decisions (packed levels layout).
 int tv_av1c_write_tu(int dw, int dh, const int* fparams, const uint32_t* mode, const uint32_t* mv, const int16_t* ly,
-                     const int16_t* lu, const int16_t* lv, const int8_t* cdef_idx, int packed, int seq_header,
-                     void* out) {
+                     const int16_t* lu, const int16_t* lv, const int8_t* cdef_idx, const int32_t* lr, int packed,
+                     int seq_header, void* out) {
   return codec_guard([&] {
     const SeqGeo g = make_seq_geo(dw, dh);
     FrameDecisions d;
@@ -1661,6 +1848,7 @@ int tv_av1c_write_tu(int dw, int dh, const int* fparams, const uint32_t* mode, c
     d.lu = lu;
     d.lv = lv;
     d.cdef_idx = cdef_idx;
+    d.lr = lr;
     d.packed = packed != 0;
     auto tu = write_temporal_unit(g, d, seq_header != 0);
     auto* bytes = static_cast<std::vector<uint8_t>*>(out);

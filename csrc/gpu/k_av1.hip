@@ -78,6 +78,42 @@ __device__ __forceinline__ void cdef_stage(const uint8_t* P, int w, int h, int x
   }
 }
 
+// cdef_filter (av1_defs.h) on taps gathered into registers: P[k][sign] primary, S[k][sign][o]
+// secondary (directions d -/+ 2); -1 = unavailable.  Same taps, same integer result.
+__device__ __forceinline__ int cdef_eval(int c, const int (&P)[2][2], const int (&S)[2][2][2], int pri, int sec,
+                                         int damping) {
+  int sum = 0, mx = c, mn = c;
+  const int pt = pri & 1;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int ptap = pt ? 3 : (k ? 2 : 4), stap = k ? 1 : 2;
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+      if (pri) {
+        const int v = P[k][sg];
+        if (v >= 0) {
+          sum += ptap * cdef_constrain(v - c, pri, damping);
+          mx = v > mx ? v : mx;
+          mn = v < mn ? v : mn;
+        }
+      }
+      if (sec) {
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const int v = S[k][sg][o];
+          if (v >= 0) {
+            sum += stap * cdef_constrain(v - c, sec, damping);
+            mx = v > mx ? v : mx;
+            mn = v < mn ? v : mn;
+          }
+        }
+      }
+    }
+  }
+  const int y0 = c + ((8 + sum - (sum < 0)) >> 4);
+  return clip3(mn, mx, y0);
+}
+
 __device__ __forceinline__ int cdef_tile_filter(const int16_t (*T)[kTile], int ty, int tx, int pri, int sec, int dmp,
                                                 int d) {
   auto get = [&](int dy, int dx) -> int { return T[ty + dy][tx + dx]; };
@@ -99,26 +135,55 @@ __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__
   cdef_stage(rec + po, w, h, x0, y0, fbw, fbh, T);
   if (threadIdx.x < kCdefPresets) acc[threadIdx.x] = 0;
   __syncthreads();
-  // evaluated presets (pmask bits) spread over the 256 threads: thread -> (preset, pixel group)
-  const int np = __popcll(pmask), ng = 256 / np;
-  const int pi = threadIdx.x % np, g = threadIdx.x / np;
-  int p = 0;
-  for (int k = 0, seen = 0; k < kCdefPresets; ++k)
-    if (pmask >> k & 1) {
-      if (seen == pi) p = k;
-      ++seen;
+  // Pixel-major: each thread gathers a pixel's 12 CDEF taps from the tile once and
+  // evaluates up to 16 presets of pmask from registers (cdef_eval = cdef_filter's
+  // arithmetic on the gathered taps), so the LDS is read once per pixel and chunk.
+  __shared__ int8_t plist[kCdefPresets];
+  if (threadIdx.x == 0)
+    for (int k = 0, n = 0; k < kCdefPresets; ++k)
+      if (pmask >> k & 1) plist[n++] = (int8_t)k;
+  __syncthreads();
+  const int np = __popcll(pmask), npx = fbw * fbh;
+  for (int c0 = 0; c0 < np; c0 += 16) {
+    const int nc = min(16, np - c0);
+    unsigned a16[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a16[k] = 0;
+    for (int q = threadIdx.x; q < npx; q += 256) {
+      const int i = q / fbw, j = q - i * fbw, x = x0 + j, y = y0 + i;
+      const long kb = (long)b * luma_n8 + (y >> bs_l2) * luma_w8 + (x >> bs_l2);
+      const int d = dir[kb], vr = chroma ? 0 : var[kb];
+      const int ty = i + kHalo, tx = j + kHalo, c = T[ty][tx];
+      int P[2][2], Sd[2][2][2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) {
+          const int m = sg ? 1 : -1;
+          P[k][sg] = T[ty + m * cdef_dir_dy(d, k)][tx + m * cdef_dir_dx(d, k)];
+#pragma unroll
+          for (int o = 0; o < 2; ++o) {
+            const int d2 = (d + (o ? 2 : -2)) & 7;
+            Sd[k][sg][o] = T[ty + m * cdef_dir_dy(d2, k)][tx + m * cdef_dir_dx(d2, k)];
+          }
+        }
+      const int e0 = (int)src[po + (long)y * w + x];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k >= nc) break;
+        const int pp = plist[c0 + k];
+        const int psec = cdef_sec_value(pp & 3), ppri = pp >> 2;
+        const int pri = chroma ? ppri : cdef_adjust_strength(ppri, vr);
+        const int f = (pri | psec) ? cdef_eval(c, P, Sd, pri, psec, dmp) : c;
+        const int e = f - e0;
+        a16[k] += (unsigned)(e * e);
+      }
     }
-  const int psec = cdef_sec_value(p & 3), ppri = p >> 2;
-  unsigned s = 0;  // <= 1024 pixels x 255^2 fits in 32 bits
-  for (int q = g; q < fbw * fbh && g < ng; q += ng) {
-    const int i = q / fbw, j = q - i * fbw, x = x0 + j, y = y0 + i;
-    const long k = (long)b * luma_n8 + (y >> bs_l2) * luma_w8 + (x >> bs_l2);
-    const int pri = chroma ? ppri : cdef_adjust_strength(ppri, var[k]);
-    const int f = (pri | psec) ? cdef_tile_filter(T, i + kHalo, j + kHalo, pri, psec, dmp, dir[k]) : T[i + kHalo][j + kHalo];
-    const int e = f - (int)src[po + (long)y * w + x];
-    s += (unsigned)(e * e);
+    for (int k = 0; k < nc; ++k) {
+      const unsigned v = a16[k];
+      if (v) atomicAdd(&acc[plist[c0 + k]], (unsigned long long)v);
+    }
   }
-  if (g < ng) atomicAdd(&acc[p], (unsigned long long)s);
   __syncthreads();
   const int nfb = nfx * ((h + fbs - 1) / fbs);
   if (threadIdx.x < kCdefPresets)

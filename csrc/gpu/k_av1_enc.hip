@@ -22,6 +22,7 @@
 #include <string>
 
 #include "gpu_common.h"
+#include "tv/av1_defs.h"
 #include "tv/av1_enc.h"
 #include "tv/av1_txfm.h"
 
@@ -515,6 +516,18 @@ __global__ void __launch_bounds__(256) k_av1e_cdef_choose(const unsigned long lo
   }
 }
 
+// ================================================================= loop restoration =====
+// per (segment, unit): projection weights of parameter set `set` from sgr_stats
+__global__ void k_av1e_lr_solve(const long long* __restrict__ st, int nu, int B, int set, int* __restrict__ prm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nu * B) return;
+  int x0, x1;
+  sgr_solve(st + 5L * i, sgr_param(set, 0), sgr_param(set, 2), &x0, &x1);
+  prm[3L * i] = set;
+  prm[3L * i + 1] = x0;
+  prm[3L * i + 2] = x1;
+}
+
 // ================================================================= host helpers =========
 thread_local std::string g_err;
 int status(const char* what) {
@@ -601,6 +614,16 @@ int tv_av1e_lfinfo(const uint32_t* mode, int W, int H, int B, const int* lvl, ui
   const int n = (W >> 2) * (H >> 2);
   k_av1e_lfinfo<<<dim3((n + 255) / 256, B), 256, 0, (hipStream_t)stream>>>(mode, W, H, lvl, iy, iu, iv);
   return status("av1e_lfinfo");
+}
+
+// st [B][nu][5] (tv_gpu_sgr_stats) -> prm [B][nu][3] = (set, xqd0, xqd1)
+int tv_av1e_lr_solve(const long long* st, int nu, int B, int set, int* prm, void* stream) {
+  if (nu < 1 || B < 1 || set < 0 || set > 15) {
+    g_err = "av1e_lr_solve: bad arguments";
+    return -1;
+  }
+  k_av1e_lr_solve<<<(nu * B + 255) / 256, 256, 0, (hipStream_t)stream>>>(st, nu, B, set, prm);
+  return status("av1e_lr_solve");
 }
 
 // sse_* [B][nfb][64]; tabs [B][16] (8 luma + 8 chroma presets); fbidx / py / puv [B][nfb]

@@ -19,6 +19,10 @@ struct SeqGeo {
   int sbw, sbh;
   int nblk() const { return bw * bh; }
   int nsb() const { return sbw * sbh; }
+  // 64x64 restoration units of plane p (ceil layout; plane 0 has the most)
+  int lr_ux(int p) const { return ((p ? W / 2 : W) + 63) / 64; }
+  int lr_uy(int p) const { return ((p ? H / 2 : H) + 63) / 64; }
+  int lr_nu() const { return lr_ux(0) * lr_uy(0); }
 };
 SeqGeo make_seq_geo(int dw, int dh);
 
@@ -46,6 +50,7 @@ struct FrameDecisions {
   const int16_t* lu = nullptr;      // [..][64]
   const int16_t* lv = nullptr;      // [..][64]
   const int8_t* cdef_idx = nullptr; // [nsb]  (-1: every block of the SB is skip)
+  const int32_t* lr = nullptr;      // [3][nu_luma][3] per plane, per 64x64 unit: (sgr set | -1, xqd0, xqd1)
   bool packed = false;
 };
 
@@ -55,6 +60,7 @@ struct FrameData {
   std::vector<uint32_t> mode, mv;
   std::vector<int16_t> ly, lu, lv;  // full (unpacked) [nblk][256|64]
   std::vector<int8_t> cdef_idx;
+  std::vector<int32_t> lr;          // [3][nu_luma][3]
   FrameDecisions view() const;
 };
 

@@ -265,6 +265,54 @@ constexpr int kCdefPriY[8] = {0, 1, 2, 3, 5, 7, 10, 13}, kCdefPriUV[4] = {0, 2, 
 constexpr uint64_t kCdefMaskY = cdef_mask(kCdefPriY, 8, kCdefSec, 2);
 constexpr uint64_t kCdefMaskUV = cdef_mask(kCdefPriUV, 4, kCdefSec, 2);
 
+// ---------------------------------------------------------------- loop restoration ------
+// Self-guided restoration (SGRPROJ) per 64x64 unit of each plane: candidate parameter sets
+// (Sgr_Params rows), projection weights by an integer least-squares solve, unit on/off by
+// SSE + rate.  xqd ranges / reference mid of the AV1 syntax (Sgrproj_Xqd_Min/Max/Mid).
+constexpr int kNumLrSets = 2;
+TV_HD int lr_set(int i) { return i == 0 ? 4 : 10; }
+constexpr int kXqdMin0 = -96, kXqdMax0 = 31, kXqdMin1 = -32, kXqdMax1 = 95, kXqdMid0 = -32, kXqdMid1 = 31;
+TV_HD int bitlen64(unsigned long long v) {
+  int n = 0;
+  while (v) {
+    ++n;
+    v >>= 1;
+  }
+  return n;
+}
+TV_HD long long div_round(long long n, long long d) { return n >= 0 ? (n + d / 2) / d : -((-n + d / 2) / d); }
+// (x0, x1) of a unit from its sgr_stats (H00 H01 H11 c0 c1): stats scaled below 2^30 so the
+// 2x2 Cramer solve stays in 64 bits; radius-0 passes get the syntax's implied values.
+TV_HD void sgr_solve(const long long* st, int r0, int r1, int* x0, int* x1) {
+  unsigned long long m = 0;
+  for (int i = 0; i < 5; ++i) {
+    const unsigned long long a = (unsigned long long)(st[i] < 0 ? -st[i] : st[i]);
+    m = a > m ? a : m;
+  }
+  const int sh = tv_max(0, bitlen64(m) - 30);
+  const long long H00 = (st[0] >> sh) + 1, H01 = st[1] >> sh, H11 = (st[2] >> sh) + 1, c0 = st[3] >> sh,
+                  c1 = st[4] >> sh;
+  long long a = 0, b = 0;
+  if (r0 && r1) {
+    const long long det = H00 * H11 - H01 * H01;
+    if (det > 0) {
+      a = div_round(c0 * H11 - c1 * H01, det);
+      b = div_round(H00 * c1 - H01 * c0, det);
+    }
+  } else if (r0) {
+    a = div_round(c0, H00);
+  } else {
+    b = div_round(c1, H11);
+  }
+  *x0 = r0 ? (int)clip3((long long)kXqdMin0, (long long)kXqdMax0, a) : 0;
+  *x1 = r1 ? (int)clip3((long long)kXqdMin1, (long long)kXqdMax1, b) : clip3(kXqdMin1, kXqdMax1, 128 - *x0);
+}
+// rate of a restored unit (~16 bits) in SSE units
+TV_HD long long lr_rate_cost(int q) {
+  const long long a = ac_q(q);
+  return ((a * a * 9) >> 10) * 16;
+}
+
 // ------------------------------------------------------------------ motion search -------
 // Full-pel window of +-kMeRange around the co-located block, then 8 half-pel and 8
 // quarter-pel refinements (SATD + lambda * mv bits, first minimum wins).

@@ -37,6 +37,17 @@ def test_golden_stream_decodes_to_golden_recon(w, h, q):
     assert res.tu_sizes[0] > res.tu_sizes[1]
 
 
+def test_loop_restoration_units_round_trip():
+    """Self-guided restoration units are chosen where they pay and survive the round trip
+    (use_sgrproj / lr_sgr_set / subexp-coded weights)."""
+    w, h = 192, 128
+    frames = _frames(3, w, h, 2)
+    res = av1.golden_encode(frames, w, h, 60)
+    assert (res.lr[..., 0] >= 0).sum() >= 4
+    dec = av1.decode(res.stream)
+    np.testing.assert_array_equal(dec.frames, res.recon)
+
+
 def test_higher_qindex_means_fewer_bits_lower_psnr():
     w, h = 128, 64
     frames = _frames(9, w, h, 3)
@@ -60,7 +71,7 @@ def test_packed_writer_matches_golden_stream():
             packed.append(np.ascontiguousarray(lev[nz]) if nz.any() else np.zeros((1, lev.shape[1]), np.int16))
         out = av1.write_tu(w, h, res.fparams[k], np.ascontiguousarray(mode), np.ascontiguousarray(res.mv[k]),
                            packed[0], packed[1], packed[2], np.ascontiguousarray(res.cdef_idx[k]), packed=True,
-                           seq_header=(k == 0))
+                           seq_header=(k == 0), lr=res.lr[k])
         assert out == tus[k]
 
 
@@ -105,6 +116,7 @@ def _gpu_vs_golden(w, h, starts, nframes, q):
         np.testing.assert_array_equal(g.mv[:, b], gold.mv, err_msg=f"segment {b}: motion vectors")
         np.testing.assert_array_equal(g.tabs[:, b, :8], gold.fparams[:, 9:17])
         np.testing.assert_array_equal(g.fbidx[:, b], gold.cdef_idx)
+        np.testing.assert_array_equal(g.lr[:, b], gold.lr, err_msg=f"segment {b}: restoration units")
         tus = futs[b].result()
         assert b"".join(tus) == gold.stream, f"segment {b}: GPU bitstream differs from the golden encoder"
         last = gold.recon[-1]

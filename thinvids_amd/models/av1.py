@@ -42,11 +42,11 @@ def _lib():
         i = C.c_int
         lib.tv_av1c_last_error.restype = C.c_char_p
         lib.tv_av1c_golden_encode.argtypes = [i, i, i, u8p, i, vp, i64p, u8p, u32p, u32p, i16p, i16p, i16p, i32p,
-                                                i8p]
+                                                i8p, i32p]
         lib.tv_av1c_golden_encode.restype = i
         lib.tv_av1c_decode.argtypes = [u8p, C.c_size_t, i, u8p, i32p, i32p]
         lib.tv_av1c_decode.restype = i
-        lib.tv_av1c_write_tu.argtypes = [i, i, i32p, u32p, u32p, i16p, i16p, i16p, i8p, i, i, vp]
+        lib.tv_av1c_write_tu.argtypes = [i, i, i32p, u32p, u32p, i16p, i16p, i16p, i8p, i32p, i, i, vp]
         lib.tv_av1c_write_tu.restype = i
         lib._av1c_sigs = True
     return lib
@@ -95,6 +95,7 @@ class GoldenResult:
     lv: np.ndarray
     fparams: np.ndarray  # (n, 25) int32 (frame_params layout)
     cdef_idx: np.ndarray  # (n, nsb) int8
+    lr: np.ndarray  # (n, 3, nu, 3) int32: per plane / 64x64 unit (sgr set | -1, xqd0, xqd1)
 
 
 def pack_i420(frames, W: int, H: int) -> np.ndarray:
@@ -132,11 +133,18 @@ def golden_encode(frames, width: int, height: int, qindex: int) -> GoldenResult:
     lv = np.zeros((n, nb, 64), np.int16)
     fparams = np.zeros((n, 25), np.int32)
     cdef = np.zeros((n, ((W + 63) // 64) * ((H + 63) // 64)), np.int8)
+    lr = np.zeros((n, 3, lr_units(W, H), 3), np.int32)
     _check(_lib().tv_av1c_golden_encode(width, height, n, ptr(yuv), qindex, out.h, sizes.ctypes.data_as(i64p),
                                         ptr(recon), mode.ctypes.data_as(u32p), mv.ctypes.data_as(u32p),
                                         ly.ctypes.data_as(i16p), lu.ctypes.data_as(i16p), lv.ctypes.data_as(i16p),
-                                        fparams.ctypes.data_as(i32p), cdef.ctypes.data_as(i8p)))
-    return GoldenResult(out.tobytes(), sizes.tolist(), recon, mode, mv, ly, lu, lv, fparams, cdef)
+                                        fparams.ctypes.data_as(i32p), cdef.ctypes.data_as(i8p),
+                                        lr.ctypes.data_as(i32p)))
+    return GoldenResult(out.tobytes(), sizes.tolist(), recon, mode, mv, ly, lu, lv, fparams, cdef, lr)
+
+
+def lr_units(W: int, H: int) -> int:
+    """64x64 restoration units of the luma plane (ceil layout; the lr array's unit stride)."""
+    return ((W + 63) // 64) * ((H + 63) // 64)
 
 
 @dataclass
@@ -193,13 +201,14 @@ def frame_params(key: bool, qindex: int, lf, sharp: int, damping: int, cdef_y, c
 
 def write_tu(width: int, height: int, fparams: np.ndarray, mode: np.ndarray, mv: np.ndarray, ly: np.ndarray,
              lu: np.ndarray, lv: np.ndarray, cdef_idx: np.ndarray, packed: bool, seq_header: bool,
-             out: Bytes | None = None) -> bytes | None:
+             out: Bytes | None = None, lr: np.ndarray | None = None) -> bytes | None:
     """One frame's temporal unit from engine decisions (appended to `out` when given)."""
     o = out if out is not None else Bytes()
     _check(_lib().tv_av1c_write_tu(width, height, fparams.ctypes.data_as(i32p), mode.ctypes.data_as(u32p),
                                    mv.ctypes.data_as(u32p), ly.ctypes.data_as(i16p), lu.ctypes.data_as(i16p),
-                                   lv.ctypes.data_as(i16p), cdef_idx.ctypes.data_as(i8p), int(packed),
-                                   int(seq_header), o.h))
+                                   lv.ctypes.data_as(i16p), cdef_idx.ctypes.data_as(i8p),
+                                   None if lr is None else np.ascontiguousarray(lr, np.int32).ctypes.data_as(i32p),
+                                   int(packed), int(seq_header), o.h))
     return None if out is not None else o.tobytes()
 
 

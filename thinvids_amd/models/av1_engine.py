@@ -45,7 +45,7 @@ def _gpu():
 
     lib = gpu_lib()
     if not getattr(lib, "_av1e_sigs", False):
-        for n in ("tv_av1e_inter", "tv_av1e_intra", "tv_av1e_lfinfo", "tv_av1e_cdef_choose"):
+        for n in ("tv_av1e_inter", "tv_av1e_intra", "tv_av1e_lfinfo", "tv_av1e_cdef_choose", "tv_av1e_lr_solve"):
             getattr(lib, n).restype = C.c_int
         lib.tv_av1e_last_error.restype = C.c_char_p
         lib._av1e_sigs = True
@@ -59,6 +59,15 @@ def _ok(rc: int):
 
 def _p(t):
     return _vp(t.data_ptr())
+
+
+LR_SETS = (4, 10)  # av1_enc.h lr_set()
+
+
+def lr_rate_cost(q: int) -> int:
+    """Rate of a restored unit in SSE units (av1_enc.h lr_rate_cost)."""
+    a = av1m.ac_q(q)
+    return ((a * a * 9) >> 10) * 16
 
 
 def lf_level(q: int) -> int:
@@ -78,6 +87,7 @@ class GopHost:
     sse: np.ndarray      # (F, B, 3) int64
     key: list            # per frame
     qm: np.ndarray = None  # (F, B) q-index per frame and segment
+    lr: np.ndarray = None  # (F, B, 3, nu, 3) restoration units (set | -1, xqd0, xqd1)
 
 
 class Av1GpuEngine:
@@ -93,6 +103,8 @@ class Av1GpuEngine:
         self.dev = torch.device("cuda", device)
         self.nb = (self.W // 16) * (self.H // 16)
         self.nfb = ((self.W + 63) // 64) * ((self.H + 63) // 64)
+        self.nu = av1m.lr_units(self.W, self.H)
+        self.lr_enabled = True
         self.lvl = self._lf_level()
         self.damping = 3 + (self.q >> 6)
         B, H, W = batch, self.H, self.W
@@ -122,10 +134,11 @@ class Av1GpuEngine:
         self.g_tabs = torch.zeros((F, B, 16), dtype=torch.uint8, device=d)
         self.g_fbidx = torch.zeros((F, B, nfb), dtype=torch.int8, device=d)
         self.g_sse = torch.zeros((F, B, 3), dtype=torch.int64, device=d)
+        self.g_lr = torch.zeros((F, B, 3, self.nu, 3), dtype=torch.int32, device=d)
         self._gop_cap = F
 
     # ------------------------------------------------------------------ one frame ----
-    def _frame(self, t: int, key: bool, nseg: int, qarr, lvl):
+    def _frame(self, t: int, key: bool, nseg: int, qarr, lvl, q_rate):
         from ..ops import av1 as ops
 
         torch = self.torch
@@ -161,6 +174,8 @@ class Av1GpuEngine:
         self.fin = (ops.cdef_apply(dy, dirs, var, py, False, self.damping),
                     ops.cdef_apply(du, dirs, var, puv, True, self.damping, luma_w8=W // 8),
                     ops.cdef_apply(dv, dirs, var, puv, True, self.damping, luma_w8=W // 8))
+        if self.lr_enabled:
+            self.fin = self._restore(t, B, q_rate)
         w, h = self.w, self.h
         if B < self.B:  # keep full-batch planes: the slice's final frames become the reference
             fin = [torch.empty_like(x) for x in self.src]
@@ -171,6 +186,43 @@ class Av1GpuEngine:
             ss = (slice(0, B), slice(0, h >> (c > 0)), slice(0, w >> (c > 0)))
             d = s[ss].to(torch.int32) - f[ss].to(torch.int32)
             self.g_sse[t, :B, c] = (d * d).sum(dim=(1, 2))
+
+    def _unit_sse(self, a, b):
+        """(B, h, w) uint8 pair -> per-64x64-unit SSE (B, units) int64 (ceil layout)."""
+        torch = self.torch
+        d = a.to(torch.int32) - b.to(torch.int32)
+        d = d * d
+        B, h, w = d.shape
+        ph, pw = -(-h // 64) * 64, -(-w // 64) * 64
+        d = torch.nn.functional.pad(d, (0, pw - w, 0, ph - h))
+        return d.reshape(B, ph // 64, 64, pw // 64, 64).sum((2, 4), dtype=torch.int64).reshape(B, -1)
+
+    def _restore(self, t: int, B: int, rate):
+        """Self-guided restoration search + apply on the CDEF output (the golden encoder's
+        per-unit off / set-4 / set-10 choice, SSE + rate, first minimum)."""
+        from ..ops import av1 as ops
+
+        torch = self.torch
+        lib = _gpu()
+        st = _vp(torch.cuda.current_stream(self.dev).cuda_stream)
+        out = []
+        for p, (S, X) in enumerate(zip((x[:B] for x in self.src), self.fin)):
+            h, w = X.shape[1], X.shape[2]
+            nu = (-(-h // 64)) * (-(-w // 64))
+            best = self._unit_sse(S, X)
+            prm_best = torch.zeros((B, nu, 3), dtype=torch.int32, device=self.dev)
+            prm_best[..., 0] = -1
+            for s in LR_SETS:
+                sts = ops.sgr_stats(S, X, s)
+                prm = torch.empty((B, nu, 3), dtype=torch.int32, device=self.dev)
+                _ok(lib.tv_av1e_lr_solve(_p(sts), nu, B, s, _p(prm), st))
+                e = self._unit_sse(S, ops.sgr_apply(X, prm)) + rate[:, None]
+                better = e < best
+                best = torch.where(better, e, best)
+                prm_best = torch.where(better[..., None], prm, prm_best)
+            self.g_lr[t, :B, p, :nu] = prm_best
+            out.append(ops.sgr_apply(X, prm_best))
+        return tuple(out)
 
     def encode_gop(self, nframes: int, load_frame, nseg: int | None = None, qmap=None) -> GopHost:
         """Run the GPU part of one GOP for all B segments.  load_frame(t, (Y, U, V)) fills
@@ -188,9 +240,12 @@ class Av1GpuEngine:
         lv = np.array([[[lf_level(int(x))] * 4 for x in row] for row in qm], np.int32)
         qd = torch.from_numpy(qm).to(self.dev)
         ld = torch.from_numpy(lv).to(self.dev)
+        rd = torch.from_numpy(np.array([[lr_rate_cost(int(x)) for x in row] for row in qm], np.int64)).to(self.dev)
+        if not self.lr_enabled:
+            self.g_lr[:nframes, :nseg, :, :, 0] = -1
         for t in range(nframes):
             load_frame(t, self.src)
-            self._frame(t, t == 0, nseg, qd[t], ld[t])
+            self._frame(t, t == 0, nseg, qd[t], ld[t], rd[t])
         self.qm = qm
         F = nframes
         self.nseg = nseg
@@ -210,6 +265,7 @@ class Av1GpuEngine:
             sse=self.g_sse[:F, :nseg].cpu().numpy(),
             key=[t == 0 for t in range(F)],
             qm=qm,
+            lr=self.g_lr[:F, :nseg].cpu().numpy(),
         )
         for lev, counts in packed:
             c = counts.cpu().numpy().astype(np.int64).reshape(-1)
@@ -230,7 +286,8 @@ class Av1GpuEngine:
                    for pk, n in zip(g.packed, (256, 64, 64))]
             tus.append(av1m.write_tu(self.w, self.h, fp, np.ascontiguousarray(g.mode[t, b]),
                                      np.ascontiguousarray(g.mv[t, b]), lev[0], lev[1], lev[2],
-                                     np.ascontiguousarray(g.fbidx[t, b]), packed=True, seq_header=g.key[t]))
+                                     np.ascontiguousarray(g.fbidx[t, b]), packed=True, seq_header=g.key[t],
+                                     lr=np.ascontiguousarray(g.lr[t, b])))
         return tus
 
     def submit_entropy(self, g: GopHost) -> list:

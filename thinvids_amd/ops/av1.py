@@ -273,7 +273,10 @@ def sgr_apply(rec, params):
 
     B, h, w = rec.shape
     out = torch.empty_like(rec)
-    pr = torch.as_tensor(np.asarray(params, np.int32)).to(rec.device).reshape(B, -1, 3).contiguous()
+    if isinstance(params, torch.Tensor):
+        pr = params.to(device=rec.device, dtype=torch.int32).reshape(B, -1, 3).contiguous()
+    else:
+        pr = torch.as_tensor(np.asarray(params, np.int32)).to(rec.device).reshape(B, -1, 3).contiguous()
     _check(_gpu().tv_gpu_sgr_apply(_t(rec.contiguous()), w, h, B, _t(pr), _t(out), _stream(rec)))
     return out
 
