@@ -1601,17 +1601,27 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
         } else {
           inter = 1;
           // integer search on the edge-extended reference
-          int bc = 1 << 30, bk = 0;
-          for (int k = 0; k < kMeSide * kMeSide; ++k) {
-            const int dx = me_cand_dx(k), dy = me_cand_dy(k);
+          auto fp_cost = [&](int dx, int dy) {
             int sad = 0;
             const uint8_t* rp = padY.data() + (size_t)(by * 16 + dy + kPad) * pw + bx * 16 + dx + kPad;
             for (int i = 0; i < 16; ++i)
               for (int j = 0; j < 16; ++j) sad += std::abs(s[0][i * 16 + j] - (int)rp[(size_t)i * pw + j]);
-            const int cost = sad + ((lam * (mv_comp_bits(dy * 8) + mv_comp_bits(dx * 8))) >> 4);
+            return sad + ((lam * (mv_comp_bits(dy * 8) + mv_comp_bits(dx * 8))) >> 4);
+          };
+          int bc = 1 << 30, bk = 0;
+          for (int k = 0; k < kMeGrid * kMeGrid; ++k) {
+            const int cost = fp_cost(me_cand_dx(k), me_cand_dy(k));
             if (cost < bc) bc = cost, bk = k;
           }
-          int mr = me_cand_dy(bk) * 8, mc = me_cand_dx(bk) * 8;
+          int fx = me_cand_dx(bk), fy = me_cand_dy(bk), bring = -1;
+          for (int k = 0; k < 8; ++k) {  // full-pel neighbours of the best grid point
+            const int dx = fx + me_ring_dx(k), dy = fy + me_ring_dy(k);
+            if (dx < -kMeRange || dx > kMeRange || dy < -kMeRange || dy > kMeRange) continue;
+            const int cost = fp_cost(dx, dy);
+            if (cost < bc) bc = cost, bring = k;
+          }
+          if (bring >= 0) fx += me_ring_dx(bring), fy += me_ring_dy(bring);
+          int mr = fy * 8, mc = fx * 8;
           auto sub_cost = [&](int r, int c) {
             int pr[256];
             predict(g, 0, bx, by, pack_mode(1, 0, 0, 0, 0), pack_mv(r, c), rec, ref, pr);

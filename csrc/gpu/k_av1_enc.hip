@@ -160,8 +160,23 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   uint32_t sv[64];
 #pragma unroll
   for (int i = 0; i < 64; ++i) sv[i] = reinterpret_cast<const uint32_t*>(sblk)[i];
+  // packed SAD of rows [i0, i0 + n) at full-pel offset (dx, dy)
+  auto sad_rows = [&](int dx, int dy, int i0, int n) -> unsigned {
+    unsigned sad = 0;
+    const int ox = kWinOff + dx, sh = ox & 3;
+    for (int i = i0; i < i0 + n; ++i) {
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(win + (kWinOff + dy + i) * kWinP + (ox & ~3));
+      const uint32_t* sr = reinterpret_cast<const uint32_t*>(sblk) + i * 4;
+      const uint32_t w0 = row[0], w1 = row[1], w2 = row[2], w3 = row[3], w4 = row[4];
+      sad = __builtin_amdgcn_sad_u8(sr[0], __builtin_amdgcn_alignbyte(w1, w0, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sr[1], __builtin_amdgcn_alignbyte(w2, w1, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sr[2], __builtin_amdgcn_alignbyte(w3, w2, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sr[3], __builtin_amdgcn_alignbyte(w4, w3, sh), sad);
+    }
+    return sad;
+  };
   unsigned best = 0xFFFFFFFFu;
-  for (int k = lane; k < kMeSide * kMeSide; k += 64) {
+  for (int k = lane; k < kMeGrid * kMeGrid; k += 64) {  // 2-pel grid, one candidate per lane
     const int dx = me_cand_dx(k), dy = me_cand_dy(k);
     unsigned sad = 0;
     const int ox = kWinOff + dx, sh = ox & 3;
@@ -180,7 +195,22 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   }
   best = wave_min_u32(best);
   const int bk = best & 4095;
-  int mr = me_cand_dy(bk) * 8, mc = me_cand_dx(bk) * 8;
+  int gx = me_cand_dx(bk), gy = me_cand_dy(bk);
+  {  // full-pel neighbours of the best grid point: 8 candidates x 8 lanes (2 rows each)
+    const int ci = lane >> 3, r2 = (lane & 7) * 2;
+    const int dx = gx + me_ring_dx(ci), dy = gy + me_ring_dy(ci);
+    const bool ok = dx >= -kMeRange && dx <= kMeRange && dy >= -kMeRange && dy <= kMeRange;
+    const int part = ok ? (int)sad_rows(dx, dy, r2, 2) : 0;
+    const int sad = row8_sum(part);
+    if ((lane & 7) == 0) cost[ci] = ok ? sad + ((lam * (mv_comp_bits(dy * 8) + mv_comp_bits(dx * 8))) >> 4) : -1;
+    __syncthreads();
+    int bc = (int)(best >> 12), bi = -1;
+    for (int k = 0; k < 8; ++k)
+      if (cost[k] >= 0 && cost[k] < bc) bc = cost[k], bi = k;
+    if (bi >= 0) gx += me_ring_dx(bi), gy += me_ring_dy(bi);
+    __syncthreads();
+  }
+  int mr = gy * 8, mc = gx * 8;
   // ---- sub-pel refinement: center + 8 ring candidates at step 4 (half) then 2 (quarter)
   auto wget = [&](int x, int y) -> int {  // window sample at block-relative (x, y)
     return win[(kWinOff + y) * kWinP + kWinOff + x];
@@ -528,6 +558,27 @@ __global__ void k_av1e_lr_solve(const long long* __restrict__ st, int nu, int B,
   prm[3L * i + 2] = x1;
 }
 
+// per (64x64 unit, segment): SSE of two planes over the valid region [0, vw) x [0, vh)
+__global__ void __launch_bounds__(256) k_av1e_unit_sse(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                                                       int w, int h, int vw, int vh, long long* __restrict__ out) {
+  const int u = blockIdx.x, s = blockIdx.y, ux = (w + 63) >> 6;
+  const int x0 = (u % ux) * 64, y0 = (u / ux) * 64;
+  const long po = (long)s * w * h;
+  unsigned acc = 0;  // <= 4096 * 255^2 < 2^32
+  for (int i = threadIdx.x; i < 4096; i += 256) {
+    const int x = x0 + (i & 63), y = y0 + (i >> 6);
+    if (x < vw && y < vh) {
+      const int d = (int)a[po + (long)y * w + x] - (int)b[po + (long)y * w + x];
+      acc += (unsigned)(d * d);
+    }
+  }
+  __shared__ long long tot[4];
+  const int v = wave_sum((int)acc);  // 1024 pixels x 255^2 per wave < 2^31
+  if ((threadIdx.x & 63) == 0) tot[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) out[(long)s * gridDim.x + u] = tot[0] + tot[1] + tot[2] + tot[3];
+}
+
 // ================================================================= host helpers =========
 thread_local std::string g_err;
 int status(const char* what) {
@@ -624,6 +675,18 @@ int tv_av1e_lr_solve(const long long* st, int nu, int B, int set, int* prm, void
   }
   k_av1e_lr_solve<<<(nu * B + 255) / 256, 256, 0, (hipStream_t)stream>>>(st, nu, B, set, prm);
   return status("av1e_lr_solve");
+}
+
+// out [B][units]: per-64x64-unit SSE of a / b ([B][h][w]) over the valid region vw x vh
+int tv_av1e_unit_sse(const uint8_t* a, const uint8_t* b, int w, int h, int vw, int vh, int B, long long* out,
+                     void* stream) {
+  if (w < 1 || h < 1 || B < 1 || vw > w || vh > h) {
+    g_err = "av1e_unit_sse: bad geometry";
+    return -1;
+  }
+  const int nu = ((w + 63) >> 6) * ((h + 63) >> 6);
+  k_av1e_unit_sse<<<dim3(nu, B), 256, 0, (hipStream_t)stream>>>(a, b, w, h, vw, vh, out);
+  return status("av1e_unit_sse");
 }
 
 // sse_* [B][nfb][64]; tabs [B][16] (8 luma + 8 chroma presets); fbidx / py / puv [B][nfb]

@@ -299,6 +299,14 @@ TV_HD void sgr_solve(const long long* st, int r0, int r1, int* x0, int* x1) {
       a = div_round(c0 * H11 - c1 * H01, det);
       b = div_round(H00 * c1 - H01 * c0, det);
     }
+    // outside the coded range: clamp one weight and re-solve the other given it
+    if (a < kXqdMin0 || a > kXqdMax0) {
+      a = clip3((long long)kXqdMin0, (long long)kXqdMax0, a);
+      b = div_round(c1 - H01 * a, H11);
+    } else if (b < kXqdMin1 || b > kXqdMax1) {
+      b = clip3((long long)kXqdMin1, (long long)kXqdMax1, b);
+      a = div_round(c0 - H01 * b, H00);
+    }
   } else if (r0) {
     a = div_round(c0, H00);
   } else {
@@ -314,12 +322,14 @@ TV_HD long long lr_rate_cost(int q) {
 }
 
 // ------------------------------------------------------------------ motion search -------
-// Full-pel window of +-kMeRange around the co-located block, then 8 half-pel and 8
-// quarter-pel refinements (SATD + lambda * mv bits, first minimum wins).
+// Full-pel search of +-kMeRange around the co-located block on a 2-pel grid (17 x 17), then
+// the 8 full-pel neighbours of the best grid point, then 8 half-pel and 8 quarter-pel
+// refinements (SAD / SATD + lambda * mv bits, first minimum wins at every stage).
 constexpr int kMeRange = 16;
+constexpr int kMeGrid = kMeRange + 1;  // grid points per axis (step 2)
 constexpr int kMeSide = 2 * kMeRange + 1;
-TV_HD int me_cand_dx(int k) { return k % kMeSide - kMeRange; }
-TV_HD int me_cand_dy(int k) { return k / kMeSide - kMeRange; }
+TV_HD int me_cand_dx(int k) { return 2 * (k % kMeGrid) - kMeRange; }
+TV_HD int me_cand_dy(int k) { return 2 * (k / kMeGrid) - kMeRange; }
 TV_HD int me_ring_dx(int k) { constexpr int8_t t[8] = {-1, 0, 1, -1, 1, -1, 0, 1}; return t[k]; }
 TV_HD int me_ring_dy(int k) { constexpr int8_t t[8] = {-1, -1, -1, 0, 0, 1, 1, 1}; return t[k]; }
 

@@ -45,7 +45,8 @@ def _gpu():
 
     lib = gpu_lib()
     if not getattr(lib, "_av1e_sigs", False):
-        for n in ("tv_av1e_inter", "tv_av1e_intra", "tv_av1e_lfinfo", "tv_av1e_cdef_choose", "tv_av1e_lr_solve"):
+        for n in ("tv_av1e_inter", "tv_av1e_intra", "tv_av1e_lfinfo", "tv_av1e_cdef_choose", "tv_av1e_lr_solve",
+                  "tv_av1e_unit_sse"):
             getattr(lib, n).restype = C.c_int
         lib.tv_av1e_last_error.restype = C.c_char_p
         lib._av1e_sigs = True
@@ -183,19 +184,17 @@ class Av1GpuEngine:
                 full[:B].copy_(part)
             self.fin = tuple(fin)
         for c, (s, f) in enumerate(zip(self.src, self.fin)):
-            ss = (slice(0, B), slice(0, h >> (c > 0)), slice(0, w >> (c > 0)))
-            d = s[ss].to(torch.int32) - f[ss].to(torch.int32)
-            self.g_sse[t, :B, c] = (d * d).sum(dim=(1, 2))
+            self.g_sse[t, :B, c] = self._unit_sse(s[:B], f[:B], w >> (c > 0), h >> (c > 0)).sum(dim=1)
 
-    def _unit_sse(self, a, b):
-        """(B, h, w) uint8 pair -> per-64x64-unit SSE (B, units) int64 (ceil layout)."""
+    def _unit_sse(self, a, b, vw: int | None = None, vh: int | None = None):
+        """(B, h, w) uint8 pair -> per-64x64-unit SSE (B, units) int64 (ceil layout) over
+        the valid region vw x vh (default: the whole plane); one fused kernel."""
         torch = self.torch
-        d = a.to(torch.int32) - b.to(torch.int32)
-        d = d * d
-        B, h, w = d.shape
-        ph, pw = -(-h // 64) * 64, -(-w // 64) * 64
-        d = torch.nn.functional.pad(d, (0, pw - w, 0, ph - h))
-        return d.reshape(B, ph // 64, 64, pw // 64, 64).sum((2, 4), dtype=torch.int64).reshape(B, -1)
+        B, h, w = a.shape
+        out = torch.empty((B, (-(-h // 64)) * (-(-w // 64))), dtype=torch.int64, device=self.dev)
+        _ok(_gpu().tv_av1e_unit_sse(_p(a), _p(b), w, h, w if vw is None else vw, h if vh is None else vh, B, _p(out),
+                                    _vp(torch.cuda.current_stream(self.dev).cuda_stream)))
+        return out
 
     def _restore(self, t: int, B: int, rate):
         """Self-guided restoration search + apply on the CDEF output (the golden encoder's
@@ -212,16 +211,22 @@ class Av1GpuEngine:
             best = self._unit_sse(S, X)
             prm_best = torch.zeros((B, nu, 3), dtype=torch.int32, device=self.dev)
             prm_best[..., 0] = -1
+            res = X
             for s in LR_SETS:
                 sts = ops.sgr_stats(S, X, s)
                 prm = torch.empty((B, nu, 3), dtype=torch.int32, device=self.dev)
                 _ok(lib.tv_av1e_lr_solve(_p(sts), nu, B, s, _p(prm), st))
-                e = self._unit_sse(S, ops.sgr_apply(X, prm)) + rate[:, None]
+                o = ops.sgr_apply(X, prm)
+                e = self._unit_sse(S, o) + rate[:, None]
                 better = e < best
                 best = torch.where(better, e, best)
                 prm_best = torch.where(better[..., None], prm, prm_best)
+                # the per-unit choice so far (units are disjoint: select, no re-filtering)
+                ux = -(-w // 64)
+                m = better.view(B, -1, ux).repeat_interleave(64, 1).repeat_interleave(64, 2)[:, :h, :w]
+                res = torch.where(m, o, res)
             self.g_lr[t, :B, p, :nu] = prm_best
-            out.append(ops.sgr_apply(X, prm_best))
+            out.append(res)
         return tuple(out)
 
     def encode_gop(self, nframes: int, load_frame, nseg: int | None = None, qmap=None) -> GopHost:

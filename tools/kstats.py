@@ -7,8 +7,8 @@ import sys
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)
-    n = n.replace("tv::gpu::(anonymous namespace)::", "").replace("tv::gpu::", "")
+    n = name.replace("tv::gpu::(anonymous namespace)::", "").replace("tv::gpu::", "")
+    n = re.sub(r"\(.*", "", n)
     return n[:60]
 
 
