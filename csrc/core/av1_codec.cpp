@@ -1533,10 +1533,11 @@ int satd_block(const int* a, const int* b, int N) {
 }
 }  // namespace
 
-GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qidx) {
+GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qidx0, const int* qmap) {
   GoldenOut out;
-  const int nb = g.nblk(), lam = lambda16(qidx);
+  const int nb = g.nblk();
   for (size_t f = 0; f < src.size(); ++f) {
+    const int qidx = qmap ? clip3(1, 255, qmap[f]) : qidx0, lam = lambda16(qidx);
     const Planes& S = src[f];
     const Planes* ref = f ? &out.recon.back() : nullptr;
     FrameData fd;
@@ -1792,7 +1793,8 @@ const char* tv_av1c_last_error() { return g_codec_err.c_str(); }
 // the temporal units go to `out` (one Bytes object) and their byte sizes to tu_sizes[n];
 // the post-filter reconstructions to recon (same layout); per-frame decisions to mode /
 // mv [n][nblk] and levels ly [n][nblk][256], lu / lv [n][nblk][64] (may be null).
-int tv_av1c_golden_encode(int dw, int dh, int n, const uint8_t* yuv, int qidx, void* out, int64_t* tu_sizes,
+int tv_av1c_golden_encode(int dw, int dh, int n, const uint8_t* yuv, int qidx, const int* qmap, void* out,
+                          int64_t* tu_sizes,
                           uint8_t* recon, uint32_t* mode, uint32_t* mv, int16_t* ly, int16_t* lu, int16_t* lv,
                           int32_t* fparams, int8_t* cdef, int32_t* lr) {
   return codec_guard([&] {
@@ -1800,7 +1802,7 @@ int tv_av1c_golden_encode(int dw, int dh, int n, const uint8_t* yuv, int qidx, v
     const size_t fsz = (size_t)g.W * g.H * 3 / 2;
     std::vector<Planes> src(n);
     for (int i = 0; i < n; ++i) split_planes(yuv + i * fsz, g, src[i]);
-    GoldenOut go = golden_encode(g, src, qidx);
+    GoldenOut go = golden_encode(g, src, qidx, qmap);
     auto* bytes = static_cast<std::vector<uint8_t>*>(out);
     bytes->clear();
     const int nb = g.nblk();

@@ -41,7 +41,7 @@ def _lib():
     if not getattr(lib, "_av1c_sigs", False):
         i = C.c_int
         lib.tv_av1c_last_error.restype = C.c_char_p
-        lib.tv_av1c_golden_encode.argtypes = [i, i, i, u8p, i, vp, i64p, u8p, u32p, u32p, i16p, i16p, i16p, i32p,
+        lib.tv_av1c_golden_encode.argtypes = [i, i, i, u8p, i, i32p, vp, i64p, u8p, u32p, u32p, i16p, i16p, i16p, i32p,
                                                 i8p, i32p]
         lib.tv_av1c_golden_encode.restype = i
         lib.tv_av1c_decode.argtypes = [u8p, C.c_size_t, i, u8p, i32p, i32p]
@@ -117,8 +117,9 @@ def pad_frame(frame, W: int, H: int):
             np.pad(v, ((0, H // 2 - h // 2), (0, W // 2 - w // 2)), mode="edge"))
 
 
-def golden_encode(frames, width: int, height: int, qindex: int) -> GoldenResult:
-    """C++ golden encoder over display-size (Y, U, V) frames (one closed GOP)."""
+def golden_encode(frames, width: int, height: int, qindex: int, qmap=None) -> GoldenResult:
+    """C++ golden encoder over display-size (Y, U, V) frames (one closed GOP); `qmap`
+    (optional): per-frame q-index of a rate-control plan."""
     W, H = coded_size(width, height)
     n = len(frames)
     yuv = pack_i420([pad_frame(f, W, H) for f in frames], W, H)
@@ -134,7 +135,10 @@ def golden_encode(frames, width: int, height: int, qindex: int) -> GoldenResult:
     fparams = np.zeros((n, 25), np.int32)
     cdef = np.zeros((n, ((W + 63) // 64) * ((H + 63) // 64)), np.int8)
     lr = np.zeros((n, 3, lr_units(W, H), 3), np.int32)
-    _check(_lib().tv_av1c_golden_encode(width, height, n, ptr(yuv), qindex, out.h, sizes.ctypes.data_as(i64p),
+    qm = None if qmap is None else np.ascontiguousarray(np.asarray(qmap, np.int32).reshape(n))
+    _check(_lib().tv_av1c_golden_encode(width, height, n, ptr(yuv), qindex,
+                                        None if qm is None else qm.ctypes.data_as(i32p), out.h,
+                                        sizes.ctypes.data_as(i64p),
                                         ptr(recon), mode.ctypes.data_as(u32p), mv.ctypes.data_as(u32p),
                                         ly.ctypes.data_as(i16p), lu.ctypes.data_as(i16p), lv.ctypes.data_as(i16p),
                                         fparams.ctypes.data_as(i32p), cdef.ctypes.data_as(i8p),

@@ -42,9 +42,38 @@ def log2_q8(x: int) -> int:
     return r
 
 
+def obu_frame_sizes(stream: bytes) -> list[int]:
+    """Bytes per temporal unit of an AV1 low-overhead OBU stream (one shown frame per
+    temporal unit here; the temporal delimiter and sequence header count toward it)."""
+    out: list[int] = []
+    pos, n, cur = 0, len(stream), -1
+    while pos < n:
+        start = pos
+        h = stream[pos]
+        pos += 1 + ((h >> 2) & 1)
+        size, shift = 0, 0
+        while True:
+            b = stream[pos]
+            pos += 1
+            size |= (b & 0x7F) << shift
+            shift += 7
+            if not b & 0x80:
+                break
+        pos += size
+        if (h >> 3) & 15 == 2:  # temporal delimiter: a new unit
+            out.append(0)
+            cur = len(out) - 1
+        if cur >= 0:
+            out[cur] += pos - start
+    return out
+
+
 def frame_sizes(annexb: bytes) -> list[int]:
     """Bytes per coded picture of an Annex-B stream (parameter sets count toward the next
-    picture, start codes included)."""
+    picture, start codes included); AV1 OBU streams (leading temporal delimiter) are split
+    per temporal unit."""
+    if annexb[:2] == b"\x12\x00":
+        return obu_frame_sizes(annexb)
     out: list[int] = []
     pending = 0
     i, n = 0, len(annexb)

@@ -252,7 +252,8 @@ def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None, fq=None) -> byte
         bs, recons = b"", []
         W, H = av1.coded_size(spec.width, spec.height)
         for a in range(0, len(frames), spec.gop):
-            r = av1.golden_encode(frames[a:a + spec.gop], spec.width, spec.height, spec.av1_qindex())
+            qm = None if fq is None else [av1.qindex_for_hevc_qp(int(x)) for x in fq[a:a + spec.gop]]
+            r = av1.golden_encode(frames[a:a + spec.gop], spec.width, spec.height, spec.av1_qindex(), qmap=qm)
             bs += r.stream
             for f in r.recon:
                 recons.append((f[:W * H].reshape(H, W), f[W * H:W * H * 5 // 4].reshape(H // 2, W // 2),
