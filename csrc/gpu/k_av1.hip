@@ -23,6 +23,7 @@
 
 #include "gpu_common.h"
 #include "tv/av1_defs.h"
+#include "tv/av1_enc.h"
 
 namespace tv {
 namespace gpu {
@@ -421,6 +422,78 @@ __global__ void __launch_bounds__(256) k_sgr(const uint8_t* __restrict__ src, co
   }
 }
 
+// Encoder restoration search for one parameter set, fused: guided filters once per unit,
+// projection statistics -> integer solve (sgr_solve, shared with the golden encoder) ->
+// projection + unit SSE vs the source, restored unit written to `out`.  Replaces the
+// stats / solve / apply / SSE launch chain (one filter pass instead of two).
+__global__ void __launch_bounds__(256) k_sgr_search(const uint8_t* __restrict__ src, const uint8_t* __restrict__ rec,
+                                                    int w, int h, int set, int* __restrict__ prm,
+                                                    long long* __restrict__ sse, uint8_t* __restrict__ out) {
+  const int b = blockIdx.y, u = blockIdx.x, nux = (w + kRu - 1) / kRu, nu = nux * ((h + kRu - 1) / kRu);
+  const int ux = (u % nux) * kRu, uy = (u / nux) * kRu, uw = min(kRu, w - ux), uh = min(kRu, h - uy);
+  const long po = (long)b * w * h;
+  __shared__ uint8_t T[kLrTile][kLrTile];
+  __shared__ int A[kAb][kAb], Bv[kAb][kAb];
+  __shared__ unsigned long long red[6];
+  __shared__ int xq[2];
+  lr_stage(rec + po, w, h, ux, uy, uw, uh, T);
+  if (threadIdx.x < 6) red[threadIdx.x] = 0;
+  __syncthreads();
+  const int r0 = sgr_param(set, 0), r1 = sgr_param(set, 2);
+  int f0[16], f1[16];
+  int n = 0;
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+    const int i = q / uw, j = q - i * uw;
+    f0[n] = f1[n] = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
+  }
+  if (r0) sgr_guided(T, w, h, ux, uy, uw, uh, r0, sgr_param(set, 1), A, Bv, f0);
+  if (r1) sgr_guided(T, w, h, ux, uy, uw, uh, r1, sgr_param(set, 3), A, Bv, f1);
+  long long a[5] = {0, 0, 0, 0, 0};
+  n = 0;
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+    const int i = q / uw, j = q - i * uw;
+    const int uu = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
+    const long long da = f0[n] - uu, db = f1[n] - uu;
+    const long long e = ((long long)(((int)src[po + (long)(uy + i) * w + ux + j]) << kSgrRstBits) - uu) << kSgrPrjBits;
+    a[0] += da * da;
+    a[1] += da * db;
+    a[2] += db * db;
+    a[3] += da * e;
+    a[4] += db * e;
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const long long v = wave_sum64(a[k]);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&red[k], (unsigned long long)v);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long st[5];
+    for (int k = 0; k < 5; ++k) st[k] = (long long)red[k];
+    sgr_solve(st, r0, r1, &xq[0], &xq[1]);
+    int* P = prm + ((long)b * nu + u) * 3;
+    P[0] = set;
+    P[1] = xq[0];
+    P[2] = xq[1];
+  }
+  __syncthreads();
+  const int w0 = xq[0], w1 = xq[1];
+  long long e2 = 0;
+  n = 0;
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+    const int i = q / uw, j = q - i * uw;
+    const int x = (int)T[i + kLrHalo][j + kLrHalo];
+    const int o = sgr_project(x, f0[n], f1[n], r0, r1, w0, w1);
+    out[po + (long)(uy + i) * w + ux + j] = (uint8_t)o;
+    const int d = o - (int)src[po + (long)(uy + i) * w + ux + j];
+    e2 += d * d;
+  }
+  const long long v = wave_sum64(e2);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&red[5], (unsigned long long)v);
+  __syncthreads();
+  if (threadIdx.x == 0) sse[(long)b * nu + u] = (long long)red[5];
+}
+
 // ----------------------------------------------------------------- deblocking filter ----
 // k_deblock: one workgroup per 64x64 output tile.  The tile plus an 8-pixel ring is staged
 // in LDS once (dword loads); the vertical edges x0..x0+64 are filtered on all 80 rows (the
@@ -519,6 +592,13 @@ int tv_gpu_cdef_apply(const uint8_t* rec, int w, int h, int B, int chroma, const
   k_cdef_apply<<<dim3(nfb, B), 256, 0, (hipStream_t)stream>>>(rec, w, h, chroma, dir, var, luma_w8, luma_n8, damping,
                                                               fb_preset, out);
   return av1_status("cdef_apply");
+}
+// encoder restoration search of set `set`: prm [B][nu][3], unit SSE [B][nu], restored planes
+int tv_gpu_sgr_search(const uint8_t* src, const uint8_t* rec, int w, int h, int B, int set, int* prm, long long* sse,
+                      uint8_t* out, void* stream) {
+  if (bad_geo(w, h, B, 2, "sgr_search") || set < 0 || set > 15) return -1;
+  k_sgr_search<<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, set, prm, sse, out);
+  return av1_status("sgr_search");
 }
 int tv_gpu_wiener_apply(const uint8_t* rec, int w, int h, int B, const int* coef, uint8_t* out, void* stream) {
   if (bad_geo(w, h, B, 2, "wiener_apply")) return -1;

@@ -22,6 +22,7 @@
 #include <string>
 
 #include "gpu_common.h"
+#include "mfma_exact.h"
 #include "tv/av1_defs.h"
 #include "tv/av1_enc.h"
 #include "tv/av1_txfm.h"
@@ -68,6 +69,31 @@ __device__ __forceinline__ const int32_t* basis(int lg, int type) {
 // One N x N 2-D transform on the calling wave (LDS in -> LDS out), the stages of
 // txfm2d_ref: forward tmp = Bc X (round f1), C = tmp Br^T (round f2); inverse
 // g = X Br (round i1), out = Bc^T g (round i2); int16 clamps after each stage.
+template <int LG>
+__device__ void wave_txfm(const int16_t* in, int16_t* tmp, int16_t* out, int tcol, int trow, bool inverse);
+
+// 16x16 on the matrix cores: each stage is one exact 16x16x16 tile (mfma_exact.h, four
+// v_mfma_f32_16x16x16f16 per stage), same integers as the VALU form below.
+template <>
+__device__ void wave_txfm<4>(const int16_t* in, int16_t* tmp, int16_t* out, int tcol, int trow, bool inverse) {
+  const int lane = threadIdx.x & 63, row0 = (lane >> 4) * 4, col = lane & 15;
+  const int32_t* Bc = basis(4, tcol);
+  const int32_t* Br = basis(4, trow);
+  constexpr int f1 = 12 + (4 - 1) / 2 - 2, f2 = 12 + 4 / 2 - 1, i1 = 13 + 4 / 2, i2 = 14 + (4 - 1) / 2;
+  long long o[4];
+  if (!inverse) exact_tile([&](int r, int k) { return (int)Bc[r * 16 + k]; }, [&](int k, int c) { return (int)in[k * 16 + c]; }, 0, 0, 16, o);
+  else exact_tile([&](int r, int k) { return (int)in[r * 16 + k]; }, [&](int k, int c) { return (int)Br[k * 16 + c]; }, 0, 0, 16, o);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tmp[(row0 + r) * 16 + col] = (int16_t)c16(rsr(o[r], inverse ? i1 : f1));
+  __syncthreads();
+  if (!inverse) exact_tile([&](int r, int k) { return (int)tmp[r * 16 + k]; }, [&](int k, int c) { return (int)Br[c * 16 + k]; }, 0, 0, 16, o);
+  else exact_tile([&](int r, int k) { return (int)Bc[k * 16 + r]; }, [&](int k, int c) { return (int)tmp[k * 16 + c]; }, 0, 0, 16, o);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) out[(row0 + r) * 16 + col] = (int16_t)c16(rsr(o[r], inverse ? i2 : f2));
+  __syncthreads();
+}
+
+// 8x8 (chroma): one lane per output, VALU
 template <int LG>
 __device__ void wave_txfm(const int16_t* in, int16_t* tmp, int16_t* out, int tcol, int trow, bool inverse) {
   constexpr int N = 1 << LG;

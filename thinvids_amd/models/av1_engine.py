@@ -212,12 +212,14 @@ class Av1GpuEngine:
             prm_best = torch.zeros((B, nu, 3), dtype=torch.int32, device=self.dev)
             prm_best[..., 0] = -1
             res = X
-            for s in LR_SETS:
-                sts = ops.sgr_stats(S, X, s)
+            for s in LR_SETS:  # fused stats -> solve -> project + SSE per unit (k_sgr_search)
                 prm = torch.empty((B, nu, 3), dtype=torch.int32, device=self.dev)
-                _ok(lib.tv_av1e_lr_solve(_p(sts), nu, B, s, _p(prm), st))
-                o = ops.sgr_apply(X, prm)
-                e = self._unit_sse(S, o) + rate[:, None]
+                e = torch.empty((B, nu), dtype=torch.int64, device=self.dev)
+                o = torch.empty_like(X)
+                rc = ops._gpu().tv_gpu_sgr_search(_p(S), _p(X), w, h, B, s, _p(prm), _p(e), _p(o), st)
+                if rc != 0:
+                    raise RuntimeError(ops._gpu().tv_av1_gpu_last_error().decode())
+                e = e + rate[:, None]
                 better = e < best
                 best = torch.where(better, e, best)
                 prm_best = torch.where(better[..., None], prm, prm_best)
