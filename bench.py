@@ -330,8 +330,10 @@ def av1_main(args) -> None:
     W, H = eng.W, eng.H
     lib = stage._lib()
 
-    def comm(futs, sse):
-        segs = [b"".join(f.result()) for f in futs]
+    def comm(gfut):
+        g = gfut.result()  # decisions on the host (copy stream, behind the next GOP's kernels)
+        sse = g.sse.sum(axis=(0, 1)).astype(np.float64)
+        segs = [b"".join(f.result()) for f in eng.submit_entropy(g)]
         stats = torch.tensor([batch * args.gop, sum(len(x) for x in segs), *sse], dtype=torch.float64, device=dev)
         dist.all_reduce(stats)
         gathered = gather_bytes_to_root(b"".join(segs), dev)
@@ -349,8 +351,7 @@ def av1_main(args) -> None:
                 stage._ok(lib.tv_pad_batch(C.c_void_p(src.ptr(c)), pw, ph, stride, fs, C.c_void_p(dst.data_ptr()),
                                            cw, chh, cw, cw * chh, batch, st))
 
-        g = eng.encode_gop(args.gop, load)
-        post.submit(comm, eng.submit_entropy(g), g.sse.sum(axis=(0, 1)).astype(np.float64))
+        post.submit(comm, eng.encode_gop(args.gop, load, async_host=True))
 
     el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), eng.pool._max_workers])
     tot = np.sum([r[0] for r in res], axis=0)

@@ -117,26 +117,48 @@ class Av1GpuEngine:
         self._gop_cap = 0
         self.lock = None  # set by the worker's engine cache
         self.staging = None
+        self._copy_stream = torch.cuda.Stream(self.dev)
+        self._copy_pool = cf.ThreadPoolExecutor(max_workers=1)
 
     def _lf_level(self, q: int | None = None) -> int:
         return lf_level(self.q if q is None else q)
 
+    _NAMES = ("mode", "mv", "ly", "lu", "lv", "tabs", "fbidx", "sse", "lr")
+
     def _alloc_gop(self, F: int):
+        """Two GOP decision buffers (slots): the GPU fills one while the previous GOP's is
+        compacted and copied to the host on the copy stream (encode_gop(async_host=True))."""
         torch = self.torch
         if F <= self._gop_cap:
             return
         B, nb, nfb = self.B, self.nb, self.nfb
         d = self.dev
-        self.g_mode = torch.zeros((F, B, nb), dtype=torch.int32, device=d)
-        self.g_mv = torch.zeros((F, B, nb), dtype=torch.int32, device=d)
-        self.g_ly = torch.zeros((F, B, nb, 256), dtype=torch.int16, device=d)
-        self.g_lu = torch.zeros((F, B, nb, 64), dtype=torch.int16, device=d)
-        self.g_lv = torch.zeros((F, B, nb, 64), dtype=torch.int16, device=d)
-        self.g_tabs = torch.zeros((F, B, 16), dtype=torch.uint8, device=d)
-        self.g_fbidx = torch.zeros((F, B, nfb), dtype=torch.int8, device=d)
-        self.g_sse = torch.zeros((F, B, 3), dtype=torch.int64, device=d)
-        self.g_lr = torch.zeros((F, B, 3, self.nu, 3), dtype=torch.int32, device=d)
+        self._slots = []
+        for _ in range(2):
+            self._slots.append({
+                "mode": torch.zeros((F, B, nb), dtype=torch.int32, device=d),
+                "mv": torch.zeros((F, B, nb), dtype=torch.int32, device=d),
+                "ly": torch.zeros((F, B, nb, 256), dtype=torch.int16, device=d),
+                "lu": torch.zeros((F, B, nb, 64), dtype=torch.int16, device=d),
+                "lv": torch.zeros((F, B, nb, 64), dtype=torch.int16, device=d),
+                "tabs": torch.zeros((F, B, 16), dtype=torch.uint8, device=d),
+                "fbidx": torch.zeros((F, B, nfb), dtype=torch.int8, device=d),
+                "sse": torch.zeros((F, B, 3), dtype=torch.int64, device=d),
+                "lr": torch.zeros((F, B, 3, self.nu, 3), dtype=torch.int32, device=d),
+            })
+        self._slot_busy = [None, None]
+        self._slot = 0
         self._gop_cap = F
+
+    def _use_slot(self):
+        s = self._slot
+        self._slot ^= 1
+        if self._slot_busy[s] is not None:  # the previous GOP in this slot is still being collected
+            self._slot_busy[s].result()
+            self._slot_busy[s] = None
+        for n in self._NAMES:
+            setattr(self, "g_" + n, self._slots[s][n])
+        return s
 
     # ------------------------------------------------------------------ one frame ----
     def _frame(self, t: int, key: bool, nseg: int, qarr, lvl, q_rate):
@@ -231,17 +253,20 @@ class Av1GpuEngine:
             out.append(res)
         return tuple(out)
 
-    def encode_gop(self, nframes: int, load_frame, nseg: int | None = None, qmap=None) -> GopHost:
+    def encode_gop(self, nframes: int, load_frame, nseg: int | None = None, qmap=None, async_host: bool = False):
         """Run the GPU part of one GOP for all B segments.  load_frame(t, (Y, U, V)) fills
         the coded-size source planes [B, H, W] of frame t (device tensors).  `qmap`
         (optional (nframes, nseg) ints): per-frame, per-segment q-index from rate control
         (2-pass / CRF plans); None = the engine's constant q-index.  Returns the host copy
-        of the decisions (one device->host transfer of compacted levels)."""
+        of the decisions (one device->host transfer of compacted levels).  async_host=True
+        returns a Future of it instead: the copy runs on a copy stream / thread behind the next
+        GOP's kernels (double-buffered decision slots)."""
         torch = self.torch
         nseg = nseg or self.B
         if not 1 <= nseg <= self.B:
             raise ValueError(f"nseg {nseg} outside 1..{self.B}")
         self._alloc_gop(nframes)
+        slot = self._use_slot()
         qm = np.full((nframes, nseg), self.q, np.int32) if qmap is None else \
             np.clip(np.asarray(qmap, np.int32).reshape(nframes, nseg), 1, 255)
         lv = np.array([[[lf_level(int(x))] * 4 for x in row] for row in qm], np.int32)
@@ -253,31 +278,45 @@ class Av1GpuEngine:
         for t in range(nframes):
             load_frame(t, self.src)
             self._frame(t, t == 0, nseg, qd[t], ld[t], rd[t])
-        self.qm = qm
-        F = nframes
         self.nseg = nseg
-        mode = self.g_mode[:F, :nseg]
-        packed = []
-        for p, lev in enumerate((self.g_ly[:F, :nseg], self.g_lu[:F, :nseg], self.g_lv[:F, :nseg])):
-            nz = ((mode >> (10 + p)) & 1).bool()
-            counts = nz.sum(dim=2)
-            packed.append((lev[nz], counts))
-        host = GopHost(
-            nframes=F,
-            mode=mode.cpu().numpy().view(np.uint32),
-            mv=self.g_mv[:F, :nseg].cpu().numpy().view(np.uint32),
-            tabs=self.g_tabs[:F, :nseg].cpu().numpy(),
-            fbidx=self.g_fbidx[:F, :nseg].cpu().numpy(),
-            packed=[],
-            sse=self.g_sse[:F, :nseg].cpu().numpy(),
-            key=[t == 0 for t in range(F)],
-            qm=qm,
-            lr=self.g_lr[:F, :nseg].cpu().numpy(),
-        )
-        for lev, counts in packed:
-            c = counts.cpu().numpy().astype(np.int64).reshape(-1)
-            off = np.concatenate([[0], np.cumsum(c)])[:-1].reshape(F, nseg)
-            host.packed.append((lev.cpu().numpy(), off))
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        S = self._slots[slot]
+        if not async_host:
+            return self._collect(S, ev, nframes, nseg, qm)
+        fut = self._copy_pool.submit(self._collect, S, ev, nframes, nseg, qm)
+        self._slot_busy[slot] = fut
+        return fut
+
+    def _collect(self, S: dict, ev, F: int, nseg: int, qm) -> GopHost:
+        """Compact the nonzero TBs of a GOP slot on the copy stream (after `ev`) and copy
+        every decision array to the host."""
+        torch = self.torch
+        torch.cuda.set_device(self.dev)
+        cs = self._copy_stream
+        with torch.cuda.stream(cs):
+            cs.wait_event(ev)
+            mode = S["mode"][:F, :nseg]
+            packed = []
+            for p, lev in enumerate((S["ly"][:F, :nseg], S["lu"][:F, :nseg], S["lv"][:F, :nseg])):
+                nz = ((mode >> (10 + p)) & 1).bool()
+                packed.append((lev[nz], nz.sum(dim=2)))
+            host = GopHost(
+                nframes=F,
+                mode=mode.cpu().numpy().view(np.uint32),
+                mv=S["mv"][:F, :nseg].cpu().numpy().view(np.uint32),
+                tabs=S["tabs"][:F, :nseg].cpu().numpy(),
+                fbidx=S["fbidx"][:F, :nseg].cpu().numpy(),
+                packed=[],
+                sse=S["sse"][:F, :nseg].cpu().numpy(),
+                key=[t == 0 for t in range(F)],
+                qm=qm,
+                lr=S["lr"][:F, :nseg].cpu().numpy(),
+            )
+            for lev, counts in packed:
+                c = counts.cpu().numpy().astype(np.int64).reshape(-1)
+                off = np.concatenate([[0], np.cumsum(c)])[:-1].reshape(F, nseg)
+                host.packed.append((lev.cpu().numpy(), off))
         return host
 
     # ------------------------------------------------------------------ entropy ------
@@ -312,4 +351,5 @@ class Av1GpuEngine:
         return out
 
     def close(self):
+        self._copy_pool.shutdown(wait=True)
         self.pool.shutdown(wait=True)
