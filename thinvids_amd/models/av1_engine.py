@@ -270,9 +270,13 @@ class Av1GpuEngine:
         qm = np.full((nframes, nseg), self.q, np.int32) if qmap is None else \
             np.clip(np.asarray(qmap, np.int32).reshape(nframes, nseg), 1, 255)
         lv = np.array([[[lf_level(int(x))] * 4 for x in row] for row in qm], np.int32)
-        qd = torch.from_numpy(qm).to(self.dev)
-        ld = torch.from_numpy(lv).to(self.dev)
-        rd = torch.from_numpy(np.array([[lr_rate_cost(int(x)) for x in row] for row in qm], np.int64)).to(self.dev)
+        # pinned + non_blocking: a pageable upload would block the host on the previous
+        # GOP's kernels (the stream drains before this GOP's first launch)
+        up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(self.dev, non_blocking=True)
+        qd = up(qm)
+        ld = up(lv)
+        rd = up(np.array([[lr_rate_cost(int(x)) for x in row] for row in qm], np.int64))
+        self._keep = (qd, ld, rd)
         if not self.lr_enabled:
             self.g_lr[:nframes, :nseg, :, :, 0] = -1
         for t in range(nframes):
