@@ -107,48 +107,59 @@ struct Cdfs {
   C17 dc_sign[2][3];
   C17 use_sgrproj;
 };
-template <size_t K> void init_all(C17 (&a)[K], int n) {
-  for (auto& c : a) cdf_init_uniform(c, n);
+template <class F> void each(C17& c, int n, F& f) { f(c, n); }
+template <size_t K, class F> void each(C17 (&a)[K], int n, F& f) {
+  for (auto& c : a) f(c, n);
 }
-template <size_t K, size_t L> void init_all(C17 (&a)[K][L], int n) {
-  for (auto& r : a) init_all(r, n);
+template <size_t K, size_t L, class F> void each(C17 (&a)[K][L], int n, F& f) {
+  for (auto& r : a) each(r, n, f);
 }
-template <size_t K, size_t L, size_t M> void init_all(C17 (&a)[K][L][M], int n) {
-  for (auto& r : a) init_all(r, n);
+template <size_t K, size_t L, size_t M, class F> void each(C17 (&a)[K][L][M], int n, F& f) {
+  for (auto& r : a) each(r, n, f);
 }
+// f(cdf, number of symbols) for every CDF of the set
+template <class F> void visit_cdfs(Cdfs& c, F f) {
+  each(c.partition[0], 4, f);
+  for (int b = 1; b < 4; ++b) each(c.partition[b], 10, f);
+  each(c.kf_y, 13, f);
+  each(c.y_mode, 13, f);
+  each(c.uv[0], 13, f);
+  each(c.uv[1], 14, f);
+  each(c.angle, 7, f);
+  each(c.skip, 2, f);
+  each(c.is_inter, 2, f);
+  each(c.single_ref, 2, f);
+  each(c.new_mv, 2, f);
+  each(c.zero_mv, 2, f);
+  each(c.ref_mv, 2, f);
+  each(c.drl, 2, f);
+  each(c.mv_joint, 4, f);
+  each(c.mv_sign, 2, f);
+  each(c.mv_class, 11, f);
+  each(c.class0_bit, 2, f);
+  each(c.class0_fr, 4, f);
+  each(c.mv_fr, 4, f);
+  each(c.mv_bits, 2, f);
+  each(c.intra_tx, 5, f);
+  each(c.inter_tx, 2, f);
+  each(c.txb_skip, 2, f);
+  for (int s = 0; s < 7; ++s) each(c.eob_pt[s], s + 5, f);
+  each(c.eob_extra, 2, f);
+  each(c.base_eob, 3, f);
+  each(c.base, 4, f);
+  each(c.br, 4, f);
+  each(c.dc_sign, 2, f);
+  each(c.use_sgrproj, 2, f);
+}
+// SUBSTITUTE for the specification's default CDFs: every CDF starts uniform
 void init_cdfs(Cdfs& c) {
-  cdf_init_uniform(c.partition[0][0], 4);
-  for (int i = 1; i < 4; ++i) cdf_init_uniform(c.partition[0][i], 4);
-  for (int b = 1; b < 4; ++b) init_all(c.partition[b], 10);
-  init_all(c.kf_y, 13);
-  init_all(c.y_mode, 13);
-  init_all(c.uv[0], 13);
-  init_all(c.uv[1], 14);
-  init_all(c.angle, 7);
-  init_all(c.skip, 2);
-  init_all(c.is_inter, 2);
-  init_all(c.single_ref, 2);
-  init_all(c.new_mv, 2);
-  init_all(c.zero_mv, 2);
-  init_all(c.ref_mv, 2);
-  init_all(c.drl, 2);
-  cdf_init_uniform(c.mv_joint, 4);
-  init_all(c.mv_sign, 2);
-  init_all(c.mv_class, 11);
-  init_all(c.class0_bit, 2);
-  init_all(c.class0_fr, 4);
-  init_all(c.mv_fr, 4);
-  init_all(c.mv_bits, 2);
-  init_all(c.intra_tx, 5);
-  init_all(c.inter_tx, 2);
-  init_all(c.txb_skip, 2);
-  for (int s = 0; s < 7; ++s) init_all(c.eob_pt[s], s + 5);
-  init_all(c.eob_extra, 2);
-  init_all(c.base_eob, 3);
-  init_all(c.base, 4);
-  init_all(c.br, 4);
-  init_all(c.dc_sign, 2);
-  cdf_init_uniform(c.use_sgrproj, 2);
+  visit_cdfs(c, [](uint16_t* p, int n) { cdf_init_uniform(p, n); });
+}
+// CDFs saved at the end of a frame (disable_frame_end_update_cdf = 0) and loaded by the
+// next frame through primary_ref_frame: probabilities kept, adaptation counters cleared
+void load_saved_cdfs(Cdfs& c, const Cdfs& saved) {
+  c = saved;
+  visit_cdfs(c, [](uint16_t* p, int n) { p[n] = 0; });
 }
 // P(symbol s) of an inverse CDF (15-bit)
 inline int sym_prob(const uint16_t* icdf, int s) { return (s ? icdf[s - 1] : 32768) - icdf[s]; }
@@ -1003,7 +1014,7 @@ void write_frame_header(BitWriter& w, const SeqGeo& g, const FrameParams& fp, co
   if (!fp.key) w.put(0, 1);  // error_resilient_mode (key + shown: implied 1)
   w.put(0, 1);  // disable_cdf_update
   w.put(0, 1);  // frame_size_override_flag
-  if (!fp.key) w.put(7, 3);  // primary_ref_frame = PRIMARY_REF_NONE
+  if (!fp.key) w.put(0, 3);  // primary_ref_frame: CDFs saved by the frame in ref slot 0
   if (!fp.key) w.put(0x01, 8);  // refresh_frame_flags: slot 0 (key frames refresh all)
   const bool diff = g.dw != g.W || g.dh != g.H;
   if (fp.key) {
@@ -1024,7 +1035,7 @@ void write_frame_header(BitWriter& w, const SeqGeo& g, const FrameParams& fp, co
     w.put(0, 2);  // interpolation_filter EIGHTTAP
     w.put(0, 1);  // is_motion_mode_switchable
   }
-  w.put(1, 1);  // disable_frame_end_update_cdf
+  w.put(0, 1);  // disable_frame_end_update_cdf: the CDFs at the end of the tile are saved
   // tile_info: uniform spacing, one tile
   const int sbc = g.sbw, sbr = g.sbh;
   w.put(1, 1);
@@ -1088,7 +1099,7 @@ FrameParams read_frame_header(BitReader& r, SeqGeo& g, bool& have_ref, int* lr_t
   expect(1, 0, "disable_cdf_update");
   expect(1, 0, "frame_size_override_flag");
   if (!fp.key) {
-    expect(3, 7, "primary_ref_frame");
+    expect(3, 0, "primary_ref_frame");
     r.u(8);
     if (!have_ref) throw std::runtime_error("av1 oracle: inter frame without a reference");
     for (int i = 0; i < 7; ++i) expect(3, 0, "ref_frame_idx");
@@ -1108,7 +1119,7 @@ FrameParams read_frame_header(BitReader& r, SeqGeo& g, bool& have_ref, int* lr_t
     expect(2, 0, "interpolation_filter");
     expect(1, 0, "is_motion_mode_switchable");
   }
-  expect(1, 1, "disable_frame_end_update_cdf");
+  expect(1, 0, "disable_frame_end_update_cdf");
   expect(1, 1, "uniform_tile_spacing_flag");
   const int maxc = tile_log2(1, std::min(g.sbw, 64)), maxr = tile_log2(1, std::min(g.sbh, 64));
   if (0 < maxc) expect(1, 0, "increment_tile_cols_log2");
@@ -1166,7 +1177,7 @@ void put_obu(std::vector<uint8_t>& out, int type, const std::vector<uint8_t>& pa
 }  // namespace
 
 // ================================================================== writer ==============
-std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& d, bool seq_header) {
+std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& d, bool seq_header, EntropyState* st) {
   const int nb = g.nblk();
   FrameParams fp = d.fp;
   std::vector<uint32_t> mode(d.mode, d.mode + nb), mv(nb, 0);
@@ -1174,6 +1185,12 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
   std::vector<int8_t> cdef(d.cdef_idx, d.cdef_idx + g.nsb());
   SymW io;
   Tile<SymW> t(io, g, fp, mode, mv, cdef);
+  if (!fp.key) {
+    if (!st || st->saved.size() != sizeof(Cdfs)) throw std::runtime_error("av1 writer: inter frame without saved CDFs");
+    Cdfs saved;
+    std::memcpy(&saved, st->saved.data(), sizeof(Cdfs));
+    load_saved_cdfs(t.cdf, saved);
+  }
   std::vector<int32_t> lr;
   if (d.lr) {
     lr.assign(d.lr, d.lr + (size_t)3 * g.lr_nu() * 3);
@@ -1197,6 +1214,10 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
     return off[p][b] < 0 ? nullptr : base[p] + (size_t)off[p][b] * sz;
   };
   t.tile();
+  if (st) {  // frame end CDF update
+    st->saved.resize(sizeof(Cdfs));
+    std::memcpy(st->saved.data(), &t.cdf, sizeof(Cdfs));
+  }
   const std::vector<uint8_t> tile = io.rc.finish();
   std::vector<uint8_t> out;
   put_obu(out, OBU_TEMPORAL_DELIMITER, {});
@@ -1377,6 +1398,8 @@ size_t read_leb128(const uint8_t* p, size_t n, size_t& pos) {
 
 Decoded decode_stream(const uint8_t* p, size_t n) {
   Decoded out;
+  Cdfs saved_cdfs;
+  init_cdfs(saved_cdfs);
   bool have_seq = false;
   size_t pos = 0;
   while (pos < n) {
@@ -1416,6 +1439,7 @@ Decoded decode_stream(const uint8_t* p, size_t n) {
     fd.cdef_idx.assign(g.nsb(), -1);
     SymR io(q + hdr, sz - hdr);
     Tile<SymR> t(io, g, fd.fp, fd.mode, fd.mv, fd.cdef_idx);
+    if (!fd.fp.key) load_saved_cdfs(t.cdf, saved_cdfs);
     t.lev_out[0] = fd.ly.data();
     t.lev_out[1] = fd.lu.data();
     t.lev_out[2] = fd.lv.data();
@@ -1424,6 +1448,7 @@ Decoded decode_stream(const uint8_t* p, size_t n) {
     t.lr = fd.lr.data();
     for (int p = 0; p < 3; ++p) t.lr_type[p] = lr_type[p];
     t.tile();
+    saved_cdfs = t.cdf;
     Planes rec;
     reconstruct(g, fd.view(), fd.fp.key ? nullptr : &out.frames.back(), rec);
     out.frames.push_back(std::move(rec));
@@ -1806,8 +1831,9 @@ int tv_av1c_golden_encode(int dw, int dh, int n, const uint8_t* yuv, int qidx, c
     auto* bytes = static_cast<std::vector<uint8_t>*>(out);
     bytes->clear();
     const int nb = g.nblk();
+    EntropyState est;
     for (int i = 0; i < n; ++i) {
-      const auto tu = write_temporal_unit(g, go.frames[i].view(), i == 0);
+      const auto tu = write_temporal_unit(g, go.frames[i].view(), i == 0, &est);
       bytes->insert(bytes->end(), tu.begin(), tu.end());
       tu_sizes[i] = (int64_t)tu.size();
       if (recon) join_planes(go.recon[i], recon + i * fsz);
@@ -1847,7 +1873,12 @@ int tv_av1c_probe(const uint8_t* data, size_t n, int* geo, int* nframes) {
 }
 
 // Write one frame's temporal unit from engine decisions (packed levels layout).
-int tv_av1c_write_tu(int dw, int dh, const int* fparams, const uint32_t* mode, const uint32_t* mv, const int16_t* ly,
+void* tv_av1c_state_new() { return new EntropyState(); }
+void tv_av1c_state_free(void* s) { delete static_cast<EntropyState*>(s); }
+
+// `state` (tv_av1c_state_new): the stream's entropy state, frames written in order.
+int tv_av1c_write_tu(void* state, int dw, int dh, const int* fparams, const uint32_t* mode, const uint32_t* mv,
+                     const int16_t* ly,
                      const int16_t* lu, const int16_t* lv, const int8_t* cdef_idx, const int32_t* lr, int packed,
                      int seq_header, void* out) {
   return codec_guard([&] {
@@ -1862,7 +1893,7 @@ int tv_av1c_write_tu(int dw, int dh, const int* fparams, const uint32_t* mode, c
     d.cdef_idx = cdef_idx;
     d.lr = lr;
     d.packed = packed != 0;
-    auto tu = write_temporal_unit(g, d, seq_header != 0);
+    auto tu = write_temporal_unit(g, d, seq_header != 0, static_cast<EntropyState*>(state));
     auto* bytes = static_cast<std::vector<uint8_t>*>(out);
     bytes->insert(bytes->end(), tu.begin(), tu.end());
   });

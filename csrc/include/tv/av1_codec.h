@@ -64,8 +64,16 @@ struct FrameData {
   FrameDecisions view() const;
 };
 
-// Temporal unit of one frame: temporal delimiter [+ sequence header] + OBU_FRAME.
-std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& d, bool seq_header);
+// Entropy state carried between the frames of one stream: the CDFs saved at the end of the
+// previous frame (disable_frame_end_update_cdf = 0), loaded by an inter frame through
+// primary_ref_frame = 0.  Opaque bytes of the internal CDF set.
+struct EntropyState {
+  std::vector<uint8_t> saved;
+};
+
+// Temporal unit of one frame: temporal delimiter [+ sequence header] + OBU_FRAME.  `st`
+// carries the CDFs from frame to frame (required for inter frames, updated by every frame).
+std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& d, bool seq_header, EntropyState* st);
 
 struct Planes {
   std::vector<uint8_t> y, u, v;  // coded size

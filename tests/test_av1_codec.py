@@ -63,15 +63,16 @@ def test_packed_writer_matches_golden_stream():
     frames = _frames(5, w, h, 3)
     res = av1.golden_encode(frames, w, h, q)
     tus = av1.split_temporal_units(res.stream, res.tu_sizes)
+    wr = av1.StreamWriter(w, h)
     for k in range(3):
         mode = res.mode[k]
         packed = []
         for p, lev in enumerate((res.ly[k], res.lu[k], res.lv[k])):
             nz = ((mode >> (10 + p)) & 1).astype(bool)
             packed.append(np.ascontiguousarray(lev[nz]) if nz.any() else np.zeros((1, lev.shape[1]), np.int16))
-        out = av1.write_tu(w, h, res.fparams[k], np.ascontiguousarray(mode), np.ascontiguousarray(res.mv[k]),
-                           packed[0], packed[1], packed[2], np.ascontiguousarray(res.cdef_idx[k]), packed=True,
-                           seq_header=(k == 0), lr=res.lr[k])
+        out = wr.write(res.fparams[k], np.ascontiguousarray(mode), np.ascontiguousarray(res.mv[k]), packed[0],
+                       packed[1], packed[2], np.ascontiguousarray(res.cdef_idx[k]), packed=True, seq_header=(k == 0),
+                       lr=res.lr[k])
         assert out == tus[k]
 
 

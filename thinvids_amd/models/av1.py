@@ -46,7 +46,9 @@ def _lib():
         lib.tv_av1c_golden_encode.restype = i
         lib.tv_av1c_decode.argtypes = [u8p, C.c_size_t, i, u8p, i32p, i32p]
         lib.tv_av1c_decode.restype = i
-        lib.tv_av1c_write_tu.argtypes = [i, i, i32p, u32p, u32p, i16p, i16p, i16p, i8p, i32p, i, i, vp]
+        lib.tv_av1c_write_tu.argtypes = [vp, i, i, i32p, u32p, u32p, i16p, i16p, i16p, i8p, i32p, i, i, vp]
+        lib.tv_av1c_state_new.restype = vp
+        lib.tv_av1c_state_free.argtypes = [vp]
         lib.tv_av1c_write_tu.restype = i
         lib._av1c_sigs = True
     return lib
@@ -203,17 +205,31 @@ def frame_params(key: bool, qindex: int, lf, sharp: int, damping: int, cdef_y, c
     return p
 
 
-def write_tu(width: int, height: int, fparams: np.ndarray, mode: np.ndarray, mv: np.ndarray, ly: np.ndarray,
-             lu: np.ndarray, lv: np.ndarray, cdef_idx: np.ndarray, packed: bool, seq_header: bool,
-             out: Bytes | None = None, lr: np.ndarray | None = None) -> bytes | None:
-    """One frame's temporal unit from engine decisions (appended to `out` when given)."""
-    o = out if out is not None else Bytes()
-    _check(_lib().tv_av1c_write_tu(width, height, fparams.ctypes.data_as(i32p), mode.ctypes.data_as(u32p),
-                                   mv.ctypes.data_as(u32p), ly.ctypes.data_as(i16p), lu.ctypes.data_as(i16p),
-                                   lv.ctypes.data_as(i16p), cdef_idx.ctypes.data_as(i8p),
-                                   None if lr is None else np.ascontiguousarray(lr, np.int32).ctypes.data_as(i32p),
-                                   int(packed), int(seq_header), o.h))
-    return None if out is not None else o.tobytes()
+class StreamWriter:
+    """Writes one stream's temporal units in order from engine decisions; carries the
+    frame-to-frame CDF state (frame-end CDF update, primary_ref_frame of inter frames)."""
+
+    def __init__(self, width: int, height: int):
+        self.w, self.h = width, height
+        self.lib = _lib()
+        self.st = self.lib.tv_av1c_state_new()
+
+    def __del__(self):
+        if getattr(self, "st", None):
+            self.lib.tv_av1c_state_free(self.st)
+            self.st = None
+
+    def write(self, fparams: np.ndarray, mode: np.ndarray, mv: np.ndarray, ly: np.ndarray, lu: np.ndarray,
+              lv: np.ndarray, cdef_idx: np.ndarray, packed: bool, seq_header: bool, lr: np.ndarray | None = None,
+              out: Bytes | None = None) -> bytes | None:
+        o = out if out is not None else Bytes()
+        _check(self.lib.tv_av1c_write_tu(self.st, self.w, self.h, fparams.ctypes.data_as(i32p),
+                                         mode.ctypes.data_as(u32p), mv.ctypes.data_as(u32p),
+                                         ly.ctypes.data_as(i16p), lu.ctypes.data_as(i16p), lv.ctypes.data_as(i16p),
+                                         cdef_idx.ctypes.data_as(i8p),
+                                         None if lr is None else np.ascontiguousarray(lr, np.int32).ctypes.data_as(i32p),
+                                         int(packed), int(seq_header), o.h))
+        return None if out is not None else o.tobytes()
 
 
 # ------------------------------------------------------------------------------- IVF ----

@@ -328,16 +328,16 @@ class Av1GpuEngine:
         """Temporal units of segment b of a GOP (runs on a pool thread; the native writer
         releases the GIL)."""
         tus = []
+        wr = av1m.StreamWriter(self.w, self.h)
         for t in range(g.nframes):
             tabs = g.tabs[t, b]
             q = int(g.qm[t, b])
             fp = av1m.frame_params(g.key[t], q, [lf_level(q)] * 4, 0, self.damping, tabs[:8], tabs[8:])
             lev = [np.ascontiguousarray(pk[0][pk[1][t, b]:]) if len(pk[0]) else np.zeros((1, n), np.int16)
                    for pk, n in zip(g.packed, (256, 64, 64))]
-            tus.append(av1m.write_tu(self.w, self.h, fp, np.ascontiguousarray(g.mode[t, b]),
-                                     np.ascontiguousarray(g.mv[t, b]), lev[0], lev[1], lev[2],
-                                     np.ascontiguousarray(g.fbidx[t, b]), packed=True, seq_header=g.key[t],
-                                     lr=np.ascontiguousarray(g.lr[t, b])))
+            tus.append(wr.write(fp, np.ascontiguousarray(g.mode[t, b]), np.ascontiguousarray(g.mv[t, b]), lev[0],
+                                lev[1], lev[2], np.ascontiguousarray(g.fbidx[t, b]), packed=True, seq_header=g.key[t],
+                                lr=np.ascontiguousarray(g.lr[t, b])))
         return tus
 
     def submit_entropy(self, g: GopHost) -> list:
