@@ -427,8 +427,11 @@ struct Tile {
     if (!mode_inter(mode[b])) return;
     search_stack(b, weight);
   }
+  int cur4 = 4;  // width (= height) of the current block in 4x4 units
+  int cand4(int r, int c) const { return 4 << mode_bsz(mode[blk(r, c)]); }
   void scan_row(int mir, int mic, int dr) {
-    const int bw4 = 4, end4 = std::min(std::min(bw4, MiCols - mic), 16);
+    const int bw4 = cur4, end4 = std::min(std::min(bw4, MiCols - mic), 16);
+    const bool step16 = bw4 >= 16;
     int dc = 0;
     if (std::abs(dr) > 1) {
       dr += mir & 1;
@@ -437,14 +440,16 @@ struct Tile {
     for (int i = 0; i < end4;) {
       const int r = mir + dr, c = mic + dc + i;
       if (!inside(r, c)) break;
-      int len = std::min(bw4, 4);
+      int len = std::min(bw4, cand4(r, c));
       if (std::abs(dr) > 1) len = std::max(2, len);
+      if (step16) len = std::max(4, len);
       add_cand(r, c, 2 * len);
       i += len;
     }
   }
   void scan_col(int mir, int mic, int dc) {
-    const int bh4 = 4, end4 = std::min(std::min(bh4, MiRows - mir), 16);
+    const int bh4 = cur4, end4 = std::min(std::min(bh4, MiRows - mir), 16);
+    const bool step16 = bh4 >= 16;
     int dr = 0;
     if (std::abs(dc) > 1) {
       dr = 1 - (mir & 1);
@@ -453,8 +458,9 @@ struct Tile {
     for (int i = 0; i < end4;) {
       const int r = mir + dr + i, c = mic + dc;
       if (!inside(r, c)) break;
-      int len = std::min(bh4, 4);
+      int len = std::min(bh4, cand4(r, c));
       if (std::abs(dc) > 1) len = std::max(2, len);
+      if (step16) len = std::max(4, len);
       add_cand(r, c, 2 * len);
       i += len;
     }
@@ -486,7 +492,7 @@ struct Tile {
     scan_col(mir, mic, -1);
     int fl = found;
     found = 0;
-    scan_point(mir, mic, -1, 4);
+    scan_point(mir, mic, -1, cur4);
     if (found) fa = 1;
     const int close = fa + fl, nearest = S.n, nnew = newcount;
     for (int i = 0; i < nearest; ++i) S.w[i] += 640;
@@ -509,11 +515,12 @@ struct Tile {
     sort_stack(0, nearest);
     sort_stack(nearest, S.n);
     if (S.n < 2) {  // extra_search
-      const int num4 = std::min(std::min(4, MiCols - mic), std::min(4, MiRows - mir));
+      const int num4 = std::min(std::min(std::min(16, cur4), MiCols - mic), std::min(std::min(16, cur4), MiRows - mir));
       for (int pass = 0; pass < 2 && S.n < 2; ++pass) {
-        for (int idx = 0; idx < num4 && S.n < 2; idx += 4) {
+        for (int idx = 0; idx < num4 && S.n < 2;) {
           const int r = pass ? mir + idx : mir - 1, c = pass ? mic - 1 : mic + idx;
           if (!inside(r, c)) break;
+          idx += cand4(r, c);
           const int b = blk(r, c);
           if (!mode_inter(mode[b])) continue;
           const int m0 = mv_row(mv[b]), m1 = mv_col(mv[b]);
@@ -531,8 +538,8 @@ struct Tile {
       for (int i = S.n; i < 2; ++i) S.mv[i][0] = S.mv[i][1] = 0;  // GlobalMvs (identity)
     }
     for (int i = 0; i < S.n; ++i) {
-      const int top = -(mir * 4 * 8), bottom = (MiRows - 4 - mir) * 4 * 8, border = 128 + 4 * 4 * 8;
-      const int left = -(mic * 4 * 8), right = (MiCols - 4 - mic) * 4 * 8;
+      const int top = -(mir * 4 * 8), bottom = (MiRows - cur4 - mir) * 4 * 8, border = 128 + cur4 * 4 * 8;
+      const int left = -(mic * 4 * 8), right = (MiCols - cur4 - mic) * 4 * 8;
       S.mv[i][0] = clip3(top - border, bottom + border, S.mv[i][0]);
       S.mv[i][1] = clip3(left - border, right + border, S.mv[i][1]);
     }
@@ -712,9 +719,10 @@ struct Tile {
     }
   }
 
-  void block(int mir, int mic) {
+  void block(int mir, int mic, int bsl) {
     const int b = blk(mir, mic);
     const bool availU = mir > 0, availL = mic > 0, kf = fp.key != 0;
+    cur4 = 1 << bsl;
     int skip = mode_skip(mode[b]);
     const int sctx = (availU ? mode_skip(mode[b - g.bw]) : 0) + (availL ? mode_skip(mode[b - 1]) : 0);
     io.sym(skip, cdf.skip[sctx], 2);
@@ -738,6 +746,7 @@ struct Tile {
       else if (availU || availL) ictx = 2 * (availU ? aI : lI);
       io.sym(inter, cdf.is_inter[ictx], 2);
     }
+    if (bsl > 2 && !(skip && inter)) throw std::runtime_error("av1: merged blocks are skip inter blocks only");
     if (inter) inter_modes(b, mir, mic, availU, availL);
     else intra_modes(b, kf, availU, availL);
     // residual
@@ -766,7 +775,7 @@ struct Tile {
       if (nz == 0) throw std::runtime_error("av1: non-skip block without coefficients");
     } else {
       for (int p = 0; p < 3; ++p) {  // reset_block_context
-        const int ss = p ? 1 : 0, w4 = 4 >> ss;
+        const int ss = p ? 1 : 0, w4 = cur4 >> ss;
         for (int i = 0; i < w4; ++i) {
           aLvl[p][(x4 >> ss) + i] = aDc[p][(x4 >> ss) + i] = 0;
           lLvl[p][(y4 >> ss) + i] = lDc[p][(y4 >> ss) + i] = 0;
@@ -774,8 +783,15 @@ struct Tile {
         if (!IO::kW) std::memset(lev_out[p] + ((size_t)b << (p ? 6 : 8)), 0, sizeof(int16_t) << (p ? 6 : 8));
       }
     }
-    if (!IO::kW) mode[b] = (mode[b] & ~(7u << 10)) | ((uint32_t)nz << 10);
-    coded[b] = 1;
+    if (!IO::kW) mode[b] = with_bsz((mode[b] & ~(7u << 10)) | ((uint32_t)nz << 10), bsl - 2);
+    const int n16 = 1 << (bsl - 2);  // 16x16 cells per side of this block
+    for (int dy = 0; dy < n16; ++dy)
+      for (int dx = 0; dx < n16; ++dx) {
+        const int c = b + dy * g.bw + dx;
+        if (!IO::kW) mode[c] = mode[b], mv[c] = mv[b];
+        ymode[c] = ymode[b];
+        coded[c] = 1;
+      }
   }
 
   // ---- loop restoration unit syntax (5.11.58 read_lr_unit, SGRPROJ frame type) ----
@@ -873,8 +889,11 @@ struct Tile {
     const bool availU = mir > 0, availL = mic > 0;
     const int half = (1 << bsl) >> 1;
     const bool hasRows = mir + half < MiRows, hasCols = mic + half < MiCols;
-    int part = bsl > 2 ? 3 : 0;  // PARTITION_SPLIT down to 16x16, then PARTITION_NONE
-    const int above = availU && 2 < bsl, left = availL && 2 < bsl;
+    // PARTITION_SPLIT down to 16x16, then PARTITION_NONE; NONE at 32 / 64 for merged blocks
+    int part = bsl > 2 ? 3 : 0;
+    if (IO::kW && bsl > 2 && hasRows && hasCols && mode_bsz(mode[blk(mir, mic)]) == bsl - 2) part = 0;
+    const int above = availU && 2 + mode_bsz(mode[blk(mir - 1, mic)]) < bsl;
+    const int left = availL && 2 + mode_bsz(mode[blk(mir, mic - 1)]) < bsl;
     uint16_t* c = cdf.partition[bsl - 1][left * 2 + above];
     if (hasRows && hasCols) {
       io.sym(part, c, 10);
@@ -898,8 +917,8 @@ struct Tile {
       partition(mir, mic + half, bsl - 1);
       partition(mir + half, mic, bsl - 1);
       partition(mir + half, mic + half, bsl - 1);
-    } else if (part == 0 && bsl == 2) {
-      block(mir, mic);
+    } else if (part == 0) {
+      block(mir, mic, bsl);
     } else {
       throw std::runtime_error("av1 oracle: partition outside the encoder subset");
     }
@@ -1289,7 +1308,7 @@ void loop_filters(const SeqGeo& g, const FrameParams& fp, const uint32_t* mode, 
     for (int y = 0; y < h4; ++y)
       for (int x = 0; x < w4; ++x) {
         const uint32_t m = mode[(y / bs4) * g.bw + x / bs4];
-        info[(size_t)y * w4 + x] = lf_word(p > 0, lv, lh, mode_skip(m) && mode_inter(m));
+        info[(size_t)y * w4 + x] = lf_word(p > 0, lv, lh, mode_skip(m) && mode_inter(m), mode_bsz(m));
       }
     const std::vector<uint8_t>& in = p == 0 ? rec.y : (p == 1 ? rec.u : rec.v);
     std::vector<uint8_t>& o = p == 0 ? db.y : (p == 1 ? db.u : db.v);
@@ -1686,6 +1705,8 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
       parallel_rows(g.bh, [&](int by) {
         for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx);
       });
+      for (int sy = 0; sy < g.sbh; ++sy)
+        for (int sx = 0; sx < g.sbw; ++sx) merge_sb(fd.mode.data(), fd.mv.data(), g.bw, g.bh, sx, sy);
     }
     // loop filters with the CDEF search on the deblocked frame
     const int W = g.W, H = g.H;

@@ -468,12 +468,23 @@ __global__ void k_av1e_lfinfo(const uint32_t* __restrict__ mode, int W, int H, c
   const int x = u % w4, y = u / w4;
   const uint32_t m = mode[(long)b * nb + (y >> 2) * bw + (x >> 2)];
   const bool si = mode_skip(m) && mode_inter(m);
-  iy[(long)b * w4 * h4 + u] = lf_word(false, lv0, lv1, si);
+  const int bz = mode_bsz(m);
+  iy[(long)b * w4 * h4 + u] = lf_word(false, lv0, lv1, si, bz);
   if (!(x & 1) && !(y & 1)) {
     const long cu = (long)b * (w4 / 2) * (h4 / 2) + (y >> 1) * (w4 / 2) + (x >> 1);
-    iu[cu] = lf_word(true, lv2, lv2, si);
-    iv[cu] = lf_word(true, lv3, lv3, si);
+    iu[cu] = lf_word(true, lv2, lv2, si, bz);
+    iv[cu] = lf_word(true, lv3, lv3, si, bz);
   }
+}
+
+// ================================================================= skip-block merging ===
+// one thread per (superblock, segment): merge_sb (tv/av1_enc.h), same rule as the golden
+__global__ void k_av1e_merge(uint32_t* __restrict__ mode, const uint32_t* __restrict__ mv, int W, int H, int B) {
+  const int bw = W >> 4, bh = H >> 4, sbw = (W + 63) >> 6, sbh = (H + 63) >> 6, nsb = sbw * sbh;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsb * B) return;
+  const int b = i / nsb, s = i - b * nsb;
+  merge_sb(mode + (long)b * bw * bh, mv + (long)b * bw * bh, bw, bh, s % sbw, s / sbw);
 }
 
 // ================================================================= CDEF preset choice ====
@@ -682,6 +693,14 @@ int tv_av1e_intra(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, uint8
                                                                        mode, mv, ly, lu, lv, W, H, qarr, d, lo);
   }
   return status("av1e_intra");
+}
+
+// skip-block merging of a P frame's decisions (before lfinfo / deblocking)
+int tv_av1e_merge(uint32_t* mode, const uint32_t* mv, int W, int H, int B, void* stream) {
+  if (bad(W, H, B, 1, "av1e_merge")) return -1;
+  const int n = ((W + 63) >> 6) * ((H + 63) >> 6) * B;
+  k_av1e_merge<<<(n + 127) / 128, 128, 0, (hipStream_t)stream>>>(mode, mv, W, H, B);
+  return status("av1e_merge");
 }
 
 // lvl: [B][4] loop_filter_level[0..3] per segment

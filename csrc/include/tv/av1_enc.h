@@ -346,13 +346,53 @@ TV_HD int mode_y(uint32_t m) { return (m >> 1) & 15; }
 TV_HD int mode_uv(uint32_t m) { return (m >> 5) & 15; }
 TV_HD int mode_skip(uint32_t m) { return (m >> 9) & 1; }
 TV_HD int mode_nz(uint32_t m) { return (m >> 10) & 7; }
+// bits 13-14: size of the (merged) block covering this 16x16 cell: 0 = 16x16, 1 = 32x32, 2 = 64x64
+TV_HD int mode_bsz(uint32_t m) { return (m >> 13) & 3; }
+TV_HD uint32_t with_bsz(uint32_t m, int s) { return (m & ~(3u << 13)) | ((uint32_t)(s & 3) << 13); }
+
+// Skip-block merging of inter frames (one 64x64 superblock at sb (sx, sy)): a fully inside
+// 32x32 quad whose four 16x16 blocks are all inter + skip with one motion vector becomes one
+// 32x32 block; four such quads with one motion vector become one 64x64 block.  Prediction is
+// unchanged (same MV), only the block size seen by the syntax and the deblocking differs.
+TV_HD void merge_sb(uint32_t* mode, const uint32_t* mv, int bw, int bh, int sx, int sy) {
+  bool q_ok[4];
+  int nq = 0;
+  for (int q = 0; q < 4; ++q) {
+    const int qx = sx * 4 + (q & 1) * 2, qy = sy * 4 + (q >> 1) * 2;
+    bool ok = qx + 1 < bw && qy + 1 < bh;
+    if (ok) {
+      const uint32_t v0 = mv[qy * bw + qx];
+      for (int k = 0; k < 4 && ok; ++k) {
+        const int c = (qy + (k >> 1)) * bw + qx + (k & 1);
+        ok = mode_inter(mode[c]) && mode_skip(mode[c]) && mv[c] == v0;
+      }
+    }
+    q_ok[q] = ok;
+    nq += ok;
+  }
+  const int x0 = sx * 4, y0 = sy * 4;
+  bool sb = nq == 4;
+  if (sb) {
+    const uint32_t v0 = mv[y0 * bw + x0];
+    for (int q = 1; q < 4 && sb; ++q) sb = mv[(y0 + (q >> 1) * 2) * bw + x0 + (q & 1) * 2] == v0;
+  }
+  for (int q = 0; q < 4; ++q) {
+    if (!q_ok[q]) continue;
+    const int qx = x0 + (q & 1) * 2, qy = y0 + (q >> 1) * 2;
+    for (int k = 0; k < 4; ++k) {
+      const int c = (qy + (k >> 1)) * bw + qx + (k & 1);
+      mode[c] = with_bsz(mode[c], sb ? 2 : 1);
+    }
+  }
+}
 TV_HD uint32_t pack_mv(int row, int col) { return (uint32_t)(row & 0xFFFF) | ((uint32_t)(col & 0xFFFF) << 16); }
 TV_HD int mv_row(uint32_t v) { return (int)(int16_t)(v & 0xFFFF); }
 TV_HD int mv_col(uint32_t v) { return (int)(int16_t)(v >> 16); }
 
-// deblocking info word for a 4x4 unit (av1_defs.h layout): tx = block = 16 luma / 8 chroma
-TV_HD uint32_t lf_word(bool chroma, int lvl_v, int lvl_h, bool skip_inter) {
-  const uint32_t l = chroma ? 1u : 2u;
+// deblocking info word for a 4x4 unit (av1_defs.h layout): tx = block = 16 << bsz luma,
+// 8 << bsz chroma
+TV_HD uint32_t lf_word(bool chroma, int lvl_v, int lvl_h, bool skip_inter, int bsz = 0) {
+  const uint32_t l = (chroma ? 1u : 2u) + (uint32_t)bsz;
   return l | (l << 3) | (l << 6) | (l << 9) | ((uint32_t)(lvl_v & 63) << 12) | ((uint32_t)(lvl_h & 63) << 18) |
          ((uint32_t)skip_inter << 24);
 }

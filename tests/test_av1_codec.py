@@ -48,6 +48,19 @@ def test_loop_restoration_units_round_trip():
     np.testing.assert_array_equal(dec.frames, res.recon)
 
 
+def test_skip_block_merging_on_static_content():
+    """Static content: inter blocks are skip with one MV, merged into 32x32 / 64x64 blocks
+    (PARTITION_NONE at 32 / 64); the stream round-trips and the P frames get cheaper."""
+    w, h = 200, 136
+    f0 = _frames(5, w, h, 1)[0]
+    frames = [f0] * 4
+    res = av1.golden_encode(frames, w, h, 120)
+    bsz = (res.mode[1:] >> 13) & 3
+    assert (bsz == 2).any() and (bsz == 1).any()
+    np.testing.assert_array_equal(av1.decode(res.stream).frames, res.recon)
+    assert max(res.tu_sizes[1:]) < 100 < res.tu_sizes[0]
+
+
 def test_higher_qindex_means_fewer_bits_lower_psnr():
     w, h = 128, 64
     frames = _frames(9, w, h, 3)
@@ -94,13 +107,15 @@ def test_qindex_mapping_monotone():
 
 
 # ---------------------------------------------------------------------------- GPU -----
-def _gpu_vs_golden(w, h, starts, nframes, q):
+def _gpu_vs_golden(w, h, starts, nframes, q, static=False):
     import torch
 
     from thinvids_amd.models.av1_engine import Av1GpuEngine
 
     W, H = av1.coded_size(w, h)
     segs = [_frames(11, w, h, nframes, t0) for t0 in starts]
+    if static:  # the first frame repeated: skip-block merging to 32x32 / 64x64
+        segs = [[s[0]] * nframes for s in segs]
     eng = Av1GpuEngine(w, h, batch=len(starts), qindex=q)
     dev = eng.dev
 
@@ -130,6 +145,12 @@ def _gpu_vs_golden(w, h, starts, nframes, q):
 @pytest.mark.gpu
 def test_gpu_av1_engine_matches_golden_small():
     _gpu_vs_golden(200, 120, [0, 7], 4, 100)
+
+
+@pytest.mark.gpu
+def test_gpu_av1_engine_matches_golden_merged_blocks():
+    g, _ = _gpu_vs_golden(264, 200, [0, 3], 3, 120, static=True)
+    assert ((g.mode[1:] >> 13) & 3).max() == 2
 
 
 @pytest.mark.gpu

@@ -46,7 +46,7 @@ def _gpu():
     lib = gpu_lib()
     if not getattr(lib, "_av1e_sigs", False):
         for n in ("tv_av1e_inter", "tv_av1e_intra", "tv_av1e_lfinfo", "tv_av1e_cdef_choose", "tv_av1e_lr_solve",
-                  "tv_av1e_unit_sse"):
+                  "tv_av1e_unit_sse", "tv_av1e_merge"):
             getattr(lib, n).restype = C.c_int
         lib.tv_av1e_last_error.restype = C.c_char_p
         lib._av1e_sigs = True
@@ -179,6 +179,7 @@ class Av1GpuEngine:
         else:
             _ok(lib.tv_av1e_inter(_p(sy), _p(su), _p(sv), _p(fy), _p(fu), _p(fv), _p(ry), _p(ru), _p(rv), _p(mode),
                                   _p(mv), _p(ly), _p(lu), _p(lv), W, H, B, _p(qarr), st))
+            _ok(lib.tv_av1e_merge(_p(mode), _p(mv), W, H, B, st))
         iy = torch.empty((B, H // 4, W // 4), dtype=torch.int32, device=self.dev)
         iu = torch.empty((B, H // 8, W // 8), dtype=torch.int32, device=self.dev)
         iv = torch.empty_like(iu)
