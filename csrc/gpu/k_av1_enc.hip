@@ -41,6 +41,8 @@ constexpr int R = kMeRange;
 constexpr int kWinP = 60;              // window pitch (bytes, multiple of 4)
 constexpr int kWinN = 16 + 2 * R + 9;  // 57 rows: [-R-4, R+20] around the block
 constexpr int kWinOff = R + 4;         // block origin inside the window
+// chroma window: block-relative x in [-12, 19] (integer MV part [-9, 8] + 8-tap reach)
+constexpr int kCWin = 32, kCWinOff = 12;
 
 __device__ __forceinline__ int rsr(long long v, int s) { return (int)((v + (1LL << (s - 1))) >> s); }
 __device__ __forceinline__ int c16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
@@ -163,6 +165,7 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
                                                    const int* __restrict__ qarr) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kWinN * kWinP + 8];
   __shared__ __attribute__((aligned(16))) uint8_t sblk[256];
+  __shared__ __attribute__((aligned(16))) uint8_t cwin[2][kCWin * kCWin];
   __shared__ int cost[9];
   __shared__ int16_t res[256], ta[256], tb[256];
   __shared__ int predc[256];
@@ -174,11 +177,41 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   const uint8_t* S = src.y + b * ysz;
   const uint8_t* Rf = ref.y + b * ysz;
   const int lam = lambda16(qidx);
-  // stage the clamped reference window and the source block
-  for (int i = lane; i < kWinN * kWinN; i += 64) {
-    const int wy = i / kWinN, wx = i - wy * kWinN;
-    const int yy = clip3(0, H - 1, y0 - kWinOff + wy), xx = clip3(0, W - 1, x0 - kWinOff + wx);
-    win[wy * kWinP + wx] = Rf[(long)yy * W + xx];
+  // stage the clamped reference windows (luma 57 x 57, chroma 32 x 32 per plane) and the
+  // source block; windows fully inside the frame take dword loads (their origins are
+  // 4-byte aligned: x0 - 20 and cx0 - 12 with x0 % 16 == 0, cx0 % 8 == 0)
+  const int wx0 = x0 - kWinOff, wy0 = y0 - kWinOff;
+  if (wx0 >= 0 && wy0 >= 0 && wx0 + kWinP <= W && wy0 + kWinN <= H) {
+    for (int i = lane; i < kWinN * (kWinP / 4); i += 64) {
+      const int wy = i / (kWinP / 4), wq = i - wy * (kWinP / 4);
+      reinterpret_cast<uint32_t*>(win + wy * kWinP)[wq] =
+          *reinterpret_cast<const uint32_t*>(Rf + (long)(wy0 + wy) * W + wx0 + 4 * wq);
+    }
+  } else {
+    for (int i = lane; i < kWinN * kWinN; i += 64) {
+      const int wy = i / kWinN, wx = i - wy * kWinN;
+      const int yy = clip3(0, H - 1, wy0 + wy), xx = clip3(0, W - 1, wx0 + wx);
+      win[wy * kWinP + wx] = Rf[(long)yy * W + xx];
+    }
+  }
+  {
+    const int Wc = W >> 1, Hc = H >> 1, cwx = bx * 8 - kCWinOff, cwy = by * 8 - kCWinOff;
+    const bool in = cwx >= 0 && cwy >= 0 && cwx + kCWin <= Wc && cwy + kCWin <= Hc;
+    for (int pl = 0; pl < 2; ++pl) {
+      const uint8_t* Rc = (pl ? ref.v : ref.u) + b * csz;
+      if (in) {
+        for (int i = lane; i < kCWin * (kCWin / 4); i += 64) {
+          const int wy = i / (kCWin / 4), wq = i - wy * (kCWin / 4);
+          reinterpret_cast<uint32_t*>(cwin[pl] + wy * kCWin)[wq] =
+              *reinterpret_cast<const uint32_t*>(Rc + (long)(cwy + wy) * Wc + cwx + 4 * wq);
+        }
+      } else {
+        for (int i = lane; i < kCWin * kCWin; i += 64) {
+          const int wy = i / kCWin, wx = i - wy * kCWin;
+          cwin[pl][i] = Rc[(long)clip3(0, Hc - 1, cwy + wy) * Wc + clip3(0, Wc - 1, cwx + wx)];
+        }
+      }
+    }
   }
   for (int i = lane; i < 256; i += 64) sblk[i] = S[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)];
   __syncthreads();
@@ -302,16 +335,16 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   for (int i = lane; i < 256; i += 64)
     rec.y[b * ysz + (long)(y0 + (i >> 4)) * W + x0 + (i & 15)] = (uint8_t)clip_pixel(predc[i] + res[i]);
   __syncthreads();
-  // ---- chroma (8x8 per plane), reference read through L2 with clamping
-  const int Wc = W >> 1, Hc = H >> 1, cx0 = bx * 8, cy0 = by * 8;
+  // ---- chroma (8x8 per plane) from the staged chroma windows
+  const int Wc = W >> 1, cx0 = bx * 8, cy0 = by * 8;
   const int ix = mv_int(mc, true), iy = mv_int(mr, true), fx = mv_frac(mc, true), fy = mv_frac(mr, true);
   for (int pl = 1; pl <= 2; ++pl) {
-    const uint8_t* Rc = (pl == 1 ? ref.u : ref.v) + b * csz;
     const uint8_t* Sc = (pl == 1 ? src.u : src.v) + b * csz;
-    auto cget = [&](int x, int y) -> int { return Rc[(long)clip3(0, Hc - 1, y) * Wc + clip3(0, Wc - 1, x)]; };
+    const uint8_t* cw = cwin[pl - 1];
+    auto cget = [&](int x, int y) -> int { return cw[(kCWinOff + y) * kCWin + kCWinOff + x]; };
     {
       const int yy = lane >> 3, xx = lane & 7;
-      const int p = inter_pred_px(cget, cx0 + xx + ix, cy0 + yy + iy, fx, fy);
+      const int p = inter_pred_px(cget, xx + ix, yy + iy, fx, fy);
       predc[lane] = p;
       res[lane] = (int16_t)((int)Sc[(long)(cy0 + yy) * Wc + cx0 + xx] - p);
     }
