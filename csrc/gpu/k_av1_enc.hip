@@ -166,7 +166,9 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   __shared__ __attribute__((aligned(16))) uint8_t win[kWinN * kWinP + 8];
   __shared__ __attribute__((aligned(16))) uint8_t sblk[256];
   __shared__ __attribute__((aligned(16))) uint8_t cwin[2][kCWin * kCWin];
+  __shared__ int16_t hpl[3][25][16];  // horizontally filtered planes of a sub-pel step
   __shared__ int cost[9];
+  int lastk = 1;
   __shared__ int16_t res[256], ta[256], tb[256];
   __shared__ int predc[256];
   int blk, b;
@@ -274,35 +276,46 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   auto wget = [&](int x, int y) -> int {  // window sample at block-relative (x, y)
     return win[(kWinOff + y) * kWinP + kWinOff + x];
   };
+  // Separable and shared: per step, the three horizontally filtered planes (column offsets
+  // -step, 0, +step) are computed once into LDS (int16, Round0), then each of the 9
+  // candidates only runs the vertical 8-tap pass (the same integers as inter_pred_px).
   const int grp = lane >> 4, b4 = lane & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
+  int yb = 0;
   for (int step = 4; step >= 2; step >>= 1) {
+    yb = ((mr - step) >> 3) - 3;
+    const int nrows = ((mr + step) >> 3) + 19 - yb + 1;  // <= 25
+    for (int idx = lane; idx < 3 * nrows * 16; idx += 64) {
+      const int k = idx / (nrows * 16), rem = idx - k * nrows * 16, yy = rem >> 4, x = rem & 15;
+      const int c = mc + (k - 1) * step, ix = mv_int(c, false), fx = mv_frac(c, false);
+      int sum = 0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) sum += subpel_tap(fx, t) * wget(x + ix + t - 3, yb + yy);
+      hpl[k][yy][x] = (int16_t)((sum + (1 << (kInterRound0 - 1))) >> kInterRound0);
+    }
+    __syncthreads();
     for (int pass = 0; pass < 3; ++pass) {
       const int ci = pass * 4 + grp;  // 0 = center, 1..8 = ring
-      int r = mr, c = mc;
+      int dr = 0, dc = 0;
       if (ci >= 1 && ci <= 8) {
-        r += me_ring_dy(ci - 1) * step;
-        c += me_ring_dx(ci - 1) * step;
+        dr = me_ring_dy(ci - 1) * step;
+        dc = me_ring_dx(ci - 1) * step;
       }
+      const int r = mr + dr, c = mc + dc, k = dc / step + 1;
+      const int iy = mv_int(r, false), fy = mv_frac(r, false), r0 = py + iy - 3 - yb;
       int d[16];
-      const int ix = mv_int(c, false), iy = mv_int(r, false), fx = mv_frac(c, false), fy = mv_frac(r, false);
-      int hrow[11][4];
+      int col[11][4];
 #pragma unroll
       for (int rr = 0; rr < 11; ++rr)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int s = 0;
-#pragma unroll
-          for (int t = 0; t < 8; ++t) s += subpel_tap(fx, t) * wget(px + j + ix + t - 3, py + rr + iy - 3);
-          hrow[rr][j] = (s + (1 << (kInterRound0 - 1))) >> kInterRound0;
-        }
+        for (int j = 0; j < 4; ++j) col[rr][j] = hpl[k][r0 + rr][px + j];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          int s = 0;
+          int sum = 0;
 #pragma unroll
-          for (int t = 0; t < 8; ++t) s += subpel_tap(fy, t) * hrow[i + t][j];
-          const int p = clip_pixel((s + (1 << (kInterRound1 - 1))) >> kInterRound1);
+          for (int t = 0; t < 8; ++t) sum += subpel_tap(fy, t) * col[i + t][j];
+          const int p = clip_pixel((sum + (1 << (kInterRound1 - 1))) >> kInterRound1);
           d[i * 4 + j] = (int)sblk[(py + i) * 16 + px + j] - p;
         }
       const int sat = row16_sum(satd4(d));
@@ -315,15 +328,22 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
     if (bi) {
       mr += me_ring_dy(bi - 1) * step;
       mc += me_ring_dx(bi - 1) * step;
+      lastk = me_ring_dx(bi - 1) + 1;
+    } else {
+      lastk = 1;
     }
     __syncthreads();
   }
-  // ---- luma prediction + residual
+  // ---- luma prediction + residual: vertical pass of the chosen candidate over the last
+  // step's horizontal plane
   {
-    const int ix = mv_int(mc, false), iy = mv_int(mr, false), fx = mv_frac(mc, false), fy = mv_frac(mr, false);
+    const int iy = mv_int(mr, false), fy = mv_frac(mr, false);
     for (int i = lane; i < 256; i += 64) {
-      const int yy = i >> 4, xx = i & 15;
-      const int p = inter_pred_px(wget, xx + ix, yy + iy, fx, fy);
+      const int yy = i >> 4, xx = i & 15, r0 = yy + iy - 3 - yb;
+      int sum = 0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) sum += subpel_tap(fy, t) * hpl[lastk][r0 + t][xx];
+      const int p = clip_pixel((sum + (1 << (kInterRound1 - 1))) >> kInterRound1);
       predc[i] = p;
       res[i] = (int16_t)((int)sblk[i] - p);
     }

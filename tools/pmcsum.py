@@ -6,7 +6,7 @@ from collections import defaultdict
 agg = defaultdict(lambda: defaultdict(float))
 calls = defaultdict(set)
 for r in csv.DictReader(open(sys.argv[1])):
-    k = r["Kernel_Name"].split("(")[0].replace("tv::gpu::", "")
+    k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("tv::gpu::", "")
     if len(sys.argv) > 2 and sys.argv[2] not in k:
         continue
     agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
