@@ -253,7 +253,7 @@ def job_main(args) -> None:
     from thinvids_amd.common import save_settings
     from thinvids_amd.worker.node_executor import live_executor, submit
 
-    save_settings({"tv_gop": str(args.gop), "tv_qp": str(args.qp), "tv_sao": "1" if args.sao else "0",
+    save_settings({"tv_codec": args.codec, "tv_gop": str(args.gop), "tv_qp": str(args.qp), "tv_sao": "1" if args.sao else "0",
                    "tv_search_range": str(args.range), "tv_node_segment_frames": str(args.gop * 16),
                    "tv_node_batch": str(max(1, (args.batch or (48 if w * h <= 1920 * 1088 else 24)) // 16))}, store)
     import threading
@@ -291,9 +291,12 @@ def job_main(args) -> None:
     print(json.dumps({
         "metric": JOB_METRIC, "value": round(frames / el, 2), "unit": "frames/s", "n_gpus": args.gpus,
         "steps": 1, "warmup": 1, "ms_per_step": round(1000 * el, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "uint8 video / int32 integer transforms (bit-exact HEVC)",
+        "vs_baseline": None, "dtype": "uint8 video / int32 integer transforms (bit-exact "
+        + ("AV1 subset)" if args.codec == "av1" else "HEVC)"),
         "data": "synthetic (seeded procedural YUV 4:2:0 .synth source generated on each GPU)",
-        "config": {"model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else ""),
+        "config": {"model": (f"AV1 subset (tv) q-index for QP{args.qp} {args.res} synthetic" if args.codec == "av1" else
+                             f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else "")),
+                   "codec": job.get("dest_codec"),
                    "job_frames": frames, "resolution": f"{w}x{h}", "parallelism": f"dp{args.gpus} node executor",
                    "job_wall_s": round(el, 3), "job_fps_reported": float(job.get("job_fps") or 0),
                    "encode_fps_reported": float(job.get("encode_fps") or 0), "psnr_y_db": float(job.get("psnr_y") or 0),
