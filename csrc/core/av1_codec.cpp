@@ -1722,11 +1722,11 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
     cdef_find_dirs(db.y.data(), W, H, dir.data(), var.data());
     std::vector<uint64_t> sy((size_t)nfb * kCdefPresets), su(sy.size()), sv(sy.size());
     cdef_search(S.y.data(), db.y.data(), W, H, false, dir.data(), var.data(), W / 8, fd.fp.cdef_damping, sy.data(),
-                kCdefMaskY);
+                kCdefMaskY, true);
     cdef_search(S.u.data(), db.u.data(), W / 2, H / 2, true, dir.data(), var.data(), W / 8, fd.fp.cdef_damping,
-                su.data(), kCdefMaskUV);
+                su.data(), kCdefMaskUV, true);
     cdef_search(S.v.data(), db.v.data(), W / 2, H / 2, true, dir.data(), var.data(), W / 8, fd.fp.cdef_damping,
-                sv.data(), kCdefMaskUV);
+                sv.data(), kCdefMaskUV, true);
     for (size_t i = 0; i < su.size(); ++i) su[i] += sv[i];
     std::vector<uint8_t> active(nfb, 0);
     for (int b = 0; b < nb; ++b)

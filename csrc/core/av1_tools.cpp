@@ -52,7 +52,7 @@ inline void block_strengths(int p, bool chroma, int v, int& pri, int& sec) {
 }  // namespace
 
 void cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, bool chroma, const uint8_t* dir,
-                 const int* var, int luma_w8, int damping, uint64_t* sse, uint64_t pmask) {
+                 const int* var, int luma_w8, int damping, uint64_t* sse, uint64_t pmask, bool checker) {
   const int bs = chroma ? 4 : 8, fbs = fb_size(chroma), nfx = (w + fbs - 1) / fbs;
   const int dmp = chroma ? damping - 1 : damping;
   std::memset(sse, 0, sizeof(uint64_t) * nfb_of(w, h, chroma) * kCdefPresets);
@@ -63,6 +63,7 @@ void cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, bool chro
   auto band = [&](int fr) {
     for (int by = fr * fbs / bs; by < std::min(h / bs, (fr + 1) * fbs / bs); ++by)
     for (int bx = 0; bx < w / bs; ++bx) {
+      if (checker && ((bx + by) & 1)) continue;  // encoder search on a checkerboard of blocks
       const int d = dir[by * luma_w8 + bx], v = var[by * luma_w8 + bx];
       uint64_t* S = sse + (long)((by * bs / fbs) * nfx + bx * bs / fbs) * kCdefPresets;
       for (int p = 0; p < kCdefPresets; ++p) {
@@ -463,7 +464,7 @@ const char* tv_av1_last_error() { return g_av1_err.c_str(); }
 void tv_av1_cdef_find_dirs(const uint8_t* Y, int w, int h, uint8_t* dir, int* var) { cdef_find_dirs(Y, w, h, dir, var); }
 void tv_av1_cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, int chroma, const uint8_t* dir,
                         const int* var, int luma_w8, int damping, uint64_t* sse) {
-  cdef_search(src, rec, w, h, chroma != 0, dir, var, luma_w8, damping, sse, ~0ull);
+  cdef_search(src, rec, w, h, chroma != 0, dir, var, luma_w8, damping, sse, ~0ull, false);
 }
 void tv_av1_cdef_apply(const uint8_t* rec, int w, int h, int chroma, const uint8_t* dir, const int* var, int luma_w8,
                        int damping, const int8_t* fb_preset, uint8_t* out) {

@@ -124,7 +124,8 @@ __device__ __forceinline__ int cdef_tile_filter(const int16_t (*T)[kTile], int t
 __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__ src, const uint8_t* __restrict__ rec,
                                                      int w, int h, int chroma, const uint8_t* __restrict__ dir,
                                                      const int* __restrict__ var, int luma_w8, int luma_n8,
-                                                     int damping, unsigned long long* sse, unsigned long long pmask) {
+                                                     int damping, unsigned long long* sse, unsigned long long pmask,
+                                                     int checker) {
   const int b = blockIdx.y, fb = blockIdx.x;
   const int bs_l2 = chroma ? 2 : 3, fbs = chroma ? 32 : 64, nfx = (w + fbs - 1) / fbs;
   const int x0 = (fb % nfx) * fbs, y0 = (fb / nfx) * fbs;
@@ -144,14 +145,28 @@ __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__
     for (int k = 0, n = 0; k < kCdefPresets; ++k)
       if (pmask >> k & 1) plist[n++] = (int8_t)k;
   __syncthreads();
-  const int np = __popcll(pmask), npx = fbw * fbh;
+  // measured blocks of this filter block (all, or the (bx + by)-even checkerboard), listed
+  // so the threads stream only over their pixels
+  __shared__ uint8_t blist[64];
+  __shared__ int nbl;
+  const int bsz = 1 << bs_l2, ppb = bsz * bsz;
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int by = 0; by < (fbh >> bs_l2); ++by)
+      for (int bx = 0; bx < (fbw >> bs_l2); ++bx)
+        if (!checker || !((bx + by) & 1)) blist[n++] = (uint8_t)(by * 8 + bx);
+    nbl = n;
+  }
+  __syncthreads();
+  const int np = __popcll(pmask), npx = nbl * ppb;
   for (int c0 = 0; c0 < np; c0 += 16) {
     const int nc = min(16, np - c0);
     unsigned a16[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) a16[k] = 0;
     for (int q = threadIdx.x; q < npx; q += 256) {
-      const int i = q / fbw, j = q - i * fbw, x = x0 + j, y = y0 + i;
+      const int bk = blist[q / ppb], pq = q - (q / ppb) * ppb;
+      const int i = (bk >> 3) * bsz + pq / bsz, j = (bk & 7) * bsz + (pq & (bsz - 1)), x = x0 + j, y = y0 + i;
       const long kb = (long)b * luma_n8 + (y >> bs_l2) * luma_w8 + (x >> bs_l2);
       const int d = dir[kb], vr = chroma ? 0 : var[kb];
       const int ty = i + kHalo, tx = j + kHalo, c = T[ty][tx];
@@ -578,11 +593,11 @@ int tv_gpu_cdef_dirs(const uint8_t* Y, int w, int h, int B, uint8_t* dir, int* v
 // sse: [B][nfb][64] (uint64)
 int tv_gpu_cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, int B, int chroma, const uint8_t* dir,
                        const int* var, int luma_w8, int luma_n8, int damping, unsigned long long* sse, void* stream,
-                       unsigned long long pmask) {
+                       unsigned long long pmask, int checker) {
   if (bad_geo(w, h, B, chroma ? 4 : 8, "cdef_search") || damping < 3 || damping > 6 || !pmask) return -1;
   const int fbs = chroma ? 32 : 64, nfb = ((w + fbs - 1) / fbs) * ((h + fbs - 1) / fbs);
   k_cdef_search<<<dim3(nfb, B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, chroma, dir, var, luma_w8, luma_n8,
-                                                               damping, sse, pmask);
+                                                               damping, sse, pmask, checker);
   return av1_status("cdef_search");
 }
 int tv_gpu_cdef_apply(const uint8_t* rec, int w, int h, int B, int chroma, const uint8_t* dir, const int* var,

@@ -19,7 +19,8 @@ void cdef_find_dirs(const uint8_t* Y, int w, int h, uint8_t* dir, int* var);
 // pmask: presets to evaluate (bit p); the others get kCdefSkipped (an SSE no evaluated
 // preset reaches, small enough that sums over every filter block cannot overflow).
 void cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, bool chroma, const uint8_t* dir,
-                 const int* var, int luma_w8, int damping, uint64_t* sse, uint64_t pmask = ~0ull);
+                 const int* var, int luma_w8, int damping, uint64_t* sse, uint64_t pmask = ~0ull,
+                 bool checker = false);  // checker: only blocks with (bx + by) even (encoder search)
 // Filter a plane with a per-filter-block preset index (-1 = off) into `out`.
 void cdef_apply(const uint8_t* rec, int w, int h, bool chroma, const uint8_t* dir, const int* var, int luma_w8,
                 int damping, const int8_t* fb_preset, uint8_t* out);

@@ -188,9 +188,9 @@ class Av1GpuEngine:
         du = ops.deblock(ru, iu, True, 0)
         dv = ops.deblock(rv, iv, True, 0)
         dirs, var = ops.cdef_dirs(dy)
-        se_y = ops.cdef_search(sy, dy, dirs, var, False, self.damping, pmask=CDEF_MASK_Y)
-        se_u = ops.cdef_search(su, du, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV)
-        se_v = ops.cdef_search(sv, dv, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV)
+        se_y = ops.cdef_search(sy, dy, dirs, var, False, self.damping, pmask=CDEF_MASK_Y, checker=True)
+        se_u = ops.cdef_search(su, du, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV, checker=True)
+        se_v = ops.cdef_search(sv, dv, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV, checker=True)
         py = torch.empty((B, self.nfb), dtype=torch.int8, device=self.dev)
         puv = torch.empty_like(py)
         _ok(lib.tv_av1e_cdef_choose(_p(se_y), _p(se_u), _p(se_v), _p(mode), W, H, B, _p(self.g_tabs[t, :B]),

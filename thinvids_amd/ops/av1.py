@@ -129,10 +129,11 @@ def cdef_dirs(Y):
 
 
 def cdef_search(src, rec, dirs, var, chroma: bool, damping: int = 5, luma_w8: int | None = None,
-                pmask: int = (1 << 64) - 1):
+                pmask: int = (1 << 64) - 1, checker: bool = False):
     """SSE of every (64x64 filter block, preset) after CDEF: numpy -> (nfb, 64) uint64;
     torch (B, h, w) -> (B, nfb, 64) int64.  `pmask` (GPU path) restricts the evaluated
-    presets (bit p); the others report 2^40."""
+    presets (bit p); the others report 2^40.  `checker`: only the 8x8 (chroma 4x4) blocks
+    with (bx + by) even are measured (the AV1 encoder's search)."""
     if _is_np(rec):
         h, w = rec.shape
         lw8 = luma_w8 or (w * (2 if chroma else 1)) // 8
@@ -148,7 +149,7 @@ def cdef_search(src, rec, dirs, var, chroma: bool, damping: int = 5, luma_w8: in
     out = torch.empty((B, n_fb(w, h, chroma), PRESETS), dtype=torch.int64, device=rec.device)
     _check(_gpu().tv_gpu_cdef_search(_t(src.contiguous()), _t(rec.contiguous()), w, h, B, int(chroma),
                                      _t(dirs), _t(var), lw8, dirs.shape[-1], damping, _t(out), _stream(rec),
-                                     C.c_ulonglong(pmask)))
+                                     C.c_ulonglong(pmask), int(checker)))
     return out
 
 
