@@ -266,7 +266,12 @@ def test_job_settings_encoder_overrides(mgr):
 
     job = {**st.hgetall(f"job:{jid}"), "source_width": 1920, "source_height": 1080, "rc_mode": "crf", "crf": "24"}
     p = _job_params(job)
-    assert p["rc"] == "crf" and p["crf"] == 24 and p["ladder"] == [1080, 720]
+    assert p["rc"] == "crf" and p["crf"] == 24 and p["ladder"] == [1080, 720] and p["codec"] == "hevc"
+    # per-job codec override (AV1 engine, BASELINE config #4)
+    assert c.post(f"/job_settings/{jid}", json={"codec": "av1"}).status_code == 200
+    assert c.get(f"/job_settings/{jid}").json["codec"] == "av1"
+    assert c.post(f"/job_settings/{jid}", json={"codec": "vp9"}).status_code == 500
+    assert _job_params({**st.hgetall(f"job:{jid}"), "source_width": 1920, "source_height": 1080})["codec"] == "av1"
 
 
 def test_nodes_detail_fields(mgr):

@@ -320,6 +320,7 @@ def settings_from_payload(p: dict, cur: dict) -> dict:
 
 # ------------------------------------------------------------------------- app
 RC_MODES = ("", "cqp", "crf", "2pass", "abr")
+CODECS = ("", "hevc", "av1")
 
 
 def encoder_overrides(d: dict) -> dict:
@@ -353,6 +354,11 @@ def encoder_overrides(d: dict) -> dict:
         out["ladder"] = ",".join(str(r) for r in rungs)
     if "node_executor" in d:
         out["node_executor"] = "" if d["node_executor"] in ("", None) else ("1" if as_bool(d["node_executor"]) else "0")
+    if "codec" in d:
+        c = str(d["codec"] or "").lower()
+        if c not in CODECS:
+            raise ValueError(f"codec must be one of {CODECS[1:]}")
+        out["codec"] = c
     return out
 
 
@@ -887,7 +893,7 @@ def create_app(store=None, housekeeping: bool = False) -> Flask:
                             # encoder knobs of this framework (per-job overrides of tv_*)
                             "rc_mode": job.get("rc_mode", ""), "qp": job.get("qp", ""), "crf": job.get("crf", ""),
                             "bitrate_kbps": job.get("bitrate_kbps", ""), "ladder": job.get("ladder", ""),
-                            "node_executor": job.get("node_executor", ""),
+                            "node_executor": job.get("node_executor", ""), "codec": job.get("codec", ""),
                             "source_fps": job.get("source_fps", "")})
         if core.job_status(job) == Status.RUNNING:
             return jsonify({"error": "Job is RUNNING; stop it or copy/restart to change settings."}), 400
