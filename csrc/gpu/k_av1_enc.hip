@@ -237,42 +237,22 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
     return sad;
   };
   unsigned best = 0xFFFFFFFFu;
-  // 2-pel grid: lane -> one column offset (cx) and a run of 6 row offsets (cy = 6g .. 6g+5);
-  // the 26 window rows of the run are read once and feed every (row offset, block row) pair
-  // that uses them (the index arithmetic is compile-time after unrolling).
-  if (lane < 3 * kMeGrid) {
-    const int cx = lane % kMeGrid, g = lane / kMeGrid, dx = 2 * cx - kMeRange, cy0 = 6 * g;
+  for (int k = lane; k < kMeGrid * kMeGrid; k += 64) {  // 2-pel grid, one candidate per lane
+    const int dx = me_cand_dx(k), dy = me_cand_dy(k);
+    unsigned sad = 0;
     const int ox = kWinOff + dx, sh = ox & 3;
-    unsigned sad[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int r = 0; r < 26; ++r) {
-      const int wy = kWinOff + 2 * cy0 - kMeRange + r;
-      if (wy >= kWinN) break;
-      const uint32_t* row = reinterpret_cast<const uint32_t*>(win + wy * kWinP + (ox & ~3));
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(win + (kWinOff + dy + i) * kWinP + (ox & ~3));
       const uint32_t w0 = row[0], w1 = row[1], w2 = row[2], w3 = row[3], w4 = row[4];
-      const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, sh), a1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-      const uint32_t a2 = __builtin_amdgcn_alignbyte(w3, w2, sh), a3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int i = r - 2 * j;  // block row of candidate cy0 + j that this window row feeds
-        if (i < 0 || i > 15) continue;
-        unsigned v = sad[j];
-        v = __builtin_amdgcn_sad_u8(sv[i * 4 + 0], a0, v);
-        v = __builtin_amdgcn_sad_u8(sv[i * 4 + 1], a1, v);
-        v = __builtin_amdgcn_sad_u8(sv[i * 4 + 2], a2, v);
-        v = __builtin_amdgcn_sad_u8(sv[i * 4 + 3], a3, v);
-        sad[j] = v;
-      }
+      sad = __builtin_amdgcn_sad_u8(sv[i * 4 + 0], __builtin_amdgcn_alignbyte(w1, w0, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sv[i * 4 + 1], __builtin_amdgcn_alignbyte(w2, w1, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sv[i * 4 + 2], __builtin_amdgcn_alignbyte(w3, w2, sh), sad);
+      sad = __builtin_amdgcn_sad_u8(sv[i * 4 + 3], __builtin_amdgcn_alignbyte(w4, w3, sh), sad);
     }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int cy = cy0 + j;
-      if (cy >= kMeGrid) break;
-      const int dy = 2 * cy - kMeRange, k = cy * kMeGrid + cx;
-      const unsigned c = sad[j] + ((lam * (mv_comp_bits(dy * 8) + mv_comp_bits(dx * 8))) >> 4);
-      const unsigned key = (c << 12) | (unsigned)k;
-      best = key < best ? key : best;
-    }
+    const unsigned c = sad + ((lam * (mv_comp_bits(dy * 8) + mv_comp_bits(dx * 8))) >> 4);
+    const unsigned key = (c << 12) | (unsigned)k;
+    best = key < best ? key : best;
   }
   best = wave_min_u32(best);
   const int bk = best & 4095;
