@@ -342,6 +342,33 @@ def av1_main(args) -> None:
         gathered = gather_bytes_to_root(b"".join(segs), dev)
         return stats.cpu().numpy(), (sum(len(x) for x in gathered) if gathered else 0)
 
+    def two_pass(load):
+        """Config #4's 2-pass: pass 1 at the base q-index -> per-frame bits of every rank's
+        segments all-reduced (RCCL) -> one global per-frame plan for the target bitrate
+        (ratecontrol.plan_frame_qps) -> pass 2 with the plan's per-frame q-index maps."""
+        from thinvids_amd.models.ratecontrol import frame_sizes, plan_frame_qps, round_qps
+
+        g1 = eng.encode_gop(args.gop, load)
+        seg1 = [b"".join(f.result()) for f in eng.submit_entropy(g1)]
+        flat = torch.zeros(world * batch * args.gop, dtype=torch.float64, device=dev)
+        mine = np.concatenate([8.0 * np.asarray(frame_sizes(x), np.float64) for x in seg1])
+        flat[rank * batch * args.gop:(rank + 1) * batch * args.gop] = torch.from_numpy(mine).to(dev)
+        dist.all_reduce(flat)  # RC statistics all-reduce over the node
+        allb = flat.cpu().numpy().reshape(world * batch, args.gop)
+        target = args.kbps * 1000.0 * (world * batch * args.gop) / 30.0
+        plan, _ = plan_frame_qps(list(allb), args.qp, target)
+        qm = np.array([[av1m.qindex_for_hevc_qp(int(v)) for v in round_qps(plan[rank * batch + b])]
+                       for b in range(batch)], np.int32).T
+        g2 = eng.encode_gop(args.gop, load, qmap=qm)
+        return g2, [b"".join(f.result()) for f in eng.submit_entropy(g2)]
+
+    def comm2(g, segs):
+        sse = g.sse.sum(axis=(0, 1)).astype(np.float64)
+        stats = torch.tensor([batch * args.gop, sum(len(x) for x in segs), *sse], dtype=torch.float64, device=dev)
+        dist.all_reduce(stats)
+        gathered = gather_bytes_to_root(b"".join(segs), dev)
+        return stats.cpu().numpy(), (sum(len(x) for x in gathered) if gathered else 0)
+
     def step(s: int):
         base = (s * world + rank) * batch
         st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -354,7 +381,11 @@ def av1_main(args) -> None:
                 stage._ok(lib.tv_pad_batch(C.c_void_p(src.ptr(c)), pw, ph, stride, fs, C.c_void_p(dst.data_ptr()),
                                            cw, chh, cw, cw * chh, batch, st))
 
-        post.submit(comm, eng.encode_gop(args.gop, load, async_host=True))
+        if args.kbps > 0:  # both passes and their collectives on this thread, in step order
+            res2 = comm2(*two_pass(load))
+            post.submit(lambda r=res2: r)
+        else:
+            post.submit(comm, eng.encode_gop(args.gop, load, async_host=True))
 
     el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), eng.pool._max_workers])
     tot = np.sum([r[0] for r in res], axis=0)
@@ -377,7 +408,10 @@ def av1_main(args) -> None:
             "dtype": "uint8 video / int32 integer transforms (bit-exact AV1 subset)",
             "data": "synthetic (seeded procedural YUV 4:2:0 source generated on GPU)",
             "config": {
-                "model": f"AV1 subset (tv) qindex {q} 16x16 blocks +deblock +CDEF {args.res} synthetic",
+                "model": f"AV1 subset (tv) qindex {q} 16x16 blocks +deblock +CDEF +LR {args.res} synthetic"
+                + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
+                "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame q-index plan, target "
+                                 f"{args.kbps:g} kbps per 30 fps stream" if args.kbps > 0 else "constant q-index"),
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",
@@ -418,6 +452,7 @@ def main() -> None:
     ap.add_argument("--job-frames", type=int, default=0)
     ap.add_argument("--codec", default="hevc", choices=["hevc", "av1"], help="av1: BASELINE config #4 engine")
     ap.add_argument("--qindex", type=int, default=0, help="AV1 q-index (0 = matched to --qp)")
+    ap.add_argument("--kbps", type=float, default=0.0, help="AV1: 2-pass rate control to this kbps per 30 fps stream")
     args = ap.parse_args()
     if args.job:
         return job_main(args)
