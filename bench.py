@@ -26,6 +26,7 @@ METRIC = "encoded frames/sec (whole node) at fixed PSNR, 1080p & 4K HEVC, 1/2/4/
 RES = {"1080p": (1920, 1080), "4k": (3840, 2160), "720p": (1280, 720), "360p": (640, 360)}
 SRC = {"8k": (7680, 4320), "4k": (3840, 2160), "1080p": (1920, 1080)}
 LADDER_METRIC = "HDR10 source frames/sec (whole node) through a tone-map + Lanczos + HEVC ABR ladder"
+AV1_KEY_QP_OFFSET = -2.0  # 2-pass: key frame QP relative to its segment's inter frames
 AV1_METRIC = "encoded frames/sec (whole node) at fixed PSNR, AV1 (CDEF in loop), 1/2/4/8 MI355X"
 
 
@@ -342,6 +343,8 @@ def av1_main(args) -> None:
         gathered = gather_bytes_to_root(b"".join(segs), dev)
         return stats.cpu().numpy(), (sum(len(x) for x in gathered) if gathered else 0)
 
+    pass1_bits = []
+
     def two_pass(load):
         """Config #4's 2-pass: pass 1 at the base q-index -> per-frame bits of every rank's
         segments all-reduced (RCCL) -> one global per-frame plan for the target bitrate
@@ -356,10 +359,11 @@ def av1_main(args) -> None:
         dist.all_reduce(flat)  # RC statistics all-reduce over the node
         allb = flat.cpu().numpy().reshape(world * batch, args.gop)
         target = args.kbps * 1000.0 * (world * batch * args.gop) / 30.0
-        plan, _ = plan_frame_qps(list(allb), args.qp, target)
+        plan, _ = plan_frame_qps(list(allb), args.qp, target, key_offset=AV1_KEY_QP_OFFSET)
         qm = np.array([[av1m.qindex_for_hevc_qp(int(v)) for v in round_qps(plan[rank * batch + b])]
                        for b in range(batch)], np.int32).T
         g2 = eng.encode_gop(args.gop, load, qmap=qm)
+        pass1_bits.append(float(mine.sum()))
         return g2, [b"".join(f.result()) for f in eng.submit_entropy(g2)]
 
     def comm2(g, segs):
@@ -422,6 +426,8 @@ def av1_main(args) -> None:
                 "psnr_y_db": round(py, 3),
                 "psnr_yuv_db": round((6 * py + pu + pv) / 8, 3),
                 "kbps_per_30fps_stream": round(tot[1] * 8 / (frames / 30.0) / 1000.0, 1),
+                "pass1_kbps_rank0": round(sum(pass1_bits[-args.steps:]) / (batch * args.gop * args.steps / 30.0)
+                                          / 1000.0, 1) if pass1_bits else None,
                 "gathered_mb_at_root": round(sum(r[1] for r in res) / 1e6, 3),
                 "per_rank_cpu": [{"busy_cores": r[0], "pinned_cpus": int(r[1]), "writer_threads": int(r[2])}
                                  for r in ranks],

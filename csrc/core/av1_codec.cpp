@@ -1589,7 +1589,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
     fd.fp.qindex = qidx;
     const int lvl = lf_level_for_q(qidx);
     for (int i = 0; i < 4; ++i) fd.fp.lf[i] = lvl;
-    fd.fp.cdef_damping = 3 + (qidx >> 6);
+    fd.fp.cdef_damping = 3 + (qidx0 >> 6);  // per stream (the engine's CDEF launches take one damping)
     fd.mode.assign(nb, 0);
     fd.mv.assign(nb, 0);
     fd.ly.assign((size_t)nb * 256, 0);

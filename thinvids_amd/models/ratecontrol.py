@@ -102,15 +102,34 @@ def predict_bits(b1: np.ndarray, q1, q) -> np.ndarray:
 
 
 def plan_frame_qps(bits1: list, q1: int, target_bits: float, qcomp: float = QCOMP, qp_min: int = 10,
-                   qp_max: int = 51) -> tuple[list, float]:
+                   qp_max: int = 51, key_offset: float | None = None) -> tuple[list, float]:
     """Per-frame real-valued QPs for pass 2.  bits1: per segment, the pass-1 bits of every
     frame (encoded at q1).  Frame f gets a share t_f proportional to b_f^qcomp (compressed
     complexity, as x264's qcomp), scaled so sum(t) == target_bits; its QP is the one the
-    model says yields t_f.  Returns (per-segment QP arrays, predicted total bits)."""
+    model says yields t_f.  `key_offset` (AV1 path): the first frame of every segment (its
+    key frame) is instead pinned `key_offset` QP from its segment's mean inter-frame QP —
+    the inter frames predict from it, so starving it costs more bits than it saves (the
+    frame-independent bits model misses that) — and one uniform shift of every QP, found
+    by bisection, restores the target.  Returns (per-segment QP arrays, predicted total)."""
     flat = np.concatenate([np.maximum(np.asarray(b, np.float64), 1.0) for b in bits1])
     w = flat ** qcomp
     t = target_bits * w / w.sum()
     q = np.clip(q1 + SLOPE * np.log2(flat / t), qp_min, qp_max)
+    if key_offset is not None:
+        k, keys = 0, []
+        for b in bits1:
+            if len(b) > 1:
+                q[k] = float(np.mean(q[k + 1:k + len(b)])) + key_offset
+            keys.append(k)
+            k += len(b)
+        lo, hi = -30.0, 30.0
+        for _ in range(50):  # predicted bits fall monotonically with a uniform shift
+            mid = (lo + hi) / 2
+            if predict_bits(flat, q1, np.clip(q + mid, qp_min, qp_max)).sum() > target_bits:
+                lo = mid
+            else:
+                hi = mid
+        q = np.clip(q + (lo + hi) / 2, qp_min, qp_max)
     out, k = [], 0
     for b in bits1:
         out.append(q[k:k + len(b)])

@@ -523,7 +523,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         for r in range(len(rungs)):
             scale = (rungs[r][0] * rungs[r][1]) / (rungs[0][0] * rungs[0][1])  # per-rung budget ~ pixels
             target = bitrate_kbps * 1000 * nfr / fps * scale
-            per_seg, _ = plan_frame_qps([rc["b1"][(r, i)] for i in range(len(segs))], qp, target)
+            per_seg, _ = plan_frame_qps([rc["b1"][(r, i)] for i in range(len(segs))], qp, target,
+                                        key_offset=-2.0 if codec == "av1" else None)
             plan.append(per_seg)
         rc["plan"] = plan
         targets = [bitrate_kbps * 1000 * nfr / fps * (rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]
