@@ -70,21 +70,11 @@ namespace {
 struct Scans {
   int16_t s8[64], s16[256];
 };
-void zigzag(int N, int16_t* out) {
-  int k = 0;
-  for (int s = 0; s <= 2 * N - 2; ++s) {
-    const int lo = std::max(0, s - N + 1), hi = std::min(s, N - 1);
-    if (s & 1)
-      for (int r = lo; r <= hi; ++r) out[k++] = (int16_t)(r * N + (s - r));
-    else
-      for (int r = hi; r >= lo; --r) out[k++] = (int16_t)(r * N + (s - r));
-  }
-}
 const Scans& scans() {
   static const Scans s = [] {
     Scans t;
-    zigzag(8, t.s8);
-    zigzag(16, t.s16);
+    zigzag_scan(8, t.s8);
+    zigzag_scan(16, t.s16);
     return t;
   }();
   return s;
@@ -1220,6 +1210,23 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
   // level access (packed layout: prefix offsets over the nonzero masks)
   std::vector<int32_t> off[3];
   const int16_t* base[3] = {d.ly, d.lu, d.lv};
+  std::vector<int16_t> expd[3];
+  if (d.scan_packed)  // [eob, eob levels in scan order] per nonzero TB -> raster TBs
+    for (int p = 0; p < 3; ++p) {
+      const int sz = p ? 64 : 256;
+      const int16_t* scan = p ? scans().s8 : scans().s16;
+      int cnt = 0;
+      for (int b = 0; b < nb; ++b) cnt += mode_nz(mode[b]) >> p & 1;
+      expd[p].assign((size_t)cnt * sz, 0);
+      const int16_t* q = base[p];
+      for (int k = 0; k < cnt; ++k) {
+        const int eob = *q++;
+        if (eob < 1 || eob > sz) throw std::runtime_error("scan-packed levels: bad eob");
+        for (int i = 0; i < eob; ++i) expd[p][(size_t)k * sz + scan[i]] = q[i];
+        q += eob;
+      }
+      base[p] = expd[p].data();
+    }
   if (d.packed)
     for (int p = 0; p < 3; ++p) {
       off[p].assign(nb, -1);
@@ -1893,7 +1900,8 @@ int tv_av1c_probe(const uint8_t* data, size_t n, int* geo, int* nframes) {
   return tv_av1c_decode(data, n, 0, nullptr, geo, nframes);
 }
 
-// Write one frame's temporal unit from engine decisions (packed levels layout).
+// Write one frame's temporal unit from engine decisions (packed levels layout; packed == 2:
+// eob-truncated scan-order TBs, FrameDecisions::scan_packed).
 void* tv_av1c_state_new() { return new EntropyState(); }
 void tv_av1c_state_free(void* s) { delete static_cast<EntropyState*>(s); }
 
@@ -1914,6 +1922,7 @@ int tv_av1c_write_tu(void* state, int dw, int dh, const int* fparams, const uint
     d.cdef_idx = cdef_idx;
     d.lr = lr;
     d.packed = packed != 0;
+    d.scan_packed = packed == 2;
     auto tu = write_temporal_unit(g, d, seq_header != 0, static_cast<EntropyState*>(state));
     auto* bytes = static_cast<std::vector<uint8_t>*>(out);
     bytes->insert(bytes->end(), tu.begin(), tu.end());

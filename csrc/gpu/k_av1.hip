@@ -341,7 +341,7 @@ constexpr int kAb = kRu + 2;  // A/B planes cover the unit + 1
 
 // guided output (RST domain) for the unit's pixels, radius r, into F (registers, 16/thread)
 __device__ void sgr_guided(const uint8_t (*T)[kLrTile], int w, int h, int ux, int uy, int uw, int uh, int r, int eps,
-                           int (*A)[kAb], int (*Bv)[kAb], int* F) {
+                           uint16_t (*A)[kAb], uint16_t (*Bv)[kAb], const uint16_t* xt, int* F) {
   // A/B at plane positions clamp(uy - 1 + i), clamp(ux - 1 + j): box sums around the clamped
   // position over clamped coordinates (tile halo covers +-3 around the unit)
   for (int q = threadIdx.x; q < (uw + 2) * (uh + 2); q += blockDim.x) {
@@ -355,7 +355,10 @@ __device__ void sgr_guided(const uint8_t (*T)[kLrTile], int w, int h, int ux, in
         s += v;
         sq += v * v;
       }
-    sgr_ab(s, sq, r, eps, &A[i][j], &Bv[i][j]);
+    int a, bb;
+    sgr_ab_x(s, sq, r, eps, [&](unsigned z) -> int { return xt[z < 255u ? z : 255u]; }, &a, &bb);
+    A[i][j] = (uint16_t)a;
+    Bv[i][j] = (uint16_t)bb;
   }
   __syncthreads();
   int n = 0;
@@ -384,7 +387,7 @@ __global__ void __launch_bounds__(256) k_sgr(const uint8_t* __restrict__ src, co
   const int ux = (u % nux) * kRu, uy = (u / nux) * kRu, uw = min(kRu, w - ux), uh = min(kRu, h - uy);
   const long po = (long)b * w * h;
   __shared__ uint8_t T[kLrTile][kLrTile];
-  __shared__ int A[kAb][kAb], Bv[kAb][kAb];
+  __shared__ uint16_t A[kAb][kAb], Bv[kAb][kAb], xt[256];
   __shared__ unsigned long long red[5];
   const int* pr = kStats ? nullptr : params + ((long)b * nu + u) * 3;
   const int set = kStats ? set_all : pr[0];
@@ -396,6 +399,7 @@ __global__ void __launch_bounds__(256) k_sgr(const uint8_t* __restrict__ src, co
     return;
   }
   lr_stage(rec + po, w, h, ux, uy, uw, uh, T);
+  if (threadIdx.x < 256) xt[threadIdx.x] = (uint16_t)sgr_xbyx1(threadIdx.x);
   if (kStats && threadIdx.x < 5) red[threadIdx.x] = 0;
   __syncthreads();
   const int r0 = sgr_param(set, 0), r1 = sgr_param(set, 2);
@@ -405,8 +409,8 @@ __global__ void __launch_bounds__(256) k_sgr(const uint8_t* __restrict__ src, co
     const int i = q / uw, j = q - i * uw;
     f0[n] = f1[n] = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
   }
-  if (r0) sgr_guided(T, w, h, ux, uy, uw, uh, r0, sgr_param(set, 1), A, Bv, f0);
-  if (r1) sgr_guided(T, w, h, ux, uy, uw, uh, r1, sgr_param(set, 3), A, Bv, f1);
+  if (r0) sgr_guided(T, w, h, ux, uy, uw, uh, r0, sgr_param(set, 1), A, Bv, xt, f0);
+  if (r1) sgr_guided(T, w, h, ux, uy, uw, uh, r1, sgr_param(set, 3), A, Bv, xt, f1);
   long long a[5] = {0, 0, 0, 0, 0};
   n = 0;
   for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
@@ -448,10 +452,11 @@ __global__ void __launch_bounds__(256) k_sgr_search(const uint8_t* __restrict__ 
   const int ux = (u % nux) * kRu, uy = (u / nux) * kRu, uw = min(kRu, w - ux), uh = min(kRu, h - uy);
   const long po = (long)b * w * h;
   __shared__ uint8_t T[kLrTile][kLrTile];
-  __shared__ int A[kAb][kAb], Bv[kAb][kAb];
+  __shared__ uint16_t A[kAb][kAb], Bv[kAb][kAb], xt[256];
   __shared__ unsigned long long red[6];
   __shared__ int xq[2];
   lr_stage(rec + po, w, h, ux, uy, uw, uh, T);
+  if (threadIdx.x < 256) xt[threadIdx.x] = (uint16_t)sgr_xbyx1(threadIdx.x);
   if (threadIdx.x < 6) red[threadIdx.x] = 0;
   __syncthreads();
   const int r0 = sgr_param(set, 0), r1 = sgr_param(set, 2);
@@ -461,8 +466,8 @@ __global__ void __launch_bounds__(256) k_sgr_search(const uint8_t* __restrict__ 
     const int i = q / uw, j = q - i * uw;
     f0[n] = f1[n] = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
   }
-  if (r0) sgr_guided(T, w, h, ux, uy, uw, uh, r0, sgr_param(set, 1), A, Bv, f0);
-  if (r1) sgr_guided(T, w, h, ux, uy, uw, uh, r1, sgr_param(set, 3), A, Bv, f1);
+  if (r0) sgr_guided(T, w, h, ux, uy, uw, uh, r0, sgr_param(set, 1), A, Bv, xt, f0);
+  if (r1) sgr_guided(T, w, h, ux, uy, uw, uh, r1, sgr_param(set, 3), A, Bv, xt, f1);
   long long a[5] = {0, 0, 0, 0, 0};
   n = 0;
   for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {

@@ -19,6 +19,7 @@
 // Grids are (blocks, segments): one launch covers the same frame of every segment.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 
 #include "gpu_common.h"
@@ -542,7 +543,11 @@ __global__ void k_av1e_merge(uint32_t* __restrict__ mode, const uint32_t* __rest
 
 // ================================================================= CDEF preset choice ====
 constexpr int kMaxFb = 4096;
-__global__ void __launch_bounds__(256) k_av1e_cdef_choose(const unsigned long long* __restrict__ sy,
+// One workgroup per segment (a sequential greedy), so the 64 presets x nfb SSE sweeps are
+// latency-bound: 16 waves (each a slice of the 64x64 blocks, lanes = presets) keep 4x more
+// loads in flight than 4 did.  Column sums and the first-minimum pick are shared helpers.
+constexpr int kCcT = 1024, kCcW = kCcT / 64;
+__global__ void __launch_bounds__(kCcT) k_av1e_cdef_choose(const unsigned long long* __restrict__ sy,
                                                           const unsigned long long* __restrict__ su,
                                                           const unsigned long long* __restrict__ sv,
                                                           const uint32_t* __restrict__ mode, int W, int H,
@@ -550,12 +555,13 @@ __global__ void __launch_bounds__(256) k_av1e_cdef_choose(const unsigned long lo
                                                           int8_t* __restrict__ py, int8_t* __restrict__ puv) {
   __shared__ unsigned long long best[kMaxFb];
   __shared__ uint8_t active[kMaxFb], asg[kMaxFb];
-  __shared__ unsigned long long part[4][64];
+  __shared__ unsigned long long part[kCcW][64];
+  __shared__ unsigned long long tot[64];
   __shared__ uint8_t ytab[8], uvtab[8];
   const int b = blockIdx.x, t = threadIdx.x;
   const int bw = W >> 4, bh = H >> 4, nb = bw * bh, sbw = (W + 63) >> 6, sbh = (H + 63) >> 6, nfb = sbw * sbh;
   const long so = (long)b * nfb * 64;
-  for (int f = t; f < nfb; f += 256) {
+  for (int f = t; f < nfb; f += kCcT) {
     const int sx = f % sbw, sy0 = f / sbw;
     int act = 0;
     for (int yy = sy0 * 4; yy < min(bh, sy0 * 4 + 4); ++yy)
@@ -567,30 +573,34 @@ __global__ void __launch_bounds__(256) k_av1e_cdef_choose(const unsigned long lo
   const int p = t & 63, pq = t >> 6;
   for (int k = 0; k < kMaxPresets; ++k) {
     unsigned long long acc = 0;
-    for (int f = pq; f < nfb; f += 4)
+    for (int f = pq; f < nfb; f += kCcW)
       if (active[f]) {
         const unsigned long long v = sy[so + f * 64 + p];
         acc += v < best[f] ? v : best[f];
       }
     part[pq][p] = acc;
     __syncthreads();
+    if (t < 64) {
+      unsigned long long s = 0;
+      for (int q = 0; q < kCcW; ++q) s += part[q][t];
+      tot[t] = s;
+    }
+    __syncthreads();
     if (t == 0) {
       int bp = 0;
       unsigned long long bt = ~0ull;
-      for (int q = 0; q < 64; ++q) {
-        const unsigned long long s = part[0][q] + part[1][q] + part[2][q] + part[3][q];
-        if (s < bt) bt = s, bp = q;
-      }
+      for (int q = 0; q < 64; ++q)
+        if (tot[q] < bt) bt = tot[q], bp = q;
       ytab[k] = (uint8_t)bp;
     }
     __syncthreads();
-    for (int f = t; f < nfb; f += 256) {
+    for (int f = t; f < nfb; f += kCcT) {
       const unsigned long long v = sy[so + f * 64 + ytab[k]];
       if (v < best[f]) best[f] = v;
     }
     __syncthreads();
   }
-  for (int f = t; f < nfb; f += 256) {
+  for (int f = t; f < nfb; f += kCcT) {
     unsigned long long bv = ~0ull;
     int a = 0;
     for (int k = 0; k < kMaxPresets; ++k) {
@@ -602,22 +612,26 @@ __global__ void __launch_bounds__(256) k_av1e_cdef_choose(const unsigned long lo
   __syncthreads();
   for (int k = 0; k < kMaxPresets; ++k) {
     unsigned long long acc = 0;
-    for (int f = pq; f < nfb; f += 4)
+    for (int f = pq; f < nfb; f += kCcW)
       if (active[f] && asg[f] == k) acc += su[so + f * 64 + p] + sv[so + f * 64 + p];
     part[pq][p] = acc;
+    __syncthreads();
+    if (t < 64) {
+      unsigned long long s = 0;
+      for (int q = 0; q < kCcW; ++q) s += part[q][t];
+      tot[t] = s;
+    }
     __syncthreads();
     if (t == 0) {
       int bp = 0;
       unsigned long long bt = ~0ull;
-      for (int q = 0; q < 64; ++q) {
-        const unsigned long long s = part[0][q] + part[1][q] + part[2][q] + part[3][q];
-        if (s < bt) bt = s, bp = q;
-      }
+      for (int q = 0; q < 64; ++q)
+        if (tot[q] < bt) bt = tot[q], bp = q;
       uvtab[k] = (uint8_t)bp;
     }
     __syncthreads();
   }
-  for (int f = t; f < nfb; f += 256) {
+  for (int f = t; f < nfb; f += kCcT) {
     int bk = -1;
     if (active[f]) {
       unsigned long long bv = ~0ull;
@@ -713,6 +727,51 @@ bool bad(int W, int H, int B, int qidx, const char* what) {
   return false;
 }
 
+// ================================================================= level packing ========
+// Device->host layout of a GOP's levels (FrameDecisions::scan_packed): every TB whose plane
+// bit is set in its mode word becomes [eob, eob levels in zigzag_scan order], TBs back to
+// back in (frame, segment, block) order; the syntax writer expands them.  Past the eob a TB
+// is all zero, so the copy moves a fraction of whole-TB bytes.  One wave per TB: length
+// pass -> inclusive scan (torch.cumsum) -> pack.  Levels / modes are [F][Bmax][nb] slots
+// of which the first `nseg` segments are used.
+__device__ __forceinline__ long tb_index(long tb, int nb, int nseg, int Bmax) {
+  const long fs = tb / nb;
+  return ((fs / nseg) * Bmax + fs % nseg) * nb + (tb - fs * nb);
+}
+__global__ void __launch_bounds__(256) k_av1e_tb_len(const int16_t* __restrict__ lev,
+                                                     const uint32_t* __restrict__ mode, long ntb, int nb, int nseg,
+                                                     int Bmax, int p, int* __restrict__ len) {
+  __shared__ int16_t sc[256];
+  const int N2 = p ? 64 : 256, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) zigzag_scan(p ? 8 : 16, sc);
+  __syncthreads();
+  for (long tb = (long)blockIdx.x * 4 + (threadIdx.x >> 6); tb < ntb; tb += (long)gridDim.x * 4) {
+    const long mi = tb_index(tb, nb, nseg, Bmax);
+    const bool nz = (mode[mi] >> (10 + p)) & 1;  // wave-uniform
+    int last = 0;                                  // scan index + 1 of the lane's last nonzero
+    if (nz)
+      for (int k = lane; k < N2; k += 64)
+        if (lev[mi * N2 + sc[k]]) last = k + 1;
+    const unsigned eob = ~wave_min_u32(~(unsigned)last);
+    if (lane == 0) len[tb] = nz ? 1 + (int)eob : 0;
+  }
+}
+__global__ void __launch_bounds__(256) k_av1e_tb_pack(const int16_t* __restrict__ lev, const int* __restrict__ len,
+                                                      const long long* __restrict__ end, long ntb, int nb, int nseg,
+                                                      int Bmax, int p, int16_t* __restrict__ out) {
+  __shared__ int16_t sc[256];
+  const int N2 = p ? 64 : 256, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) zigzag_scan(p ? 8 : 16, sc);
+  __syncthreads();
+  for (long tb = (long)blockIdx.x * 4 + (threadIdx.x >> 6); tb < ntb; tb += (long)gridDim.x * 4) {
+    const int L = len[tb];
+    if (!L) continue;
+    const long mi = tb_index(tb, nb, nseg, Bmax), o = end[tb] - L;
+    if (lane == 0) out[o] = (int16_t)(L - 1);
+    for (int k = lane; k < L - 1; k += 64) out[o + 1 + k] = lev[mi * N2 + sc[k]];
+  }
+}
+
 }  // namespace
 }  // namespace gpu
 }  // namespace tv
@@ -756,6 +815,31 @@ int tv_av1e_merge(uint32_t* mode, const uint32_t* mv, int W, int H, int B, void*
   return status("av1e_merge");
 }
 
+// eob-truncated level packing of `ntb` = F * nseg * nb TBs of plane p (0 luma, 1/2 chroma)
+int tv_av1e_tb_len(const int16_t* lev, const uint32_t* mode, long ntb, int nb, int nseg, int Bmax, int p, int* len,
+                   void* stream) {
+  if (ntb < 0 || nb <= 0 || nseg <= 0 || nseg > Bmax || p < 0 || p > 2 || ntb % ((long)nb * nseg)) {
+    g_err = "av1e_tb_len: bad geometry";
+    return -1;
+  }
+  if (!ntb) return 0;
+  const long g = std::min((ntb + 3) / 4, 1L << 18);
+  k_av1e_tb_len<<<(unsigned)g, 256, 0, (hipStream_t)stream>>>(lev, mode, ntb, nb, nseg, Bmax, p, len);
+  return status("av1e_tb_len");
+}
+// end: inclusive prefix sum of len (int64); out sized end[ntb - 1]
+int tv_av1e_tb_pack(const int16_t* lev, const int* len, const long long* end, long ntb, int nb, int nseg, int Bmax,
+                    int p, int16_t* out, void* stream) {
+  if (ntb < 0 || nb <= 0 || nseg <= 0 || nseg > Bmax || p < 0 || p > 2 || ntb % ((long)nb * nseg)) {
+    g_err = "av1e_tb_pack: bad geometry";
+    return -1;
+  }
+  if (!ntb) return 0;
+  const long g = std::min((ntb + 3) / 4, 1L << 18);
+  k_av1e_tb_pack<<<(unsigned)g, 256, 0, (hipStream_t)stream>>>(lev, len, end, ntb, nb, nseg, Bmax, p, out);
+  return status("av1e_tb_pack");
+}
+
 // lvl: [B][4] loop_filter_level[0..3] per segment
 int tv_av1e_lfinfo(const uint32_t* mode, int W, int H, int B, const int* lvl, uint32_t* iy, uint32_t* iu,
                    uint32_t* iv, void* stream) {
@@ -796,7 +880,7 @@ int tv_av1e_cdef_choose(const unsigned long long* sy, const unsigned long long* 
     g_err = "av1e_cdef_choose: frame too large";
     return -1;
   }
-  k_av1e_cdef_choose<<<B, 256, 0, (hipStream_t)stream>>>(sy, su, sv, mode, W, H, tabs, fbidx, py, puv);
+  k_av1e_cdef_choose<<<B, kCcT, 0, (hipStream_t)stream>>>(sy, su, sv, mode, W, H, tabs, fbidx, py, puv);
   return status("av1e_cdef_choose");
 }
 }

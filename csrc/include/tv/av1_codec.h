@@ -41,7 +41,7 @@ struct FrameParams {
 // Decisions of one frame.  Levels are raster order inside each transform block.  A null
 // level pointer means "all TBs of that plane are packed": blocks whose nonzero mask
 // (mode word bits 10-12) has the plane's bit set appear consecutively in raster block
-// order in ly / lu / lv.  `packed` selects that layout.
+// order in ly / lu / lv.  `packed` selects that layout (`scan_packed`: eob-truncated).
 struct FrameDecisions {
   FrameParams fp;
   const uint32_t* mode = nullptr;   // [nblk]
@@ -52,6 +52,9 @@ struct FrameDecisions {
   const int8_t* cdef_idx = nullptr; // [nsb]  (-1: every block of the SB is skip)
   const int32_t* lr = nullptr;      // [3][nu_luma][3] per plane, per 64x64 unit: (sgr set | -1, xqd0, xqd1)
   bool packed = false;
+  // with packed: each nonzero TB is [eob, eob levels in zigzag_scan order] (int16), TBs
+  // back to back (the GPU engine's eob-truncated device->host layout)
+  bool scan_packed = false;
 };
 
 // Owned variant (decoder output / golden encoder).

@@ -176,23 +176,34 @@ TV_HD int sgr_param(int set, int k) {
 }
 constexpr int kSgrMtableBits = 20, kSgrSgrBits = 8, kSgrRecipBits = 12, kSgrRstBits = 4, kSgrPrjBits = 7;
 
-// (a, b) guide coefficients of one pixel from its (2r+1)^2 box sum / square sum
-TV_HD void sgr_ab(int sum, int sq, int r, int eps, int* A, int* B) {
+// x_by_xplus1: 256 * z / (z + 1) rounded, 1 at 0, 256 from 255 on
+TV_HD int sgr_xbyx1(unsigned z) {
+  if (z >= 255) return 256;
+  if (z == 0) return 1;
+  return (int)(((z << kSgrSgrBits) + (z / 2)) / (z + 1));
+}
+// (a, b) guide coefficients of one pixel from its (2r+1)^2 box sum / square sum; `xb(z)`
+// evaluates sgr_xbyx1 (the GPU passes a lookup in an LDS table of it)
+template <class XB>
+TV_HD void sgr_ab_x(int sum, int sq, int r, int eps, XB xb, int* A, int* B) {
   const int n = (2 * r + 1) * (2 * r + 1);
   const int n2e = n * n * eps;
   const unsigned s = ((1u << kSgrMtableBits) + (unsigned)(n2e / 2)) / (unsigned)n2e;
   const long long p0 = (long long)sq * n - (long long)sum * sum;
   const unsigned p = p0 > 0 ? (unsigned)p0 : 0u;
   const unsigned z = (unsigned)(((unsigned long long)p * s + (1u << (kSgrMtableBits - 1))) >> kSgrMtableBits);
-  int a2;
-  if (z >= 255) a2 = 256;
-  else if (z == 0) a2 = 1;
-  else a2 = (int)(((z << kSgrSgrBits) + (z / 2)) / (z + 1));
+  const int a2 = xb(z);
   const int one_over_n = ((1 << kSgrRecipBits) + n / 2) / n;
-  const long long b2 = (long long)((1 << kSgrSgrBits) - a2) * sum * one_over_n;
+  // 8-bit: (256 - a2) * sum * one_over_n <= 255 * 6375 * 164 < 2^31, so B < 2^16 and both
+  // coefficients fit 16-bit storage (the GPU keeps them as uint16 in LDS)
+  const int b2 = ((1 << kSgrSgrBits) - a2) * sum * one_over_n;
   *A = a2;
-  *B = (int)((b2 + (1 << (kSgrRecipBits - 1))) >> kSgrRecipBits);
+  *B = (b2 + (1 << (kSgrRecipBits - 1))) >> kSgrRecipBits;
 }
+struct SgrXbDiv {
+  TV_HD int operator()(unsigned z) const { return sgr_xbyx1(z); }
+};
+TV_HD void sgr_ab(int sum, int sq, int r, int eps, int* A, int* B) { sgr_ab_x(sum, sq, r, eps, SgrXbDiv{}, A, B); }
 
 // projection of the two guided outputs (flt = filtered << RST_BITS domain) onto the pixel
 TV_HD int sgr_project(int x, int f0, int f1, int r0, int r1, int w0, int w1) {

@@ -97,6 +97,20 @@ TV_HD int lf_level_for_q(int q) {
 // lambda for SAD/SATD-domain decisions (bits -> distortion units, x16)
 TV_HD int lambda16(int q) { return tv_max(16, (ac_q(q) * 16 * 3) / 32); }
 
+// Coefficient scan (zigzag over anti-diagonals, odd diagonals top-down): raster position of
+// scan index k for N x N, written to out[0..N*N).  The syntax writer's scan and the order
+// of the GPU's eob-truncated level packing (k_av1e_tb_pack).
+TV_HD void zigzag_scan(int N, int16_t* out) {
+  int k = 0;
+  for (int s = 0; s <= 2 * N - 2; ++s) {
+    const int lo = s - N + 1 > 0 ? s - N + 1 : 0, hi = s < N - 1 ? s : N - 1;
+    if (s & 1)
+      for (int r = lo; r <= hi; ++r) out[k++] = (int16_t)(r * N + (s - r));
+    else
+      for (int r = hi; r >= lo; --r) out[k++] = (int16_t)(r * N + (s - r));
+  }
+}
+
 // ------------------------------------------------------------------ intra prediction ----
 // Smooth weights (Sm_Weights_Tx_*)
 TV_HD int sm_weight(int N, int i) {

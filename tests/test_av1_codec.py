@@ -87,6 +87,14 @@ def test_packed_writer_matches_golden_stream():
                        packed[1], packed[2], np.ascontiguousarray(res.cdef_idx[k]), packed=True, seq_header=(k == 0),
                        lr=res.lr[k])
         assert out == tus[k]
+    # the GPU engine's eob-truncated scan-order layout (scan_pack == k_av1e_tb_pack)
+    wr = av1.StreamWriter(w, h)
+    for k in range(3):
+        mode = np.ascontiguousarray(res.mode[k])
+        sp = [av1.scan_pack(lev, mode, p) for p, lev in enumerate((res.ly[k], res.lu[k], res.lv[k]))]
+        out = wr.write(res.fparams[k], mode, np.ascontiguousarray(res.mv[k]), sp[0], sp[1], sp[2],
+                       np.ascontiguousarray(res.cdef_idx[k]), packed=2, seq_header=(k == 0), lr=res.lr[k])
+        assert out == tus[k]
 
 
 def test_ivf_round_trip():

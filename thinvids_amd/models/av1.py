@@ -205,6 +205,29 @@ def frame_params(key: bool, qindex: int, lf, sharp: int, damping: int, cdef_y, c
     return p
 
 
+def zigzag_scan(N: int) -> np.ndarray:
+    """Raster position of each scan index (av1_enc.h zigzag_scan)."""
+    out = []
+    for s in range(2 * N - 1):
+        lo, hi = max(0, s - N + 1), min(s, N - 1)
+        rows = range(lo, hi + 1) if s & 1 else range(hi, lo - 1, -1)
+        out.extend(r * N + (s - r) for r in rows)
+    return np.asarray(out, np.int64)
+
+
+def scan_pack(lev: np.ndarray, mode: np.ndarray, plane: int) -> np.ndarray:
+    """Host model of the GPU engine's device->host level layout (k_av1e_tb_pack): each TB
+    with the plane's nonzero bit as [eob, eob levels in zigzag order], back to back."""
+    n = lev.shape[-1]
+    sc = zigzag_scan(16 if n == 256 else 8)
+    parts = []
+    for b in np.nonzero((mode >> (10 + plane)) & 1)[0]:
+        z = lev[b][sc]
+        eob = int(np.nonzero(z)[0][-1]) + 1
+        parts.append(np.concatenate([[eob], z[:eob]]).astype(np.int16))
+    return np.concatenate(parts) if parts else np.zeros(1, np.int16)
+
+
 class StreamWriter:
     """Writes one stream's temporal units in order from engine decisions; carries the
     frame-to-frame CDF state (frame-end CDF update, primary_ref_frame of inter frames)."""
@@ -220,8 +243,9 @@ class StreamWriter:
             self.st = None
 
     def write(self, fparams: np.ndarray, mode: np.ndarray, mv: np.ndarray, ly: np.ndarray, lu: np.ndarray,
-              lv: np.ndarray, cdef_idx: np.ndarray, packed: bool, seq_header: bool, lr: np.ndarray | None = None,
+              lv: np.ndarray, cdef_idx: np.ndarray, packed: int, seq_header: bool, lr: np.ndarray | None = None,
               out: Bytes | None = None) -> bytes | None:
+        """packed: 0 = full [nblk][N*N] levels, 1 = nonzero TBs back to back, 2 = scan_pack."""
         o = out if out is not None else Bytes()
         _check(self.lib.tv_av1c_write_tu(self.st, self.w, self.h, fparams.ctypes.data_as(i32p),
                                          mode.ctypes.data_as(u32p), mv.ctypes.data_as(u32p),

@@ -46,7 +46,7 @@ def _gpu():
     lib = gpu_lib()
     if not getattr(lib, "_av1e_sigs", False):
         for n in ("tv_av1e_inter", "tv_av1e_intra", "tv_av1e_lfinfo", "tv_av1e_cdef_choose", "tv_av1e_lr_solve",
-                  "tv_av1e_unit_sse", "tv_av1e_merge"):
+                  "tv_av1e_unit_sse", "tv_av1e_merge", "tv_av1e_tb_len", "tv_av1e_tb_pack"):
             getattr(lib, n).restype = C.c_int
         lib.tv_av1e_last_error.restype = C.c_char_p
         lib._av1e_sigs = True
@@ -84,7 +84,7 @@ class GopHost:
     mv: np.ndarray
     tabs: np.ndarray     # (F, B, 16) uint8
     fbidx: np.ndarray    # (F, B, nfb) int8
-    packed: list         # per plane: (levels (K, n) int16, offsets (F, B) int64)
+    packed: list         # per plane: (eob-truncated scan-order TBs int16, start offsets (F, B) int64)
     sse: np.ndarray      # (F, B, 3) int64
     key: list            # per frame
     qm: np.ndarray = None  # (F, B) q-index per frame and segment
@@ -294,34 +294,44 @@ class Av1GpuEngine:
         return fut
 
     def _collect(self, S: dict, ev, F: int, nseg: int, qm) -> GopHost:
-        """Compact the nonzero TBs of a GOP slot on the copy stream (after `ev`) and copy
-        every decision array to the host."""
+        """Pack the nonzero TBs of a GOP slot eob-truncated in scan order on the copy stream
+        (after `ev`: k_av1e_tb_len -> cumsum -> k_av1e_tb_pack) and copy every decision
+        array to the host."""
         torch = self.torch
         torch.cuda.set_device(self.dev)
         cs = self._copy_stream
+        lib = _gpu()
+        Bmax, nb = S["mode"].shape[1], S["mode"].shape[2]
+        ntb = F * nseg * nb
         with torch.cuda.stream(cs):
             cs.wait_event(ev)
-            mode = S["mode"][:F, :nseg]
-            packed = []
-            for p, lev in enumerate((S["ly"][:F, :nseg], S["lu"][:F, :nseg], S["lv"][:F, :nseg])):
-                nz = ((mode >> (10 + p)) & 1).bool()
-                packed.append((lev[nz], nz.sum(dim=2)))
+            st = _vp(cs.cuda_stream)
+            lens, ends = [], []
+            for p, k in enumerate(("ly", "lu", "lv")):
+                ln = torch.empty(ntb, dtype=torch.int32, device=self.dev)
+                _ok(lib.tv_av1e_tb_len(_p(S[k]), _p(S["mode"]), C.c_long(ntb), nb, nseg, Bmax, p, _p(ln), st))
+                lens.append(ln)
+                ends.append(torch.cumsum(ln, 0, dtype=torch.int64))
+            totals = torch.stack([e[-1] for e in ends]).cpu().tolist()
+            outs = []
+            for p, k in enumerate(("ly", "lu", "lv")):
+                o = torch.empty(max(1, totals[p]), dtype=torch.int16, device=self.dev)
+                _ok(lib.tv_av1e_tb_pack(_p(S[k]), _p(lens[p]), _p(ends[p]), C.c_long(ntb), nb, nseg, Bmax, p, _p(o),
+                                        st))
+                outs.append((o, (ends[p] - lens[p]).view(F, nseg, nb)[:, :, 0]))
             host = GopHost(
                 nframes=F,
-                mode=mode.cpu().numpy().view(np.uint32),
+                mode=S["mode"][:F, :nseg].cpu().numpy().view(np.uint32),
                 mv=S["mv"][:F, :nseg].cpu().numpy().view(np.uint32),
                 tabs=S["tabs"][:F, :nseg].cpu().numpy(),
                 fbidx=S["fbidx"][:F, :nseg].cpu().numpy(),
-                packed=[],
+                packed=[(o[:max(1, t)].cpu().numpy(), off.cpu().numpy().astype(np.int64))
+                        for (o, off), t in zip(outs, totals)],
                 sse=S["sse"][:F, :nseg].cpu().numpy(),
                 key=[t == 0 for t in range(F)],
                 qm=qm,
                 lr=S["lr"][:F, :nseg].cpu().numpy(),
             )
-            for lev, counts in packed:
-                c = counts.cpu().numpy().astype(np.int64).reshape(-1)
-                off = np.concatenate([[0], np.cumsum(c)])[:-1].reshape(F, nseg)
-                host.packed.append((lev.cpu().numpy(), off))
         return host
 
     # ------------------------------------------------------------------ entropy ------
@@ -334,10 +344,9 @@ class Av1GpuEngine:
             tabs = g.tabs[t, b]
             q = int(g.qm[t, b])
             fp = av1m.frame_params(g.key[t], q, [lf_level(q)] * 4, 0, self.damping, tabs[:8], tabs[8:])
-            lev = [np.ascontiguousarray(pk[0][pk[1][t, b]:]) if len(pk[0]) else np.zeros((1, n), np.int16)
-                   for pk, n in zip(g.packed, (256, 64, 64))]
+            lev = [pk[0][pk[1][t, b]:] for pk in g.packed]  # eob-truncated scan-order TBs
             tus.append(wr.write(fp, np.ascontiguousarray(g.mode[t, b]), np.ascontiguousarray(g.mv[t, b]), lev[0],
-                                lev[1], lev[2], np.ascontiguousarray(g.fbidx[t, b]), packed=True, seq_header=g.key[t],
+                                lev[1], lev[2], np.ascontiguousarray(g.fbidx[t, b]), packed=2, seq_header=g.key[t],
                                 lr=np.ascontiguousarray(g.lr[t, b])))
         return tus
 
