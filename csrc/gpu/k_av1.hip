@@ -514,6 +514,114 @@ __global__ void __launch_bounds__(256) k_sgr_search(const uint8_t* __restrict__ 
   if (threadIdx.x == 0) sse[(long)b * nu + u] = (long long)red[5];
 }
 
+// Encoder restoration choice per unit, fused over the candidate sets: the unit's SSE left
+// unrestored, then for each set of lr_set() the guided filters -> projection statistics ->
+// sgr_solve -> projection + SSE with the outputs kept in registers; the first minimum of
+// SSE + rate (rate[b] = lr_rate_cost of segment b's q-index, 0 when unrestored) is written
+// with its parameters (set | -1, xqd0, xqd1).  The golden encoder's decision (av1_codec.cpp)
+// in one launch: one tile staging and one source read per unit instead of one per set plus
+// the unit-SSE and per-set select passes.
+__global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ src, const uint8_t* __restrict__ rec,
+                                                    int w, int h, const long long* __restrict__ rate,
+                                                    int* __restrict__ prm, uint8_t* __restrict__ out) {
+  const int b = blockIdx.y, u = blockIdx.x, nux = (w + kRu - 1) / kRu, nu = nux * ((h + kRu - 1) / kRu);
+  const int ux = (u % nux) * kRu, uy = (u / nux) * kRu, uw = min(kRu, w - ux), uh = min(kRu, h - uy);
+  const long po = (long)b * w * h;
+  __shared__ uint8_t T[kLrTile][kLrTile];
+  __shared__ uint16_t A[kAb][kAb], Bv[kAb][kAb], xt[256];
+  __shared__ unsigned long long red[1 + 6 * kNumLrSets];
+  __shared__ int xq[2];
+  lr_stage(rec + po, w, h, ux, uy, uw, uh, T);
+  if (threadIdx.x < 256) xt[threadIdx.x] = (uint16_t)sgr_xbyx1(threadIdx.x);
+  if (threadIdx.x < 1 + 6 * kNumLrSets) red[threadIdx.x] = 0;
+  __syncthreads();
+  auto block_add = [&](long long v, int slot) {
+    v = wave_sum64(v);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&red[slot], (unsigned long long)v);
+  };
+  int sv[16], ob[16];
+  long long e0 = 0;
+  int n = 0;
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+    const int i = q / uw, j = q - i * uw;
+    sv[n] = src[po + (long)(uy + i) * w + ux + j];
+    ob[n] = T[i + kLrHalo][j + kLrHalo];
+    const int d = ob[n] - sv[n];
+    e0 += d * d;
+  }
+  block_add(e0, 0);
+  __syncthreads();
+  long long best = (long long)red[0];
+  int bset = -1, b0 = 0, b1 = 0;
+  const long long rt = rate[b];
+  for (int k = 0; k < kNumLrSets; ++k) {
+    const int set = lr_set(k), r0 = sgr_param(set, 0), r1 = sgr_param(set, 2), sl = 1 + 6 * k;
+    int f0[16], f1[16];
+    n = 0;
+    for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+      const int i = q / uw, j = q - i * uw;
+      f0[n] = f1[n] = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
+    }
+    if (r0) sgr_guided(T, w, h, ux, uy, uw, uh, r0, sgr_param(set, 1), A, Bv, xt, f0);
+    if (r1) sgr_guided(T, w, h, ux, uy, uw, uh, r1, sgr_param(set, 3), A, Bv, xt, f1);
+    long long a[5] = {0, 0, 0, 0, 0};
+    n = 0;
+    for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+      const int i = q / uw, j = q - i * uw;
+      const int uu = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
+      const long long da = f0[n] - uu, db = f1[n] - uu;
+      const long long e = ((long long)(sv[n] << kSgrRstBits) - uu) << kSgrPrjBits;
+      a[0] += da * da;
+      a[1] += da * db;
+      a[2] += db * db;
+      a[3] += da * e;
+      a[4] += db * e;
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) block_add(a[c], sl + c);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long st[5];
+      for (int c = 0; c < 5; ++c) st[c] = (long long)red[sl + c];
+      sgr_solve(st, r0, r1, &xq[0], &xq[1]);
+    }
+    __syncthreads();
+    const int w0 = xq[0], w1 = xq[1];
+    long long e2 = 0;
+    n = 0;
+    for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+      const int i = q / uw, j = q - i * uw;
+      const int o = sgr_project((int)T[i + kLrHalo][j + kLrHalo], f0[n], f1[n], r0, r1, w0, w1);
+      f0[n] = o;
+      const int d = o - sv[n];
+      e2 += d * d;
+    }
+    block_add(e2, sl + 5);
+    __syncthreads();
+    const long long ek = (long long)red[sl + 5] + rt;
+    if (ek < best) {  // block-uniform
+      best = ek;
+      bset = set;
+      b0 = w0;
+      b1 = w1;
+      n = 0;
+      for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) ob[n] = f0[n];
+    }
+    __syncthreads();  // xq / A / Bv reused by the next set
+  }
+  n = 0;
+  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+    const int i = q / uw, j = q - i * uw;
+    out[po + (long)(uy + i) * w + ux + j] = (uint8_t)ob[n];
+  }
+  if (threadIdx.x == 0) {
+    int* P = prm + ((long)b * nu + u) * 3;
+    P[0] = bset;
+    P[1] = bset < 0 ? 0 : b0;
+    P[2] = bset < 0 ? 0 : b1;
+  }
+}
+
 // ----------------------------------------------------------------- deblocking filter ----
 // k_deblock: one workgroup per 64x64 output tile.  The tile plus an 8-pixel ring is staged
 // in LDS once (dword loads); the vertical edges x0..x0+64 are filtered on all 80 rows (the
@@ -619,6 +727,14 @@ int tv_gpu_sgr_search(const uint8_t* src, const uint8_t* rec, int w, int h, int 
   if (bad_geo(w, h, B, 2, "sgr_search") || set < 0 || set > 15) return -1;
   k_sgr_search<<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, set, prm, sse, out);
   return av1_status("sgr_search");
+}
+// encoder restoration choice over every lr_set() candidate: rate [B] (int64), prm
+// [B][nu][3], restored planes (unrestored units copied)
+int tv_gpu_sgr_select(const uint8_t* src, const uint8_t* rec, int w, int h, int B, const long long* rate, int* prm,
+                      uint8_t* out, void* stream) {
+  if (bad_geo(w, h, B, 2, "sgr_select")) return -1;
+  k_sgr_select<<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, rate, prm, out);
+  return av1_status("sgr_select");
 }
 int tv_gpu_wiener_apply(const uint8_t* rec, int w, int h, int B, const int* coef, uint8_t* out, void* stream) {
   if (bad_geo(w, h, B, 2, "wiener_apply")) return -1;

@@ -220,38 +220,25 @@ class Av1GpuEngine:
         return out
 
     def _restore(self, t: int, B: int, rate):
-        """Self-guided restoration search + apply on the CDEF output (the golden encoder's
-        per-unit off / set-4 / set-10 choice, SSE + rate, first minimum)."""
+        """Self-guided restoration search + apply on the CDEF output: the golden encoder's
+        per-unit off / set-4 / set-10 choice (SSE + rate, first minimum), one fused
+        k_sgr_select launch per plane."""
         from ..ops import av1 as ops
 
         torch = self.torch
-        lib = _gpu()
         st = _vp(torch.cuda.current_stream(self.dev).cuda_stream)
+        rate = rate.to(torch.int64).contiguous()
         out = []
         for p, (S, X) in enumerate(zip((x[:B] for x in self.src), self.fin)):
             h, w = X.shape[1], X.shape[2]
             nu = (-(-h // 64)) * (-(-w // 64))
-            best = self._unit_sse(S, X)
-            prm_best = torch.zeros((B, nu, 3), dtype=torch.int32, device=self.dev)
-            prm_best[..., 0] = -1
-            res = X
-            for s in LR_SETS:  # fused stats -> solve -> project + SSE per unit (k_sgr_search)
-                prm = torch.empty((B, nu, 3), dtype=torch.int32, device=self.dev)
-                e = torch.empty((B, nu), dtype=torch.int64, device=self.dev)
-                o = torch.empty_like(X)
-                rc = ops._gpu().tv_gpu_sgr_search(_p(S), _p(X), w, h, B, s, _p(prm), _p(e), _p(o), st)
-                if rc != 0:
-                    raise RuntimeError(ops._gpu().tv_av1_gpu_last_error().decode())
-                e = e + rate[:, None]
-                better = e < best
-                best = torch.where(better, e, best)
-                prm_best = torch.where(better[..., None], prm, prm_best)
-                # the per-unit choice so far (units are disjoint: select, no re-filtering)
-                ux = -(-w // 64)
-                m = better.view(B, -1, ux).repeat_interleave(64, 1).repeat_interleave(64, 2)[:, :h, :w]
-                res = torch.where(m, o, res)
-            self.g_lr[t, :B, p, :nu] = prm_best
-            out.append(res)
+            prm = torch.empty((B, nu, 3), dtype=torch.int32, device=self.dev)
+            o = torch.empty_like(X)
+            rc = ops._gpu().tv_gpu_sgr_select(_p(S), _p(X), w, h, B, _p(rate), _p(prm), _p(o), st)
+            if rc != 0:
+                raise RuntimeError(ops._gpu().tv_av1_gpu_last_error().decode())
+            self.g_lr[t, :B, p, :nu] = prm
+            out.append(o)
         return tuple(out)
 
     def encode_gop(self, nframes: int, load_frame, nseg: int | None = None, qmap=None, async_host: bool = False):

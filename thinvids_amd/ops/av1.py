@@ -68,7 +68,7 @@ def _gpu():
     if not getattr(lib, "_av1_sigs", False):
         for name in ("tv_gpu_cdef_dirs", "tv_gpu_cdef_search", "tv_gpu_cdef_apply", "tv_gpu_wiener_apply",
                      "tv_gpu_wiener_stats", "tv_gpu_sgr_stats", "tv_gpu_sgr_apply", "tv_gpu_av1_deblock",
-                     "tv_gpu_sgr_search"):
+                     "tv_gpu_sgr_search", "tv_gpu_sgr_select"):
             getattr(lib, name).restype = C.c_int
         lib.tv_av1_gpu_last_error.restype = C.c_char_p
         lib._av1_sigs = True
