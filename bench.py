@@ -345,13 +345,14 @@ def av1_main(args) -> None:
 
     pass1_bits = []
 
-    def two_pass(load):
-        """Config #4's 2-pass: pass 1 at the base q-index -> per-frame bits of every rank's
-        segments all-reduced (RCCL) -> one global per-frame plan for the target bitrate
-        (ratecontrol.plan_frame_qps) -> pass 2 with the plan's per-frame q-index maps."""
+    def plan_pass2(g1fut):
+        """Config #4's 2-pass, post thread (the only thread issuing collectives): pass-1
+        per-frame bits of every rank's segments all-reduced over RCCL -> one global
+        per-frame plan for the target bitrate (ratecontrol.plan_frame_qps) -> this rank's
+        per-frame q-index maps for pass 2."""
         from thinvids_amd.models.ratecontrol import frame_sizes, plan_frame_qps, round_qps
 
-        g1 = eng.encode_gop(args.gop, load)
+        g1 = g1fut.result()
         seg1 = [b"".join(f.result()) for f in eng.submit_entropy(g1)]
         flat = torch.zeros(world * batch * args.gop, dtype=torch.float64, device=dev)
         mine = np.concatenate([8.0 * np.asarray(frame_sizes(x), np.float64) for x in seg1])
@@ -360,18 +361,9 @@ def av1_main(args) -> None:
         allb = flat.cpu().numpy().reshape(world * batch, args.gop)
         target = args.kbps * 1000.0 * (world * batch * args.gop) / 30.0
         plan, _ = plan_frame_qps(list(allb), args.qp, target, key_offset=AV1_KEY_QP_OFFSET)
-        qm = np.array([[av1m.qindex_for_hevc_qp(int(v)) for v in round_qps(plan[rank * batch + b])]
-                       for b in range(batch)], np.int32).T
-        g2 = eng.encode_gop(args.gop, load, qmap=qm)
         pass1_bits.append(float(mine.sum()))
-        return g2, [b"".join(f.result()) for f in eng.submit_entropy(g2)]
-
-    def comm2(g, segs):
-        sse = g.sse.sum(axis=(0, 1)).astype(np.float64)
-        stats = torch.tensor([batch * args.gop, sum(len(x) for x in segs), *sse], dtype=torch.float64, device=dev)
-        dist.all_reduce(stats)
-        gathered = gather_bytes_to_root(b"".join(segs), dev)
-        return stats.cpu().numpy(), (sum(len(x) for x in gathered) if gathered else 0)
+        return np.array([[av1m.qindex_for_hevc_qp(int(v)) for v in round_qps(plan[rank * batch + b])]
+                         for b in range(batch)], np.int32).T
 
     def step(s: int):
         base = (s * world + rank) * batch
@@ -385,9 +377,12 @@ def av1_main(args) -> None:
                 stage._ok(lib.tv_pad_batch(C.c_void_p(src.ptr(c)), pw, ph, stride, fs, C.c_void_p(dst.data_ptr()),
                                            cw, chh, cw, cw * chh, batch, st))
 
-        if args.kbps > 0:  # both passes and their collectives on this thread, in step order
-            res2 = comm2(*two_pass(load))
-            post.submit(lambda r=res2: r)
+        if args.kbps > 0:
+            # pass 1 on the GPU while the post thread entropy-codes the previous step's pass 2;
+            # the plan (pass-1 entropy + all-reduce) runs on the post thread in step order
+            g1 = eng.encode_gop(args.gop, load, async_host=True)
+            qm = post.ex.submit(plan_pass2, g1).result()
+            post.submit(comm, eng.encode_gop(args.gop, load, qmap=qm, async_host=True))
         else:
             post.submit(comm, eng.encode_gop(args.gop, load, async_host=True))
 
