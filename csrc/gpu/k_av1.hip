@@ -632,7 +632,8 @@ __global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ 
 constexpr int kLfT = 64, kLfR = 8, kLfP = kLfT + 2 * kLfR;  // tile, ring, LDS pitch (80)
 
 __global__ void __launch_bounds__(256) k_deblock(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int w,
-                                                 int h, int chroma, const uint32_t* __restrict__ info, int sharp) {
+                                                 int h, int chroma, const uint32_t* __restrict__ info, int sharp,
+                                                 int estep) {
   __shared__ __attribute__((aligned(16))) uint8_t T[kLfP * kLfP];
   const int x0 = blockIdx.x * kLfT, y0 = blockIdx.y * kLfT, b = blockIdx.z, w4 = w >> 2;
   const uint8_t* P = in + (long)b * w * h;
@@ -644,24 +645,27 @@ __global__ void __launch_bounds__(256) k_deblock(const uint8_t* __restrict__ in,
     *(uint32_t*)(T + r * kLfP + c4 * 4) = v;
   }
   __syncthreads();
-  // pass 0: 17 vertical edges (x0 .. x0+64) x 80 rows; item = edge * 80 + row
-  for (int i = threadIdx.x; i < (kLfT / 4 + 1) * kLfP; i += blockDim.x) {
-    const int e = i / kLfP, r = i - e * kLfP, y = y0 - kLfR + r, x = x0 + e * 4;
+  // pass 0: vertical edges x0, x0 + estep, .., x0 + 64 (17 at estep 4) x 80 rows; item =
+  // edge * 80 + row.  estep > 4 when every transform / block edge of the plane lies on that
+  // grid (the AV1 encoder: 16 luma, 8 chroma): the skipped positions hold no edge.
+  const int ne = kLfT / estep + 1;
+  for (int i = threadIdx.x; i < ne * kLfP; i += blockDim.x) {
+    const int e = i / kLfP, r = i - e * kLfP, y = y0 - kLfR + r, x = x0 + e * estep;
     if (y < 0 || y >= h || x >= w) continue;
     const uint32_t* row = I + (long)(y >> 2) * w4;
     int lvl = 0;
     const int size = lf_edge(x > 0 ? row[(x >> 2) - 1] : 0u, row[x >> 2], x, w, 0, chroma, &lvl);
-    if (size) lf_filter(T + r * kLfP + kLfR + e * 4, 1, size, lvl, sharp);
+    if (size) lf_filter(T + r * kLfP + kLfR + e * estep, 1, size, lvl, sharp);
   }
   __syncthreads();
-  // pass 1: 17 horizontal edges (y0 .. y0+64) x 64 columns; item = edge * 64 + column
-  for (int i = threadIdx.x; i < (kLfT / 4 + 1) * kLfT; i += blockDim.x) {
-    const int e = i / kLfT, c = i - e * kLfT, y = y0 + e * 4, x = x0 + c;
+  // pass 1: horizontal edges y0 .. y0+64 (step estep) x 64 columns; item = edge * 64 + column
+  for (int i = threadIdx.x; i < ne * kLfT; i += blockDim.x) {
+    const int e = i / kLfT, c = i - e * kLfT, y = y0 + e * estep, x = x0 + c;
     if (y >= h || x >= w) continue;
     int lvl = 0;
     const int size = lf_edge(y > 0 ? I[(long)((y >> 2) - 1) * w4 + (x >> 2)] : 0u, I[(long)(y >> 2) * w4 + (x >> 2)],
                              y, h, 1, chroma, &lvl);
-    if (size) lf_filter(T + (kLfR + e * 4) * kLfP + kLfR + c, kLfP, size, lvl, sharp);
+    if (size) lf_filter(T + (kLfR + e * estep) * kLfP + kLfR + c, kLfP, size, lvl, sharp);
   }
   __syncthreads();
   uint8_t* O = out + (long)b * w * h;
@@ -754,12 +758,20 @@ int tv_gpu_sgr_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int B
   return av1_status("sgr_stats");
 }
 // B planes (w, h multiples of 4), info [B][h/4][w/4] (av1_defs.h layout), sharp 0..7
+// estep: edge grid in samples (4 = every 4x4 boundary; 8 / 16 only when all transform and
+// block edges of the plane lie on that grid)
+int tv_gpu_av1_deblock_step(const uint8_t* in, uint8_t* out, int w, int h, int B, int chroma, const uint32_t* info,
+                            int sharp, int estep, void* stream) {
+  if (bad_geo(w, h, B, 4, "av1_deblock") || sharp < 0 || sharp > 7 || (estep != 4 && estep != 8 && estep != 16))
+    return -1;
+  k_deblock<<<dim3((w + kLfT - 1) / kLfT, (h + kLfT - 1) / kLfT, B), 256, 0, (hipStream_t)stream>>>(in, out, w, h,
+                                                                                                  chroma, info, sharp,
+                                                                                                  estep);
+  return av1_status("av1_deblock");
+}
 int tv_gpu_av1_deblock(const uint8_t* in, uint8_t* out, int w, int h, int B, int chroma, const uint32_t* info,
                        int sharp, void* stream) {
-  if (bad_geo(w, h, B, 4, "av1_deblock") || sharp < 0 || sharp > 7) return -1;
-  k_deblock<<<dim3((w + kLfT - 1) / kLfT, (h + kLfT - 1) / kLfT, B), 256, 0, (hipStream_t)stream>>>(in, out, w, h,
-                                                                                                  chroma, info, sharp);
-  return av1_status("av1_deblock");
+  return tv_gpu_av1_deblock_step(in, out, w, h, B, chroma, info, sharp, 4, stream);
 }
 int tv_gpu_sgr_apply(const uint8_t* rec, int w, int h, int B, const int* params, uint8_t* out, void* stream) {
   if (bad_geo(w, h, B, 2, "sgr_apply")) return -1;

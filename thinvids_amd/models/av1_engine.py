@@ -184,9 +184,11 @@ class Av1GpuEngine:
         iu = torch.empty((B, H // 8, W // 8), dtype=torch.int32, device=self.dev)
         iv = torch.empty_like(iu)
         _ok(lib.tv_av1e_lfinfo(_p(mode), W, H, B, _p(lvl), _p(iy), _p(iu), _p(iv), st))
-        dy = ops.deblock(ry, iy, False, 0)
-        du = ops.deblock(ru, iu, True, 0)
-        dv = ops.deblock(rv, iv, True, 0)
+        # every transform / block edge of the encoder's planes is on the 16 (luma) / 8
+        # (chroma) grid: blocks are 16x16 or merged 32 / 64 with one TX per plane
+        dy = ops.deblock(ry, iy, False, 0, estep=16)
+        du = ops.deblock(ru, iu, True, 0, estep=8)
+        dv = ops.deblock(rv, iv, True, 0, estep=8)
         dirs, var = ops.cdef_dirs(dy)
         se_y = ops.cdef_search(sy, dy, dirs, var, False, self.damping, pmask=CDEF_MASK_Y, checker=True)
         se_u = ops.cdef_search(su, du, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV, checker=True)

@@ -68,7 +68,7 @@ def _gpu():
     if not getattr(lib, "_av1_sigs", False):
         for name in ("tv_gpu_cdef_dirs", "tv_gpu_cdef_search", "tv_gpu_cdef_apply", "tv_gpu_wiener_apply",
                      "tv_gpu_wiener_stats", "tv_gpu_sgr_stats", "tv_gpu_sgr_apply", "tv_gpu_av1_deblock",
-                     "tv_gpu_sgr_search", "tv_gpu_sgr_select"):
+                     "tv_gpu_sgr_search", "tv_gpu_sgr_select", "tv_gpu_av1_deblock_step"):
             getattr(lib, name).restype = C.c_int
         lib.tv_av1_gpu_last_error.restype = C.c_char_p
         lib._av1_sigs = True
@@ -436,10 +436,11 @@ def random_lf_info(w: int, h: int, rng: np.random.Generator, chroma: bool = Fals
     return lf_info(f["txw"], f["txh"], f["bw"], f["bh"], f["lv"], f["lh"], f["sk"])
 
 
-def deblock(rec, info, chroma: bool = False, sharpness: int = 0):
+def deblock(rec, info, chroma: bool = False, sharpness: int = 0, estep: int = 4):
     """AV1 deblocking loop filter (7.14) of a plane: numpy (h, w) + info (h/4, w/4) -> the
     C++ golden model; torch (B, h, w) cuda + info (B, h/4, w/4) -> one fused HIP launch
-    (k_deblock, both passes per 64x64 LDS tile)."""
+    (k_deblock, both passes per 64x64 LDS tile).  estep (GPU): edge grid in samples, 8 / 16
+    only when every transform and block edge lies on it (the AV1 encoder's planes)."""
     if _is_np(rec):
         h, w = rec.shape
         out = np.empty_like(rec)
@@ -455,8 +456,8 @@ def deblock(rec, info, chroma: bool = False, sharpness: int = 0):
         info = torch.from_numpy(np.ascontiguousarray(info, np.uint32).view(np.int32))
     inf = info.to(device=rec.device, dtype=torch.int32).reshape(B, h // 4, w // 4).contiguous()
     out = torch.empty_like(rec)
-    _check(_gpu().tv_gpu_av1_deblock(_t(rec.contiguous()), _t(out), w, h, B, int(chroma), _t(inf), sharpness,
-                                     _stream(rec)))
+    _check(_gpu().tv_gpu_av1_deblock_step(_t(rec.contiguous()), _t(out), w, h, B, int(chroma), _t(inf), sharpness,
+                                          estep, _stream(rec)))
     return out
 
 
