@@ -1,5 +1,5 @@
-"""Bits / PSNR of the golden AV1 encoder with and without the MV refinement pass
-(TV_AV1_NOREFINE=1 disables it) on the synthetic source."""
+"""Bits / PSNR of the golden AV1 encoder on the synthetic source (used to evaluate the
+rejected MV-refinement pass, profiles/README.md).  Usage: w h frames qindex."""
 import os, sys, numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from thinvids_amd.models import av1, hevc
