@@ -291,16 +291,6 @@ void cdf_init_uniform(uint16_t* icdf, int n) {
   icdf[n] = 0;
 }
 
-void cdf_adapt(uint16_t* icdf, int n, int sym) {
-  const int cnt = icdf[n];
-  const int rate = 3 + (cnt > 15) + (cnt > 31) + std::min(floor_log2((unsigned)n), 2);
-  for (int i = 0; i < n - 1; ++i) {
-    if (i < sym) icdf[i] = (uint16_t)(icdf[i] + ((32768 - icdf[i]) >> rate));
-    else icdf[i] = (uint16_t)(icdf[i] - (icdf[i] >> rate));
-  }
-  icdf[n] = (uint16_t)(cnt + (cnt < 32));
-}
-
 namespace {
 constexpr int kProbShift = 6, kMinProb = 4;
 inline int ilog(uint32_t v) { return 32 - __builtin_clz(v); }
@@ -308,53 +298,6 @@ inline uint32_t bound(uint32_t r, int icdf_v, int n, int k) {
   return ((r >> 8) * (uint32_t)(icdf_v >> kProbShift) >> (7 - kProbShift)) + kMinProb * (n - 1 - k);
 }
 }  // namespace
-
-void RangeEncoder::emit(uint32_t, uint32_t r) {
-  // low_ already holds the new low; normalise the range back to [2^15, 2^16)
-  const int d = 16 - ilog(r);
-  int c = cnt_, s = c + d;
-  uint64_t l = low_;
-  if (s >= 0) {
-    c += 16;
-    uint64_t m = (1ull << c) - 1;
-    if (s >= 8) {
-      pre_.push_back((uint16_t)(l >> c));
-      l &= m;
-      c -= 8;
-      m >>= 8;
-    }
-    pre_.push_back((uint16_t)(l >> c));
-    s = c + d - 24;
-    l &= m;
-  }
-  low_ = l << d;
-  rng_ = r << d;
-  cnt_ = s;
-}
-
-void RangeEncoder::encode(int sym, uint16_t* icdf, int n, bool adapt) {
-  if (sym < 0 || sym >= n) throw std::runtime_error("range coder: symbol out of range");
-  const uint32_t r = rng_;
-  uint32_t nr;
-  if (sym > 0) {
-    const uint32_t u = bound(r, icdf[sym - 1], n, sym - 1), v = bound(r, icdf[sym], n, sym);
-    low_ += r - u;
-    nr = u - v;
-  } else {
-    nr = r - bound(r, icdf[0], n, 0);
-  }
-  emit(0, nr);
-  if (adapt) cdf_adapt(icdf, n, sym);
-}
-
-void RangeEncoder::encode_bool(int bit, int p0_q15) {
-  uint16_t icdf[3] = {(uint16_t)(32768 - clip3(1, 32767, p0_q15)), 0, 0};
-  encode(bit ? 1 : 0, icdf, 2, false);
-}
-
-void RangeEncoder::encode_literal(uint32_t v, int bits) {
-  for (int b = bits - 1; b >= 0; --b) encode_bool((v >> b) & 1, 16384);
-}
 
 size_t RangeEncoder::bits_written() const { return pre_.size() * 8 + (size_t)(cnt_ + 10); }
 

@@ -5,6 +5,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <stdexcept>
 #include <vector>
 
 namespace tv {
@@ -51,18 +52,74 @@ void deblock(const uint8_t* in, int w, int h, bool chroma, const uint32_t* info,
 // Probabilities are AV1 inverse CDFs: icdf[i] = 32768 * P(X > i), icdf[n-1] = 0, plus one
 // adaptation counter at icdf[n] (n <= 16).
 void cdf_init_uniform(uint16_t* icdf, int n);
-void cdf_adapt(uint16_t* icdf, int n, int sym);
+// CDF adaptation after coding `sym` (inline: the syntax writer / reader call it per symbol)
+inline void cdf_adapt(uint16_t* icdf, int n, int sym) {
+  const int cnt = icdf[n];
+  const int lg = 31 - __builtin_clz((unsigned)n);
+  const int rate = 3 + (cnt > 15) + (cnt > 31) + (lg < 2 ? lg : 2);
+  for (int i = 0; i < n - 1; ++i) {
+    if (i < sym) icdf[i] = (uint16_t)(icdf[i] + ((32768 - icdf[i]) >> rate));
+    else icdf[i] = (uint16_t)(icdf[i] - (icdf[i] >> rate));
+  }
+  icdf[n] = (uint16_t)(cnt + (cnt < 32));
+}
 
+// Multi-symbol range encoder (the per-symbol paths are inline: the OBU writer codes ~10^5
+// symbols per frame)
 class RangeEncoder {
  public:
-  void encode(int sym, uint16_t* icdf, int n, bool adapt = true);
-  void encode_bool(int bit, int p0_q15);  // p0 = P(bit == 0) in 1/32768
-  void encode_literal(uint32_t v, int bits);
+  void encode(int sym, uint16_t* icdf, int n, bool adapt = true) {
+    if (sym < 0 || sym >= n) throw std::runtime_error("range coder: symbol out of range");
+    const uint32_t r = rng_;
+    uint32_t nr;
+    if (sym > 0) {
+      const uint32_t u = bound(r, icdf[sym - 1], n, sym - 1), v = bound(r, icdf[sym], n, sym);
+      low_ += r - u;
+      nr = u - v;
+    } else {
+      nr = r - bound(r, icdf[0], n, 0);
+    }
+    emit(nr);
+    if (adapt) cdf_adapt(icdf, n, sym);
+  }
+  void encode_bool(int bit, int p0_q15) {  // p0 = P(bit == 0) in 1/32768
+    const int p = p0_q15 < 1 ? 1 : (p0_q15 > 32767 ? 32767 : p0_q15);
+    uint16_t icdf[3] = {(uint16_t)(32768 - p), 0, 0};
+    encode(bit ? 1 : 0, icdf, 2, false);
+  }
+  void encode_literal(uint32_t v, int bits) {
+    for (int b = bits - 1; b >= 0; --b) encode_bool((v >> b) & 1, 16384);
+  }
   std::vector<uint8_t> finish();
   size_t bits_written() const;
 
  private:
-  void emit(uint32_t low_new, uint32_t rng_new);
+  static constexpr int kProbShift = 6, kMinProb = 4;
+  static uint32_t bound(uint32_t r, int icdf_v, int n, int k) {
+    return ((r >> 8) * (uint32_t)(icdf_v >> kProbShift) >> (7 - kProbShift)) + kMinProb * (n - 1 - k);
+  }
+  // low_ already holds the new low; normalise the range back to [2^15, 2^16)
+  void emit(uint32_t r) {
+    const int d = 16 - (32 - __builtin_clz(r));
+    int c = cnt_, s = c + d;
+    uint64_t l = low_;
+    if (s >= 0) {
+      c += 16;
+      uint64_t m = (1ull << c) - 1;
+      if (s >= 8) {
+        pre_.push_back((uint16_t)(l >> c));
+        l &= m;
+        c -= 8;
+        m >>= 8;
+      }
+      pre_.push_back((uint16_t)(l >> c));
+      s = c + d - 24;
+      l &= m;
+    }
+    low_ = l << d;
+    rng_ = r << d;
+    cnt_ = s;
+  }
   uint64_t low_ = 0;
   uint32_t rng_ = 0x8000;
   int cnt_ = -9;
