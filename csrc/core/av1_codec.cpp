@@ -199,6 +199,8 @@ struct Tile {
   std::vector<uint8_t> aLvl[3], aDc[3], lLvl[3], lDc[3];
   // level access: writer reads, reader writes (full layout [nblk][N*N])
   std::function<const int16_t*(int, int)> lev_in;
+  const int16_t* eob_in[3] = {nullptr, nullptr, nullptr};  // writer: eob per packed TB (scan_packed)
+  const int32_t* eob_off[3] = {nullptr, nullptr, nullptr};   // block -> packed TB index (-1: none)
   int16_t* lev_out[3] = {nullptr, nullptr, nullptr};
 
   Tile(IO& io_, const SeqGeo& g_, FrameParams& fp_, std::vector<uint32_t>& mode_, std::vector<uint32_t>& mv_,
@@ -246,7 +248,7 @@ struct Tile {
   }
 
   // one transform block; L = raster levels (writer: input, reader: output)
-  void coeffs(int plane, int lg, int x4, int y4, int16_t* L, bool is_inter, int intra_dir) {
+  void coeffs(int plane, int lg, int x4, int y4, int16_t* L, bool is_inter, int intra_dir, int eob_hint = -1) {
     const int N = 1 << lg, area = N * N, w4 = N >> 2, ptype = plane > 0, txc = lg - 2;
     const int16_t* scan = lg == 4 ? scans().s16 : scans().s8;
     auto& AL = aLvl[plane];
@@ -262,8 +264,8 @@ struct Tile {
       }
       ctx = 7 + (above != 0) + (left != 0);
     }
-    int eob = 0;
-    if (IO::kW)
+    int eob = IO::kW && eob_hint >= 0 ? eob_hint : 0;
+    if (IO::kW && eob_hint < 0)
       for (int c = area - 1; c >= 0; --c)
         if (L[scan[c]]) {
           eob = c + 1;
@@ -754,7 +756,9 @@ struct Tile {
         } else {
           L = lev_out[p] + ((size_t)b << (2 * lg));
         }
-        coeffs(p, lg, p ? x4 >> 1 : x4, p ? y4 >> 1 : y4, L, inter != 0, ymode[b]);
+        int hint = -1;
+        if (IO::kW && eob_in[p]) hint = eob_off[p][b] < 0 ? 0 : eob_in[p][eob_off[p][b]];
+        coeffs(p, lg, p ? x4 >> 1 : x4, p ? y4 >> 1 : y4, L, inter != 0, ymode[b], hint);
         for (int i = 0; i < (1 << (2 * lg)); ++i)
           if (L[i]) {
             nz |= 1 << p;
@@ -1210,7 +1214,7 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
   // level access (packed layout: prefix offsets over the nonzero masks)
   std::vector<int32_t> off[3];
   const int16_t* base[3] = {d.ly, d.lu, d.lv};
-  std::vector<int16_t> expd[3];
+  std::vector<int16_t> expd[3], eobs[3];
   if (d.scan_packed)  // [eob, eob levels in scan order] per nonzero TB -> raster TBs
     for (int p = 0; p < 3; ++p) {
       const int sz = p ? 64 : 256;
@@ -1218,10 +1222,12 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
       int cnt = 0;
       for (int b = 0; b < nb; ++b) cnt += mode_nz(mode[b]) >> p & 1;
       expd[p].assign((size_t)cnt * sz, 0);
+      eobs[p].resize(cnt);
       const int16_t* q = base[p];
       for (int k = 0; k < cnt; ++k) {
         const int eob = *q++;
         if (eob < 1 || eob > sz) throw std::runtime_error("scan-packed levels: bad eob");
+        eobs[p][k] = (int16_t)eob;
         for (int i = 0; i < eob; ++i) expd[p][(size_t)k * sz + scan[i]] = q[i];
         q += eob;
       }
@@ -1233,6 +1239,11 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
       int k = 0;
       for (int b = 0; b < nb; ++b)
         if (mode_nz(mode[b]) >> p & 1) off[p][b] = k++;
+    }
+  if (d.scan_packed)
+    for (int p = 0; p < 3; ++p) {  // eob hints: the writer skips the backward eob scan
+      t.eob_in[p] = eobs[p].data();
+      t.eob_off[p] = off[p].data();
     }
   t.lev_in = [&](int p, int b) -> const int16_t* {
     const size_t sz = p ? 64 : 256;
