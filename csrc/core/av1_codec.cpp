@@ -10,14 +10,15 @@
 // specification's derivations (partition, skip, is_inter, y/uv modes, single_ref_p*,
 // new/zero/ref mv + drl from the spatial MV stack of 7.10.2, mv joints/classes, all_zero,
 // eob_pt / eob_extra, coeff_base(_eob) / coeff_br with the 2-D context offsets, dc_sign,
-// Golomb remainders).  SUBSTITUTE: every CDF starts uniform (the specification's default
-// CDF tables are not available offline) and adapts with the AV1 counter-based rate.
+// Golomb remainders).  CDFs start from the specification's defaults (tv/av1_tables.h) and
+// adapt with the AV1 counter-based rate.
 //
 // Reference parity: thinvids rejects AV1 sources (/root/reference/worker/tasks.py:929-939)
 // and encodes H.264 (:1532-1586); this is the north-star AV1 encoder of BASELINE.json.
 #include "tv/av1_codec.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <cstring>
 #include <functional>
@@ -27,6 +28,8 @@
 
 #include "tv/av1.h"
 #include "tv/av1_defs.h"
+#include "tv/av1_itx.h"
+#include "tv/av1_tables.h"
 #include "tv/av1_txfm.h"
 #include "tv/bitstream.h"
 
@@ -141,9 +144,68 @@ template <class F> void visit_cdfs(Cdfs& c, F f) {
   each(c.dc_sign, 2, f);
   each(c.use_sgrproj, 2, f);
 }
-// SUBSTITUTE for the specification's default CDFs: every CDF starts uniform
-void init_cdfs(Cdfs& c) {
-  visit_cdfs(c, [](uint16_t* p, int n) { cdf_init_uniform(p, n); });
+// The specification's default CDFs (tv/av1_tables.h holds them as cumulative values):
+// init_non_coeff_cdfs + init_coeff_cdfs with the coefficient set of base_q_idx's context.
+void set_cdf(uint16_t* c, const uint16_t* cum, int n) {
+  for (int i = 0; i < n - 1; ++i) c[i] = (uint16_t)(32768 - cum[i]);
+  c[n - 1] = 0;
+  c[n] = 0;
+}
+template <size_t K> void set_cdfs(C17 (&c)[K], const uint16_t* cum, int stride, int n) {
+  for (size_t k = 0; k < K; ++k) set_cdf(c[k], cum + k * stride, n);
+}
+int coeff_qctx(int qidx) { return qidx <= 20 ? 0 : (qidx <= 60 ? 1 : (qidx <= 120 ? 2 : 3)); }
+void init_cdfs(Cdfs& c, int qidx) {
+  using namespace tab;
+  std::memset(&c, 0, sizeof(c));
+  for (int b = 0; b < 4; ++b) set_cdfs(c.partition[b], kPartition[b * 4], 9, b ? 10 : 4);
+  for (int a = 0; a < 5; ++a) set_cdfs(c.kf_y[a], kKfYMode[a][0], 12, 13);
+  set_cdfs(c.y_mode, kYMode[0], 12, 13);
+  set_cdfs(c.uv[0], kUvMode0[0], 12, 13);
+  set_cdfs(c.uv[1], kUvMode1[0], 13, 14);
+  set_cdfs(c.angle, kAngleDelta[0], 6, 7);
+  set_cdfs(c.skip, kSkip[0], 1, 2);
+  set_cdfs(c.is_inter, kIntraInter[0], 1, 2);
+  for (int r = 0; r < 3; ++r) set_cdfs(c.single_ref[r], kSingleRef[r][0], 1, 2);
+  set_cdfs(c.new_mv, kNewmv[0], 1, 2);
+  set_cdfs(c.zero_mv, kZeromv[0], 1, 2);
+  set_cdfs(c.ref_mv, kRefmv[0], 1, 2);
+  set_cdfs(c.drl, kDrl[0], 1, 2);
+  set_cdf(c.mv_joint, kMvJoint, 4);
+  for (int k = 0; k < 2; ++k) {
+    const uint16_t half[1] = {16384};
+    set_cdf(c.mv_sign[k], half, 2);
+    set_cdf(c.mv_class[k], kMvClass, 11);
+    set_cdf(c.class0_bit[k], kMvClass0Bit, 2);
+    set_cdfs(c.class0_fr[k], kMvClass0Fr[0], 3, 4);
+    set_cdf(c.mv_fr[k], kMvFr, 4);
+    set_cdfs(c.mv_bits[k], kMvBits[0], 1, 2);
+  }
+  for (int t = 0; t < 4; ++t) set_cdfs(c.intra_tx[t], kIntraTxSet2[t][0], 4, 5);
+  set_cdfs(c.inter_tx, kInterTxSet3[0], 1, 2);
+  set_cdf(c.use_sgrproj, kUseSgrproj, 2);
+  const int q = coeff_qctx(qidx);
+  for (int t = 0; t < 5; ++t) {
+    set_cdfs(c.txb_skip[t], kTxbSkip[q][t][0], 1, 2);
+    for (int p = 0; p < 2; ++p) {
+      set_cdfs(c.eob_extra[t][p], kEobExtra[q][t][p][0], 1, 2);
+      set_cdfs(c.base_eob[t][p], kCoeffBaseEob[q][t][p][0], 2, 3);
+      set_cdfs(c.base[t][p], kCoeffBase[q][t][p][0], 3, 4);
+      if (t < 4) set_cdfs(c.br[t][p], kCoeffBr[q][t][p][0], 3, 4);
+    }
+  }
+  for (int p = 0; p < 2; ++p) {
+    set_cdfs(c.dc_sign[p], kDcSign[q][p][0], 1, 2);
+    for (int k = 0; k < 2; ++k) {
+      set_cdf(c.eob_pt[0][p][k], kEobPt16[q][p][k], 5);
+      set_cdf(c.eob_pt[1][p][k], kEobPt32[q][p][k], 6);
+      set_cdf(c.eob_pt[2][p][k], kEobPt64[q][p][k], 7);
+      set_cdf(c.eob_pt[3][p][k], kEobPt128[q][p][k], 8);
+      set_cdf(c.eob_pt[4][p][k], kEobPt256[q][p][k], 9);
+      set_cdf(c.eob_pt[5][p][k], kEobPt512[q][p][k], 10);
+      set_cdf(c.eob_pt[6][p][k], kEobPt1024[q][p][k], 11);
+    }
+  }
 }
 // CDFs saved at the end of a frame (disable_frame_end_update_cdf = 0) and loaded by the
 // next frame through primary_ref_frame: probabilities kept, adaptation counters cleared
@@ -206,7 +268,7 @@ struct Tile {
   Tile(IO& io_, const SeqGeo& g_, FrameParams& fp_, std::vector<uint32_t>& mode_, std::vector<uint32_t>& mv_,
        std::vector<int8_t>& cdef_)
       : io(io_), g(g_), fp(fp_), MiRows(g_.H / 4), MiCols(g_.W / 4), mode(mode_), mv(mv_), cdef_idx(cdef_) {
-    init_cdfs(cdf);
+    init_cdfs(cdf, fp_.qindex);
     ymode.assign(g.nblk(), 0);
     coded.assign(g.nblk(), 0);
     cdef_seen.assign(g.nsb(), -1);
@@ -1280,20 +1342,22 @@ struct PlaneRef {
   int operator()(int x, int y) const { return p[(size_t)clip3(0, h - 1, y) * w + clip3(0, w - 1, x)]; }
 };
 
-// dequantise + inverse transform a TB of levels into a residual (int16 raster)
+// dequantise + inverse transform a TB of levels into a residual (int16 raster): 7.12.3
+// dequantisation and the 7.13.3 2-D inverse transform process
 void residual_of(const int16_t* lev, int lg, int qidx, int txt, int16_t* res) {
   const int N = 1 << lg, area = N * N;
-  int16_t dq[256];
+  int32_t dq[256], r[256];
   bool any = false;
   for (int i = 0; i < area; ++i) {
-    dq[i] = (int16_t)dequant(lev[i], i == 0 ? dc_q(qidx) : ac_q(qidx));
+    dq[i] = dequant(lev[i], i == 0 ? dc_q(qidx) : ac_q(qidx));
     any |= dq[i] != 0;
   }
   if (!any) {
     std::memset(res, 0, sizeof(int16_t) * area);
     return;
   }
-  txfm2d_ref(dq, res, 1, lg, txt & 1, (txt >> 1) & 1, true);
+  inv_txfm2d(dq, lg, txt & 1, (txt >> 1) & 1, r);
+  for (int i = 0; i < area; ++i) res[i] = (int16_t)r[i];
 }
 
 // self-guided restoration of the CDEF output with the per-unit (set, xqd0, xqd1)
@@ -1436,7 +1500,7 @@ size_t read_leb128(const uint8_t* p, size_t n, size_t& pos) {
 Decoded decode_stream(const uint8_t* p, size_t n) {
   Decoded out;
   Cdfs saved_cdfs;
-  init_cdfs(saved_cdfs);
+  init_cdfs(saved_cdfs, 0);
   bool have_seq = false;
   size_t pos = 0;
   while (pos < n) {
@@ -1598,6 +1662,10 @@ int satd_block(const int* a, const int* b, int N) {
 GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qidx0, const int* qmap) {
   GoldenOut out;
   const int nb = g.nblk();
+  // TV_AV1_DBG (conformance bring-up): 1 no deblocking, 2 no CDEF, 4 no loop restoration,
+  // 8 DC_PRED only, 16 no residual
+  const char* dbg_env = std::getenv("TV_AV1_DBG");
+  const int dbg = dbg_env ? std::atoi(dbg_env) : 0;
   for (size_t f = 0; f < src.size(); ++f) {
     const int qidx = qmap ? clip3(1, 255, qmap[f]) : qidx0, lam = lambda16(qidx);
     const Planes& S = src[f];
@@ -1605,7 +1673,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
     FrameData fd;
     fd.fp.key = f == 0;
     fd.fp.qindex = qidx;
-    const int lvl = lf_level_for_q(qidx);
+    const int lvl = (dbg & 1) ? 0 : lf_level_for_q(qidx);
     for (int i = 0; i < 4; ++i) fd.fp.lf[i] = lvl;
     fd.fp.cdef_damping = 3 + (qidx0 >> 6);  // per stream (the engine's CDEF launches take one damping)
     fd.mode.assign(nb, 0);
@@ -1640,7 +1708,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
         uint32_t mvw = 0;
         if (fd.fp.key) {
           int best = 1 << 30;
-          for (int k = 0; k < kNumIntraCand; ++k) {
+          for (int k = 0; k < ((dbg & 8) ? 1 : kNumIntraCand); ++k) {
             const uint32_t m = pack_mode(0, intra_cand(k), 0, 0, 0);
             int pr[256];
             predict(g, 0, bx, by, m, 0, rec, nullptr, pr);
@@ -1648,7 +1716,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
             if (cost < best) best = cost, ym = intra_cand(k), std::memcpy(pred[0], pr, sizeof(pr));
           }
           best = 1 << 30;
-          for (int k = 0; k < kNumIntraCand; ++k) {
+          for (int k = 0; k < ((dbg & 8) ? 1 : kNumIntraCand); ++k) {
             const uint32_t m = pack_mode(0, 0, intra_cand(k), 0, 0);
             int pu[64], pv[64];
             predict(g, 1, bx, by, m, 0, rec, nullptr, pu);
@@ -1708,6 +1776,9 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
           const int N = p ? 8 : 16, lg = p ? 3 : 4, w = p ? g.W / 2 : g.W;
           const int txt = p == 0 || inter ? 0 : uv_txtype(uvm);
           int16_t* lev = p == 0 ? &fd.ly[(size_t)b * 256] : (p == 1 ? &fd.lu[(size_t)b * 64] : &fd.lv[(size_t)b * 64]);
+          if (dbg & 16) {
+            for (int i = 0; i < N * N; ++i) s[p][i] = pred[p][i];
+          }
           if (code_tb(s[p], pred[p], lg, qidx, txt, inter ? kRndInter : kRndIntra, lev, rc)) nz |= 1 << p;
           std::vector<uint8_t>& P = p == 0 ? rec.y : (p == 1 ? rec.u : rec.v);
           for (int i = 0; i < N; ++i)
@@ -1751,6 +1822,12 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
       if (!mode_skip(fd.mode[b])) active[((b / g.bw) / 4) * g.sbw + (b % g.bw) / 4] = 1;
     fd.cdef_idx.assign(nfb, -1);
     cdef_choose(sy.data(), su.data(), active.data(), nfb, fd.fp.cdef_y, fd.fp.cdef_uv, fd.cdef_idx.data());
+    if (dbg & 2) {
+      fd.fp.cdef_bits = 0;
+      std::memset(fd.fp.cdef_y, 0, sizeof(fd.fp.cdef_y));
+      std::memset(fd.fp.cdef_uv, 0, sizeof(fd.fp.cdef_uv));
+      for (int f = 0; f < nfb; ++f) fd.cdef_idx[f] = active[f] ? 0 : -1;
+    }
     // final recon: CDEF applied to the deblocked frame, then the self-guided restoration
     // search per 64x64 unit on the CDEF output (off / candidate sets, SSE + rate)
     Planes fin;
@@ -1765,7 +1842,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
       std::vector<long long> best(nu);
       unit_sse(Sp.data(), X.data(), pw, ph, best.data());
       for (int u = 0; u < nu; ++u) P[3 * u] = -1, P[3 * u + 1] = P[3 * u + 2] = 0;
-      for (int k = 0; k < kNumLrSets; ++k) {
+      for (int k = 0; k < ((dbg & 4) ? 0 : kNumLrSets); ++k) {
         const int set = lr_set(k);
         std::vector<int64_t> st((size_t)nu * 5);
         sgr_stats(Sp.data(), X.data(), pw, ph, set, st.data());

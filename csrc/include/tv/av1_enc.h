@@ -15,14 +15,13 @@
 //     syntax writer from the spatial MV stack (the mode does not change the reconstruction);
 //   * deblocking with frame levels, CDEF (8 presets per frame, 64x64 cdef_idx).
 //
-// Tables the AV1 specification defines but that are not available offline (no spec text,
-// libaom or dav1d in the image) are substituted and marked "SUBSTITUTE" below: the q-index
-// lookup, default CDFs (csrc/core/av1_codec.cpp) and the transform rounding (av1_txfm.h).
-// The stream syntax follows AV1 (OBUs, uncompressed header, partition / mode / coefficient
-// symbols and contexts); parity with libaom / dav1d is unpinned.
+// Every normative table (q lookup, default CDFs) is the specification's (tv/av1_tables.h)
+// and the inverse transforms are the specification's (tv/av1_itx.h): streams decode with
+// any conformant AV1 decoder (tests/test_av1_conformance.py decodes them with dav1d).
 #pragma once
 #include <cstdint>
 
+#include "tv/av1_tables.h"
 #include "tv/hevc_defs.h"  // TV_HD, clip3, tv_abs
 
 namespace tv {
@@ -56,25 +55,9 @@ TV_HD int uv_txtype(int uv_mode) {
 }
 
 // ---------------------------------------------------------------- quantizer ------------
-// SUBSTITUTE for Dc_Qlookup / Ac_Qlookup (8-bit): same end points (4 at qindex 0, AC 1828 /
-// DC 1336 at 255), +1 per index up to 96 as in the spec's linear region, then geometric.
-TV_HD int ac_q(int q) {
-  q = clip3(0, 255, q);
-  if (q == 0) return 4;
-  if (q <= 96) return q + 7;
-  // 103 * 2^((q - 96) / 38.3): integer fixed point so host == device
-  const int e = (q - 96) * 1711;  // (q-96)/38.3 in 1/65536 units
-  const int ip = e >> 16, fp = e & 65535;
-  // 2^f ~ 1 + f (0.6565 + 0.3435 f) on [0, 1)
-  const long long two_f = 65536 + (((long long)fp * (43025 + ((22511LL * fp) >> 16))) >> 16);
-  long long v = (103LL * two_f) << ip;
-  int r = (int)((v + 32768) >> 16);
-  return r > 1828 ? 1828 : r;
-}
-TV_HD int dc_q(int q) {
-  const int a = ac_q(q);
-  return a - (int)(((long long)a * 27 * clip3(0, 255, q)) / (100 * 255));
-}
+// Dc_Qlookup / Ac_Qlookup (8-bit) of the specification (tv/av1_tables.h)
+TV_HD int ac_q(int q) { return tab::kAcQLookup[clip3(0, 255, q)]; }
+TV_HD int dc_q(int q) { return tab::kDcQLookup[clip3(0, 255, q)]; }
 // encoder quantisation rounding (1/128 of the step): intra 1/3, inter 1/6 (dead zone)
 constexpr int kRndIntra = 43, kRndInter = 21;
 TV_HD int quant(int c, int q, int rnd) {
