@@ -1375,6 +1375,14 @@ void apply_lr(const SeqGeo& g, const int32_t* lr, Planes& io) {
   }
 }
 
+// flag the 8x8 blocks of skip blocks in a CDEF direction array (kCdefSkipBlock)
+void mark_cdef_skip(const SeqGeo& g, const uint32_t* mode, uint8_t* dir) {
+  const int w8 = g.W / 8, h8 = g.H / 8;
+  for (int y = 0; y < h8; ++y)
+    for (int x = 0; x < w8; ++x)
+      if (mode_skip(mode[(y / 2) * g.bw + x / 2])) dir[y * w8 + x] |= kCdefSkipBlock;
+}
+
 void loop_filters(const SeqGeo& g, const FrameParams& fp, const uint32_t* mode, const int8_t* cdef_idx, Planes& rec,
                   Planes& out, const int32_t* lr = nullptr) {
   const int W = g.W, H = g.H;
@@ -1402,6 +1410,7 @@ void loop_filters(const SeqGeo& g, const FrameParams& fp, const uint32_t* mode, 
   std::vector<uint8_t> dir(n8);
   std::vector<int> var(n8);
   cdef_find_dirs(db.y.data(), W, H, dir.data(), var.data());
+  mark_cdef_skip(g, mode, dir.data());
   std::vector<int8_t> py(g.nsb()), puv(g.nsb());
   for (int s = 0; s < g.nsb(); ++s) {
     py[s] = cdef_idx[s] < 0 ? -1 : (int8_t)fp.cdef_y[cdef_idx[s]];
@@ -1809,6 +1818,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
     std::vector<uint8_t> dir(n8);
     std::vector<int> var(n8);
     cdef_find_dirs(db.y.data(), W, H, dir.data(), var.data());
+    mark_cdef_skip(g, fd.mode.data(), dir.data());
     std::vector<uint64_t> sy((size_t)nfb * kCdefPresets), su(sy.size()), sv(sy.size());
     cdef_search(S.y.data(), db.y.data(), W, H, false, dir.data(), var.data(), W / 8, fd.fp.cdef_damping, sy.data(),
                 kCdefMaskY, true);

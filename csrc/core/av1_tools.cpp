@@ -64,7 +64,7 @@ void cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, bool chro
     for (int by = fr * fbs / bs; by < std::min(h / bs, (fr + 1) * fbs / bs); ++by)
     for (int bx = 0; bx < w / bs; ++bx) {
       if (checker && ((bx + by) & 1)) continue;  // encoder search on a checkerboard of blocks
-      const int d = dir[by * luma_w8 + bx], v = var[by * luma_w8 + bx];
+      const int d0 = dir[by * luma_w8 + bx], v = var[by * luma_w8 + bx];
       uint64_t* S = sse + (long)((by * bs / fbs) * nfx + bx * bs / fbs) * kCdefPresets;
       for (int p = 0; p < kCdefPresets; ++p) {
         if (!(pmask >> p & 1)) {
@@ -73,11 +73,13 @@ void cdef_search(const uint8_t* src, const uint8_t* rec, int w, int h, bool chro
         }
         int pri, sec;
         block_strengths(p, chroma, v, pri, sec);
+        if (d0 & kCdefSkipBlock) pri = sec = 0;  // skip blocks are not filtered
+        const int d = cdef_dir_used(p, d0);
         uint64_t acc = 0;
         for (int i = 0; i < bs; ++i)
           for (int j = 0; j < bs; ++j) {
             const int x = bx * bs + j, y = by * bs + i;
-            const int f = cdef_filter_pixel(rec, w, w, h, x, y, pri, sec, dmp, d);
+            const int f = (pri | sec) ? cdef_filter_pixel(rec, w, w, h, x, y, pri, sec, dmp, d) : rec[(long)y * w + x];
             const int e = f - (int)src[(long)y * w + x];
             acc += (uint64_t)(e * e);
           }
@@ -100,9 +102,10 @@ void cdef_apply(const uint8_t* rec, int w, int h, bool chroma, const uint8_t* di
   for (int by = 0; by < h / bs; ++by)
     for (int bx = 0; bx < w / bs; ++bx) {
       const int p = fb_preset[(by * bs / fbs) * nfx + bx * bs / fbs];
-      const int d = dir[by * luma_w8 + bx], v = var[by * luma_w8 + bx];
+      const int d0 = dir[by * luma_w8 + bx], v = var[by * luma_w8 + bx];
       int pri = 0, sec = 0;
-      if (p >= 0) block_strengths(p, chroma, v, pri, sec);
+      if (p >= 0 && !(d0 & kCdefSkipBlock)) block_strengths(p, chroma, v, pri, sec);
+      const int d = cdef_dir_used(p, d0);
       for (int i = 0; i < bs; ++i)
         for (int j = 0; j < bs; ++j) {
           const int x = bx * bs + j, y = by * bs + i;

@@ -132,6 +132,12 @@ TV_HD int cdef_filter_pixel(const uint8_t* P, int p, int w, int h, int x, int y,
 
 // CDEF strength preset: index = pri * 4 + sec_idx; sec_idx 3 means strength 4.
 TV_HD int cdef_sec_value(int sec_idx) { return sec_idx == 3 ? 4 : sec_idx; }
+// Direction-array flag of an 8x8 block whose four 4x4 units are all skip (7.15 cdef_block:
+// such blocks are not filtered); set by the callers that know the block modes.
+constexpr int kCdefSkipBlock = 0x80;
+// 7.15.1: the filter direction is the block's direction unless the preset's (unadjusted)
+// primary strength is 0, then 0 (the secondary taps still run along directions 2 / 6)
+TV_HD int cdef_dir_used(int preset, int d) { return (preset >> 2) == 0 ? 0 : (d & 7); }
 constexpr int kCdefPresets = 64;  // 16 primary x 4 secondary
 constexpr uint64_t kCdefSkipped = 1ull << 40;  // SSE reported for presets a search skipped
 

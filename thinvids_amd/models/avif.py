@@ -87,26 +87,26 @@ def _item_props(width: int, height: int, seq_obu: bytes) -> bytes:
     return _box(b"ipco", ispe + _box(b"av1C", av1c(seq_obu)) + pixi)
 
 
-def avif_still(tu: bytes, width: int, height: int) -> bytes:
-    """One key-frame temporal unit -> AVIF file bytes (the item holds the sequence header
-    and frame OBUs; the temporal delimiter is dropped, as MIAF requires)."""
-    item = strip_td(tu)
-    seq = sequence_header(tu)
-    ftyp = _box(b"ftyp", b"avif" + struct.pack(">I", 0) + b"avifmif1miaf")
+def _meta(width: int, height: int, seq: bytes, off: int, size: int) -> bytes:
+    """HEIF meta box of one av01 item whose data is `size` bytes at file offset `off`."""
     hdlr = _fbox(b"hdlr", 0, 0, b"\0\0\0\0pict" + b"\0" * 12 + b"\0")
     pitm = _fbox(b"pitm", 0, 0, struct.pack(">H", 1))
     infe = _fbox(b"infe", 2, 0, struct.pack(">HH", 1, 0) + b"av01" + b"\0")
     iinf = _fbox(b"iinf", 0, 0, struct.pack(">H", 1) + infe)
     ipma = _fbox(b"ipma", 0, 0, struct.pack(">IHB", 1, 1, 3) + bytes([0x81, 0x82, 0x03]))
     iprp = _box(b"iprp", _item_props(width, height, seq) + ipma)
+    iloc = _fbox(b"iloc", 0, 0, bytes([0x44, 0x00]) + struct.pack(">HHHHII", 1, 1, 0, 1, off, size))
+    return _fbox(b"meta", 0, 0, hdlr + pitm + iloc + iinf + iprp)
 
-    def build(off: int) -> bytes:
-        iloc = _fbox(b"iloc", 0, 0, bytes([0x44, 0x00]) + struct.pack(">HHHHII", 1, 1, 0, 1, off, len(item)))
-        return _fbox(b"meta", 0, 0, hdlr + pitm + iloc + iinf + iprp)
 
-    meta = build(0)
-    off = len(ftyp) + len(meta) + 8
-    meta = build(off)
+def avif_still(tu: bytes, width: int, height: int) -> bytes:
+    """One key-frame temporal unit -> AVIF file bytes (the item holds the sequence header
+    and frame OBUs; the temporal delimiter is dropped, as MIAF requires)."""
+    item = strip_td(tu)
+    seq = sequence_header(tu)
+    ftyp = _box(b"ftyp", b"avif" + struct.pack(">I", 0) + b"avifmif1miaf")
+    n = len(_meta(width, height, seq, 0, len(item)))
+    meta = _meta(width, height, seq, len(ftyp) + n + 8, len(item))
     return ftyp + meta + _box(b"mdat", item)
 
 
@@ -144,9 +144,11 @@ def avis_sequence(tus: list, width: int, height: int, fps: int = 30) -> bytes:
         mdia = _box(b"mdia", mdhd + hdlr + minf)
         return _box(b"moov", mvhd + _box(b"trak", tkhd + mdia))
 
-    moov = build(0)
-    moov = build(len(ftyp) + len(moov) + 8)
-    return ftyp + moov + _box(b"mdat", b"".join(samples))
+    # the first frame is also the primary image item (what still-image readers show)
+    nm = len(_meta(width, height, seq, 0, len(samples[0])))
+    data_off = len(ftyp) + nm + len(build(0)) + 8
+    meta = _meta(width, height, seq, data_off, len(samples[0]))
+    return ftyp + meta + build(data_off) + _box(b"mdat", b"".join(samples))
 
 
 # ------------------------------------------------------------------ dav1d via libavif --
