@@ -64,6 +64,32 @@ def sequence_header(tu: bytes) -> bytes:
     raise ValueError("no sequence header OBU in the temporal unit")
 
 
+def seq_frame_size(seq_obu: bytes) -> tuple[int, int]:
+    """max_frame_width / height of a sequence header OBU (one operating point, no timing
+    or decoder-model info: the encoder's headers)."""
+    h = seq_obu[0]
+    _, i = _leb128(seq_obu, 1 + ((h >> 2) & 1))
+    bits = int.from_bytes(seq_obu[i:i + 16].ljust(16, b"\0"), "big")
+    pos = [0]
+
+    def u(n):
+        pos[0] += n
+        return (bits >> (128 - pos[0])) & ((1 << n) - 1)
+
+    u(3), u(1)
+    if u(1):  # reduced_still_picture_header
+        raise ValueError("reduced still-picture headers are not written by this encoder")
+    if u(1) or u(1):
+        raise ValueError("timing / display-delay info not supported")
+    if u(5) != 0:
+        raise ValueError("one operating point expected")
+    u(12)
+    if u(5) > 7:
+        u(1)
+    wb, hb = u(4) + 1, u(4) + 1
+    return u(wb) + 1, u(hb) + 1
+
+
 def av1c(seq_obu: bytes) -> bytes:
     """AV1CodecConfigurationRecord for the encoder's sequence header (Main profile, 8-bit
     4:2:0, colocated-unknown chroma position; seq_level_idx 31 as written)."""
@@ -81,10 +107,15 @@ def _fbox(typ: bytes, version: int, flags: int, payload: bytes) -> bytes:
     return _box(typ, struct.pack(">I", (version << 24) | flags) + payload)
 
 
-def _item_props(width: int, height: int, seq_obu: bytes) -> bytes:
-    ispe = _fbox(b"ispe", 0, 0, struct.pack(">II", width, height))
+def _item_props(width: int, height: int, seq_obu: bytes) -> tuple[bytes, int]:
+    """ipco and its property count.  ispe is the coded frame size: readers rescale a frame
+    whose size differs from ispe (libavif does), so the display size lives only in the
+    stream's render_size."""
+    del width, height
+    W, H = seq_frame_size(seq_obu)
+    ispe = _fbox(b"ispe", 0, 0, struct.pack(">II", W, H))
     pixi = _fbox(b"pixi", 0, 0, bytes([3, 8, 8, 8]))
-    return _box(b"ipco", ispe + _box(b"av1C", av1c(seq_obu)) + pixi)
+    return _box(b"ipco", ispe + _box(b"av1C", av1c(seq_obu)) + pixi), 3
 
 
 def _meta(width: int, height: int, seq: bytes, off: int, size: int) -> bytes:
@@ -93,8 +124,9 @@ def _meta(width: int, height: int, seq: bytes, off: int, size: int) -> bytes:
     pitm = _fbox(b"pitm", 0, 0, struct.pack(">H", 1))
     infe = _fbox(b"infe", 2, 0, struct.pack(">HH", 1, 0) + b"av01" + b"\0")
     iinf = _fbox(b"iinf", 0, 0, struct.pack(">H", 1) + infe)
-    ipma = _fbox(b"ipma", 0, 0, struct.pack(">IHB", 1, 1, 3) + bytes([0x81, 0x82, 0x03]))
-    iprp = _box(b"iprp", _item_props(width, height, seq) + ipma)
+    ipco, nprop = _item_props(width, height, seq)
+    ipma = _fbox(b"ipma", 0, 0, struct.pack(">IHB", 1, 1, nprop) + bytes([0x81, 0x82, 0x03, 0x84][:nprop]))
+    iprp = _box(b"iprp", ipco + ipma)
     iloc = _fbox(b"iloc", 0, 0, bytes([0x44, 0x00]) + struct.pack(">HHHHII", 1, 1, 0, 1, off, size))
     return _fbox(b"meta", 0, 0, hdlr + pitm + iloc + iinf + iprp)
 
@@ -114,6 +146,7 @@ def avis_sequence(tus: list, width: int, height: int, fps: int = 30) -> bytes:
     """Temporal units of one closed GOP (key frame first) -> AVIF image-sequence bytes."""
     samples = [strip_td(t) for t in tus]
     seq = sequence_header(tus[0])
+    W, H = seq_frame_size(seq)
     n = len(samples)
     ftyp = _box(b"ftyp", b"avis" + struct.pack(">I", 0) + b"avisavifmsf1iso8mif1miaf")
     ts, dur = fps, 1
@@ -122,13 +155,13 @@ def avis_sequence(tus: list, width: int, height: int, fps: int = 30) -> bytes:
                  + struct.pack(">I", 2))
     tkhd = _fbox(b"tkhd", 0, 3, struct.pack(">IIIII", 0, 0, 1, 0, n * dur) + b"\0" * 8 + struct.pack(">hhhH", 0, 0, 0, 0)
                  + struct.pack(">9I", 0x10000, 0, 0, 0, 0x10000, 0, 0, 0, 0x40000000)
-                 + struct.pack(">II", width << 16, height << 16))
+                 + struct.pack(">II", W << 16, H << 16))
     mdhd = _fbox(b"mdhd", 0, 0, struct.pack(">IIII", 0, 0, ts, n * dur) + struct.pack(">HH", 0x55C4, 0))
     hdlr = _fbox(b"hdlr", 0, 0, b"\0\0\0\0pict" + b"\0" * 12 + b"\0")
     vmhd = _fbox(b"vmhd", 0, 1, b"\0" * 8)
     dref = _fbox(b"dref", 0, 0, struct.pack(">I", 1) + _fbox(b"url ", 0, 1, b""))
     dinf = _box(b"dinf", dref)
-    av01 = _box(b"av01", b"\0" * 6 + struct.pack(">H", 1) + b"\0" * 16 + struct.pack(">HH", width, height)
+    av01 = _box(b"av01", b"\0" * 6 + struct.pack(">H", 1) + b"\0" * 16 + struct.pack(">HH", W, H)
                 + struct.pack(">II", 0x00480000, 0x00480000) + b"\0" * 4 + struct.pack(">H", 1) + b"\0" * 32
                 + struct.pack(">Hh", 0x18, -1) + _box(b"av1C", av1c(seq)))
     stsd = _fbox(b"stsd", 0, 0, struct.pack(">I", 1) + av01)
@@ -198,7 +231,9 @@ _STRICT_FLAGS_IDX, _IMAGE_PTR_OFF = 10, 48
 
 def dav1d_decode(data: bytes) -> list:
     """Decode an AVIF / AVIS file with libavif's dav1d; returns [(Y, U, V)] uint8 planes
-    per frame (frame size, as the decoder outputs them)."""
+    per frame at the decoded frame size (libavif applies no clean-aperture crop; it does
+    rescale to an ``ispe`` that differs from the frame size, which this module's writers
+    never produce)."""
     lib = _libavif()
     d = lib.avifDecoderCreate()
     if not d:
