@@ -1360,8 +1360,9 @@ void residual_of(const int16_t* lev, int lg, int qidx, int txt, int16_t* res) {
   for (int i = 0; i < area; ++i) res[i] = (int16_t)r[i];
 }
 
-// self-guided restoration of the CDEF output with the per-unit (set, xqd0, xqd1)
-void apply_lr(const SeqGeo& g, const int32_t* lr, Planes& io) {
+// normative self-guided restoration of the CDEF output `io` with the per-unit (set, xqd0,
+// xqd1); `db` = the deblocked (pre-CDEF) frame the stripe boundaries read
+void apply_lr(const SeqGeo& g, const int32_t* lr, const Planes& db, Planes& io) {
   for (int p = 0; p < 3; ++p) {
     const int nu = g.lr_ux(p) * g.lr_uy(p);
     const int32_t* P = lr + (size_t)p * g.lr_nu() * 3;
@@ -1369,8 +1370,9 @@ void apply_lr(const SeqGeo& g, const int32_t* lr, Planes& io) {
     for (int u = 0; u < nu; ++u) any |= P[3 * u] >= 0;
     if (!any) continue;
     std::vector<uint8_t>& X = p == 0 ? io.y : (p == 1 ? io.u : io.v);
+    const std::vector<uint8_t>& D = p == 0 ? db.y : (p == 1 ? db.u : db.v);
     std::vector<uint8_t> o(X.size());
-    sgr_apply(X.data(), p ? g.W / 2 : g.W, p ? g.H / 2 : g.H, P, o.data());
+    lr_apply(X.data(), D.data(), p ? g.W / 2 : g.W, p ? g.H / 2 : g.H, p ? 1 : 0, P, o.data());
     X.swap(o);
   }
 }
@@ -1384,7 +1386,7 @@ void mark_cdef_skip(const SeqGeo& g, const uint32_t* mode, uint8_t* dir) {
 }
 
 void loop_filters(const SeqGeo& g, const FrameParams& fp, const uint32_t* mode, const int8_t* cdef_idx, Planes& rec,
-                  Planes& out, const int32_t* lr = nullptr) {
+                  Planes& out, const int32_t* lr = nullptr, Planes* db_out = nullptr) {
   const int W = g.W, H = g.H;
   // deblocking: one info word per 4x4 unit of each plane
   Planes db;
@@ -1424,7 +1426,8 @@ void loop_filters(const SeqGeo& g, const FrameParams& fp, const uint32_t* mode, 
              out.u.data());
   cdef_apply(db.v.data(), W / 2, H / 2, true, dir.data(), var.data(), W / 8, fp.cdef_damping, puv.data(),
              out.v.data());
-  if (lr) apply_lr(g, lr, out);
+  if (lr) apply_lr(g, lr, db, out);
+  if (db_out) *db_out = std::move(db);
 }
 
 // prediction of one block (luma 16x16 or chroma 8x8) into pred[]
@@ -1840,22 +1843,32 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
     }
     // final recon: CDEF applied to the deblocked frame, then the self-guided restoration
     // search per 64x64 unit on the CDEF output (off / candidate sets, SSE + rate)
-    Planes fin;
-    loop_filters(g, fd.fp, fd.mode.data(), fd.cdef_idx.data(), rec, fin);
+    Planes fin, dbk;
+    loop_filters(g, fd.fp, fd.mode.data(), fd.cdef_idx.data(), rec, fin, nullptr, &dbk);
     fd.lr.assign((size_t)3 * g.lr_nu() * 3, 0);
     const long long rate = lr_rate_cost(qidx);
     for (int p = 0; p < 3; ++p) {
-      const int pw = p ? W / 2 : W, ph = p ? H / 2 : H, nu = g.lr_ux(p) * g.lr_uy(p);
+      const int pw = p ? W / 2 : W, ph = p ? H / 2 : H, nu = g.lr_ux(p) * g.lr_uy(p), ux = g.lr_ux(p);
       const std::vector<uint8_t>& X = p == 0 ? fin.y : (p == 1 ? fin.u : fin.v);
+      const std::vector<uint8_t>& D = p == 0 ? dbk.y : (p == 1 ? dbk.u : dbk.v);
       const std::vector<uint8_t>& Sp = p == 0 ? S.y : (p == 1 ? S.u : S.v);
       int32_t* P = fd.lr.data() + (size_t)p * g.lr_nu() * 3;
-      std::vector<long long> best(nu);
-      unit_sse(Sp.data(), X.data(), pw, ph, best.data());
+      // per-unit SSE in the normative unit grid
+      auto unit_sse = [&](const std::vector<uint8_t>& O, std::vector<long long>& e) {
+        e.assign(nu, 0);
+        for (int y = 0; y < ph; ++y)
+          for (int x = 0; x < pw; ++x) {
+            const int d = (int)Sp[(size_t)y * pw + x] - (int)O[(size_t)y * pw + x];
+            e[lr_unit_row(y, ph, p ? 1 : 0) * ux + lr_unit_col(x, pw)] += d * d;
+          }
+      };
+      std::vector<long long> best;
+      unit_sse(X, best);
       for (int u = 0; u < nu; ++u) P[3 * u] = -1, P[3 * u + 1] = P[3 * u + 2] = 0;
       for (int k = 0; k < ((dbg & 4) ? 0 : kNumLrSets); ++k) {
         const int set = lr_set(k);
         std::vector<int64_t> st((size_t)nu * 5);
-        sgr_stats(Sp.data(), X.data(), pw, ph, set, st.data());
+        lr_stats(Sp.data(), X.data(), D.data(), pw, ph, p ? 1 : 0, set, st.data());
         std::vector<int32_t> prm((size_t)nu * 3);
         for (int u = 0; u < nu; ++u) {
           prm[3 * u] = set;
@@ -1863,9 +1876,9 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
                     &prm[3 * u + 2]);
         }
         std::vector<uint8_t> o(X.size());
-        sgr_apply(X.data(), pw, ph, prm.data(), o.data());
-        std::vector<long long> e(nu);
-        unit_sse(Sp.data(), o.data(), pw, ph, e.data());
+        lr_apply(X.data(), D.data(), pw, ph, p ? 1 : 0, prm.data(), o.data());
+        std::vector<long long> e;
+        unit_sse(o, e);
         for (int u = 0; u < nu; ++u)
           if (e[u] + rate < best[u]) {
             best[u] = e[u] + rate;
@@ -1873,7 +1886,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
           }
       }
     }
-    apply_lr(g, fd.lr.data(), fin);
+    apply_lr(g, fd.lr.data(), dbk, fin);
     out.recon.push_back(std::move(fin));
     out.frames.push_back(std::move(fd));
   }

@@ -261,6 +261,91 @@ void sgr_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int set, in
     }
 }
 
+// ------------------------------------------------- normative self-guided restoration ----
+void sgr_flt(const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, int set, int32_t* f0, int32_t* f1) {
+  const int S = 64 >> ss, off = 8 >> ss;
+  for (long i = 0; i < (long)w * h; ++i) f0[i] = f1[i] = (int)cdef[i] << kSgrRstBits;
+  std::vector<int> A, B;
+  for (int s0 = -off; s0 < h; s0 += S) {  // stripes: rows [max(0, s0), min(h, s0 + S))
+    const int y0 = std::max(0, s0), y1 = std::min(h, s0 + S);
+    if (y0 >= y1) continue;
+    auto src = [&](int x, int y) -> int {
+      bool db;
+      const int yy = lr_src_row(y, h, s0, ss, &db);
+      return (db ? dbk : cdef)[(size_t)yy * w + clip3(0, w - 1, x)];
+    };
+    const int ah = y1 - y0 + 2, aw = w + 2;  // (A, B) rows y0-1 .. y1, columns -1 .. w
+    for (int pass = 0; pass < 2; ++pass) {
+      const int r = sgr_param(set, 2 * pass), eps = sgr_param(set, 2 * pass + 1);
+      if (!r) continue;
+      A.assign((size_t)ah * aw, 0);
+      B.assign((size_t)ah * aw, 0);
+      for (int i = 0; i < ah; ++i)
+        for (int j = 0; j < aw; ++j) {
+          const int y = y0 - 1 + i, x = j - 1;
+          int sum = 0, sq = 0;
+          for (int dy = -r; dy <= r; ++dy)
+            for (int dx = -r; dx <= r; ++dx) {
+              const int v = src(x + dx, y + dy);
+              sum += v;
+              sq += v * v;
+            }
+          sgr_ab(sum, sq, r, eps, &A[(size_t)i * aw + j], &B[(size_t)i * aw + j]);
+        }
+      int32_t* F = pass ? f1 : f0;
+      for (int y = y0; y < y1; ++y)
+        for (int x = 0; x < w; ++x) {
+          const size_t c = (size_t)(y - y0 + 1) * aw + x + 1;
+          F[(size_t)y * w + x] = sgr_output(
+              pass, y, cdef[(size_t)y * w + x], [&](int dy, int dx) { return A[c + dy * aw + dx]; },
+              [&](int dy, int dx) { return B[c + dy * aw + dx]; });
+        }
+    }
+  }
+}
+
+void lr_apply(const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, const int* params, uint8_t* out) {
+  const int ux = lr_count_units(w), uy = lr_count_units(h);
+  std::vector<int> sets;
+  for (int u = 0; u < ux * uy; ++u)
+    if (params[3 * u] >= 0 && std::find(sets.begin(), sets.end(), params[3 * u]) == sets.end())
+      sets.push_back(params[3 * u]);
+  std::memcpy(out, cdef, (size_t)w * h);
+  std::vector<int32_t> f0((size_t)w * h), f1((size_t)w * h);
+  for (int set : sets) {
+    sgr_flt(cdef, dbk, w, h, ss, set, f0.data(), f1.data());
+    const int r0 = sgr_param(set, 0), r1 = sgr_param(set, 2);
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        const int* p = params + 3 * (lr_unit_row(y, h, ss) * ux + lr_unit_col(x, w));
+        if (p[0] != set) continue;
+        const size_t i = (size_t)y * w + x;
+        out[i] = (uint8_t)sgr_project_xqd(cdef[i], f0[i], f1[i], r0, r1, p[1], p[2]);
+      }
+  }
+}
+
+void lr_stats(const uint8_t* src, const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, int set,
+              int64_t* stats) {
+  const int ux = lr_count_units(w), uy = lr_count_units(h);
+  std::vector<int32_t> f0((size_t)w * h), f1((size_t)w * h);
+  sgr_flt(cdef, dbk, w, h, ss, set, f0.data(), f1.data());
+  std::memset(stats, 0, sizeof(int64_t) * 5 * ux * uy);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const size_t i = (size_t)y * w + x;
+      const int u = (int)cdef[i] << kSgrRstBits;
+      const int64_t a = f0[i] - u, b = f1[i] - u;
+      const int64_t e = (((int64_t)src[i] << kSgrRstBits) - u) << kSgrPrjBits;
+      int64_t* S = stats + 5 * (lr_unit_row(y, h, ss) * ux + lr_unit_col(x, w));
+      S[0] += a * a;
+      S[1] += a * b;
+      S[2] += b * b;
+      S[3] += a * e;
+      S[4] += b * e;
+    }
+}
+
 // ================================================================== range coder ======
 
 // ---------------------------------------------------------------- deblocking loop filter ----

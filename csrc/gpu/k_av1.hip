@@ -168,9 +168,12 @@ __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__
       const int bk = blist[q / ppb], pq = q - (q / ppb) * ppb;
       const int i = (bk >> 3) * bsz + pq / bsz, j = (bk & 7) * bsz + (pq & (bsz - 1)), x = x0 + j, y = y0 + i;
       const long kb = (long)b * luma_n8 + (y >> bs_l2) * luma_w8 + (x >> bs_l2);
-      const int d = dir[kb], vr = chroma ? 0 : var[kb];
+      const int d0 = dir[kb], d = d0 & 7, vr = chroma ? 0 : var[kb];
+      const bool skip = d0 & kCdefSkipBlock;
       const int ty = i + kHalo, tx = j + kHalo, c = T[ty][tx];
-      int P[2][2], Sd[2][2][2];
+      // taps along the block direction, plus the secondary taps of direction 0 (presets
+      // whose primary strength is 0 filter along directions 2 / 6: cdef_dir_used)
+      int P[2][2], Sd[2][2][2], S0[2][2][2];
 #pragma unroll
       for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -179,8 +182,9 @@ __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__
           P[k][sg] = T[ty + m * cdef_dir_dy(d, k)][tx + m * cdef_dir_dx(d, k)];
 #pragma unroll
           for (int o = 0; o < 2; ++o) {
-            const int d2 = (d + (o ? 2 : -2)) & 7;
+            const int d2 = (d + (o ? 2 : -2)) & 7, z2 = o ? 2 : 6;
             Sd[k][sg][o] = T[ty + m * cdef_dir_dy(d2, k)][tx + m * cdef_dir_dx(d2, k)];
+            S0[k][sg][o] = T[ty + m * cdef_dir_dy(z2, k)][tx + m * cdef_dir_dx(z2, k)];
           }
         }
       const int e0 = (int)src[po + (long)y * w + x];
@@ -190,7 +194,7 @@ __global__ void __launch_bounds__(256) k_cdef_search(const uint8_t* __restrict__
         const int pp = plist[c0 + k];
         const int psec = cdef_sec_value(pp & 3), ppri = pp >> 2;
         const int pri = chroma ? ppri : cdef_adjust_strength(ppri, vr);
-        const int f = (pri | psec) ? cdef_eval(c, P, Sd, pri, psec, dmp) : c;
+        const int f = (!skip && (pri | psec)) ? cdef_eval(c, P, ppri ? Sd : S0, pri, psec, dmp) : c;
         const int e = f - e0;
         a16[k] += (unsigned)(e * e);
       }
@@ -225,13 +229,15 @@ __global__ void __launch_bounds__(256) k_cdef_apply(const uint8_t* __restrict__ 
   for (int q = threadIdx.x; q < fbw * fbh; q += blockDim.x) {
     const int i = q / fbw, j = q - i * fbw, x = x0 + j, y = y0 + i;
     const long k = (long)b * luma_n8 + (y >> bs_l2) * luma_w8 + (x >> bs_l2);
+    const int d0 = dir[k];
     int pri = 0, sec = 0;
-    if (p >= 0) {
+    if (p >= 0 && !(d0 & kCdefSkipBlock)) {
       sec = cdef_sec_value(p & 3);
       pri = chroma ? (p >> 2) : cdef_adjust_strength(p >> 2, var[k]);
     }
-    out[po + (long)y * w + x] =
-        (uint8_t)((pri | sec) ? cdef_tile_filter(T, i + kHalo, j + kHalo, pri, sec, dmp, dir[k]) : T[i + kHalo][j + kHalo]);
+    out[po + (long)y * w + x] = (uint8_t)((pri | sec) ? cdef_tile_filter(T, i + kHalo, j + kHalo, pri, sec, dmp,
+                                                                         cdef_dir_used(p, d0))
+                                                       : T[i + kHalo][j + kHalo]);
   }
 }
 

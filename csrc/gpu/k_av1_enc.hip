@@ -8,7 +8,7 @@
 //                  alignbyte-unaligned LDS rows, half- then quarter-pel refinement (4
 //                  candidates x 16 4x4-SATD lanes per pass, 16-lane DPP reductions),
 //                  luma / chroma prediction, forward transform, quantisation,
-//                  dequantisation, inverse transform and reconstruction.
+//                  dequantisation, the specification's inverse transform, reconstruction.
 //   k_av1e_intra   one wave per 16x16 block of an anti-diagonal (key frames): the seven
 //                  candidate modes read no above-right samples, so the frame is a plain
 //                  (rows + cols - 1)-step wavefront; 4 luma modes x 16 lanes per pass, all
@@ -26,6 +26,7 @@
 #include "mfma_exact.h"
 #include "tv/av1_defs.h"
 #include "tv/av1_enc.h"
+#include "tv/av1_itx.h"
 #include "tv/av1_txfm.h"
 
 namespace tv {
@@ -126,9 +127,11 @@ __device__ void wave_txfm(const int16_t* in, int16_t* tmp, int16_t* out, int tco
 
 // Residual coding of one TB held in LDS: res (int16, src - pred) -> levels (global),
 // reconstruction added onto pred (int, LDS) -> returns 1 if any level is nonzero.
-// Scratch a/b: LDS int16 [N*N] each.
+// Scratch a/b: LDS int16 [N*N] each; ti: LDS int32 [N*N].  Forward: the basis-matrix
+// transform (MFMA for 16x16); inverse: the specification's 2-D process (tv/av1_itx.h), one
+// lane per row, then one lane per column.
 template <int LG>
-__device__ int code_tb(int16_t* res, int16_t* a, int16_t* b, int tcol, int trow, int qidx, int rnd,
+__device__ int code_tb(int16_t* res, int16_t* a, int16_t* b, int32_t* ti, int tcol, int trow, int qidx, int rnd,
                        int16_t* __restrict__ lev_out) {
   constexpr int N = 1 << LG;
   const int lane = threadIdx.x & 63;
@@ -144,7 +147,22 @@ __device__ int code_tb(int16_t* res, int16_t* a, int16_t* b, int tcol, int trow,
   const bool any = __any(nz);
   __syncthreads();
   if (any) {
-    wave_txfm<LG>(a, b, res, tcol, trow, true);  // residual back in res
+    if (lane < N) {
+      int32_t in[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) in[j] = a[lane * N + j];
+      inv_row<LG>(in, trow, ti + lane * N);
+    }
+    __syncthreads();
+    if (lane < N) {
+      int32_t t[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) t[i] = ti[i * N + lane];
+      inv_col<LG>(t, tcol);
+#pragma unroll
+      for (int i = 0; i < N; ++i) res[i * N + lane] = (int16_t)t[i];
+    }
+    __syncthreads();
   } else {
     for (int i = lane; i < N * N; i += 64) res[i] = 0;
     __syncthreads();
@@ -171,6 +189,7 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   __shared__ int cost[9];
   int lastk = 1;
   __shared__ int16_t res[256], ta[256], tb[256];
+  __shared__ int32_t ti[256];
   __shared__ int predc[256];
   int blk, b;
   xcd_ctb(blk, b);
@@ -352,7 +371,7 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   __syncthreads();
   const int nb = bw * (H >> 4);
   const long bo = (long)b * nb + blk;
-  int nz = code_tb<4>(res, ta, tb, 0, 0, qidx, kRndInter, ly + bo * 256);
+  int nz = code_tb<4>(res, ta, tb, ti, 0, 0, qidx, kRndInter, ly + bo * 256);
   for (int i = lane; i < 256; i += 64)
     rec.y[b * ysz + (long)(y0 + (i >> 4)) * W + x0 + (i & 15)] = (uint8_t)clip_pixel(predc[i] + res[i]);
   __syncthreads();
@@ -371,7 +390,7 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
     }
     __syncthreads();
     int16_t* lo = (pl == 1 ? lu : lv) + bo * 64;
-    if (code_tb<3>(res, ta, tb, 0, 0, qidx, kRndInter, lo)) nz |= 1 << pl;
+    if (code_tb<3>(res, ta, tb, ti, 0, 0, qidx, kRndInter, lo)) nz |= 1 << pl;
     uint8_t* Rw = (pl == 1 ? rec.u : rec.v) + b * csz;
     Rw[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)] = (uint8_t)clip_pixel(predc[lane] + res[lane]);
     __syncthreads();
@@ -426,6 +445,7 @@ __global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, ui
   __shared__ uint8_t sc[2][64];
   __shared__ int cost[8];
   __shared__ int16_t res[256], ta[256], tb[256];
+  __shared__ int32_t ti[256];
   __shared__ int predc[256];
   const int lane = threadIdx.x, b = blockIdx.y, qidx = qarr[b];
   const int bw = W >> 4, bx = bx_lo + blockIdx.x, by = diag - bx, x0 = bx * 16, y0 = by * 16;
@@ -467,7 +487,7 @@ __global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, ui
   __syncthreads();
   const int nb = bw * (H >> 4), blk = by * bw + bx;
   const long bo = (long)b * nb + blk;
-  int nz = code_tb<4>(res, ta, tb, 0, 0, qidx, kRndIntra, ly + bo * 256);
+  int nz = code_tb<4>(res, ta, tb, ti, 0, 0, qidx, kRndIntra, ly + bo * 256);
   for (int i = lane; i < 256; i += 64)
     RY[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)] = (uint8_t)clip_pixel(predc[i] + res[i]);
   __syncthreads();
@@ -503,7 +523,7 @@ __global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, ui
     res[lane] = (int16_t)((int)sc[pl][lane] - p);
     __syncthreads();
     int16_t* lo = (pl == 0 ? lu : lv) + bo * 64;
-    if (code_tb<3>(res, ta, tb, txt & 1, (txt >> 1) & 1, qidx, kRndIntra, lo)) nz |= 2 << pl;
+    if (code_tb<3>(res, ta, tb, ti, txt & 1, (txt >> 1) & 1, qidx, kRndIntra, lo)) nz |= 2 << pl;
     uint8_t* Rw = pl == 0 ? RU : RV;
     Rw[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)] = (uint8_t)clip_pixel(predc[lane] + res[lane]);
   }
@@ -529,6 +549,17 @@ __global__ void k_av1e_lfinfo(const uint32_t* __restrict__ mode, int W, int H, c
     iu[cu] = lf_word(true, lv2, lv2, si, bz);
     iv[cu] = lf_word(true, lv3, lv3, si, bz);
   }
+}
+
+// ================================================================= CDEF skip flags =======
+// one thread per 8x8 luma block: flag the blocks of skip blocks in the direction array
+// (kCdefSkipBlock: 7.15 cdef_block filters no 8x8 whose 4x4 units are all skip)
+__global__ void k_av1e_cdef_skip(const uint32_t* __restrict__ mode, uint8_t* __restrict__ dir, int W, int H) {
+  const int b = blockIdx.y, w8 = W >> 3, n8 = w8 * (H >> 3), bw = W >> 4, nb = bw * (H >> 4);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const int y = i / w8, x = i - y * w8;
+  if (mode_skip(mode[(long)b * nb + (y >> 1) * bw + (x >> 1)])) dir[(long)b * n8 + i] |= (uint8_t)kCdefSkipBlock;
 }
 
 // ================================================================= skip-block merging ===
@@ -805,6 +836,14 @@ int tv_av1e_intra(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, uint8
                                                                        mode, mv, ly, lu, lv, W, H, qarr, d, lo);
   }
   return status("av1e_intra");
+}
+
+// flag the 8x8 blocks of skip blocks in dir [B][n8] (after tv_gpu_cdef_dirs)
+int tv_av1e_cdef_skip(const uint32_t* mode, uint8_t* dir, int W, int H, int B, void* stream) {
+  if (bad(W, H, B, 1, "av1e_cdef_skip")) return -1;
+  const int n8 = (W >> 3) * (H >> 3);
+  k_av1e_cdef_skip<<<dim3((n8 + 255) / 256, B), 256, 0, (hipStream_t)stream>>>(mode, dir, W, H);
+  return status("av1e_cdef_skip");
 }
 
 // skip-block merging of a P frame's decisions (before lfinfo / deblocking)

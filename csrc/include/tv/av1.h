@@ -43,6 +43,17 @@ void sgr_stats(const uint8_t* src, const uint8_t* rec, int w, int h, int set, in
 // The two guided-filter outputs (RST domain) of one plane, for tests / the GPU check.
 void sgr_filter_planes(const uint8_t* rec, int w, int h, int set, int32_t* f0, int32_t* f1);
 
+// ---- normative self-guided restoration (AV1 7.17; 64x64 units, 4:2:0) ----------------------
+// One plane w x h (ss: 0 luma, 1 chroma): cdef = CDEF output, dbk = deblocked pre-CDEF
+// plane (the rows beyond a stripe come from it).  Units follow av1_defs.h lr_count_units.
+// F0 / F1 (RST domain) of parameter set `set` for every pixel.
+void sgr_flt(const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, int set, int32_t* f0, int32_t* f1);
+// restore with per-unit (set | -1, xqd0, xqd1), units row-major
+void lr_apply(const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, const int* params, uint8_t* out);
+// per-unit normal equations [units][5] = H00 H01 H11 c0 c1 of parameter set `set`
+void lr_stats(const uint8_t* src, const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, int set,
+              int64_t* stats);
+
 // ---- deblocking loop filter (AV1 7.14) -------------------------------------------------
 // Filter every tx edge of a plane: `info` holds one word per 4x4 unit (layout in
 // av1_defs.h: tx / block log2 sizes, per-direction levels, skip && inter); sharp 0..7.

@@ -19,9 +19,9 @@ struct SeqGeo {
   int sbw, sbh;
   int nblk() const { return bw * bh; }
   int nsb() const { return sbw * sbh; }
-  // 64x64 restoration units of plane p (ceil layout; plane 0 has the most)
-  int lr_ux(int p) const { return ((p ? W / 2 : W) + 63) / 64; }
-  int lr_uy(int p) const { return ((p ? H / 2 : H) + 63) / 64; }
+  // 64x64 restoration units of plane p (7.17 count_units_in_frame; plane 0 has the most)
+  int lr_ux(int p) const { int n = ((p ? W / 2 : W) + 32) / 64; return n > 1 ? n : 1; }
+  int lr_uy(int p) const { int n = ((p ? H / 2 : H) + 32) / 64; return n > 1 ? n : 1; }
   int lr_nu() const { return lr_ux(0) * lr_uy(0); }
 };
 SeqGeo make_seq_geo(int dw, int dh);

@@ -172,7 +172,7 @@ TV_HD int wiener_v(const int* col /* 7 intermediates, stride cs */, int cs, cons
   return clip3(0, 255, (s + (1 << (kRound1 - 1))) >> kRound1);
 }
 
-// Self-guided restoration: parameter sets {r0, e0, r1, e1}.
+// Self-guided restoration: parameter sets {r0, s0, r1, s1} (radius, scale of each pass).
 TV_HD int sgr_param(int set, int k) {
   constexpr int16_t t[16][4] = {{2, 140, 1, 3236}, {2, 112, 1, 2158}, {2, 93, 1, 1618}, {2, 80, 1, 1438},
                                 {2, 70, 1, 1295},  {2, 58, 1, 1177},  {2, 47, 1, 1079}, {2, 37, 1, 996},
@@ -190,11 +190,12 @@ TV_HD int sgr_xbyx1(unsigned z) {
 }
 // (a, b) guide coefficients of one pixel from its (2r+1)^2 box sum / square sum; `xb(z)`
 // evaluates sgr_xbyx1 (the GPU passes a lookup in an LDS table of it)
+// `s` is the parameter set's scale (the Sgr_Params entry next to the radius: the table holds
+// the scale factor itself, not an epsilon)
 template <class XB>
-TV_HD void sgr_ab_x(int sum, int sq, int r, int eps, XB xb, int* A, int* B) {
+TV_HD void sgr_ab_x(int sum, int sq, int r, int s_param, XB xb, int* A, int* B) {
   const int n = (2 * r + 1) * (2 * r + 1);
-  const int n2e = n * n * eps;
-  const unsigned s = ((1u << kSgrMtableBits) + (unsigned)(n2e / 2)) / (unsigned)n2e;
+  const unsigned s = (unsigned)s_param;
   const long long p0 = (long long)sq * n - (long long)sum * sum;
   const unsigned p = p0 > 0 ? (unsigned)p0 : 0u;
   const unsigned z = (unsigned)(((unsigned long long)p * s + (1u << (kSgrMtableBits - 1))) >> kSgrMtableBits);
@@ -209,7 +210,7 @@ TV_HD void sgr_ab_x(int sum, int sq, int r, int eps, XB xb, int* A, int* B) {
 struct SgrXbDiv {
   TV_HD int operator()(unsigned z) const { return sgr_xbyx1(z); }
 };
-TV_HD void sgr_ab(int sum, int sq, int r, int eps, int* A, int* B) { sgr_ab_x(sum, sq, r, eps, SgrXbDiv{}, A, B); }
+TV_HD void sgr_ab(int sum, int sq, int r, int s, int* A, int* B) { sgr_ab_x(sum, sq, r, s, SgrXbDiv{}, A, B); }
 
 // projection of the two guided outputs (flt = filtered << RST_BITS domain) onto the pixel
 TV_HD int sgr_project(int x, int f0, int f1, int r0, int r1, int w0, int w1) {
@@ -221,6 +222,89 @@ TV_HD int sgr_project(int x, int f0, int f1, int r0, int r1, int w0, int w1) {
   return clip3(0, 255, (v + (1 << (s - 1))) >> s);
 }
 
+
+// ------------------------------------------------ normative self-guided restoration ----
+// 7.17 with 64x64 restoration units (lr_unit_shift 0, lr_uv_shift 0) and 4:2:0 chroma
+// (ss = 1): units are counted with rounding (the last row / column of units absorbs up to
+// half a unit), unit rows are offset 8 luma rows up, and the filters read the CDEF output
+// inside the current 64-luma-row stripe (also offset by 8) and up to 2 rows of the
+// deblocked, pre-CDEF frame beyond it.
+TV_HD int lr_count_units(int size) { int n = (size + 32) / 64; return n > 1 ? n : 1; }
+TV_HD int lr_unit_row(int y, int h, int ss) {
+  const int r = (y + (8 >> ss)) / 64, n = lr_count_units(h);
+  return r < n ? r : n - 1;
+}
+TV_HD int lr_unit_col(int x, int w) {
+  const int c = x / 64, n = lr_count_units(w);
+  return c < n ? c : n - 1;
+}
+// rows [y0, y1) of unit row ur / columns [x0, x1) of unit column uc
+TV_HD void lr_unit_rows(int ur, int h, int ss, int* y0, int* y1) {
+  const int off = 8 >> ss, n = lr_count_units(h);
+  *y0 = ur ? ur * 64 - off : 0;
+  *y1 = ur == n - 1 ? h : (ur + 1) * 64 - off;
+}
+TV_HD void lr_unit_cols(int uc, int w, int* x0, int* x1) {
+  *x0 = uc * 64;
+  *x1 = uc == lr_count_units(w) - 1 ? w : (uc + 1) * 64;
+}
+// stripe of row y: first row StripeStartY and last row StripeEndY (may lie outside the plane)
+TV_HD int lr_stripe_start(int y, int ss) {
+  const int S = 64 >> ss, off = 8 >> ss;
+  return ((y + off) / S) * S - off;
+}
+// get_source_sample: the plane row that feeds (x, y) of the stripe [s0, s0 + S) and whether
+// it comes from the deblocked (pre-CDEF) frame
+TV_HD int lr_src_row(int y, int h, int s0, int ss, bool* dbk) {
+  const int s1 = s0 + (64 >> ss) - 1;
+  y = clip3(0, h - 1, y);
+  *dbk = false;
+  if (y < s0) {
+    *dbk = true;
+    return y > s0 - 2 ? y : s0 - 2;
+  }
+  if (y > s1) {
+    *dbk = true;
+    return y < s1 + 2 ? y : s1 + 2;
+  }
+  return y;
+}
+// guided-filter output of pixel (row y, value c) from the 3x3 (A, B) neighbourhood (pass 0:
+// radius-2 filter, (A, B) used on odd rows only; pass 1: radius 1, all rows).  getA(dy, dx)
+// / getB(dy, dx) read the neighbour's coefficients.
+template <class GA, class GB>
+TV_HD int sgr_output(int pass, int y, int c, GA getA, GB getB) {
+  int a = 0, b = 0, shift = 5;
+  if (pass == 0) {
+    if (y & 1) shift = 4;
+    for (int dy = -1; dy <= 1; ++dy) {
+      if (!((y + dy) & 1)) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int wt = dx == 0 ? 6 : 5;
+        a += wt * getA(dy, dx);
+        b += wt * getB(dy, dx);
+      }
+    }
+  } else {
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int wt = (dy == 0 || dx == 0) ? 4 : 3;
+        a += wt * getA(dy, dx);
+        b += wt * getB(dy, dx);
+      }
+  }
+  const int s = kSgrSgrBits + shift - kSgrRstBits;
+  return (a * c + b + (1 << (s - 1))) >> s;
+}
+// projection with the coded weights (7.17.? self guided filter process): w0 = xqd0 weights
+// F0, w1 = xqd1 weights the CDEF sample u, w2 = 128 - w0 - w1 weights F1 (a radius-0 pass
+// contributes u instead)
+TV_HD int sgr_project_xqd(int x, int f0, int f1, int r0, int r1, int xqd0, int xqd1) {
+  const int u = x << kSgrRstBits, w2 = (1 << kSgrPrjBits) - xqd0 - xqd1;
+  const int v = xqd1 * u + xqd0 * (r0 ? f0 : u) + w2 * (r1 ? f1 : u);
+  const int s = kSgrRstBits + kSgrPrjBits;
+  return clip3(0, 255, (v + (1 << (s - 1))) >> s);
+}
 
 // ------------------------------------------------------------ deblocking loop filter ----
 // One 32-bit info word per 4x4 unit of a plane (row-major, w/4 per row):

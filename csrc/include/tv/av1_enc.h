@@ -278,9 +278,13 @@ TV_HD int bitlen64(unsigned long long v) {
   return n;
 }
 TV_HD long long div_round(long long n, long long d) { return n >= 0 ? (n + d / 2) / d : -((-n + d / 2) / d); }
-// (x0, x1) of a unit from its sgr_stats (H00 H01 H11 c0 c1): stats scaled below 2^30 so the
-// 2x2 Cramer solve stays in 64 bits; radius-0 passes get the syntax's implied values.
-TV_HD void sgr_solve(const long long* st, int r0, int r1, int* x0, int* x1) {
+// Coded weights (xqd0, xqd1) of a unit from its sgr_stats (H00 H01 H11 c0 c1: normal
+// equations of the weights a, b of F0 - u and F1 - u, 1/128 units).  The decoder applies
+// a to F0, 128 - xqd0 - xqd1 to F1 and xqd1 to u (sgr_project_xqd), so xqd0 = a and
+// xqd1 = 128 - a - b, each clamped to its coded range (one weight clamped, the other
+// re-solved given it); radius-0 passes get the syntax's implied values.  Stats are scaled
+// below 2^30 so the 2x2 Cramer solve stays in 64 bits.
+TV_HD void sgr_solve(const long long* st, int r0, int r1, int* xqd0, int* xqd1) {
   unsigned long long m = 0;
   for (int i = 0; i < 5; ++i) {
     const unsigned long long a = (unsigned long long)(st[i] < 0 ? -st[i] : st[i]);
@@ -296,21 +300,22 @@ TV_HD void sgr_solve(const long long* st, int r0, int r1, int* x0, int* x1) {
       a = div_round(c0 * H11 - c1 * H01, det);
       b = div_round(H00 * c1 - H01 * c0, det);
     }
-    // outside the coded range: clamp one weight and re-solve the other given it
     if (a < kXqdMin0 || a > kXqdMax0) {
       a = clip3((long long)kXqdMin0, (long long)kXqdMax0, a);
       b = div_round(c1 - H01 * a, H11);
-    } else if (b < kXqdMin1 || b > kXqdMax1) {
-      b = clip3((long long)kXqdMin1, (long long)kXqdMax1, b);
-      a = div_round(c0 - H01 * b, H00);
+    } else if (b < 128 - kXqdMax1 - a || b > 128 - kXqdMin1 - a) {
+      b = clip3(128 - kXqdMax1 - a, 128 - kXqdMin1 - a, b);
+      a = clip3((long long)kXqdMin0, (long long)kXqdMax0, div_round(c0 - H01 * b, H00));
     }
+    *xqd0 = (int)a;
+    *xqd1 = (int)clip3((long long)kXqdMin1, (long long)kXqdMax1, 128 - a - b);
   } else if (r0) {
-    a = div_round(c0, H00);
+    *xqd0 = (int)clip3((long long)kXqdMin0, (long long)kXqdMax0, div_round(c0, H00));
+    *xqd1 = clip3(kXqdMin1, kXqdMax1, 128 - *xqd0);
   } else {
-    b = div_round(c1, H11);
+    *xqd0 = 0;
+    *xqd1 = (int)clip3((long long)kXqdMin1, (long long)kXqdMax1, 128 - div_round(c1, H11));
   }
-  *x0 = r0 ? (int)clip3((long long)kXqdMin0, (long long)kXqdMax0, a) : 0;
-  *x1 = r1 ? (int)clip3((long long)kXqdMin1, (long long)kXqdMax1, b) : clip3(kXqdMin1, kXqdMax1, 128 - *x0);
 }
 // rate of a restored unit (~16 bits) in SSE units
 TV_HD long long lr_rate_cost(int q) {

@@ -98,27 +98,29 @@ TV_HD void idct_odd(int32_t* o, int n, Range c) {
   }
 }
 
-// permuted input -> output (recursion over the even half)
+// N-point DCT of a bit-reversal-permuted array: the 2-point core, then for every size
+// 4, 8, .. N the odd half of that size and its output butterfly (the recursion over the
+// even half, unrolled bottom-up)
 TV_HD void idct_core(int32_t* t, int n, Range c) {
-  if (n == 1) {
+  {
     const int32_t a = t[0], b = t[1];
     t[0] = hbtf(2896, a, 2896, b);
     t[1] = hbtf(2896, a, -2896, b);
-    return;
   }
-  const int N = 1 << n;
-  idct_core(t, n - 1, c);
-  idct_odd(t + N / 2, n, c);
-  for (int i = 0; i < N / 2; ++i) {
-    const int32_t a = t[i], b = t[N - 1 - i];
-    t[i] = c((int64_t)a + b);
-    t[N - 1 - i] = c((int64_t)a - b);
+  for (int m = 2; m <= n; ++m) {
+    const int M = 1 << m;
+    idct_odd(t + M / 2, m, c);
+    for (int i = 0; i < M / 2; ++i) {
+      const int32_t a = t[i], b = t[M - 1 - i];
+      t[i] = c((int64_t)a + b);
+      t[M - 1 - i] = c((int64_t)a - b);
+    }
   }
 }
 
-TV_HD void idct(int32_t* t, int n, Range c) {
-  int32_t p[64];
-  const int N = 1 << n;
+template <int n> TV_HD void idct(int32_t* t, Range c) {
+  constexpr int N = 1 << n;
+  int32_t p[N];
   for (int i = 0; i < N; ++i) p[i] = t[brev(n, i)];
   idct_core(p, n, c);
   for (int i = 0; i < N; ++i) t[i] = p[i];
@@ -223,8 +225,8 @@ TV_HD void iadst16(int32_t* t, Range c) {
   t[12] = a[5], t[13] = -a[13], t[14] = a[9], t[15] = -a[1];
 }
 
-TV_HD void iidentity(int32_t* t, int n) {
-  const int N = 1 << n;
+template <int n> TV_HD void iidentity(int32_t* t) {
+  constexpr int N = 1 << n;
   for (int i = 0; i < N; ++i) {
     const int64_t v = t[i];
     t[i] = n == 2 ? (int32_t)((v * 5793 + 2048) >> 12)
@@ -235,46 +237,69 @@ TV_HD void iidentity(int32_t* t, int n) {
 }
 
 // 1-D inverse of type (0 DCT, 1 ADST, 3 IDTX; tv::av1::TxType1D) on T[0..2^n)
-TV_HD void inv_1d(int32_t* t, int n, int type, Range c) {
-  if (type == 3) iidentity(t, n);
-  else if (type == 1) {
-    if (n == 2) iadst4(t);
-    else if (n == 3) iadst8(t, c);
-    else iadst16(t, c);
-  } else {
-    idct(t, n, c);
-  }
+template <int n> TV_HD void inv_1d(int32_t* t, int type, Range c) {
+  if (type == 3) iidentity<n>(t);
+  else if (type == 1 && n == 2) iadst4(t);
+  else if (type == 1 && n == 3) iadst8(t, c);
+  else if (type == 1 && n == 4) iadst16(t, c);
+  else idct<n>(t, c);
 }
 
 // Transform_Row_Shift of the square sizes (log2 N = 2..6)
-TV_HD int row_shift(int lg) { return lg == 2 ? 0 : (lg == 3 ? 1 : 2); }
+TV_HD constexpr int row_shift(int lg) { return lg == 2 ? 0 : (lg == 3 ? 1 : 2); }
+constexpr int32_t kRowLo = -(1 << 15), kRowHi = (1 << 15) - 1;  // BitDepth + 8
+constexpr int32_t kColLo = -(1 << 15), kColHi = (1 << 15) - 1;  // Max(BitDepth + 6, 16)
+
+// One row of the 2-D inverse transform (7.13.3): dequantised coefficients in[0..N) ->
+// the row transform, Round2(.., rowShift), clamped to the column range.  Row i >= 32 of a
+// 64-point transform and all-zero rows stay zero.
+template <int lg> TV_HD void inv_row(const int32_t* in, int trow, int32_t* out) {
+  constexpr int N = 1 << lg, nz = N < 32 ? N : 32, rs = row_shift(lg);
+  const Range rr{kRowLo, kRowHi}, cr{kColLo, kColHi};
+  int32_t t[N];
+  bool any = false;
+  for (int j = 0; j < N; ++j) {
+    t[j] = j < nz ? rr(in[j]) : 0;
+    any |= t[j] != 0;
+  }
+  if (!any) {
+    for (int j = 0; j < N; ++j) out[j] = 0;
+    return;
+  }
+  inv_1d<lg>(t, trow, rr);
+  for (int j = 0; j < N; ++j) out[j] = cr(((int64_t)t[j] + ((1 << rs) >> 1)) >> rs);
+}
+// One column: the column transform and Round2(.., 4) (colShift, 8-bit).
+template <int lg> TV_HD void inv_col(int32_t* t, int tcol) {
+  constexpr int N = 1 << lg;
+  inv_1d<lg>(t, tcol, Range{kColLo, kColHi});
+  for (int i = 0; i < N; ++i) t[i] = (t[i] + 8) >> 4;
+}
 
 // 2-D inverse transform process (7.13.3) of an N x N block, 8-bit: `coef` are the
 // dequantised coefficients in raster order (row i = vertical frequency), `res` the
 // residual.  tcol / trow: 1-D types of the columns (vertical) and rows (horizontal).
-// Only the top-left min(N, 32)^2 coefficients may be nonzero.
-TV_HD void inv_txfm2d(const int32_t* coef, int lg, int tcol, int trow, int32_t* res) {
-  const int N = 1 << lg, nz = N < 32 ? N : 32, rs = row_shift(lg);
-  const Range rr{-(1 << 15), (1 << 15) - 1};   // BitDepth + 8
-  const Range cr{-(1 << 15), (1 << 15) - 1};   // Max(BitDepth + 6, 16)
-  int32_t t[64];
+template <int lg> TV_HD void inv_txfm2d(const int32_t* coef, int tcol, int trow, int32_t* res) {
+  constexpr int N = 1 << lg, nz = N < 32 ? N : 32;
   for (int i = 0; i < N; ++i) {
-    if (i >= nz) {
+    if (i < nz) inv_row<lg>(coef + i * N, trow, res + i * N);
+    else
       for (int j = 0; j < N; ++j) res[i * N + j] = 0;
-      continue;
-    }
-    bool any = false;
-    for (int j = 0; j < N; ++j) {
-      t[j] = j < nz ? rr(coef[i * N + j]) : 0;
-      any |= t[j] != 0;
-    }
-    if (any) inv_1d(t, lg, trow, rr);
-    for (int j = 0; j < N; ++j) res[i * N + j] = cr(any ? (((int64_t)t[j] + ((1 << rs) >> 1)) >> rs) : 0);
   }
+  int32_t t[N];
   for (int j = 0; j < N; ++j) {
     for (int i = 0; i < N; ++i) t[i] = res[i * N + j];
-    inv_1d(t, lg, tcol, cr);
-    for (int i = 0; i < N; ++i) res[i * N + j] = (t[i] + 8) >> 4;
+    inv_col<lg>(t, tcol);
+    for (int i = 0; i < N; ++i) res[i * N + j] = t[i];
+  }
+}
+inline void inv_txfm2d(const int32_t* coef, int lg, int tcol, int trow, int32_t* res) {
+  switch (lg) {
+    case 2: inv_txfm2d<2>(coef, tcol, trow, res); break;
+    case 3: inv_txfm2d<3>(coef, tcol, trow, res); break;
+    case 4: inv_txfm2d<4>(coef, tcol, trow, res); break;
+    case 5: inv_txfm2d<5>(coef, tcol, trow, res); break;
+    default: inv_txfm2d<6>(coef, tcol, trow, res); break;
   }
 }
 
