@@ -1953,6 +1953,9 @@ extern "C" {
 using namespace tv::av1;
 const char* tv_av1c_last_error() { return g_codec_err.c_str(); }
 
+// Dc_Qlookup / Ac_Qlookup (8-bit) of q-index q (dc != 0: the DC table)
+int tv_av1c_qlookup(int q, int dc) { return dc ? dc_q(q) : ac_q(q); }
+
 // Golden encode of n coded-size I420 frames (concatenated Y U V per frame) at `qidx`:
 // the temporal units go to `out` (one Bytes object) and their byte sizes to tu_sizes[n];
 // the post-filter reconstructions to recon (same layout); per-frame decisions to mode /

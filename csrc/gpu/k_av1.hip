@@ -520,24 +520,83 @@ __global__ void __launch_bounds__(256) k_sgr_search(const uint8_t* __restrict__ 
   if (threadIdx.x == 0) sse[(long)b * nu + u] = (long long)red[5];
 }
 
-// Encoder restoration choice per unit, fused over the candidate sets: the unit's SSE left
-// unrestored, then for each set of lr_set() the guided filters -> projection statistics ->
-// sgr_solve -> projection + SSE with the outputs kept in registers; the first minimum of
-// SSE + rate (rate[b] = lr_rate_cost of segment b's q-index, 0 when unrestored) is written
-// with its parameters (set | -1, xqd0, xqd1).  The golden encoder's decision (av1_codec.cpp)
-// in one launch: one tile staging and one source read per unit instead of one per set plus
-// the unit-SSE and per-set select passes.
-__global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ src, const uint8_t* __restrict__ rec,
-                                                    int w, int h, const long long* __restrict__ rate,
-                                                    int* __restrict__ prm, uint8_t* __restrict__ out) {
-  const int b = blockIdx.y, u = blockIdx.x, nux = (w + kRu - 1) / kRu, nu = nux * ((h + kRu - 1) / kRu);
-  const int ux = (u % nux) * kRu, uy = (u / nux) * kRu, uw = min(kRu, w - ux), uh = min(kRu, h - uy);
-  const long po = (long)b * w * h;
-  __shared__ uint8_t T[kLrTile][kLrTile];
-  __shared__ uint16_t A[kAb][kAb], Bv[kAb][kAb], xt[256];
+// Encoder restoration choice per normative restoration unit (av1_defs.h lr_* geometry; 7.17
+// stripes), fused over the candidate sets: the unit's SSE unrestored, then for each set of
+// lr_set() the guided filters -> projection statistics -> sgr_solve -> projection + SSE; the
+// first minimum of SSE + rate (rate[b] = lr_rate_cost of segment b's q-index, 0 when
+// unrestored) wins.  Per stripe chunk of the unit, the source tile (CDEF output inside the
+// stripe, up to 2 deblocked rows beyond it, clamped at the plane edges) and the (A, B) planes
+// of a pass are staged in LDS; F0 / F1 of the chunk stay in LDS for the statistics and the
+// projection.  Candidate outputs go to cand[k] (scratch); the chosen one to `out`.  The
+// golden encoder's decision (av1_codec.cpp) bit for bit.
+constexpr int kLrCh = 64, kLrUw = 96;  // max stripe chunk height, max unit width (round layout)
+constexpr int kLrTw = kLrUw + 6, kLrAw = kLrUw + 2;
+
+__device__ void lr_chunk_flt(const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, int s0, int ya, int yb,
+                             int x0, int x1, int set, const uint16_t* xt, uint8_t (*T)[kLrTw],
+                             uint16_t (*A)[kLrAw], uint16_t (*Bv)[kLrAw], int16_t (*F)[2][kLrUw]) {
+  const int uw = x1 - x0, ch = yb - ya, th = ch + 6, tw = uw + 6;
+  for (int q = threadIdx.x; q < th * tw; q += blockDim.x) {
+    const int ty = q / tw, tx = q - ty * tw;
+    bool db;
+    const int yy = lr_src_row(ya - 3 + ty, h, s0, ss, &db), xx = clampi(x0 - 3 + tx, 0, w - 1);
+    T[ty][tx] = (db ? dbk : cdef)[(long)yy * w + xx];
+  }
+  __syncthreads();
+  for (int pass = 0; pass < 2; ++pass) {
+    const int r = sgr_param(set, 2 * pass), sp = sgr_param(set, 2 * pass + 1);
+    if (!r) {
+      for (int q = threadIdx.x; q < ch * uw; q += blockDim.x) {
+        const int i = q / uw, j = q - i * uw;
+        F[i][pass][j] = (int16_t)((int)T[i + 3][j + 3] << kSgrRstBits);
+      }
+      continue;
+    }
+    const int ah = ch + 2, aw = uw + 2;
+    for (int q = threadIdx.x; q < ah * aw; q += blockDim.x) {
+      const int i = q / aw, j = q - i * aw;  // position (ya - 1 + i, x0 - 1 + j) = tile (i + 2, j + 2)
+      if (pass == 0 && !((ya - 1 + i) & 1)) continue;  // the radius-2 pass reads odd rows only
+      int sum = 0, sq = 0;
+      for (int dy = -r; dy <= r; ++dy)
+        for (int dx = -r; dx <= r; ++dx) {
+          const int v = T[i + 2 + dy][j + 2 + dx];
+          sum += v;
+          sq += v * v;
+        }
+      int a, bb;
+      sgr_ab_x(sum, sq, r, sp, [&](unsigned z) -> int { return xt[z < 255u ? z : 255u]; }, &a, &bb);
+      A[i][j] = (uint16_t)a;
+      Bv[i][j] = (uint16_t)bb;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < ch * uw; q += blockDim.x) {
+      const int i = q / uw, j = q - i * uw;
+      F[i][pass][j] = (int16_t)sgr_output(
+          pass, ya + i, (int)T[i + 3][j + 3], [&](int dy, int dx) -> int { return A[i + 1 + dy][j + 1 + dx]; },
+          [&](int dy, int dx) -> int { return Bv[i + 1 + dy][j + 1 + dx]; });
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ src, const uint8_t* __restrict__ cdef,
+                                                    const uint8_t* __restrict__ dbk, int w, int h, int ss,
+                                                    const long long* __restrict__ rate, int* __restrict__ prm,
+                                                    uint8_t* __restrict__ cand, uint8_t* __restrict__ out) {
+  const int b = blockIdx.y, u = blockIdx.x, nux = lr_count_units(w);
+  const int ur = u / nux, uc = u - ur * nux, nu = nux * lr_count_units(h);
+  int x0, x1, y0, y1;
+  lr_unit_cols(uc, w, &x0, &x1);
+  lr_unit_rows(ur, h, ss, &y0, &y1);
+  const int uw = x1 - x0, S = 64 >> ss;
+  const long po = (long)b * w * h, psz = (long)gridDim.y * w * h;
+  const uint8_t* C = cdef + po;
+  const uint8_t* D = dbk + po;
+  __shared__ uint8_t T[kLrCh + 6][kLrTw];
+  __shared__ uint16_t A[kLrCh + 2][kLrAw], Bv[kLrCh + 2][kLrAw], xt[256];
+  __shared__ int16_t F[kLrCh][2][kLrUw];
   __shared__ unsigned long long red[1 + 6 * kNumLrSets];
   __shared__ int xq[2];
-  lr_stage(rec + po, w, h, ux, uy, uw, uh, T);
   if (threadIdx.x < 256) xt[threadIdx.x] = (uint16_t)sgr_xbyx1(threadIdx.x);
   if (threadIdx.x < 1 + 6 * kNumLrSets) red[threadIdx.x] = 0;
   __syncthreads();
@@ -545,86 +604,81 @@ __global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ 
     v = wave_sum64(v);
     if ((threadIdx.x & 63) == 0) atomicAdd(&red[slot], (unsigned long long)v);
   };
-  int sv[16], ob[16];
   long long e0 = 0;
-  int n = 0;
-  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+  for (int q = threadIdx.x; q < (y1 - y0) * uw; q += blockDim.x) {
     const int i = q / uw, j = q - i * uw;
-    sv[n] = src[po + (long)(uy + i) * w + ux + j];
-    ob[n] = T[i + kLrHalo][j + kLrHalo];
-    const int d = ob[n] - sv[n];
+    const long o = (long)(y0 + i) * w + x0 + j;
+    const int d = (int)C[o] - (int)src[po + o];
     e0 += d * d;
   }
   block_add(e0, 0);
   __syncthreads();
   long long best = (long long)red[0];
-  int bset = -1, b0 = 0, b1 = 0;
+  int bk = -1, b0 = 0, b1 = 0;
   const long long rt = rate[b];
   for (int k = 0; k < kNumLrSets; ++k) {
     const int set = lr_set(k), r0 = sgr_param(set, 0), r1 = sgr_param(set, 2), sl = 1 + 6 * k;
-    int f0[16], f1[16];
-    n = 0;
-    for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
-      const int i = q / uw, j = q - i * uw;
-      f0[n] = f1[n] = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
-    }
-    if (r0) sgr_guided(T, w, h, ux, uy, uw, uh, r0, sgr_param(set, 1), A, Bv, xt, f0);
-    if (r1) sgr_guided(T, w, h, ux, uy, uw, uh, r1, sgr_param(set, 3), A, Bv, xt, f1);
-    long long a[5] = {0, 0, 0, 0, 0};
-    n = 0;
-    for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
-      const int i = q / uw, j = q - i * uw;
-      const int uu = (int)T[i + kLrHalo][j + kLrHalo] << kSgrRstBits;
-      const long long da = f0[n] - uu, db = f1[n] - uu;
-      const long long e = ((long long)(sv[n] << kSgrRstBits) - uu) << kSgrPrjBits;
-      a[0] += da * da;
-      a[1] += da * db;
-      a[2] += db * db;
-      a[3] += da * e;
-      a[4] += db * e;
-    }
+    for (int sweep = 0; sweep < 2; ++sweep) {  // 0: statistics -> solve, 1: projection -> SSE
+      long long acc[5] = {0, 0, 0, 0, 0};
+      for (int s0 = lr_stripe_start(y0, ss); s0 < y1; s0 += S) {
+        const int ya = s0 > y0 ? s0 : y0, yb = s0 + S < y1 ? s0 + S : y1;
+        lr_chunk_flt(C, D, w, h, ss, s0, ya, yb, x0, x1, set, xt, T, A, Bv, F);
+        for (int q = threadIdx.x; q < (yb - ya) * uw; q += blockDim.x) {
+          const int i = q / uw, j = q - i * uw;
+          const long o = (long)(ya + i) * w + x0 + j;
+          const int x = T[i + 3][j + 3], sv = src[po + o];
+          if (sweep == 0) {
+            const int uu = x << kSgrRstBits;
+            const long long da = F[i][0][j] - uu, db = F[i][1][j] - uu;
+            const long long e = ((long long)(sv << kSgrRstBits) - uu) << kSgrPrjBits;
+            acc[0] += da * da;
+            acc[1] += da * db;
+            acc[2] += db * db;
+            acc[3] += da * e;
+            acc[4] += db * e;
+          } else {
+            const int v = sgr_project_xqd(x, F[i][0][j], F[i][1][j], r0, r1, xq[0], xq[1]);
+            cand[k * psz + po + o] = (uint8_t)v;
+            acc[0] += (v - sv) * (v - sv);
+          }
+        }
+        __syncthreads();  // T / A / F reused by the next chunk
+      }
+      if (sweep == 0) {
 #pragma unroll
-    for (int c = 0; c < 5; ++c) block_add(a[c], sl + c);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      long long st[5];
-      for (int c = 0; c < 5; ++c) st[c] = (long long)red[sl + c];
-      sgr_solve(st, r0, r1, &xq[0], &xq[1]);
+        for (int c = 0; c < 5; ++c) block_add(acc[c], sl + c);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          long long st[5];
+          for (int c = 0; c < 5; ++c) st[c] = (long long)red[sl + c];
+          sgr_solve(st, r0, r1, &xq[0], &xq[1]);
+        }
+        __syncthreads();
+      } else {
+        block_add(acc[0], sl + 5);
+        __syncthreads();
+      }
     }
-    __syncthreads();
-    const int w0 = xq[0], w1 = xq[1];
-    long long e2 = 0;
-    n = 0;
-    for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
-      const int i = q / uw, j = q - i * uw;
-      const int o = sgr_project((int)T[i + kLrHalo][j + kLrHalo], f0[n], f1[n], r0, r1, w0, w1);
-      f0[n] = o;
-      const int d = o - sv[n];
-      e2 += d * d;
-    }
-    block_add(e2, sl + 5);
-    __syncthreads();
     const long long ek = (long long)red[sl + 5] + rt;
     if (ek < best) {  // block-uniform
       best = ek;
-      bset = set;
-      b0 = w0;
-      b1 = w1;
-      n = 0;
-      for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) ob[n] = f0[n];
+      bk = k;
+      b0 = xq[0];
+      b1 = xq[1];
     }
-    __syncthreads();  // xq / A / Bv reused by the next set
+    __syncthreads();  // xq reused by the next set
   }
-  n = 0;
-  for (int q = threadIdx.x; q < uw * uh; q += blockDim.x, ++n) {
+  const uint8_t* O = bk < 0 ? C : cand + bk * psz + po;
+  for (int q = threadIdx.x; q < (y1 - y0) * uw; q += blockDim.x) {
     const int i = q / uw, j = q - i * uw;
-    out[po + (long)(uy + i) * w + ux + j] = (uint8_t)ob[n];
+    const long o = (long)(y0 + i) * w + x0 + j;
+    out[po + o] = O[o];
   }
   if (threadIdx.x == 0) {
     int* P = prm + ((long)b * nu + u) * 3;
-    P[0] = bset;
-    P[1] = bset < 0 ? 0 : b0;
-    P[2] = bset < 0 ? 0 : b1;
+    P[0] = bk < 0 ? -1 : lr_set(bk);
+    P[1] = bk < 0 ? 0 : b0;
+    P[2] = bk < 0 ? 0 : b1;
   }
 }
 
@@ -740,10 +794,11 @@ int tv_gpu_sgr_search(const uint8_t* src, const uint8_t* rec, int w, int h, int 
 }
 // encoder restoration choice over every lr_set() candidate: rate [B] (int64), prm
 // [B][nu][3], restored planes (unrestored units copied)
-int tv_gpu_sgr_select(const uint8_t* src, const uint8_t* rec, int w, int h, int B, const long long* rate, int* prm,
-                      uint8_t* out, void* stream) {
-  if (bad_geo(w, h, B, 2, "sgr_select")) return -1;
-  k_sgr_select<<<dim3(nunits(w, h), B), 256, 0, (hipStream_t)stream>>>(src, rec, w, h, rate, prm, out);
+int tv_gpu_sgr_select(const uint8_t* src, const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, int B,
+                      const long long* rate, int* prm, uint8_t* cand, uint8_t* out, void* stream) {
+  if (bad_geo(w, h, B, 2, "sgr_select") || ss < 0 || ss > 1) return -1;
+  const int nu = lr_count_units(w) * lr_count_units(h);
+  k_sgr_select<<<dim3(nu, B), 256, 0, (hipStream_t)stream>>>(src, cdef, dbk, w, h, ss, rate, prm, cand, out);
   return av1_status("sgr_select");
 }
 int tv_gpu_wiener_apply(const uint8_t* rec, int w, int h, int B, const int* coef, uint8_t* out, void* stream) {

@@ -1,8 +1,7 @@
 """AV1 encode path (BASELINE config #4): golden encoder -> OBU stream ->
 decoder oracle round trip, the packed-decision writer used by the GPU engine, IVF, and
-(GPU) the gfx950 engine against the golden encoder bit for bit.  Decoding by libaom /
-dav1d is parity unpinned (neither exists in the image; CDF / q tables are substitutes,
-csrc/include/tv/av1_enc.h)."""
+(GPU) the gfx950 engine against the golden encoder bit for bit.  Conformance with an
+independent decoder (dav1d) is pinned in tests/test_av1_conformance.py."""
 import numpy as np
 import pytest
 

@@ -6,16 +6,17 @@ current HIP stream:
 
     key frame   k_av1e_intra (anti-diagonal wavefront of 16x16 blocks)
     P frame     k_av1e_inter (full-pel +-16 LDS search, quarter-pel refine, recon)
-    both        k_av1e_lfinfo -> k_deblock (Y, U, V) -> k_cdef_dir -> k_cdef_search
-                (Y, U, V) -> k_av1e_cdef_choose -> k_cdef_apply -> next reference
+    both        k_av1e_lfinfo -> k_deblock (Y, U, V) -> k_cdef_dir -> k_av1e_cdef_skip ->
+                k_cdef_search (Y, U, V) -> k_av1e_cdef_choose -> k_cdef_apply -> next reference
 
 Decisions (mode / MV words, quantised levels, CDEF tables and indices) of the whole GOP
 stay resident in HBM; at the end of the GOP the nonzero transform blocks are compacted on
 the device and copied to the host once, and a CPU thread pool writes every segment's OBU
 temporal units (range coder) while the GPU moves on to the next GOP.
 
-Bit-exact with the C++ golden encoder (``av1.golden_encode``) and decodable by the
-decoder oracle (``av1.decode``): tests/test_av1_codec.py.
+Bit-exact with the C++ golden encoder (``av1.golden_encode``), whose streams decode
+bit-exactly with dav1d (tests/test_av1_conformance.py), and with the decoder oracle
+(``av1.decode``): tests/test_av1_codec.py.
 """
 from __future__ import annotations
 
@@ -46,7 +47,7 @@ def _gpu():
     lib = gpu_lib()
     if not getattr(lib, "_av1e_sigs", False):
         for n in ("tv_av1e_inter", "tv_av1e_intra", "tv_av1e_lfinfo", "tv_av1e_cdef_choose", "tv_av1e_lr_solve",
-                  "tv_av1e_unit_sse", "tv_av1e_merge", "tv_av1e_tb_len", "tv_av1e_tb_pack"):
+                  "tv_av1e_unit_sse", "tv_av1e_merge", "tv_av1e_tb_len", "tv_av1e_tb_pack", "tv_av1e_cdef_skip"):
             getattr(lib, n).restype = C.c_int
         lib.tv_av1e_last_error.restype = C.c_char_p
         lib._av1e_sigs = True
@@ -63,6 +64,11 @@ def _p(t):
 
 
 LR_SETS = (4, 10)  # av1_enc.h lr_set()
+
+
+def lr_grid(size: int) -> int:
+    """Restoration units along a plane dimension (av1_defs.h lr_count_units, 64-px units)."""
+    return max(1, (size + 32) // 64)
 
 
 def lr_rate_cost(q: int) -> int:
@@ -190,6 +196,7 @@ class Av1GpuEngine:
         du = ops.deblock(ru, iu, True, 0, estep=8)
         dv = ops.deblock(rv, iv, True, 0, estep=8)
         dirs, var = ops.cdef_dirs(dy)
+        _ok(lib.tv_av1e_cdef_skip(_p(mode), _p(dirs), W, H, B, st))  # skip blocks are not filtered
         se_y = ops.cdef_search(sy, dy, dirs, var, False, self.damping, pmask=CDEF_MASK_Y, checker=True)
         se_u = ops.cdef_search(su, du, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV, checker=True)
         se_v = ops.cdef_search(sv, dv, dirs, var, True, self.damping, luma_w8=W // 8, pmask=CDEF_MASK_UV, checker=True)
@@ -201,7 +208,7 @@ class Av1GpuEngine:
                     ops.cdef_apply(du, dirs, var, puv, True, self.damping, luma_w8=W // 8),
                     ops.cdef_apply(dv, dirs, var, puv, True, self.damping, luma_w8=W // 8))
         if self.lr_enabled:
-            self.fin = self._restore(t, B, q_rate)
+            self.fin = self._restore(t, B, q_rate, (dy, du, dv))
         w, h = self.w, self.h
         if B < self.B:  # keep full-batch planes: the slice's final frames become the reference
             fin = [torch.empty_like(x) for x in self.src]
@@ -221,22 +228,25 @@ class Av1GpuEngine:
                                     _vp(torch.cuda.current_stream(self.dev).cuda_stream)))
         return out
 
-    def _restore(self, t: int, B: int, rate):
-        """Self-guided restoration search + apply on the CDEF output: the golden encoder's
-        per-unit off / set-4 / set-10 choice (SSE + rate, first minimum), one fused
-        k_sgr_select launch per plane."""
+    def _restore(self, t: int, B: int, rate, dbk):
+        """Normative self-guided restoration search + apply on the CDEF output (7.17 unit
+        grid and stripes; `dbk` = the deblocked pre-CDEF planes the stripe edges read): the
+        golden encoder's per-unit off / set-4 / set-10 choice (SSE + rate, first minimum), one
+        fused k_sgr_select launch per plane."""
         from ..ops import av1 as ops
 
         torch = self.torch
         st = _vp(torch.cuda.current_stream(self.dev).cuda_stream)
         rate = rate.to(torch.int64).contiguous()
         out = []
-        for p, (S, X) in enumerate(zip((x[:B] for x in self.src), self.fin)):
+        for p, (S, X, D) in enumerate(zip((x[:B] for x in self.src), self.fin, dbk)):
             h, w = X.shape[1], X.shape[2]
-            nu = (-(-h // 64)) * (-(-w // 64))
+            nu = lr_grid(w) * lr_grid(h)
             prm = torch.empty((B, nu, 3), dtype=torch.int32, device=self.dev)
             o = torch.empty_like(X)
-            rc = ops._gpu().tv_gpu_sgr_select(_p(S), _p(X), w, h, B, _p(rate), _p(prm), _p(o), st)
+            cand = torch.empty((len(LR_SETS),) + tuple(X.shape), dtype=torch.uint8, device=self.dev)
+            rc = ops._gpu().tv_gpu_sgr_select(_p(S), _p(X), _p(D), w, h, 1 if p else 0, B, _p(rate), _p(prm),
+                                              _p(cand), _p(o), st)
             if rc != 0:
                 raise RuntimeError(ops._gpu().tv_av1_gpu_last_error().decode())
             self.g_lr[t, :B, p, :nu] = prm
