@@ -579,7 +579,9 @@ __device__ void lr_chunk_flt(const uint8_t* cdef, const uint8_t* dbk, int w, int
   }
 }
 
-__global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ src, const uint8_t* __restrict__ cdef,
+constexpr int kLrThreads = 512, kLrMaxPx = 104 * 96, kLrPer = (kLrMaxPx + kLrThreads - 1) / kLrThreads;  // unit <= 103 x 95
+
+__global__ void __launch_bounds__(kLrThreads) k_sgr_select(const uint8_t* __restrict__ src, const uint8_t* __restrict__ cdef,
                                                     const uint8_t* __restrict__ dbk, int w, int h, int ss,
                                                     const long long* __restrict__ rate, int* __restrict__ prm,
                                                     uint8_t* __restrict__ cand, uint8_t* __restrict__ out) {
@@ -588,7 +590,7 @@ __global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ 
   int x0, x1, y0, y1;
   lr_unit_cols(uc, w, &x0, &x1);
   lr_unit_rows(ur, h, ss, &y0, &y1);
-  const int uw = x1 - x0, S = 64 >> ss;
+  const int uw = x1 - x0, npx = (y1 - y0) * uw, S = 64 >> ss;
   const long po = (long)b * w * h, psz = (long)gridDim.y * w * h;
   const uint8_t* C = cdef + po;
   const uint8_t* D = dbk + po;
@@ -597,19 +599,29 @@ __global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ 
   __shared__ int16_t F[kLrCh][2][kLrUw];
   __shared__ unsigned long long red[1 + 6 * kNumLrSets];
   __shared__ int xq[2];
-  if (threadIdx.x < 256) xt[threadIdx.x] = (uint16_t)sgr_xbyx1(threadIdx.x);
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) xt[i] = (uint16_t)sgr_xbyx1(threadIdx.x);
   if (threadIdx.x < 1 + 6 * kNumLrSets) red[threadIdx.x] = 0;
   __syncthreads();
   auto block_add = [&](long long v, int slot) {
     v = wave_sum64(v);
     if ((threadIdx.x & 63) == 0) atomicAdd(&red[slot], (unsigned long long)v);
   };
+  // the thread's pixels (q = tid + kLrThreads n, row-major over the unit): CDEF and source samples
+  // and, per set, the packed guided outputs F0 | F1 << 16, kept in registers across the
+  // statistics -> solve -> projection steps (the filters run once per set)
+  uint32_t xs[kLrPer], fv[kLrPer];
   long long e0 = 0;
-  for (int q = threadIdx.x; q < (y1 - y0) * uw; q += blockDim.x) {
-    const int i = q / uw, j = q - i * uw;
-    const long o = (long)(y0 + i) * w + x0 + j;
-    const int d = (int)C[o] - (int)src[po + o];
-    e0 += d * d;
+#pragma unroll
+  for (int n = 0; n < kLrPer; ++n) {
+    const int q = threadIdx.x + kLrThreads * n;
+    xs[n] = 0;
+    if (q < npx) {
+      const int i = q / uw, j = q - i * uw;
+      const long o = (long)(y0 + i) * w + x0 + j;
+      const int c = C[o], sv = src[po + o];
+      xs[n] = (uint32_t)c | ((uint32_t)sv << 8);
+      e0 += (c - sv) * (c - sv);
+    }
   }
   block_add(e0, 0);
   __syncthreads();
@@ -618,47 +630,53 @@ __global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ 
   const long long rt = rate[b];
   for (int k = 0; k < kNumLrSets; ++k) {
     const int set = lr_set(k), r0 = sgr_param(set, 0), r1 = sgr_param(set, 2), sl = 1 + 6 * k;
-    for (int sweep = 0; sweep < 2; ++sweep) {  // 0: statistics -> solve, 1: projection -> SSE
-      long long acc[5] = {0, 0, 0, 0, 0};
-      for (int s0 = lr_stripe_start(y0, ss); s0 < y1; s0 += S) {
-        const int ya = s0 > y0 ? s0 : y0, yb = s0 + S < y1 ? s0 + S : y1;
-        lr_chunk_flt(C, D, w, h, ss, s0, ya, yb, x0, x1, set, xt, T, A, Bv, F);
-        for (int q = threadIdx.x; q < (yb - ya) * uw; q += blockDim.x) {
-          const int i = q / uw, j = q - i * uw;
-          const long o = (long)(ya + i) * w + x0 + j;
-          const int x = T[i + 3][j + 3], sv = src[po + o];
-          if (sweep == 0) {
-            const int uu = x << kSgrRstBits;
-            const long long da = F[i][0][j] - uu, db = F[i][1][j] - uu;
-            const long long e = ((long long)(sv << kSgrRstBits) - uu) << kSgrPrjBits;
-            acc[0] += da * da;
-            acc[1] += da * db;
-            acc[2] += db * db;
-            acc[3] += da * e;
-            acc[4] += db * e;
-          } else {
-            const int v = sgr_project_xqd(x, F[i][0][j], F[i][1][j], r0, r1, xq[0], xq[1]);
-            cand[k * psz + po + o] = (uint8_t)v;
-            acc[0] += (v - sv) * (v - sv);
-          }
-        }
-        __syncthreads();  // T / A / F reused by the next chunk
-      }
-      if (sweep == 0) {
+    for (int s0 = lr_stripe_start(y0, ss); s0 < y1; s0 += S) {
+      const int ya = s0 > y0 ? s0 : y0, yb = s0 + S < y1 ? s0 + S : y1;
+      lr_chunk_flt(C, D, w, h, ss, s0, ya, yb, x0, x1, set, xt, T, A, Bv, F);
 #pragma unroll
-        for (int c = 0; c < 5; ++c) block_add(acc[c], sl + c);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          long long st[5];
-          for (int c = 0; c < 5; ++c) st[c] = (long long)red[sl + c];
-          sgr_solve(st, r0, r1, &xq[0], &xq[1]);
-        }
-        __syncthreads();
-      } else {
-        block_add(acc[0], sl + 5);
-        __syncthreads();
+      for (int n = 0; n < kLrPer; ++n) {
+        const int q = threadIdx.x + kLrThreads * n;
+        const int i = q / uw, j = q - i * uw, yy = y0 + i;
+        if (q < npx && yy >= ya && yy < yb)
+          fv[n] = (uint32_t)(uint16_t)F[yy - ya][0][j] | ((uint32_t)(uint16_t)F[yy - ya][1][j] << 16);
       }
+      __syncthreads();  // T / A / F reused by the next chunk
     }
+    long long acc[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int n = 0; n < kLrPer; ++n) {
+      if (threadIdx.x + kLrThreads * n >= npx) continue;
+      const int uu = (int)(xs[n] & 255) << kSgrRstBits;
+      const long long da = (int)(int16_t)(fv[n] & 0xFFFF) - uu, db = (int)(int16_t)(fv[n] >> 16) - uu;
+      const long long e = ((long long)((int)(xs[n] >> 8) << kSgrRstBits) - uu) << kSgrPrjBits;
+      acc[0] += da * da;
+      acc[1] += da * db;
+      acc[2] += db * db;
+      acc[3] += da * e;
+      acc[4] += db * e;
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) block_add(acc[c], sl + c);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long st[5];
+      for (int c = 0; c < 5; ++c) st[c] = (long long)red[sl + c];
+      sgr_solve(st, r0, r1, &xq[0], &xq[1]);
+    }
+    __syncthreads();
+    long long e2 = 0;
+#pragma unroll
+    for (int n = 0; n < kLrPer; ++n) {
+      const int q = threadIdx.x + kLrThreads * n;
+      if (q >= npx) continue;
+      const int i = q / uw, j = q - i * uw;
+      const int x = xs[n] & 255, sv = xs[n] >> 8;
+      const int v = sgr_project_xqd(x, (int16_t)(fv[n] & 0xFFFF), (int16_t)(fv[n] >> 16), r0, r1, xq[0], xq[1]);
+      cand[k * psz + po + (long)(y0 + i) * w + x0 + j] = (uint8_t)v;
+      e2 += (v - sv) * (v - sv);
+    }
+    block_add(e2, sl + 5);
+    __syncthreads();
     const long long ek = (long long)red[sl + 5] + rt;
     if (ek < best) {  // block-uniform
       best = ek;
@@ -669,7 +687,7 @@ __global__ void __launch_bounds__(256) k_sgr_select(const uint8_t* __restrict__ 
     __syncthreads();  // xq reused by the next set
   }
   const uint8_t* O = bk < 0 ? C : cand + bk * psz + po;
-  for (int q = threadIdx.x; q < (y1 - y0) * uw; q += blockDim.x) {
+  for (int q = threadIdx.x; q < npx; q += blockDim.x) {
     const int i = q / uw, j = q - i * uw;
     const long o = (long)(y0 + i) * w + x0 + j;
     out[po + o] = O[o];
@@ -798,7 +816,7 @@ int tv_gpu_sgr_select(const uint8_t* src, const uint8_t* cdef, const uint8_t* db
                       const long long* rate, int* prm, uint8_t* cand, uint8_t* out, void* stream) {
   if (bad_geo(w, h, B, 2, "sgr_select") || ss < 0 || ss > 1) return -1;
   const int nu = lr_count_units(w) * lr_count_units(h);
-  k_sgr_select<<<dim3(nu, B), 256, 0, (hipStream_t)stream>>>(src, cdef, dbk, w, h, ss, rate, prm, cand, out);
+  k_sgr_select<<<dim3(nu, B), kLrThreads, 0, (hipStream_t)stream>>>(src, cdef, dbk, w, h, ss, rate, prm, cand, out);
   return av1_status("sgr_select");
 }
 int tv_gpu_wiener_apply(const uint8_t* rec, int w, int h, int B, const int* coef, uint8_t* out, void* stream) {

@@ -192,6 +192,30 @@ def test_worker_software_av1_part_and_mp4_probe(tmp_path):
         np.testing.assert_array_equal(got[k][0], dec.planes(k)[0])
 
 
+def test_stitch_concat_parts_av1(tmp_path):
+    """The split/encode/stitch path with tv_codec=av1: two av01 part MP4s through the
+    stitcher's concat_parts give one av01 MP4 whose samples are the parts' frames."""
+    from thinvids_amd.models import media
+    from thinvids_amd.worker.tasks import concat_parts
+
+    w, h = 80, 48
+    parts = [_frames(4, w, h, 4, 0), _frames(4, w, h, 3, 4)]
+    paths = []
+    for i, fr in enumerate(parts):
+        bits = av1.golden_encode(fr, w, h, 100).stream
+        pth = tmp_path / f"enc_{i + 1:03d}.mp4"
+        hevc.mux_mp4_file([bits], w, h, 30, 1, str(pth))
+        paths.append(str(pth))
+    out, n = concat_parts(paths, str(tmp_path / "job_output.mp4"), w, h, 30, 1)
+    info = media.probe(out)
+    assert info["codec"] == "av1" and info["frames"] == 7 and n > 0
+    src = media.open_source(out)
+    got = src.read(4, 3)
+    dec = av1.decode(av1.golden_encode(parts[1], w, h, 100).stream)
+    for k in range(3):
+        np.testing.assert_array_equal(got[k][0], dec.planes(k)[0])
+
+
 @pytest.mark.gpu
 def test_gpu_worker_av1_parts_match_golden():
     """The worker's GPU path for tv_codec=av1 (staging, per-segment q-index map) equals the

@@ -77,3 +77,16 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "1"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
+
+
+def test_visible_gpu_count_without_hip(monkeypatch):
+    """The node supervisor counts GPUs from the visibility list / sysfs (no HIP call)."""
+    from thinvids_amd.parallel import launch
+
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,2,5")
+    assert launch.visible_gpu_count() == 3
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    for v in ("ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setattr(launch, "gpu_numa_nodes", lambda: [0, 0, 1, 1])
+    assert launch.visible_gpu_count() == 4

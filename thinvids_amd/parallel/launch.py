@@ -133,6 +133,17 @@ def gpu_numa_nodes() -> list[int]:
     return out
 
 
+def visible_gpu_count() -> int:
+    """GPUs a rank launcher may use, counted without any HIP call (a supervisor that never
+    initialises the GPU can fork / exec ranks safely): the *_VISIBLE_DEVICES list when set,
+    otherwise the AMD GPU functions in sysfs.  0 when none is visible."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() and x.strip() != "-1"])
+    return len(gpu_numa_nodes())
+
+
 def plan_affinity(local_rank: int, local_world: int, allowed: list[int] | None = None,
                   nodes: dict[int, list[int]] | None = None, gpu_nodes: list[int] | None = None) -> list[int]:
     """Disjoint CPU set for one rank: the ranks that share a NUMA node split that node's

@@ -195,13 +195,19 @@ class WorkQueue:
         return all(self._add(f"rq_c_{i}", 0) >= 1 for i in range(n2))
 
 
+# bumped whenever the encoders' output for identical settings changes (a checkpoint written
+# by an older build must not be mixed into a newer job's output)
+BITSTREAM_VERSION = 3
+
+
 class Checkpoint:
     """Segment-level resume: every encoded segment is published atomically
     as ``<dir>/<fingerprint>/r<rung>_s<idx>_q<qp>.hevc`` with a ``.sha256`` sidecar written
     last; a rerun (or an elastic restart) reuses every segment whose checksum verifies.
     Keyed by QP, so first-pass segments double as the 2-pass statistics checkpoint.  The
     fingerprint covers everything that changes a segment's bytes (source identity, ladder
-    geometry, GOP, segmentation, search range), so a reused directory never mixes jobs."""
+    geometry, GOP, segmentation, search range, codec, q-index, CRF, rate-control mode and
+    the bitstream version), so a reused directory never mixes jobs or codecs."""
 
     def __init__(self, root: str | None, fingerprint: str = ""):
         self.root = os.path.join(root, fingerprint) if root and fingerprint else root
@@ -249,6 +255,9 @@ class JobHooks:
 
     def segment_done(self, frames: int) -> None:
         pass
+
+    def new_pass(self, index: int) -> None:
+        """A rate-control pass starts (0 = the first): per-pass progress restarts."""
 
     def halted(self) -> bool:
         return False
@@ -327,7 +336,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     ckpt = Checkpoint(resume_dir, Checkpoint.fingerprint(
         src=os.path.abspath(input_path), size=st.st_size if st else 0, mtime=st.st_mtime_ns if st else 0,
         rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software,
-        deblock=deblock, sao=sao, scenecut=scenecut))
+        deblock=deblock, sao=sao, scenecut=scenecut, codec=codec, qindex=qindex, crf=crf,
+        rc="2pass" if bitrate_kbps > 0 else ("crf" if crf else "cqp"), bitstream_version=BITSTREAM_VERSION))
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
     quality: dict = {}  # (r, i) -> PartStats of segments encoded here
 
@@ -497,6 +507,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         """encode_pass + a collective verdict: a rank that failed (halt, abort, engine
         error) never strands its peers inside the next collective."""
         err, got = None, {}
+        hooks.new_pass(agreed_pass.n)
+        agreed_pass.n += 1
         try:
             got = encode_pass()
         except Exception as e:  # noqa: BLE001 - re-raised below on every rank
@@ -506,6 +518,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             raise err if err is not None else RuntimeError("a peer rank failed this job")
         return got
 
+    agreed_pass.n = 0
     passes = 1
     if bitrate_kbps > 0:
         # pass 1 at the base QP -> every frame's bits, all-reduced over the node (RCCL) ->

@@ -82,18 +82,28 @@ class _StoreHooks:
     def __init__(self, job_id: str, total: int, stage_t0: float, beat=None):
         self.job_id, self.total, self.t0, self.beat = job_id, total, stage_t0, beat
         self._halt_checked, self._halted = 0.0, False
+        self.pass_idx = 0
+
+    def new_pass(self, index: int) -> None:
+        self.pass_idx = index
 
     def segment_done(self, frames: int) -> None:
+        """Per-pass counters (2-pass / 3-pass jobs): every rank increments the pass's own
+        fields and mirrors them into parts_done / completed_chunks, so those never exceed
+        parts_total; encoded_frames counts the frames of the final pass the same way."""
         if self.beat is not None:
             self.beat.progress("segment")
         st = get_store()
         k = job_key(self.job_id)
+        sfx = f"_p{self.pass_idx}" if self.pass_idx else ""
         p = st.pipeline()
-        p.hincrby(k, "completed_chunks", 1)
-        p.hincrby(k, "parts_done", 1)
-        p.hincrby(k, "encoded_frames", int(frames))
+        p.hincrby(k, "completed_chunks" + sfx, 1)
+        p.hincrby(k, "parts_done" + sfx, 1)
+        p.hincrby(k, "encoded_frames" + sfx, int(frames))
         res = p.execute()
         done = int(res[1])
+        if sfx:
+            st.hset(k, mapping={"completed_chunks": int(res[0]), "parts_done": done, "encoded_frames": int(res[2])})
         prog = int(done * 100 / max(1, self.total))
         if prog > int(st.hget(k, "encode_progress") or 0):
             st.hset(k, mapping={"encode_progress": prog, "encode_elapsed": int(now() - self.t0)})
@@ -401,10 +411,10 @@ def main(argv=None) -> int:
     if not launched_by_torchrun():
         n = a.gpus
         cpu = os.environ.get("TV_FORCE_CPU") == "1"
-        if n is None:  # count devices without initialising HIP in this (launcher) process
-            import torch
+        if n is None:  # count devices from sysfs / the visibility list: no HIP call here
+            from ..parallel.launch import visible_gpu_count
 
-            n = 1 if cpu else max(1, torch.cuda.device_count())
+            n = 1 if cpu else max(1, visible_gpu_count())
         rank_argv = ["-m", "thinvids_amd.worker.node_executor", *(argv if argv is not None else sys.argv[1:])]
         if a.no_supervise:
             return spawn_ranks(n, rank_argv)

@@ -434,10 +434,14 @@ def concat_parts(paths: list[str], out_path: str, width: int, height: int, fps_n
     extension is the plan's (.mkv when English subtitles are carried)."""
     from ..models import streams
 
+    from ..models import av1
+
     segs = []
     for p in paths:  # each part's elementary stream; the output is streamed from these buffers
         with open(p, "rb") as f:
-            segs.append(hevc.demux_mp4(f.read())["annexb"])
+            data = f.read()
+        # tv_codec=av1 parts are av01 MP4s (OBU temporal units), HEVC parts hvc1 (Annex-B)
+        segs.append(av1.mp4_av1_stream(data)[1] if av1.mp4_av1_track(data) else hevc.demux_mp4(data)["annexb"])
     ensure_dirs(os.path.dirname(out_path) or ".")
     return streams.write_output(segs, width, height, fps_num, fps_den, out_path, plan)
 
