@@ -434,6 +434,13 @@ def av1_main(args) -> None:
     dist.destroy_process_group()
 
 
+# the benchmarked configuration is the shipped worker configuration (common/settings.py)
+from thinvids_amd.common.settings import DEFAULT_SETTINGS as _DEFAULTS  # noqa: E402
+
+_WORKER_GOP = int(_DEFAULTS.get("tv_gop", 64))
+_WORKER_SAO = str(_DEFAULTS.get("tv_sao", "1")) == "1"
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -441,9 +448,12 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--res", default="1080p", choices=sorted(RES))
     ap.add_argument("--batch", type=int, default=0, help="segments per GPU per step (0 = auto)")
-    ap.add_argument("--gop", type=int, default=16, help="frames per GOP-aligned segment")
+    ap.add_argument("--gop", type=int, default=_WORKER_GOP,
+                    help="frames per GOP-aligned segment (default: the worker's shipped tv_gop)")
     ap.add_argument("--qp", type=int, default=27)
-    ap.add_argument("--sao", action="store_true", help="enable SAO (in-loop sample adaptive offset)")
+    ap.add_argument("--sao", dest="sao", action="store_true", default=_WORKER_SAO,
+                    help="enable SAO (in-loop sample adaptive offset; default: the worker's shipped tv_sao)")
+    ap.add_argument("--no-sao", dest="sao", action="store_false", help="disable SAO")
     ap.add_argument("--range", type=int, default=64, help="motion search range (full-res pels, multiple of 16)")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)

@@ -17,7 +17,7 @@ int main(int argc, char** argv) {
   cfg.height = H;
   cfg.qp = qp;
   cfg.finalize();
-  CpuEncoder enc(cfg, 4);
+  CpuEncoder enc(cfg, 16);
   std::vector<uint8_t> planes[3] = {std::vector<uint8_t>(W * H), std::vector<uint8_t>(W * H / 4),
                                     std::vector<uint8_t>(W * H / 4)};
   std::vector<FrameDecisions> decs;
