@@ -86,6 +86,52 @@ def test_agent_gc_and_suspend(agent_env):
     assert busy.tick(t + 50)["action"] is None
 
 
+def test_agent_publishes_xgmi_counters_and_rates(agent_env):
+    """amdsmi per-link accumulators (KB) -> node totals (bytes) -> per-second rates in
+    metrics:node:<host>; unsupported links ("N/A" / sentinel) are skipped, and a GPU whose
+    metrics table lacks xGMI falls back to the link-metrics API."""
+    from thinvids_amd.agent import Agent
+    from thinvids_amd.agent.gpu import GpuSampler, xgmi_bytes
+
+    class FakeSmi:
+        class AmdSmiMemoryType:
+            VRAM = 0
+
+        def __init__(self):
+            self.kb = 0
+
+        def amdsmi_get_gpu_activity(self, h):
+            return {"gfx_activity": 50, "umc_activity": 10}
+
+        def amdsmi_get_gpu_metrics_info(self, h):
+            if h == 1:
+                return {"xgmi_read_data_acc": "N/A"}
+            return {"xgmi_read_data_acc": [self.kb, self.kb, "N/A", 2 ** 64 - 1],
+                    "xgmi_write_data_acc": [self.kb // 2, 0, "N/A", "N/A"]}
+
+        def amdsmi_get_link_metrics(self, h):
+            return {"num_links": 2, "links": [{"read": 7, "write": 3}, {"read": 1, "write": 1}, {"read": 99, "write": 99}]}
+
+    smi = FakeSmi()
+    assert xgmi_bytes(smi, 0) == (0, 0)
+    assert xgmi_bytes(smi, 1) == (8 * 1024, 4 * 1024)
+    gs = GpuSampler.__new__(GpuSampler)
+    gs._smi, gs._handles = smi, [0, 1]
+    st, _ = agent_env
+    a = Agent(store=st, gpu=gs, suspend_fn=lambda: None)
+    a.tick()
+    m = st.hgetall("metrics:node:node3")
+    assert int(m["xgmi_read_bytes"]) == 8 * 1024 and int(m["xgmi_rx_bps"]) == 0
+    smi.kb = 1000  # 2 links x 1000 KB read, 500 KB written since the last beat
+    a.last_ts -= 1.0
+    a.tick()
+    m = st.hgetall("metrics:node:node3")
+    assert int(m["xgmi_read_bytes"]) == 2000 * 1024 + 8 * 1024 and int(m["xgmi_write_bytes"]) == 500 * 1024 + 4 * 1024
+    assert 0.5 * 2000 * 1024 < int(m["xgmi_rx_bps"]) <= 2000 * 1024 and int(m["xgmi_tx_bps"]) > 0
+    g = json.loads(m["gpus_json"])
+    assert g[0]["xgmi_read_bytes"] == 2000 * 1024
+
+
 def test_rocm_smi_parser():
     from thinvids_amd.agent.gpu import parse_rocm_smi
 

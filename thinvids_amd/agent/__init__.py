@@ -4,7 +4,9 @@ A 1 Hz loop that is the cluster's liveness signal:
 
 * publishes ``metrics:node:<host>`` = {ts, hostname, ip, mac, cpu, gpu, mem, mem_used,
   mem_total, disk, rx_bps, tx_bps, worker_role} + MI355X fields {gpu_count, gpu_name,
-  hbm_used, hbm_total, gpus_json} with ``EXPIRE TTL_SEC`` (C7, C8);
+  hbm_used, hbm_total, xgmi_rx_bps, xgmi_tx_bps, xgmi_read_bytes, xgmi_write_bytes,
+  gpus_json} with ``EXPIRE TTL_SEC`` (C7, C8, SURVEY 5.5: xGMI bytes are the node's
+  collective traffic, as the NIC counters were the reference's data-plane traffic);
 * publishes ``nodes:mac[host]`` hourly (manager discovery / WOL);
 * role sync: the encode service always runs, the pipeline service only when
   ``pipeline:node_roles[host] == "pipeline"`` (C9);
@@ -134,6 +136,7 @@ class Agent:
         self.last_suspend = 0.0
         self.last_net = psutil.net_io_counters()
         self.last_ts = time.time()
+        self.last_xgmi = None  # (read, write) bytes of the previous sample
         psutil.cpu_percent(interval=None)  # prime
 
     @property
@@ -181,6 +184,12 @@ class Agent:
                    "gpu_count": 0 if g is None else g["gpu_count"], "gpu_name": "" if g is None else g["gpu_name"],
                    "hbm_used": 0 if g is None else g["hbm_used"], "hbm_total": 0 if g is None else g["hbm_total"],
                    "gpus_json": json.dumps([] if g is None else g["gpus"])}
+        if g is not None and "xgmi_read_bytes" in g:
+            cur = (int(g["xgmi_read_bytes"]), int(g["xgmi_write_bytes"]))
+            prev = self.last_xgmi or cur
+            payload.update(xgmi_read_bytes=cur[0], xgmi_write_bytes=cur[1],
+                           xgmi_rx_bps=max(0, int((cur[0] - prev[0]) / dt)), xgmi_tx_bps=max(0, int((cur[1] - prev[1]) / dt)))
+            self.last_xgmi = cur
         return payload, g
 
     def suspend_settings(self) -> tuple[bool, int, float, bool]:

@@ -2,8 +2,11 @@
 ``intel_gpu_top -J`` video-engine busy %, agent/agent.py:42-117).
 
 Uses the ``amdsmi`` Python API (graphics activity, VRAM/HBM used/total, power, edge
-temperature, market name) and falls back to ``rocm-smi --json`` when the library cannot
-be initialised.  Returns ``None`` when no AMD GPU is visible (the agent then publishes
+temperature, market name, accumulated xGMI read / write bytes over all links) and falls
+back to ``rocm-smi --json`` when the library cannot be initialised.  The xGMI totals are
+monotonically increasing byte counters; the agent turns them into per-second rates the
+same way it does for the NIC (reference payload ``rx_bps`` / ``tx_bps``,
+agent/agent.py:410-429).  Returns ``None`` when no AMD GPU is visible (the agent then publishes
 ``gpu = -1`` exactly like the reference did without an iGPU).
 """
 from __future__ import annotations
@@ -64,6 +67,9 @@ class GpuSampler:
                 g["power_w"] = _num(p.get("current_socket_power", p.get("average_socket_power")))
             except Exception:
                 pass
+            rd, wr = xgmi_bytes(smi, h)
+            if rd is not None:
+                g["xgmi_read_bytes"], g["xgmi_write_bytes"] = rd, wr
             try:
                 g["temp_c"] = _num(smi.amdsmi_get_temp_metric(h, smi.AmdSmiTemperatureType.HOTSPOT,
                                                                smi.AmdSmiTemperatureMetric.CURRENT))
@@ -90,10 +96,49 @@ class GpuSampler:
         if not gpus:
             return None
         utils = [g["util"] for g in gpus if g.get("util", -1) >= 0]
-        return {"gpu_count": len(gpus), "util": sum(utils) / len(utils) if utils else -1.0,
-                "hbm_used": sum(g.get("hbm_used", 0) for g in gpus),
-                "hbm_total": sum(g.get("hbm_total", 0) for g in gpus),
-                "gpu_name": gpus[0].get("name", ""), "gpus": gpus}
+        out = {"gpu_count": len(gpus), "util": sum(utils) / len(utils) if utils else -1.0,
+               "hbm_used": sum(g.get("hbm_used", 0) for g in gpus),
+               "hbm_total": sum(g.get("hbm_total", 0) for g in gpus),
+               "gpu_name": gpus[0].get("name", ""), "gpus": gpus}
+        if any("xgmi_read_bytes" in g for g in gpus):
+            out["xgmi_read_bytes"] = sum(g.get("xgmi_read_bytes", 0) for g in gpus)
+            out["xgmi_write_bytes"] = sum(g.get("xgmi_write_bytes", 0) for g in gpus)
+        return out
+
+
+def _kb_sum(vals) -> int | None:
+    """Sum of the numeric entries of an amdsmi per-link counter list (unsupported links are
+    reported as "N/A" / max-uint sentinels and skipped); None when no entry is numeric."""
+    tot, seen = 0, False
+    for v in vals if isinstance(vals, (list, tuple)) else [vals]:
+        if isinstance(v, bool) or not isinstance(v, (int, float)) or v < 0 or v >= 2 ** 63:
+            continue
+        tot += int(v)
+        seen = True
+    return tot if seen else None
+
+
+def xgmi_bytes(smi, handle) -> tuple[int | None, int | None]:
+    """(read, write) bytes accumulated over every xGMI link of one GPU since driver load.
+    GPU metrics table first (``xgmi_read_data_acc`` / ``xgmi_write_data_acc``, KB per link),
+    then the link-metrics API (``read`` / ``write``, KB per link); (None, None) if neither
+    reports a number (single-GPU or PCIe-only boxes)."""
+    try:
+        m = smi.amdsmi_get_gpu_metrics_info(handle)
+        rd, wr = _kb_sum(m.get("xgmi_read_data_acc")), _kb_sum(m.get("xgmi_write_data_acc"))
+        if rd is not None and wr is not None:
+            return rd * 1024, wr * 1024
+    except Exception:
+        pass
+    try:
+        lm = smi.amdsmi_get_link_metrics(handle)
+        links = lm.get("links", [])[: int(lm.get("num_links", 0) or 0)]
+        rd, wr = _kb_sum([x.get("read") for x in links]), _kb_sum([x.get("write") for x in links])
+        if rd is not None and wr is not None:
+            return rd * 1024, wr * 1024
+    except Exception:
+        pass
+    return None, None
 
 
 def parse_rocm_smi(data: dict) -> list[dict]:
