@@ -107,6 +107,41 @@ def test_node_job_world2(tmp_path, source, kw):
         assert res["passes"] in (2, 3) and len(res["qp_plan"][0]) == 3
 
 
+def test_rotating_scatter_gloo_world4(tmp_path, source):
+    """Scatter mode on 4 ranks: the root rotates per round (comm.scatter_root), so the
+    source reads and sends are spread over the ranks instead of rank 0 reading everything;
+    every segment reaches its rank and the stitched output decodes to the whole clip."""
+    from thinvids_amd.models import hevc
+    from thinvids_amd.parallel.comm import scatter_root
+
+    assert [scatter_root(r, 4) for r in range(6)] == [0, 1, 2, 3, 0, 1]
+    src, frames = source
+    res, out = _spawn_job(tmp_path, source, {"mode": "scatter", "gop": 2, "segment_frames": 2}, {}, world=4)
+    r0 = res[0]
+    assert "error" not in r0, r0
+    per = r0["per_rank"]
+    # 12 segments = 3 rounds rooted at ranks 0, 1, 2; each root read its round's 4 segments
+    assert [p.get("roots", 0) for p in per] == [1, 1, 1, 0]
+    assert [p["reads"] for p in per] == [4, 4, 4, 0]
+    assert [p["encoded"] for p in per] == [3, 3, 3, 3]
+    with open(out, "rb") as f:
+        dec = hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False)
+    assert len(dec.frames) == 24
+    assert min(hevc.psnr(a[0], b[0]) for a, b in zip(frames, dec.frames)) > 28
+
+
+def test_stage_segment_frames_packs_i420_rows():
+    import torch
+
+    from thinvids_amd.parallel.comm import stage_segment_frames
+
+    fr = [(np.full((4, 6), 1 + t, np.uint8), np.full((2, 3), 100 + t, np.uint8), np.full((2, 3), 200 + t, np.uint8))
+          for t in range(3)]
+    buf = stage_segment_frames(fr, (5, 36), torch.device("cpu")).numpy()
+    assert (buf[1, :24] == 2).all() and (buf[1, 24:30] == 101).all() and (buf[1, 30:] == 201).all()
+    assert (buf[3:] == 0).all()  # rows past the segment's frames stay zero (padding to n_max)
+
+
 def test_node_job_ladder_single_process(tmp_path, source):
     """ABR ladder fan-out (rungs x segments) with Lanczos down-scaling, world 1."""
     from thinvids_amd.models import hevc

@@ -66,16 +66,20 @@ def gather_bytes_to_root(payload: bytes, device: torch.device, root: int = 0):
 
 def scatter_frames_from_root(frames: list | None, shape: tuple, device: torch.device, root: int = 0):
     """Scatter one uint8 tensor of `shape` per rank from `root` (GOP frames of a segment).
-    `frames` (root only) is a list of world tensors/arrays."""
+    `frames` (root only) is a list of world tensors/arrays; device tensors are sent as they
+    are (no host bounce), host arrays are uploaded first."""
     world, rank = _world()
-    out = torch.empty(shape, dtype=torch.uint8, device=device)
+
+    def dev_t(x):
+        return (x if isinstance(x, torch.Tensor) else torch.as_tensor(np.asarray(x))).to(device)
+
     if world == 1:
-        out.copy_(torch.as_tensor(np.asarray(frames[0])))
-        return out
+        return dev_t(frames[0]).reshape(shape).clone()
+    out = torch.empty(shape, dtype=torch.uint8, device=device)
     if rank == root:
         ops = []
         for r in range(world):
-            t = torch.as_tensor(np.asarray(frames[r])).to(device)
+            t = dev_t(frames[r])
             if r == root:
                 out.copy_(t)
             else:
@@ -86,6 +90,35 @@ def scatter_frames_from_root(frames: list | None, shape: tuple, device: torch.de
         for req in dist.batch_isend_irecv([dist.P2POp(dist.irecv, out, root)]):
             req.wait()
     return out
+
+
+def scatter_root(round_idx: int, world: int) -> int:
+    """Root of scatter round `round_idx`: rotates over the ranks, so the source reads, the
+    host->device staging and the world-1 sends of a job are spread evenly (each xGMI link of
+    the fully connected node carries one hop per round) instead of serialising on rank 0."""
+    return round_idx % max(1, world)
+
+
+def stage_segment_frames(frames, shape: tuple, device: torch.device) -> torch.Tensor:
+    """Pack decoded frames [(Y, U, V) host planes] into one device tensor of `shape`
+    (frames x packed I420 bytes): each plane is copied straight into its slice of the device
+    buffer through a pinned host staging row; no host-side concatenation."""
+    buf = torch.zeros(shape, dtype=torch.uint8, device=device)
+    pin = device.type == "cuda"
+    row = torch.empty(shape[1], dtype=torch.uint8, pin_memory=pin) if pin else None
+    for f, planes in enumerate(frames):
+        o = 0
+        for p in planes:
+            a = torch.from_numpy(np.ascontiguousarray(p).reshape(-1))
+            n = a.numel()
+            if row is not None:
+                row[o:o + n].copy_(a)
+            else:
+                buf[f, o:o + n].copy_(a)
+            o += n
+        if row is not None:  # one H2D copy per frame, ordered on the stream before the reuse
+            buf[f].copy_(row, non_blocking=False)
+    return buf
 
 
 def allreduce_stats(values, device: torch.device, op: str = "sum") -> np.ndarray:

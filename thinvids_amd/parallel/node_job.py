@@ -306,7 +306,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     from ..models.streams import write_output
     from ..worker.encoder import EncodeSpec, EngineCache, PartStats, SynthRange, gpu_available, psnr_from_sse
     from ..worker.helpers import output_geometry
-    from .comm import allreduce_stats, gather_bytes_to_root, scatter_frames_from_root
+    from .comm import allreduce_stats, gather_bytes_to_root, scatter_frames_from_root, scatter_root, stage_segment_frames
 
     hooks = hooks or JobHooks()
     _job_seq[0] += 1
@@ -414,26 +414,26 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     def encode_pass() -> dict:
         mine = {}
         if mode == "scatter" and world > 1:
-            # rounds: rank 0 reads `world` segments and sends each rank its segment over one
-            # xGMI hop; the received tensor stays on the device (no host bounce)
+            # rounds of `world` segments; the round's root (rotating, comm.scatter_root) reads
+            # them, stages each one straight into a device buffer and sends each peer its
+            # segment over one xGMI hop; the received tensor stays on the device
             fsz = w0 * h0 * 3 // 2
-            for base in range(0, len(segs), world):
+            for rd, base in enumerate(range(0, len(segs), world)):
                 if hooks.halted():
                     raise RuntimeError("job halted")
                 rnd = list(range(base, min(len(segs), base + world)))
                 n_max = max(segs[i][1] for i in rnd)
                 shape = (n_max, fsz)
+                root = scatter_root(rd, world)
                 payload = None
-                if rank == 0:
+                if rank == root:
                     payload = []
                     for k in range(world):
-                        buf = np.zeros(shape, np.uint8)
-                        if k < len(rnd):
-                            for f, (y, u, v) in enumerate(src.read(*segs[rnd[k]])):
-                                buf[f] = np.concatenate([y.ravel(), u.ravel(), v.ravel()])
-                            stats["reads"] += 1
-                        payload.append(buf)
-                got = scatter_frames_from_root(payload, shape, dev)
+                        fr = src.read(*segs[rnd[k]]) if k < len(rnd) else []
+                        stats["reads"] += k < len(rnd)
+                        stats["roots"] = stats.get("roots", 0) + (k == 0)
+                        payload.append(stage_segment_frames(fr, shape, dev))
+                got = scatter_frames_from_root(payload, shape, dev, root=root)
                 if rank < len(rnd):
                     i = rnd[rank]
                     n = segs[i][1]
