@@ -727,3 +727,99 @@ size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
 }
 
 }  // namespace tv
+
+// ------------------------------------------------------------------ table export --------
+// Every H.265 table the encoder (and its decoder oracle) codes with, exported by name for
+// tests/test_hevc_spec_tables.py, which diffs them against an independently transcribed copy
+// that shares no header with csrc/.  Returns the number of values (written to out when cap
+// allows), -1 for an unknown name.  "ctx:<element>" = the element's init values, initType 0
+// (I), 1 (P), 2 (B) concatenated, as the spec's ctxIdx tables list them.
+namespace {
+struct CtxRange {
+  const char* name;
+  int off, n;
+};
+constexpr CtxRange kCtxRanges[] = {
+    {"sao_merge_flag", tv::CTX_SAO_MERGE, 1},        {"sao_type_idx", tv::CTX_SAO_TYPE, 1},
+    {"split_cu_flag", tv::CTX_SPLIT_CU, 3},          {"cu_transquant_bypass_flag", tv::CTX_TQ_BYPASS, 1},
+    {"cu_skip_flag", tv::CTX_CU_SKIP, 3},            {"pred_mode_flag", tv::CTX_PRED_MODE, 1},
+    {"part_mode", tv::CTX_PART_MODE, 1},             {"prev_intra_luma_pred_flag", tv::CTX_PREV_INTRA, 1},
+    {"intra_chroma_pred_mode", tv::CTX_CHROMA_PRED, 1}, {"rqt_root_cbf", tv::CTX_RQT_ROOT_CBF, 1},
+    {"merge_flag", tv::CTX_MERGE_FLAG, 1},           {"merge_idx", tv::CTX_MERGE_IDX, 1},
+    {"inter_pred_idc", tv::CTX_INTER_PRED_IDC, 5},   {"ref_idx", tv::CTX_REF_IDX, 2},
+    {"mvp_flag", tv::CTX_MVP_FLAG, 1},               {"split_transform_flag", tv::CTX_SPLIT_TF, 3},
+    {"cbf_luma", tv::CTX_CBF_LUMA, 2},               {"cbf_chroma", tv::CTX_CBF_CHROMA, 4},
+    {"abs_mvd_greater0_flag", tv::CTX_MVD_G0, 1},    {"abs_mvd_greater1_flag", tv::CTX_MVD_G1, 1},
+    {"cu_qp_delta_abs", tv::CTX_CU_QP_DELTA, 2},     {"transform_skip_flag", tv::CTX_TRANSFORM_SKIP, 2},
+    {"last_sig_coeff_x_prefix", tv::CTX_LAST_X, 18}, {"last_sig_coeff_y_prefix", tv::CTX_LAST_Y, 18},
+    {"coded_sub_block_flag", tv::CTX_CSBF, 4},       {"sig_coeff_flag", tv::CTX_SIG, 44},
+    {"coeff_abs_level_greater1_flag", tv::CTX_G1, 24}, {"coeff_abs_level_greater2_flag", tv::CTX_G2, 6},
+};
+}  // namespace
+
+extern "C" int tv_hevc_spec_table(const char* name, int* out, int cap) {
+  using namespace tv;
+  std::vector<int> v;
+  const std::string s(name ? name : "");
+  auto put = [&](const auto* a, int n) {
+    for (int i = 0; i < n; ++i) v.push_back((int)a[i]);
+  };
+  if (s.rfind("ctx:", 0) == 0) {
+    bool found = false;
+    for (const auto& r : kCtxRanges)
+      if (s.compare(4, std::string::npos, r.name) == 0) {
+        for (int t = 0; t < 3; ++t)
+          for (int i = 0; i < r.n; ++i) v.push_back(ctx_init_table().v[t][r.off + i]);
+        found = true;
+      }
+    if (!found) return -1;
+  } else if (s == "range_tab_lps") {
+    put(&kRangeTabLps[0][0], 256);
+  } else if (s == "trans_idx_lps") {
+    put(kTransIdxLps, 64);
+  } else if (s == "trans_idx_mps") {
+    put(kTransIdxMps, 64);
+  } else if (s == "ctx_idx_map") {
+    put(kCtxIdxMap4x4, 16);
+  } else if (s == "group_idx") {
+    put(kGroupIdx, 32);
+  } else if (s == "min_in_group") {
+    put(kMinInGroup, 10);
+  } else if (s == "dct32") {
+    put(&kDct32.m[0][0], 1024);
+  } else if (s == "level_scale") {
+    for (int q = 0; q < 6; ++q) v.push_back(level_scale(q));
+  } else if (s == "beta") {
+    put(kBetaTable, 52);
+  } else if (s == "tc") {
+    put(kTcTable, 54);
+  } else if (s == "chroma_qp") {  // QpC of qPi = 0..57 (4:2:0)
+    for (int q = 0; q <= 57; ++q) v.push_back(chroma_qp(q, 0));
+  } else if (s == "intra_pred_angle") {
+    put(kIntraPredAngle, 35);
+  } else if (s == "inv_angle") {
+    put(kInvAngle, 15);
+  } else if (s == "intra_filter") {  // filterFlag of (log2 size 2..5, mode 0..34)
+    for (int l = 2; l <= 5; ++l)
+      for (int m = 0; m < 35; ++m) v.push_back(intra_filter_refs(l, m) ? 1 : 0);
+  } else if (s == "luma_filter") {
+    put(&kLumaFilter[0][0], 32);
+  } else if (s == "chroma_filter") {
+    put(&kChromaFilter[0][0], 32);
+  } else if (s == "scan_diag4x4") {
+    put(kScanDiag4x4, 16);
+  } else if (s == "scan_hor4x4") {
+    put(kScanHor4x4, 16);
+  } else if (s == "scan_ver4x4") {
+    put(kScanVer4x4, 16);
+  } else if (s == "scan_diag8x8") {
+    put(kScanDiag8x8.s, 64);
+  } else if (s == "scan_idx") {  // scanIdx of (log2 size 2..3, mode 0..34), intra luma
+    for (int l = 2; l <= 3; ++l)
+      for (int m = 0; m < 35; ++m) v.push_back(scan_idx_for(true, l, 0, m));
+  } else {
+    return -1;
+  }
+  for (int i = 0; i < (int)v.size() && i < cap; ++i) out[i] = v[i];
+  return (int)v.size();
+}
