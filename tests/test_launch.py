@@ -90,3 +90,16 @@ def test_visible_gpu_count_without_hip(monkeypatch):
         monkeypatch.delenv(v, raising=False)
     monkeypatch.setattr(launch, "gpu_numa_nodes", lambda: [0, 0, 1, 1])
     assert launch.visible_gpu_count() == 4
+
+
+def test_tv_cpus_caps_the_rank_cpu_set(tmp_path):
+    """TV_CPUS=N restricts a rank (and the CABAC pool it spawns later) to N CPUs."""
+    script = tmp_path / "c.py"
+    script.write_text(f"import os, sys\nsys.path.insert(0, {ROOT!r})\n"
+                      "from thinvids_amd.parallel.launch import pin_rank\n"
+                      "c = pin_rank(0, 1)\nprint(len(c), len(os.sched_getaffinity(0)))\n")
+    env = dict(os.environ, TV_CPUS="2")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=60)
+    a, b = map(int, r.stdout.split())
+    want = min(2, len(os.sched_getaffinity(0)))
+    assert a == b == want, r.stdout + r.stderr

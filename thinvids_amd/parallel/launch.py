@@ -168,15 +168,23 @@ def plan_affinity(local_rank: int, local_world: int, allowed: list[int] | None =
 
 def pin_rank(local_rank: int, local_world: int) -> list[int]:
     """Apply :func:`plan_affinity` to this process (inherited by the engine's CABAC threads,
-    which are created later).  No-op when TV_NO_PIN=1 or the platform lacks affinity."""
-    if os.environ.get("TV_NO_PIN") == "1" or not hasattr(os, "sched_setaffinity"):
+    which are created later).  ``TV_CPUS=N`` caps the rank at the first N CPUs of its set
+    (the "1/8 of a host" experiment: an 8-GPU node's per-rank share on any box).  Pinning is
+    skipped when TV_NO_PIN=1 (the cap still applies) or the platform lacks affinity."""
+    if not hasattr(os, "sched_setaffinity"):
         return sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
-    gpu_nodes = None
-    phys = [int(x) for x in os.environ.get("TV_PHYS_GPUS", "").split(",") if x.strip()]
-    if phys:  # a supervisor restarted this node on a subset of its GPUs (HIP_VISIBLE_DEVICES)
-        allg = gpu_numa_nodes()
-        gpu_nodes = [allg[g] if g < len(allg) else 0 for g in phys]
-    cpus = plan_affinity(local_rank, local_world, gpu_nodes=gpu_nodes)
+    cap = int(os.environ.get("TV_CPUS", "0") or 0)
+    if os.environ.get("TV_NO_PIN") == "1":
+        cpus = sorted(os.sched_getaffinity(0))
+    else:
+        gpu_nodes = None
+        phys = [int(x) for x in os.environ.get("TV_PHYS_GPUS", "").split(",") if x.strip()]
+        if phys:  # a supervisor restarted this node on a subset of its GPUs (HIP_VISIBLE_DEVICES)
+            allg = gpu_numa_nodes()
+            gpu_nodes = [allg[g] if g < len(allg) else 0 for g in phys]
+        cpus = plan_affinity(local_rank, local_world, gpu_nodes=gpu_nodes)
+    if cap > 0:
+        cpus = cpus[:cap]
     try:
         os.sched_setaffinity(0, cpus)
     except OSError:
