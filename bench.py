@@ -302,7 +302,9 @@ def job_main(args) -> None:
                    "job_wall_s": round(el, 3), "job_fps_reported": float(job.get("job_fps") or 0),
                    "encode_fps_reported": float(job.get("encode_fps") or 0), "psnr_y_db": float(job.get("psnr_y") or 0),
                    "kbps": float(job.get("bitrate_kbps") or 0), "segments": int(job.get("parts_total") or 0),
-                   "output_bytes": int(job.get("dest_file_size") or 0)},
+                   "output_bytes": int(job.get("dest_file_size") or 0),
+                   "encode_elapsed_s": float(job.get("encode_elapsed") or 0), "run_job_s": float(job.get("job_seconds") or 0),
+                   "rank0_spans_ms": {k: v for k, v in json.loads(job.get("trace_json") or "{}").items()}},
     }), flush=True)
     srv.shutdown()
 

@@ -244,9 +244,8 @@ class Av1GpuEngine:
             nu = lr_grid(w) * lr_grid(h)
             prm = torch.empty((B, nu, 3), dtype=torch.int32, device=self.dev)
             o = torch.empty_like(X)
-            cand = torch.empty((len(LR_SETS),) + tuple(X.shape), dtype=torch.uint8, device=self.dev)
             rc = ops._gpu().tv_gpu_sgr_select(_p(S), _p(X), _p(D), w, h, 1 if p else 0, B, _p(rate), _p(prm),
-                                              _p(cand), _p(o), st)
+                                              _p(o), st)
             if rc != 0:
                 raise RuntimeError(ops._gpu().tv_av1_gpu_last_error().decode())
             self.g_lr[t, :B, p, :nu] = prm

@@ -309,6 +309,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     from .comm import allreduce_stats, gather_bytes_to_root, scatter_frames_from_root, scatter_root, stage_segment_frames
 
     hooks = hooks or JobHooks()
+    trace0 = trace.summary()
     _job_seq[0] += 1
     job_tag = f"j{_job_seq[0]}"  # rendezvous-store keys of this job (a long-lived executor runs many)
     dist = _dist()
@@ -396,7 +397,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             with trace.span("node_job.encode", segments=len(todo)):
                 got, qual = _encode_many(todo, cache)
             for (r, i), b in got.items():
-                ckpt.save(r, i, plans[(r, i)][1], b)
+                with trace.span("node_job.ckpt_save"):
+                    ckpt.save(r, i, plans[(r, i)][1], b)
                 out[(r, i)] = b
                 quality[(r, i)] = qual[(r, i)]
                 stats["encoded"] += 1
@@ -407,8 +409,9 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             q = plans[(r, i)][0]
             if q is not None:  # rate feedback: actual vs the model's prediction at these QPs
                 rc["fb"].record(8.0 * sum(fb), float(predict_bits(rc["b1"][(r, i)], qp, q).sum()))
-        for i in seg_ids:
-            hooks.segment_done(segs[i][1])
+        with trace.span("node_job.hooks"):
+            for i in seg_ids:
+                hooks.segment_done(segs[i][1])
         return out
 
     def encode_pass() -> dict:
@@ -474,7 +477,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 if hooks.halted():
                     wq.fail_all("job halted")
                     raise RuntimeError("job halted")
-                claimed = wq.claim(batch_segments)  # a batch -> one batched launch per rung
+                with trace.span("node_job.claim"):
+                    claimed = wq.claim(batch_segments)  # a batch -> one batched launch per rung
                 if not claimed:
                     break
                 run(claimed)
@@ -513,7 +517,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             got = encode_pass()
         except Exception as e:  # noqa: BLE001 - re-raised below on every rank
             err = e
-        failed = allreduce_stats([1.0 if err else 0.0], cdev, op="max")[0]
+        with trace.span("node_job.verdict"):
+            failed = allreduce_stats([1.0 if err else 0.0], cdev, op="max")[0]
         if failed:
             raise err if err is not None else RuntimeError("a peer rank failed this job")
         return got
@@ -595,7 +600,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         if missing:
             raise RuntimeError(f"segments missing at stitch: {missing}")
         outs = []
-        side = _side_plan(input_path, audio_stream)
+        with trace.span("node_job.side_plan"):
+            side = _side_plan(input_path, audio_stream)
         for r, (ow, oh) in enumerate(rungs):
             seg_bits = [streams[(r, i)] for i in range(len(segs))]
             path = output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4"
@@ -609,7 +615,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                          "quality_frames": int(qv[r, 0])})
         el = time.time() - t0
         result.update(side_fields=side.fields if side else {}, side_warnings=side.warnings if side else [])
-        result.update(trace=trace.summary(), per_rank=per_rank, outputs=outs, qp_plan=[[round(float(np.mean(q)), 2) for q in row] for row in rc["plan"]] if rc["plan"] else
+        result.update(trace=trace.since(trace0), per_rank=per_rank, outputs=outs, qp_plan=[[round(float(np.mean(q)), 2) for q in row] for row in rc["plan"]] if rc["plan"] else
                       [[qp] * len(segs) for _ in rungs], rc_offset=round(rc["fb"].offset(), 3),
                       seconds=round(el, 3), encode_seconds=round(t_enc, 3),
                       fps=round(nfr * len(rungs) / el, 2), encode_fps=round(nfr * len(rungs) * passes / max(t_enc, 1e-9), 2))

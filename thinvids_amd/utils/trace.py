@@ -95,6 +95,18 @@ def summary(reset: bool = False) -> dict:
     return out
 
 
+def since(before: dict) -> dict:
+    """The spans recorded after the :func:`summary` snapshot `before` (count / total per
+    name; max_ms is over the whole process)."""
+    out = {}
+    for k, v in summary().items():
+        b = before.get(k, {"count": 0, "total_ms": 0.0})
+        c, t = v["count"] - b["count"], round(v["total_ms"] - b["total_ms"], 3)
+        if c > 0:
+            out[k] = {"count": c, "total_ms": t, "max_ms": v["max_ms"], "avg_ms": round(t / c, 3)}
+    return out
+
+
 def _trace_file() -> str | None:
     return os.environ.get("TV_TRACE_FILE")
 

@@ -245,7 +245,9 @@ def _publish(job_id: str, spec: dict, res: dict) -> None:
               "encode_elapsed": round(res.get("encode_seconds", 0.0), 2), "job_fps": res.get("fps"),
               "encode_fps": res.get("encode_fps"), "psnr_y": outs[0].get("psnr_y"), "psnr_yuv": outs[0].get("psnr_yuv"),
               "bitrate_kbps": round(outs[0]["kbps"], 1), "rc_passes": res.get("passes", 1),
-              "qp_plan_json": json.dumps(res.get("qp_plan", [])[:1]), "ladder_outputs_json": json.dumps(
+              "qp_plan_json": json.dumps(res.get("qp_plan", [])[:1]),
+              "trace_json": json.dumps(res.get("trace") or {}), "job_seconds": res.get("seconds"),
+              "ladder_outputs_json": json.dumps(
                   [{"path": f, "width": o["width"], "height": o["height"], "kbps": round(o["kbps"], 1),
                     "psnr_y": o.get("psnr_y")} for f, o in zip(finals, outs)]) if len(outs) > 1 else ""}
     # dest_* from the muxer's own accounting (re-probing a multi-GB output would read it back)
