@@ -521,184 +521,234 @@ __global__ void __launch_bounds__(256) k_sgr_search(const uint8_t* __restrict__ 
 }
 
 // Encoder restoration choice per normative restoration unit (av1_defs.h lr_* geometry; 7.17
-// stripes), fused over the candidate sets: the unit's SSE unrestored, then for each set of
-// lr_set() the guided filters -> projection statistics -> sgr_solve -> projection + SSE; the
-// first minimum of SSE + rate (rate[b] = lr_rate_cost of segment b's q-index, 0 when
-// unrestored) wins.  Per stripe chunk of the unit, the source tile (CDEF output inside the
-// stripe, up to 2 deblocked rows beyond it, clamped at the plane edges) and the (A, B) planes
-// of a pass are staged in LDS; F0 / F1 of the chunk stay in LDS for the statistics and the
-// projection.  Candidate outputs go to cand[k] (scratch); the chosen one to `out`.  The
-// golden encoder's decision (av1_codec.cpp) bit for bit.
+// stripes), fused over the candidate sets of lr_set(): the unit's SSE unrestored, then per
+// set the guided filters -> projection statistics -> sgr_solve -> projection SSE; the first
+// minimum of SSE + rate (rate[b] = lr_rate_cost of segment b's q-index, 0 when unrestored)
+// wins and only the winner is written.  The golden encoder's decision (av1_codec.cpp) bit for
+// bit.
+//
+// Layout: 512 threads own the unit's pixels (q = tid + 512 n, row-major) in registers: the
+// CDEF | source samples and, per set, the packed guided outputs F0 | F1 << 16.  Per stripe
+// chunk the source tile (CDEF output inside the stripe, up to 2 deblocked rows beyond it,
+// clamped at the plane edges) is staged in LDS ONCE for every set (batched loads, all in
+// flight together), the box sums of a pass are computed once and turned into the (A, B)
+// planes of every set that uses the pass (the radius-1 sums serve sets 4 and 10 alike), and
+// each thread filters its own pixels straight into registers (no F plane in LDS); A and B
+// share one LDS word.  LDS ~60 KB.
 constexpr int kLrCh = 64, kLrUw = 96;  // max stripe chunk height, max unit width (round layout)
 constexpr int kLrTw = kLrUw + 6, kLrAw = kLrUw + 2;
+constexpr int kLrThreads = 512, kLrMaxPx = 104 * 96, kLrPer = (kLrMaxPx + kLrThreads - 1) / kLrThreads;  // unit <= 103 x 95
+constexpr int kLrBatch = 5;  // tile loads per thread in flight together
 
-__device__ void lr_chunk_flt(const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, int s0, int ya, int yb,
-                             int x0, int x1, int set, const uint16_t* xt, uint8_t (*T)[kLrTw],
-                             uint16_t (*A)[kLrAw], uint16_t (*Bv)[kLrAw], int16_t (*F)[2][kLrUw]) {
-  const int uw = x1 - x0, ch = yb - ya, th = ch + 6, tw = uw + 6;
-  for (int q = threadIdx.x; q < th * tw; q += blockDim.x) {
-    const int ty = q / tw, tx = q - ty * tw;
-    bool db;
-    const int yy = lr_src_row(ya - 3 + ty, h, s0, ss, &db), xx = clampi(x0 - 3 + tx, 0, w - 1);
-    T[ty][tx] = (db ? dbk : cdef)[(long)yy * w + xx];
-  }
-  __syncthreads();
-  for (int pass = 0; pass < 2; ++pass) {
-    const int r = sgr_param(set, 2 * pass), sp = sgr_param(set, 2 * pass + 1);
-    if (!r) {
-      for (int q = threadIdx.x; q < ch * uw; q += blockDim.x) {
-        const int i = q / uw, j = q - i * uw;
-        F[i][pass][j] = (int16_t)((int)T[i + 3][j + 3] << kSgrRstBits);
-      }
-      continue;
-    }
-    const int ah = ch + 2, aw = uw + 2;
-    for (int q = threadIdx.x; q < ah * aw; q += blockDim.x) {
-      const int i = q / aw, j = q - i * aw;  // position (ya - 1 + i, x0 - 1 + j) = tile (i + 2, j + 2)
-      if (pass == 0 && !((ya - 1 + i) & 1)) continue;  // the radius-2 pass reads odd rows only
-      int sum = 0, sq = 0;
-      for (int dy = -r; dy <= r; ++dy)
-        for (int dx = -r; dx <= r; ++dx) {
-          const int v = T[i + 2 + dy][j + 2 + dx];
-          sum += v;
-          sq += v * v;
-        }
-      int a, bb;
-      sgr_ab_x(sum, sq, r, sp, [&](unsigned z) -> int { return xt[z < 255u ? z : 255u]; }, &a, &bb);
-      A[i][j] = (uint16_t)a;
-      Bv[i][j] = (uint16_t)bb;
-    }
-    __syncthreads();
-    for (int q = threadIdx.x; q < ch * uw; q += blockDim.x) {
-      const int i = q / uw, j = q - i * uw;
-      F[i][pass][j] = (int16_t)sgr_output(
-          pass, ya + i, (int)T[i + 3][j + 3], [&](int dy, int dx) -> int { return A[i + 1 + dy][j + 1 + dx]; },
-          [&](int dy, int dx) -> int { return Bv[i + 1 + dy][j + 1 + dx]; });
-    }
-    __syncthreads();
-  }
+// q / d for 0 <= q < 2^20, 1 <= d <= 128 by a float reciprocal: (q + 0.5) / d lies >= 0.5 / d
+// away from an integer, far beyond the float error
+__device__ __forceinline__ int lr_div(int q, float rd) { return (int)(((float)q + 0.5f) * rd); }
+// a value the compiler must treat as unknown at this point: keeps it from hoisting the 20
+// per-pixel (row, column) pairs out of the chunk loop into live registers
+__device__ __forceinline__ float lr_opaque(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
 }
 
-constexpr int kLrThreads = 512, kLrMaxPx = 104 * 96, kLrPer = (kLrMaxPx + kLrThreads - 1) / kLrThreads;  // unit <= 103 x 95
-
 __global__ void __launch_bounds__(kLrThreads) k_sgr_select(const uint8_t* __restrict__ src, const uint8_t* __restrict__ cdef,
-                                                    const uint8_t* __restrict__ dbk, int w, int h, int ss,
-                                                    const long long* __restrict__ rate, int* __restrict__ prm,
-                                                    uint8_t* __restrict__ cand, uint8_t* __restrict__ out) {
+                                                       const uint8_t* __restrict__ dbk, int w, int h, int ss,
+                                                       const long long* __restrict__ rate, int* __restrict__ prm,
+                                                       uint8_t* __restrict__ out) {
   const int b = blockIdx.y, u = blockIdx.x, nux = lr_count_units(w);
   const int ur = u / nux, uc = u - ur * nux, nu = nux * lr_count_units(h);
   int x0, x1, y0, y1;
   lr_unit_cols(uc, w, &x0, &x1);
   lr_unit_rows(ur, h, ss, &y0, &y1);
-  const int uw = x1 - x0, npx = (y1 - y0) * uw, S = 64 >> ss;
-  const long po = (long)b * w * h, psz = (long)gridDim.y * w * h;
+  const int uw = x1 - x0, npx = (y1 - y0) * uw, S = 64 >> ss, aw = uw + 2, tw = uw + 6;
+  const float ruw = 1.f / (float)uw, raw = 1.f / (float)aw, rtw = 1.f / (float)tw;
+  const long po = (long)b * w * h;
   const uint8_t* C = cdef + po;
   const uint8_t* D = dbk + po;
   __shared__ uint8_t T[kLrCh + 6][kLrTw];
-  __shared__ uint16_t A[kLrCh + 2][kLrAw], Bv[kLrCh + 2][kLrAw], xt[256];
-  __shared__ int16_t F[kLrCh][2][kLrUw];
+  __shared__ uint32_t AB[kNumLrSets][kLrCh + 2][kLrAw];  // A | B << 16
+  __shared__ uint16_t xt[256];
   __shared__ unsigned long long red[1 + 6 * kNumLrSets];
-  __shared__ int xq[2];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) xt[i] = (uint16_t)sgr_xbyx1(threadIdx.x);
+  __shared__ int xq[kNumLrSets][2];
+  if (threadIdx.x < 256) xt[threadIdx.x] = (uint16_t)sgr_xbyx1(threadIdx.x);
   if (threadIdx.x < 1 + 6 * kNumLrSets) red[threadIdx.x] = 0;
-  __syncthreads();
   auto block_add = [&](long long v, int slot) {
     v = wave_sum64(v);
     if ((threadIdx.x & 63) == 0) atomicAdd(&red[slot], (unsigned long long)v);
   };
-  // the thread's pixels (q = tid + kLrThreads n, row-major over the unit): CDEF and source samples
-  // and, per set, the packed guided outputs F0 | F1 << 16, kept in registers across the
-  // statistics -> solve -> projection steps (the filters run once per set)
-  uint32_t xs[kLrPer], fv[kLrPer];
+  // xp: CDEF | source << 8 of pixel n in half-word n & 1 of xp[n >> 1]
+  uint32_t xp[(kLrPer + 1) / 2], fv[kNumLrSets][kLrPer];
+#define XS(n) ((xp[(n) >> 1] >> (((n) & 1) * 16)) & 0xFFFFu)
   long long e0 = 0;
 #pragma unroll
   for (int n = 0; n < kLrPer; ++n) {
     const int q = threadIdx.x + kLrThreads * n;
-    xs[n] = 0;
+    if (!(n & 1)) xp[n >> 1] = 0;
+    if (n % 5 == 0) asm volatile("" ::: "memory");  // at most 5 pixels' loads in flight: bounds the address registers
     if (q < npx) {
-      const int i = q / uw, j = q - i * uw;
+      const int i = lr_div(q, ruw), j = q - i * uw;
       const long o = (long)(y0 + i) * w + x0 + j;
       const int c = C[o], sv = src[po + o];
-      xs[n] = (uint32_t)c | ((uint32_t)sv << 8);
+      xp[n >> 1] |= ((uint32_t)c | ((uint32_t)sv << 8)) << ((n & 1) * 16);
       e0 += (c - sv) * (c - sv);
     }
+    const uint32_t uu = (XS(n) & 255) << kSgrRstBits;  // a radius-0 pass outputs the sample itself
+#pragma unroll
+    for (int k = 0; k < kNumLrSets; ++k) fv[k][n] = uu | (uu << 16);
   }
-  block_add(e0, 0);
-  __syncthreads();
-  long long best = (long long)red[0];
-  int bk = -1, b0 = 0, b1 = 0;
-  const long long rt = rate[b];
-  for (int k = 0; k < kNumLrSets; ++k) {
-    const int set = lr_set(k), r0 = sgr_param(set, 0), r1 = sgr_param(set, 2), sl = 1 + 6 * k;
-    for (int s0 = lr_stripe_start(y0, ss); s0 < y1; s0 += S) {
-      const int ya = s0 > y0 ? s0 : y0, yb = s0 + S < y1 ? s0 + S : y1;
-      lr_chunk_flt(C, D, w, h, ss, s0, ya, yb, x0, x1, set, xt, T, A, Bv, F);
+  for (int s0 = lr_stripe_start(y0, ss); s0 < y1; s0 += S) {
+    const int ya = s0 > y0 ? s0 : y0, yb = s0 + S < y1 ? s0 + S : y1, ntl = (yb - ya + 6) * tw;
+    for (int q0 = threadIdx.x; q0 < ntl; q0 += kLrThreads * kLrBatch) {  // kLrBatch loads in flight
+      uint8_t tv[kLrBatch];
+#pragma unroll
+      for (int n = 0; n < kLrBatch; ++n) {
+        const int q = q0 + kLrThreads * n;
+        if (q < ntl) {
+          const int ty = lr_div(q, rtw), tx = q - ty * tw;
+          bool db;
+          const int yy = lr_src_row(ya - 3 + ty, h, s0, ss, &db), xx = clampi(x0 - 3 + tx, 0, w - 1);
+          tv[n] = (db ? D : C)[(long)yy * w + xx];
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < kLrBatch; ++n) {
+        const int q = q0 + kLrThreads * n;
+        if (q < ntl) {
+          const int ty = lr_div(q, rtw);
+          T[ty][q - ty * tw] = tv[n];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      bool used = false;
+#pragma unroll
+      for (int k = 0; k < kNumLrSets; ++k) used |= sgr_param(lr_set(k), 2 * pass) != 0;
+      if (!used) continue;
+      // (A, B) rows y in [ya - 1, yb + 1) (pass 0: odd rows only) x columns [x0 - 1, x1 + 1)
+      const int r = pass ? 1 : 2, step = pass ? 1 : 2, fy = pass ? ya - 1 : ((ya - 1) | 1);
+      const int nr = pass ? yb - ya + 2 : (yb + 1 - fy + 1) >> 1;
+      for (int q = threadIdx.x; q < nr * aw; q += kLrThreads) {
+        const int ri = lr_div(q, raw), j = q - ri * aw, i = fy + step * ri - (ya - 1);
+        int sum = 0, sq = 0;
+        for (int dy = -r; dy <= r; ++dy)
+          for (int dx = -r; dx <= r; ++dx) {
+            const int v = T[i + 2 + dy][j + 2 + dx];
+            sum += v;
+            sq += v * v;
+          }
+#pragma unroll
+        for (int k = 0; k < kNumLrSets; ++k) {
+          if (!sgr_param(lr_set(k), 2 * pass)) continue;
+          int a, bb;
+          sgr_ab_x(sum, sq, r, sgr_param(lr_set(k), 2 * pass + 1),
+                   [&](unsigned z) -> int { return xt[z < 255u ? z : 255u]; }, &a, &bb);
+          AB[k][i][j] = (uint32_t)a | ((uint32_t)bb << 16);
+        }
+      }
+      __syncthreads();
+      const float ru = lr_opaque(ruw);
 #pragma unroll
       for (int n = 0; n < kLrPer; ++n) {
         const int q = threadIdx.x + kLrThreads * n;
-        const int i = q / uw, j = q - i * uw, yy = y0 + i;
-        if (q < npx && yy >= ya && yy < yb)
-          fv[n] = (uint32_t)(uint16_t)F[yy - ya][0][j] | ((uint32_t)(uint16_t)F[yy - ya][1][j] << 16);
+        const int i = lr_div(q, ru), j = q - i * uw, yy = y0 + i, ci = yy - ya;
+        if (q >= npx || yy < ya || yy >= yb) continue;
+        const int c = XS(n) & 255;
+#pragma unroll
+        for (int k = 0; k < kNumLrSets; ++k) {
+          if (!sgr_param(lr_set(k), 2 * pass)) continue;
+          uint32_t nb[3][3];  // one LDS read per neighbour for both coefficients
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+              nb[dy][dx] = (pass || ((yy + dy - 1) & 1)) ? AB[k][ci + dy][j + dx] : 0u;
+          const uint32_t f = (uint16_t)sgr_output(
+              pass, yy, c, [&](int dy, int dx) -> int { return nb[dy + 1][dx + 1] & 0xFFFF; },
+              [&](int dy, int dx) -> int { return nb[dy + 1][dx + 1] >> 16; });
+          fv[k][n] = pass ? (fv[k][n] & 0xFFFFu) | (f << 16) : (fv[k][n] & 0xFFFF0000u) | f;
+        }
       }
-      __syncthreads();  // T / A / F reused by the next chunk
+      __syncthreads();  // A / B (and T after pass 1) reused next
     }
-    long long acc[5] = {0, 0, 0, 0, 0};
+  }
+  // projection statistics of every set -> solve
+  block_add(e0, 0);
+#pragma unroll
+  for (int k = 0; k < kNumLrSets; ++k) {
+    // |F - u| < 2^12: the squares and cross term fit 32 bits per pixel and per thread (<= 20
+    // pixels); the source correlation terms (<< kSgrPrjBits) need 64
+    int q00 = 0, q01 = 0, q11 = 0;
+    long long q0e = 0, q1e = 0;
 #pragma unroll
     for (int n = 0; n < kLrPer; ++n) {
       if (threadIdx.x + kLrThreads * n >= npx) continue;
-      const int uu = (int)(xs[n] & 255) << kSgrRstBits;
-      const long long da = (int)(int16_t)(fv[n] & 0xFFFF) - uu, db = (int)(int16_t)(fv[n] >> 16) - uu;
-      const long long e = ((long long)((int)(xs[n] >> 8) << kSgrRstBits) - uu) << kSgrPrjBits;
-      acc[0] += da * da;
-      acc[1] += da * db;
-      acc[2] += db * db;
-      acc[3] += da * e;
-      acc[4] += db * e;
+      const int uu = (int)(XS(n) & 255) << kSgrRstBits;
+      const int da = (int)(int16_t)(fv[k][n] & 0xFFFF) - uu, db = (int)(int16_t)(fv[k][n] >> 16) - uu;
+      const int e = ((int)(XS(n) >> 8) << kSgrRstBits) - uu;
+      q00 += da * da;
+      q01 += da * db;
+      q11 += db * db;
+      q0e += (long long)(da * e);
+      q1e += (long long)(db * e);
     }
+    const long long acc[5] = {q00, q01, q11, q0e << kSgrPrjBits, q1e << kSgrPrjBits};
 #pragma unroll
-    for (int c = 0; c < 5; ++c) block_add(acc[c], sl + c);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      long long st[5];
-      for (int c = 0; c < 5; ++c) st[c] = (long long)red[sl + c];
-      sgr_solve(st, r0, r1, &xq[0], &xq[1]);
-    }
-    __syncthreads();
+    for (int c = 0; c < 5; ++c) block_add(acc[c], 1 + 6 * k + c);
+  }
+  __syncthreads();
+  if (threadIdx.x < kNumLrSets) {
+    const int k = threadIdx.x, set = lr_set(k);
+    long long st[5];
+    for (int c = 0; c < 5; ++c) st[c] = (long long)red[1 + 6 * k + c];
+    sgr_solve(st, sgr_param(set, 0), sgr_param(set, 2), &xq[k][0], &xq[k][1]);
+  }
+  __syncthreads();
+  // projection SSE of every set; the winner is written from the registers
+#pragma unroll
+  for (int k = 0; k < kNumLrSets; ++k) {
+    const int set = lr_set(k), r0 = sgr_param(set, 0), r1 = sgr_param(set, 2), w0 = xq[k][0], w1 = xq[k][1];
     long long e2 = 0;
 #pragma unroll
     for (int n = 0; n < kLrPer; ++n) {
-      const int q = threadIdx.x + kLrThreads * n;
-      if (q >= npx) continue;
-      const int i = q / uw, j = q - i * uw;
-      const int x = xs[n] & 255, sv = xs[n] >> 8;
-      const int v = sgr_project_xqd(x, (int16_t)(fv[n] & 0xFFFF), (int16_t)(fv[n] >> 16), r0, r1, xq[0], xq[1]);
-      cand[k * psz + po + (long)(y0 + i) * w + x0 + j] = (uint8_t)v;
-      e2 += (v - sv) * (v - sv);
+      if (threadIdx.x + kLrThreads * n >= npx) continue;
+      const int v = sgr_project_xqd(XS(n) & 255, (int16_t)(fv[k][n] & 0xFFFF), (int16_t)(fv[k][n] >> 16), r0, r1, w0, w1);
+      const int d = v - (int)(XS(n) >> 8);
+      e2 += d * d;
     }
-    block_add(e2, sl + 5);
-    __syncthreads();
-    const long long ek = (long long)red[sl + 5] + rt;
-    if (ek < best) {  // block-uniform
-      best = ek;
-      bk = k;
-      b0 = xq[0];
-      b1 = xq[1];
-    }
-    __syncthreads();  // xq reused by the next set
+    block_add(e2, 1 + 6 * k + 5);
   }
-  const uint8_t* O = bk < 0 ? C : cand + bk * psz + po;
-  for (int q = threadIdx.x; q < npx; q += blockDim.x) {
-    const int i = q / uw, j = q - i * uw;
-    const long o = (long)(y0 + i) * w + x0 + j;
-    out[po + o] = O[o];
+  __syncthreads();
+  long long best = (long long)red[0];
+  int bk = -1;
+  const long long rt = rate[b];
+  for (int k = 0; k < kNumLrSets; ++k)
+    if ((long long)red[1 + 6 * k + 5] + rt < best) {  // block-uniform
+      best = (long long)red[1 + 6 * k + 5] + rt;
+      bk = k;
+    }
+  const float ru = lr_opaque(ruw);  // recompute (row, column): not kept live from the first loop
+#pragma unroll
+  for (int n = 0; n < kLrPer; ++n) {
+    const int q = threadIdx.x + kLrThreads * n;
+    if (q >= npx) continue;
+    const int i = lr_div(q, ru), j = q - i * uw, x = XS(n) & 255;
+    int v = x;
+#pragma unroll
+    for (int k = 0; k < kNumLrSets; ++k)
+      if (k == bk)
+        v = sgr_project_xqd(x, (int16_t)(fv[k][n] & 0xFFFF), (int16_t)(fv[k][n] >> 16), sgr_param(lr_set(k), 0),
+                            sgr_param(lr_set(k), 2), xq[k][0], xq[k][1]);
+    out[po + (long)(y0 + i) * w + x0 + j] = (uint8_t)v;
   }
   if (threadIdx.x == 0) {
     int* P = prm + ((long)b * nu + u) * 3;
     P[0] = bk < 0 ? -1 : lr_set(bk);
-    P[1] = bk < 0 ? 0 : b0;
-    P[2] = bk < 0 ? 0 : b1;
+    P[1] = bk < 0 ? 0 : xq[bk][0];
+    P[2] = bk < 0 ? 0 : xq[bk][1];
   }
 }
+#undef XS
 
 // ----------------------------------------------------------------- deblocking filter ----
 // k_deblock: one workgroup per 64x64 output tile.  The tile plus an 8-pixel ring is staged
@@ -811,12 +861,13 @@ int tv_gpu_sgr_search(const uint8_t* src, const uint8_t* rec, int w, int h, int 
   return av1_status("sgr_search");
 }
 // encoder restoration choice over every lr_set() candidate: rate [B] (int64), prm
-// [B][nu][3], restored planes (unrestored units copied)
+// [B][nu][3], restored planes (unrestored units copied).  lr_count_units rounding keeps every
+// unit within 95 columns x 103 rows, the kernel's register / LDS footprint
 int tv_gpu_sgr_select(const uint8_t* src, const uint8_t* cdef, const uint8_t* dbk, int w, int h, int ss, int B,
-                      const long long* rate, int* prm, uint8_t* cand, uint8_t* out, void* stream) {
+                      const long long* rate, int* prm, uint8_t* out, void* stream) {
   if (bad_geo(w, h, B, 2, "sgr_select") || ss < 0 || ss > 1) return -1;
   const int nu = lr_count_units(w) * lr_count_units(h);
-  k_sgr_select<<<dim3(nu, B), kLrThreads, 0, (hipStream_t)stream>>>(src, cdef, dbk, w, h, ss, rate, prm, cand, out);
+  k_sgr_select<<<dim3(nu, B), kLrThreads, 0, (hipStream_t)stream>>>(src, cdef, dbk, w, h, ss, rate, prm, out);
   return av1_status("sgr_select");
 }
 int tv_gpu_wiener_apply(const uint8_t* rec, int w, int h, int B, const int* coef, uint8_t* out, void* stream) {
