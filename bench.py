@@ -346,12 +346,24 @@ def av1_main(args) -> None:
         return stats.cpu().numpy(), (sum(len(x) for x in gathered) if gathered else 0)
 
     pass1_bits = []
+    from thinvids_amd.models.ratecontrol import BatchRateController
 
-    def plan_pass2(g1fut):
+    ctl = BatchRateController()
+    nominal = args.kbps * 1000.0 * (world * batch * args.gop) / 30.0  # bits per step, whole node
+    predicted = {}
+
+    def comm_rc(i, gfut):
+        out = comm(gfut)
+        if args.kbps > 0:  # the post thread: every rank records the same all-reduced totals
+            ctl.record(nominal, predicted.pop(i), 8.0 * float(out[0][1]))
+        return out
+
+    def plan_pass2(i, g1fut):
         """Config #4's 2-pass, post thread (the only thread issuing collectives): pass-1
         per-frame bits of every rank's segments all-reduced over RCCL -> one global
-        per-frame plan for the target bitrate (ratecontrol.plan_frame_qps) -> this rank's
-        per-frame q-index maps for pass 2."""
+        per-frame plan for this step's share of the target, corrected by the finished steps'
+        bias and debt (ratecontrol.BatchRateController) -> this rank's per-frame q-index
+        maps for pass 2."""
         from thinvids_amd.models.ratecontrol import frame_sizes, plan_frame_qps, round_qps
 
         g1 = g1fut.result()
@@ -361,34 +373,50 @@ def av1_main(args) -> None:
         flat[rank * batch * args.gop:(rank + 1) * batch * args.gop] = torch.from_numpy(mine).to(dev)
         dist.all_reduce(flat)  # RC statistics all-reduce over the node
         allb = flat.cpu().numpy().reshape(world * batch, args.gop)
-        target = args.kbps * 1000.0 * (world * batch * args.gop) / 30.0
-        plan, _ = plan_frame_qps(list(allb), args.qp, target, key_offset=AV1_KEY_QP_OFFSET)
+        ask, _ = ctl.request(nominal)
+        plan, pred = plan_frame_qps(list(allb), args.qp, ask, key_offset=AV1_KEY_QP_OFFSET)
+        predicted[i] = pred
         pass1_bits.append(float(mine.sum()))
         return np.array([[av1m.qindex_for_hevc_qp(int(v)) for v in round_qps(plan[rank * batch + b])]
                          for b in range(batch)], np.int32).T
 
-    def step(s: int):
-        base = (s * world + rank) * batch
-        st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    def loader(i: int):
+        base = (i * world + rank) * batch
 
         def load(t, planes):
+            st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
             src = stage.synth_frames(args.seed, w, h, [(base + b) * args.gop + t for b in range(batch)], dev)
             for c, dst in enumerate(planes):
                 off, pw, ph, stride, fs = src.planes[c]
                 cw, chh = (W, H) if c == 0 else (W // 2, H // 2)
                 stage._ok(lib.tv_pad_batch(C.c_void_p(src.ptr(c)), pw, ph, stride, fs, C.c_void_p(dst.data_ptr()),
                                            cw, chh, cw, cw * chh, batch, st))
+        return load
 
+    plans = {}
+    counter = [0]
+
+    def pass1(i: int):  # pass 1 of step i on the GPU; its plan queues on the post thread
+        plans[i] = post.ex.submit(plan_pass2, i, eng.encode_gop(args.gop, loader(i), async_host=True))
+
+    def step(_s: int):
+        i = counter[0]
+        counter[0] += 1
         if args.kbps > 0:
-            # pass 1 on the GPU while the post thread entropy-codes the previous step's pass 2;
-            # the plan (pass-1 entropy + all-reduce) runs on the post thread in step order
-            g1 = eng.encode_gop(args.gop, load, async_host=True)
-            qm = post.ex.submit(plan_pass2, g1).result()
-            post.submit(comm, eng.encode_gop(args.gop, load, qmap=qm, async_host=True))
+            # software pipeline: step i runs pass 1 of step i + 1 on the GPU, then pass 2 of
+            # step i, whose plan (pass-1 entropy + all-reduce, post thread) was computed
+            # behind the previous step's GPU work -- the GPU never waits for the host plan
+            if i == 0:
+                pass1(0)
+            pass1(i + 1)
+            qm = plans.pop(i).result()
+            post.submit(comm_rc, i, eng.encode_gop(args.gop, loader(i), qmap=qm, async_host=True))
         else:
-            post.submit(comm, eng.encode_gop(args.gop, load, async_host=True))
+            post.submit(comm, eng.encode_gop(args.gop, loader(i), async_host=True))
 
     el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), eng.pool._max_workers])
+    for f in plans.values():  # the look-ahead pass 1 of the step after the last one
+        f.result()
     tot = np.sum([r[0] for r in res], axis=0)
     frames = tot[0]
     npx = frames * w * h
@@ -412,7 +440,10 @@ def av1_main(args) -> None:
                 "model": f"AV1 subset (tv) qindex {q} 16x16 blocks +deblock +CDEF +LR {args.res} synthetic"
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
                 "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame q-index plan, target "
-                                 f"{args.kbps:g} kbps per 30 fps stream" if args.kbps > 0 else "constant q-index"),
+                                 f"{args.kbps:g} kbps per 30 fps stream, batch feedback (bias + debt)"
+                                 if args.kbps > 0 else "constant q-index"),
+                "kbps_error_pct": round(100 * (tot[1] * 8 / (frames / 30.0) / 1000.0 / args.kbps - 1), 2)
+                if args.kbps > 0 else None,
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",
@@ -465,7 +496,7 @@ def main() -> None:
     ap.add_argument("--job-frames", type=int, default=0)
     ap.add_argument("--codec", default="hevc", choices=["hevc", "av1"], help="av1: BASELINE config #4 engine")
     ap.add_argument("--qindex", type=int, default=0, help="AV1 q-index (0 = matched to --qp)")
-    ap.add_argument("--kbps", type=float, default=0.0, help="AV1: 2-pass rate control to this kbps per 30 fps stream")
+    ap.add_argument("--kbps", type=float, default=0.0, help="2-pass rate control to this kbps per 30 fps stream")
     args = ap.parse_args()
     if args.job:
         return job_main(args)
@@ -505,9 +536,45 @@ def main() -> None:
         gathered = gather_bytes_to_root(b"".join(segs), dev)
         return stats.cpu().numpy(), (sum(len(x) for x in gathered) if gathered else 0)
 
+    from thinvids_amd.models.ratecontrol import BatchRateController, frame_sizes, plan_frame_qps, round_qps
+
+    ctl = BatchRateController()
+    nominal = args.kbps * 1000.0 * (world * batch * args.gop) / 30.0  # bits per step, whole node
+    predicted = {}
+    pass1_bits = []
+
+    def plan_pass2(i, segs1):
+        """2-pass, post thread (the only thread issuing collectives): pass-1 per-frame bits
+        of every rank all-reduced over RCCL -> one global per-frame QP plan for this step's
+        share of the target (ratecontrol.plan_frame_qps), corrected by the finished steps'
+        bias and debt (BatchRateController) -> this rank's [batch, gop] QP map."""
+        flat = torch.zeros(world * batch * args.gop, dtype=torch.float64, device=dev)
+        mine = np.concatenate([8.0 * np.asarray(frame_sizes(x), np.float64) for x in segs1])
+        flat[rank * batch * args.gop:(rank + 1) * batch * args.gop] = torch.from_numpy(mine).to(dev)
+        dist.all_reduce(flat)
+        ask, _ = ctl.request(nominal)
+        plan, predicted[i] = plan_frame_qps(list(flat.cpu().numpy().reshape(world * batch, args.gop)), args.qp, ask)
+        pass1_bits.append(float(mine.sum()))
+        return np.stack([round_qps(plan[rank * batch + b]) for b in range(batch)])
+
+    def comm_rc(i, segs, sse):
+        out = comm(segs, sse)
+        ctl.record(nominal, predicted.pop(i), 8.0 * float(out[0][1]))
+        return out
+
+    counter = [0]
+
     def step(s: int):
+        i = counter[0]
+        counter[0] += 1
         base = (s * world + rank) * batch
-        segs = eng.encode_synthetic([(base + b) * args.gop for b in range(batch)])
+        starts = [(base + b) * args.gop for b in range(batch)]
+        if args.kbps > 0:  # pass 1 at the base QP -> plan (post thread) -> pass 2 at the plan's QPs
+            qm = post.ex.submit(plan_pass2, i, eng.encode_synthetic(starts)).result()
+            segs = eng.encode_synthetic(starts, qp=qm)
+            post.submit(comm_rc, i, segs, np.array([eng.sse(b) for b in range(batch)]).sum(0))
+            return
+        segs = eng.encode_synthetic(starts)
         post.submit(comm, segs, np.array([eng.sse(b) for b in range(batch)]).sum(0))
 
     el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), eng.threads])
@@ -535,7 +602,13 @@ def main() -> None:
             "dtype": "uint8 video / int32 integer transforms (bit-exact HEVC)",
             "data": "synthetic (seeded procedural YUV 4:2:0 source generated on GPU)",
             "config": {
-                "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else ""),
+                "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else "")
+                + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
+                "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame QP plan, target {args.kbps:g} "
+                                 "kbps per 30 fps stream, batch feedback (bias + debt)" if args.kbps > 0 else f"CQP {args.qp}"),
+                "kbps_error_pct": round(100 * (kbps / args.kbps - 1), 2) if args.kbps > 0 else None,
+                "pass1_kbps_rank0": round(sum(pass1_bits[-args.steps:]) / (batch * args.gop * args.steps / 30.0) / 1000.0, 1)
+                if pass1_bits else None,
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",

@@ -150,6 +150,32 @@ def round_qps(qf: np.ndarray, offset: float = 0.0, qp_min: int = 10, qp_max: int
     return out
 
 
+class BatchRateController:
+    """Batch-sequential 2-pass feedback (the bench's steps, a worker's claims): each batch is
+    planned from its own pass-1 statistics, and the error of the batches already finished is
+    carried into the next plan -- the model's bias (actual / predicted bits, which absorbs a
+    content-dependent bits(QP) slope the fixed SLOPE misses) and half of the accumulated
+    overshoot / undershoot (the debt is repaid over about two batches).  Deterministic in
+    the (all-reduced) inputs, so every rank computes the same plan."""
+
+    def __init__(self, repay: float = 0.5):
+        self.target = self.actual = self.pred = 0.0
+        self.repay = repay
+
+    def request(self, nominal: float) -> tuple[float, float]:
+        """(bits to ask the planner for, bits this batch should really produce)."""
+        bias = self.actual / self.pred if self.pred > 0 else 1.0
+        want = max(0.5 * nominal, nominal + self.repay * (self.target - self.actual))
+        return want / bias, want
+
+    def record(self, nominal: float, predicted: float, actual: float) -> None:
+        """nominal: the batch's share of the target; predicted: the planner's total for the
+        bits it was asked for; actual: what the batch produced."""
+        self.target += nominal
+        self.pred += predicted
+        self.actual += actual
+
+
 class RateFeedback:
     """Rank-local pass-2 correction: the log-ratio of actual to planned bits over the
     segments encoded so far becomes a QP offset for the segments still to come."""
