@@ -122,6 +122,7 @@ class Core {
     if ((c.width & 1) || (c.height & 1)) throw std::runtime_error("odd frame size");
     if (c.width < 64 || c.height < 64) throw std::runtime_error("frame must be at least 64x64");
     HIP_OK(hipSetDevice(c.device));
+    fetch_ = std::make_unique<ThreadPool>(1, c.device);
     HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     {  // I-frame wavefront stream: highest priority, so its 100+ short dependent launches are
        // dispatched ahead of the other stream group's queued P-frame workgroups
@@ -202,6 +203,7 @@ class Core {
   }
 
   ~Core() {
+    fetch_.reset();  // the fetch thread drains (every issued slot was waited for by finish())
     (void)hipStreamSynchronize(stream_);
     for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u, rec_[1].v,
                     rec_[2].y, rec_[2].u, rec_[2].v})
@@ -509,7 +511,11 @@ class Core {
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(s.ev, stream_));
     s.pending.store(B + 1, std::memory_order_release);
-    pool_->submit([this, &s, B, f] {
+    // The slot's GPU wait + D2H runs on this core's one fetch thread (slots complete in
+    // stream order, so a FIFO of waits loses nothing): one thread per core spins on the
+    // completion events instead of one pool thread per in-flight slot, and the pool's
+    // threads only ever run CABAC.
+    fetch_->submit([this, &s, B, f] {
       try {
         Range r("engine.d2h");
         fetch_slot(s, B);
@@ -624,6 +630,7 @@ class Core {
   std::vector<double> sse_host_;
   std::atomic<long> coef_bytes_{0};
   std::atomic<long> entropy_ns_{0};
+  std::unique_ptr<ThreadPool> fetch_;  // declared last: its thread stops before anything above is freed
 };
 
 // The engine: `groups` cores, each owning batch/groups segments on its own stream.  Frame f

@@ -351,17 +351,29 @@ void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipS
   k_phase_planes<<<grid, 256, 0, s>>>(ref, phase, g);
 }
 // ---------------------------------------- SAO ------------------------------------------
-// One block per CTB.  The deblocked CTB of every component plus a one-sample border is
-// staged in LDS (-1 marks samples outside the picture), so the EO neighbour reads never touch
-// global memory.  Statistics without LDS-atomic storms:
+// One block per CTB: statistics -> integer RD decision -> the SAO'd CTB, in one launch.  The
+// deblocked CTB of every component plus a one-sample border is staged in LDS (-1 marks
+// samples outside the picture; every global load of the stage is issued before the first
+// store), so the EO neighbour reads of both the statistics and the filter never touch global
+// memory, and the filtered CTB is written straight from the tile (no separate apply pass
+// re-reading the deblocked frame).  Statistics without LDS-atomic storms:
 //   * EO: each thread accumulates its samples' 4 classes x 4 categories (count, sum) in
 //     registers; one DPP wave reduction per counter, one LDS add per wave;
 //   * band: per wave, loop over the distinct bands present (ballot + readlane): one wave
 //     reduction and one LDS add per distinct band.
-// Then the shared integer RD decision (tv::sao_decide: identical to the CPU golden model).
+// Then the shared integer RD decision (tv::sao_item / sao_window / sao_finish_pos: identical
+// to the CPU golden model), the band-position argmin of the 3 components on 3 waves.
 constexpr int kSaoT = 34;   // luma tile side with border
 constexpr int kSaoTc = 18;  // chroma
-__global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, uint32_t* sao, Geo g,
+constexpr int kSaoTile = kSaoT * kSaoT + 2 * kSaoTc * kSaoTc;
+constexpr int kSaoStage = (kSaoTile + 255) / 256;
+
+__device__ __forceinline__ void sao_tile_pos(int i, int& c, int& j) {
+  c = i < kSaoT * kSaoT ? 0 : (i < kSaoT * kSaoT + kSaoTc * kSaoTc ? 1 : 2);
+  j = c == 0 ? i : i - kSaoT * kSaoT - (c - 1) * kSaoTc * kSaoTc;
+}
+
+__global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, Geo g,
                                                     const int8_t* qp, const RcTables* rc) {
   const int tid = threadIdx.x, lane = tid & 63;
   int ctu, b;
@@ -369,38 +381,55 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   const long long lam16 = rc->sao_lam16[qp[b]];
   const int cx = ctu % g.wc, cy = ctu / g.wc;
   __shared__ SaoStats st[3];
-  __shared__ int16_t tl[kSaoT * kSaoT];
-  __shared__ int16_t tc[2][kSaoTc * kSaoTc];
+  __shared__ int16_t tile[kSaoTile];  // luma 34 x 34, then Cb, Cr 18 x 18
+  __shared__ int bpos[3];
   for (int i = tid; i < 3 * (int)(sizeof(SaoStats) / 4); i += 256) reinterpret_cast<int*>(st)[i] = 0;
-  for (int i = tid; i < kSaoT * kSaoT + 2 * kSaoTc * kSaoTc; i += 256) {
-    const int c = i < kSaoT * kSaoT ? 0 : (i < kSaoT * kSaoT + kSaoTc * kSaoTc ? 1 : 2);
-    const int j = c == 0 ? i : i - kSaoT * kSaoT - (c - 1) * kSaoTc * kSaoTc;
-    const int T = c ? kSaoTc : kSaoT, n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
-    const int x = cx * n + j % T - 1, y = cy * n + j / T - 1;
-    const int16_t v = (x < 0 || y < 0 || x >= w || y >= h) ? (int16_t)-1 : (int16_t)deb.plane(c, b, g)[y * w + x];
-    if (c == 0) tl[j] = v;
-    else tc[c - 1][j] = v;
+  {
+    int16_t v[kSaoStage];
+#pragma unroll
+    for (int k = 0; k < kSaoStage; ++k) {
+      const int i = tid + 256 * k;
+      v[k] = -1;
+      if (i < kSaoTile) {
+        int c, j;
+        sao_tile_pos(i, c, j);
+        const int T = c ? kSaoTc : kSaoT, n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
+        const int x = cx * n + j % T - 1, y = cy * n + j / T - 1;
+        if (x >= 0 && y >= 0 && x < w && y < h) v[k] = (int16_t)deb.plane(c, b, g)[y * w + x];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kSaoStage; ++k)
+      if (tid + 256 * k < kSaoTile) tile[tid + 256 * k] = v[k];
   }
-  __syncthreads();
   // one region per wave: waves 0/1 = luma rows 0-15 / 16-31 (8 samples per lane), wave 2 =
   // Cb, wave 3 = Cr (4 per lane).  Counts and sums travel packed as sum * 2048 + count
   // (count <= 1024, |sum| <= 255 * 1024): one wave reduction per EO counter, not two.
   const int wave = tid >> 6;
   const int c = wave < 2 ? 0 : wave - 1;
   const int n = c ? 16 : 32, T = c ? kSaoTc : kSaoT, w = c ? g.W / 2 : g.W;
-  const int16_t* t = c == 0 ? tl : tc[c - 1];
+  const int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
   const int iters = c ? 4 : 8;
+  const uint8_t* S = src.plane(c, b, g) + (long)(cy * n) * w + cx * n;
+  int sv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {  // source samples of this lane, loads in flight together
+    const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
+    sv[k] = k < iters ? S[(i / n) * w + i % n] : 0;
+  }
+  __syncthreads();
   int eo[4][4];
 #pragma unroll
   for (int d = 0; d < 4; ++d)
 #pragma unroll
     for (int q = 0; q < 4; ++q) eo[d][q] = 0;
-  for (int k = 0; k < iters; ++k) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (k >= iters) break;
     const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
     const int lx = i % n, ly = i / n;
     const int v = t[(ly + 1) * T + lx + 1];
-    const int diff = (int)src.plane(c, b, g)[(cy * n + ly) * w + cx * n + lx] - v;
-    const int packed = diff * 2048 + 1;
+    const int packed = (sv[k] - v) * 2048 + 1;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       int dx, dy;
@@ -437,33 +466,57 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       }
     }
   __shared__ SaoTables tab;
+  __shared__ uint32_t prm[3];
   __syncthreads();
   if (tid < kSaoItems) sao_item(st, lam16, tid, tab);  // 144 offset/cost items in parallel
   __syncthreads();
   if (tid < 96) sao_window(tid, tab);  // 3 x 32 band windows
   __syncthreads();
-  if (tid == 0) sao_finish(tab, lam16, sao + 3 * ((long)b * g.wc * g.hc + ctu));
-}
-
-// every sample of `out`: the SAO'd deblocked sample (or the deblocked sample itself)
-__global__ void __launch_bounds__(256) k_sao_apply(FrameSet deb, FrameSet out, const uint32_t* sao, Geo g) {
-  const int b = blockIdx.y;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  const long ny = g.ysz, nc = g.csz;
-  if (i >= ny + 2 * nc) return;
-  const int c = i < ny ? 0 : (i < ny + nc ? 1 : 2);
-  const long j = c == 0 ? i : i - ny - (c - 1) * nc;
-  const int w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H, n = c ? 16 : 32;
-  const int x = (int)(j % w), y = (int)(j / w);
-  const uint32_t p = sao[3 * ((long)b * g.wc * g.hc + (y / n) * g.wc + x / n) + c];
-  const uint8_t* D = deb.plane(c, b, g);
-  out.plane(c, b, g)[j] = sao_type(p) ? (uint8_t)sao_sample(D, w, h, x, y, p) : D[j];
+  if (wave < 3) {  // best band position of component `wave`: first minimum over 32 windows
+    long long j = lane < 32 ? tab.win_j[wave][lane] : LLONG_MAX;
+    int p = lane < 32 ? lane : 64;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const long long j2 = __shfl_xor(j, o);
+      const int p2 = __shfl_xor(p, o);
+      if (j2 < j || (j2 == j && p2 < p)) {
+        j = j2;
+        p = p2;
+      }
+    }
+    if (lane == 0) bpos[wave] = p;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    sao_finish_pos(tab, lam16, bpos, prm);
+    uint32_t* o = sao + 3 * ((long)b * g.wc * g.hc + ctu);
+    o[0] = prm[0];
+    o[1] = prm[1];
+    o[2] = prm[2];
+  }
+  __syncthreads();
+  // the SAO'd CTB from the tile: luma 1024 + 2 x 256 chroma samples, 6 per thread
+  for (int i = tid; i < 1024 + 512; i += 256) {
+    const int cc = i < 1024 ? 0 : (i < 1280 ? 1 : 2);
+    const int j = cc == 0 ? i : i - 1024 - (cc - 1) * 256;
+    const int nn = cc ? 16 : 32, TT = cc ? kSaoTc : kSaoT, ww = cc ? g.W / 2 : g.W;
+    const int lx = j % nn, ly = j / nn;
+    const int16_t* tt = tile + (cc == 0 ? 0 : kSaoT * kSaoT + (cc - 1) * kSaoTc * kSaoTc);
+    const uint32_t p = prm[cc];
+    const int v = tt[(ly + 1) * TT + lx + 1];
+    int r = v;
+    if (sao_type(p)) {
+      int dx = 0, dy = 0;
+      if (sao_type(p) == 2) sao_eo_dir(sao_class(p), dx, dy);
+      r = sao_sample_nb(v, tt[(ly + 1 + dy) * TT + lx + 1 + dx], tt[(ly + 1 - dy) * TT + lx + 1 - dx], p);
+    }
+    out.plane(cc, b, g)[(long)(cy * nn + ly) * ww + cx * nn + lx] = (uint8_t)r;
+  }
 }
 
 void launch_sao(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, const int8_t* qp, const RcTables* rc,
                 const Geo& g, int B, hipStream_t s) {
-  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, sao, g, qp, rc);
-  k_sao_apply<<<dim3((unsigned)((g.ysz + 2 * g.csz + 255) / 256), B), 256, 0, s>>>(deb, out, sao, g);
+  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, out, sao, g, qp, rc);
 }
 
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int B, hipStream_t s) {

@@ -581,23 +581,30 @@ TV_HD int sao_eo_category(int p, int a, int b) {
   const int e = 2 + (p > a) - (p < a) + (p > b) - (p < b);
   return e == 2 ? 0 : (e < 2 ? e + 1 : e);
 }
-// one SAO'd sample.  x, y: component coordinates; src: deblocked plane (w x h).
-TV_HD int sao_sample(const uint8_t* src, int w, int h, int x, int y, uint32_t p) {
-  const int v = src[y * w + x];
+// one SAO'd sample from its deblocked value v and the two EO neighbours of the parameter
+// set's class (a, b < 0: outside the picture -> the sample is left unchanged)
+TV_HD int sao_sample_nb(int v, int a, int b, uint32_t p) {
   const int t = sao_type(p);
   if (t == 1) {
     const int k = ((v >> 3) - sao_class(p)) & 31;
     return k < 4 ? clip_pixel(v + sao_offset(p, k)) : v;
   }
   if (t == 2) {
-    int dx, dy;
-    sao_eo_dir(sao_class(p), dx, dy);
-    const int ax = x + dx, ay = y + dy, bx = x - dx, by = y - dy;
-    if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= w || ay >= h || bx >= w || by >= h) return v;
-    const int c = sao_eo_category(v, src[ay * w + ax], src[by * w + bx]);
+    if (a < 0 || b < 0) return v;
+    const int c = sao_eo_category(v, a, b);
     return c ? clip_pixel(v + sao_offset(p, c - 1)) : v;
   }
   return v;
+}
+// one SAO'd sample.  x, y: component coordinates; src: deblocked plane (w x h).
+TV_HD int sao_sample(const uint8_t* src, int w, int h, int x, int y, uint32_t p) {
+  const int v = src[y * w + x];
+  if (sao_type(p) != 2) return sao_sample_nb(v, 0, 0, p);
+  int dx, dy;
+  sao_eo_dir(sao_class(p), dx, dy);
+  const int ax = x + dx, ay = y + dy, bx = x - dx, by = y - dy;
+  const bool in = !(ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= w || ay >= h || bx >= w || by >= h);
+  return sao_sample_nb(v, in ? src[ay * w + ax] : -1, in ? src[by * w + bx] : -1, p);
 }
 
 // Statistics of one CTB component: count and sum(orig - deblocked) per EO class/category
@@ -681,9 +688,9 @@ TV_HD long long sao_eo_j(const SaoTables& t, int c, int cls) {
   return t.eo_j[c][cls][0] + t.eo_j[c][cls][1] + t.eo_j[c][cls][2] + t.eo_j[c][cls][3];
 }
 // Rate in bits: type TR bins (off 1, band 2, edge 2), EO class 2, band position 5, offsets.
-TV_HD void sao_finish(const SaoTables& t, long long lam16, uint32_t* out) {
-  int pos[3];
-  for (int c = 0; c < 3; ++c) pos[c] = sao_best_band(t, c);
+// the final choice given each component's best band position (sao_best_band; the GPU finds
+// it with a wave-parallel argmin)
+TV_HD void sao_finish_pos(const SaoTables& t, long long lam16, const int* pos, uint32_t* out) {
   {  // luma
     long long best = lam16 * 1;
     out[0] = sao_off_param();
@@ -712,6 +719,11 @@ TV_HD void sao_finish(const SaoTables& t, long long lam16, uint32_t* out) {
       out[2] = sao_pack_bo(t, 2, pos[2]);
     }
   }
+}
+TV_HD void sao_finish(const SaoTables& t, long long lam16, uint32_t* out) {
+  int pos[3];
+  for (int c = 0; c < 3; ++c) pos[c] = sao_best_band(t, c);
+  sao_finish_pos(t, lam16, pos, out);
 }
 // Sequential form of the three phases (CPU golden model).
 inline void sao_decide(const SaoStats* st, long long lam16, uint32_t* out) {
