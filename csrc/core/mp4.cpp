@@ -431,6 +431,64 @@ namespace {
 
 using muxi::MuxPlan;
 
+// VisualSampleEntry of the video track: 'hvc1' / 'hev1' + hvcC, or 'av01' + av1C
+std::vector<uint8_t> visual_entry(const muxi::MuxPlan& P, int width, int height) {
+  Box se;
+  se.zeros(6);
+  se.u16(1);
+  se.zeros(16);
+  se.u16((uint32_t)width);
+  se.u16((uint32_t)height);
+  se.u32(0x00480000);
+  se.u32(0x00480000);
+  se.u32(0);
+  se.u16(1);
+  char name[32] = {0};
+  const char* nm = P.codec == muxi::MUX_AV1 ? "thinvids-amd AV1" : "thinvids-amd HEVC";
+  name[0] = (char)std::strlen(nm);
+  std::memcpy(name + 1, nm, std::strlen(nm));
+  se.str(name, 32);
+  se.u16(0x0018);
+  se.u16(0xffff);
+  if (P.codec == muxi::MUX_AV1) {
+    se.bytes(box("av1C", P.av1c));
+    return box("av01", se.b);
+  }
+  se.bytes(box("hvcC", muxi::hvcc_record(P)));
+  return box(P.ps_consistent ? "hvc1" : "hev1", se.b);
+}
+
+// moov of the given tracks (chunk offsets already filled in)
+std::vector<uint8_t> moov_box(const std::vector<TrakInfo>& I, const std::vector<TrakTables>& T, bool large) {
+  uint64_t movie_ms = 0;
+  for (size_t k = 0; k < T.size(); ++k) movie_ms = std::max(movie_ms, T[k].media_dur * 1000 / I[k].timescale);
+  Box mvhd;
+  mvhd.u32(0);
+  mvhd.u32(0);
+  mvhd.u32(1000);
+  mvhd.u32((uint32_t)movie_ms);
+  mvhd.u32(0x00010000);
+  mvhd.u16(0x0100);
+  mvhd.zeros(10);
+  matrix(mvhd);
+  mvhd.zeros(24);
+  mvhd.u32((uint32_t)T.size() + 1);
+  std::vector<uint8_t> body = fullbox("mvhd", 0, 0, mvhd.b);
+  for (size_t k = 0; k < T.size(); ++k) {
+    const auto tb = trak_box(I[k], T[k], large);
+    body.insert(body.end(), tb.begin(), tb.end());
+  }
+  return box("moov", body);
+}
+
+std::vector<uint8_t> ftyp_box(int codec) {
+  Box ftyp;
+  ftyp.str("isom", 4);
+  ftyp.u32(512);
+  ftyp.str(codec == muxi::MUX_AV1 ? "isomiso2av01mp41" : "isomiso2hvc1mp41", 16);
+  return box("ftyp", ftyp.b);
+}
+
 // Faststart MP4 of the plan + side tracks.  Returns the file size.
 // Output goes to `mem` when it is non-null, else to the file `path`.
 uint64_t write_mp4(const MuxPlan& P, int width, int height, int fps_num, int fps_den, const SideTrack* tracks,
@@ -459,31 +517,7 @@ uint64_t write_mp4(const MuxPlan& P, int width, int height, int fps_num, int fps
       chunks.push_back({0, f, n, (double)f * fps_den / fps_num, b});
       V.chunk_n.push_back((uint32_t)n);
     }
-    I[0] = {1, "vide", "VideoHandler", vts, pack_lang(nullptr), true, 0, 0, width, height, {}};
-    Box se;  // VisualSampleEntry
-    se.zeros(6);
-    se.u16(1);
-    se.zeros(16);
-    se.u16((uint32_t)width);
-    se.u16((uint32_t)height);
-    se.u32(0x00480000);
-    se.u32(0x00480000);
-    se.u32(0);
-    se.u16(1);
-    char name[32] = {0};
-    const char* nm = P.codec == muxi::MUX_AV1 ? "thinvids-amd AV1" : "thinvids-amd HEVC";
-    name[0] = (char)std::strlen(nm);
-    std::memcpy(name + 1, nm, std::strlen(nm));
-    se.str(name, 32);
-    se.u16(0x0018);
-    se.u16(0xffff);
-    if (P.codec == muxi::MUX_AV1) {
-      se.bytes(box("av1C", P.av1c));
-      I[0].entry = box("av01", se.b);
-    } else {
-      se.bytes(box("hvcC", muxi::hvcc_record(P)));
-      I[0].entry = box(P.ps_consistent ? "hvc1" : "hev1", se.b);
-    }
+    I[0] = {1, "vide", "VideoHandler", vts, pack_lang(nullptr), true, 0, 0, width, height, visual_entry(P, width, height)};
   }
   // ---- side tracks
   bool first_audio = true;
@@ -554,8 +588,6 @@ uint64_t write_mp4(const MuxPlan& P, int width, int height, int fps_num, int fps
   uint64_t payload = 0;
   for (const auto& c : chunks) payload += c.bytes;
   const bool large = payload + (1 << 20) > 0xffffffffull;
-  uint64_t movie_ms = 0;
-  for (int k = 0; k < ntrak; ++k) movie_ms = std::max(movie_ms, T[k].media_dur * 1000 / I[k].timescale);
   auto build_moov = [&](uint64_t base) {
     for (auto& x : T) x.chunk_off.clear();
     uint64_t o = base;
@@ -563,33 +595,13 @@ uint64_t write_mp4(const MuxPlan& P, int width, int height, int fps_num, int fps
       T[c.track].chunk_off.push_back(o);
       o += c.bytes;
     }
-    Box mvhd;
-    mvhd.u32(0);
-    mvhd.u32(0);
-    mvhd.u32(1000);
-    mvhd.u32((uint32_t)movie_ms);
-    mvhd.u32(0x00010000);
-    mvhd.u16(0x0100);
-    mvhd.zeros(10);
-    matrix(mvhd);
-    mvhd.zeros(24);
-    mvhd.u32((uint32_t)ntrak + 1);
-    std::vector<uint8_t> body = fullbox("mvhd", 0, 0, mvhd.b);
-    for (int k = 0; k < ntrak; ++k) {
-      const auto tb = trak_box(I[k], T[k], large);
-      body.insert(body.end(), tb.begin(), tb.end());
-    }
-    return box("moov", body);
+    return moov_box(I, T, large);
   };
-  Box ftyp;
-  ftyp.str("isom", 4);
-  ftyp.u32(512);
-  ftyp.str(P.codec == muxi::MUX_AV1 ? "isomiso2av01mp41" : "isomiso2hvc1mp41", 16);
-  const auto ftyp_box = box("ftyp", ftyp.b);
+  const auto ftyp_b = ftyp_box(P.codec);
   const uint64_t mdat_hdr = large ? 16 : 8;
   const size_t moov_size = build_moov(0).size();  // offsets do not change the size
-  std::vector<uint8_t> head = ftyp_box;
-  const auto moov = build_moov(ftyp_box.size() + moov_size + mdat_hdr);
+  std::vector<uint8_t> head = ftyp_b;
+  const auto moov = build_moov(ftyp_b.size() + moov_size + mdat_hdr);
   head.insert(head.end(), moov.begin(), moov.end());
   Box mh;
   if (large) {
@@ -652,6 +664,104 @@ uint64_t write_mp4(const MuxPlan& P, int width, int height, int fps_num, int fps
   if (!ok) throw std::runtime_error(std::string("mux: write failed: ") + path);
   return head.size() + payload;
 }
+
+// Streaming faststart writer of one video track (no side tracks): segments are appended as
+// they arrive and their samples go straight to disk; the head (ftyp + moov + 'free' padding)
+// is reserved up front from the sample-count bound and written in place at close(), so the
+// finished file is faststart without a second copy of the payload.  The moov size is bounded
+// by a fixed part plus 12 bytes per sample (stsz 4 + stss 4 when every sample were a sync
+// sample, + slack); co64 chunk offsets make the bound independent of the file size.
+class Mp4Stream {
+ public:
+  Mp4Stream(const char* path, int width, int height, int fps_num, int fps_den, uint64_t max_samples)
+      : path_(path), w_(width), h_(height), fn_(fps_num), fd_(fps_den), max_(max_samples) {
+    if (fps_num <= 0 || fps_den <= 0) throw std::runtime_error("mux stream: bad frame rate");
+    if (!max_samples) throw std::runtime_error("mux stream: no samples expected");
+    reserve_ = 8192 + 12 * max_samples;
+    f_ = std::fopen(path, "wb");
+    if (!f_) throw std::runtime_error(std::string("mux stream: cannot open ") + path);
+    std::vector<uint8_t> z(reserve_, 0);
+    if (std::fwrite(z.data(), 1, z.size(), f_) != z.size()) fail("write failed");
+  }
+  ~Mp4Stream() {
+    if (f_) std::fclose(f_);
+  }
+  void append(const uint8_t* seg, size_t n) {
+    if (!f_) throw std::runtime_error("mux stream: closed");
+    const MuxPlan P = muxi::plan_mux(&seg, &n, 1);
+    if (!have_) {
+      head_.codec = P.codec;
+      head_.vps = P.vps;
+      head_.sps = P.sps;
+      head_.pps = P.pps;
+      head_.av1c = P.av1c;
+      have_ = true;
+    } else if (P.codec != head_.codec || P.vps != head_.vps || P.sps != head_.sps || P.pps != head_.pps ||
+               P.av1c != head_.av1c || !P.ps_consistent) {
+      fail("segments with different parameter sets (use the whole-job muxer)");
+    }
+    if (!P.ps_consistent) fail("segment with inconsistent parameter sets");
+    if (sizes_.size() + P.samples.size() > max_) fail("more samples than reserved");
+    buf_.clear();
+    for (const auto& smp : P.samples) {
+      muxi::append_sample(smp, buf_);
+      sizes_.push_back(smp.size);
+      if (smp.sync) sync_.push_back((uint32_t)sizes_.size());
+    }
+    if (std::fwrite(buf_.data(), 1, buf_.size(), f_) != buf_.size()) fail("write failed");
+    payload_ += buf_.size();
+  }
+  uint64_t close() {
+    if (!f_) throw std::runtime_error("mux stream: closed");
+    if (!have_ || sizes_.empty()) fail("no samples");
+    std::vector<TrakTables> T(1);
+    std::vector<TrakInfo> I(1);
+    auto& V = T[0];
+    V.nsamples = sizes_.size();
+    V.has_stss = true;
+    V.sizes = sizes_;
+    V.sync = sync_;
+    for (size_t i = 0; i < sizes_.size(); ++i) V.delta((uint32_t)fd_ * 1000u);
+    V.chunk_n = {(uint32_t)sizes_.size()};
+    V.chunk_off = {reserve_};
+    I[0] = {1, "vide", "VideoHandler", (uint32_t)fn_ * 1000u, pack_lang(nullptr), true, 0, 0, w_, h_,
+            visual_entry(head_, w_, h_)};
+    const auto ftyp = ftyp_box(head_.codec);
+    const auto moov = moov_box(I, T, true);
+    const uint64_t used = ftyp.size() + moov.size() + 16;  // + the 64-bit mdat header
+    if (used + 8 > reserve_) fail("moov exceeds the reserved head");
+    Box head;
+    head.bytes(ftyp);
+    head.bytes(moov);
+    head.u32((uint32_t)(reserve_ - used));  // 'free' padding up to the mdat header
+    head.str("free", 4);
+    head.zeros(reserve_ - used - 8);
+    head.u32(1);
+    head.str("mdat", 4);
+    head.u64(payload_ + 16);
+    if (head.b.size() != reserve_) fail("head layout");
+    if (std::fseek(f_, 0, SEEK_SET) != 0 || std::fwrite(head.b.data(), 1, head.b.size(), f_) != head.b.size())
+      fail("head write failed");
+    const bool ok = std::fclose(f_) == 0;
+    f_ = nullptr;
+    if (!ok) throw std::runtime_error("mux stream: close failed: " + path_);
+    return reserve_ + payload_;
+  }
+  uint64_t samples() const { return sizes_.size(); }
+
+ private:
+  [[noreturn]] void fail(const char* what) {
+    throw std::runtime_error(std::string("mux stream: ") + what + ": " + path_);
+  }
+  std::string path_;
+  int w_, h_, fn_, fd_;
+  uint64_t max_, reserve_ = 0, payload_ = 0;
+  FILE* f_ = nullptr;
+  MuxPlan head_;
+  bool have_ = false;
+  std::vector<uint32_t> sizes_, sync_;
+  std::vector<uint8_t> buf_;
+};
 
 }  // namespace
 
@@ -815,3 +925,42 @@ std::vector<uint8_t> demux_mp4(const uint8_t* mp4, size_t n, int* width, int* he
 }
 
 }  // namespace tv
+
+// ------------------------------------- streaming writer C API ---------------------------
+namespace {
+thread_local std::string g_mp4s_err;
+}
+extern "C" {
+void* tv_mp4s_open(const char* path, int width, int height, int fps_num, int fps_den, unsigned long long max_samples) {
+  try {
+    return new tv::Mp4Stream(path, width, height, fps_num, fps_den, max_samples);
+  } catch (const std::exception& e) {
+    g_mp4s_err = e.what();
+    return nullptr;
+  }
+}
+int tv_mp4s_append(void* h, const uint8_t* data, size_t n) {
+  try {
+    static_cast<tv::Mp4Stream*>(h)->append(data, n);
+    return 0;
+  } catch (const std::exception& e) {
+    g_mp4s_err = e.what();
+    return -1;
+  }
+}
+// finishes the file (returns 0 and its size in *bytes) and frees the handle either way
+int tv_mp4s_close(void* h, unsigned long long* bytes) {
+  auto* s = static_cast<tv::Mp4Stream*>(h);
+  int rc = 0;
+  try {
+    *bytes = s->close();
+  } catch (const std::exception& e) {
+    g_mp4s_err = e.what();
+    rc = -1;
+  }
+  delete s;
+  return rc;
+}
+void tv_mp4s_abort(void* h) { delete static_cast<tv::Mp4Stream*>(h); }
+const char* tv_mp4s_last_error() { return g_mp4s_err.c_str(); }
+}

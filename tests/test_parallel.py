@@ -107,6 +107,30 @@ def test_node_job_world2(tmp_path, source, kw):
         assert res["passes"] in (2, 3) and len(res["qp_plan"][0]) == 3
 
 
+def test_streaming_stitch_world2_matches_end_mux(tmp_path, source):
+    """Single-pass job on 2 ranks: rank 0 appends every segment to the streaming faststart
+    writer while the ranks encode (rank 1's through part files), so no bitstream is gathered
+    or muxed at the end -- and the file carries exactly the stream the end-of-job muxer
+    writes (TV_STREAM_STITCH=0)."""
+    from thinvids_amd.models import hevc
+
+    src, frames = source
+    os.makedirs(tmp_path / "a", exist_ok=True)
+    os.makedirs(tmp_path / "b", exist_ok=True)
+    res_a, out_a = _spawn_job(tmp_path / "a", source, {}, {})
+    res_b, out_b = _spawn_job(tmp_path / "b", source, {}, {"TV_STREAM_STITCH": "0"})
+    tr_a, tr_b = res_a[0]["trace"], res_b[0]["trace"]
+    assert tr_a["node_job.stitch_append"]["count"] == 3 and "node_job.mux" not in tr_a, tr_a
+    assert "node_job.mux" in tr_b and "node_job.stitch_append" not in tr_b
+    assert not os.path.exists(out_a + ".parts")
+    da = hevc.demux_mp4(open(out_a, "rb").read())
+    db = hevc.demux_mp4(open(out_b, "rb").read())
+    assert da["annexb"] == db["annexb"] and da["frames"] == 24
+    assert res_a[0]["outputs"][0]["kbps"] == res_b[0]["outputs"][0]["kbps"]
+    dec = hevc.decode(da["annexb"], coded=False)
+    assert min(hevc.psnr(a[0], b[0]) for a, b in zip(frames, dec.frames)) > 28
+
+
 def test_rotating_scatter_gloo_world4(tmp_path, source):
     """Scatter mode on 4 ranks: the root rotates per round (comm.scatter_root), so the
     source reads and sends are spread over the ranks instead of rank 0 reading everything;

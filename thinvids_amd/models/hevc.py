@@ -228,6 +228,56 @@ def mux_mp4_file(segments, width: int, height: int, fps_num: int, fps_den: int, 
     return int(out.value)
 
 
+class Mp4StreamWriter:
+    """Streaming faststart MP4 of one video track (csrc/core/mp4.cpp Mp4Stream): Annex-B (or
+    AV1 OBU) segments are appended as they are encoded and written straight to `path`; the
+    head (ftyp + moov + free padding) is reserved for `max_samples` frames and filled in by
+    close(), so the finished file is faststart without re-copying the payload.  Segments
+    must share one set of parameter sets (one encoder configuration per job)."""
+
+    def __init__(self, path: str, width: int, height: int, fps_num: int, fps_den: int, max_samples: int):
+        lib = core_lib()
+        if not getattr(lib, "_mp4s_sig", False):
+            lib.tv_mp4s_open.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_ulonglong]
+            lib.tv_mp4s_open.restype = C.c_void_p
+            lib.tv_mp4s_append.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+            lib.tv_mp4s_append.restype = C.c_int
+            lib.tv_mp4s_close.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+            lib.tv_mp4s_close.restype = C.c_int
+            lib.tv_mp4s_abort.argtypes = [C.c_void_p]
+            lib.tv_mp4s_last_error.restype = C.c_char_p
+            lib._mp4s_sig = True
+        self.lib, self.path = lib, path
+        self.h = lib.tv_mp4s_open(path.encode(), width, height, fps_num, fps_den, max(1, int(max_samples)))
+        if not self.h:
+            raise RuntimeError(lib.tv_mp4s_last_error().decode())
+        self.payload = 0
+
+    def append(self, segment) -> None:
+        buf = np.frombuffer(segment, np.uint8)
+        if not len(buf):
+            return
+        if self.lib.tv_mp4s_append(self.h, buf.ctypes.data, len(buf)) != 0:
+            raise RuntimeError(self.lib.tv_mp4s_last_error().decode())
+        self.payload += len(buf)
+
+    def close(self) -> int:
+        """Finish the file; returns its size."""
+        h, self.h = self.h, None
+        out = C.c_ulonglong()
+        if self.lib.tv_mp4s_close(h, C.byref(out)) != 0:
+            raise RuntimeError(self.lib.tv_mp4s_last_error().decode())
+        return int(out.value)
+
+    def abort(self) -> None:
+        if self.h:
+            self.lib.tv_mp4s_abort(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.abort()
+
+
 def demux_mp4(data: bytes) -> dict:
     lib = core_lib()
     out = Bytes()

@@ -16,18 +16,24 @@ Flow (the reference's split -> encode -> stitch, without HTTP or disk in between
 4. with ``--bitrate-kbps`` a first pass measures bits per segment at the base QP; the
    per-segment sizes are **all-reduced** and every rank derives the same per-segment QP
    plan (complexity^0.6 allocation), then encodes pass 2;
-5. bitstreams are gathered to rank 0 (all_gather of sizes + grouped send/recv) and muxed
-   in segment order into one faststart MP4; ``--ladder`` fans rungs x segments out over
-   all ranks and writes one MP4 per rung.
+5. single-pass jobs with a plain MP4 output are **stitched while they encode**: every
+   finished segment goes to rank 0 (its own in memory, the peers' as part files in the
+   node-local job directory, written off the critical path), whose stitch thread appends
+   each rung's segments in order to a streaming faststart MP4 writer (ranks keep no
+   bitstreams); otherwise bitstreams are gathered to rank 0 after the last pass (all_gather
+   of sizes + grouped send/recv) and muxed in segment order.  ``--ladder`` fans rungs x
+   segments out over all ranks and writes one MP4 per rung.
 """
 from __future__ import annotations
 
 import argparse
+import concurrent.futures as cf
 import hashlib
 import json
 import math
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -265,6 +271,97 @@ class JobHooks:
         return False
 
 
+def _part_path(parts_dir: str, r: int, i: int) -> str:
+    return os.path.join(parts_dir, f"r{r}_s{i}.part")
+
+
+def publish_part(parts_dir: str, r: int, i: int, data: bytes) -> None:
+    """A peer rank's finished segment for the stitch rank: written to a temporary name and
+    renamed, so the stitcher never sees a partial part."""
+    p = _part_path(parts_dir, r, i)
+    tmp = f"{p}.{os.getpid()}.tmp"
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, p)
+
+
+class StreamStitcher:
+    """Rank 0's stitch thread (reference overlap: the stitcher ingests parts while encoders
+    run, worker/tasks.py:1805-1822, :1898-2029): segment i of every rung is appended, in
+    segment order, to that rung's streaming faststart MP4 (models.hevc.Mp4StreamWriter) as
+    soon as it exists -- rank 0's own segments arrive through put(), the peers' as part
+    files (publish_part) that are read once and deleted.  Nothing is joined or copied at
+    the end: close() only writes each file's head."""
+
+    def __init__(self, parts_dir: str, paths: list, geoms: list, nseg: int, frames: int, fps_num: int, fps_den: int):
+        from ..models.hevc import Mp4StreamWriter
+
+        self.parts_dir, self.paths, self.nseg = parts_dir, paths, nseg
+        self.own: dict = {}
+        self.cv = threading.Condition()
+        self.err: BaseException | None = None
+        self.stop = False
+        self.bytes = [0] * len(paths)
+        self.sizes: list = []
+        self.writers = [Mp4StreamWriter(p, w, h, fps_num, fps_den, frames) for p, (w, h) in zip(paths, geoms)]
+        self.th = threading.Thread(target=self._run, name="stitch", daemon=True)
+        self.th.start()
+
+    def put(self, r: int, i: int, data: bytes) -> None:
+        with self.cv:
+            self.own[(r, i)] = data
+            self.cv.notify()
+
+    def _get(self, r: int, i: int) -> bytes:
+        path = _part_path(self.parts_dir, r, i)
+        while True:
+            with self.cv:
+                if (r, i) in self.own:
+                    return self.own.pop((r, i))
+                if self.stop:
+                    raise RuntimeError("stitch cancelled")
+            if os.path.exists(path):
+                with open(path, "rb") as f:
+                    data = f.read()
+                os.remove(path)
+                return data
+            with self.cv:
+                self.cv.wait(0.005)
+
+    def _run(self) -> None:
+        try:
+            for i in range(self.nseg):  # rung-interleaved: every rung's file grows together
+                for r, w in enumerate(self.writers):
+                    b = self._get(r, i)
+                    with trace.span("node_job.stitch_append"):
+                        w.append(b)
+                    self.bytes[r] += len(b)
+            with trace.span("node_job.stitch_close"):
+                self.sizes = [w.close() for w in self.writers]
+        except BaseException as e:  # noqa: BLE001 - surfaced by finish()
+            self.err = e
+            for w in self.writers:
+                w.abort()
+
+    def finish(self) -> list:
+        """Wait for the last segment; returns the file sizes (raises the thread's error)."""
+        self.th.join()
+        if self.err is not None:
+            raise RuntimeError(f"streaming stitch failed: {self.err}") from self.err
+        return self.sizes
+
+    def cancel(self) -> None:
+        with self.cv:
+            self.stop = True
+            self.cv.notify_all()
+        self.th.join(timeout=30)
+        for w in self.writers:
+            w.abort()
+        for p in self.paths:
+            if os.path.exists(p):
+                os.remove(p)
+
+
 def _encode_many(items: list, cache) -> tuple[dict, dict]:
     """items: [(key, part, spec, per-frame QPs or None)] -> ({key: annexb}, {key: PartStats});
     batched per spec on the engine (a part may be host frames, device frames or a synthetic
@@ -343,6 +440,28 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         rc="2pass" if bitrate_kbps > 0 else ("crf" if crf else "cqp"), bitstream_version=BITSTREAM_VERSION))
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
     quality: dict = {}  # (r, i) -> PartStats of segments encoded here
+    # streaming stitch (single pass, plain MP4 output): decided identically on every rank
+    side = _side_plan(input_path, audio_stream)
+    streaming = (bitrate_kbps <= 0 and os.environ.get("TV_STREAM_STITCH", "1") != "0"
+                 and (side is None or (not side.tracks and side.ext == ".mp4")))
+    out_paths = [output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4" for _, oh in rungs]
+    if side is not None:
+        out_paths = [os.path.splitext(p)[0] + side.ext for p in out_paths]
+    parts_dir = f"{output}.parts"
+    stitcher = None
+    if streaming:
+        os.makedirs(parts_dir, exist_ok=True)
+        if rank == 0:
+            stitcher = StreamStitcher(parts_dir, [p + ".tmp" for p in out_paths], rungs, len(segs), nfr,
+                                      src.fps_num, src.fps_den)
+    # checkpoint (hash + write) and peer part files are written off the critical path
+    io_pool = cf.ThreadPoolExecutor(1)
+    io_futs: list = []
+
+    def drain_io():
+        for f in io_futs:
+            f.result()
+        io_futs.clear()
 
     def spec(r):  # the QP is a per-frame input now: one resident engine per rung, whatever the plan
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=qp, gop=gop, search_range=search_range,
@@ -399,8 +518,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             with trace.span("node_job.encode", segments=len(todo)):
                 got, qual = _encode_many(todo, cache)
             for (r, i), b in got.items():
-                with trace.span("node_job.ckpt_save"):
-                    ckpt.save(r, i, plans[(r, i)][1], b)
+                io_futs.append(io_pool.submit(ckpt.save, r, i, plans[(r, i)][1], b))
                 out[(r, i)] = b
                 quality[(r, i)] = qual[(r, i)]
                 stats["encoded"] += 1
@@ -411,6 +529,13 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             q = plans[(r, i)][0]
             if q is not None:  # rate feedback: actual vs the model's prediction at these QPs
                 rc["fb"].record(8.0 * sum(fb), float(predict_bits(rc["b1"][(r, i)], qp, q).sum()))
+        if streaming:  # the stitch rank takes them now; this rank keeps no bitstream
+            for (r, i), b in out.items():
+                if stitcher is not None:
+                    stitcher.put(r, i, b)
+                else:
+                    io_futs.append(io_pool.submit(publish_part, parts_dir, r, i, b))
+            out = {k: b"" for k in out}
         with trace.span("node_job.hooks"):
             for i in seg_ids:
                 hooks.segment_done(segs[i][1])
@@ -506,124 +631,144 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         encode_pass.calls += 1
         return mine
 
-    encode_pass.calls = 0
-    cdev = dev if dev.type == "cuda" else torch.device("cpu")
+    try:
+        encode_pass.calls = 0
+        cdev = dev if dev.type == "cuda" else torch.device("cpu")
 
-    def agreed_pass():
-        """encode_pass + a collective verdict: a rank that failed (halt, abort, engine
-        error) never strands its peers inside the next collective."""
-        err, got = None, {}
-        hooks.new_pass(agreed_pass.n)
-        agreed_pass.n += 1
-        try:
-            got = encode_pass()
-        except Exception as e:  # noqa: BLE001 - re-raised below on every rank
-            err = e
-        with trace.span("node_job.verdict"):
-            failed = allreduce_stats([1.0 if err else 0.0], cdev, op="max")[0]
-        if failed:
-            raise err if err is not None else RuntimeError("a peer rank failed this job")
-        return got
+        def agreed_pass():
+            """encode_pass + a collective verdict: a rank that failed (halt, abort, engine
+            error) never strands its peers inside the next collective."""
+            err, got = None, {}
+            hooks.new_pass(agreed_pass.n)
+            agreed_pass.n += 1
+            try:
+                got = encode_pass()
+                with trace.span("node_job.io_drain"):
+                    drain_io()  # checkpoints and part files of this pass are on disk
+            except Exception as e:  # noqa: BLE001 - re-raised below on every rank
+                err = e
+            with trace.span("node_job.verdict"):
+                failed = allreduce_stats([1.0 if err else 0.0], cdev, op="max")[0]
+            if failed:
+                raise err if err is not None else RuntimeError("a peer rank failed this job")
+            return got
 
-    agreed_pass.n = 0
-    passes = 1
-    rc_errors: list = []  # per pass after pass 1: achieved / target - 1, per rung
-    if bitrate_kbps > 0:
-        # pass 1 at the base QP -> every frame's bits, all-reduced over the node (RCCL) ->
-        # one global per-frame QP plan -> pass 2 with rank-local rate feedback
-        agreed_pass()
-        starts = np.cumsum([0] + [n for _, n in segs])
-        flat = np.zeros(len(rungs) * nfr)
-        for (r, i), fb in rc["bits"].items():
-            flat[r * nfr + starts[i]:r * nfr + starts[i] + len(fb)] = 8.0 * np.asarray(fb, np.float64)
-        flat = allreduce_stats(flat, cdev)  # RC statistics all-reduce
-        fps = src.fps_num / src.fps_den
-        rc["b1"] = {(r, i): flat[r * nfr + starts[i]:r * nfr + starts[i] + n] for r in range(len(rungs))
-                    for i, (_, n) in enumerate(segs)}
-        plan = []
-        for r in range(len(rungs)):
-            scale = (rungs[r][0] * rungs[r][1]) / (rungs[0][0] * rungs[0][1])  # per-rung budget ~ pixels
-            target = bitrate_kbps * 1000 * nfr / fps * scale
-            per_seg, _ = plan_frame_qps([rc["b1"][(r, i)] for i in range(len(segs))], qp, target,
-                                        key_offset=-2.0 if codec == "av1" else None)
-            plan.append(per_seg)
-        rc["plan"] = plan
-        targets = [bitrate_kbps * 1000 * nfr / fps * (rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]
+        agreed_pass.n = 0
         passes = 1
-        for _ in range(2):  # pass 2, plus a corrected pass 3 only when pass 2 misses by > RC_TOLERANCE
-            rc["bits"] = {}
-            rc["fb"] = RateFeedback()
-            quality.clear()
-            mine = agreed_pass()
-            passes += 1
-            got = np.zeros(len(rungs))
+        rc_errors: list = []  # per pass after pass 1: achieved / target - 1, per rung
+        if bitrate_kbps > 0:
+            # pass 1 at the base QP -> every frame's bits, all-reduced over the node (RCCL) ->
+            # one global per-frame QP plan -> pass 2 with rank-local rate feedback
+            agreed_pass()
+            starts = np.cumsum([0] + [n for _, n in segs])
+            flat = np.zeros(len(rungs) * nfr)
             for (r, i), fb in rc["bits"].items():
-                if (r, i) in mine:
-                    got[r] += 8.0 * sum(fb)
-            got = allreduce_stats(got, cdev)
-            err = got / np.asarray(targets) - 1.0
-            rc_errors.append([round(float(e), 4) for e in err])
-            if np.all(np.abs(err) <= RC_TOLERANCE):
-                break
-            # the response to a uniform QP shift around the pass-2 operating point: move
-            # every frame's plan by the rung's residual (the model slope only scales it)
+                flat[r * nfr + starts[i]:r * nfr + starts[i] + len(fb)] = 8.0 * np.asarray(fb, np.float64)
+            flat = allreduce_stats(flat, cdev)  # RC statistics all-reduce
+            fps = src.fps_num / src.fps_den
+            rc["b1"] = {(r, i): flat[r * nfr + starts[i]:r * nfr + starts[i] + n] for r in range(len(rungs))
+                        for i, (_, n) in enumerate(segs)}
+            plan = []
             for r in range(len(rungs)):
-                d = SLOPE * math.log2(max(got[r], 1.0) / targets[r])
-                plan[r] = [q + d for q in plan[r]]
-                for i in range(len(segs)):  # feedback baseline = pass-2 bits at the pass-2 QPs
-                    rc["b1"][(r, i)] = predict_bits(rc["b1"][(r, i)], 0, -d)
-    else:
-        mine = agreed_pass()
-    t_enc = time.time() - t0
-    # quality: per-rung frames + SSE of the segments encoded on this rank, all-reduced
-    qv = np.zeros((len(rungs), 4))
-    for (r, i), ps in quality.items():
-        qv[r] += [ps.frames, *ps.sse]
-    qv = allreduce_stats(qv.reshape(-1), cdev).reshape(len(rungs), 4)
-    # gather bitstreams to rank 0 (one message per rank: json index + concatenated bytes)
-    keys = sorted(mine)
-    header = json.dumps({"seg": [[r, i, len(mine[(r, i)])] for r, i in keys], "stats": stats}).encode()
-    blob = len(header).to_bytes(8, "little") + header + b"".join(mine[k] for k in keys)
-    with trace.span("node_job.gather"):
-        parts = gather_bytes_to_root(blob, cdev) if world > 1 else [blob]
-    result = {"world": world, "segments": len(segs), "rungs": [list(x) for x in rungs], "passes": passes,
-              "rc_errors": rc_errors}
-    if rank == 0:
-        streams: dict = {}
-        per_rank = []
-        for p in parts:
-            p = memoryview(p)
-            hl = int.from_bytes(p[:8], "little")
-            hdr = json.loads(bytes(p[8:8 + hl]))
-            idx = hdr["seg"]
-            per_rank.append(hdr["stats"])
-            off = 8 + hl
-            for r, i, n in idx:
-                streams[(r, i)] = p[off:off + n]
-                off += n
-        missing = [k for k in jobs if k not in streams]
-        if missing:
-            raise RuntimeError(f"segments missing at stitch: {missing}")
-        outs = []
-        with trace.span("node_job.side_plan"):
-            side = _side_plan(input_path, audio_stream)
-        for r, (ow, oh) in enumerate(rungs):
-            seg_bits = [streams[(r, i)] for i in range(len(segs))]
-            path = output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4"
-            with trace.span("node_job.mux"):  # streamed from the gathered buffers, no joined copy
-                path, nbytes = write_output(seg_bits, ow, oh, src.fps_num, src.fps_den, path, side)
-            q = psnr_from_sse(qv[r, 1:], ow * oh * qv[r, 0]) if qv[r, 0] else {}
-            outs.append({"path": path, "bytes": nbytes, "width": ow, "height": oh, "frames": nfr,
-                         "fps_num": src.fps_num, "fps_den": src.fps_den,
-                         "kbps": sum(len(b) for b in seg_bits) * 8 / (nfr * src.fps_den / src.fps_num) / 1000,
-                         "psnr_y": round(q["y"], 3) if q else None, "psnr_yuv": round(q["yuv"], 3) if q else None,
-                         "quality_frames": int(qv[r, 0])})
-        el = time.time() - t0
-        result.update(side_fields=side.fields if side else {}, side_warnings=side.warnings if side else [])
-        result.update(trace=trace.since(trace0), per_rank=per_rank, outputs=outs, qp_plan=[[round(float(np.mean(q)), 2) for q in row] for row in rc["plan"]] if rc["plan"] else
-                      [[qp] * len(segs) for _ in rungs], rc_offset=round(rc["fb"].offset(), 3),
-                      seconds=round(el, 3), encode_seconds=round(t_enc, 3),
-                      fps=round(nfr * len(rungs) / el, 2), encode_fps=round(nfr * len(rungs) * passes / max(t_enc, 1e-9), 2))
+                scale = (rungs[r][0] * rungs[r][1]) / (rungs[0][0] * rungs[0][1])  # per-rung budget ~ pixels
+                target = bitrate_kbps * 1000 * nfr / fps * scale
+                per_seg, _ = plan_frame_qps([rc["b1"][(r, i)] for i in range(len(segs))], qp, target,
+                                            key_offset=-2.0 if codec == "av1" else None)
+                plan.append(per_seg)
+            rc["plan"] = plan
+            targets = [bitrate_kbps * 1000 * nfr / fps * (rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]
+            passes = 1
+            for _ in range(2):  # pass 2, plus a corrected pass 3 only when pass 2 misses by > RC_TOLERANCE
+                rc["bits"] = {}
+                rc["fb"] = RateFeedback()
+                quality.clear()
+                mine = agreed_pass()
+                passes += 1
+                got = np.zeros(len(rungs))
+                for (r, i), fb in rc["bits"].items():
+                    if (r, i) in mine:
+                        got[r] += 8.0 * sum(fb)
+                got = allreduce_stats(got, cdev)
+                err = got / np.asarray(targets) - 1.0
+                rc_errors.append([round(float(e), 4) for e in err])
+                if np.all(np.abs(err) <= RC_TOLERANCE):
+                    break
+                # the response to a uniform QP shift around the pass-2 operating point: move
+                # every frame's plan by the rung's residual (the model slope only scales it)
+                for r in range(len(rungs)):
+                    d = SLOPE * math.log2(max(got[r], 1.0) / targets[r])
+                    plan[r] = [q + d for q in plan[r]]
+                    for i in range(len(segs)):  # feedback baseline = pass-2 bits at the pass-2 QPs
+                        rc["b1"][(r, i)] = predict_bits(rc["b1"][(r, i)], 0, -d)
+        else:
+            mine = agreed_pass()
+        t_enc = time.time() - t0
+        # quality: per-rung frames + SSE of the segments encoded on this rank, all-reduced
+        qv = np.zeros((len(rungs), 4))
+        for (r, i), ps in quality.items():
+            qv[r] += [ps.frames, *ps.sse]
+        qv = allreduce_stats(qv.reshape(-1), cdev).reshape(len(rungs), 4)
+        # gather bitstreams to rank 0 (one message per rank: json index + concatenated bytes)
+        keys = sorted(mine)
+        header = json.dumps({"seg": [[r, i, len(mine[(r, i)])] for r, i in keys], "stats": stats}).encode()
+        blob = len(header).to_bytes(8, "little") + header + b"".join(mine[k] for k in keys)
+        with trace.span("node_job.gather"):
+            parts = gather_bytes_to_root(blob, cdev) if world > 1 else [blob]
+        result = {"world": world, "segments": len(segs), "rungs": [list(x) for x in rungs], "passes": passes,
+                  "rc_errors": rc_errors}
+        if rank == 0:
+            streams: dict = {}
+            per_rank = []
+            for p in parts:  # (empty bitstream lists when the stitch streamed)
+                p = memoryview(p)
+                hl = int.from_bytes(p[:8], "little")
+                hdr = json.loads(bytes(p[8:8 + hl]))
+                idx = hdr["seg"]
+                per_rank.append(hdr["stats"])
+                off = 8 + hl
+                for r, i, n in idx:
+                    streams[(r, i)] = p[off:off + n]
+                    off += n
+            outs = []
+            if stitcher is not None:  # every segment is already in the streaming files
+                with trace.span("node_job.stitch_wait"):
+                    sizes = stitcher.finish()
+                for r, (ow, oh) in enumerate(rungs):
+                    os.replace(out_paths[r] + ".tmp", out_paths[r])
+                    outs.append({"path": out_paths[r], "bytes": sizes[r], "width": ow, "height": oh,
+                                 "seg_bytes": stitcher.bytes[r]})
+            else:
+                missing = [k for k in jobs if k not in streams]
+                if missing:
+                    raise RuntimeError(f"segments missing at stitch: {missing}")
+                for r, (ow, oh) in enumerate(rungs):
+                    seg_bits = [streams[(r, i)] for i in range(len(segs))]
+                    with trace.span("node_job.mux"):  # streamed from the gathered buffers, no joined copy
+                        path, nbytes = write_output(seg_bits, ow, oh, src.fps_num, src.fps_den, out_paths[r], side)
+                    outs.append({"path": path, "bytes": nbytes, "width": ow, "height": oh,
+                                 "seg_bytes": sum(len(b) for b in seg_bits)})
+            for r, o in enumerate(outs):
+                q = psnr_from_sse(qv[r, 1:], o["width"] * o["height"] * qv[r, 0]) if qv[r, 0] else {}
+                o.update(frames=nfr, fps_num=src.fps_num, fps_den=src.fps_den,
+                         kbps=o.pop("seg_bytes") * 8 / (nfr * src.fps_den / src.fps_num) / 1000,
+                         psnr_y=round(q["y"], 3) if q else None, psnr_yuv=round(q["yuv"], 3) if q else None,
+                         quality_frames=int(qv[r, 0]))
+            el = time.time() - t0
+            result.update(side_fields=side.fields if side else {}, side_warnings=side.warnings if side else [])
+            result.update(trace=trace.since(trace0), per_rank=per_rank, outputs=outs, qp_plan=[[round(float(np.mean(q)), 2) for q in row] for row in rc["plan"]] if rc["plan"] else
+                          [[qp] * len(segs) for _ in rungs], rc_offset=round(rc["fb"].offset(), 3),
+                          seconds=round(el, 3), encode_seconds=round(t_enc, 3),
+                          fps=round(nfr * len(rungs) / el, 2), encode_fps=round(nfr * len(rungs) * passes / max(t_enc, 1e-9), 2))
+    except BaseException:
+        if stitcher is not None:
+            stitcher.cancel()
+        raise
+    finally:
+        io_pool.shutdown(wait=True)
+        if streaming and rank == 0:
+            import shutil
+
+            shutil.rmtree(parts_dir, ignore_errors=True)
     if own_cache:
         cache.close()
     return result
