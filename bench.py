@@ -355,7 +355,8 @@ def av1_main(args) -> None:
     def comm_rc(i, gfut):
         out = comm(gfut)
         if args.kbps > 0:  # the post thread: every rank records the same all-reduced totals
-            ctl.record(nominal, predicted.pop(i), 8.0 * float(out[0][1]))
+            b1, qall = predicted.pop(i)
+            ctl.record(nominal, b1, qall, args.qp, 8.0 * float(out[0][1]))
         return out
 
     def plan_pass2(i, g1fut):
@@ -374,10 +375,11 @@ def av1_main(args) -> None:
         dist.all_reduce(flat)  # RC statistics all-reduce over the node
         allb = flat.cpu().numpy().reshape(world * batch, args.gop)
         ask, _ = ctl.request(nominal)
-        plan, pred = plan_frame_qps(list(allb), args.qp, ask, key_offset=AV1_KEY_QP_OFFSET)
-        predicted[i] = pred
+        plan, _ = plan_frame_qps(list(allb), args.qp, ask, key_offset=AV1_KEY_QP_OFFSET, slope=ctl.slope)
+        qall = np.stack([round_qps(p) for p in plan])  # every rank's integer plan (for the slope fit)
+        predicted[i] = (allb, qall)
         pass1_bits.append(float(mine.sum()))
-        return np.array([[av1m.qindex_for_hevc_qp(int(v)) for v in round_qps(plan[rank * batch + b])]
+        return np.array([[av1m.qindex_for_hevc_qp(int(v)) for v in qall[rank * batch + b]]
                          for b in range(batch)], np.int32).T
 
     def loader(i: int):
@@ -396,8 +398,17 @@ def av1_main(args) -> None:
     plans = {}
     counter = [0]
 
-    def pass1(i: int):  # pass 1 of step i on the GPU; its plan queues on the post thread
-        plans[i] = post.ex.submit(plan_pass2, i, eng.encode_gop(args.gop, loader(i), async_host=True))
+    def pass1(i: int):
+        """Pass 1 of step i on the GPU, a fast first pass (x264-style): no restoration
+        search, whose ~28 % of the GPU step only fine-tunes the reconstruction; the fitted
+        bits(QP) slope absorbs the small pass-1 / pass-2 difference.  Its plan queues on the
+        post thread."""
+        eng.lr_enabled = False
+        try:
+            g1 = eng.encode_gop(args.gop, loader(i), async_host=True)
+        finally:
+            eng.lr_enabled = True
+        plans[i] = post.ex.submit(plan_pass2, i, g1)
 
     def step(_s: int):
         i = counter[0]
@@ -440,10 +451,12 @@ def av1_main(args) -> None:
                 "model": f"AV1 subset (tv) qindex {q} 16x16 blocks +deblock +CDEF +LR {args.res} synthetic"
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
                 "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame q-index plan, target "
-                                 f"{args.kbps:g} kbps per 30 fps stream, batch feedback (bias + debt)"
-                                 if args.kbps > 0 else "constant q-index"),
+                                 f"{args.kbps:g} kbps per 30 fps stream, fast first pass (no LR search), batch "
+                                 "feedback (fitted bits(QP) slope + bounded debt)" if args.kbps > 0 else "constant q-index"),
                 "kbps_error_pct": round(100 * (tot[1] * 8 / (frames / 30.0) / 1000.0 / args.kbps - 1), 2)
                 if args.kbps > 0 else None,
+                "rc_fitted_slope": round(ctl.slope, 3) if args.kbps > 0 else None,
+                "rc_steps_actual_pred_slope": ctl.log if args.kbps > 0 else None,
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",
@@ -553,13 +566,17 @@ def main() -> None:
         flat[rank * batch * args.gop:(rank + 1) * batch * args.gop] = torch.from_numpy(mine).to(dev)
         dist.all_reduce(flat)
         ask, _ = ctl.request(nominal)
-        plan, predicted[i] = plan_frame_qps(list(flat.cpu().numpy().reshape(world * batch, args.gop)), args.qp, ask)
+        allb = flat.cpu().numpy().reshape(world * batch, args.gop)
+        plan, _ = plan_frame_qps(list(allb), args.qp, ask, slope=ctl.slope)
+        qall = np.stack([round_qps(p) for p in plan])
+        predicted[i] = (allb, qall)
         pass1_bits.append(float(mine.sum()))
-        return np.stack([round_qps(plan[rank * batch + b]) for b in range(batch)])
+        return qall[rank * batch:(rank + 1) * batch]
 
     def comm_rc(i, segs, sse):
         out = comm(segs, sse)
-        ctl.record(nominal, predicted.pop(i), 8.0 * float(out[0][1]))
+        b1, qall = predicted.pop(i)
+        ctl.record(nominal, b1, qall, args.qp, 8.0 * float(out[0][1]))
         return out
 
     counter = [0]
@@ -605,8 +622,11 @@ def main() -> None:
                 "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else "")
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
                 "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame QP plan, target {args.kbps:g} "
-                                 "kbps per 30 fps stream, batch feedback (bias + debt)" if args.kbps > 0 else f"CQP {args.qp}"),
+                                 "kbps per 30 fps stream, batch feedback (fitted bits(QP) slope + bounded debt)"
+                                 if args.kbps > 0 else f"CQP {args.qp}"),
                 "kbps_error_pct": round(100 * (kbps / args.kbps - 1), 2) if args.kbps > 0 else None,
+                "rc_fitted_slope": round(ctl.slope, 3) if args.kbps > 0 else None,
+                "rc_steps_actual_pred_slope": ctl.log if args.kbps > 0 else None,
                 "pass1_kbps_rank0": round(sum(pass1_bits[-args.steps:]) / (batch * args.gop * args.steps / 30.0) / 1000.0, 1)
                 if pass1_bits else None,
                 "global_batch": world * batch,

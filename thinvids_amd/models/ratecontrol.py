@@ -97,12 +97,12 @@ def frame_sizes(annexb: bytes) -> list[int]:
     return out
 
 
-def predict_bits(b1: np.ndarray, q1, q) -> np.ndarray:
-    return np.asarray(b1, np.float64) * np.power(2.0, -(np.asarray(q, np.float64) - np.asarray(q1, np.float64)) / SLOPE)
+def predict_bits(b1: np.ndarray, q1, q, slope: float = SLOPE) -> np.ndarray:
+    return np.asarray(b1, np.float64) * np.power(2.0, -(np.asarray(q, np.float64) - np.asarray(q1, np.float64)) / slope)
 
 
 def plan_frame_qps(bits1: list, q1: int, target_bits: float, qcomp: float = QCOMP, qp_min: int = 10,
-                   qp_max: int = 51, key_offset: float | None = None) -> tuple[list, float]:
+                   qp_max: int = 51, key_offset: float | None = None, slope: float = SLOPE) -> tuple[list, float]:
     """Per-frame real-valued QPs for pass 2.  bits1: per segment, the pass-1 bits of every
     frame (encoded at q1).  Frame f gets a share t_f proportional to b_f^qcomp (compressed
     complexity, as x264's qcomp), scaled so sum(t) == target_bits; its QP is the one the
@@ -110,11 +110,13 @@ def plan_frame_qps(bits1: list, q1: int, target_bits: float, qcomp: float = QCOM
     key frame) is instead pinned `key_offset` QP from its segment's mean inter-frame QP —
     the inter frames predict from it, so starving it costs more bits than it saves (the
     frame-independent bits model misses that) — and one uniform shift of every QP, found
-    by bisection, restores the target.  Returns (per-segment QP arrays, predicted total)."""
+    by bisection, restores the target.  `slope`: QP steps per halving of the bits (a fitted
+    value from BatchRateController, else SLOPE).  Returns (per-segment QP arrays, predicted
+    total)."""
     flat = np.concatenate([np.maximum(np.asarray(b, np.float64), 1.0) for b in bits1])
     w = flat ** qcomp
     t = target_bits * w / w.sum()
-    q = np.clip(q1 + SLOPE * np.log2(flat / t), qp_min, qp_max)
+    q = np.clip(q1 + slope * np.log2(flat / t), qp_min, qp_max)
     if key_offset is not None:
         k, keys = 0, []
         for b in bits1:
@@ -125,7 +127,7 @@ def plan_frame_qps(bits1: list, q1: int, target_bits: float, qcomp: float = QCOM
         lo, hi = -30.0, 30.0
         for _ in range(50):  # predicted bits fall monotonically with a uniform shift
             mid = (lo + hi) / 2
-            if predict_bits(flat, q1, np.clip(q + mid, qp_min, qp_max)).sum() > target_bits:
+            if predict_bits(flat, q1, np.clip(q + mid, qp_min, qp_max), slope).sum() > target_bits:
                 lo = mid
             else:
                 hi = mid
@@ -134,7 +136,7 @@ def plan_frame_qps(bits1: list, q1: int, target_bits: float, qcomp: float = QCOM
     for b in bits1:
         out.append(q[k:k + len(b)])
         k += len(b)
-    return out, float(predict_bits(flat, q1, q).sum())
+    return out, float(predict_bits(flat, q1, q, slope).sum())
 
 
 def round_qps(qf: np.ndarray, offset: float = 0.0, qp_min: int = 10, qp_max: int = 51) -> np.ndarray:
@@ -151,29 +153,60 @@ def round_qps(qf: np.ndarray, offset: float = 0.0, qp_min: int = 10, qp_max: int
 
 
 class BatchRateController:
-    """Batch-sequential 2-pass feedback (the bench's steps, a worker's claims): each batch is
-    planned from its own pass-1 statistics, and the error of the batches already finished is
-    carried into the next plan -- the model's bias (actual / predicted bits, which absorbs a
-    content-dependent bits(QP) slope the fixed SLOPE misses) and half of the accumulated
-    overshoot / undershoot (the debt is repaid over about two batches).  Deterministic in
-    the (all-reduced) inputs, so every rank computes the same plan."""
+    """Batch-sequential 2-pass feedback (the bench's steps, a worker's claims).  Each batch
+    is planned from its own pass-1 statistics; the finished batches teach the model:
 
-    def __init__(self, repay: float = 0.5):
-        self.target = self.actual = self.pred = 0.0
-        self.repay = repay
+    * the bits(QP) slope is re-fitted to them -- the one slope s for which
+      sum_f b1_f * 2^(-(q_f - q1) / s) over every finished frame equals the bits those
+      frames really produced at their planned QPs (a content- and codec-dependent value:
+      5.8 - 9.9 QP per halving measured on this repo's encoders, vs the fixed SLOPE);
+    * any residual model bias (actual / predicted with the fitted slope) scales the request;
+    * a quarter of the accumulated overshoot / undershoot is repaid by the next batch, at
+      most 4 % of its share (a batch never strays further than that from the target once
+      the model has been fitted).
+
+    Deterministic in the (all-reduced) inputs, so every rank computes the same plan."""
+
+    def __init__(self, repay: float = 0.25, max_repay: float = 0.04, slope: float = SLOPE):
+        self.target = self.actual = 0.0
+        self.repay, self.max_repay, self.slope = repay, max_repay, slope
+        self.hist: list = []  # (pass-1 bits per frame, planned integer QP per frame, q1, actual bits)
+        self.log: list = []  # per recorded batch: actual / nominal, model prediction / nominal, slope after
+
+    def _pred(self, slope: float) -> float:
+        return float(sum(predict_bits(b, q1, q, slope).sum() for b, q, q1, _ in self.hist))
 
     def request(self, nominal: float) -> tuple[float, float]:
         """(bits to ask the planner for, bits this batch should really produce)."""
-        bias = self.actual / self.pred if self.pred > 0 else 1.0
-        want = max(0.5 * nominal, nominal + self.repay * (self.target - self.actual))
+        lim = self.max_repay * nominal
+        want = nominal + float(np.clip(self.repay * (self.target - self.actual), -lim, lim))
+        pred = self._pred(self.slope) if self.hist else 0.0
+        bias = sum(h[3] for h in self.hist) / pred if pred > 0 else 1.0
         return want / bias, want
 
-    def record(self, nominal: float, predicted: float, actual: float) -> None:
-        """nominal: the batch's share of the target; predicted: the planner's total for the
-        bits it was asked for; actual: what the batch produced."""
+    def record(self, nominal: float, bits1, qps, q1: float, actual: float) -> None:
+        """nominal: the batch's share of the target; bits1 / qps: every frame's pass-1 bits
+        and planned (integer) QP; actual: the bits the batch produced."""
         self.target += nominal
-        self.pred += predicted
         self.actual += actual
+        pred0 = float(predict_bits(bits1, q1, qps, self.slope).sum())
+        self.hist.append((np.asarray(bits1, np.float64).ravel(), np.asarray(qps, np.float64).ravel(), float(q1),
+                          float(actual)))
+        act = sum(h[3] for h in self.hist)
+        lo, hi = 3.0, 24.0
+        flo = self._pred(lo) - act
+        self.log.append([round(actual / nominal, 4), round(pred0 / nominal, 4), round(self.slope, 3)])
+        if flo * (self._pred(hi) - act) > 0:
+            return  # no slope explains it (plan too close to q1): the bias term covers it
+        for _ in range(40):
+            mid = 0.5 * (lo + hi)
+            fm = self._pred(mid) - act
+            if (fm > 0) == (flo > 0):
+                lo, flo = mid, fm
+            else:
+                hi = mid
+        self.slope = 0.5 * (lo + hi)
+        self.log[-1][2] = round(self.slope, 3)
 
 
 class RateFeedback:
