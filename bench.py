@@ -355,8 +355,8 @@ def av1_main(args) -> None:
     def comm_rc(i, gfut):
         out = comm(gfut)
         if args.kbps > 0:  # the post thread: every rank records the same all-reduced totals
-            b1, qall = predicted.pop(i)
-            ctl.record(nominal, b1, qall, args.qp, 8.0 * float(out[0][1]))
+            want, u = predicted.pop(i)
+            ctl.record(nominal, want, u, 8.0 * float(out[0][1]))
         return out
 
     def plan_pass2(i, g1fut):
@@ -374,10 +374,10 @@ def av1_main(args) -> None:
         flat[rank * batch * args.gop:(rank + 1) * batch * args.gop] = torch.from_numpy(mine).to(dev)
         dist.all_reduce(flat)  # RC statistics all-reduce over the node
         allb = flat.cpu().numpy().reshape(world * batch, args.gop)
-        ask, _ = ctl.request(nominal)
-        plan, _ = plan_frame_qps(list(allb), args.qp, ask, key_offset=AV1_KEY_QP_OFFSET, slope=ctl.slope)
-        qall = np.stack([round_qps(p) for p in plan])  # every rank's integer plan (for the slope fit)
-        predicted[i] = (allb, qall)
+        ask, want, u = ctl.request(nominal)
+        plan, _ = plan_frame_qps(list(allb), args.qp, ask, key_offset=AV1_KEY_QP_OFFSET)
+        qall = np.stack([round_qps(p, u) for p in plan])
+        predicted[i] = (want, u)
         pass1_bits.append(float(mine.sum()))
         return np.array([[av1m.qindex_for_hevc_qp(int(v)) for v in qall[rank * batch + b]]
                          for b in range(batch)], np.int32).T
@@ -400,8 +400,8 @@ def av1_main(args) -> None:
 
     def pass1(i: int):
         """Pass 1 of step i on the GPU, a fast first pass (x264-style): no restoration
-        search, whose ~28 % of the GPU step only fine-tunes the reconstruction; the fitted
-        bits(QP) slope absorbs the small pass-1 / pass-2 difference.  Its plan queues on the
+        search, whose ~28 % of the GPU step only fine-tunes the reconstruction; the measured
+        QP-offset response absorbs the small pass-1 / pass-2 difference.  Its plan queues on the
         post thread."""
         eng.lr_enabled = False
         try:
@@ -452,11 +452,10 @@ def av1_main(args) -> None:
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
                 "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame q-index plan, target "
                                  f"{args.kbps:g} kbps per 30 fps stream, fast first pass (no LR search), batch "
-                                 "feedback (fitted bits(QP) slope + bounded debt)" if args.kbps > 0 else "constant q-index"),
+                                 "feedback (measured QP offset response + bounded debt)" if args.kbps > 0 else "constant q-index"),
                 "kbps_error_pct": round(100 * (tot[1] * 8 / (frames / 30.0) / 1000.0 / args.kbps - 1), 2)
                 if args.kbps > 0 else None,
-                "rc_fitted_slope": round(ctl.slope, 3) if args.kbps > 0 else None,
-                "rc_steps_actual_pred_slope": ctl.log if args.kbps > 0 else None,
+                "rc_steps_actual_wanted_offset": ctl.log if args.kbps > 0 else None,
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",
@@ -565,18 +564,18 @@ def main() -> None:
         mine = np.concatenate([8.0 * np.asarray(frame_sizes(x), np.float64) for x in segs1])
         flat[rank * batch * args.gop:(rank + 1) * batch * args.gop] = torch.from_numpy(mine).to(dev)
         dist.all_reduce(flat)
-        ask, _ = ctl.request(nominal)
+        ask, want, u = ctl.request(nominal)
         allb = flat.cpu().numpy().reshape(world * batch, args.gop)
-        plan, _ = plan_frame_qps(list(allb), args.qp, ask, slope=ctl.slope)
-        qall = np.stack([round_qps(p) for p in plan])
-        predicted[i] = (allb, qall)
+        plan, _ = plan_frame_qps(list(allb), args.qp, ask)
+        qall = np.stack([round_qps(p, u) for p in plan])
+        predicted[i] = (want, u)
         pass1_bits.append(float(mine.sum()))
         return qall[rank * batch:(rank + 1) * batch]
 
     def comm_rc(i, segs, sse):
         out = comm(segs, sse)
-        b1, qall = predicted.pop(i)
-        ctl.record(nominal, b1, qall, args.qp, 8.0 * float(out[0][1]))
+        want, u = predicted.pop(i)
+        ctl.record(nominal, want, u, 8.0 * float(out[0][1]))
         return out
 
     counter = [0]
@@ -622,11 +621,10 @@ def main() -> None:
                 "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else "")
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
                 "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame QP plan, target {args.kbps:g} "
-                                 "kbps per 30 fps stream, batch feedback (fitted bits(QP) slope + bounded debt)"
+                                 "kbps per 30 fps stream, batch feedback (measured QP offset response + bounded debt)"
                                  if args.kbps > 0 else f"CQP {args.qp}"),
                 "kbps_error_pct": round(100 * (kbps / args.kbps - 1), 2) if args.kbps > 0 else None,
-                "rc_fitted_slope": round(ctl.slope, 3) if args.kbps > 0 else None,
-                "rc_steps_actual_pred_slope": ctl.log if args.kbps > 0 else None,
+                "rc_steps_actual_wanted_offset": ctl.log if args.kbps > 0 else None,
                 "pass1_kbps_rank0": round(sum(pass1_bits[-args.steps:]) / (batch * args.gop * args.steps / 30.0) / 1000.0, 1)
                 if pass1_bits else None,
                 "global_batch": world * batch,

@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
     f.coef[0] = d.coef_y.data();
     f.coef[1] = d.coef_u.data();
     f.coef[2] = d.coef_v.data();
-    const int reps = 20;
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
     size_t bytes = 0;
     auto t0 = std::chrono::steady_clock::now();
     for (int r = 0; r < reps; ++r) {
