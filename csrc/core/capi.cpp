@@ -58,8 +58,9 @@ void* tv_cpu_encoder_new(int width, int height, int qp, int deblock, int range, 
   cfg.width = width;
   cfg.height = height;
   cfg.qp = qp;
-  cfg.deblock = (deblock & 1) != 0;  // bit 0: deblocking, bit 1: SAO
+  cfg.deblock = (deblock & 1) != 0;  // bit 0: deblocking, bit 1: SAO, bit 2: WPP
   cfg.sao = (deblock & 2) != 0;
+  cfg.wpp = (deblock & 4) != 0;
   cfg.max_merge_cand = max_merge;
   cfg.finalize();
   CpuEncoder* e = nullptr;  // a bad config becomes tv_last_error, not an abort across the FFI
@@ -73,6 +74,7 @@ void* tv_cpu_encoder_new_crf(int width, int height, int qp, int deblock, int ran
   cfg.qp = qp;
   cfg.deblock = (deblock & 1) != 0;
   cfg.sao = (deblock & 2) != 0;
+  cfg.wpp = (deblock & 4) != 0;
   cfg.max_merge_cand = max_merge;
   cfg.crf = crf;
   cfg.finalize();

@@ -32,6 +32,7 @@ struct Pps {
   int init_qp = 26;
   bool deblock = true;
   bool sign_hiding = false;
+  bool wpp = false;
   bool valid = false;
 };
 
@@ -114,7 +115,8 @@ Pps parse_pps(BitReader& br) {
   br.u(1);
   if (br.u(1) || br.u(1)) fail("weighted prediction unsupported");
   if (br.u(1)) fail("transquant bypass unsupported");
-  if (br.u(1) || br.u(1)) fail("tiles / WPP unsupported");
+  if (br.u(1)) fail("tiles unsupported");
+  p.wpp = br.u(1) != 0;
   br.u(1);
   if (br.u(1)) {
     if (br.u(1)) fail("deblocking override unsupported");
@@ -130,9 +132,10 @@ Pps parse_pps(BitReader& br) {
 class SliceDecoder {
  public:
   SliceDecoder(const Sps& sps, const Pps& pps, bool islice, int qp, int max_merge, BitReader* br,
-               Picture* cur, const Picture* ref, FrameDecisions* fd, bool sao)
-      : sps_(sps), islice_(islice), qp_(qp), max_merge_(max_merge), dec_(br), cur_(cur), ref_(ref),
-        fd_(fd), sao_(sao) {
+               Picture* cur, const Picture* ref, FrameDecisions* fd, bool sao,
+               std::vector<size_t> row_start = {})
+      : sps_(sps), islice_(islice), qp_(qp), max_merge_(max_merge), dec_(br), br_(br), cur_(cur), ref_(ref),
+        fd_(fd), sao_(sao), row_start_(std::move(row_start)) {
     (void)pps;
     ctx_.init(islice ? 0 : 1, qp);
     skip_.assign((size_t)fd->w8 * fd->h8, 0);
@@ -140,16 +143,30 @@ class SliceDecoder {
     dec_.start();
   }
 
+  // WPP (row_start_ = byte position of every CTB row's substream in the RBSP): each row
+  // restarts the arithmetic decoder at its entry point with the contexts stored after the
+  // second CTB of the row above (9.3.1 / 9.3.2.4)
   void run() {
     const int wc = sps_.coded_w >> kCtbLog2, hc = sps_.coded_h >> kCtbLog2;
-    for (int cy = 0; cy < hc; ++cy)
+    const bool wpp = !row_start_.empty();
+    if (wpp && (int)row_start_.size() != hc) fail("entry points do not match the CTB rows");
+    ContextSet synced{};
+    for (int cy = 0; cy < hc; ++cy) {
+      if (wpp && cy > 0) {
+        br_->seek(row_start_[cy] * 8);
+        dec_.start();
+        ctx_ = synced;
+      }
       for (int cx = 0; cx < wc; ++cx) {
         if (sao_) parse_sao(cx, cy);
         quadtree(cx << kCtbLog2, cy << kCtbLog2, kCtbLog2, 0);
+        if (wpp && cx == 1) synced = ctx_;
         const int end = dec_.decode_terminate();
         const bool last = (cy == hc - 1) && (cx == wc - 1);
         if (end != (last ? 1 : 0)) fail("end_of_slice_segment_flag mismatch");
+        if (wpp && !last && cx == wc - 1 && dec_.decode_terminate() != 1) fail("end_of_subset_one_bit missing");
       }
+    }
   }
 
  private:
@@ -564,11 +581,13 @@ class SliceDecoder {
   bool islice_;
   int qp_, max_merge_;
   CabacDecoder dec_;
+  BitReader* br_;
   ContextSet ctx_;
   Picture* cur_;
   const Picture* ref_;
   FrameDecisions* fd_;
   bool sao_;
+  std::vector<size_t> row_start_;
   std::vector<uint8_t> skip_, decoded_;
 };
 
@@ -627,7 +646,8 @@ void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int cou
     } else if (type <= 21 && (pic < start_pic || pic >= end_pic)) {
       continue;
     }
-    std::vector<uint8_t> rbsp = unescape_rbsp(nal.data + 2, nal.size - 2);
+    std::vector<size_t> removed;  // escaped indices of the emulation-prevention bytes
+    std::vector<uint8_t> rbsp = unescape_rbsp_map(nal.data + 2, nal.size - 2, &removed);
     BitReader br(rbsp.data(), rbsp.size());
     if (type == NAL_VPS || type == NAL_AUD || type >= 36) continue;
     if (type == NAL_SPS) {
@@ -668,10 +688,36 @@ void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int cou
       max_merge = 5 - (int)br.ue();
     }
     const int qp = pps.init_qp + br.se();
+    std::vector<size_t> entry;  // substream sizes (escaped bytes)
+    if (pps.wpp) {
+      const uint32_t n = br.ue();
+      if (n) {
+        const int len = (int)br.ue() + 1;
+        if (len > 32) fail("bad offset_len");
+        for (uint32_t i = 0; i < n; ++i) entry.push_back((size_t)br.u(len) + 1);
+      }
+    }
     // byte_alignment()
     if (br.bit() != 1) fail("missing alignment bit");
     while (br.pos() & 7)
       if (br.bit() != 0) fail("bad alignment bits");
+    std::vector<size_t> row_start;
+    if (pps.wpp) {  // entry points count emulation-prevention bytes: map them to RBSP bytes
+      const size_t d0 = br.byte_pos();
+      size_t esc = d0;
+      for (size_t e : removed)
+        if (e <= esc) ++esc;  // escaped index of RBSP byte d0
+      auto rbsp_of = [&](size_t e) {
+        size_t k = 0;
+        while (k < removed.size() && removed[k] < e) ++k;
+        return e - k;
+      };
+      row_start.push_back(d0);
+      for (size_t s : entry) {
+        esc += s;
+        row_start.push_back(rbsp_of(esc));
+      }
+    }
     DecodedPicture dp;
     dp.poc = poc;
     dp.idr = idr;
@@ -682,7 +728,7 @@ void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int cou
       ref = &ref_pic;
     }
     last_decisions.alloc(sps.coded_w, sps.coded_h);
-    SliceDecoder sd(sps, pps, islice, qp, max_merge, &br, &dp.pic, ref, &last_decisions, sao);
+    SliceDecoder sd(sps, pps, islice, qp, max_merge, &br, &dp.pic, ref, &last_decisions, sao, row_start);
     sd.run();
     if (pps.deblock) deblock_picture(dp.pic, last_decisions.view(), qp);
     if (sao) sao_picture(dp.pic, last_decisions.sao.data());

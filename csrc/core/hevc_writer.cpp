@@ -154,7 +154,7 @@ void write_parameter_sets(const SeqConfig& cfg, std::vector<uint8_t>& out) {
     bw.put(0, 1);  // weighted_bipred_flag
     bw.put(0, 1);  // transquant_bypass_enabled_flag
     bw.put(0, 1);  // tiles_enabled_flag
-    bw.put(0, 1);  // entropy_coding_sync_enabled_flag
+    bw.put(cfg.wpp ? 1 : 0, 1);  // entropy_coding_sync_enabled_flag
     bw.put(0, 1);  // pps_loop_filter_across_slices_enabled_flag
     bw.put(1, 1);  // deblocking_filter_control_present_flag
     bw.put(0, 1);  //   deblocking_filter_override_enabled_flag
@@ -190,15 +190,30 @@ class SliceWriter {
     enc_.start();
   }
 
-  void write_all() {
+  // rows (WPP): one BitWriter per CTB row; row 0 may be the slice's own writer
+  void write_all(std::vector<BitWriter>* rows = nullptr) {
     const int wc = cfg_.coded_w >> kCtbLog2, hc = cfg_.coded_h >> kCtbLog2;
-    for (int cy = 0; cy < hc; ++cy)
+    ContextSet synced{};  // WPP: the contexts after the second CTB of the row above
+    for (int cy = 0; cy < hc; ++cy) {
+      if (rows && cy > 0) {  // a new substream: fresh arithmetic coder, synced contexts
+        enc_.rebind(&(*rows)[cy]);
+        enc_.start();
+        ctx_ = synced;
+      }
       for (int cx = 0; cx < wc; ++cx) {
         if (cfg_.sao) write_sao(cx, cy, wc);
         quadtree(cx << kCtbLog2, cy << kCtbLog2, kCtbLog2, 0);
         const bool last = (cy == hc - 1) && (cx == wc - 1);
-        enc_.encode_terminate(last ? 1 : 0);
+        if (rows && cx == 1) synced = ctx_;  // storage process (9.3.2.4) after CtbAddrX == 1
+        enc_.encode_terminate(last ? 1 : 0);  // end_of_slice_segment_flag
+        if (rows && !last && cx == wc - 1) {   // end_of_subset_one_bit + byte_alignment()
+          enc_.encode_terminate(1);
+          enc_.finish();
+          (*rows)[cy].put_bit(1);
+          (*rows)[cy].align_zero();
+        }
       }
+    }
     enc_.finish();
   }
 
@@ -694,6 +709,39 @@ class SliceWriter {
 
 }  // namespace
 
+size_t finish_wpp_slice(BitWriter& hdr, const std::vector<BitWriter>& rows, int nal, std::vector<uint8_t>& out) {
+  std::vector<const uint8_t*> p(rows.size());
+  std::vector<size_t> n(rows.size());
+  for (size_t r = 0; r < rows.size(); ++r) {
+    p[r] = rows[r].bytes().data();
+    n[r] = rows[r].bytes().size();
+  }
+  return finish_wpp_slice(hdr, p.data(), n.data(), (int)rows.size(), nal, out);
+}
+
+size_t finish_wpp_slice(BitWriter& hdr, const uint8_t* const* rows, const size_t* sizes, int nrows, int nal,
+                        std::vector<uint8_t>& out) {
+  std::vector<size_t> esc(nrows > 1 ? nrows - 1 : 0);
+  size_t mx = 1;
+  for (int r = 0; r + 1 < nrows; ++r) {
+    esc[r] = escaped_size(rows[r], sizes[r]);
+    mx = std::max(mx, esc[r]);
+  }
+  hdr.ue((uint32_t)esc.size());  // num_entry_point_offsets
+  if (!esc.empty()) {
+    int len = 1;
+    while (len < 32 && ((mx - 1) >> len)) ++len;
+    hdr.ue((uint32_t)(len - 1));  // offset_len_minus1
+    for (size_t e : esc) hdr.put((uint32_t)(e - 1), len);
+  }
+  hdr.put_bit(1);  // byte_alignment()
+  hdr.align_zero();
+  for (int r = 0; r < nrows; ++r) hdr.put_bytes(rows[r], sizes[r]);
+  const size_t before = out.size();
+  append_nal(out, nal, hdr.bytes());
+  return out.size() - before;
+}
+
 size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
                    std::vector<uint8_t>& out) {
   BitWriter bw;
@@ -715,15 +763,27 @@ size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
     bw.ue((uint32_t)(5 - cfg.max_merge_cand));  // five_minus_max_num_merge_cand
   }
   bw.se(fd.qp >= 0 ? fd.qp - cfg.qp : 0);  // slice_qp_delta (per-frame rate control)
-  // byte_alignment()
-  bw.put_bit(1);
-  bw.align_zero();
-  SliceWriter sw(cfg, fd, idr, &bw);
-  sw.write_all();
-  bw.trailing_bits();
-  const size_t before = out.size();
-  append_nal(out, nal, bw.bytes());
-  return out.size() - before;
+  if (!cfg.wpp) {
+    // byte_alignment()
+    bw.put_bit(1);
+    bw.align_zero();
+    SliceWriter sw(cfg, fd, idr, &bw);
+    sw.write_all();
+    bw.trailing_bits();
+    const size_t before = out.size();
+    append_nal(out, nal, bw.bytes());
+    return out.size() - before;
+  }
+  // WPP: the CTB rows are coded first (one substream each), then the header can carry their
+  // entry points (sizes after emulation prevention, which each substream's own bytes fix)
+  const int hc = cfg.coded_h >> kCtbLog2;
+  std::vector<BitWriter> rows(hc);
+  {
+    SliceWriter sw(cfg, fd, idr, &rows[0]);
+    sw.write_all(&rows);
+  }
+  rows[hc - 1].trailing_bits();  // rbsp_slice_segment_trailing_bits
+  return finish_wpp_slice(bw, rows, nal, out);
 }
 
 }  // namespace tv

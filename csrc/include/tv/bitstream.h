@@ -83,6 +83,7 @@ class BitReader {
     return (k & 1) ? (int32_t)((k + 1) / 2) : -(int32_t)(k / 2);
   }
   void byte_align() { pos_ = (pos_ + 7) & ~(size_t)7; }
+  void seek(size_t bit_pos) { pos_ = bit_pos; }
   size_t pos() const { return pos_; }
   size_t byte_pos() const { return pos_ >> 3; }
   size_t size() const { return n_; }
@@ -133,6 +134,39 @@ inline std::vector<uint8_t> unescape_rbsp(const uint8_t* p, size_t n) {
   for (size_t i = 0; i < n; ++i) {
     if (zeros >= 2 && p[i] == 3) {
       zeros = 0;
+      continue;
+    }
+    r.push_back(p[i]);
+    zeros = p[i] == 0 ? zeros + 1 : 0;
+  }
+  return r;
+}
+
+// Size of `n` RBSP bytes after emulation prevention, when the byte before them is nonzero
+// (a WPP substream: the previous one ends in its alignment '1' bit, the slice header in its
+// byte_alignment()), so its escaping depends on its own bytes only.
+inline size_t escaped_size(const uint8_t* p, size_t n) {
+  size_t out = n;
+  int zeros = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (zeros >= 2 && p[i] <= 3) {
+      ++out;
+      zeros = 0;
+    }
+    zeros = p[i] == 0 ? zeros + 1 : 0;
+  }
+  return out;
+}
+// unescape_rbsp that also records the escaped index of every removed byte (entry point
+// offsets count emulation-prevention bytes)
+inline std::vector<uint8_t> unescape_rbsp_map(const uint8_t* p, size_t n, std::vector<size_t>* removed) {
+  std::vector<uint8_t> r;
+  r.reserve(n);
+  int zeros = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (zeros >= 2 && p[i] == 3) {
+      zeros = 0;
+      removed->push_back(i);
       continue;
     }
     r.push_back(p[i]);

@@ -161,6 +161,7 @@ struct ContextSet {
 class CabacEncoder {
  public:
   explicit CabacEncoder(BitWriter* bw) : bw_(bw) {}
+  void rebind(BitWriter* bw) { bw_ = bw; }
   void start() {
     low_ = 0;
     range_ = 510;

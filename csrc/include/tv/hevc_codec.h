@@ -28,6 +28,10 @@ struct SeqConfig {
   int crf = 0;  // > 0: per-frame QP from the lookahead complexity (tv/rc_model.h)
   bool deblock = true;
   bool sao = false;
+  // wavefront parallel processing (entropy_coding_sync_enabled_flag): one CABAC substream per
+  // CTB row, contexts synced from the row above after its second CTB, entry points in the
+  // slice header -- the rows can be entropy-coded in parallel (the GPU CABAC path)
+  bool wpp = false;
   int fps_num = 30, fps_den = 1;
   void finalize() {
     coded_w = (width + kCtb - 1) / kCtb * kCtb;
@@ -121,6 +125,12 @@ struct Picture {
 
 // ----------------------------- bitstream generation -------------------------------------
 void write_parameter_sets(const SeqConfig& cfg, std::vector<uint8_t>& out);
+class BitWriter;
+// WPP slice assembly: `hdr` holds the slice header up to slice_qp_delta; appends the entry
+// points of the row substreams, byte_alignment(), the substreams (the last one already ends
+// in rbsp_slice_segment_trailing_bits) and emits the NAL.  Returns bytes appended.
+size_t finish_wpp_slice(BitWriter& hdr, const uint8_t* const* rows, const size_t* sizes, int nrows, int nal,
+                        std::vector<uint8_t>& out);
 // Encode one picture as a single slice NAL; returns bytes appended.
 size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
                    std::vector<uint8_t>& out);

@@ -154,3 +154,20 @@ def test_rc_log2_fixed_point():
     for x in (1, 2, 3, 640, 1024, 12345, 2 ** 31 - 1):
         assert abs(ratecontrol.log2_q8(x) - ref(x)) <= 1
     del C
+
+
+@pytest.mark.parametrize("w,h,sao", [(192, 128, False), (320, 200, True), (1920, 1080, True)])
+def test_wpp_substreams_decode_to_the_same_pictures(w, h, sao):
+    """entropy_coding_sync (WPP): one CABAC substream per CTB row, contexts synced after the
+    second CTB of the row above, entry points (counting emulation-prevention bytes) in the
+    slice header.  The reconstruction is unchanged, the oracle decodes every substream from
+    its entry point, and the rate cost of the context resets is small."""
+    frames = [hevc.synth_frame(3, t, w, h) for t in range(4)]
+    a, ra = hevc.encode_sequence_cpu(frames, qp=27, gop=4, search_range=32, sao=sao)
+    b, rb = hevc.encode_sequence_cpu(frames, qp=27, gop=4, search_range=32, sao=sao, wpp=True)
+    assert all((x[0] == y[0]).all() for x, y in zip(ra, rb))
+    assert len(b) > len(a) and len(b) < 1.03 * len(a)
+    dec = hevc.decode(b, coded=False)
+    assert len(dec.frames) == 4
+    for x, y in zip(dec.frames, rb):
+        assert (x[0] == y[0][:h, :w]).all() and (x[1] == y[1][:h // 2, :w // 2]).all()

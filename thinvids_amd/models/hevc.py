@@ -42,7 +42,7 @@ class CpuEncoder:
     """Scalar C++ HEVC encoder (software path; reference `software_encode`)."""
 
     def __init__(self, width: int, height: int, qp: int = 27, deblock: bool = True,
-                 search_range: int = 64, max_merge: int = 5, sao: bool = False, crf: int = 0):
+                 search_range: int = 64, max_merge: int = 5, sao: bool = False, crf: int = 0, wpp: bool = False):
         if width % 2 or height % 2:
             raise ValueError("width/height must be even")
         self.lib = core_lib()
@@ -52,10 +52,11 @@ class CpuEncoder:
             f = self.lib.tv_cpu_encoder_new_crf
             f.restype = C.c_void_p
             f.argtypes = [C.c_int] * 7
-            self.h = f(width, height, qp, int(deblock) | (2 if sao else 0), search_range, max_merge, int(crf))
+            self.h = f(width, height, qp, int(deblock) | (2 if sao else 0) | (4 if wpp else 0), search_range, max_merge,
+                       int(crf))
         else:
-            self.h = self.lib.tv_cpu_encoder_new(width, height, qp, int(deblock) | (2 if sao else 0), search_range,
-                                                 max_merge)
+            self.h = self.lib.tv_cpu_encoder_new(width, height, qp, int(deblock) | (2 if sao else 0) | (4 if wpp else 0),
+                                                 search_range, max_merge)
         if not self.h:
             raise ValueError(self.lib.tv_last_error().decode())
         self.out = Bytes()
