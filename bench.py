@@ -446,7 +446,7 @@ def av1_main(args) -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "uint8 video / int32 integer transforms (bit-exact AV1 subset)",
-            "data": "synthetic (seeded procedural YUV 4:2:0 source generated on GPU)",
+            "data": f"synthetic ({args.content} seeded procedural YUV 4:2:0 source generated on GPU)",
             "config": {
                 "model": f"AV1 subset (tv) qindex {q} 16x16 blocks +deblock +CDEF +LR {args.res} synthetic"
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
@@ -502,6 +502,9 @@ def main() -> None:
     ap.add_argument("--range", type=int, default=64, help="motion search range (full-res pels, multiple of 16)")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--content", choices=("smooth", "textured"), default="smooth",
+                    help="synthetic source: smooth value noise (default) or the textured variant (fine detail, "
+                         "per-pixel temporal grain, faster motion; tv/synth.h)")
     ap.add_argument("--ladder", default="", help="ABR mode (config #5): rung heights, e.g. 2160,1440,1080,720,480")
     ap.add_argument("--src", default="8k", choices=sorted(SRC), help="ABR mode: HDR10 source resolution")
     ap.add_argument("--job", action="store_true", help="end-to-end job mode (node executor, add -> DONE)")
@@ -510,6 +513,8 @@ def main() -> None:
     ap.add_argument("--qindex", type=int, default=0, help="AV1 q-index (0 = matched to --qp)")
     ap.add_argument("--kbps", type=float, default=0.0, help="2-pass rate control to this kbps per 30 fps stream")
     args = ap.parse_args()
+    if args.content == "textured":  # tv/synth.h kSynthTextured
+        args.seed = (args.seed | 0x80000000) & 0xFFFFFFFF
     if args.job:
         return job_main(args)
     from thinvids_amd.parallel.launch import launched_by_torchrun, spawn_ranks
@@ -616,7 +621,7 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "uint8 video / int32 integer transforms (bit-exact HEVC)",
-            "data": "synthetic (seeded procedural YUV 4:2:0 source generated on GPU)",
+            "data": f"synthetic ({args.content} seeded procedural YUV 4:2:0 source generated on GPU)",
             "config": {
                 "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else "")
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),

@@ -114,13 +114,13 @@ def test_qindex_mapping_monotone():
 
 
 # ---------------------------------------------------------------------------- GPU -----
-def _gpu_vs_golden(w, h, starts, nframes, q, static=False):
+def _gpu_vs_golden(w, h, starts, nframes, q, static=False, seed=11):
     import torch
 
     from thinvids_amd.models.av1_engine import Av1GpuEngine
 
     W, H = av1.coded_size(w, h)
-    segs = [_frames(11, w, h, nframes, t0) for t0 in starts]
+    segs = [_frames(seed, w, h, nframes, t0) for t0 in starts]
     if static:  # the first frame repeated: skip-block merging to 32x32 / 64x64
         segs = [[s[0]] * nframes for s in segs]
     eng = Av1GpuEngine(w, h, batch=len(starts), qindex=q)
@@ -152,6 +152,13 @@ def _gpu_vs_golden(w, h, starts, nframes, q, static=False):
 @pytest.mark.gpu
 def test_gpu_av1_engine_matches_golden_small():
     _gpu_vs_golden(200, 120, [0, 7], 4, 100)
+
+
+@pytest.mark.gpu
+def test_gpu_av1_engine_matches_golden_textured():
+    """Textured synthetic content (fine detail, per-pixel grain, fast motion: many large
+    levels, Golomb escapes, little skip): GPU == golden bit for bit."""
+    _gpu_vs_golden(200, 120, [0, 9], 4, 90, seed=3 | 0x80000000)
 
 
 @pytest.mark.gpu

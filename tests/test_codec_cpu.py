@@ -171,3 +171,19 @@ def test_wpp_substreams_decode_to_the_same_pictures(w, h, sao):
     assert len(dec.frames) == 4
     for x, y in zip(dec.frames, rb):
         assert (x[0] == y[0][:h, :w]).all() and (x[1] == y[1][:h // 2, :w // 2]).all()
+
+
+def test_textured_synthetic_variant():
+    """Seed bit 31 selects the textured source: deterministic, different from the smooth
+    one, grain that changes every frame, and much harder to code at the same QP."""
+    w, h = 160, 96
+    a = hevc.synth_frame(9 | 0x80000000, 3, w, h)
+    b = hevc.synth_frame(9 | 0x80000000, 3, w, h)
+    s = hevc.synth_frame(9, 3, w, h)
+    assert all((x == y).all() for x, y in zip(a, b))
+    assert (a[0] != s[0]).mean() > 0.5
+    t = [hevc.synth_frame(9 | 0x80000000, k, w, h) for k in range(4)]
+    sm = [hevc.synth_frame(9, k, w, h) for k in range(4)]
+    bt, _ = hevc.encode_sequence_cpu(t, qp=27, gop=4, search_range=32)
+    bs, _ = hevc.encode_sequence_cpu(sm, qp=27, gop=4, search_range=32)
+    assert len(bt) > 1.5 * len(bs)

@@ -87,3 +87,19 @@ def test_gpu_crf_bit_exact():
         frames = [hevc.synth_frame(5, start + f, w, h) for f in range(gop)]
         cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, crf=30, search_range=16)
         assert segs[b] == cpu_bs
+
+
+@pytest.mark.parametrize("sao", [False, True])
+def test_gpu_bit_exact_on_textured_content(sao):
+    """The textured synthetic variant (tv/synth.h: 2-pixel detail, per-pixel temporal grain,
+    faster motion) generated on the GPU and on the CPU, encoded by the engine and the golden
+    model: identical bitstreams."""
+    w, h, gop, rng = 320, 192, 4, 32
+    seed = 7 | 0x80000000
+    eng = _engine(width=w, height=h, qp=27, batch=2, gop=gop, search_range=rng, sao=sao, seed=seed)
+    segs = eng.encode_synthetic([0, 20])
+    for b, start in enumerate([0, 20]):
+        frames = [hevc.synth_frame(seed, start + f, w, h) for f in range(gop)]
+        cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, sao=sao, search_range=rng)
+        assert segs[b] == cpu_bs, f"segment {b}"
+    eng.close()
