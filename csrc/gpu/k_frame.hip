@@ -69,6 +69,9 @@ __device__ __forceinline__ int synth_objects(const SynthFrameCtx& f, int c, int 
   return v;
 }
 
+// kTex: the textured variant (seed bit 31) is a separate instantiation so the smooth source
+// keeps its register budget (a runtime branch doubled its time).
+template <bool kTex>
 __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t seed, FrameIdx fi) {
   const int c = blockIdx.y, b = blockIdx.z;
   const int pw = c ? g.W / 2 : g.W, ph = c ? g.H / 2 : g.H;
@@ -78,29 +81,38 @@ __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t see
   __syncthreads();
   uint8_t* P = src.plane(c, b, g);
   const int s = c ? 1 : 0, pq = pw >> 2;  // pw is a multiple of 16
+  constexpr bool tex = kTex;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < pq * ph; i += gridDim.x * blockDim.x) {
     const int y = i / pq, x0 = (i - y * pq) * 4;
-    const int yl = tv_min(y, dh - 1) << s;
-    const int32_t by16 = yl * 16 + ctx.t * 12;
-    VNoiseRow n0, n1, n2;
+    const int yc = tv_min(y, dh - 1), yl = yc << s;
+    const int32_t by16 = yl * 16 + ctx.t * (tex ? 36 : 12);
+    VNoiseRow n0, n1, n2, n3;
     if (c == 0) {
       n0.init(by16, 7, ctx.seed);
       n1.init(by16, 5, ctx.seed + 1);
       n2.init(by16, 3, ctx.seed + 2);
+      if (tex) n3.init(by16, 1, ctx.seed + 3);
     } else {
       n0.init(by16, 8, ctx.seed + 10 * c);
     }
     uint32_t word = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int xl = tv_min(x0 + j, dw - 1) << s;
-      const int32_t bx16 = xl * 16 + ctx.t * 36;
+      const int xc = tv_min(x0 + j, dw - 1), xl = xc << s;
+      const int32_t bx16 = xl * 16 + ctx.t * (tex ? 88 : 36);
       int v;
-      if (c == 0)
+      if (c == 0 && tex)
+        v = (n0.eval(bx16) * 3 + n1.eval(bx16) * 2 + n2.eval(bx16) * 2 + n3.eval(bx16)) >> 3;
+      else if (c == 0)
         v = (n0.eval(bx16) * 5 + n1.eval(bx16) * 2 + n2.eval(bx16)) >> 3;
       else
         v = 96 + (n0.eval(bx16) >> 1);
-      word |= (uint32_t)clip_pixel(synth_objects(ctx, c, xl, yl, v)) << (8 * j);
+      v = synth_objects(ctx, c, xl, yl, v);
+      if (tex) {  // per-frame grain, as synth_sample_ctx
+        const uint32_t gr = synth_hash(xc + ctx.t * 7919, yc + c * 104729, ctx.seed ^ 0x5bd1e995u);
+        v += c ? (int)(gr & 3) - 2 : (int)(gr & 7) - 4;
+      }
+      word |= (uint32_t)clip_pixel(v) << (8 * j);
     }
     *reinterpret_cast<uint32_t*>(P + (long)y * pw + x0) = word;
   }
@@ -340,7 +352,10 @@ __global__ void __launch_bounds__(256) k_deblock(FrameSet rec, DecisionSet dec, 
 // ------------------------------------ launchers -----------------------------------------
 void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi, int B, hipStream_t s) {
   dim3 grid((unsigned)tv_min(512, (int)((g.ysz + 1023) / 1024)), 3, B);
-  k_synth<<<grid, 256, 0, s>>>(src, g, seed, fi);
+  if (synth_textured(seed))
+    k_synth<true><<<grid, 256, 0, s>>>(src, g, seed, fi);
+  else
+    k_synth<false><<<grid, 256, 0, s>>>(src, g, seed, fi);
 }
 void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s) {
   dim3 grid((unsigned)tv_min(256, (int)((g.ysz / 4 + 4095) / 4096)), 3, B);
