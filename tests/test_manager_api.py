@@ -272,6 +272,13 @@ def test_job_settings_encoder_overrides(mgr):
     assert c.get(f"/job_settings/{jid}").json["codec"] == "av1"
     assert c.post(f"/job_settings/{jid}", json={"codec": "vp9"}).status_code == 500
     assert _job_params({**st.hgetall(f"job:{jid}"), "source_width": 1920, "source_height": 1080})["codec"] == "av1"
+    # single-pass ABR under a VBV (per-job overrides, validated)
+    assert c.post(f"/job_settings/{jid}", json={"rc_mode": "abr", "bitrate_kbps": 4000, "vbv_maxrate_kbps": 6000,
+                                                "vbv_bufsize_kbit": 8000}).status_code == 200
+    assert c.get(f"/job_settings/{jid}").json["vbv_maxrate_kbps"] in (6000, "6000", 6000.0, "6000.0")
+    assert c.post(f"/job_settings/{jid}", json={"vbv_bufsize_kbit": -1}).status_code == 500
+    p = _job_params({**st.hgetall(f"job:{jid}"), "source_width": 1920, "source_height": 1080})
+    assert p["rc"] == "abr" and p["bitrate_kbps"] == 4000 and p["vbv"] == [6000.0, 8000.0]
 
 
 def test_nodes_detail_fields(mgr):

@@ -1,0 +1,186 @@
+"""Single-pass ABR and the per-segment VBV model (thinvids_amd/models/ratecontrol.py,
+node_job rc_mode="abr").  The reference only runs CQP / CRF (reference
+worker/tasks.py:66-67, :1558-1586); ABR/VBV is this framework's addition to K5g."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from thinvids_amd.models.ratecontrol import (AbrController, frame_sizes, vbv_levels, vbv_ok, vbv_repair_offset,
+                                             vbv_scale)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_vbv_levels_by_hand():
+    # 30 fps, 300 kbit/s -> 10 kbit refill per frame, 40 kbit buffer starting at 36 kbit
+    low, end = vbv_levels([30e3, 5e3, 5e3], 30, 300e3, 40e3, init=0.9)
+    assert low == pytest.approx(6e3)  # 36 - 30
+    # 36-30=6 ->16 ; 16-5=11 -> 21 ; 21-5=16 -> 26
+    assert end == pytest.approx(26e3)
+    assert not vbv_ok([30e3, 5e3, 5e3], 30, 300e3, 40e3)  # ends emptier than it started
+    assert vbv_ok([30e3, 1e3, 1e3, 1e3, 1e3], 30, 300e3, 40e3)  # 36-30+4*9 -> capped at 40 >= 36
+    assert not vbv_ok([37e3], 30, 300e3, 40e3)  # underflow on the first frame
+
+
+def test_vbv_scale_is_the_compliance_boundary():
+    bits = np.array([60e3, 20e3, 18e3, 25e3, 12e3, 30e3])
+    s = vbv_scale(bits, 30, 300e3, 40e3)
+    assert 0 < s < 1
+    assert vbv_ok(bits * s, 30, 300e3, 40e3)
+    assert not vbv_ok(bits * s * 1.01, 30, 300e3, 40e3)
+    assert vbv_scale(bits * 0.1, 30, 300e3, 40e3) == 1.0
+    assert vbv_repair_offset(0.5, 0) == 7 and vbv_repair_offset(0.5, 2) == 9 and vbv_repair_offset(0.999, 0) == 1
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.lists(st.floats(100.0, 30e3), min_size=1, max_size=12), min_size=1, max_size=8),
+       st.floats(0.3, 1.0))
+def test_vbv_per_segment_compliance_implies_stream_compliance(segments, init):
+    """The decomposition the distributed check relies on: if every segment is compliant on
+    its own (start at init x bufsize, never underflow, end at least as full), the
+    concatenated stream never underflows, in any segment order."""
+    fps, rate, buf = 30.0, 300e3, 40e3
+    ok_segs = [s for s in segments if vbv_ok(s, fps, rate, buf, init)]
+    stream = [b for s in ok_segs for b in s]
+    low, _ = vbv_levels(stream, fps, rate, buf, init)
+    assert low >= -1e-6
+
+
+def test_abr_controller_converges_on_a_bits_model():
+    """Batches of varying complexity; bits = c * 2^(-(q - 27) / 7) (a slope the controller's
+    prior does not know).  The running total lands within 3 % of the target and the late
+    batches within 10 % each."""
+    rng = np.random.default_rng(3)
+    ctl = AbrController(27)
+    nominal = 1e6
+    tot_a = tot_t = 0.0
+    errs = []
+    for k in range(24):
+        c = 2.2e6 * float(np.exp(rng.normal(0, 0.15)))  # base QP would overshoot 2.2x
+        q = ctl.plan(nominal, [16, 16])
+        qm = float(np.mean(np.concatenate(q)))
+        actual = c * 2.0 ** (-(qm - 27) / 7.0)
+        ctl.record(actual)
+        tot_a += actual
+        tot_t += nominal
+        errs.append(actual / nominal - 1)
+    assert abs(tot_a / tot_t - 1) < 0.03, tot_a / tot_t
+    assert max(abs(e) for e in errs[-8:]) < 0.35
+    assert len(ctl.log) == 24 and ctl.log[0][2] == 0.0
+
+
+def _job(tmp_path, frames=96, kbps=None, frac=0.6, vbv=None, world=1):
+    from thinvids_amd.models import hevc, media
+
+    fr = [hevc.synth_frame(5, t, 160, 96) for t in range(frames)]
+    src = str(tmp_path / "abr.y4m")
+    media.write_y4m(src, fr, 30, 1)
+    if kbps is None:
+        base, _ = hevc.encode_sequence_cpu(fr, qp=27, gop=4, search_range=64)
+        kbps = len(base) * 8 / (frames / 30) / 1000 * frac
+    return src, kbps
+
+
+def _segment_bits(path, seg_frames):
+    from thinvids_amd.models import hevc
+
+    with open(path, "rb") as f:
+        fs = frame_sizes(hevc.demux_mp4(f.read())["annexb"])
+    return [8.0 * np.asarray(fs[i:i + seg_frames]) for i in range(0, len(fs), seg_frames)]
+
+
+def test_abr_single_pass_job_hits_target_and_streams(tmp_path, monkeypatch):
+    monkeypatch.setenv("TV_FORCE_CPU", "1")
+    from thinvids_amd.parallel.node_job import run_job
+
+    src, kbps = _job(tmp_path)
+    out = str(tmp_path / "o.mp4")
+    res = run_job(src, out, software=True, gop=4, segment_frames=4, bitrate_kbps=kbps, rc_mode="abr",
+                  batch_segments=2)
+    assert res["rc"] == "abr" and res["passes"] == 1
+    got = res["outputs"][0]["kbps"]
+    assert abs(got / kbps - 1) < 0.10, (got, kbps, res["abr_steps_rank0"])
+    assert abs(res["rc_errors"][0][0] - (got / kbps - 1)) < 0.02
+    assert not os.path.exists(out + ".parts")  # streamed stitch, parts cleaned up
+    from thinvids_amd.models import hevc
+
+    with open(out, "rb") as f:
+        assert len(hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False).frames) == 96
+
+
+def test_abr_vbv_repairs_every_segment(tmp_path, monkeypatch):
+    """A tight VBV (peak 1.1x the average rate, a buffer of ~0.3 s): the IDR-led segments
+    that underflow it are re-encoded coarser; every segment of the output is compliant."""
+    monkeypatch.setenv("TV_FORCE_CPU", "1")
+    from thinvids_amd.parallel.node_job import run_job
+
+    src, kbps = _job(tmp_path, frames=64)
+    maxrate, buf = kbps * 1.1, kbps * 0.3
+    out = str(tmp_path / "v.mp4")
+    res = run_job(src, out, software=True, gop=8, segment_frames=8, bitrate_kbps=kbps, rc_mode="abr",
+                  batch_segments=2, vbv_maxrate_kbps=maxrate, vbv_bufsize_kbit=buf)
+    v = res["vbv"]
+    assert v["checked"] == 8 and v["violations"] == 0 and v["repaired"] >= 1, v
+    for seg in _segment_bits(out, 8):
+        assert vbv_ok(seg, 30, maxrate * 1000, buf * 1000)
+
+
+def _abr_worker(rank, world, port, src, out, kbps, res_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), TV_FORCE_CPU="1")
+    import torch.distributed as dist
+
+    from thinvids_amd.parallel.node_job import run_job
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = run_job(src, out, software=True, gop=4, segment_frames=4, bitrate_kbps=kbps, rc_mode="abr",
+                  batch_segments=2)
+    if rank == 0:
+        with open(res_path, "w") as f:
+            json.dump(res, f)
+    dist.destroy_process_group()
+
+
+def test_abr_on_two_ranks(tmp_path):
+    """Rank-local controllers, no per-batch collective: the node total still lands near the
+    target, and the all-reduced achieved rate is what rank 0 reports."""
+    src, kbps = _job(tmp_path, frac=1.6)
+    res_path = str(tmp_path / "res.json")
+    mp.spawn(_abr_worker, args=(2, _free_port(), src, str(tmp_path / "o.mp4"), kbps, res_path), nprocs=2, join=True)
+    res = json.load(open(res_path))
+    got = res["outputs"][0]["kbps"]
+    assert res["world"] == 2 and abs(got / kbps - 1) < 0.12, (got, kbps)
+    assert abs(res["rc_errors"][0][0] - (got / kbps - 1)) < 0.02
+
+
+@pytest.mark.gpu
+def test_abr_vbv_gpu_engine(tmp_path, monkeypatch):
+    """Single-pass ABR + VBV on the HIP engine (per-frame QP maps on the device, VBV
+    re-encodes batched on the engine): on target within 10 %, every segment compliant."""
+    monkeypatch.delenv("TV_FORCE_CPU", raising=False)
+    from thinvids_amd.models import hevc, media
+    from thinvids_amd.parallel.node_job import run_job
+
+    fr = [hevc.synth_frame(12, t, 256, 160) for t in range(128)]
+    src = str(tmp_path / "g.y4m")
+    media.write_y4m(src, fr, 30, 1)
+    r1 = run_job(src, str(tmp_path / "a.mp4"), gop=16, segment_frames=16)
+    kbps = r1["outputs"][0]["kbps"] * 0.6
+    maxrate, buf = kbps * 1.2, kbps * 0.5
+    out = str(tmp_path / "b.mp4")
+    r2 = run_job(src, out, gop=16, segment_frames=16, bitrate_kbps=kbps, rc_mode="abr", batch_segments=2,
+                 vbv_maxrate_kbps=maxrate, vbv_bufsize_kbit=buf)
+    assert r2["passes"] == 1 and abs(r2["outputs"][0]["kbps"] / kbps - 1) < 0.10, (r2["outputs"], kbps)
+    assert r2["vbv"]["violations"] == 0, r2["vbv"]
+    for seg in _segment_bits(out, 16):
+        assert vbv_ok(seg, 30, maxrate * 1000, buf * 1000)

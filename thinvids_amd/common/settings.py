@@ -42,7 +42,9 @@ DEFAULT_SETTINGS: dict[str, str] = {
     "tv_deblock": "1",
     "tv_sao": "1",
     "tv_segment_frames": "0",  # 0 = derive from target_segment_mb
-    "tv_bitrate_kbps": "0",  # tv_rc=2pass target
+    "tv_bitrate_kbps": "0",  # tv_rc=2pass / abr target
+    "tv_vbv_maxrate_kbps": "0",  # tv_rc=abr: VBV peak rate (0: no VBV)
+    "tv_vbv_bufsize_kbit": "0",  # tv_rc=abr: VBV decoder buffer
     "tv_crf": "27",  # tv_rc=crf quality level
     "tv_scenecut": "1",  # IDR (closed-GOP restart) at detected scene cuts
     "tv_ladder": "",  # e.g. "2160,1440,1080,720,480": one MP4 per rung (ABR fan-out)

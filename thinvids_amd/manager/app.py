@@ -342,11 +342,12 @@ def encoder_overrides(d: dict) -> dict:
                 raise ValueError(f"{k} out of range")
             else:
                 out[k] = int(v)
-    if "bitrate_kbps" in d:
-        v = d["bitrate_kbps"]
-        out["bitrate_kbps"] = "" if v in ("", None) else float(v)
-        if out["bitrate_kbps"] != "" and out["bitrate_kbps"] <= 0:
-            raise ValueError("bitrate_kbps must be positive")
+    for k in ("bitrate_kbps", "vbv_maxrate_kbps", "vbv_bufsize_kbit"):  # VBV: rc_mode abr only
+        if k in d:
+            v = d[k]
+            out[k] = "" if v in ("", None) else float(v)
+            if out[k] != "" and out[k] <= 0:
+                raise ValueError(f"{k} must be positive")
     if "ladder" in d:
         rungs = [int(x) for x in str(d["ladder"] or "").replace(" ", "").split(",") if x]
         if any(not 64 <= r <= 4320 for r in rungs):
@@ -894,6 +895,8 @@ def create_app(store=None, housekeeping: bool = False) -> Flask:
                             # encoder knobs of this framework (per-job overrides of tv_*)
                             "rc_mode": job.get("rc_mode", ""), "qp": job.get("qp", ""), "crf": job.get("crf", ""),
                             "bitrate_kbps": job.get("bitrate_kbps", ""), "ladder": job.get("ladder", ""),
+                            "vbv_maxrate_kbps": job.get("vbv_maxrate_kbps", ""),
+                            "vbv_bufsize_kbit": job.get("vbv_bufsize_kbit", ""),
                             "node_executor": job.get("node_executor", ""), "codec": job.get("codec", ""),
                             "source_fps": job.get("source_fps", "")})
         if core.job_status(job) == Status.RUNNING:

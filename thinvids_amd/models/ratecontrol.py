@@ -12,7 +12,18 @@ worker/tasks.py:66-67, :1573-1586) or libx264 CRF 23 (:1558-1571).  Here:
   bits; the per-frame statistics of all ranks are all-reduced (RCCL), a global allocation
   (bits^qcomp complexity compression) becomes a per-frame QP plan, and pass 2 encodes it
   with rank-local rate feedback between batches (each completed batch corrects the QP
-  offset of the segments a rank still has to encode).
+  offset of the segments a rank still has to encode);
+* ``abr``   — single pass at a target bitrate (no pass 1, so it streams the stitch): every
+  rank plans each claimed batch at one uniform QP offset from its own finished batches
+  (AbrController, the offset regression of BatchRateController), optionally under a VBV:
+  the decoder-buffer model is checked per segment and a violating segment is re-encoded
+  coarser (vbv_scale / vbv_repair_offset).
+
+VBV decomposition.  Segments are closed GOPs encoded on different ranks in any order, so a
+global leaky-bucket simulation would serialise the node.  Instead every segment must, starting
+from the buffer at ``init`` x bufsize, never underflow and end at least that full again; then
+any concatenation of segments is compliant (each one hands the next a buffer at least as full
+as the one it assumed), and the check is local to the rank that encoded the segment.
 
 The bits(QP) model is bits = b1 * 2^(-(QP - QP1) / SLOPE) with SLOPE QP steps per halving
 (measured on this encoder: 5.9 - 7.5 between QP 17 and 42).
@@ -214,3 +225,99 @@ class RateFeedback:
     def record(self, actual_bits: float, planned_bits: float) -> None:
         self.actual += actual_bits
         self.planned += planned_bits
+
+
+def vbv_levels(bits, fps: float, maxrate_bps: float, bufsize_bits: float, init: float = 0.9) -> tuple[float, float]:
+    """Decoder-buffer (leaky bucket) levels of one segment: the buffer starts at init x
+    bufsize, frame f's bits leave it at its removal time, and it refills at maxrate per frame
+    interval up to bufsize.  Returns (lowest level right after a removal, level at the end of
+    the segment's last interval); the segment is compliant iff the first is >= 0 and the
+    second >= the starting level (see the module docstring)."""
+    fill = maxrate_bps / fps
+    level = init * bufsize_bits
+    low = level
+    for b in bits:
+        level -= float(b)
+        low = min(low, level)
+        level = min(bufsize_bits, level + fill)
+    return low, level
+
+
+def vbv_ok(bits, fps: float, maxrate_bps: float, bufsize_bits: float, init: float = 0.9) -> bool:
+    low, end = vbv_levels(bits, fps, maxrate_bps, bufsize_bits, init)
+    return low >= 0.0 and end >= init * bufsize_bits - 1e-6
+
+
+def vbv_scale(bits, fps: float, maxrate_bps: float, bufsize_bits: float, init: float = 0.9) -> float:
+    """Largest uniform factor s <= 1 such that s x bits is compliant (bisection; the levels
+    fall monotonically in s)."""
+    b = np.asarray(bits, np.float64)
+    if vbv_ok(b, fps, maxrate_bps, bufsize_bits, init):
+        return 1.0
+    lo, hi = 0.0, 1.0
+    for _ in range(40):
+        mid = (lo + hi) / 2
+        if vbv_ok(b * mid, fps, maxrate_bps, bufsize_bits, init):
+            lo = mid
+        else:
+            hi = mid
+    return lo
+
+
+def vbv_repair_offset(scale: float, attempt: int, slope: float = SLOPE) -> int:
+    """QP increase for a re-encode that must shrink a segment by `scale`: the model's
+    -slope*log2(scale), plus one step per previous failed attempt (the I frame at the head of
+    the segment responds less than the model)."""
+    return max(1, int(math.ceil(-slope * math.log2(max(scale, 1e-6)))) + attempt)
+
+
+class AbrController:
+    """Single-pass average-bitrate control of one rank's batches on one rung.  A batch of
+    segments is encoded at base QP + u.  The finished batches' misses r = log2(actual /
+    nominal) are regressed on their offsets (r = a + b u over the last `window` batches; slope
+    b measured once two operating points differ, else the SLOPE prior, clipped to 3.5..16 QP
+    per halving) and the next u puts the line at log2(want / nominal), where want repays 25 %
+    of the accumulated miss (at most 10 % of the batch).  Rank-local: every rank meets the
+    target on its own segments, so the node meets it with no collective per batch."""
+
+    def __init__(self, base_qp: float, qp_min: int = 10, qp_max: int = 51, max_offset: float = 16.0,
+                 window: int = 4, repay: float = 0.25, max_repay: float = 0.10):
+        self.base = float(base_qp)
+        self.qp_min, self.qp_max, self.max_offset = qp_min, qp_max, max_offset
+        self.window, self.repay, self.max_repay = window, repay, max_repay
+        self.target = self.actual = 0.0
+        self.pts: list = []  # (u, log2(actual / nominal)) per finished batch
+        self.log: list = []  # per finished batch: actual / nominal, want / nominal, u
+        self.pending: tuple | None = None
+
+    def offset(self, want_ratio: float = 1.0) -> float:
+        pts = self.pts[-self.window:]
+        if not pts:
+            return 0.0
+        u = np.array([p[0] for p in pts])
+        r = np.array([p[1] for p in pts])
+        b = -1.0 / SLOPE
+        if np.ptp(u) > 0.25:
+            b = float(np.clip(np.polyfit(u, r, 1)[0], -1.0 / 3.5, -1.0 / 16.0))
+        u_next = u.mean() + (math.log2(max(want_ratio, 1e-6)) - r.mean()) / b
+        return float(np.clip(u_next, -self.max_offset, self.max_offset))
+
+    def plan(self, nominal_bits: float, frames: list) -> list:
+        """Per-segment integer QP arrays (lengths `frames`) for a batch worth nominal_bits;
+        the fractional QP is error-diffused along each segment."""
+        lim = self.max_repay * nominal_bits
+        want = nominal_bits + float(np.clip(self.repay * (self.target - self.actual), -lim, lim))
+        u = self.offset(want / max(nominal_bits, 1.0))
+        q = float(np.clip(self.base + u, self.qp_min, self.qp_max))
+        self.pending = (nominal_bits, want, q - self.base)
+        return [round_qps(np.full(n, q), 0.0, self.qp_min, self.qp_max) for n in frames]
+
+    def record(self, actual_bits: float) -> None:
+        if self.pending is None:
+            return
+        nominal, want, u = self.pending
+        self.pending = None
+        self.target += nominal
+        self.actual += actual_bits
+        self.pts.append((u, math.log2(max(actual_bits, 1.0) / max(nominal, 1.0))))
+        self.log.append([round(actual_bits / nominal, 4), round(want / nominal, 4), round(u, 3)])

@@ -38,7 +38,8 @@ import time
 
 import numpy as np
 
-from ..models.ratecontrol import SLOPE, RateFeedback, frame_sizes, plan_frame_qps, predict_bits, round_qps
+from ..models.ratecontrol import (SLOPE, AbrController, RateFeedback, frame_sizes, plan_frame_qps, predict_bits,
+                                  round_qps, vbv_ok, vbv_repair_offset, vbv_scale)
 from ..utils import fault, trace
 
 RC_TOLERANCE = 0.04  # a pass within +-4 % of the target bitrate is final (the contract is +-5 %)
@@ -398,7 +399,12 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             search_range: int = 64, software: bool = False, batch_segments: int = 8,
             resume_dir: str | None = None, max_retries: int = 3, hooks: JobHooks | None = None,
             deblock: bool = True, sao: bool = False, cache=None, crf: int = 0, scenecut: bool = False,
-            audio_stream: int = 0, codec: str = "hevc", qindex: int = 0) -> dict:
+            audio_stream: int = 0, codec: str = "hevc", qindex: int = 0, rc_mode: str = "",
+            vbv_maxrate_kbps: float = 0.0, vbv_bufsize_kbit: float = 0.0) -> dict:
+    """One job over the node's ranks (SPMD).  Rate control: ``bitrate_kbps`` > 0 selects
+    frame-level 2-pass, or single-pass ABR when ``rc_mode == "abr"`` (optionally under a VBV:
+    ``vbv_maxrate_kbps`` / ``vbv_bufsize_kbit``, checked and repaired per segment, see
+    models/ratecontrol.py); else ``crf`` > 0 in-engine CRF; else constant ``qp``."""
     import torch
 
     from ..models import hevc, media
@@ -423,6 +429,10 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     segs = plan_segments(nfr, segment_frames, gop)
     software = software or not gpu_available()
     synthetic = isinstance(src, media.SynthSource)
+    fps = src.fps_num / src.fps_den
+    abr = rc_mode == "abr" and bitrate_kbps > 0
+    vbv = abr and vbv_maxrate_kbps > 0 and vbv_bufsize_kbit > 0
+    rc_name = "abr" if abr else ("2pass" if bitrate_kbps > 0 else ("crf" if crf else "cqp"))
     if getattr(src, "bits", 8) != 8 and mode == "scatter":
         mode = "direct"  # 10-bit sources: every rank reads its own range
     # one engine per rung stays resident (a 5-rung ladder thrashed the default 4-engine cache:
@@ -437,12 +447,13 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         src=os.path.abspath(input_path), size=st.st_size if st else 0, mtime=st.st_mtime_ns if st else 0,
         rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software,
         deblock=deblock, sao=sao, scenecut=scenecut, codec=codec, qindex=qindex, crf=crf,
-        rc="2pass" if bitrate_kbps > 0 else ("crf" if crf else "cqp"), bitstream_version=BITSTREAM_VERSION))
+        rc=rc_name, bitstream_version=BITSTREAM_VERSION,
+        **({"kbps": bitrate_kbps, "vbv": [vbv_maxrate_kbps, vbv_bufsize_kbit] if vbv else None} if abr else {})))
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
     quality: dict = {}  # (r, i) -> PartStats of segments encoded here
     # streaming stitch (single pass, plain MP4 output): decided identically on every rank
     side = _side_plan(input_path, audio_stream)
-    streaming = (bitrate_kbps <= 0 and os.environ.get("TV_STREAM_STITCH", "1") != "0"
+    streaming = ((bitrate_kbps <= 0 or abr) and os.environ.get("TV_STREAM_STITCH", "1") != "0"
                  and (side is None or (not side.tracks and side.ext == ".mp4")))
     out_paths = [output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4" for _, oh in rungs]
     if side is not None:
@@ -469,9 +480,15 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                           crf=0 if bitrate_kbps > 0 else crf, scenecut=scenecut, codec=codec, qindex=qindex)
 
     rc = {"plan": None, "fb": RateFeedback(), "bits": {}}  # pass-2 plan, feedback, per-frame bits
+    rung_scale = [(rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]  # per-rung budget ~ pixels
+    if abr:  # one rank-local controller per rung; this batch's plans
+        rc.update(abr=[AbrController(qp) for _ in rungs], abr_q={})
+    vstat = {"checked": 0, "repaired": 0, "reencodes": 0, "violations": 0}
 
     def seg_qps(r, i, offset):
         """(integer per-frame QPs or None, checkpoint key) of segment i on rung r."""
+        if abr:  # an ABR segment on disk is reused whatever plan produced it (same target)
+            return rc["abr_q"][(r, i)], "abr"
         if rc["plan"] is None:
             return None, qp
         q = round_qps(rc["plan"][r][i], offset)
@@ -498,6 +515,12 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         every segment is offset by this rank's rate feedback so far."""
         out, todo, keep, plans = {}, [], [], {}
         offset = rc["fb"].offset()
+        if abr:
+            frames = [segs[i][1] for i in seg_ids]
+            for r, ctl in enumerate(rc["abr"]):
+                nominal = bitrate_kbps * 1000 * sum(frames) / fps * rung_scale[r]
+                for i, q in zip(seg_ids, ctl.plan(nominal, frames)):
+                    rc["abr_q"][(r, i)] = q
         for i in seg_ids:
             need = []
             for r in range(len(rungs)):
@@ -517,6 +540,9 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         if todo:
             with trace.span("node_job.encode", segments=len(todo)):
                 got, qual = _encode_many(todo, cache)
+            if vbv:
+                with trace.span("node_job.vbv", segments=len(todo)):
+                    vbv_repair(todo, got, qual, plans)
             for (r, i), b in got.items():
                 io_futs.append(io_pool.submit(ckpt.save, r, i, plans[(r, i)][1], b))
                 out[(r, i)] = b
@@ -527,8 +553,11 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             fb = frame_sizes(b)
             rc["bits"][(r, i)] = fb
             q = plans[(r, i)][0]
-            if q is not None:  # rate feedback: actual vs the model's prediction at these QPs
+            if q is not None and not abr:  # rate feedback: actual vs the model's prediction at these QPs
                 rc["fb"].record(8.0 * sum(fb), float(predict_bits(rc["b1"][(r, i)], qp, q).sum()))
+        if abr:
+            for r, ctl in enumerate(rc["abr"]):
+                ctl.record(sum(8.0 * sum(rc["bits"][(r, i)]) for i in seg_ids))
         if streaming:  # the stitch rank takes them now; this rank keeps no bitstream
             for (r, i), b in out.items():
                 if stitcher is not None:
@@ -540,6 +569,44 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             for i in seg_ids:
                 hooks.segment_done(segs[i][1])
         return out
+
+    def vbv_repair(todo, got, qual, plans):
+        """Per-segment VBV (see models/ratecontrol.py): a segment that underflows the decoder
+        buffer or ends emptier than it started is re-encoded at a coarser QP (the model's
+        offset for its compliant scale, +1 per failed attempt), batched with the other
+        violators of this claim; after 3 attempts it is kept and counted as a violation."""
+        maxrate, buf = vbv_maxrate_kbps * 1000 * 1.0, vbv_bufsize_kbit * 1000.0
+        items = {k: (part, sp) for k, part, sp, _ in todo}
+        bad = {}
+        for k, b in got.items():
+            vstat["checked"] += 1
+            fb = 8.0 * np.asarray(frame_sizes(b), np.float64)
+            if not vbv_ok(fb, fps * 1.0, maxrate * rung_scale[k[0]], buf * rung_scale[k[0]]):
+                bad[k] = fb
+        fixed = set()
+        for attempt in range(3):
+            if not bad:
+                break
+            redo = []
+            for k, fb in bad.items():
+                sc = vbv_scale(fb, fps, maxrate * rung_scale[k[0]], buf * rung_scale[k[0]])
+                q0 = plans[k][0] if plans[k][0] is not None else np.full(len(fb), qp)
+                q = np.clip(np.asarray(q0) + vbv_repair_offset(sc, attempt), 0, 51)
+                plans[k] = (q, plans[k][1])
+                rc["abr_q"][k] = q  # the reported plan is the one encoded
+                redo.append((k, items[k][0], items[k][1], q))
+            vstat["reencodes"] += len(redo)
+            g2, q2 = _encode_many(redo, cache)
+            bad = {}
+            for k, b in g2.items():
+                got[k], qual[k] = b, q2[k]
+                fb = 8.0 * np.asarray(frame_sizes(b), np.float64)
+                if vbv_ok(fb, fps, maxrate * rung_scale[k[0]], buf * rung_scale[k[0]]):
+                    fixed.add(k)
+                else:
+                    bad[k] = fb
+        vstat["repaired"] += len(fixed)
+        vstat["violations"] += len(bad)
 
     def encode_pass() -> dict:
         mine = {}
@@ -656,7 +723,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         agreed_pass.n = 0
         passes = 1
         rc_errors: list = []  # per pass after pass 1: achieved / target - 1, per rung
-        if bitrate_kbps > 0:
+        if bitrate_kbps > 0 and not abr:
             # pass 1 at the base QP -> every frame's bits, all-reduced over the node (RCCL) ->
             # one global per-frame QP plan -> pass 2 with rank-local rate feedback
             agreed_pass()
@@ -665,13 +732,11 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             for (r, i), fb in rc["bits"].items():
                 flat[r * nfr + starts[i]:r * nfr + starts[i] + len(fb)] = 8.0 * np.asarray(fb, np.float64)
             flat = allreduce_stats(flat, cdev)  # RC statistics all-reduce
-            fps = src.fps_num / src.fps_den
             rc["b1"] = {(r, i): flat[r * nfr + starts[i]:r * nfr + starts[i] + n] for r in range(len(rungs))
                         for i, (_, n) in enumerate(segs)}
             plan = []
             for r in range(len(rungs)):
-                scale = (rungs[r][0] * rungs[r][1]) / (rungs[0][0] * rungs[0][1])  # per-rung budget ~ pixels
-                target = bitrate_kbps * 1000 * nfr / fps * scale
+                target = bitrate_kbps * 1000 * nfr / fps * rung_scale[r]
                 per_seg, _ = plan_frame_qps([rc["b1"][(r, i)] for i in range(len(segs))], qp, target,
                                             key_offset=-2.0 if codec == "av1" else None)
                 plan.append(per_seg)
@@ -702,6 +767,16 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                         rc["b1"][(r, i)] = predict_bits(rc["b1"][(r, i)], 0, -d)
         else:
             mine = agreed_pass()
+            if abr:  # one pass: the achieved rate per rung over the node, and the VBV record
+                got = np.zeros(len(rungs))
+                for (r, i), fb in rc["bits"].items():
+                    if (r, i) in mine:
+                        got[r] += 8.0 * sum(fb)
+                vv = allreduce_stats(np.concatenate([got, [vstat[k] for k in sorted(vstat)]]), cdev)
+                targets = [bitrate_kbps * 1000 * nfr / fps * sc for sc in rung_scale]
+                rc_errors.append([round(float(e), 4) for e in vv[:len(rungs)] / np.asarray(targets) - 1.0])
+                for j, k in enumerate(sorted(vstat)):
+                    vstat[k] = int(vv[len(rungs) + j])
         t_enc = time.time() - t0
         # quality: per-rung frames + SSE of the segments encoded on this rank, all-reduced
         qv = np.zeros((len(rungs), 4))
@@ -715,7 +790,11 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         with trace.span("node_job.gather"):
             parts = gather_bytes_to_root(blob, cdev) if world > 1 else [blob]
         result = {"world": world, "segments": len(segs), "rungs": [list(x) for x in rungs], "passes": passes,
-                  "rc_errors": rc_errors}
+                  "rc": rc_name, "rc_errors": rc_errors}
+        if abr:
+            result["abr_steps_rank0"] = [c.log for c in rc["abr"]]  # [actual, want, offset] / nominal
+        if vbv:
+            result["vbv"] = dict(vstat, maxrate_kbps=vbv_maxrate_kbps, bufsize_kbit=vbv_bufsize_kbit)
         if rank == 0:
             streams: dict = {}
             per_rank = []
@@ -756,6 +835,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             el = time.time() - t0
             result.update(side_fields=side.fields if side else {}, side_warnings=side.warnings if side else [])
             result.update(trace=trace.since(trace0), per_rank=per_rank, outputs=outs, qp_plan=[[round(float(np.mean(q)), 2) for q in row] for row in rc["plan"]] if rc["plan"] else
+                          [[round(float(np.mean(rc["abr_q"][(r, i)])), 2) if (r, i) in rc["abr_q"] else None
+                            for i in range(len(segs))] for r in range(len(rungs))] if abr else
                           [[qp] * len(segs) for _ in rungs], rc_offset=round(rc["fb"].offset(), 3),
                           seconds=round(el, 3), encode_seconds=round(t_enc, 3),
                           fps=round(nfr * len(rungs) / el, 2), encode_fps=round(nfr * len(rungs) * passes / max(t_enc, 1e-9), 2))

@@ -129,11 +129,13 @@ def _job_params(job: dict) -> dict:
     rc = str(job.get("rc_mode") or s.get("tv_rc") or "cqp").lower()
     kbps = as_float(job.get("bitrate_kbps") or s.get("tv_bitrate_kbps"), 0.0) if rc in ("2pass", "abr") else 0.0
     crf = as_int(job.get("crf") or s.get("tv_crf"), 27) if rc == "crf" else 0
+    vbv = ([as_float(job.get("vbv_maxrate_kbps") or s.get("tv_vbv_maxrate_kbps"), 0.0),
+            as_float(job.get("vbv_bufsize_kbit") or s.get("tv_vbv_bufsize_kbit"), 0.0)] if rc == "abr" else [0.0, 0.0])
     return {"height": th, "qp": spec.qp, "gop": spec.gop, "search_range": spec.search_range, "deblock": spec.deblock,
             "sao": spec.sao, "software": spec.software, "ladder": ladder or None, "bitrate_kbps": kbps,
             "segment_frames": max(spec.gop, as_int(s.get("tv_node_segment_frames"), 256)),
             "mode": str(s.get("tv_node_mode") or "direct"), "batch_segments": as_int(s.get("tv_node_batch"), 8),
-            "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc,
+            "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc, "vbv": vbv,
             "scenecut": spec.scenecut, "codec": spec.codec, "qindex": spec.qindex}
 
 
@@ -204,7 +206,8 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                       batch_segments=p["batch_segments"], hooks=hooks, deblock=p["deblock"], sao=p["sao"],
                       cache=None if p["software"] else cache, crf=p["crf"], resume_dir=spec["ckpt"],
                       scenecut=p.get("scenecut", False), codec=p.get("codec", "hevc"), qindex=p.get("qindex", 0),
-                      audio_stream=int(spec["job"].get("selected_a_stream") or 0))
+                      audio_stream=int(spec["job"].get("selected_a_stream") or 0), rc_mode=p.get("rc", ""),
+                      vbv_maxrate_kbps=p.get("vbv", [0, 0])[0], vbv_bufsize_kbit=p.get("vbv", [0, 0])[1])
     except Exception as e:
         if is_comm_failure(e):  # the job is fine, the communicator is not: requeue + re-init
             log.error("[%s] communicator failure on rank %d: %s", job_id, rank, e)
