@@ -67,6 +67,45 @@ void* tv_cpu_encoder_new(int width, int height, int qp, int deblock, int range, 
   guard([&] { e = new CpuEncoder(cfg, range); });
   return e;
 }
+// hierarchical-B golden encoder (mgop > 1): frames go in the plan's coding order
+void* tv_cpu_encoder_new_b(int width, int height, int qp, int deblock, int range, int max_merge, int mgop) {
+  SeqConfig cfg;
+  cfg.width = width;
+  cfg.height = height;
+  cfg.qp = qp;
+  cfg.deblock = (deblock & 1) != 0;
+  cfg.sao = (deblock & 2) != 0;
+  cfg.wpp = (deblock & 4) != 0;
+  cfg.max_merge_cand = max_merge;
+  cfg.mgop = mgop;
+  cfg.finalize();
+  CpuEncoder* e = nullptr;
+  guard([&] { e = new CpuEncoder(cfg, range); });
+  return e;
+}
+// plan the next segment; disp (capacity nframes) receives the coding order's display indices
+int tv_cpu_encoder_begin_gop(void* e, int nframes, int* disp) {
+  return guard([&] {
+    auto* enc = static_cast<CpuEncoder*>(e);
+    enc->begin_gop(nframes);
+    for (size_t k = 0; k < enc->plan().pics.size(); ++k) disp[k] = enc->plan().pics[k].disp;
+  });
+}
+// GOP plan of nframes with mini-GOP mgop: per coded picture (coding order) display index,
+// slice type, list-0 / list-1 reference, temporal layer; info = {dpb_size, num_reorder}
+int tv_gop_plan(int nframes, int mgop, int* disp, int* type, int* ref0, int* ref1, int* layer, int* info) {
+  const GopPlan g = plan_gop(nframes, mgop);
+  for (size_t k = 0; k < g.pics.size(); ++k) {
+    disp[k] = g.pics[k].disp;
+    type[k] = g.pics[k].type;
+    ref0[k] = g.pics[k].ref[0];
+    ref1[k] = g.pics[k].ref[1];
+    layer[k] = g.pics[k].layer;
+  }
+  info[0] = g.dpb_size;
+  info[1] = g.num_reorder;
+  return (int)g.pics.size();
+}
 void* tv_cpu_encoder_new_crf(int width, int height, int qp, int deblock, int range, int max_merge, int crf) {
   SeqConfig cfg;
   cfg.width = width;

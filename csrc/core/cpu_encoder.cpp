@@ -185,13 +185,30 @@ void coarse_search(const uint8_t* qcur, const uint8_t* qprev, int W, int H, int 
     }
 }
 
-void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, const int16_t* cmv,
-                   const int16_t* prev_mv, int range, FrameDecisions& fd) {
+namespace {
+// block geometry of the 21 ME blocks: 16 x 8x8 (raster), 4 x 16x16, 1 x 32x32
+void me_blk(int bi, int& bx, int& by, int& n) {
+  if (bi < 16) {
+    bx = (bi & 3) * 8, by = (bi >> 2) * 8, n = 8;
+  } else if (bi < 20) {
+    bx = ((bi - 16) & 1) * 16, by = ((bi - 16) >> 1) * 16, n = 16;
+  } else {
+    bx = by = 0, n = 32;
+  }
+}
+int me_blk8_of(int q, int r) { return (((q >> 1) * 2 + (r >> 1)) << 2) + (q & 1) * 2 + (r & 1); }
+
+// Motion search of one CTB against one reference: the 21 blocks' best cost (SAD + MV rate),
+// vector and rate part (the GPU's k_inter_me computes exactly this).
+struct CtbMe {
+  int cost[21], mv[21][2], pen[21];
+};
+void me_ctb(const SeqConfig& cfg, const Picture& src, const Picture& ref, const int16_t* cmv, const int16_t* prev_mv,
+            int range, int cxi, int cyi, int w8, CtbMe& out) {
   const double lam = lambda_sad(cfg.qp);
   const int W = cfg.coded_w, H = cfg.coded_h, wc = W / kCtb, hc = H / kCtb;
   int penmv[64];
   for (int i = 0; i < 64; ++i) penmv[i] = (int)(lam * i);
-  const int pen_split = (int)(lam * 4);
   const uint8_t* S = src.y.data();
   const uint8_t* R = ref.y.data();
   auto sad8 = [&](int x, int y, int dx, int dy) {  // one 8x8 block, integer displacement
@@ -211,98 +228,160 @@ void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref,
         s += tv_abs(S[(size_t)(y + j) * W + x + i] - mc_luma_sample(R, W, W, H, bx + i, by + j, fx, fy));
     return s;
   };
-  // block geometry of the 21 ME blocks: 16 x 8x8 (raster), 4 x 16x16, 1 x 32x32
-  auto blk = [](int bi, int& bx, int& by, int& n) {
-    if (bi < 16) {
-      bx = (bi & 3) * 8, by = (bi >> 2) * 8, n = 8;
-    } else if (bi < 20) {
-      bx = ((bi - 16) & 1) * 16, by = ((bi - 16) >> 1) * 16, n = 16;
-    } else {
-      bx = by = 0, n = 32;
-    }
-  };
-  auto blk8_of = [](int q, int r) { return (((q >> 1) * 2 + (r >> 1)) << 2) + (q & 1) * 2 + (r & 1); };
   const int lim = range - 4;
+  const int cx = cxi * kCtb, cy = cyi * kCtb;
+  const int u0 = (cy >> 3) * w8 + (cx >> 3);
+  int cand[kMeMaxCand][2], pmv[2];
+  const int nc = me_candidates(cmv, wc, hc, cxi, cyi, prev_mv[2 * u0], prev_mv[2 * u0 + 1], lim, cand, pmv);
+  // integer refinement: the 21 block costs at every window position (8x8 SADs reused)
+  unsigned best[21];
+  for (int k = 0; k < 21; ++k) best[k] = 0xffffffffu;
+  for (int pos = 0; pos < nc * kMePosPerCand; ++pos) {
+    int mx, my;
+    me_pos_to_mv(pos, cand, mx, my);
+    const unsigned pen = (unsigned)penmv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])];
+    int s8[16], s16[4] = {0, 0, 0, 0}, s32 = 0;
+    for (int k = 0; k < 16; ++k) {
+      s8[k] = sad8(cx + (k & 3) * 8, cy + (k >> 2) * 8, mx, my);
+      s16[((k >> 3) << 1) | ((k >> 1) & 1)] += s8[k];
+      s32 += s8[k];
+    }
+    auto upd = [&](int bi, int sad) {
+      const unsigned v = ((unsigned)sad + pen) << 11 | (unsigned)pos;
+      best[bi] = v < best[bi] ? v : best[bi];
+    };
+    for (int k = 0; k < 16; ++k) upd(k, s8[k]);
+    for (int q = 0; q < 4; ++q) upd(16 + q, s16[q]);
+    upd(20, s32);
+  }
+  for (int bi = 0; bi < 21; ++bi) {
+    int mx, my;
+    me_pos_to_mv((int)(best[bi] & 2047), cand, mx, my);
+    int* bmv = out.mv[bi];
+    bmv[0] = 4 * mx;
+    bmv[1] = 4 * my;
+    out.cost[bi] = (int)(best[bi] >> 11);
+    int bx, by, n;
+    me_blk(bi, bx, by, n);
+    // half then quarter pel refinement (centre wins ties, then the lowest neighbour)
+    for (int step = 2; step >= 1; step >>= 1) {
+      const int c0x = bmv[0], c0y = bmv[1];
+      for (int k = 0; k < 8; ++k) {
+        int ox, oy;
+        me_cand_offset(k, ox, oy);
+        const int qx = c0x + ox * step, qy = c0y + oy * step;
+        const int c = sad_qpel(cx + bx, cy + by, n, qx, qy) + penmv[me_pen_index(qx - pmv[0], qy - pmv[1])];
+        if (c < out.cost[bi]) {
+          out.cost[bi] = c;
+          bmv[0] = qx;
+          bmv[1] = qy;
+        }
+      }
+    }
+    out.pen[bi] = penmv[me_pen_index(bmv[0] - pmv[0], bmv[1] - pmv[1])];
+  }
+}
+
+// Bottom-up CU split of one CTB from per-block costs; writes cu_log2 and the block's index
+// into `sel` per 8x8 unit (the caller copies that block's motion).
+void split_ctb(const int* bcost, int pen_split, int sel[16], uint8_t l2[16]) {
+  int sum16 = 0;
+  for (int q = 0; q < 4; ++q) {
+    int sum8 = 0;
+    for (int r = 0; r < 4; ++r) sum8 += bcost[me_blk8_of(q, r)] + pen_split;
+    const bool split = sum8 < bcost[16 + q] + pen_split;
+    sum16 += split ? sum8 : bcost[16 + q] + pen_split;
+    for (int r = 0; r < 4; ++r) {
+      const int ux = (q & 1) * 2 + (r & 1), uy = (q >> 1) * 2 + (r >> 1);
+      sel[uy * 4 + ux] = split ? me_blk8_of(q, r) : 16 + q;
+      l2[uy * 4 + ux] = split ? 3 : 4;
+    }
+  }
+  if (bcost[20] + pen_split <= sum16)
+    for (int k = 0; k < 16; ++k) {
+      sel[k] = 20;
+      l2[k] = 5;
+    }
+}
+}  // namespace
+
+void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, const int16_t* cmv,
+                   const int16_t* prev_mv, int range, FrameDecisions& fd) {
+  const int pen_split = (int)(lambda_sad(cfg.qp) * 4);
+  const int wc = cfg.coded_w / kCtb, hc = cfg.coded_h / kCtb;
+  for (int cyi = 0; cyi < hc; ++cyi)
+    for (int cxi = 0; cxi < wc; ++cxi) {
+      CtbMe me;
+      me_ctb(cfg, src, ref, cmv, prev_mv, range, cxi, cyi, fd.w8, me);
+      int sel[16];
+      uint8_t l2[16];
+      split_ctb(me.cost, pen_split, sel, l2);
+      const int u0 = (cyi * kCtb >> 3) * fd.w8 + (cxi * kCtb >> 3);
+      for (int k = 0; k < 16; ++k) {
+        const int u = u0 + (k >> 2) * fd.w8 + (k & 3);
+        fd.cu_log2[u] = l2[k];
+        fd.mv[2 * u] = (int16_t)me.mv[sel[k]][0];
+        fd.mv[2 * u + 1] = (int16_t)me.mv[sel[k]][1];
+        fd.intra[u] = 0;
+        fd.ipm[u] = 1;
+      }
+    }
+}
+
+int bipred_sad(const Picture& src, const Picture& ref0, const Picture& ref1, int x, int y, int n, const int* mv0,
+               const int* mv1) {
+  const int W = src.w, H = src.h;
+  int s = 0;
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) {
+      const int p0 = mc_luma_sample(ref0.y.data(), W, W, H, x + i + (mv0[0] >> 2), y + j + (mv0[1] >> 2), mv0[0] & 3, mv0[1] & 3);
+      const int p1 = mc_luma_sample(ref1.y.data(), W, W, H, x + i + (mv1[0] >> 2), y + j + (mv1[1] >> 2), mv1[0] & 3, mv1[1] & 3);
+      s += tv_abs((int)src.y[(size_t)(y + j) * W + x + i] - ((p0 + p1 + 1) >> 1));
+    }
+  return s;
+}
+
+void analyze_inter_b(const SeqConfig& cfg, const Picture& src, const Picture& ref0, const Picture& ref1,
+                     const int16_t* cmv0, const int16_t* cmv1, const int16_t* prev_mv, int range, FrameDecisions& fd) {
+  const int pen_split = (int)(lambda_sad(cfg.qp) * 4);
+  const int wc = cfg.coded_w / kCtb, hc = cfg.coded_h / kCtb;
   for (int cyi = 0; cyi < hc; ++cyi)
     for (int cxi = 0; cxi < wc; ++cxi) {
       const int cx = cxi * kCtb, cy = cyi * kCtb;
-      const int u0 = (cy >> 3) * fd.w8 + (cx >> 3);
-      int cand[kMeMaxCand][2], pmv[2];
-      const int nc = me_candidates(cmv, wc, hc, cxi, cyi, prev_mv[2 * u0], prev_mv[2 * u0 + 1], lim, cand, pmv);
-      // integer refinement: the 21 block costs at every window position (8x8 SADs reused)
-      unsigned best[21];
-      for (int k = 0; k < 21; ++k) best[k] = 0xffffffffu;
-      for (int pos = 0; pos < nc * kMePosPerCand; ++pos) {
-        int mx, my;
-        me_pos_to_mv(pos, cand, mx, my);
-        const unsigned pen = (unsigned)penmv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])];
-        int s8[16], s16[4] = {0, 0, 0, 0}, s32 = 0;
-        for (int k = 0; k < 16; ++k) {
-          s8[k] = sad8(cx + (k & 3) * 8, cy + (k >> 2) * 8, mx, my);
-          s16[((k >> 3) << 1) | ((k >> 1) & 1)] += s8[k];
-          s32 += s8[k];
-        }
-        auto upd = [&](int bi, int sad) {
-          const unsigned v = ((unsigned)sad + pen) << 11 | (unsigned)pos;
-          best[bi] = v < best[bi] ? v : best[bi];
-        };
-        for (int k = 0; k < 16; ++k) upd(k, s8[k]);
-        for (int q = 0; q < 4; ++q) upd(16 + q, s16[q]);
-        upd(20, s32);
-      }
-      int bcost[21], bmv[21][2];
+      CtbMe m0, m1;
+      me_ctb(cfg, src, ref0, cmv0, prev_mv, range, cxi, cyi, fd.w8, m0);
+      me_ctb(cfg, src, ref1, cmv1, prev_mv, range, cxi, cyi, fd.w8, m1);
+      int cost[21], dir[21];
       for (int bi = 0; bi < 21; ++bi) {
-        int mx, my;
-        me_pos_to_mv((int)(best[bi] & 2047), cand, mx, my);
-        bmv[bi][0] = 4 * mx;
-        bmv[bi][1] = 4 * my;
-        bcost[bi] = (int)(best[bi] >> 11);
         int bx, by, n;
-        blk(bi, bx, by, n);
-        // half then quarter pel refinement (centre wins ties, then the lowest neighbour)
-        for (int step = 2; step >= 1; step >>= 1) {
-          const int c0x = bmv[bi][0], c0y = bmv[bi][1];
-          for (int k = 0; k < 8; ++k) {
-            int ox, oy;
-            me_cand_offset(k, ox, oy);
-            const int qx = c0x + ox * step, qy = c0y + oy * step;
-            const int c = sad_qpel(cx + bx, cy + by, n, qx, qy) + penmv[me_pen_index(qx - pmv[0], qy - pmv[1])];
-            if (c < bcost[bi]) {
-              bcost[bi] = c;
-              bmv[bi][0] = qx;
-              bmv[bi][1] = qy;
-            }
-          }
+        me_blk(bi, bx, by, n);
+        const int cb = bipred_sad(src, ref0, ref1, cx + bx, cy + by, n, m0.mv[bi], m1.mv[bi]) + m0.pen[bi] + m1.pen[bi];
+        cost[bi] = m0.cost[bi];
+        dir[bi] = 1;
+        if (m1.cost[bi] < cost[bi]) {
+          cost[bi] = m1.cost[bi];
+          dir[bi] = 2;
+        }
+        if (cb < cost[bi]) {
+          cost[bi] = cb;
+          dir[bi] = 3;
         }
       }
-      // bottom-up CU split decision
-      int sum16 = 0;
-      for (int q = 0; q < 4; ++q) {
-        int sum8 = 0;
-        for (int r = 0; r < 4; ++r) sum8 += bcost[blk8_of(q, r)] + pen_split;
-        const bool split = sum8 < bcost[16 + q] + pen_split;
-        sum16 += split ? sum8 : bcost[16 + q] + pen_split;
-        for (int r = 0; r < 4; ++r) {
-          const int ux = (q & 1) * 2 + (r & 1), uy = (q >> 1) * 2 + (r >> 1);
-          const int u = u0 + uy * fd.w8 + ux;
-          const int sbi = split ? blk8_of(q, r) : 16 + q;
-          fd.cu_log2[u] = split ? 3 : 4;
-          fd.mv[2 * u] = (int16_t)bmv[sbi][0];
-          fd.mv[2 * u + 1] = (int16_t)bmv[sbi][1];
-        }
+      int sel[16];
+      uint8_t l2[16];
+      split_ctb(cost, pen_split, sel, l2);
+      const int u0 = (cy >> 3) * fd.w8 + (cx >> 3);
+      for (int k = 0; k < 16; ++k) {
+        const int u = u0 + (k >> 2) * fd.w8 + (k & 3), b = sel[k];
+        fd.cu_log2[u] = l2[k];
+        fd.dir[u] = (uint8_t)dir[b];
+        fd.mv[2 * u] = (int16_t)(dir[b] & 1 ? m0.mv[b][0] : 0);
+        fd.mv[2 * u + 1] = (int16_t)(dir[b] & 1 ? m0.mv[b][1] : 0);
+        fd.mv1[2 * u] = (int16_t)(dir[b] & 2 ? m1.mv[b][0] : 0);
+        fd.mv1[2 * u + 1] = (int16_t)(dir[b] & 2 ? m1.mv[b][1] : 0);
+        fd.intra[u] = 0;
+        fd.ipm[u] = 1;
       }
-      const bool whole = bcost[20] + pen_split <= sum16;
-      for (int j = 0; j < 4; ++j)
-        for (int i = 0; i < 4; ++i) {
-          const int u = u0 + j * fd.w8 + i;
-          if (whole) {
-            fd.cu_log2[u] = 5;
-            fd.mv[2 * u] = (int16_t)bmv[20][0];
-            fd.mv[2 * u + 1] = (int16_t)bmv[20][1];
-          }
-          fd.intra[u] = 0;
-          fd.ipm[u] = 1;
-        }
     }
 }
 
@@ -330,7 +409,7 @@ static int code_tb(const int* resid, int log2N, int qp, bool intra, int16_t* lev
 }
 
 void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* ref,
-                       FrameDecisions& fd, Picture& rec) {
+                       FrameDecisions& fd, Picture& rec, const Picture* ref1) {
   const int W = cfg.coded_w, Wc = W >> 1, qp = cfg.qp, qpc = chroma_qp(qp, 0);
   int pred[32 * 32], resid[32 * 32];
   // walk CUs in z-order per CTU (needed for intra; harmless for inter)
@@ -343,8 +422,11 @@ void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* 
       const int l2 = c ? log2 - 1 : log2, n = 1 << l2;
       const int x = c ? x0 >> 1 : x0, y = c ? y0 >> 1 : y0;
       const int stride = c ? Wc : W;
+      const int dir = ref1 ? fd.dir[u] : 1;
       if (intra) predict_intra_tb(rec, c, x, y, l2, fd.ipm[u], pred);
-      else predict_inter_block(*ref, c, x, y, n, n, fd.mv[2 * u], fd.mv[2 * u + 1], pred);
+      else if (dir == 1) predict_inter_block(*ref, c, x, y, n, n, fd.mv[2 * u], fd.mv[2 * u + 1], pred);
+      else if (dir == 2) predict_inter_block(*ref1, c, x, y, n, n, fd.mv1[2 * u], fd.mv1[2 * u + 1], pred);
+      else predict_bi_block(*ref, *ref1, c, x, y, n, n, &fd.mv[2 * u], &fd.mv1[2 * u], pred);
       const uint8_t* S = src.plane(c) + (size_t)y * stride + x;
       for (int j = 0; j < n; ++j)
         for (int i = 0; i < n; ++i) resid[j * n + i] = S[j * stride + i] - pred[j * n + i];
@@ -387,15 +469,83 @@ CpuEncoder::CpuEncoder(const SeqConfig& cfg, int search_range) : cfg_(cfg), rang
   if (search_range < 16 || search_range > 128 || (search_range & 15))
     throw std::runtime_error("search range must be a multiple of 16 in 16..128");
   cfg_.finalize();
+  if (cfg_.mgop > 1) {  // parameter sets announce the steady-state DPB / reorder needs
+    const GopPlan g = plan_gop(2 * cfg_.mgop + 1, cfg_.mgop);
+    cfg_.dpb_size = g.dpb_size;
+    cfg_.num_reorder = g.num_reorder;
+  }
   src_.alloc(cfg_.coded_w, cfg_.coded_h);
   rec_.alloc(cfg_.coded_w, cfg_.coded_h);
   ref_.alloc(cfg_.coded_w, cfg_.coded_h);
   dec.alloc(cfg_.coded_w, cfg_.coded_h);
 }
 
+void CpuEncoder::begin_gop(int nframes) {
+  if (cfg_.mgop <= 1) throw std::runtime_error("begin_gop: B frames are off (mgop <= 1)");
+  plan_ = plan_gop(nframes, cfg_.mgop);
+  next_ = 0;
+  dpb_.clear();
+}
+
+void CpuEncoder::encode_b_structured(std::vector<uint8_t>& out, int qp) {
+  if (next_ >= (int)plan_.pics.size()) throw std::runtime_error("encode: GOP plan exhausted (call begin_gop)");
+  const CodedPic& p = plan_.pics[next_++];
+  dec.alloc(cfg_.coded_w, cfg_.coded_h);
+  const int wc = cfg_.coded_w / kCtb, hc = cfg_.coded_h / kCtb;
+  std::vector<uint8_t> q;
+  quarter_luma(src_, q);
+  auto find = [&](int d) -> DpbEntry& {
+    for (auto& e : dpb_)
+      if (e.disp == d) return e;
+    throw std::runtime_error("reference picture not in the encoder DPB");
+  };
+  SeqConfig fc = cfg_;
+  const int base = qp >= 0 ? qp : cfg_.qp;
+  fc.qp = clip3(0, 51, base + gop_layer_qp_offset(p.type, p.layer, cfg_.mgop));
+  std::vector<int16_t> cmv[2];
+  int penmv[64];
+  for (int i = 0; i < 64; ++i) penmv[i] = (int)(lambda_sad(cfg_.qp) * i);
+  for (int l = 0; l < 2; ++l) {
+    if (p.ref[l] < 0) continue;
+    cmv[l].assign(2 * (size_t)wc * hc, 0);
+    std::vector<int> ccost((size_t)wc * hc);
+    coarse_search(q.data(), find(p.ref[l]).q.data(), cfg_.coded_w, cfg_.coded_h, range_, penmv, cmv[l].data(), ccost.data());
+  }
+  if (prev_mv_.empty()) prev_mv_.assign(2 * (size_t)dec.w8 * dec.h8, 0);
+  dec.refs = slice_refs(p);  // before reconstruction: B deblocking reads the directions
+  dec.has_refs = true;
+  if (p.type == 2) {
+    write_parameter_sets(cfg_, out);
+    analyze_intra(fc, src_, dec);
+    reconstruct_frame(fc, src_, nullptr, dec, rec_);
+  } else if (p.type == 1) {
+    const Picture& r0 = find(p.ref[0]).rec;
+    analyze_inter(fc, src_, r0, cmv[0].data(), prev_mv_.data(), range_, dec);
+    reconstruct_frame(fc, src_, &r0, dec, rec_);
+  } else {
+    const Picture& r0 = find(p.ref[0]).rec;
+    const Picture& r1 = find(p.ref[1]).rec;
+    analyze_inter_b(fc, src_, r0, r1, cmv[0].data(), cmv[1].data(), prev_mv_.data(), range_, dec);
+    reconstruct_frame(fc, src_, &r0, dec, rec_, &r1);
+  }
+  prev_mv_ = dec.mv;
+  dec.qp = fc.qp;
+  write_slice(cfg_, dec.view(), p.disp, p.type == 2, out);
+  // DPB: keep what later pictures reference (this picture's RPS, plus itself if referenced)
+  std::vector<DpbEntry> kept;
+  for (auto& e : dpb_)
+    if (std::find(p.rps.begin(), p.rps.end(), e.disp) != p.rps.end()) kept.push_back(std::move(e));
+  dpb_ = std::move(kept);
+  if (p.referenced) dpb_.push_back(DpbEntry{p.disp, rec_, std::move(q)});
+}
+
 void CpuEncoder::encode_frame(const uint8_t* const planes[3], const int strides[3], bool idr,
                               int poc, std::vector<uint8_t>& out, int qp) {
   pad_source(planes, strides, cfg_.width, cfg_.height, src_);
+  if (cfg_.mgop > 1) {
+    encode_b_structured(out, qp);
+    return;
+  }
   dec.alloc(cfg_.coded_w, cfg_.coded_h);
   const int wc = cfg_.coded_w / kCtb, hc = cfg_.coded_h / kCtb, qw = cfg_.coded_w / 4;
   quarter_luma(src_, qcur_);

@@ -131,13 +131,16 @@ Pps parse_pps(BitReader& br) {
 
 class SliceDecoder {
  public:
-  SliceDecoder(const Sps& sps, const Pps& pps, bool islice, int qp, int max_merge, BitReader* br,
-               Picture* cur, const Picture* ref, FrameDecisions* fd, bool sao,
+  // ref[0] / ref[1]: RefPicList0[0] / RefPicList1[0] (B slices), ref_poc their POCs
+  SliceDecoder(const Sps& sps, const Pps& pps, int stype, int qp, int max_merge, BitReader* br,
+               Picture* cur, const Picture* const* ref, const int* ref_poc, int poc, FrameDecisions* fd, bool sao,
                std::vector<size_t> row_start = {})
-      : sps_(sps), islice_(islice), qp_(qp), max_merge_(max_merge), dec_(br), br_(br), cur_(cur), ref_(ref),
-        fd_(fd), sao_(sao), row_start_(std::move(row_start)) {
+      : sps_(sps), islice_(stype == 2), bslice_(stype == 0), qp_(qp), max_merge_(max_merge), dec_(br), br_(br),
+        cur_(cur), ref_(ref[0]), ref1_(ref[1]), poc_(poc), fd_(fd), sao_(sao), row_start_(std::move(row_start)) {
     (void)pps;
-    ctx_.init(islice ? 0 : 1, qp);
+    ref_poc_[0] = ref_poc[0];
+    ref_poc_[1] = ref_poc[1];
+    ctx_.init(islice_ ? 0 : (bslice_ ? 2 : 1), qp);
     skip_.assign((size_t)fd->w8 * fd->h8, 0);
     decoded_.assign((size_t)fd->w8 * fd->h8, 0);
     dec_.start();
@@ -257,6 +260,81 @@ class SliceDecoder {
     mv.y = fd_->mv[2 * u + 1];
     return true;
   }
+  bool motion_at(int xc, int yc, int xn, int yn, Motion& m) const {
+    if (!avail(xc, yc, xn, yn)) return false;
+    const int u = unit(xn, yn);
+    if (!decoded_[u] || fd_->intra[u]) return false;
+    m.dir = fd_->dir[u];
+    m.mv[0] = Mv{fd_->mv[2 * u], fd_->mv[2 * u + 1]};
+    m.mv[1] = Mv{fd_->mv1[2 * u], fd_->mv1[2 * u + 1]};
+    return true;
+  }
+  void fill_motion(int x0, int y0, int log2, const Motion& m) {
+    const int n = 1 << (log2 - 3);
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) {
+        const int u = unit(x0 + 8 * i, y0 + 8 * j);
+        fd_->dir[u] = (uint8_t)m.dir;
+        fd_->mv1[2 * u] = (int16_t)m.mv[1].x;
+        fd_->mv1[2 * u + 1] = (int16_t)m.mv[1].y;
+      }
+  }
+
+  // B-slice inter CU: skip / merge / AMVP per list (7.3.8.5-7.3.8.6)
+  void coding_unit_b(int x0, int y0, int log2, bool skip) {
+    const int N = 1 << log2;
+    auto at = [&](int xn, int yn, Motion& o) { return motion_at(x0, y0, xn, yn, o); };
+    Motion m;
+    bool has_res = !skip;
+    bool merge = skip;
+    if (!skip) {
+      if (bin(CTX_PRED_MODE)) fail("intra CU in a B slice unsupported");
+      if (!bin(CTX_PART_MODE)) fail("only 2Nx2N inter partitions supported");
+      merge = bin(CTX_MERGE_FLAG) != 0;
+    }
+    if (merge) {
+      const int mi = parse_merge_idx();
+      Motion cand[5];
+      merge_candidates_b(x0, y0, N, N, max_merge_, ref_poc_[0] == ref_poc_[1], at, cand);
+      m = cand[mi];
+    } else {
+      m.dir = bin(CTX_INTER_PRED_IDC + (kCtbLog2 - log2)) ? 3 : (bin(CTX_INTER_PRED_IDC + 4) ? 2 : 1);
+      for (int X = 0; X < 2; ++X) {
+        if (!((m.dir >> X) & 1)) continue;
+        const Mv d = parse_mvd();
+        const int sel = bin(CTX_MVP_FLAG);
+        Mv mvp[2];
+        amvp_candidates_b(x0, y0, N, N, X, ref_poc_, poc_, at, mvp);
+        m.mv[X].x = (int16_t)(mvp[sel].x + d.x);
+        m.mv[X].y = (int16_t)(mvp[sel].y + d.y);
+      }
+      has_res = bin(CTX_RQT_ROOT_CBF) != 0;
+    }
+    if (!(m.dir & 1)) m.mv[0] = Mv{};
+    if (!(m.dir & 2)) m.mv[1] = Mv{};
+    fill(x0, y0, log2, 0, 1, m.mv[0], 0, skip ? 1 : 0);
+    fill_motion(x0, y0, log2, m);
+    int cbf = 0;
+    if (has_res) cbf = transform_tree(x0, y0, log2, false, 0);
+    fill(x0, y0, log2, 0, 1, m.mv[0], cbf, skip ? 1 : 0);
+    recon_motion(x0, y0, log2, m, cbf);
+  }
+  void recon_motion(int x0, int y0, int log2, const Motion& m, int cbf) {
+    if (m.dir == 1) return recon_inter(x0, y0, log2, m.mv[0], cbf, ref_);
+    if (m.dir == 2) return recon_inter(x0, y0, log2, m.mv[1], cbf, ref1_);
+    if (!ref_ || !ref1_) fail("bi-prediction without two references");
+    const int N = 1 << log2, W = sps_.coded_w, Wc = W >> 1;
+    int pred[32 * 32];
+    const int16_t v0[2] = {(int16_t)m.mv[0].x, (int16_t)m.mv[0].y}, v1[2] = {(int16_t)m.mv[1].x, (int16_t)m.mv[1].y};
+    predict_bi_block(*ref_, *ref1_, 0, x0, y0, N, N, v0, v1, pred);
+    recon_tb(fd_->coef_y.data() + (size_t)y0 * W + x0, W, cbf & 1, log2, qp_, pred, cur_->y.data() + (size_t)y0 * W + x0, W);
+    const int qpc = chroma_qp(qp_, 0);
+    for (int c = 1; c <= 2; ++c) {
+      predict_bi_block(*ref_, *ref1_, c, x0 >> 1, y0 >> 1, N >> 1, N >> 1, v0, v1, pred);
+      const int16_t* L = (c == 1 ? fd_->coef_u : fd_->coef_v).data() + (size_t)(y0 >> 1) * Wc + (x0 >> 1);
+      recon_tb(L, Wc, (cbf >> c) & 1, log2 - 1, qpc, pred, cur_->plane(c) + (size_t)(y0 >> 1) * Wc + (x0 >> 1), Wc);
+    }
+  }
 
   int parse_merge_idx() {
     if (max_merge_ <= 1) return 0;
@@ -306,13 +384,17 @@ class SliceDecoder {
       if (avail(x0, y0, x0 - 1, y0) && skip_[unit(x0 - 1, y0)]) ++inc;
       if (avail(x0, y0, x0, y0 - 1) && skip_[unit(x0, y0 - 1)]) ++inc;
       const int skip = bin(CTX_CU_SKIP + inc);
+      if (bslice_) {
+        coding_unit_b(x0, y0, log2, skip != 0);
+        return;
+      }
       auto f = [&](int xn, int yn, Mv& m) { return inter_at(x0, y0, xn, yn, m); };
       if (skip) {
         const int mi = parse_merge_idx();
         Mv cand[5];
         merge_candidates(x0, y0, N, N, max_merge_, f, cand);
         fill(x0, y0, log2, 0, 1, cand[mi], 0, 1);
-        recon_inter(x0, y0, log2, cand[mi], 0);
+        recon_inter(x0, y0, log2, cand[mi], 0, ref_);
         return;
       }
       const int intra = bin(CTX_PRED_MODE);
@@ -339,7 +421,7 @@ class SliceDecoder {
         fill(x0, y0, log2, 0, 1, mv, 0, 0);
         if (has_res) cbf = transform_tree(x0, y0, log2, false, 0);
         fill(x0, y0, log2, 0, 1, mv, cbf, 0);
-        recon_inter(x0, y0, log2, mv, cbf);
+        recon_inter(x0, y0, log2, mv, cbf, ref_);
         return;
       }
     }
@@ -548,16 +630,16 @@ class SliceDecoder {
     return cIdx == 0 ? sigCtx : 27 + sigCtx;
   }
 
-  void recon_inter(int x0, int y0, int log2, Mv mv, int cbf) {
-    if (!ref_) fail("P slice without reference");
+  void recon_inter(int x0, int y0, int log2, Mv mv, int cbf, const Picture* ref) {
+    if (!ref) fail("inter prediction without a reference");
     const int N = 1 << log2, W = sps_.coded_w, Wc = W >> 1;
     int pred[32 * 32];
-    predict_inter_block(*ref_, 0, x0, y0, N, N, mv.x, mv.y, pred);
+    predict_inter_block(*ref, 0, x0, y0, N, N, mv.x, mv.y, pred);
     recon_tb(fd_->coef_y.data() + (size_t)y0 * W + x0, W, cbf & 1, log2, qp_, pred,
              cur_->y.data() + (size_t)y0 * W + x0, W);
     const int qpc = chroma_qp(qp_, 0);
     for (int c = 1; c <= 2; ++c) {
-      predict_inter_block(*ref_, c, x0 >> 1, y0 >> 1, N >> 1, N >> 1, mv.x, mv.y, pred);
+      predict_inter_block(*ref, c, x0 >> 1, y0 >> 1, N >> 1, N >> 1, mv.x, mv.y, pred);
       const int16_t* L = (c == 1 ? fd_->coef_u : fd_->coef_v).data() + (size_t)(y0 >> 1) * Wc + (x0 >> 1);
       recon_tb(L, Wc, (cbf >> c) & 1, log2 - 1, qpc, pred, cur_->plane(c) + (size_t)(y0 >> 1) * Wc + (x0 >> 1), Wc);
     }
@@ -578,13 +660,14 @@ class SliceDecoder {
   }
 
   const Sps& sps_;
-  bool islice_;
+  bool islice_, bslice_;
   int qp_, max_merge_;
   CabacDecoder dec_;
   BitReader* br_;
   ContextSet ctx_;
   Picture* cur_;
-  const Picture* ref_;
+  const Picture *ref_, *ref1_;
+  int poc_, ref_poc_[2];
   FrameDecisions* fd_;
   bool sao_;
   std::vector<size_t> row_start_;
@@ -620,7 +703,9 @@ void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int cou
   Sps sps;
   Pps pps;
   const auto nals = split_annexb(data, n);
-  // picture index of every slice NAL and the last IDR at or before `first`
+  // picture index of every slice NAL and the last IDR at or before `first`.  Pictures of one
+  // coded video sequence (IDR to IDR) occupy the same index range in decoding and output
+  // order (closed GOPs), so whole sequences are decoded and reordered by POC.
   int start_pic = 0;
   {
     int k = 0;
@@ -633,17 +718,33 @@ void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int cou
     }
   }
   const int end_pic = count < 0 ? INT_MAX : first + count;
-  Picture ref_pic;
-  bool have_ref = false;
+  struct DpbPic {
+    int poc;
+    Picture pic;
+  };
+  std::vector<DpbPic> dpb;          // reference pictures of the current sequence
+  std::vector<DecodedPicture> cvs;  // decoded pictures of the current sequence (decoding order)
+  int cvs_start = 0;                // output index of the sequence's first picture
+  int prev_poc = 0;
+  auto flush = [&] {
+    std::stable_sort(cvs.begin(), cvs.end(), [](const DecodedPicture& a, const DecodedPicture& b) { return a.poc < b.poc; });
+    for (size_t i = 0; i < cvs.size(); ++i) {
+      const int o = cvs_start + (int)i;
+      if (o >= first && o < end_pic) pictures.push_back(std::move(cvs[i]));
+    }
+    cvs_start += (int)cvs.size();
+    cvs.clear();
+  };
   int pic = -1;
   for (const auto& nal : nals) {
     if (nal.size < 2) continue;
     const int type = nal.type();
     if (type <= 21 && nal.size >= 3 && (nal.data[2] & 0x80)) {
       ++pic;
+      const bool is_idr = type == NAL_IDR_W_RADL || type == NAL_IDR_N_LP;
       if (pic < start_pic) continue;
-      if (pic >= end_pic) break;
-    } else if (type <= 21 && (pic < start_pic || pic >= end_pic)) {
+      if (is_idr && pic > start_pic && pic >= end_pic) break;
+    } else if (type <= 21 && pic < start_pic) {
       continue;
     }
     std::vector<size_t> removed;  // escaped indices of the emulation-prevention bytes
@@ -669,12 +770,40 @@ void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int cou
     if (type >= 16 && type <= 23) br.u(1);  // no_output_of_prior_pics_flag
     br.ue();
     const int stype = (int)br.ue();
-    if (stype == 0) fail("B slices unsupported");
+    if (stype > 2) fail("bad slice_type");
     const bool islice = stype == 2;
     int poc = 0;
-    if (!idr) {
-      poc = (int)br.u(sps.log2_poc_lsb);
-      if (!br.u(1)) fail("explicit slice RPS unsupported");
+    std::vector<int> rps_poc, rps_used;  // the picture's reference picture set
+    if (idr) {
+      flush();
+      cvs_start = pic;
+      dpb.clear();
+      prev_poc = 0;
+    } else {
+      const int lsb = (int)br.u(sps.log2_poc_lsb), max_lsb = 1 << sps.log2_poc_lsb;
+      const int prev_lsb = prev_poc & (max_lsb - 1), prev_msb = prev_poc - prev_lsb;
+      int msb = prev_msb;  // 8.3.1
+      if (lsb < prev_lsb && prev_lsb - lsb >= max_lsb / 2) msb += max_lsb;
+      else if (lsb > prev_lsb && lsb - prev_lsb > max_lsb / 2) msb -= max_lsb;
+      poc = msb + lsb;
+      if (br.u(1)) {  // short_term_ref_pic_set_sps_flag: the SPS set {-1, used}
+        rps_poc.push_back(poc - 1);
+        rps_used.push_back(1);
+      } else {  // st_ref_pic_set(num_short_term_ref_pic_sets)
+        if (br.u(1)) fail("inter RPS prediction unsupported");
+        const int nn = (int)br.ue(), np = (int)br.ue();
+        if (nn + np > kMaxRps) fail("RPS too large");
+        for (int i = 0, p = poc; i < nn; ++i) {
+          p -= (int)br.ue() + 1;
+          rps_poc.push_back(p);
+          rps_used.push_back((int)br.u(1));
+        }
+        for (int i = 0, p = poc; i < np; ++i) {
+          p += (int)br.ue() + 1;
+          rps_poc.push_back(p);
+          rps_used.push_back((int)br.u(1));
+        }
+      }
     }
     bool sao = false;
     if (sps.sao) {
@@ -685,6 +814,7 @@ void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int cou
     int max_merge = 5;
     if (!islice) {
       if (br.u(1)) fail("num_ref_idx override unsupported");
+      if (stype == 0 && br.u(1)) fail("mvd_l1_zero_flag unsupported");
       max_merge = 5 - (int)br.ue();
     }
     const int qp = pps.init_qp + br.se();
@@ -718,24 +848,60 @@ void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int cou
         row_start.push_back(rbsp_of(esc));
       }
     }
+    // reference marking (8.3.2): pictures outside the RPS leave the DPB; lists with one
+    // active entry each (8.3.4): L0 = the closest used past picture (else future), L1 = the
+    // closest used future picture (else past)
+    const Picture* ref[2] = {nullptr, nullptr};
+    int ref_poc[2] = {-1, -1};
+    if (!idr) {
+      std::vector<DpbPic> kept;
+      for (auto& d : dpb)
+        for (int p : rps_poc)
+          if (d.poc == p) {
+            kept.push_back(std::move(d));
+            break;
+          }
+      dpb = std::move(kept);
+      int before = INT_MIN, after = INT_MAX;
+      for (size_t i = 0; i < rps_poc.size(); ++i) {
+        if (!rps_used[i]) continue;
+        const int p = rps_poc[i];
+        bool present = false;
+        for (const auto& d : dpb) present = present || d.poc == p;
+        if (!present) fail("reference picture missing from the DPB");
+        if (p < poc) before = std::max(before, p);
+        else after = std::min(after, p);
+      }
+      const int l0 = before != INT_MIN ? before : after, l1 = after != INT_MAX ? after : before;
+      if (l0 == INT_MAX) fail("inter slice without a reference");
+      ref_poc[0] = l0;
+      ref_poc[1] = stype == 0 ? l1 : -1;
+      for (const auto& d : dpb) {
+        if (d.poc == ref_poc[0]) ref[0] = &d.pic;
+        if (d.poc == ref_poc[1]) ref[1] = &d.pic;
+      }
+    }
     DecodedPicture dp;
     dp.poc = poc;
     dp.idr = idr;
     dp.pic.alloc(sps.coded_w, sps.coded_h);
-    const Picture* ref = nullptr;
-    if (!islice) {
-      if (!have_ref) fail("P slice without a decoded reference");
-      ref = &ref_pic;
-    }
     last_decisions.alloc(sps.coded_w, sps.coded_h);
-    SliceDecoder sd(sps, pps, islice, qp, max_merge, &br, &dp.pic, ref, &last_decisions, sao, row_start);
+    if (stype == 0) {
+      last_decisions.has_refs = true;
+      last_decisions.refs.type = 0;
+      last_decisions.refs.poc = poc;
+      last_decisions.refs.ref_poc[0] = ref_poc[0];
+      last_decisions.refs.ref_poc[1] = ref_poc[1];
+    }
+    SliceDecoder sd(sps, pps, stype, qp, max_merge, &br, &dp.pic, ref, ref_poc, poc, &last_decisions, sao, row_start);
     sd.run();
     if (pps.deblock) deblock_picture(dp.pic, last_decisions.view(), qp);
     if (sao) sao_picture(dp.pic, last_decisions.sao.data());
-    ref_pic = dp.pic;
-    have_ref = true;
-    if (pic >= first) pictures.push_back(std::move(dp));
+    dpb.push_back(DpbPic{poc, dp.pic});
+    prev_poc = poc;
+    cvs.push_back(std::move(dp));
   }
+  flush();
 }
 
 }  // namespace tv

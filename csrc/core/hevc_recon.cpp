@@ -53,6 +53,24 @@ void predict_inter_block(const Picture& ref, int cIdx, int x, int y, int w, int 
   }
 }
 
+void predict_bi_block(const Picture& ref0, const Picture& ref1, int cIdx, int x, int y, int w, int h,
+                      const int16_t* mv0, const int16_t* mv1, int* pred) {
+  const Picture* R[2] = {&ref0, &ref1};
+  const int16_t* M[2] = {mv0, mv1};
+  const int pw = ref0.pw(cIdx), ph = ref0.ph(cIdx);
+  for (int j = 0; j < h; ++j)
+    for (int i = 0; i < w; ++i) {
+      int p[2];
+      for (int l = 0; l < 2; ++l) {
+        const uint8_t* P = R[l]->plane(cIdx);
+        const int mvx = M[l][0], mvy = M[l][1];
+        p[l] = cIdx == 0 ? mc_luma_inter(P, pw, pw, ph, x + (mvx >> 2) + i, y + (mvy >> 2) + j, mvx & 3, mvy & 3)
+                         : mc_chroma_inter(P, pw, pw, ph, x + (mvx >> 3) + i, y + (mvy >> 3) + j, mvx & 7, mvy & 7);
+      }
+      pred[j * w + i] = bipred_sample(p[0], p[1]);
+    }
+}
+
 void recon_tb(const int16_t* levels, int ls, bool cbf, int log2N, int qp, const int* pred,
               uint8_t* dst, int ds) {
   const int N = 1 << log2N;
@@ -71,7 +89,7 @@ void recon_tb(const int16_t* levels, int ls, bool cbf, int log2N, int qp, const 
 
 namespace {
 inline int edge_bs(const FrameData& fd, int xp, int yp, int xq, int yq) {
-  return deblock_edge_bs(fd.cu_log2, fd.intra, fd.cbf, fd.mv, fd.w8, xp, yp, xq, yq);
+  return deblock_edge_bs(fd.cu_log2, fd.intra, fd.cbf, fd.mv, fd.w8, xp, yp, xq, yq, fd.dir, fd.mv1);
 }
 }  // namespace
 

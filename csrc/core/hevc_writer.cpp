@@ -73,8 +73,8 @@ void write_parameter_sets(const SeqConfig& cfg, std::vector<uint8_t>& out) {
     bw.put(0xffff, 16); // reserved
     write_ptl(bw, cfg.level_idc());
     bw.put(1, 1);  // vps_sub_layer_ordering_info_present_flag
-    bw.ue(1);      // vps_max_dec_pic_buffering_minus1
-    bw.ue(0);      // vps_max_num_reorder_pics
+    bw.ue((uint32_t)std::max(1, cfg.dpb_size - 1));  // vps_max_dec_pic_buffering_minus1
+    bw.ue((uint32_t)cfg.num_reorder);                 // vps_max_num_reorder_pics
     bw.ue(0);      // vps_max_latency_increase_plus1
     bw.put(0, 6);  // vps_max_layer_id
     bw.ue(0);      // vps_num_layer_sets_minus1
@@ -105,8 +105,8 @@ void write_parameter_sets(const SeqConfig& cfg, std::vector<uint8_t>& out) {
     bw.ue(0);  // bit_depth_chroma_minus8
     bw.ue(4);  // log2_max_pic_order_cnt_lsb_minus4 -> 8 bits
     bw.put(1, 1);  // sps_sub_layer_ordering_info_present_flag
-    bw.ue(1);      // sps_max_dec_pic_buffering_minus1
-    bw.ue(0);      // sps_max_num_reorder_pics
+    bw.ue((uint32_t)std::max(1, cfg.dpb_size - 1));  // sps_max_dec_pic_buffering_minus1
+    bw.ue((uint32_t)cfg.num_reorder);                 // sps_max_num_reorder_pics
     bw.ue(0);      // sps_max_latency_increase_plus1
     bw.ue(kMinCbLog2 - 3);           // log2_min_luma_coding_block_size_minus3
     bw.ue(kCtbLog2 - kMinCbLog2);    // log2_diff_max_min_luma_coding_block_size
@@ -184,9 +184,10 @@ constexpr uint8_t kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
 class SliceWriter {
  public:
   SliceWriter(const SeqConfig& cfg, const FrameData& fd, bool islice, BitWriter* bw)
-      : cfg_(cfg), fd_(fd), islice_(islice), enc_(bw) {
+      : cfg_(cfg), fd_(fd), islice_(islice), bslice_(fd.refs && fd.refs->type == 0), enc_(bw) {
     skip_.assign((size_t)fd.w8 * fd.h8, 0);
-    ctx_.init(islice ? 0 : 1, fd.qp >= 0 ? fd.qp : cfg.qp);  // contexts start from SliceQpY
+    // initType 0 / 1 / 2 for I / P / B (no cabac_init_flag); contexts start from SliceQpY
+    ctx_.init(islice ? 0 : (bslice_ ? 2 : 1), fd.qp >= 0 ? fd.qp : cfg.qp);
     enc_.start();
   }
 
@@ -301,12 +302,89 @@ class SliceWriter {
     return true;
   }
 
+  Motion motion_of(int u) const {
+    Motion m;
+    m.dir = fd_.dir ? fd_.dir[u] : 1;
+    m.mv[0] = Mv{fd_.mv[2 * u], fd_.mv[2 * u + 1]};
+    if (fd_.mv1) m.mv[1] = Mv{fd_.mv1[2 * u], fd_.mv1[2 * u + 1]};
+    return m;
+  }
+  bool motion_at(int xc, int yc, int xn, int yn, Motion& m) const {
+    if (!avail(xc, yc, xn, yn)) return false;
+    const int u = unit(xn, yn);
+    if (fd_.intra[u]) return false;
+    m = motion_of(u);
+    return true;
+  }
+
+  // B-slice inter CU (7.3.8.5 / 7.3.8.6): skip / merge when the PU's motion equals a merge
+  // candidate, else inter_pred_idc + per-list mvd / mvp flag against the AMVP lists
+  void coding_unit_b(int x0, int y0, int log2, int cbf) {
+    const int u = unit(x0, y0), N = 1 << log2;
+    const Motion m = motion_of(u);
+    const SliceRefs& r = *fd_.refs;
+    auto at = [&](int xn, int yn, Motion& o) { return motion_at(x0, y0, xn, yn, o); };
+    Motion cand[5];
+    const int nc = merge_candidates_b(x0, y0, N, N, cfg_.max_merge_cand, r.ref_poc[0] == r.ref_poc[1], at, cand);
+    int merge_idx = -1;
+    for (int i = 0; i < nc; ++i)
+      if (cand[i] == m) {
+        merge_idx = i;
+        break;
+      }
+    const bool skip = merge_idx >= 0 && cbf == 0;
+    int inc = 0;
+    if (has_left(x0) && skip_[unit(x0 - 1, y0)]) ++inc;
+    if (has_up(y0) && skip_[unit(x0, y0 - 1)]) ++inc;
+    bin(skip ? 1 : 0, CTX_CU_SKIP + inc);
+    set_skip(x0, y0, log2, skip ? 1 : 0);
+    if (skip) {
+      write_merge_idx(merge_idx);
+      return;
+    }
+    bin(0, CTX_PRED_MODE);  // MODE_INTER
+    bin(1, CTX_PART_MODE);  // 2Nx2N
+    bin(merge_idx >= 0 ? 1 : 0, CTX_MERGE_FLAG);
+    if (merge_idx >= 0) {
+      write_merge_idx(merge_idx);
+    } else {
+      // inter_pred_idc (9.3.4.2.2): bin 0 (PRED_BI?) at ctx CtDepth, bin 1 (L1?) at ctx 4
+      bin(m.dir == 3 ? 1 : 0, CTX_INTER_PRED_IDC + (kCtbLog2 - log2));
+      if (m.dir != 3) bin(m.dir == 2 ? 1 : 0, CTX_INTER_PRED_IDC + 4);
+      for (int X = 0; X < 2; ++X) {
+        if (!((m.dir >> X) & 1)) continue;
+        Mv mvp[2];
+        amvp_candidates_b(x0, y0, N, N, X, r.ref_poc, r.poc, at, mvp);
+        const Mv v = m.mv[X];
+        const int c0 = mvd_cost(v.x - mvp[0].x) + mvd_cost(v.y - mvp[0].y);
+        const int c1 = mvd_cost(v.x - mvp[1].x) + mvd_cost(v.y - mvp[1].y);
+        const int sel = c1 < c0 ? 1 : 0;
+        write_mvd(v.x - mvp[sel].x, v.y - mvp[sel].y);
+        bin(sel, CTX_MVP_FLAG);
+      }
+      bin(cbf ? 1 : 0, CTX_RQT_ROOT_CBF);
+      if (!cbf) return;
+    }
+    transform_tree(x0, y0, log2, false, 0);
+  }
+
   void coding_unit(int x0, int y0, int log2) {
     const int u = unit(x0, y0);
     const int N = 1 << log2;
     const bool intra = fd_.intra[u] != 0;
     const int cbf = fd_.cbf[u];
-    if (!islice_) {
+    if (bslice_ && !intra) {
+      coding_unit_b(x0, y0, log2, cbf);
+      return;
+    }
+    if (bslice_) {  // intra CU in a B slice
+      int inc = 0;
+      if (has_left(x0) && skip_[unit(x0 - 1, y0)]) ++inc;
+      if (has_up(y0) && skip_[unit(x0, y0 - 1)]) ++inc;
+      bin(0, CTX_CU_SKIP + inc);
+      set_skip(x0, y0, log2, 0);
+      bin(1, CTX_PRED_MODE);
+    } else if (!islice_) {
       // decide skip / merge / amvp from the motion field
       int merge_idx = -1;
       Mv mv{fd_.mv[2 * u], fd_.mv[2 * u + 1]};
@@ -701,7 +779,7 @@ class SliceWriter {
 
   const SeqConfig& cfg_;
   const FrameData& fd_;
-  bool islice_;
+  bool islice_, bslice_;
   CabacEncoder enc_;
   ContextSet ctx_;
   std::vector<uint8_t> skip_;
@@ -742,24 +820,84 @@ size_t finish_wpp_slice(BitWriter& hdr, const uint8_t* const* rows, const size_t
   return out.size() - before;
 }
 
+SliceRefs slice_refs(const CodedPic& p) {
+  SliceRefs r;
+  r.type = p.type;
+  r.poc = p.disp;
+  r.ref_poc[0] = p.ref[0];
+  r.ref_poc[1] = p.ref[1];
+  if ((int)p.rps.size() > kMaxRps) throw std::runtime_error("reference picture set too large");
+  r.nrps = (int)p.rps.size();
+  for (int i = 0; i < r.nrps; ++i) {
+    r.rps_poc[i] = p.rps[i];
+    r.rps_used[i] = (uint8_t)p.rps_used[i];
+  }
+  return r;
+}
+
 size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
                    std::vector<uint8_t>& out) {
   BitWriter bw;
+  const SliceRefs* r = fd.refs;
+  if (r) {
+    idr = r->type == 2;
+    poc = r->poc;
+  }
+  const int stype = r ? r->type : (idr ? 2 : 1);
   const int nal = idr ? NAL_IDR_N_LP : NAL_TRAIL_R;
   bw.put(1, 1);  // first_slice_segment_in_pic_flag
   if (idr) bw.put(0, 1);  // no_output_of_prior_pics_flag
   bw.ue(0);               // slice_pic_parameter_set_id
-  bw.ue(idr ? 2 : 1);     // slice_type: I = 2, P = 1
+  bw.ue((uint32_t)stype);  // slice_type: B = 0, P = 1, I = 2
   if (!idr) {
     bw.put((uint32_t)(poc & 0xff), 8);  // slice_pic_order_cnt_lsb
-    bw.put(1, 1);                       // short_term_ref_pic_set_sps_flag (idx 0 implied)
+    if (!r) {
+      bw.put(1, 1);  // short_term_ref_pic_set_sps_flag (idx 0 implied)
+    } else {  // explicit st_ref_pic_set(num_short_term_ref_pic_sets = 1)
+      bw.put(0, 1);  // short_term_ref_pic_set_sps_flag
+      bw.put(0, 1);  // inter_ref_pic_set_prediction_flag (stRpsIdx != 0: present)
+      int neg[kMaxRps], pos[kMaxRps], un[kMaxRps], up[kMaxRps], nn = 0, np = 0;
+      for (int i = 0; i < r->nrps; ++i) {
+        if (r->rps_poc[i] < poc) {
+          neg[nn] = r->rps_poc[i];
+          un[nn++] = r->rps_used[i];
+        } else {
+          pos[np] = r->rps_poc[i];
+          up[np++] = r->rps_used[i];
+        }
+      }
+      // S0: decreasing POC (closest first); S1: increasing POC
+      for (int i = 0; i < nn; ++i)
+        for (int j = i + 1; j < nn; ++j)
+          if (neg[j] > neg[i]) {
+            std::swap(neg[i], neg[j]);
+            std::swap(un[i], un[j]);
+          }
+      for (int i = 0; i < np; ++i)
+        for (int j = i + 1; j < np; ++j)
+          if (pos[j] < pos[i]) {
+            std::swap(pos[i], pos[j]);
+            std::swap(up[i], up[j]);
+          }
+      bw.ue((uint32_t)nn);  // num_negative_pics
+      bw.ue((uint32_t)np);  // num_positive_pics
+      for (int i = 0, prev = poc; i < nn; prev = neg[i++]) {
+        bw.ue((uint32_t)(prev - neg[i] - 1));  // delta_poc_s0_minus1
+        bw.put(un[i], 1);                      // used_by_curr_pic_s0_flag
+      }
+      for (int i = 0, prev = poc; i < np; prev = pos[i++]) {
+        bw.ue((uint32_t)(pos[i] - prev - 1));  // delta_poc_s1_minus1
+        bw.put(up[i], 1);                      // used_by_curr_pic_s1_flag
+      }
+    }
   }
   if (cfg.sao) {
     bw.put(1, 1);  // slice_sao_luma_flag
     bw.put(1, 1);  // slice_sao_chroma_flag
   }
   if (!idr) {
-    bw.put(0, 1);  // num_ref_idx_active_override_flag
+    bw.put(0, 1);  // num_ref_idx_active_override_flag (one picture per list)
+    if (stype == 0) bw.put(0, 1);  // mvd_l1_zero_flag
     bw.ue((uint32_t)(5 - cfg.max_merge_cand));  // five_minus_max_num_merge_cand
   }
   bw.se(fd.qp >= 0 ? fd.qp - cfg.qp : 0);  // slice_qp_delta (per-frame rate control)

@@ -7,7 +7,9 @@
 //   cu_log2[u]  log2 size of the covering CU (3..5)
 //   intra[u]    1 = MODE_INTRA, 0 = MODE_INTER
 //   ipm[u]      luma intra prediction mode (intra CUs)
-//   mv[2u+0/1]  quarter-pel motion vector (inter CUs; reference = previous picture)
+//   mv[2u+0/1]  quarter-pel motion vector (inter CUs; list-0 reference)
+//   dir[u]      B slices only: 1 = list 0, 2 = list 1, 3 = bi-prediction (P slices: 1)
+//   mv1[2u+..]  B slices only: the list-1 motion vector
 //   cbf[u]      bit0 = cbf_luma, bit1 = cbf_cb, bit2 = cbf_cr
 //   coef[c]     quantised levels, each TB stored at its picture position (int16 planes,
 //               luma stride = coded_w, chroma stride = coded_w/2)
@@ -16,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "gop.h"
 #include "hevc_defs.h"
 
 namespace tv {
@@ -32,6 +35,10 @@ struct SeqConfig {
   // CTB row, contexts synced from the row above after its second CTB, entry points in the
   // slice header -- the rows can be entropy-coded in parallel (the GPU CABAC path)
   bool wpp = false;
+  // hierarchical-B coding structure (tv/gop.h): mini-GOP size (1 = I P P P ...), and the
+  // DPB size / reorder depth the parameter sets announce for it
+  int mgop = 1;
+  int dpb_size = 2, num_reorder = 0;
   int fps_num = 30, fps_den = 1;
   void finalize() {
     coded_w = (width + kCtb - 1) / kCtb * kCtb;
@@ -41,6 +48,19 @@ struct SeqConfig {
   int h8() const { return coded_h >> 3; }
   int level_idc() const;
 };
+
+// Coding-structure part of a slice header (hierarchical-B streams, tv/gop.h): slice type,
+// POC, the list-0 / list-1 reference POCs and the explicit reference picture set.
+constexpr int kMaxRps = 16;
+struct SliceRefs {
+  int type = 2;                  // 2 = I, 1 = P, 0 = B
+  int poc = 0;
+  int ref_poc[2] = {-1, -1};
+  int nrps = 0;
+  int rps_poc[kMaxRps] = {};
+  uint8_t rps_used[kMaxRps] = {};
+};
+SliceRefs slice_refs(const CodedPic& p);
 
 struct FrameData {
   int w8 = 0, h8 = 0;
@@ -61,6 +81,11 @@ struct FrameData {
   // SAO parameters, 3 packed words (Y, Cb, Cr) per CTB in raster order (nullptr: SAO off)
   const uint32_t* sao = nullptr;
   int qp = -1;  // slice QP (rate control); -1: the sequence QP (PPS init_qp)
+  // hierarchical-B streams: the slice's coding structure (nullptr: IPPP, SPS RPS 0) and, for
+  // B slices, per-unit prediction direction and list-1 vectors
+  const SliceRefs* refs = nullptr;
+  const uint8_t* dir = nullptr;
+  const int16_t* mv1 = nullptr;
 };
 
 // Owning storage for one frame's decisions (CPU side).
@@ -70,7 +95,12 @@ struct FrameDecisions {
   std::vector<int16_t> mv, coef_y, coef_u, coef_v;
   std::vector<uint32_t> sao;  // 3 per CTB
   int qp = -1;                // slice QP of this frame (-1: sequence QP)
+  std::vector<uint8_t> dir;   // B slices (see FrameData)
+  std::vector<int16_t> mv1;
+  SliceRefs refs;
+  bool has_refs = false;      // refs describe this slice (hierarchical-B stream)
   void alloc(int coded_w, int coded_h) {
+    has_refs = false;
     sao.assign(3 * (size_t)(coded_w >> kCtbLog2) * (coded_h >> kCtbLog2), sao_off_param());
     qp = -1;
     cw = coded_w;
@@ -83,6 +113,8 @@ struct FrameDecisions {
     ipm.assign(n, 1);
     cbf.assign(n, 0);
     mv.assign(2 * n, 0);
+    dir.assign(n, 1);
+    mv1.assign(2 * n, 0);
     coef_y.assign((size_t)coded_w * coded_h, 0);
     coef_u.assign((size_t)coded_w * coded_h / 4, 0);
     coef_v.assign((size_t)coded_w * coded_h / 4, 0);
@@ -102,6 +134,13 @@ struct FrameDecisions {
     f.sao = sao.data();
     f.wc = cw >> kCtbLog2;
     f.qp = qp;
+    if (has_refs) {
+      f.refs = &refs;
+      if (refs.type == 0) {
+        f.dir = dir.data();
+        f.mv1 = mv1.data();
+      }
+    }
     return f;
   }
 };
@@ -141,11 +180,15 @@ void predict_intra_tb(const Picture& rec, int cIdx, int x, int y, int log2N, int
 // Inter prediction (uni, L0) of a w x h block of component cIdx at component position (x,y).
 void predict_inter_block(const Picture& ref, int cIdx, int x, int y, int w, int h, int mvx,
                          int mvy, int* pred);
+// Bi-prediction (8.5.3.3.4.2): both lists' 14-bit intermediate samples, (p0 + p1 + 64) >> 7.
+void predict_bi_block(const Picture& ref0, const Picture& ref1, int cIdx, int x, int y, int w, int h,
+                      const int16_t* mv0, const int16_t* mv1, int* pred);
 // Dequantise + inverse transform the levels of a TB (plane stride `ls`) and add to `pred`,
 // writing the clipped reconstruction into `dst` (stride ds).  cbf=false -> copy pred.
 void recon_tb(const int16_t* levels, int ls, bool cbf, int log2N, int qp, const int* pred,
               uint8_t* dst, int ds);
-// In-loop deblocking of a reconstructed picture given the frame decisions.
+// In-loop deblocking of a reconstructed picture given the frame decisions (B slices: the
+// boundary strength compares prediction directions and both lists' vectors).
 void deblock_picture(Picture& pic, const FrameData& fd, int qp);
 // SAO statistics of CTB (cx, cy), component c: source vs deblocked picture.
 void sao_ctb_stats(const Picture& src, const Picture& deb, int c, int cx, int cy, SaoStats& st);
@@ -213,6 +256,138 @@ void amvp_candidates(int xPb, int yPb, int nW, int nH, F&& inter_at, Mv* out) {
   if (!isScaled && fB) { fA = true; A = B; }
   // (!isScaled): B re-derived by the scaled pass -> same first available B candidate
   Mv list[3];
+  int n = 0;
+  if (fA) list[n++] = A;
+  if (fB) list[n++] = B;
+  if (n == 2 && list[0] == list[1]) n = 1;
+  while (n < 2) list[n++] = Mv{0, 0};
+  out[0] = list[0];
+  out[1] = list[1];
+}
+
+// ---------------------------- B-slice motion (one ref per list) --------------------------
+// Motion of a B-slice PU: prediction direction (1 = L0, 2 = L1, 3 = bi) and both lists'
+// vectors (refIdx is always 0: each list holds one picture, tv/gop.h).
+struct Motion {
+  int dir = 1;
+  Mv mv[2];
+  bool operator==(const Motion& o) const {
+    return dir == o.dir && (!(dir & 1) || mv[0] == o.mv[0]) && (!(dir & 2) || mv[1] == o.mv[1]);
+  }
+};
+
+// Merge candidate list of a 2Nx2N PU in a B slice (8.5.3.2.2-8.5.3.2.5, no temporal
+// candidate): spatial candidates, combined bi-predictive candidates, zero candidates.
+// `same_ref` = RefPicList0[0] and RefPicList1[0] are the same picture.
+template <class F>
+int merge_candidates_b(int xPb, int yPb, int nW, int nH, int maxCand, bool same_ref, F&& at, Motion* out) {
+  Motion a1, b1, b0, a0, b2;
+  const bool avA1 = at(xPb - 1, yPb + nH - 1, a1);
+  const bool avB1 = at(xPb + nW - 1, yPb - 1, b1);
+  const bool avB0 = at(xPb + nW, yPb - 1, b0);
+  const bool avA0 = at(xPb - 1, yPb + nH, a0);
+  const bool avB2 = at(xPb - 1, yPb - 1, b2);
+  const bool fA1 = avA1;
+  const bool fB1 = avB1 && !(avA1 && a1 == b1);
+  const bool fB0 = avB0 && !(avB1 && b1 == b0);
+  const bool fA0 = avA0 && !(avA1 && a1 == a0);
+  bool fB2 = avB2 && !(avA1 && a1 == b2) && !(avB1 && b1 == b2);
+  if ((int)fA0 + (int)fA1 + (int)fB0 + (int)fB1 == 4) fB2 = false;
+  int n = 0;
+  if (fA1 && n < maxCand) out[n++] = a1;
+  if (fB1 && n < maxCand) out[n++] = b1;
+  if (fB0 && n < maxCand) out[n++] = b0;
+  if (fA0 && n < maxCand) out[n++] = a0;
+  if (fB2 && n < maxCand) out[n++] = b2;
+  const int orig = n;
+  if (orig > 1 && orig < maxCand) {
+    static const int l0i[12] = {0, 1, 0, 2, 1, 2, 0, 3, 1, 3, 2, 3};
+    static const int l1i[12] = {1, 0, 2, 0, 2, 1, 3, 0, 3, 1, 3, 2};
+    for (int c = 0; c < orig * (orig - 1) && n < maxCand; ++c) {
+      const Motion& p = out[l0i[c]];
+      const Motion& q = out[l1i[c]];
+      if ((p.dir & 1) && (q.dir & 2) && (!same_ref || p.mv[0] != q.mv[1])) {
+        Motion m;
+        m.dir = 3;
+        m.mv[0] = p.mv[0];
+        m.mv[1] = q.mv[1];
+        out[n++] = m;
+      }
+    }
+  }
+  while (n < maxCand) {
+    Motion z;
+    z.dir = 3;
+    out[n++] = z;
+  }
+  return n;
+}
+
+// Spatial MV scaling (8.5.3.2.7): td / tb are POC distances to the candidate's and the
+// target reference picture.
+inline Mv scale_mv(Mv m, int td, int tb) {
+  td = clip3(-128, 127, td);
+  tb = clip3(-128, 127, tb);
+  const int tx = (16384 + (tv_abs(td) >> 1)) / td;
+  const int dsf = clip3(-4096, 4095, (tb * tx + 32) >> 6);
+  auto s = [&](int v) {
+    const long long p = (long long)dsf * v;
+    const long long a = ((p < 0 ? -p : p) + 127) >> 8;
+    return (int)clip3<long long>(-32768, 32767, p < 0 ? -a : a);
+  };
+  return Mv{s(m.x), s(m.y)};
+}
+
+// AMVP candidate list (2 entries) of list X for a 2Nx2N PU in a B slice with one picture
+// per list (POCs ref_poc[0..1], current POC cur_poc): spatial candidates with the
+// other-list and scaled fallbacks, no temporal candidate.
+template <class F>
+void amvp_candidates_b(int xPb, int yPb, int nW, int nH, int X, const int* ref_poc, int cur_poc, F&& at, Mv* out) {
+  const int Y = 1 - X, target = ref_poc[X];
+  Motion nA[2], nB[3];
+  const bool avA[2] = {at(xPb - 1, yPb + nH, nA[0]), at(xPb - 1, yPb + nH - 1, nA[1])};
+  const bool isScaled = avA[0] || avA[1];
+  // first pass: a neighbour vector that points at the target picture as it is
+  auto same_pic = [&](const Motion& m, Mv& v) {
+    if ((m.dir >> X) & 1) {  // list X of the neighbour holds the same picture
+      v = m.mv[X];
+      return true;
+    }
+    if (((m.dir >> Y) & 1) && ref_poc[Y] == target) {
+      v = m.mv[Y];
+      return true;
+    }
+    return false;
+  };
+  // second pass: any vector of the neighbour, scaled to the target picture's distance
+  auto scaled = [&](const Motion& m, Mv& v) {
+    int l;
+    if ((m.dir >> X) & 1) l = X;
+    else if ((m.dir >> Y) & 1) l = Y;
+    else return false;
+    v = m.mv[l];
+    v = scale_mv(v, cur_poc - ref_poc[l], cur_poc - target);
+    return true;
+  };
+  bool fA = false, fB = false;
+  Mv A, B;
+  for (int k = 0; k < 2 && !fA; ++k)
+    if (avA[k]) fA = same_pic(nA[k], A);
+  for (int k = 0; k < 2 && !fA; ++k)
+    if (avA[k]) fA = scaled(nA[k], A);
+  const bool avB[3] = {at(xPb + nW, yPb - 1, nB[0]), at(xPb + nW - 1, yPb - 1, nB[1]), at(xPb - 1, yPb - 1, nB[2])};
+  for (int k = 0; k < 3 && !fB; ++k)
+    if (avB[k]) fB = same_pic(nB[k], B);
+  if (!isScaled && fB) {
+    fA = true;
+    A = B;
+  }
+  if (!isScaled) {
+    fB = false;
+    for (int k = 0; k < 3 && !fB; ++k)
+      if (avB[k]) fB = scaled(nB[k], B);
+  }
+  Mv list[2];
   int n = 0;
   if (fA) list[n++] = A;
   if (fB) list[n++] = B;

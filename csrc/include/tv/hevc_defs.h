@@ -301,8 +301,21 @@ constexpr int8_t kChromaFilter[8][4] = {{0, 64, 0, 0},     {-2, 58, 10, -2}, {-4
 // One luma prediction sample at integer position (xi, yi) with fraction (fx, fy) in quarter
 // pel, reference plane clamped at its borders (w x h).  Returns the final 8-bit sample
 // (uni-prediction, default weighting).
-TV_HD int mc_luma_sample(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx,
-                         int fy) {
+TV_HD int mc_luma_inter(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx,
+                        int fy);
+TV_HD int mc_chroma_inter(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx,
+                          int fy);
+TV_HD int mc_luma_sample(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx, int fy) {
+  return clip_pixel((mc_luma_inter(ref, stride, w, h, xi, yi, fx, fy) + 32) >> 6);
+}
+TV_HD int mc_chroma_sample(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx, int fy) {
+  return clip_pixel((mc_chroma_inter(ref, stride, w, h, xi, yi, fx, fy) + 32) >> 6);
+}
+// bi-prediction of one sample from the two 14-bit intermediates (8.5.3.3.4.2, 8-bit)
+TV_HD int bipred_sample(int p0, int p1) { return clip_pixel((p0 + p1 + 64) >> 7); }
+// 14-bit intermediate luma prediction sample (8.5.3.3.3.1: shift1 = 0, shift2 = 6, shift3 = 6)
+TV_HD int mc_luma_inter(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx,
+                        int fy) {
   auto px = [&](int x, int y) -> int {
     x = clip3(0, w - 1, x);
     y = clip3(0, h - 1, y);
@@ -326,11 +339,11 @@ TV_HD int mc_luma_sample(const uint8_t* ref, int stride, int w, int h, int xi, i
     }
     v >>= 6;
   }
-  return clip_pixel((v + 32) >> 6);
+  return v;
 }
 
-TV_HD int mc_chroma_sample(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx,
-                           int fy) {
+TV_HD int mc_chroma_inter(const uint8_t* ref, int stride, int w, int h, int xi, int yi, int fx,
+                          int fy) {
   auto px = [&](int x, int y) -> int {
     x = clip3(0, w - 1, x);
     y = clip3(0, h - 1, y);
@@ -354,7 +367,7 @@ TV_HD int mc_chroma_sample(const uint8_t* ref, int stride, int w, int h, int xi,
     }
     v >>= 6;
   }
-  return clip_pixel((v + 32) >> 6);
+  return v;
 }
 
 // ------------------------------------ deblocking ----------------------------------------
@@ -437,8 +450,12 @@ TV_HD void deblock_chroma_edge(uint8_t* q0ptr, int xstep, int lstep, int len, in
 // Boundary strength of the deblocking edge between luma positions P and Q (H.265 8.7.2.4)
 // for this engine's structure (TB = PU = CU, one reference picture).  Arrays are the
 // per-8x8-unit decision planes (see hevc_codec.h).  Returns 0 for edges inside a CU.
+// B slices (dir != nullptr): the two lists hold different pictures (tv/gop.h), so the
+// reference sets of P and Q match iff their directions do; then every used list's vectors
+// are compared (8.7.2.4).
 TV_HD int deblock_edge_bs(const uint8_t* cu_log2, const uint8_t* intra, const uint8_t* cbf,
-                          const int16_t* mv, int w8, int xp, int yp, int xq, int yq) {
+                          const int16_t* mv, int w8, int xp, int yp, int xq, int yq,
+                          const uint8_t* dir = nullptr, const int16_t* mv1 = nullptr) {
   const int up = (yp >> 3) * w8 + (xp >> 3), uq = (yq >> 3) * w8 + (xq >> 3);
   const int sp = cu_log2[up], sq = cu_log2[uq];
   if (sp == sq) {
@@ -447,7 +464,14 @@ TV_HD int deblock_edge_bs(const uint8_t* cu_log2, const uint8_t* intra, const ui
   }
   if (intra[up] || intra[uq]) return 2;
   if ((cbf[up] & 1) || (cbf[uq] & 1)) return 1;
-  if (tv_abs(mv[2 * up] - mv[2 * uq]) >= 4 || tv_abs(mv[2 * up + 1] - mv[2 * uq + 1]) >= 4) return 1;
+  auto differ = [&](const int16_t* v) {
+    return tv_abs(v[2 * up] - v[2 * uq]) >= 4 || tv_abs(v[2 * up + 1] - v[2 * uq + 1]) >= 4;
+  };
+  if (!dir) return differ(mv) ? 1 : 0;
+  const int d = dir[up];
+  if (d != dir[uq]) return 1;
+  if ((d & 1) && differ(mv)) return 1;
+  if ((d & 2) && differ(mv1)) return 1;
   return 0;
 }
 

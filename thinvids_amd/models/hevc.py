@@ -42,13 +42,23 @@ class CpuEncoder:
     """Scalar C++ HEVC encoder (software path; reference `software_encode`)."""
 
     def __init__(self, width: int, height: int, qp: int = 27, deblock: bool = True,
-                 search_range: int = 64, max_merge: int = 5, sao: bool = False, crf: int = 0, wpp: bool = False):
+                 search_range: int = 64, max_merge: int = 5, sao: bool = False, crf: int = 0, wpp: bool = False,
+                 bframes: int = 1):
         if width % 2 or height % 2:
             raise ValueError("width/height must be even")
         self.lib = core_lib()
         self.width, self.height, self.qp = width, height, qp
         self.cw, self.ch = coded_size(width, height)
-        if crf:
+        self.bframes = int(bframes)
+        if self.bframes > 1:
+            if crf:
+                raise ValueError("CRF with B frames is not supported by the golden encoder")
+            f = self.lib.tv_cpu_encoder_new_b
+            f.restype = C.c_void_p
+            f.argtypes = [C.c_int] * 7
+            self.h = f(width, height, qp, int(deblock) | (2 if sao else 0) | (4 if wpp else 0), search_range, max_merge,
+                       self.bframes)
+        elif crf:
             f = self.lib.tv_cpu_encoder_new_crf
             f.restype = C.c_void_p
             f.argtypes = [C.c_int] * 7
@@ -65,6 +75,16 @@ class CpuEncoder:
         if getattr(self, "h", None):
             self.lib.tv_cpu_encoder_free(self.h)
             self.h = None
+
+    def begin_gop(self, nframes: int) -> list[int]:
+        """Hierarchical-B mode: plan the next segment; returns the display index of every
+        picture in coding order (feed the frames to :meth:`encode` in that order)."""
+        disp = (C.c_int * nframes)()
+        f = self.lib.tv_cpu_encoder_begin_gop
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        check(f(self.h, nframes, disp))
+        return list(disp)
 
     def encode(self, frame: Frame, idr: bool, poc: int, qp: int | None = None) -> bytes:
         """One frame; `qp` overrides the slice QP of this frame (rate control)."""
@@ -97,11 +117,41 @@ class CpuEncoder:
         return d
 
 
-def encode_sequence_cpu(frames, qp: int = 27, gop: int = 0, frame_qps=None, **kw) -> tuple[bytes, list]:
-    """Encode frames (first is IDR; IDR every `gop` frames if gop>0). Returns (annexb, recons).
-    `frame_qps`: optional per-frame slice QP (rate control); `qp` stays the PPS init QP."""
+def gop_plan(nframes: int, bframes: int) -> dict:
+    """Coding structure of one segment (tv/gop.h): per coded picture the display index,
+    slice type (2 I / 1 P / 0 B), references and temporal layer, plus DPB size / reorder."""
+    lib = core_lib()
+    arrs = [(C.c_int * max(1, nframes))() for _ in range(5)]
+    info = (C.c_int * 2)()
+    f = lib.tv_gop_plan
+    f.restype = C.c_int
+    f.argtypes = [C.c_int, C.c_int] + [C.POINTER(C.c_int)] * 6
+    n = f(nframes, bframes, *arrs, info)
+    keys = ("disp", "type", "ref0", "ref1", "layer")
+    out = {k: list(a)[:n] for k, a in zip(keys, arrs)}
+    out["dpb_size"], out["num_reorder"] = info[0], info[1]
+    return out
+
+
+def encode_sequence_cpu(frames, qp: int = 27, gop: int = 0, frame_qps=None, bframes: int = 1,
+                        **kw) -> tuple[bytes, list]:
+    """Encode frames (first is IDR; IDR every `gop` frames if gop>0). Returns (annexb, recons)
+    with the reconstructions in display order.  `frame_qps`: optional per-frame slice QP
+    (display order; with B frames the base to which the layer offset is added); `qp` stays
+    the PPS init QP.  `bframes` > 1: hierarchical-B mini-GOPs of that size (tv/gop.h)."""
     frames = list(frames)
     h, w = frames[0][0].shape
+    if bframes > 1:
+        enc = CpuEncoder(w, h, qp=qp, bframes=bframes, **kw)
+        seg = gop if gop > 0 else len(frames)
+        out, recons = bytearray(), [None] * len(frames)
+        for s0 in range(0, len(frames), seg):
+            n = min(seg, len(frames) - s0)
+            for d in enc.begin_gop(n):
+                i = s0 + d
+                out += enc.encode(frames[i], d == 0, d, None if frame_qps is None else int(frame_qps[i]))
+                recons[i] = enc.recon()
+        return bytes(out), recons
     enc = CpuEncoder(w, h, qp=qp, **kw)
     out, recons, poc = bytearray(), [], 0
     for i, f in enumerate(frames):
