@@ -484,6 +484,7 @@ from thinvids_amd.common.settings import DEFAULT_SETTINGS as _DEFAULTS  # noqa: 
 
 _WORKER_GOP = int(_DEFAULTS.get("tv_gop", 64))
 _WORKER_SAO = str(_DEFAULTS.get("tv_sao", "1")) == "1"
+_WORKER_BFRAMES = int(_DEFAULTS.get("tv_bframes", 1))
 
 
 def main() -> None:
@@ -499,6 +500,8 @@ def main() -> None:
     ap.add_argument("--sao", dest="sao", action="store_true", default=_WORKER_SAO,
                     help="enable SAO (in-loop sample adaptive offset; default: the worker's shipped tv_sao)")
     ap.add_argument("--no-sao", dest="sao", action="store_false", help="disable SAO")
+    ap.add_argument("--bframes", type=int, default=_WORKER_BFRAMES,
+                    help="hierarchical-B mini-GOP size (1 = I P P P; default: the worker's tv_bframes)")
     ap.add_argument("--range", type=int, default=64, help="motion search range (full-res pels, multiple of 16)")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1)
@@ -542,8 +545,10 @@ def main() -> None:
     # engine splits them into two stream groups one frame apart (measured on MI355X:
     # 1080p 32 -> 48 segments +3 %, 4K 16 -> 24 segments +9 %; profiles/README.md)
     batch = args.batch or (48 if args.res in ("1080p", "720p", "360p") else 24)
+    if args.bframes > 1 and args.kbps > 0:
+        raise SystemExit("--kbps with --bframes > 1 is not supported yet")
     eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=args.sao,
-                    seed=args.seed, threads=args.threads or None, device=local)
+                    seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes)
     post = _PostQueue(local)
 
     def comm(segs, sse):
@@ -624,7 +629,9 @@ def main() -> None:
             "data": f"synthetic ({args.content} seeded procedural YUV 4:2:0 source generated on GPU)",
             "config": {
                 "model": f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else "")
+                + (f" hier-B{args.bframes}" if args.bframes > 1 else "")
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
+                "bframes": args.bframes,
                 "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame QP plan, target {args.kbps:g} "
                                  "kbps per 30 fps stream, batch feedback (measured QP offset response + bounded debt)"
                                  if args.kbps > 0 else f"CQP {args.qp}"),

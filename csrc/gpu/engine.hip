@@ -110,6 +110,7 @@ struct EngineCfg {
   uint32_t seed;
   int groups;
   int crf;  // > 0: in-engine CRF (per-frame QP from the lookahead, tv/rc_model.h)
+  int mgop = 1;  // hierarchical-B mini-GOP (tv/gop.h); 1 = I P P P
 };
 
 // One group of segments on its own HIP stream (buffers, pinned slot ring, events).
@@ -140,27 +141,38 @@ class Core {
       HIP_OK(hipMalloc(&f.v, B * g_.csz));
     };
     alloc_set(src_);
-    // recon ring: final recon of the previous frame (reference), the frame being
-    // reconstructed, and with SAO a third buffer the in-loop filter writes into (no copy of
-    // the deblocked picture: the three rotate by index)
-    nrec_ = (c.deblock & 2) ? 3 : 2;
-    for (int k = 0; k < nrec_; ++k) alloc_set(rec_[k]);
+    // Decoded picture buffer (tv/gop.h): every picture is reconstructed into a free DPB entry
+    // that keeps its final (deblocked + SAO) samples, the 16 quarter-pel phase planes of its
+    // luma (only when a later picture references it) and its quarter-res source luma (the
+    // coarse search's reference); an entry is free again once no later picture needs it.
+    // I P P P needs 2 entries, hierarchical-B mini-GOPs of M frames log2(M) + 2.  With SAO
+    // one scratch set holds the deblocked picture the filter reads.
+    if (c.mgop < 1 || c.mgop > 32 || (c.mgop & (c.mgop - 1))) throw std::runtime_error("bframes must be a power of 2 <= 32");
+    if (c.mgop > 1 && c.crf > 0) throw std::runtime_error("in-engine CRF is not supported with B frames");
+    ndpb_ = c.mgop > 1 ? plan_gop(2 * c.mgop + 1, c.mgop).dpb_size : 2;
+    if (ndpb_ > kMaxDpb) throw std::runtime_error("DPB too large");
+    qsz_ = (long)(g_.W / 4) * (g_.H / 4);
+    for (int k = 0; k < ndpb_; ++k) {
+      alloc_set(dpb_[k].rec);
+      HIP_OK(hipMalloc(&dpb_[k].phase, B * 16 * g_.psz));
+      HIP_OK(hipMalloc(&dpb_[k].q, B * qsz_));
+    }
+    if (c.deblock & 2) alloc_set(deb_);
     HIP_OK(hipMalloc(&coef_y_, B * g_.ysz * sizeof(int16_t)));
     HIP_OK(hipMalloc(&coef_u_, B * g_.csz * sizeof(int16_t)));
     HIP_OK(hipMalloc(&coef_v_, B * g_.csz * sizeof(int16_t)));
     HIP_OK(hipMalloc(&d_sse_, B * 3 * sizeof(unsigned long long)));
-    HIP_OK(hipMalloc(&phase_, B * 16 * g_.psz));
     HIP_OK(hipMalloc(&count_scratch_, B * nctu_ * sizeof(int)));
-    // hierarchical motion search: quarter-res source luma (this / previous frame), coarse field
-    qsz_ = (long)(g_.W / 4) * (g_.H / 4);
-    HIP_OK(hipMalloc(&q_[0], B * qsz_));
-    HIP_OK(hipMalloc(&q_[1], B * qsz_));
-    HIP_OK(hipMalloc(&cmv_, B * nctu_ * 2 * sizeof(int16_t)));
-    HIP_OK(hipMalloc(&ccost_, B * nctu_ * sizeof(int)));
+    // hierarchical motion search: coarse field (+ cost) per list; B pictures: per-list fine
+    // search results for the bi decision
+    HIP_OK(hipMalloc(&cmv_, 2 * B * nctu_ * 2 * sizeof(int16_t)));
+    HIP_OK(hipMalloc(&ccost_, 2 * B * nctu_ * sizeof(int)));
+    if (c.mgop > 1) HIP_OK(hipMalloc(&meout_, 2 * B * nctu_ * sizeof(CtbMeOut)));
     cap_ = g_.ysz + 2 * g_.csz;
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
     slot_bytes_ = align(B * nctu_ * 12) + align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * nctu_ * 8) +
-                  align(B * nctu_ * 4) + align(B * nctu_ * 4) + align(B * 4) + align(B) + align(B * cap_ * 2);
+                  align(B * nctu_ * 4) + align(B * nctu_ * 4) + align(B * 4) + align(B) + align(B * g_.usz) +
+                  align(B * g_.usz * 4) + align(B * cap_ * 2);
     HIP_OK(hipHostMalloc(&qhost_, (size_t)c.gop * B, hipHostMallocDefault));
     HIP_OK(hipHostMalloc(&quni_, (size_t)B, hipHostMallocDefault));
     std::memset(quni_, c.qp, (size_t)B);
@@ -199,23 +211,27 @@ class Core {
     seq_.deblock = (c.deblock & 1) != 0;  // bit 0: deblocking, bit 1: SAO
     seq_.sao = (c.deblock & 2) != 0;
     seq_.max_merge_cand = c.max_merge;
+    seq_.mgop = c.mgop;
+    if (c.mgop > 1) {
+      const GopPlan gp = plan_gop(2 * c.mgop + 1, c.mgop);
+      seq_.dpb_size = gp.dpb_size;
+      seq_.num_reorder = gp.num_reorder;
+    }
     seq_.finalize();
   }
 
   ~Core() {
     fetch_.reset();  // the fetch thread drains (every issued slot was waited for by finish())
     (void)hipStreamSynchronize(stream_);
-    for (auto* p : {src_.y, src_.u, src_.v, rec_[0].y, rec_[0].u, rec_[0].v, rec_[1].y, rec_[1].u, rec_[1].v,
-                    rec_[2].y, rec_[2].u, rec_[2].v})
-      (void)hipFree(p);
+    for (auto* p : {src_.y, src_.u, src_.v, deb_.y, deb_.u, deb_.v}) (void)hipFree(p);
+    for (int k = 0; k < ndpb_; ++k)
+      for (auto* p : {dpb_[k].rec.y, dpb_[k].rec.u, dpb_[k].rec.v, dpb_[k].phase, dpb_[k].q}) (void)hipFree(p);
+    (void)hipFree(meout_);
     (void)hipFree(coef_y_);
     (void)hipFree(coef_u_);
     (void)hipFree(coef_v_);
     (void)hipFree(d_sse_);
-    (void)hipFree(phase_);
     (void)hipFree(count_scratch_);
-    (void)hipFree(q_[0]);
-    (void)hipFree(q_[1]);
     (void)hipFree(cmv_);
     (void)hipFree(ccost_);
     (void)hipFree(rc_);
@@ -240,7 +256,8 @@ class Core {
   long coef_bytes() const { return coef_bytes_; }
   double entropy_ms() const { return entropy_ns_ / 1e6; }
   const Geo& geo() const { return g_; }
-  FrameSet last_recon() const { return rec_[fin_]; }
+  // reconstruction of the segment's last display frame (after finish())
+  FrameSet last_recon() const { return dpb_[last_entry_].rec; }
   hipStream_t stream() const { return stream_; }
 
  private:
@@ -263,8 +280,8 @@ class Core {
   };
   // carve one slot buffer (device or host) into its arrays
   struct Parts {
-    uint8_t *cu_log2, *intra, *ipm, *cbf;
-    int16_t* mv;
+    uint8_t *cu_log2, *intra, *ipm, *cbf, *dir;
+    int16_t *mv, *mv1;
     unsigned long long* mask_y;
     unsigned* mask_c;
     int *count, *offset, *total;
@@ -295,6 +312,11 @@ class Core {
     q += align(B * nctu_ * 12);
     p.qp = reinterpret_cast<int8_t*>(q);
     q += align(B);
+    // B pictures only (copied to the host only in hierarchical-B streams)
+    p.dir = q;
+    q += align(B * U);
+    p.mv1 = reinterpret_cast<int16_t*>(q);
+    q += align(B * U * 4);
     p.packed = reinterpret_cast<int16_t*>(q);
     p.count = nullptr;  // device count array lives in the scratch below
     return p;
@@ -313,6 +335,14 @@ class Core {
     d.coef_v = coef_v_;
     return d;
   }
+  // the slot's decisions of a B picture (direction and list-1 planes attached)
+  DecisionSet slot_dec_b(const Slot& s) const {
+    DecisionSet d = slot_dec(s);
+    const Parts p = carve(s.dev);
+    d.dir = p.dir;
+    d.mv1 = p.mv1;
+    return d;
+  }
   CompactSet slot_compact(const Slot& s) const {
     const Parts p = carve(s.dev);
     CompactSet c;
@@ -329,7 +359,7 @@ class Core {
   void* coef_count_scratch() const { return count_scratch_; }
 
   // host view of segment b in a slot (compact levels)
-  FrameData host_view(const Slot& s, int b) const {
+  FrameData host_view(const Slot& s, int b, const SliceRefs* refs) const {
     const Parts p = carve(s.host);
     const long U = g_.usz;
     FrameData f;
@@ -349,6 +379,11 @@ class Core {
     f.wc = g_.wc;
     f.sao = seq_.sao ? p.sao + (long)b * nctu_ * 3 : nullptr;
     f.qp = p.qp[b];
+    f.refs = refs;  // hierarchical-B streams: slice type, POCs, RPS
+    if (refs && refs->type == 0) {
+      f.dir = p.dir + b * U;
+      f.mv1 = p.mv1 + b * U * 2;
+    }
     return f;
   }
 
@@ -397,12 +432,16 @@ class Core {
     // moves the whole contiguous header (decision planes .. SAO params) in one copy and all
     // segments' packed levels (back to back) in a second one.
     if (B == cfg_.batch) {
-      const long head = reinterpret_cast<uint8_t*>(d.packed) - d.cu_log2;
+      const long head = (seq_.mgop > 1 ? reinterpret_cast<uint8_t*>(d.packed) : d.dir) - d.cu_log2;
       HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, head, hipMemcpyDeviceToHost, ws));
     } else {  // partial batch: each plane is laid out for cfg_.batch segments
       HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.qp, d.qp, B, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
+      if (seq_.mgop > 1) {
+        HIP_OK(hipMemcpyAsync(h.mv1, d.mv1, B * U * 4, hipMemcpyDeviceToHost, ws));
+        HIP_OK(hipMemcpyAsync(h.dir, d.dir, B * U, hipMemcpyDeviceToHost, ws));
+      }
       if (seq_.sao) HIP_OK(hipMemcpyAsync(h.sao, d.sao, B * nctu_ * 12, hipMemcpyDeviceToHost, ws));
       for (uint8_t* const* pl : {&h.cu_log2, &h.intra, &h.ipm, &h.cbf}) {
         const long off = *pl - h.cu_log2;
@@ -431,12 +470,18 @@ class Core {
     if (nframes < 1 || nframes > cfg_.gop) throw std::runtime_error("nframes out of range");
     B_ = nseg;
     F_ = nframes;
-    qmap_given_ = qmap != nullptr;
-    for (int f = 0; f < nframes; ++f)
+    plan_ = plan_gop(nframes, cfg_.mgop);
+    refs_.assign(plan_.pics.size(), SliceRefs{});
+    for (size_t k = 0; k < plan_.pics.size(); ++k) refs_[k] = slice_refs(plan_.pics[k]);
+    for (auto& e : dpb_) e.disp = -1;
+    // per-picture QPs in coding order: the caller's base (display order) + the layer offset
+    qmap_given_ = qmap != nullptr || cfg_.mgop > 1;
+    for (int k = 0; k < nframes; ++k)
       for (int b = 0; b < nseg; ++b) {
-        const int q = qmap ? qmap[b * nframes + f] : cfg_.qp;
-        if (q < 0 || q > 51) throw std::runtime_error("slice QP out of range");
-        qhost_[f * nseg + b] = (int8_t)q;
+        const CodedPic& p = plan_.pics[k];
+        const int base = qmap ? qmap[b * nframes + p.disp] : cfg_.qp;
+        if (base < 0 || base > 51) throw std::runtime_error("slice QP out of range");
+        qhost_[k * nseg + b] = (int8_t)clip3(0, 51, base + gop_layer_qp_offset(p.type, p.layer, cfg_.mgop));
       }
     last_frames_ = nframes;
     out_.assign(B_, {});
@@ -453,23 +498,39 @@ class Core {
   // decisions to the CABAC pool.  Blocks only when the slot ring is full.
   template <class Upload> void issue(int f, Upload&& upload) {
     const int B = B_, F = F_;
-    Range frame_range(f == 0 ? "engine.frame.intra" : "engine.frame.inter");
+    Range frame_range(plan_.pics[f].type == 2 ? "engine.frame.intra" : "engine.frame.inter");
     Slot& s = slots_[f % nslots_];
     wait_slot(s);
-    const DecisionSet dec = slot_dec(s);
+    const DecisionSet dec0 = slot_dec(s);
     // this frame's QPs: copied only when they differ from what the slot already holds (a
     // constant-QP stream pays nothing per frame; a QP map or CRF rewrites them every frame)
     if (qmap_given_) {
-      HIP_OK(hipMemcpyAsync(dec.qp, qhost_ + f * B, B, hipMemcpyHostToDevice, stream_));
+      HIP_OK(hipMemcpyAsync(dec0.qp, qhost_ + f * B, B, hipMemcpyHostToDevice, stream_));
       s.qp_dirty = true;
     } else if (s.qp_dirty) {  // back to the sequence QP for every segment slot
-      HIP_OK(hipMemcpyAsync(dec.qp, quni_, cfg_.batch, hipMemcpyHostToDevice, stream_));
+      HIP_OK(hipMemcpyAsync(dec0.qp, quni_, cfg_.batch, hipMemcpyHostToDevice, stream_));
       s.qp_dirty = false;
     }
     if (cfg_.crf > 0 && !qmap_given_) s.qp_dirty = true;  // k_rc_crf overwrites them
-    upload(f, B);
-    const int cur_i = f == 0 ? 0 : (fin_ + 1) % nrec_;
-    FrameSet cur = rec_[cur_i], prev = rec_[fin_];
+    const CodedPic& pic = plan_.pics[f];
+    const bool intra = pic.type == 2, bpic = pic.type == 0;
+    upload(pic.disp, B);
+    // a free DPB entry: none of the pictures this or a later picture still references
+    int e = -1;
+    for (int k = 0; k < ndpb_ && e < 0; ++k) {
+      const int d = dpb_[k].disp;
+      if (d < 0 || std::find(pic.rps.begin(), pic.rps.end(), d) == pic.rps.end()) e = k;
+    }
+    if (e < 0) throw std::runtime_error("no free DPB entry");
+    auto entry_of = [&](int disp) -> DpbEntry& {
+      for (int k = 0; k < ndpb_; ++k)
+        if (dpb_[k].disp == disp) return dpb_[k];
+      throw std::runtime_error("reference picture not in the DPB");
+    };
+    DpbEntry& cur_e = dpb_[e];
+    const FrameSet fin_set = cur_e.rec;
+    const FrameSet cur = seq_.sao ? deb_ : fin_set;  // SAO filters deb_ into the entry
+    const DecisionSet dec = bpic ? slot_dec_b(s) : dec0;
     // TV_SYNC_DEBUG=1: synchronise and check after every stage (fault isolation)
     auto stage = [&](const char* name) {
       if (!sync_debug_) return;
@@ -479,34 +540,44 @@ class Core {
                                  hipGetErrorString(e1 != hipSuccess ? e1 : e2));
     };
     stage("upload");
-    launch_quarter(src_, q_[f & 1], g_, B, stream_);  // lookahead plane (next frame's coarse ref)
-    // the previous frame's decisions still sit in its slot (reused only nslots_ frames later)
-    const MeBuffers me{q_[f & 1], q_[(f + 1) & 1], f ? slot_dec(slots_[(f - 1) % nslots_]).mv : nullptr, cmv_,
-                       ccost_};
-    if (f > 0) launch_coarse_me(me, g_, rc_, cfg_.qp, cfg_.range, B, stream_);
-    if (cfg_.crf > 0 && !qmap_given_) launch_rc_crf(q_[f & 1], ccost_, dec.qp, g_, cfg_.crf, f == 0, B, stream_);
-    if (f == 0) {  // fork onto the priority stream and join back
+    launch_quarter(src_, cur_e.q, g_, B, stream_);  // lookahead plane (coarse reference of later pictures)
+    // the previous coded picture's decisions still sit in its slot (reused only nslots_ frames later)
+    const int16_t* prev_mv = f ? slot_dec(slots_[(f - 1) % nslots_]).mv : nullptr;
+    const long cstride = (long)B * nctu_;
+    MeBuffers me[2];
+    for (int l = 0; l < 2; ++l) {
+      if (pic.ref[l] < 0) continue;
+      me[l] = MeBuffers{cur_e.q, entry_of(pic.ref[l]).q, prev_mv, cmv_ + l * cstride * 2, ccost_ + l * cstride};
+      launch_coarse_me(me[l], g_, rc_, cfg_.qp, cfg_.range, B, stream_);
+    }
+    if (cfg_.crf > 0 && !qmap_given_) launch_rc_crf(cur_e.q, ccost_, dec.qp, g_, cfg_.crf, intra, B, stream_);
+    if (intra) {  // fork onto the priority stream and join back
       HIP_OK(hipEventRecord(iev_[0], stream_));
       HIP_OK(hipStreamWaitEvent(istream_, iev_[0], 0));
       launch_intra_frame(src_, cur, dec, g_, rc_, B, istream_);
       HIP_OK(hipEventRecord(iev_[1], istream_));
       HIP_OK(hipStreamWaitEvent(stream_, iev_[1], 0));
-    } else launch_inter_frame(src_, prev, phase_, cur, dec, g_, rc_, cfg_.range, me, B, stream_);
-    stage(f == 0 ? "intra" : "inter");
+    } else if (!bpic) {
+      const DpbEntry& r0 = entry_of(pic.ref[0]);
+      launch_inter_frame(src_, r0.rec, r0.phase, cur, dec, g_, rc_, cfg_.range, me[0], B, stream_);
+    } else {
+      const DpbEntry& r0 = entry_of(pic.ref[0]);
+      const DpbEntry& r1 = entry_of(pic.ref[1]);
+      launch_inter_frame_b(src_, r0.rec, r0.phase, r1.rec, r1.phase, cur, dec, g_, rc_, cfg_.range, me[0], me[1],
+                           meout_, B, stream_);
+    }
+    stage(intra ? "intra" : "inter");
     launch_compact(dec, g_, slot_compact(s), B, stream_);
     stage("compact");
     if (seq_.deblock) launch_deblock(cur, dec, g_, B, stream_);
     stage("deblock");
-    int fin = cur_i;
-    if (seq_.sao) {  // deblocked `cur` -> SAO output in the ring's third buffer
-      fin = f == 0 ? 1 : 3 - cur_i - fin_;  // the ring index neither reference nor current
-      launch_sao(src_, cur, rec_[fin], carve(s.dev).sao, dec.qp, rc_, g_, B, stream_);
-    }
+    if (seq_.sao) launch_sao(src_, cur, fin_set, carve(s.dev).sao, dec.qp, rc_, g_, B, stream_);
     stage("sao");
-    fin_ = fin;
-    if (f + 1 < F) launch_phase_planes(rec_[fin], phase_, g_, B, stream_);  // reference of f+1
+    cur_e.disp = pic.disp;
+    if (pic.disp == F - 1) last_entry_ = e;
+    if (pic.referenced) launch_phase_planes(fin_set, cur_e.phase, g_, B, stream_);  // a later picture's reference
     stage("phase_planes");
-    launch_sse(src_, rec_[fin], g_, d_sse_, B, stream_);
+    launch_sse(src_, fin_set, g_, d_sse_, B, stream_);
     stage("sse");
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(s.ev, stream_));
@@ -530,7 +601,9 @@ class Core {
           try {
             Range r("engine.cabac_slice");
             const auto c0 = std::chrono::steady_clock::now();
-            write_slice(seq_, host_view(s, b), f, f == 0, slices_[b][f]);
+            const CodedPic& p = plan_.pics[f];
+            write_slice(seq_, host_view(s, b, seq_.mgop > 1 ? &refs_[f] : nullptr), p.disp, p.type == 2,
+                        slices_[b][f]);
             entropy_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(
                                std::chrono::steady_clock::now() - c0).count();
           } catch (const std::exception& e) {
@@ -597,13 +670,22 @@ class Core {
   int8_t* quni_ = nullptr;   // pinned: the sequence QP for every segment slot
   hipStream_t stream_{}, istream_{};
   hipEvent_t iev_[2]{};
-  FrameSet src_{}, rec_[3]{};
-  int nrec_ = 2, fin_ = 0;  // recon ring size; index of the last finished (reference) picture
+  static constexpr int kMaxDpb = 8;
+  struct DpbEntry {
+    FrameSet rec{};
+    uint8_t* phase = nullptr;
+    uint8_t* q = nullptr;
+    int disp = -1;  // display index of the picture held (-1: free)
+  };
+  FrameSet src_{}, deb_{};
+  DpbEntry dpb_[kMaxDpb];
+  int ndpb_ = 2, last_entry_ = 0;
+  GopPlan plan_;
+  std::vector<SliceRefs> refs_;
+  CtbMeOut* meout_ = nullptr;
   int16_t *coef_y_ = nullptr, *coef_u_ = nullptr, *coef_v_ = nullptr;
   unsigned long long* d_sse_ = nullptr;
-  uint8_t* phase_ = nullptr;
   void* count_scratch_ = nullptr;
-  uint8_t* q_[2]{};
   int16_t* cmv_ = nullptr;
   int* ccost_ = nullptr;
   long qsz_ = 0;
@@ -798,6 +880,20 @@ void* tv_engine_new(int width, int height, int qp, int batch, int gop, int range
     const int groups = ge ? std::max(1, atoi(ge)) : (batch >= 2 ? 2 : 1);
     if (crf < 0 || crf > 51) throw std::runtime_error("crf must be 0 (off) or 1..51");
     tv::gpu::EngineCfg c{width, height, qp, batch, gop, range, deblock, threads, device, max_merge, seed, groups, crf};
+    r = new tv::gpu::Engine(c);
+  });
+  return r;
+}
+// hierarchical-B engine (tv/gop.h): mgop = mini-GOP size (power of 2; 1 = I P P P)
+void* tv_engine_new_b(int width, int height, int qp, int batch, int gop, int range, int deblock, uint32_t seed,
+                      int threads, int device, int max_merge, int crf, int mgop) {
+  void* r = nullptr;
+  gguard([&] {
+    const char* ge = getenv("TV_ENGINE_GROUPS");
+    const int groups = ge ? std::max(1, atoi(ge)) : (batch >= 2 ? 2 : 1);
+    if (crf < 0 || crf > 51) throw std::runtime_error("crf must be 0 (off) or 1..51");
+    tv::gpu::EngineCfg c{width, height, qp, batch, gop, range, deblock, threads, device, max_merge, seed, groups, crf};
+    c.mgop = mgop;
     r = new tv::gpu::Engine(c);
   });
   return r;

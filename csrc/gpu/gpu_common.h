@@ -61,6 +61,9 @@ struct DecisionSet {
   int16_t* coef_y;
   int16_t* coef_u;
   int16_t* coef_v;
+  // B pictures only (nullptr otherwise): per-unit direction (1 L0, 2 L1, 3 bi), list-1 MVs
+  uint8_t* dir = nullptr;
+  int16_t* mv1 = nullptr;
 };
 
 // ---- wave-level data movement on the VALU (DPP) instead of LDS (ds_bpermute) ----------

@@ -52,6 +52,19 @@ void launch_rc_crf(const uint8_t* q, const int* ccost, int8_t* qp, const Geo& g,
 // fine motion search + P-frame reconstruction (after launch_coarse_me)
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
                         const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s);
+// One list's fine-search result for a CTB of a B picture: the 21 ME blocks' cost (SAD +
+// MV rate), rate part and vector (tv::me_ctb in the golden encoder).
+struct CtbMeOut {
+  int cost[21];
+  int pen[21];
+  int mv[21][2];
+};
+// B picture: fine search against both references (after both lists' launch_coarse_me), per
+// block the best of L0 / L1 / their average, the CU split, then bi-predictive reconstruction.
+// meout: scratch of 2 x B x nctu CtbMeOut.
+void launch_inter_frame_b(FrameSet src, FrameSet ref0, const uint8_t* phase0, FrameSet ref1, const uint8_t* phase1,
+                          FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, int range,
+                          const MeBuffers& me0, const MeBuffers& me1, CtbMeOut* meout, int B, hipStream_t s);
 // 16 quarter-pel phase planes (B x 16 x psz bytes) of the luma reference
 void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipStream_t s);
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int B, hipStream_t s);

@@ -161,7 +161,8 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
 
 __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                          DecisionSet dec, const int16_t* prev_mv, const int16_t* cmv,
-                                                         Geo g, const RcTables* rc, int range, int diag_stop) {
+                                                         Geo g, const RcTables* rc, int range, int diag_stop,
+                                                         CtbMeOut* bout) {
   const int tid = threadIdx.x;
   int ctu, b;
   xcd_ctb(ctu, b);
@@ -383,6 +384,17 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
     __syncthreads();
   }
 
+  // B picture: hand this list's 21 block results to k_bi_decide
+  if (bout) {
+    if (tid < 21) {
+      CtbMeOut& o = bout[(long)b * g.wc * g.hc + ctu];
+      o.cost[tid] = bcost[tid];
+      o.mv[tid][0] = bmv[tid][0];
+      o.mv[tid][1] = bmv[tid][1];
+      o.pen[tid] = pen.mv[me_pen_index(bmv[tid][0] - pmv[0], bmv[tid][1] - pmv[1])];
+    }
+    return;
+  }
   // ------------------------------- CU split decision ------------------------------------
   if (tid == 0) {
     const int ps = pen.split_inter;
@@ -415,6 +427,99 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
 }
 
 // ---------------------------------------------------------------------------------------
+// B picture pass A, second half (golden: tv::analyze_inter_b): the SAD of the 8-bit average
+// of both lists' predictions for all 21 ME blocks (one wave covers one 8x8 block or a 64-
+// sample quarter of a larger one: a wave sum, one LDS atomic), then per block the cheapest of
+// list 0, list 1 and bi (ties keep the earlier), then the bottom-up CU split.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_bi_decide(FrameSet src, const uint8_t* phase0, const uint8_t* phase1,
+                                                    const CtbMeOut* me0, const CtbMeOut* me1, DecisionSet dec, Geo g,
+                                                    const RcTables* rc) {
+  const int tid = threadIdx.x;
+  int ctu, b;
+  xcd_ctb(ctu, b);
+  const long o = (long)b * g.wc * g.hc + ctu;
+  const CtbMeOut& A = me0[o];
+  const CtbMeOut& Bm = me1[o];
+  const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
+  __shared__ int sad[21];
+  if (tid < 21) sad[tid] = 0;
+  __syncthreads();
+  const uint8_t* S = src.plane(0, b, g);
+  const uint8_t* p0b = phase0 + (long)b * 16 * g.psz;
+  const uint8_t* p1b = phase1 + (long)b * 16 * g.psz;
+  for (int i = tid; i < 3072; i += 256) {
+    int bi, x, y;
+    if (i < 1024) {
+      bi = i >> 6;
+      x = (bi & 3) * 8 + (i & 7);
+      y = (bi >> 2) * 8 + ((i >> 3) & 7);
+    } else if (i < 2048) {
+      const int j = i - 1024;
+      bi = 16 + (j >> 8);
+      x = ((bi - 16) & 1) * 16 + (j & 15);
+      y = ((bi - 16) >> 1) * 16 + ((j >> 4) & 15);
+    } else {
+      const int j = i - 2048;
+      bi = 20;
+      x = j & 31;
+      y = j >> 5;
+    }
+    const int m0x = A.mv[bi][0], m0y = A.mv[bi][1], m1x = Bm.mv[bi][0], m1y = Bm.mv[bi][1];
+    const int px = cx + x, py = cy + y;
+    const int a = phase_at(p0b + (long)((m0x & 3) + 4 * (m0y & 3)) * g.psz, g, px + (m0x >> 2), py + (m0y >> 2));
+    const int c = phase_at(p1b + (long)((m1x & 3) + 4 * (m1y & 3)) * g.psz, g, px + (m1x >> 2), py + (m1y >> 2));
+    const int d = tv_abs((int)S[(long)py * g.W + px] - ((a + c + 1) >> 1));
+    const int w = wave_sum(d);  // the wave's 64 samples belong to one block
+    if ((tid & 63) == 0) atomicAdd(&sad[bi], w);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const Penalties& pen = rc->pen[dec.qp[b]];
+    int cost[21], dir[21];
+    for (int bi = 0; bi < 21; ++bi) {
+      const int cb = sad[bi] + A.pen[bi] + Bm.pen[bi];
+      cost[bi] = A.cost[bi];
+      dir[bi] = 1;
+      if (Bm.cost[bi] < cost[bi]) {
+        cost[bi] = Bm.cost[bi];
+        dir[bi] = 2;
+      }
+      if (cb < cost[bi]) {
+        cost[bi] = cb;
+        dir[bi] = 3;
+      }
+    }
+    const int ps = pen.split_inter;
+    int sel[16], l2u[16], sum16 = 0;
+    for (int q = 0; q < 4; ++q) {
+      int sum8 = 0;
+      for (int r = 0; r < 4; ++r) sum8 += cost[me_blk8_of(q, r)] + ps;
+      const bool split = sum8 < cost[16 + q] + ps;
+      sum16 += split ? sum8 : cost[16 + q] + ps;
+      for (int r = 0; r < 4; ++r) {
+        const int k = ((q >> 1) * 2 + (r >> 1)) * 4 + (q & 1) * 2 + (r & 1);
+        sel[k] = split ? me_blk8_of(q, r) : 16 + q;
+        l2u[k] = split ? 3 : 4;
+      }
+    }
+    const bool whole = cost[20] + ps <= sum16;
+    for (int k = 0; k < 16; ++k) {
+      const long u = b * g.usz + (long)((cy >> 3) + (k >> 2)) * g.w8 + (cx >> 3) + (k & 3);
+      const int s = whole ? 20 : sel[k], d = dir[s];
+      dec.cu_log2[u] = (uint8_t)(whole ? 5 : l2u[k]);
+      dec.dir[u] = (uint8_t)d;
+      dec.mv[2 * u] = (int16_t)(d & 1 ? A.mv[s][0] : 0);
+      dec.mv[2 * u + 1] = (int16_t)(d & 1 ? A.mv[s][1] : 0);
+      dec.mv1[2 * u] = (int16_t)(d & 2 ? Bm.mv[s][0] : 0);
+      dec.mv1[2 * u + 1] = (int16_t)(d & 2 ? Bm.mv[s][1] : 0);
+      dec.intra[u] = 0;
+      dec.ipm[u] = 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // P-frame pass B on matrix cores: every TB of the CTB is coded by 16x16 MFMA tiles.
 //
 // A P frame has only inter CUs, so all predictions and residuals of the CTB exist up front
@@ -437,6 +542,8 @@ struct PReconLds {
   uint8_t predY[32 * 32];
   uint8_t predC[2][16 * 16];
   int mv[16][2];              // per 8x8 unit (raster within the CTB)
+  int mv1[16][2];             // B pictures: list-1 vectors and directions
+  int dir[16];
   int nz[48], sa[48], dc[48];  // per-TB statistics: luma 0..15, Cb 16..31, Cr 32..47
   int qtype[4];               // luma quadrant: 0 part of a 32x32 CU, 1 16x16 CU, 2 four 8x8 CUs
   int tzero[8];               // stage-3/4 tile t has no surviving level: reconstruction = prediction
@@ -466,7 +573,8 @@ __device__ __forceinline__ bool pr_zeroed(const PReconLds& L, int id) {
 }
 
 __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
-                                                     FrameSet rec, DecisionSet dec, Geo g, int tile_skip) {
+                                                     FrameSet rec, DecisionSet dec, Geo g, int tile_skip,
+                                                     FrameSet ref1, const uint8_t* phase1) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   int ctu, b;
   xcd_ctb(ctu, b);
@@ -480,6 +588,9 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
     const long u = ub + (long)((cy >> 3) + (tid >> 2)) * g.w8 + (cx >> 3) + (tid & 3);
     L.mv[tid][0] = dec.mv[2 * u];
     L.mv[tid][1] = dec.mv[2 * u + 1];
+    L.dir[tid] = dec.dir ? dec.dir[u] : 1;
+    L.mv1[tid][0] = dec.mv1 ? dec.mv1[2 * u] : 0;
+    L.mv1[tid][1] = dec.mv1 ? dec.mv1[2 * u + 1] : 0;
   }
   if (tid < 48) L.nz[tid] = L.sa[tid] = L.dc[tid] = 0;
   if (tid < 4) {
@@ -491,20 +602,43 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
   {
     const uint8_t* S = src.plane(0, b, g);
     const uint8_t* ph = phase + (long)b * 16 * g.psz;
+    const uint8_t* ph1 = phase1 ? phase1 + (long)b * 16 * g.psz : nullptr;
     for (int i = tid; i < 1024; i += 256) {
       const int x = i & 31, y = i >> 5, un = (y >> 3) * 4 + (x >> 3);
-      const int mvx = L.mv[un][0], mvy = L.mv[un][1];
-      const uint8_t* P = ph + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
-      const int p = phase_at(P, g, cx + x + (mvx >> 2), cy + y + (mvy >> 2));
+      const int d = L.dir[un];
+      int p;
+      if (d != 3) {  // uni-prediction: the reference's phase plane holds the final samples
+        const int mvx = d == 1 ? L.mv[un][0] : L.mv1[un][0], mvy = d == 1 ? L.mv[un][1] : L.mv1[un][1];
+        const uint8_t* P = (d == 1 ? ph : ph1) + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
+        p = phase_at(P, g, cx + x + (mvx >> 2), cy + y + (mvy >> 2));
+      } else {  // bi: both lists' 14-bit intermediate samples (8.5.3.3.4.2)
+        const int m0x = L.mv[un][0], m0y = L.mv[un][1], m1x = L.mv1[un][0], m1y = L.mv1[un][1];
+        const int a = mc_luma_inter(ref.plane(0, b, g), g.W, g.W, g.H, cx + x + (m0x >> 2), cy + y + (m0y >> 2), m0x & 3,
+                                    m0y & 3);
+        const int c = mc_luma_inter(ref1.plane(0, b, g), g.W, g.W, g.H, cx + x + (m1x >> 2), cy + y + (m1y >> 2),
+                                    m1x & 3, m1y & 3);
+        p = bipred_sample(a, c);
+      }
       L.predY[i] = (uint8_t)p;
       L.resY[i] = (int16_t)((int)S[(long)(cy + y) * g.W + cx + x] - p);
     }
     for (int i = tid; i < 512; i += 256) {
       const int pl = i >> 8, x = i & 15, y = (i >> 4) & 15, un = (y >> 2) * 4 + (x >> 2);
-      const int mvx = L.mv[un][0], mvy = L.mv[un][1];
-      const uint8_t* Rf = ref.plane(1 + pl, b, g);
+      const int d = L.dir[un];
       const int gx = (cx >> 1) + x, gy = (cy >> 1) + y;
-      const int p = mc_chroma_sample(Rf, Wc, Wc, Hc, gx + (mvx >> 3), gy + (mvy >> 3), mvx & 7, mvy & 7);
+      int p;
+      if (d != 3) {
+        const int mvx = d == 1 ? L.mv[un][0] : L.mv1[un][0], mvy = d == 1 ? L.mv[un][1] : L.mv1[un][1];
+        const uint8_t* Rf = (d == 1 ? ref : ref1).plane(1 + pl, b, g);
+        p = mc_chroma_sample(Rf, Wc, Wc, Hc, gx + (mvx >> 3), gy + (mvy >> 3), mvx & 7, mvy & 7);
+      } else {
+        const int m0x = L.mv[un][0], m0y = L.mv[un][1], m1x = L.mv1[un][0], m1y = L.mv1[un][1];
+        const int a = mc_chroma_inter(ref.plane(1 + pl, b, g), Wc, Wc, Hc, gx + (m0x >> 3), gy + (m0y >> 3), m0x & 7,
+                                      m0y & 7);
+        const int c = mc_chroma_inter(ref1.plane(1 + pl, b, g), Wc, Wc, Hc, gx + (m1x >> 3), gy + (m1y >> 3), m1x & 7,
+                                      m1y & 7);
+        p = bipred_sample(a, c);
+      }
       L.predC[pl][y * 16 + x] = (uint8_t)p;
       L.resC[pl][y * 16 + x] = (int16_t)((int)src.plane(1 + pl, b, g)[(long)gy * Wc + gx] - p);
     }
@@ -775,6 +909,16 @@ void launch_rc_crf(const uint8_t* q, const int* ccost, int8_t* qp, const Geo& g,
   k_rc_crf<<<B, 256, 0, s>>>(q, ccost, qp, g, crf, intra ? 1 : 0);
 }
 
+// TV_RECON_TILE_SKIP=0 runs the inverse transform on all-zero tiles too (same output; kept
+// as a same-box A/B switch for the skip)
+static int recon_tile_skip() {
+  static const int v = [] {
+    const char* e = std::getenv("TV_RECON_TILE_SKIP");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
                         const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s) {
   static const int diag_stop = [] {
@@ -782,14 +926,20 @@ void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameS
     return e ? std::atoi(e) : 0;
   }();
   k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range,
-                                                         diag_stop);
-  // TV_RECON_TILE_SKIP=0 runs the inverse transform on all-zero tiles too (same output;
-  // kept as a same-box A/B switch for the skip)
-  static const int tile_skip = [] {
-    const char* e = std::getenv("TV_RECON_TILE_SKIP");
-    return e ? std::atoi(e) : 1;
-  }();
-  k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, tile_skip);
+                                                         diag_stop, nullptr);
+  k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, recon_tile_skip(), FrameSet{},
+                                                     nullptr);
+}
+
+void launch_inter_frame_b(FrameSet src, FrameSet ref0, const uint8_t* phase0, FrameSet ref1, const uint8_t* phase1,
+                          FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, int range,
+                          const MeBuffers& me0, const MeBuffers& me1, CtbMeOut* meout, int B, hipStream_t s) {
+  const dim3 grid(g.wc * g.hc, B);
+  CtbMeOut* o1 = meout + (long)B * g.wc * g.hc;
+  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref0, phase0, dec, me0.prev_mv, me0.cmv, g, rc, range, 0, meout);
+  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref1, phase1, dec, me1.prev_mv, me1.cmv, g, rc, range, 0, o1);
+  k_bi_decide<<<grid, 256, 0, s>>>(src, phase0, phase1, meout, o1, dec, g, rc);
+  k_inter_recon<<<grid, 256, 0, s>>>(src, ref0, phase0, rec, dec, g, recon_tile_skip(), ref1, phase1);
 }
 
 }  // namespace gpu

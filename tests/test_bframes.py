@@ -96,3 +96,47 @@ def test_bd_rate_helper():
     r, p = [1000, 600, 360, 220], [45.0, 42.0, 39.0, 36.0]
     assert abs(bd_rate(r, p, r, p)) < 1e-9
     assert abs(bd_rate(r, p, [x * 0.9 for x in r], p) + 10.0) < 1e-6
+
+
+def _gpu_engine(**kw):
+    from thinvids_amd.models.gpu_engine import GpuEngine
+    return GpuEngine(**kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,m,gop,sao,seed", [(192, 128, 4, 9, False, 5), (192, 128, 8, 17, True, 5),
+                                                (320, 192, 8, 12, True, 7 | 0x80000000), (160, 90, 2, 5, False, 3)])
+def test_gpu_bframes_bit_exact(w, h, m, gop, sao, seed):
+    """The GPU engine's hierarchical-B streams (per-list fine search, bi decision, exact
+    bi-prediction, DPB of phase planes) equal the golden encoder's byte for byte."""
+    rng = 32
+    eng = _gpu_engine(width=w, height=h, qp=27, batch=2, gop=gop, search_range=rng, sao=sao, seed=seed, bframes=m)
+    segs = eng.encode_synthetic([0, 10])
+    for b, start in enumerate([0, 10]):
+        frames = [hevc.synth_frame(seed, start + f, w, h) for f in range(gop)]
+        cpu_bs, recons = hevc.encode_sequence_cpu(frames, qp=27, sao=sao, search_range=rng, bframes=m)
+        assert segs[b] == cpu_bs, f"segment {b}: GPU bitstream differs from the golden encoder"
+        d = hevc.decode(segs[b])
+        assert len(d.coded_frames) == gop
+        gy, gu, _ = eng.last_recon(b)  # last display frame
+        np.testing.assert_array_equal(d.coded_frames[-1][0], gy)
+        np.testing.assert_array_equal(d.coded_frames[-1][1], gu)
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_bframes_qp_map_and_benchmark_geometry():
+    """1080p, search range 64, two stream groups, SAO, a per-frame base QP map (display
+    order) under the layer offsets: bit-exact with the golden encoder."""
+    w, h, gop, m = 1920, 1080, 9, 8
+    eng = _gpu_engine(width=w, height=h, qp=27, batch=4, gop=gop, search_range=64, sao=True, seed=3, bframes=m)
+    qmap = np.array([[27, 29, 25, 27, 30, 26, 27, 28, 27]] * 4, np.int8)
+    qmap[2] += 2
+    starts = [0, 100, 200, 300]
+    segs = eng.encode_synthetic(starts, qp=qmap)
+    for b in (2,):
+        frames = [hevc.synth_frame(3, starts[b] + f, w, h) for f in range(gop)]
+        cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, sao=True, search_range=64, bframes=m,
+                                             frame_qps=list(qmap[b]))
+        assert segs[b] == cpu_bs
+    eng.close()

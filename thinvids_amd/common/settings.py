@@ -41,6 +41,7 @@ DEFAULT_SETTINGS: dict[str, str] = {
     "tv_search_range": "64",
     "tv_deblock": "1",
     "tv_sao": "1",
+    "tv_bframes": "1",  # hierarchical-B mini-GOP (1 = I P P P; 2/4/8/16: B pictures, tv/gop.h)
     "tv_segment_frames": "0",  # 0 = derive from target_segment_mb
     "tv_bitrate_kbps": "0",  # tv_rc=2pass / abr target
     "tv_vbv_maxrate_kbps": "0",  # tv_rc=abr: VBV peak rate (0: no VBV)

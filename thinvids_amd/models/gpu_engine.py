@@ -23,6 +23,8 @@ def _lib():
         lib.tv_gpu_device_count.restype = C.c_int
         lib.tv_engine_new.restype = vp
         lib.tv_engine_new.argtypes = [C.c_int] * 7 + [C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int]
+        lib.tv_engine_new_b.restype = vp
+        lib.tv_engine_new_b.argtypes = [C.c_int] * 7 + [C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
         lib.tv_engine_free.argtypes = [vp]
         lib.tv_engine_encode_synth.restype = C.c_int
         lib.tv_engine_encode_synth.argtypes = [vp, C.POINTER(C.c_int), C.c_int, C.c_int, vp]
@@ -84,7 +86,10 @@ class GpuEngine:
     def __init__(self, width: int, height: int, qp: int = 27, batch: int = 8, gop: int = 16,
                  search_range: int = 64, deblock: bool = True, sao: bool = False, seed: int = 1,
                  threads: int | None = None,
-                 device: int = 0, max_merge: int = 5, crf: int = 0):
+                 device: int = 0, max_merge: int = 5, crf: int = 0, bframes: int = 1):
+        """`bframes` > 1: hierarchical-B mini-GOPs of that size (power of 2, tv/gop.h); the
+        segments' streams are then in coding order (the decoder reorders by POC) and
+        :meth:`last_recon` returns the last DISPLAY frame."""
         self.lib = _lib()
         self.width, self.height, self.qp = width, height, qp
         self.batch, self.gop = batch, gop
@@ -92,8 +97,9 @@ class GpuEngine:
         self.threads = threads or default_threads()
         self.sao = sao
         self.device = device
-        self.h = self.lib.tv_engine_new(width, height, qp, batch, gop, search_range, int(deblock) | (2 if sao else 0),
-                                        seed & 0xFFFFFFFF, self.threads, device, max_merge, int(crf))
+        self.bframes = int(bframes)
+        self.h = self.lib.tv_engine_new_b(width, height, qp, batch, gop, search_range, int(deblock) | (2 if sao else 0),
+                                          seed & 0xFFFFFFFF, self.threads, device, max_merge, int(crf), self.bframes)
         if not self.h:
             raise RuntimeError("GPU engine init failed: " + self.lib.tv_gpu_last_error().decode())
 
