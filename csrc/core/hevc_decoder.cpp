@@ -697,6 +697,58 @@ StreamInfo probe_annexb(const uint8_t* data, size_t n) {
   return info;
 }
 
+std::vector<int> display_offsets(const uint8_t* data, size_t n) {
+  // slice headers only: POC per picture (IDR resets it), then each coded video sequence's
+  // pictures ranked by POC
+  std::vector<int> poc, cvs_of;
+  int log2_lsb = 8, prev = 0, cvs = -1;
+  for (const auto& nal : split_annexb(data, n)) {
+    if (nal.size < 3) continue;
+    const int t = nal.type();
+    if (t == NAL_SPS) {
+      std::vector<uint8_t> rbsp = unescape_rbsp(nal.data + 2, nal.size - 2);
+      BitReader br(rbsp.data(), rbsp.size());
+      log2_lsb = parse_sps(br).log2_poc_lsb;
+      continue;
+    }
+    if (t > 21 || !(nal.data[2] & 0x80)) continue;
+    const bool idr = t == NAL_IDR_W_RADL || t == NAL_IDR_N_LP;
+    int p = 0;
+    if (idr) {
+      ++cvs;
+    } else {
+      std::vector<uint8_t> rbsp = unescape_rbsp(nal.data + 2, std::min<size_t>(nal.size - 2, 32));
+      BitReader br(rbsp.data(), rbsp.size());
+      br.u(1);                   // first_slice_segment_in_pic_flag
+      if (t >= 16) br.u(1);      // no_output_of_prior_pics_flag (IRAP)
+      br.ue();                   // slice_pic_parameter_set_id
+      br.ue();                   // slice_type (no extra header bits / output flag in our PPS)
+      const int lsb = (int)br.u(log2_lsb), max_lsb = 1 << log2_lsb;
+      const int prev_lsb = prev & (max_lsb - 1);
+      int msb = prev - prev_lsb;
+      if (lsb < prev_lsb && prev_lsb - lsb >= max_lsb / 2) msb += max_lsb;
+      else if (lsb > prev_lsb && lsb - prev_lsb > max_lsb / 2) msb -= max_lsb;
+      p = msb + lsb;
+      if (cvs < 0) cvs = 0;
+    }
+    prev = p;
+    poc.push_back(p);
+    cvs_of.push_back(cvs);
+  }
+  std::vector<int> off(poc.size(), 0);
+  for (size_t a = 0; a < poc.size();) {
+    size_t b = a;
+    while (b < poc.size() && cvs_of[b] == cvs_of[a]) ++b;
+    for (size_t i = a; i < b; ++i) {
+      int rank = 0;
+      for (size_t j = a; j < b; ++j) rank += poc[j] < poc[i] || (poc[j] == poc[i] && j < i);
+      off[i] = (int)(a + rank) - (int)i;
+    }
+    a = b;
+  }
+  return off;
+}
+
 void HevcDecoder::decode(const uint8_t* data, size_t n) { decode_range(data, n, 0, -1); }
 
 void HevcDecoder::decode_range(const uint8_t* data, size_t n, int first, int count) {

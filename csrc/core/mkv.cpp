@@ -97,9 +97,10 @@ const char* codec_id(const SideTrack& t) {
 
 // one block to place: track 0 = video sample `idx`, k = side track k-1 sample `idx`
 struct Ev {
-  int64_t ms;
+  int64_t ms;  // ordering time (video: decode time)
   int track;
   int64_t idx;
+  int64_t pts = 0;  // video: presentation time (ms)
 };
 
 // SeekHead with fixed-width positions, so it can be rewritten in place once Cues is placed
@@ -175,10 +176,13 @@ uint64_t write_mkv(const MuxPlan& P, int width, int height, int fps_num, int fps
   // ---- events in presentation order (video first on ties)
   std::vector<Ev> ev;
   ev.reserve(P.samples.size());
-  for (size_t i = 0; i < P.samples.size(); ++i) ev.push_back({video_ms((int64_t)i), 0, (int64_t)i});
+  // video blocks stay in decoding order (sorted by decode time) but carry presentation
+  // timestamps (B frames: the sample's composition offset)
+  for (size_t i = 0; i < P.samples.size(); ++i)
+    ev.push_back({video_ms((int64_t)i), 0, (int64_t)i, video_ms((int64_t)i + P.samples[i].cto)});
   for (int k = 0; k < ntracks; ++k)
     for (int64_t i = 0; i < tracks[k].nsamples; ++i)
-      ev.push_back({(int64_t)((__int128)tracks[k].pts[i] * 1000 / tracks[k].timescale), k + 1, i});
+      ev.push_back({(int64_t)((__int128)tracks[k].pts[i] * 1000 / tracks[k].timescale), k + 1, i, 0});
   std::stable_sort(ev.begin(), ev.end(), [](const Ev& a, const Ev& b) {
     return a.ms < b.ms || (a.ms == b.ms && a.track < b.track);
   });
@@ -251,7 +255,7 @@ uint64_t write_mkv(const MuxPlan& P, int width, int height, int fps_num, int fps
       }
       payload.clear();
       payload.push_back((uint8_t)(0x80 | (e.track + 1)));  // track number vint (< 127 tracks)
-      const int64_t rel = e.ms - cl_ms;
+      const int64_t rel = (e.track == 0 ? e.pts : e.ms) - cl_ms;
       payload.push_back((uint8_t)(rel >> 8));
       payload.push_back((uint8_t)rel);
       const SideTrack* t = e.track ? &tracks[e.track - 1] : nullptr;

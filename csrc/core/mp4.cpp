@@ -160,6 +160,20 @@ struct TrakTables {
   std::vector<uint32_t> sync;          // 1-based; empty = every sample is a sync sample
   bool has_stss = false;
   uint64_t media_dur = 0;
+  // B frames: composition offsets (count, offset) and the edit list's media_time that maps
+  // the first displayed frame to time 0 (offsets are shifted to be non-negative)
+  std::vector<std::pair<uint32_t, uint32_t>> ctts;
+  int64_t edit_media_time = -1;
+  void ctts_from(const std::vector<int>& cto, uint32_t delta) {
+    int mn = 0;
+    for (int c : cto) mn = std::min(mn, c);
+    for (int c : cto) {
+      const uint32_t o = (uint32_t)(c - mn) * delta;
+      if (!ctts.empty() && ctts.back().second == o) ++ctts.back().first;
+      else ctts.push_back({1, o});
+    }
+    edit_media_time = (int64_t)(-mn) * delta;
+  }
   void delta(uint32_t d) {
     if (!stts.empty() && stts.back().second == d) ++stts.back().first;
     else stts.push_back({1, d});
@@ -230,6 +244,15 @@ std::vector<uint8_t> stbl_box(const std::vector<uint8_t>& entry, const TrakTable
     else co.u32((uint32_t)o);
   }
   std::vector<uint8_t> parts = cat({fullbox("stsd", 0, 0, stsd.b), fullbox("stts", 0, 0, stts.b)});
+  if (!T.ctts.empty()) {
+    Box ctts;
+    ctts.u32((uint32_t)T.ctts.size());
+    for (auto [c, o] : T.ctts) {
+      ctts.u32(c);
+      ctts.u32(o);
+    }
+    parts = cat({parts, fullbox("ctts", 0, 0, ctts.b)});
+  }
   if (T.has_stss) {
     Box stss;
     stss.u32((uint32_t)T.sync.size());
@@ -294,6 +317,15 @@ std::vector<uint8_t> trak_box(const TrakInfo& I, const TrakTables& T, bool large
   matrix(tkhd);
   tkhd.u32((uint32_t)I.width << 16);
   tkhd.u32((uint32_t)I.height << 16);
+  if (T.edit_media_time >= 0) {  // edts/elst: the presentation starts at the first display frame
+    Box elst;
+    elst.u32(1);
+    elst.u32((uint32_t)dur_ms);  // segment_duration (movie timescale, ms)
+    elst.u32((uint32_t)T.edit_media_time);
+    elst.u32(0x00010000);        // media_rate 1.0
+    const auto edts = box("edts", fullbox("elst", 0, 0, elst.b));
+    return box("trak", cat({fullbox("tkhd", 0, I.enabled ? 3 : 2, tkhd.b), edts, mdia}));
+  }
   return box("trak", cat({fullbox("tkhd", 0, I.enabled ? 3 : 2, tkhd.b), mdia}));
 }
 
@@ -373,6 +405,7 @@ MuxPlan plan_mux(const uint8_t* const* segs, const size_t* sizes, int nseg) {
   MuxPlan P;
   std::vector<NalView> pending_ps;
   for (int k = 0; k < nseg; ++k) {
+    const size_t first = P.samples.size();
     for (const auto& nal : split_annexb(segs[k], sizes[k])) {
       const int t = nal.type();
       if (t == NAL_VPS || t == NAL_SPS || t == NAL_PPS) {
@@ -390,6 +423,13 @@ MuxPlan plan_mux(const uint8_t* const* segs, const size_t* sizes, int nseg) {
       s.nals.push_back(nal);
       pending_ps.clear();
       P.samples.push_back(std::move(s));
+    }
+    // composition offsets from the slice POCs (hierarchical-B segments are reordered)
+    const std::vector<int> off = display_offsets(segs[k], sizes[k]);
+    if (off.size() != P.samples.size() - first) throw std::runtime_error("mux: picture count mismatch");
+    for (size_t i = 0; i < off.size(); ++i) {
+      P.samples[first + i].cto = off[i];
+      P.reordered = P.reordered || off[i] != 0;
     }
   }
   if (P.sps.empty() || P.pps.empty() || P.vps.empty()) throw std::runtime_error("mux: missing parameter sets");
@@ -508,6 +548,11 @@ uint64_t write_mp4(const MuxPlan& P, int width, int height, int fps_num, int fps
       V.sizes.push_back(P.samples[i].size);
       V.delta(vdelta);
       if (P.samples[i].sync) V.sync.push_back((uint32_t)i + 1);
+    }
+    if (P.reordered) {
+      std::vector<int> cto;
+      for (const auto& smp : P.samples) cto.push_back(smp.cto);
+      V.ctts_from(cto, vdelta);
     }
     const int64_t per = ntracks ? std::max<int64_t>(1, (fps_num + fps_den - 1) / fps_den) : (int64_t)V.nsamples;
     for (int64_t f = 0; f < (int64_t)V.nsamples; f += per) {
@@ -677,7 +722,7 @@ class Mp4Stream {
       : path_(path), w_(width), h_(height), fn_(fps_num), fd_(fps_den), max_(max_samples) {
     if (fps_num <= 0 || fps_den <= 0) throw std::runtime_error("mux stream: bad frame rate");
     if (!max_samples) throw std::runtime_error("mux stream: no samples expected");
-    reserve_ = 8192 + 12 * max_samples;
+    reserve_ = 8192 + 20 * max_samples;  // stsz + stss + ctts entries
     f_ = std::fopen(path, "wb");
     if (!f_) throw std::runtime_error(std::string("mux stream: cannot open ") + path);
     std::vector<uint8_t> z(reserve_, 0);
@@ -706,6 +751,8 @@ class Mp4Stream {
     for (const auto& smp : P.samples) {
       muxi::append_sample(smp, buf_);
       sizes_.push_back(smp.size);
+      cto_.push_back(smp.cto);
+      reordered_ = reordered_ || smp.cto != 0;
       if (smp.sync) sync_.push_back((uint32_t)sizes_.size());
     }
     if (std::fwrite(buf_.data(), 1, buf_.size(), f_) != buf_.size()) fail("write failed");
@@ -722,6 +769,7 @@ class Mp4Stream {
     V.sizes = sizes_;
     V.sync = sync_;
     for (size_t i = 0; i < sizes_.size(); ++i) V.delta((uint32_t)fd_ * 1000u);
+    if (reordered_) V.ctts_from(cto_, (uint32_t)fd_ * 1000u);
     V.chunk_n = {(uint32_t)sizes_.size()};
     V.chunk_off = {reserve_};
     I[0] = {1, "vide", "VideoHandler", (uint32_t)fn_ * 1000u, pack_lang(nullptr), true, 0, 0, w_, h_,
@@ -760,6 +808,8 @@ class Mp4Stream {
   MuxPlan head_;
   bool have_ = false;
   std::vector<uint32_t> sizes_, sync_;
+  std::vector<int> cto_;
+  bool reordered_ = false;
   std::vector<uint8_t> buf_;
 };
 

@@ -21,6 +21,7 @@ struct Sample {
   uint32_t size = 0;  // length-prefixed bytes (HEVC) / raw OBU bytes (AV1)
   bool sync = false;
   bool raw = false;   // AV1: the single view is the temporal unit's OBUs, written as is
+  int cto = 0;        // composition offset in frames: display index - decoding index (B frames)
 };
 
 enum MuxCodec : int { MUX_HEVC = 0, MUX_AV1 = 1 };
@@ -32,6 +33,7 @@ struct MuxPlan {
   bool ps_consistent = true;
   std::vector<Sample> samples;
   uint64_t mdat_payload = 0;
+  bool reordered = false;  // some sample has cto != 0 (ctts + edit list / Matroska PTS)
 };
 
 // Scan the segments (in order) into samples; no payload bytes are copied.  Annex-B HEVC,

@@ -429,6 +429,10 @@ struct StreamInfo {
   int width = 0, height = 0, coded_w = 0, coded_h = 0, pictures = 0, idrs = 0;
 };
 StreamInfo probe_annexb(const uint8_t* data, size_t n);
+// Composition offset of every picture (decoding order): display index - decoding index,
+// from the slice headers' POCs ranked within each coded video sequence (0 everywhere for
+// I P P P streams; hierarchical-B streams reorder).  Used by the MP4 / Matroska muxers.
+std::vector<int> display_offsets(const uint8_t* data, size_t n);
 
 // ------------------------------------- containers ---------------------------------------
 // Build an ISO-BMFF (.mp4, 'hvc1') file from an Annex-B HEVC stream.  Returns bytes.

@@ -140,3 +140,65 @@ def test_gpu_bframes_qp_map_and_benchmark_geometry():
                                              frame_qps=list(qmap[b]))
         assert segs[b] == cpu_bs
     eng.close()
+
+
+def _box_payload(data: bytes, path: list[str]):
+    """Payload of the first box at `path` (container boxes descended in order)."""
+    import struct
+
+    def find(buf, typ):
+        o = 0
+        while o + 8 <= len(buf):
+            n, t = struct.unpack(">I4s", buf[o:o + 8])
+            if t.decode() == typ:
+                return buf[o + 8:o + n]
+            o += n
+        return None
+
+    b = data
+    for t in path:
+        b = find(b, t)
+        if b is None:
+            return None
+    return b
+
+
+def test_bframes_mp4_ctts_and_mkv_pts(tmp_path):
+    """Containers carry the reordering: MP4 gets ctts (composition offsets, non-negative)
+    plus an edit list starting the presentation at the first display frame; Matroska blocks
+    stay in decoding order with presentation timestamps; both demux to the same pictures."""
+    import struct
+
+    from thinvids_amd.models import streams
+
+    frames = [hevc.synth_frame(2, t, 96, 64) for t in range(9)]
+    bs, _ = hevc.encode_sequence_cpu(frames, qp=30, bframes=4, search_range=16)
+    mp4 = hevc.mux_mp4(bs, 96, 64, 25, 1)
+    ctts = _box_payload(mp4, ["moov", "trak", "mdia", "minf", "stbl", "ctts"])
+    assert ctts is not None
+    n = struct.unpack(">I", ctts[4:8])[0]
+    offs = []
+    for k in range(n):
+        c, o = struct.unpack(">II", ctts[8 + 8 * k:16 + 8 * k])
+        offs += [o] * c
+    delta = 1000  # fps_den * 1000
+    plan = hevc.gop_plan(9, 4)
+    d0 = -min(d - i for i, d in enumerate(plan["disp"]))
+    assert offs == [(d - i + d0) * delta for i, d in enumerate(plan["disp"])]
+    elst = _box_payload(mp4, ["moov", "trak", "edts", "elst"])
+    assert struct.unpack(">I", elst[12:16])[0] == d0 * delta
+    dm = hevc.demux_mp4(mp4)
+    assert dm["frames"] == 9
+    a, b = hevc.decode(bs), hevc.decode(dm["annexb"])
+    for x, y in zip(a.frames, b.frames):
+        np.testing.assert_array_equal(x[0], y[0])
+    # IPPP streams keep the plain layout
+    ip, _ = hevc.encode_sequence_cpu(frames, qp=30, search_range=16)
+    assert _box_payload(hevc.mux_mp4(ip, 96, 64, 25, 1), ["moov", "trak", "edts"]) is None
+    out = str(tmp_path / "b.mkv")
+    streams.mux([bs], 96, 64, 25, 1, out, [], streams.CONTAINER_MKV)
+    v = streams.mkv_video(streams.mkv_read(out))
+    assert [blk[0] for blk in v.blocks] == [40 * d for d in plan["disp"]]
+    annexb, _, _ = streams.mkv_hevc_annexb(out)
+    for x, y in zip(a.frames, hevc.decode(annexb).frames):
+        np.testing.assert_array_equal(x[0], y[0])
