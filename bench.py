@@ -545,8 +545,6 @@ def main() -> None:
     # engine splits them into two stream groups one frame apart (measured on MI355X:
     # 1080p 32 -> 48 segments +3 %, 4K 16 -> 24 segments +9 %; profiles/README.md)
     batch = args.batch or (48 if args.res in ("1080p", "720p", "360p") else 24)
-    if args.bframes > 1 and args.kbps > 0:
-        raise SystemExit("--kbps with --bframes > 1 is not supported yet")
     eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=args.sao,
                     seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes)
     post = _PostQueue(local)

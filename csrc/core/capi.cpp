@@ -242,6 +242,17 @@ int tv_decoder_decode_range(void* d, const uint8_t* data, size_t n, int first, i
   return guard([&] { static_cast<HevcDecoder*>(d)->decode_range(data, n, first, count); });
 }
 // header-only probe: geometry + picture count, no slice decoding
+// display index - decoding index of every picture (hierarchical-B reordering); returns the
+// picture count (out receives at most cap values)
+int tv_hevc_display_offsets(const uint8_t* data, size_t n, int* out, int cap) {
+  int r = -1;
+  guard([&] {
+    const std::vector<int> off = display_offsets(data, n);
+    for (int i = 0; i < (int)off.size() && i < cap; ++i) out[i] = off[i];
+    r = (int)off.size();
+  });
+  return r;
+}
 int tv_hevc_probe(const uint8_t* data, size_t n, int* w, int* h, int* pictures, int* idrs) {
   return guard([&] {
     const StreamInfo s = probe_annexb(data, n);

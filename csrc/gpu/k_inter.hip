@@ -432,6 +432,21 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
 // sample quarter of a larger one: a wave sum, one LDS atomic), then per block the cheapest of
 // list 0, list 1 and bi (ties keep the earlier), then the bottom-up CU split.
 // ---------------------------------------------------------------------------------------
+// 4 phase-plane samples at (x .. x+3, y), any alignment: two dword loads + v_alignbyte
+// inside the padded plane, per-byte clamped loads at the border
+__device__ __forceinline__ uint32_t phase4(const uint8_t* P, const Geo& g, int x, int y) {
+  const int a = x & ~3;
+  if (x >= -8 && a + 7 <= g.W + 7 && y >= -8 && y <= g.H + 7) {
+    const uint8_t* row = P + (long)(y + 8) * g.pw16 + a + 8;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row), w1 = *reinterpret_cast<const uint32_t*>(row + 4);
+    return __builtin_amdgcn_alignbyte(w1, w0, x & 3);
+  }
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v |= (uint32_t)phase_at(P, g, x + k, y) << (8 * k);
+  return v;
+}
+
 __global__ void __launch_bounds__(256) k_bi_decide(FrameSet src, const uint8_t* phase0, const uint8_t* phase1,
                                                     const CtbMeOut* me0, const CtbMeOut* me1, DecisionSet dec, Geo g,
                                                     const RcTables* rc) {
@@ -442,80 +457,90 @@ __global__ void __launch_bounds__(256) k_bi_decide(FrameSet src, const uint8_t* 
   const CtbMeOut& A = me0[o];
   const CtbMeOut& Bm = me1[o];
   const int cx = (ctu % g.wc) * 32, cy = (ctu / g.wc) * 32;
+  __shared__ uint32_t s32[256];  // the source CTB, 8 words per row
   __shared__ int sad[21];
-  if (tid < 21) sad[tid] = 0;
-  __syncthreads();
+  __shared__ int mvs[2][21][2];
   const uint8_t* S = src.plane(0, b, g);
-  const uint8_t* p0b = phase0 + (long)b * 16 * g.psz;
-  const uint8_t* p1b = phase1 + (long)b * 16 * g.psz;
-  for (int i = tid; i < 3072; i += 256) {
-    int bi, x, y;
-    if (i < 1024) {
-      bi = i >> 6;
-      x = (bi & 3) * 8 + (i & 7);
-      y = (bi >> 2) * 8 + ((i >> 3) & 7);
-    } else if (i < 2048) {
-      const int j = i - 1024;
-      bi = 16 + (j >> 8);
-      x = ((bi - 16) & 1) * 16 + (j & 15);
-      y = ((bi - 16) >> 1) * 16 + ((j >> 4) & 15);
-    } else {
-      const int j = i - 2048;
-      bi = 20;
-      x = j & 31;
-      y = j >> 5;
-    }
-    const int m0x = A.mv[bi][0], m0y = A.mv[bi][1], m1x = Bm.mv[bi][0], m1y = Bm.mv[bi][1];
-    const int px = cx + x, py = cy + y;
-    const int a = phase_at(p0b + (long)((m0x & 3) + 4 * (m0y & 3)) * g.psz, g, px + (m0x >> 2), py + (m0y >> 2));
-    const int c = phase_at(p1b + (long)((m1x & 3) + 4 * (m1y & 3)) * g.psz, g, px + (m1x >> 2), py + (m1y >> 2));
-    const int d = tv_abs((int)S[(long)py * g.W + px] - ((a + c + 1) >> 1));
-    const int w = wave_sum(d);  // the wave's 64 samples belong to one block
-    if ((tid & 63) == 0) atomicAdd(&sad[bi], w);
+  s32[tid] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (tid >> 3)) * g.W + cx + 4 * (tid & 7));
+  if (tid < 21) sad[tid] = 0;
+  if (tid < 84) {
+    const int l = tid / 42, r = tid - l * 42;
+    mvs[l][r >> 1][r & 1] = (l ? Bm : A).mv[r >> 1][r & 1];
   }
   __syncthreads();
-  if (tid == 0) {
-    const Penalties& pen = rc->pen[dec.qp[b]];
-    int cost[21], dir[21];
-    for (int bi = 0; bi < 21; ++bi) {
-      const int cb = sad[bi] + A.pen[bi] + Bm.pen[bi];
-      cost[bi] = A.cost[bi];
-      dir[bi] = 1;
-      if (Bm.cost[bi] < cost[bi]) {
-        cost[bi] = Bm.cost[bi];
-        dir[bi] = 2;
-      }
-      if (cb < cost[bi]) {
-        cost[bi] = cb;
-        dir[bi] = 3;
-      }
+  const uint8_t* p0b = phase0 + (long)b * 16 * g.psz;
+  const uint8_t* p1b = phase1 + (long)b * 16 * g.psz;
+  // item = 4 horizontally adjacent samples of one block: 256 for the 16 8x8 blocks, 256 for
+  // the 4 16x16, 256 for the 32x32; the 8-bit average of both predictions is one
+  // (a | c) - ((a ^ c) >> 1) per dword and its SAD one v_sad_u8
+  for (int item = tid; item < 768; item += 256) {
+    int bi, x, y;
+    if (item < 256) {
+      bi = item >> 4;
+      const int r = item & 15;
+      x = (bi & 3) * 8 + (r & 1) * 4;
+      y = (bi >> 2) * 8 + (r >> 1);
+    } else if (item < 512) {
+      const int j = item - 256;
+      bi = 16 + (j >> 6);
+      const int r = j & 63;
+      x = ((bi - 16) & 1) * 16 + (r & 3) * 4;
+      y = ((bi - 16) >> 1) * 16 + (r >> 2);
+    } else {
+      const int j = item - 512;
+      bi = 20;
+      x = (j & 7) * 4;
+      y = j >> 3;
     }
-    const int ps = pen.split_inter;
-    int sel[16], l2u[16], sum16 = 0;
-    for (int q = 0; q < 4; ++q) {
-      int sum8 = 0;
-      for (int r = 0; r < 4; ++r) sum8 += cost[me_blk8_of(q, r)] + ps;
-      const bool split = sum8 < cost[16 + q] + ps;
-      sum16 += split ? sum8 : cost[16 + q] + ps;
-      for (int r = 0; r < 4; ++r) {
-        const int k = ((q >> 1) * 2 + (r >> 1)) * 4 + (q & 1) * 2 + (r & 1);
-        sel[k] = split ? me_blk8_of(q, r) : 16 + q;
-        l2u[k] = split ? 3 : 4;
-      }
+    const int m0x = mvs[0][bi][0], m0y = mvs[0][bi][1], m1x = mvs[1][bi][0], m1y = mvs[1][bi][1];
+    const uint32_t a = phase4(p0b + (long)((m0x & 3) + 4 * (m0y & 3)) * g.psz, g, cx + x + (m0x >> 2), cy + y + (m0y >> 2));
+    const uint32_t c = phase4(p1b + (long)((m1x & 3) + 4 * (m1y & 3)) * g.psz, g, cx + x + (m1x >> 2), cy + y + (m1y >> 2));
+    const uint32_t avg = (a | c) - (((a ^ c) >> 1) & 0x7f7f7f7fu);
+    atomicAdd(&sad[bi], (int)__builtin_amdgcn_sad_u8(avg, s32[y * 8 + (x >> 2)], 0u));
+  }
+  __syncthreads();
+  // per block: the cheapest of list 0, list 1 and bi (ties keep the earlier); then the
+  // quadrant splits, the whole-CTB choice and each unit's motion, one lane each
+  __shared__ int cost[21], dirb[21], qsum[4], qsplit[4], whole;
+  const Penalties& pen = rc->pen[dec.qp[b]];
+  const int ps = pen.split_inter;
+  if (tid < 21) {
+    const int cb = sad[tid] + A.pen[tid] + Bm.pen[tid];
+    int c = A.cost[tid], d = 1;
+    if (Bm.cost[tid] < c) {
+      c = Bm.cost[tid];
+      d = 2;
     }
-    const bool whole = cost[20] + ps <= sum16;
-    for (int k = 0; k < 16; ++k) {
-      const long u = b * g.usz + (long)((cy >> 3) + (k >> 2)) * g.w8 + (cx >> 3) + (k & 3);
-      const int s = whole ? 20 : sel[k], d = dir[s];
-      dec.cu_log2[u] = (uint8_t)(whole ? 5 : l2u[k]);
-      dec.dir[u] = (uint8_t)d;
-      dec.mv[2 * u] = (int16_t)(d & 1 ? A.mv[s][0] : 0);
-      dec.mv[2 * u + 1] = (int16_t)(d & 1 ? A.mv[s][1] : 0);
-      dec.mv1[2 * u] = (int16_t)(d & 2 ? Bm.mv[s][0] : 0);
-      dec.mv1[2 * u + 1] = (int16_t)(d & 2 ? Bm.mv[s][1] : 0);
-      dec.intra[u] = 0;
-      dec.ipm[u] = 1;
+    if (cb < c) {
+      c = cb;
+      d = 3;
     }
+    cost[tid] = c;
+    dirb[tid] = d;
+  }
+  __syncthreads();
+  if (tid < 4) {
+    int sum8 = 0;
+    for (int r = 0; r < 4; ++r) sum8 += cost[me_blk8_of(tid, r)] + ps;
+    const bool split = sum8 < cost[16 + tid] + ps;
+    qsplit[tid] = split;
+    qsum[tid] = split ? sum8 : cost[16 + tid] + ps;
+  }
+  __syncthreads();
+  if (tid == 0) whole = cost[20] + ps <= qsum[0] + qsum[1] + qsum[2] + qsum[3];
+  __syncthreads();
+  if (tid < 16) {
+    const int k = tid, q = ((k >> 3) << 1) | ((k >> 1) & 1), r = ((k >> 2) & 1) * 2 + (k & 1);
+    const int s = whole ? 20 : (qsplit[q] ? me_blk8_of(q, r) : 16 + q), d = dirb[s];
+    const long u = b * g.usz + (long)((cy >> 3) + (k >> 2)) * g.w8 + (cx >> 3) + (k & 3);
+    dec.cu_log2[u] = (uint8_t)(whole ? 5 : (qsplit[q] ? 3 : 4));
+    dec.dir[u] = (uint8_t)d;
+    dec.mv[2 * u] = (int16_t)(d & 1 ? mvs[0][s][0] : 0);
+    dec.mv[2 * u + 1] = (int16_t)(d & 1 ? mvs[0][s][1] : 0);
+    dec.mv1[2 * u] = (int16_t)(d & 2 ? mvs[1][s][0] : 0);
+    dec.mv1[2 * u + 1] = (int16_t)(d & 2 ? mvs[1][s][1] : 0);
+    dec.intra[u] = 0;
+    dec.ipm[u] = 1;
   }
 }
 
@@ -544,6 +569,8 @@ struct PReconLds {
   int mv[16][2];              // per 8x8 unit (raster within the CTB)
   int mv1[16][2];             // B pictures: list-1 vectors and directions
   int dir[16];
+  uint8_t bwin[4][15 * 16];   // per wave: 15x15 luma reference window of a bi unit
+  int16_t bh[4][15 * 8];      // per wave: horizontal filter pass (15 rows x 8)
   int nz[48], sa[48], dc[48];  // per-TB statistics: luma 0..15, Cb 16..31, Cr 32..47
   int qtype[4];               // luma quadrant: 0 part of a 32x32 CU, 1 16x16 CU, 2 four 8x8 CUs
   int tzero[8];               // stage-3/4 tile t has no surviving level: reconstruction = prediction
@@ -611,16 +638,62 @@ __global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref,
         const int mvx = d == 1 ? L.mv[un][0] : L.mv1[un][0], mvy = d == 1 ? L.mv[un][1] : L.mv1[un][1];
         const uint8_t* P = (d == 1 ? ph : ph1) + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
         p = phase_at(P, g, cx + x + (mvx >> 2), cy + y + (mvy >> 2));
-      } else {  // bi: both lists' 14-bit intermediate samples (8.5.3.3.4.2)
-        const int m0x = L.mv[un][0], m0y = L.mv[un][1], m1x = L.mv1[un][0], m1y = L.mv1[un][1];
-        const int a = mc_luma_inter(ref.plane(0, b, g), g.W, g.W, g.H, cx + x + (m0x >> 2), cy + y + (m0y >> 2), m0x & 3,
-                                    m0y & 3);
-        const int c = mc_luma_inter(ref1.plane(0, b, g), g.W, g.W, g.H, cx + x + (m1x >> 2), cy + y + (m1y >> 2),
-                                    m1x & 3, m1y & 3);
-        p = bipred_sample(a, c);
+      } else {
+        continue;  // bi units: below, one wave per unit
       }
       L.predY[i] = (uint8_t)p;
       L.resY[i] = (int16_t)((int)S[(long)(cy + y) * g.W + cx + x] - p);
+    }
+    // bi-predicted 8x8 units (8.5.3.3.4.2): per list the 15x15 reference window is staged
+    // in this wave's LDS, the 8-tap horizontal pass gives 15 x 8 intermediates, the vertical
+    // pass one 14-bit sample per lane; then (p0 + p1 + 64) >> 7.  Wave-local: no barrier.
+    for (int un = wave; un < 16; un += 4) {
+      if (L.dir[un] != 3) continue;  // wave-uniform
+      const int x0 = cx + (un & 3) * 8, y0 = cy + (un >> 2) * 8;
+      int pl[2];
+      for (int l = 0; l < 2; ++l) {
+        const int mvx = l ? L.mv1[un][0] : L.mv[un][0], mvy = l ? L.mv1[un][1] : L.mv[un][1];
+        const int fx = mvx & 3, fy = mvy & 3, bx = x0 + (mvx >> 2) - 3, by = y0 + (mvy >> 2) - 3;
+        const uint8_t* R = (l ? ref1 : ref).plane(0, b, g);
+        uint8_t* win = L.bwin[wave];
+        for (int k = lane; k < 225; k += 64) {
+          const int r = k / 15, c = k - r * 15;
+          win[r * 16 + c] = R[(long)clip3(0, g.H - 1, by + r) * g.W + clip3(0, g.W - 1, bx + c)];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int16_t* hb = L.bh[wave];
+        for (int k = lane; k < 120; k += 64) {
+          const int r = k >> 3, c = k & 7;
+          int h;
+          if (fx) {
+            h = 0;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) h += kLumaFilter[fx][t] * win[r * 16 + c + t];
+          } else {
+            h = win[r * 16 + c + 3] << 6;
+          }
+          hb[k] = (int16_t)h;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int xo = lane & 7, yo = lane >> 3;
+        if (fy) {
+          int v = 0;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) v += kLumaFilter[fy][t] * hb[(yo + t) * 8 + xo];
+          pl[l] = v >> 6;
+        } else {
+          pl[l] = hb[(yo + 3) * 8 + xo];
+        }
+        __builtin_amdgcn_wave_barrier();  // the window / pass buffers are reused by list 1
+      }
+      const int x = (un & 3) * 8 + (lane & 7), y = (un >> 2) * 8 + (lane >> 3);
+      const int p = bipred_sample(pl[0], pl[1]);
+      L.predY[y * 32 + x] = (uint8_t)p;
+      L.resY[y * 32 + x] = (int16_t)((int)S[(long)(cy + y) * g.W + cx + x] - p);
     }
     for (int i = tid; i < 512; i += 256) {
       const int pl = i >> 8, x = i & 15, y = (i >> 4) & 15, un = (y >> 2) * 4 + (x >> 2);

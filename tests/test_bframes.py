@@ -202,3 +202,25 @@ def test_bframes_mp4_ctts_and_mkv_pts(tmp_path):
     annexb, _, _ = streams.mkv_hevc_annexb(out)
     for x, y in zip(a.frames, hevc.decode(annexb).frames):
         np.testing.assert_array_equal(x[0], y[0])
+
+
+def test_bframes_frame_sizes_display_order_and_spec_plumbing():
+    """2-pass reads pass-1 bits per DISPLAY frame (the QP map the engine takes is display-
+    indexed); the worker spec carries the mini-GOP (in-engine CRF keeps I P P P)."""
+    from thinvids_amd.models.ratecontrol import frame_sizes
+    from thinvids_amd.worker.encoder import EncodeSpec
+    from thinvids_amd.worker.tasks import _pow2
+
+    frames = [hevc.synth_frame(2, t, 96, 64) for t in range(9)]
+    bs, _ = hevc.encode_sequence_cpu(frames, qp=30, bframes=8, search_range=16)
+    off = hevc.display_offsets(bs)
+    plan = hevc.gop_plan(9, 8)
+    assert list(off) == [d - i for i, d in enumerate(plan["disp"])]
+    sizes = frame_sizes(bs)
+    assert len(sizes) == 9 and sum(sizes) == len(bs)
+    assert sizes[0] == max(sizes)  # the IDR (display 0) is the biggest picture
+    ip, _ = hevc.encode_sequence_cpu(frames, qp=30, search_range=16)
+    assert not hevc.display_offsets(ip).any()
+    assert EncodeSpec(96, 64, bframes=8).hevc_bframes() == 8
+    assert EncodeSpec(96, 64, bframes=8, crf=27).hevc_bframes() == 1
+    assert [_pow2(n) for n in (0, 1, 3, 4, 7, 8, 40)] == [1, 1, 2, 4, 4, 8, 16]

@@ -88,7 +88,8 @@ def source(tmp_path_factory):
 
 
 @pytest.mark.parametrize("kw", [dict(mode="direct"), dict(mode="scatter"),
-                                dict(mode="direct", bitrate_kbps=300.0)])
+                                dict(mode="direct", bitrate_kbps=300.0), dict(mode="direct", bframes=4),
+                                dict(mode="scatter", bitrate_kbps=300.0, bframes=8)])
 def test_node_job_world2(tmp_path, source, kw):
     from thinvids_amd.models import hevc
 

@@ -162,6 +162,22 @@ def encode_sequence_cpu(frames, qp: int = 27, gop: int = 0, frame_qps=None, bfra
     return bytes(out), recons
 
 
+def display_offsets(annexb: bytes) -> np.ndarray:
+    """Per picture in decoding order: display index - decoding index (all zero for I P P P;
+    hierarchical-B streams are reordered), from the slice headers only."""
+    lib = core_lib()
+    buf = np.frombuffer(annexb, np.uint8)
+    cap = max(1, annexb.count(b"\x00\x00\x01"))
+    out = np.zeros(cap, np.int32)
+    f = lib.tv_hevc_display_offsets
+    f.restype = C.c_int
+    f.argtypes = [C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_int), C.c_int]
+    n = f(buf.ctypes.data_as(C.POINTER(C.c_uint8)), len(buf), out.ctypes.data_as(C.POINTER(C.c_int)), cap)
+    if n < 0:
+        raise ValueError(lib.tv_last_error().decode())
+    return out[:n]
+
+
 @dataclass
 class DecodedStream:
     width: int

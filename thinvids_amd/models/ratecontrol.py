@@ -80,9 +80,10 @@ def obu_frame_sizes(stream: bytes) -> list[int]:
 
 
 def frame_sizes(annexb: bytes) -> list[int]:
-    """Bytes per coded picture of an Annex-B stream (parameter sets count toward the next
-    picture, start codes included); AV1 OBU streams (leading temporal delimiter) are split
-    per temporal unit."""
+    """Bytes per coded picture of an Annex-B stream in DISPLAY order (parameter sets count
+    toward the next picture in decoding order, start codes included; hierarchical-B streams
+    are mapped back by their POCs, so the list lines up with a display-order QP map); AV1
+    OBU streams (leading temporal delimiter) are split per temporal unit."""
     if annexb[:2] == b"\x12\x00":
         return obu_frame_sizes(annexb)
     out: list[int] = []
@@ -105,6 +106,14 @@ def frame_sizes(annexb: bytes) -> list[int]:
             pending = 0
         else:
             pending += size
+    from .hevc import display_offsets
+
+    off = display_offsets(annexb)
+    if len(off) == len(out) and off.any():
+        disp = [0] * len(out)
+        for i, o in enumerate(off):
+            disp[i + int(o)] = out[i]
+        return disp
     return out
 
 

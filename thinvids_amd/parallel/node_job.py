@@ -400,7 +400,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             resume_dir: str | None = None, max_retries: int = 3, hooks: JobHooks | None = None,
             deblock: bool = True, sao: bool = False, cache=None, crf: int = 0, scenecut: bool = False,
             audio_stream: int = 0, codec: str = "hevc", qindex: int = 0, rc_mode: str = "",
-            vbv_maxrate_kbps: float = 0.0, vbv_bufsize_kbit: float = 0.0) -> dict:
+            vbv_maxrate_kbps: float = 0.0, vbv_bufsize_kbit: float = 0.0, bframes: int = 1) -> dict:
     """One job over the node's ranks (SPMD).  Rate control: ``bitrate_kbps`` > 0 selects
     frame-level 2-pass, or single-pass ABR when ``rc_mode == "abr"`` (optionally under a VBV:
     ``vbv_maxrate_kbps`` / ``vbv_bufsize_kbit``, checked and repaired per segment, see
@@ -446,7 +446,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     ckpt = Checkpoint(resume_dir, Checkpoint.fingerprint(
         src=os.path.abspath(input_path), size=st.st_size if st else 0, mtime=st.st_mtime_ns if st else 0,
         rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software,
-        deblock=deblock, sao=sao, scenecut=scenecut, codec=codec, qindex=qindex, crf=crf,
+        deblock=deblock, sao=sao, scenecut=scenecut, codec=codec, qindex=qindex, crf=crf, bframes=bframes,
         rc=rc_name, bitstream_version=BITSTREAM_VERSION,
         **({"kbps": bitrate_kbps, "vbv": [vbv_maxrate_kbps, vbv_bufsize_kbit] if vbv else None} if abr else {})))
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
@@ -477,7 +477,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     def spec(r):  # the QP is a per-frame input now: one resident engine per rung, whatever the plan
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=qp, gop=gop, search_range=search_range,
                           software=software, deblock=deblock, sao=sao, seed=getattr(src, "seed", 1),
-                          crf=0 if bitrate_kbps > 0 else crf, scenecut=scenecut, codec=codec, qindex=qindex)
+                          crf=0 if bitrate_kbps > 0 else crf, scenecut=scenecut, codec=codec, qindex=qindex,
+                          bframes=bframes)
 
     rc = {"plan": None, "fb": RateFeedback(), "bits": {}}  # pass-2 plan, feedback, per-frame bits
     rung_scale = [(rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]  # per-rung budget ~ pixels
@@ -867,6 +868,7 @@ def main(argv=None) -> int:
     ap.add_argument("--bitrate-kbps", type=float, default=0.0)
     ap.add_argument("--ladder", default="")
     ap.add_argument("--software", action="store_true")
+    ap.add_argument("--bframes", type=int, default=1, help="HEVC hierarchical-B mini-GOP (1 = I P P P)")
     ap.add_argument("--backend", default=None)
     ap.add_argument("--resume-dir", default=None, help="segment checkpoint directory (resume / elastic restart)")
     ap.add_argument("--max-retries", type=int, default=3, help="per-segment retry budget before the job aborts")
@@ -884,7 +886,7 @@ def main(argv=None) -> int:
         dist.init_process_group(backend, timeout=datetime.timedelta(seconds=a.timeout_sec))
     ladder = [int(x) for x in a.ladder.split(",") if x.strip()] or None
     res = run_job(a.input, a.output, a.height, a.qp, a.gop, a.segment_frames, a.mode, a.bitrate_kbps, ladder,
-                  software=a.software, resume_dir=a.resume_dir, max_retries=a.max_retries)
+                  software=a.software, resume_dir=a.resume_dir, max_retries=a.max_retries, bframes=a.bframes)
     if int(os.environ.get("RANK", "0")) == 0:
         print(json.dumps(res), flush=True)
     if dist.is_initialized():

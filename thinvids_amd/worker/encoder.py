@@ -46,12 +46,18 @@ class EncodeSpec:
     scenecut: bool = False  # restart the closed GOP (IDR) at detected scene cuts
     codec: str = "hevc"  # "av1": the AV1 engine (models/av1_engine.py), BASELINE config #4
     qindex: int = 0  # AV1 q-index (0: matched to qp)
+    bframes: int = 1  # HEVC hierarchical-B mini-GOP (1: I P P P; tv/gop.h)
 
     def engine_key(self):
         if self.codec == "av1":
             return ("av1", self.width, self.height, self.av1_qindex())
         return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed,
-                self.crf)
+                self.crf, self.hevc_bframes())
+
+    def hevc_bframes(self) -> int:
+        """Mini-GOP actually used: in-engine CRF keeps I P P P (its lookahead QP is per
+        frame in coding order)."""
+        return 1 if self.crf > 0 else max(1, int(self.bframes))
 
     def av1_qindex(self) -> int:
         from ..models.av1 import qindex_for_hevc_qp
@@ -127,7 +133,7 @@ class EngineCache:
                 else:
                     eng = GpuEngine(spec.width, spec.height, qp=spec.qp, batch=self.batch or auto_batch(spec),
                                     gop=spec.gop, search_range=spec.search_range, deblock=spec.deblock, sao=spec.sao,
-                                    seed=spec.seed, device=self.device, crf=spec.crf)
+                                    seed=spec.seed, device=self.device, crf=spec.crf, bframes=spec.hevc_bframes())
                 eng.lock = threading.Lock()
                 eng.staging = None
                 self._engines[key] = eng
@@ -260,7 +266,8 @@ def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None, fq=None) -> byte
                                f[W * H * 5 // 4:].reshape(H // 2, W // 2)))
     else:
         bs, recons = hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock, sao=spec.sao,
-                                              search_range=spec.search_range, frame_qps=fq, crf=spec.crf)
+                                              search_range=spec.search_range, frame_qps=fq, crf=spec.crf,
+                                              bframes=spec.hevc_bframes())
     if st is not None:
         sse = np.zeros(3)
         for f, r in zip(frames, recons):

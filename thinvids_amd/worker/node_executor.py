@@ -136,7 +136,7 @@ def _job_params(job: dict) -> dict:
             "segment_frames": max(spec.gop, as_int(s.get("tv_node_segment_frames"), 256)),
             "mode": str(s.get("tv_node_mode") or "direct"), "batch_segments": as_int(s.get("tv_node_batch"), 8),
             "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc, "vbv": vbv,
-            "scenecut": spec.scenecut, "codec": spec.codec, "qindex": spec.qindex}
+            "scenecut": spec.scenecut, "codec": spec.codec, "qindex": spec.qindex, "bframes": spec.hevc_bframes()}
 
 
 class CommFailure(RuntimeError):
@@ -206,6 +206,7 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                       batch_segments=p["batch_segments"], hooks=hooks, deblock=p["deblock"], sao=p["sao"],
                       cache=None if p["software"] else cache, crf=p["crf"], resume_dir=spec["ckpt"],
                       scenecut=p.get("scenecut", False), codec=p.get("codec", "hevc"), qindex=p.get("qindex", 0),
+                      bframes=p.get("bframes", 1),
                       audio_stream=int(spec["job"].get("selected_a_stream") or 0), rc_mode=p.get("rc", ""),
                       vbv_maxrate_kbps=p.get("vbv", [0, 0])[0], vbv_bufsize_kbit=p.get("vbv", [0, 0])[1])
     except Exception as e:

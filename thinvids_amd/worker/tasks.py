@@ -104,7 +104,14 @@ def encode_spec_for_job(job: dict, settings: dict | None = None) -> EncodeSpec:
                       if str(job.get("rc_mode") or s.get("tv_rc") or "cqp").lower() == "crf" else 0,
                       scenecut=as_bool(s.get("tv_scenecut"), True),
                       codec="av1" if str(job.get("codec") or s.get("tv_codec") or "hevc").lower() == "av1" else "hevc",
-                      qindex=as_int(job.get("qindex") or s.get("tv_qindex"), 0))
+                      qindex=as_int(job.get("qindex") or s.get("tv_qindex"), 0),
+                      bframes=_pow2(as_int(job.get("bframes") or s.get("tv_bframes"), 1)))
+
+
+def _pow2(n: int) -> int:
+    """Largest power of two <= n in 1..16 (the engine's mini-GOP sizes)."""
+    n = max(1, min(16, int(n)))
+    return 1 << (n.bit_length() - 1)
 
 
 # =====================================================================  transcode
