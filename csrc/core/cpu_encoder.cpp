@@ -342,15 +342,16 @@ int bipred_sad(const Picture& src, const Picture& ref0, const Picture& ref1, int
 }
 
 void analyze_inter_b(const SeqConfig& cfg, const Picture& src, const Picture& ref0, const Picture& ref1,
-                     const int16_t* cmv0, const int16_t* cmv1, const int16_t* prev_mv, int range, FrameDecisions& fd) {
+                     const int16_t* cmv0, const int16_t* cmv1, const int16_t* prev_mv, const int* range,
+                     FrameDecisions& fd) {
   const int pen_split = (int)(lambda_sad(cfg.qp) * 4);
   const int wc = cfg.coded_w / kCtb, hc = cfg.coded_h / kCtb;
   for (int cyi = 0; cyi < hc; ++cyi)
     for (int cxi = 0; cxi < wc; ++cxi) {
       const int cx = cxi * kCtb, cy = cyi * kCtb;
       CtbMe m0, m1;
-      me_ctb(cfg, src, ref0, cmv0, prev_mv, range, cxi, cyi, fd.w8, m0);
-      me_ctb(cfg, src, ref1, cmv1, prev_mv, range, cxi, cyi, fd.w8, m1);
+      me_ctb(cfg, src, ref0, cmv0, prev_mv, range[0], cxi, cyi, fd.w8, m0);
+      me_ctb(cfg, src, ref1, cmv1, prev_mv, range[1], cxi, cyi, fd.w8, m1);
       int cost[21], dir[21];
       for (int bi = 0; bi < 21; ++bi) {
         int bx, by, n;
@@ -503,13 +504,16 @@ void CpuEncoder::encode_b_structured(std::vector<uint8_t>& out, int qp) {
   const int base = qp >= 0 ? qp : cfg_.qp;
   fc.qp = clip3(0, 51, base + gop_layer_qp_offset(p.type, p.layer, cfg_.mgop));
   std::vector<int16_t> cmv[2];
+  int rng[2] = {range_, range_};
   int penmv[64];
   for (int i = 0; i < 64; ++i) penmv[i] = (int)(lambda_sad(cfg_.qp) * i);
   for (int l = 0; l < 2; ++l) {
     if (p.ref[l] < 0) continue;
     cmv[l].assign(2 * (size_t)wc * hc, 0);
     std::vector<int> ccost((size_t)wc * hc);
-    coarse_search(q.data(), find(p.ref[l]).q.data(), cfg_.coded_w, cfg_.coded_h, range_, penmv, cmv[l].data(), ccost.data());
+    rng[l] = gop_search_range(range_, std::abs(p.disp - p.ref[l]), cfg_.mgop);
+    coarse_search(q.data(), find(p.ref[l]).q.data(), cfg_.coded_w, cfg_.coded_h, rng[l], penmv, cmv[l].data(),
+                  ccost.data());
   }
   if (prev_mv_.empty()) prev_mv_.assign(2 * (size_t)dec.w8 * dec.h8, 0);
   dec.refs = slice_refs(p);  // before reconstruction: B deblocking reads the directions
@@ -520,12 +524,12 @@ void CpuEncoder::encode_b_structured(std::vector<uint8_t>& out, int qp) {
     reconstruct_frame(fc, src_, nullptr, dec, rec_);
   } else if (p.type == 1) {
     const Picture& r0 = find(p.ref[0]).rec;
-    analyze_inter(fc, src_, r0, cmv[0].data(), prev_mv_.data(), range_, dec);
+    analyze_inter(fc, src_, r0, cmv[0].data(), prev_mv_.data(), rng[0], dec);
     reconstruct_frame(fc, src_, &r0, dec, rec_);
   } else {
     const Picture& r0 = find(p.ref[0]).rec;
     const Picture& r1 = find(p.ref[1]).rec;
-    analyze_inter_b(fc, src_, r0, r1, cmv[0].data(), cmv[1].data(), prev_mv_.data(), range_, dec);
+    analyze_inter_b(fc, src_, r0, r1, cmv[0].data(), cmv[1].data(), prev_mv_.data(), rng, dec);
     reconstruct_frame(fc, src_, &r0, dec, rec_, &r1);
   }
   prev_mv_ = dec.mv;

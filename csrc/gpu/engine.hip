@@ -545,10 +545,12 @@ class Core {
     const int16_t* prev_mv = f ? slot_dec(slots_[(f - 1) % nslots_]).mv : nullptr;
     const long cstride = (long)B * nctu_;
     MeBuffers me[2];
+    int rng[2] = {cfg_.range, cfg_.range};
     for (int l = 0; l < 2; ++l) {
       if (pic.ref[l] < 0) continue;
       me[l] = MeBuffers{cur_e.q, entry_of(pic.ref[l]).q, prev_mv, cmv_ + l * cstride * 2, ccost_ + l * cstride};
-      launch_coarse_me(me[l], g_, rc_, cfg_.qp, cfg_.range, B, stream_);
+      rng[l] = gop_search_range(cfg_.range, std::abs(pic.disp - pic.ref[l]), cfg_.mgop);
+      launch_coarse_me(me[l], g_, rc_, cfg_.qp, rng[l], B, stream_);
     }
     if (cfg_.crf > 0 && !qmap_given_) launch_rc_crf(cur_e.q, ccost_, dec.qp, g_, cfg_.crf, intra, B, stream_);
     if (intra) {  // fork onto the priority stream and join back
@@ -559,12 +561,12 @@ class Core {
       HIP_OK(hipStreamWaitEvent(stream_, iev_[1], 0));
     } else if (!bpic) {
       const DpbEntry& r0 = entry_of(pic.ref[0]);
-      launch_inter_frame(src_, r0.rec, r0.phase, cur, dec, g_, rc_, cfg_.range, me[0], B, stream_);
+      launch_inter_frame(src_, r0.rec, r0.phase, cur, dec, g_, rc_, rng[0], me[0], B, stream_);
     } else {
       const DpbEntry& r0 = entry_of(pic.ref[0]);
       const DpbEntry& r1 = entry_of(pic.ref[1]);
-      launch_inter_frame_b(src_, r0.rec, r0.phase, r1.rec, r1.phase, cur, dec, g_, rc_, cfg_.range, me[0], me[1],
-                           meout_, B, stream_);
+      launch_inter_frame_b(src_, r0.rec, r0.phase, r1.rec, r1.phase, cur, dec, g_, rc_, rng, me[0], me[1], meout_,
+                           B, stream_);
     }
     stage(intra ? "intra" : "inter");
     launch_compact(dec, g_, slot_compact(s), B, stream_);

@@ -63,7 +63,7 @@ struct CtbMeOut {
 // block the best of L0 / L1 / their average, the CU split, then bi-predictive reconstruction.
 // meout: scratch of 2 x B x nctu CtbMeOut.
 void launch_inter_frame_b(FrameSet src, FrameSet ref0, const uint8_t* phase0, FrameSet ref1, const uint8_t* phase1,
-                          FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, int range,
+                          FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, const int* range,
                           const MeBuffers& me0, const MeBuffers& me1, CtbMeOut* meout, int B, hipStream_t s);
 // 16 quarter-pel phase planes (B x 16 x psz bytes) of the luma reference
 void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipStream_t s);

@@ -1005,12 +1005,12 @@ void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameS
 }
 
 void launch_inter_frame_b(FrameSet src, FrameSet ref0, const uint8_t* phase0, FrameSet ref1, const uint8_t* phase1,
-                          FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, int range,
+                          FrameSet rec, DecisionSet dec, const Geo& g, const RcTables* rc, const int* range,
                           const MeBuffers& me0, const MeBuffers& me1, CtbMeOut* meout, int B, hipStream_t s) {
   const dim3 grid(g.wc * g.hc, B);
   CtbMeOut* o1 = meout + (long)B * g.wc * g.hc;
-  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref0, phase0, dec, me0.prev_mv, me0.cmv, g, rc, range, 0, meout);
-  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref1, phase1, dec, me1.prev_mv, me1.cmv, g, rc, range, 0, o1);
+  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref0, phase0, dec, me0.prev_mv, me0.cmv, g, rc, range[0], 0, meout);
+  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref1, phase1, dec, me1.prev_mv, me1.cmv, g, rc, range[1], 0, o1);
   k_bi_decide<<<grid, 256, 0, s>>>(src, phase0, phase1, meout, o1, dec, g, rc);
   k_inter_recon<<<grid, 256, 0, s>>>(src, ref0, phase0, rec, dec, g, recon_tile_skip(), ref1, phase1);
 }

@@ -21,7 +21,8 @@ void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref,
 // B pictures (tv/gop.h): both lists' searches, then per block the best of list 0, list 1
 // and their 8-bit average (bi-prediction), then the same CU split.
 void analyze_inter_b(const SeqConfig& cfg, const Picture& src, const Picture& ref0, const Picture& ref1,
-                     const int16_t* cmv0, const int16_t* cmv1, const int16_t* prev_mv, int range, FrameDecisions& fd);
+                     const int16_t* cmv0, const int16_t* cmv1, const int16_t* prev_mv, const int* range,
+                     FrameDecisions& fd);
 // Pass B: prediction + transform/quant + reconstruction (+ deblocking) from decisions
 // (ref1 != nullptr: a B picture, fd.dir / fd.mv1 select the lists).
 void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* ref,

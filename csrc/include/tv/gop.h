@@ -95,6 +95,16 @@ inline GopPlan plan_gop(int nframes, int mgop) {
   return g;
 }
 
+// Motion search range of a reference `dist` pictures away in a hierarchical-B GOP: the
+// anchors' range covers M frames of motion, nearer references need proportionally less
+// (range * dist / 4, in steps of 16, at least 16) -- the coarse quarter-res search shrinks
+// quadratically with it.  I P P P streams keep the configured range.
+inline int gop_search_range(int range, int dist, int mgop) {
+  if (mgop <= 1) return range;
+  const int r = (range * dist + 63) / 64 * 16;
+  return std::min(range, std::max(16, r));
+}
+
 // QP offset of a temporal layer (hierarchical-B QP cascade).  IPPP streams: none.  With B
 // frames the anchor P pictures take +1 and B layer L takes +3 + L: the B pictures are never
 // (layer max) or briefly referenced, so their bits buy little quality for the rest of the
