@@ -82,9 +82,32 @@ const Scans& scans() {
   }();
   return s;
 }
+// writer fast path: per scan index of an N x N TB the padded-raster index (stride N + 4) and
+// the base-context offset of its position
+struct ScanPad {
+  int16_t pad8[64], pad16[256];
+  uint8_t off8[64], off16[256];
+};
+const ScanPad& scan_pad();
 constexpr int kCoeffBaseOffset[5][5] = {
     {0, 1, 6, 6, 21}, {1, 6, 6, 21, 21}, {6, 6, 21, 21, 21}, {6, 21, 21, 21, 21}, {21, 21, 21, 21, 21}};
 constexpr int kIntraModeCtx[13] = {0, 1, 2, 3, 4, 4, 4, 4, 3, 0, 1, 2, 0};
+const ScanPad& scan_pad() {
+  static const ScanPad s = [] {
+    ScanPad t;
+    for (int lg = 3; lg <= 4; ++lg) {
+      const int N = 1 << lg, S = N + 4;
+      const int16_t* sc = lg == 4 ? scans().s16 : scans().s8;
+      for (int c = 0; c < N * N; ++c) {
+        const int r = sc[c] >> lg, k = sc[c] & (N - 1);
+        (lg == 4 ? t.pad16 : t.pad8)[c] = (int16_t)(r * S + k);
+        (lg == 4 ? t.off16 : t.off8)[c] = (uint8_t)kCoeffBaseOffset[std::min(r, 4)][std::min(k, 4)];
+      }
+    }
+    return t;
+  }();
+  return s;
+}
 inline bool directional(int m) { return m >= V_PRED && m <= 8; }
 
 // ------------------------------------------------------------------------ CDFs ----------
@@ -263,6 +286,8 @@ struct Tile {
   std::function<const int16_t*(int, int)> lev_in;
   const int16_t* eob_in[3] = {nullptr, nullptr, nullptr};  // writer: eob per packed TB (scan_packed)
   const int32_t* eob_off[3] = {nullptr, nullptr, nullptr};   // block -> packed TB index (-1: none)
+  const int16_t* scan_in[3] = {nullptr, nullptr, nullptr};   // writer: scan-packed stream per plane
+  const int32_t* scan_off[3] = {nullptr, nullptr, nullptr};  // block -> offset of its [eob, ...] record
   int16_t* lev_out[3] = {nullptr, nullptr, nullptr};
 
   Tile(IO& io_, const SeqGeo& g_, FrameParams& fp_, std::vector<uint32_t>& mode_, std::vector<uint32_t>& mv_,
@@ -307,6 +332,120 @@ struct Tile {
     mag = std::min((mag + 1) >> 1, 6);
     if (!pos) return mag;
     return (row < 2 && col < 2) ? mag + 7 : mag + 14;
+  }
+
+  // Writer fast path of coeffs(): the levels come in scan order (lv[0..eob-1], the engine's
+  // scan-packed layout), the contexts read a zero-padded raster of the coded magnitudes
+  // (stride N + 4: no bounds checks) that is cleared again at the eob positions only.
+  uint8_t qpad_[20 * 20] = {};
+  void coeffs_w(int plane, int lg, int x4, int y4, const int16_t* lv, int eob, bool is_inter, int intra_dir) {
+    const int N = 1 << lg, area = N * N, w4 = N >> 2, ptype = plane > 0, txc = lg - 2, S = N + 4;
+    auto& AL = aLvl[plane];
+    auto& AD = aDc[plane];
+    auto& LL = lLvl[plane];
+    auto& LD = lDc[plane];
+    const int na = std::max(0, std::min(w4, (int)AL.size() - x4)), nl = std::max(0, std::min(w4, (int)LL.size() - y4));
+    int ctx = 0;
+    if (plane) {
+      int above = 0, left = 0;
+      for (int i = 0; i < na; ++i) above |= AL[x4 + i] | AD[x4 + i];
+      for (int i = 0; i < nl; ++i) left |= LL[y4 + i] | LD[y4 + i];
+      ctx = 7 + (above != 0) + (left != 0);
+    }
+    auto set_ctx = [&](int lvl, int dc) {
+      for (int i = 0; i < na; ++i) AL[x4 + i] = (uint8_t)lvl, AD[x4 + i] = (uint8_t)dc;
+      for (int i = 0; i < nl; ++i) LL[y4 + i] = (uint8_t)lvl, LD[y4 + i] = (uint8_t)dc;
+    };
+    int all_zero = eob == 0;
+    io.sym(all_zero, cdf.txb_skip[txc][ctx], 2);
+    if (all_zero) {
+      set_ctx(0, 0);
+      return;
+    }
+    if (plane == 0) {
+      int s = 1;
+      if (is_inter) io.sym(s, cdf.inter_tx[txc], 2);
+      else io.sym(s, cdf.intra_tx[txc][intra_dir], 5);
+    }
+    const int ems = 2 * lg - 4;
+    const int eobPt = eob <= 2 ? eob : floor_log2((unsigned)(eob - 1)) + 2;
+    int s = eobPt - 1;
+    io.sym(s, cdf.eob_pt[ems][ptype][0], ems + 5);
+    if (eobPt >= 3) {
+      const int rem = eob - ((1 << (eobPt - 2)) + 1);
+      int bit = (rem >> (eobPt - 3)) & 1;
+      io.sym(bit, cdf.eob_extra[txc][ptype][eobPt - 3], 2);
+      for (int i = 1; i < eobPt - 2; ++i) {
+        bit = (rem >> (eobPt - 3 - i)) & 1;
+        io.lit(bit, 1);
+      }
+    }
+    const ScanPad& sp = scan_pad();
+    const int16_t* pad = lg == 4 ? sp.pad16 : sp.pad8;
+    const uint8_t* boff = lg == 4 ? sp.off16 : sp.off8;
+    uint8_t* Q = qpad_;
+    C17* cb = cdf.base[txc][ptype];
+    C17* cbr = cdf.br[std::min(txc, 3)][ptype];
+    for (int c = eob - 1; c >= 0; --c) {
+      const int pi = pad[c], a = std::abs((int)lv[c]);
+      int level;
+      if (c == eob - 1) {
+        const int bctx = c == 0 ? 0 : (c <= area / 8 ? 1 : (c <= area / 4 ? 2 : 3));
+        int v = std::min(a, 3) - 1;
+        io.sym(v, cdf.base_eob[txc][ptype][bctx], 3);
+        level = v + 1;
+      } else {
+        int v = std::min(a, 3);
+        int bc = 0;
+        if (c) {
+          const int mag = std::min<int>(Q[pi + 1], 3) + std::min<int>(Q[pi + S], 3) + std::min<int>(Q[pi + S + 1], 3) +
+                          std::min<int>(Q[pi + 2], 3) + std::min<int>(Q[pi + 2 * S], 3);
+          bc = std::min((mag + 1) >> 1, 4) + boff[c];
+        }
+        io.sym(v, cb[bc], 4);
+        level = v;
+      }
+      if (level > 2) {
+        const int mag = std::min((Q[pi + 1] + Q[pi + S] + Q[pi + S + 1] + 1) >> 1, 6);
+        const int row = pi / S, col = pi - row * S;
+        const int bctx = !c ? mag : ((row < 2 && col < 2) ? mag + 7 : mag + 14);
+        for (int k = 0; k < 4; ++k) {
+          int v = std::min(a - level, 3);
+          io.sym(v, cbr[bctx], 4);
+          level += v;
+          if (v < 3) break;
+        }
+      }
+      Q[pi] = (uint8_t)level;  // <= 15
+    }
+    int dcs = 0;
+    for (int i = 0; i < na; ++i) dcs += AD[x4 + i] == 1 ? -1 : (AD[x4 + i] == 2 ? 1 : 0);
+    for (int i = 0; i < nl; ++i) dcs += LD[y4 + i] == 1 ? -1 : (LD[y4 + i] == 2 ? 1 : 0);
+    const int dctx = dcs < 0 ? 1 : (dcs > 0 ? 2 : 0);
+    int cul = 0, dcCat = 0;
+    for (int c = 0; c < eob; ++c) {
+      const int l = lv[c];
+      Q[pad[c]] = 0;
+      if (!l) continue;
+      int sign = l < 0;
+      if (c == 0) io.sym(sign, cdf.dc_sign[ptype][dctx], 2);
+      else io.lit(sign, 1);
+      const int a = std::abs(l);
+      if (a >= 15) {  // Golomb of a - 14
+        const int x = a - 14, length = floor_log2((unsigned)x) + 1;
+        for (int i = 0; i < length; ++i) {
+          int b = i == length - 1;
+          io.lit(b, 1);
+        }
+        for (int i = length - 2; i >= 0; --i) {
+          int b = (x >> i) & 1;
+          io.lit(b, 1);
+        }
+      }
+      if (c == 0) dcCat = sign ? 1 : 2;  // scan index 0 is position 0
+      cul += std::min(a, 15);  // as the raster path: only culLevel != 0 reaches a context
+    }
+    set_ctx(std::min(63, cul), dcCat);
   }
 
   // one transform block; L = raster levels (writer: input, reader: output)
@@ -806,7 +945,32 @@ struct Tile {
     // residual
     int nz = 0;
     const int x4 = mic, y4 = mir;
-    if (!skip) {
+    if (IO::kW && !skip) {
+      for (int p = 0; p < 3; ++p) {
+        const int lg = p ? 3 : 4, area = 1 << (2 * lg);
+        const int16_t* lv = nullptr;
+        int eob = 0;
+        int16_t tmp[256];
+        if (scan_in[p]) {  // engine layout: [eob, levels in scan order] per nonzero TB
+          const int32_t o = scan_off[p][b];
+          if (o >= 0) {
+            eob = scan_in[p][o];
+            lv = scan_in[p] + o + 1;
+          }
+        } else if (const int16_t* src = lev_in(p, b)) {  // raster input: to scan order
+          const int16_t* sc = lg == 4 ? scans().s16 : scans().s8;
+          for (int c = 0; c < area; ++c) {
+            tmp[c] = src[sc[c]];
+            if (tmp[c]) eob = c + 1;
+          }
+          lv = tmp;
+        }
+        coeffs_w(p, lg, p ? x4 >> 1 : x4, p ? y4 >> 1 : y4, lv, eob, inter != 0, ymode[b]);
+        if (eob) nz |= 1 << p;
+      }
+      if (nz != mode_nz(mode[b])) throw std::runtime_error("av1 writer: nonzero mask mismatch");
+      if (nz == 0) throw std::runtime_error("av1: non-skip block without coefficients");
+    } else if (!skip) {
       for (int p = 0; p < 3; ++p) {
         const int lg = p ? 3 : 4;
         int16_t tmp[256];
@@ -1255,8 +1419,10 @@ void put_obu(std::vector<uint8_t>& out, int type, const std::vector<uint8_t>& pa
 std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& d, bool seq_header, EntropyState* st) {
   const int nb = g.nblk();
   FrameParams fp = d.fp;
-  std::vector<uint32_t> mode(d.mode, d.mode + nb), mv(nb, 0);
+  thread_local std::vector<uint32_t> mode, mv;  // reused across calls (no per-frame page faults)
+  mode.assign(d.mode, d.mode + nb);
   if (d.mv) mv.assign(d.mv, d.mv + nb);
+  else mv.assign(nb, 0);
   std::vector<int8_t> cdef(d.cdef_idx, d.cdef_idx + g.nsb());
   SymW io;
   Tile<SymW> t(io, g, fp, mode, mv, cdef);
@@ -1276,36 +1442,28 @@ std::vector<uint8_t> write_temporal_unit(const SeqGeo& g, const FrameDecisions& 
   // level access (packed layout: prefix offsets over the nonzero masks)
   std::vector<int32_t> off[3];
   const int16_t* base[3] = {d.ly, d.lu, d.lv};
-  std::vector<int16_t> expd[3], eobs[3];
-  if (d.scan_packed)  // [eob, eob levels in scan order] per nonzero TB -> raster TBs
+  thread_local std::vector<int32_t> soff[3];
+  if (d.scan_packed)  // [eob, eob levels in scan order] per nonzero TB: coded straight from it
     for (int p = 0; p < 3; ++p) {
       const int sz = p ? 64 : 256;
-      const int16_t* scan = p ? scans().s8 : scans().s16;
-      int cnt = 0;
-      for (int b = 0; b < nb; ++b) cnt += mode_nz(mode[b]) >> p & 1;
-      expd[p].assign((size_t)cnt * sz, 0);
-      eobs[p].resize(cnt);
-      const int16_t* q = base[p];
-      for (int k = 0; k < cnt; ++k) {
-        const int eob = *q++;
+      soff[p].assign(nb, -1);
+      int32_t o = 0;
+      for (int b = 0; b < nb; ++b) {
+        if (!(mode_nz(mode[b]) >> p & 1)) continue;
+        const int eob = base[p][o];
         if (eob < 1 || eob > sz) throw std::runtime_error("scan-packed levels: bad eob");
-        eobs[p][k] = (int16_t)eob;
-        for (int i = 0; i < eob; ++i) expd[p][(size_t)k * sz + scan[i]] = q[i];
-        q += eob;
+        soff[p][b] = o;
+        o += 1 + eob;
       }
-      base[p] = expd[p].data();
+      t.scan_in[p] = base[p];
+      t.scan_off[p] = soff[p].data();
     }
-  if (d.packed)
+  if (d.packed && !d.scan_packed)
     for (int p = 0; p < 3; ++p) {
       off[p].assign(nb, -1);
       int k = 0;
       for (int b = 0; b < nb; ++b)
         if (mode_nz(mode[b]) >> p & 1) off[p][b] = k++;
-    }
-  if (d.scan_packed)
-    for (int p = 0; p < 3; ++p) {  // eob hints: the writer skips the backward eob scan
-      t.eob_in[p] = eobs[p].data();
-      t.eob_off[p] = off[p].data();
     }
   t.lev_in = [&](int p, int b) -> const int16_t* {
     const size_t sz = p ? 64 : 256;

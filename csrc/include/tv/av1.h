@@ -79,8 +79,11 @@ inline void cdf_adapt(uint16_t* icdf, int n, int sym) {
 // symbols per frame)
 class RangeEncoder {
  public:
-  void encode(int sym, uint16_t* icdf, int n, bool adapt = true) {
-    if (sym < 0 || sym >= n) throw std::runtime_error("range coder: symbol out of range");
+  // The pre-carry buffer is thread-local and reused (cleared, capacity kept): a writer per
+  // frame would otherwise map and fault fresh pages for it on every call.
+  RangeEncoder() : pre_(tl_buffer()) { pre_.clear(); }
+  __attribute__((always_inline)) void encode(int sym, uint16_t* icdf, int n, bool adapt = true) {
+    if (__builtin_expect(sym < 0 || sym >= n, 0)) throw std::runtime_error("range coder: symbol out of range");
     const uint32_t r = rng_;
     uint32_t nr;
     if (sym > 0) {
@@ -110,7 +113,7 @@ class RangeEncoder {
     return ((r >> 8) * (uint32_t)(icdf_v >> kProbShift) >> (7 - kProbShift)) + kMinProb * (n - 1 - k);
   }
   // low_ already holds the new low; normalise the range back to [2^15, 2^16)
-  void emit(uint32_t r) {
+  __attribute__((always_inline)) void emit(uint32_t r) {
     const int d = 16 - (32 - __builtin_clz(r));
     int c = cnt_, s = c + d;
     uint64_t l = low_;
@@ -134,7 +137,11 @@ class RangeEncoder {
   uint64_t low_ = 0;
   uint32_t rng_ = 0x8000;
   int cnt_ = -9;
-  std::vector<uint16_t> pre_;  // pre-carry bytes
+  static std::vector<uint16_t>& tl_buffer() {
+    thread_local std::vector<uint16_t> b;
+    return b;
+  }
+  std::vector<uint16_t>& pre_;  // pre-carry bytes (one live encoder per thread)
 };
 
 class RangeDecoder {
