@@ -344,24 +344,52 @@ TV_HD int lf_edge(uint32_t prev, uint32_t cur, int pos, int dim, int pass, int c
 TV_HD int lf_s8(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
 
 // AV1 7.14.6: filter one line of an edge.  q0 points at the first q-side pixel, `step` is
-// the distance between taps (1 for a vertical edge, the pitch for a horizontal one).
-TV_HD void lf_filter(uint8_t* q0, int step, int size, int lvl, int sharp) {
+// the distance between taps (1 for a vertical edge, the pitch for a horizontal one).  Every
+// loop bound is a template constant, so the tap arrays live in registers (a runtime-sized
+// version spilled them to scratch memory in the GPU deblocking kernel).
+template <int n, int log2, int n2> TV_HD void lf_wide(uint8_t* q0, int step, const int* p, const int* q) {
+  // wide filter (7.14.6.4): n taps modified per side, weight 2 within |j| <= n2
+  int F[14];  // F[7 + k]: k >= 0 -> q[k], k < 0 -> p[-k-1]
+#pragma unroll
+  for (int k = 0; k <= n; ++k) {
+    F[7 + k] = q[k];
+    F[6 - k] = p[k];
+  }
+  int o[12];
+#pragma unroll
+  for (int i = -n; i < n; ++i) {
+    int t = 0;
+#pragma unroll
+    for (int j = -n; j <= n; ++j) {
+      const int k = clip3(-(n + 1), n, i + j);
+      t += F[7 + k] * ((j <= n2 && j >= -n2) ? 2 : 1);
+    }
+    o[i + n] = (t + (1 << (log2 - 1))) >> log2;
+  }
+#pragma unroll
+  for (int i = -n; i < n; ++i) q0[i * step] = (uint8_t)o[i + n];
+}
+
+template <int SIZE> TV_HD void lf_filter_n(uint8_t* q0, int step, int lvl, int sharp) {
   const int shift = sharp > 4 ? 2 : (sharp > 0 ? 1 : 0);
   int limit = lvl >> shift;
   limit = sharp > 0 ? clip3(1, 9 - sharp, limit) : (limit < 1 ? 1 : limit);
   const int blimit = 2 * (lvl + 2) + limit, thresh = lvl >> 4;
-  const int nr = size == 16 ? 7 : (size == 8 ? 4 : (size == 6 ? 3 : 2));  // taps read per side
+  constexpr int nr = SIZE == 16 ? 7 : (SIZE == 8 ? 4 : (SIZE == 6 ? 3 : 2));  // taps read per side
+  constexpr int lm = SIZE == 4 ? 2 : (SIZE == 6 ? 3 : 4);
   int p[7], q[7];
+#pragma unroll
   for (int k = 0; k < nr; ++k) {
     q[k] = q0[k * step];
     p[k] = q0[-(k + 1) * step];
   }
-  const int lm = size == 4 ? 2 : (size == 6 ? 3 : 4);
   bool mask = tv_abs(p[0] - q[0]) * 2 + (tv_abs(p[1] - q[1]) >> 1) <= blimit;
+#pragma unroll
   for (int k = 1; k < lm; ++k) mask = mask && tv_abs(p[k] - p[k - 1]) <= limit && tv_abs(q[k] - q[k - 1]) <= limit;
   if (!mask) return;
-  bool flat = size >= 6;
-  for (int k = 1; k < lm && flat; ++k) flat = tv_abs(p[k] - p[0]) <= 1 && tv_abs(q[k] - q[0]) <= 1;
+  bool flat = SIZE >= 6;
+#pragma unroll
+  for (int k = 1; k < lm; ++k) flat = flat && tv_abs(p[k] - p[0]) <= 1 && tv_abs(q[k] - q[0]) <= 1;
   if (!flat) {  // narrow filter (7.14.6.3)
     const bool hev = tv_abs(p[1] - p[0]) > thresh || tv_abs(q[1] - q[0]) > thresh;
     const int ps1 = p[1] - 128, ps0 = p[0] - 128, qs0 = q[0] - 128, qs1 = q[1] - 128;
@@ -377,25 +405,26 @@ TV_HD void lf_filter(uint8_t* q0, int step, int size, int lvl, int sharp) {
     }
     return;
   }
-  bool flat2 = size == 16;
-  for (int k = 4; k < 7 && flat2; ++k) flat2 = tv_abs(p[k] - p[0]) <= 1 && tv_abs(q[k] - q[0]) <= 1;
-  // wide filter (7.14.6.4): n taps modified per side, weight 2 within |j| <= n2
-  const int log2 = flat2 ? 4 : 3, n = flat2 ? 6 : (size == 6 ? 2 : 3), n2 = (log2 == 3 && size != 6) ? 0 : 1;
-  int F[14];  // F[7 + k]: k >= 0 -> q[k], k < 0 -> p[-k-1]
-  for (int k = 0; k <= n; ++k) {
-    F[7 + k] = q[k];
-    F[6 - k] = p[k];
+  if constexpr (SIZE == 16) {
+    bool flat2 = true;
+#pragma unroll
+    for (int k = 4; k < 7; ++k) flat2 = flat2 && tv_abs(p[k] - p[0]) <= 1 && tv_abs(q[k] - q[0]) <= 1;
+    if (flat2) lf_wide<6, 4, 1>(q0, step, p, q);
+    else lf_wide<3, 3, 0>(q0, step, p, q);
+  } else if constexpr (SIZE == 8) {
+    lf_wide<3, 3, 0>(q0, step, p, q);
+  } else if constexpr (SIZE == 6) {
+    lf_wide<2, 3, 1>(q0, step, p, q);
   }
-  int o[12];
-  for (int i = -n; i < n; ++i) {
-    int t = 0;
-    for (int j = -n; j <= n; ++j) {
-      const int k = clip3(-(n + 1), n, i + j);
-      t += F[7 + k] * ((j <= n2 && j >= -n2) ? 2 : 1);
-    }
-    o[i + n] = (t + (1 << (log2 - 1))) >> log2;
+}
+
+TV_HD void lf_filter(uint8_t* q0, int step, int size, int lvl, int sharp) {
+  switch (size) {
+    case 16: lf_filter_n<16>(q0, step, lvl, sharp); break;
+    case 8: lf_filter_n<8>(q0, step, lvl, sharp); break;
+    case 6: lf_filter_n<6>(q0, step, lvl, sharp); break;
+    default: lf_filter_n<4>(q0, step, lvl, sharp); break;
   }
-  for (int i = -n; i < n; ++i) q0[i * step] = (uint8_t)o[i + n];
 }
 
 }  // namespace av1
