@@ -389,17 +389,19 @@ class Core {
 
   // worker: fetch exactly the used bytes of slot s from the device on a private stream
   // wait for everything queued on `st` without spinning a CPU core
-  // Host waits for GPU work: TV_SYNC_MODE=spin (default: hipStreamSynchronize /
-  // hipEventSynchronize spin — lowest wake-up latency), poll (query + 40 us sleeps) or block
-  // (blocking-sync events).  Same-box A/B on the 1080p bench (profiles/README.md): spin 7510-7632
-  // frames/s; poll 6399-6663 and block 6522-6932 although they free 5-6 of the 16 CPUs — the
-  // slot turnaround latency, not the CPU, sets the pace once CABAC keeps up.
+  // Host waits for GPU work: TV_SYNC_MODE=poll (default: hipEventQuery + 40 us sleeps), spin
+  // (hipStreamSynchronize / hipEventSynchronize spin) or block (blocking-sync events).
+  // Round 2, when a pool thread per in-flight slot waited, spin won (7510-7632 vs poll
+  // 6399-6663 frames/s); since each stream group's slots complete in order on one fetch
+  // thread with 3 more slots queued behind it, the wake-up latency is hidden: same-box A/B
+  // (profiles/r3s2_sync_ab.txt) spin 7127 / 7091 frames/s at 10.5 / 10.3 busy cores, poll
+  // 7124 / 7104 at 8.2 / 8.1, block 7121 / 7121 at 10.0 / 10.1.
   static int sync_mode() {
     static const int m = [] {
       const char* e = getenv("TV_SYNC_MODE");
-      if (e && std::string(e) == "poll") return 0;
+      if (e && std::string(e) == "spin") return 1;
       if (e && std::string(e) == "block") return 2;
-      return 1;
+      return 0;
     }();
     return m;
   }
