@@ -556,7 +556,8 @@ def main() -> None:
         gathered = gather_bytes_to_root(b"".join(segs), dev)
         return stats.cpu().numpy(), (sum(len(x) for x in gathered) if gathered else 0)
 
-    from thinvids_amd.models.ratecontrol import BatchRateController, frame_sizes, plan_frame_qps, round_qps
+    from thinvids_amd.models.ratecontrol import (QCOMP, QCOMP_BFRAMES, BatchRateController, frame_sizes,
+                                                 plan_frame_qps, round_qps)
 
     ctl = BatchRateController()
     nominal = args.kbps * 1000.0 * (world * batch * args.gop) / 30.0  # bits per step, whole node
@@ -574,7 +575,7 @@ def main() -> None:
         dist.all_reduce(flat)
         ask, want, u = ctl.request(nominal)
         allb = flat.cpu().numpy().reshape(world * batch, args.gop)
-        plan, _ = plan_frame_qps(list(allb), args.qp, ask)
+        plan, _ = plan_frame_qps(list(allb), args.qp, ask, qcomp=QCOMP_BFRAMES if args.bframes > 1 else QCOMP)
         qall = np.stack([round_qps(p, u) for p in plan])
         predicted[i] = (want, u)
         pass1_bits.append(float(mine.sum()))
