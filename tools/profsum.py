@@ -11,7 +11,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    return name.split("(")[0].replace("tv::gpu::", "").replace("tv::ops::", "")
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("tv::gpu::", "").replace("tv::ops::", "")
 
 
 def main():
