@@ -537,7 +537,7 @@ __global__ void __launch_bounds__(256) k_sgr_search(const uint8_t* __restrict__ 
 // share one LDS word.  LDS ~60 KB.
 constexpr int kLrCh = 64, kLrUw = 96;  // max stripe chunk height, max unit width (round layout)
 constexpr int kLrTw = kLrUw + 6, kLrAw = kLrUw + 2;
-constexpr int kLrThreads = 512, kLrMaxPx = 104 * 96, kLrPer = (kLrMaxPx + kLrThreads - 1) / kLrThreads;  // unit <= 103 x 95
+constexpr int kLrThreads = 1024, kLrMaxPx = 104 * 96, kLrPer = (kLrMaxPx + kLrThreads - 1) / kLrThreads;  // unit <= 103 x 95
 constexpr int kLrBatch = 5;  // tile loads per thread in flight together
 
 // q / d for 0 <= q < 2^20, 1 <= d <= 128 by a float reciprocal: (q + 0.5) / d lies >= 0.5 / d

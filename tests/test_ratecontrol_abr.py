@@ -118,9 +118,11 @@ def test_abr_single_pass_job_hits_target_and_streams(tmp_path, monkeypatch):
         assert len(hevc.decode(hevc.demux_mp4(f.read())["annexb"], coded=False).frames) == 96
 
 
-def test_abr_vbv_repairs_every_segment(tmp_path, monkeypatch):
+@pytest.mark.parametrize("bframes", [1, 4])
+def test_abr_vbv_repairs_every_segment(tmp_path, monkeypatch, bframes):
     """A tight VBV (peak 1.1x the average rate, a buffer of ~0.3 s): the IDR-led segments
-    that underflow it are re-encoded coarser; every segment of the output is compliant."""
+    that underflow it are re-encoded coarser; every segment of the output is compliant (with
+    hierarchical-B segments the buffer is simulated in decoding order)."""
     monkeypatch.setenv("TV_FORCE_CPU", "1")
     from thinvids_amd.parallel.node_job import run_job
 
@@ -128,7 +130,7 @@ def test_abr_vbv_repairs_every_segment(tmp_path, monkeypatch):
     maxrate, buf = kbps * 1.1, kbps * 0.3
     out = str(tmp_path / "v.mp4")
     res = run_job(src, out, software=True, gop=8, segment_frames=8, bitrate_kbps=kbps, rc_mode="abr",
-                  batch_segments=2, vbv_maxrate_kbps=maxrate, vbv_bufsize_kbit=buf)
+                  batch_segments=2, vbv_maxrate_kbps=maxrate, vbv_bufsize_kbit=buf, bframes=bframes)
     v = res["vbv"]
     assert v["checked"] == 8 and v["violations"] == 0 and v["repaired"] >= 1, v
     for seg in _segment_bits(out, 8):

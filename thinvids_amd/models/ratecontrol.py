@@ -84,11 +84,12 @@ def obu_frame_sizes(stream: bytes) -> list[int]:
     return out
 
 
-def frame_sizes(annexb: bytes) -> list[int]:
+def frame_sizes(annexb: bytes, decode_order: bool = False) -> list[int]:
     """Bytes per coded picture of an Annex-B stream in DISPLAY order (parameter sets count
     toward the next picture in decoding order, start codes included; hierarchical-B streams
     are mapped back by their POCs, so the list lines up with a display-order QP map); AV1
-    OBU streams (leading temporal delimiter) are split per temporal unit."""
+    OBU streams (leading temporal delimiter) are split per temporal unit.  `decode_order`:
+    the pictures as they enter the decoder (VBV buffer model)."""
     if annexb[:2] == b"\x12\x00":
         return obu_frame_sizes(annexb)
     out: list[int] = []
@@ -113,6 +114,8 @@ def frame_sizes(annexb: bytes) -> list[int]:
             pending += size
     from .hevc import display_offsets
 
+    if decode_order:
+        return out
     off = display_offsets(annexb)
     if len(off) == len(out) and off.any():
         disp = [0] * len(out)

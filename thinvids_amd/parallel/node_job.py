@@ -581,7 +581,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         bad = {}
         for k, b in got.items():
             vstat["checked"] += 1
-            fb = 8.0 * np.asarray(frame_sizes(b), np.float64)
+            fb = 8.0 * np.asarray(frame_sizes(b, decode_order=True), np.float64)  # VBV: decoding order
             if not vbv_ok(fb, fps * 1.0, maxrate * rung_scale[k[0]], buf * rung_scale[k[0]]):
                 bad[k] = fb
         fixed = set()
@@ -601,7 +601,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             bad = {}
             for k, b in g2.items():
                 got[k], qual[k] = b, q2[k]
-                fb = 8.0 * np.asarray(frame_sizes(b), np.float64)
+                fb = 8.0 * np.asarray(frame_sizes(b, decode_order=True), np.float64)  # VBV: decoding order
                 if vbv_ok(fb, fps, maxrate * rung_scale[k[0]], buf * rung_scale[k[0]]):
                     fixed.add(k)
                 else:
