@@ -170,9 +170,9 @@ class Core {
     if (c.mgop > 1) HIP_OK(hipMalloc(&meout_, 2 * B * nctu_ * sizeof(CtbMeOut)));
     cap_ = g_.ysz + 2 * g_.csz;
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
-    slot_bytes_ = align(B * nctu_ * 12) + align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * nctu_ * 8) +
-                  align(B * nctu_ * 4) + align(B * nctu_ * 4) + align(B * 4) + align(B) + align(B * g_.usz) +
-                  align(B * g_.usz * 4) + align(B * cap_ * 2);
+    slot_bytes_ = align(B * g_.usz) + align(B * g_.usz * 4) + align(B * nctu_ * 8) + align(B * nctu_ * 4) +
+                  align(B * nctu_ * 4) + align(B * 4) + align(B * nctu_ * 12) + align(B) + align(B * g_.usz) +
+                  align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * cap_ * 2);
     HIP_OK(hipHostMalloc(&qhost_, (size_t)c.gop * B, hipHostMallocDefault));
     HIP_OK(hipHostMalloc(&quni_, (size_t)B, hipHostMallocDefault));
     std::memset(quni_, c.qp, (size_t)B);
@@ -280,7 +280,7 @@ class Core {
   };
   // carve one slot buffer (device or host) into its arrays
   struct Parts {
-    uint8_t *cu_log2, *intra, *ipm, *cbf, *dir;
+    uint8_t *flags, *cu_log2, *intra, *ipm, *cbf, *dir;
     int16_t *mv, *mv1;
     unsigned long long* mask_y;
     unsigned* mask_c;
@@ -292,12 +292,13 @@ class Core {
   Parts carve(uint8_t* base) const {
     const long B = cfg_.batch, U = g_.usz;
     Parts p;
+    // D2H order: flags (one byte per unit: the CU's cu_log2 / intra / cbf / dir, packed by
+    // k_pack_flags) .. qp is the head every picture copies; ipm (I pictures) and mv1 (B
+    // pictures) follow; the separate decision planes the kernels write stay on the device
+    // and are re-expanded from the flags into the host slot by each segment's CABAC task.
     uint8_t* q = base;
-    p.cu_log2 = q;
-    p.intra = q + B * U;
-    p.ipm = q + 2 * B * U;
-    p.cbf = q + 3 * B * U;
-    q += align(B * U * 4);
+    p.flags = q;
+    q += align(B * U);
     p.mv = reinterpret_cast<int16_t*>(q);
     q += align(B * U * 4);
     p.mask_y = reinterpret_cast<unsigned long long*>(q);
@@ -312,10 +313,14 @@ class Core {
     q += align(B * nctu_ * 12);
     p.qp = reinterpret_cast<int8_t*>(q);
     q += align(B);
-    // B pictures only (copied to the host only in hierarchical-B streams)
-    p.dir = q;
+    p.ipm = q;
     q += align(B * U);
     p.mv1 = reinterpret_cast<int16_t*>(q);
+    q += align(B * U * 4);
+    p.cu_log2 = q;
+    p.intra = q + B * U;
+    p.cbf = q + 2 * B * U;
+    p.dir = q + 3 * B * U;
     q += align(B * U * 4);
     p.packed = reinterpret_cast<int16_t*>(q);
     p.count = nullptr;  // device count array lives in the scratch below
@@ -358,6 +363,18 @@ class Core {
   // per-CTB counts are consumed by the scan within the same frame: one scratch suffices
   void* coef_count_scratch() const { return count_scratch_; }
 
+  // segment b's decision planes in the host slot from the transferred flag bytes
+  void expand_flags(const Slot& s, int b) const {
+    const Parts p = carve(s.host);
+    const long U = g_.usz, o = b * U;
+    for (long u = 0; u < U; ++u) {
+      const uint8_t f = p.flags[o + u];
+      p.cu_log2[o + u] = (uint8_t)(3 + (f & 3));
+      p.intra[o + u] = (uint8_t)((f >> 2) & 1);
+      p.cbf[o + u] = (uint8_t)((f >> 3) & 7);
+      p.dir[o + u] = (uint8_t)(f >> 6);
+    }
+  }
   // host view of segment b in a slot (compact levels)
   FrameData host_view(const Slot& s, int b, const SliceRefs* refs) const {
     const Parts p = carve(s.host);
@@ -424,7 +441,7 @@ class Core {
     HIP_OK(hipEventRecord(ev, st));
     wait_event(ev);
   }
-  void fetch_slot(Slot& s, int B) {
+  void fetch_slot(Slot& s, int B, int ptype) {
     thread_local hipStream_t ws = nullptr;
     if (!ws) HIP_OK(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
     wait_event(s.ev);
@@ -434,25 +451,20 @@ class Core {
     // moves the whole contiguous header (decision planes .. SAO params) in one copy and all
     // segments' packed levels (back to back) in a second one.
     if (B == cfg_.batch) {
-      const long head = (seq_.mgop > 1 ? reinterpret_cast<uint8_t*>(d.packed) : d.dir) - d.cu_log2;
-      HIP_OK(hipMemcpyAsync(h.cu_log2, d.cu_log2, head, hipMemcpyDeviceToHost, ws));
+      const long head = reinterpret_cast<uint8_t*>(d.qp) + B - d.flags;
+      HIP_OK(hipMemcpyAsync(h.flags, d.flags, head, hipMemcpyDeviceToHost, ws));
     } else {  // partial batch: each plane is laid out for cfg_.batch segments
       HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.qp, d.qp, B, hipMemcpyDeviceToHost, ws));
-      HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
-      if (seq_.mgop > 1) {
-        HIP_OK(hipMemcpyAsync(h.mv1, d.mv1, B * U * 4, hipMemcpyDeviceToHost, ws));
-        HIP_OK(hipMemcpyAsync(h.dir, d.dir, B * U, hipMemcpyDeviceToHost, ws));
-      }
+      HIP_OK(hipMemcpyAsync(h.flags, d.flags, B * U, hipMemcpyDeviceToHost, ws));
+      if (ptype != 2) HIP_OK(hipMemcpyAsync(h.mv, d.mv, B * U * 4, hipMemcpyDeviceToHost, ws));
       if (seq_.sao) HIP_OK(hipMemcpyAsync(h.sao, d.sao, B * nctu_ * 12, hipMemcpyDeviceToHost, ws));
-      for (uint8_t* const* pl : {&h.cu_log2, &h.intra, &h.ipm, &h.cbf}) {
-        const long off = *pl - h.cu_log2;
-        HIP_OK(hipMemcpyAsync(*pl, d.cu_log2 + off, B * U, hipMemcpyDeviceToHost, ws));
-      }
       HIP_OK(hipMemcpyAsync(h.mask_y, d.mask_y, B * nctu_ * 8, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.mask_c, d.mask_c, B * nctu_ * 4, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.offset, d.offset, B * nctu_ * 4, hipMemcpyDeviceToHost, ws));
     }
+    if (ptype == 2) HIP_OK(hipMemcpyAsync(h.ipm, d.ipm, B * U, hipMemcpyDeviceToHost, ws));
+    if (ptype == 0) HIP_OK(hipMemcpyAsync(h.mv1, d.mv1, B * U * 4, hipMemcpyDeviceToHost, ws));
     sleep_sync(ws);
     long groups = 0;
     for (int b = 0; b < B; ++b) groups += h.total[b];
@@ -572,6 +584,7 @@ class Core {
     }
     stage(intra ? "intra" : "inter");
     launch_compact(dec, g_, slot_compact(s), B, stream_);
+    launch_pack_flags(dec, carve(s.dev).flags, g_, B, stream_);
     stage("compact");
     if (seq_.deblock) launch_deblock(cur, dec, g_, B, stream_);
     stage("deblock");
@@ -593,7 +606,7 @@ class Core {
     fetch_->submit([this, &s, B, f] {
       try {
         Range r("engine.d2h");
-        fetch_slot(s, B);
+        fetch_slot(s, B, plan_.pics[f].type);
       } catch (const std::exception& e) {
         fail(e);
         release(s, B + 1);
@@ -606,6 +619,7 @@ class Core {
             Range r("engine.cabac_slice");
             const auto c0 = std::chrono::steady_clock::now();
             const CodedPic& p = plan_.pics[f];
+            expand_flags(s, b);
             write_slice(seq_, host_view(s, b, seq_.mgop > 1 ? &refs_[f] : nullptr), p.disp, p.type == 2,
                         slices_[b][f]);
             entropy_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(

@@ -113,6 +113,18 @@ __global__ void __launch_bounds__(256) k_sb_pack(DecisionSet dec, Geo g, Compact
   }
 }
 
+__global__ void __launch_bounds__(256) k_pack_flags(DecisionSet dec, uint8_t* flags, long n) {
+  for (long u = blockIdx.x * 256L + threadIdx.x; u < n; u += (long)gridDim.x * 256) {
+    const int d = dec.dir ? dec.dir[u] : 1;
+    flags[u] = (uint8_t)((dec.cu_log2[u] - 3) | (dec.intra[u] << 2) | ((dec.cbf[u] & 7) << 3) | (d << 6));
+  }
+}
+
+void launch_pack_flags(DecisionSet dec, uint8_t* flags, const Geo& g, int B, hipStream_t s) {
+  const long n = (long)B * g.usz;
+  k_pack_flags<<<(unsigned)tv_min(1024L, (n + 255) / 256), 256, 0, s>>>(dec, flags, n);
+}
+
 void launch_compact(DecisionSet dec, const Geo& g, CompactSet cs, int B, hipStream_t s) {
   const int nctu = g.wc * g.hc;
   k_sb_count<<<dim3((nctu + 3) / 4, B), 256, 0, s>>>(dec, g, cs);
