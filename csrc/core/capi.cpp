@@ -242,6 +242,12 @@ int tv_decoder_decode_range(void* d, const uint8_t* data, size_t n, int first, i
   return guard([&] { static_cast<HevcDecoder*>(d)->decode_range(data, n, first, count); });
 }
 // header-only probe: geometry + picture count, no slice decoding
+// spatial MV scaling of the B-slice AMVP (8.5.3.2.7), exported for the formula test
+void tv_hevc_scale_mv(int mvx, int mvy, int td, int tb, int* out) {
+  const Mv m = scale_mv(Mv{mvx, mvy}, td, tb);
+  out[0] = m.x;
+  out[1] = m.y;
+}
 // display index - decoding index of every picture (hierarchical-B reordering); returns the
 // picture count (out receives at most cap values)
 int tv_hevc_display_offsets(const uint8_t* data, size_t n, int* out, int cap) {

@@ -1,5 +1,7 @@
 // k_frame.hip — frame-level kernels: synthetic source, PSNR SSE, quarter-pel phase planes,
 // in-loop deblocking.  Batched: blockIdx.z (or .y) selects the segment.
+#include <cstdlib>
+
 #include "gpu_common.h"
 #include "k_encode.h"
 #include "tv/synth.h"
@@ -391,7 +393,7 @@ __device__ __forceinline__ void sao_tile_pos(int i, int& c, int& j) {
 }
 
 __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, Geo g,
-                                                    const int8_t* qp, const RcTables* rc) {
+                                                    const int8_t* qp, const RcTables* rc, int diag) {
   const int tid = threadIdx.x, lane = tid & 63;
   int ctu, b;
   xcd_ctb(ctu, b);
@@ -435,6 +437,12 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
     sv[k] = k < iters ? S[(i / n) * w + i % n] : 0;
   }
   __syncthreads();
+  // timing diagnostics only (TV_DIAG_SAO_STOP=1/2/3: stop after staging / statistics /
+  // decision; the output is then incomplete) -- never set in production
+  if (diag == 1) {
+    if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)(sv[0] + sv[7] + tile[tid]);
+    return;
+  }
   int eo[4][4];
 #pragma unroll
   for (int d = 0; d < 4; ++d)
@@ -485,6 +493,10 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   __shared__ SaoTables tab;
   __shared__ uint32_t prm[3];
   __syncthreads();
+  if (diag == 2) {
+    if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)st[0].eo_n[0][1];
+    return;
+  }
   if (tid < kSaoItems) sao_item(st, lam16, tid, tab);  // 144 offset/cost items in parallel
   __syncthreads();
   if (tid < 96) sao_window(tid, tab);  // 3 x 32 band windows
@@ -511,6 +523,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
     o[1] = prm[1];
     o[2] = prm[2];
   }
+  if (diag == 3) return;
   __syncthreads();
   // the SAO'd CTB from the tile: luma 1024 + 2 x 256 chroma samples, 6 per thread
   for (int i = tid; i < 1024 + 512; i += 256) {
@@ -533,7 +546,11 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
 
 void launch_sao(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, const int8_t* qp, const RcTables* rc,
                 const Geo& g, int B, hipStream_t s) {
-  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, out, sao, g, qp, rc);
+  static const int diag = [] {
+    const char* e = std::getenv("TV_DIAG_SAO_STOP");
+    return e ? std::atoi(e) : 0;
+  }();
+  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, out, sao, g, qp, rc, diag);
 }
 
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int B, hipStream_t s) {

@@ -224,3 +224,61 @@ def test_bframes_frame_sizes_display_order_and_spec_plumbing():
     assert EncodeSpec(96, 64, bframes=8).hevc_bframes() == 8
     assert EncodeSpec(96, 64, bframes=8, crf=27).hevc_bframes() == 1
     assert [_pow2(n) for n in (0, 1, 3, 4, 7, 8, 40)] == [1, 1, 2, 4, 4, 8, 16]
+
+
+def _scale_mv_spec(mv, td, tb):
+    """H.265 8.5.3.2.7 (8-179..8-183) transcribed independently of csrc/: C division
+    truncates toward zero."""
+    def cdiv(a, b):
+        q = abs(a) // abs(b)
+        return q if (a >= 0) == (b >= 0) else -q
+
+    td = max(-128, min(127, td))
+    tb = max(-128, min(127, tb))
+    tx = cdiv(16384 + (abs(td) >> 1), td)
+    dsf = max(-4096, min(4095, (tb * tx + 32) >> 6))
+    out = []
+    for v in mv:
+        p = dsf * v
+        s = -1 if p < 0 else 1
+        out.append(max(-32768, min(32767, s * ((abs(p) + 127) >> 8))))
+    return out
+
+
+def test_amvp_spatial_scaling_matches_spec_formula():
+    import ctypes as C
+
+    from thinvids_amd._native import core_lib
+
+    f = core_lib().tv_hevc_scale_mv
+    f.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_int)]
+    rng = np.random.default_rng(3)
+    out = (C.c_int * 2)()
+    cases = [((7, -3), 2, -2), ((-64, 33), -4, 4), ((1, 1), 1, 3), ((5000, -4000), 3, -1), ((-1, 0), -8, 7),
+             ((32767, -32768), 1, 127)]
+    cases += [((int(a), int(b)), int(td), int(tb)) for a, b, td, tb in
+              zip(rng.integers(-2000, 2000, 200), rng.integers(-2000, 2000, 200), rng.choice([-16, -8, -4, -3, -2, -1, 1, 2, 3, 4, 8, 16], 200),
+                  rng.choice([-16, -8, -4, -3, -2, -1, 1, 2, 3, 4, 8, 16], 200))]
+    for mv, td, tb in cases:
+        f(mv[0], mv[1], td, tb, out)
+        assert list(out) == _scale_mv_spec(mv, td, tb), (mv, td, tb)
+
+
+def test_bframes_multi_segment_mp4_order(tmp_path):
+    """Two hierarchical-B segments muxed into one MP4 (streaming writer and whole-file
+    muxer): composition offsets restart at every IDR and the file decodes to the display
+    order of both segments."""
+    frames = [hevc.synth_frame(6, t, 96, 64) for t in range(14)]
+    segs = [hevc.encode_sequence_cpu(frames[a:b], qp=30, bframes=4, search_range=16)[0] for a, b in ((0, 9), (9, 14))]
+    ref = hevc.decode(b"".join(segs)).frames
+    assert len(ref) == 14
+    p = str(tmp_path / "m.mp4")
+    hevc.mux_mp4_file(segs, 96, 64, 30, 1, p)
+    with open(p, "rb") as fh:
+        dm = hevc.demux_mp4(fh.read())
+    assert dm["frames"] == 14
+    got = hevc.decode(dm["annexb"]).frames
+    for a, b in zip(ref, got):
+        np.testing.assert_array_equal(a[0], b[0])
+    for i in range(14):  # display order == source order (the two segments' pictures interleave right)
+        assert hevc.psnr(frames[i][0], got[i][0]) > 30
