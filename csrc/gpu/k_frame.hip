@@ -402,7 +402,11 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   __shared__ SaoStats st[3];
   __shared__ int16_t tile[kSaoTile];  // luma 34 x 34, then Cb, Cr 18 x 18
   __shared__ int bpos[3];
+  // band statistics: a packed (sum * 2048 + count) histogram per component with 16 copies
+  // (lane & 15), so same-band lanes of a wave rarely hit one LDS address
+  __shared__ int bh[3][32][16];
   for (int i = tid; i < 3 * (int)(sizeof(SaoStats) / 4); i += 256) reinterpret_cast<int*>(st)[i] = 0;
+  for (int i = tid; i < 3 * 32 * 16; i += 256) (&bh[0][0][0])[i] = 0;
   {
     int16_t v[kSaoStage];
 #pragma unroll
@@ -464,21 +468,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
 #pragma unroll
       for (int q = 0; q < 4; ++q) eo[d][q] += cat == q + 1 ? packed : 0;
     }
-    // band statistics: one reduction per distinct band in the wave (ballot + readlane)
-    const int band = v >> 3;
-    bool pending = true;
-    for (;;) {
-      const unsigned long long m = __ballot(pending);
-      if (m == 0) break;
-      const int bsel = __builtin_amdgcn_readlane(band, __ffsll((long long)m) - 1);
-      const bool mine = pending && band == bsel;
-      const int tot = wave_sum(mine ? packed : 0);
-      if (lane == 0) {
-        atomicAdd(&st[c].bo_n[bsel], tot & 2047);
-        atomicAdd(&st[c].bo_s[bsel], (tot - (tot & 2047)) / 2048);
-      }
-      pending = pending && !mine;
-    }
+    atomicAdd(&bh[c][v >> 3][lane & 15], packed);  // band statistics
   }
 #pragma unroll
   for (int d = 0; d < 4; ++d)
@@ -492,6 +482,15 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
     }
   __shared__ SaoTables tab;
   __shared__ uint32_t prm[3];
+  __syncthreads();
+  if (tid < 96) {  // fold the histogram copies into the band counters
+    const int cc = tid >> 5, band = tid & 31;
+    int tot = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tot += bh[cc][band][k];
+    st[cc].bo_n[band] = tot & 2047;
+    st[cc].bo_s[band] = (tot - (tot & 2047)) / 2048;
+  }
   __syncthreads();
   if (diag == 2) {
     if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)st[0].eo_n[0][1];
