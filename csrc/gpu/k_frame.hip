@@ -407,23 +407,39 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   __shared__ int bh[3][32][16];
   for (int i = tid; i < 3 * (int)(sizeof(SaoStats) / 4); i += 256) reinterpret_cast<int*>(st)[i] = 0;
   for (int i = tid; i < 3 * 32 * 16; i += 256) (&bh[0][0][0])[i] = 0;
-  {
-    int16_t v[kSaoStage];
+  {  // deblocked CTB + 1-sample ring as aligned dwords (a CTB edge is a multiple of 4, so a
+     // dword is wholly inside or wholly outside the plane): luma 34 rows x 10 dwords, chroma
+     // 18 x 6 each; every load is issued before the first LDS store
+    constexpr int kL = 34 * 10, kC = 18 * 6, kItems = kL + 2 * kC, kPer = (kItems + 255) / 256;
+    uint32_t v[kPer], inside = 0;
 #pragma unroll
-    for (int k = 0; k < kSaoStage; ++k) {
+    for (int k = 0; k < kPer; ++k) {
       const int i = tid + 256 * k;
-      v[k] = -1;
-      if (i < kSaoTile) {
-        int c, j;
-        sao_tile_pos(i, c, j);
-        const int T = c ? kSaoTc : kSaoT, n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
-        const int x = cx * n + j % T - 1, y = cy * n + j / T - 1;
-        if (x >= 0 && y >= 0 && x < w && y < h) v[k] = (int16_t)deb.plane(c, b, g)[y * w + x];
+      v[k] = 0;
+      if (i < kItems) {
+        const int c = i < kL ? 0 : (i < kL + kC ? 1 : 2), j = c == 0 ? i : i - kL - (c - 1) * kC;
+        const int nd = c ? 6 : 10, n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
+        const int x = cx * n - 4 + 4 * (j % nd), y = cy * n - 1 + j / nd;
+        if (x >= 0 && x < w && y >= 0 && y < h) {
+          v[k] = *reinterpret_cast<const uint32_t*>(deb.plane(c, b, g) + (long)y * w + x);
+          inside |= 1u << k;
+        }
       }
     }
 #pragma unroll
-    for (int k = 0; k < kSaoStage; ++k)
-      if (tid + 256 * k < kSaoTile) tile[tid + 256 * k] = v[k];
+    for (int k = 0; k < kPer; ++k) {
+      const int i = tid + 256 * k;
+      if (i >= kItems) continue;
+      const int c = i < kL ? 0 : (i < kL + kC ? 1 : 2), j = c == 0 ? i : i - kL - (c - 1) * kC;
+      const int nd = c ? 6 : 10, T = c ? kSaoTc : kSaoT;
+      int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
+      const int row = j / nd, col0 = 4 * (j % nd) - 3;  // tile column of the dword's first byte
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int col = col0 + q;
+        if (col >= 0 && col < T) t[row * T + col] = (inside >> k) & 1 ? (int16_t)((v[k] >> (8 * q)) & 255) : (int16_t)-1;
+      }
+    }
   }
   // one region per wave: waves 0/1 = luma rows 0-15 / 16-31 (8 samples per lane), wave 2 =
   // Cb, wave 3 = Cr (4 per lane).  Counts and sums travel packed as sum * 2048 + count
@@ -524,22 +540,27 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   }
   if (diag == 3) return;
   __syncthreads();
-  // the SAO'd CTB from the tile: luma 1024 + 2 x 256 chroma samples, 6 per thread
-  for (int i = tid; i < 1024 + 512; i += 256) {
-    const int cc = i < 1024 ? 0 : (i < 1280 ? 1 : 2);
-    const int j = cc == 0 ? i : i - 1024 - (cc - 1) * 256;
-    const int nn = cc ? 16 : 32, TT = cc ? kSaoTc : kSaoT, ww = cc ? g.W / 2 : g.W;
-    const int lx = j % nn, ly = j / nn;
+  // the SAO'd CTB from the tile, 4 samples per dword store: luma 32 rows x 8, chroma 16 x 4
+  for (int i = tid; i < 256 + 128; i += 256) {
+    const int cc = i < 256 ? 0 : (i < 320 ? 1 : 2);
+    const int j = cc == 0 ? i : i - 256 - (cc - 1) * 64;
+    const int nd = cc ? 4 : 8, nn = cc ? 16 : 32, TT = cc ? kSaoTc : kSaoT, ww = cc ? g.W / 2 : g.W;
+    const int ly = j / nd, lx0 = 4 * (j % nd);
     const int16_t* tt = tile + (cc == 0 ? 0 : kSaoT * kSaoT + (cc - 1) * kSaoTc * kSaoTc);
     const uint32_t p = prm[cc];
-    const int v = tt[(ly + 1) * TT + lx + 1];
-    int r = v;
-    if (sao_type(p)) {
-      int dx = 0, dy = 0;
-      if (sao_type(p) == 2) sao_eo_dir(sao_class(p), dx, dy);
-      r = sao_sample_nb(v, tt[(ly + 1 + dy) * TT + lx + 1 + dx], tt[(ly + 1 - dy) * TT + lx + 1 - dx], p);
+    int dx = 0, dy = 0;
+    if (sao_type(p) == 2) sao_eo_dir(sao_class(p), dx, dy);
+    uint32_t word = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int lx = lx0 + q;
+      const int v = tt[(ly + 1) * TT + lx + 1];
+      const int r = sao_type(p) ? sao_sample_nb(v, tt[(ly + 1 + dy) * TT + lx + 1 + dx],
+                                                tt[(ly + 1 - dy) * TT + lx + 1 - dx], p)
+                                : v;
+      word |= (uint32_t)r << (8 * q);
     }
-    out.plane(cc, b, g)[(long)(cy * nn + ly) * ww + cx * nn + lx] = (uint8_t)r;
+    *reinterpret_cast<uint32_t*>(out.plane(cc, b, g) + (long)(cy * nn + ly) * ww + cx * nn + lx0) = word;
   }
 }
 
