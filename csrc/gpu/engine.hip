@@ -588,13 +588,13 @@ class Core {
     stage("compact");
     if (seq_.deblock) launch_deblock(cur, dec, g_, B, stream_);
     stage("deblock");
-    if (seq_.sao) launch_sao(src_, cur, fin_set, carve(s.dev).sao, dec.qp, rc_, g_, B, stream_);
+    if (seq_.sao) launch_sao(src_, cur, fin_set, carve(s.dev).sao, dec.qp, rc_, g_, B, stream_, d_sse_);
     stage("sao");
     cur_e.disp = pic.disp;
     if (pic.disp == F - 1) last_entry_ = e;
     if (pic.referenced) launch_phase_planes(fin_set, cur_e.phase, g_, B, stream_);  // a later picture's reference
     stage("phase_planes");
-    launch_sse(src_, fin_set, g_, d_sse_, B, stream_);
+    if (!seq_.sao) launch_sse(src_, fin_set, g_, d_sse_, B, stream_);  // with SAO: summed by k_sao_decide
     stage("sse");
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(s.ev, stream_));

@@ -71,7 +71,7 @@ void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int B, hipStrea
 // SAO: per-CTB statistics (source vs deblocked `deb`) + RD decision into `sao` (3 packed
 // words per CTB, B x nctu x 3), then the filter from `deb` into `out` (every sample written).
 void launch_sao(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, const int8_t* qp, const RcTables* rc,
-                const Geo& g, int B, hipStream_t s);
+                const Geo& g, int B, hipStream_t s, unsigned long long* sse = nullptr);  // sse: + SSE vs src
 
 // Compact (non-zero 4x4 groups only) level representation for the D2H transfer.
 struct CompactSet {

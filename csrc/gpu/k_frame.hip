@@ -393,7 +393,8 @@ __device__ __forceinline__ void sao_tile_pos(int i, int& c, int& j) {
 }
 
 __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, Geo g,
-                                                    const int8_t* qp, const RcTables* rc, int diag) {
+                                                    const int8_t* qp, const RcTables* rc, int diag,
+                                                    unsigned long long* sse) {
   const int tid = threadIdx.x, lane = tid & 63;
   int ctu, b;
   xcd_ctb(ctu, b);
@@ -540,7 +541,9 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   }
   if (diag == 3) return;
   __syncthreads();
-  // the SAO'd CTB from the tile, 4 samples per dword store: luma 32 rows x 8, chroma 16 x 4
+  // the SAO'd CTB from the tile, 4 samples per dword store: luma 32 rows x 8, chroma 16 x 4;
+  // the squared error against the source (display area) is summed on the way (no k_sse)
+  unsigned e2[3] = {0, 0, 0};
   for (int i = tid; i < 256 + 128; i += 256) {
     const int cc = i < 256 ? 0 : (i < 320 ? 1 : 2);
     const int j = cc == 0 ? i : i - 256 - (cc - 1) * 64;
@@ -560,17 +563,39 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
                                 : v;
       word |= (uint32_t)r << (8 * q);
     }
-    *reinterpret_cast<uint32_t*>(out.plane(cc, b, g) + (long)(cy * nn + ly) * ww + cx * nn + lx0) = word;
+    const long at = (long)(cy * nn + ly) * ww + cx * nn + lx0;
+    *reinterpret_cast<uint32_t*>(out.plane(cc, b, g) + at) = word;
+    const int dwc = cc ? g.dw / 2 : g.dw, dhc = cc ? g.dh / 2 : g.dh;
+    if (sse && cy * nn + ly < dhc) {
+      const uint32_t sw = *reinterpret_cast<const uint32_t*>(src.plane(cc, b, g) + at);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = (int)((sw >> (8 * q)) & 255) - (int)((word >> (8 * q)) & 255);
+        e2[cc] += cx * nn + lx0 + q < dwc ? (unsigned)(d * d) : 0u;
+      }
+    }
+  }
+  if (sse) {
+    __shared__ unsigned long long esum[3];
+    if (tid < 3) esum[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int c2 = 0; c2 < 3; ++c2) {
+      const int t = wave_sum((int)e2[c2]);  // <= 2 dwords x 4 x 65025 per lane: fits
+      if (lane == 0 && t) atomicAdd(&esum[c2], (unsigned long long)(unsigned)t);
+    }
+    __syncthreads();
+    if (tid < 3 && esum[tid]) atomicAdd(sse + b * 3 + tid, esum[tid]);
   }
 }
 
 void launch_sao(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, const int8_t* qp, const RcTables* rc,
-                const Geo& g, int B, hipStream_t s) {
+                const Geo& g, int B, hipStream_t s, unsigned long long* sse) {
   static const int diag = [] {
     const char* e = std::getenv("TV_DIAG_SAO_STOP");
     return e ? std::atoi(e) : 0;
   }();
-  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, out, sao, g, qp, rc, diag);
+  k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, out, sao, g, qp, rc, diag, sse);
 }
 
 void launch_deblock(FrameSet rec, DecisionSet dec, const Geo& g, int B, hipStream_t s) {
