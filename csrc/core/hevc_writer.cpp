@@ -6,6 +6,7 @@
 // the GPU analysis fully parallel while the serial CABAC runs on CPU threads — the
 // MI355X-native split of the reference's single ffmpeg call (reference
 // worker/tasks.py:1532-1586).
+#include <emmintrin.h>
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -556,31 +557,22 @@ class SliceWriter {
         }
       return;
     }
+    // a TB (= CU) never straddles a CTB: its groups are a rectangle of the CTB's group mask
+    // (luma 8 groups per row; Cb / Cr 4 per row at bit 0 / 16), pointers only for set bits
     v.stride = 4;
-    for (int ys = 0; ys < nsb; ++ys)
-      for (int xs = 0; xs < nsb; ++xs) {
-        const int X = x + 4 * xs, Y = y + 4 * ys;
-        int ctb, bit;
-        if (c == 0) {
-          ctb = (Y >> 5) * fd_.wc + (X >> 5);
-          bit = ((Y & 31) >> 2) * 8 + ((X & 31) >> 2);
-        } else {
-          ctb = (Y >> 4) * fd_.wc + (X >> 4);
-          bit = ((Y & 15) >> 2) * 4 + ((X & 15) >> 2) + (c == 2 ? 16 : 0);
-        }
-        const uint64_t my = fd_.sb_mask_y[ctb];
-        const uint32_t mc = fd_.sb_mask_c[ctb];
-        int rank;
-        if (c == 0) {
-          if (!((my >> bit) & 1)) continue;
-          rank = __builtin_popcountll(my & ((1ull << bit) - 1));
-        } else {
-          if (!((mc >> bit) & 1)) continue;
-          rank = __builtin_popcountll(my) + __builtin_popcount(mc & ((1u << bit) - 1));
-        }
-        v.sb[ys * nsb + xs] = fd_.sb_packed + ((size_t)fd_.sb_offset[ctb] + rank) * 16;
-        v.nz |= 1ull << (ys * nsb + xs);
-      }
+    const int sh = c ? 4 : 5, gw = c ? 4 : 8;
+    const int ctb = (y >> sh) * fd_.wc + (x >> sh);
+    const uint64_t my = fd_.sb_mask_y[ctb];
+    const uint64_t m = c ? (uint64_t)fd_.sb_mask_c[ctb] : my;
+    const int base = (c == 2 ? 16 : 0) + ((y & ((1 << sh) - 1)) >> 2) * gw + ((x & ((1 << sh) - 1)) >> 2);
+    const uint64_t row = (1ull << nsb) - 1;
+    for (int ys = 0; ys < nsb; ++ys) v.nz |= ((m >> (base + ys * gw)) & row) << (ys * nsb);
+    const int16_t* groups = fd_.sb_packed + (size_t)fd_.sb_offset[ctb] * 16;
+    const int skip = c ? __builtin_popcountll(my) : 0;
+    for (uint64_t b = v.nz; b; b &= b - 1) {
+      const int r = __builtin_ctzll(b), bit = base + (r >> (log2N - 2)) * gw + (r & (nsb - 1));
+      v.sb[r] = groups + (size_t)(skip + __builtin_popcountll(m & ((1ull << bit) - 1))) * 16;
+    }
   }
 
   void write_last_prefix(int pos, int log2N, int cIdx, int base) {
@@ -637,8 +629,24 @@ class SliceWriter {
   // sigCtx pattern (0..2) of the 16 scan positions for each prevCsbf (H.265 9.3.4.2.5),
   // precomputed per scanIdx so the per-coefficient context is one table lookup.
   struct SigPattern {
-    uint8_t p[3][4][16];
+    uint8_t p[3][4][16], p4[3][16];  // p4: 4x4 TBs (ctxIdxMap of the position)
+    uint16_t lo[3][256], hi[3][256];  // raster non-zero mask (bit y * 4 + x) -> scan-order mask
     SigPattern() {
+      for (int sc = 0; sc < 3; ++sc) {
+        int inv[16];
+        for (int n = 0; n < 16; ++n) {
+          p4[sc][n] = kCtxIdxMap4x4[in_sb_scan(sc)[n]];
+          inv[in_sb_scan(sc)[n]] = n;
+        }
+        for (int v = 0; v < 256; ++v) {
+          lo[sc][v] = hi[sc][v] = 0;
+          for (int j = 0; j < 8; ++j)
+            if ((v >> j) & 1) {
+              lo[sc][v] |= (uint16_t)(1u << inv[j]);
+              hi[sc][v] |= (uint16_t)(1u << inv[j + 8]);
+            }
+        }
+      }
       for (int sc = 0; sc < 3; ++sc)
         for (int pc = 0; pc < 4; ++pc)
           for (int n = 0; n < 16; ++n) {
@@ -653,31 +661,53 @@ class SliceWriter {
     }
   };
 
+  // Sub-block scan of each TB size / scanIdx: raster index (ys * nsb + xs) of scan position
+  // i, and the scan position of each raster index.
+  struct SbScan {
+    uint8_t pos[4][3][64], inv[4][3][64];
+    SbScan() {
+      for (int l = 0; l < 4; ++l)
+        for (int sc = 0; sc < 3; ++sc)
+          for (int i = 0; i < (1 << (2 * l)); ++i) {
+            int xs, ys;
+            subblock_pos(l + 2, sc, i, xs, ys);
+            pos[l][sc][i] = (uint8_t)((ys << l) + xs);
+            inv[l][sc][(ys << l) + xs] = (uint8_t)i;
+          }
+    }
+  };
+
   void residual(const TbView& v, int log2N, int cIdx, int scanIdx) {
     static const SigPattern kPat;
+    static const SbScan kSb;
     const int nsb = 1 << (log2N - 2);  // sub-blocks per side
-    const int numSb = nsb * nsb;
     const uint8_t* ps = in_sb_scan(scanIdx);
+    const uint8_t* sbpos = kSb.pos[log2N - 2][scanIdx];
+    const uint8_t* sbinv = kSb.inv[log2N - 2][scanIdx];
     int off[16];
     for (int n = 0; n < 16; ++n) off[n] = (ps[n] >> 2) * v.stride + (ps[n] & 3);
-    // last significant coefficient in scan order: the last non-zero sub-block, then its last
-    // non-zero scan position
+    // last significant coefficient in scan order: the non-zero sub-block latest in scan
+    // order, then its last non-zero scan position
     if (!v.nz) throw std::runtime_error("residual_coding of an all-zero block");
-    int lastSb = -1, lastN = -1;
-    for (int i = numSb - 1; i >= 0; --i) {
-      int xs, ys;
-      subblock_pos(log2N, scanIdx, i, xs, ys);
-      if (!((v.nz >> (ys * nsb + xs)) & 1)) continue;
-      const int16_t* b = v.sb[ys * nsb + xs];
-      unsigned m = 0;
-      for (int n = 0; n < 16; ++n) m |= (unsigned)(b[off[n]] != 0) << n;
-      lastSb = i;
-      lastN = 31 - __builtin_clz(m);
-      break;
-    }
+    int lastSb = 0;
+    for (uint64_t b = v.nz; b; b &= b - 1) lastSb = tv_max(lastSb, (int)sbinv[__builtin_ctzll(b)]);
+    auto sig_mask = [&](const int16_t* b) {  // bit n: scan position n is non-zero
+      // four rows of four levels -> 16 bytes (saturating: non-zero stays non-zero) -> raster
+      // mask -> scan order through two byte tables
+      const size_t st = (size_t)v.stride;
+      const __m128i r01 = _mm_unpacklo_epi64(_mm_loadl_epi64((const __m128i*)b),
+                                             _mm_loadl_epi64((const __m128i*)(b + st)));
+      const __m128i r23 = _mm_unpacklo_epi64(_mm_loadl_epi64((const __m128i*)(b + 2 * st)),
+                                             _mm_loadl_epi64((const __m128i*)(b + 3 * st)));
+      const __m128i z = _mm_cmpeq_epi8(_mm_packs_epi16(r01, r23), _mm_setzero_si128());
+      const unsigned raster = ~(unsigned)_mm_movemask_epi8(z) & 0xffffu;
+      return (unsigned)(kPat.lo[scanIdx][raster & 255] | kPat.hi[scanIdx][raster >> 8]);
+    };
+    const unsigned lastMask = sig_mask(v.sb[sbpos[lastSb]]);
+    const int lastN = 31 - __builtin_clz(lastMask);
     {
-      int xs, ys, xc, yc;
-      subblock_pos(log2N, scanIdx, lastSb, xs, ys);
+      const int xs = sbpos[lastSb] & (nsb - 1), ys = sbpos[lastSb] >> (log2N - 2);
+      int xc, yc;
       coef_pos_in_sb(scanIdx, lastN, xc, yc);
       int lx = (xs << 2) + xc, ly = (ys << 2) + yc;
       if (scanIdx == 2) std::swap(lx, ly);
@@ -689,61 +719,42 @@ class SliceWriter {
     // context offset added to the 0..2 pattern (H.265 9.3.4.2.5), per sub-block class
     const int sizeOff = log2N == 3 ? (scanIdx == 0 ? 9 : 15) : (cIdx == 0 ? 21 : 12);
     const int compOff = CTX_SIG + (cIdx ? 27 : 0);
-    uint8_t csbf[8][8];
-    std::memset(csbf, 0, sizeof(csbf));
+    uint64_t coded = 0;  // coded_sub_block_flag per raster sub-block (1 = coded / inferred)
     int c1 = 1;
     for (int i = lastSb; i >= 0; --i) {
-      int xs, ys;
-      subblock_pos(log2N, scanIdx, i, xs, ys);
-      const bool any = (v.nz >> (ys * nsb + xs)) & 1;
-      int vals[16];
-      if (any) {
-        const int16_t* b = v.sb[ys * nsb + xs];
-        for (int n = 0; n < 16; ++n) vals[n] = b[off[n]];
-      } else {
-        std::memset(vals, 0, sizeof(vals));  // DC sub-block: coded (inferred) even when empty
-      }
+      const int r = sbpos[i], xs = r & (nsb - 1), ys = r >> (log2N - 2);
+      const bool any = (v.nz >> r) & 1;
+      // csbf of the right / lower neighbours (both later in scan order, already decided)
+      const int right = xs < nsb - 1 ? (int)((coded >> (r + 1)) & 1) : 0;
+      const int below = ys < nsb - 1 ? (int)((coded >> (r + nsb)) & 1) : 0;
       bool inferDc = false;
       if (i < lastSb && i > 0) {
-        int ctx = 0;
-        if (xs < nsb - 1) ctx += csbf[xs + 1][ys];
-        if (ys < nsb - 1) ctx += csbf[xs][ys + 1];
-        ctx = ctx > 1 ? 1 : ctx;
-        bin(any ? 1 : 0, CTX_CSBF + ctx + (cIdx ? 2 : 0));
-        csbf[xs][ys] = any ? 1 : 0;
+        bin(any ? 1 : 0, CTX_CSBF + (right | below) + (cIdx ? 2 : 0));
+        if (!any) continue;
         inferDc = true;
-      } else {
-        csbf[xs][ys] = 1;
       }
-      if (!csbf[xs][ys]) continue;
+      coded |= 1ull << r;
+      // DC sub-block: coded (inferred) even when empty
+      const int16_t* b = any ? v.sb[r] : nullptr;
+      const unsigned m = i == lastSb ? lastMask : (any ? sig_mask(b) : 0u);
       // significance
-      int prevCsbf = 0;
-      if (xs < nsb - 1) prevCsbf += csbf[xs + 1][ys];
-      if (ys < nsb - 1) prevCsbf += csbf[xs][ys + 1] << 1;
-      int ctxs[16];
-      if (log2N == 2) {
-        for (int n = 0; n < 16; ++n) ctxs[n] = compOff + kCtxIdxMap4x4[ps[n]];
-      } else {
-        const uint8_t* pat = kPat.p[scanIdx][prevCsbf];
-        const int add = compOff + sizeOff + ((cIdx == 0 && i > 0) ? 3 : 0);
-        for (int n = 0; n < 16; ++n) ctxs[n] = add + pat[n];
-        if (i == 0) ctxs[0] = compOff;  // DC of the TB
-      }
+      const int prevCsbf = right + (below << 1);
+      const uint8_t* pat = log2N == 2 ? kPat.p4[scanIdx] : kPat.p[scanIdx][prevCsbf];
+      const int add = log2N == 2 ? compOff : compOff + sizeOff + ((cIdx == 0 && i > 0) ? 3 : 0);
       const int nStart = (i == lastSb) ? lastN - 1 : 15;
-      for (int n = nStart; n >= 0; --n) {
-        if (n == 0 && inferDc) break;  // DC inferred significant
-        const int sig = vals[n] != 0;
-        bin(sig, ctxs[n]);
-        if (sig) inferDc = false;
-      }
-      // levels
+      const bool dcInferred = inferDc && (m & ((2u << nStart) - 2)) == 0;
+      for (int n = nStart; n >= 1; --n) bin((m >> n) & 1, add + pat[n]);
+      if (nStart >= 0 && !dcInferred)  // the TB's DC has its own context
+        bin(m & 1, (log2N > 2 && i == 0) ? compOff : add + pat[0]);
+      // levels, in reverse scan order
       int absv[16], signs[16], cnt = 0;
-      for (int n = 15; n >= 0; --n)
-        if (vals[n]) {
-          absv[cnt] = vals[n] < 0 ? -vals[n] : vals[n];
-          signs[cnt] = vals[n] < 0;
-          ++cnt;
-        }
+      for (unsigned s = m; s; ++cnt) {
+        const int n = 31 - __builtin_clz(s);
+        s &= ~(1u << n);
+        const int x = b[off[n]];
+        absv[cnt] = x < 0 ? -x : x;
+        signs[cnt] = x < 0;
+      }
       int ctxSet = (i > 0 && cIdx == 0) ? 2 : 0;
       if (c1 == 0) ++ctxSet;
       c1 = 1;

@@ -558,9 +558,8 @@ TV_HD int scan_idx_for(bool intra, int log2TrafoSize, int cIdx, int predMode) {
 
 // z-order index of a 4x4 unit inside a 32x32 CTB (x4,y4 in 0..7)
 TV_HD int zorder4(int x4, int y4) {
-  int z = 0;
-  for (int b = 0; b < 3; ++b) z |= (((x4 >> b) & 1) << (2 * b)) | (((y4 >> b) & 1) << (2 * b + 1));
-  return z;
+  // bit interleave x2 y2 x1 y1 x0 y0 -> y2 x2 y1 x1 y0 x0
+  return (x4 & 1) | ((y4 & 1) << 1) | ((x4 & 2) << 1) | ((y4 & 2) << 2) | ((x4 & 4) << 2) | ((y4 & 4) << 3);
 }
 
 // Availability of luma location (xN,yN) for the block at (xC,yC) (H.265 6.4.1), for a

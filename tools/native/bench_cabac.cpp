@@ -91,13 +91,17 @@ int main(int argc, char** argv) {
     }
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
     size_t bytes = 0;
-    auto t0 = std::chrono::steady_clock::now();
+    double ms = 1e30, sum = 0;  // best and mean of the repetitions (the host is shared: min is stable)
     for (int r = 0; r < reps; ++r) {
       out.clear();
+      auto t0 = std::chrono::steady_clock::now();
       bytes = write_slice(cfg, f, t, t == 0, out);
+      const double d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      ms = d < ms ? d : ms;
+      sum += d;
     }
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / reps;
-    printf("frame %d (%s): %zu bytes, %.3f ms / slice, %.1f MB/s\n", t, t ? "P" : "I", bytes, ms, bytes / ms / 1e3);
+    printf("frame %d (%s): %zu bytes, %.3f ms / slice (min), %.3f mean, %.1f MB/s\n", t, t ? "P" : "I", bytes, ms,
+           sum / reps, bytes / ms / 1e3);
   }
   return 0;
 }
