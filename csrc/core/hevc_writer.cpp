@@ -303,6 +303,52 @@ class SliceWriter {
     return true;
   }
 
+  // Index of `mv` in the P-slice merge list of the 2Nx2N PU at (x0, y0) (the list of
+  // merge_candidates(), hevc_codec.h, 8.5.3.2.2-3), or -1: the list is built in order and the
+  // search stops at the first match.  A1, B1 and B2 precede the PU in z-scan whenever they
+  // are inside the picture, so only B0 and A0 need the z-scan availability test.
+  int merge_index_p(int x0, int y0, int N, Mv mv) const {
+    const int maxc = cfg_.max_merge_cand;
+    auto get = [&](int xn, int yn, Mv& m) {
+      const int u = unit(xn, yn);
+      if (fd_.intra[u]) return false;
+      m.x = fd_.mv[2 * u];
+      m.y = fd_.mv[2 * u + 1];
+      return true;
+    };
+    Mv a1, b1, b0, a0, b2;
+    int n = 0;
+    const bool avA1 = x0 > 0 && get(x0 - 1, y0 + N - 1, a1);
+    if (avA1) {
+      if (a1 == mv) return 0;
+      if (++n == maxc) return -1;
+    }
+    const bool avB1 = y0 > 0 && get(x0 + N - 1, y0 - 1, b1);
+    const bool fB1 = avB1 && !(avA1 && a1 == b1);
+    if (fB1) {
+      if (b1 == mv) return n;
+      if (++n == maxc) return -1;
+    }
+    const bool avB0 = avail(x0, y0, x0 + N, y0 - 1) && get(x0 + N, y0 - 1, b0);
+    const bool fB0 = avB0 && !(avB1 && b1 == b0);
+    if (fB0) {
+      if (b0 == mv) return n;
+      if (++n == maxc) return -1;
+    }
+    const bool avA0 = avail(x0, y0, x0 - 1, y0 + N) && get(x0 - 1, y0 + N, a0);
+    const bool fA0 = avA0 && !(avA1 && a1 == a0);
+    if (fA0) {
+      if (a0 == mv) return n;
+      if (++n == maxc) return -1;
+    }
+    const bool avB2 = x0 > 0 && y0 > 0 && get(x0 - 1, y0 - 1, b2);
+    if (avB2 && !(avA1 && a1 == b2) && !(avB1 && b1 == b2) && (int)avA1 + (int)fB1 + (int)fB0 + (int)fA0 < 4) {
+      if (b2 == mv) return n;
+      if (++n == maxc) return -1;
+    }
+    return (mv.x == 0 && mv.y == 0) ? n : -1;  // zero candidates fill the list
+  }
+
   Motion motion_of(int u) const {
     Motion m;
     m.dir = fd_.dir ? fd_.dir[u] : 1;
@@ -387,18 +433,8 @@ class SliceWriter {
       bin(1, CTX_PRED_MODE);
     } else if (!islice_) {
       // decide skip / merge / amvp from the motion field
-      int merge_idx = -1;
       Mv mv{fd_.mv[2 * u], fd_.mv[2 * u + 1]};
-      if (!intra) {
-        Mv cand[5];
-        auto f = [&](int xn, int yn, Mv& m) { return inter_at(x0, y0, xn, yn, m); };
-        const int nc = merge_candidates(x0, y0, N, N, cfg_.max_merge_cand, f, cand);
-        for (int i = 0; i < nc; ++i)
-          if (cand[i] == mv) {
-            merge_idx = i;
-            break;
-          }
-      }
+      const int merge_idx = intra ? -1 : merge_index_p(x0, y0, N, mv);
       const bool skip = !intra && merge_idx >= 0 && cbf == 0;
       int inc = 0;
       if (has_left(x0) && skip_[unit(x0 - 1, y0)]) ++inc;
