@@ -720,8 +720,6 @@ class SliceWriter {
     const uint8_t* ps = in_sb_scan(scanIdx);
     const uint8_t* sbpos = kSb.pos[log2N - 2][scanIdx];
     const uint8_t* sbinv = kSb.inv[log2N - 2][scanIdx];
-    int off[16];
-    for (int n = 0; n < 16; ++n) off[n] = (ps[n] >> 2) * v.stride + (ps[n] & 3);
     // last significant coefficient in scan order: the non-zero sub-block latest in scan
     // order, then its last non-zero scan position
     if (!v.nz) throw std::runtime_error("residual_coding of an all-zero block");
@@ -779,7 +777,11 @@ class SliceWriter {
       const int add = log2N == 2 ? compOff : compOff + sizeOff + ((cIdx == 0 && i > 0) ? 3 : 0);
       const int nStart = (i == lastSb) ? lastN - 1 : 15;
       const bool dcInferred = inferDc && (m & ((2u << nStart) - 2)) == 0;
-      for (int n = nStart; n >= 1; --n) bin((m >> n) & 1, add + pat[n]);
+      if (nStart >= 1)
+        enc_.encode_run(nStart, [&](int k, int& bn, CtxState*& cs) {
+          bn = (m >> (nStart - k)) & 1;
+          cs = &ctx_.c[add + pat[nStart - k]];
+        });
       if (nStart >= 0 && !dcInferred)  // the TB's DC has its own context
         bin(m & 1, (log2N > 2 && i == 0) ? compOff : add + pat[0]);
       // levels, in reverse scan order
@@ -787,7 +789,7 @@ class SliceWriter {
       for (unsigned s = m; s; ++cnt) {
         const int n = 31 - __builtin_clz(s);
         s &= ~(1u << n);
-        const int x = b[off[n]];
+        const int x = b[(ps[n] >> 2) * v.stride + (ps[n] & 3)];
         absv[cnt] = x < 0 ? -x : x;
         signs[cnt] = x < 0;
       }
@@ -797,16 +799,16 @@ class SliceWriter {
       const int g1base = CTX_G1 + 4 * ctxSet + (cIdx ? 16 : 0);
       const int nG1 = cnt < 8 ? cnt : 8;
       int firstG2 = -1;
-      for (int k = 0; k < nG1; ++k) {
-        const int g1 = absv[k] > 1;
-        bin(g1, g1base + c1);
-        if (g1) {
+      enc_.encode_run(nG1, [&](int k, int& bn, CtxState*& cs) {
+        bn = absv[k] > 1;
+        cs = &ctx_.c[g1base + c1];
+        if (bn) {
           c1 = 0;
           if (firstG2 < 0) firstG2 = k;
         } else if (c1 > 0 && c1 < 3) {
           ++c1;
         }
-      }
+      });
       if (firstG2 >= 0) bin(absv[firstG2] > 2, CTX_G2 + ctxSet + (cIdx ? 4 : 0));
       uint32_t sbits = 0;
       for (int k = 0; k < cnt; ++k) sbits = (sbits << 1) | (uint32_t)signs[k];

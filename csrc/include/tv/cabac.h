@@ -169,21 +169,46 @@ class CabacEncoder {
     num_buffered_ = 0;
     buffered_ = 0xff;
   }
-  // Branch-free on the coded value (significance / greater-1 bins are unpredictable): both
-  // outcomes are formed and selected, renormalisation is one clz.
-  void encode_bin(int bin, CtxState& ctx) {
-    const uint32_t lps = kRangeTabLps[ctx.state][(range_ >> 6) & 3];
-    const uint32_t rmps = range_ - lps;
+  // Both outcomes are formed and selected, renormalisation is one clz.
+  static inline void bin_step(uint32_t& low, uint32_t& range, int& bits_left, int bin, CtxState& ctx) {
+    const uint32_t lps = kRangeTabLps[ctx.state][(range >> 6) & 3];
+    const uint32_t rmps = range - lps;
     const bool is_lps = bin != ctx.mps;
     const uint32_t r = is_lps ? lps : rmps;
-    const uint32_t l = is_lps ? low_ + rmps : low_;
+    const uint32_t l = is_lps ? low + rmps : low;
     const int nb = __builtin_clz(r) - 23;  // shifts bringing r (>= 6) to >= 256; 0 if already
-    low_ = l << nb;
-    range_ = r << nb;
-    bits_left_ -= nb;
+    low = l << nb;
+    range = r << nb;
+    bits_left -= nb;
     ctx.mps = (uint8_t)(ctx.mps ^ (is_lps & (ctx.state == 0)));
     ctx.state = is_lps ? kTransIdxLps[ctx.state] : kTransIdxMps[ctx.state];
+  }
+  void encode_bin(int bin, CtxState& ctx) {
+    bin_step(low_, range_, bits_left_, bin, ctx);
     test_write_out();
+  }
+  // A run of `count` context-coded bins with the coder state in registers (the members are
+  // only touched around the byte output): next(k, bin, ctx) names the k-th bin and context.
+  template <class F>
+  void encode_run(int count, F&& next) {
+    uint32_t low = low_, range = range_;
+    int bl = bits_left_;
+    for (int k = 0; k < count; ++k) {
+      int bin;
+      CtxState* c;
+      next(k, bin, c);
+      bin_step(low, range, bl, bin, *c);
+      if (bl < 12) {
+        low_ = low;
+        bits_left_ = bl;
+        write_out();
+        low = low_;
+        bl = bits_left_;
+      }
+    }
+    low_ = low;
+    range_ = range;
+    bits_left_ = bl;
   }
   void encode_bypass(int bin) {
     low_ <<= 1;
