@@ -548,6 +548,17 @@ def main() -> None:
     eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=args.sao,
                     seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes)
     post = _PostQueue(local)
+    # 2-pass: a second engine runs the fast first pass (SAO off: its statistics, decision and
+    # filter are ~15 % of the GPU step and only fine-tune the reconstruction; the measured
+    # QP-offset response absorbs the pass-1 / pass-2 difference) one step ahead, on its own
+    # thread and HIP streams, concurrently with pass 2 of the current step
+    eng1 = pre = None
+    if args.kbps > 0:
+        import concurrent.futures as cf
+
+        eng1 = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=False,
+                         seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes)
+        pre = cf.ThreadPoolExecutor(1, initializer=lambda: torch.cuda.set_device(local))
 
     def comm(segs, sse):
         # rate-control / quality statistics all-reduce + bitstreams -> stitch rank (rank 0)
@@ -588,21 +599,31 @@ def main() -> None:
         return out
 
     counter = [0]
+    first = {}
+
+    def starts_of(s: int):
+        base = (s * world + rank) * batch
+        return [(base + b) * args.gop for b in range(batch)]
 
     def step(s: int):
         i = counter[0]
         counter[0] += 1
-        base = (s * world + rank) * batch
-        starts = [(base + b) * args.gop for b in range(batch)]
-        if args.kbps > 0:  # pass 1 at the base QP -> plan (post thread) -> pass 2 at the plan's QPs
-            qm = post.ex.submit(plan_pass2, i, eng.encode_synthetic(starts)).result()
-            segs = eng.encode_synthetic(starts, qp=qm)
+        if args.kbps > 0:
+            # pass 1 of step i + 1 (pre thread, eng1) overlaps the plan and pass 2 of step i;
+            # every collective is queued on the post thread from this thread, in step order
+            if i == 0:
+                first[0] = pre.submit(eng1.encode_synthetic, starts_of(0))
+            first[i + 1] = pre.submit(eng1.encode_synthetic, starts_of(i + 1))
+            qm = post.ex.submit(plan_pass2, i, first.pop(i).result()).result()
+            segs = eng.encode_synthetic(starts_of(i), qp=qm)
             post.submit(comm_rc, i, segs, np.array([eng.sse(b) for b in range(batch)]).sum(0))
             return
-        segs = eng.encode_synthetic(starts)
+        segs = eng.encode_synthetic(starts_of(s))
         post.submit(comm, segs, np.array([eng.sse(b) for b in range(batch)]).sum(0))
 
     el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), eng.threads])
+    for f in first.values():  # the look-ahead pass 1 of the step after the last one
+        f.result()
     tot = np.sum([r[0] for r in res], axis=0)
     gathered_bytes = sum(r[1] for r in res)
     frames = tot[0]
@@ -632,7 +653,8 @@ def main() -> None:
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
                 "bframes": args.bframes,
                 "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame QP plan, target {args.kbps:g} "
-                                 "kbps per 30 fps stream, batch feedback (measured QP offset response + bounded debt)"
+                                 "kbps per 30 fps stream, fast first pass (SAO off) one step ahead on a second engine, batch feedback "
+                                 "(measured QP offset response + bounded debt)"
                                  if args.kbps > 0 else f"CQP {args.qp}"),
                 "kbps_error_pct": round(100 * (kbps / args.kbps - 1), 2) if args.kbps > 0 else None,
                 "rc_steps_actual_wanted_offset": ctl.log if args.kbps > 0 else None,
@@ -659,6 +681,9 @@ def main() -> None:
             },
         }), flush=True)
     post.close()
+    if eng1 is not None:
+        pre.shutdown()
+        eng1.close()
     eng.close()
     dist.destroy_process_group()
 
