@@ -330,7 +330,14 @@ def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats, qps) -> list
 
 def _encode_gpu_av1(eng, chunks: dict, out: list, spec: EncodeSpec, dev, stats) -> list[bytes]:
     """AV1 engine: equal-length chunks in groups of up to eng.B segments; sources are
-    staged (tone-map / resize / edge pad) straight into the engine's coded-size planes."""
+    staged (tone-map / resize / edge pad) straight into the engine's coded-size planes.
+
+    The groups are software-pipelined: group k + 1 is staged and its GPU part issued
+    (encode_gop async_host: decisions collected on the copy stream) before group k's
+    decisions go to the OBU writers, so entropy coding overlaps the next group's kernels.  The
+    chunks are cut into equal groups, at least two (>= 8 segments) to get that overlap.  Staging
+    and the per-frame source copies are ordered on the current stream, so reusing the staging
+    buffer for the next group never races the previous group's copies."""
     import torch
 
     from ..models import av1
@@ -339,35 +346,53 @@ def _encode_gpu_av1(eng, chunks: dict, out: list, spec: EncodeSpec, dev, stats) 
     cw, ch = av1.coded_size(spec.width, spec.height)
     fsz = cw * ch * 3 // 2
     ysz, csz = cw * ch, cw * ch // 4
+    groups = []
+    for n, items in chunks.items():
+        ng = max(-(-len(items) // eng.B), 2 if len(items) >= 8 else 1)  # equal groups, >= 2 to overlap
+        step = -(-len(items) // ng)
+        groups += [(n, items[i:i + step]) for i in range(0, len(items), step)]
+    writers = []  # (part index, chunk index, writer future)
+
+    def to_writers(n, grp, fut):
+        g = fut.result()
+        for j, ((pi, c, _, _), fu) in enumerate(zip(grp, eng.submit_entropy(g))):
+            writers.append((pi, c, fu))
+            if stats is not None:
+                stats[pi].add(n, g.sse[:, j].sum(axis=0))
+
     with eng.lock:
-        for n, items in chunks.items():
-            for i in range(0, len(items), eng.B):
-                grp = items[i:i + eng.B]
-                need = len(grp) * n * fsz
-                if eng.staging is None or eng.staging.numel() < need:
-                    eng.staging = torch.empty(need, dtype=torch.uint8, device=dev)
-                for j, (_, _, s, _) in enumerate(grp):
-                    if isinstance(s, SynthRange):
-                        s = stage.synth_frames(s.seed, s.width, s.height, range(s.t0, s.t0 + s.n), dev)
-                    stage.to_staging(s, spec.width, spec.height, eng.staging, j * n, coded=(cw, ch))
-                frames = eng.staging[:need].view(len(grp), n, fsz)
+        pending = None
+        for n, grp in groups:
+            need = len(grp) * n * fsz
+            if eng.staging is None or eng.staging.numel() < need:
+                if pending is not None:  # the previous group's copies still read the old buffer
+                    to_writers(*pending)
+                    pending = None
+                eng.staging = torch.empty(need, dtype=torch.uint8, device=dev)
+            for j, (_, _, s, _) in enumerate(grp):
+                if isinstance(s, SynthRange):
+                    s = stage.synth_frames(s.seed, s.width, s.height, range(s.t0, s.t0 + s.n), dev)
+                stage.to_staging(s, spec.width, spec.height, eng.staging, j * n, coded=(cw, ch))
+            frames = eng.staging[:need].view(len(grp), n, fsz)
 
-                def load(t, planes, frames=frames):
-                    f = frames[:, t]
-                    planes[0][:len(grp)].copy_(f[:, :ysz].view(-1, ch, cw))
-                    planes[1][:len(grp)].copy_(f[:, ysz:ysz + csz].view(-1, ch // 2, cw // 2))
-                    planes[2][:len(grp)].copy_(f[:, ysz + csz:].view(-1, ch // 2, cw // 2))
+            def load(t, planes, frames=frames, k=len(grp)):
+                f = frames[:, t]
+                planes[0][:k].copy_(f[:, :ysz].view(-1, ch, cw))
+                planes[1][:k].copy_(f[:, ysz:ysz + csz].view(-1, ch // 2, cw // 2))
+                planes[2][:k].copy_(f[:, ysz + csz:].view(-1, ch // 2, cw // 2))
 
-                qmap = None
-                if any(x[3] is not None for x in grp):  # rate-control plan: per-frame HEVC QP -> q-index
-                    qmap = np.array([[av1.qindex_for_hevc_qp(int(x[3][t])) if x[3] is not None
-                                      else spec.av1_qindex() for x in grp] for t in range(n)], np.int32)
-                g = eng.encode_gop(n, load, nseg=len(grp), qmap=qmap)
-                futs = eng.submit_entropy(g)
-                for j, ((pi, c, _, _), fu) in enumerate(zip(grp, futs)):
-                    out[pi][c] = b"".join(fu.result())
-                    if stats is not None:
-                        stats[pi].add(n, g.sse[:, j].sum(axis=0))
+            qmap = None
+            if any(x[3] is not None for x in grp):  # rate-control plan: per-frame HEVC QP -> q-index
+                qmap = np.array([[av1.qindex_for_hevc_qp(int(x[3][t])) if x[3] is not None
+                                  else spec.av1_qindex() for x in grp] for t in range(n)], np.int32)
+            fut = eng.encode_gop(n, load, nseg=len(grp), qmap=qmap, async_host=True)
+            if pending is not None:
+                to_writers(*pending)
+            pending = (n, grp, fut)
+        if pending is not None:
+            to_writers(*pending)
+        for pi, c, fu in writers:
+            out[pi][c] = b"".join(fu.result())
     return [b"".join(x) for x in out]
 
 
