@@ -599,7 +599,7 @@ __device__ __forceinline__ bool pr_zeroed(const PReconLds& L, int id) {
   return L.nz[id] == 0 || (L.nz[id] == 1 && L.sa[id] == 1 && L.dc[id] == 0);
 }
 
-__global__ void __launch_bounds__(256) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                      FrameSet rec, DecisionSet dec, Geo g, int tile_skip,
                                                      FrameSet ref1, const uint8_t* phase1) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
