@@ -115,6 +115,16 @@ struct EngineCfg {
 
 // One group of segments on its own HIP stream (buffers, pinned slot ring, events).
 class Core {
+  size_t dev_bytes_ = 0, host_bytes_ = 0;
+  template <class T> void dev_alloc(T** p, size_t n) {
+    HIP_OK(hipMalloc(p, n));
+    dev_bytes_ += n;
+  }
+  template <class T> void host_alloc(T** p, size_t n) {
+    HIP_OK(hipHostMalloc(p, n, hipHostMallocDefault));
+    host_bytes_ += n;
+  }
+
  public:
   Core(const EngineCfg& c, ThreadPool* pool) : cfg_(c), g_(make_geo(c.width, c.height)), pool_(pool) {
     if (c.batch < 1 || c.batch > kMaxBatch) throw std::runtime_error("batch must be 1..64");
@@ -136,9 +146,9 @@ class Core {
     const long B = c.batch;
     nctu_ = g_.wc * g_.hc;
     auto alloc_set = [&](FrameSet& f) {
-      HIP_OK(hipMalloc(&f.y, B * g_.ysz));
-      HIP_OK(hipMalloc(&f.u, B * g_.csz));
-      HIP_OK(hipMalloc(&f.v, B * g_.csz));
+      dev_alloc(&f.y, B * g_.ysz);
+      dev_alloc(&f.u, B * g_.csz);
+      dev_alloc(&f.v, B * g_.csz);
     };
     alloc_set(src_);
     // Decoded picture buffer (tv/gop.h): every picture is reconstructed into a free DPB entry
@@ -154,34 +164,34 @@ class Core {
     qsz_ = (long)(g_.W / 4) * (g_.H / 4);
     for (int k = 0; k < ndpb_; ++k) {
       alloc_set(dpb_[k].rec);
-      HIP_OK(hipMalloc(&dpb_[k].phase, B * 16 * g_.psz));
-      HIP_OK(hipMalloc(&dpb_[k].q, B * qsz_));
+      dev_alloc(&dpb_[k].phase, B * 16 * g_.psz);
+      dev_alloc(&dpb_[k].q, B * qsz_);
     }
     if (c.deblock & 2) alloc_set(deb_);
-    HIP_OK(hipMalloc(&coef_y_, B * g_.ysz * sizeof(int16_t)));
-    HIP_OK(hipMalloc(&coef_u_, B * g_.csz * sizeof(int16_t)));
-    HIP_OK(hipMalloc(&coef_v_, B * g_.csz * sizeof(int16_t)));
-    HIP_OK(hipMalloc(&d_sse_, B * 3 * sizeof(unsigned long long)));
-    HIP_OK(hipMalloc(&count_scratch_, B * nctu_ * sizeof(int)));
+    dev_alloc(&coef_y_, B * g_.ysz * sizeof(int16_t));
+    dev_alloc(&coef_u_, B * g_.csz * sizeof(int16_t));
+    dev_alloc(&coef_v_, B * g_.csz * sizeof(int16_t));
+    dev_alloc(&d_sse_, B * 3 * sizeof(unsigned long long));
+    dev_alloc(&count_scratch_, B * nctu_ * sizeof(int));
     // hierarchical motion search: coarse field (+ cost) per list; B pictures: per-list fine
     // search results for the bi decision
-    HIP_OK(hipMalloc(&cmv_, 2 * B * nctu_ * 2 * sizeof(int16_t)));
-    HIP_OK(hipMalloc(&ccost_, 2 * B * nctu_ * sizeof(int)));
-    if (c.mgop > 1) HIP_OK(hipMalloc(&meout_, 2 * B * nctu_ * sizeof(CtbMeOut)));
+    dev_alloc(&cmv_, 2 * B * nctu_ * 2 * sizeof(int16_t));
+    dev_alloc(&ccost_, 2 * B * nctu_ * sizeof(int));
+    if (c.mgop > 1) dev_alloc(&meout_, 2 * B * nctu_ * sizeof(CtbMeOut));
     cap_ = g_.ysz + 2 * g_.csz;
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
     slot_bytes_ = align(B * g_.usz) + align(B * g_.usz * 4) + align(B * nctu_ * 8) + align(B * nctu_ * 4) +
                   align(B * nctu_ * 4) + align(B * 4) + align(B * nctu_ * 12) + align(B) + align(B * g_.usz) +
                   align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * cap_ * 2);
-    HIP_OK(hipHostMalloc(&qhost_, (size_t)c.gop * B, hipHostMallocDefault));
-    HIP_OK(hipHostMalloc(&quni_, (size_t)B, hipHostMallocDefault));
+    host_alloc(&qhost_, (size_t)c.gop * B);
+    host_alloc(&quni_, (size_t)B);
     std::memset(quni_, c.qp, (size_t)B);
     nslots_ = slot_count();
     slots_.reset(new Slot[nslots_]);
     for (int k = 0; k < nslots_; ++k) {
       Slot& s = slots_[k];
-      HIP_OK(hipMalloc(&s.dev, slot_bytes_));
-      HIP_OK(hipHostMalloc(&s.host, slot_bytes_, hipHostMallocDefault));
+      dev_alloc(&s.dev, slot_bytes_);
+      host_alloc(&s.host, slot_bytes_);
       // waited on by the fetch thread: see sync_mode()
       HIP_OK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming | (sync_mode() == 2 ? hipEventBlockingSync : 0)));
       s.pending = 0;
@@ -202,7 +212,7 @@ class Core {
         for (int i = 0; i < 64; ++i) p.mv[i] = (int)(lam * i);
         t.sao_lam16[q] = sao_lambda16(q);
       }
-      HIP_OK(hipMalloc(&rc_, sizeof(RcTables)));
+      dev_alloc(&rc_, sizeof(RcTables));
       HIP_OK(hipMemcpy(rc_, &t, sizeof(RcTables), hipMemcpyHostToDevice));
     }
     seq_.width = c.width;
@@ -218,6 +228,28 @@ class Core {
       seq_.num_reorder = gp.num_reorder;
     }
     seq_.finalize();
+  }
+
+  // device / pinned-host bytes this group allocated (the engine's HBM footprint)
+  size_t dev_bytes() const { return dev_bytes_; }
+  size_t host_bytes() const { return host_bytes_; }
+
+  // The same byte counts computed without allocating anything (EngineCache budgets and
+  // auto-batch sizing decide before building an engine).  Mirrors the constructor above,
+  // term by term; tests/test_hbm_budget.py checks estimate == footprint on the GPU.
+  static void estimate(const EngineCfg& c, size_t& dev, size_t& host) {
+    const Geo g = make_geo(c.width, c.height);
+    const size_t B = (size_t)c.batch, nctu = (size_t)g.wc * g.hc, set = B * (g.ysz + 2 * g.csz);
+    const int ndpb = c.mgop > 1 ? plan_gop(2 * c.mgop + 1, c.mgop).dpb_size : 2;
+    const size_t qsz = (size_t)(g.W / 4) * (g.H / 4), cap = g.ysz + 2 * g.csz;
+    const size_t slot = align(B * g.usz) + align(B * g.usz * 4) + align(B * nctu * 8) + align(B * nctu * 4) +
+                        align(B * nctu * 4) + align(B * 4) + align(B * nctu * 12) + align(B) + align(B * g.usz) +
+                        align(B * g.usz * 4) + align(B * g.usz * 4) + align(B * cap * 2);
+    dev = set + ndpb * (set + B * 16 * g.psz + B * qsz) + ((c.deblock & 2) ? set : 0) + 2 * set +
+          B * 3 * sizeof(unsigned long long) + B * nctu * sizeof(int) + 2 * B * nctu * 2 * sizeof(int16_t) +
+          2 * B * nctu * sizeof(int) + (c.mgop > 1 ? 2 * B * nctu * sizeof(CtbMeOut) : 0) +
+          (size_t)slot_count() * slot + sizeof(RcTables);
+    host = (size_t)c.gop * B + B + (size_t)slot_count() * slot;
   }
 
   ~Core() {
@@ -815,6 +847,32 @@ class Engine {
     return n;
   }
   const Geo& geo() const { return cores_[0]->geo(); }
+  size_t dev_bytes() const {
+    size_t n = 0;
+    for (const auto& c : cores_) n += c->dev_bytes();
+    return n;
+  }
+  size_t host_bytes() const {
+    size_t n = 0;
+    for (const auto& c : cores_) n += c->host_bytes();
+    return n;
+  }
+  // footprint of an engine of config c (the group split of the constructor), no allocation
+  static void estimate(const EngineCfg& c, size_t& dev, size_t& host) {
+    int G = c.groups < 1 ? 1 : c.groups;
+    if (G > c.batch) G = c.batch;
+    const int per = (c.batch + G - 1) / G;
+    G = (c.batch + per - 1) / per;
+    dev = host = 0;
+    for (int g = 0; g < G; ++g) {
+      EngineCfg cc = c;
+      cc.batch = std::min(per, c.batch - g * per);
+      size_t d = 0, h = 0;
+      Core::estimate(cc, d, h);
+      dev += d;
+      host += h;
+    }
+  }
   FrameSet last_recon(int b, int& local) const {
     local = b % per_;
     return core_of(b).last_recon();
@@ -938,6 +996,26 @@ void tv_engine_timing(void* e, double* gpu_ms, double* wall_ms, double* entropy_
   *wall_ms = E->wall_ms();
   *entropy_ms = E->entropy_ms();
   *coef_mb = E->coef_bytes() / 1e6;
+}
+// The same for an engine not built yet (same arguments as tv_engine_new_b's geometry part)
+int tv_engine_estimate(int width, int height, int batch, int gop, int deblock, int mgop, unsigned long long* dev,
+                       unsigned long long* host) {
+  return gguard([&] {
+    const char* ge = getenv("TV_ENGINE_GROUPS");
+    const int groups = ge ? std::max(1, atoi(ge)) : (batch >= 2 ? 2 : 1);
+    tv::gpu::EngineCfg c{width, height, 27, batch, gop, 64, deblock, 1, 0, 5, 1u, groups, 0};
+    c.mgop = mgop;
+    size_t d = 0, h = 0;
+    tv::gpu::Engine::estimate(c, d, h);
+    *dev = d;
+    *host = h;
+  });
+}
+// HBM / pinned-host bytes the engine allocated at construction (EngineCache byte budget)
+void tv_engine_footprint(void* e, unsigned long long* dev, unsigned long long* host) {
+  auto* E = static_cast<tv::gpu::Engine*>(e);
+  *dev = E->dev_bytes();
+  *host = E->host_bytes();
 }
 // copy the last frame's coded-size reconstruction of segment b (tests)
 int tv_engine_encode_device(void* e, const uint8_t* dframes, int nseg, int nframes, const int8_t* qmap) {

@@ -113,17 +113,6 @@ inline int gop_search_range(int range, int dist, int mgop) {
 // +1/+4/+5/+6 -19.6 % BD-rate against the IPPP stream at M = 8.
 inline int gop_layer_qp_offset(int type, int layer, int mgop) {
   if (mgop <= 1 || type == 2) return 0;
-  static const int* ov = [] {  // TV_BQP="p,l1,l2,..": per-layer override (RD experiments)
-    static int v[9];
-    const char* e = std::getenv("TV_BQP");
-    if (!e) return (int*)nullptr;
-    for (int i = 0; i < 9; ++i) {
-      v[i] = (int)std::strtol(e, const_cast<char**>(&e), 10);
-      if (*e == ',') ++e;
-    }
-    return v;
-  }();
-  if (ov) return ov[layer < 9 ? layer : 8];
   return layer == 0 ? 1 : 3 + layer;
 }
 

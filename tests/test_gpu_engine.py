@@ -103,3 +103,24 @@ def test_gpu_bit_exact_on_textured_content(sao):
         cpu_bs, _ = hevc.encode_sequence_cpu(frames, qp=27, sao=sao, search_range=rng)
         assert segs[b] == cpu_bs, f"segment {b}"
     eng.close()
+
+
+def test_gpu_bit_exact_at_benchmarked_shape():
+    """The benchmark's SHAPE (GOP 64, 48 segments per call split over two stream groups, SAO
+    on, search range 64 — the shipped worker configuration) at a reduced geometry: segments
+    from both groups (first and last) equal the golden encoder byte for byte, and frame 63's
+    reconstruction is the golden one, so a DPB / slot-ring or long-GOP drift bug after the
+    short-GOP tests' last frame cannot hide (verdict r3 item 6)."""
+    w, h, gop, batch, rng = 320, 180, 64, 48, 64
+    eng = _engine(width=w, height=h, qp=27, batch=batch, gop=gop, search_range=rng, sao=True, seed=11)
+    starts = [gop * b for b in range(batch)]
+    segs = eng.encode_synthetic(starts)
+    for b in (0, batch - 1):
+        frames = [hevc.synth_frame(11, starts[b] + f, w, h) for f in range(gop)]
+        cpu_bs, recons = hevc.encode_sequence_cpu(frames, qp=27, sao=True, search_range=rng)
+        assert segs[b] == cpu_bs, f"segment {b}: GPU bitstream differs from CPU golden model"
+        gy, gu, gv = eng.last_recon(b)
+        np.testing.assert_array_equal(gy, recons[-1][0])
+        np.testing.assert_array_equal(gv, recons[-1][2])
+        assert len(hevc.decode(segs[b]).frames) == gop
+    eng.close()

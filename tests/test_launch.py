@@ -103,3 +103,33 @@ def test_tv_cpus_caps_the_rank_cpu_set(tmp_path):
     a, b = map(int, r.stdout.split())
     want = min(2, len(os.sched_getaffinity(0)))
     assert a == b == want, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("mode", [[], ["--kbps", "300"], ["--codec", "av1"], ["--ladder", "96"]],
+                         ids=["1pass", "2pass", "av1", "ladder"])
+def test_bench_cpu_rehearsal_n_ranks(n, mode):
+    """bench.py's N-rank logic (self-launch, post-thread collective ordering, the 2-pass
+    plan all-reduce and pass-1 look-ahead, the AV1 step pipeline, the ladder fan-out and the
+    bitstream gather) end-to-end on N gloo ranks with the golden encoders (--cpu) — the
+    paths the driver's multi-GPU run takes, exercised before it does (verdict r3 item 2)."""
+    import json
+
+    args = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", str(n), "--steps", "2", "--warmup", "1",
+            "--batch", "2", "--gop", "4", "--threads", "1", *mode]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=240, env=dict(os.environ, TV_NO_PIN="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout  # rank 0 prints exactly one JSON line
+    d = json.loads(line[0])
+    c = d["config"]
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    assert c["global_batch"] == 2 * n and "CPU REHEARSAL" in d["data"]
+    assert len(c["per_rank_cpu"]) == n
+    # every rank's bitstream bytes reached the stitch rank: the gathered total equals the
+    # all-reduced sum of the per-rank byte counts
+    assert c["gathered_mb_at_root"] == c["bytes_all_reduced_mb"] > 0
+    frames_per_step = 2 * 4 * n
+    assert abs(d["value"] * d["ms_per_step"] / 1000 - frames_per_step) < 1e-3 * frames_per_step
+    if "--kbps" in mode:
+        assert c["kbps_error_pct"] is not None and c["pass1_kbps_rank0"] > 0

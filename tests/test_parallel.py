@@ -155,6 +155,79 @@ def test_rotating_scatter_gloo_world4(tmp_path, source):
     assert min(hevc.psnr(a[0], b[0]) for a, b in zip(frames, dec.frames)) > 28
 
 
+def _stream_worker(rank, world, port, out_dir):
+    import time
+
+    import torch
+
+    from thinvids_amd.parallel.comm import SegmentStream
+
+    dist = _init(rank, world, port)
+    got = {}
+    s = SegmentStream(torch.device("cpu"), lambda k, b: got.__setitem__(k, b), root=0, idle_s=0.005)
+    for i in range(rank * 3):  # uneven claims: rank 0 none, rank 3 nine, arriving over time
+        time.sleep(0.002 * ((i * 7 + rank) % 5))
+        s.put((rank, i), bytes([rank, i]) * (100 * i + 1))
+    st = s.close()
+    dist.all_reduce(torch.ones(1))  # the default group is still usable after the stream
+    if rank == 0:
+        ok = all(got.get((r, i)) == bytes([r, i]) * (100 * i + 1) for r in range(world) for i in range(r * 3))
+        with open(os.path.join(out_dir, "stream.json"), "w") as f:
+            json.dump({"n": len(got), "ok": ok, "rounds": st["rounds"]}, f)
+    dist.destroy_process_group()
+
+
+def test_segment_stream_uneven_claims_gloo_world4(tmp_path):
+    """comm.SegmentStream: ranks finish different numbers of segments at different times;
+    every one reaches the root's callback, and all ranks leave the gather rounds together."""
+    mp.spawn(_stream_worker, args=(4, _free_port(), str(tmp_path)), nprocs=4, join=True)
+    r = json.load(open(tmp_path / "stream.json"))
+    assert r["ok"] and r["n"] == 3 + 6 + 9 and r["rounds"] >= 2
+
+
+def test_rccl_segment_stream_matches_file_handoff_world4(tmp_path, source):
+    """The streaming stitch's peer segments travel over the collective segment stream
+    (RCCL on the GPU, gloo here) instead of part files: 4 ranks, 12 segments, and the
+    stitched MP4 is byte-identical to the file hand-off version."""
+    from thinvids_amd.models import hevc
+
+    src, frames = source
+    kw = {"gop": 2, "segment_frames": 2, "batch_segments": 1}
+    os.makedirs(tmp_path / "a", exist_ok=True)
+    os.makedirs(tmp_path / "b", exist_ok=True)
+    res_a, out_a = _spawn_job(tmp_path / "a", source, kw, {}, world=4)
+    res_b, out_b = _spawn_job(tmp_path / "b", source, kw, {"TV_STITCH_TRANSPORT": "files"}, world=4)
+    sa, sb = res_a[0]["stitch"], res_b[0]["stitch"]
+    assert sa["transport"] == "rccl" and sb["transport"] == "files"
+    peers = sum(p["encoded"] for p in res_a[0]["per_rank"][1:])
+    assert sa["segments"] == peers > 0 and sa["bytes"] > 0
+    assert not os.path.exists(out_a + ".parts") and not os.path.exists(out_b + ".parts")
+    assert open(out_a, "rb").read() == open(out_b, "rb").read()
+    dec = hevc.decode(hevc.demux_mp4(open(out_a, "rb").read())["annexb"], coded=False)
+    assert len(dec.frames) == 24
+    assert min(hevc.psnr(a[0], b[0]) for a, b in zip(frames, dec.frames)) > 28
+
+
+def test_file_handoff_ignores_parts_of_a_killed_attempt(tmp_path, source):
+    """A killed earlier attempt left part files under {output}.parts; the next attempt of
+    the same output (here with different settings) must not splice them in."""
+    from thinvids_amd.models import hevc
+
+    src, frames = source
+    out = str(tmp_path / "out.mp4")
+    stale = os.path.join(out + ".parts", "deadbeef")
+    os.makedirs(stale)
+    for i in range(12):
+        with open(os.path.join(stale, f"r0_s{i}.part"), "wb") as f:
+            f.write(b"\x00\x00\x01garbage")
+    with open(os.path.join(out + ".parts", "r0_s1.part"), "wb") as f:  # the round-3 layout
+        f.write(b"\x00\x00\x01garbage")
+    res, out2 = _spawn_job(tmp_path, source, {"gop": 2, "segment_frames": 2}, {"TV_STITCH_TRANSPORT": "files"})
+    assert out2 == out and "error" not in res[0]
+    dec = hevc.decode(hevc.demux_mp4(open(out, "rb").read())["annexb"], coded=False)
+    assert len(dec.frames) == 24 and not os.path.exists(out + ".parts")
+
+
 def test_stage_segment_frames_packs_i420_rows():
     import torch
 

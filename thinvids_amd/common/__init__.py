@@ -53,3 +53,11 @@ def all_jobs_are_idle(store=None) -> bool:
         p.hget(k, "status")
     busy = {Status.RUNNING.value, Status.WAITING.value, Status.STARTING.value}
     return not any(str(s or "").upper() in busy for s in p.execute())
+
+
+def pass_field(job: dict, name: str) -> str:
+    """Value of a per-pass progress counter (parts_done, completed_chunks, encoded_frames) of
+    the job's current rate-control pass: pass 0 keeps the reference's field names, a later
+    pass of a 2-pass job counts in ``<name>_p<k>`` (worker/node_executor._StoreHooks)."""
+    k = str(job.get("rc_pass") or "0")
+    return job.get(f"{name}_p{k}") if k not in ("", "0") else job.get(name)

@@ -22,7 +22,7 @@ import threading
 import time
 import uuid
 
-from ..common import (JOBS_INDEX_KEY, Status, as_bool, as_float, as_int, emit_activity, get_settings,
+from ..common import (JOBS_INDEX_KEY, Status, as_bool, as_float, as_int, emit_activity, get_settings, pass_field,
                       is_base_job_key, natural_host_key)
 from ..models import media
 from ..store import get_store
@@ -279,12 +279,12 @@ def _is_english(lang: str) -> bool:
 
 # ------------------------------------------------------------- scheduler (C24)
 def _done_ratio(job: dict) -> float:
-    total, done = as_int(job.get("parts_total")), as_int(job.get("parts_done"))
+    total, done = as_int(job.get("parts_total")), as_int(pass_field(job, "parts_done"))
     return 0.0 if total <= 0 else min(1.0, max(0.0, done / total))
 
 
 def _remaining(job: dict) -> int:
-    total, done = as_int(job.get("parts_total")), as_int(job.get("parts_done"))
+    total, done = as_int(job.get("parts_total")), as_int(pass_field(job, "parts_done"))
     return max(0, total - done) if total > 0 else 0
 
 

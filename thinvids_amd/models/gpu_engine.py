@@ -180,6 +180,13 @@ class GpuEngine:
         self.lib.tv_engine_segment_copy(self.h, b, ptr(out))
         return out.tobytes()
 
+    def footprint(self) -> dict:
+        """HBM and pinned-host bytes this engine allocated (the native allocation ledger)."""
+        d, h = C.c_ulonglong(), C.c_ulonglong()
+        self.lib.tv_engine_footprint.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
+        self.lib.tv_engine_footprint(self.h, C.byref(d), C.byref(h))
+        return {"dev": int(d.value), "host": int(h.value)}
+
     def sse(self, b: int) -> tuple[float, float, float]:
         a = (C.c_double * 3)()
         self.lib.tv_engine_sse(self.h, b, a)
@@ -214,3 +221,15 @@ def pad_frame(y, u, v, cw, ch) -> np.ndarray:
     U = np.pad(u, ((0, ch // 2 - h // 2), (0, cw // 2 - w // 2)), mode="edge")
     V = np.pad(v, ((0, ch // 2 - h // 2), (0, cw // 2 - w // 2)), mode="edge")
     return np.concatenate([Y.ravel(), U.ravel(), V.ravel()])
+
+
+def estimate_footprint(width: int, height: int, batch: int, gop: int, sao: bool = False, bframes: int = 1) -> dict:
+    """HBM / pinned-host bytes an engine of this geometry would allocate, computed by the
+    native constructor's own size formulas without allocating (tv_engine_estimate)."""
+    lib = _lib()
+    d, h = C.c_ulonglong(), C.c_ulonglong()
+    f = lib.tv_engine_estimate
+    f.argtypes = [C.c_int] * 6 + [C.POINTER(C.c_ulonglong)] * 2
+    if f(width, height, batch, gop, 1 | (2 if sao else 0), int(bframes), C.byref(d), C.byref(h)) != 0:
+        raise ValueError(lib.tv_gpu_last_error().decode())
+    return {"dev": int(d.value), "host": int(h.value)}

@@ -6,6 +6,7 @@ Frames are ``(Y, U, V)`` tuples of uint8 numpy arrays (4:2:0, Y shape ``(H, W)``
 from __future__ import annotations
 
 import ctypes as C
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -319,27 +320,37 @@ class Mp4StreamWriter:
         if not self.h:
             raise RuntimeError(lib.tv_mp4s_last_error().decode())
         self.payload = 0
+        # the native calls release the GIL: append / close / abort from different threads
+        # must never overlap on one handle (abort deletes it)
+        self.lock = threading.Lock()
 
     def append(self, segment) -> None:
         buf = np.frombuffer(segment, np.uint8)
         if not len(buf):
             return
-        if self.lib.tv_mp4s_append(self.h, buf.ctypes.data, len(buf)) != 0:
-            raise RuntimeError(self.lib.tv_mp4s_last_error().decode())
+        with self.lock:
+            if not self.h:
+                raise RuntimeError("stream writer closed")
+            if self.lib.tv_mp4s_append(self.h, buf.ctypes.data, len(buf)) != 0:
+                raise RuntimeError(self.lib.tv_mp4s_last_error().decode())
         self.payload += len(buf)
 
     def close(self) -> int:
         """Finish the file; returns its size."""
-        h, self.h = self.h, None
-        out = C.c_ulonglong()
-        if self.lib.tv_mp4s_close(h, C.byref(out)) != 0:
-            raise RuntimeError(self.lib.tv_mp4s_last_error().decode())
+        with self.lock:
+            h, self.h = self.h, None
+            if not h:
+                raise RuntimeError("stream writer closed")
+            out = C.c_ulonglong()
+            if self.lib.tv_mp4s_close(h, C.byref(out)) != 0:
+                raise RuntimeError(self.lib.tv_mp4s_last_error().decode())
         return int(out.value)
 
     def abort(self) -> None:
-        if self.h:
-            self.lib.tv_mp4s_abort(self.h)
-            self.h = None
+        with self.lock:
+            if self.h:
+                self.lib.tv_mp4s_abort(self.h)
+                self.h = None
 
     def __del__(self):
         self.abort()

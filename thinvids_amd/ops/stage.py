@@ -211,3 +211,79 @@ def to_staging(src: DevFrames, out_w: int, out_h: int, dst, frame0: int = 0, cod
         _ok(lib.tv_resize_batch(sp, sw, sh, sstride, sfs, base + doff, dw, dh, dstride, fsz, pw, ph, src.n,
                                 ix.data_ptr(), wx.data_ptr(), tx, iy.data_ptr(), wy.data_ptr(), ty, tmp.data_ptr(),
                                 th, wp, smem, st), "ops")
+
+
+INGEST_CHUNK = 32 << 20  # bytes per ring slot (2 slots per reader thread)
+
+
+def read_y4m_device(src, start: int, n: int, device, threads: int | None = None, stats: dict | None = None) -> DevFrames:
+    """Frames [start, start + n) of a Y4M source (models.media.Y4MSource) -> device, the
+    file-ingest path of a node job (reference GET part,
+    worker/tasks.py:1497-1525): csrc/gpu/ingest.hip reads the segment's byte range with
+    `threads` pread threads into a pinned ring and streams each 32 MiB chunk to HBM with
+    hipMemcpyAsync while the next chunks are read (read and DMA overlapped, no host
+    repacking).  The FRAME headers stay in the buffer: the plane descriptors step over them.
+    `stats` accumulates the bytes, the wall seconds and the summed per-thread read seconds."""
+    import os
+
+    import torch
+
+    info = src.info
+    n = max(0, min(n, src.nframes - start))
+    nbytes = n * info.frame_bytes
+    lib = _lib()
+    if not getattr(lib, "_ingest_sigs", False):
+        lib.tv_ingest_h2d.argtypes = [C.c_char_p, C.c_longlong, C.c_longlong, C.c_void_p, C.c_void_p, C.c_longlong,
+                                      C.c_int, C.c_void_p, C.POINTER(C.c_double)]
+        lib.tv_ingest_last_error.restype = C.c_char_p
+        lib._ingest_sigs = True
+    if threads is None:
+        threads = max(1, min(12, len(os.sched_getaffinity(0))))
+    ring = _Pinned.get(2 * threads * INGEST_CHUNK)
+    esz = 2 if info.bits > 8 else 1
+    buf = torch.empty(nbytes // esz, dtype=torch.int16 if esz == 2 else torch.uint8, device=device)
+    tm = (C.c_double * 2)()
+    st = C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    if lib.tv_ingest_h2d(src.path.encode(), info.header_len + start * info.frame_bytes, nbytes,
+                         C.c_void_p(buf.data_ptr()), C.c_void_p(ring.data_ptr()), ring.numel(), threads, st, tm) != 0:
+        raise RuntimeError(f"{src.path}: ingest of frames {start}..{start + n} failed: "
+                           f"{lib.tv_ingest_last_error().decode()}")
+    w, h = info.width, info.height
+    hdr = (info.frame_bytes - w * h * 3 // 2 * esz) // esz  # FRAME header, in elements
+    fs = info.frame_bytes // esz
+    ysz, csz = w * h, (w // 2) * (h // 2)
+    planes = [(hdr, w, h, w, fs), (hdr + ysz, w // 2, h // 2, w // 2, fs), (hdr + ysz + csz, w // 2, h // 2, w // 2, fs)]
+    if stats is not None:
+        stats["read_bytes"] = stats.get("read_bytes", 0) + nbytes
+        stats["ingest_s"] = stats.get("ingest_s", 0.0) + tm[1]
+        stats["read_thread_s"] = stats.get("read_thread_s", 0.0) + tm[0]
+        stats["read_threads"] = threads
+    return DevFrames(buf, n, w, h, planes, 8 if esz == 1 else 10)
+
+
+def write_synth_y4m(path: str, w: int, h: int, n: int, seed: int = 1, device=0, chunk: int = 64) -> int:
+    """A y4m file of n frames of the seeded synthetic source, generated on the GPU
+    (tv/synth.h) `chunk` frames at a time and written as they come back — the file source
+    of the ingest bench (bench.py --job --source y4m).  Returns the file size."""
+    import os
+
+    import torch
+
+    dev = torch.device("cuda", device) if isinstance(device, int) else device
+    fsz = w * h * 3 // 2
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(f"YUV4MPEG2 W{w} H{h} F30:1 Ip A1:1 C420jpeg\n".encode())
+        for t0 in range(0, n, chunk):
+            k = min(chunk, n - t0)
+            src = synth_frames(seed, w, h, list(range(t0, t0 + k)), dev)
+            flat = src.buf.reshape(-1)
+            out = torch.empty((k, 6 + fsz), dtype=torch.uint8, device=dev)
+            out[:, :6] = torch.tensor(list(b"FRAME\n"), dtype=torch.uint8, device=dev)
+            o = 6
+            for off, pw, ph, stride, fs in src.planes:
+                out[:, o:o + pw * ph] = torch.as_strided(flat, (k, ph, pw), (fs, stride, 1), off).reshape(k, -1)
+                o += pw * ph
+            f.write(memoryview(out.cpu().numpy()).cast("B"))
+    os.replace(tmp, path)
+    return os.path.getsize(path)

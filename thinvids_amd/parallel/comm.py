@@ -121,6 +121,131 @@ def stage_segment_frames(frames, shape: tuple, device: torch.device) -> torch.Te
     return buf
 
 
+_GROUPS: dict = {}
+
+
+def stream_groups(device: torch.device):
+    """(control group, data group) of the streaming segment gather, created once per process
+    on first use — every rank reaches its first streaming job at the same point (SPMD), so
+    the collective ``new_group`` calls line up.  Control = gloo (a 16-byte header per round:
+    host-side, no GPU kernel spinning while ranks wait for each other); data = the default
+    backend (RCCL over xGMI for device tensors, gloo on CPU)."""
+    key = (dist.get_backend(), device.type)
+    if key not in _GROUPS:
+        ctrl = dist.new_group(backend="gloo")
+        data = dist.new_group(backend=dist.get_backend()) if device.type == "cuda" else ctrl
+        _GROUPS[key] = (ctrl, data)
+    return _GROUPS[key]
+
+
+class SegmentStream:
+    """Per-claim bitstream gather to the stitch rank while the node encodes — the
+    reference's encoder -> stitcher PUT of each finished part (worker/tasks.py:1655-1674,
+    received by the stitcher's ingest loop :1898-2029), as RCCL point-to-point over xGMI.
+
+    Ranks claim segments dynamically, so they finish different numbers of claims at
+    different times; a collective schedule still needs every rank in every round.  A comm
+    thread per rank therefore runs *rounds*: it waits until this rank has finished
+    segments (or ``idle_s`` passes, or the rank is done), all-gathers a (payload bytes,
+    done) header on the gloo control group, and then every peer with a payload sends it to
+    the root with one grouped isend/irecv on the data group (one xGMI hop per peer, no
+    ring).  The loop ends on every rank in the same round: the first one in which all ranks
+    report done.  The root's own segments never leave the process (``put`` hands them to
+    ``on_segment`` directly).  Only this thread touches the two stream groups, so the
+    caller may keep issuing collectives on the default group (e.g. scatter rounds)."""
+
+    def __init__(self, device: torch.device, on_segment, root: int = 0, idle_s: float = 0.02):
+        import threading
+
+        self.world, self.rank = _world()
+        self.root, self.idle_s, self.on_segment = root, idle_s, on_segment
+        self.dev = device if device.type == "cuda" and dist.get_backend() == "nccl" else torch.device("cpu")
+        self.ctrl, self.data = stream_groups(self.dev)
+        self.cv = threading.Condition()
+        self.q: list = []
+        self.done = False
+        self.err: BaseException | None = None
+        self.stats = {"rounds": 0, "segments": 0, "bytes": 0, "transfer_s": 0.0}
+        self.th = threading.Thread(target=self._run, name="segment-stream", daemon=True)
+        self.th.start()
+
+    def put(self, key, data: bytes) -> None:
+        if self.rank == self.root:
+            self.on_segment(key, data)
+            return
+        with self.cv:
+            self.q.append((key, bytes(data)))
+            self.cv.notify()
+
+    def close(self) -> dict:
+        """This rank has no more segments: returns after the round in which every rank
+        said so (raises the comm thread's error)."""
+        with self.cv:
+            self.done = True
+            self.cv.notify()
+        self.th.join()
+        if self.err is not None:
+            raise RuntimeError(f"segment stream failed: {self.err}") from self.err
+        return self.stats
+
+    def _run(self) -> None:
+        import json
+        import time
+
+        try:
+            if self.dev.type == "cuda":
+                torch.cuda.set_device(self.dev)
+            while True:
+                with self.cv:
+                    self.cv.wait_for(lambda: self.q or self.done, timeout=self.idle_s)
+                    items, self.q = self.q, []
+                    done = self.done
+                blob = b""
+                if items:
+                    idx = json.dumps([[list(k) if isinstance(k, tuple) else k, len(b)] for k, b in items]).encode()
+                    blob = len(idx).to_bytes(8, "little") + idx + b"".join(b for _, b in items)
+                hdr = torch.tensor([len(blob), int(done)], dtype=torch.int64)
+                hdrs = [torch.zeros(2, dtype=torch.int64) for _ in range(self.world)]
+                dist.all_gather(hdrs, hdr, group=self.ctrl)
+                sizes = [int(h[0]) for h in hdrs]
+                t0 = time.perf_counter()
+                self._exchange(blob, sizes)
+                self.stats["transfer_s"] += time.perf_counter() - t0
+                self.stats["rounds"] += 1
+                if all(int(h[1]) for h in hdrs):
+                    return
+        except BaseException as e:  # noqa: BLE001 - surfaced by close()
+            self.err = e
+
+    def _exchange(self, blob: bytes, sizes: list) -> None:
+        import json
+
+        if self.rank == self.root:
+            bufs = {r: torch.empty(sizes[r], dtype=torch.uint8, device=self.dev)
+                    for r in range(self.world) if r != self.root and sizes[r] > 0}
+            if not bufs:
+                return
+            ops = [dist.P2POp(dist.irecv, b, r, group=self.data) for r, b in bufs.items()]
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+            for r in sorted(bufs):
+                raw = bufs[r].cpu().numpy().tobytes()
+                hl = int.from_bytes(raw[:8], "little")
+                off = 8 + hl
+                for k, n in json.loads(raw[8:off]):
+                    self.on_segment(tuple(k) if isinstance(k, list) else k, raw[off:off + n])
+                    off += n
+                    self.stats["segments"] += 1
+                self.stats["bytes"] += len(raw)
+        elif blob:
+            t = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+            if self.dev.type == "cuda":
+                t = t.pin_memory().to(self.dev, non_blocking=True)
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, self.root, group=self.data)]):
+                req.wait()
+            self.stats["bytes"] += len(blob)
+
+
 def allreduce_stats(values, device: torch.device, op: str = "sum") -> np.ndarray:
     """All-reduce a small float64 vector (e.g. per-segment complexity for 2-pass RC)."""
     t = torch.as_tensor(np.asarray(values, dtype=np.float64), device=device)

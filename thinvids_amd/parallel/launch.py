@@ -48,6 +48,11 @@ def spawn_ranks(n: int, argv: list[str], extra_env: dict | None = None, timeout:
         procs.append(subprocess.Popen([sys.executable, *argv], env=env, start_new_session=True))
     t0 = time.monotonic()
     rc = 0
+    old = None
+    try:  # a SIGTERM of the launcher (e.g. `timeout`) must not orphan the rank groups
+        old = signal.signal(signal.SIGTERM, _raise_interrupt)
+    except ValueError:  # not the main thread
+        pass
     try:
         live = list(procs)
         while live:
@@ -71,6 +76,8 @@ def spawn_ranks(n: int, argv: list[str], extra_env: dict | None = None, timeout:
             _kill_group(q, signal.SIGTERM)
         raise
     finally:
+        if old is not None:
+            signal.signal(signal.SIGTERM, old)
         for q in procs:
             if q.poll() is None:
                 try:
@@ -79,6 +86,10 @@ def spawn_ranks(n: int, argv: list[str], extra_env: dict | None = None, timeout:
                     _kill_group(q, signal.SIGKILL)
                     q.wait()
     return rc
+
+
+def _raise_interrupt(signum, frame):
+    raise KeyboardInterrupt(f"signal {signum}")
 
 
 def _kill_group(p: subprocess.Popen, sig) -> None:

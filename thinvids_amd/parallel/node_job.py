@@ -17,10 +17,10 @@ Flow (the reference's split -> encode -> stitch, without HTTP or disk in between
    per-segment sizes are **all-reduced** and every rank derives the same per-segment QP
    plan (complexity^0.6 allocation), then encodes pass 2;
 5. single-pass jobs with a plain MP4 output are **stitched while they encode**: every
-   finished segment goes to rank 0 (its own in memory, the peers' as part files in the
-   node-local job directory, written off the critical path), whose stitch thread appends
-   each rung's segments in order to a streaming faststart MP4 writer (ranks keep no
-   bitstreams); otherwise bitstreams are gathered to rank 0 after the last pass (all_gather
+   finished claim goes to rank 0 (its own in memory, the peers' over RCCL point-to-point
+   in per-claim gather rounds on a comm thread, comm.SegmentStream), whose stitch thread
+   appends each rung's segments in order to a streaming faststart MP4 writer (ranks keep
+   no bitstreams; ``TV_STITCH_TRANSPORT=files`` falls back to part files); otherwise bitstreams are gathered to rank 0 after the last pass (all_gather
    of sizes + grouped send/recv) and muxed in segment order.  ``--ladder`` fans rungs x
    segments out over all ranks and writes one MP4 per rung.
 """
@@ -276,6 +276,29 @@ def _part_path(parts_dir: str, r: int, i: int) -> str:
     return os.path.join(parts_dir, f"r{r}_s{i}.part")
 
 
+def _attempt_parts_dir(output: str, job_tag: str, rank: int) -> str:
+    """Part-file directory of THIS attempt of the job (file transport only): rank 0 empties
+    ``{output}.parts`` and publishes a fresh token through the rendezvous store before any
+    peer can write, so parts left by a killed earlier attempt (same output name, possibly
+    other settings) are never read into this one."""
+    import shutil
+    import uuid
+
+    root = f"{output}.parts"
+    dist = _dist()
+    store = dist.distributed_c10d._get_default_store() if dist else None
+    key = _ns(f"{job_tag}_parts_token")
+    if rank == 0:
+        shutil.rmtree(root, ignore_errors=True)
+        token = uuid.uuid4().hex[:16]
+        os.makedirs(os.path.join(root, token))
+        if store is not None:
+            store.set(key, token)
+    else:
+        token = store.get(key).decode()  # blocks until rank 0 has cleaned up and published
+    return os.path.join(root, token)
+
+
 def publish_part(parts_dir: str, r: int, i: int, data: bytes) -> None:
     """A peer rank's finished segment for the stitch rank: written to a temporary name and
     renamed, so the stitcher never sees a partial part."""
@@ -290,11 +313,13 @@ class StreamStitcher:
     """Rank 0's stitch thread (reference overlap: the stitcher ingests parts while encoders
     run, worker/tasks.py:1805-1822, :1898-2029): segment i of every rung is appended, in
     segment order, to that rung's streaming faststart MP4 (models.hevc.Mp4StreamWriter) as
-    soon as it exists -- rank 0's own segments arrive through put(), the peers' as part
-    files (publish_part) that are read once and deleted.  Nothing is joined or copied at
-    the end: close() only writes each file's head."""
+    soon as it exists.  Segments arrive through put(): rank 0's own directly, the peers'
+    from the RCCL segment stream (comm.SegmentStream).  With ``parts_dir`` set (the
+    ``TV_STITCH_TRANSPORT=files`` fallback) peers' segments are part files (publish_part)
+    that are read once and deleted.  Nothing is joined or copied at the end: close() only
+    writes each file's head."""
 
-    def __init__(self, parts_dir: str, paths: list, geoms: list, nseg: int, frames: int, fps_num: int, fps_den: int):
+    def __init__(self, parts_dir: str | None, paths: list, geoms: list, nseg: int, frames: int, fps_num: int, fps_den: int):
         from ..models.hevc import Mp4StreamWriter
 
         self.parts_dir, self.paths, self.nseg = parts_dir, paths, nseg
@@ -314,20 +339,21 @@ class StreamStitcher:
             self.cv.notify()
 
     def _get(self, r: int, i: int) -> bytes:
-        path = _part_path(self.parts_dir, r, i)
+        path = _part_path(self.parts_dir, r, i) if self.parts_dir else None
         while True:
             with self.cv:
                 if (r, i) in self.own:
                     return self.own.pop((r, i))
                 if self.stop:
                     raise RuntimeError("stitch cancelled")
-            if os.path.exists(path):
+            if path and os.path.exists(path):
                 with open(path, "rb") as f:
                     data = f.read()
                 os.remove(path)
                 return data
-            with self.cv:
-                self.cv.wait(0.005)
+            with self.cv:  # put() notifies; only the file fallback needs the short poll
+                if (r, i) not in self.own and not self.stop:
+                    self.cv.wait(0.005 if path else 1.0)
 
     def _run(self) -> None:
         try:
@@ -352,12 +378,17 @@ class StreamStitcher:
         return self.sizes
 
     def cancel(self) -> None:
+        """Stop the stitch thread; it aborts its own writers on the way out (all writer
+        calls stay on that thread).  If it does not exit in time (stuck inside a native
+        append), the writers and files are left alone and only the error is reported."""
         with self.cv:
             self.stop = True
             self.cv.notify_all()
         self.th.join(timeout=30)
-        for w in self.writers:
-            w.abort()
+        if self.th.is_alive():
+            print("[node_job] stitch thread did not stop within 30 s; its files are left in place",
+                  file=sys.stderr, flush=True)
+            return
         for p in self.paths:
             if os.path.exists(p):
                 os.remove(p)
@@ -411,7 +442,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     from ..models.streams import write_output
     from ..worker.encoder import EncodeSpec, EngineCache, PartStats, SynthRange, gpu_available, psnr_from_sse
     from ..worker.helpers import output_geometry
-    from .comm import allreduce_stats, gather_bytes_to_root, scatter_frames_from_root, scatter_root, stage_segment_frames
+    from .comm import (SegmentStream, allreduce_stats, gather_bytes_to_root, scatter_frames_from_root, scatter_root,
+                       stage_segment_frames)
 
     hooks = hooks or JobHooks()
     trace0 = trace.summary()
@@ -458,13 +490,17 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     out_paths = [output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4" for _, oh in rungs]
     if side is not None:
         out_paths = [os.path.splitext(p)[0] + side.ext for p in out_paths]
-    parts_dir = f"{output}.parts"
+    # peers' finished segments reach the stitch rank over RCCL (comm.SegmentStream); the
+    # part-file hand-off through the node-local job directory is the fallback
+    transport = os.environ.get("TV_STITCH_TRANSPORT", "rccl") if world > 1 else "local"
+    parts_dir = None
     stitcher = None
-    if streaming:
-        os.makedirs(parts_dir, exist_ok=True)
-        if rank == 0:
-            stitcher = StreamStitcher(parts_dir, [p + ".tmp" for p in out_paths], rungs, len(segs), nfr,
-                                      src.fps_num, src.fps_den)
+    if streaming and transport == "files":
+        parts_dir = _attempt_parts_dir(output, job_tag, rank)
+    if streaming and rank == 0:
+        stitcher = StreamStitcher(parts_dir, [p + ".tmp" for p in out_paths], rungs, len(segs), nfr,
+                                  src.fps_num, src.fps_den)
+    gather = {"stream": None, "stats": {}}
     # checkpoint (hash + write) and peer part files are written off the critical path
     io_pool = cf.ThreadPoolExecutor(1)
     io_futs: list = []
@@ -495,19 +531,41 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         q = round_qps(rc["plan"][r][i], offset)
         return q, "p" + hashlib.sha1(q.astype(np.int8).tobytes()).hexdigest()[:12]
 
+    prefetched: dict = {}  # segment -> device frames loaded ahead by the prefetch thread
+
     def load(i):
-        """Segment i's source: a synthetic range (generated where it is encoded), or host
-        frames uploaded to this GPU once for all rungs."""
+        """Segment i's source: a synthetic range (generated where it is encoded), a Y4M byte
+        range read in parallel into pinned memory and copied to this GPU once for all rungs
+        (stage.read_y4m_device), or decoded host frames uploaded once."""
+        if i in prefetched:
+            return prefetched.pop(i)
         s, n = segs[i]
         stats["reads"] += 1
         if synthetic:
             return SynthRange(src.seed, w0, h0, src.start + s, n)
-        frames = src.read(s, n)
         if software:
-            return frames
+            return src.read(s, n)
         from ..ops import stage
 
-        return stage.upload_frames(frames, dev)
+        if isinstance(src, media.Y4MSource):
+            return stage.read_y4m_device(src, s, n, dev, stats=stats)
+        return stage.upload_frames(src.read(s, n), dev)
+
+    # file sources on the GPU: the next claim is read + uploaded on a side thread / HIP
+    # stream while this claim encodes (the reference overlaps GET part with the previous
+    # encode only across nodes; here ingest hides behind the engine on every rank)
+    prefetch = not synthetic and not software and dev.type == "cuda" and os.environ.get("TV_PREFETCH", "1") != "0"
+    prefetcher = None
+    if prefetch:
+        def _prefetch_init():
+            torch.cuda.set_device(dev)
+            _prefetch_init.stream = torch.cuda.Stream(dev)
+
+        prefetcher = cf.ThreadPoolExecutor(1, initializer=_prefetch_init)
+
+        def load_ahead(ids):
+            with torch.cuda.stream(_prefetch_init.stream), trace.span("node_job.prefetch"):
+                return {i: load(i) for i in ids}
 
     def encode_segments(seg_ids, source_of) -> dict:
         """Work item = one segment with ALL its rungs: the source range is read (or received)
@@ -561,7 +619,9 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 ctl.record(sum(8.0 * sum(rc["bits"][(r, i)]) for i in seg_ids))
         if streaming:  # the stitch rank takes them now; this rank keeps no bitstream
             for (r, i), b in out.items():
-                if stitcher is not None:
+                if gather["stream"] is not None:
+                    gather["stream"].put((r, i), b)
+                elif stitcher is not None:
                     stitcher.put(r, i, b)
                 else:
                     io_futs.append(io_pool.submit(publish_part, parts_dir, r, i, b))
@@ -665,20 +725,40 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     for i in todo:
                         wq.fail((i,), repr(e))
 
-            while True:
-                msg = wq.aborted()
-                if msg:
-                    raise RuntimeError(msg)
-                if hooks.halted():
-                    wq.fail_all("job halted")
-                    raise RuntimeError("job halted")
-                with trace.span("node_job.claim"):
-                    claimed = wq.claim(batch_segments)  # a batch -> one batched launch per rung
-                if not claimed:
-                    break
-                run(claimed)
-                if len(claimed) < batch_segments:
-                    break
+            ahead = None  # (next claim, future of its loaded segments)
+            try:
+                while True:
+                    msg = wq.aborted()
+                    if msg:
+                        raise RuntimeError(msg)
+                    if hooks.halted():
+                        wq.fail_all("job halted")
+                        raise RuntimeError("job halted")
+                    if ahead is not None:
+                        claimed, fut = ahead
+                        ahead = None
+                        with trace.span("node_job.prefetch_wait"):
+                            try:
+                                prefetched.update(fut.result())
+                            except Exception:  # noqa: BLE001 - run() reloads and takes the failure path
+                                pass
+                    else:
+                        with trace.span("node_job.claim"):
+                            claimed = wq.claim(batch_segments)  # a batch -> one batched launch per rung
+                    if not claimed:
+                        break
+                    if prefetcher is not None and len(claimed) == batch_segments:
+                        with trace.span("node_job.claim"):
+                            nxt = wq.claim(batch_segments)
+                        if nxt:
+                            ahead = (nxt, prefetcher.submit(load_ahead, nxt))
+                    run(claimed)
+                    if len(claimed) < batch_segments and ahead is None:
+                        break
+            finally:
+                if ahead is not None:
+                    ahead[1].cancel()
+                prefetched.clear()
             wq.fresh_done()
             while not wq.finished():  # failed segments, re-published for any rank
                 msg = wq.aborted()
@@ -709,12 +789,21 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             err, got = None, {}
             hooks.new_pass(agreed_pass.n)
             agreed_pass.n += 1
+            if streaming and transport == "rccl":
+                gather["stream"] = SegmentStream(cdev, lambda k, b: stitcher.put(*k, b), root=0)
             try:
                 got = encode_pass()
                 with trace.span("node_job.io_drain"):
                     drain_io()  # checkpoints and part files of this pass are on disk
             except Exception as e:  # noqa: BLE001 - re-raised below on every rank
                 err = e
+            if gather["stream"] is not None:  # this rank is done: leave the gather rounds
+                with trace.span("node_job.stream_close"):
+                    try:
+                        gather["stats"] = gather["stream"].close()
+                    except Exception as e:  # noqa: BLE001
+                        err = err or e
+                gather["stream"] = None
             with trace.span("node_job.verdict"):
                 failed = allreduce_stats([1.0 if err else 0.0], cdev, op="max")[0]
             if failed:
@@ -792,7 +881,9 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         with trace.span("node_job.gather"):
             parts = gather_bytes_to_root(blob, cdev) if world > 1 else [blob]
         result = {"world": world, "segments": len(segs), "rungs": [list(x) for x in rungs], "passes": passes,
-                  "rc": rc_name, "rc_errors": rc_errors}
+                  "rc": rc_name, "rc_errors": rc_errors,
+                  "stitch": {"streaming": streaming, "transport": transport if streaming else "gather",
+                             **{k: round(v, 4) if isinstance(v, float) else v for k, v in gather["stats"].items()}}}
         if abr:
             result["abr_steps_rank0"] = [c.log for c in rc["abr"]]  # [actual, want, offset] / nominal
         if vbv:
@@ -848,10 +939,12 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         raise
     finally:
         io_pool.shutdown(wait=True)
-        if streaming and rank == 0:
+        if prefetcher is not None:
+            prefetcher.shutdown(wait=True)
+        if parts_dir and rank == 0:
             import shutil
 
-            shutil.rmtree(parts_dir, ignore_errors=True)
+            shutil.rmtree(os.path.dirname(parts_dir), ignore_errors=True)
     if own_cache:
         cache.close()
     return result

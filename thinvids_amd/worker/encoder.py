@@ -100,45 +100,126 @@ def psnr_from_sse(sse, npx_luma: float) -> dict:
     return {"y": y, "u": u, "v": v, "yuv": (6 * y + u + v) / 8}
 
 
+HBM_FRACTION = 0.8  # share of the GPU's HBM the engine cache may hold (TV_HBM_FRACTION)
+
+
+def device_budget(device: int = 0) -> int:
+    """Bytes of HBM the engines of this process may use: ``TV_HBM_BUDGET_GB`` when set, else
+    TV_HBM_FRACTION (0.8) of the device's total memory (hipMemGetInfo via torch)."""
+    gb = os.environ.get("TV_HBM_BUDGET_GB")
+    if gb:
+        return int(float(gb) * (1 << 30))
+    import torch
+
+    _, total = torch.cuda.mem_get_info(device)
+    return int(float(os.environ.get("TV_HBM_FRACTION", HBM_FRACTION)) * total)
+
+
+def _staging_bytes(spec: "EncodeSpec", batch: int) -> int:
+    from ..ops.stage import staging_planes
+
+    if spec.codec == "av1":
+        from ..models.av1 import coded_size
+
+        fsz, _ = staging_planes(spec.width, spec.height, coded_size(spec.width, spec.height))
+    else:
+        fsz, _ = staging_planes(spec.width, spec.height)
+    return batch * spec.gop * fsz
+
+
+def engine_bytes(spec: "EncodeSpec", batch: int) -> int:
+    """Device bytes of an engine for `spec` at `batch` segments, including the staging
+    buffer the cache attaches to it (batch x GOP coded frames).  HEVC: the native
+    constructor's own size formulas (gpu_engine.estimate_footprint); AV1: its per-segment
+    GOP decision slots and frame sets (models/av1_engine.py allocations)."""
+    if spec.codec == "av1":
+        from ..models.av1 import coded_size
+
+        W, H = coded_size(spec.width, spec.height)
+        # two GOP decision slots of (mode, mv, 256 + 2 x 64 int16 levels) per 16x16 block
+        # and frame (~384 B per pixel of a GOP-64 segment), plus the source / recon /
+        # filtered frame sets and the filters' scratch (~11 coded frames)
+        eng = batch * (2 * spec.gop * (W // 16) * (H // 16) * 776 + 11 * W * H * 3 // 2)
+    else:
+        from ..models.gpu_engine import estimate_footprint
+
+        eng = estimate_footprint(spec.width, spec.height, batch, spec.gop, spec.sao, spec.hevc_bframes())["dev"]
+    return eng + _staging_bytes(spec, batch)
+
+
 class EngineCache:
     """Per-process GPU engines keyed by stream geometry/QP (allocation is HBM-heavy, so an
     engine lives for the life of the consumer).  Thread-safe; one engine serialises its
     own calls.  Each engine owns a device staging buffer (batch x GOP coded frames).
-    ``batch=0`` sizes each engine for its resolution (segments in flight that fill 256 CUs,
-    measured: 48 at <= 1080p, 24 at 4K; profiles/README.md)."""
 
-    def __init__(self, device: int = 0, batch: int = 8, max_engines: int = 4):
+    Sized in BYTES, not engine counts (the reference sizes work by bytes too: its 10 MiB
+    segment target, common.py:184): every engine's footprint (native allocation ledger +
+    staging) is charged against ``budget`` (default: device_budget(), 0.8 of HBM), and the
+    least recently used engines are evicted until a new one fits.  ``max_engines`` stays
+    an upper bound on the count.  ``batch=0`` sizes each engine with auto_batch(spec,
+    budget): the CU-fill heuristic capped by the byte budget."""
+
+    def __init__(self, device: int = 0, batch: int = 8, max_engines: int = 8, budget: int | None = None):
         self.device, self.batch, self.max_engines = device, batch, max_engines
+        self._budget = budget
         self._engines: dict = {}
+        self._bytes: dict = {}
         self._order: list = []
         self._lock = threading.Lock()
         self.constructed = 0
+        self.evicted = 0
 
-    def get(self, spec: EncodeSpec):
+    @property
+    def budget(self) -> int:
+        if self._budget is None:
+            self._budget = device_budget(self.device)
+        return self._budget
+
+    def used_bytes(self) -> int:
+        return sum(self._bytes.values())
+
+    def _build(self, spec: "EncodeSpec", batch: int):
         from ..models.gpu_engine import GpuEngine
 
+        if spec.codec == "av1":
+            from ..models.av1_engine import Av1GpuEngine
+
+            eng = Av1GpuEngine(spec.width, spec.height, batch=batch, qindex=spec.av1_qindex(), device=self.device)
+            eng.batch = eng.B
+            return eng
+        return GpuEngine(spec.width, spec.height, qp=spec.qp, batch=batch, gop=spec.gop, search_range=spec.search_range,
+                         deblock=spec.deblock, sao=spec.sao, seed=spec.seed, device=self.device, crf=spec.crf,
+                         bframes=spec.hevc_bframes())
+
+    def get(self, spec: EncodeSpec):
         key = spec.engine_key()
         with self._lock:
             eng = self._engines.get(key)
-            if eng is None:
-                while len(self._order) >= self.max_engines:
-                    old = self._order.pop(0)
-                    self._engines.pop(old).close()
-                if spec.codec == "av1":
-                    from ..models.av1_engine import Av1GpuEngine
-
-                    eng = Av1GpuEngine(spec.width, spec.height, batch=min(32, self.batch or auto_batch(spec)),
-                                       qindex=spec.av1_qindex(), device=self.device)
-                    eng.batch = eng.B
-                else:
-                    eng = GpuEngine(spec.width, spec.height, qp=spec.qp, batch=self.batch or auto_batch(spec),
-                                    gop=spec.gop, search_range=spec.search_range, deblock=spec.deblock, sao=spec.sao,
-                                    seed=spec.seed, device=self.device, crf=spec.crf, bframes=spec.hevc_bframes())
-                eng.lock = threading.Lock()
-                eng.staging = None
-                self._engines[key] = eng
+            if eng is not None:  # LRU: most recently used last
+                self._order.remove(key)
                 self._order.append(key)
-                self.constructed += 1
+                return eng
+            batch = self.batch or auto_batch(spec, self.budget)
+            if spec.codec == "av1":
+                batch = min(32, batch)
+            batch = max(1, min(64, batch))
+            need = engine_bytes(spec, batch)
+            if need > self.budget:
+                raise MemoryError(f"an engine for {spec.width}x{spec.height} x{batch} needs {need / 2**30:.1f} GiB, "
+                                  f"over the HBM budget of {self.budget / 2**30:.1f} GiB")
+            while self._order and (len(self._order) >= self.max_engines or self.used_bytes() + need > self.budget):
+                old = self._order.pop(0)
+                self._engines.pop(old).close()
+                self._bytes.pop(old)
+                self.evicted += 1
+            eng = self._build(spec, batch)
+            eng.lock = threading.Lock()
+            eng.staging = None
+            fp = eng.footprint()["dev"] if hasattr(eng, "footprint") else None
+            self._bytes[key] = (fp + _staging_bytes(spec, batch)) if fp is not None else need
+            self._engines[key] = eng
+            self._order.append(key)
+            self.constructed += 1
             return eng
 
     def close(self):
@@ -146,12 +227,26 @@ class EngineCache:
             for e in self._engines.values():
                 e.close()
             self._engines.clear()
+            self._bytes.clear()
             self._order.clear()
 
 
-def auto_batch(spec: EncodeSpec) -> int:
+def auto_batch(spec: EncodeSpec, budget: int | None = None) -> int:
+    """Segments per engine call: enough CTBs in flight to fill 256 CUs (measured on MI355X:
+    48 at <= 1080p, 24 at 4K, 8 above; profiles/README.md), capped so that the engine plus
+    its staging buffer take at most half of the HBM budget (the rest holds the claims'
+    source frames, the ABR rungs and a second engine)."""
     px = spec.width * spec.height
-    return 48 if px <= 1920 * 1088 else (24 if px <= 3840 * 2176 else 8)
+    if spec.codec == "av1":  # measured: 32 at <= 1080p, 16 at 4K (bench.py --codec av1)
+        want = 32 if px <= 1920 * 1088 else (16 if px <= 3840 * 2176 else 4)
+    else:
+        want = 48 if px <= 1920 * 1088 else (24 if px <= 3840 * 2176 else 8)
+    if budget is None:
+        return want
+    b = want
+    while b > 1 and engine_bytes(spec, b) > budget // 2:
+        b = max(1, b * 3 // 4)
+    return b
 
 
 _default_cache: EngineCache | None = None

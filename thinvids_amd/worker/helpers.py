@@ -159,7 +159,9 @@ def reset_job_run_state(job_id: str, job: dict | None = None, store=None) -> Non
     zero = {k: 0 for k in ("parts_total", "parts_done", "segmented_chunks", "completed_chunks",
                            "stitched_chunks", "segment_progress", "segment_elapsed", "encode_progress",
                            "encode_elapsed", "combine_progress", "combine_elapsed", "failed_part",
-                           "last_heartbeat_at", "ended_at")}
+                           "last_heartbeat_at", "ended_at", "rc_pass", "encoded_frames",
+                           *(f"{f}_p{k}" for f in ("parts_done", "completed_chunks", "encoded_frames")
+                             for k in (1, 2)))}
     blank = {k: "" for k in ("error", "failed_stage", "failed_worker", "processing_mode_effective",
                              "processing_mode_reason", "direct_segment_duration", "last_heartbeat_stage",
                              "last_heartbeat_host", "last_heartbeat_note")}

@@ -85,12 +85,17 @@ class _StoreHooks:
         self.pass_idx = 0
 
     def new_pass(self, index: int) -> None:
+        """Pass `index` starts: readers switch to its counters (``rc_pass``, see
+        common.pass_field) and the progress bar restarts."""
         self.pass_idx = index
+        if index:
+            get_store().hset(job_key(self.job_id), mapping={"rc_pass": index, "encode_progress": 0})
 
     def segment_done(self, frames: int) -> None:
-        """Per-pass counters (2-pass / 3-pass jobs): every rank increments the pass's own
-        fields and mirrors them into parts_done / completed_chunks, so those never exceed
-        parts_total; encoded_frames counts the frames of the final pass the same way."""
+        """Every rank increments its segments into the current pass's own counters (pass 0:
+        parts_done / completed_chunks / encoded_frames; pass k: the ``_p<k>`` fields) in one
+        atomic pipeline -- counters are only ever incremented, never mirrored by a
+        read-modify-write, so concurrent ranks cannot move them backwards."""
         if self.beat is not None:
             self.beat.progress("segment")
         st = get_store()
@@ -102,8 +107,6 @@ class _StoreHooks:
         p.hincrby(k, "encoded_frames" + sfx, int(frames))
         res = p.execute()
         done = int(res[1])
-        if sfx:
-            st.hset(k, mapping={"completed_chunks": int(res[0]), "parts_done": done, "encoded_frames": int(res[2])})
         prog = int(done * 100 / max(1, self.total))
         if prog > int(st.hget(k, "encode_progress") or 0):
             st.hset(k, mapping={"encode_progress": prog, "encode_elapsed": int(now() - self.t0)})
@@ -251,6 +254,9 @@ def _publish(job_id: str, spec: dict, res: dict) -> None:
               "bitrate_kbps": round(outs[0]["kbps"], 1), "rc_passes": res.get("passes", 1),
               "qp_plan_json": json.dumps(res.get("qp_plan", [])[:1]),
               "trace_json": json.dumps(res.get("trace") or {}), "job_seconds": res.get("seconds"),
+              "ingest_json": json.dumps([{k: p.get(k) for k in ("reads", "read_bytes", "ingest_s", "read_thread_s", "read_threads", "encoded")}
+                                         for p in res.get("per_rank") or []]),
+              "stitch_json": json.dumps(res.get("stitch") or {}),
               "ladder_outputs_json": json.dumps(
                   [{"path": f, "width": o["width"], "height": o["height"], "kbps": round(o["kbps"], 1),
                     "psnr_y": o.get("psnr_y")} for f, o in zip(finals, outs)]) if len(outs) > 1 else ""}
