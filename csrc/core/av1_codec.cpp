@@ -1865,7 +1865,9 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
       for (int y = 0; y < g.H + 2 * kPad; ++y)
         for (int x = 0; x < pw; ++x) padY[(size_t)y * pw + x] = (uint8_t)ry(x - kPad, y - kPad);
     }
-    auto code_block = [&](int by, int bx) {
+    // intra blocks, inter blocks at a given MV (force_mv), or the motion search alone
+    // (search_out: the block's MV, nothing coded)
+    auto code_block = [&](int by, int bx, const uint32_t* force_mv, uint32_t* search_out) {
         const int b = by * g.bw + bx;
         int s[3][256], pred[3][256], rc[256];
         for (int p = 0; p < 3; ++p) {
@@ -1899,6 +1901,10 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
               std::memcpy(pred[2], pv, sizeof(pv));
             }
           }
+        } else if (force_mv) {
+          inter = 1;
+          mvw = *force_mv;
+          for (int p = 0; p < 3; ++p) predict(g, p, bx, by, pack_mode(1, 0, 0, 0, 0), mvw, rec, ref, pred[p]);
         } else {
           inter = 1;
           // integer search on the edge-extended reference
@@ -1939,6 +1945,10 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
             mc = bcc;
           }
           mvw = pack_mv(mr, mc);
+          if (search_out) {
+            *search_out = mvw;
+            return;
+          }
           for (int p = 0; p < 3; ++p) predict(g, p, bx, by, pack_mode(1, 0, 0, 0, 0), mvw, rec, ref, pred[p]);
         }
         int nz = 0;
@@ -1959,10 +1969,36 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
     };
     if (fd.fp.key) {  // intra: left / above dependencies (raster order)
       for (int by = 0; by < g.bh; ++by)
-        for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx);
+        for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx, nullptr, nullptr);
     } else {  // inter blocks only read the reference: rows in parallel
+      // per-block search (the MVs only), kMvRefineRounds rounds of the neighbour-MV
+      // refinement (tv/av1_enc.h), then every block coded with its final MV
+      std::vector<uint32_t> mvs(nb), nxt(nb);
       parallel_rows(g.bh, [&](int by) {
-        for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx);
+        for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx, nullptr, &mvs[by * g.bw + bx]);
+      });
+      for (int round = 0; round < kMvRefineRounds; ++round) {
+        parallel_rows(g.bh, [&](int by) {
+          for (int bx = 0; bx < g.bw; ++bx) {
+            const int b = by * g.bw + bx;
+            uint32_t cand[kMvRefineMaxCand];
+            const int nc = mv_refine_cands(mvs.data(), g.bw, g.bh, bx, by, cand);
+            int s0[256];
+            for (int i = 0; i < 16; ++i)
+              for (int j = 0; j < 16; ++j) s0[i * 16 + j] = S.y[(size_t)(by * 16 + i) * g.W + bx * 16 + j];
+            int best = 1 << 30;
+            for (int k = 0; k < nc; ++k) {
+              int pr[256];
+              predict(g, 0, bx, by, pack_mode(1, 0, 0, 0, 0), cand[k], rec, ref, pr);
+              const int c = satd_block(s0, pr, 16);
+              if (c < best) best = c, nxt[b] = cand[k];
+            }
+          }
+        });
+        mvs.swap(nxt);
+      }
+      parallel_rows(g.bh, [&](int by) {
+        for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx, &mvs[by * g.bw + bx], nullptr);
       });
       for (int sy = 0; sy < g.sbh; ++sy)
         for (int sx = 0; sx < g.sbw; ++sx) merge_sb(fd.mode.data(), fd.mv.data(), g.bw, g.bh, sx, sy);

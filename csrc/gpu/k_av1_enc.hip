@@ -178,10 +178,13 @@ struct Planes3W {
 };
 
 // ================================================================= inter ================
+// STAGE 0: the motion search only (mvout = the block's MV).  STAGE 1: prediction at mvin
+// (the refined field) + residual coding + reconstruction (mvout = mvin).
+template <int STAGE>
 __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Planes3W rec, uint32_t* __restrict__ mode,
-                                                   uint32_t* __restrict__ mvout, int16_t* __restrict__ ly,
-                                                   int16_t* __restrict__ lu, int16_t* __restrict__ lv, int W, int H,
-                                                   const int* __restrict__ qarr) {
+                                                   const uint32_t* __restrict__ mvin, uint32_t* __restrict__ mvout,
+                                                   int16_t* __restrict__ ly, int16_t* __restrict__ lu,
+                                                   int16_t* __restrict__ lv, int W, int H, const int* __restrict__ qarr) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kWinN * kWinP + 8];
   __shared__ __attribute__((aligned(16))) uint8_t sblk[256];
   __shared__ __attribute__((aligned(16))) uint8_t cwin[2][kCWin * kCWin];
@@ -216,7 +219,7 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
       win[wy * kWinP + wx] = Rf[(long)yy * W + xx];
     }
   }
-  {
+  if (STAGE == 1) {
     const int Wc = W >> 1, Hc = H >> 1, cwx = bx * 8 - kCWinOff, cwy = by * 8 - kCWinOff;
     const bool in = cwx >= 0 && cwy >= 0 && cwx + kCWin <= Wc && cwy + kCWin <= Hc;
     for (int pl = 0; pl < 2; ++pl) {
@@ -237,6 +240,28 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   }
   for (int i = lane; i < 256; i += 64) sblk[i] = S[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)];
   __syncthreads();
+  const int nb = bw * (H >> 4);
+  const long bo = (long)b * nb + blk;
+  auto wget = [&](int x, int y) -> int {  // window sample at block-relative (x, y)
+    return win[(kWinOff + y) * kWinP + kWinOff + x];
+  };
+  int mr = 0, mc = 0, yb = 0;
+  if (STAGE == 1) {
+    // the refined MV: its horizontal plane (column offset 0) for the luma prediction below
+    mr = mv_row(mvin[bo]);
+    mc = mv_col(mvin[bo]);
+    yb = (mr >> 3) - 3;
+    const int ix = mv_int(mc, false), fx = mv_frac(mc, false);
+    for (int idx = lane; idx < 23 * 16; idx += 64) {
+      const int yy = idx >> 4, x = idx & 15;
+      int sum = 0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) sum += subpel_tap(fx, t) * wget(x + ix + t - 3, yb + yy);
+      hpl[1][yy][x] = (int16_t)((sum + (1 << (kInterRound0 - 1))) >> kInterRound0);
+    }
+    lastk = 1;
+    __syncthreads();
+  } else {
   // ---- full-pel search: packed SAD, first minimum of (cost, index)
   uint32_t sv[64];
 #pragma unroll
@@ -291,16 +316,12 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
     if (bi >= 0) gx += me_ring_dx(bi), gy += me_ring_dy(bi);
     __syncthreads();
   }
-  int mr = gy * 8, mc = gx * 8;
+  mr = gy * 8, mc = gx * 8;
   // ---- sub-pel refinement: center + 8 ring candidates at step 4 (half) then 2 (quarter)
-  auto wget = [&](int x, int y) -> int {  // window sample at block-relative (x, y)
-    return win[(kWinOff + y) * kWinP + kWinOff + x];
-  };
   // Separable and shared: per step, the three horizontally filtered planes (column offsets
   // -step, 0, +step) are computed once into LDS (int16, Round0), then each of the 9
   // candidates only runs the vertical 8-tap pass (the same integers as inter_pred_px).
   const int grp = lane >> 4, b4 = lane & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
-  int yb = 0;
   for (int step = 4; step >= 2; step >>= 1) {
     yb = ((mr - step) >> 3) - 3;
     const int nrows = ((mr + step) >> 3) + 19 - yb + 1;  // <= 25
@@ -354,8 +375,11 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
     }
     __syncthreads();
   }
-  // ---- luma prediction + residual: vertical pass of the chosen candidate over the last
-  // step's horizontal plane
+  if (lane == 0) mvout[bo] = pack_mv(mr, mc);
+  return;
+  }  // STAGE 0
+  // ---- luma prediction + residual: vertical pass of the chosen candidate over the
+  // horizontal plane
   {
     const int iy = mv_int(mr, false), fy = mv_frac(mr, false);
     for (int i = lane; i < 256; i += 64) {
@@ -369,8 +393,6 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
     }
   }
   __syncthreads();
-  const int nb = bw * (H >> 4);
-  const long bo = (long)b * nb + blk;
   int nz = code_tb<4>(res, ta, tb, ti, 0, 0, qidx, kRndInter, ly + bo * 256);
   for (int i = lane; i < 256; i += 64)
     rec.y[b * ysz + (long)(y0 + (i >> 4)) * W + x0 + (i & 15)] = (uint8_t)clip_pixel(predc[i] + res[i]);
@@ -398,6 +420,96 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   if (lane == 0) {
     mode[bo] = pack_mode(1, 0, 0, nz == 0, nz);
     mvout[bo] = pack_mv(mr, mc);
+  }
+}
+
+// One Jacobi round of the motion-field refinement (tv/av1_enc.h mv_refine_cands): one wave
+// per 16x16 block re-chooses among its neighbours' current MVs by luma SATD (first
+// minimum, own MV first).  Candidates x 16 lanes: each lane predicts one 4x4 of the block
+// from the staged reference window (the 8-tap separable filter of inter_pred_px) and
+// takes its SATD; 4 candidates per pass.
+__global__ void __launch_bounds__(64) k_av1e_mv_refine(const uint8_t* __restrict__ srcy, const uint8_t* __restrict__ refy,
+                                                       const uint32_t* __restrict__ cur, uint32_t* __restrict__ nxt,
+                                                       int W, int H) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kWinN * kWinP + 8];
+  __shared__ __attribute__((aligned(16))) uint8_t sblk[256];
+  __shared__ uint32_t cand[kMvRefineMaxCand];
+  __shared__ int cost[kMvRefineMaxCand + 4];
+  __shared__ int ncand;
+  int blk, b;
+  xcd_ctb(blk, b);
+  const int lane = threadIdx.x;
+  const int bw = W >> 4, bh = H >> 4, bx = blk % bw, by = blk / bw, x0 = bx * 16, y0 = by * 16;
+  const long ysz = (long)W * H;
+  const uint8_t* S = srcy + b * ysz;
+  const uint8_t* Rf = refy + b * ysz;
+  const long nb = (long)bw * bh;
+  const uint32_t* C = cur + b * nb;
+  const int wx0 = x0 - kWinOff, wy0 = y0 - kWinOff;
+  if (wx0 >= 0 && wy0 >= 0 && wx0 + kWinP <= W && wy0 + kWinN <= H) {
+    for (int i = lane; i < kWinN * (kWinP / 4); i += 64) {
+      const int wy = i / (kWinP / 4), wq = i - wy * (kWinP / 4);
+      reinterpret_cast<uint32_t*>(win + wy * kWinP)[wq] =
+          *reinterpret_cast<const uint32_t*>(Rf + (long)(wy0 + wy) * W + wx0 + 4 * wq);
+    }
+  } else {
+    for (int i = lane; i < kWinN * kWinN; i += 64) {
+      const int wy = i / kWinN, wx = i - wy * kWinN;
+      const int yy = clip3(0, H - 1, wy0 + wy), xx = clip3(0, W - 1, wx0 + wx);
+      win[wy * kWinP + wx] = Rf[(long)yy * W + xx];
+    }
+  }
+  for (int i = lane; i < 256; i += 64) sblk[i] = S[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)];
+  if (lane == 0) ncand = mv_refine_cands(C, bw, bh, bx, by, cand);
+  __syncthreads();
+  auto wget = [&](int x, int y) -> int { return win[(kWinOff + y) * kWinP + kWinOff + x]; };
+  const int grp = lane >> 4, b4 = lane & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
+  const int n = ncand;
+  for (int base = 0; base < n; base += 4) {
+    const int ci = base + grp;
+    int sat = 0;
+    if (ci < n) {
+      const uint32_t m = cand[ci];
+      const int r = mv_row(m), c = mv_col(m);
+      const int ix = mv_int(c, false), iy = mv_int(r, false), fx = mv_frac(c, false), fy = mv_frac(r, false);
+      int d[16];
+      if (!fx && !fy) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d[i * 4 + j] = (int)sblk[(py + i) * 16 + px + j] - wget(px + j + ix, py + i + iy);
+      } else {
+        int col[11][4];
+#pragma unroll
+        for (int rr = 0; rr < 11; ++rr)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            int sum = 0;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) sum += subpel_tap(fx, t) * wget(px + j + ix + t - 3, py + rr + iy - 3);
+            col[rr][j] = (sum + (1 << (kInterRound0 - 1))) >> kInterRound0;
+          }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            int sum = 0;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) sum += subpel_tap(fy, t) * col[i + t][j];
+            d[i * 4 + j] = (int)sblk[(py + i) * 16 + px + j] - clip_pixel((sum + (1 << (kInterRound1 - 1))) >> kInterRound1);
+          }
+      }
+      sat = satd4(d);
+    }
+    sat = row16_sum(sat);
+    if (b4 == 0 && ci < n) cost[ci] = sat;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    int bc = cost[0], bi = 0;
+    for (int k = 1; k < n; ++k)
+      if (cost[k] < bc) bc = cost[k], bi = k;
+    nxt[b * nb + blk] = cand[bi];
   }
 }
 
@@ -813,14 +925,22 @@ extern "C" {
 const char* tv_av1e_last_error() { return g_err.c_str(); }
 
 // P frame of B segments: src / ref / rec planes [B][H][W] (+ chroma [B][H/2][W/2]); qarr:
-// device q-index per segment (1..255, range-checked by the host engine).
+// device q-index per segment (1..255, range-checked by the host engine).  The motion field
+// goes through `tmp` ([B][nb] words): search -> tmp, kMvRefineRounds refinement rounds
+// ping-ponging between tmp and mv (ending in mv), then the recon at mv.
 int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* ry, const uint8_t* ru,
-                  const uint8_t* rv, uint8_t* oy, uint8_t* ou, uint8_t* ov, uint32_t* mode, uint32_t* mv, int16_t* ly,
-                  int16_t* lu, int16_t* lv, int W, int H, int B, const int* qarr, void* stream) {
+                  const uint8_t* rv, uint8_t* oy, uint8_t* ou, uint8_t* ov, uint32_t* mode, uint32_t* mv, uint32_t* tmp,
+                  int16_t* ly, int16_t* lu, int16_t* lv, int W, int H, int B, const int* qarr, void* stream) {
   if (bad(W, H, B, 1, "av1e_inter") || ensure_tables()) return -1;
+  static_assert(kMvRefineRounds % 2 == 1, "an odd round count ends the field in `mv`");
   const int nb = (W >> 4) * (H >> 4);
-  k_av1e_inter<<<dim3(nb, B), 64, 0, (hipStream_t)stream>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv},
-                                                            Planes3W{oy, ou, ov}, mode, mv, ly, lu, lv, W, H, qarr);
+  hipStream_t st = (hipStream_t)stream;
+  k_av1e_inter<0><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
+                                               nullptr, tmp, ly, lu, lv, W, H, qarr);
+  for (int r = 0; r < kMvRefineRounds; ++r)
+    k_av1e_mv_refine<<<dim3(nb, B), 64, 0, st>>>(sy, ry, (r & 1) ? mv : tmp, (r & 1) ? tmp : mv, W, H);
+  k_av1e_inter<1><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
+                                               mv, mv, ly, lu, lv, W, H, qarr);
   return status("av1e_inter");
 }
 
