@@ -1997,6 +1997,44 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
         });
         mvs.swap(nxt);
       }
+      // MV unification (tv/av1_enc.h): every complete 32x32 quad, then every complete 64x64
+      // superblock, takes one of its members' MVs when that costs at most a few bits' worth
+      // of luma SATD (skip blocks then merge into 32x32 / 64x64 blocks)
+      auto blk_satd = [&](int bx, int by, uint32_t m) {
+        int s0[256], pr[256];
+        for (int i = 0; i < 16; ++i)
+          for (int j = 0; j < 16; ++j) s0[i * 16 + j] = S.y[(size_t)(by * 16 + i) * g.W + bx * 16 + j];
+        predict(g, 0, bx, by, pack_mode(1, 0, 0, 0, 0), m, rec, ref, pr);
+        return satd_block(s0, pr, 16);
+      };
+      parallel_rows(g.bh / 2, [&](int qy) {
+        for (int qx = 0; qx < g.bw / 2; ++qx) {
+          int sat[4][4];
+          uint32_t m[4];
+          for (int k = 0; k < 4; ++k) m[k] = mvs[(2 * qy + (k >> 1)) * g.bw + 2 * qx + (k & 1)];
+          for (int k = 0; k < 4; ++k)
+            for (int c = 0; c < 4; ++c) sat[k][c] = blk_satd(2 * qx + (k & 1), 2 * qy + (k >> 1), m[c]);
+          const int c = quad_unify(sat, lam);
+          if (c >= 0)
+            for (int k = 0; k < 4; ++k) mvs[(2 * qy + (k >> 1)) * g.bw + 2 * qx + (k & 1)] = m[c];
+        }
+      });
+      parallel_rows(g.sbh, [&](int sy) {
+        for (int sx = 0; sx < g.sbw; ++sx) {
+          if (sx * 4 + 3 >= g.bw || sy * 4 + 3 >= g.bh) continue;
+          uint32_t cand[4];
+          int own = 0, tot[4] = {0, 0, 0, 0};
+          for (int q = 0; q < 4; ++q) cand[q] = mvs[(sy * 4 + (q >> 1) * 2) * g.bw + sx * 4 + (q & 1) * 2];
+          for (int k = 0; k < 16; ++k) {
+            const int bx = sx * 4 + (k & 3), by = sy * 4 + (k >> 2);
+            own += blk_satd(bx, by, mvs[by * g.bw + bx]);
+            for (int c = 0; c < 4; ++c) tot[c] += blk_satd(bx, by, cand[c]);
+          }
+          const int c = sb_unify(own, tot, lam);
+          if (c >= 0)
+            for (int k = 0; k < 16; ++k) mvs[(sy * 4 + (k >> 2)) * g.bw + sx * 4 + (k & 3)] = cand[c];
+        }
+      });
       parallel_rows(g.bh, [&](int by) {
         for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx, &mvs[by * g.bw + bx], nullptr);
       });

@@ -513,6 +513,128 @@ __global__ void __launch_bounds__(64) k_av1e_mv_refine(const uint8_t* __restrict
   }
 }
 
+// MV unification (tv/av1_enc.h quad_unify / sb_unify): one 256-thread workgroup per 64x64
+// superblock.  The superblock's reference window (104 x 104, clamped) and source are staged
+// in LDS; (block, candidate MV) pairs are scored 16 per pass, 16 lanes per pair (one 4x4
+// SATD each).  The quads of the superblock first, then the superblock itself; only the
+// superblock's own 16 MV words are read and written.
+constexpr int kSbWin = 104, kSbWinOff = 20;
+__global__ void __launch_bounds__(256) k_av1e_mv_unify(const uint8_t* __restrict__ srcy, const uint8_t* __restrict__ refy,
+                                                       uint32_t* __restrict__ mv, int W, int H, const int* __restrict__ qarr) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kSbWin * kSbWin];
+  __shared__ __attribute__((aligned(16))) uint8_t sb[64 * 64];
+  __shared__ uint32_t mvl[16];
+  __shared__ int sat[80];
+  const int sbi = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int bw = W >> 4, bh = H >> 4, sbw = (W + 63) >> 6, sx = sbi % sbw, sy = sbi / sbw;
+  const int X0 = sx * 64, Y0 = sy * 64;
+  const long ysz = (long)W * H, nb = (long)bw * bh;
+  const uint8_t* S = srcy + b * ysz;
+  const uint8_t* Rf = refy + b * ysz;
+  uint32_t* M = mv + b * nb;
+  const int lam = lambda16(qarr[b]);
+  for (int i = t; i < kSbWin * kSbWin; i += 256) {
+    const int wy = i / kSbWin, wx = i - wy * kSbWin;
+    win[i] = Rf[(long)clip3(0, H - 1, Y0 - kSbWinOff + wy) * W + clip3(0, W - 1, X0 - kSbWinOff + wx)];
+  }
+  for (int i = t; i < 64 * 64; i += 256) {
+    const int yy = Y0 + (i >> 6), xx = X0 + (i & 63);
+    sb[i] = (yy < H && xx < W) ? S[(long)yy * W + xx] : 0;
+  }
+  if (t < 16) {
+    const int bx = sx * 4 + (t & 3), by = sy * 4 + (t >> 2);
+    mvl[t] = (bx < bw && by < bh) ? M[by * bw + bx] : 0u;
+  }
+  __syncthreads();
+  const int grp = t >> 4, b4 = t & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
+  // SATD of SB-local block k (raster 4 x 4) at MV m: each lane one 4x4, summed over 16 lanes
+  auto pair_satd = [&](int k, uint32_t m) -> int {
+    const int ox = (k & 3) * 16 + px, oy = (k >> 2) * 16 + py;  // SB-relative 4x4 origin
+    const int r = mv_row(m), c = mv_col(m);
+    const int ix = mv_int(c, false), iy = mv_int(r, false), fx = mv_frac(c, false), fy = mv_frac(r, false);
+    auto wget = [&](int x, int y) -> int { return win[(kSbWinOff + y) * kSbWin + kSbWinOff + x]; };
+    int d[16];
+    if (!fx && !fy) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i * 4 + j] = (int)sb[(oy + i) * 64 + ox + j] - wget(ox + j + ix, oy + i + iy);
+    } else {
+      int col[11][4];
+#pragma unroll
+      for (int rr = 0; rr < 11; ++rr)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int sum = 0;
+#pragma unroll
+          for (int tp = 0; tp < 8; ++tp) sum += subpel_tap(fx, tp) * wget(ox + j + ix + tp - 3, oy + rr + iy - 3);
+          col[rr][j] = (sum + (1 << (kInterRound0 - 1))) >> kInterRound0;
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int sum = 0;
+#pragma unroll
+          for (int tp = 0; tp < 8; ++tp) sum += subpel_tap(fy, tp) * col[i + tp][j];
+          d[i * 4 + j] = (int)sb[(oy + i) * 64 + ox + j] - clip_pixel((sum + (1 << (kInterRound1 - 1))) >> kInterRound1);
+        }
+    }
+    return row16_sum(satd4(d));
+  };
+  // ---- quads: pair p = q * 16 + k * 4 + c (block k of quad q at member c's MV)
+  auto quad_ok = [&](int q) {
+    const int qx = sx * 2 + (q & 1), qy = sy * 2 + (q >> 1);
+    return 2 * qx + 1 < bw && 2 * qy + 1 < bh;
+  };
+  auto qblk = [&](int q, int k) { return ((q >> 1) * 2 + (k >> 1)) * 4 + (q & 1) * 2 + (k & 1); };
+  for (int p0 = 0; p0 < 64; p0 += 16) {
+    const int p = p0 + grp, q = p >> 4, k = (p >> 2) & 3, c = p & 3;
+    int v = 0;
+    if (quad_ok(q)) v = pair_satd(qblk(q, k), mvl[qblk(q, c)]);
+    if (b4 == 0) sat[p] = v;  // (80-entry scratch: quads use 64)
+  }
+  __syncthreads();
+  if (t < 4 && quad_ok(t)) {
+    int q4[4][4];
+    for (int k = 0; k < 4; ++k)
+      for (int c = 0; c < 4; ++c) q4[k][c] = sat[t * 16 + k * 4 + c];
+    const int c = quad_unify(q4, lam);
+    if (c >= 0) {
+      const uint32_t m = mvl[qblk(t, c)];
+      for (int k = 0; k < 4; ++k) mvl[qblk(t, k)] = m;  // each thread writes its own quad
+    }
+  }
+  __syncthreads();
+  // ---- the superblock: pair p < 16: block p at its MV; p >= 16: block (p-16)>>2 at quad (p-16)&3's
+  if (sx * 4 + 3 < bw && sy * 4 + 3 < bh) {
+    for (int p0 = 0; p0 < 80; p0 += 16) {
+      const int p = p0 + grp;
+      const uint32_t m = p < 16 ? mvl[p] : mvl[qblk((p - 16) & 3, 0)];
+      const int v = pair_satd(p < 16 ? p : (p - 16) >> 2, m);
+      if (b4 == 0) sat[p] = v;
+    }
+    __syncthreads();
+    if (t == 0) {
+      int own = 0, tot[4] = {0, 0, 0, 0};
+      for (int k = 0; k < 16; ++k) {
+        own += sat[k];
+        for (int c = 0; c < 4; ++c) tot[c] += sat[16 + k * 4 + c];
+      }
+      const int c = sb_unify(own, tot, lam);
+      if (c >= 0) {
+        const uint32_t m = mvl[qblk(c, 0)];
+        for (int k = 0; k < 16; ++k) mvl[k] = m;
+      }
+    }
+    __syncthreads();
+  }
+  if (t < 16) {
+    const int bx = sx * 4 + (t & 3), by = sy * 4 + (t >> 2);
+    if (bx < bw && by < bh) M[by * bw + bx] = mvl[t];
+  }
+}
+
 // ================================================================= intra ================
 struct EdgeLds {
   IntraEdge e;
@@ -939,6 +1061,7 @@ int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const
                                                nullptr, tmp, ly, lu, lv, W, H, qarr);
   for (int r = 0; r < kMvRefineRounds; ++r)
     k_av1e_mv_refine<<<dim3(nb, B), 64, 0, st>>>(sy, ry, (r & 1) ? mv : tmp, (r & 1) ? tmp : mv, W, H);
+  k_av1e_mv_unify<<<dim3(((W + 63) >> 6) * ((H + 63) >> 6), B), 256, 0, st>>>(sy, ry, mv, W, H, qarr);
   k_av1e_inter<1><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
                                                mv, mv, ly, lu, lv, W, H, qarr);
   return status("av1e_inter");
