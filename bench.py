@@ -538,7 +538,8 @@ def av1_main(args) -> None:
             "dtype": "uint8 video / int32 integer transforms (bit-exact AV1 subset)",
             "data": CPU_DATA if args.cpu else f"synthetic ({args.content} seeded procedural YUV 4:2:0 source generated on GPU)",
             "config": {
-                "model": f"AV1 subset (tv) qindex {q} 16x16 blocks +deblock +CDEF +LR {args.res} synthetic"
+                "model": f"AV1 subset (tv) qindex {q} 16x16 blocks, refined + unified MV field, 32/64 merged skip blocks, "
+                         f"+deblock +CDEF +LR {args.res} synthetic"
                 + (f" 2-pass {args.kbps:g} kbps" if args.kbps > 0 else ""),
                 "rate_control": (f"2-pass: pass-1 per-frame bits all-reduced, per-frame q-index plan, target "
                                  f"{args.kbps:g} kbps per 30 fps stream, fast first pass (no LR search), batch "

@@ -423,102 +423,116 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   }
 }
 
-// One Jacobi round of the motion-field refinement (tv/av1_enc.h mv_refine_cands): one wave
-// per 16x16 block re-chooses among its neighbours' current MVs by luma SATD (first
-// minimum, own MV first).  Candidates x 16 lanes: each lane predicts one 4x4 of the block
-// from the staged reference window (the 8-tap separable filter of inter_pred_px) and
-// takes its SATD; 4 candidates per pass.
-__global__ void __launch_bounds__(64) k_av1e_mv_refine(const uint8_t* __restrict__ srcy, const uint8_t* __restrict__ refy,
-                                                       const uint32_t* __restrict__ cur, uint32_t* __restrict__ nxt,
-                                                       int W, int H) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kWinN * kWinP + 8];
-  __shared__ __attribute__((aligned(16))) uint8_t sblk[256];
-  __shared__ uint32_t cand[kMvRefineMaxCand];
-  __shared__ int cost[kMvRefineMaxCand + 4];
-  __shared__ int ncand;
-  int blk, b;
-  xcd_ctb(blk, b);
-  const int lane = threadIdx.x;
-  const int bw = W >> 4, bh = H >> 4, bx = blk % bw, by = blk / bw, x0 = bx * 16, y0 = by * 16;
-  const long ysz = (long)W * H;
-  const uint8_t* S = srcy + b * ysz;
-  const uint8_t* Rf = refy + b * ysz;
-  const long nb = (long)bw * bh;
-  const uint32_t* C = cur + b * nb;
-  const int wx0 = x0 - kWinOff, wy0 = y0 - kWinOff;
-  if (wx0 >= 0 && wy0 >= 0 && wx0 + kWinP <= W && wy0 + kWinN <= H) {
-    for (int i = lane; i < kWinN * (kWinP / 4); i += 64) {
-      const int wy = i / (kWinP / 4), wq = i - wy * (kWinP / 4);
-      reinterpret_cast<uint32_t*>(win + wy * kWinP)[wq] =
-          *reinterpret_cast<const uint32_t*>(Rf + (long)(wy0 + wy) * W + wx0 + 4 * wq);
-    }
-  } else {
-    for (int i = lane; i < kWinN * kWinN; i += 64) {
-      const int wy = i / kWinN, wx = i - wy * kWinN;
-      const int yy = clip3(0, H - 1, wy0 + wy), xx = clip3(0, W - 1, wx0 + wx);
-      win[wy * kWinP + wx] = Rf[(long)yy * W + xx];
-    }
-  }
-  for (int i = lane; i < 256; i += 64) sblk[i] = S[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)];
-  if (lane == 0) ncand = mv_refine_cands(C, bw, bh, bx, by, cand);
-  __syncthreads();
-  auto wget = [&](int x, int y) -> int { return win[(kWinOff + y) * kWinP + kWinOff + x]; };
-  const int grp = lane >> 4, b4 = lane & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
-  const int n = ncand;
-  for (int base = 0; base < n; base += 4) {
-    const int ci = base + grp;
-    int sat = 0;
-    if (ci < n) {
-      const uint32_t m = cand[ci];
-      const int r = mv_row(m), c = mv_col(m);
-      const int ix = mv_int(c, false), iy = mv_int(r, false), fx = mv_frac(c, false), fy = mv_frac(r, false);
-      int d[16];
-      if (!fx && !fy) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) d[i * 4 + j] = (int)sblk[(py + i) * 16 + px + j] - wget(px + j + ix, py + i + iy);
-      } else {
-        int col[11][4];
-#pragma unroll
-        for (int rr = 0; rr < 11; ++rr)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            int sum = 0;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) sum += subpel_tap(fx, t) * wget(px + j + ix + t - 3, py + rr + iy - 3);
-            col[rr][j] = (sum + (1 << (kInterRound0 - 1))) >> kInterRound0;
-          }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            int sum = 0;
-#pragma unroll
-            for (int t = 0; t < 8; ++t) sum += subpel_tap(fy, t) * col[i + t][j];
-            d[i * 4 + j] = (int)sblk[(py + i) * 16 + px + j] - clip_pixel((sum + (1 << (kInterRound1 - 1))) >> kInterRound1);
-          }
-      }
-      sat = satd4(d);
-    }
-    sat = row16_sum(sat);
-    if (b4 == 0 && ci < n) cost[ci] = sat;
-  }
-  __syncthreads();
-  if (lane == 0) {
-    int bc = cost[0], bi = 0;
-    for (int k = 1; k < n; ++k)
-      if (cost[k] < bc) bc = cost[k], bi = k;
-    nxt[b * nb + blk] = cand[bi];
-  }
-}
-
 // MV unification (tv/av1_enc.h quad_unify / sb_unify): one 256-thread workgroup per 64x64
 // superblock.  The superblock's reference window (104 x 104, clamped) and source are staged
 // in LDS; (block, candidate MV) pairs are scored 16 per pass, 16 lanes per pair (one 4x4
 // SATD each).  The quads of the superblock first, then the superblock itself; only the
 // superblock's own 16 MV words are read and written.
 constexpr int kSbWin = 104, kSbWinOff = 20;
+
+// Stage a superblock's clamped reference window and its source (zero outside the frame).
+__device__ void stage_sb(const uint8_t* S, const uint8_t* Rf, int W, int H, int X0, int Y0, uint8_t* win, uint8_t* sb) {
+  const int t = threadIdx.x;
+  for (int i = t; i < kSbWin * kSbWin; i += 256) {
+    const int wy = i / kSbWin, wx = i - wy * kSbWin;
+    win[i] = Rf[(long)clip3(0, H - 1, Y0 - kSbWinOff + wy) * W + clip3(0, W - 1, X0 - kSbWinOff + wx)];
+  }
+  for (int i = t; i < 64 * 64; i += 256) {
+    const int yy = Y0 + (i >> 6), xx = X0 + (i & 63);
+    sb[i] = (yy < H && xx < W) ? S[(long)yy * W + xx] : 0;
+  }
+}
+
+// Luma SATD of superblock-local block k (4 x 4 raster of 16x16) at MV m, from the staged
+// window / source: the calling lane's 4x4 (b4 = lane & 15) predicted with the 8-tap
+// separable filter of inter_pred_px, summed over its 16-lane row.
+__device__ __forceinline__ int sb_pair_satd(const uint8_t* win, const uint8_t* sb, int k, uint32_t m, int b4) {
+  const int px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
+  const int ox = (k & 3) * 16 + px, oy = (k >> 2) * 16 + py;
+  const int r = mv_row(m), c = mv_col(m);
+  const int ix = mv_int(c, false), iy = mv_int(r, false), fx = mv_frac(c, false), fy = mv_frac(r, false);
+  auto wget = [&](int x, int y) -> int { return win[(kSbWinOff + y) * kSbWin + kSbWinOff + x]; };
+  int d[16];
+  if (!fx && !fy) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[i * 4 + j] = (int)sb[(oy + i) * 64 + ox + j] - wget(ox + j + ix, oy + i + iy);
+  } else {
+    int col[11][4];
+#pragma unroll
+    for (int rr = 0; rr < 11; ++rr)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int sum = 0;
+#pragma unroll
+        for (int tp = 0; tp < 8; ++tp) sum += subpel_tap(fx, tp) * wget(ox + j + ix + tp - 3, oy + rr + iy - 3);
+        col[rr][j] = (sum + (1 << (kInterRound0 - 1))) >> kInterRound0;
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int sum = 0;
+#pragma unroll
+        for (int tp = 0; tp < 8; ++tp) sum += subpel_tap(fy, tp) * col[i + tp][j];
+        d[i * 4 + j] = (int)sb[(oy + i) * 64 + ox + j] - clip_pixel((sum + (1 << (kInterRound1 - 1))) >> kInterRound1);
+      }
+  }
+  return row16_sum(satd4(d));
+}
+
+// One Jacobi round of the motion-field refinement (tv/av1_enc.h mv_refine_cands), one
+// 256-thread workgroup per superblock: each of its 16x16 blocks re-chooses among its
+// neighbours' current MVs (read from `cur`, across superblock edges too) by luma SATD
+// (first minimum, own MV first) and writes `nxt`.  (block, candidate) pairs 16 per pass
+// on the staged superblock window.
+__global__ void __launch_bounds__(256) k_av1e_mv_refine(const uint8_t* __restrict__ srcy, const uint8_t* __restrict__ refy,
+                                                        const uint32_t* __restrict__ cur, uint32_t* __restrict__ nxt,
+                                                        int W, int H) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[kSbWin * kSbWin];
+  __shared__ __attribute__((aligned(16))) uint8_t sb[64 * 64];
+  __shared__ uint32_t cand[16][kMvRefineMaxCand];
+  __shared__ int ncand[16];
+  __shared__ int sat[16][kMvRefineMaxCand];
+  __shared__ int pk[16 * kMvRefineMaxCand];  // pair -> (block << 8) | candidate
+  __shared__ int npairs;
+  const int sbi = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int bw = W >> 4, bh = H >> 4, sbw = (W + 63) >> 6, sx = sbi % sbw, sy = sbi / sbw;
+  const long ysz = (long)W * H, nb = (long)bw * bh;
+  stage_sb(srcy + b * ysz, refy + b * ysz, W, H, sx * 64, sy * 64, win, sb);
+  const uint32_t* C = cur + b * nb;
+  if (t < 16) {
+    const int bx = sx * 4 + (t & 3), by = sy * 4 + (t >> 2);
+    ncand[t] = (bx < bw && by < bh) ? mv_refine_cands(C, bw, bh, bx, by, cand[t]) : 0;
+  }
+  __syncthreads();
+  if (t == 0) {
+    int n = 0;
+    for (int k = 0; k < 16; ++k)
+      for (int c = 0; c < ncand[k]; ++c) pk[n++] = (k << 8) | c;
+    npairs = n;
+  }
+  __syncthreads();
+  const int grp = t >> 4, b4 = t & 15, n = npairs;
+  for (int p0 = 0; p0 < n; p0 += 16) {
+    const int p = p0 + grp;
+    if (p < n) {  // uniform over each 16-lane row (the row16_sum DPP stays inside it)
+      const int k = pk[p] >> 8, c = pk[p] & 255;
+      const int v = sb_pair_satd(win, sb, k, cand[k][c], b4);
+      if (b4 == 0) sat[k][c] = v;
+    }
+  }
+  __syncthreads();
+  if (t < 16 && ncand[t]) {
+    int bc = sat[t][0], bi = 0;
+    for (int c = 1; c < ncand[t]; ++c)
+      if (sat[t][c] < bc) bc = sat[t][c], bi = c;
+    const int bx = sx * 4 + (t & 3), by = sy * 4 + (t >> 2);
+    nxt[b * nb + by * bw + bx] = cand[t][bi];
+  }
+}
+
 __global__ void __launch_bounds__(256) k_av1e_mv_unify(const uint8_t* __restrict__ srcy, const uint8_t* __restrict__ refy,
                                                        uint32_t* __restrict__ mv, int W, int H, const int* __restrict__ qarr) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kSbWin * kSbWin];
@@ -533,55 +547,14 @@ __global__ void __launch_bounds__(256) k_av1e_mv_unify(const uint8_t* __restrict
   const uint8_t* Rf = refy + b * ysz;
   uint32_t* M = mv + b * nb;
   const int lam = lambda16(qarr[b]);
-  for (int i = t; i < kSbWin * kSbWin; i += 256) {
-    const int wy = i / kSbWin, wx = i - wy * kSbWin;
-    win[i] = Rf[(long)clip3(0, H - 1, Y0 - kSbWinOff + wy) * W + clip3(0, W - 1, X0 - kSbWinOff + wx)];
-  }
-  for (int i = t; i < 64 * 64; i += 256) {
-    const int yy = Y0 + (i >> 6), xx = X0 + (i & 63);
-    sb[i] = (yy < H && xx < W) ? S[(long)yy * W + xx] : 0;
-  }
+  stage_sb(S, Rf, W, H, X0, Y0, win, sb);
   if (t < 16) {
     const int bx = sx * 4 + (t & 3), by = sy * 4 + (t >> 2);
     mvl[t] = (bx < bw && by < bh) ? M[by * bw + bx] : 0u;
   }
   __syncthreads();
-  const int grp = t >> 4, b4 = t & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
-  // SATD of SB-local block k (raster 4 x 4) at MV m: each lane one 4x4, summed over 16 lanes
-  auto pair_satd = [&](int k, uint32_t m) -> int {
-    const int ox = (k & 3) * 16 + px, oy = (k >> 2) * 16 + py;  // SB-relative 4x4 origin
-    const int r = mv_row(m), c = mv_col(m);
-    const int ix = mv_int(c, false), iy = mv_int(r, false), fx = mv_frac(c, false), fy = mv_frac(r, false);
-    auto wget = [&](int x, int y) -> int { return win[(kSbWinOff + y) * kSbWin + kSbWinOff + x]; };
-    int d[16];
-    if (!fx && !fy) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d[i * 4 + j] = (int)sb[(oy + i) * 64 + ox + j] - wget(ox + j + ix, oy + i + iy);
-    } else {
-      int col[11][4];
-#pragma unroll
-      for (int rr = 0; rr < 11; ++rr)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int sum = 0;
-#pragma unroll
-          for (int tp = 0; tp < 8; ++tp) sum += subpel_tap(fx, tp) * wget(ox + j + ix + tp - 3, oy + rr + iy - 3);
-          col[rr][j] = (sum + (1 << (kInterRound0 - 1))) >> kInterRound0;
-        }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int sum = 0;
-#pragma unroll
-          for (int tp = 0; tp < 8; ++tp) sum += subpel_tap(fy, tp) * col[i + tp][j];
-          d[i * 4 + j] = (int)sb[(oy + i) * 64 + ox + j] - clip_pixel((sum + (1 << (kInterRound1 - 1))) >> kInterRound1);
-        }
-    }
-    return row16_sum(satd4(d));
-  };
+  const int grp = t >> 4, b4 = t & 15;
+  auto pair_satd = [&](int k, uint32_t m) -> int { return sb_pair_satd(win, sb, k, m, b4); };
   // ---- quads: pair p = q * 16 + k * 4 + c (block k of quad q at member c's MV)
   auto quad_ok = [&](int q) {
     const int qx = sx * 2 + (q & 1), qy = sy * 2 + (q >> 1);
@@ -1055,13 +1028,13 @@ int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const
                   int16_t* ly, int16_t* lu, int16_t* lv, int W, int H, int B, const int* qarr, void* stream) {
   if (bad(W, H, B, 1, "av1e_inter") || ensure_tables()) return -1;
   static_assert(kMvRefineRounds % 2 == 1, "an odd round count ends the field in `mv`");
-  const int nb = (W >> 4) * (H >> 4);
+  const int nb = (W >> 4) * (H >> 4), nsb = ((W + 63) >> 6) * ((H + 63) >> 6);
   hipStream_t st = (hipStream_t)stream;
   k_av1e_inter<0><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
                                                nullptr, tmp, ly, lu, lv, W, H, qarr);
   for (int r = 0; r < kMvRefineRounds; ++r)
-    k_av1e_mv_refine<<<dim3(nb, B), 64, 0, st>>>(sy, ry, (r & 1) ? mv : tmp, (r & 1) ? tmp : mv, W, H);
-  k_av1e_mv_unify<<<dim3(((W + 63) >> 6) * ((H + 63) >> 6), B), 256, 0, st>>>(sy, ry, mv, W, H, qarr);
+    k_av1e_mv_refine<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, (r & 1) ? mv : tmp, (r & 1) ? tmp : mv, W, H);
+  k_av1e_mv_unify<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, mv, W, H, qarr);
   k_av1e_inter<1><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
                                                mv, mv, ly, lu, lv, W, H, qarr);
   return status("av1e_inter");
