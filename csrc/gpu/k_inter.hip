@@ -46,9 +46,19 @@ constexpr int kMeThreads = 256;
 constexpr int kFRows = kCtb + kMeWinH - 1;  // 38 window rows per candidate
 constexpr int kFWords = 12;                 // 48 bytes staged (40 used: 32 + 7 offsets + 1)
 constexpr int kFChunks = kFWords / 4;       // 16-byte chunks per staged row
-constexpr int kFPitch = kFWords + 1;        // odd pitch: lanes walking rows hit distinct banks
-// LDS pitch (words) of a source-CTB row (uniform s0/s1 reads stay one aligned 8-byte read)
-constexpr int kSrcP = 8;
+// Window layout: pitch 12 words, rows >= 16 kWinSkew words further (per candidate).  A
+// half-wave of the integer search reads 8 (row, 4-position group) items x 4 quadrants,
+// rows r and r + 16 together; brute force over pitch / skew (ds_read_b32 banks (a/4) % 32)
+// gives 1344 extra LDS cycles over all item phases for 12 / +2 against 2016 for the former
+// odd pitch 13, in less LDS.
+constexpr int kFPitch = kFWords, kWinSkew = 2, kWinCand = kFRows * kFPitch + kWinSkew;
+__device__ __forceinline__ int win_word(int k, int r, int w) { return k * kWinCand + r * kFPitch + (r >= 16 ? kWinSkew : 0) + w; }
+// LDS pitch (words) of a source-CTB row (uniform s0/s1 reads stay one aligned 8-byte read).
+// The bottom 16 rows sit kSrcSkew words further: the four quadrant lanes of an integer-
+// search item read rows r and r + 16 at the same time, which with a flat 8-word pitch are
+// 128 words apart -- the same LDS bank (a 2-way conflict on every source read).
+constexpr int kSrcP = 8, kSrcSkew = 2;
+__device__ __forceinline__ int src_word(int row, int w) { return row * kSrcP + w + ((row >> 4) & 1) * kSrcSkew; }
 
 __device__ __forceinline__ void me_blk_geom(int bi, int& bx, int& by, int& l2) {
   if (bi < 16) {
@@ -170,8 +180,8 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   const int cxi = ctu % g.wc, cyi = ctu / g.wc, cx = cxi * 32, cy = cyi * 32;
   const uint8_t* S = src.plane(0, b, g);
   const uint8_t* R = ref.plane(0, b, g);
-  __shared__ uint32_t s32[32 * kSrcP];
-  __shared__ uint32_t win[kMeMaxCand * kFRows * kFPitch];
+  __shared__ uint32_t s32[32 * kSrcP + kSrcSkew];
+  __shared__ uint32_t win[kMeMaxCand * kWinCand];
   __shared__ int cand[kMeMaxCand][2];
   __shared__ int pmv[2], ncand;
   __shared__ unsigned best[21];
@@ -179,7 +189,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   __shared__ int subsad[21][8];
   __shared__ int sad16[kMeMaxCand * kMePosPerCand][4];  // per position: the 4 quadrant 16x16 SADs
   for (int t = tid; t < 256; t += kMeThreads)
-    s32[(t >> 3) * kSrcP + (t & 7)] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (t >> 3)) * g.W + cx + 4 * (t & 7));
+    s32[src_word(t >> 3, t & 7)] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (t >> 3)) * g.W + cx + 4 * (t & 7));
   if (tid == 0) {
     const long u0 = b * g.usz + (long)(cy >> 3) * g.w8 + (cx >> 3);
     ncand = me_candidates(cmv + (long)b * g.wc * g.hc * 2, g.wc, g.hc, cxi, cyi, prev_mv[2 * u0], prev_mv[2 * u0 + 1],
@@ -196,7 +206,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
     const int r = rem / kFChunks, ch = rem - r * kFChunks;
     const uint8_t* row = R + (long)clip3(0, g.H - 1, cy + cand[k][1] + kMeWinY0 + r) * g.W;
     const int x = cx + cand[k][0] + kMeWinX0 + 16 * ch, a = x & ~3, sh = x & 3;
-    uint32_t* dst = win + (k * kFRows + r) * kFPitch + 4 * ch;
+    uint32_t* dst = win + win_word(k, r, 4 * ch);
     if (x >= 0 && a + 20 <= g.W) {
       const uint4 u = *reinterpret_cast<const uint4*>(row + a);
       const uint32_t u4 = *reinterpret_cast<const uint32_t*>(row + a + 16);
@@ -237,7 +247,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       mvc[sft] = (unsigned)pen.mv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])];
     }
     const int qx = (qd & 1) * 16, qy = (qd >> 1) * 16;
-    const uint32_t* W0 = win + (k * kFRows + dyi) * kFPitch + gs;
+
     unsigned q16[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int j8 = 0; j8 < 4; ++j8) {
@@ -245,9 +255,9 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       unsigned acc[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int srow = (by + j) * kSrcP + (bx >> 2);
+        const int srow = src_word(by + j, bx >> 2);
         const uint32_t s0 = s32[srow], s1 = s32[srow + 1];
-        const uint32_t* wp = W0 + (by + j) * kFPitch + (bx >> 2);
+        const uint32_t* wp = win + win_word(k, dyi + by + j, gs + (bx >> 2));
         const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
         acc[0] = __builtin_amdgcn_sad_u8(w1, s1, __builtin_amdgcn_sad_u8(w0, s0, acc[0]));
 #pragma unroll
@@ -337,7 +347,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       const uint8_t* P = ph + (long)((mx & 3) + 4 * (my & 3)) * g.psz;
       const int gx0 = cx + bx + col0 + (mx >> 2);
       const int gy0 = cy + by + row0 + (my >> 2);
-      const int sw = (by + row0) * kSrcP + ((bx + col0) >> 2);  // source word index of row 0
+      const int sr0 = by + row0, sw0 = (bx + col0) >> 2;  // source row / word of row 0
       unsigned sad = 0;
       if (gx0 >= -8 && gx0 + 11 <= g.W + 7 && gy0 >= -8 && gy0 + 7 <= g.H + 7) {
         const int a = gx0 & ~3, sh = gx0 & 3;
@@ -348,14 +358,15 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
           const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
           const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
           const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-          sad = __builtin_amdgcn_sad_u8(hi, s32[sw + kSrcP * j + 1], __builtin_amdgcn_sad_u8(lo, s32[sw + kSrcP * j], sad));
+          const int sw = src_word(sr0 + j, sw0);
+          sad = __builtin_amdgcn_sad_u8(hi, s32[sw + 1], __builtin_amdgcn_sad_u8(lo, s32[sw], sad));
         }
       } else {  // touches the clamped border: per-pixel path
         for (int j = 0; j < 8; ++j) {
           const int gy = clip3(-8, g.H + 7, gy0 + j);
           for (int i = 0; i < 8; ++i) {
             const int gx = clip3(-8, g.W + 7, gx0 + i);
-            sad += tv_abs((int)sb[(by + row0 + j) * 4 * kSrcP + bx + col0 + i] - (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
+            sad += tv_abs((int)sb[4 * src_word(sr0 + j, 0) + bx + col0 + i] - (int)P[(long)(gy + 8) * g.pw16 + gx + 8]);
           }
         }
       }
