@@ -1867,6 +1867,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
     }
     // intra blocks, inter blocks at a given MV (force_mv), or the motion search alone
     // (search_out: the block's MV, nothing coded)
+    int frame_rnd = kRndInter;
     auto code_block = [&](int by, int bx, const uint32_t* force_mv, uint32_t* search_out) {
         const int b = by * g.bw + bx;
         int s[3][256], pred[3][256], rc[256];
@@ -1959,7 +1960,7 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
           if (dbg & 16) {
             for (int i = 0; i < N * N; ++i) s[p][i] = pred[p][i];
           }
-          if (code_tb(s[p], pred[p], lg, qidx, txt, inter ? kRndInter : kRndIntra, lev, rc)) nz |= 1 << p;
+          if (code_tb(s[p], pred[p], lg, qidx, txt, inter ? frame_rnd : kRndIntra, lev, rc)) nz |= 1 << p;
           std::vector<uint8_t>& P = p == 0 ? rec.y : (p == 1 ? rec.u : rec.v);
           for (int i = 0; i < N; ++i)
             for (int j = 0; j < N; ++j) P[(size_t)(by * N + i) * w + bx * N + j] = (uint8_t)rc[i * N + j];
@@ -2035,6 +2036,15 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
             for (int k = 0; k < 16; ++k) mvs[(sy * 4 + (k >> 2)) * g.bw + sx * 4 + (k & 3)] = cand[c];
         }
       });
+      {  // the frame's inter rounding from its luma SATD at the final MVs (tv/av1_enc.h)
+        std::vector<long long> row(g.bh, 0);
+        parallel_rows(g.bh, [&](int by) {
+          for (int bx = 0; bx < g.bw; ++bx) row[by] += blk_satd(bx, by, mvs[by * g.bw + bx]);
+        });
+        long long tot = 0;
+        for (long long r : row) tot += r;
+        frame_rnd = inter_rounding(tot, g.W, g.H);
+      }
       parallel_rows(g.bh, [&](int by) {
         for (int bx = 0; bx < g.bw; ++bx) code_block(by, bx, &mvs[by * g.bw + bx], nullptr);
       });

@@ -184,7 +184,8 @@ template <int STAGE>
 __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Planes3W rec, uint32_t* __restrict__ mode,
                                                    const uint32_t* __restrict__ mvin, uint32_t* __restrict__ mvout,
                                                    int16_t* __restrict__ ly, int16_t* __restrict__ lu,
-                                                   int16_t* __restrict__ lv, int W, int H, const int* __restrict__ qarr) {
+                                                   int16_t* __restrict__ lv, int W, int H, const int* __restrict__ qarr,
+                                                   const unsigned long long* __restrict__ satd_acc) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kWinN * kWinP + 8];
   __shared__ __attribute__((aligned(16))) uint8_t sblk[256];
   __shared__ __attribute__((aligned(16))) uint8_t cwin[2][kCWin * kCWin];
@@ -393,7 +394,8 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
     }
   }
   __syncthreads();
-  int nz = code_tb<4>(res, ta, tb, ti, 0, 0, qidx, kRndInter, ly + bo * 256);
+  const int rnd = inter_rounding((long long)satd_acc[b], W, H);
+  int nz = code_tb<4>(res, ta, tb, ti, 0, 0, qidx, rnd, ly + bo * 256);
   for (int i = lane; i < 256; i += 64)
     rec.y[b * ysz + (long)(y0 + (i >> 4)) * W + x0 + (i & 15)] = (uint8_t)clip_pixel(predc[i] + res[i]);
   __syncthreads();
@@ -412,7 +414,7 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
     }
     __syncthreads();
     int16_t* lo = (pl == 1 ? lu : lv) + bo * 64;
-    if (code_tb<3>(res, ta, tb, ti, 0, 0, qidx, kRndInter, lo)) nz |= 1 << pl;
+    if (code_tb<3>(res, ta, tb, ti, 0, 0, qidx, rnd, lo)) nz |= 1 << pl;
     uint8_t* Rw = (pl == 1 ? rec.u : rec.v) + b * csz;
     Rw[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)] = (uint8_t)clip_pixel(predc[lane] + res[lane]);
     __syncthreads();
@@ -534,7 +536,8 @@ __global__ void __launch_bounds__(256) k_av1e_mv_refine(const uint8_t* __restric
 }
 
 __global__ void __launch_bounds__(256) k_av1e_mv_unify(const uint8_t* __restrict__ srcy, const uint8_t* __restrict__ refy,
-                                                       uint32_t* __restrict__ mv, int W, int H, const int* __restrict__ qarr) {
+                                                       uint32_t* __restrict__ mv, int W, int H, const int* __restrict__ qarr,
+                                                       unsigned long long* __restrict__ satd_acc) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kSbWin * kSbWin];
   __shared__ __attribute__((aligned(16))) uint8_t sb[64 * 64];
   __shared__ uint32_t mvl[16];
@@ -605,6 +608,21 @@ __global__ void __launch_bounds__(256) k_av1e_mv_unify(const uint8_t* __restrict
   if (t < 16) {
     const int bx = sx * 4 + (t & 3), by = sy * 4 + (t >> 2);
     if (bx < bw && by < bh) M[by * bw + bx] = mvl[t];
+  }
+  // the frame's luma SATD at the final MVs (tv/av1_enc.h inter_rounding): this superblock's
+  // blocks, one pass of 16 pairs, summed into the segment's accumulator
+  {
+    const int bx = sx * 4 + (grp & 3), by = sy * 4 + (grp >> 2);
+    const bool in = bx < bw && by < bh;
+    const int v = in ? pair_satd(grp, mvl[grp]) : 0;
+    __shared__ int part[16];
+    if (b4 == 0) part[grp] = v;
+    __syncthreads();
+    if (t == 0) {
+      long long sum = 0;
+      for (int k = 0; k < 16; ++k) sum += part[k];
+      atomicAdd(satd_acc + b, (unsigned long long)sum);
+    }
   }
 }
 
@@ -1025,18 +1043,20 @@ const char* tv_av1e_last_error() { return g_err.c_str(); }
 // ping-ponging between tmp and mv (ending in mv), then the recon at mv.
 int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* ry, const uint8_t* ru,
                   const uint8_t* rv, uint8_t* oy, uint8_t* ou, uint8_t* ov, uint32_t* mode, uint32_t* mv, uint32_t* tmp,
-                  int16_t* ly, int16_t* lu, int16_t* lv, int W, int H, int B, const int* qarr, void* stream) {
+                  unsigned long long* satd_acc, int16_t* ly, int16_t* lu, int16_t* lv, int W, int H, int B,
+                  const int* qarr, void* stream) {
   if (bad(W, H, B, 1, "av1e_inter") || ensure_tables()) return -1;
   static_assert(kMvRefineRounds % 2 == 1, "an odd round count ends the field in `mv`");
   const int nb = (W >> 4) * (H >> 4), nsb = ((W + 63) >> 6) * ((H + 63) >> 6);
   hipStream_t st = (hipStream_t)stream;
   k_av1e_inter<0><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
-                                               nullptr, tmp, ly, lu, lv, W, H, qarr);
+                                               nullptr, tmp, ly, lu, lv, W, H, qarr, satd_acc);
   for (int r = 0; r < kMvRefineRounds; ++r)
     k_av1e_mv_refine<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, (r & 1) ? mv : tmp, (r & 1) ? tmp : mv, W, H);
-  k_av1e_mv_unify<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, mv, W, H, qarr);
+  if (hipMemsetAsync(satd_acc, 0, (size_t)B * sizeof(unsigned long long), st) != hipSuccess) return status("av1e_inter");
+  k_av1e_mv_unify<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, mv, W, H, qarr, satd_acc);
   k_av1e_inter<1><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
-                                               mv, mv, ly, lu, lv, W, H, qarr);
+                                               mv, mv, ly, lu, lv, W, H, qarr, satd_acc);
   return status("av1e_inter");
 }
 

@@ -52,11 +52,12 @@ struct VNoiseRow {
   }
 };
 
-__device__ __forceinline__ int synth_objects(const SynthFrameCtx& f, int c, int xl, int yl, int v) {
-  for (int k = 0; k < kSynthObjects; ++k) {  // later objects on top
+__device__ __forceinline__ int synth_objects(const SynthFrameCtx& f, int c, int xl, int yl, int v, unsigned rows) {
+  for (; rows; rows &= rows - 1) {  // later objects on top: ascending k over the row's objects
+    const int k = __builtin_ctz(rows);
     const SynthObject& o = f.obj[k];
     const int32_t rx16 = xl * 16 - f.ox[k], ry16 = yl * 16 - f.oy[k];
-    if (rx16 < 0 || ry16 < 0 || rx16 >= o.w * 16 || ry16 >= o.h * 16) continue;
+    if (rx16 < 0 || rx16 >= o.w * 16) continue;
     if (o.shape == 1) {
       const int64_t dx = 2 * (int64_t)rx16 - o.w * 16, dy = 2 * (int64_t)ry16 - o.h * 16;
       const int64_t ww = (int64_t)o.w * 16, hh = (int64_t)o.h * 16;
@@ -72,7 +73,10 @@ __device__ __forceinline__ int synth_objects(const SynthFrameCtx& f, int c, int 
 }
 
 // kTex: the textured variant (seed bit 31) is a separate instantiation so the smooth source
-// keeps its register budget (a runtime branch doubled its time).
+// keeps its register budget (a runtime branch doubled its time).  One item = 16 samples of a
+// row (4 dword stores): the value-noise cell hashes of the three octaves are shared by the
+// 16 samples (VNoiseRow), and the objects are filtered once per row (their vertical extent)
+// before the per-sample horizontal / shape tests.
 template <bool kTex>
 __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t seed, FrameIdx fi) {
   const int c = blockIdx.y, b = blockIdx.z;
@@ -82,12 +86,18 @@ __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t see
   if (threadIdx.x == 0) synth_frame_ctx(seed, fi.t[b], g.dw, g.dh, ctx);
   __syncthreads();
   uint8_t* P = src.plane(c, b, g);
-  const int s = c ? 1 : 0, pq = pw >> 2;  // pw is a multiple of 16
+  const int s = c ? 1 : 0, pq = pw >> 4;  // pw is a multiple of 16
   constexpr bool tex = kTex;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < pq * ph; i += gridDim.x * blockDim.x) {
-    const int y = i / pq, x0 = (i - y * pq) * 4;
+    const int y = i / pq, x0 = (i - y * pq) * 16;
     const int yc = tv_min(y, dh - 1), yl = yc << s;
     const int32_t by16 = yl * 16 + ctx.t * (tex ? 36 : 12);
+    unsigned rows = 0;
+#pragma unroll
+    for (int k = 0; k < kSynthObjects; ++k) {
+      const int32_t ry16 = yl * 16 - ctx.oy[k];
+      rows |= (ry16 >= 0 && ry16 < ctx.obj[k].h * 16) ? 1u << k : 0u;
+    }
     VNoiseRow n0, n1, n2, n3;
     if (c == 0) {
       n0.init(by16, 7, ctx.seed);
@@ -97,26 +107,31 @@ __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t see
     } else {
       n0.init(by16, 8, ctx.seed + 10 * c);
     }
-    uint32_t word = 0;
+    uint32_t words[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int xc = tv_min(x0 + j, dw - 1), xl = xc << s;
-      const int32_t bx16 = xl * 16 + ctx.t * (tex ? 88 : 36);
-      int v;
-      if (c == 0 && tex)
-        v = (n0.eval(bx16) * 3 + n1.eval(bx16) * 2 + n2.eval(bx16) * 2 + n3.eval(bx16)) >> 3;
-      else if (c == 0)
-        v = (n0.eval(bx16) * 5 + n1.eval(bx16) * 2 + n2.eval(bx16)) >> 3;
-      else
-        v = 96 + (n0.eval(bx16) >> 1);
-      v = synth_objects(ctx, c, xl, yl, v);
-      if (tex) {  // per-frame grain, as synth_sample_ctx
-        const uint32_t gr = synth_hash(xc + ctx.t * 7919, yc + c * 104729, ctx.seed ^ 0x5bd1e995u);
-        v += c ? (int)(gr & 3) - 2 : (int)(gr & 7) - 4;
+    for (int q = 0; q < 4; ++q) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int xc = tv_min(x0 + 4 * q + j, dw - 1), xl = xc << s;
+        const int32_t bx16 = xl * 16 + ctx.t * (tex ? 88 : 36);
+        int v;
+        if (c == 0 && tex)
+          v = (n0.eval(bx16) * 3 + n1.eval(bx16) * 2 + n2.eval(bx16) * 2 + n3.eval(bx16)) >> 3;
+        else if (c == 0)
+          v = (n0.eval(bx16) * 5 + n1.eval(bx16) * 2 + n2.eval(bx16)) >> 3;
+        else
+          v = 96 + (n0.eval(bx16) >> 1);
+        if (rows) v = synth_objects(ctx, c, xl, yl, v, rows);
+        if (tex) {  // per-frame grain, as synth_sample_ctx
+          const uint32_t gr = synth_hash(xc + ctx.t * 7919, yc + c * 104729, ctx.seed ^ 0x5bd1e995u);
+          v += c ? (int)(gr & 3) - 2 : (int)(gr & 7) - 4;
+        }
+        word |= (uint32_t)clip_pixel(v) << (8 * j);
       }
-      word |= (uint32_t)clip_pixel(v) << (8 * j);
+      words[q] = word;
     }
-    *reinterpret_cast<uint32_t*>(P + (long)y * pw + x0) = word;
+    *reinterpret_cast<uint4*>(P + (long)y * pw + x0) = make_uint4(words[0], words[1], words[2], words[3]);
   }
 }
 

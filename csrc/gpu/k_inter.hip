@@ -187,7 +187,9 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   __shared__ unsigned best[21];
   __shared__ int bcost[21], bmv[21][2];
   __shared__ int subsad[21][8];
-  __shared__ int sad16[kMeMaxCand * kMePosPerCand][4];  // per position: the 4 quadrant 16x16 SADs
+  // per position: the 4 quadrant 16x16 SADs, row stride 5 (odd): the quadrant lanes of 8
+  // items write 32 distinct banks (stride 4 put them on 8 banks: 4-way conflicts)
+  __shared__ int sad16[kMeMaxCand * kMePosPerCand][5];
   for (int t = tid; t < 256; t += kMeThreads)
     s32[src_word(t >> 3, t & 7)] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (t >> 3)) * g.W + cx + 4 * (t & 7));
   if (tid == 0) {
@@ -317,8 +319,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   const uint8_t* ph = phase + (long)b * 16 * g.psz;
   const int last_step = skip_sub ? 4 : (diag_stop == 3 ? 2 : 1);
   for (int step = 2; step >= last_step; step >>= 1) {
-    for (int t = tid; t < 168; t += kMeThreads) subsad[t >> 3][t & 7] = 0;
-    __syncthreads();
+    __syncthreads();  // bmv of the previous step / the integer search
     // A thread owns a group of 8 rows x 8 pixels of one (block, candidate): per row it loads
     // 3 aligned dwords of the phase plane, forms the 2 shifted dwords with v_alignbyte and
     // accumulates with v_sad_u8.  Groups per candidate: 16 (8x8) + 16 (16x16) + 16 (32x32).
@@ -370,7 +371,20 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
           }
         }
       }
-      atomicAdd(&subsad[bi][k], (int)sad);
+      // group sums on the VALU instead of LDS atomics (r < 16: one 8x8 group per block;
+      // 16..31: 4 aligned lanes per 16x16 block; 32..47: one aligned 16-lane row per 32x32)
+      // -- every (block, candidate) cell is written exactly once, by a plain store
+      int q4 = (int)sad;
+      q4 += dpp::mov<dpp::kQuadXor1>(q4);
+      q4 += dpp::mov<dpp::kQuadXor2>(q4);
+      int s16 = q4 + dpp::mov<dpp::kRowHalfMirror>(q4);
+      s16 += dpp::mov<dpp::kRowMirror>(s16);
+      if (r < 16) subsad[bi][k] = (int)sad;
+      else if (r < 32) {
+        if (((r - 16) & 3) == 0) subsad[bi][k] = q4;
+      } else if (r == 32) {
+        subsad[bi][k] = s16;
+      }
     }
     __syncthreads();
     if (tid < 21) {

@@ -58,11 +58,17 @@ TV_HD int uv_txtype(int uv_mode) {
 // Dc_Qlookup / Ac_Qlookup (8-bit) of the specification (tv/av1_tables.h)
 TV_HD int ac_q(int q) { return tab::kAcQLookup[clip3(0, 255, q)]; }
 TV_HD int dc_q(int q) { return tab::kDcQLookup[clip3(0, 255, q)]; }
-// encoder quantisation rounding (1/128 of the step): 1/3 for intra and inter blocks.  With
-// the refined motion field the inter residual is small and coherent, so the narrower dead
-// zone pays: inter 1/6 -> 1/3 is -2.3 % BD-rate on the bench content (tools/rd_curve.py
-// --codec av1; 1/4.6 -1.2 %, 1/2.6 -1.8 %, 1/2.1 +1.7 %).
-constexpr int kRndIntra = 43, kRndInter = 43;
+// encoder quantisation rounding (1/128 of the step): 1/3 for intra blocks; inter frames
+// choose per frame (inter_rounding).  With the refined motion field a clean source leaves a
+// small, coherent residual that is worth keeping (1/3: -2.3 % BD-rate against 1/6 on the
+// smooth bench content), while sensor grain is not (1/6: -5.5 % on the textured variant).
+// The frame's mean luma SATD per pixel at its final MVs tells them apart: 1.8-3.5 on the
+// smooth content, 6.3-10 on the textured one at QP 22..37 (tools/rd_curve.py --codec av1).
+constexpr int kRndIntra = 43, kRndInter = 43, kRndInterNoisy = 21;
+constexpr int kNoisySatdPerPx = 5;
+TV_HD int inter_rounding(long long satd_sum, int W, int H) {
+  return satd_sum > (long long)kNoisySatdPerPx * W * H ? kRndInterNoisy : kRndInter;
+}
 TV_HD int quant(int c, int q, int rnd) {
   const int a = c < 0 ? -c : c;
   const int l = (a + ((q * rnd) >> 7)) / q;
