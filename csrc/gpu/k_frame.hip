@@ -73,10 +73,10 @@ __device__ __forceinline__ int synth_objects(const SynthFrameCtx& f, int c, int 
 }
 
 // kTex: the textured variant (seed bit 31) is a separate instantiation so the smooth source
-// keeps its register budget (a runtime branch doubled its time).  One item = 16 samples of a
-// row (4 dword stores): the value-noise cell hashes of the three octaves are shared by the
-// 16 samples (VNoiseRow), and the objects are filtered once per row (their vertical extent)
-// before the per-sample horizontal / shape tests.
+// keeps its register budget (a runtime branch doubled its time).  The objects are filtered
+// once per item by their vertical extent before the per-sample horizontal / shape tests.
+// (16 samples per item shared more cell hashes but cut occupancy 22 -> 13 waves/CU and was
+// 16 % slower: profiles/README.md.)
 template <bool kTex>
 __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t seed, FrameIdx fi) {
   const int c = blockIdx.y, b = blockIdx.z;
@@ -86,10 +86,10 @@ __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t see
   if (threadIdx.x == 0) synth_frame_ctx(seed, fi.t[b], g.dw, g.dh, ctx);
   __syncthreads();
   uint8_t* P = src.plane(c, b, g);
-  const int s = c ? 1 : 0, pq = pw >> 4;  // pw is a multiple of 16
+  const int s = c ? 1 : 0, pq = pw >> 2;  // pw is a multiple of 16
   constexpr bool tex = kTex;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < pq * ph; i += gridDim.x * blockDim.x) {
-    const int y = i / pq, x0 = (i - y * pq) * 16;
+    const int y = i / pq, x0 = (i - y * pq) * 4;
     const int yc = tv_min(y, dh - 1), yl = yc << s;
     const int32_t by16 = yl * 16 + ctx.t * (tex ? 36 : 12);
     unsigned rows = 0;
@@ -107,31 +107,26 @@ __global__ void __launch_bounds__(256) k_synth(FrameSet src, Geo g, uint32_t see
     } else {
       n0.init(by16, 8, ctx.seed + 10 * c);
     }
-    uint32_t words[4];
+    uint32_t word = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t word = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int xc = tv_min(x0 + 4 * q + j, dw - 1), xl = xc << s;
-        const int32_t bx16 = xl * 16 + ctx.t * (tex ? 88 : 36);
-        int v;
-        if (c == 0 && tex)
-          v = (n0.eval(bx16) * 3 + n1.eval(bx16) * 2 + n2.eval(bx16) * 2 + n3.eval(bx16)) >> 3;
-        else if (c == 0)
-          v = (n0.eval(bx16) * 5 + n1.eval(bx16) * 2 + n2.eval(bx16)) >> 3;
-        else
-          v = 96 + (n0.eval(bx16) >> 1);
-        if (rows) v = synth_objects(ctx, c, xl, yl, v, rows);
-        if (tex) {  // per-frame grain, as synth_sample_ctx
-          const uint32_t gr = synth_hash(xc + ctx.t * 7919, yc + c * 104729, ctx.seed ^ 0x5bd1e995u);
-          v += c ? (int)(gr & 3) - 2 : (int)(gr & 7) - 4;
-        }
-        word |= (uint32_t)clip_pixel(v) << (8 * j);
+    for (int j = 0; j < 4; ++j) {
+      const int xc = tv_min(x0 + j, dw - 1), xl = xc << s;
+      const int32_t bx16 = xl * 16 + ctx.t * (tex ? 88 : 36);
+      int v;
+      if (c == 0 && tex)
+        v = (n0.eval(bx16) * 3 + n1.eval(bx16) * 2 + n2.eval(bx16) * 2 + n3.eval(bx16)) >> 3;
+      else if (c == 0)
+        v = (n0.eval(bx16) * 5 + n1.eval(bx16) * 2 + n2.eval(bx16)) >> 3;
+      else
+        v = 96 + (n0.eval(bx16) >> 1);
+      if (rows) v = synth_objects(ctx, c, xl, yl, v, rows);
+      if (tex) {  // per-frame grain, as synth_sample_ctx
+        const uint32_t gr = synth_hash(xc + ctx.t * 7919, yc + c * 104729, ctx.seed ^ 0x5bd1e995u);
+        v += c ? (int)(gr & 3) - 2 : (int)(gr & 7) - 4;
       }
-      words[q] = word;
+      word |= (uint32_t)clip_pixel(v) << (8 * j);
     }
-    *reinterpret_cast<uint4*>(P + (long)y * pw + x0) = make_uint4(words[0], words[1], words[2], words[3]);
+    *reinterpret_cast<uint32_t*>(P + (long)y * pw + x0) = word;
   }
 }
 
@@ -457,61 +452,79 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       }
     }
   }
-  // one region per wave: waves 0/1 = luma rows 0-15 / 16-31 (8 samples per lane), wave 2 =
-  // Cb, wave 3 = Cr (4 per lane).  Counts and sums travel packed as sum * 2048 + count
-  // (count <= 1024, |sum| <= 255 * 1024): one wave reduction per EO counter, not two.
+  // statistics, 6 samples per lane on every wave (1536 = 1024 luma + 2 x 256 chroma
+  // samples over 4 waves): wave 0 / 1 = luma samples [0, 384) / [384, 768); wave 2 = luma
+  // [768, 1024) + Cb [0, 128); wave 3 = Cb [128, 256) + Cr.  (One component per wave put
+  // 8 samples per lane on the luma waves and 4 on the chroma ones.)  Counts and sums travel
+  // packed as sum * 2048 + count (count <= 1024, |sum| <= 255 * 1024): one wave reduction
+  // per EO counter, not two.
   const int wave = tid >> 6;
-  const int c = wave < 2 ? 0 : wave - 1;
-  const int n = c ? 16 : 32, T = c ? kSaoTc : kSaoT, w = c ? g.W / 2 : g.W;
-  const int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
-  const int iters = c ? 4 : 8;
-  const uint8_t* S = src.plane(c, b, g) + (long)(cy * n) * w + cx * n;
-  int sv[8];
+  constexpr int kSegC[4][2] = {{0, -1}, {0, -1}, {0, 1}, {1, 2}};
+  constexpr int kSegI0[4][2] = {{0, 0}, {384, 0}, {768, 0}, {128, 0}};
+  constexpr int kSegN[4][2] = {{6, 0}, {6, 0}, {4, 2}, {2, 4}};  // samples per lane
+  int sv[6];
+  {
+    int k = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {  // source samples of this lane, loads in flight together
-    const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
-    sv[k] = k < iters ? S[(i / n) * w + i % n] : 0;
+    for (int sg = 0; sg < 2; ++sg) {
+      const int c = kSegC[wave][sg];
+      if (c < 0) continue;
+      const int n = c ? 16 : 32, w = c ? g.W / 2 : g.W;
+      const uint8_t* S = src.plane(c, b, g) + (long)(cy * n) * w + cx * n;
+      for (int q = 0; q < kSegN[wave][sg]; ++q, ++k) {  // loads in flight together
+        const int i = kSegI0[wave][sg] + lane + 64 * q;
+        sv[k] = S[(i / n) * w + i % n];
+      }
+    }
   }
   __syncthreads();
   // timing diagnostics only (TV_DIAG_SAO_STOP=1/2/3: stop after staging / statistics /
   // decision; the output is then incomplete) -- never set in production
   if (diag == 1) {
-    if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)(sv[0] + sv[7] + tile[tid]);
+    if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)(sv[0] + sv[5] + tile[tid]);
     return;
   }
-  int eo[4][4];
+  {
+    int k = 0;
 #pragma unroll
-  for (int d = 0; d < 4; ++d)
+    for (int sg = 0; sg < 2; ++sg) {
+      const int c = kSegC[wave][sg];
+      if (c < 0) continue;
+      const int n = c ? 16 : 32, T = c ? kSaoTc : kSaoT;
+      const int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
+      int eo[4][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) eo[d][q] = 0;
+      for (int d = 0; d < 4; ++d)
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (k >= iters) break;
-    const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
-    const int lx = i % n, ly = i / n;
-    const int v = t[(ly + 1) * T + lx + 1];
-    const int packed = (sv[k] - v) * 2048 + 1;
+        for (int q = 0; q < 4; ++q) eo[d][q] = 0;
+      for (int q = 0; q < kSegN[wave][sg]; ++q, ++k) {
+        const int i = kSegI0[wave][sg] + lane + 64 * q;
+        const int lx = i % n, ly = i / n;
+        const int v = t[(ly + 1) * T + lx + 1];
+        const int packed = (sv[k] - v) * 2048 + 1;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      int dx, dy;
-      sao_eo_dir(d, dx, dy);
-      const int a = t[(ly + 1 + dy) * T + lx + 1 + dx], bb = t[(ly + 1 - dy) * T + lx + 1 - dx];
-      const int cat = (a < 0 || bb < 0) ? 0 : sao_eo_category(v, a, bb);
+        for (int d = 0; d < 4; ++d) {
+          int dx, dy;
+          sao_eo_dir(d, dx, dy);
+          const int a = t[(ly + 1 + dy) * T + lx + 1 + dx], bb = t[(ly + 1 - dy) * T + lx + 1 - dx];
+          const int cat = (a < 0 || bb < 0) ? 0 : sao_eo_category(v, a, bb);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) eo[d][q] += cat == q + 1 ? packed : 0;
-    }
-    atomicAdd(&bh[c][v >> 3][lane & 15], packed);  // band statistics
-  }
-#pragma unroll
-  for (int d = 0; d < 4; ++d)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int tot = wave_sum(eo[d][q]);
-      if (lane == 0 && (tot & 2047)) {
-        atomicAdd(&st[c].eo_n[d][q + 1], tot & 2047);
-        atomicAdd(&st[c].eo_s[d][q + 1], (tot - (tot & 2047)) / 2048);
+          for (int e = 0; e < 4; ++e) eo[d][e] += cat == e + 1 ? packed : 0;
+        }
+        atomicAdd(&bh[c][v >> 3][lane & 15], packed);  // band statistics
       }
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int tot = wave_sum(eo[d][e]);
+          if (lane == 0 && (tot & 2047)) {
+            atomicAdd(&st[c].eo_n[d][e + 1], tot & 2047);
+            atomicAdd(&st[c].eo_s[d][e + 1], (tot - (tot & 2047)) / 2048);
+          }
+        }
     }
+  }
   __shared__ SaoTables tab;
   __shared__ uint32_t prm[3];
   __syncthreads();
