@@ -453,7 +453,7 @@ def av1_main(args) -> None:
         per-frame plan for this step's share of the target, corrected by the finished steps'
         bias and debt (ratecontrol.BatchRateController) -> this rank's per-frame q-index
         maps for pass 2."""
-        from thinvids_amd.models.ratecontrol import frame_sizes, plan_frame_qps, round_qps
+        from thinvids_amd.models.ratecontrol import AV1_SLOPE, frame_sizes, plan_frame_qps, round_qps
 
         g1 = g1fut.result()
         seg1 = [b"".join(f.result()) for f in eng.submit_entropy(g1)]
@@ -463,7 +463,7 @@ def av1_main(args) -> None:
         dist.all_reduce(flat)  # RC statistics all-reduce over the node
         allb = flat.cpu().numpy().reshape(world * batch, args.gop)
         ask, want, u = ctl.request(nominal)
-        plan, _ = plan_frame_qps(list(allb), args.qp, ask, key_offset=AV1_KEY_QP_OFFSET)
+        plan, _ = plan_frame_qps(list(allb), args.qp, ask, key_offset=AV1_KEY_QP_OFFSET, slope=AV1_SLOPE)
         qall = np.stack([round_qps(p, u) for p in plan])
         predicted[i] = (want, u)
         pass1_bits.append(float(mine.sum()))

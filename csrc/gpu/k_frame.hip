@@ -452,79 +452,61 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       }
     }
   }
-  // statistics, 6 samples per lane on every wave (1536 = 1024 luma + 2 x 256 chroma
-  // samples over 4 waves): wave 0 / 1 = luma samples [0, 384) / [384, 768); wave 2 = luma
-  // [768, 1024) + Cb [0, 128); wave 3 = Cb [128, 256) + Cr.  (One component per wave put
-  // 8 samples per lane on the luma waves and 4 on the chroma ones.)  Counts and sums travel
-  // packed as sum * 2048 + count (count <= 1024, |sum| <= 255 * 1024): one wave reduction
-  // per EO counter, not two.
+  // one region per wave: waves 0/1 = luma rows 0-15 / 16-31 (8 samples per lane), wave 2 =
+  // Cb, wave 3 = Cr (4 per lane).  Counts and sums travel packed as sum * 2048 + count
+  // (count <= 1024, |sum| <= 255 * 1024): one wave reduction per EO counter, not two.
   const int wave = tid >> 6;
-  constexpr int kSegC[4][2] = {{0, -1}, {0, -1}, {0, 1}, {1, 2}};
-  constexpr int kSegI0[4][2] = {{0, 0}, {384, 0}, {768, 0}, {128, 0}};
-  constexpr int kSegN[4][2] = {{6, 0}, {6, 0}, {4, 2}, {2, 4}};  // samples per lane
-  int sv[6];
-  {
-    int k = 0;
+  const int c = wave < 2 ? 0 : wave - 1;
+  const int n = c ? 16 : 32, T = c ? kSaoTc : kSaoT, w = c ? g.W / 2 : g.W;
+  const int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
+  const int iters = c ? 4 : 8;
+  const uint8_t* S = src.plane(c, b, g) + (long)(cy * n) * w + cx * n;
+  int sv[8];
 #pragma unroll
-    for (int sg = 0; sg < 2; ++sg) {
-      const int c = kSegC[wave][sg];
-      if (c < 0) continue;
-      const int n = c ? 16 : 32, w = c ? g.W / 2 : g.W;
-      const uint8_t* S = src.plane(c, b, g) + (long)(cy * n) * w + cx * n;
-      for (int q = 0; q < kSegN[wave][sg]; ++q, ++k) {  // loads in flight together
-        const int i = kSegI0[wave][sg] + lane + 64 * q;
-        sv[k] = S[(i / n) * w + i % n];
-      }
-    }
+  for (int k = 0; k < 8; ++k) {  // source samples of this lane, loads in flight together
+    const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
+    sv[k] = k < iters ? S[(i / n) * w + i % n] : 0;
   }
   __syncthreads();
   // timing diagnostics only (TV_DIAG_SAO_STOP=1/2/3: stop after staging / statistics /
   // decision; the output is then incomplete) -- never set in production
   if (diag == 1) {
-    if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)(sv[0] + sv[5] + tile[tid]);
+    if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)(sv[0] + sv[7] + tile[tid]);
     return;
   }
-  {
-    int k = 0;
+  int eo[4][4];
 #pragma unroll
-    for (int sg = 0; sg < 2; ++sg) {
-      const int c = kSegC[wave][sg];
-      if (c < 0) continue;
-      const int n = c ? 16 : 32, T = c ? kSaoTc : kSaoT;
-      const int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
-      int eo[4][4];
+  for (int d = 0; d < 4; ++d)
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
+    for (int q = 0; q < 4; ++q) eo[d][q] = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) eo[d][q] = 0;
-      for (int q = 0; q < kSegN[wave][sg]; ++q, ++k) {
-        const int i = kSegI0[wave][sg] + lane + 64 * q;
-        const int lx = i % n, ly = i / n;
-        const int v = t[(ly + 1) * T + lx + 1];
-        const int packed = (sv[k] - v) * 2048 + 1;
+  for (int k = 0; k < 8; ++k) {
+    if (k >= iters) break;
+    const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
+    const int lx = i % n, ly = i / n;
+    const int v = t[(ly + 1) * T + lx + 1];
+    const int packed = (sv[k] - v) * 2048 + 1;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          int dx, dy;
-          sao_eo_dir(d, dx, dy);
-          const int a = t[(ly + 1 + dy) * T + lx + 1 + dx], bb = t[(ly + 1 - dy) * T + lx + 1 - dx];
-          const int cat = (a < 0 || bb < 0) ? 0 : sao_eo_category(v, a, bb);
+    for (int d = 0; d < 4; ++d) {
+      int dx, dy;
+      sao_eo_dir(d, dx, dy);
+      const int a = t[(ly + 1 + dy) * T + lx + 1 + dx], bb = t[(ly + 1 - dy) * T + lx + 1 - dx];
+      const int cat = (a < 0 || bb < 0) ? 0 : sao_eo_category(v, a, bb);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) eo[d][e] += cat == e + 1 ? packed : 0;
-        }
-        atomicAdd(&bh[c][v >> 3][lane & 15], packed);  // band statistics
-      }
-#pragma unroll
-      for (int d = 0; d < 4; ++d)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int tot = wave_sum(eo[d][e]);
-          if (lane == 0 && (tot & 2047)) {
-            atomicAdd(&st[c].eo_n[d][e + 1], tot & 2047);
-            atomicAdd(&st[c].eo_s[d][e + 1], (tot - (tot & 2047)) / 2048);
-          }
-        }
+      for (int q = 0; q < 4; ++q) eo[d][q] += cat == q + 1 ? packed : 0;
     }
+    atomicAdd(&bh[c][v >> 3][lane & 15], packed);  // band statistics
   }
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int tot = wave_sum(eo[d][q]);
+      if (lane == 0 && (tot & 2047)) {
+        atomicAdd(&st[c].eo_n[d][q + 1], tot & 2047);
+        atomicAdd(&st[c].eo_s[d][q + 1], (tot - (tot & 2047)) / 2048);
+      }
+    }
   __shared__ SaoTables tab;
   __shared__ uint32_t prm[3];
   __syncthreads();

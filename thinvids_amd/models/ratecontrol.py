@@ -180,6 +180,11 @@ def round_qps(qf: np.ndarray, offset: float = 0.0, qp_min: int = 10, qp_max: int
     return out
 
 
+# AV1 (this repo's q-index map, qindex_for_hevc_qp): measured 4.4-5.6 QP per halving of the
+# bits around the 4K 20 Mbps operating point (profiles/README.md, round 4)
+AV1_SLOPE = 5.0
+
+
 class BatchRateController:
     """Batch-sequential 2-pass feedback (the bench's steps, a worker's claims).  Each batch
     is planned from its own pass-1 statistics (plan_frame_qps: the relative per-frame
@@ -192,9 +197,13 @@ class BatchRateController:
     the accumulated overshoot / undershoot is repaid by the next batch, at most 4 % of its
     share.  Deterministic in the (all-reduced) inputs, so every rank plans the same."""
 
-    def __init__(self, repay: float = 0.25, max_repay: float = 0.04, window: int = 4, max_offset: float = 12.0):
+    def __init__(self, repay: float = 0.25, max_repay: float = 0.04, window: int = 4, max_offset: float = 12.0,
+                 slope: float | None = None):
         self.target = self.actual = 0.0
         self.repay, self.max_repay, self.window, self.max_offset = repay, max_repay, window, max_offset
+        # QP per halving of the bits until two operating points measure it (codec-dependent:
+        # AV1_SLOPE for the AV1 q-index map)
+        self.slope = SLOPE if slope is None else float(slope)
         self.pts: list = []  # (offset u, log2(actual / wanted)) per finished batch
         self.log: list = []  # per finished batch: actual / nominal, wanted / nominal, offset
 
@@ -204,7 +213,7 @@ class BatchRateController:
             return 0.0
         u = np.array([p[0] for p in pts])
         r = np.array([p[1] for p in pts])
-        b = -1.0 / SLOPE
+        b = -1.0 / self.slope
         if np.ptp(u) > 0.25:  # two operating points: the measured response
             bu = float(np.polyfit(u, r, 1)[0])
             b = float(np.clip(bu, -1.0 / 3.5, -1.0 / 16.0))

@@ -38,8 +38,8 @@ import time
 
 import numpy as np
 
-from ..models.ratecontrol import (QCOMP, QCOMP_BFRAMES, SLOPE, AbrController, RateFeedback, frame_sizes, plan_frame_qps, predict_bits,
-                                  round_qps, vbv_ok, vbv_repair_offset, vbv_scale)
+from ..models.ratecontrol import (AV1_SLOPE, QCOMP, QCOMP_BFRAMES, SLOPE, AbrController, RateFeedback, frame_sizes,
+                                  plan_frame_qps, predict_bits, round_qps, vbv_ok, vbv_repair_offset, vbv_scale)
 from ..utils import fault, trace
 
 RC_TOLERANCE = 0.04  # a pass within +-4 % of the target bitrate is final (the contract is +-5 %)
@@ -829,7 +829,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 target = bitrate_kbps * 1000 * nfr / fps * rung_scale[r]
                 per_seg, _ = plan_frame_qps([rc["b1"][(r, i)] for i in range(len(segs))], qp, target,
                                             key_offset=-2.0 if codec == "av1" else None,
-                                            qcomp=QCOMP_BFRAMES if bframes > 1 and codec != "av1" else QCOMP)
+                                            qcomp=QCOMP_BFRAMES if bframes > 1 and codec != "av1" else QCOMP,
+                                            slope=AV1_SLOPE if codec == "av1" else SLOPE)
                 plan.append(per_seg)
             rc["plan"] = plan
             targets = [bitrate_kbps * 1000 * nfr / fps * (rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]
