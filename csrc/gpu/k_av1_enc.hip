@@ -207,7 +207,17 @@ __global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Pla
   // source block; windows fully inside the frame take dword loads (their origins are
   // 4-byte aligned: x0 - 20 and cx0 - 12 with x0 % 16 == 0, cx0 % 8 == 0)
   const int wx0 = x0 - kWinOff, wy0 = y0 - kWinOff;
-  if (wx0 >= 0 && wy0 >= 0 && wx0 + kWinP <= W && wy0 + kWinN <= H) {
+  if (STAGE == 1) {
+    // the recon reads only the 23 x 23 reference samples of its MV's 8-tap footprint: stage
+    // just those (clamped) into their window positions
+    const uint32_t m = mvin[(long)b * (bw * (H >> 4)) + blk];
+    const int ix = mv_int(mv_col(m), false) - 3, iy = mv_int(mv_row(m), false) - 3;
+    for (int i = lane; i < 23 * 23; i += 64) {
+      const int wy = i / 23, wx = i - wy * 23;
+      const int yy = clip3(0, H - 1, y0 + iy + wy), xx = clip3(0, W - 1, x0 + ix + wx);
+      win[(kWinOff + iy + wy) * kWinP + kWinOff + ix + wx] = Rf[(long)yy * W + xx];
+    }
+  } else if (wx0 >= 0 && wy0 >= 0 && wx0 + kWinP <= W && wy0 + kWinN <= H) {
     for (int i = lane; i < kWinN * (kWinP / 4); i += 64) {
       const int wy = i / (kWinP / 4), wq = i - wy * (kWinP / 4);
       reinterpret_cast<uint32_t*>(win + wy * kWinP)[wq] =
@@ -489,9 +499,17 @@ __device__ __forceinline__ int sb_pair_satd(const uint8_t* win, const uint8_t* s
 // neighbours' current MVs (read from `cur`, across superblock edges too) by luma SATD
 // (first minimum, own MV first) and writes `nxt`.  (block, candidate) pairs 16 per pass
 // on the staged superblock window.
+// Memo: each round records, per block, the (MV, SATD) pairs it scored ([B][nb] records of
+// kMvRefineMaxCand + a count); the next round takes the SATD of a candidate it already scored
+// from there (its own MV always, most neighbours' MVs too) instead of recomputing it.
+struct MvMemo {
+  uint32_t* mv;   // [B][nb][kMvRefineMaxCand]
+  int* sat;       // [B][nb][kMvRefineMaxCand]
+  uint8_t* n;     // [B][nb]
+};
 __global__ void __launch_bounds__(256) k_av1e_mv_refine(const uint8_t* __restrict__ srcy, const uint8_t* __restrict__ refy,
                                                         const uint32_t* __restrict__ cur, uint32_t* __restrict__ nxt,
-                                                        int W, int H) {
+                                                        int W, int H, MvMemo prev, MvMemo next, int use_prev) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kSbWin * kSbWin];
   __shared__ __attribute__((aligned(16))) uint8_t sb[64 * 64];
   __shared__ uint32_t cand[16][kMvRefineMaxCand];
@@ -502,21 +520,46 @@ __global__ void __launch_bounds__(256) k_av1e_mv_refine(const uint8_t* __restric
   const int sbi = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   const int bw = W >> 4, bh = H >> 4, sbw = (W + 63) >> 6, sx = sbi % sbw, sy = sbi / sbw;
   const long ysz = (long)W * H, nb = (long)bw * bh;
-  stage_sb(srcy + b * ysz, refy + b * ysz, W, H, sx * 64, sy * 64, win, sb);
   const uint32_t* C = cur + b * nb;
+  constexpr int kM = kMvRefineMaxCand;
+  __shared__ uint32_t pmv[16][kM];
+  __shared__ int psat[16][kM], pn[16];
+  // lanes (k, j) = (t / kM, t % kM) of the first 16 * kM: block k's record j of the previous round
+  const int mk = t / kM, mj = t - mk * kM;
+  const int mbx = sx * 4 + (mk & 3), mby = sy * 4 + (mk >> 2);
+  const bool mlane = t < 16 * kM && mbx < bw && mby < bh;
+  const long mr = b * nb + (long)mby * bw + mbx;
   if (t < 16) {
     const int bx = sx * 4 + (t & 3), by = sy * 4 + (t >> 2);
-    ncand[t] = (bx < bw && by < bh) ? mv_refine_cands(C, bw, bh, bx, by, cand[t]) : 0;
+    const bool in = bx < bw && by < bh;
+    ncand[t] = in ? mv_refine_cands(C, bw, bh, bx, by, cand[t]) : 0;
+    pn[t] = (in && use_prev) ? prev.n[b * nb + (long)by * bw + bx] : 0;
+  }
+  if (mlane && use_prev) {
+    pmv[mk][mj] = prev.mv[mr * kM + mj];
+    psat[mk][mj] = prev.sat[mr * kM + mj];
+  }
+  __syncthreads();
+  if (mlane && mj < ncand[mk]) {  // memo lookup of pair (mk, mj)
+    int v = -1;
+    for (int j = 0; j < pn[mk]; ++j)
+      if (pmv[mk][j] == cand[mk][mj]) v = psat[mk][j];
+    sat[mk][mj] = v;
   }
   __syncthreads();
   if (t == 0) {
     int n = 0;
     for (int k = 0; k < 16; ++k)
-      for (int c = 0; c < ncand[k]; ++c) pk[n++] = (k << 8) | c;
+      for (int c = 0; c < ncand[k]; ++c)
+        if (sat[k][c] < 0) pk[n++] = (k << 8) | c;
     npairs = n;
   }
   __syncthreads();
   const int grp = t >> 4, b4 = t & 15, n = npairs;
+  if (n) {  // a converged superblock (every candidate memoised) skips the staging
+    stage_sb(srcy + b * ysz, refy + b * ysz, W, H, sx * 64, sy * 64, win, sb);
+    __syncthreads();
+  }
   for (int p0 = 0; p0 < n; p0 += 16) {
     const int p = p0 + grp;
     if (p < n) {  // uniform over each 16-lane row (the row16_sum DPP stays inside it)
@@ -531,7 +574,13 @@ __global__ void __launch_bounds__(256) k_av1e_mv_refine(const uint8_t* __restric
     for (int c = 1; c < ncand[t]; ++c)
       if (sat[t][c] < bc) bc = sat[t][c], bi = c;
     const int bx = sx * 4 + (t & 3), by = sy * 4 + (t >> 2);
-    nxt[b * nb + by * bw + bx] = cand[t][bi];
+    const long r = b * nb + (long)by * bw + bx;
+    nxt[r] = cand[t][bi];
+    if (next.n) next.n[r] = (uint8_t)ncand[t];
+  }
+  if (next.n && mlane && mj < ncand[mk]) {
+    next.mv[mr * kM + mj] = cand[mk][mj];
+    next.sat[mr * kM + mj] = sat[mk][mj];
   }
 }
 
@@ -1043,16 +1092,29 @@ const char* tv_av1e_last_error() { return g_err.c_str(); }
 // ping-ponging between tmp and mv (ending in mv), then the recon at mv.
 int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* ry, const uint8_t* ru,
                   const uint8_t* rv, uint8_t* oy, uint8_t* ou, uint8_t* ov, uint32_t* mode, uint32_t* mv, uint32_t* tmp,
-                  unsigned long long* satd_acc, int16_t* ly, int16_t* lu, int16_t* lv, int W, int H, int B,
-                  const int* qarr, void* stream) {
+                  unsigned long long* satd_acc, uint8_t* memo, int16_t* ly, int16_t* lu, int16_t* lv, int W, int H,
+                  int B, const int* qarr, void* stream) {
   if (bad(W, H, B, 1, "av1e_inter") || ensure_tables()) return -1;
   static_assert(kMvRefineRounds % 2 == 1, "an odd round count ends the field in `mv`");
   const int nb = (W >> 4) * (H >> 4), nsb = ((W + 63) >> 6) * ((H + 63) >> 6);
   hipStream_t st = (hipStream_t)stream;
   k_av1e_inter<0><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
                                                nullptr, tmp, ly, lu, lv, W, H, qarr, satd_acc);
-  for (int r = 0; r < kMvRefineRounds; ++r)
-    k_av1e_mv_refine<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, (r & 1) ? mv : tmp, (r & 1) ? tmp : mv, W, H);
+  // memo: two [B][nb] record sets (mv words, SATDs, counts), ping-ponged across the rounds
+  const long nrec = (long)B * nb;
+  MvMemo mm[2];
+  for (int k = 0; k < 2; ++k) {
+    uint8_t* base = memo + k * nrec * (kMvRefineMaxCand * 8 + 1);
+    mm[k].mv = reinterpret_cast<uint32_t*>(base);
+    mm[k].sat = reinterpret_cast<int*>(base + nrec * kMvRefineMaxCand * 4);
+    mm[k].n = base + nrec * kMvRefineMaxCand * 8;
+  }
+  for (int r = 0; r < kMvRefineRounds; ++r) {
+    const MvMemo none{nullptr, nullptr, nullptr};
+    k_av1e_mv_refine<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, (r & 1) ? mv : tmp, (r & 1) ? tmp : mv, W, H,
+                                                    r ? mm[(r - 1) & 1] : none, r + 1 < kMvRefineRounds ? mm[r & 1] : none,
+                                                    r > 0);
+  }
   if (hipMemsetAsync(satd_acc, 0, (size_t)B * sizeof(unsigned long long), st) != hipSuccess) return status("av1e_inter");
   k_av1e_mv_unify<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, mv, W, H, qarr, satd_acc);
   k_av1e_inter<1><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,

@@ -186,9 +186,11 @@ class Av1GpuEngine:
             if getattr(self, "_mvtmp", None) is None:
                 self._mvtmp = torch.empty(self.B * self.nb, dtype=torch.int32, device=self.dev)
                 self._satd = torch.empty(self.B, dtype=torch.int64, device=self.dev)  # per-segment frame SATD
+                # refinement memo: 2 x [B][nb] x (11 MV words + 11 SATDs + a count)
+                self._memo = torch.empty(2 * self.B * self.nb * (11 * 8 + 1), dtype=torch.uint8, device=self.dev)
             _ok(lib.tv_av1e_inter(_p(sy), _p(su), _p(sv), _p(fy), _p(fu), _p(fv), _p(ry), _p(ru), _p(rv), _p(mode),
-                                  _p(mv), _p(self._mvtmp), _p(self._satd), _p(ly), _p(lu), _p(lv), W, H, B, _p(qarr),
-                                  st))
+                                  _p(mv), _p(self._mvtmp), _p(self._satd), _p(self._memo), _p(ly), _p(lu), _p(lv), W, H,
+                                  B, _p(qarr), st))
             _ok(lib.tv_av1e_merge(_p(mode), _p(mv), W, H, B, st))
         iy = torch.empty((B, H // 4, W // 4), dtype=torch.int32, device=self.dev)
         iu = torch.empty((B, H // 8, W // 8), dtype=torch.int32, device=self.dev)
