@@ -80,33 +80,39 @@ void pad_source(const uint8_t* const planes[3], const int strides[3], int width,
 }
 
 // ------------------------------------ analysis ------------------------------------------
+namespace {
+struct IntraBest {
+  int cost, mode;
+};
+// two-stage mode search (tv/me_model.h kIntraCoarseModes): planar, DC and every 4th angular
+// mode, then the +-1/+-2 neighbours of the best coarse angular mode; SATD against the SOURCE
+// neighbours' prediction + the mode penalty (k_intra_analysis / k_pintra_analysis)
+IntraBest intra_best_mode(const Picture& src, int W, double lam, int x, int y, int log2, int* pred) {
+  unsigned best = 0xffffffffu, best_ang = 0xffffffffu;
+  auto eval = [&](int m) {
+    predict_intra_tb(src, 0, x, y, log2, m, pred);
+    int c = block_satd(src.y.data() + (size_t)y * W + x, W, pred, 1 << log2);
+    c += (int)(lam * (m <= 1 ? 2 : 5));
+    const unsigned v = ((unsigned)c << 6) | (unsigned)m;
+    best = v < best ? v : best;
+    if (m >= 2) best_ang = v < best_ang ? v : best_ang;
+  };
+  for (int i = 0; i < kIntraCoarseModes; ++i) eval(intra_coarse_mode(i));
+  const int ma = (int)(best_ang & 63);
+  for (int i = 0; i < 4; ++i) {
+    const int m = intra_refine_mode(ma, i);
+    if (m >= 2) eval(m);
+  }
+  return IntraBest{(int)(best >> 6), (int)(best & 63)};
+}
+}  // namespace
+
 void analyze_intra(const SeqConfig& cfg, const Picture& src, FrameDecisions& fd) {
   const double lam = lambda_sad(cfg.qp);
   const int W = cfg.coded_w, H = cfg.coded_h;
   int pred[32 * 32];
-  struct Best {
-    int cost, mode;
-  };
-  // two-stage mode search (tv/me_model.h kIntraCoarseModes): planar, DC and every 4th
-  // angular mode, then the +-1/+-2 neighbours of the best coarse angular mode
-  auto best_mode = [&](int x, int y, int log2) -> Best {
-    unsigned best = 0xffffffffu, best_ang = 0xffffffffu;
-    auto eval = [&](int m) {
-      predict_intra_tb(src, 0, x, y, log2, m, pred);
-      int c = block_satd(src.y.data() + (size_t)y * W + x, W, pred, 1 << log2);
-      c += (int)(lam * (m <= 1 ? 2 : 5));
-      const unsigned v = ((unsigned)c << 6) | (unsigned)m;
-      best = v < best ? v : best;
-      if (m >= 2) best_ang = v < best_ang ? v : best_ang;
-    };
-    for (int i = 0; i < kIntraCoarseModes; ++i) eval(intra_coarse_mode(i));
-    const int ma = (int)(best_ang & 63);
-    for (int i = 0; i < 4; ++i) {
-      const int m = intra_refine_mode(ma, i);
-      if (m >= 2) eval(m);
-    }
-    return Best{(int)(best >> 6), (int)(best & 63)};
-  };
+  using Best = IntraBest;
+  auto best_mode = [&](int x, int y, int log2) -> Best { return intra_best_mode(src, W, lam, x, y, log2, pred); };
   for (int cy = 0; cy < H; cy += 32)
     for (int cx = 0; cx < W; cx += 32) {
       // bottom-up quadtree on source-based costs
@@ -305,10 +311,25 @@ void split_ctb(const int* bcost, int pen_split, int sel[16], uint8_t l2[16]) {
 }
 }  // namespace
 
+// Intra candidate of the P-picture quadrant at (x, y) (tv/me_model.h pintra_*): 0x80 | mode
+// when the best intra mode's SAD + penalty beats the quadrant's 16x16 inter cost, else 0.
+static uint8_t pintra_candidate(const Picture& src, int W, double lam, int x, int y, int inter_cost) {
+  if (inter_cost <= kPIntraGate * 256) return 0;
+  int pred[16 * 16];
+  const IntraBest ib = intra_best_mode(src, W, lam, x, y, 4, pred);
+  predict_intra_tb(src, 0, x, y, 4, ib.mode, pred);
+  int sad = 0;
+  for (int j = 0; j < 16; ++j)
+    for (int i = 0; i < 16; ++i) sad += tv_abs((int)src.y[(size_t)(y + j) * W + x + i] - pred[j * 16 + i]);
+  return pintra_cost(sad, (int)(lam * kPIntraPenBits)) < inter_cost ? (uint8_t)(0x80 | ib.mode) : (uint8_t)0;
+}
+
 void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, const int16_t* cmv,
                    const int16_t* prev_mv, int range, FrameDecisions& fd) {
-  const int pen_split = (int)(lambda_sad(cfg.qp) * 4);
+  const double lam = lambda_sad(cfg.qp);
+  const int pen_split = (int)(lam * 4);
   const int wc = cfg.coded_w / kCtb, hc = cfg.coded_h / kCtb;
+  std::vector<uint8_t> cand(cfg.pintra ? (size_t)wc * hc * 4 : 0, 0);
   for (int cyi = 0; cyi < hc; ++cyi)
     for (int cxi = 0; cxi < wc; ++cxi) {
       CtbMe me;
@@ -324,6 +345,34 @@ void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref,
         fd.mv[2 * u + 1] = (int16_t)me.mv[sel[k]][1];
         fd.intra[u] = 0;
         fd.ipm[u] = 1;
+      }
+      if (cfg.pintra)
+        for (int q = 0; q < 4; ++q)
+          cand[((size_t)cyi * wc + cxi) * 4 + q] = pintra_candidate(
+              src, cfg.coded_w, lam, cxi * kCtb + (q & 1) * 16, cyi * kCtb + (q >> 1) * 16, me.cost[16 + q]);
+    }
+  if (cfg.pintra) apply_pintra(cand.data(), wc, hc, fd);
+}
+
+// Accepted intra quadrants (tv/me_model.h pintra_accepted) into the decisions: the CTB becomes
+// four 16x16 CUs (a 32x32 inter CU's vector kept by the other quadrants), the quadrant a
+// 16x16 intra CU with vector 0 (k_pintra_select).
+void apply_pintra(const uint8_t* cand, int wc, int hc, FrameDecisions& fd) {
+  for (int cyi = 0; cyi < hc; ++cyi)
+    for (int cxi = 0; cxi < wc; ++cxi) {
+      bool acc[4], any = false;
+      for (int q = 0; q < 4; ++q) any |= acc[q] = pintra_accepted(cand, wc, hc, cxi, cyi, q);
+      if (!any) continue;
+      const int u0 = (cyi * kCtb >> 3) * fd.w8 + (cxi * kCtb >> 3);
+      const bool whole = fd.cu_log2[u0] == 5;
+      for (int k = 0; k < 16; ++k) {
+        const int u = u0 + (k >> 2) * fd.w8 + (k & 3), q = ((k >> 3) << 1) | ((k >> 1) & 1);
+        if (whole) fd.cu_log2[u] = 4;
+        if (!acc[q]) continue;
+        fd.cu_log2[u] = 4;
+        fd.intra[u] = 1;
+        fd.ipm[u] = (uint8_t)(cand[((size_t)cyi * wc + cxi) * 4 + q] & 63);
+        fd.mv[2 * u] = fd.mv[2 * u + 1] = 0;
       }
     }
 }

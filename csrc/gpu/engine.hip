@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "k_encode.h"
+#include "tv/me_model.h"
 #include "tv/cpu_encoder.h"
 #include "tv/hevc_codec.h"
 
@@ -178,6 +179,17 @@ class Core {
     dev_alloc(&cmv_, 2 * B * nctu_ * 2 * sizeof(int16_t));
     dev_alloc(&ccost_, 2 * B * nctu_ * sizeof(int));
     if (c.mgop > 1) dev_alloc(&meout_, 2 * B * nctu_ * sizeof(CtbMeOut));
+    if (SeqConfig::pintra_default()) {  // intra-in-P scores and lists (tv/me_model.h pintra_*)
+      uint8_t* m = nullptr;
+      dev_alloc(&m, pintra_bytes(B, nctu_));
+      const long n = B * nctu_;
+      pi_.qcost = reinterpret_cast<int*>(m);
+      pi_.gate = reinterpret_cast<int*>(m + align(n * 16));
+      pi_.pass = reinterpret_cast<int*>(m + 2 * align(n * 16));
+      pi_.clist = reinterpret_cast<int*>(m + 3 * align(n * 16));
+      pi_.count = reinterpret_cast<int*>(m + 4 * align(n * 16));
+      pi_.cand = m + 4 * align(n * 16) + 256;
+    }
     cap_ = g_.ysz + 2 * g_.csz;
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
     slot_bytes_ = align(B * g_.usz) + align(B * g_.usz * 4) + align(B * nctu_ * 8) + align(B * nctu_ * 4) +
@@ -209,6 +221,7 @@ class Core {
         p.mode_ang = (int)(lam * 5);
         p.split_intra = (int)(lam * 3);
         p.split_inter = (int)(lam * 4);
+        p.pintra = (int)(lam * kPIntraPenBits);
         for (int i = 0; i < 64; ++i) p.mv[i] = (int)(lam * i);
         t.sao_lam16[q] = sao_lambda16(q);
       }
@@ -248,7 +261,8 @@ class Core {
     dev = set + ndpb * (set + B * 16 * g.psz + B * qsz) + ((c.deblock & 2) ? set : 0) + 2 * set +
           B * 3 * sizeof(unsigned long long) + B * nctu * sizeof(int) + 2 * B * nctu * 2 * sizeof(int16_t) +
           2 * B * nctu * sizeof(int) + (c.mgop > 1 ? 2 * B * nctu * sizeof(CtbMeOut) : 0) +
-          (size_t)slot_count() * slot + sizeof(RcTables);
+          (SeqConfig::pintra_default() ? pintra_bytes((long)B, (long)nctu) : 0) + (size_t)slot_count() * slot +
+          sizeof(RcTables);
     host = (size_t)c.gop * B + B + (size_t)slot_count() * slot;
   }
 
@@ -259,6 +273,7 @@ class Core {
     for (int k = 0; k < ndpb_; ++k)
       for (auto* p : {dpb_[k].rec.y, dpb_[k].rec.u, dpb_[k].rec.v, dpb_[k].phase, dpb_[k].q}) (void)hipFree(p);
     (void)hipFree(meout_);
+    (void)hipFree(pi_.qcost);
     (void)hipFree(coef_y_);
     (void)hipFree(coef_u_);
     (void)hipFree(coef_v_);
@@ -303,6 +318,8 @@ class Core {
     return n;
   }
   static long align(long n) { return (n + 255) & ~255L; }
+  // qcost, gate list, pass lists, candidate list (16 bytes per CTB each), counters, candidate bytes
+  static size_t pintra_bytes(long B, long nctu) { return 4 * align(B * nctu * 16) + 256 + align(B * nctu * 4); }
   struct Slot {
     uint8_t* dev = nullptr;
     uint8_t* host = nullptr;
@@ -482,10 +499,13 @@ class Core {
     // Every D2H copy is a blit-kernel launch (~10 us of CU time each): the full-batch case
     // moves the whole contiguous header (decision planes .. SAO params) in one copy and all
     // segments' packed levels (back to back) in a second one.
+    // a P picture with intra quadrants needs the mode plane too (right after the head)
+    const bool pipm = ptype == 1 && pi_.qcost;
     if (B == cfg_.batch) {
-      const long head = reinterpret_cast<uint8_t*>(d.qp) + B - d.flags;
+      const long head = (pipm ? d.ipm + B * U : reinterpret_cast<uint8_t*>(d.qp) + B) - d.flags;
       HIP_OK(hipMemcpyAsync(h.flags, d.flags, head, hipMemcpyDeviceToHost, ws));
-    } else {  // partial batch: each plane is laid out for cfg_.batch segments
+    } else {
+      if (pipm) HIP_OK(hipMemcpyAsync(h.ipm, d.ipm, B * U, hipMemcpyDeviceToHost, ws));  // partial batch: each plane is laid out for cfg_.batch segments
       HIP_OK(hipMemcpyAsync(h.total, d.total, B * 4, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.qp, d.qp, B, hipMemcpyDeviceToHost, ws));
       HIP_OK(hipMemcpyAsync(h.flags, d.flags, B * U, hipMemcpyDeviceToHost, ws));
@@ -607,7 +627,8 @@ class Core {
       HIP_OK(hipStreamWaitEvent(stream_, iev_[1], 0));
     } else if (!bpic) {
       const DpbEntry& r0 = entry_of(pic.ref[0]);
-      launch_inter_frame(src_, r0.rec, r0.phase, cur, dec, g_, rc_, rng[0], me[0], B, stream_);
+      launch_inter_frame(src_, r0.rec, r0.phase, cur, dec, g_, rc_, rng[0], me[0], B, stream_,
+                         pi_.qcost ? &pi_ : nullptr);
     } else {
       const DpbEntry& r0 = entry_of(pic.ref[0]);
       const DpbEntry& r1 = entry_of(pic.ref[1]);
@@ -733,6 +754,7 @@ class Core {
   GopPlan plan_;
   std::vector<SliceRefs> refs_;
   CtbMeOut* meout_ = nullptr;
+  PIntraBuffers pi_{};  // qcost == nullptr: intra-in-P off (TV_PINTRA=0)
   int16_t *coef_y_ = nullptr, *coef_u_ = nullptr, *coef_v_ = nullptr;
   unsigned long long* d_sse_ = nullptr;
   void* count_scratch_ = nullptr;

@@ -16,7 +16,7 @@ struct FrameIdx {
 // Integer rate penalties (lambda * bits) precomputed on the host exactly like the CPU
 // reference encoder computes them, so GPU and CPU decisions agree.
 struct Penalties {
-  int mode_dcpl, mode_ang, split_intra, split_inter;
+  int mode_dcpl, mode_ang, split_intra, split_inter, pintra;
   int mv[64];
 };
 // Every QP's decision constants (device-resident, indexed by the per-segment slice QP of
@@ -49,9 +49,26 @@ void launch_coarse_me(const MeBuffers& me, const Geo& g, const RcTables* rc, int
 // CRF: per-segment frame QP from the lookahead complexity into qp[B]
 void launch_rc_crf(const uint8_t* q, const int* ccost, int8_t* qp, const Geo& g, int crf, bool intra, int B,
                    hipStream_t s);
-// fine motion search + P-frame reconstruction (after launch_coarse_me)
+// Intra 16x16 CUs in P pictures (tv/me_model.h pintra_*): k_inter_me lists the quadrants
+// whose inter cost passes the gate, k_pintra_analysis scores them, k_pintra_select accepts
+// and lists them per reconstruction pass, k_pintra_recon codes pass q after k_inter_recon.
+struct PIntraBuffers {
+  int* qcost;     // [B][nctu][4] best 16x16 inter cost per quadrant
+  uint8_t* cand;  // [B][nctu][4] 0x80 | mode for a candidate, else 0
+  int* count;     // [6] gated, accepted of pass 0..3, candidates (zeroed per frame)
+  int* gate;      // [B * nctu * 4] gated quadrant indices ((b * nctu + ctu) * 4 + q)
+  int* clist;     // [B * nctu * 4] candidate quadrant indices
+  int* pass;      // [4][B * nctu] accepted CTBs (b * nctu + ctu) of each pass
+};
+void launch_pintra_decide(FrameSet src, DecisionSet dec, const Geo& g, const RcTables* rc, const PIntraBuffers& pi,
+                          int B, hipStream_t s);
+void launch_pintra_recon(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, const PIntraBuffers& pi, int B,
+                         hipStream_t s);
+// fine motion search + P-frame reconstruction (after launch_coarse_me); pi: intra quadrants
+// (nullptr: inter only)
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
-                        const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s);
+                        const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s,
+                        const PIntraBuffers* pi = nullptr);
 // One list's fine-search result for a CTB of a B picture: the 21 ME blocks' cost (SAD +
 // MV rate), rate part and vector (tv::me_ctb in the golden encoder).
 struct CtbMeOut {

@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
 __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                          DecisionSet dec, const int16_t* prev_mv, const int16_t* cmv,
                                                          Geo g, const RcTables* rc, int range, int diag_stop,
-                                                         CtbMeOut* bout) {
+                                                         CtbMeOut* bout, PIntraBuffers pi) {
   const int tid = threadIdx.x;
   int ctu, b;
   xcd_ctb(ctu, b);
@@ -447,6 +447,14 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       dec.mv[2 * u + 1] = (int16_t)(whole ? bmv[20][1] : mvu[k][1]);
       dec.intra[u] = 0;
       dec.ipm[u] = 1;
+    }
+    if (pi.qcost) {  // intra-in-P: quadrants past the gate go on k_pintra_analysis' list
+      for (int q = 0; q < 4; ++q) {
+        const long qi = ((long)b * g.wc * g.hc + ctu) * 4 + q;
+        pi.qcost[qi] = bcost[16 + q];
+        pi.cand[qi] = 0;
+        if (bcost[16 + q] > kPIntraGate * 256) pi.gate[atomicAdd(&pi.count[0], 1)] = (int)qi;
+      }
     }
   }
 }
@@ -1018,15 +1026,20 @@ static int recon_tile_skip() {
 }
 
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
-                        const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s) {
+                        const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s,
+                        const PIntraBuffers* pi) {
   static const int diag_stop = [] {
     const char* e = std::getenv("TV_DIAG_ME_STOP");
     return e ? std::atoi(e) : 0;
   }();
+  const PIntraBuffers none{};
+  if (pi && hipMemsetAsync(pi->count, 0, 6 * sizeof(int), s) != hipSuccess) return;
   k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range,
-                                                         diag_stop, nullptr);
+                                                         diag_stop, nullptr, pi ? *pi : none);
+  if (pi) launch_pintra_decide(src, dec, g, rc, *pi, B, s);
   k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, recon_tile_skip(), FrameSet{},
                                                      nullptr);
+  if (pi) launch_pintra_recon(src, rec, dec, g, *pi, B, s);
 }
 
 void launch_inter_frame_b(FrameSet src, FrameSet ref0, const uint8_t* phase0, FrameSet ref1, const uint8_t* phase1,
@@ -1034,8 +1047,9 @@ void launch_inter_frame_b(FrameSet src, FrameSet ref0, const uint8_t* phase0, Fr
                           const MeBuffers& me0, const MeBuffers& me1, CtbMeOut* meout, int B, hipStream_t s) {
   const dim3 grid(g.wc * g.hc, B);
   CtbMeOut* o1 = meout + (long)B * g.wc * g.hc;
-  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref0, phase0, dec, me0.prev_mv, me0.cmv, g, rc, range[0], 0, meout);
-  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref1, phase1, dec, me1.prev_mv, me1.cmv, g, rc, range[1], 0, o1);
+  const PIntraBuffers none{};
+  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref0, phase0, dec, me0.prev_mv, me0.cmv, g, rc, range[0], 0, meout, none);
+  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref1, phase1, dec, me1.prev_mv, me1.cmv, g, rc, range[1], 0, o1, none);
   k_bi_decide<<<grid, 256, 0, s>>>(src, phase0, phase1, meout, o1, dec, g, rc);
   k_inter_recon<<<grid, 256, 0, s>>>(src, ref0, phase0, rec, dec, g, recon_tile_skip(), ref1, phase1);
 }

@@ -381,6 +381,236 @@ void launch_intra_frame(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& 
   }
 }
 
+// ----------------------- intra 16x16 CUs in P pictures (tv/me_model.h) --------------------
+// k_pintra_analysis  one wave per gated quadrant (listed by k_inter_me): the I-frame
+//                    analysis' 15-mode SATD search from SOURCE neighbours, then the SAD of
+//                    the chosen mode -> candidate byte (golden: tv::pintra_candidate).
+// k_pintra_select    per CTB: acceptance from the candidate bytes of its neighbourhood
+//                    (tv::pintra_accepted), the CTB's decisions rewritten (tv::apply_pintra),
+//                    each accepted quadrant listed for its reconstruction pass.
+// k_pintra_recon     pass q over the listed CTBs after k_inter_recon: quadrant q's 16x16 CU
+//                    with the normative intra prediction from the reconstruction and the TB
+//                    coding of k_intra_recon (one wave per component), written over the inter
+//                    result.  Acceptance guarantees every neighbour it reads is final.
+__global__ void __launch_bounds__(256) k_pintra_analysis(FrameSet src, DecisionSet dec, Geo g, const RcTables* rc,
+                                                         PIntraBuffers pi) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = pi.count[0], nctu = g.wc * g.hc;
+  if ((int)blockIdx.x * 4 >= n) return;  // workgroup-uniform: nothing gated for this block
+  __shared__ AngleLds ang;
+  __shared__ int16_t R[4][4][33];  // per wave: left, top, smoothed left, smoothed top
+  __shared__ bool av[4][2][33];
+  __shared__ int dcv[4];
+  ang.load(threadIdx.x, 256);
+  __syncthreads();
+  for (int it = blockIdx.x * 4 + w; it < n; it += gridDim.x * 4) {  // wave-uniform
+    const int qi = pi.gate[it], q = qi & 3, cb = qi >> 2, b = cb / nctu, ctu = cb - b * nctu;
+    const Penalties& pen = rc->pen[dec.qp[b]];
+    const int x = (ctu % g.wc) * 32 + (q & 1) * 16, y = (ctu / g.wc) * 32 + (q >> 1) * 16;
+    const uint8_t* S = src.plane(0, b, g);
+    int16_t* L = R[w][0];
+    int16_t* T = R[w][1];
+    if (lane == 0) {
+      const bool a = zscan_available(x, y, x - 1, y - 1, g.W, g.H);
+      av[w][0][0] = av[w][1][0] = a;
+      L[0] = T[0] = a ? S[(long)(y - 1) * g.W + x - 1] : 0;
+    } else if (lane < 33) {
+      const bool al = zscan_available(x, y, x - 1, y + lane - 1, g.W, g.H);
+      av[w][0][lane] = al;
+      L[lane] = al ? S[(long)(y + lane - 1) * g.W + x - 1] : 0;
+      const bool at = zscan_available(x, y, x + lane - 1, y - 1, g.W, g.H);
+      av[w][1][lane] = at;
+      T[lane] = at ? S[(long)(y - 1) * g.W + x + lane - 1] : 0;
+    }
+    wave_sync();
+    if (lane == 0) {
+      intra_substitute(L, T, av[w][0], av[w][1], 16);
+      dcv[w] = intra_dc_value(L, T, 4);
+    }
+    wave_sync();
+    if (lane <= 32) {  // [1 2 1] smoothed copies
+      if (lane == 0) {
+        R[w][2][0] = R[w][3][0] = (int16_t)((L[1] + 2 * L[0] + T[1] + 2) >> 2);
+      } else if (lane == 32) {
+        R[w][2][32] = L[32];
+        R[w][3][32] = T[32];
+      } else {
+        R[w][2][lane] = (int16_t)((L[lane + 1] + 2 * L[lane] + L[lane - 1] + 2) >> 2);
+        R[w][3][lane] = (int16_t)((T[lane + 1] + 2 * T[lane] + T[lane - 1] + 2) >> 2);
+      }
+    }
+    wave_sync();
+    int sv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      sv[k] = S[(long)(y + (k >> 1) * 8 + (lane >> 3)) * g.W + x + (k & 1) * 8 + (lane & 7)];
+    auto pred = [&](int mode, int k) {
+      const bool filt = intra_filter_refs(4, mode);
+      return intra_pred_pixel_ai(R[w][filt ? 2 : 0], R[w][filt ? 3 : 1], 4, mode, ang.angle[mode], ang.inv[mode], true,
+                                 dcv[w], (k & 1) * 8 + (lane & 7), (k >> 1) * 8 + (lane >> 3));
+    };
+    unsigned best = 0xffffffffu, best_ang = 0xffffffffu;
+    auto eval = [&](int mode) {
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sum += wave_satd8x8(sv[k] - pred(mode, k));
+      const unsigned v = ((unsigned)(sum + (mode <= 1 ? pen.mode_dcpl : pen.mode_ang)) << 6) | (unsigned)mode;
+      best = v < best ? v : best;
+      if (mode >= 2) best_ang = v < best_ang ? v : best_ang;
+    };
+    for (int i = 0; i < kIntraCoarseModes; ++i) eval(intra_coarse_mode(i));
+    const int ma = (int)(best_ang & 63);
+    for (int i = 0; i < 4; ++i) {
+      const int m = intra_refine_mode(ma, i);
+      if (m >= 2) eval(m);
+    }
+    const int mode = (int)(best & 63);
+    int d = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d += tv_abs(sv[k] - pred(mode, k));
+    const int sad = wave_sum(d);
+    if (lane == 0 && pintra_cost(sad, pen.pintra) < pi.qcost[qi]) {
+      pi.cand[qi] = (uint8_t)(0x80 | mode);
+      pi.clist[atomicAdd(&pi.count[5], 1)] = qi;  // k_pintra_select walks the candidates only
+    }
+    wave_sync();  // the wave's LDS is reused by its next item
+  }
+}
+
+// One thread per candidate quadrant (k_pintra_analysis' list).  The CTB-wide 32x32 -> 16x16
+// rewrite is idempotent: whichever candidate of a CTB reads its first unit still at 32x32
+// rewrites all 16 units to 16x16, and every other write sets the same values.
+__global__ void __launch_bounds__(256) k_pintra_select(DecisionSet dec, Geo g, PIntraBuffers pi, int B) {
+  const int n = pi.count[5], nctu = g.wc * g.hc;
+  for (int it = blockIdx.x * 256 + threadIdx.x; it < n; it += gridDim.x * 256) {
+    const int qi = pi.clist[it], q = qi & 3, cb = qi >> 2, b = cb / nctu, ctu = cb - b * nctu;
+    const int i = ctu % g.wc, j = ctu / g.wc;
+    const uint8_t* C = pi.cand + (long)b * nctu * 4;
+    if (!pintra_accepted(C, g.wc, g.hc, i, j, q)) continue;
+    pi.pass[q * (long)B * nctu + atomicAdd(&pi.count[1 + q], 1)] = cb;
+    const long u0 = b * g.usz + (long)(j * 4) * g.w8 + i * 4;
+    if (dec.cu_log2[u0] == 5)
+      for (int k = 0; k < 16; ++k) dec.cu_log2[u0 + (long)(k >> 2) * g.w8 + (k & 3)] = 4;
+    for (int k = 0; k < 4; ++k) {
+      const long u = u0 + (long)((q >> 1) * 2 + (k >> 1)) * g.w8 + (q & 1) * 2 + (k & 1);
+      dec.cu_log2[u] = 4;
+      dec.intra[u] = 1;
+      dec.ipm[u] = (uint8_t)(C[(long)ctu * 4 + q] & 63);
+      dec.mv[2 * u] = dec.mv[2 * u + 1] = 0;
+    }
+  }
+}
+
+struct PIntraLds {
+  uint8_t pred[256];
+  int16_t resid[256];
+  int V[65];
+  int L[33], T[33], FL[33], FT[33];
+  WaveTbScratch tb;
+};
+
+__global__ void __launch_bounds__(192) k_pintra_recon(FrameSet src, FrameSet rec, DecisionSet dec, Geo g,
+                                                      PIntraBuffers pi, int q, int B) {
+  const int c = threadIdx.x >> 6, lane = threadIdx.x & 63, nctu = g.wc * g.hc;
+  const int n = pi.count[1 + q];
+  if ((int)blockIdx.x >= n) return;  // workgroup-uniform
+  __shared__ int Tm[32][33];
+  __shared__ AngleLds ang;
+  __shared__ PIntraLds W[3];
+  __shared__ unsigned cbfs;
+  tb_load_matrix(Tm);
+  ang.load(threadIdx.x, 192);
+  __syncthreads();
+  PIntraLds& L = W[c];
+  const int sh = c ? 1 : 0, l2 = 4 - sh, N = 1 << l2, total = 4 * N + 1;
+  const int pw = g.W >> sh;
+  for (int it = blockIdx.x; it < n; it += gridDim.x) {  // workgroup-uniform
+    const int cb = pi.pass[(long)q * B * nctu + it], b = cb / nctu, ctu = cb - b * nctu;
+    const int x0 = (ctu % g.wc) * 32 + (q & 1) * 16, y0 = (ctu / g.wc) * 32 + (q >> 1) * 16;
+    const int mode = pi.cand[(long)cb * 4 + q] & 63, qp = dec.qp[b];
+    const int x = x0 >> sh, y = y0 >> sh;
+    const uint8_t* Sp = src.plane(c, b, g);
+    uint8_t* Rp = rec.plane(c, b, g);
+    if (threadIdx.x == 0) cbfs = 0;
+    // reference samples in canonical order (bottom-left .. corner .. top-right), final
+    // reconstruction read straight from the plane
+    unsigned long long m[2] = {0, 0};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = lane + 64 * r;
+      bool a = false;
+      if (i < total) {
+        const int xn = i < 2 * N ? x - 1 : x - 1 + (i - 2 * N), yn = i < 2 * N ? y + 2 * N - 1 - i : y - 1;
+        a = zscan_available(x0, y0, xn << sh, yn << sh, g.W, g.H);
+        L.V[i] = a ? Rp[(long)yn * pw + xn] : 0;
+      }
+      m[r] = __ballot(a);
+    }
+    wave_sync();
+    for (int i = lane; i < total; i += 64) {  // substitution (H.265 8.4.4.2.2): nearest available below
+      int jj = -1;
+      for (int wv = i >> 6; wv >= 0 && jj < 0; --wv) {
+        const unsigned long long mm =
+            (wv == (i >> 6)) ? (m[wv] & (((i & 63) == 63) ? ~0ull : ((2ull << (i & 63)) - 1))) : m[wv];
+        if (mm) jj = wv * 64 + 63 - __clzll(mm);
+      }
+      if (jj < 0)
+        for (int wv = 0; wv < 2 && jj < 0; ++wv)
+          if (m[wv]) jj = wv * 64 + __ffsll(m[wv]) - 1;
+      const int v = jj < 0 ? 128 : L.V[jj];
+      if (i < 2 * N) L.L[2 * N - i] = v;
+      else if (i == 2 * N) L.L[0] = L.T[0] = v;
+      else L.T[i - 2 * N] = v;
+    }
+    wave_sync();
+    const bool filt = c == 0 && intra_filter_refs(l2, mode);
+    if (filt) {
+      for (int i = lane; i <= 2 * N; i += 64) {
+        if (i == 0) {
+          L.FL[0] = L.FT[0] = (L.L[1] + 2 * L.L[0] + L.T[1] + 2) >> 2;
+        } else if (i == 2 * N) {
+          L.FL[i] = L.L[i];
+          L.FT[i] = L.T[i];
+        } else {
+          L.FL[i] = (L.L[i + 1] + 2 * L.L[i] + L.L[i - 1] + 2) >> 2;
+          L.FT[i] = (L.T[i + 1] + 2 * L.T[i] + L.T[i - 1] + 2) >> 2;
+        }
+      }
+      wave_sync();
+    }
+    const int* RL = filt ? L.FL : L.L;
+    const int* RT = filt ? L.FT : L.T;
+    const int dc = mode == 1 ? intra_dc_value(RL, RT, l2) : 0;
+    for (int i = lane; i < N * N; i += 64) {
+      const int px = i & (N - 1), py = i >> l2;
+      const int p = intra_pred_pixel_ai(RL, RT, l2, mode, (int)ang.angle[mode], (int)ang.inv[mode], c == 0, dc, px, py);
+      L.pred[i] = (uint8_t)p;
+      L.resid[i] = (int16_t)((int)Sp[(long)(y + py) * pw + x + px] - p);
+    }
+    wave_sync();
+    int16_t* coefp = (c == 0 ? dec.coef_y + b * g.ysz : (c == 1 ? dec.coef_u : dec.coef_v) + b * g.csz);
+    const int cbit = wave_code_tb(L.resid, L.pred, l2, c ? chroma_qp(qp, 0) : qp, true, coefp + (long)y * pw + x, pw,
+                                  Rp + (long)y * pw + x, pw, Tm, L.tb);
+    if (lane == 0 && cbit) atomicOr(&cbfs, 1u << c);
+    __syncthreads();
+    if (threadIdx.x < 4)
+      dec.cbf[b * g.usz + (long)((y0 >> 3) + (threadIdx.x >> 1)) * g.w8 + (x0 >> 3) + (threadIdx.x & 1)] = (uint8_t)cbfs;
+    __syncthreads();  // cbfs and the LDS are reused by the next item
+  }
+}
+
+void launch_pintra_decide(FrameSet src, DecisionSet dec, const Geo& g, const RcTables* rc, const PIntraBuffers& pi,
+                          int B, hipStream_t s) {
+  // list-driven: a fixed grid walks the gated quadrants (the count is on the device)
+  k_pintra_analysis<<<512, 256, 0, s>>>(src, dec, g, rc, pi);
+  k_pintra_select<<<64, 256, 0, s>>>(dec, g, pi, B);
+}
+
+void launch_pintra_recon(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, const PIntraBuffers& pi, int B,
+                         hipStream_t s) {
+  for (int q = 0; q < 4; ++q) k_pintra_recon<<<512, 192, 0, s>>>(src, rec, dec, g, pi, q, B);
+}
+
 bool intra_timing() {
   static const bool on = [] {
     const char* e = std::getenv("TV_DIAG_INTRA");

@@ -18,6 +18,8 @@ void coarse_search(const uint8_t* qcur, const uint8_t* qprev, int W, int H, int 
                    int16_t* cmv, int* ccost);
 void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, const int16_t* cmv,
                    const int16_t* prev_mv, int range, FrameDecisions& fd);
+// intra quadrants of a P picture: cand = [hc][wc][4] candidate bytes (tv/me_model.h pintra_*)
+void apply_pintra(const uint8_t* cand, int wc, int hc, FrameDecisions& fd);
 // B pictures (tv/gop.h): both lists' searches, then per block the best of list 0, list 1
 // and their 8-bit average (bi-prediction), then the same CU split.
 void analyze_inter_b(const SeqConfig& cfg, const Picture& src, const Picture& ref0, const Picture& ref1,

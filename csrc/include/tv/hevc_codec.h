@@ -15,6 +15,7 @@
 //               luma stride = coded_w, chroma stride = coded_w/2)
 #pragma once
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -39,6 +40,15 @@ struct SeqConfig {
   // DPB size / reorder depth the parameter sets announce for it
   int mgop = 1;
   int dpb_size = 2, num_reorder = 0;
+  // intra 16x16 CUs in P pictures (tv/me_model.h, pintra_*): on unless TV_PINTRA=0
+  bool pintra = pintra_default();
+  static bool pintra_default() {
+    static const bool on = [] {
+      const char* e = std::getenv("TV_PINTRA");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   int fps_num = 30, fps_den = 1;
   void finalize() {
     coded_w = (width + kCtb - 1) / kCtb * kCtb;

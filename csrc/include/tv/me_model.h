@@ -116,4 +116,51 @@ TV_HD int intra_refine_mode(int m, int i) {
   return (r >= 2 && r <= 34) ? r : -1;
 }
 
+// ---- intra CUs in P pictures (CPU == GPU) -----------------------------------------------
+// Unit of decision: the four 16x16 quadrants q (z-order) of a 32x32 CTB.  A quadrant whose
+// best 16x16 inter cost (SAD + MV rate, after sub-pel refinement) exceeds kPIntraGate per
+// sample is evaluated for intra: the 15-mode SATD search of the I-frame analysis on SOURCE
+// neighbours picks the mode, and it becomes a candidate when that mode's SAD + pintra
+// penalty beats the inter cost (a 16x16 intra CU, 2Nx2N, chroma DM).
+//
+// Reconstruction is four passes, pass q coding quadrant q of every CTB in parallel after the
+// inter reconstruction.  Intra prediction reads the reconstructed left / above / above-right
+// / below-left / corner neighbours that are available in z-scan order; a candidate is
+// accepted only if none of those neighbours is an accepted intra quadrant of a LATER pass
+// (which would not be reconstructed yet).  For quadrant q of CTB (i, j) those are:
+//   q = 3: none;   q = 2: quadrant 3 of (i-1, j);
+//   q = 1: quadrant 3 of (i, j-1), quadrant 2 of (i, j-1) and (i+1, j-1);
+//   q = 0: quadrant 1 and 3 of (i-1, j), 3 of (i-1, j-1), 2 and 3 of (i, j-1).
+// Deciding 3 -> 2 -> 1 -> 0 makes acceptance a pure function of the candidate flags of a
+// 3 x 2 CTB neighbourhood (no sequential pass over the picture).
+constexpr int kPIntraGate = 6;  // mean inter SAD per sample before intra is tried
+// intra cost against the inter SAD + MV rate: SAD * 5/4 (intra residuals cost more bits per
+// unit of SAD) + lambda * kPIntraPenBits (mode, CU overhead).  Tuned on the golden encoder
+// (tests/test_pintra.py clip, QP 30): a scene cut coded as P -3.9 % bytes at +0.13 dB Y-PSNR,
+// panning content neutral; gate 6 instead of 4 gives up 0.2 % of that for fewer searches.
+constexpr int kPIntraPenBits = 16;
+TV_HD int pintra_cost(int sad, int pen) { return sad * 5 / 4 + pen; }
+// cand: the frame's [hc][wc][4] quadrant bytes (0x80 | mode for a candidate, else 0)
+TV_HD bool pintra_c(const uint8_t* cand, int wc, int hc, int i, int j, int q) {
+  return i >= 0 && j >= 0 && i < wc && j < hc && (cand[((long)j * wc + i) * 4 + q] & 0x80);
+}
+TV_HD bool pintra_acc2(const uint8_t* c, int wc, int hc, int i, int j) {
+  return pintra_c(c, wc, hc, i, j, 2) && !pintra_c(c, wc, hc, i - 1, j, 3);
+}
+TV_HD bool pintra_acc1(const uint8_t* c, int wc, int hc, int i, int j) {
+  return pintra_c(c, wc, hc, i, j, 1) && !pintra_c(c, wc, hc, i, j - 1, 3) && !pintra_acc2(c, wc, hc, i, j - 1) &&
+         !pintra_acc2(c, wc, hc, i + 1, j - 1);
+}
+TV_HD bool pintra_accepted(const uint8_t* c, int wc, int hc, int i, int j, int q) {
+  switch (q) {
+    case 3: return pintra_c(c, wc, hc, i, j, 3);
+    case 2: return pintra_acc2(c, wc, hc, i, j);
+    case 1: return pintra_acc1(c, wc, hc, i, j);
+    default:
+      return pintra_c(c, wc, hc, i, j, 0) && !pintra_acc1(c, wc, hc, i - 1, j) && !pintra_c(c, wc, hc, i - 1, j, 3) &&
+             !pintra_c(c, wc, hc, i - 1, j - 1, 3) && !pintra_acc2(c, wc, hc, i, j - 1) &&
+             !pintra_c(c, wc, hc, i, j - 1, 3);
+  }
+}
+
 }  // namespace tv
