@@ -316,12 +316,17 @@ void split_ctb(const int* bcost, int pen_split, int sel[16], uint8_t l2[16]) {
 static uint8_t pintra_candidate(const Picture& src, int W, double lam, int x, int y, int inter_cost) {
   if (inter_cost <= kPIntraGate * 256) return 0;
   int pred[16 * 16];
+  auto sad_of = [&]() {
+    int s = 0;
+    for (int j = 0; j < 16; ++j)
+      for (int i = 0; i < 16; ++i) s += tv_abs((int)src.y[(size_t)(y + j) * W + x + i] - pred[j * 16 + i]);
+    return s;
+  };
+  predict_intra_tb(src, 0, x, y, 4, 1, pred);  // DC first: hopeless quadrants skip the search
+  if (!pintra_worth_search(sad_of(), (int)(lam * kPIntraPenBits), inter_cost)) return 0;
   const IntraBest ib = intra_best_mode(src, W, lam, x, y, 4, pred);
   predict_intra_tb(src, 0, x, y, 4, ib.mode, pred);
-  int sad = 0;
-  for (int j = 0; j < 16; ++j)
-    for (int i = 0; i < 16; ++i) sad += tv_abs((int)src.y[(size_t)(y + j) * W + x + i] - pred[j * 16 + i]);
-  return pintra_cost(sad, (int)(lam * kPIntraPenBits)) < inter_cost ? (uint8_t)(0x80 | ib.mode) : (uint8_t)0;
+  return pintra_cost(sad_of(), (int)(lam * kPIntraPenBits)) < inter_cost ? (uint8_t)(0x80 | ib.mode) : (uint8_t)0;
 }
 
 void analyze_inter(const SeqConfig& cfg, const Picture& src, const Picture& ref, const int16_t* cmv,

@@ -410,6 +410,7 @@ __global__ void __launch_bounds__(256) k_pintra_analysis(FrameSet src, DecisionS
     const uint8_t* S = src.plane(0, b, g);
     int16_t* L = R[w][0];
     int16_t* T = R[w][1];
+    wave_sync();  // the previous item's reads of this wave's LDS are done
     if (lane == 0) {
       const bool a = zscan_available(x, y, x - 1, y - 1, g.W, g.H);
       av[w][0][0] = av[w][1][0] = a;
@@ -449,6 +450,10 @@ __global__ void __launch_bounds__(256) k_pintra_analysis(FrameSet src, DecisionS
       return intra_pred_pixel_ai(R[w][filt ? 2 : 0], R[w][filt ? 3 : 1], 4, mode, ang.angle[mode], ang.inv[mode], true,
                                  dcv[w], (k & 1) * 8 + (lane & 7), (k >> 1) * 8 + (lane >> 3));
     };
+    int d0 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d0 += tv_abs(sv[k] - pred(1, k));
+    if (!pintra_worth_search(wave_sum(d0), pen.pintra, pi.qcost[qi])) continue;  // wave-uniform
     unsigned best = 0xffffffffu, best_ang = 0xffffffffu;
     auto eval = [&](int mode) {
       int sum = 0;
@@ -473,7 +478,6 @@ __global__ void __launch_bounds__(256) k_pintra_analysis(FrameSet src, DecisionS
       pi.cand[qi] = (uint8_t)(0x80 | mode);
       pi.clist[atomicAdd(&pi.count[5], 1)] = qi;  // k_pintra_select walks the candidates only
     }
-    wave_sync();  // the wave's LDS is reused by its next item
   }
 }
 
@@ -608,7 +612,7 @@ void launch_pintra_decide(FrameSet src, DecisionSet dec, const Geo& g, const RcT
 
 void launch_pintra_recon(FrameSet src, FrameSet rec, DecisionSet dec, const Geo& g, const PIntraBuffers& pi, int B,
                          hipStream_t s) {
-  for (int q = 0; q < 4; ++q) k_pintra_recon<<<512, 192, 0, s>>>(src, rec, dec, g, pi, q, B);
+  for (int q = 0; q < 4; ++q) k_pintra_recon<<<128, 192, 0, s>>>(src, rec, dec, g, pi, q, B);
 }
 
 bool intra_timing() {

@@ -140,6 +140,9 @@ constexpr int kPIntraGate = 6;  // mean inter SAD per sample before intra is tri
 // panning content neutral; gate 6 instead of 4 gives up 0.2 % of that for fewer searches.
 constexpr int kPIntraPenBits = 16;
 TV_HD int pintra_cost(int sad, int pen) { return sad * 5 / 4 + pen; }
+// the 15-mode search runs only when the DC prediction's cost is within 2x of the inter cost
+// (textured / fast-moving quadrants past the gate stop after one prediction)
+TV_HD bool pintra_worth_search(int sad_dc, int pen, int inter_cost) { return pintra_cost(sad_dc, pen) < 2 * inter_cost; }
 // cand: the frame's [hc][wc][4] quadrant bytes (0x80 | mode for a candidate, else 0)
 TV_HD bool pintra_c(const uint8_t* cand, int wc, int hc, int i, int j, int q) {
   return i >= 0 && j >= 0 && i < wc && j < hc && (cand[((long)j * wc + i) * 4 + q] & 0x80);
