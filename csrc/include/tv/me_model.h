@@ -70,7 +70,7 @@ TV_HD int me_candidates(const int16_t* cmv, int wc, int hc, int cxi, int cyi, in
   for (int i = 0; i < n; ++i) {
     const int x = clip3(-lim, lim, raw[i][0]), y = clip3(-lim, lim, raw[i][1]);
     bool dup = false;
-    for (int j = 0; j < m; ++j) dup = dup || (cand[j][0] == x && cand[j][1] == y);
+    for (int j = 0; j < m; ++j) dup = dup || (tv_abs(cand[j][0] - x) <= 3 && tv_abs(cand[j][1] - y) <= 2);
     if (dup) continue;
     cand[m][0] = x;
     cand[m][1] = y;
