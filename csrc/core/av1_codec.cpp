@@ -1881,23 +1881,27 @@ GoldenOut golden_encode(const SeqGeo& g, const std::vector<Planes>& src, int qid
         uint32_t mvw = 0;
         if (fd.fp.key) {
           int best = 1 << 30;
-          for (int k = 0; k < ((dbg & 8) ? 1 : kNumIntraCand); ++k) {
-            const uint32_t m = pack_mode(0, intra_cand(k), 0, 0, 0);
+          // TV_AV1_DBG bit 32: the search also tries D113 / D135 / D157 (conformance tests of
+          // the directional predictor; the shipped search leaves them out, av1_enc.h)
+          const int ncand = (dbg & 8) ? 1 : kNumIntraCand + ((dbg & 32) ? 3 : 0);
+          auto cand = [](int k) { return k < kNumIntraCand ? intra_cand(k) : D135_PRED + (k - kNumIntraCand); };
+          for (int k = 0; k < ncand; ++k) {
+            const uint32_t m = pack_mode(0, cand(k), 0, 0, 0);
             int pr[256];
             predict(g, 0, bx, by, m, 0, rec, nullptr, pr);
-            const int cost = satd_block(s[0], pr, 16) + ((lam * intra_mode_bits16(intra_cand(k))) >> 8);
-            if (cost < best) best = cost, ym = intra_cand(k), std::memcpy(pred[0], pr, sizeof(pr));
+            const int cost = satd_block(s[0], pr, 16) + ((lam * intra_mode_bits16(cand(k))) >> 8);
+            if (cost < best) best = cost, ym = cand(k), std::memcpy(pred[0], pr, sizeof(pr));
           }
           best = 1 << 30;
-          for (int k = 0; k < ((dbg & 8) ? 1 : kNumIntraCand); ++k) {
-            const uint32_t m = pack_mode(0, 0, intra_cand(k), 0, 0);
+          for (int k = 0; k < ncand; ++k) {
+            const uint32_t m = pack_mode(0, 0, cand(k), 0, 0);
             int pu[64], pv[64];
             predict(g, 1, bx, by, m, 0, rec, nullptr, pu);
             predict(g, 2, bx, by, m, 0, rec, nullptr, pv);
             const int cost = satd_block(s[1], pu, 8) + satd_block(s[2], pv, 8) +
-                             ((lam * intra_mode_bits16(intra_cand(k))) >> 8);
+                             ((lam * intra_mode_bits16(cand(k))) >> 8);
             if (cost < best) {
-              best = cost, uvm = intra_cand(k);
+              best = cost, uvm = cand(k);
               std::memcpy(pred[1], pu, sizeof(pu));
               std::memcpy(pred[2], pv, sizeof(pv));
             }

@@ -717,7 +717,7 @@ __global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, ui
   __shared__ EdgeLds E[2];
   __shared__ uint8_t sblk[256];
   __shared__ uint8_t sc[2][64];
-  __shared__ int cost[8];
+  __shared__ int cost[16];
   __shared__ int16_t res[256], ta[256], tb[256];
   __shared__ int32_t ti[256];
   __shared__ int predc[256];
@@ -731,9 +731,9 @@ __global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, ui
   sc[0][lane] = (src.u + b * csz)[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)];
   sc[1][lane] = (src.v + b * csz)[(long)(cy0 + (lane >> 3)) * Wc + cx0 + (lane & 7)];
   load_edges(RY, W, x0, y0, 16, E[0]);
-  // ---- luma: 7 candidates, 4 per pass (16 lanes = 16 4x4 SATDs each)
+  // ---- luma: kNumIntraCand candidates, 4 per pass (16 lanes = 16 4x4 SATDs each)
   const int grp = lane >> 4, b4 = lane & 15, px = (b4 & 3) * 4, py = (b4 >> 2) * 4;
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int pass = 0; pass < (kNumIntraCand + 3) / 4; ++pass) {
     const int ci = pass * 4 + grp;
     const int m = intra_cand(ci < kNumIntraCand ? ci : 0);
     int d[16];
@@ -765,13 +765,13 @@ __global__ void __launch_bounds__(64) k_av1e_intra(Planes3 src, Planes3W rec, ui
   for (int i = lane; i < 256; i += 64)
     RY[(long)(y0 + (i >> 4)) * W + x0 + (i & 15)] = (uint8_t)clip_pixel(predc[i] + res[i]);
   __syncthreads();
-  // ---- chroma: 7 candidates x 8 lanes (U: 4 blocks, V: 4 blocks) in one pass
+  // ---- chroma: kNumIntraCand candidates x 8 lanes (U: 4 blocks, V: 4 blocks), 8 per pass
   uint8_t* RU = rec.u + b * csz;
   uint8_t* RV = rec.v + b * csz;
   load_edges(RU, Wc, cx0, cy0, 8, E[0]);
   load_edges(RV, Wc, cx0, cy0, 8, E[1]);
-  {
-    const int ci = lane >> 3, q = lane & 7, pl = q >> 2, qb = q & 3, qx = (qb & 1) * 4, qy = (qb >> 1) * 4;
+  for (int pass = 0; pass < (kNumIntraCand + 7) / 8; ++pass) {
+    const int ci = pass * 8 + (lane >> 3), q = lane & 7, pl = q >> 2, qb = q & 3, qx = (qb & 1) * 4, qy = (qb >> 1) * 4;
     const int m = intra_cand(ci < kNumIntraCand ? ci : 0);
     int d[16];
 #pragma unroll

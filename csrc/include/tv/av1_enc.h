@@ -7,9 +7,10 @@
 //   * 64x64 superblocks, coded size padded to a multiple of 16 (render_size = display size);
 //     every superblock splits to 16x16 coding blocks (PARTITION_SPLIT / split_or_* at edges);
 //   * TX_MODE_LARGEST: one 16x16 luma and two 8x8 chroma transforms per block, reduced_tx_set;
-//   * key frames: intra modes DC / V / H / SMOOTH / SMOOTH_V / SMOOTH_H / PAETH (the seven
-//     modes that read no above-right samples: the I-frame wavefront is a plain diagonal);
-//     intra edge filter / filter intra / CfL / palette off;
+//   * key frames: intra modes DC / V / H / SMOOTH / SMOOTH_V / SMOOTH_H / PAETH searched (D113 /
+//     D135 / D157 predicted and decodable too); all read no above-right / below-left samples,
+//     so the I-frame wavefront is a plain diagonal; angle delta 0; intra edge filter / filter
+//     intra / CfL / palette off;
 //   * inter frames: one reference (LAST = previous frame), quarter-pel motion, EIGHTTAP
 //     (regular) filters; the NEWMV / NEARESTMV / NEARMV / GLOBALMV choice is made by the
 //     syntax writer from the spatial MV stack (the mode does not change the reconstruction);
@@ -33,10 +34,15 @@ constexpr int kSb = 64;    // superblock
 constexpr int kMaxPresets = 8;
 
 // intra modes (AV1 numbering)
-enum : int { DC_PRED = 0, V_PRED = 1, H_PRED = 2, SMOOTH_PRED = 9, SMOOTH_V_PRED = 10, SMOOTH_H_PRED = 11,
-             PAETH_PRED = 12 };
+enum : int { DC_PRED = 0, V_PRED = 1, H_PRED = 2, D135_PRED = 4, D113_PRED = 5, D157_PRED = 6, SMOOTH_PRED = 9,
+             SMOOTH_V_PRED = 10, SMOOTH_H_PRED = 11, PAETH_PRED = 12 };
 // inter modes (YModes of inter blocks)
 enum : int { NEARESTMV = 13, NEARMV = 14, GLOBALMV = 15, NEWMV = 16 };
+// Mode search candidates.  D113 / D135 / D157 are predicted exactly (intra_dir_px; dav1d
+// decodes them bit-exactly) but the SATD-driven search picked them where they cost more than
+// they saved: key-frame-only clips at QP 27 +1.0 % bytes at -0.09 dB even with a 10-bit mode
+// penalty (profiles/README.md, round 4), so the search keeps the seven non-directional-delta
+// modes until it gets a rate-aware decision.
 constexpr int kNumIntraCand = 7;
 TV_HD int intra_cand(int i) {
   constexpr int8_t m[kNumIntraCand] = {DC_PRED, V_PRED, H_PRED, SMOOTH_PRED, SMOOTH_V_PRED, SMOOTH_H_PRED, PAETH_PRED};
@@ -47,9 +53,9 @@ TV_HD int intra_cand(int i) {
 // (column) type in bit 0, horizontal (row) type in bit 1.
 TV_HD int uv_txtype(int uv_mode) {
   switch (uv_mode) {
-    case V_PRED: case SMOOTH_V_PRED: return 1;              // ADST_DCT
-    case H_PRED: case SMOOTH_H_PRED: return 2;              // DCT_ADST
-    case SMOOTH_PRED: case PAETH_PRED: return 3;            // ADST_ADST
+    case V_PRED: case D113_PRED: case SMOOTH_V_PRED: return 1;      // ADST_DCT
+    case H_PRED: case D157_PRED: case SMOOTH_H_PRED: return 2;      // DCT_ADST
+    case D135_PRED: case SMOOTH_PRED: case PAETH_PRED: return 3;    // ADST_ADST
     default: return 0;                                      // DCT_DCT
   }
 }
@@ -153,9 +159,32 @@ TV_HD int intra_dc(const IntraEdge& e, int N) {
   return 128;
 }
 
+// Directional prediction for 90 < pAngle < 180 (7.11.2.4; no edge filter, no upsampling):
+// the above row at x = j - (i + 1) * dx / 64 while that lands at or right of the corner
+// (index -1 = top-left), else the left column at y = i - (j + 1) * dy / 64; linear
+// interpolation in 1/32 steps.  dx = Dr_Intra_Derivative[180 - pAngle], dy = [pAngle - 90].
+// Every read is inside above[-1 .. N-1] / left[-1 .. N-1]: no above-right, no below-left.
+TV_HD int intra_dir_px(const IntraEdge& e, int i, int j, int dx, int dy) {
+  int idx = (j << 6) - (i + 1) * dx;
+  int base = idx >> 6;
+  if (base >= -1) {
+    const int shift = (idx >> 1) & 0x1f;
+    const int a0 = base < 0 ? e.tl : e.above[base], a1 = e.above[base + 1];
+    return (a0 * (32 - shift) + a1 * shift + 16) >> 5;
+  }
+  idx = (i << 6) - (j + 1) * dy;
+  base = idx >> 6;
+  const int shift = (idx >> 1) & 0x1f;
+  const int l0 = base < 0 ? e.tl : e.left[base], l1 = e.left[base + 1];
+  return (l0 * (32 - shift) + l1 * shift + 16) >> 5;
+}
+
 // predicted sample (row i, col j); dc = intra_dc(e, N) precomputed for DC_PRED
 TV_HD int intra_pred_px(int mode, const IntraEdge& e, int N, int i, int j, int dc) {
   switch (mode) {
+    case D113_PRED: return intra_dir_px(e, i, j, 27, 151);  // Dr_Intra_Derivative[67], [23]
+    case D135_PRED: return intra_dir_px(e, i, j, 64, 64);   // [45], [45]
+    case D157_PRED: return intra_dir_px(e, i, j, 151, 27);  // [23], [67]
     case V_PRED: return e.above[j];
     case H_PRED: return e.left[i];
     case SMOOTH_PRED: {

@@ -118,3 +118,18 @@ def test_gpu_engine_stream_decodes_exactly_1080p():
     eng.close()
     stream = b"".join(tus)
     _check(stream, [len(t) for t in tus], recon, w, h)
+
+
+def test_directional_intra_decodes_exactly(monkeypatch):
+    """D135 / D113 / D157 (7.11.2.4 without the edge filter, av1_enc.h intra_dir_px): with the
+    search widened to them (TV_AV1_DBG bit 32) key frames use them and dav1d reproduces the
+    encoder's reconstruction bit for bit, luma and chroma."""
+    monkeypatch.setenv("TV_AV1_DBG", "32")
+    w, h = 200, 120
+    fr = _frames(1, w, h, 2) + _frames(1 | (1 << 31), w, h, 1, t0=5)
+    for f in (fr[:2], fr[2:]):
+        r = av1.golden_encode(f, w, h, 100)
+        ym = (np.asarray(r.mode[0]).astype(np.uint32) >> 1) & 15
+        uvm = (np.asarray(r.mode[0]).astype(np.uint32) >> 5) & 15
+        assert np.isin(ym, (4, 5, 6)).sum() > 0 and np.isin(uvm, (4, 5, 6)).sum() > 0
+        _check(r.stream, r.tu_sizes, r.recon, w, h)
