@@ -1,6 +1,6 @@
 // Micro-benchmark of the CABAC slice writer on CPU-encoder decisions (1080p synthetic).
 //   g++ -O2 -std=c++17 -Icsrc/include tools/native/bench_cabac.cpp -Lthinvids_amd/_lib -ltvcore -o /tmp/bench_cabac
-//   /tmp/bench_cabac [qp] [reps] [compact: 1 = the GPU engine's compact level layout]
+//   /tmp/bench_cabac [qp] [reps] [compact: 1 = the GPU engine's compact level layout] [textured: 1]
 #include <chrono>
 #include <cstdio>
 #include <vector>
@@ -25,7 +25,7 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> out;
   for (int t = 0; t < 3; ++t) {
     SynthFrameCtx ctx;
-    synth_frame_ctx(1, t, W, H, ctx);
+    synth_frame_ctx(argc > 4 && atoi(argv[4]) ? 1u | kSynthTextured : 1u, t, W, H, ctx);
     for (int c = 0; c < 3; ++c) {
       const int w = c ? W / 2 : W, h = c ? H / 2 : H;
       for (int j = 0; j < h; ++j)
