@@ -171,6 +171,7 @@ int tv_reconstruct_frame(int width, int height, int qp, int deblock, const uint8
     cfg.height = height;
     cfg.qp = qp;
     cfg.deblock = deblock != 0;
+    cfg.rqt = false;  // no transform splits (tv_write_frame codes every split flag as 0)
     cfg.finalize();
     const int W = cfg.coded_w, H = cfg.coded_h;
     Picture src, ref, rec;
@@ -214,7 +215,7 @@ int tv_write_frame(int width, int height, int qp, int deblock, int max_merge, in
     cfg.qp = qp;
     cfg.deblock = deblock != 0;
     cfg.max_merge_cand = max_merge;
-    cfg.finalize();
+    cfg.finalize();  // no tu plane: inter CUs code split_transform_flag 0
     FrameData f;
     f.w8 = cfg.w8();
     f.h8 = cfg.h8();

@@ -467,8 +467,10 @@ void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* 
                        FrameDecisions& fd, Picture& rec, const Picture* ref1) {
   const int W = cfg.coded_w, Wc = W >> 1, qp = cfg.qp, qpc = chroma_qp(qp, 0);
   int pred[32 * 32], resid[32 * 32];
-  // walk CUs in z-order per CTU (needed for intra; harmless for inter)
-  auto do_cu = [&](int x0, int y0, int log2) {
+  // walk CUs in z-order per CTU (needed for intra; harmless for inter).  code_tbs codes the
+  // CU's TBs at (x0, y0) of size 2^log2 (a whole CU, or one 16x16 quadrant of an RQT-split CU:
+  // inter prediction is per sample, so a quadrant predicts exactly like its CU).
+  auto code_tbs = [&](int x0, int y0, int log2) {
     const int u = (y0 >> 3) * fd.w8 + (x0 >> 3);
     const bool intra = fd.intra[u] != 0;
     const int N = 1 << log2;
@@ -493,6 +495,22 @@ void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* 
     }
     for (int j = 0; j < (N >> 3); ++j)
       for (int i = 0; i < (N >> 3); ++i) fd.cbf[u + j * fd.w8 + i] = (uint8_t)cbf;
+  };
+  auto do_cu = [&](int x0, int y0, int log2) {
+    const int u = (y0 >> 3) * fd.w8 + (x0 >> 3);
+    if (cfg.rqt && !ref1 && log2 == 5 && !fd.intra[u]) {  // RQT decision (hevc_defs.h rqt_split)
+      predict_inter_block(*ref, 0, x0, y0, 32, 32, fd.mv[2 * u], fd.mv[2 * u + 1], pred);
+      int sad4[4] = {0, 0, 0, 0};
+      for (int j = 0; j < 32; ++j)
+        for (int i = 0; i < 32; ++i)
+          sad4[(j >> 4) * 2 + (i >> 4)] += tv_abs((int)src.y[(size_t)(y0 + j) * W + x0 + i] - pred[j * 32 + i]);
+      if (rqt_split(sad4)) {
+        for (int q = 0; q < 4; ++q) code_tbs(x0 + (q & 1) * 16, y0 + (q >> 1) * 16, 4);
+        for (int k = 0; k < 16; ++k) fd.tu[u + (k >> 2) * fd.w8 + (k & 3)] = 1;
+        return;
+      }
+    }
+    code_tbs(x0, y0, log2);
   };
   for (int cy = 0; cy < cfg.coded_h; cy += 32)
     for (int cx = 0; cx < W; cx += 32) {

@@ -25,6 +25,7 @@ struct Sps {
   int width = 0, height = 0, coded_w = 0, coded_h = 0;
   int conf[4] = {0, 0, 0, 0};
   int log2_poc_lsb = 8;
+  int depth_inter = 0;  // max_transform_hierarchy_depth_inter (0 or 1)
   bool sao = false;
   bool valid = false;
 };
@@ -78,8 +79,9 @@ Sps parse_sps(BitReader& br) {
   const int max_tb = min_tb + (int)br.ue();
   const int dinter = (int)br.ue(), dintra = (int)br.ue();
   if (min_cb != kMinCbLog2 || ctb != kCtbLog2 || min_tb != kMinTbLog2 || max_tb != kMaxTbLog2 ||
-      dinter != 0 || dintra != 0)
+      dinter > 1 || dintra != 0)
     fail("unsupported block-size configuration");
+  s.depth_inter = dinter;
   if (br.u(1)) fail("scaling lists unsupported");
   if (br.u(1)) fail("AMP unsupported");
   s.sao = br.u(1) != 0;
@@ -247,6 +249,7 @@ class SliceDecoder {
         fd_->mv[2 * u] = (int16_t)mv.x;
         fd_->mv[2 * u + 1] = (int16_t)mv.y;
         fd_->cbf[u] = (uint8_t)cbf;
+        fd_->tu[u] = 0;
         skip_[u] = (uint8_t)skip;
         decoded_[u] = 1;
       }
@@ -316,8 +319,22 @@ class SliceDecoder {
     fill_motion(x0, y0, log2, m);
     int cbf = 0;
     if (has_res) cbf = transform_tree(x0, y0, log2, false, 0);
-    fill(x0, y0, log2, 0, 1, m.mv[0], cbf, skip ? 1 : 0);
-    recon_motion(x0, y0, log2, m, cbf);
+    fill(x0, y0, log2, 0, 1, m.mv[0], cbf & 7, skip ? 1 : 0);
+    set_split_cbf(x0, y0, cbf);
+    if (cbf >> 12) {
+      for (int q = 0; q < 4; ++q) recon_motion(x0 + (q & 1) * 16, y0 + (q >> 1) * 16, 4, m, (cbf >> (3 * q)) & 7);
+    } else {
+      recon_motion(x0, y0, log2, m, cbf);
+    }
+  }
+  // an RQT-split CU (transform_tree result bit 12): per-unit cbf of its 16x16 TB, tu = 1
+  void set_split_cbf(int x0, int y0, int res) {
+    if (!(res >> 12)) return;
+    for (int k = 0; k < 16; ++k) {
+      const int u = unit(x0 + 8 * (k & 3), y0 + 8 * (k >> 2)), q = ((k >> 3) << 1) | ((k >> 1) & 1);
+      fd_->cbf[u] = (uint8_t)((res >> (3 * q)) & 7);
+      fd_->tu[u] = 1;
+    }
   }
   void recon_motion(int x0, int y0, int log2, const Motion& m, int cbf) {
     if (m.dir == 1) return recon_inter(x0, y0, log2, m.mv[0], cbf, ref_);
@@ -420,8 +437,14 @@ class SliceDecoder {
         int cbf = 0;
         fill(x0, y0, log2, 0, 1, mv, 0, 0);
         if (has_res) cbf = transform_tree(x0, y0, log2, false, 0);
-        fill(x0, y0, log2, 0, 1, mv, cbf, 0);
-        recon_inter(x0, y0, log2, mv, cbf, ref_);
+        fill(x0, y0, log2, 0, 1, mv, cbf & 7, 0);
+        set_split_cbf(x0, y0, cbf);
+        if (cbf >> 12) {  // inter prediction is per sample: the quadrants predict like the CU
+          for (int q = 0; q < 4; ++q)
+            recon_inter(x0 + (q & 1) * 16, y0 + (q >> 1) * 16, 4, mv, (cbf >> (3 * q)) & 7, ref_);
+        } else {
+          recon_inter(x0, y0, log2, mv, cbf, ref_);
+        }
         return;
       }
     }
@@ -456,8 +479,29 @@ class SliceDecoder {
     recon_intra(x0, y0, log2, mode, cmode, cbf);
   }
 
-  // returns cbf bits; parses coefficients into fd_ planes
+  // returns cbf bits; parses coefficients into fd_ planes.  An inter CU's transform tree may
+  // split once (RQT, max_transform_hierarchy_depth_inter 1): then bit 12 is set and bits
+  // 3q..3q+2 hold quadrant q's cbfs.
   int transform_tree(int x0, int y0, int log2, bool intra, int mode, int cmode = 0) {
+    if (!intra && sps_.depth_inter > 0 && bin(CTX_SPLIT_TF + 5 - log2)) {
+      if (log2 != 5) fail("transform split below 32x32 unsupported");
+      const int W = sps_.coded_w, Wc = W >> 1;
+      clear_tb(fd_->coef_y.data() + (size_t)y0 * W + x0, W, log2);
+      clear_tb(fd_->coef_u.data() + (size_t)(y0 >> 1) * Wc + (x0 >> 1), Wc, log2 - 1);
+      clear_tb(fd_->coef_v.data() + (size_t)(y0 >> 1) * Wc + (x0 >> 1), Wc, log2 - 1);
+      const int cb0 = bin(CTX_CBF_CHROMA + 0), cr0 = bin(CTX_CBF_CHROMA + 0);
+      int res = 1 << 12;
+      for (int q = 0; q < 4; ++q) {
+        const int x = x0 + (q & 1) * 16, y = y0 + (q >> 1) * 16;
+        const int cb = cb0 ? bin(CTX_CBF_CHROMA + 1) : 0, cr = cr0 ? bin(CTX_CBF_CHROMA + 1) : 0;
+        const int cl = bin(CTX_CBF_LUMA + 0);
+        if (cl) residual(fd_->coef_y.data() + (size_t)y * W + x, W, 4, 0, 0);
+        if (cb) residual(fd_->coef_u.data() + (size_t)(y >> 1) * Wc + (x >> 1), Wc, 3, 1, 0);
+        if (cr) residual(fd_->coef_v.data() + (size_t)(y >> 1) * Wc + (x >> 1), Wc, 3, 2, 0);
+        res |= (cl | (cb << 1) | (cr << 2)) << (3 * q);
+      }
+      return res;
+    }
     const int cb = bin(CTX_CBF_CHROMA + 0);
     const int cr = bin(CTX_CBF_CHROMA + 0);
     int cl = 1;

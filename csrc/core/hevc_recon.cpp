@@ -89,7 +89,7 @@ void recon_tb(const int16_t* levels, int ls, bool cbf, int log2N, int qp, const 
 
 namespace {
 inline int edge_bs(const FrameData& fd, int xp, int yp, int xq, int yq) {
-  return deblock_edge_bs(fd.cu_log2, fd.intra, fd.cbf, fd.mv, fd.w8, xp, yp, xq, yq, fd.dir, fd.mv1);
+  return deblock_edge_bs(fd.cu_log2, fd.intra, fd.cbf, fd.mv, fd.w8, xp, yp, xq, yq, fd.dir, fd.mv1, fd.tu);
 }
 }  // namespace
 

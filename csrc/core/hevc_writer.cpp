@@ -113,7 +113,7 @@ void write_parameter_sets(const SeqConfig& cfg, std::vector<uint8_t>& out) {
     bw.ue(kCtbLog2 - kMinCbLog2);    // log2_diff_max_min_luma_coding_block_size
     bw.ue(kMinTbLog2 - 2);           // log2_min_luma_transform_block_size_minus2
     bw.ue(kMaxTbLog2 - kMinTbLog2);  // log2_diff_max_min_luma_transform_block_size
-    bw.ue(0);      // max_transform_hierarchy_depth_inter
+    bw.ue(cfg.rqt ? 1 : 0);  // max_transform_hierarchy_depth_inter (RQT: 32x32 -> 4 x 16x16)
     bw.ue(0);      // max_transform_hierarchy_depth_intra
     bw.put(0, 1);  // scaling_list_enabled_flag
     bw.put(0, 1);  // amp_enabled_flag
@@ -419,7 +419,7 @@ class SliceWriter {
     const int u = unit(x0, y0);
     const int N = 1 << log2;
     const bool intra = fd_.intra[u] != 0;
-    const int cbf = fd_.cbf[u];
+    const int cbf = cu_cbf(x0, y0);
     if (bslice_ && !intra) {
       coding_unit_b(x0, y0, log2, cbf);
       return;
@@ -539,7 +539,54 @@ class SliceWriter {
     }
   }
 
+  bool tu_split(int x0, int y0) const { return fd_.tu && fd_.tu[unit(x0, y0)]; }
+  // cbf bits of the CU at (x0, y0): an RQT-split CU's are the OR of its four TBs'
+  int cu_cbf(int x0, int y0) const {
+    if (!tu_split(x0, y0)) return fd_.cbf[unit(x0, y0)];
+    int c = 0;
+    for (int q = 0; q < 4; ++q) c |= fd_.cbf[unit(x0 + (q & 1) * 16, y0 + (q >> 1) * 16)];
+    return c;
+  }
+  // A 32x32 inter CU split once (7.3.8.8 at trafoDepth 0 -> 1): the chroma cbfs at depth 0 are
+  // the OR of the quadrants', then per 16x16 quadrant in z-order its chroma cbfs (under a set
+  // parent), cbf_luma (always coded at depth 1) and the residuals.
+  void transform_split(int x0, int y0) {
+    int c[4], cb0 = 0, cr0 = 0;
+    for (int q = 0; q < 4; ++q) {
+      c[q] = fd_.cbf[unit(x0 + (q & 1) * 16, y0 + (q >> 1) * 16)];
+      cb0 |= (c[q] >> 1) & 1;
+      cr0 |= (c[q] >> 2) & 1;
+    }
+    bin(cb0, CTX_CBF_CHROMA + 0);
+    bin(cr0, CTX_CBF_CHROMA + 0);
+    for (int q = 0; q < 4; ++q) {
+      const int x = x0 + (q & 1) * 16, y = y0 + (q >> 1) * 16;
+      const int cl = c[q] & 1, cb = (c[q] >> 1) & 1, cr = (c[q] >> 2) & 1;
+      if (cb0) bin(cb, CTX_CBF_CHROMA + 1);
+      if (cr0) bin(cr, CTX_CBF_CHROMA + 1);
+      bin(cl, CTX_CBF_LUMA + 0);
+      TbView v;
+      if (cl) {
+        tb_view(0, x, y, 4, v);
+        residual(v, 4, 0, 0);
+      }
+      if (cb) {
+        tb_view(1, x >> 1, y >> 1, 3, v);
+        residual(v, 3, 1, 0);
+      }
+      if (cr) {
+        tb_view(2, x >> 1, y >> 1, 3, v);
+        residual(v, 3, 2, 0);
+      }
+    }
+  }
+
   void transform_tree(int x0, int y0, int log2, bool intra, int mode) {
+    if (!intra && cfg_.rqt) {  // split_transform_flag of an inter CU (depth 0, ctx 5 - log2)
+      const bool split = tu_split(x0, y0);
+      bin(split ? 1 : 0, CTX_SPLIT_TF + 5 - log2);
+      if (split) return transform_split(x0, y0);
+    }
     const int cbf = fd_.cbf[unit(x0, y0)];
     const int cl = cbf & 1, cb = (cbf >> 1) & 1, cr = (cbf >> 2) & 1;
     // log2 >= 3 here, so chroma cbfs are coded at depth 0

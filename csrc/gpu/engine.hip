@@ -194,7 +194,7 @@ class Core {
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
     slot_bytes_ = align(B * g_.usz) + align(B * g_.usz * 4) + align(B * nctu_ * 8) + align(B * nctu_ * 4) +
                   align(B * nctu_ * 4) + align(B * 4) + align(B * nctu_ * 12) + align(B) + align(B * g_.usz) +
-                  align(B * g_.usz * 4) + align(B * g_.usz * 4) + align(B * cap_ * 2);
+                  align(B * g_.usz * 4) + align(B * g_.usz * 5) + align(B * cap_ * 2);
     host_alloc(&qhost_, (size_t)c.gop * B);
     host_alloc(&quni_, (size_t)B);
     std::memset(quni_, c.qp, (size_t)B);
@@ -257,7 +257,7 @@ class Core {
     const size_t qsz = (size_t)(g.W / 4) * (g.H / 4), cap = g.ysz + 2 * g.csz;
     const size_t slot = align(B * g.usz) + align(B * g.usz * 4) + align(B * nctu * 8) + align(B * nctu * 4) +
                         align(B * nctu * 4) + align(B * 4) + align(B * nctu * 12) + align(B) + align(B * g.usz) +
-                        align(B * g.usz * 4) + align(B * g.usz * 4) + align(B * cap * 2);
+                        align(B * g.usz * 4) + align(B * g.usz * 5) + align(B * cap * 2);
     dev = set + ndpb * (set + B * 16 * g.psz + B * qsz) + ((c.deblock & 2) ? set : 0) + 2 * set +
           B * 3 * sizeof(unsigned long long) + B * nctu * sizeof(int) + 2 * B * nctu * 2 * sizeof(int16_t) +
           2 * B * nctu * sizeof(int) + (c.mgop > 1 ? 2 * B * nctu * sizeof(CtbMeOut) : 0) +
@@ -329,7 +329,7 @@ class Core {
   };
   // carve one slot buffer (device or host) into its arrays
   struct Parts {
-    uint8_t *flags, *cu_log2, *intra, *ipm, *cbf, *dir;
+    uint8_t *flags, *cu_log2, *intra, *ipm, *cbf, *dir, *tu;
     int16_t *mv, *mv1;
     unsigned long long* mask_y;
     unsigned* mask_c;
@@ -370,7 +370,8 @@ class Core {
     p.intra = q + B * U;
     p.cbf = q + 2 * B * U;
     p.dir = q + 3 * B * U;
-    q += align(B * U * 4);
+    p.tu = q + 4 * B * U;
+    q += align(B * U * 5);
     p.packed = reinterpret_cast<int16_t*>(q);
     p.count = nullptr;  // device count array lives in the scratch below
     return p;
@@ -418,7 +419,8 @@ class Core {
     const long U = g_.usz, o = b * U;
     for (long u = 0; u < U; ++u) {
       const uint8_t f = p.flags[o + u];
-      p.cu_log2[o + u] = (uint8_t)(3 + (f & 3));
+      p.cu_log2[o + u] = (uint8_t)((f & 3) == 3 ? 5 : 3 + (f & 3));  // 3: 32x32 with four 16x16 TBs
+      p.tu[o + u] = (uint8_t)((f & 3) == 3);
       p.intra[o + u] = (uint8_t)((f >> 2) & 1);
       p.cbf[o + u] = (uint8_t)((f >> 3) & 7);
       p.dir[o + u] = (uint8_t)(f >> 6);
@@ -435,6 +437,7 @@ class Core {
     f.intra = p.intra + b * U;
     f.ipm = p.ipm + b * U;
     f.cbf = p.cbf + b * U;
+    f.tu = p.tu + b * U;
     f.mv = p.mv + b * U * 2;
     f.sb_mask_y = reinterpret_cast<const uint64_t*>(p.mask_y + (long)b * nctu_);
     f.sb_mask_c = p.mask_c + (long)b * nctu_;
@@ -596,7 +599,8 @@ class Core {
     DpbEntry& cur_e = dpb_[e];
     const FrameSet fin_set = cur_e.rec;
     const FrameSet cur = seq_.sao ? deb_ : fin_set;  // SAO filters deb_ into the entry
-    const DecisionSet dec = bpic ? slot_dec_b(s) : dec0;
+    DecisionSet dec = bpic ? slot_dec_b(s) : dec0;
+    if (pic.type == 1 && seq_.rqt) dec.tu = carve(s.dev).tu;  // RQT: P pictures only
     // TV_SYNC_DEBUG=1: synchronise and check after every stage (fault isolation)
     auto stage = [&](const char* name) {
       if (!sync_debug_) return;

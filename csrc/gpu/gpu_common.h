@@ -64,6 +64,9 @@ struct DecisionSet {
   // B pictures only (nullptr otherwise): per-unit direction (1 L0, 2 L1, 3 bi), list-1 MVs
   uint8_t* dir = nullptr;
   int16_t* mv1 = nullptr;
+  // P pictures with RQT (hevc_defs.h rqt_split): 1 = the unit's 32x32 inter CU codes four
+  // 16x16 TBs; written by k_inter_recon for every unit (nullptr: no splits)
+  uint8_t* tu = nullptr;
 };
 
 // ---- wave-level data movement on the VALU (DPP) instead of LDS (ds_bpermute) ----------

@@ -116,7 +116,8 @@ __global__ void __launch_bounds__(256) k_sb_pack(DecisionSet dec, Geo g, Compact
 __global__ void __launch_bounds__(256) k_pack_flags(DecisionSet dec, uint8_t* flags, long n) {
   for (long u = blockIdx.x * 256L + threadIdx.x; u < n; u += (long)gridDim.x * 256) {
     const int d = dec.dir ? dec.dir[u] : 1;
-    flags[u] = (uint8_t)((dec.cu_log2[u] - 3) | (dec.intra[u] << 2) | ((dec.cbf[u] & 7) << 3) | (d << 6));
+    const int l = dec.tu && dec.tu[u] ? 3 : dec.cu_log2[u] - 3;  // 3: a 32x32 CU with four 16x16 TBs
+    flags[u] = (uint8_t)(l | (dec.intra[u] << 2) | ((dec.cbf[u] & 7) << 3) | (d << 6));
   }
 }
 

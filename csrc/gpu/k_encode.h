@@ -101,8 +101,8 @@ struct CompactSet {
   long cap;                    // int16 capacity per segment
 };
 void launch_compact(DecisionSet dec, const Geo& g, CompactSet cs, int B, hipStream_t s);
-// one byte per 8x8 unit for the D2H transfer: (cu_log2 - 3) | intra << 2 | cbf << 3 | dir << 6
-// (dir = 1 when dec.dir is null)
+// one byte per 8x8 unit for the D2H transfer: (cu_log2 - 3, or 3 for an RQT-split 32x32 CU) |
+// intra << 2 | cbf << 3 | dir << 6 (dir = 1 when dec.dir is null)
 void launch_pack_flags(DecisionSet dec, uint8_t* flags, const Geo& g, int B, hipStream_t s);
 
 }  // namespace gpu

@@ -324,6 +324,7 @@ __global__ void __launch_bounds__(256) k_deblock(FrameSet rec, DecisionSet dec, 
   const int16_t* mv = dec.mv + 2 * ub;
   const uint8_t* dir = dec.dir ? dec.dir + ub : nullptr;  // B pictures
   const int16_t* mv1 = dec.mv1 ? dec.mv1 + 2 * ub : nullptr;
+  const uint8_t* tu = dec.tu ? dec.tu + ub : nullptr;  // RQT-split 32x32 CUs (P pictures)
   uint8_t* Y = rec.plane(0, b, g);
   uint8_t* U = rec.plane(1, b, g);
   uint8_t* V = rec.plane(2, b, g);
@@ -335,25 +336,25 @@ __global__ void __launch_bounds__(256) k_deblock(FrameSet rec, DecisionSet dec, 
     if (i < nl) {
       if (!horizontal) {
         const int x = 8 * (1 + i % (W / 8 - 1)), y = 4 * (i / (W / 8 - 1));
-        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, x - 1, y, x, y, dir, mv1);
+        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, x - 1, y, x, y, dir, mv1, tu);
         if (bs) deblock_luma_edge4(Y + (long)y * W + x, 1, W, bs, qp);
       } else {
         const int y = 8 * (1 + i % (H / 8 - 1)), x = 4 * (i / (H / 8 - 1));
-        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, x, y - 1, x, y, dir, mv1);
+        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, x, y - 1, x, y, dir, mv1, tu);
         if (bs) deblock_luma_edge4(Y + (long)y * W + x, W, 1, bs, qp);
       }
     } else {
       const int j = i - nl;
       if (!horizontal) {
         const int xc = 8 * (1 + j % (W / 16 - 1)), yc = 4 * (j / (W / 16 - 1));
-        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, 2 * xc - 1, 2 * yc, 2 * xc, 2 * yc, dir, mv1);
+        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, 2 * xc - 1, 2 * yc, 2 * xc, 2 * yc, dir, mv1, tu);
         if (bs == 2) {
           deblock_chroma_edge(U + (long)yc * Wc + xc, 1, Wc, 4, qpc);
           deblock_chroma_edge(V + (long)yc * Wc + xc, 1, Wc, 4, qpc);
         }
       } else {
         const int yc = 8 * (1 + j % (H / 16 - 1)), xc = 4 * (j / (H / 16 - 1));
-        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, 2 * xc, 2 * yc - 1, 2 * xc, 2 * yc, dir, mv1);
+        const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, 2 * xc, 2 * yc - 1, 2 * xc, 2 * yc, dir, mv1, tu);
         if (bs == 2) {
           deblock_chroma_edge(U + (long)yc * Wc + xc, Wc, 1, 4, qpc);
           deblock_chroma_edge(V + (long)yc * Wc + xc, Wc, 1, 4, qpc);

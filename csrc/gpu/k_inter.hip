@@ -607,6 +607,7 @@ struct PReconLds {
   int nz[48], sa[48], dc[48];  // per-TB statistics: luma 0..15, Cb 16..31, Cr 32..47
   int qtype[4];               // luma quadrant: 0 part of a 32x32 CU, 1 16x16 CU, 2 four 8x8 CUs
   int tzero[8];               // stage-3/4 tile t has no surviving level: reconstruction = prediction
+  int qsad[4], split;         // RQT: luma residual SAD per quadrant of a 32x32 CU, the decision
 };
 
 // block size (log2) of the TB owning luma sample (x, y) / chroma sample (x, y) of the CTB
@@ -653,6 +654,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k
     L.mv1[tid][1] = dec.mv1 ? dec.mv1[2 * u + 1] : 0;
   }
   if (tid < 48) L.nz[tid] = L.sa[tid] = L.dc[tid] = 0;
+  if (tid == 0) L.split = 0;
   if (tid < 4) {
     const int l2 = dec.cu_log2[ub + (long)((cy >> 3) + (tid >> 1) * 2) * g.w8 + (cx >> 3) + (tid & 1) * 2];
     L.qtype[tid] = l2 == 5 ? 0 : (l2 == 4 ? 1 : 2);
@@ -750,6 +752,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k
     }
   }
   __syncthreads();
+  if (dec.tu) {  // RQT (P pictures): a 32x32 CU may code four 16x16 TBs (hevc_defs.h rqt_split)
+    if (L.qtype[0] == 0) {  // workgroup-uniform
+      const int qx = (wave & 1) * 16, qy = (wave >> 1) * 16;
+      int d = 0;
+      for (int k = lane; k < 256; k += 64) d += tv_abs((int)L.resY[(qy + (k >> 4)) * 32 + qx + (k & 15)]);
+      d = wave_sum(d);
+      if (lane == 0) L.qsad[wave] = d;
+      __syncthreads();
+      if (tid == 0 && rqt_split(L.qsad)) {
+        L.split = 1;
+        L.qtype[0] = L.qtype[1] = L.qtype[2] = L.qtype[3] = 1;  // the 16x16-CU tile layout
+      }
+      __syncthreads();
+    }
+    if (tid < 16) dec.tu[ub + (long)((cy >> 3) + (tid >> 2)) * g.w8 + (cx >> 3) + (tid & 3)] = (uint8_t)L.split;
+  }
   const bool whole = L.qtype[0] == 0;
   const int ntiles = whole ? 6 : 8;
   // tile t: luma (whole: 32x32 tile ti,tj = t>>1, t&1; else quadrant t) for t < 4, chroma

@@ -42,6 +42,16 @@ struct SeqConfig {
   int dpb_size = 2, num_reorder = 0;
   // intra 16x16 CUs in P pictures (tv/me_model.h, pintra_*): on unless TV_PINTRA=0
   bool pintra = pintra_default();
+  // residual quadtree: inter 32x32 CUs of P pictures may code four 16x16 TBs
+  // (max_transform_hierarchy_depth_inter 1; hevc_defs.h rqt_split): on unless TV_RQT=0
+  bool rqt = rqt_default();
+  static bool rqt_default() {
+    static const bool on = [] {
+      const char* e = std::getenv("TV_RQT");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   static bool pintra_default() {
     static const bool on = [] {
       const char* e = std::getenv("TV_PINTRA");
@@ -96,12 +106,15 @@ struct FrameData {
   const SliceRefs* refs = nullptr;
   const uint8_t* dir = nullptr;
   const int16_t* mv1 = nullptr;
+  // 1: the unit's inter 32x32 CU codes four 16x16 TBs (RQT split); cbf[u] is then the cbf of
+  // the unit's 16x16 TB (nullptr: no splits)
+  const uint8_t* tu = nullptr;
 };
 
 // Owning storage for one frame's decisions (CPU side).
 struct FrameDecisions {
   int w8 = 0, h8 = 0, cw = 0, ch = 0;
-  std::vector<uint8_t> cu_log2, intra, ipm, cbf;
+  std::vector<uint8_t> cu_log2, intra, ipm, cbf, tu;
   std::vector<int16_t> mv, coef_y, coef_u, coef_v;
   std::vector<uint32_t> sao;  // 3 per CTB
   int qp = -1;                // slice QP of this frame (-1: sequence QP)
@@ -122,6 +135,7 @@ struct FrameDecisions {
     intra.assign(n, 0);
     ipm.assign(n, 1);
     cbf.assign(n, 0);
+    tu.assign(n, 0);
     mv.assign(2 * n, 0);
     dir.assign(n, 1);
     mv1.assign(2 * n, 0);
@@ -138,6 +152,7 @@ struct FrameDecisions {
     f.ipm = ipm.data();
     f.mv = mv.data();
     f.cbf = cbf.data();
+    f.tu = tu.data();
     f.coef[0] = coef_y.data();
     f.coef[1] = coef_u.data();
     f.coef[2] = coef_v.data();
