@@ -498,8 +498,11 @@ void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* 
   };
   auto do_cu = [&](int x0, int y0, int log2) {
     const int u = (y0 >> 3) * fd.w8 + (x0 >> 3);
-    if (cfg.rqt && !ref1 && log2 == 5 && !fd.intra[u]) {  // RQT decision (hevc_defs.h rqt_split)
-      predict_inter_block(*ref, 0, x0, y0, 32, 32, fd.mv[2 * u], fd.mv[2 * u + 1], pred);
+    if (cfg.rqt && ref && log2 == 5 && !fd.intra[u]) {  // RQT decision (hevc_defs.h rqt_split)
+      const int dir = ref1 ? fd.dir[u] : 1;
+      if (dir == 1) predict_inter_block(*ref, 0, x0, y0, 32, 32, fd.mv[2 * u], fd.mv[2 * u + 1], pred);
+      else if (dir == 2) predict_inter_block(*ref1, 0, x0, y0, 32, 32, fd.mv1[2 * u], fd.mv1[2 * u + 1], pred);
+      else predict_bi_block(*ref, *ref1, 0, x0, y0, 32, 32, &fd.mv[2 * u], &fd.mv1[2 * u], pred);
       int sad4[4] = {0, 0, 0, 0};
       for (int j = 0; j < 32; ++j)
         for (int i = 0; i < 32; ++i)

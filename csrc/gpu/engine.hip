@@ -600,7 +600,7 @@ class Core {
     const FrameSet fin_set = cur_e.rec;
     const FrameSet cur = seq_.sao ? deb_ : fin_set;  // SAO filters deb_ into the entry
     DecisionSet dec = bpic ? slot_dec_b(s) : dec0;
-    if (pic.type == 1 && seq_.rqt) dec.tu = carve(s.dev).tu;  // RQT: P pictures only
+    if (!intra && seq_.rqt) dec.tu = carve(s.dev).tu;  // RQT: P and B pictures
     // TV_SYNC_DEBUG=1: synchronise and check after every stage (fault isolation)
     auto stage = [&](const char* name) {
       if (!sync_debug_) return;
