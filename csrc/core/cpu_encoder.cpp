@@ -498,18 +498,19 @@ void reconstruct_frame(const SeqConfig& cfg, const Picture& src, const Picture* 
   };
   auto do_cu = [&](int x0, int y0, int log2) {
     const int u = (y0 >> 3) * fd.w8 + (x0 >> 3);
-    if (cfg.rqt && ref && log2 == 5 && !fd.intra[u]) {  // RQT decision (hevc_defs.h rqt_split)
-      const int dir = ref1 ? fd.dir[u] : 1;
-      if (dir == 1) predict_inter_block(*ref, 0, x0, y0, 32, 32, fd.mv[2 * u], fd.mv[2 * u + 1], pred);
-      else if (dir == 2) predict_inter_block(*ref1, 0, x0, y0, 32, 32, fd.mv1[2 * u], fd.mv1[2 * u + 1], pred);
-      else predict_bi_block(*ref, *ref1, 0, x0, y0, 32, 32, &fd.mv[2 * u], &fd.mv1[2 * u], pred);
+    if (cfg.rqt && ref && log2 >= kRqtMinLog2 && !fd.intra[u]) {  // RQT decision (hevc_defs.h rqt_split)
+      const int N = 1 << log2, h = N >> 1, dir = ref1 ? fd.dir[u] : 1;
+      if (dir == 1) predict_inter_block(*ref, 0, x0, y0, N, N, fd.mv[2 * u], fd.mv[2 * u + 1], pred);
+      else if (dir == 2) predict_inter_block(*ref1, 0, x0, y0, N, N, fd.mv1[2 * u], fd.mv1[2 * u + 1], pred);
+      else predict_bi_block(*ref, *ref1, 0, x0, y0, N, N, &fd.mv[2 * u], &fd.mv1[2 * u], pred);
       int sad4[4] = {0, 0, 0, 0};
-      for (int j = 0; j < 32; ++j)
-        for (int i = 0; i < 32; ++i)
-          sad4[(j >> 4) * 2 + (i >> 4)] += tv_abs((int)src.y[(size_t)(y0 + j) * W + x0 + i] - pred[j * 32 + i]);
-      if (rqt_split(sad4)) {
-        for (int q = 0; q < 4; ++q) code_tbs(x0 + (q & 1) * 16, y0 + (q >> 1) * 16, 4);
-        for (int k = 0; k < 16; ++k) fd.tu[u + (k >> 2) * fd.w8 + (k & 3)] = 1;
+      for (int j = 0; j < N; ++j)
+        for (int i = 0; i < N; ++i)
+          sad4[(j / h) * 2 + i / h] += tv_abs((int)src.y[(size_t)(y0 + j) * W + x0 + i] - pred[j * N + i]);
+      if (rqt_split(sad4, h * h)) {
+        for (int q = 0; q < 4; ++q) code_tbs(x0 + (q & 1) * h, y0 + (q >> 1) * h, log2 - 1);
+        for (int j = 0; j < (N >> 3); ++j)
+          for (int i = 0; i < (N >> 3); ++i) fd.tu[u + j * fd.w8 + i] = 1;
         return;
       }
     }

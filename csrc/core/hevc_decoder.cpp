@@ -320,21 +320,24 @@ class SliceDecoder {
     int cbf = 0;
     if (has_res) cbf = transform_tree(x0, y0, log2, false, 0);
     fill(x0, y0, log2, 0, 1, m.mv[0], cbf & 7, skip ? 1 : 0);
-    set_split_cbf(x0, y0, cbf);
+    set_split_cbf(x0, y0, log2, cbf);
     if (cbf >> 12) {
-      for (int q = 0; q < 4; ++q) recon_motion(x0 + (q & 1) * 16, y0 + (q >> 1) * 16, 4, m, (cbf >> (3 * q)) & 7);
+      const int h = 1 << (log2 - 1);
+      for (int q = 0; q < 4; ++q) recon_motion(x0 + (q & 1) * h, y0 + (q >> 1) * h, log2 - 1, m, (cbf >> (3 * q)) & 7);
     } else {
       recon_motion(x0, y0, log2, m, cbf);
     }
   }
   // an RQT-split CU (transform_tree result bit 12): per-unit cbf of its 16x16 TB, tu = 1
-  void set_split_cbf(int x0, int y0, int res) {
+  void set_split_cbf(int x0, int y0, int log2, int res) {
     if (!(res >> 12)) return;
-    for (int k = 0; k < 16; ++k) {
-      const int u = unit(x0 + 8 * (k & 3), y0 + 8 * (k >> 2)), q = ((k >> 3) << 1) | ((k >> 1) & 1);
-      fd_->cbf[u] = (uint8_t)((res >> (3 * q)) & 7);
-      fd_->tu[u] = 1;
-    }
+    const int n = 1 << (log2 - 3), hb = n >> 1;  // units per side, per quadrant side
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) {
+        const int u = unit(x0 + 8 * i, y0 + 8 * j), q = (j / hb) * 2 + i / hb;
+        fd_->cbf[u] = (uint8_t)((res >> (3 * q)) & 7);
+        fd_->tu[u] = 1;
+      }
   }
   void recon_motion(int x0, int y0, int log2, const Motion& m, int cbf) {
     if (m.dir == 1) return recon_inter(x0, y0, log2, m.mv[0], cbf, ref_);
@@ -438,10 +441,11 @@ class SliceDecoder {
         fill(x0, y0, log2, 0, 1, mv, 0, 0);
         if (has_res) cbf = transform_tree(x0, y0, log2, false, 0);
         fill(x0, y0, log2, 0, 1, mv, cbf & 7, 0);
-        set_split_cbf(x0, y0, cbf);
+        set_split_cbf(x0, y0, log2, cbf);
         if (cbf >> 12) {  // inter prediction is per sample: the quadrants predict like the CU
+          const int h = 1 << (log2 - 1);
           for (int q = 0; q < 4; ++q)
-            recon_inter(x0 + (q & 1) * 16, y0 + (q >> 1) * 16, 4, mv, (cbf >> (3 * q)) & 7, ref_);
+            recon_inter(x0 + (q & 1) * h, y0 + (q >> 1) * h, log2 - 1, mv, (cbf >> (3 * q)) & 7, ref_);
         } else {
           recon_inter(x0, y0, log2, mv, cbf, ref_);
         }
@@ -484,7 +488,8 @@ class SliceDecoder {
   // 3q..3q+2 hold quadrant q's cbfs.
   int transform_tree(int x0, int y0, int log2, bool intra, int mode, int cmode = 0) {
     if (!intra && sps_.depth_inter > 0 && bin(CTX_SPLIT_TF + 5 - log2)) {
-      if (log2 != 5) fail("transform split below 32x32 unsupported");
+      if (log2 < 4) fail("transform split below 16x16 unsupported");
+      const int h = 1 << (log2 - 1), l = log2 - 1;
       const int W = sps_.coded_w, Wc = W >> 1;
       clear_tb(fd_->coef_y.data() + (size_t)y0 * W + x0, W, log2);
       clear_tb(fd_->coef_u.data() + (size_t)(y0 >> 1) * Wc + (x0 >> 1), Wc, log2 - 1);
@@ -492,12 +497,12 @@ class SliceDecoder {
       const int cb0 = bin(CTX_CBF_CHROMA + 0), cr0 = bin(CTX_CBF_CHROMA + 0);
       int res = 1 << 12;
       for (int q = 0; q < 4; ++q) {
-        const int x = x0 + (q & 1) * 16, y = y0 + (q >> 1) * 16;
+        const int x = x0 + (q & 1) * h, y = y0 + (q >> 1) * h;
         const int cb = cb0 ? bin(CTX_CBF_CHROMA + 1) : 0, cr = cr0 ? bin(CTX_CBF_CHROMA + 1) : 0;
         const int cl = bin(CTX_CBF_LUMA + 0);
-        if (cl) residual(fd_->coef_y.data() + (size_t)y * W + x, W, 4, 0, 0);
-        if (cb) residual(fd_->coef_u.data() + (size_t)(y >> 1) * Wc + (x >> 1), Wc, 3, 1, 0);
-        if (cr) residual(fd_->coef_v.data() + (size_t)(y >> 1) * Wc + (x >> 1), Wc, 3, 2, 0);
+        if (cl) residual(fd_->coef_y.data() + (size_t)y * W + x, W, l, 0, 0);
+        if (cb) residual(fd_->coef_u.data() + (size_t)(y >> 1) * Wc + (x >> 1), Wc, l - 1, 1, 0);
+        if (cr) residual(fd_->coef_v.data() + (size_t)(y >> 1) * Wc + (x >> 1), Wc, l - 1, 2, 0);
         res |= (cl | (cb << 1) | (cr << 2)) << (3 * q);
       }
       return res;

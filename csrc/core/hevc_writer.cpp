@@ -419,7 +419,7 @@ class SliceWriter {
     const int u = unit(x0, y0);
     const int N = 1 << log2;
     const bool intra = fd_.intra[u] != 0;
-    const int cbf = cu_cbf(x0, y0);
+    const int cbf = cu_cbf(x0, y0, log2);
     if (bslice_ && !intra) {
       coding_unit_b(x0, y0, log2, cbf);
       return;
@@ -541,42 +541,44 @@ class SliceWriter {
 
   bool tu_split(int x0, int y0) const { return fd_.tu && fd_.tu[unit(x0, y0)]; }
   // cbf bits of the CU at (x0, y0): an RQT-split CU's are the OR of its four TBs'
-  int cu_cbf(int x0, int y0) const {
+  int cu_cbf(int x0, int y0, int log2) const {
     if (!tu_split(x0, y0)) return fd_.cbf[unit(x0, y0)];
+    const int h = 1 << (log2 - 1);
     int c = 0;
-    for (int q = 0; q < 4; ++q) c |= fd_.cbf[unit(x0 + (q & 1) * 16, y0 + (q >> 1) * 16)];
+    for (int q = 0; q < 4; ++q) c |= fd_.cbf[unit(x0 + (q & 1) * h, y0 + (q >> 1) * h)];
     return c;
   }
-  // A 32x32 inter CU split once (7.3.8.8 at trafoDepth 0 -> 1): the chroma cbfs at depth 0 are
-  // the OR of the quadrants', then per 16x16 quadrant in z-order its chroma cbfs (under a set
-  // parent), cbf_luma (always coded at depth 1) and the residuals.
-  void transform_split(int x0, int y0) {
+  // An inter CU (32x32 or 16x16) split once (7.3.8.8 at trafoDepth 0 -> 1): the chroma cbfs
+  // at depth 0 are the OR of the quadrants', then per quadrant in z-order its chroma cbfs
+  // (under a set parent), cbf_luma (always coded at depth 1) and the residuals.
+  void transform_split(int x0, int y0, int log2) {
+    const int h = 1 << (log2 - 1), l = log2 - 1;
     int c[4], cb0 = 0, cr0 = 0;
     for (int q = 0; q < 4; ++q) {
-      c[q] = fd_.cbf[unit(x0 + (q & 1) * 16, y0 + (q >> 1) * 16)];
+      c[q] = fd_.cbf[unit(x0 + (q & 1) * h, y0 + (q >> 1) * h)];
       cb0 |= (c[q] >> 1) & 1;
       cr0 |= (c[q] >> 2) & 1;
     }
     bin(cb0, CTX_CBF_CHROMA + 0);
     bin(cr0, CTX_CBF_CHROMA + 0);
     for (int q = 0; q < 4; ++q) {
-      const int x = x0 + (q & 1) * 16, y = y0 + (q >> 1) * 16;
+      const int x = x0 + (q & 1) * h, y = y0 + (q >> 1) * h;
       const int cl = c[q] & 1, cb = (c[q] >> 1) & 1, cr = (c[q] >> 2) & 1;
       if (cb0) bin(cb, CTX_CBF_CHROMA + 1);
       if (cr0) bin(cr, CTX_CBF_CHROMA + 1);
       bin(cl, CTX_CBF_LUMA + 0);
       TbView v;
       if (cl) {
-        tb_view(0, x, y, 4, v);
-        residual(v, 4, 0, 0);
+        tb_view(0, x, y, l, v);
+        residual(v, l, 0, 0);
       }
       if (cb) {
-        tb_view(1, x >> 1, y >> 1, 3, v);
-        residual(v, 3, 1, 0);
+        tb_view(1, x >> 1, y >> 1, l - 1, v);
+        residual(v, l - 1, 1, 0);
       }
       if (cr) {
-        tb_view(2, x >> 1, y >> 1, 3, v);
-        residual(v, 3, 2, 0);
+        tb_view(2, x >> 1, y >> 1, l - 1, v);
+        residual(v, l - 1, 2, 0);
       }
     }
   }
@@ -585,7 +587,7 @@ class SliceWriter {
     if (!intra && cfg_.rqt) {  // split_transform_flag of an inter CU (depth 0, ctx 5 - log2)
       const bool split = tu_split(x0, y0);
       bin(split ? 1 : 0, CTX_SPLIT_TF + 5 - log2);
-      if (split) return transform_split(x0, y0);
+      if (split) return transform_split(x0, y0, log2);
     }
     const int cbf = fd_.cbf[unit(x0, y0)];
     const int cl = cbf & 1, cb = (cbf >> 1) & 1, cr = (cbf >> 2) & 1;

@@ -419,9 +419,10 @@ class Core {
     const long U = g_.usz, o = b * U;
     for (long u = 0; u < U; ++u) {
       const uint8_t f = p.flags[o + u];
-      p.cu_log2[o + u] = (uint8_t)((f & 3) == 3 ? 5 : 3 + (f & 3));  // 3: 32x32 with four 16x16 TBs
-      p.tu[o + u] = (uint8_t)((f & 3) == 3);
-      p.intra[o + u] = (uint8_t)((f >> 2) & 1);
+      const bool sp = (f & 3) == 3;  // an RQT-split inter CU: its size (32 / 16) in bit 2
+      p.cu_log2[o + u] = (uint8_t)(sp ? ((f >> 2) & 1 ? 4 : 5) : 3 + (f & 3));
+      p.tu[o + u] = (uint8_t)sp;
+      p.intra[o + u] = (uint8_t)(sp ? 0 : (f >> 2) & 1);
       p.cbf[o + u] = (uint8_t)((f >> 3) & 7);
       p.dir[o + u] = (uint8_t)(f >> 6);
     }

@@ -521,6 +521,9 @@ __global__ void __launch_bounds__(256) k_av1e_mv_refine(const uint8_t* __restric
   const int bw = W >> 4, bh = H >> 4, sbw = (W + 63) >> 6, sx = sbi % sbw, sy = sbi / sbw;
   const long ysz = (long)W * H, nb = (long)bw * bh;
   const uint32_t* C = cur + b * nb;
+  // round 0 (nothing memoised) stages up front, its loads overlapping the candidate lists;
+  // later rounds stage only superblocks with a pair left to score (below)
+  if (!use_prev) stage_sb(srcy + b * ysz, refy + b * ysz, W, H, sx * 64, sy * 64, win, sb);
   constexpr int kM = kMvRefineMaxCand;
   __shared__ uint32_t pmv[16][kM];
   __shared__ int psat[16][kM], pn[16];
@@ -556,7 +559,7 @@ __global__ void __launch_bounds__(256) k_av1e_mv_refine(const uint8_t* __restric
   }
   __syncthreads();
   const int grp = t >> 4, b4 = t & 15, n = npairs;
-  if (n) {  // a converged superblock (every candidate memoised) skips the staging
+  if (n && use_prev) {  // a converged superblock (every candidate memoised) skips the staging
     stage_sb(srcy + b * ysz, refy + b * ysz, W, H, sx * 64, sy * 64, win, sb);
     __syncthreads();
   }

@@ -116,8 +116,10 @@ __global__ void __launch_bounds__(256) k_sb_pack(DecisionSet dec, Geo g, Compact
 __global__ void __launch_bounds__(256) k_pack_flags(DecisionSet dec, uint8_t* flags, long n) {
   for (long u = blockIdx.x * 256L + threadIdx.x; u < n; u += (long)gridDim.x * 256) {
     const int d = dec.dir ? dec.dir[u] : 1;
-    const int l = dec.tu && dec.tu[u] ? 3 : dec.cu_log2[u] - 3;  // 3: a 32x32 CU with four 16x16 TBs
-    flags[u] = (uint8_t)(l | (dec.intra[u] << 2) | ((dec.cbf[u] & 7) << 3) | (d << 6));
+    // size code 3: an RQT-split inter CU, its size in the intra bit (0: 32x32, 1: 16x16)
+    const bool sp = dec.tu && dec.tu[u];
+    const int l = sp ? 3 : dec.cu_log2[u] - 3, in = sp ? (dec.cu_log2[u] == 4) : dec.intra[u];
+    flags[u] = (uint8_t)(l | (in << 2) | ((dec.cbf[u] & 7) << 3) | (d << 6));
   }
 }
 

@@ -475,28 +475,41 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
     if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)(sv[0] + sv[7] + tile[tid]);
     return;
   }
-  int eo[4][4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) eo[d][q] = 0;
+  // EO statistics per lane in one 64-bit register per class: four signed 16-bit fields
+  // (category 1..4) of sum(orig - deb) * 16 + count over the lane's <= 8 samples (|field| <=
+  // 255 * 8 * 16 + 8 < 2^15), added as one shifted 64-bit value per (sample, class) instead
+  // of four compare/select/adds; unpacked into the wave-sum format afterwards.
+  unsigned long long eo64[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     if (k >= iters) break;
     const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
     const int lx = i % n, ly = i / n;
     const int v = t[(ly + 1) * T + lx + 1];
-    const int packed = (sv[k] - v) * 2048 + 1;
+    const int d16 = (sv[k] - v) * 16 + 1;
+    const unsigned long long p64 = (unsigned long long)(long long)d16;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       int dx, dy;
       sao_eo_dir(d, dx, dy);
       const int a = t[(ly + 1 + dy) * T + lx + 1 + dx], bb = t[(ly + 1 - dy) * T + lx + 1 - dx];
-      const int cat = (a < 0 || bb < 0) ? 0 : sao_eo_category(v, a, bb);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) eo[d][q] += cat == q + 1 ? packed : 0;
+      const int e = tv_min(tv_max(v - a, -1), 1) + tv_min(tv_max(v - bb, -1), 1);  // -2..2, 0 = none
+      const int f = e + 2 - (e > 0);  // category 1..4 -> field 0..3 (e = 0 is masked below)
+      eo64[d] += (a >= 0 && bb >= 0 && e != 0) ? p64 << (16 * f) : 0ull;
     }
-    atomicAdd(&bh[c][v >> 3][lane & 15], packed);  // band statistics
+    atomicAdd(&bh[c][v >> 3][lane & 15], (sv[k] - v) * 2048 + 1);  // band statistics
+  }
+  int eo[4][4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    unsigned long long acc = eo64[d];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int fv = (int)(int16_t)(acc & 0xffffu);  // 16 * sum + count
+      acc = (acc - (unsigned long long)(long long)fv) >> 16;
+      const int cnt = fv & 15;
+      eo[d][q] = ((fv - cnt) >> 4) * 2048 + cnt;  // sum * 2048 + count, as before
+    }
   }
 #pragma unroll
   for (int d = 0; d < 4; ++d)

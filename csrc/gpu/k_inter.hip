@@ -608,6 +608,8 @@ struct PReconLds {
   int qtype[4];               // luma quadrant: 0 part of a 32x32 CU, 1 16x16 CU, 2 four 8x8 CUs
   int tzero[8];               // stage-3/4 tile t has no surviving level: reconstruction = prediction
   int qsad[4], split;         // RQT: luma residual SAD per quadrant of a 32x32 CU, the decision
+  int qsplit[4];              // RQT of the 16x16 CU in quadrant q (four 8x8 TBs)
+  int qintra[4];              // quadrant q is an intra CU of a P picture (k_pintra_recon codes it)
 };
 
 // block size (log2) of the TB owning luma sample (x, y) / chroma sample (x, y) of the CTB
@@ -655,6 +657,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k
   }
   if (tid < 48) L.nz[tid] = L.sa[tid] = L.dc[tid] = 0;
   if (tid == 0) L.split = 0;
+  if (tid < 4) {
+    L.qsplit[tid] = 0;
+    L.qintra[tid] = dec.intra[ub + (long)((cy >> 3) + (tid >> 1) * 2) * g.w8 + (cx >> 3) + (tid & 1) * 2];
+  }
   if (tid < 4) {
     const int l2 = dec.cu_log2[ub + (long)((cy >> 3) + (tid >> 1) * 2) * g.w8 + (cx >> 3) + (tid & 1) * 2];
     L.qtype[tid] = l2 == 5 ? 0 : (l2 == 4 ? 1 : 2);
@@ -765,8 +771,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k
         L.qtype[0] = L.qtype[1] = L.qtype[2] = L.qtype[3] = 1;  // the 16x16-CU tile layout
       }
       __syncthreads();
+    } else if (kRqtMinLog2 <= 4) {  // 16x16 CUs: quadrant `wave`'s four 8x8 SADs, four 8x8 TBs on a split
+      if (L.qtype[wave] == 1 && !L.qintra[wave]) {  // wave-uniform
+        const int qx = (wave & 1) * 16, qy = (wave >> 1) * 16;
+        int s4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          s4[k] = wave_sum(tv_abs((int)L.resY[(qy + (k >> 1) * 8 + (lane >> 3)) * 32 + qx + (k & 1) * 8 + (lane & 7)]));
+        if (lane == 0 && rqt_split(s4, 64)) L.qsplit[wave] = 1;
+      }
+      __syncthreads();
+      if (tid < 4 && L.qsplit[tid]) L.qtype[tid] = 2;  // the 8x8-CU tile layout
+      __syncthreads();
     }
-    if (tid < 16) dec.tu[ub + (long)((cy >> 3) + (tid >> 2)) * g.w8 + (cx >> 3) + (tid & 3)] = (uint8_t)L.split;
+    if (tid < 16)
+      dec.tu[ub + (long)((cy >> 3) + (tid >> 2)) * g.w8 + (cx >> 3) + (tid & 3)] =
+          (uint8_t)(L.split | L.qsplit[((tid >> 3) << 1) | ((tid >> 1) & 1)]);
   }
   const bool whole = L.qtype[0] == 0;
   const int ntiles = whole ? 6 : 8;

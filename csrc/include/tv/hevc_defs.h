@@ -464,9 +464,9 @@ TV_HD int deblock_edge_bs(const uint8_t* cu_log2, const uint8_t* intra, const ui
   if (sp == sq) {
     const int m = ~((1 << sp) - 1);
     if ((xp & m) == (xq & m) && (yp & m) == (yq & m)) {
-      // inside one CU: an edge only between the 16x16 TBs of an RQT-split 32x32 inter CU
-      // (one motion: bS 1 iff either TB has luma levels)
-      if (!(tu && tu[up] && (((xp ^ xq) | (yp ^ yq)) & 16))) return 0;
+      // inside one CU: an edge only between the TBs of an RQT-split inter CU (half its size;
+      // one motion: bS 1 iff either TB has luma levels)
+      if (!(tu && tu[up] && (((xp ^ xq) | (yp ^ yq)) & (1 << (sp - 1))))) return 0;
       return ((cbf[up] & 1) || (cbf[uq] & 1)) ? 1 : 0;
     }
   }
@@ -490,13 +490,14 @@ TV_HD int deblock_edge_bs(const uint8_t* cu_log2, const uint8_t* intra, const ui
 // (640x360, 32 frames, QP 22-37): -1.51 % BD-rate smooth, -1.15 % textured against no RQT;
 // a quarter instead of half: -0.5 / -0.2 %.
 constexpr int kRqtClean = 6;
-TV_HD bool rqt_split(const int* sad4) {
+constexpr int kRqtMinLog2 = 4;  // 32x32 and 16x16 inter CUs may split (TV_RQT16 experiments)
+TV_HD bool rqt_split(const int* sad4, int npx = 256) {  // npx: samples per quadrant
   int lo = sad4[0], hi = sad4[0];
   for (int q = 1; q < 4; ++q) {
     lo = sad4[q] < lo ? sad4[q] : lo;
     hi = sad4[q] > hi ? sad4[q] : hi;
   }
-  return 2 * lo < hi && lo < 256 * kRqtClean;
+  return 2 * lo < hi && lo < npx * kRqtClean;
 }
 
 // Rough bin count of an mvd pair (encoder cost model; CPU and GPU use the same).
