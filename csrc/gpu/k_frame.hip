@@ -459,6 +459,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   const int wave = tid >> 6;
   const int c = wave < 2 ? 0 : wave - 1;
   const int n = c ? 16 : 32, T = c ? kSaoTc : kSaoT, w = c ? g.W / 2 : g.W;
+  const int nsh = c ? 4 : 5;  // log2 n: the sample index splits with shifts, not a runtime division
   const int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
   const int iters = c ? 4 : 8;
   const uint8_t* S = src.plane(c, b, g) + (long)(cy * n) * w + cx * n;
@@ -466,7 +467,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
 #pragma unroll
   for (int k = 0; k < 8; ++k) {  // source samples of this lane, loads in flight together
     const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
-    sv[k] = k < iters ? S[(i / n) * w + i % n] : 0;
+    sv[k] = k < iters ? S[(i >> nsh) * w + (i & (n - 1))] : 0;
   }
   __syncthreads();
   // timing diagnostics only (TV_DIAG_SAO_STOP=1/2/3: stop after staging / statistics /
@@ -484,7 +485,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   for (int k = 0; k < 8; ++k) {
     if (k >= iters) break;
     const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
-    const int lx = i % n, ly = i / n;
+    const int lx = i & (n - 1), ly = i >> nsh;
     const int v = t[(ly + 1) * T + lx + 1];
     const int d16 = (sv[k] - v) * 16 + 1;
     const unsigned long long p64 = (unsigned long long)(long long)d16;
@@ -572,7 +573,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
     const int cc = i < 256 ? 0 : (i < 320 ? 1 : 2);
     const int j = cc == 0 ? i : i - 256 - (cc - 1) * 64;
     const int nd = cc ? 4 : 8, nn = cc ? 16 : 32, TT = cc ? kSaoTc : kSaoT, ww = cc ? g.W / 2 : g.W;
-    const int ly = j / nd, lx0 = 4 * (j % nd);
+    const int ly = j >> (cc ? 2 : 3), lx0 = 4 * (j & (nd - 1));  // nd = 4 / 8 dwords per row
     const int16_t* tt = tile + (cc == 0 ? 0 : kSaoT * kSaoT + (cc - 1) * kSaoTc * kSaoTc);
     const uint32_t p = prm[cc];
     int dx = 0, dy = 0;
