@@ -418,7 +418,8 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   // (lane & 15), so same-band lanes of a wave rarely hit one LDS address
   __shared__ int bh[3][32][16];
   for (int i = tid; i < 3 * (int)(sizeof(SaoStats) / 4); i += 256) reinterpret_cast<int*>(st)[i] = 0;
-  for (int i = tid; i < 3 * 32 * 16; i += 256) (&bh[0][0][0])[i] = 0;
+  if (kSaoBandOffsets)
+    for (int i = tid; i < 3 * 32 * 16; i += 256) (&bh[0][0][0])[i] = 0;
   {  // deblocked CTB + 1-sample ring as aligned dwords (a CTB edge is a multiple of 4, so a
      // dword is wholly inside or wholly outside the plane): luma 34 rows x 10 dwords, chroma
      // 18 x 6 each; every load is issued before the first LDS store
@@ -498,7 +499,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       const int f = e + 2 - (e > 0);  // category 1..4 -> field 0..3 (e = 0 is masked below)
       eo64[d] += (a >= 0 && bb >= 0 && e != 0) ? p64 << (16 * f) : 0ull;
     }
-    atomicAdd(&bh[c][v >> 3][lane & 15], (sv[k] - v) * 2048 + 1);  // band statistics
+    if (kSaoBandOffsets) atomicAdd(&bh[c][v >> 3][lane & 15], (sv[k] - v) * 2048 + 1);  // band statistics
   }
   int eo[4][4];
 #pragma unroll
@@ -525,7 +526,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   __shared__ SaoTables tab;
   __shared__ uint32_t prm[3];
   __syncthreads();
-  if (tid < 96) {  // fold the histogram copies into the band counters
+  if (kSaoBandOffsets && tid < 96) {  // fold the histogram copies into the band counters
     const int cc = tid >> 5, band = tid & 31;
     int tot = 0;
 #pragma unroll
@@ -538,11 +539,14 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
     if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)st[0].eo_n[0][1];
     return;
   }
-  if (tid < kSaoItems) sao_item(st, lam16, tid, tab);  // 144 offset/cost items in parallel
+  // 144 offset/cost items in parallel (the 96 band items only with band offsets on)
+  if (tid < kSaoItems && (kSaoBandOffsets || tid % 48 < 16)) sao_item(st, lam16, tid, tab);
   __syncthreads();
-  if (tid < 96) sao_window(tid, tab);  // 3 x 32 band windows
+  if (kSaoBandOffsets && tid < 96) sao_window(tid, tab);  // 3 x 32 band windows
   __syncthreads();
-  if (wave < 3) {  // best band position of component `wave`: first minimum over 32 windows
+  if (!kSaoBandOffsets) {
+    if (tid < 3) bpos[tid] = 0;
+  } else if (wave < 3) {  // best band position of component `wave`: first minimum over 32 windows
     long long j = lane < 32 ? tab.win_j[wave][lane] : LLONG_MAX;
     int p = lane < 32 ? lane : 64;
 #pragma unroll

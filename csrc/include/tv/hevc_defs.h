@@ -735,6 +735,10 @@ TV_HD uint32_t sao_pack_bo(const SaoTables& t, int c, int pos) {
 TV_HD long long sao_eo_j(const SaoTables& t, int c, int cls) {
   return t.eo_j[c][cls][0] + t.eo_j[c][cls][1] + t.eo_j[c][cls][2] + t.eo_j[c][cls][3];
 }
+// Band offsets are not chosen: with this RD estimate they cost more than they gain (golden,
+// 640x360, 32 frames, QP 22-37: dropping them -1.04 % BD-rate smooth, -0.38 % textured) and
+// their statistics were a third of k_sao_decide's statistics phase (LDS histogram atomics).
+constexpr bool kSaoBandOffsets = false;
 // Rate in bits: type TR bins (off 1, band 2, edge 2), EO class 2, band position 5, offsets.
 // the final choice given each component's best band position (sao_best_band; the GPU finds
 // it with a wave-parallel argmin)
@@ -749,7 +753,7 @@ TV_HD void sao_finish_pos(const SaoTables& t, long long lam16, const int* pos, u
         out[0] = sao_pack_eo(t, 0, cls);
       }
     }
-    if (t.win_j[0][pos[0]] + lam16 * 7 < best) out[0] = sao_pack_bo(t, 0, pos[0]);
+    if (kSaoBandOffsets && t.win_j[0][pos[0]] + lam16 * 7 < best) out[0] = sao_pack_bo(t, 0, pos[0]);
   }
   {  // chroma: one type (and EO class) for Cb and Cr
     long long best = lam16 * 1;
@@ -762,7 +766,7 @@ TV_HD void sao_finish_pos(const SaoTables& t, long long lam16, const int* pos, u
         out[2] = sao_pack_eo(t, 2, cls);
       }
     }
-    if (t.win_j[1][pos[1]] + t.win_j[2][pos[2]] + lam16 * 12 < best) {
+    if (kSaoBandOffsets && t.win_j[1][pos[1]] + t.win_j[2][pos[2]] + lam16 * 12 < best) {
       out[1] = sao_pack_bo(t, 1, pos[1]);
       out[2] = sao_pack_bo(t, 2, pos[2]);
     }

@@ -206,7 +206,7 @@ class WorkQueue:
 
 # bumped whenever the encoders' output for identical settings changes (a checkpoint written
 # by an older build must not be mixed into a newer job's output)
-BITSTREAM_VERSION = 7
+BITSTREAM_VERSION = 8
 
 
 class Checkpoint:
