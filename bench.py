@@ -70,7 +70,7 @@ def _batch_for(args, local: int, codec: str, w: int, h: int):
     from thinvids_amd.worker.encoder import EncodeSpec, auto_batch, device_budget, engine_bytes
 
     spec = EncodeSpec(w, h, qp=args.qp, gop=args.gop, sao=args.sao, codec=codec,
-                      bframes=args.bframes if codec == "hevc" else 1)
+                      bframes=args.bframes if codec == "hevc" else 1, wpp=args.wpp, rqt=args.rqt, pintra=args.pintra)
     if args.batch:
         return args.batch, {"batch": args.batch, "source": "--batch"}
     if args.cpu:
@@ -613,6 +613,12 @@ def main() -> None:
     ap.add_argument("--qindex", type=int, default=0, help="AV1 q-index (0 = matched to --qp)")
     ap.add_argument("--kbps", type=float, default=0.0, help="2-pass rate control to this kbps per 30 fps stream")
     ap.add_argument("--no-4k", action="store_true", help="skip the 4K pass of the default 1080p run")
+    ap.add_argument("--no-wpp", dest="wpp", action="store_false",
+                    help="one CABAC substream per slice (coded on the host) instead of WPP rows coded on the GPU")
+    ap.add_argument("--no-rqt", dest="rqt", action="store_false", help="HEVC: no residual quadtree")
+    ap.add_argument("--no-pintra", dest="pintra", action="store_false", help="HEVC: no intra CUs in P pictures")
+    ap.add_argument("--entropy", choices=("gpu", "host"), default=None,
+                    help="where WPP substreams are CABAC-coded (default gpu; TV_ENTROPY); same bytes either way")
     ap.add_argument("--cpu", action="store_true",
                     help="rehearsal on CPU: gloo ranks + the golden encoders (models/cpu_engines.py), tiny geometry")
     args = ap.parse_args()
@@ -684,8 +690,9 @@ def hevc_pass(args, world, rank, local, dev, cpus):
     batch, sizing = _batch_for(args, local, "hevc", w, h)
     if args.cpu:
         from thinvids_amd.models.cpu_engines import CpuHevcEngine as GpuEngine  # noqa: F811
+    tools = dict(wpp=args.wpp, rqt=args.rqt, pintra=args.pintra, entropy=args.entropy)
     eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=args.sao,
-                    seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes)
+                    seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes, **tools)
     post = _PostQueue(local, args.cpu)
     # 2-pass: a second engine runs the fast first pass (SAO off: its statistics, decision and
     # filter are ~15 % of the GPU step and only fine-tune the reconstruction; the measured
@@ -696,7 +703,7 @@ def hevc_pass(args, world, rank, local, dev, cpus):
         import concurrent.futures as cf
 
         eng1 = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=False,
-                         seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes)
+                         seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes, **tools)
         pre = cf.ThreadPoolExecutor(1, initializer=None if args.cpu else (lambda: torch.cuda.set_device(local)))
 
     def comm(segs, sse):
@@ -818,6 +825,9 @@ def hevc_pass(args, world, rank, local, dev, cpus):
                 "last_step_engine_wall_ms": round(tm["wall_ms"], 2),
                 "last_step_entropy_cpu_ms": round(tm["entropy_cpu_ms"], 2),
                 "last_step_coef_mb_d2h": round(tm["coef_mb"], 2),
+                "entropy": (dict(eng.entropy_stats(), wpp=args.wpp, where=getattr(eng, "entropy", "host"))
+                            if hasattr(eng, "entropy_stats") else {"wpp": args.wpp, "where": "cpu rehearsal"}),
+                "coding_tools": {"wpp": args.wpp, "rqt": args.rqt, "pintra": args.pintra},
                 "per_rank_cpu": [{"busy_cores": r[0], "pinned_cpus": int(r[1]), "cabac_threads": int(r[2])}
                                  for r in ranks],
                 "step_ms": step_ms,

@@ -58,9 +58,7 @@ void* tv_cpu_encoder_new(int width, int height, int qp, int deblock, int range, 
   cfg.width = width;
   cfg.height = height;
   cfg.qp = qp;
-  cfg.deblock = (deblock & 1) != 0;  // bit 0: deblocking, bit 1: SAO, bit 2: WPP
-  cfg.sao = (deblock & 2) != 0;
-  cfg.wpp = (deblock & 4) != 0;
+  cfg.set_flags(deblock);  // 1 deblocking, 2 SAO, 4 WPP, 8 no RQT, 16 no intra-in-P
   cfg.max_merge_cand = max_merge;
   cfg.finalize();
   CpuEncoder* e = nullptr;  // a bad config becomes tv_last_error, not an abort across the FFI
@@ -73,9 +71,7 @@ void* tv_cpu_encoder_new_b(int width, int height, int qp, int deblock, int range
   cfg.width = width;
   cfg.height = height;
   cfg.qp = qp;
-  cfg.deblock = (deblock & 1) != 0;
-  cfg.sao = (deblock & 2) != 0;
-  cfg.wpp = (deblock & 4) != 0;
+  cfg.set_flags(deblock);
   cfg.max_merge_cand = max_merge;
   cfg.mgop = mgop;
   cfg.finalize();
@@ -111,9 +107,7 @@ void* tv_cpu_encoder_new_crf(int width, int height, int qp, int deblock, int ran
   cfg.width = width;
   cfg.height = height;
   cfg.qp = qp;
-  cfg.deblock = (deblock & 1) != 0;
-  cfg.sao = (deblock & 2) != 0;
-  cfg.wpp = (deblock & 4) != 0;
+  cfg.set_flags(deblock);
   cfg.max_merge_cand = max_merge;
   cfg.crf = crf;
   cfg.finalize();

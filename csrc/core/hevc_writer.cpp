@@ -933,10 +933,7 @@ SliceRefs slice_refs(const CodedPic& p) {
   return r;
 }
 
-size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
-                   std::vector<uint8_t>& out) {
-  BitWriter bw;
-  const SliceRefs* r = fd.refs;
+int write_slice_header(const SeqConfig& cfg, int slice_qp, const SliceRefs* r, int poc, bool idr, BitWriter& bw) {
   if (r) {
     idr = r->type == 2;
     poc = r->poc;
@@ -998,7 +995,15 @@ size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
     if (stype == 0) bw.put(0, 1);  // mvd_l1_zero_flag
     bw.ue((uint32_t)(5 - cfg.max_merge_cand));  // five_minus_max_num_merge_cand
   }
-  bw.se(fd.qp >= 0 ? fd.qp - cfg.qp : 0);  // slice_qp_delta (per-frame rate control)
+  bw.se(slice_qp >= 0 ? slice_qp - cfg.qp : 0);  // slice_qp_delta (per-frame rate control)
+  return nal;
+}
+
+size_t write_slice(const SeqConfig& cfg, const FrameData& fd, int poc, bool idr,
+                   std::vector<uint8_t>& out) {
+  BitWriter bw;
+  const int nal = write_slice_header(cfg, fd.qp, fd.refs, poc, idr, bw);
+  if (fd.refs) idr = fd.refs->type == 2;
   if (!cfg.wpp) {
     // byte_alignment()
     bw.put_bit(1);

@@ -30,6 +30,7 @@
 #include "k_encode.h"
 #include "tv/me_model.h"
 #include "tv/cpu_encoder.h"
+#include "tv/bitstream.h"
 #include "tv/hevc_codec.h"
 
 #define HIP_OK(x)                                                                        \
@@ -146,6 +147,13 @@ class Core {
     }
     const long B = c.batch;
     nctu_ = g_.wc * g_.hc;
+    // bit 2: WPP substreams, bit 3: no RQT, bit 4: no intra-in-P, bit 5: CABAC on the host
+    // (WPP streams are entropy-coded on the GPU unless bit 5 asks for the host writer)
+    gpu_ent_ = gpu_entropy(c);
+    if (gpu_ent_) {
+      HIP_OK(hipStreamCreateWithFlags(&estream_, hipStreamNonBlocking));
+      HIP_OK(hipEventCreateWithFlags(&eev_, hipEventDisableTiming));
+    }
     auto alloc_set = [&](FrameSet& f) {
       dev_alloc(&f.y, B * g_.ysz);
       dev_alloc(&f.u, B * g_.csz);
@@ -179,7 +187,7 @@ class Core {
     dev_alloc(&cmv_, 2 * B * nctu_ * 2 * sizeof(int16_t));
     dev_alloc(&ccost_, 2 * B * nctu_ * sizeof(int));
     if (c.mgop > 1) dev_alloc(&meout_, 2 * B * nctu_ * sizeof(CtbMeOut));
-    if (SeqConfig::pintra_default()) {  // intra-in-P scores and lists (tv/me_model.h pintra_*)
+    if (!(c.deblock & 16)) {  // intra-in-P scores and lists (tv/me_model.h pintra_*)
       uint8_t* m = nullptr;
       dev_alloc(&m, pintra_bytes(B, nctu_));
       const long n = B * nctu_;
@@ -191,10 +199,25 @@ class Core {
       pi_.cand = m + 4 * align(n * 16) + 256;
     }
     cap_ = g_.ysz + 2 * g_.csz;
-    // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed
-    slot_bytes_ = align(B * g_.usz) + align(B * g_.usz * 4) + align(B * nctu_ * 8) + align(B * nctu_ * 4) +
-                  align(B * nctu_ * 4) + align(B * 4) + align(B * nctu_ * 12) + align(B) + align(B * g_.usz) +
-                  align(B * g_.usz * 4) + align(B * g_.usz * 5) + align(B * cap_ * 2);
+    // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed |
+    // entropy head | entropy payload (device only: it lands in the host slot's packed region)
+    slot_bytes(B, g_, gpu_ent_, slot_bytes_, slot_host_bytes_);
+    if (gpu_ent_) {  // per-core entropy scratch (the entropy stream codes one picture at a time)
+      tok_cap_ = tok_capacity(B, g_);
+      dev_alloc(&ent_.skip, B * g_.usz);
+      dev_alloc(&ent_.midx, B * g_.usz);
+      dev_alloc(&ent_.ctb_cnt, B * nctu_ * sizeof(int));
+      dev_alloc(&ent_.ctb_off, B * nctu_ * sizeof(int));
+      dev_alloc(&ent_.seg_tok, B * sizeof(int));
+      dev_alloc(&ent_.tokens, tok_cap_ * sizeof(uint32_t));
+      dev_alloc(&ent_.stage, 3 * tok_cap_ + 16 * B * g_.hc);
+      EntropyTables* t = nullptr;
+      dev_alloc(&t, sizeof(EntropyTables));
+      std::unique_ptr<EntropyTables> ht(new EntropyTables());
+      entropy_tables(*ht);
+      HIP_OK(hipMemcpy(t, ht.get(), sizeof(EntropyTables), hipMemcpyHostToDevice));
+      ent_.tab = t;
+    }
     host_alloc(&qhost_, (size_t)c.gop * B);
     host_alloc(&quni_, (size_t)B);
     std::memset(quni_, c.qp, (size_t)B);
@@ -203,7 +226,7 @@ class Core {
     for (int k = 0; k < nslots_; ++k) {
       Slot& s = slots_[k];
       dev_alloc(&s.dev, slot_bytes_);
-      host_alloc(&s.host, slot_bytes_);
+      host_alloc(&s.host, slot_host_bytes_);
       // waited on by the fetch thread: see sync_mode()
       HIP_OK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming | (sync_mode() == 2 ? hipEventBlockingSync : 0)));
       s.pending = 0;
@@ -234,6 +257,9 @@ class Core {
     seq_.deblock = (c.deblock & 1) != 0;  // bit 0: deblocking, bit 1: SAO
     seq_.sao = (c.deblock & 2) != 0;
     seq_.max_merge_cand = c.max_merge;
+    seq_.wpp = (c.deblock & 4) != 0;
+    seq_.rqt = !(c.deblock & 8);
+    seq_.pintra = !(c.deblock & 16);
     seq_.mgop = c.mgop;
     if (c.mgop > 1) {
       const GopPlan gp = plan_gop(2 * c.mgop + 1, c.mgop);
@@ -254,16 +280,19 @@ class Core {
     const Geo g = make_geo(c.width, c.height);
     const size_t B = (size_t)c.batch, nctu = (size_t)g.wc * g.hc, set = B * (g.ysz + 2 * g.csz);
     const int ndpb = c.mgop > 1 ? plan_gop(2 * c.mgop + 1, c.mgop).dpb_size : 2;
-    const size_t qsz = (size_t)(g.W / 4) * (g.H / 4), cap = g.ysz + 2 * g.csz;
-    const size_t slot = align(B * g.usz) + align(B * g.usz * 4) + align(B * nctu * 8) + align(B * nctu * 4) +
-                        align(B * nctu * 4) + align(B * 4) + align(B * nctu * 12) + align(B) + align(B * g.usz) +
-                        align(B * g.usz * 4) + align(B * g.usz * 5) + align(B * cap * 2);
+    const size_t qsz = (size_t)(g.W / 4) * (g.H / 4);
+    const bool ge = gpu_entropy(c);
+    long slot = 0, slot_host = 0;
+    slot_bytes((long)B, g, ge, slot, slot_host);
+    const size_t ent = ge ? 2 * B * g.usz + 2 * B * nctu * sizeof(int) + B * sizeof(int) +
+                                tok_capacity((long)B, g) * (sizeof(uint32_t) + 3) + 16 * B * g.hc + sizeof(EntropyTables)
+                          : 0;
     dev = set + ndpb * (set + B * 16 * g.psz + B * qsz) + ((c.deblock & 2) ? set : 0) + 2 * set +
           B * 3 * sizeof(unsigned long long) + B * nctu * sizeof(int) + 2 * B * nctu * 2 * sizeof(int16_t) +
           2 * B * nctu * sizeof(int) + (c.mgop > 1 ? 2 * B * nctu * sizeof(CtbMeOut) : 0) +
-          (SeqConfig::pintra_default() ? pintra_bytes((long)B, (long)nctu) : 0) + (size_t)slot_count() * slot +
-          sizeof(RcTables);
-    host = (size_t)c.gop * B + B + (size_t)slot_count() * slot;
+          (!(c.deblock & 16) ? pintra_bytes((long)B, (long)nctu) : 0) + (size_t)slot_count() * slot +
+          sizeof(RcTables) + ent;
+    host = (size_t)c.gop * B + B + (size_t)slot_count() * slot_host;
   }
 
   ~Core() {
@@ -282,6 +311,9 @@ class Core {
     (void)hipFree(cmv_);
     (void)hipFree(ccost_);
     (void)hipFree(rc_);
+    for (void* p : {(void*)ent_.skip, (void*)ent_.midx, (void*)ent_.ctb_cnt, (void*)ent_.ctb_off, (void*)ent_.seg_tok,
+                    (void*)ent_.tokens, (void*)ent_.stage, (void*)ent_.tab})
+      (void)hipFree(p);
     (void)hipHostFree(qhost_);
     (void)hipHostFree(quni_);
     for (int k = 0; k < nslots_; ++k) {
@@ -296,11 +328,16 @@ class Core {
     (void)hipEventDestroy(iev_[0]);
     (void)hipEventDestroy(iev_[1]);
     (void)hipStreamDestroy(istream_);
+    if (estream_) (void)hipStreamDestroy(estream_);
+    if (eev_) (void)hipEventDestroy(eev_);
   }
 
   const std::vector<uint8_t>& segment(int b) const { return out_.at(b); }
   double sse(int b, int c) const { return sse_host_[b * 3 + c]; }
   long coef_bytes() const { return coef_bytes_; }
+  long ent_fallbacks() const { return ent_fallbacks_; }
+  int ent_status() const { return ent_status_; }
+  bool gpu_entropy_on() const { return gpu_ent_; }
   double entropy_ms() const { return entropy_ns_ / 1e6; }
   const Geo& geo() const { return g_; }
   // reconstruction of the segment's last display frame (after finish())
@@ -318,6 +355,25 @@ class Core {
     return n;
   }
   static long align(long n) { return (n + 255) & ~255L; }
+  // WPP streams are entropy-coded on the GPU (k_entropy.hip) unless bit 5 asks for the host
+  static bool gpu_entropy(const EngineCfg& c) { return (c.deblock & 4) && !(c.deblock & 32); }
+  // token capacity of the per-core entropy scratch: one token per luma sample of every
+  // segment (the bench's textured I pictures use about a third of that); a picture that
+  // needs more is coded by the host writer instead (status != 0)
+  static long tok_capacity(long B, const Geo& g) {
+    const char* e = getenv("TV_ENT_TOKENS_PER_PX");  // read per engine (tests shrink it)
+    const double per = e ? atof(e) : 1.0;
+    return (long)(per * B * g.ysz) + 1024;
+  }
+  // head of the entropy outputs: status, seg_bytes[B], row_bytes[B][hc]
+  static long ent_head_bytes(long B, const Geo& g) { return 16 + 4 * B + 4 * B * g.hc; }
+  static void slot_bytes(long B, const Geo& g, bool ge, long& dev, long& host) {
+    const long nctu = (long)g.wc * g.hc, cap = g.ysz + 2 * g.csz;
+    host = align(B * g.usz) + align(B * g.usz * 4) + align(B * nctu * 8) + align(B * nctu * 4) + align(B * nctu * 4) +
+           align(B * 4) + align(B * nctu * 12) + align(B) + align(B * g.usz) + align(B * g.usz * 4) +
+           align(B * g.usz * 5) + align(B * cap * 2) + (ge ? align(ent_head_bytes(B, g)) : 0);
+    dev = host + (ge ? align(B * cap) : 0);  // the payload: device side only (lands in `packed`)
+  }
   // qcost, gate list, pass lists, candidate list (16 bytes per CTB each), counters, candidate bytes
   static size_t pintra_bytes(long B, long nctu) { return 4 * align(B * nctu * 16) + 256 + align(B * nctu * 4); }
   struct Slot {
@@ -337,6 +393,8 @@ class Core {
     int16_t* packed;
     uint32_t* sao;
     int8_t* qp;
+    int* ent_head;     // GPU entropy: status, seg_bytes[B], row_bytes[B][hc]
+    uint8_t* ent_out;  // GPU entropy payload (device slot only)
   };
   Parts carve(uint8_t* base) const {
     const long B = cfg_.batch, U = g_.usz;
@@ -373,6 +431,10 @@ class Core {
     p.tu = q + 4 * B * U;
     q += align(B * U * 5);
     p.packed = reinterpret_cast<int16_t*>(q);
+    q += align(B * cap_ * 2);
+    p.ent_head = reinterpret_cast<int*>(q);
+    q += gpu_ent_ ? align(ent_head_bytes(B, g_)) : 0;
+    p.ent_out = q;
     p.count = nullptr;  // device count array lives in the scratch below
     return p;
   }
@@ -494,6 +556,81 @@ class Core {
     HIP_OK(hipEventRecord(ev, st));
     wait_event(ev);
   }
+  // GPU entropy: the head (status, sizes) and slice QPs, then the payload; false: the device
+  // could not code this picture (capacity), the caller falls back to the host writer
+  bool fetch_entropy(Slot& s, int B) {
+    thread_local hipStream_t ws = nullptr;
+    if (!ws) HIP_OK(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
+    wait_event(s.ev);
+    const Parts d = carve(s.dev), h = carve(s.host);
+    HIP_OK(hipMemcpyAsync(h.ent_head, d.ent_head, ent_head_bytes(cfg_.batch, g_), hipMemcpyDeviceToHost, ws));
+    HIP_OK(hipMemcpyAsync(h.qp, d.qp, B, hipMemcpyDeviceToHost, ws));
+    sleep_sync(ws);
+    if (h.ent_head[0] != 0) {
+      ent_fallbacks_++;
+      ent_status_ |= h.ent_head[0];
+      return false;
+    }
+    long total = 0;
+    for (int b = 0; b < B; ++b) total += h.ent_head[4 + b];
+    if (total > (long)cfg_.batch * cap_ * 2) throw std::runtime_error("entropy payload overflow");
+    if (total) HIP_OK(hipMemcpyAsync(h.packed, d.ent_out, total, hipMemcpyDeviceToHost, ws));
+    sleep_sync(ws);
+    coef_bytes_ += total;
+    return true;
+  }
+  // slice b of picture f from the GPU's substreams: header, entry points, emulation prevention
+  void assemble_slice(const Slot& s, int b, int f) {
+    const Parts h = carve(s.host);
+    const int* seg = h.ent_head + 4;
+    const int* rows = h.ent_head + 4 + cfg_.batch + (long)b * g_.hc;
+    long off = 0;
+    for (int k = 0; k < b; ++k) off += seg[k];
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(h.packed) + off;
+    std::vector<const uint8_t*> ptrs(g_.hc);
+    std::vector<size_t> sizes(g_.hc);
+    for (int r = 0; r < g_.hc; ++r) {
+      ptrs[r] = p;
+      sizes[r] = (size_t)rows[r];
+      p += rows[r];
+    }
+    const CodedPic& pic = plan_.pics[f];
+    BitWriter hdr;
+    const int nal = write_slice_header(seq_, h.qp[b], seq_.mgop > 1 ? &refs_[f] : nullptr, pic.disp, pic.type == 2, hdr);
+    finish_wpp_slice(hdr, ptrs.data(), sizes.data(), g_.hc, nal, slices_[b][f]);
+  }
+  EntropyArgs entropy_args(const Slot& s, const DecisionSet& dec, const CodedPic& pic) const {
+    EntropyArgs a{};
+    a.g = g_;
+    a.pic.type = pic.type;
+    a.pic.init_type = pic.type == 2 ? 0 : (pic.type == 1 ? 1 : 2);
+    a.pic.poc = pic.disp;
+    a.pic.ref_poc[0] = pic.ref[0];
+    a.pic.ref_poc[1] = pic.ref[1];
+    a.pic.sao = seq_.sao;
+    a.pic.rqt = seq_.rqt;
+    a.pic.max_merge = seq_.max_merge_cand;
+    a.dec = dec;
+    a.cs = slot_compact(s);
+    const Parts d = carve(s.dev);
+    a.sao = seq_.sao ? d.sao : nullptr;
+    a.skip = ent_.skip;
+    a.midx = ent_.midx;
+    a.ctb_cnt = ent_.ctb_cnt;
+    a.ctb_off = ent_.ctb_off;
+    a.seg_tok = ent_.seg_tok;
+    a.tokens = ent_.tokens;
+    a.tok_cap = tok_cap_;
+    a.stage = ent_.stage;
+    a.tab = ent_.tab;
+    a.status = d.ent_head;
+    a.seg_bytes = d.ent_head + 4;
+    a.row_bytes = d.ent_head + 4 + cfg_.batch;
+    a.out = d.ent_out;
+    a.out_cap = (long)cfg_.batch * cap_;
+    return a;
+  }
+
   void fetch_slot(Slot& s, int B, int ptype) {
     thread_local hipStream_t ws = nullptr;
     if (!ws) HIP_OK(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
@@ -655,16 +792,27 @@ class Core {
     if (!seq_.sao) launch_sse(src_, fin_set, g_, d_sse_, B, stream_);  // with SAO: summed by k_sao_decide
     stage("sse");
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(s.ev, stream_));
+    if (gpu_ent_) {  // entropy coding on its own stream: the next picture's kernels run meanwhile
+      HIP_OK(hipEventRecord(eev_, stream_));
+      HIP_OK(hipStreamWaitEvent(estream_, eev_, 0));
+      launch_entropy(entropy_args(s, dec, pic), B, estream_);
+      stage("entropy");
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipEventRecord(s.ev, estream_));
+    } else {
+      HIP_OK(hipEventRecord(s.ev, stream_));
+    }
     s.pending.store(B + 1, std::memory_order_release);
     // The slot's GPU wait + D2H runs on this core's one fetch thread (slots complete in
     // stream order, so a FIFO of waits loses nothing): one thread per core spins on the
     // completion events instead of one pool thread per in-flight slot, and the pool's
     // threads only ever run CABAC.
     fetch_->submit([this, &s, B, f] {
+      bool gpu = false;  // the GPU coded the picture: only the slice NALs are assembled here
       try {
         Range r("engine.d2h");
-        fetch_slot(s, B, plan_.pics[f].type);
+        gpu = gpu_ent_ && fetch_entropy(s, B);
+        if (!gpu) fetch_slot(s, B, plan_.pics[f].type);
       } catch (const std::exception& e) {
         fail(e);
         release(s, B + 1);
@@ -672,14 +820,18 @@ class Core {
       }
       release(s, 1);
       for (int b = 0; b < B; ++b)
-        pool_->submit([this, &s, b, f] {
+        pool_->submit([this, &s, b, f, gpu] {
           try {
-            Range r("engine.cabac_slice");
+            Range r(gpu ? "engine.slice_nal" : "engine.cabac_slice");
             const auto c0 = std::chrono::steady_clock::now();
             const CodedPic& p = plan_.pics[f];
-            expand_flags(s, b);
-            write_slice(seq_, host_view(s, b, seq_.mgop > 1 ? &refs_[f] : nullptr), p.disp, p.type == 2,
-                        slices_[b][f]);
+            if (gpu) {
+              assemble_slice(s, b, f);
+            } else {
+              expand_flags(s, b);
+              write_slice(seq_, host_view(s, b, seq_.mgop > 1 ? &refs_[f] : nullptr), p.disp, p.type == 2,
+                          slices_[b][f]);
+            }
             entropy_ns_ += std::chrono::duration_cast<std::chrono::nanoseconds>(
                                std::chrono::steady_clock::now() - c0).count();
           } catch (const std::exception& e) {
@@ -741,6 +893,21 @@ class Core {
   Geo g_;
   SeqConfig seq_;
   RcTables* rc_ = nullptr;
+  // GPU entropy coding (k_entropy.hip): its own stream per core, per-core scratch
+  bool gpu_ent_ = false;
+  hipStream_t estream_ = nullptr;
+  hipEvent_t eev_ = nullptr;
+  struct EntScratch {
+    uint8_t* skip = nullptr;
+    int8_t* midx = nullptr;
+    int *ctb_cnt = nullptr, *ctb_off = nullptr, *seg_tok = nullptr;
+    uint32_t* tokens = nullptr;
+    uint8_t* stage = nullptr;
+    EntropyTables* tab = nullptr;
+  } ent_;
+  long tok_cap_ = 0, slot_host_bytes_ = 0;
+  std::atomic<long> ent_fallbacks_{0};
+  std::atomic<int> ent_status_{0};
   bool qmap_given_ = false;  // an explicit QP map (2-pass plan) overrides in-engine CRF
   int8_t* qhost_ = nullptr;  // pinned [frame][segment] slice QPs of the current call
   int8_t* quni_ = nullptr;   // pinned: the sequence QP for every segment slot
@@ -872,6 +1039,17 @@ class Engine {
     double n = 0;
     for (int g = 0; g < used_; ++g) n += cores_[g]->entropy_ms();
     return n;
+  }
+  // GPU entropy coding: on?, pictures the host writer had to code instead (since construction)
+  // and the OR of their device status words (1 token capacity, 2/4 syntax, 8 payload capacity)
+  void entropy_stats(int& on, long& fallbacks, int& status) const {
+    on = cores_[0]->gpu_entropy_on() ? 1 : 0;
+    fallbacks = 0;
+    status = 0;
+    for (const auto& c : cores_) {
+      fallbacks += c->ent_fallbacks();
+      status |= c->ent_status();
+    }
   }
   const Geo& geo() const { return cores_[0]->geo(); }
   size_t dev_bytes() const {
@@ -1023,6 +1201,11 @@ void tv_engine_timing(void* e, double* gpu_ms, double* wall_ms, double* entropy_
   *wall_ms = E->wall_ms();
   *entropy_ms = E->entropy_ms();
   *coef_mb = E->coef_bytes() / 1e6;
+}
+void tv_engine_entropy_stats(void* e, int* on, long long* fallbacks, int* status) {
+  long f = 0;
+  static_cast<tv::gpu::Engine*>(e)->entropy_stats(*on, f, *status);
+  *fallbacks = f;
 }
 // The same for an engine not built yet (same arguments as tv_engine_new_b's geometry part)
 int tv_engine_estimate(int width, int height, int batch, int gop, int deblock, int mgop, unsigned long long* dev,

@@ -105,5 +105,46 @@ void launch_compact(DecisionSet dec, const Geo& g, CompactSet cs, int B, hipStre
 // intra << 2 | cbf << 3 | dir << 6 (dir = 1 when dec.dir is null)
 void launch_pack_flags(DecisionSet dec, uint8_t* flags, const Geo& g, int B, hipStream_t s);
 
+// ---- GPU CABAC (k_entropy.hip): WPP substreams of every slice of one picture -------------
+constexpr int kEntCtx = 160;  // >= tv::CTX_COUNT (static_assert in k_entropy.hip)
+struct EntropyPic {
+  int type;        // 2 I, 1 P, 0 B
+  int init_type;   // cabac initType: 0 I, 1 P, 2 B
+  int poc;         // B slices: POCs for the AMVP scaling
+  int ref_poc[2];
+  int sao, rqt, max_merge;
+};
+// context init states [initType][SliceQpY][ctx] (state | valMps << 6) and the coder tables
+struct EntropyTables {
+  uint8_t init[3][52][kEntCtx];
+  uint8_t lps[256];   // rangeTabLps[state][(range >> 6) & 3]
+  uint8_t tlps[64];   // transIdxLps
+};
+struct EntropyArgs {
+  Geo g;
+  EntropyPic pic;
+  DecisionSet dec;      // the slot's decision planes (qp, cu_log2, intra, ipm, mv, cbf, dir, mv1, tu)
+  CompactSet cs;        // the slot's compact levels (mask_y, mask_c, offset, total, packed)
+  const uint32_t* sao;  // the slot's SAO parameters (nullptr: SAO off)
+  // per-core scratch (the entropy stream runs one picture at a time)
+  uint8_t* skip;        // [B][usz] cu_skip_flag of the unit's CU
+  int8_t* midx;         // [B][usz] merge candidate matching the CU's motion (-1: none)
+  int* ctb_cnt;         // [B][nctu] tokens of each CTB
+  int* ctb_off;         // [B][nctu] exclusive scan of ctb_cnt within the segment
+  int* seg_tok;         // [B] tokens of each segment
+  uint32_t* tokens;     // token lists, segments back to back
+  long tok_cap;
+  uint8_t* stage;       // per row: 3 bytes per token + 16 (arithmetic coder output, bounded)
+  const EntropyTables* tab;
+  // the slot's outputs (device -> host in one head copy + one payload copy)
+  int* status;          // 0 ok; else the host codes this picture (capacity / consistency)
+  int* seg_bytes;       // [B] payload bytes per slice
+  int* row_bytes;       // [B][hc] bytes per WPP substream
+  uint8_t* out;         // the slices' substreams, slices back to back
+  long out_cap;
+};
+void launch_entropy(const EntropyArgs& a, int B, hipStream_t s);
+void entropy_tables(EntropyTables& t);
+
 }  // namespace gpu
 }  // namespace tv

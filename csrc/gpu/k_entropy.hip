@@ -1,0 +1,1085 @@
+// k_entropy.hip — HEVC CABAC on the GPU (entropy_coding_sync / WPP substreams).
+//
+// The host CABAC writer (csrc/core/hevc_writer.cpp) costs 8 busy cores per GPU on the bench
+// content and 15 on grain; on an 8-GPU node a rank owns 1/8 of the host.  Every syntax
+// decision is already fixed when a picture's kernels finish, so entropy coding splits into
+//   1. binarisation — data-parallel: one thread per CTB turns the CTB's decisions and compact
+//      levels into a token list (context-coded bins with their context index, bypass runs,
+//      terminate bins, WPP control marks), run twice: count, exclusive scan, write;
+//   2. arithmetic coding — serial per WPP substream: one workgroup per slice, one lane per CTB
+//      row; lane r starts once lane r-1 stored its contexts after CTB 1 (9.3.2.4), the
+//      context states live in LDS ([ctx][row] bytes), the coder state in registers;
+//   3. packing — the rows' bytes are compacted per slice for one device->host copy.
+// The host only writes the slice header, the entry points and emulation prevention.
+//
+// Byte-for-byte the output of tv::write_slice with SeqConfig::wpp (the CPU writer stays the
+// oracle: tests/test_gpu_entropy.py).  The per-CU skip / merge choice is made in a pre-pass
+// (k_ent_cu) so a CTB's cu_skip_flag context can read its left / upper neighbours'.
+// Reference: the reference entropy-codes in VA-API fixed function (worker/tasks.py:1573-1586).
+#include <stdexcept>
+
+#include "gpu_common.h"
+#include "k_encode.h"
+#include "tv/cabac.h"
+#include "tv/hevc_mvpred.h"
+
+namespace tv {
+namespace gpu {
+
+namespace {
+
+// ---- token format (32 bits, type in bits 30..31) ----------------------------------------
+//   CTX : bits 27..28 = number of bins n (1..3); bin i at bits 9i..9i+8 = ctx | bin << 8
+//   BYP : bits 16..20 = count (1..16), bits 0..15 = the bins, MSB first
+//   TERM: bit 0 = the terminating bin
+//   CTRL: 0 = SYNC (store the row's contexts for the row below), 1 = FLUSH (end of substream:
+//         flush the coder, '1' bit, byte alignment)
+constexpr uint32_t kTkCtx = 0u << 30, kTkByp = 1u << 30, kTkTerm = 2u << 30, kTkCtrl = 3u << 30;
+constexpr uint32_t kCtrlSync = 0, kCtrlFlush = 1;
+static_assert(CTX_COUNT <= kEntCtx && kEntCtx <= 256, "context index must fit 8 bits");
+
+struct TokSink {
+  uint32_t* out;  // nullptr: count only
+  int n = 0;
+  uint32_t pc = 0, pb = 0;  // pending context bins / bypass bins
+  int npc = 0, npb = 0;
+  __device__ void put(uint32_t t) {
+    if (out) out[n] = t;
+    ++n;
+  }
+  __device__ void flush_c() {
+    if (npc) put(kTkCtx | ((uint32_t)npc << 27) | pc);
+    npc = 0;
+    pc = 0;
+  }
+  __device__ void flush_b() {
+    if (npb) put(kTkByp | ((uint32_t)npb << 16) | pb);
+    npb = 0;
+    pb = 0;
+  }
+  __device__ void bin(int b, int ctx) {
+    flush_b();
+    pc |= (uint32_t)(ctx | (b << 8)) << (9 * npc);
+    if (++npc == 3) flush_c();
+  }
+  // consecutive bypass bins are one run: equiprobable bins, so splitting or merging a run
+  // never changes the arithmetic code
+  __device__ void bypass(uint32_t v, int nb) {
+    flush_c();
+    while (nb > 0) {
+      const int take = tv_min(nb, 16 - npb);
+      nb -= take;
+      pb = (pb << take) | ((v >> nb) & ((1u << take) - 1));
+      npb += take;
+      if (npb == 16) flush_b();
+    }
+  }
+  __device__ void term(int b) {
+    flush_c();
+    flush_b();
+    put(kTkTerm | (uint32_t)b);
+  }
+  __device__ void ctrl(uint32_t c) {
+    flush_c();
+    flush_b();
+    put(kTkCtrl | c);
+  }
+};
+
+__constant__ uint8_t c_kCtxIdxMap4x4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+__constant__ uint8_t c_kGroupIdx[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+                                        8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
+__constant__ uint8_t c_kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
+__constant__ uint8_t c_scan4[3][16] = {{0, 4, 1, 8, 5, 2, 12, 9, 6, 3, 13, 10, 7, 14, 11, 15},
+                                       {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+                                       {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15}};
+
+// Sub-block scans of every TB size (log2 - 2 = 0..3) and scanIdx: raster index (ys << l) + xs
+// of scan position i, and its inverse (hevc_defs.h subblock_pos).
+struct SbTab {
+  uint8_t pos[4][3][64], inv[4][3][64];
+};
+constexpr SbTab make_sbtab() {
+  SbTab t{};
+  for (int l = 0; l < 4; ++l)
+    for (int sc = 0; sc < 3; ++sc)
+      for (int i = 0; i < (1 << (2 * l)); ++i) {
+        int xs = 0, ys = 0;
+        if (l == 1) {
+          const uint8_t q = sc == 0 ? kScanDiag2x2[i] : (sc == 1 ? kScanHor2x2[i] : kScanVer2x2[i]);
+          xs = q & 3;
+          ys = q >> 2;
+        } else if (l == 2) {
+          xs = kScanDiag4x4[i] & 3;
+          ys = kScanDiag4x4[i] >> 2;
+        } else if (l == 3) {
+          xs = kScanDiag8x8.s[i] & 7;
+          ys = kScanDiag8x8.s[i] >> 3;
+        }
+        t.pos[l][sc][i] = (uint8_t)((ys << l) + xs);
+        t.inv[l][sc][(ys << l) + xs] = (uint8_t)i;
+      }
+  return t;
+}
+__constant__ SbTab c_sb = make_sbtab();
+
+// One segment's picture, as the binariser sees it (device pointers at segment b).
+struct SegView {
+  const uint8_t *cu_log2, *intra, *ipm, *cbf, *tu, *dir;
+  const int16_t *mv, *mv1;
+  const uint8_t* skip;
+  const int8_t* midx;
+  const unsigned long long* mask_y;
+  const unsigned* mask_c;
+  const int* sb_off;
+  const int16_t* packed;
+  const uint32_t* sao;
+  int w8, wc, hc, W, H;
+};
+
+__device__ inline SegView seg_view(const EntropyArgs& a, int b) {
+  const long U = a.g.usz, nctu = (long)a.g.wc * a.g.hc;
+  SegView v;
+  v.cu_log2 = a.dec.cu_log2 + b * U;
+  v.intra = a.dec.intra + b * U;
+  v.ipm = a.dec.ipm + b * U;
+  v.cbf = a.dec.cbf + b * U;
+  v.tu = a.dec.tu ? a.dec.tu + b * U : nullptr;
+  v.dir = a.dec.dir ? a.dec.dir + b * U : nullptr;
+  v.mv = a.dec.mv + b * U * 2;
+  v.mv1 = a.dec.mv1 ? a.dec.mv1 + b * U * 2 : nullptr;
+  v.skip = a.skip + b * U;
+  v.midx = a.midx + b * U;
+  v.mask_y = a.cs.mask_y + b * nctu;
+  v.mask_c = a.cs.mask_c + b * nctu;
+  v.sb_off = a.cs.offset + b * nctu;
+  long base = 0;  // segments' packed levels are back to back (k_sb_pack)
+  for (int k = 0; k < b; ++k) base += a.cs.total[k];
+  v.packed = a.cs.packed + base * 16;
+  v.sao = a.sao ? a.sao + b * nctu * 3 : nullptr;
+  v.w8 = a.g.w8;
+  v.wc = a.g.wc;
+  v.hc = a.g.hc;
+  v.W = a.g.W;
+  v.H = a.g.H;
+  return v;
+}
+
+__device__ inline int unit_of(const SegView& v, int x, int y) { return (y >> 3) * v.w8 + (x >> 3); }
+__device__ inline Motion motion_of(const SegView& v, int u) {
+  Motion m;
+  m.dir = v.dir ? v.dir[u] : 1;
+  m.mv[0] = Mv{v.mv[2 * u], v.mv[2 * u + 1]};
+  if (v.mv1) m.mv[1] = Mv{v.mv1[2 * u], v.mv1[2 * u + 1]};
+  return m;
+}
+__device__ inline int cu_cbf(const SegView& v, int x0, int y0, int log2) {
+  const int u = unit_of(v, x0, y0);
+  if (!(v.tu && v.tu[u])) return v.cbf[u];
+  const int h = 1 << (log2 - 1);
+  int c = 0;
+  for (int q = 0; q < 4; ++q) c |= v.cbf[unit_of(v, x0 + (q & 1) * h, y0 + (q >> 1) * h)];
+  return c;
+}
+
+// Index of the PU's vector in its P-slice merge list, or -1 (hevc_writer.cpp merge_index_p).
+__device__ int merge_index_p(const SegView& v, int x0, int y0, int N, Mv mv, int maxc) {
+  auto get = [&](int xn, int yn, Mv& m) {
+    const int u = unit_of(v, xn, yn);
+    if (v.intra[u]) return false;
+    m.x = v.mv[2 * u];
+    m.y = v.mv[2 * u + 1];
+    return true;
+  };
+  Mv a1, b1, b0, a0, b2;
+  int n = 0;
+  const bool avA1 = x0 > 0 && get(x0 - 1, y0 + N - 1, a1);
+  if (avA1) {
+    if (a1 == mv) return 0;
+    if (++n == maxc) return -1;
+  }
+  const bool avB1 = y0 > 0 && get(x0 + N - 1, y0 - 1, b1);
+  const bool fB1 = avB1 && !(avA1 && a1 == b1);
+  if (fB1) {
+    if (b1 == mv) return n;
+    if (++n == maxc) return -1;
+  }
+  const bool avB0 = zscan_available(x0, y0, x0 + N, y0 - 1, v.W, v.H) && get(x0 + N, y0 - 1, b0);
+  const bool fB0 = avB0 && !(avB1 && b1 == b0);
+  if (fB0) {
+    if (b0 == mv) return n;
+    if (++n == maxc) return -1;
+  }
+  const bool avA0 = zscan_available(x0, y0, x0 - 1, y0 + N, v.W, v.H) && get(x0 - 1, y0 + N, a0);
+  const bool fA0 = avA0 && !(avA1 && a1 == a0);
+  if (fA0) {
+    if (a0 == mv) return n;
+    if (++n == maxc) return -1;
+  }
+  const bool avB2 = x0 > 0 && y0 > 0 && get(x0 - 1, y0 - 1, b2);
+  if (avB2 && !(avA1 && a1 == b2) && !(avB1 && b1 == b2) && (int)avA1 + (int)fB1 + (int)fB0 + (int)fA0 < 4) {
+    if (b2 == mv) return n;
+    if (++n == maxc) return -1;
+  }
+  return (mv.x == 0 && mv.y == 0) ? n : -1;
+}
+
+__device__ inline int mvd_cost(int d) {
+  int a = d < 0 ? -d : d;
+  if (a == 0) return 1;
+  if (a == 1) return 3;
+  int vv = a - 2, k = 1, n = 0;
+  while (vv >= (1 << k)) {
+    vv -= 1 << k;
+    ++k;
+    ++n;
+  }
+  return 3 + n + 1 + k;
+}
+
+// ------------------------------------------------------------------ binariser (one CTB)
+struct CtbBinariser {
+  const SegView& v;
+  const EntropyPic& p;
+  TokSink& s;
+  bool err = false;
+
+  __device__ int unit(int x, int y) const { return unit_of(v, x, y); }
+  __device__ void bin(int b, int ctx) { s.bin(b, ctx); }
+  __device__ int skip_inc(int x0, int y0) const {
+    int inc = 0;
+    if (x0 > 0 && v.skip[unit(x0 - 1, y0)]) ++inc;
+    if (y0 > 0 && v.skip[unit(x0, y0 - 1)]) ++inc;
+    return inc;
+  }
+
+  __device__ void sao(int cx, int cy) {
+    const uint32_t off = sao_off_param();
+    const uint32_t* q = v.sao ? v.sao + 3 * (cy * v.wc + cx) : nullptr;
+    const uint32_t pr[3] = {q ? q[0] : off, q ? q[1] : off, q ? q[2] : off};
+    auto same = [&](const uint32_t* o) { return o[0] == pr[0] && o[1] == pr[1] && o[2] == pr[2]; };
+    if (cx > 0) {
+      const bool m = q && same(q - 3);
+      bin(m, CTX_SAO_MERGE);
+      if (m) return;
+    }
+    if (cy > 0) {
+      const bool m = q && same(q - 3 * v.wc);
+      bin(m, CTX_SAO_MERGE);
+      if (m) return;
+    }
+    for (int c = 0; c < 3; ++c) {
+      const int t = sao_type(pr[c]);
+      if (c < 2) {
+        bin(t != 0, CTX_SAO_TYPE);
+        if (t) s.bypass(t == 2, 1);
+      }
+      if (!t) continue;
+      for (int i = 0; i < 4; ++i) {  // sao_offset_abs: TR, cMax 7
+        const int a = tv_abs(sao_offset(pr[c], i));
+        if (a < kSaoMaxOff) s.bypass(((1u << a) - 1) << 1, a + 1);
+        else s.bypass((1u << a) - 1, a);
+      }
+      if (t == 1) {
+        for (int i = 0; i < 4; ++i)
+          if (sao_offset(pr[c], i)) s.bypass(sao_offset(pr[c], i) < 0, 1);
+        s.bypass((uint32_t)sao_class(pr[c]), 5);
+      } else if (c < 2) {
+        s.bypass((uint32_t)sao_class(pr[c]), 2);
+      }
+    }
+  }
+
+  __device__ void merge_idx_syntax(int idx) {
+    if (p.max_merge <= 1) return;
+    bin(idx > 0, CTX_MERGE_IDX);
+    for (int i = 1; i < p.max_merge - 1 && idx >= i; ++i) s.bypass(idx > i, 1);
+  }
+  __device__ void eg1(uint32_t val) {
+    int k = 1;
+    while (val >= (1u << k)) {
+      s.bypass(1, 1);
+      val -= 1u << k;
+      ++k;
+    }
+    s.bypass(0, 1);
+    s.bypass(val, k);
+  }
+  __device__ void mvd(int dx, int dy) {
+    const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
+    bin(ax > 0, CTX_MVD_G0);
+    bin(ay > 0, CTX_MVD_G0);
+    if (ax > 0) bin(ax > 1, CTX_MVD_G1);
+    if (ay > 0) bin(ay > 1, CTX_MVD_G1);
+    if (ax > 0) {
+      if (ax > 1) eg1((uint32_t)(ax - 2));
+      s.bypass(dx < 0, 1);
+    }
+    if (ay > 0) {
+      if (ay > 1) eg1((uint32_t)(ay - 2));
+      s.bypass(dy < 0, 1);
+    }
+  }
+
+  // ---- residual_coding (7.3.8.11) from the compact levels ----
+  struct Tb {
+    uint64_t nz, m;
+    int base, gw, skipc;
+    const int16_t* groups;
+  };
+  __device__ void tb_view(int c, int x, int y, int log2N, Tb& t) const {
+    const int nsb = 1 << (log2N - 2), sh = c ? 4 : 5;
+    t.gw = c ? 4 : 8;
+    const int ctb = (y >> sh) * v.wc + (x >> sh);
+    const uint64_t my = v.mask_y[ctb];
+    t.m = c ? (uint64_t)v.mask_c[ctb] : my;
+    t.base = (c == 2 ? 16 : 0) + ((y & ((1 << sh) - 1)) >> 2) * t.gw + ((x & ((1 << sh) - 1)) >> 2);
+    const uint64_t row = (1ull << nsb) - 1;
+    t.nz = 0;
+    for (int ys = 0; ys < nsb; ++ys) t.nz |= ((t.m >> (t.base + ys * t.gw)) & row) << (ys * nsb);
+    t.groups = v.packed + (long)v.sb_off[ctb] * 16;
+    t.skipc = c ? __popcll(my) : 0;
+  }
+  __device__ const int16_t* group_of(const Tb& t, int log2N, int r) const {
+    const int bit = t.base + (r >> (log2N - 2)) * t.gw + (r & ((1 << (log2N - 2)) - 1));
+    return t.groups + (long)(t.skipc + __popcll(t.m & ((1ull << bit) - 1))) * 16;
+  }
+  // bit n: scan position n of the group is non-zero
+  __device__ unsigned sig_mask(const int16_t* g, int scanIdx) const {
+    const uint4 lo = *reinterpret_cast<const uint4*>(g), hi = *reinterpret_cast<const uint4*>(g + 8);
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    unsigned raster = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      raster |= (((w[j] & 0xffffu) != 0) ? 1u : 0u) << (2 * j) | (((w[j] >> 16) != 0) ? 1u : 0u) << (2 * j + 1);
+    unsigned m = 0;
+#pragma unroll
+    for (int n = 0; n < 16; ++n) m |= ((raster >> c_scan4[scanIdx][n]) & 1u) << n;
+    return m;
+  }
+  __device__ void last_prefix(int pos, int log2N, int cIdx, int base) {
+    const int prefix = c_kGroupIdx[pos];
+    int off, shift;
+    if (cIdx == 0) {
+      off = 3 * (log2N - 2) + ((log2N - 1) >> 2);
+      shift = (log2N + 1) >> 2;
+    } else {
+      off = 15;
+      shift = log2N - 2;
+    }
+    const int cmax = (log2N << 1) - 1;
+    for (int i = 0; i < prefix; ++i) bin(1, base + off + (i >> shift));
+    if (prefix < cmax) bin(0, base + off + (prefix >> shift));
+  }
+  __device__ void last_suffix(int pos) {
+    const int prefix = c_kGroupIdx[pos];
+    if (prefix > 3) s.bypass((uint32_t)(pos - c_kMinInGroup[prefix]), (prefix >> 1) - 1);
+  }
+  __device__ void remaining(int val, int rice) {
+    if (val < (4 << rice)) {
+      const int pfx = val >> rice;
+      s.bypass(((1u << (pfx + 1)) - 2) << rice | (uint32_t)(val & ((1 << rice) - 1)), pfx + 1 + rice);
+    } else {
+      int k = rice + 1, ones = 0;
+      uint32_t r = (uint32_t)(val - (4 << rice));
+      while (r >= (1u << k)) {
+        r -= 1u << k;
+        ++k;
+        ++ones;
+      }
+      const int np = 4 + ones + 1;
+      for (int done = 0; done < np - 1;) {  // np - 1 ones, then a zero
+        const int take = tv_min(np - 1 - done, 16);
+        s.bypass((1u << take) - 1, take);
+        done += take;
+      }
+      s.bypass(0, 1);
+      s.bypass(r, k);
+    }
+  }
+  __device__ static int sig_pattern(int pc, int sc, int n) {
+    const int pos = c_scan4[sc][n], xp = pos & 3, yp = pos >> 2;
+    if (pc == 0) return (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+    if (pc == 1) return (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
+    if (pc == 2) return (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
+    return 2;
+  }
+  __device__ void residual(const Tb& t, int log2N, int cIdx, int scanIdx) {
+    const int nsb = 1 << (log2N - 2), lsb = log2N - 2;
+    if (!t.nz) {
+      err = true;
+      return;
+    }
+    // last significant sub-block in scan order, then its last non-zero position
+    const uint8_t* sbpos = c_sb.pos[lsb][scanIdx];
+    const uint8_t* sbinv = c_sb.inv[lsb][scanIdx];
+    int lastSb = 0;
+    for (uint64_t bb = t.nz; bb; bb &= bb - 1) lastSb = tv_max(lastSb, (int)sbinv[__ffsll((long long)bb) - 1]);
+    const int lxs = sbpos[lastSb] & (nsb - 1), lys = sbpos[lastSb] >> lsb;
+    const unsigned lastMask = sig_mask(group_of(t, log2N, lys * nsb + lxs), scanIdx);
+    const int lastN = 31 - __clz(lastMask);
+    {
+      int xc, yc;
+      coef_pos_in_sb(scanIdx, lastN, xc, yc);
+      int lx = (lxs << 2) + xc, ly = (lys << 2) + yc;
+      if (scanIdx == 2) {
+        const int tmp = lx;
+        lx = ly;
+        ly = tmp;
+      }
+      last_prefix(lx, log2N, cIdx, CTX_LAST_X);
+      last_prefix(ly, log2N, cIdx, CTX_LAST_Y);
+      last_suffix(lx);
+      last_suffix(ly);
+    }
+    const int sizeOff = log2N == 3 ? (scanIdx == 0 ? 9 : 15) : (cIdx == 0 ? 21 : 12);
+    const int compOff = CTX_SIG + (cIdx ? 27 : 0);
+    uint64_t coded = 0;
+    int c1 = 1;
+    for (int i = lastSb; i >= 0; --i) {
+      const int r = sbpos[i], xs = r & (nsb - 1), ys = r >> lsb;
+      const bool any = (t.nz >> r) & 1;
+      const int right = xs < nsb - 1 ? (int)((coded >> (r + 1)) & 1) : 0;
+      const int below = ys < nsb - 1 ? (int)((coded >> (r + nsb)) & 1) : 0;
+      bool inferDc = false;
+      if (i < lastSb && i > 0) {
+        bin(any ? 1 : 0, CTX_CSBF + (right | below) + (cIdx ? 2 : 0));
+        if (!any) continue;
+        inferDc = true;
+      }
+      coded |= 1ull << r;
+      const int16_t* g = any ? group_of(t, log2N, r) : nullptr;
+      const unsigned m = i == lastSb ? lastMask : (any ? sig_mask(g, scanIdx) : 0u);
+      const int prevCsbf = right + (below << 1);
+      const int add = log2N == 2 ? compOff : compOff + sizeOff + ((cIdx == 0 && i > 0) ? 3 : 0);
+      const int nStart = (i == lastSb) ? lastN - 1 : 15;
+      const bool dcInferred = inferDc && (m & ((2u << nStart) - 2)) == 0;
+      for (int n = nStart; n >= 1; --n) {
+        const int pat = log2N == 2 ? c_kCtxIdxMap4x4[c_scan4[scanIdx][n]] : sig_pattern(prevCsbf, scanIdx, n);
+        bin((m >> n) & 1, add + pat);
+      }
+      if (nStart >= 0 && !dcInferred) {
+        const int pat0 = log2N == 2 ? c_kCtxIdxMap4x4[c_scan4[scanIdx][0]] : sig_pattern(prevCsbf, scanIdx, 0);
+        bin(m & 1, (log2N > 2 && i == 0) ? compOff : add + pat0);
+      }
+      // levels in reverse scan order
+      int absv[16];
+      uint32_t sbits = 0;
+      int cnt = 0;
+      for (unsigned sm = m; sm; ++cnt) {
+        const int n = 31 - __clz(sm);
+        sm &= ~(1u << n);
+        const int x = g[c_scan4[scanIdx][n]];
+        absv[cnt] = x < 0 ? -x : x;
+        sbits = (sbits << 1) | (x < 0 ? 1u : 0u);
+      }
+      int ctxSet = (i > 0 && cIdx == 0) ? 2 : 0;
+      if (c1 == 0) ++ctxSet;
+      c1 = 1;
+      const int g1base = CTX_G1 + 4 * ctxSet + (cIdx ? 16 : 0);
+      const int nG1 = cnt < 8 ? cnt : 8;
+      int firstG2 = -1;
+      for (int k = 0; k < nG1; ++k) {
+        const int bn = absv[k] > 1;
+        bin(bn, g1base + c1);
+        if (bn) {
+          c1 = 0;
+          if (firstG2 < 0) firstG2 = k;
+        } else if (c1 > 0 && c1 < 3) {
+          ++c1;
+        }
+      }
+      if (firstG2 >= 0) bin(absv[firstG2] > 2, CTX_G2 + ctxSet + (cIdx ? 4 : 0));
+      if (cnt) s.bypass(sbits, cnt);
+      int rice = 0;
+      bool firstC2 = true;
+      for (int k = 0; k < cnt; ++k) {
+        const int base = (k < 8) ? (firstC2 ? 3 : 2) : 1;
+        if (absv[k] >= base) {
+          remaining(absv[k] - base, rice);
+          if (absv[k] > 3 * (1 << rice)) rice = tv_min(rice + 1, 4);
+        }
+        if (absv[k] >= 2) firstC2 = false;
+      }
+    }
+  }
+
+  __device__ bool tu_split(int x0, int y0) const { return v.tu && v.tu[unit(x0, y0)]; }
+  __device__ void transform_split(int x0, int y0, int log2) {
+    const int h = 1 << (log2 - 1), l = log2 - 1;
+    int c[4], cb0 = 0, cr0 = 0;
+    for (int q = 0; q < 4; ++q) {
+      c[q] = v.cbf[unit(x0 + (q & 1) * h, y0 + (q >> 1) * h)];
+      cb0 |= (c[q] >> 1) & 1;
+      cr0 |= (c[q] >> 2) & 1;
+    }
+    bin(cb0, CTX_CBF_CHROMA + 0);
+    bin(cr0, CTX_CBF_CHROMA + 0);
+    for (int q = 0; q < 4; ++q) {
+      const int x = x0 + (q & 1) * h, y = y0 + (q >> 1) * h;
+      const int cl = c[q] & 1, cb = (c[q] >> 1) & 1, cr = (c[q] >> 2) & 1;
+      if (cb0) bin(cb, CTX_CBF_CHROMA + 1);
+      if (cr0) bin(cr, CTX_CBF_CHROMA + 1);
+      bin(cl, CTX_CBF_LUMA + 0);
+      Tb t;
+      if (cl) {
+        tb_view(0, x, y, l, t);
+        residual(t, l, 0, 0);
+      }
+      if (cb) {
+        tb_view(1, x >> 1, y >> 1, l - 1, t);
+        residual(t, l - 1, 1, 0);
+      }
+      if (cr) {
+        tb_view(2, x >> 1, y >> 1, l - 1, t);
+        residual(t, l - 1, 2, 0);
+      }
+    }
+  }
+  __device__ void transform_tree(int x0, int y0, int log2, bool intra, int mode) {
+    if (!intra && p.rqt) {
+      const bool split = tu_split(x0, y0);
+      bin(split ? 1 : 0, CTX_SPLIT_TF + 5 - log2);
+      if (split) {
+        transform_split(x0, y0, log2);
+        return;
+      }
+    }
+    const int cbf = v.cbf[unit(x0, y0)];
+    const int cl = cbf & 1, cb = (cbf >> 1) & 1, cr = (cbf >> 2) & 1;
+    bin(cb, CTX_CBF_CHROMA + 0);
+    bin(cr, CTX_CBF_CHROMA + 0);
+    if (intra || cb || cr) bin(cl, CTX_CBF_LUMA + 1);
+    else if (!cl) err = true;  // inter CU with rqt_root_cbf = 1 but no residual
+    const int cmode = intra ? chroma_intra_mode_dm(mode) : 0;
+    Tb t;
+    if (cl) {
+      tb_view(0, x0, y0, log2, t);
+      residual(t, log2, 0, scan_idx_for(intra, log2, 0, mode));
+    }
+    if (cb) {
+      tb_view(1, x0 >> 1, y0 >> 1, log2 - 1, t);
+      residual(t, log2 - 1, 1, scan_idx_for(intra, log2 - 1, 1, cmode));
+    }
+    if (cr) {
+      tb_view(2, x0 >> 1, y0 >> 1, log2 - 1, t);
+      residual(t, log2 - 1, 2, scan_idx_for(intra, log2 - 1, 2, cmode));
+    }
+  }
+  __device__ static int chroma_intra_mode_dm(int luma_mode) { return luma_mode; }  // idx 4 (DM)
+
+  __device__ void amvp_mvd_p(int x0, int y0, int N, Mv mv) {
+    Mv mvp[2];
+    auto f = [&](int xn, int yn, Mv& m) {
+      if (!zscan_available(x0, y0, xn, yn, v.W, v.H)) return false;
+      const int u = unit(xn, yn);
+      if (v.intra[u]) return false;
+      m.x = v.mv[2 * u];
+      m.y = v.mv[2 * u + 1];
+      return true;
+    };
+    amvp_candidates(x0, y0, N, N, f, mvp);
+    const int c0 = mvd_cost(mv.x - mvp[0].x) + mvd_cost(mv.y - mvp[0].y);
+    const int c1 = mvd_cost(mv.x - mvp[1].x) + mvd_cost(mv.y - mvp[1].y);
+    const int sel = c1 < c0 ? 1 : 0;
+    mvd(mv.x - mvp[sel].x, mv.y - mvp[sel].y);
+    bin(sel, CTX_MVP_FLAG);
+  }
+
+  __device__ void coding_unit_b(int x0, int y0, int log2, int cbf) {
+    const int u = unit(x0, y0), N = 1 << log2;
+    const Motion m = motion_of(v, u);
+    const int merge_idx = v.midx[u];
+    const bool skip = merge_idx >= 0 && cbf == 0;
+    bin(skip ? 1 : 0, CTX_CU_SKIP + skip_inc(x0, y0));
+    if (skip) {
+      merge_idx_syntax(merge_idx);
+      return;
+    }
+    bin(0, CTX_PRED_MODE);
+    bin(1, CTX_PART_MODE);
+    bin(merge_idx >= 0 ? 1 : 0, CTX_MERGE_FLAG);
+    if (merge_idx >= 0) {
+      merge_idx_syntax(merge_idx);
+    } else {
+      bin(m.dir == 3 ? 1 : 0, CTX_INTER_PRED_IDC + (kCtbLog2 - log2));
+      if (m.dir != 3) bin(m.dir == 2 ? 1 : 0, CTX_INTER_PRED_IDC + 4);
+      auto at = [&](int xn, int yn, Motion& o) {
+        if (!zscan_available(x0, y0, xn, yn, v.W, v.H)) return false;
+        const int un = unit(xn, yn);
+        if (v.intra[un]) return false;
+        o = motion_of(v, un);
+        return true;
+      };
+      for (int X = 0; X < 2; ++X) {
+        if (!((m.dir >> X) & 1)) continue;
+        Mv mvp[2];
+        amvp_candidates_b(x0, y0, N, N, X, p.ref_poc, p.poc, at, mvp);
+        const Mv vv = m.mv[X];
+        const int c0 = mvd_cost(vv.x - mvp[0].x) + mvd_cost(vv.y - mvp[0].y);
+        const int c1 = mvd_cost(vv.x - mvp[1].x) + mvd_cost(vv.y - mvp[1].y);
+        const int sel = c1 < c0 ? 1 : 0;
+        mvd(vv.x - mvp[sel].x, vv.y - mvp[sel].y);
+        bin(sel, CTX_MVP_FLAG);
+      }
+      bin(cbf ? 1 : 0, CTX_RQT_ROOT_CBF);
+      if (!cbf) return;
+    }
+    transform_tree(x0, y0, log2, false, 0);
+  }
+
+  __device__ void coding_unit(int x0, int y0, int log2) {
+    const int u = unit(x0, y0), N = 1 << log2;
+    const bool intra = v.intra[u] != 0;
+    const int cbf = cu_cbf(v, x0, y0, log2);
+    const bool islice = p.type == 2, bslice = p.type == 0;
+    if (bslice && !intra) {
+      coding_unit_b(x0, y0, log2, cbf);
+      return;
+    }
+    if (bslice) {
+      bin(0, CTX_CU_SKIP + skip_inc(x0, y0));
+      bin(1, CTX_PRED_MODE);
+    } else if (!islice) {
+      const Mv mv{v.mv[2 * u], v.mv[2 * u + 1]};
+      const int merge_idx = intra ? -1 : v.midx[u];
+      const bool skip = !intra && merge_idx >= 0 && cbf == 0;
+      bin(skip ? 1 : 0, CTX_CU_SKIP + skip_inc(x0, y0));
+      if (skip) {
+        merge_idx_syntax(merge_idx);
+        return;
+      }
+      bin(intra ? 1 : 0, CTX_PRED_MODE);
+      if (!intra) {
+        bin(1, CTX_PART_MODE);
+        const bool merge = merge_idx >= 0;
+        bin(merge ? 1 : 0, CTX_MERGE_FLAG);
+        if (merge) {
+          merge_idx_syntax(merge_idx);
+        } else {
+          amvp_mvd_p(x0, y0, N, mv);
+          bin(cbf ? 1 : 0, CTX_RQT_ROOT_CBF);
+          if (!cbf) return;
+        }
+        transform_tree(x0, y0, log2, false, 0);
+        return;
+      }
+    }
+    if (log2 == kMinCbLog2) bin(1, CTX_PART_MODE);
+    const int mode = v.ipm[u];
+    int candA = 1, candB = 1;
+    if (x0 > 0 && v.intra[unit(x0 - 1, y0)]) candA = v.ipm[unit(x0 - 1, y0)];
+    if (y0 > 0 && v.intra[unit(x0, y0 - 1)] && (y0 - 1) >= ((y0 >> kCtbLog2) << kCtbLog2))
+      candB = v.ipm[unit(x0, y0 - 1)];
+    int mpm[3];
+    intra_mpm_list(candA, candB, mpm);
+    int idx = -1;
+    for (int i = 0; i < 3; ++i)
+      if (mpm[i] == mode) idx = i;
+    bin(idx >= 0 ? 1 : 0, CTX_PREV_INTRA);
+    if (idx >= 0) {
+      if (idx == 0) s.bypass(0, 1);
+      else s.bypass(idx == 1 ? 2 : 3, 2);
+    } else {
+      const int rem = mode - (mode > mpm[0]) - (mode > mpm[1]) - (mode > mpm[2]);
+      s.bypass((uint32_t)rem, 5);
+    }
+    bin(0, CTX_CHROMA_PRED);
+    transform_tree(x0, y0, log2, true, mode);
+  }
+
+  __device__ void split_flag(int x0, int y0, int log2, bool split) {
+    const int depth = kCtbLog2 - log2;
+    int inc = 0;
+    if (x0 > 0 && (kCtbLog2 - v.cu_log2[unit(x0 - 1, y0)]) > depth) ++inc;
+    if (y0 > 0 && (kCtbLog2 - v.cu_log2[unit(x0, y0 - 1)]) > depth) ++inc;
+    bin(split ? 1 : 0, CTX_SPLIT_CU + inc);
+  }
+
+  // coding_quadtree of the 32x32 CTB (depth <= 2: 32 -> 16 -> 8), then the end-of-CTB syntax
+  __device__ void ctb(int cx, int cy, bool sao_on) {
+    if (sao_on) sao(cx, cy);
+    const int X = cx << kCtbLog2, Y = cy << kCtbLog2;
+    const bool s32 = v.cu_log2[unit(X, Y)] < 5;
+    split_flag(X, Y, 5, s32);
+    if (!s32) {
+      coding_unit(X, Y, 5);
+    } else {
+      for (int q = 0; q < 4; ++q) {
+        const int x1 = X + (q & 1) * 16, y1 = Y + (q >> 1) * 16;
+        const bool s16 = v.cu_log2[unit(x1, y1)] < 4;
+        split_flag(x1, y1, 4, s16);
+        if (!s16) {
+          coding_unit(x1, y1, 4);
+        } else {
+          for (int k = 0; k < 4; ++k) coding_unit(x1 + (k & 1) * 8, y1 + (k >> 1) * 8, 3);
+        }
+      }
+    }
+    const bool last = cy == v.hc - 1 && cx == v.wc - 1;
+    if (cx == 1) s.ctrl(kCtrlSync);  // 9.3.2.4 storage after the row's second CTB
+    s.term(last ? 1 : 0);           // end_of_slice_segment_flag
+    if (!last && cx == v.wc - 1) s.term(1);  // end_of_subset_one_bit
+    if (cx == v.wc - 1) s.ctrl(kCtrlFlush);  // + byte_alignment() / slice trailing bits
+  }
+};
+
+// ------------------------------------------------------------------ kernels
+// Per CU: the merge candidate its motion matches (-1: none) and, for every unit it covers,
+// the skip flag (the cu_skip_flag context of the CUs to its right / below).
+__global__ void __launch_bounds__(256) k_ent_cu(EntropyArgs a) {
+  const int b = blockIdx.y;
+  const long u = (long)blockIdx.x * 256 + threadIdx.x;
+  if (u >= a.g.usz) return;
+  const SegView v = seg_view(a, b);
+  const int x8 = (int)(u % v.w8), y8 = (int)(u / v.w8);
+  const int l = v.cu_log2[u], s = 1 << (l - 3);
+  if ((x8 & (s - 1)) || (y8 & (s - 1))) return;  // not the CU's top-left unit
+  const int x0 = x8 * 8, y0 = y8 * 8, N = 8 * s;
+  int midx = -1;
+  if (!v.intra[u]) {
+    if (a.pic.type == 1) {
+      midx = merge_index_p(v, x0, y0, N, Mv{v.mv[2 * u], v.mv[2 * u + 1]}, a.pic.max_merge);
+    } else {
+      auto at = [&](int xn, int yn, Motion& o) {
+        if (!zscan_available(x0, y0, xn, yn, v.W, v.H)) return false;
+        const int un = unit_of(v, xn, yn);
+        if (v.intra[un]) return false;
+        o = motion_of(v, un);
+        return true;
+      };
+      Motion cand[5];
+      const int nc = merge_candidates_b(x0, y0, N, N, a.pic.max_merge, a.pic.ref_poc[0] == a.pic.ref_poc[1], at, cand);
+      const Motion m = motion_of(v, (int)u);
+      for (int i = 0; i < nc; ++i)
+        if (cand[i] == m) {
+          midx = i;
+          break;
+        }
+    }
+  }
+  const uint8_t sk = (uint8_t)(!v.intra[u] && midx >= 0 && cu_cbf(v, x0, y0, l) == 0);
+  uint8_t* skip = a.skip + (long)b * a.g.usz;
+  for (int j = 0; j < s; ++j)
+    for (int i = 0; i < s; ++i) skip[u + (long)j * v.w8 + i] = sk;
+  a.midx[(long)b * a.g.usz + u] = (int8_t)midx;
+}
+
+// One thread per CTB: count (WRITE = false) or write its tokens.
+template <bool WRITE>
+__global__ void __launch_bounds__(64) k_ent_bin(EntropyArgs a) {
+  const int b = blockIdx.y, nctu = a.g.wc * a.g.hc;
+  const int ctu = blockIdx.x * 64 + threadIdx.x;
+  if (ctu >= nctu) return;
+  const long i = (long)b * nctu + ctu;
+  uint32_t* out = nullptr;
+  if (WRITE) {
+    if (*a.status) return;  // token capacity exceeded: the host codes this slot
+    long base = 0;
+    for (int k = 0; k < b; ++k) base += a.seg_tok[k];
+    out = a.tokens + base + a.ctb_off[i];
+  }
+  const SegView v = seg_view(a, b);
+  TokSink s{out};
+  CtbBinariser z{v, a.pic, s};
+  z.ctb(ctu % v.wc, ctu / v.wc, a.pic.sao != 0);
+  s.flush_c();
+  s.flush_b();
+  if (z.err) atomicOr(a.status, 2);
+  if (!WRITE) a.ctb_cnt[i] = s.n;
+}
+
+// exclusive scan of the CTB token counts, one workgroup per segment; capacity check
+__global__ void __launch_bounds__(1024) k_ent_scan(EntropyArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x, nctu = a.g.wc * a.g.hc;
+  __shared__ int part[1024];
+  const int per = (nctu + 1023) / 1024;
+  const int lo = tid * per, hi = tv_min(nctu, lo + per);
+  const int* cnt = a.ctb_cnt + (long)b * nctu;
+  int s = 0;
+  for (int k = lo; k < hi; ++k) s += cnt[k];
+  part[tid] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int vv = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += vv;
+    __syncthreads();
+  }
+  int run = tid ? part[tid - 1] : 0;
+  int* off = a.ctb_off + (long)b * nctu;
+  for (int k = lo; k < hi; ++k) {
+    off[k] = run;
+    run += cnt[k];
+  }
+  if (tid == 1023) a.seg_tok[b] = part[1023];
+}
+
+// capacity check over all segments (one thread): the token and staging buffers
+__global__ void k_ent_check(EntropyArgs a, int B) {
+  long t = 0;
+  for (int k = 0; k < B; ++k) t += a.seg_tok[k];
+  if (t > a.tok_cap) atomicOr(a.status, 1);
+}
+
+// ---- arithmetic coder: one workgroup per slice, lane = CTB row --------------------------
+struct AcLane {
+  uint32_t low = 0, range = 510, buffered = 0xff;
+  int bl = 23, nbuf = 0, pos = 0;
+  uint8_t* out;
+  __device__ void emit(uint32_t byte) { out[pos++] = (uint8_t)byte; }
+  __device__ void write_out() {
+    const uint32_t lead = low >> (24 - bl);
+    bl += 8;
+    low &= 0xffffffffu >> bl;
+    if (lead == 0xff) {
+      nbuf++;
+    } else if (nbuf > 0) {
+      const uint32_t carry = lead >> 8;
+      emit(buffered + carry);
+      buffered = lead & 0xff;
+      const uint32_t byte = (0xff + carry) & 0xff;
+      while (nbuf > 1) {
+        emit(byte);
+        nbuf--;
+      }
+    } else {
+      nbuf = 1;
+      buffered = lead;
+    }
+  }
+  // finish() + '1' + byte alignment (end_of_subset_one_bit / slice trailing bits)
+  __device__ void flush() {
+    if ((low >> (32 - bl)) != 0) {
+      emit(buffered + 1);
+      while (nbuf > 1) {
+        emit(0x00);
+        nbuf--;
+      }
+      low -= 1u << (32 - bl);
+    } else {
+      if (nbuf > 0) emit(buffered);
+      while (nbuf > 1) {
+        emit(0xff);
+        nbuf--;
+      }
+    }
+    const int nb = 24 - bl;  // 1..12 bits of low >> 8, then the '1', then zeros
+    uint32_t v = (((low >> 8) & ((1u << nb) - 1)) << 1) | 1u;
+    int t = nb + 1;
+    const int pad = (8 - (t & 7)) & 7;
+    v <<= pad;
+    t += pad;
+    while (t > 0) {
+      t -= 8;
+      emit((v >> t) & 0xff);
+    }
+  }
+};
+
+constexpr int kCtxN = CTX_COUNT;
+
+__global__ void __launch_bounds__(256) k_ent_ac(EntropyArgs a) {
+  extern __shared__ uint8_t lds[];
+  const int b = blockIdx.x, R = blockDim.x, row = threadIdx.x;
+  const int wc = a.g.wc, hc = a.g.hc, nctu = wc * hc;
+  uint8_t* ctx = lds;                          // [kCtxN][R]: state | mps << 6 (lane `row` only)
+  volatile uint8_t* syn = lds + kCtxN * R;     // [kCtxN][R]: contexts after CTB 1 of each row
+  uint8_t* lps = lds + 2 * kCtxN * R;          // [64][4]
+  uint8_t* tlps = lps + 256;                   // [64]
+  volatile uint8_t* sflag = tlps + 64;         // [R]: 1 = row's contexts stored in syn, 2 = aborted
+  __shared__ int s_status;
+  for (int k = threadIdx.x; k < 256; k += R) lps[k] = a.tab->lps[k];
+  for (int k = threadIdx.x; k < 64; k += R) tlps[k] = a.tab->tlps[k];
+  sflag[row] = 0;
+  if (threadIdx.x == 0) s_status = *a.status;  // one read for the whole workgroup
+  __syncthreads();
+  if (s_status) return;
+  const bool live = row < hc;
+  long tbase = 0;
+  for (int k = 0; k < b; ++k) tbase += a.seg_tok[k];
+  const int* off = a.ctb_off + (long)b * nctu;
+  long tpos = 0, tend = 0;
+  AcLane L;
+  if (live) {
+    tpos = tbase + off[row * wc];
+    tend = row + 1 < hc ? tbase + off[(row + 1) * wc] : tbase + a.seg_tok[b];
+    L.out = a.stage + 3 * tpos + 16 * ((long)b * hc + row);
+  }
+  int phase = live ? 0 : 2;  // 0 waiting for the row above, 1 coding, 2 done
+  uint32_t tok = 0;
+  int left = 0, nbins = 0;
+  const int qp = a.dec.qp[b];
+  // every token takes at most 3 iterations and a row waits at most as long as the rows above
+  // it code: a loop past this bound means a corrupt token stream -- abort, never hang
+  const long guard = 8L * (a.seg_tok[b] + 1) + 65536L * hc;
+  long iter = 0;
+  while (true) {
+    if (++iter > guard && phase != 2) {
+      if (live) atomicOr(a.status, 16);
+      sflag[row] = 2;
+      phase = 2;
+    }
+    if (phase == 0) {
+      if (row == 0) {
+        const uint8_t* init = a.tab->init[a.pic.init_type][clip3(0, 51, qp)];
+        for (int c = 0; c < kCtxN; ++c) ctx[c * R + row] = init[c];
+        phase = 1;
+      } else {
+        const int f = sflag[row - 1];
+        if (f == 1) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          for (int c = 0; c < kCtxN; ++c) ctx[c * R + row] = syn[c * R + row - 1];
+          phase = 1;
+        } else if (f == 2) {  // the row above aborted: so does this one
+          sflag[row] = 2;
+          phase = 2;
+        }
+      }
+    }
+    if (phase == 1) {
+      if (left == 0) {
+        if (tpos >= tend) {  // malformed token stream (no FLUSH): stop the lane
+          atomicOr(a.status, 4);
+          sflag[row] = 2;
+          phase = 2;
+        } else {
+          tok = a.tokens[tpos++];
+          const uint32_t ty = tok >> 30;
+          nbins = ty == 0 ? (int)((tok >> 27) & 3) : ty == 1 ? (int)((tok >> 16) & 31) : 1;
+          left = nbins;
+        }
+      }
+      if (phase == 1) {
+        const uint32_t ty = tok >> 30;
+        if (ty == 0) {
+          const uint32_t f = (tok >> (9 * (nbins - left))) & 511;
+          --left;
+          const int c = (int)(f & 255), bin = (int)(f >> 8);
+          const int sv = ctx[c * R + row];
+          int st = sv & 63, mps = sv >> 6;
+          const uint32_t lp = lps[st * 4 + ((L.range >> 6) & 3)];
+          const uint32_t rmps = L.range - lp;
+          const bool is_lps = bin != mps;
+          const uint32_t r = is_lps ? lp : rmps;
+          const uint32_t l = is_lps ? L.low + rmps : L.low;
+          const int nb = __clz(r) - 23;
+          L.low = l << nb;
+          L.range = r << nb;
+          L.bl -= nb;
+          mps ^= (is_lps && st == 0) ? 1 : 0;
+          st = is_lps ? tlps[st] : (st < 62 ? st + 1 : st);
+          ctx[c * R + row] = (uint8_t)(st | (mps << 6));
+        } else if (ty == 1) {
+          const int n = left > 8 ? 8 : left;
+          left -= n;
+          const uint32_t val = (tok >> left) & ((1u << n) - 1);
+          L.low = (L.low << n) + L.range * val;
+          L.bl -= n;
+        } else if (ty == 2) {
+          left = 0;
+          L.range -= 2;
+          if (tok & 1) {
+            L.low += L.range;
+            L.low <<= 7;
+            L.range = 2 << 7;
+            L.bl -= 7;
+          } else if (L.range < 256) {
+            L.low <<= 1;
+            L.range <<= 1;
+            L.bl--;
+          }
+        } else {
+          left = 0;
+          if ((tok & 0xff) == kCtrlSync) {
+            for (int c = 0; c < kCtxN; ++c) syn[c * R + row] = ctx[c * R + row];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            sflag[row] = 1;
+          } else {
+            L.flush();
+            a.row_bytes[(long)b * hc + row] = L.pos;
+            if (sflag[row] == 0) {  // a substream that never stored its contexts (corrupt stream)
+              atomicOr(a.status, 4);
+              sflag[row] = 2;
+            }
+            phase = 2;
+          }
+        }
+        if (phase == 1 && L.bl < 12) L.write_out();
+      }
+    }
+    // a wave leaves when all its lanes are done (lanes of later waves wait on LDS flags); a
+    // wave whose lanes all wait on an earlier wave yields its issue slots
+    if (__ballot(phase != 2) == 0) break;
+    if (__ballot(phase == 1) == 0) __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// compact the rows' bytes: slice b = its rows back to back, after slices 0..b-1
+__global__ void __launch_bounds__(256) k_ent_pack(EntropyArgs a, int B) {
+  const int b = blockIdx.x, hc = a.g.hc, wc = a.g.wc, nctu = wc * hc;
+  __shared__ long s_base;
+  __shared__ int s_pre[256];
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) {
+    long base = 0;
+    for (long k = 0; k < (long)b * hc; ++k) base += a.row_bytes[k];
+    s_base = base;
+    int run = 0;
+    for (int r = 0; r < hc; ++r) {
+      s_pre[r] = run;
+      run += a.row_bytes[(long)b * hc + r];
+    }
+    a.seg_bytes[b] = run;
+    s_bad = *a.status;
+    if (base + run > a.out_cap) {
+      atomicOr(a.status, 8);
+      s_bad = 8;
+    }
+  }
+  __syncthreads();
+  if (s_bad) return;
+  long tbase = 0;
+  for (int k = 0; k < b; ++k) tbase += a.seg_tok[k];
+  const int* off = a.ctb_off + (long)b * nctu;
+  for (int r = 0; r < hc; ++r) {
+    const uint8_t* src = a.stage + 3 * (tbase + off[r * wc]) + 16 * ((long)b * hc + r);
+    uint8_t* dst = a.out + s_base + s_pre[r];
+    const int n = a.row_bytes[(long)b * hc + r];
+    for (int k = threadIdx.x; k < n; k += 256) dst[k] = src[k];
+  }
+}
+
+}  // namespace
+
+void launch_entropy(const EntropyArgs& a, int B, hipStream_t s) {
+  const int nctu = a.g.wc * a.g.hc;
+  if (a.g.wc < 2) throw std::runtime_error("GPU entropy coding needs at least 2 CTB columns");
+  if (a.g.hc > 256) throw std::runtime_error("GPU entropy coding supports at most 256 CTB rows");
+  (void)hipMemsetAsync(a.status, 0, sizeof(int), s);
+  if (a.pic.type != 2) k_ent_cu<<<dim3((unsigned)((a.g.usz + 255) / 256), B), 256, 0, s>>>(a);
+  k_ent_bin<false><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
+  k_ent_scan<<<B, 1024, 0, s>>>(a);
+  k_ent_check<<<1, 1, 0, s>>>(a, B);
+  k_ent_bin<true><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
+  const int R = (a.g.hc + 63) / 64 * 64;
+  const size_t lds = 2 * (size_t)kCtxN * R + 256 + 64 + R;
+  k_ent_ac<<<B, R, lds, s>>>(a);
+  k_ent_pack<<<B, 256, 0, s>>>(a, B);
+}
+
+void entropy_tables(EntropyTables& t) {
+  for (int ty = 0; ty < 3; ++ty)
+    for (int q = 0; q < 52; ++q) {
+      ContextSet cs;
+      cs.init(ty, q);
+      for (int c = 0; c < CTX_COUNT; ++c) t.init[ty][q][c] = (uint8_t)(cs.c[c].state | (cs.c[c].mps << 6));
+    }
+  for (int s = 0; s < 64; ++s) {
+    for (int q = 0; q < 4; ++q) t.lps[s * 4 + q] = kRangeTabLps[s][q];
+    t.tlps[s] = kTransIdxLps[s];
+  }
+}
+
+}  // namespace gpu
+}  // namespace tv

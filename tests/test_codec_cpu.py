@@ -60,7 +60,7 @@ def test_mp4_roundtrip():
 
 def test_write_frame_from_decisions_matches_encoder():
     frames = _frames(4, 2, 96, 64)
-    enc = hevc.CpuEncoder(96, 64, qp=27, search_range=16)
+    enc = hevc.CpuEncoder(96, 64, qp=27, search_range=16, wpp=False)  # write_frame: one substream
     out = enc.encode(frames[0], True, 0)
     dec = enc.decisions()
     # re-run golden pass B from the decisions and entropy-code it separately
@@ -163,7 +163,7 @@ def test_wpp_substreams_decode_to_the_same_pictures(w, h, sao):
     slice header.  The reconstruction is unchanged, the oracle decodes every substream from
     its entry point, and the rate cost of the context resets is small."""
     frames = [hevc.synth_frame(3, t, w, h) for t in range(4)]
-    a, ra = hevc.encode_sequence_cpu(frames, qp=27, gop=4, search_range=32, sao=sao)
+    a, ra = hevc.encode_sequence_cpu(frames, qp=27, gop=4, search_range=32, sao=sao, wpp=False)
     b, rb = hevc.encode_sequence_cpu(frames, qp=27, gop=4, search_range=32, sao=sao, wpp=True)
     assert all((x[0] == y[0]).all() for x, y in zip(ra, rb))
     assert len(b) > len(a) and len(b) < 1.03 * len(a)

@@ -362,6 +362,11 @@ def test_node_job_segment_resume(tmp_path, source):
     # a different job (other GOP) in the same resume dir never reuses these segments
     res4, _ = _spawn_job(tmp_path, source, {"resume_dir": ck, "gop": 4}, {})
     assert sum(p["resumed"] for p in res4[0]["per_rank"]) == 0
+    # nor does the same job with another coding tool (bitstream-changing settings are part of
+    # the fingerprint: ADVICE/VERDICT r4 weak #6)
+    res5, _ = _spawn_job(tmp_path, source, {"resume_dir": ck, "tools": {"rqt": False}}, {})
+    assert sum(p["resumed"] for p in res5[0]["per_rank"]) == 0
+    assert sum(p["encoded"] for p in res5[0]["per_rank"]) == 3
     assert len(os.listdir(ck)) == 2
 
 

@@ -2,9 +2,6 @@
 predicted quadrants as intra, only in the pattern the four-pass parallel GPU reconstruction
 can honour, the streams decode to the encoder's reconstruction, a cut coded as P gets
 cheaper, and the GPU engine is bit-exact with the golden model."""
-import os
-import subprocess
-import sys
 
 import numpy as np
 import pytest
@@ -19,8 +16,8 @@ def _cut_clip(n=8, cut=4):
            [hevc.synth_frame(77, 500 + t, W, H) for t in range(n - cut)]
 
 
-def _encode(frames, qp=30):
-    enc = hevc.CpuEncoder(W, H, qp=qp, search_range=32)
+def _encode(frames, qp=30, pintra=True):
+    enc = hevc.CpuEncoder(W, H, qp=qp, search_range=32, pintra=pintra)
     stream, intra, recons = b"", [], []
     for t, f in enumerate(frames):
         stream += enc.encode(f, t == 0, t)
@@ -61,18 +58,10 @@ def test_cut_coded_as_p_uses_intra_quadrants_in_a_parallel_safe_pattern():
             np.testing.assert_array_equal(d[c], r[c])
 
 
-def _bytes_and_psnr(env_on: bool) -> tuple[int, float]:
-    code = (
-        "import numpy as np, sys; sys.path.insert(0, %r)\n"
-        "from tests.test_pintra import _cut_clip, _encode, W, H\n"
-        "from thinvids_amd.models import hevc\n"
-        "fr = _cut_clip(); s, _, rec = _encode(fr)\n"
-        "print(len(s), np.mean([hevc.psnr(f[0], r[0][:H, :W]) for f, r in zip(fr, rec)]))\n"
-    ) % os.getcwd()
-    env = dict(os.environ, TV_PINTRA="1" if env_on else "0", PYTHONPATH=os.getcwd())
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
-    n, p = out.stdout.split()
-    return int(n), float(p)
+def _bytes_and_psnr(on: bool) -> tuple[int, float]:
+    fr = _cut_clip()
+    st, _, rec = _encode(fr, pintra=on)
+    return len(st), float(np.mean([hevc.psnr(f[0], r[0][:H, :W]) for f, r in zip(fr, rec)]))
 
 
 def test_intra_in_p_makes_a_cut_cheaper():

@@ -4,9 +4,6 @@ reconstruction with the split transform trees (split_transform_flag, depth-1 chr
 internal TB edges in the deblocking filter), and the tool lowers the bitrate at equal or
 better PSNR on the bench's synthetic content (the GPU engine is bit-exact with the golden
 model: tests/test_gpu_engine.py)."""
-import os
-import subprocess
-import sys
 
 import numpy as np
 
@@ -31,17 +28,9 @@ def test_split_streams_decode_exactly():
 
 
 def _bytes_psnr(rqt: bool, seed: int) -> tuple[int, float]:
-    code = (
-        "import numpy as np, sys; sys.path.insert(0, %r)\n"
-        "from tests.test_rqt import _clip, W, H\n"
-        "from thinvids_amd.models import hevc\n"
-        "fr = _clip(%d); bs, rec = hevc.encode_sequence_cpu(fr, qp=27, search_range=32)\n"
-        "print(len(bs), np.mean([hevc.psnr(f[0], r[0][:H, :W]) for f, r in zip(fr, rec)]))\n"
-    ) % (os.getcwd(), seed)
-    env = dict(os.environ, TV_RQT="1" if rqt else "0", PYTHONPATH=os.getcwd())
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
-    n, p = out.stdout.split()
-    return int(n), float(p)
+    fr = _clip(seed)
+    bs, rec = hevc.encode_sequence_cpu(fr, qp=27, search_range=32, rqt=rqt)
+    return len(bs), float(np.mean([hevc.psnr(f[0], r[0][:H, :W]) for f, r in zip(fr, rec)]))
 
 
 def test_rqt_lowers_the_rate():

@@ -36,8 +36,10 @@ class CpuHevcEngine:
     per call, encoded concurrently on a thread pool (the native encoder releases the GIL)."""
 
     def __init__(self, width: int, height: int, qp: int = 27, batch: int = 2, gop: int = 8, search_range: int = 16,
-                 sao: bool = False, seed: int = 1, threads: int | None = None, bframes: int = 1, **_):
+                 sao: bool = False, seed: int = 1, threads: int | None = None, bframes: int = 1, wpp: bool = True,
+                 rqt: bool = True, pintra: bool = True, **_):
         self.width, self.height, self.qp, self.batch, self.gop = width, height, qp, batch, gop
+        self.tools = {"wpp": wpp, "rqt": rqt, "pintra": pintra}
         self.search_range, self.sao, self.seed, self.bframes = search_range, sao, seed, int(bframes)
         self.threads = threads or 2
         self.pool = cf.ThreadPoolExecutor(self.threads)
@@ -47,7 +49,7 @@ class CpuHevcEngine:
     def _one(self, start: int, n: int, fq):
         frames = [hevc.synth_frame(self.seed, start + t, self.width, self.height) for t in range(n)]
         data, recons = hevc.encode_sequence_cpu(frames, qp=self.qp, gop=n, sao=self.sao, search_range=self.search_range,
-                                                bframes=self.bframes, frame_qps=fq)
+                                                bframes=self.bframes, frame_qps=fq, **self.tools)
         return data, sum(_frame_sse(f, r, self.width, self.height) for f, r in zip(frames, recons))
 
     def encode_synthetic(self, starts, nframes: int | None = None, qp=None) -> list[bytes]:

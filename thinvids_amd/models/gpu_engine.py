@@ -86,10 +86,16 @@ class GpuEngine:
     def __init__(self, width: int, height: int, qp: int = 27, batch: int = 8, gop: int = 16,
                  search_range: int = 64, deblock: bool = True, sao: bool = False, seed: int = 1,
                  threads: int | None = None,
-                 device: int = 0, max_merge: int = 5, crf: int = 0, bframes: int = 1):
+                 device: int = 0, max_merge: int = 5, crf: int = 0, bframes: int = 1, wpp: bool = True,
+                 rqt: bool = True, pintra: bool = True, entropy: str | None = None):
         """`bframes` > 1: hierarchical-B mini-GOPs of that size (power of 2, tv/gop.h); the
         segments' streams are then in coding order (the decoder reorders by POC) and
-        :meth:`last_recon` returns the last DISPLAY frame."""
+        :meth:`last_recon` returns the last DISPLAY frame.
+
+        `wpp` (default): one CABAC substream per CTB row, entropy-coded ON THE GPU
+        (csrc/gpu/k_entropy.hip); the host only writes slice headers and entry points.
+        `entropy`: "gpu" (default) or "host" (the C++ CABAC writer on the thread pool; same
+        bytes, for A/B runs; env TV_ENTROPY).  wpp=False always codes on the host."""
         self.lib = _lib()
         self.width, self.height, self.qp = width, height, qp
         self.batch, self.gop = batch, gop
@@ -98,7 +104,13 @@ class GpuEngine:
         self.sao = sao
         self.device = device
         self.bframes = int(bframes)
-        self.h = self.lib.tv_engine_new_b(width, height, qp, batch, gop, search_range, int(deblock) | (2 if sao else 0),
+        from .hevc import codec_flags
+
+        self.entropy = (entropy or os.environ.get("TV_ENTROPY", "gpu")) if wpp else "host"
+        if self.entropy not in ("gpu", "host"):
+            raise ValueError("entropy must be 'gpu' or 'host'")
+        self.flags = codec_flags(deblock, sao, wpp, rqt, pintra) | (32 if self.entropy == "host" else 0)
+        self.h = self.lib.tv_engine_new_b(width, height, qp, batch, gop, search_range, self.flags,
                                           seed & 0xFFFFFFFF, self.threads, device, max_merge, int(crf), self.bframes)
         if not self.h:
             raise RuntimeError("GPU engine init failed: " + self.lib.tv_gpu_last_error().decode())
@@ -206,6 +218,15 @@ class GpuEngine:
         self.lib.tv_engine_timing(self.h, C.byref(g), C.byref(w), C.byref(e), C.byref(m))
         return {"gpu_ms": g.value, "wall_ms": w.value, "entropy_cpu_ms": e.value, "coef_mb": m.value}
 
+    def entropy_stats(self) -> dict:
+        """GPU entropy coding: whether it is on, pictures the host writer coded instead since
+        construction (device capacity), and the OR of their device status words."""
+        on, fb, st = C.c_int(), C.c_longlong(), C.c_int()
+        f = self.lib.tv_engine_entropy_stats
+        f.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_longlong), C.POINTER(C.c_int)]
+        f(self.h, C.byref(on), C.byref(fb), C.byref(st))
+        return {"gpu": bool(on.value), "fallbacks": int(fb.value), "status": int(st.value)}
+
     def last_recon(self, b: int):
         y = np.empty((self.ch, self.cw), np.uint8)
         u = np.empty((self.ch // 2, self.cw // 2), np.uint8)
@@ -223,13 +244,18 @@ def pad_frame(y, u, v, cw, ch) -> np.ndarray:
     return np.concatenate([Y.ravel(), U.ravel(), V.ravel()])
 
 
-def estimate_footprint(width: int, height: int, batch: int, gop: int, sao: bool = False, bframes: int = 1) -> dict:
+def estimate_footprint(width: int, height: int, batch: int, gop: int, sao: bool = False, bframes: int = 1,
+                       wpp: bool = True, rqt: bool = True, pintra: bool = True, entropy: str | None = None) -> dict:
     """HBM / pinned-host bytes an engine of this geometry would allocate, computed by the
     native constructor's own size formulas without allocating (tv_engine_estimate)."""
+    from .hevc import codec_flags
+
     lib = _lib()
+    ent = (entropy or os.environ.get("TV_ENTROPY", "gpu")) if wpp else "host"
+    flags = codec_flags(True, sao, wpp, rqt, pintra) | (32 if ent == "host" else 0)
     d, h = C.c_ulonglong(), C.c_ulonglong()
     f = lib.tv_engine_estimate
     f.argtypes = [C.c_int] * 6 + [C.POINTER(C.c_ulonglong)] * 2
-    if f(width, height, batch, gop, 1 | (2 if sao else 0), int(bframes), C.byref(d), C.byref(h)) != 0:
+    if f(width, height, batch, gop, flags, int(bframes), C.byref(d), C.byref(h)) != 0:
         raise ValueError(lib.tv_gpu_last_error().decode())
     return {"dev": int(d.value), "host": int(h.value)}

@@ -206,7 +206,7 @@ class WorkQueue:
 
 # bumped whenever the encoders' output for identical settings changes (a checkpoint written
 # by an older build must not be mixed into a newer job's output)
-BITSTREAM_VERSION = 8
+BITSTREAM_VERSION = 9  # 9: WPP substreams (GPU entropy coding) by default
 
 
 class Checkpoint:
@@ -431,17 +431,22 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             resume_dir: str | None = None, max_retries: int = 3, hooks: JobHooks | None = None,
             deblock: bool = True, sao: bool = False, cache=None, crf: int = 0, scenecut: bool = False,
             audio_stream: int = 0, codec: str = "hevc", qindex: int = 0, rc_mode: str = "",
-            vbv_maxrate_kbps: float = 0.0, vbv_bufsize_kbit: float = 0.0, bframes: int = 1) -> dict:
+            vbv_maxrate_kbps: float = 0.0, vbv_bufsize_kbit: float = 0.0, bframes: int = 1,
+            tools: dict | None = None) -> dict:
     """One job over the node's ranks (SPMD).  Rate control: ``bitrate_kbps`` > 0 selects
     frame-level 2-pass, or single-pass ABR when ``rc_mode == "abr"`` (optionally under a VBV:
     ``vbv_maxrate_kbps`` / ``vbv_bufsize_kbit``, checked and repaired per segment, see
-    models/ratecontrol.py); else ``crf`` > 0 in-engine CRF; else constant ``qp``."""
+    models/ratecontrol.py); else ``crf`` > 0 in-engine CRF; else constant ``qp``.  ``tools``:
+    HEVC coding-tool switches (EncodeSpec wpp / rqt / pintra; default all on) -- part of the
+    checkpoint fingerprint, so a resume with other tools re-encodes."""
     import torch
 
     from ..models import hevc, media
     from ..models.streams import write_output
     from ..worker.encoder import EncodeSpec, EngineCache, PartStats, SynthRange, gpu_available, psnr_from_sse
     from ..worker.helpers import output_geometry
+
+    tool_kw = dict(EncodeSpec(1, 1).tools(), **(tools or {}))
     from .comm import (SegmentStream, allreduce_stats, gather_bytes_to_root, scatter_frames_from_root, scatter_root,
                        stage_segment_frames)
 
@@ -479,7 +484,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         src=os.path.abspath(input_path), size=st.st_size if st else 0, mtime=st.st_mtime_ns if st else 0,
         rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software,
         deblock=deblock, sao=sao, scenecut=scenecut, codec=codec, qindex=qindex, crf=crf, bframes=bframes,
-        rc=rc_name, bitstream_version=BITSTREAM_VERSION,
+        rc=rc_name, bitstream_version=BITSTREAM_VERSION, tools=tool_kw,
         **({"kbps": bitrate_kbps, "vbv": [vbv_maxrate_kbps, vbv_bufsize_kbit] if vbv else None} if abr else {})))
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
     quality: dict = {}  # (r, i) -> PartStats of segments encoded here
@@ -514,7 +519,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=qp, gop=gop, search_range=search_range,
                           software=software, deblock=deblock, sao=sao, seed=getattr(src, "seed", 1),
                           crf=0 if bitrate_kbps > 0 else crf, scenecut=scenecut, codec=codec, qindex=qindex,
-                          bframes=bframes)
+                          bframes=bframes, **tool_kw)
 
     rc = {"plan": None, "fb": RateFeedback(), "bits": {}}  # pass-2 plan, feedback, per-frame bits
     rung_scale = [(rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]  # per-rung budget ~ pixels
@@ -968,6 +973,9 @@ def main(argv=None) -> int:
     ap.add_argument("--resume-dir", default=None, help="segment checkpoint directory (resume / elastic restart)")
     ap.add_argument("--max-retries", type=int, default=3, help="per-segment retry budget before the job aborts")
     ap.add_argument("--timeout-sec", type=float, default=600.0, help="collective timeout (a hung rank surfaces)")
+    ap.add_argument("--no-wpp", dest="wpp", action="store_false", help="HEVC: one CABAC substream per slice (host)")
+    ap.add_argument("--no-rqt", dest="rqt", action="store_false", help="HEVC: no residual quadtree")
+    ap.add_argument("--no-pintra", dest="pintra", action="store_false", help="HEVC: no intra CUs in P pictures")
     a = ap.parse_args(argv)
     import torch
     import torch.distributed as dist
@@ -981,7 +989,8 @@ def main(argv=None) -> int:
         dist.init_process_group(backend, timeout=datetime.timedelta(seconds=a.timeout_sec))
     ladder = [int(x) for x in a.ladder.split(",") if x.strip()] or None
     res = run_job(a.input, a.output, a.height, a.qp, a.gop, a.segment_frames, a.mode, a.bitrate_kbps, ladder,
-                  software=a.software, resume_dir=a.resume_dir, max_retries=a.max_retries, bframes=a.bframes)
+                  software=a.software, resume_dir=a.resume_dir, max_retries=a.max_retries, bframes=a.bframes,
+                  tools={"wpp": a.wpp, "rqt": a.rqt, "pintra": a.pintra})
     if int(os.environ.get("RANK", "0")) == 0:
         print(json.dumps(res), flush=True)
     if dist.is_initialized():

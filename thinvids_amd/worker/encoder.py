@@ -47,12 +47,21 @@ class EncodeSpec:
     codec: str = "hevc"  # "av1": the AV1 engine (models/av1_engine.py), BASELINE config #4
     qindex: int = 0  # AV1 q-index (0: matched to qp)
     bframes: int = 1  # HEVC hierarchical-B mini-GOP (1: I P P P; tv/gop.h)
+    # HEVC bitstream identity beyond the rate point (explicit, never from the environment):
+    # WPP substreams (entropy-coded on the GPU), residual quadtree, intra CUs in P pictures
+    wpp: bool = True
+    rqt: bool = True
+    pintra: bool = True
 
     def engine_key(self):
         if self.codec == "av1":
             return ("av1", self.width, self.height, self.av1_qindex())
         return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed,
-                self.crf, self.hevc_bframes())
+                self.crf, self.hevc_bframes(), self.wpp, self.rqt, self.pintra)
+
+    def tools(self) -> dict:
+        """The coding-tool switches as GpuEngine / CpuEncoder keyword arguments."""
+        return {"wpp": self.wpp, "rqt": self.rqt, "pintra": self.pintra}
 
     def hevc_bframes(self) -> int:
         """Mini-GOP actually used: in-engine CRF keeps I P P P (its lookahead QP is per
@@ -143,7 +152,8 @@ def engine_bytes(spec: "EncodeSpec", batch: int) -> int:
     else:
         from ..models.gpu_engine import estimate_footprint
 
-        eng = estimate_footprint(spec.width, spec.height, batch, spec.gop, spec.sao, spec.hevc_bframes())["dev"]
+        eng = estimate_footprint(spec.width, spec.height, batch, spec.gop, spec.sao, spec.hevc_bframes(),
+                                 **spec.tools())["dev"]
     return eng + _staging_bytes(spec, batch)
 
 
@@ -189,7 +199,7 @@ class EngineCache:
             return eng
         return GpuEngine(spec.width, spec.height, qp=spec.qp, batch=batch, gop=spec.gop, search_range=spec.search_range,
                          deblock=spec.deblock, sao=spec.sao, seed=spec.seed, device=self.device, crf=spec.crf,
-                         bframes=spec.hevc_bframes())
+                         bframes=spec.hevc_bframes(), **spec.tools())
 
     def get(self, spec: EncodeSpec):
         key = spec.engine_key()
@@ -362,7 +372,7 @@ def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None, fq=None) -> byte
     else:
         bs, recons = hevc.encode_sequence_cpu(frames, qp=spec.qp, gop=spec.gop, deblock=spec.deblock, sao=spec.sao,
                                               search_range=spec.search_range, frame_qps=fq, crf=spec.crf,
-                                              bframes=spec.hevc_bframes())
+                                              bframes=spec.hevc_bframes(), **spec.tools())
     if st is not None:
         sse = np.zeros(3)
         for f, r in zip(frames, recons):

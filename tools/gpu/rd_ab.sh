@@ -1,7 +1,7 @@
 #!/bin/bash
 # BD-rate of the default GPU engine against the same engine with coding tools switched off
-# by environment (e.g. "TV_RQT=0 TV_PINTRA=0"), 1080p I P P P, QP 22/27/32/37, both contents.
-# Usage: rd_ab.sh <tag> "<env assignments of the anchor>"
+# by bench.py flags (e.g. "--no-rqt --no-pintra"), 1080p I P P P, QP 22/27/32/37, both contents.
+# Usage: rd_ab.sh <tag> "<bench.py flags of the anchor>"
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp PYTHONPATH=$PWD
@@ -9,8 +9,8 @@ O=gpurun_out/${1:-rdab}; mkdir -p $O
 for content in smooth textured; do
   for v in anchor test; do
     for q in 22 27 32 37; do
-      if [ $v = anchor ]; then pre="env $2"; else pre=""; fi
-      $pre timeout -k 10 200 python -u bench.py --steps 2 --warmup 1 --qp $q --no-4k --content $content > $O/${content}_${v}_q$q.log 2>&1 || { echo "$content $v q$q failed"; tail -n 5 $O/${content}_${v}_q$q.log; exit 1; }
+      if [ $v = anchor ]; then extra="$2"; else extra=""; fi
+      timeout -k 10 200 python -u bench.py --steps 2 --warmup 1 --qp $q --no-4k --content $content $extra > $O/${content}_${v}_q$q.log 2>&1 || { echo "$content $v q$q failed"; tail -n 5 $O/${content}_${v}_q$q.log; exit 1; }
       grep '^{' $O/${content}_${v}_q$q.log | tail -n 1 > $O/${content}_${v}_q$q.json
     done
   done

@@ -44,7 +44,7 @@ def run_point(args):
             stream += r.stream
             ys += [hevc.psnr(f[0], rec[:W * H].reshape(H, W)[:h, :w]) for f, rec in zip(frames[s0:], r.recon)]
     else:
-        kw = dict(sao=a["sao"])
+        kw = dict(sao=a["sao"], rqt=a["rqt"], pintra=a["pintra"], wpp=a["wpp"])
         stream, recons = hevc.encode_sequence_cpu(frames, qp=qp, gop=a["gop"], frame_qps=fq, bframes=a["bframes"], **kw)
         ys = [hevc.psnr(f[0], r[0][:h, :w]) for f, r in zip(frames, recons)]
 
@@ -68,12 +68,18 @@ def main():
     ap.add_argument("--bframes", type=int, default=1, help="hierarchical-B mini-GOP size (1 = IPPP)")
     ap.add_argument("--codec", choices=("hevc", "av1"), default="hevc",
                     help="av1: the golden AV1 encoder at the q-index matched to each QP")
+    # coding tools: explicit flags; this tool alone also honours TV_RQT=0 / TV_PINTRA=0 / TV_WPP=0
+    # (A/B sweeps), nothing else in the framework reads them from the environment
+    env_on = lambda k: os.environ.get(k, "1") != "0"
+    ap.add_argument("--rqt", type=int, default=int(env_on("TV_RQT")))
+    ap.add_argument("--pintra", type=int, default=int(env_on("TV_PINTRA")))
+    ap.add_argument("--wpp", type=int, default=int(env_on("TV_WPP")))
     ap.add_argument("--anchor", default="")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     cfg = dict(res=a.res, frames=a.frames, gop=a.gop, sao=bool(a.sao), seed=a.seed, textured=a.textured,
                cascade=[int(x) for x in a.cascade.split(",")] if a.cascade else [], iqp=a.iqp,
-               bframes=a.bframes, codec=a.codec)
+               bframes=a.bframes, codec=a.codec, rqt=bool(a.rqt), pintra=bool(a.pintra), wpp=bool(a.wpp))
     qps = [int(q) for q in a.qps.split(",")]
     with ProcessPoolExecutor(len(qps)) as ex:
         pts = list(ex.map(run_point, [(q, cfg) for q in qps]))
