@@ -50,13 +50,17 @@ def _dist_setup(args):
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     cpus = pin_rank(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    import datetime
+
+    # a stuck rank fails the collectives in minutes, not at the driver's time limit
+    timeout = datetime.timedelta(seconds=float(os.environ.get("TV_COLL_TIMEOUT", "240")))
     if args.cpu:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timeout)
         assert dist.get_world_size() == args.gpus, "live group size != --gpus"
         return dist.get_world_size(), dist.get_rank(), local, torch.device("cpu"), cpus
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist.init_process_group("nccl", device_id=dev)
+    dist.init_process_group("nccl", device_id=dev, timeout=timeout)
     assert dist.get_world_size() == args.gpus, "live group size != --gpus"
     return dist.get_world_size(), dist.get_rank(), local, dev, cpus
 

@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -150,10 +151,7 @@ class Core {
     // bit 2: WPP substreams, bit 3: no RQT, bit 4: no intra-in-P, bit 5: CABAC on the host
     // (WPP streams are entropy-coded on the GPU unless bit 5 asks for the host writer)
     gpu_ent_ = gpu_entropy(c);
-    if (gpu_ent_) {
-      HIP_OK(hipStreamCreateWithFlags(&estream_, hipStreamNonBlocking));
-      HIP_OK(hipEventCreateWithFlags(&eev_, hipEventDisableTiming));
-    }
+    if (gpu_ent_) HIP_OK(hipEventCreateWithFlags(&eev_, hipEventDisableTiming));  // estream_: init_entropy_stream()
     auto alloc_set = [&](FrameSet& f) {
       dev_alloc(&f.y, B * g_.ysz);
       dev_alloc(&f.u, B * g_.csz);
@@ -207,16 +205,17 @@ class Core {
       dev_alloc(&ent_.skip, B * g_.usz);
       dev_alloc(&ent_.midx, B * g_.usz);
       dev_alloc(&ent_.ctb_cnt, B * nctu_ * sizeof(int));
-      dev_alloc(&ent_.ctb_off, B * nctu_ * sizeof(int));
-      dev_alloc(&ent_.seg_tok, B * sizeof(int));
-      dev_alloc(&ent_.tokens, tok_cap_ * sizeof(uint32_t));
-      dev_alloc(&ent_.stage, 3 * tok_cap_ + 16 * B * g_.hc);
       EntropyTables* t = nullptr;
       dev_alloc(&t, sizeof(EntropyTables));
       std::unique_ptr<EntropyTables> ht(new EntropyTables());
       entropy_tables(*ht);
       HIP_OK(hipMemcpy(t, ht.get(), sizeof(EntropyTables), hipMemcpyHostToDevice));
       ent_.tab = t;
+      const char* dbg = getenv("TV_ENT_DEBUG");
+      if (dbg && *dbg == '1') {
+        dev_alloc(&ent_dbg_, 8 * sizeof(unsigned long long));
+        HIP_OK(hipMemset(ent_dbg_, 0, 8 * sizeof(unsigned long long)));
+      }
     }
     host_alloc(&qhost_, (size_t)c.gop * B);
     host_alloc(&quni_, (size_t)B);
@@ -229,6 +228,7 @@ class Core {
       host_alloc(&s.host, slot_host_bytes_);
       // waited on by the fetch thread: see sync_mode()
       HIP_OK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming | (sync_mode() == 2 ? hipEventBlockingSync : 0)));
+
       s.pending = 0;
     }
     HIP_OK(hipEventCreate(&t0_));
@@ -269,6 +269,15 @@ class Core {
     seq_.finalize();
   }
 
+  // The core's entropy stream, created by the Engine after every core's main stream: HIP
+  // assigns streams to its (GPU_MAX_HW_QUEUES, 4 by default) hardware queues in creation order,
+  // and a hardware queue runs its packets in order -- a main stream sharing a queue with an
+  // entropy stream waits behind the latency-bound coder (measured: main-stream queues 36 %
+  // busy).  Main streams first, then the entropy streams, gives each its own queue at 2 cores.
+  void init_entropy_stream() {
+    if (gpu_ent_ && !estream_) HIP_OK(hipStreamCreateWithFlags(&estream_, hipStreamNonBlocking));
+  }
+
   // device / pinned-host bytes this group allocated (the engine's HBM footprint)
   size_t dev_bytes() const { return dev_bytes_; }
   size_t host_bytes() const { return host_bytes_; }
@@ -284,9 +293,7 @@ class Core {
     const bool ge = gpu_entropy(c);
     long slot = 0, slot_host = 0;
     slot_bytes((long)B, g, ge, slot, slot_host);
-    const size_t ent = ge ? 2 * B * g.usz + 2 * B * nctu * sizeof(int) + B * sizeof(int) +
-                                tok_capacity((long)B, g) * (sizeof(uint32_t) + 3) + 16 * B * g.hc + sizeof(EntropyTables)
-                          : 0;
+    const size_t ent = ge ? 2 * B * g.usz + B * nctu * sizeof(int) + sizeof(EntropyTables) : 0;
     dev = set + ndpb * (set + B * 16 * g.psz + B * qsz) + ((c.deblock & 2) ? set : 0) + 2 * set +
           B * 3 * sizeof(unsigned long long) + B * nctu * sizeof(int) + 2 * B * nctu * 2 * sizeof(int16_t) +
           2 * B * nctu * sizeof(int) + (c.mgop > 1 ? 2 * B * nctu * sizeof(CtbMeOut) : 0) +
@@ -297,6 +304,16 @@ class Core {
 
   ~Core() {
     fetch_.reset();  // the fetch thread drains (every issued slot was waited for by finish())
+    if (ent_dbg_) {
+      unsigned long long h[8] = {};
+      (void)hipDeviceSynchronize();
+      (void)hipMemcpy(h, ent_dbg_, sizeof(h), hipMemcpyDeviceToHost);
+      const double n = h[0] ? (double)h[0] : 1.0;
+      fprintf(stderr, "[tv entropy] rows %llu: ctx bins/row %.0f, tokens/row %.0f, clocks/ctx bin %.1f, "
+              "wait us/row %.1f, coding us/row %.1f, max row span us %.1f\n", h[0], h[1] / n, h[2] / n,
+              h[1] ? (double)h[3] / h[1] : 0.0, h[4] / n / 100.0, h[3] / n / 2400.0, h[5] / 100.0);
+      (void)hipFree(ent_dbg_);
+    }
     (void)hipStreamSynchronize(stream_);
     for (auto* p : {src_.y, src_.u, src_.v, deb_.y, deb_.u, deb_.v}) (void)hipFree(p);
     for (int k = 0; k < ndpb_; ++k)
@@ -311,8 +328,7 @@ class Core {
     (void)hipFree(cmv_);
     (void)hipFree(ccost_);
     (void)hipFree(rc_);
-    for (void* p : {(void*)ent_.skip, (void*)ent_.midx, (void*)ent_.ctb_cnt, (void*)ent_.ctb_off, (void*)ent_.seg_tok,
-                    (void*)ent_.tokens, (void*)ent_.stage, (void*)ent_.tab})
+    for (void* p : {(void*)ent_.skip, (void*)ent_.midx, (void*)ent_.ctb_cnt, (void*)ent_.tab})
       (void)hipFree(p);
     (void)hipHostFree(qhost_);
     (void)hipHostFree(quni_);
@@ -321,6 +337,7 @@ class Core {
       (void)hipFree(s.dev);
       (void)hipHostFree(s.host);
       (void)hipEventDestroy(s.ev);
+
     }
     (void)hipEventDestroy(t0_);
     (void)hipEventDestroy(t1_);
@@ -365,6 +382,7 @@ class Core {
     const double per = e ? atof(e) : 1.0;
     return (long)(per * B * g.ysz) + 1024;
   }
+  static constexpr long kTokPad = 64;
   // head of the entropy outputs: status, seg_bytes[B], row_bytes[B][hc]
   static long ent_head_bytes(long B, const Geo& g) { return 16 + 4 * B + 4 * B * g.hc; }
   static void slot_bytes(long B, const Geo& g, bool ge, long& dev, long& host) {
@@ -372,7 +390,15 @@ class Core {
     host = align(B * g.usz) + align(B * g.usz * 4) + align(B * nctu * 8) + align(B * nctu * 4) + align(B * nctu * 4) +
            align(B * 4) + align(B * nctu * 12) + align(B) + align(B * g.usz) + align(B * g.usz * 4) +
            align(B * g.usz * 5) + align(B * cap * 2) + (ge ? align(ent_head_bytes(B, g)) : 0);
-    dev = host + (ge ? align(B * cap) : 0);  // the payload: device side only (lands in `packed`)
+    // device side only: the picture's token lists, CTB token offsets, segment token counts, the
+    // coder's output staging and the rows' WPP hand-off (the payload itself goes straight into
+    // the host slot's `packed` region)
+    dev = host + (ge ? ent_slot_bytes(B, g) : 0);
+  }
+  static long ent_slot_bytes(long B, const Geo& g) {
+    const long cap = tok_capacity(B, g), nctu = (long)g.wc * g.hc;
+    return align((cap + kTokPad) * 4) + align(3 * cap + 20 * B * g.hc + 16) + align(B * nctu * 4) + align(B * 4) +
+           align(B * g.hc * 4) + align(B * g.hc * kEntCtx);
   }
   // qcost, gate list, pass lists, candidate list (16 bytes per CTB each), counters, candidate bytes
   static size_t pintra_bytes(long B, long nctu) { return 4 * align(B * nctu * 16) + 256 + align(B * nctu * 4); }
@@ -394,7 +420,11 @@ class Core {
     uint32_t* sao;
     int8_t* qp;
     int* ent_head;     // GPU entropy: status, seg_bytes[B], row_bytes[B][hc]
-    uint8_t* ent_out;  // GPU entropy payload (device slot only)
+    uint32_t* tokens;  // GPU entropy, device slot only: token lists of the picture
+    uint8_t* stage;    //   arithmetic coder output staging
+    int *ctb_off, *seg_tok;
+    int* wflag;        //   WPP hand-off flags and contexts between the rows' coder waves
+    uint8_t* wctx;
   };
   Parts carve(uint8_t* base) const {
     const long B = cfg_.batch, U = g_.usz;
@@ -434,7 +464,18 @@ class Core {
     q += align(B * cap_ * 2);
     p.ent_head = reinterpret_cast<int*>(q);
     q += gpu_ent_ ? align(ent_head_bytes(B, g_)) : 0;
-    p.ent_out = q;
+    const long tc = gpu_ent_ ? tok_capacity(B, g_) : 0;
+    p.tokens = reinterpret_cast<uint32_t*>(q);
+    q += gpu_ent_ ? align((tc + kTokPad) * 4) : 0;
+    p.stage = q;
+    q += gpu_ent_ ? align(3 * tc + 20 * B * g_.hc + 16) : 0;
+    p.ctb_off = reinterpret_cast<int*>(q);
+    q += gpu_ent_ ? align(B * nctu_ * 4) : 0;
+    p.seg_tok = reinterpret_cast<int*>(q);
+    q += gpu_ent_ ? align(B * 4) : 0;
+    p.wflag = reinterpret_cast<int*>(q);
+    q += gpu_ent_ ? align(B * g_.hc * 4) : 0;
+    p.wctx = q;
     p.count = nullptr;  // device count array lives in the scratch below
     return p;
   }
@@ -556,16 +597,12 @@ class Core {
     HIP_OK(hipEventRecord(ev, st));
     wait_event(ev);
   }
-  // GPU entropy: the head (status, sizes) and slice QPs, then the payload; false: the device
-  // could not code this picture (capacity), the caller falls back to the host writer
+  // GPU entropy: the pack kernel stored status, sizes, slice QPs and payload straight into the
+  // pinned host slot (no copy engine, no blit kernel); false: the device could not code this
+  // picture (capacity), the caller falls back to the host writer
   bool fetch_entropy(Slot& s, int B) {
-    thread_local hipStream_t ws = nullptr;
-    if (!ws) HIP_OK(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
-    wait_event(s.ev);
-    const Parts d = carve(s.dev), h = carve(s.host);
-    HIP_OK(hipMemcpyAsync(h.ent_head, d.ent_head, ent_head_bytes(cfg_.batch, g_), hipMemcpyDeviceToHost, ws));
-    HIP_OK(hipMemcpyAsync(h.qp, d.qp, B, hipMemcpyDeviceToHost, ws));
-    sleep_sync(ws);
+    wait_event(s.ev);  // the pack kernel wrote head, slice QPs and payload into the host slot
+    const Parts h = carve(s.host);
     if (h.ent_head[0] != 0) {
       ent_fallbacks_++;
       ent_status_ |= h.ent_head[0];
@@ -573,9 +610,6 @@ class Core {
     }
     long total = 0;
     for (int b = 0; b < B; ++b) total += h.ent_head[4 + b];
-    if (total > (long)cfg_.batch * cap_ * 2) throw std::runtime_error("entropy payload overflow");
-    if (total) HIP_OK(hipMemcpyAsync(h.packed, d.ent_out, total, hipMemcpyDeviceToHost, ws));
-    sleep_sync(ws);
     coef_bytes_ += total;
     return true;
   }
@@ -617,17 +651,23 @@ class Core {
     a.skip = ent_.skip;
     a.midx = ent_.midx;
     a.ctb_cnt = ent_.ctb_cnt;
-    a.ctb_off = ent_.ctb_off;
-    a.seg_tok = ent_.seg_tok;
-    a.tokens = ent_.tokens;
+    a.ctb_off = d.ctb_off;
+    a.seg_tok = d.seg_tok;
+    a.tokens = d.tokens;
     a.tok_cap = tok_cap_;
-    a.stage = ent_.stage;
+    a.stage = d.stage;
+    a.wflag = d.wflag;
+    a.wctx = d.wctx;
     a.tab = ent_.tab;
     a.status = d.ent_head;
     a.seg_bytes = d.ent_head + 4;
     a.row_bytes = d.ent_head + 4 + cfg_.batch;
-    a.out = d.ent_out;
-    a.out_cap = (long)cfg_.batch * cap_;
+    const Parts h = carve(s.host);  // the pack kernel's destination (pinned, device-visible)
+    HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.hhead), h.ent_head, 0));
+    HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.hqp), h.qp, 0));
+    HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.hout), h.packed, 0));
+    a.hout_cap = (long)cfg_.batch * cap_ * 2;
+    a.dbg = ent_dbg_;
     return a;
   }
 
@@ -795,10 +835,20 @@ class Core {
     if (gpu_ent_) {  // entropy coding on its own stream: the next picture's kernels run meanwhile
       HIP_OK(hipEventRecord(eev_, stream_));
       HIP_OK(hipStreamWaitEvent(estream_, eev_, 0));
-      launch_entropy(entropy_args(s, dec, pic), B, estream_);
+      // binarisation on the core's entropy stream (one picture at a time: its scratch is per
+      // core), the serial arithmetic coder on the slot's own stream, so the coders of the
+      // pictures in flight overlap (each is a handful of latency-bound waves)
+      const EntropyArgs ea = entropy_args(s, dec, pic);
+      static const bool serial = [] {  // TV_ENT_SERIAL=1: entropy on the main stream (diagnostics)
+        const char* e = getenv("TV_ENT_SERIAL");
+        return e && *e == '1';
+      }();
+      hipStream_t es = serial ? stream_ : estream_;
+      launch_entropy_bin(ea, B, es);
+      launch_entropy_ac(ea, B, es);
       stage("entropy");
       HIP_OK(hipGetLastError());
-      HIP_OK(hipEventRecord(s.ev, estream_));
+      HIP_OK(hipEventRecord(s.ev, es));
     } else {
       HIP_OK(hipEventRecord(s.ev, stream_));
     }
@@ -900,12 +950,11 @@ class Core {
   struct EntScratch {
     uint8_t* skip = nullptr;
     int8_t* midx = nullptr;
-    int *ctb_cnt = nullptr, *ctb_off = nullptr, *seg_tok = nullptr;
-    uint32_t* tokens = nullptr;
-    uint8_t* stage = nullptr;
+    int* ctb_cnt = nullptr;
     EntropyTables* tab = nullptr;
   } ent_;
   long tok_cap_ = 0, slot_host_bytes_ = 0;
+  unsigned long long* ent_dbg_ = nullptr;  // TV_ENT_DEBUG=1: coder counters (EntropyArgs::dbg)
   std::atomic<long> ent_fallbacks_{0};
   std::atomic<int> ent_status_{0};
   bool qmap_given_ = false;  // an explicit QP map (2-pass plan) overrides in-engine CRF
@@ -978,6 +1027,7 @@ class Engine {
       cc.batch = std::min(per_, c.batch - g * per_);
       cores_.push_back(std::make_unique<Core>(cc, pool_.get()));
     }
+    for (auto& core : cores_) core->init_entropy_stream();
   }
   ~Engine() {
     intra_timing_report();

@@ -126,24 +126,38 @@ struct EntropyArgs {
   DecisionSet dec;      // the slot's decision planes (qp, cu_log2, intra, ipm, mv, cbf, dir, mv1, tu)
   CompactSet cs;        // the slot's compact levels (mask_y, mask_c, offset, total, packed)
   const uint32_t* sao;  // the slot's SAO parameters (nullptr: SAO off)
-  // per-core scratch (the entropy stream runs one picture at a time)
+  // per-core binariser scratch (the entropy stream binarises one picture at a time)
   uint8_t* skip;        // [B][usz] cu_skip_flag of the unit's CU
   int8_t* midx;         // [B][usz] merge candidate matching the CU's motion (-1: none)
   int* ctb_cnt;         // [B][nctu] tokens of each CTB
+  // per slot (the coders of several pictures run concurrently)
   int* ctb_off;         // [B][nctu] exclusive scan of ctb_cnt within the segment
   int* seg_tok;         // [B] tokens of each segment
   uint32_t* tokens;     // token lists, segments back to back
   long tok_cap;
-  uint8_t* stage;       // per row: 3 bytes per token + 16 (arithmetic coder output, bounded)
+  uint8_t* stage;       // per row: 3 bytes per token + 20 (arithmetic coder output, bounded)
+  int* wflag;           // [B][hc] WPP hand-off: 1 = row's contexts stored in wctx, 2 = aborted
+  uint8_t* wctx;        // [B][hc][kEntCtx] contexts after CTB 1 of each row
   const EntropyTables* tab;
   // the slot's outputs (device -> host in one head copy + one payload copy)
   int* status;          // 0 ok; else the host codes this picture (capacity / consistency)
   int* seg_bytes;       // [B] payload bytes per slice
   int* row_bytes;       // [B][hc] bytes per WPP substream
-  uint8_t* out;         // the slices' substreams, slices back to back
-  long out_cap;
+  // the host slot (pinned, device-visible): the pack kernel writes the head (status,
+  // seg_bytes, row_bytes -- the layout of status / seg_bytes / row_bytes above), the slice QPs
+  // and the payload there directly
+  int* hhead;
+  int8_t* hqp;
+  uint8_t* hout;
+  long hout_cap;
+  // TV_ENT_DEBUG: coder counters (k_ent_ac): rows, context bins, tokens, coding clocks, wait
+  // ticks (100 MHz), max row span (nullptr: off)
+  unsigned long long* dbg = nullptr;
 };
-void launch_entropy(const EntropyArgs& a, int B, hipStream_t s);
+// binarisation (merge/skip pre-pass, token count, scan, token write) and the arithmetic coder +
+// payload packing, on separate streams (the second waits for the first)
+void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s);
+void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s);
 void entropy_tables(EntropyTables& t);
 
 }  // namespace gpu

@@ -43,28 +43,28 @@ struct TokSink {
   int n = 0;
   uint32_t pc = 0, pb = 0;  // pending context bins / bypass bins
   int npc = 0, npb = 0;
-  __device__ void put(uint32_t t) {
+  __device__ __forceinline__ void put(uint32_t t) {
     if (out) out[n] = t;
     ++n;
   }
-  __device__ void flush_c() {
+  __device__ __forceinline__ void flush_c() {
     if (npc) put(kTkCtx | ((uint32_t)npc << 27) | pc);
     npc = 0;
     pc = 0;
   }
-  __device__ void flush_b() {
+  __device__ __forceinline__ void flush_b() {
     if (npb) put(kTkByp | ((uint32_t)npb << 16) | pb);
     npb = 0;
     pb = 0;
   }
-  __device__ void bin(int b, int ctx) {
+  __device__ __forceinline__ void bin(int b, int ctx) {
     flush_b();
     pc |= (uint32_t)(ctx | (b << 8)) << (9 * npc);
     if (++npc == 3) flush_c();
   }
   // consecutive bypass bins are one run: equiprobable bins, so splitting or merging a run
   // never changes the arithmetic code
-  __device__ void bypass(uint32_t v, int nb) {
+  __device__ __forceinline__ void bypass(uint32_t v, int nb) {
     flush_c();
     while (nb > 0) {
       const int take = tv_min(nb, 16 - npb);
@@ -74,33 +74,52 @@ struct TokSink {
       if (npb == 16) flush_b();
     }
   }
-  __device__ void term(int b) {
+  __device__ __forceinline__ void term(int b) {
     flush_c();
     flush_b();
     put(kTkTerm | (uint32_t)b);
   }
-  __device__ void ctrl(uint32_t c) {
+  __device__ __forceinline__ void ctrl(uint32_t c) {
     flush_c();
     flush_b();
     put(kTkCtrl | c);
   }
 };
 
-__constant__ uint8_t c_kCtxIdxMap4x4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
-__constant__ uint8_t c_kGroupIdx[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
-                                        8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
-__constant__ uint8_t c_kMinInGroup[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
-__constant__ uint8_t c_scan4[3][16] = {{0, 4, 1, 8, 5, 2, 12, 9, 6, 3, 13, 10, 7, 14, 11, 15},
-                                       {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
-                                       {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15}};
-
-// Sub-block scans of every TB size (log2 - 2 = 0..3) and scanIdx: raster index (ys << l) + xs
-// of scan position i, and its inverse (hevc_defs.h subblock_pos).
-struct SbTab {
-  uint8_t pos[4][3][64], inv[4][3][64];
+// Residual-coding tables (H.265 9.3.4.2.x), built at compile time, copied to LDS by every
+// binariser workgroup: per-bin table reads from global / constant memory were the kernel's
+// critical path (a dependent ~1 us round trip per bin).
+struct BinTables {
+  uint8_t scan4[3][16];      // in-sub-block scan position -> raster (x | y << 2), scanIdx 0/1/2
+  uint8_t map4[3][16];       // 4x4 TBs: ctxIdxMap of the position
+  uint8_t sigpat[3][4][16];  // larger TBs: sigCtx pattern (0..2) per scanIdx, prevCsbf, position
+  uint8_t group_idx[32];
+  uint8_t min_in_group[16];
+  uint8_t sbpos[4][3][64];   // sub-block scans of every TB size (log2 - 2): raster index of scan pos
+  uint8_t sbinv[4][3][64];   // and its inverse (hevc_defs.h subblock_pos)
 };
-constexpr SbTab make_sbtab() {
-  SbTab t{};
+constexpr BinTables make_tables() {
+  BinTables t{};
+  constexpr uint8_t map[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+  constexpr uint8_t gi[32] = {0, 1, 2, 3, 4, 4, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7,
+                              8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9};
+  constexpr uint8_t mg[10] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 24};
+  for (int i = 0; i < 32; ++i) t.group_idx[i] = gi[i];
+  for (int i = 0; i < 10; ++i) t.min_in_group[i] = mg[i];
+  for (int sc = 0; sc < 3; ++sc)
+    for (int n = 0; n < 16; ++n) {
+      const uint8_t pos = sc == 0 ? kScanDiag4x4[n] : (sc == 1 ? kScanHor4x4[n] : kScanVer4x4[n]);
+      t.scan4[sc][n] = pos;
+      t.map4[sc][n] = map[pos];
+      const int xp = pos & 3, yp = pos >> 2;
+      for (int pc = 0; pc < 4; ++pc) {
+        int v = 2;
+        if (pc == 0) v = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+        else if (pc == 1) v = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
+        else if (pc == 2) v = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
+        t.sigpat[sc][pc][n] = (uint8_t)v;
+      }
+    }
   for (int l = 0; l < 4; ++l)
     for (int sc = 0; sc < 3; ++sc)
       for (int i = 0; i < (1 << (2 * l)); ++i) {
@@ -116,12 +135,23 @@ constexpr SbTab make_sbtab() {
           xs = kScanDiag8x8.s[i] & 7;
           ys = kScanDiag8x8.s[i] >> 3;
         }
-        t.pos[l][sc][i] = (uint8_t)((ys << l) + xs);
-        t.inv[l][sc][(ys << l) + xs] = (uint8_t)i;
+        t.sbpos[l][sc][i] = (uint8_t)((ys << l) + xs);
+        t.sbinv[l][sc][(ys << l) + xs] = (uint8_t)i;
       }
   return t;
 }
-__constant__ SbTab c_sb = make_sbtab();
+__constant__ BinTables c_tab = make_tables();
+static_assert(sizeof(BinTables) % 4 == 0, "copied as words");
+
+// level at raster position p (0..15) of a 4x4 group held as 8 packed int16 pairs
+__device__ __forceinline__ int level_at(const uint4& lo, const uint4& hi, int p) {
+  const int q = p >> 1;
+  const uint32_t a = (q & 1) ? lo.y : lo.x, b = (q & 1) ? lo.w : lo.z;
+  const uint32_t c = (q & 1) ? hi.y : hi.x, d = (q & 1) ? hi.w : hi.z;
+  const uint32_t e = (q & 2) ? b : a, f = (q & 2) ? d : c;
+  const uint32_t w = (q & 4) ? f : e;
+  return (int)(int16_t)(w >> ((p & 1) * 16));
+}
 
 // One segment's picture, as the binariser sees it (device pointers at segment b).
 struct SegView {
@@ -137,7 +167,7 @@ struct SegView {
   int w8, wc, hc, W, H;
 };
 
-__device__ inline SegView seg_view(const EntropyArgs& a, int b) {
+__device__ __forceinline__ SegView seg_view(const EntropyArgs& a, int b) {
   const long U = a.g.usz, nctu = (long)a.g.wc * a.g.hc;
   SegView v;
   v.cu_log2 = a.dec.cu_log2 + b * U;
@@ -165,15 +195,15 @@ __device__ inline SegView seg_view(const EntropyArgs& a, int b) {
   return v;
 }
 
-__device__ inline int unit_of(const SegView& v, int x, int y) { return (y >> 3) * v.w8 + (x >> 3); }
-__device__ inline Motion motion_of(const SegView& v, int u) {
+__device__ __forceinline__ int unit_of(const SegView& v, int x, int y) { return (y >> 3) * v.w8 + (x >> 3); }
+__device__ __forceinline__ Motion motion_of(const SegView& v, int u) {
   Motion m;
   m.dir = v.dir ? v.dir[u] : 1;
   m.mv[0] = Mv{v.mv[2 * u], v.mv[2 * u + 1]};
   if (v.mv1) m.mv[1] = Mv{v.mv1[2 * u], v.mv1[2 * u + 1]};
   return m;
 }
-__device__ inline int cu_cbf(const SegView& v, int x0, int y0, int log2) {
+__device__ __forceinline__ int cu_cbf(const SegView& v, int x0, int y0, int log2) {
   const int u = unit_of(v, x0, y0);
   if (!(v.tu && v.tu[u])) return v.cbf[u];
   const int h = 1 << (log2 - 1);
@@ -183,7 +213,7 @@ __device__ inline int cu_cbf(const SegView& v, int x0, int y0, int log2) {
 }
 
 // Index of the PU's vector in its P-slice merge list, or -1 (hevc_writer.cpp merge_index_p).
-__device__ int merge_index_p(const SegView& v, int x0, int y0, int N, Mv mv, int maxc) {
+__device__ __forceinline__ int merge_index_p(const SegView& v, int x0, int y0, int N, Mv mv, int maxc) {
   auto get = [&](int xn, int yn, Mv& m) {
     const int u = unit_of(v, xn, yn);
     if (v.intra[u]) return false;
@@ -224,7 +254,7 @@ __device__ int merge_index_p(const SegView& v, int x0, int y0, int N, Mv mv, int
   return (mv.x == 0 && mv.y == 0) ? n : -1;
 }
 
-__device__ inline int mvd_cost(int d) {
+__device__ __forceinline__ int mvd_cost(int d) {
   int a = d < 0 ? -d : d;
   if (a == 0) return 1;
   if (a == 1) return 3;
@@ -242,18 +272,19 @@ struct CtbBinariser {
   const SegView& v;
   const EntropyPic& p;
   TokSink& s;
+  const BinTables& T;  // LDS
   bool err = false;
 
-  __device__ int unit(int x, int y) const { return unit_of(v, x, y); }
-  __device__ void bin(int b, int ctx) { s.bin(b, ctx); }
-  __device__ int skip_inc(int x0, int y0) const {
+  __device__ __forceinline__ int unit(int x, int y) const { return unit_of(v, x, y); }
+  __device__ __forceinline__ void bin(int b, int ctx) { s.bin(b, ctx); }
+  __device__ __forceinline__ int skip_inc(int x0, int y0) const {
     int inc = 0;
     if (x0 > 0 && v.skip[unit(x0 - 1, y0)]) ++inc;
     if (y0 > 0 && v.skip[unit(x0, y0 - 1)]) ++inc;
     return inc;
   }
 
-  __device__ void sao(int cx, int cy) {
+  __device__ __forceinline__ void sao(int cx, int cy) {
     const uint32_t off = sao_off_param();
     const uint32_t* q = v.sao ? v.sao + 3 * (cy * v.wc + cx) : nullptr;
     const uint32_t pr[3] = {q ? q[0] : off, q ? q[1] : off, q ? q[2] : off};
@@ -290,12 +321,12 @@ struct CtbBinariser {
     }
   }
 
-  __device__ void merge_idx_syntax(int idx) {
+  __device__ __forceinline__ void merge_idx_syntax(int idx) {
     if (p.max_merge <= 1) return;
     bin(idx > 0, CTX_MERGE_IDX);
     for (int i = 1; i < p.max_merge - 1 && idx >= i; ++i) s.bypass(idx > i, 1);
   }
-  __device__ void eg1(uint32_t val) {
+  __device__ __forceinline__ void eg1(uint32_t val) {
     int k = 1;
     while (val >= (1u << k)) {
       s.bypass(1, 1);
@@ -305,7 +336,7 @@ struct CtbBinariser {
     s.bypass(0, 1);
     s.bypass(val, k);
   }
-  __device__ void mvd(int dx, int dy) {
+  __device__ __forceinline__ void mvd(int dx, int dy) {
     const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
     bin(ax > 0, CTX_MVD_G0);
     bin(ay > 0, CTX_MVD_G0);
@@ -327,7 +358,7 @@ struct CtbBinariser {
     int base, gw, skipc;
     const int16_t* groups;
   };
-  __device__ void tb_view(int c, int x, int y, int log2N, Tb& t) const {
+  __device__ __forceinline__ void tb_view(int c, int x, int y, int log2N, Tb& t) const {
     const int nsb = 1 << (log2N - 2), sh = c ? 4 : 5;
     t.gw = c ? 4 : 8;
     const int ctb = (y >> sh) * v.wc + (x >> sh);
@@ -340,25 +371,29 @@ struct CtbBinariser {
     t.groups = v.packed + (long)v.sb_off[ctb] * 16;
     t.skipc = c ? __popcll(my) : 0;
   }
-  __device__ const int16_t* group_of(const Tb& t, int log2N, int r) const {
+  __device__ __forceinline__ const int16_t* group_of(const Tb& t, int log2N, int r) const {
     const int bit = t.base + (r >> (log2N - 2)) * t.gw + (r & ((1 << (log2N - 2)) - 1));
     return t.groups + (long)(t.skipc + __popcll(t.m & ((1ull << bit) - 1))) * 16;
   }
-  // bit n: scan position n of the group is non-zero
-  __device__ unsigned sig_mask(const int16_t* g, int scanIdx) const {
-    const uint4 lo = *reinterpret_cast<const uint4*>(g), hi = *reinterpret_cast<const uint4*>(g + 8);
+  // bit n: scan position n of the group (levels in lo / hi) is non-zero
+  __device__ __forceinline__ unsigned sig_mask(const uint4& lo, const uint4& hi, int scanIdx) const {
     const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     unsigned raster = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       raster |= (((w[j] & 0xffffu) != 0) ? 1u : 0u) << (2 * j) | (((w[j] >> 16) != 0) ? 1u : 0u) << (2 * j + 1);
     unsigned m = 0;
+    const uint8_t* sc = T.scan4[scanIdx];
 #pragma unroll
-    for (int n = 0; n < 16; ++n) m |= ((raster >> c_scan4[scanIdx][n]) & 1u) << n;
+    for (int n = 0; n < 16; ++n) m |= ((raster >> sc[n]) & 1u) << n;
     return m;
   }
-  __device__ void last_prefix(int pos, int log2N, int cIdx, int base) {
-    const int prefix = c_kGroupIdx[pos];
+  __device__ __forceinline__ static void load_group(const int16_t* g, uint4& lo, uint4& hi) {
+    lo = *reinterpret_cast<const uint4*>(g);
+    hi = *reinterpret_cast<const uint4*>(g + 8);
+  }
+  __device__ __forceinline__ void last_prefix(int pos, int log2N, int cIdx, int base) {
+    const int prefix = T.group_idx[pos];
     int off, shift;
     if (cIdx == 0) {
       off = 3 * (log2N - 2) + ((log2N - 1) >> 2);
@@ -371,11 +406,11 @@ struct CtbBinariser {
     for (int i = 0; i < prefix; ++i) bin(1, base + off + (i >> shift));
     if (prefix < cmax) bin(0, base + off + (prefix >> shift));
   }
-  __device__ void last_suffix(int pos) {
-    const int prefix = c_kGroupIdx[pos];
-    if (prefix > 3) s.bypass((uint32_t)(pos - c_kMinInGroup[prefix]), (prefix >> 1) - 1);
+  __device__ __forceinline__ void last_suffix(int pos) {
+    const int prefix = T.group_idx[pos];
+    if (prefix > 3) s.bypass((uint32_t)(pos - T.min_in_group[prefix]), (prefix >> 1) - 1);
   }
-  __device__ void remaining(int val, int rice) {
+  __device__ __forceinline__ void remaining(int val, int rice) {
     if (val < (4 << rice)) {
       const int pfx = val >> rice;
       s.bypass(((1u << (pfx + 1)) - 2) << rice | (uint32_t)(val & ((1 << rice) - 1)), pfx + 1 + rice);
@@ -397,31 +432,25 @@ struct CtbBinariser {
       s.bypass(r, k);
     }
   }
-  __device__ static int sig_pattern(int pc, int sc, int n) {
-    const int pos = c_scan4[sc][n], xp = pos & 3, yp = pos >> 2;
-    if (pc == 0) return (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
-    if (pc == 1) return (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
-    if (pc == 2) return (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
-    return 2;
-  }
-  __device__ void residual(const Tb& t, int log2N, int cIdx, int scanIdx) {
+  __device__ __forceinline__ void residual(const Tb& t, int log2N, int cIdx, int scanIdx) {
     const int nsb = 1 << (log2N - 2), lsb = log2N - 2;
     if (!t.nz) {
       err = true;
       return;
     }
     // last significant sub-block in scan order, then its last non-zero position
-    const uint8_t* sbpos = c_sb.pos[lsb][scanIdx];
-    const uint8_t* sbinv = c_sb.inv[lsb][scanIdx];
+    const uint8_t* sbpos = T.sbpos[lsb][scanIdx];
+    const uint8_t* sbinv = T.sbinv[lsb][scanIdx];
     int lastSb = 0;
     for (uint64_t bb = t.nz; bb; bb &= bb - 1) lastSb = tv_max(lastSb, (int)sbinv[__ffsll((long long)bb) - 1]);
     const int lxs = sbpos[lastSb] & (nsb - 1), lys = sbpos[lastSb] >> lsb;
-    const unsigned lastMask = sig_mask(group_of(t, log2N, lys * nsb + lxs), scanIdx);
+    uint4 llo, lhi;
+    load_group(group_of(t, log2N, lys * nsb + lxs), llo, lhi);
+    const unsigned lastMask = sig_mask(llo, lhi, scanIdx);
     const int lastN = 31 - __clz(lastMask);
     {
-      int xc, yc;
-      coef_pos_in_sb(scanIdx, lastN, xc, yc);
-      int lx = (lxs << 2) + xc, ly = (lys << 2) + yc;
+      const int pc = T.scan4[scanIdx][lastN];
+      int lx = (lxs << 2) + (pc & 3), ly = (lys << 2) + (pc >> 2);
       if (scanIdx == 2) {
         const int tmp = lx;
         lx = ly;
@@ -448,200 +477,140 @@ struct CtbBinariser {
         inferDc = true;
       }
       coded |= 1ull << r;
-      const int16_t* g = any ? group_of(t, log2N, r) : nullptr;
-      const unsigned m = i == lastSb ? lastMask : (any ? sig_mask(g, scanIdx) : 0u);
+      uint4 lo = llo, hi = lhi;
+      if (i != lastSb && any) load_group(group_of(t, log2N, r), lo, hi);
+      const unsigned m = i == lastSb ? lastMask : (any ? sig_mask(lo, hi, scanIdx) : 0u);
       const int prevCsbf = right + (below << 1);
       const int add = log2N == 2 ? compOff : compOff + sizeOff + ((cIdx == 0 && i > 0) ? 3 : 0);
       const int nStart = (i == lastSb) ? lastN - 1 : 15;
       const bool dcInferred = inferDc && (m & ((2u << nStart) - 2)) == 0;
-      for (int n = nStart; n >= 1; --n) {
-        const int pat = log2N == 2 ? c_kCtxIdxMap4x4[c_scan4[scanIdx][n]] : sig_pattern(prevCsbf, scanIdx, n);
-        bin((m >> n) & 1, add + pat);
-      }
-      if (nStart >= 0 && !dcInferred) {
-        const int pat0 = log2N == 2 ? c_kCtxIdxMap4x4[c_scan4[scanIdx][0]] : sig_pattern(prevCsbf, scanIdx, 0);
-        bin(m & 1, (log2N > 2 && i == 0) ? compOff : add + pat0);
-      }
-      // levels in reverse scan order
-      int absv[16];
-      uint32_t sbits = 0;
-      int cnt = 0;
-      for (unsigned sm = m; sm; ++cnt) {
-        const int n = 31 - __clz(sm);
-        sm &= ~(1u << n);
-        const int x = g[c_scan4[scanIdx][n]];
-        absv[cnt] = x < 0 ? -x : x;
-        sbits = (sbits << 1) | (x < 0 ? 1u : 0u);
-      }
+      const uint8_t* pat = log2N == 2 ? T.map4[scanIdx] : T.sigpat[scanIdx][prevCsbf];
+      for (int n = nStart; n >= 1; --n) bin((m >> n) & 1, add + pat[n]);
+      if (nStart >= 0 && !dcInferred) bin(m & 1, (log2N > 2 && i == 0) ? compOff : add + pat[0]);
+      // levels in reverse scan order, read from the group's registers (two passes: greater-1
+      // / greater-2 flags and signs, then the remaining absolute levels)
+      const uint8_t* sc = T.scan4[scanIdx];
       int ctxSet = (i > 0 && cIdx == 0) ? 2 : 0;
       if (c1 == 0) ++ctxSet;
       c1 = 1;
       const int g1base = CTX_G1 + 4 * ctxSet + (cIdx ? 16 : 0);
-      const int nG1 = cnt < 8 ? cnt : 8;
-      int firstG2 = -1;
-      for (int k = 0; k < nG1; ++k) {
-        const int bn = absv[k] > 1;
-        bin(bn, g1base + c1);
-        if (bn) {
-          c1 = 0;
-          if (firstG2 < 0) firstG2 = k;
-        } else if (c1 > 0 && c1 < 3) {
-          ++c1;
+      uint32_t sbits = 0;
+      int cnt = 0, g2 = -1;
+      for (unsigned sm = m; sm; ++cnt) {
+        const int n = 31 - __clz(sm);
+        sm &= ~(1u << n);
+        const int x = level_at(lo, hi, sc[n]), a = x < 0 ? -x : x;
+        sbits = (sbits << 1) | (x < 0 ? 1u : 0u);
+        if (cnt < 8) {
+          const int bn = a > 1;
+          bin(bn, g1base + c1);
+          if (bn) {
+            c1 = 0;
+            if (g2 < 0) g2 = a > 2;
+          } else if (c1 > 0 && c1 < 3) {
+            ++c1;
+          }
         }
       }
-      if (firstG2 >= 0) bin(absv[firstG2] > 2, CTX_G2 + ctxSet + (cIdx ? 4 : 0));
+      if (g2 >= 0) bin(g2, CTX_G2 + ctxSet + (cIdx ? 4 : 0));
       if (cnt) s.bypass(sbits, cnt);
-      int rice = 0;
+      int rice = 0, k = 0;
       bool firstC2 = true;
-      for (int k = 0; k < cnt; ++k) {
+      for (unsigned sm = m; sm; ++k) {
+        const int n = 31 - __clz(sm);
+        sm &= ~(1u << n);
+        const int x = level_at(lo, hi, sc[n]), a = x < 0 ? -x : x;
         const int base = (k < 8) ? (firstC2 ? 3 : 2) : 1;
-        if (absv[k] >= base) {
-          remaining(absv[k] - base, rice);
-          if (absv[k] > 3 * (1 << rice)) rice = tv_min(rice + 1, 4);
+        if (a >= base) {
+          remaining(a - base, rice);
+          if (a > 3 * (1 << rice)) rice = tv_min(rice + 1, 4);
         }
-        if (absv[k] >= 2) firstC2 = false;
+        if (a >= 2) firstC2 = false;
       }
     }
   }
 
-  __device__ bool tu_split(int x0, int y0) const { return v.tu && v.tu[unit(x0, y0)]; }
-  __device__ void transform_split(int x0, int y0, int log2) {
-    const int h = 1 << (log2 - 1), l = log2 - 1;
-    int c[4], cb0 = 0, cr0 = 0;
-    for (int q = 0; q < 4; ++q) {
-      c[q] = v.cbf[unit(x0 + (q & 1) * h, y0 + (q >> 1) * h)];
-      cb0 |= (c[q] >> 1) & 1;
-      cr0 |= (c[q] >> 2) & 1;
-    }
-    bin(cb0, CTX_CBF_CHROMA + 0);
-    bin(cr0, CTX_CBF_CHROMA + 0);
-    for (int q = 0; q < 4; ++q) {
-      const int x = x0 + (q & 1) * h, y = y0 + (q >> 1) * h;
-      const int cl = c[q] & 1, cb = (c[q] >> 1) & 1, cr = (c[q] >> 2) & 1;
-      if (cb0) bin(cb, CTX_CBF_CHROMA + 1);
-      if (cr0) bin(cr, CTX_CBF_CHROMA + 1);
-      bin(cl, CTX_CBF_LUMA + 0);
-      Tb t;
-      if (cl) {
-        tb_view(0, x, y, l, t);
-        residual(t, l, 0, 0);
-      }
-      if (cb) {
-        tb_view(1, x >> 1, y >> 1, l - 1, t);
-        residual(t, l - 1, 1, 0);
-      }
-      if (cr) {
-        tb_view(2, x >> 1, y >> 1, l - 1, t);
-        residual(t, l - 1, 2, 0);
-      }
-    }
-  }
-  __device__ void transform_tree(int x0, int y0, int log2, bool intra, int mode) {
-    if (!intra && p.rqt) {
-      const bool split = tu_split(x0, y0);
+  __device__ __forceinline__ bool tu_split(int x0, int y0) const { return v.tu && v.tu[unit(x0, y0)]; }
+
+  // transform_tree (7.3.8.8) of a CU: depth 0, or (inter CUs with RQT) four depth-1 TUs.  One
+  // residual call site and one TU loop, so the whole binariser inlines into registers.
+  __device__ __forceinline__ void transform_tree(int x0, int y0, int log2, bool intra, int mode) {
+    bool split = false;
+    if (!intra && p.rqt) {  // split_transform_flag of an inter CU (depth 0, ctx 5 - log2)
+      split = tu_split(x0, y0);
       bin(split ? 1 : 0, CTX_SPLIT_TF + 5 - log2);
+    }
+    const int h = 1 << (log2 - 1), l = split ? log2 - 1 : log2;
+    int cb0 = 0, cr0 = 0;
+    if (split) {  // chroma cbfs at depth 0: the OR of the quadrants'
+      for (int q = 0; q < 4; ++q) {
+        const int c = v.cbf[unit(x0 + (q & 1) * h, y0 + (q >> 1) * h)];
+        cb0 |= (c >> 1) & 1;
+        cr0 |= (c >> 2) & 1;
+      }
+      bin(cb0, CTX_CBF_CHROMA + 0);
+      bin(cr0, CTX_CBF_CHROMA + 0);
+    }
+    const int cmode = intra ? mode : 0;  // chroma: DM (intra_chroma_pred_mode 4)
+    for (int q = 0; q < (split ? 4 : 1); ++q) {
+      const int x = x0 + (q & 1) * h, y = y0 + (q >> 1) * h;
+      const int cbf = v.cbf[unit(x, y)];
+      const int cl = cbf & 1, cb = (cbf >> 1) & 1, cr = (cbf >> 2) & 1;
       if (split) {
-        transform_split(x0, y0, log2);
-        return;
+        if (cb0) bin(cb, CTX_CBF_CHROMA + 1);
+        if (cr0) bin(cr, CTX_CBF_CHROMA + 1);
+        bin(cl, CTX_CBF_LUMA + 0);
+      } else {
+        bin(cb, CTX_CBF_CHROMA + 0);  // log2 >= 3: chroma cbfs coded at depth 0
+        bin(cr, CTX_CBF_CHROMA + 0);
+        if (intra || cb || cr) bin(cl, CTX_CBF_LUMA + 1);
+        else if (!cl) err = true;  // inter CU with rqt_root_cbf = 1 but no residual
+      }
+      for (int c = 0; c < 3; ++c) {
+        if (!((cbf >> c) & 1)) continue;
+        const int lc = c ? l - 1 : l;
+        Tb t;
+        tb_view(c, c ? x >> 1 : x, c ? y >> 1 : y, lc, t);
+        residual(t, lc, c, split ? 0 : scan_idx_for(intra, lc, c, c ? cmode : mode));
       }
     }
-    const int cbf = v.cbf[unit(x0, y0)];
-    const int cl = cbf & 1, cb = (cbf >> 1) & 1, cr = (cbf >> 2) & 1;
-    bin(cb, CTX_CBF_CHROMA + 0);
-    bin(cr, CTX_CBF_CHROMA + 0);
-    if (intra || cb || cr) bin(cl, CTX_CBF_LUMA + 1);
-    else if (!cl) err = true;  // inter CU with rqt_root_cbf = 1 but no residual
-    const int cmode = intra ? chroma_intra_mode_dm(mode) : 0;
-    Tb t;
-    if (cl) {
-      tb_view(0, x0, y0, log2, t);
-      residual(t, log2, 0, scan_idx_for(intra, log2, 0, mode));
-    }
-    if (cb) {
-      tb_view(1, x0 >> 1, y0 >> 1, log2 - 1, t);
-      residual(t, log2 - 1, 1, scan_idx_for(intra, log2 - 1, 1, cmode));
-    }
-    if (cr) {
-      tb_view(2, x0 >> 1, y0 >> 1, log2 - 1, t);
-      residual(t, log2 - 1, 2, scan_idx_for(intra, log2 - 1, 2, cmode));
-    }
   }
-  __device__ static int chroma_intra_mode_dm(int luma_mode) { return luma_mode; }  // idx 4 (DM)
 
-  __device__ void amvp_mvd_p(int x0, int y0, int N, Mv mv) {
-    Mv mvp[2];
-    auto f = [&](int xn, int yn, Mv& m) {
+  __device__ __forceinline__ void amvp_mvd(int x0, int y0, int N, int X, const Motion& m) {
+    auto at = [&](int xn, int yn, Motion& o) {
       if (!zscan_available(x0, y0, xn, yn, v.W, v.H)) return false;
-      const int u = unit(xn, yn);
-      if (v.intra[u]) return false;
-      m.x = v.mv[2 * u];
-      m.y = v.mv[2 * u + 1];
+      const int un = unit(xn, yn);
+      if (v.intra[un]) return false;
+      o = motion_of(v, un);
       return true;
     };
-    amvp_candidates(x0, y0, N, N, f, mvp);
-    const int c0 = mvd_cost(mv.x - mvp[0].x) + mvd_cost(mv.y - mvp[0].y);
-    const int c1 = mvd_cost(mv.x - mvp[1].x) + mvd_cost(mv.y - mvp[1].y);
+    Mv mvp[2];
+    if (p.type == 0) {
+      amvp_candidates_b(x0, y0, N, N, X, p.ref_poc, p.poc, at, mvp);
+    } else {
+      auto f = [&](int xn, int yn, Mv& o) {
+        Motion mm;
+        if (!at(xn, yn, mm)) return false;
+        o = mm.mv[0];
+        return true;
+      };
+      amvp_candidates(x0, y0, N, N, f, mvp);
+    }
+    const Mv vv = m.mv[X];
+    const int c0 = mvd_cost(vv.x - mvp[0].x) + mvd_cost(vv.y - mvp[0].y);
+    const int c1 = mvd_cost(vv.x - mvp[1].x) + mvd_cost(vv.y - mvp[1].y);
     const int sel = c1 < c0 ? 1 : 0;
-    mvd(mv.x - mvp[sel].x, mv.y - mvp[sel].y);
+    mvd(vv.x - mvp[sel].x, vv.y - mvp[sel].y);
     bin(sel, CTX_MVP_FLAG);
   }
 
-  __device__ void coding_unit_b(int x0, int y0, int log2, int cbf) {
-    const int u = unit(x0, y0), N = 1 << log2;
-    const Motion m = motion_of(v, u);
-    const int merge_idx = v.midx[u];
-    const bool skip = merge_idx >= 0 && cbf == 0;
-    bin(skip ? 1 : 0, CTX_CU_SKIP + skip_inc(x0, y0));
-    if (skip) {
-      merge_idx_syntax(merge_idx);
-      return;
-    }
-    bin(0, CTX_PRED_MODE);
-    bin(1, CTX_PART_MODE);
-    bin(merge_idx >= 0 ? 1 : 0, CTX_MERGE_FLAG);
-    if (merge_idx >= 0) {
-      merge_idx_syntax(merge_idx);
-    } else {
-      bin(m.dir == 3 ? 1 : 0, CTX_INTER_PRED_IDC + (kCtbLog2 - log2));
-      if (m.dir != 3) bin(m.dir == 2 ? 1 : 0, CTX_INTER_PRED_IDC + 4);
-      auto at = [&](int xn, int yn, Motion& o) {
-        if (!zscan_available(x0, y0, xn, yn, v.W, v.H)) return false;
-        const int un = unit(xn, yn);
-        if (v.intra[un]) return false;
-        o = motion_of(v, un);
-        return true;
-      };
-      for (int X = 0; X < 2; ++X) {
-        if (!((m.dir >> X) & 1)) continue;
-        Mv mvp[2];
-        amvp_candidates_b(x0, y0, N, N, X, p.ref_poc, p.poc, at, mvp);
-        const Mv vv = m.mv[X];
-        const int c0 = mvd_cost(vv.x - mvp[0].x) + mvd_cost(vv.y - mvp[0].y);
-        const int c1 = mvd_cost(vv.x - mvp[1].x) + mvd_cost(vv.y - mvp[1].y);
-        const int sel = c1 < c0 ? 1 : 0;
-        mvd(vv.x - mvp[sel].x, vv.y - mvp[sel].y);
-        bin(sel, CTX_MVP_FLAG);
-      }
-      bin(cbf ? 1 : 0, CTX_RQT_ROOT_CBF);
-      if (!cbf) return;
-    }
-    transform_tree(x0, y0, log2, false, 0);
-  }
-
-  __device__ void coding_unit(int x0, int y0, int log2) {
+  // coding_unit (7.3.8.5): skip / merge / AMVP from the motion field (P and B), intra modes
+  __device__ __forceinline__ void coding_unit(int x0, int y0, int log2) {
     const int u = unit(x0, y0), N = 1 << log2;
     const bool intra = v.intra[u] != 0;
     const int cbf = cu_cbf(v, x0, y0, log2);
     const bool islice = p.type == 2, bslice = p.type == 0;
-    if (bslice && !intra) {
-      coding_unit_b(x0, y0, log2, cbf);
-      return;
-    }
-    if (bslice) {
-      bin(0, CTX_CU_SKIP + skip_inc(x0, y0));
-      bin(1, CTX_PRED_MODE);
-    } else if (!islice) {
-      const Mv mv{v.mv[2 * u], v.mv[2 * u + 1]};
+    if (!islice) {
       const int merge_idx = intra ? -1 : v.midx[u];
       const bool skip = !intra && merge_idx >= 0 && cbf == 0;
       bin(skip ? 1 : 0, CTX_CU_SKIP + skip_inc(x0, y0));
@@ -649,15 +618,20 @@ struct CtbBinariser {
         merge_idx_syntax(merge_idx);
         return;
       }
-      bin(intra ? 1 : 0, CTX_PRED_MODE);
+      bin(intra ? 1 : 0, CTX_PRED_MODE);  // pred_mode_flag
       if (!intra) {
-        bin(1, CTX_PART_MODE);
-        const bool merge = merge_idx >= 0;
-        bin(merge ? 1 : 0, CTX_MERGE_FLAG);
-        if (merge) {
+        bin(1, CTX_PART_MODE);  // part_mode 2Nx2N
+        bin(merge_idx >= 0 ? 1 : 0, CTX_MERGE_FLAG);
+        if (merge_idx >= 0) {
           merge_idx_syntax(merge_idx);
         } else {
-          amvp_mvd_p(x0, y0, N, mv);
+          const Motion m = motion_of(v, u);
+          if (bslice) {  // inter_pred_idc: bin 0 (PRED_BI?) at ctx CtDepth, bin 1 (L1?) at ctx 4
+            bin(m.dir == 3 ? 1 : 0, CTX_INTER_PRED_IDC + (kCtbLog2 - log2));
+            if (m.dir != 3) bin(m.dir == 2 ? 1 : 0, CTX_INTER_PRED_IDC + 4);
+          }
+          for (int X = 0; X < 2; ++X)
+            if ((m.dir >> X) & 1) amvp_mvd(x0, y0, N, X, m);
           bin(cbf ? 1 : 0, CTX_RQT_ROOT_CBF);
           if (!cbf) return;
         }
@@ -665,7 +639,7 @@ struct CtbBinariser {
         return;
       }
     }
-    if (log2 == kMinCbLog2) bin(1, CTX_PART_MODE);
+    if (log2 == kMinCbLog2) bin(1, CTX_PART_MODE);  // 2Nx2N
     const int mode = v.ipm[u];
     int candA = 1, candB = 1;
     if (x0 > 0 && v.intra[unit(x0 - 1, y0)]) candA = v.ipm[unit(x0 - 1, y0)];
@@ -673,48 +647,38 @@ struct CtbBinariser {
       candB = v.ipm[unit(x0, y0 - 1)];
     int mpm[3];
     intra_mpm_list(candA, candB, mpm);
-    int idx = -1;
-    for (int i = 0; i < 3; ++i)
-      if (mpm[i] == mode) idx = i;
+    const int idx = mpm[0] == mode ? 0 : (mpm[1] == mode ? 1 : (mpm[2] == mode ? 2 : -1));
     bin(idx >= 0 ? 1 : 0, CTX_PREV_INTRA);
     if (idx >= 0) {
       if (idx == 0) s.bypass(0, 1);
       else s.bypass(idx == 1 ? 2 : 3, 2);
-    } else {
+    } else {  // rem_intra_luma_pred_mode: the mode minus the MPMs below it
       const int rem = mode - (mode > mpm[0]) - (mode > mpm[1]) - (mode > mpm[2]);
       s.bypass((uint32_t)rem, 5);
     }
-    bin(0, CTX_CHROMA_PRED);
+    bin(0, CTX_CHROMA_PRED);  // intra_chroma_pred_mode = 4 (DM)
     transform_tree(x0, y0, log2, true, mode);
   }
 
-  __device__ void split_flag(int x0, int y0, int log2, bool split) {
-    const int depth = kCtbLog2 - log2;
-    int inc = 0;
-    if (x0 > 0 && (kCtbLog2 - v.cu_log2[unit(x0 - 1, y0)]) > depth) ++inc;
-    if (y0 > 0 && (kCtbLog2 - v.cu_log2[unit(x0, y0 - 1)]) > depth) ++inc;
-    bin(split ? 1 : 0, CTX_SPLIT_CU + inc);
-  }
-
-  // coding_quadtree of the 32x32 CTB (depth <= 2: 32 -> 16 -> 8), then the end-of-CTB syntax
-  __device__ void ctb(int cx, int cy, bool sao_on) {
+  // coding_quadtree of the 32x32 CTB as a z-order walk (one split-flag and one coding_unit
+  // call site), then the end-of-CTB syntax and the WPP marks
+  __device__ __forceinline__ void ctb(int cx, int cy, bool sao_on) {
     if (sao_on) sao(cx, cy);
     const int X = cx << kCtbLog2, Y = cy << kCtbLog2;
-    const bool s32 = v.cu_log2[unit(X, Y)] < 5;
-    split_flag(X, Y, 5, s32);
-    if (!s32) {
-      coding_unit(X, Y, 5);
-    } else {
-      for (int q = 0; q < 4; ++q) {
-        const int x1 = X + (q & 1) * 16, y1 = Y + (q >> 1) * 16;
-        const bool s16 = v.cu_log2[unit(x1, y1)] < 4;
-        split_flag(x1, y1, 4, s16);
-        if (!s16) {
-          coding_unit(x1, y1, 4);
-        } else {
-          for (int k = 0; k < 4; ++k) coding_unit(x1 + (k & 1) * 8, y1 + (k >> 1) * 8, 3);
-        }
+    for (int z = 0; z < 16;) {
+      const int x = X + 8 * ((z & 1) | ((z >> 1) & 2)), y = Y + 8 * (((z >> 1) & 1) | ((z >> 2) & 2));
+      int l = z == 0 ? 5 : ((z & 3) == 0 ? 4 : 3);
+      for (; l > kMinCbLog2; --l) {  // split_cu_flag of every node that starts here, top down
+        const bool split = v.cu_log2[unit(x, y)] < l;
+        const int depth = kCtbLog2 - l;
+        int inc = 0;
+        if (x > 0 && (kCtbLog2 - v.cu_log2[unit(x - 1, y)]) > depth) ++inc;
+        if (y > 0 && (kCtbLog2 - v.cu_log2[unit(x, y - 1)]) > depth) ++inc;
+        bin(split ? 1 : 0, CTX_SPLIT_CU + inc);
+        if (!split) break;
       }
+      coding_unit(x, y, l);
+      z += 1 << (2 * (l - kMinCbLog2));
     }
     const bool last = cy == v.hc - 1 && cx == v.wc - 1;
     if (cx == 1) s.ctrl(kCtrlSync);  // 9.3.2.4 storage after the row's second CTB
@@ -768,6 +732,14 @@ __global__ void __launch_bounds__(256) k_ent_cu(EntropyArgs a) {
 // One thread per CTB: count (WRITE = false) or write its tokens.
 template <bool WRITE>
 __global__ void __launch_bounds__(64) k_ent_bin(EntropyArgs a) {
+  __builtin_amdgcn_s_setprio(2);  // latency-bound per-lane chains beside the analysis kernels
+  __shared__ BinTables T;
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&c_tab);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
+    for (int k = threadIdx.x; k < (int)(sizeof(BinTables) / 4); k += 64) dst[k] = src[k];
+  }
+  __syncthreads();
   const int b = blockIdx.y, nctu = a.g.wc * a.g.hc;
   const int ctu = blockIdx.x * 64 + threadIdx.x;
   if (ctu >= nctu) return;
@@ -781,7 +753,7 @@ __global__ void __launch_bounds__(64) k_ent_bin(EntropyArgs a) {
   }
   const SegView v = seg_view(a, b);
   TokSink s{out};
-  CtbBinariser z{v, a.pic, s};
+  CtbBinariser z{v, a.pic, s, T};
   z.ctb(ctu % v.wc, ctu / v.wc, a.pic.sao != 0);
   s.flush_c();
   s.flush_b();
@@ -822,13 +794,106 @@ __global__ void k_ent_check(EntropyArgs a, int B) {
   if (t > a.tok_cap) atomicOr(a.status, 1);
 }
 
-// ---- arithmetic coder: one workgroup per slice, lane = CTB row --------------------------
-struct AcLane {
+// ---- arithmetic coder -------------------------------------------------------------------
+
+// Staging of a row's output: 4-aligned, 3 bytes per token + 20 of slack per row (a context-coded
+// token is at most 3 bins x 6 renormalisation bits, a bypass token 16 bits; the flush adds <= 4
+// bytes), so rows never overlap.
+__device__ __forceinline__ long stage_off(long tpos, long row_idx) { return (3 * tpos + 20 * row_idx + 3) & ~3L; }
+
+constexpr int kCtxN = CTX_COUNT;
+constexpr int kTokT = 64;   // token ring entries
+constexpr int kTokK = 32;   // tokens per refill
+
+
+// One WAVE per CTB row (substream), one active lane: every value of the coder is wave-uniform
+// (the compiler runs it on the scalar unit; context states and tables in LDS).  A lane-per-row
+// layout executed the union of every row's path each iteration with two thirds of the rows
+// still waiting on WPP (~1500 clocks per bin); this runs ~700 (TV_ENT_DEBUG).  (Context states
+// in VGPRs via wave-uniform indexed moves measured slower: ~970.)  The WPP storage (9.3.2.4) goes to the row below through
+// global memory: plain stores, agent release fence, flag; the reader polls the flag
+// (agent-scope atomic load = sc1, no stale L1), then acquires.  Workgroups are dispatched in
+// row order, so a row only ever waits on a row that is already running.  Tokens come through a
+// 64-entry LDS ring refilled 32 at a time (a token load kept in registers across the loop's
+// branches forces a vmcnt(0) wait at its use); output bytes leave as dword stores.
+__global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
+  __shared__ uint8_t lps[256], tlps[64], ctx[kEntCtx];
+  for (int k = threadIdx.x; k < 256; k += 64) lps[k] = a.tab->lps[k];
+  tlps[threadIdx.x] = a.tab->tlps[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  __builtin_amdgcn_s_setprio(3);  // a latency-bound chain beside the analysis waves
+  const int row = blockIdx.x, b = blockIdx.y;
+  const int wc = a.g.wc, hc = a.g.hc, nctu = wc * hc;
+  __shared__ uint4 tring[kTokT / 4];
+  const uint32_t* tring32 = reinterpret_cast<const uint32_t*>(tring);
+  int* wflag = a.wflag + (long)b * hc;
+  uint32_t* wctx = reinterpret_cast<uint32_t*>(a.wctx + (long)b * hc * kEntCtx);
+  if (*a.status) {  // the binariser gave up on this picture: the host codes it
+    __hip_atomic_store(&wflag[row], 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  long tbase = 0;
+  for (int k = 0; k < b; ++k) tbase += a.seg_tok[k];
+  const int* off = a.ctb_off + (long)b * nctu;
+  const long tpos = tbase + off[row * wc];
+  long ntok = (row + 1 < hc ? tbase + off[(row + 1) * wc] : tbase + a.seg_tok[b]) - tpos;
+  uint32_t* out = reinterpret_cast<uint32_t*>(a.stage + stage_off(tpos, (long)b * hc + row));
+  long head = tpos, tail = tpos & ~3L;  // next token to code / to load (whole uint4s)
+  const uint4* gtok = reinterpret_cast<const uint4*>(a.tokens);
+  auto refill = [&]() {
+    uint4 v[kTokK / 4];
+#pragma unroll
+    for (int k = 0; k < kTokK / 4; ++k) v[k] = gtok[(tail >> 2) + k];
+#pragma unroll
+    for (int k = 0; k < kTokK / 4; ++k) tring[((tail >> 2) + k) & (kTokT / 4 - 1)] = v[k];
+    tail += kTokK;
+  };
+  refill();
+  refill();
+  auto abort_row = [&](int code) {
+    atomicOr(a.status, code);
+    __hip_atomic_store(&wflag[row], 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  const unsigned long long w0 = wall_clock64();
+  // contexts: row 0 from the init table, else the row above's after its CTB 1
+  const uint32_t* src;
+  if (row == 0) {
+    src = reinterpret_cast<const uint32_t*>(a.tab->init[a.pic.init_type][clip3(0, 51, (int)a.dec.qp[b])]);
+  } else {
+    int f = 0;
+    for (long spin = 0; (f = __hip_atomic_load(&wflag[row - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0;
+         ++spin) {
+      if (spin > (1L << 26)) {  // seconds: the row above never came (never expected)
+        abort_row(32);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (f != 1) {  // the row above aborted: so does this one
+      __hip_atomic_store(&wflag[row], 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    src = wctx + (long)(row - 1) * (kEntCtx / 4);
+  }
+  uint32_t* ctx32 = reinterpret_cast<uint32_t*>(ctx);
+#pragma unroll
+  for (int i = 0; i < kEntCtx / 4; ++i) ctx32[i] = src[i];
+  // coder state (CabacEncoder): low, range, bits left, outstanding bytes, buffered byte
   uint32_t low = 0, range = 510, buffered = 0xff;
   int bl = 23, nbuf = 0, pos = 0;
-  uint8_t* out;
-  __device__ void emit(uint32_t byte) { out[pos++] = (uint8_t)byte; }
-  __device__ void write_out() {
+  uint32_t ow = 0;  // output bytes not yet stored (little-endian = memory order)
+  const unsigned long long w1 = wall_clock64(), c1 = clock64();
+  long nctxbins = 0, ntoks = 0;
+  auto put = [&](uint32_t byte) {
+    ow |= (byte & 255) << (8 * (pos & 3));
+    if ((++pos & 3) == 0) {
+      out[(pos >> 2) - 1] = ow;
+      ow = 0;
+    }
+  };
+  auto write_out = [&]() {  // CabacEncoder::write_out
     const uint32_t lead = low >> (24 - bl);
     bl += 8;
     low &= 0xffffffffu >> bl;
@@ -836,188 +901,127 @@ struct AcLane {
       nbuf++;
     } else if (nbuf > 0) {
       const uint32_t carry = lead >> 8;
-      emit(buffered + carry);
+      put(buffered + carry);
       buffered = lead & 0xff;
       const uint32_t byte = (0xff + carry) & 0xff;
-      while (nbuf > 1) {
-        emit(byte);
-        nbuf--;
-      }
+      for (; nbuf > 1; --nbuf) put(byte);
     } else {
       nbuf = 1;
       buffered = lead;
     }
-  }
-  // finish() + '1' + byte alignment (end_of_subset_one_bit / slice trailing bits)
-  __device__ void flush() {
-    if ((low >> (32 - bl)) != 0) {
-      emit(buffered + 1);
-      while (nbuf > 1) {
-        emit(0x00);
-        nbuf--;
-      }
-      low -= 1u << (32 - bl);
-    } else {
-      if (nbuf > 0) emit(buffered);
-      while (nbuf > 1) {
-        emit(0xff);
-        nbuf--;
-      }
-    }
-    const int nb = 24 - bl;  // 1..12 bits of low >> 8, then the '1', then zeros
-    uint32_t v = (((low >> 8) & ((1u << nb) - 1)) << 1) | 1u;
-    int t = nb + 1;
-    const int pad = (8 - (t & 7)) & 7;
-    v <<= pad;
-    t += pad;
-    while (t > 0) {
-      t -= 8;
-      emit((v >> t) & 0xff);
-    }
-  }
-};
-
-constexpr int kCtxN = CTX_COUNT;
-
-__global__ void __launch_bounds__(256) k_ent_ac(EntropyArgs a) {
-  extern __shared__ uint8_t lds[];
-  const int b = blockIdx.x, R = blockDim.x, row = threadIdx.x;
-  const int wc = a.g.wc, hc = a.g.hc, nctu = wc * hc;
-  uint8_t* ctx = lds;                          // [kCtxN][R]: state | mps << 6 (lane `row` only)
-  volatile uint8_t* syn = lds + kCtxN * R;     // [kCtxN][R]: contexts after CTB 1 of each row
-  uint8_t* lps = lds + 2 * kCtxN * R;          // [64][4]
-  uint8_t* tlps = lps + 256;                   // [64]
-  volatile uint8_t* sflag = tlps + 64;         // [R]: 1 = row's contexts stored in syn, 2 = aborted
-  __shared__ int s_status;
-  for (int k = threadIdx.x; k < 256; k += R) lps[k] = a.tab->lps[k];
-  for (int k = threadIdx.x; k < 64; k += R) tlps[k] = a.tab->tlps[k];
-  sflag[row] = 0;
-  if (threadIdx.x == 0) s_status = *a.status;  // one read for the whole workgroup
-  __syncthreads();
-  if (s_status) return;
-  const bool live = row < hc;
-  long tbase = 0;
-  for (int k = 0; k < b; ++k) tbase += a.seg_tok[k];
-  const int* off = a.ctb_off + (long)b * nctu;
-  long tpos = 0, tend = 0;
-  AcLane L;
-  if (live) {
-    tpos = tbase + off[row * wc];
-    tend = row + 1 < hc ? tbase + off[(row + 1) * wc] : tbase + a.seg_tok[b];
-    L.out = a.stage + 3 * tpos + 16 * ((long)b * hc + row);
-  }
-  int phase = live ? 0 : 2;  // 0 waiting for the row above, 1 coding, 2 done
-  uint32_t tok = 0;
-  int left = 0, nbins = 0;
-  const int qp = a.dec.qp[b];
-  // every token takes at most 3 iterations and a row waits at most as long as the rows above
-  // it code: a loop past this bound means a corrupt token stream -- abort, never hang
-  const long guard = 8L * (a.seg_tok[b] + 1) + 65536L * hc;
-  long iter = 0;
+  };
+  // a row longer than its token count is a corrupt token stream -- abort, never hang
+  bool synced = false;
   while (true) {
-    if (++iter > guard && phase != 2) {
-      if (live) atomicOr(a.status, 16);
-      sflag[row] = 2;
-      phase = 2;
+    if (ntok-- <= 0) {  // no FLUSH before the row's tokens ran out
+      abort_row(4);
+      return;
     }
-    if (phase == 0) {
-      if (row == 0) {
-        const uint8_t* init = a.tab->init[a.pic.init_type][clip3(0, 51, qp)];
-        for (int c = 0; c < kCtxN; ++c) ctx[c * R + row] = init[c];
-        phase = 1;
+    if (tail - head < kTokK) refill();
+    const uint32_t tok = __builtin_amdgcn_readfirstlane(tring32[head & (kTokT - 1)]);
+    ++head;
+    ++ntoks;
+    const uint32_t ty = tok >> 30;
+    if (ty == 0) {  // 1..3 context-coded bins (CabacEncoder::bin_step)
+      const int nbins = (tok >> 27) & 3;
+      nctxbins += nbins;
+      for (int k = 0; k < nbins; ++k) {
+        const uint32_t f = (tok >> (9 * k)) & 511;
+        const int c = (int)(f & 255);
+        const int sv = ctx[c];
+        const int st = sv & 63, mps = sv >> 6;
+        const uint32_t lp = lps[st * 4 + ((range >> 6) & 3)];
+        int nsv;
+        const uint32_t rmps = range - lp;
+        if ((int)(f >> 8) != mps) {  // LPS
+          const int nb = __clz(lp) - 23;
+          low = (low + rmps) << nb;
+          range = lp << nb;
+          bl -= nb;
+          nsv = tlps[st] | ((mps ^ (st == 0 ? 1 : 0)) << 6);
+        } else {
+          const int nb = __clz(rmps) - 23;  // 0 or 1
+          low <<= nb;
+          range = rmps << nb;
+          bl -= nb;
+          nsv = (st < 62 ? st + 1 : st) | (mps << 6);
+        }
+        ctx[c] = (uint8_t)nsv;
+        if (bl < 12) write_out();
+      }
+    } else if (ty == 1) {  // bypass bins, MSB first, <= 8 per step (encode_bypass_bins)
+      int n = (tok >> 16) & 31;
+      while (n > 0) {
+        const int m = n > 8 ? 8 : n;
+        n -= m;
+        low = (low << m) + range * ((tok >> n) & ((1u << m) - 1));
+        bl -= m;
+        if (bl < 12) write_out();
+      }
+    } else if (ty == 2) {  // terminating bin (encode_terminate)
+      range -= 2;
+      if (tok & 1) {
+        low += range;
+        low <<= 7;
+        range = 2 << 7;
+        bl -= 7;
+        if (bl < 12) write_out();
+      } else if (range < 256) {
+        low <<= 1;
+        range <<= 1;
+        bl--;
+        if (bl < 12) write_out();
+      }
+    } else if ((tok & 0xff) == kCtrlSync) {  // 9.3.2.4 storage for the row below
+      uint32_t* dst = wctx + (long)row * (kEntCtx / 4);
+#pragma unroll
+      for (int i = 0; i < kEntCtx / 4; ++i) dst[i] = ctx32[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&wflag[row], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      synced = true;
+    } else {  // finish() + '1' + byte alignment (end_of_subset_one_bit / slice trailing bits)
+      if ((low >> (32 - bl)) != 0) {
+        put(buffered + 1);
+        for (; nbuf > 1; --nbuf) put(0x00);
+        low -= 1u << (32 - bl);
       } else {
-        const int f = sflag[row - 1];
-        if (f == 1) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          for (int c = 0; c < kCtxN; ++c) ctx[c * R + row] = syn[c * R + row - 1];
-          phase = 1;
-        } else if (f == 2) {  // the row above aborted: so does this one
-          sflag[row] = 2;
-          phase = 2;
-        }
+        if (nbuf > 0) put(buffered);
+        for (; nbuf > 1; --nbuf) put(0xff);
       }
+      const int nb = 24 - bl;  // 1..12 bits of low >> 8, then the '1', then zeros
+      uint32_t v = (((low >> 8) & ((1u << nb) - 1)) << 1) | 1u;
+      int t = nb + 1;
+      const int pad = (8 - (t & 7)) & 7;
+      v <<= pad;
+      t += pad;
+      while (t > 0) {
+        t -= 8;
+        put((v >> t) & 0xff);
+      }
+      uint8_t* o8 = reinterpret_cast<uint8_t*>(out);
+      for (int k = pos & ~3; k < pos; ++k) o8[k] = (uint8_t)(ow >> (8 * (k & 3)));
+      a.row_bytes[(long)b * hc + row] = pos;
+      if (!synced) abort_row(4);  // a substream that never stored its contexts (corrupt stream)
+      if (a.dbg) {  // TV_ENT_DEBUG: rows, context bins, tokens, coding clocks, wait ticks, max row span
+        atomicAdd(&a.dbg[0], 1ull);
+        atomicAdd(&a.dbg[1], (unsigned long long)nctxbins);
+        atomicAdd(&a.dbg[2], (unsigned long long)ntoks);
+        atomicAdd(&a.dbg[3], clock64() - c1);
+        atomicAdd(&a.dbg[4], w1 - w0);
+        atomicMax(&a.dbg[5], wall_clock64() - w0);
+      }
+      break;
     }
-    if (phase == 1) {
-      if (left == 0) {
-        if (tpos >= tend) {  // malformed token stream (no FLUSH): stop the lane
-          atomicOr(a.status, 4);
-          sflag[row] = 2;
-          phase = 2;
-        } else {
-          tok = a.tokens[tpos++];
-          const uint32_t ty = tok >> 30;
-          nbins = ty == 0 ? (int)((tok >> 27) & 3) : ty == 1 ? (int)((tok >> 16) & 31) : 1;
-          left = nbins;
-        }
-      }
-      if (phase == 1) {
-        const uint32_t ty = tok >> 30;
-        if (ty == 0) {
-          const uint32_t f = (tok >> (9 * (nbins - left))) & 511;
-          --left;
-          const int c = (int)(f & 255), bin = (int)(f >> 8);
-          const int sv = ctx[c * R + row];
-          int st = sv & 63, mps = sv >> 6;
-          const uint32_t lp = lps[st * 4 + ((L.range >> 6) & 3)];
-          const uint32_t rmps = L.range - lp;
-          const bool is_lps = bin != mps;
-          const uint32_t r = is_lps ? lp : rmps;
-          const uint32_t l = is_lps ? L.low + rmps : L.low;
-          const int nb = __clz(r) - 23;
-          L.low = l << nb;
-          L.range = r << nb;
-          L.bl -= nb;
-          mps ^= (is_lps && st == 0) ? 1 : 0;
-          st = is_lps ? tlps[st] : (st < 62 ? st + 1 : st);
-          ctx[c * R + row] = (uint8_t)(st | (mps << 6));
-        } else if (ty == 1) {
-          const int n = left > 8 ? 8 : left;
-          left -= n;
-          const uint32_t val = (tok >> left) & ((1u << n) - 1);
-          L.low = (L.low << n) + L.range * val;
-          L.bl -= n;
-        } else if (ty == 2) {
-          left = 0;
-          L.range -= 2;
-          if (tok & 1) {
-            L.low += L.range;
-            L.low <<= 7;
-            L.range = 2 << 7;
-            L.bl -= 7;
-          } else if (L.range < 256) {
-            L.low <<= 1;
-            L.range <<= 1;
-            L.bl--;
-          }
-        } else {
-          left = 0;
-          if ((tok & 0xff) == kCtrlSync) {
-            for (int c = 0; c < kCtxN; ++c) syn[c * R + row] = ctx[c * R + row];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            sflag[row] = 1;
-          } else {
-            L.flush();
-            a.row_bytes[(long)b * hc + row] = L.pos;
-            if (sflag[row] == 0) {  // a substream that never stored its contexts (corrupt stream)
-              atomicOr(a.status, 4);
-              sflag[row] = 2;
-            }
-            phase = 2;
-          }
-        }
-        if (phase == 1 && L.bl < 12) L.write_out();
-      }
-    }
-    // a wave leaves when all its lanes are done (lanes of later waves wait on LDS flags); a
-    // wave whose lanes all wait on an earlier wave yields its issue slots
-    if (__ballot(phase != 2) == 0) break;
-    if (__ballot(phase == 1) == 0) __builtin_amdgcn_s_sleep(2);
   }
 }
 
-// compact the rows' bytes: slice b = its rows back to back, after slices 0..b-1
+// Slice b's rows back to back after slices 0..b-1, written straight into the pinned host slot
+// (device-visible): the head (sizes), the slice QP and the payload -- the host needs no copy.
 __global__ void __launch_bounds__(256) k_ent_pack(EntropyArgs a, int B) {
   const int b = blockIdx.x, hc = a.g.hc, wc = a.g.wc, nctu = wc * hc;
+  int* hseg = a.hhead + (a.seg_bytes - a.status);
+  int* hrow = a.hhead + (a.row_bytes - a.status);
   __shared__ long s_base;
   __shared__ int s_pre[256];
   __shared__ int s_bad;
@@ -1030,29 +1034,39 @@ __global__ void __launch_bounds__(256) k_ent_pack(EntropyArgs a, int B) {
       s_pre[r] = run;
       run += a.row_bytes[(long)b * hc + r];
     }
-    a.seg_bytes[b] = run;
+    hseg[b] = run;
+    a.hqp[b] = a.dec.qp[b];
     s_bad = *a.status;
-    if (base + run > a.out_cap) {
+    if (base + run > a.hout_cap) {
       atomicOr(a.status, 8);
       s_bad = 8;
     }
   }
   __syncthreads();
-  if (s_bad) return;
-  long tbase = 0;
-  for (int k = 0; k < b; ++k) tbase += a.seg_tok[k];
-  const int* off = a.ctb_off + (long)b * nctu;
-  for (int r = 0; r < hc; ++r) {
-    const uint8_t* src = a.stage + 3 * (tbase + off[r * wc]) + 16 * ((long)b * hc + r);
-    uint8_t* dst = a.out + s_base + s_pre[r];
-    const int n = a.row_bytes[(long)b * hc + r];
-    for (int k = threadIdx.x; k < n; k += 256) dst[k] = src[k];
+  if (!s_bad) {
+    for (int r = threadIdx.x; r < hc; r += 256) hrow[(long)b * hc + r] = a.row_bytes[(long)b * hc + r];
+    long tbase = 0;
+    for (int k = 0; k < b; ++k) tbase += a.seg_tok[k];
+    const int* off = a.ctb_off + (long)b * nctu;
+    for (int r = 0; r < hc; ++r) {
+      const uint8_t* src = a.stage + stage_off(tbase + off[r * wc], (long)b * hc + r);
+      uint8_t* dst = a.hout + s_base + s_pre[r];
+      const int n = a.row_bytes[(long)b * hc + r];
+      for (int k = threadIdx.x; k < n; k += 256) dst[k] = src[k];
+    }
   }
+  __threadfence_system();
+}
+
+// the picture's final status into the host slot (after every pack workgroup)
+__global__ void k_ent_status(EntropyArgs a) {
+  a.hhead[0] = *a.status;
+  __threadfence_system();
 }
 
 }  // namespace
 
-void launch_entropy(const EntropyArgs& a, int B, hipStream_t s) {
+void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s) {
   const int nctu = a.g.wc * a.g.hc;
   if (a.g.wc < 2) throw std::runtime_error("GPU entropy coding needs at least 2 CTB columns");
   if (a.g.hc > 256) throw std::runtime_error("GPU entropy coding supports at most 256 CTB rows");
@@ -1062,10 +1076,13 @@ void launch_entropy(const EntropyArgs& a, int B, hipStream_t s) {
   k_ent_scan<<<B, 1024, 0, s>>>(a);
   k_ent_check<<<1, 1, 0, s>>>(a, B);
   k_ent_bin<true><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
-  const int R = (a.g.hc + 63) / 64 * 64;
-  const size_t lds = 2 * (size_t)kCtxN * R + 256 + 64 + R;
-  k_ent_ac<<<B, R, lds, s>>>(a);
+}
+
+void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s) {
+  (void)hipMemsetAsync(a.wflag, 0, (size_t)B * a.g.hc * sizeof(int), s);
+  k_ent_ac<<<dim3(a.g.hc, B), 64, 0, s>>>(a);
   k_ent_pack<<<B, 256, 0, s>>>(a, B);
+  k_ent_status<<<1, 1, 0, s>>>(a);
 }
 
 void entropy_tables(EntropyTables& t) {

@@ -134,6 +134,14 @@ def stream_groups(device: torch.device):
     if key not in _GROUPS:
         ctrl = dist.new_group(backend="gloo")
         data = dist.new_group(backend=dist.get_backend()) if device.type == "cuda" else ctrl
+        if device.type == "cuda":
+            # every rank joins one collective on the new data group right away, so its RCCL
+            # communicator is created by all ranks together -- its first user is otherwise a
+            # batch_isend_irecv among the root and the peers that happen to have a payload
+            # (a first call on a subset of ranks is undefined for NCCL/RCCL)
+            t = torch.zeros(1, device=device)
+            dist.all_reduce(t, group=data)
+            torch.cuda.synchronize(device)
         _GROUPS[key] = (ctrl, data)
     return _GROUPS[key]
 
@@ -207,15 +215,25 @@ class SegmentStream:
                 hdr = torch.tensor([len(blob), int(done)], dtype=torch.int64)
                 hdrs = [torch.zeros(2, dtype=torch.int64) for _ in range(self.world)]
                 dist.all_gather(hdrs, hdr, group=self.ctrl)
+                if any(int(h[1]) == 2 for h in hdrs):  # a peer's thread failed: leave together
+                    raise RuntimeError("a peer's segment stream failed")
                 sizes = [int(h[0]) for h in hdrs]
                 t0 = time.perf_counter()
-                self._exchange(blob, sizes)
+                try:
+                    self._exchange(blob, sizes)
+                except BaseException as e:  # noqa: BLE001 - e.g. on_segment at the root
+                    self.err = e
+                    # one more header round carries the failure (2) to every rank, so no peer
+                    # blocks in the next all_gather until the process-group timeout
+                    dist.all_gather(hdrs, torch.tensor([0, 2], dtype=torch.int64), group=self.ctrl)
+                    return
                 self.stats["transfer_s"] += time.perf_counter() - t0
                 self.stats["rounds"] += 1
                 if all(int(h[1]) for h in hdrs):
                     return
         except BaseException as e:  # noqa: BLE001 - surfaced by close()
-            self.err = e
+            if self.err is None:
+                self.err = e
 
     def _exchange(self, blob: bytes, sizes: list) -> None:
         import json

@@ -982,11 +982,14 @@ def main(argv=None) -> int:
 
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         backend = a.backend or ("nccl" if torch.cuda.is_available() and not a.software else "gloo")
-        if backend == "nccl":
-            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
         import datetime
 
-        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=a.timeout_sec))
+        kw = {}
+        if backend == "nccl":  # eager communicator on this rank's GPU (not lazily on a first p2p)
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=a.timeout_sec), **kw)
     ladder = [int(x) for x in a.ladder.split(",") if x.strip()] or None
     res = run_job(a.input, a.output, a.height, a.qp, a.gop, a.segment_frames, a.mode, a.bitrate_kbps, ladder,
                   software=a.software, resume_dir=a.resume_dir, max_retries=a.max_retries, bframes=a.bframes,

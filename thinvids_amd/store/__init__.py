@@ -55,3 +55,16 @@ def set_store(store) -> None:
 
 # reference-compatible name
 get_redis = get_store
+
+
+_HMAX_LUA = ("local v = tonumber(redis.call('HGET', KEYS[1], ARGV[1]) or '0') or 0 "
+             "local n = tonumber(ARGV[2]) if n > v then redis.call('HSET', KEYS[1], ARGV[1], n) v = n end "
+             "return v")
+
+
+def hmax(st, key, field, value) -> int:
+    """Atomically raise hash field `field` of `key` to at least `value` (monotone progress
+    counters written by several ranks: a read-then-write could move them backwards)."""
+    if hasattr(st, "hmax"):
+        return int(st.hmax(key, field, int(value)))
+    return int(st.eval(_HMAX_LUA, 1, key, field, int(value)))  # redis-py

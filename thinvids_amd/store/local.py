@@ -240,6 +240,16 @@ class LocalStore:
             h[_s(field)] = str(v)
             return v
 
+    def hmax(self, key, field, value) -> int:
+        """Atomic max of an integer hash field (raise it to `value` unless it is already
+        higher); returns the field's value afterwards.  Redis has no HMAX: on redis-py the
+        store.hmax() helper runs the same as one Lua script."""
+        with self._lock:
+            h = self._new(_s(key), dict)
+            v = max(int(float(h.get(_s(field), "0") or 0)), int(value))
+            h[_s(field)] = str(v)
+            return v
+
     def hincrbyfloat(self, key, field, amount=1.0) -> float:
         with self._lock:
             h = self._new(_s(key), dict)

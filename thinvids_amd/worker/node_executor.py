@@ -40,7 +40,7 @@ import time
 import traceback
 
 from ..common import Status, emit_activity, get_logging
-from ..store import get_store
+from ..store import get_store, hmax
 from .helpers import (effective_target_height, elapsed_ms, ensure_dirs, final_output_path, is_job_halted,
                       job_base_dir, job_heartbeat, job_key, job_title, now, reset_job_run_state,
                       task_token_is_current)
@@ -108,8 +108,8 @@ class _StoreHooks:
         res = p.execute()
         done = int(res[1])
         prog = int(done * 100 / max(1, self.total))
-        if prog > int(st.hget(k, "encode_progress") or 0):
-            st.hset(k, mapping={"encode_progress": prog, "encode_elapsed": int(now() - self.t0)})
+        hmax(st, k, "encode_progress", prog)  # atomic max: ranks never move it backwards
+        hmax(st, k, "encode_elapsed", int(now() - self.t0))
         job_heartbeat(self.job_id, "encode", note=f"{done}/{self.total} segments")
 
     def halted(self) -> bool:
