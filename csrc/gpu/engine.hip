@@ -202,9 +202,28 @@ class Core {
     slot_bytes(B, g_, gpu_ent_, slot_bytes_, slot_host_bytes_);
     if (gpu_ent_) {  // per-core entropy scratch (the entropy stream codes one picture at a time)
       tok_cap_ = tok_capacity(B, g_);
+      {  // one allocation carved like ent_core_bytes()
+        uint8_t* q = nullptr;
+        dev_alloc(&q, ent_core_bytes(B, g_));
+        ent_.base = q;
+        ent_.regions = reinterpret_cast<uint32_t*>(q);
+        q += align(B * nctu_ * kEntRegion * 4);
+        ent_.tokens = reinterpret_cast<uint32_t*>(q);
+        q += align((tok_cap_ + kTokPad) * 4);
+        ent_.stage = q;
+        q += align(3 * tok_cap_ + 20 * B * g_.hc + 16);
+        ent_.ctb_cnt = reinterpret_cast<int*>(q);
+        q += align(B * nctu_ * 4);
+        ent_.ctb_off = reinterpret_cast<int*>(q);
+        q += align(B * nctu_ * 4);
+        ent_.seg_tok = reinterpret_cast<int*>(q);
+        q += align(B * 4);
+        ent_.wflag = reinterpret_cast<int*>(q);
+        q += align(B * g_.hc * 4);
+        ent_.wctx = q;
+      }
       dev_alloc(&ent_.skip, B * g_.usz);
       dev_alloc(&ent_.midx, B * g_.usz);
-      dev_alloc(&ent_.ctb_cnt, B * nctu_ * sizeof(int));
       EntropyTables* t = nullptr;
       dev_alloc(&t, sizeof(EntropyTables));
       std::unique_ptr<EntropyTables> ht(new EntropyTables());
@@ -293,7 +312,7 @@ class Core {
     const bool ge = gpu_entropy(c);
     long slot = 0, slot_host = 0;
     slot_bytes((long)B, g, ge, slot, slot_host);
-    const size_t ent = ge ? 2 * B * g.usz + B * nctu * sizeof(int) + sizeof(EntropyTables) : 0;
+    const size_t ent = ge ? 2 * B * g.usz + ent_core_bytes((long)B, g) + sizeof(EntropyTables) : 0;
     dev = set + ndpb * (set + B * 16 * g.psz + B * qsz) + ((c.deblock & 2) ? set : 0) + 2 * set +
           B * 3 * sizeof(unsigned long long) + B * nctu * sizeof(int) + 2 * B * nctu * 2 * sizeof(int16_t) +
           2 * B * nctu * sizeof(int) + (c.mgop > 1 ? 2 * B * nctu * sizeof(CtbMeOut) : 0) +
@@ -328,7 +347,7 @@ class Core {
     (void)hipFree(cmv_);
     (void)hipFree(ccost_);
     (void)hipFree(rc_);
-    for (void* p : {(void*)ent_.skip, (void*)ent_.midx, (void*)ent_.ctb_cnt, (void*)ent_.tab})
+    for (void* p : {(void*)ent_.skip, (void*)ent_.midx, (void*)ent_.base, (void*)ent_.tab})
       (void)hipFree(p);
     (void)hipHostFree(qhost_);
     (void)hipHostFree(quni_);
@@ -383,6 +402,7 @@ class Core {
     return (long)(per * B * g.ysz) + 1024;
   }
   static constexpr long kTokPad = 64;
+  static constexpr long kEntRegion = kEntRegionTokens;
   // head of the entropy outputs: status, seg_bytes[B], row_bytes[B][hc]
   static long ent_head_bytes(long B, const Geo& g) { return 16 + 4 * B + 4 * B * g.hc; }
   static void slot_bytes(long B, const Geo& g, bool ge, long& dev, long& host) {
@@ -390,15 +410,16 @@ class Core {
     host = align(B * g.usz) + align(B * g.usz * 4) + align(B * nctu * 8) + align(B * nctu * 4) + align(B * nctu * 4) +
            align(B * 4) + align(B * nctu * 12) + align(B) + align(B * g.usz) + align(B * g.usz * 4) +
            align(B * g.usz * 5) + align(B * cap * 2) + (ge ? align(ent_head_bytes(B, g)) : 0);
-    // device side only: the picture's token lists, CTB token offsets, segment token counts, the
-    // coder's output staging and the rows' WPP hand-off (the payload itself goes straight into
-    // the host slot's `packed` region)
-    dev = host + (ge ? ent_slot_bytes(B, g) : 0);
+    // (the GPU entropy payload goes straight into the host slot's `packed` region)
+    dev = host;
   }
-  static long ent_slot_bytes(long B, const Geo& g) {
+  // per-core entropy scratch (the entropy stream codes one picture at a time): CTB token
+  // regions of the single binarisation pass, the picture's contiguous token lists, CTB offsets,
+  // segment totals, coder output staging and the rows' WPP hand-off
+  static long ent_core_bytes(long B, const Geo& g) {
     const long cap = tok_capacity(B, g), nctu = (long)g.wc * g.hc;
-    return align((cap + kTokPad) * 4) + align(3 * cap + 20 * B * g.hc + 16) + align(B * nctu * 4) + align(B * 4) +
-           align(B * g.hc * 4) + align(B * g.hc * kEntCtx);
+    return align(B * nctu * kEntRegion * 4) + align((cap + kTokPad) * 4) + align(3 * cap + 20 * B * g.hc + 16) +
+           2 * align(B * nctu * 4) + align(B * 4) + align(B * g.hc * 4) + align(B * g.hc * kEntCtx);
   }
   // qcost, gate list, pass lists, candidate list (16 bytes per CTB each), counters, candidate bytes
   static size_t pintra_bytes(long B, long nctu) { return 4 * align(B * nctu * 16) + 256 + align(B * nctu * 4); }
@@ -420,11 +441,6 @@ class Core {
     uint32_t* sao;
     int8_t* qp;
     int* ent_head;     // GPU entropy: status, seg_bytes[B], row_bytes[B][hc]
-    uint32_t* tokens;  // GPU entropy, device slot only: token lists of the picture
-    uint8_t* stage;    //   arithmetic coder output staging
-    int *ctb_off, *seg_tok;
-    int* wflag;        //   WPP hand-off flags and contexts between the rows' coder waves
-    uint8_t* wctx;
   };
   Parts carve(uint8_t* base) const {
     const long B = cfg_.batch, U = g_.usz;
@@ -464,18 +480,6 @@ class Core {
     q += align(B * cap_ * 2);
     p.ent_head = reinterpret_cast<int*>(q);
     q += gpu_ent_ ? align(ent_head_bytes(B, g_)) : 0;
-    const long tc = gpu_ent_ ? tok_capacity(B, g_) : 0;
-    p.tokens = reinterpret_cast<uint32_t*>(q);
-    q += gpu_ent_ ? align((tc + kTokPad) * 4) : 0;
-    p.stage = q;
-    q += gpu_ent_ ? align(3 * tc + 20 * B * g_.hc + 16) : 0;
-    p.ctb_off = reinterpret_cast<int*>(q);
-    q += gpu_ent_ ? align(B * nctu_ * 4) : 0;
-    p.seg_tok = reinterpret_cast<int*>(q);
-    q += gpu_ent_ ? align(B * 4) : 0;
-    p.wflag = reinterpret_cast<int*>(q);
-    q += gpu_ent_ ? align(B * g_.hc * 4) : 0;
-    p.wctx = q;
     p.count = nullptr;  // device count array lives in the scratch below
     return p;
   }
@@ -651,13 +655,14 @@ class Core {
     a.skip = ent_.skip;
     a.midx = ent_.midx;
     a.ctb_cnt = ent_.ctb_cnt;
-    a.ctb_off = d.ctb_off;
-    a.seg_tok = d.seg_tok;
-    a.tokens = d.tokens;
+    a.regions = ent_.regions;
+    a.ctb_off = ent_.ctb_off;
+    a.seg_tok = ent_.seg_tok;
+    a.tokens = ent_.tokens;
     a.tok_cap = tok_cap_;
-    a.stage = d.stage;
-    a.wflag = d.wflag;
-    a.wctx = d.wctx;
+    a.stage = ent_.stage;
+    a.wflag = ent_.wflag;
+    a.wctx = ent_.wctx;
     a.tab = ent_.tab;
     a.status = d.ent_head;
     a.seg_bytes = d.ent_head + 4;
@@ -950,7 +955,11 @@ class Core {
   struct EntScratch {
     uint8_t* skip = nullptr;
     int8_t* midx = nullptr;
-    int* ctb_cnt = nullptr;
+    uint8_t* base = nullptr;  // the ent_core_bytes() allocation
+    uint32_t *regions = nullptr, *tokens = nullptr;
+    uint8_t* stage = nullptr;
+    int *ctb_cnt = nullptr, *ctb_off = nullptr, *seg_tok = nullptr, *wflag = nullptr;
+    uint8_t* wctx = nullptr;
     EntropyTables* tab = nullptr;
   } ent_;
   long tok_cap_ = 0, slot_host_bytes_ = 0;

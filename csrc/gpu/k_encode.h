@@ -107,6 +107,9 @@ void launch_pack_flags(DecisionSet dec, uint8_t* flags, const Geo& g, int B, hip
 
 // ---- GPU CABAC (k_entropy.hip): WPP substreams of every slice of one picture -------------
 constexpr int kEntCtx = 160;  // >= tv::CTX_COUNT (static_assert in k_entropy.hip)
+// tokens per CTB region of the single binarisation pass (a CTB that needs more is binarised
+// again straight into the picture's token list)
+constexpr int kEntRegionTokens = 2048;
 struct EntropyPic {
   int type;        // 2 I, 1 P, 0 B
   int init_type;   // cabac initType: 0 I, 1 P, 2 B
@@ -130,7 +133,7 @@ struct EntropyArgs {
   uint8_t* skip;        // [B][usz] cu_skip_flag of the unit's CU
   int8_t* midx;         // [B][usz] merge candidate matching the CU's motion (-1: none)
   int* ctb_cnt;         // [B][nctu] tokens of each CTB
-  // per slot (the coders of several pictures run concurrently)
+  uint32_t* regions;    // [B][nctu][kEntRegionTokens] the CTBs' tokens as first written
   int* ctb_off;         // [B][nctu] exclusive scan of ctb_cnt within the segment
   int* seg_tok;         // [B] tokens of each segment
   uint32_t* tokens;     // token lists, segments back to back

@@ -40,11 +40,12 @@ static_assert(CTX_COUNT <= kEntCtx && kEntCtx <= 256, "context index must fit 8 
 
 struct TokSink {
   uint32_t* out;  // nullptr: count only
+  int cap;        // tokens past `cap` are counted, not written
   int n = 0;
   uint32_t pc = 0, pb = 0;  // pending context bins / bypass bins
   int npc = 0, npb = 0;
   __device__ __forceinline__ void put(uint32_t t) {
-    if (out) out[n] = t;
+    if (out && n < cap) out[n] = t;
     ++n;
   }
   __device__ __forceinline__ void flush_c() {
@@ -730,35 +731,62 @@ __global__ void __launch_bounds__(256) k_ent_cu(EntropyArgs a) {
 }
 
 // One thread per CTB: count (WRITE = false) or write its tokens.
-template <bool WRITE>
+// One thread per CTB.  REGION (the single full pass): the CTB's tokens into its fixed region
+// (kEntRegionTokens) and its exact count.  !REGION (after the scan): only CTBs whose tokens
+// did not fit binarise again, straight into the picture's token list; the others were moved by
+// k_ent_place.  (A count pass + write pass binarised every CTB twice.)
+template <bool REGION>
 __global__ void __launch_bounds__(64) k_ent_bin(EntropyArgs a) {
-  __builtin_amdgcn_s_setprio(2);  // latency-bound per-lane chains beside the analysis kernels
   __shared__ BinTables T;
+  const int b = blockIdx.y, nctu = a.g.wc * a.g.hc;
+  const int ctu = blockIdx.x * 64 + threadIdx.x;
+  const long i = (long)b * nctu + ctu;
+  bool work = ctu < nctu;
+  if (!REGION) {  // the whole workgroup leaves unless one of its CTBs overflowed
+    work = work && !*a.status && a.ctb_cnt[i] > kEntRegionTokens;
+    if (__syncthreads_or(work) == 0) return;
+  }
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&c_tab);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
     for (int k = threadIdx.x; k < (int)(sizeof(BinTables) / 4); k += 64) dst[k] = src[k];
   }
   __syncthreads();
-  const int b = blockIdx.y, nctu = a.g.wc * a.g.hc;
-  const int ctu = blockIdx.x * 64 + threadIdx.x;
-  if (ctu >= nctu) return;
-  const long i = (long)b * nctu + ctu;
-  uint32_t* out = nullptr;
-  if (WRITE) {
-    if (*a.status) return;  // token capacity exceeded: the host codes this slot
+  if (!work) return;
+  uint32_t* out;
+  int cap;
+  if (REGION) {
+    out = a.regions + i * kEntRegionTokens;
+    cap = kEntRegionTokens;
+  } else {
     long base = 0;
     for (int k = 0; k < b; ++k) base += a.seg_tok[k];
     out = a.tokens + base + a.ctb_off[i];
+    cap = 1 << 30;
   }
   const SegView v = seg_view(a, b);
-  TokSink s{out};
+  TokSink s{out, cap};
   CtbBinariser z{v, a.pic, s, T};
   z.ctb(ctu % v.wc, ctu / v.wc, a.pic.sao != 0);
   s.flush_c();
   s.flush_b();
   if (z.err) atomicOr(a.status, 2);
-  if (!WRITE) a.ctb_cnt[i] = s.n;
+  if (REGION) a.ctb_cnt[i] = s.n;
+}
+
+// the CTBs whose tokens fit their region: region -> the picture's token list (one wave per CTB)
+__global__ void __launch_bounds__(256) k_ent_place(EntropyArgs a) {
+  const int b = blockIdx.y, nctu = a.g.wc * a.g.hc;
+  const int ctu = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (ctu >= nctu || *a.status) return;
+  const long i = (long)b * nctu + ctu;
+  const int n = a.ctb_cnt[i];
+  if (n > kEntRegionTokens) return;  // binarised again by k_ent_bin<false>
+  long base = 0;
+  for (int k = 0; k < b; ++k) base += a.seg_tok[k];
+  uint32_t* dst = a.tokens + base + a.ctb_off[i];
+  const uint32_t* src = a.regions + i * kEntRegionTokens;
+  for (int k = lane; k < n; k += 64) dst[k] = src[k];
 }
 
 // exclusive scan of the CTB token counts, one workgroup per segment; capacity check
@@ -1072,10 +1100,11 @@ void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s) {
   if (a.g.hc > 256) throw std::runtime_error("GPU entropy coding supports at most 256 CTB rows");
   (void)hipMemsetAsync(a.status, 0, sizeof(int), s);
   if (a.pic.type != 2) k_ent_cu<<<dim3((unsigned)((a.g.usz + 255) / 256), B), 256, 0, s>>>(a);
-  k_ent_bin<false><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
+  k_ent_bin<true><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
   k_ent_scan<<<B, 1024, 0, s>>>(a);
   k_ent_check<<<1, 1, 0, s>>>(a, B);
-  k_ent_bin<true><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
+  k_ent_place<<<dim3((nctu + 3) / 4, B), 256, 0, s>>>(a);
+  k_ent_bin<false><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
 }
 
 void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s) {

@@ -367,7 +367,7 @@ def test_node_job_segment_resume(tmp_path, source):
     res5, _ = _spawn_job(tmp_path, source, {"resume_dir": ck, "tools": {"rqt": False}}, {})
     assert sum(p["resumed"] for p in res5[0]["per_rank"]) == 0
     assert sum(p["encoded"] for p in res5[0]["per_rank"]) == 3
-    assert len(os.listdir(ck)) == 2
+    assert len(os.listdir(ck)) == 3  # base job, gop 4, no RQT
 
 
 def test_node_job_elastic_restart_torchrun(tmp_path, source):

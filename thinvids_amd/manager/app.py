@@ -805,11 +805,9 @@ def create_app(store=None, housekeeping: bool = False) -> Flask:
         clear = {f: "" for f in ("error", "failed_stage", "failed_worker", "rejected_reason", "rejected_at",
                                  "stalled_stage", "stalled_detected_at", "output_path", "queue_blocked_reason",
                                  "pipeline_run_token", "last_part_error")}
-        zero = {f: 0 for f in ("parts_total", "parts_done", "segmented_chunks", "completed_chunks",
-                               "stitched_chunks", "segment_progress", "encode_progress", "combine_progress",
-                               "segment_elapsed", "encode_elapsed", "combine_elapsed", "failed_part", "ended_at",
-                               "last_heartbeat_at", "queue_dispatch_attempts", "node_restarts",
-                               "encoded_frames")}
+        from ..worker.helpers import RUN_COUNTER_FIELDS
+
+        zero = {f: 0 for f in (*RUN_COUNTER_FIELDS, "queue_dispatch_attempts", "node_restarts")}
         mapping = {**clear, **zero, **details, "scratch_mode": smode, "scratch_root": sroot,
                    "processing_mode": pmode, "processing_mode_effective": "", "processing_mode_reason": "",
                    "target_height": normalize_target_height(job.get("target_height", default_target_height()))}

@@ -77,6 +77,9 @@ def flat_layout(w: int, h: int) -> list:
     return [(0, w, h, w, fsz), (ysz, w // 2, h // 2, w // 2, fsz), (ysz + csz, w // 2, h // 2, w // 2, fsz)]
 
 
+_STATS_LOCK = threading.Lock()
+
+
 class _Pinned:
     """Grow-only pinned host buffer per thread (H2D uploads without pageable staging)."""
 
@@ -253,11 +256,12 @@ def read_y4m_device(src, start: int, n: int, device, threads: int | None = None,
     fs = info.frame_bytes // esz
     ysz, csz = w * h, (w // 2) * (h // 2)
     planes = [(hdr, w, h, w, fs), (hdr + ysz, w // 2, h // 2, w // 2, fs), (hdr + ysz + csz, w // 2, h // 2, w // 2, fs)]
-    if stats is not None:
-        stats["read_bytes"] = stats.get("read_bytes", 0) + nbytes
-        stats["ingest_s"] = stats.get("ingest_s", 0.0) + tm[1]
-        stats["read_thread_s"] = stats.get("read_thread_s", 0.0) + tm[0]
-        stats["read_threads"] = threads
+    if stats is not None:  # the node job's prefetch thread and its main thread share `stats`
+        with _STATS_LOCK:
+            stats["read_bytes"] = stats.get("read_bytes", 0) + nbytes
+            stats["ingest_s"] = stats.get("ingest_s", 0.0) + tm[1]
+            stats["read_thread_s"] = stats.get("read_thread_s", 0.0) + tm[0]
+            stats["read_threads"] = threads
     return DevFrames(buf, n, w, h, planes, 8 if esz == 1 else 10)
 
 

@@ -92,6 +92,10 @@ class _Counter:
             return self.local - 1
         return int(self.store.add(self.key, 1)) - 1
 
+    def peek(self) -> int:
+        """Items handed out so far (no claim)."""
+        return self.local if self.store is None else int(self.store.add(self.key, 0))
+
 
 def _ns(key: str) -> str:
     """Store keys are namespaced by the elastic restart count, so a torchrun restart of the
@@ -156,6 +160,11 @@ class WorkQueue:
                 break
             out.append(self.items[k])
         return out
+
+    def unclaimed(self) -> int:
+        """Fresh items nobody has claimed yet (a snapshot: other ranks keep claiming)."""
+        taken = self.ctr.peek() if self.ctr is not None else self._local_next
+        return max(0, len(self.items) - taken)
 
     def fresh_done(self) -> None:
         self._add("done")
@@ -543,7 +552,11 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         range read in parallel into pinned memory and copied to this GPU once for all rungs
         (stage.read_y4m_device), or decoded host frames uploaded once."""
         if i in prefetched:
-            return prefetched.pop(i)
+            fr = prefetched.pop(i)
+            buf = getattr(fr, "buf", None)
+            if buf is not None and buf.is_cuda:  # allocated on the prefetch stream, used on this one
+                buf.record_stream(torch.cuda.current_stream(buf.device))
+            return fr
         s, n = segs[i]
         stats["reads"] += 1
         if synthetic:
@@ -559,7 +572,11 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     # file sources on the GPU: the next claim is read + uploaded on a side thread / HIP
     # stream while this claim encodes (the reference overlaps GET part with the previous
     # encode only across nodes; here ingest hides behind the engine on every rank)
-    prefetch = not synthetic and not software and dev.type == "cuda" and os.environ.get("TV_PREFETCH", "1") != "0"
+    # Only Y4M sources: their reads are pread threads + DMA, so the side thread costs the
+    # engine nothing; a decoded source (HEVC / AV1 / MPEG-2) would run a whole CPU decode there
+    # (ADVICE r4), unmeasured -- those load on demand.
+    prefetch = (not synthetic and not software and dev.type == "cuda" and isinstance(src, media.Y4MSource)
+                and os.environ.get("TV_PREFETCH", "1") != "0")
     prefetcher = None
     if prefetch:
         def _prefetch_init():
@@ -752,7 +769,10 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                             claimed = wq.claim(batch_segments)  # a batch -> one batched launch per rung
                     if not claimed:
                         break
-                    if prefetcher is not None and len(claimed) == batch_segments:
+                    # claim ahead only while enough work remains for every rank: at the tail of a
+                    # job a prefetched batch would sit idle on this rank while others starve
+                    if (prefetcher is not None and len(claimed) == batch_segments
+                            and wq.unclaimed() >= world * batch_segments):
                         with trace.span("node_job.claim"):
                             nxt = wq.claim(batch_segments)
                         if nxt:

@@ -144,6 +144,14 @@ def part_paths(job_id: str, idx: int, job: dict | None = None, store=None) -> tu
             os.path.join(base, "encoded", f"enc_{idx:03d}.mp4"))
 
 
+# Per-run counters of a job: zeroed by every restart / requeue path (worker reset and the
+# manager's restart route share this list, so a requeued 2-pass job never reads a stale pass)
+RUN_COUNTER_FIELDS = ("parts_total", "parts_done", "segmented_chunks", "completed_chunks", "stitched_chunks",
+                      "segment_progress", "segment_elapsed", "encode_progress", "encode_elapsed", "combine_progress",
+                      "combine_elapsed", "failed_part", "last_heartbeat_at", "ended_at", "rc_pass", "encoded_frames",
+                      *(f"{f}_p{k}" for f in ("parts_done", "completed_chunks", "encoded_frames") for k in (1, 2)))
+
+
 def reset_job_run_state(job_id: str, job: dict | None = None, store=None) -> None:
     """Clear per-run files and counters so restarts never reuse old parts (:318-378)."""
     st = store or get_store()
@@ -156,12 +164,7 @@ def reset_job_run_state(job_id: str, job: dict | None = None, store=None) -> Non
             os.remove(os.path.join(base, name))
         except FileNotFoundError:
             pass
-    zero = {k: 0 for k in ("parts_total", "parts_done", "segmented_chunks", "completed_chunks",
-                           "stitched_chunks", "segment_progress", "segment_elapsed", "encode_progress",
-                           "encode_elapsed", "combine_progress", "combine_elapsed", "failed_part",
-                           "last_heartbeat_at", "ended_at", "rc_pass", "encoded_frames",
-                           *(f"{f}_p{k}" for f in ("parts_done", "completed_chunks", "encoded_frames")
-                             for k in (1, 2)))}
+    zero = {k: 0 for k in RUN_COUNTER_FIELDS}
     blank = {k: "" for k in ("error", "failed_stage", "failed_worker", "processing_mode_effective",
                              "processing_mode_reason", "direct_segment_duration", "last_heartbeat_stage",
                              "last_heartbeat_host", "last_heartbeat_note")}
