@@ -294,9 +294,25 @@ def job_main(args) -> None:
     w, h = RES[args.res]
     tmp = tempfile.mkdtemp(prefix="tvjob_", dir=os.environ.get("TV_BENCH_SCRATCH") or None)
     y4m = args.source == "y4m"
+    dvd = args.source == "mpeg2"
     seg_frames = args.gop * 16
     frames = args.job_frames or (args.gop * 16 * 3 * 4 * args.gpus if y4m else args.gop * 16 * 2 * 48 * args.gpus)
     warm_frames = args.gop * 16 * (3 if y4m else 1) * args.gpus
+    if dvd:  # DVD-native: 720x480 kept (never upscaled), bwdif, segments of 2 GOPs
+        w, h = 720, 480
+        seg_frames = args.gop * 2
+        frames = args.job_frames or 3000 * args.gpus
+        warm_frames = 300 * args.gpus
+        os.makedirs(f"{tmp}/watch/dvd", exist_ok=True)
+        t0 = time.perf_counter()
+        code = ("import sys, json; sys.path.insert(0, %r); from thinvids_amd.models.mpeg2 import write_dvd_title; "
+                "write_dvd_title(%r, %d, seed=%d); print(json.dumps(write_dvd_title(%r, %d, seed=%d)))"
+                % (ROOT, f"{tmp}/watch/dvd/warmup.mkv", warm_frames, args.seed + 7,
+                   f"{tmp}/watch/dvd/timed.mkv", frames, args.seed))
+        dvd_info = json.loads(subprocess.run([sys.executable, "-c", code], check=True, capture_output=True,
+                                             text=True).stdout.strip().splitlines()[-1])
+        frames = dvd_info["frames"]
+        gen_s = time.perf_counter() - t0
     if y4m:  # source files first, in a child process (this parent never touches the GPU)
         os.makedirs(f"{tmp}/watch", exist_ok=True)
         t0 = time.perf_counter()
@@ -321,7 +337,8 @@ def job_main(args) -> None:
     save_settings({"tv_codec": args.codec, "tv_gop": str(args.gop), "tv_qp": str(args.qp), "tv_sao": "1" if args.sao else "0",
                    "tv_search_range": str(args.range), "tv_node_segment_frames": str(seg_frames),
                    "tv_node_mode": args.job_mode,
-                   "tv_node_batch": str(max(1, (args.batch or (48 if w * h <= 1920 * 1088 else 24)) // 16))}, store)
+                   "tv_node_batch": str(16 if dvd else max(1, (args.batch or (48 if w * h <= 1920 * 1088 else 24)) // 16))},
+                  store)
     import threading
 
     res = {}
@@ -335,7 +352,9 @@ def job_main(args) -> None:
         time.sleep(0.1)
 
     def run(name, n):
-        if y4m:
+        if dvd:
+            spec, fname = f"{tmp}/watch/dvd/{name}.mkv", f"dvd/{name}.mkv"
+        elif y4m:
             spec, fname = f"{tmp}/watch/{name}.y4m", f"{name}.y4m"
         else:
             spec, fname = f"{tmp}/watch/{name}.synth", f"{name}.synth"
@@ -359,6 +378,12 @@ def job_main(args) -> None:
     ingest = json.loads(job.get("ingest_json") or "[]")
     gb = lambda b, s: round(b / 1e9 / s, 2) if s else None  # noqa: E731
     cfg_src = {}
+    if dvd:
+        cfg_src = {"source_file": f"DVD title: MPEG-2 MP@ML 720x480 interlaced (tff) in Matroska V_MPEG2, {frames} frames, "
+                                  f"{dvd_info['kbps']} kbps ({dvd_info['unique']} unique frames repeated; written before the "
+                                  "timed region); decoded on host threads, bwdif (k_bwdif) + HEVC on the GPU",
+                   "source_gen_s": round(gen_s, 2), "job_mode": args.job_mode,
+                   "decode_threads_per_rank": os.environ.get("TV_DECODE_THREADS") or "auto (min(8, cpus))"}
     if y4m:
         fb = w * h * 3 // 2
         cfg_src = {"source_file": f"y4m {w}x{h} 8-bit 4:2:0, {frames} frames, {round(frames * (fb + 6) / 1e9, 2)} GB "
@@ -378,9 +403,11 @@ def job_main(args) -> None:
         "vs_baseline": None, "dtype": "uint8 video / int32 integer transforms (bit-exact "
         + ("AV1 subset)" if args.codec == "av1" else "HEVC)"),
         "data": ("synthetic frames in a raw y4m FILE read by the job (native pread threads -> pinned ring -> overlapped H2D DMA)" if y4m
+                 else "synthetic interlaced frames in an MPEG-2 DVD title read and decoded by the job" if dvd
                  else "synthetic (seeded procedural YUV 4:2:0 .synth source generated on each GPU)"),
         "config": {"model": (f"AV1 subset (tv) q-index for QP{args.qp} {args.res} synthetic" if args.codec == "av1" else
-                             f"HEVC Main CQP{args.qp} CTB32 {args.res} synthetic" + (" +SAO" if args.sao else "")),
+                             f"HEVC Main CQP{args.qp} CTB32 {'480p DVD' if dvd else args.res} synthetic"
+                             + (" +SAO" if args.sao else "")),
                    "codec": job.get("dest_codec"), "source": args.source, **cfg_src,
                    "job_frames": frames, "resolution": f"{w}x{h}", "parallelism": f"dp{args.gpus} node executor",
                    "job_wall_s": round(el, 3), "job_fps_reported": float(job.get("job_fps") or 0),
@@ -609,8 +636,9 @@ def main() -> None:
     ap.add_argument("--src", default=None, choices=sorted(SRC), help="ABR mode: HDR10 source resolution (default 8k; tiny with --cpu)")
     ap.add_argument("--job", action="store_true", help="end-to-end job mode (node executor, add -> DONE)")
     ap.add_argument("--job-frames", type=int, default=0)
-    ap.add_argument("--source", choices=("synth", "y4m"), default="synth",
-                    help="job mode: synthetic .synth source (generated on each GPU) or a raw y4m file read by the job")
+    ap.add_argument("--source", choices=("synth", "y4m", "mpeg2"), default="synth",
+                    help="job mode: synthetic .synth source (generated on each GPU), a raw y4m file read by the job, "
+                         "or a DVD title (720x480 interlaced MPEG-2 in Matroska: decode + bwdif + HEVC)")
     ap.add_argument("--job-mode", choices=("direct", "scatter"), default="direct",
                     help="job mode: every rank reads its own range (direct) or rotating-root xGMI scatter")
     ap.add_argument("--codec", default="hevc", choices=["hevc", "av1"], help="av1: BASELINE config #4 engine")

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -137,7 +138,13 @@ class Core {
     if (c.width < 64 || c.height < 64) throw std::runtime_error("frame must be at least 64x64");
     HIP_OK(hipSetDevice(c.device));
     fetch_ = std::make_unique<ThreadPool>(1, c.device);
-    HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (const char* e = std::getenv("TV_MAIN_PRIO"); e && *e == '1') {  // experiment
+      int lo = 0, hi = 0;
+      HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+    } else {
+      HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    }
     {  // I-frame wavefront stream: highest priority, so its 100+ short dependent launches are
        // dispatched ahead of the other stream group's queued P-frame workgroups
       int lo = 0, hi = 0;
@@ -294,7 +301,19 @@ class Core {
   // entropy stream waits behind the latency-bound coder (measured: main-stream queues 36 %
   // busy).  Main streams first, then the entropy streams, gives each its own queue at 2 cores.
   void init_entropy_stream() {
-    if (gpu_ent_ && !estream_) HIP_OK(hipStreamCreateWithFlags(&estream_, hipStreamNonBlocking));
+    if (gpu_ent_ && !estream_) {
+      const char* e = getenv("TV_ENT_CUS");  // experiment: entropy stream on every k-th CU
+      const int k = e ? atoi(e) : 0;
+      if (k > 1) {
+        hipDeviceProp_t prop;
+        HIP_OK(hipGetDeviceProperties(&prop, cfg_.device));
+        std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
+        for (int cu = 0; cu < prop.multiProcessorCount; cu += k) mask[cu / 32] |= 1u << (cu % 32);
+        HIP_OK(hipExtStreamCreateWithCUMask(&estream_, (uint32_t)mask.size(), mask.data()));
+      } else {
+        HIP_OK(hipStreamCreateWithFlags(&estream_, hipStreamNonBlocking));
+      }
+    }
   }
 
   // device / pinned-host bytes this group allocated (the engine's HBM footprint)

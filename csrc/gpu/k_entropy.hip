@@ -16,6 +16,7 @@
 // oracle: tests/test_gpu_entropy.py).  The per-CU skip / merge choice is made in a pre-pass
 // (k_ent_cu) so a CTB's cu_skip_flag context can read its left / upper neighbours'.
 // Reference: the reference entropy-codes in VA-API fixed function (worker/tasks.py:1573-1586).
+#include <cstdlib>
 #include <stdexcept>
 
 #include "gpu_common.h"
@@ -839,8 +840,9 @@ constexpr int kTokK = 32;   // tokens per refill
 // layout executed the union of every row's path each iteration with two thirds of the rows
 // still waiting on WPP (~1500 clocks per bin); this runs ~700 (TV_ENT_DEBUG).  (Context states
 // in VGPRs via wave-uniform indexed moves measured slower: ~970.)  The WPP storage (9.3.2.4) goes to the row below through
-// global memory: plain stores, agent release fence, flag; the reader polls the flag
-// (agent-scope atomic load = sc1, no stale L1), then acquires.  Workgroups are dispatched in
+// global memory: agent-scope relaxed stores (sc1), vmcnt(0), flag; the reader polls the flag and
+// reads the contexts with agent-scope loads -- no fences (an agent fence is a whole-L2 write-back
+// or invalidate on this XCD).  Workgroups are dispatched in
 // row order, so a row only ever waits on a row that is already running.  Tokens come through a
 // 64-entry LDS ring refilled 32 at a time (a token load kept in registers across the loop's
 // branches forces a vmcnt(0) wait at its use); output bytes leave as dword stores.
@@ -850,7 +852,7 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
   tlps[threadIdx.x] = a.tab->tlps[threadIdx.x];
   __syncthreads();
   if (threadIdx.x != 0) return;
-  __builtin_amdgcn_s_setprio(3);  // a latency-bound chain beside the analysis waves
+  if (a.prio) __builtin_amdgcn_s_setprio(3);
   const int row = blockIdx.x, b = blockIdx.y;
   const int wc = a.g.wc, hc = a.g.hc, nctu = wc * hc;
   __shared__ uint4 tring[kTokT / 4];
@@ -890,24 +892,36 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
     src = reinterpret_cast<const uint32_t*>(a.tab->init[a.pic.init_type][clip3(0, 51, (int)a.dec.qp[b])]);
   } else {
     int f = 0;
-    for (long spin = 0; (f = __hip_atomic_load(&wflag[row - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0;
+    // agent-scope polls go past the XCD's L2 to the fabric, all rows of a picture on one line:
+    // a few quick polls, then ~3 us apart (a row waits ~2 CTBs of every row above it)
+    for (int spin = 0; (f = __hip_atomic_load(&wflag[row - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0;
          ++spin) {
-      if (spin > (1L << 26)) {  // seconds: the row above never came (never expected)
+      if (spin > (1 << 23)) {  // ~25 s: the row above never came (never expected)
         abort_row(32);
         return;
       }
-      __builtin_amdgcn_s_sleep(2);
+      if (spin < 8)
+        __builtin_amdgcn_s_sleep(4);
+      else
+        __builtin_amdgcn_s_sleep(127);
     }
     if (f != 1) {  // the row above aborted: so does this one
       __hip_atomic_store(&wflag[row], 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     src = wctx + (long)(row - 1) * (kEntCtx / 4);
   }
   uint32_t* ctx32 = reinterpret_cast<uint32_t*>(ctx);
+  if (row == 0) {
 #pragma unroll
-  for (int i = 0; i < kEntCtx / 4; ++i) ctx32[i] = src[i];
+    for (int i = 0; i < kEntCtx / 4; ++i) ctx32[i] = src[i];
+  } else {  // agent-scope loads (sc1): the row above may run on another XCD
+    uint32_t t[kEntCtx / 4];
+#pragma unroll
+    for (int i = 0; i < kEntCtx / 4; ++i) t[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int i = 0; i < kEntCtx / 4; ++i) ctx32[i] = t[i];
+  }
   // coder state (CabacEncoder): low, range, bits left, outstanding bytes, buffered byte
   uint32_t low = 0, range = 510, buffered = 0xff;
   int bl = 23, nbuf = 0, pos = 0;
@@ -1002,9 +1016,14 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
       }
     } else if ((tok & 0xff) == kCtrlSync) {  // 9.3.2.4 storage for the row below
       uint32_t* dst = wctx + (long)row * (kEntCtx / 4);
+      // agent-scope stores (sc1, written through to the fabric), completed before the flag:
+      // an agent release fence here wrote back the whole L2 of the XCD for every row, which
+      // cost the concurrently running analysis kernels ~9 % of the step
+      uint32_t t[kEntCtx / 4];
 #pragma unroll
-      for (int i = 0; i < kEntCtx / 4; ++i) dst[i] = ctx32[i];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      for (int i = 0; i < kEntCtx / 4; ++i) t[i] = ctx32[i];
+#pragma unroll
+      for (int i = 0; i < kEntCtx / 4; ++i) __hip_atomic_store(dst + i, t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&wflag[row], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       synced = true;
@@ -1083,22 +1102,80 @@ __global__ void __launch_bounds__(256) k_ent_pack(EntropyArgs a, int B) {
       for (int k = threadIdx.x; k < n; k += 256) dst[k] = src[k];
     }
   }
-  __threadfence_system();
+  // no system fence: the host reads the slot after the stream's completion event
 }
 
 // the picture's final status into the host slot (after every pack workgroup)
 __global__ void k_ent_status(EntropyArgs a) {
   a.hhead[0] = *a.status;
-  __threadfence_system();
+}
+
+// TV_ENT_SKIP timing experiment only (wrong bytes): every row one byte long
+__global__ void k_ent_fake_rows(EntropyArgs a, int n) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k < n) a.row_bytes[k] = 1;
+}
+
+template <int I>
+__device__ __forceinline__ uint32_t big_body(uint32_t x) {
+  if constexpr (I < 400) {
+    x = __builtin_amdgcn_readfirstlane((x ^ (x >> (I % 13 + 1))) * (2654435761u + 2u * I) + I);
+    return big_body<I + 1>(x);
+  } else {
+    return x;
+  }
+}
+
+// TV_ENT_SKIP 4/8/16/32 (experiment): one wave per row for ~0.9 ms sleeping (4), in a scalar
+// ALU chain (8) or in a dependent LDS chain (16), in place of the coder
+__global__ void __launch_bounds__(64) k_ent_spin(EntropyArgs a, int mode) {
+  __shared__ uint32_t lds[256];
+  lds[threadIdx.x] = threadIdx.x;
+  lds[threadIdx.x + 64] = threadIdx.x;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  uint32_t x = blockIdx.x;
+  while (wall_clock64() - t0 < 90) {
+    if (mode & 4) {
+      __builtin_amdgcn_s_sleep(127);
+    } else if (mode & 32) {  // ~8 KB of straight-line code (instruction-cache footprint)
+      x = big_body<0>(x);
+    } else if (mode & 8) {
+      for (int k = 0; k < 64; ++k) x = __builtin_amdgcn_readfirstlane(x * 1664525u + 1013904223u);
+    } else {
+      for (int k = 0; k < 64; ++k) {
+        x = lds[x & 127];
+        lds[(x + 1) & 127] = x + k;
+      }
+    }
+  }
+  if (x == 0xdeadbeef) a.row_bytes[0] = 0;
+  a.row_bytes[(long)blockIdx.y * a.g.hc + blockIdx.x] = 1;
 }
 
 }  // namespace
+
+// TV_ENT_SKIP (timing experiments; the bitstream is wrong): 1 skips the arithmetic coder, 2 the
+// binariser as well
+static int ent_skip() {
+  static const int v = [] {
+    const char* e = std::getenv("TV_ENT_SKIP");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 
 void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s) {
   const int nctu = a.g.wc * a.g.hc;
   if (a.g.wc < 2) throw std::runtime_error("GPU entropy coding needs at least 2 CTB columns");
   if (a.g.hc > 256) throw std::runtime_error("GPU entropy coding supports at most 256 CTB rows");
   (void)hipMemsetAsync(a.status, 0, sizeof(int), s);
+  if (ent_skip() & 2) {
+    (void)hipMemsetAsync(a.ctb_off, 0, (size_t)B * nctu * sizeof(int), s);
+    (void)hipMemsetAsync(a.seg_tok, 0, (size_t)B * sizeof(int), s);
+    return;
+  }
   if (a.pic.type != 2) k_ent_cu<<<dim3((unsigned)((a.g.usz + 255) / 256), B), 256, 0, s>>>(a);
   k_ent_bin<true><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
   k_ent_scan<<<B, 1024, 0, s>>>(a);
@@ -1109,7 +1186,19 @@ void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s) {
 
 void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s) {
   (void)hipMemsetAsync(a.wflag, 0, (size_t)B * a.g.hc * sizeof(int), s);
-  k_ent_ac<<<dim3(a.g.hc, B), 64, 0, s>>>(a);
+  if (ent_skip() & 60)
+    k_ent_spin<<<dim3(a.g.hc, B), 64, 0, s>>>(a, ent_skip());
+  else if (ent_skip())
+    k_ent_fake_rows<<<(B * a.g.hc + 255) / 256, 256, 0, s>>>(a, B * a.g.hc);
+  else {
+    static const int prio = [] {
+      const char* e = std::getenv("TV_ENT_PRIO");
+      return e ? std::atoi(e) : 1;
+    }();
+    EntropyArgs c = a;
+    c.prio = prio;
+    k_ent_ac<<<dim3(a.g.hc, B), 64, 0, s>>>(c);
+  }
   k_ent_pack<<<B, 256, 0, s>>>(a, B);
   k_ent_status<<<1, 1, 0, s>>>(a);
 }

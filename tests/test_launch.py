@@ -105,7 +105,7 @@ def test_tv_cpus_caps_the_rank_cpu_set(tmp_path):
     assert a == b == want, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 @pytest.mark.parametrize("mode", [[], ["--kbps", "300"], ["--codec", "av1"], ["--ladder", "96"]],
                          ids=["1pass", "2pass", "av1", "ladder"])
 def test_bench_cpu_rehearsal_n_ranks(n, mode):

@@ -185,18 +185,20 @@ def test_segment_stream_uneven_claims_gloo_world4(tmp_path):
     assert r["ok"] and r["n"] == 3 + 6 + 9 and r["rounds"] >= 2
 
 
-def test_rccl_segment_stream_matches_file_handoff_world4(tmp_path, source):
+@pytest.mark.parametrize("world", [4, 8])
+def test_rccl_segment_stream_matches_file_handoff(tmp_path, source, world):
     """The streaming stitch's peer segments travel over the collective segment stream
-    (RCCL on the GPU, gloo here) instead of part files: 4 ranks, 12 segments, and the
-    stitched MP4 is byte-identical to the file hand-off version."""
+    (RCCL on the GPU, gloo here) instead of part files: 4 and 8 ranks (the SCALE shape),
+    12 segments, and the stitched MP4 is byte-identical to the file hand-off version (the
+    default transport)."""
     from thinvids_amd.models import hevc
 
     src, frames = source
     kw = {"gop": 2, "segment_frames": 2, "batch_segments": 1}
     os.makedirs(tmp_path / "a", exist_ok=True)
     os.makedirs(tmp_path / "b", exist_ok=True)
-    res_a, out_a = _spawn_job(tmp_path / "a", source, kw, {}, world=4)
-    res_b, out_b = _spawn_job(tmp_path / "b", source, kw, {"TV_STITCH_TRANSPORT": "files"}, world=4)
+    res_a, out_a = _spawn_job(tmp_path / "a", source, kw, {"TV_STITCH_TRANSPORT": "rccl"}, world=world)
+    res_b, out_b = _spawn_job(tmp_path / "b", source, kw, {}, world=world)
     sa, sb = res_a[0]["stitch"], res_b[0]["stitch"]
     assert sa["transport"] == "rccl" and sb["transport"] == "files"
     peers = sum(p["encoded"] for p in res_a[0]["per_rank"][1:])

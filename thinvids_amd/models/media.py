@@ -24,7 +24,7 @@ from fractions import Fraction
 
 import numpy as np
 
-from . import hevc
+from . import hevc, mpeg2
 
 VIDEO_EXTS = (".y4m", ".synth", ".hevc", ".265", ".mp4", ".mkv")
 
@@ -269,6 +269,8 @@ def open_source(path: str):
         return SynthSource(path)
     if ext == ".ivf" or (ext == ".mp4" and _is_av1_file(path)):
         return Av1Source(path)
+    if ext in mpeg2.ES_EXTS or (ext == ".mkv" and mpeg2.is_mpeg2_mkv(path)):
+        return mpeg2.Mpeg2Source(path)  # DVD titles (MakeMKV V_MPEG2) / raw MPEG-2 video
     if ext in (".hevc", ".265", ".mp4", ".mkv"):
         return HevcSource(path)
     raise ValueError(f"unsupported input format: {path}")
@@ -280,7 +282,8 @@ def probe(path: str) -> dict:
     size = os.path.getsize(path) if os.path.exists(path) else 0
     fps = src.fps_num / src.fps_den
     dur = src.nframes / fps if fps else 0.0
-    codec = {"rawvideo": "rawvideo", "synthetic": "synthetic", "hevc": "hevc", "av1": "av1"}[src.kind]
+    codec = {"rawvideo": "rawvideo", "synthetic": "synthetic", "hevc": "hevc", "av1": "av1",
+             "mpeg2": "mpeg2video"}[src.kind]
     return {
         "codec": codec,
         "width": src.width,
@@ -293,6 +296,7 @@ def probe(path: str) -> dict:
         "duration": round(dur, 3),
         "size": size,
         "bits": int(getattr(src, "bits", 8)),
+        "field_order": getattr(src, "field_order", "progressive"),
         "bitrate_kbps": round(size * 8 / dur / 1000.0, 1) if dur else 0.0,
         "streams": _stream_list(path, codec, src),
     }

@@ -76,6 +76,35 @@ def bwdif_plane(prev, cur, nxt, tff: bool = True):
     return out
 
 
+def deinterlace_device(df, tff: bool = True):
+    """bwdif (send_frame) over a segment of 8-bit device frames (ops.stage.DevFrames) with
+    ``k_bwdif``: frame i from (i-1, i, i+1), the segment's edges repeat (the split pipeline's
+    per-part rule).  Returns new DevFrames in the same layout."""
+    import torch
+
+    from .._native import gpu_lib
+    from .stage import DevFrames
+
+    if df.bits != 8:
+        raise ValueError("bwdif: 8-bit frames only")
+    out = torch.empty_like(df.buf)
+    lib = gpu_lib()
+    stream = C.c_void_p(torch.cuda.current_stream(df.buf.device).cuda_stream)
+    esz = df.buf.element_size()
+    src, dst = df.buf.data_ptr(), out.data_ptr()
+    for i in range(df.n):
+        for off, pw, ph, st, fs in df.planes:
+            if st != pw:
+                raise ValueError("bwdif: planes must be packed")
+            at = lambda base, k: C.c_void_p(base + (off + k * fs) * esz)  # noqa: E731
+            rc = lib.tv_bwdif_plane(at(src, max(0, i - 1)), at(src, i), at(src, min(df.n - 1, i + 1)), at(dst, i),
+                                    pw, ph, int(tff), stream)
+            if rc != 0:
+                lib.tv_ops_last_error.restype = C.c_char_p
+                raise RuntimeError(lib.tv_ops_last_error().decode())
+    return DevFrames(out, df.n, df.w, df.h, df.planes, df.bits, [df.buf, *df.keep])
+
+
 def deinterlace_frames(frames: list, tff: bool = True) -> list:
     """send_frame mode over a sequence: frame i uses (i-1, i, i+1), edges repeat."""
     n = len(frames)

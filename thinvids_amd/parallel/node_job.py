@@ -17,10 +17,10 @@ Flow (the reference's split -> encode -> stitch, without HTTP or disk in between
    per-segment sizes are **all-reduced** and every rank derives the same per-segment QP
    plan (complexity^0.6 allocation), then encodes pass 2;
 5. single-pass jobs with a plain MP4 output are **stitched while they encode**: every
-   finished claim goes to rank 0 (its own in memory, the peers' over RCCL point-to-point
-   in per-claim gather rounds on a comm thread, comm.SegmentStream), whose stitch thread
-   appends each rung's segments in order to a streaming faststart MP4 writer (ranks keep
-   no bitstreams; ``TV_STITCH_TRANSPORT=files`` falls back to part files); otherwise bitstreams are gathered to rank 0 after the last pass (all_gather
+   finished claim goes to rank 0 (its own in memory, the peers' as part files, or with
+   ``TV_STITCH_TRANSPORT=rccl`` point-to-point in per-claim gather rounds on a comm thread,
+   comm.SegmentStream), whose stitch thread appends each rung's segments in order to a
+   streaming faststart MP4 writer; otherwise bitstreams are gathered to rank 0 after the last pass (all_gather
    of sizes + grouped send/recv) and muxed in segment order.  ``--ladder`` fans rungs x
    segments out over all ranks and writes one MP4 per rung.
 """
@@ -441,13 +441,15 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             deblock: bool = True, sao: bool = False, cache=None, crf: int = 0, scenecut: bool = False,
             audio_stream: int = 0, codec: str = "hevc", qindex: int = 0, rc_mode: str = "",
             vbv_maxrate_kbps: float = 0.0, vbv_bufsize_kbit: float = 0.0, bframes: int = 1,
-            tools: dict | None = None) -> dict:
+            tools: dict | None = None, deinterlace: bool = False) -> dict:
     """One job over the node's ranks (SPMD).  Rate control: ``bitrate_kbps`` > 0 selects
     frame-level 2-pass, or single-pass ABR when ``rc_mode == "abr"`` (optionally under a VBV:
     ``vbv_maxrate_kbps`` / ``vbv_bufsize_kbit``, checked and repaired per segment, see
     models/ratecontrol.py); else ``crf`` > 0 in-engine CRF; else constant ``qp``.  ``tools``:
     HEVC coding-tool switches (EncodeSpec wpp / rqt / pintra; default all on) -- part of the
-    checkpoint fingerprint, so a resume with other tools re-encodes."""
+    checkpoint fingerprint, so a resume with other tools re-encodes.  ``deinterlace``: bwdif
+    (K3, the DVD-native rule of worker/helpers.effective_target_height) on every segment
+    before the resize, in the source's field order."""
     import torch
 
     from ..models import hevc, media
@@ -475,6 +477,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     segs = plan_segments(nfr, segment_frames, gop)
     software = software or not gpu_available()
     synthetic = isinstance(src, media.SynthSource)
+    deinterlace = bool(deinterlace) and not synthetic
+    tff = bool(getattr(src, "top_field_first", True))
     fps = src.fps_num / src.fps_den
     abr = rc_mode == "abr" and bitrate_kbps > 0
     vbv = abr and vbv_maxrate_kbps > 0 and vbv_bufsize_kbit > 0
@@ -493,7 +497,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         src=os.path.abspath(input_path), size=st.st_size if st else 0, mtime=st.st_mtime_ns if st else 0,
         rungs=rungs, gop=gop, segment_frames=segment_frames, search_range=search_range, software=software,
         deblock=deblock, sao=sao, scenecut=scenecut, codec=codec, qindex=qindex, crf=crf, bframes=bframes,
-        rc=rc_name, bitstream_version=BITSTREAM_VERSION, tools=tool_kw,
+        rc=rc_name, bitstream_version=BITSTREAM_VERSION, tools=tool_kw, deinterlace=bool(deinterlace),
         **({"kbps": bitrate_kbps, "vbv": [vbv_maxrate_kbps, vbv_bufsize_kbit] if vbv else None} if abr else {})))
     stats = {"encoded": 0, "resumed": 0, "retried": 0, "reads": 0}
     quality: dict = {}  # (r, i) -> PartStats of segments encoded here
@@ -504,9 +508,12 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     out_paths = [output if len(rungs) == 1 else f"{os.path.splitext(output)[0]}_{oh}p.mp4" for _, oh in rungs]
     if side is not None:
         out_paths = [os.path.splitext(p)[0] + side.ext for p in out_paths]
-    # peers' finished segments reach the stitch rank over RCCL (comm.SegmentStream); the
-    # part-file hand-off through the node-local job directory is the fallback
-    transport = os.environ.get("TV_STITCH_TRANSPORT", "rccl") if world > 1 else "local"
+    # peers' finished segments reach the stitch rank as part files through the node-local job
+    # directory, or with TV_STITCH_TRANSPORT=rccl over the collective backend
+    # (comm.SegmentStream).  The stream is proven byte-identical on gloo at world 4 and 8
+    # (tests/test_parallel.py) but has not yet run on RCCL at world > 1 (1-GPU test boxes), so
+    # the part files stay the default until it has
+    transport = os.environ.get("TV_STITCH_TRANSPORT", "files") if world > 1 else "local"
     parts_dir = None
     stitcher = None
     if streaming and transport == "files":
@@ -561,13 +568,39 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         stats["reads"] += 1
         if synthetic:
             return SynthRange(src.seed, w0, h0, src.start + s, n)
-        if software:
-            return src.read(s, n)
-        from ..ops import stage
+        if isinstance(src, media.Y4MSource) and not software:
+            from ..ops import stage
 
-        if isinstance(src, media.Y4MSource):
-            return stage.read_y4m_device(src, s, n, dev, stats=stats)
-        return stage.upload_frames(src.read(s, n), dev)
+            return finish(stage.read_y4m_device(src, s, n, dev, stats=stats))
+        return finish(src.read(s, n))
+
+    def finish(fr):
+        """Decoded host frames (or Y4M device frames) -> this rank's encoder input: bwdif when
+        asked, on the device for GPU encodes."""
+        from ..ops import deint
+
+        if software:
+            return deint.deinterlace_frames(fr, tff) if deinterlace else fr
+        if isinstance(fr, list):
+            from ..ops import stage
+
+            fr = stage.upload_frames(fr, dev)
+        return deint.deinterlace_device(fr, tff) if deinterlace else fr
+
+    # decoded sources (MPEG-2 / HEVC / AV1 files): a claim's segments are decoded on parallel
+    # host threads (each decode is one GOP range; the native decoders release the GIL)
+    decoded = not synthetic and not isinstance(src, media.Y4MSource)
+    ndec = int(os.environ.get("TV_DECODE_THREADS", "0") or 0) or min(8, len(os.sched_getaffinity(0)))
+    dec_pool = cf.ThreadPoolExecutor(ndec) if decoded and ndec > 1 else None
+
+    def preload(ids):
+        ids = [i for i in ids if i not in prefetched]
+        if dec_pool is None or len(ids) < 2:
+            return {}
+        with trace.span("node_job.decode", segments=len(ids)):
+            hosts = list(dec_pool.map(lambda i: src.read(*segs[i]), ids))
+        stats["reads"] += len(ids)
+        return {i: finish(fr) for i, fr in zip(ids, hosts)}
 
     # file sources on the GPU: the next claim is read + uploaded on a side thread / HIP
     # stream while this claim encodes (the reference overlaps GET part with the previous
@@ -575,7 +608,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     # Only Y4M sources: their reads are pread threads + DMA, so the side thread costs the
     # engine nothing; a decoded source (HEVC / AV1 / MPEG-2) would run a whole CPU decode there
     # (ADVICE r4), unmeasured -- those load on demand.
-    prefetch = (not synthetic and not software and dev.type == "cuda" and isinstance(src, media.Y4MSource)
+    prefetch = (not synthetic and not software and dev.type == "cuda"
+                and (isinstance(src, media.Y4MSource) or dec_pool is not None)
                 and os.environ.get("TV_PREFETCH", "1") != "0")
     prefetcher = None
     if prefetch:
@@ -587,7 +621,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
 
         def load_ahead(ids):
             with torch.cuda.stream(_prefetch_init.stream), trace.span("node_job.prefetch"):
-                return {i: load(i) for i in ids}
+                got = preload(ids)
+                return {i: got[i] if i in got else load(i) for i in ids}
 
     def encode_segments(seg_ids, source_of) -> dict:
         """Work item = one segment with ALL its rungs: the source range is read (or received)
@@ -742,6 +777,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 if not todo:
                     return
                 try:
+                    prefetched.update(preload(todo))
                     mine.update(encode_segments(todo, load))
                 except Exception as e:  # a real engine/IO failure: every item goes back
                     for i in todo:
@@ -967,6 +1003,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         io_pool.shutdown(wait=True)
         if prefetcher is not None:
             prefetcher.shutdown(wait=True)
+        if dec_pool is not None:
+            dec_pool.shutdown(wait=True)
         if parts_dir and rank == 0:
             import shutil
 
@@ -996,6 +1034,7 @@ def main(argv=None) -> int:
     ap.add_argument("--no-wpp", dest="wpp", action="store_false", help="HEVC: one CABAC substream per slice (host)")
     ap.add_argument("--no-rqt", dest="rqt", action="store_false", help="HEVC: no residual quadtree")
     ap.add_argument("--no-pintra", dest="pintra", action="store_false", help="HEVC: no intra CUs in P pictures")
+    ap.add_argument("--deinterlace", action="store_true", help="bwdif every segment (DVD-native interlaced sources)")
     a = ap.parse_args(argv)
     import torch
     import torch.distributed as dist
@@ -1013,7 +1052,7 @@ def main(argv=None) -> int:
     ladder = [int(x) for x in a.ladder.split(",") if x.strip()] or None
     res = run_job(a.input, a.output, a.height, a.qp, a.gop, a.segment_frames, a.mode, a.bitrate_kbps, ladder,
                   software=a.software, resume_dir=a.resume_dir, max_retries=a.max_retries, bframes=a.bframes,
-                  tools={"wpp": a.wpp, "rqt": a.rqt, "pintra": a.pintra})
+                  tools={"wpp": a.wpp, "rqt": a.rqt, "pintra": a.pintra}, deinterlace=a.deinterlace)
     if int(os.environ.get("RANK", "0")) == 0:
         print(json.dumps(res), flush=True)
     if dist.is_initialized():

@@ -127,7 +127,7 @@ def _job_params(job: dict) -> dict:
 
     s = get_settings()
     spec = encode_spec_for_job(job, s)
-    th, _ = effective_target_height(job)
+    th, deint = effective_target_height(job)
     ladder = [int(x) for x in str(job.get("ladder") or s.get("tv_ladder") or "").split(",") if x.strip()]
     rc = str(job.get("rc_mode") or s.get("tv_rc") or "cqp").lower()
     kbps = as_float(job.get("bitrate_kbps") or s.get("tv_bitrate_kbps"), 0.0) if rc in ("2pass", "abr") else 0.0
@@ -139,7 +139,8 @@ def _job_params(job: dict) -> dict:
             "segment_frames": max(spec.gop, as_int(s.get("tv_node_segment_frames"), 256)),
             "mode": str(s.get("tv_node_mode") or "direct"), "batch_segments": as_int(s.get("tv_node_batch"), 8),
             "settings_ok": as_bool(s.get("tv_node_executor"), True), "crf": crf, "rc": rc, "vbv": vbv,
-            "scenecut": spec.scenecut, "codec": spec.codec, "qindex": spec.qindex, "bframes": spec.hevc_bframes()}
+            "scenecut": spec.scenecut, "codec": spec.codec, "qindex": spec.qindex, "bframes": spec.hevc_bframes(),
+            "deinterlace": deint}
 
 
 class CommFailure(RuntimeError):
@@ -166,7 +167,7 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
 
                 path = resolve_input_path(job)
                 info = media.probe(path)
-                job.update(source_width=info["width"], source_height=info["height"])
+                job.update(source_width=info["width"], source_height=info["height"], source_codec=info["codec"])
                 params = _job_params(job)
                 segs = plan_segments(int(info["frames"]), params["segment_frames"], params["gop"])
                 reset_job_run_state(job_id, job)  # keeps <base>/ckpt: a requeued job resumes
@@ -211,7 +212,8 @@ def execute(job_id: str, run_token: str | None, rank: int, world: int, cache, lo
                       scenecut=p.get("scenecut", False), codec=p.get("codec", "hevc"), qindex=p.get("qindex", 0),
                       bframes=p.get("bframes", 1),
                       audio_stream=int(spec["job"].get("selected_a_stream") or 0), rc_mode=p.get("rc", ""),
-                      vbv_maxrate_kbps=p.get("vbv", [0, 0])[0], vbv_bufsize_kbit=p.get("vbv", [0, 0])[1])
+                      vbv_maxrate_kbps=p.get("vbv", [0, 0])[0], vbv_bufsize_kbit=p.get("vbv", [0, 0])[1],
+                      deinterlace=p.get("deinterlace", False))
     except Exception as e:
         if is_comm_failure(e):  # the job is fine, the communicator is not: requeue + re-init
             log.error("[%s] communicator failure on rank %d: %s", job_id, rank, e)
