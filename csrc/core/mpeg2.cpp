@@ -315,24 +315,30 @@ size_t next_start_code(const uint8_t* d, size_t n, size_t p) {
 void idct(const int32_t* F, int16_t* out) {
   const auto& c = tabs().cosx;
   double t[64];
+  int rows[8], nr = 0;  // rows with a coefficient (all-zero rows add exact zeros: skipped)
   for (int v = 0; v < 8; ++v) {
     const int32_t* r = F + v * 8;
     bool any = false;
     for (int u = 0; u < 8; ++u) any |= r[u] != 0;
-    for (int x = 0; x < 8; ++x) {
-      double s = 0;
-      if (any)
-        for (int u = 0; u < 8; ++u) s += c[u][x] * r[u];
-      t[v * 8 + x] = s;
+    if (!any) continue;
+    rows[nr++] = v;
+    double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int u = 0; u < 8; ++u) {
+      if (!r[u]) continue;  // exact: a zero coefficient adds zeros
+      const double f = r[u];
+      for (int x = 0; x < 8; ++x) s[x] += c[u][x] * f;
     }
+    for (int x = 0; x < 8; ++x) t[v * 8 + x] = s[x];
   }
-  for (int y = 0; y < 8; ++y)
-    for (int x = 0; x < 8; ++x) {
-      double s = 0;
-      for (int v = 0; v < 8; ++v) s += c[v][y] * t[v * 8 + x];
-      const int r = (int)std::floor(s + 0.5);
-      out[y * 8 + x] = int16_t(std::clamp(r, -256, 255));
+  for (int y = 0; y < 8; ++y) {
+    double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // x innermost (vectorised); per element the
+    for (int k = 0; k < nr; ++k) {           // same ascending-row order of additions
+      const double cv = c[rows[k]][y];
+      const double* tr = t + rows[k] * 8;
+      for (int x = 0; x < 8; ++x) s[x] += cv * tr[x];
     }
+    for (int x = 0; x < 8; ++x) out[y * 8 + x] = int16_t(std::clamp((int)std::floor(s[x] + 0.5), -256, 255));
+  }
 }
 
 void fdct(const int16_t* in, double* F) {
@@ -380,6 +386,21 @@ struct View {  // a plane (frame or field) of a reference
 // 7.6.4 half-sample prediction of a w x h block at integer (x, y) + half flags
 void mc(const View& r, int x, int y, int hx, int hy, int w, int h, uint8_t* dst, int ds) {
   const bool inside = x >= 0 && y >= 0 && x + w + hx <= r.w && y + h + hy <= r.h;
+  if (inside) {  // the common case, one loop per half-sample phase
+    const uint8_t* q = r.p + (size_t)y * r.stride + x;
+    const int s = r.stride;
+    for (int j = 0; j < h; ++j, q += s, dst += ds) {
+      if (hx && hy)
+        for (int i = 0; i < w; ++i) dst[i] = uint8_t((q[i] + q[i + 1] + q[i + s] + q[i + s + 1] + 2) >> 2);
+      else if (hx)
+        for (int i = 0; i < w; ++i) dst[i] = uint8_t((q[i] + q[i + 1] + 1) >> 1);
+      else if (hy)
+        for (int i = 0; i < w; ++i) dst[i] = uint8_t((q[i] + q[i + s] + 1) >> 1);
+      else
+        std::memcpy(dst, q, w);
+    }
+    return;
+  }
   for (int j = 0; j < h; ++j)
     for (int i = 0; i < w; ++i) {
       int a, b, c, d;

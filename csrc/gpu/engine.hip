@@ -391,6 +391,18 @@ class Core {
   double sse(int b, int c) const { return sse_host_[b * 3 + c]; }
   long coef_bytes() const { return coef_bytes_; }
   long ent_fallbacks() const { return ent_fallbacks_; }
+  long ent_host_pictures() const { return ent_host_pics_; }
+  static int host_share() {
+    static const int n = [] {
+      const char* e = getenv("TV_ENT_HOST");
+      return e ? atoi(e) : 0;
+    }();
+    return n;
+  }
+  static std::atomic<int>& host_inflight() {  // pictures in the (process-wide) host writer pool
+    static std::atomic<int> n{0};
+    return n;
+  }
   int ent_status() const { return ent_status_; }
   bool gpu_entropy_on() const { return gpu_ent_; }
   double entropy_ms() const { return entropy_ns_ / 1e6; }
@@ -447,6 +459,7 @@ class Core {
     uint8_t* host = nullptr;
     hipEvent_t ev{};
     std::atomic<int> pending{0};
+    std::atomic<int> host_coded{0};  // hybrid entropy: slices of a host-routed picture still open
     bool qp_dirty = true;  // the slot's device QP array may not hold the sequence QP
   };
   // carve one slot buffer (device or host) into its arrays
@@ -856,7 +869,16 @@ class Core {
     if (!seq_.sao) launch_sse(src_, fin_set, g_, d_sse_, B, stream_);  // with SAO: summed by k_sao_decide
     stage("sse");
     HIP_OK(hipGetLastError());
-    if (gpu_ent_) {  // entropy coding on its own stream: the next picture's kernels run meanwhile
+    // hybrid entropy (TV_ENT_HOST = n > 0): while fewer than n pictures sit in the host writer
+    // pool, the next one is coded there (its decisions are fetched as in host mode) and its
+    // entropy kernels never compete with the analysis kernels; otherwise the GPU codes it
+    const bool on_host = gpu_ent_ && host_share() > 0 && host_inflight().load(std::memory_order_relaxed) < host_share();
+    if (on_host) {
+      host_inflight().fetch_add(1, std::memory_order_relaxed);
+      ent_host_pics_++;
+    }
+    const bool use_gpu = gpu_ent_ && !on_host;
+    if (use_gpu) {  // entropy coding on its own stream: the next picture's kernels run meanwhile
       HIP_OK(hipEventRecord(eev_, stream_));
       HIP_OK(hipStreamWaitEvent(estream_, eev_, 0));
       // binarisation on the core's entropy stream (one picture at a time: its scratch is per
@@ -881,11 +903,12 @@ class Core {
     // stream order, so a FIFO of waits loses nothing): one thread per core spins on the
     // completion events instead of one pool thread per in-flight slot, and the pool's
     // threads only ever run CABAC.
-    fetch_->submit([this, &s, B, f] {
+    if (on_host) s.host_coded.store(B, std::memory_order_relaxed);
+    fetch_->submit([this, &s, B, f, use_gpu] {
       bool gpu = false;  // the GPU coded the picture: only the slice NALs are assembled here
       try {
         Range r("engine.d2h");
-        gpu = gpu_ent_ && fetch_entropy(s, B);
+        gpu = use_gpu && fetch_entropy(s, B);
         if (!gpu) fetch_slot(s, B, plan_.pics[f].type);
       } catch (const std::exception& e) {
         fail(e);
@@ -911,6 +934,8 @@ class Core {
           } catch (const std::exception& e) {
             fail(e);
           }
+          if (s.host_coded.load(std::memory_order_relaxed) && s.host_coded.fetch_sub(1) == 1)
+            host_inflight().fetch_sub(1, std::memory_order_relaxed);  // the picture's last slice
           release(s, 1);
         });
     });
@@ -984,6 +1009,7 @@ class Core {
   long tok_cap_ = 0, slot_host_bytes_ = 0;
   unsigned long long* ent_dbg_ = nullptr;  // TV_ENT_DEBUG=1: coder counters (EntropyArgs::dbg)
   std::atomic<long> ent_fallbacks_{0};
+  std::atomic<long> ent_host_pics_{0};
   std::atomic<int> ent_status_{0};
   bool qmap_given_ = false;  // an explicit QP map (2-pass plan) overrides in-engine CRF
   int8_t* qhost_ = nullptr;  // pinned [frame][segment] slice QPs of the current call
@@ -1128,6 +1154,11 @@ class Engine {
       fallbacks += c->ent_fallbacks();
       status |= c->ent_status();
     }
+  }
+  long entropy_host_pictures() const {
+    long n = 0;
+    for (const auto& c : cores_) n += c->ent_host_pictures();
+    return n;
   }
   const Geo& geo() const { return cores_[0]->geo(); }
   size_t dev_bytes() const {
@@ -1284,6 +1315,10 @@ void tv_engine_entropy_stats(void* e, int* on, long long* fallbacks, int* status
   long f = 0;
   static_cast<tv::gpu::Engine*>(e)->entropy_stats(*on, f, *status);
   *fallbacks = f;
+}
+// pictures the hybrid policy (TV_ENT_HOST) sent to the host writer since construction
+long long tv_engine_entropy_host_pictures(void* e) {
+  return static_cast<tv::gpu::Engine*>(e)->entropy_host_pictures();
 }
 // The same for an engine not built yet (same arguments as tv_engine_new_b's geometry part)
 int tv_engine_estimate(int width, int height, int batch, int gop, int deblock, int mgop, unsigned long long* dev,

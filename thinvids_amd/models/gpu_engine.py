@@ -225,7 +225,10 @@ class GpuEngine:
         f = self.lib.tv_engine_entropy_stats
         f.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_longlong), C.POINTER(C.c_int)]
         f(self.h, C.byref(on), C.byref(fb), C.byref(st))
-        return {"gpu": bool(on.value), "fallbacks": int(fb.value), "status": int(st.value)}
+        hp = self.lib.tv_engine_entropy_host_pictures
+        hp.argtypes, hp.restype = [C.c_void_p], C.c_longlong
+        return {"gpu": bool(on.value), "fallbacks": int(fb.value), "status": int(st.value),
+                "host_pictures": int(hp(self.h))}
 
     def last_recon(self, b: int):
         y = np.empty((self.ch, self.cw), np.uint8)
