@@ -649,8 +649,9 @@ def main() -> None:
                     help="one CABAC substream per slice (coded on the host) instead of WPP rows coded on the GPU")
     ap.add_argument("--no-rqt", dest="rqt", action="store_false", help="HEVC: no residual quadtree")
     ap.add_argument("--no-pintra", dest="pintra", action="store_false", help="HEVC: no intra CUs in P pictures")
-    ap.add_argument("--entropy", choices=("gpu", "host"), default=None,
-                    help="where WPP substreams are CABAC-coded (default gpu; TV_ENTROPY); same bytes either way")
+    ap.add_argument("--entropy", choices=("gpu", "host", "auto"), default=None,
+                    help="where WPP substreams are CABAC-coded (default auto: the host writer with >= 12 CPUs "
+                         "per rank, else the GPU; TV_ENTROPY); same bytes either way")
     ap.add_argument("--cpu", action="store_true",
                     help="rehearsal on CPU: gloo ranks + the golden encoders (models/cpu_engines.py), tiny geometry")
     args = ap.parse_args()

@@ -392,13 +392,7 @@ class Core {
   long coef_bytes() const { return coef_bytes_; }
   long ent_fallbacks() const { return ent_fallbacks_; }
   long ent_host_pictures() const { return ent_host_pics_; }
-  static int host_share() {
-    static const int n = [] {
-      const char* e = getenv("TV_ENT_HOST");
-      return e ? atoi(e) : 0;
-    }();
-    return n;
-  }
+  int host_share() const { return host_share_; }
   static std::atomic<int>& host_inflight() {  // pictures in the (process-wide) host writer pool
     static std::atomic<int> n{0};
     return n;
@@ -1010,6 +1004,12 @@ class Core {
   unsigned long long* ent_dbg_ = nullptr;  // TV_ENT_DEBUG=1: coder counters (EntropyArgs::dbg)
   std::atomic<long> ent_fallbacks_{0};
   std::atomic<long> ent_host_pics_{0};
+  // hybrid entropy: pictures allowed in the host writer at once (TV_ENT_HOST, read when the
+  // core is built; 0 = every picture on the GPU)
+  int host_share_ = [] {
+    const char* e = getenv("TV_ENT_HOST");
+    return e ? atoi(e) : 0;
+  }();
   std::atomic<int> ent_status_{0};
   bool qmap_given_ = false;  // an explicit QP map (2-pass plan) overrides in-engine CRF
   int8_t* qhost_ = nullptr;  // pinned [frame][segment] slice QPs of the current call

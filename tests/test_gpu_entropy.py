@@ -13,6 +13,7 @@ pytestmark = pytest.mark.gpu
 
 def _engine(**kw):
     from thinvids_amd.models.gpu_engine import GpuEngine
+    kw.setdefault("entropy", "gpu")  # "auto" would pick the host writer on a many-CPU box
     return GpuEngine(**kw)
 
 
@@ -37,7 +38,7 @@ def test_gpu_entropy_equals_host_writer(w, h, qp, sao, extra):
     assert eng.entropy == "gpu"
     segs = eng.encode_synthetic(starts)
     st = eng.entropy_stats()
-    assert st == {"gpu": True, "fallbacks": 0, "status": 0}, st
+    assert (st["gpu"], st["fallbacks"], st["status"], st["host_pictures"]) == (True, 0, 0, 0), st
     gold = _golden(seed, starts, w, h, gop, qp=qp, sao=sao, search_range=rng, **extra)
     for b in range(len(starts)):
         assert segs[b] == gold[b], f"segment {b}: GPU CABAC differs from the host writer"
@@ -107,3 +108,16 @@ def test_gpu_entropy_capacity_fallback(monkeypatch):
     assert segs == gold
     eng.close()
     assert st["gpu"] and st["fallbacks"] > 0 and st["status"] & 1, st
+
+
+def test_hybrid_entropy_routes_pictures_to_the_host(monkeypatch):
+    """TV_ENT_HOST=n: while fewer than n pictures sit in the host writer pool the next one is
+    coded there instead of on the GPU; the stream is the same either way."""
+    monkeypatch.setenv("TV_ENT_HOST", "1")
+    w, h, gop, rng, seed = 192, 128, 6, 16, 5
+    eng = _engine(width=w, height=h, qp=27, batch=2, gop=gop, search_range=rng, seed=seed, sao=True)
+    segs = eng.encode_synthetic([0, 10])
+    st = eng.entropy_stats()
+    eng.close()
+    assert st["gpu"] and st["host_pictures"] > 0 and st["fallbacks"] == 0, st
+    assert segs == _golden(seed, [0, 10], w, h, gop, qp=27, search_range=rng, sao=True)

@@ -92,10 +92,11 @@ class GpuEngine:
         segments' streams are then in coding order (the decoder reorders by POC) and
         :meth:`last_recon` returns the last DISPLAY frame.
 
-        `wpp` (default): one CABAC substream per CTB row, entropy-coded ON THE GPU
-        (csrc/gpu/k_entropy.hip); the host only writes slice headers and entry points.
-        `entropy`: "gpu" (default) or "host" (the C++ CABAC writer on the thread pool; same
-        bytes, for A/B runs; env TV_ENTROPY).  wpp=False always codes on the host."""
+        `wpp` (default): one CABAC substream per CTB row.  `entropy` (same bytes either way):
+        "gpu" codes them ON THE GPU (csrc/gpu/k_entropy.hip; the host only writes slice
+        headers and entry points), "host" with the C++ CABAC writer on the thread pool, "auto"
+        (default; env TV_ENTROPY) picks by the host CPU budget (:func:`auto_entropy`).
+        wpp=False always codes on the host."""
         self.lib = _lib()
         self.width, self.height, self.qp = width, height, qp
         self.batch, self.gop = batch, gop
@@ -106,9 +107,7 @@ class GpuEngine:
         self.bframes = int(bframes)
         from .hevc import codec_flags
 
-        self.entropy = (entropy or os.environ.get("TV_ENTROPY", "gpu")) if wpp else "host"
-        if self.entropy not in ("gpu", "host"):
-            raise ValueError("entropy must be 'gpu' or 'host'")
+        self.entropy = resolve_entropy(entropy) if wpp else "host"
         self.flags = codec_flags(deblock, sao, wpp, rqt, pintra) | (32 if self.entropy == "host" else 0)
         self.h = self.lib.tv_engine_new_b(width, height, qp, batch, gop, search_range, self.flags,
                                           seed & 0xFFFFFFFF, self.threads, device, max_merge, int(crf), self.bframes)
@@ -247,6 +246,26 @@ def pad_frame(y, u, v, cw, ch) -> np.ndarray:
     return np.concatenate([Y.ravel(), U.ravel(), V.ravel()])
 
 
+def auto_entropy(cpus: int | None = None) -> str:
+    """Where WPP substreams are CABAC-coded when nobody asked: the host writer costs ~1 core
+    per 1000 frames/s of 1080p (8.4 busy cores at the 1080p bench rate, ~15 on grainy
+    content) and leaves the GPU at its full analysis rate; the GPU coder frees the host (1.4
+    busy cores) for a ~12 % longer GPU step (profiles/README.md, round 5).  A process with at
+    least TV_ENT_AUTO_CPUS (12) CPUs in its affinity set -- one rank's share of an 8-GPU,
+    128-CPU node is 16 -- codes on the host, a smaller share on the GPU."""
+    n = cpus if cpus is not None else len(os.sched_getaffinity(0))
+    return "host" if n >= int(os.environ.get("TV_ENT_AUTO_CPUS", "12")) else "gpu"
+
+
+def resolve_entropy(entropy: str | None = None) -> str:
+    e = entropy or os.environ.get("TV_ENTROPY", "auto")
+    if e == "auto":
+        e = auto_entropy()
+    if e not in ("gpu", "host"):
+        raise ValueError("entropy must be 'gpu', 'host' or 'auto'")
+    return e
+
+
 def estimate_footprint(width: int, height: int, batch: int, gop: int, sao: bool = False, bframes: int = 1,
                        wpp: bool = True, rqt: bool = True, pintra: bool = True, entropy: str | None = None) -> dict:
     """HBM / pinned-host bytes an engine of this geometry would allocate, computed by the
@@ -254,7 +273,7 @@ def estimate_footprint(width: int, height: int, batch: int, gop: int, sao: bool 
     from .hevc import codec_flags
 
     lib = _lib()
-    ent = (entropy or os.environ.get("TV_ENTROPY", "gpu")) if wpp else "host"
+    ent = resolve_entropy(entropy) if wpp else "host"
     flags = codec_flags(True, sao, wpp, rqt, pintra) | (32 if ent == "host" else 0)
     d, h = C.c_ulonglong(), C.c_ulonglong()
     f = lib.tv_engine_estimate

@@ -478,6 +478,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     software = software or not gpu_available()
     synthetic = isinstance(src, media.SynthSource)
     deinterlace = bool(deinterlace) and not synthetic
+    # file sources need the host for ingest / decode: their WPP substreams are coded on the GPU
+    entropy = os.environ.get("TV_ENTROPY") or ("auto" if synthetic else "gpu")
     tff = bool(getattr(src, "top_field_first", True))
     fps = src.fps_num / src.fps_den
     abr = rc_mode == "abr" and bitrate_kbps > 0
@@ -535,7 +537,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         return EncodeSpec(rungs[r][0], rungs[r][1], qp=qp, gop=gop, search_range=search_range,
                           software=software, deblock=deblock, sao=sao, seed=getattr(src, "seed", 1),
                           crf=0 if bitrate_kbps > 0 else crf, scenecut=scenecut, codec=codec, qindex=qindex,
-                          bframes=bframes, **tool_kw)
+                          bframes=bframes, entropy=entropy, **tool_kw)
 
     rc = {"plan": None, "fb": RateFeedback(), "bits": {}}  # pass-2 plan, feedback, per-frame bits
     rung_scale = [(rw * rh) / (rungs[0][0] * rungs[0][1]) for rw, rh in rungs]  # per-rung budget ~ pixels

@@ -52,12 +52,15 @@ class EncodeSpec:
     wpp: bool = True
     rqt: bool = True
     pintra: bool = True
+    # where the WPP substreams are CABAC-coded ("auto" / "gpu" / "host"): the same bytes, so
+    # not a coding tool (not in tools() / the checkpoint fingerprint), but its own engine
+    entropy: str = "auto"
 
     def engine_key(self):
         if self.codec == "av1":
             return ("av1", self.width, self.height, self.av1_qindex())
         return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed,
-                self.crf, self.hevc_bframes(), self.wpp, self.rqt, self.pintra)
+                self.crf, self.hevc_bframes(), self.wpp, self.rqt, self.pintra, self.entropy)
 
     def tools(self) -> dict:
         """The coding-tool switches as GpuEngine / CpuEncoder keyword arguments."""
@@ -199,7 +202,7 @@ class EngineCache:
             return eng
         return GpuEngine(spec.width, spec.height, qp=spec.qp, batch=batch, gop=spec.gop, search_range=spec.search_range,
                          deblock=spec.deblock, sao=spec.sao, seed=spec.seed, device=self.device, crf=spec.crf,
-                         bframes=spec.hevc_bframes(), **spec.tools())
+                         bframes=spec.hevc_bframes(), entropy=spec.entropy, **spec.tools())
 
     def get(self, spec: EncodeSpec):
         key = spec.engine_key()

@@ -11,4 +11,4 @@ run() {  # name, env...
   local rc=$?; echo "bench $n rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/bench_$n.log; return $rc; }
   python3 -c "import json; r=json.loads([l for l in open('$O/bench_$n.log') if l.startswith('{')][-1]); c=r['config']; print('$n', r['value'], c['per_rank_cpu'][0]['busy_cores'], c['last_step_gpu_ms'], c['step_ms'], c['entropy'])"
 }
-run base TV_X=0 && run sleep TV_ENT_SKIP=4 && run bigcode TV_ENT_SKIP=32 && run cus8 TV_ENT_CUS=8 && run cus16 TV_ENT_CUS=16 && run host1 TV_ENT_HOST=1 && run host2 TV_ENT_HOST=2 && run host4 TV_ENT_HOST=4
+run base TV_X=0 && run synthtok TV_ENT_SKIP=512
