@@ -207,36 +207,37 @@ class Core {
     // per-slot device + pinned host buffers: decisions | masks | offsets | totals | packed |
     // entropy head | entropy payload (device only: it lands in the host slot's packed region)
     slot_bytes(B, g_, gpu_ent_, slot_bytes_, slot_host_bytes_);
-    if (gpu_ent_) {  // per-core entropy scratch (the entropy stream codes one picture at a time)
+    if (gpu_ent_) {  // per-lane entropy scratch (each lane's stream codes one picture at a time)
       tok_cap_ = tok_capacity(B, g_);
-      {  // one allocation carved like ent_core_bytes()
-        uint8_t* q = nullptr;
-        dev_alloc(&q, ent_core_bytes(B, g_));
-        ent_.base = q;
-        ent_.regions = reinterpret_cast<uint32_t*>(q);
-        q += align(B * nctu_ * kEntRegion * 4);
-        ent_.tokens = reinterpret_cast<uint32_t*>(q);
-        q += align((tok_cap_ + kTokPad) * 4);
-        ent_.stage = q;
-        q += align(3 * tok_cap_ + 20 * B * g_.hc + 16);
-        ent_.ctb_cnt = reinterpret_cast<int*>(q);
-        q += align(B * nctu_ * 4);
-        ent_.ctb_off = reinterpret_cast<int*>(q);
-        q += align(B * nctu_ * 4);
-        ent_.seg_tok = reinterpret_cast<int*>(q);
-        q += align(B * 4);
-        ent_.wflag = reinterpret_cast<int*>(q);
-        q += align(B * g_.hc * 4);
-        ent_.wctx = q;
-      }
-      dev_alloc(&ent_.skip, B * g_.usz);
-      dev_alloc(&ent_.midx, B * g_.usz);
       EntropyTables* t = nullptr;
       dev_alloc(&t, sizeof(EntropyTables));
       std::unique_ptr<EntropyTables> ht(new EntropyTables());
       entropy_tables(*ht);
       HIP_OK(hipMemcpy(t, ht.get(), sizeof(EntropyTables), hipMemcpyHostToDevice));
-      ent_.tab = t;
+      for (int l = 0; l < ent_lanes(); ++l) {  // one allocation carved like ent_core_bytes()
+        EntScratch& e = ent_[l];
+        uint8_t* q = nullptr;
+        dev_alloc(&q, ent_core_bytes(B, g_));
+        e.base = q;
+        e.regions = reinterpret_cast<uint32_t*>(q);
+        q += align(B * nctu_ * kEntRegion * 4);
+        e.tokens = reinterpret_cast<uint32_t*>(q);
+        q += align((tok_cap_ + kTokPad) * 4);
+        e.stage = q;
+        q += align(3 * tok_cap_ + 20 * B * g_.hc + 16);
+        e.ctb_cnt = reinterpret_cast<int*>(q);
+        q += align(B * nctu_ * 4);
+        e.ctb_off = reinterpret_cast<int*>(q);
+        q += align(B * nctu_ * 4);
+        e.seg_tok = reinterpret_cast<int*>(q);
+        q += align(B * 4);
+        e.wflag = reinterpret_cast<int*>(q);
+        q += align(B * g_.hc * 4);
+        e.wctx = q;
+        dev_alloc(&e.skip, B * g_.usz);
+        dev_alloc(&e.midx, B * g_.usz);
+        e.tab = t;
+      }
       const char* dbg = getenv("TV_ENT_DEBUG");
       if (dbg && *dbg == '1') {
         dev_alloc(&ent_dbg_, 8 * sizeof(unsigned long long));
@@ -301,6 +302,9 @@ class Core {
   // entropy stream waits behind the latency-bound coder (measured: main-stream queues 36 %
   // busy).  Main streams first, then the entropy streams, gives each its own queue at 2 cores.
   void init_entropy_stream() {
+    for (int l = 0; l < ent_lanes(); ++l) init_entropy_lane(estream_[l]);
+  }
+  void init_entropy_lane(hipStream_t& estream_) {
     if (gpu_ent_ && !estream_) {
       const char* e = getenv("TV_ENT_CUS");  // experiment: entropy stream on every k-th CU
       const int k = e ? atoi(e) : 0;
@@ -331,7 +335,7 @@ class Core {
     const bool ge = gpu_entropy(c);
     long slot = 0, slot_host = 0;
     slot_bytes((long)B, g, ge, slot, slot_host);
-    const size_t ent = ge ? 2 * B * g.usz + ent_core_bytes((long)B, g) + sizeof(EntropyTables) : 0;
+    const size_t ent = ge ? env_lanes() * (2 * B * g.usz + ent_core_bytes((long)B, g)) + sizeof(EntropyTables) : 0;
     dev = set + ndpb * (set + B * 16 * g.psz + B * qsz) + ((c.deblock & 2) ? set : 0) + 2 * set +
           B * 3 * sizeof(unsigned long long) + B * nctu * sizeof(int) + 2 * B * nctu * 2 * sizeof(int16_t) +
           2 * B * nctu * sizeof(int) + (c.mgop > 1 ? 2 * B * nctu * sizeof(CtbMeOut) : 0) +
@@ -366,8 +370,9 @@ class Core {
     (void)hipFree(cmv_);
     (void)hipFree(ccost_);
     (void)hipFree(rc_);
-    for (void* p : {(void*)ent_.skip, (void*)ent_.midx, (void*)ent_.base, (void*)ent_.tab})
-      (void)hipFree(p);
+    if (ent_[0].tab) (void)hipFree(ent_[0].tab);
+    for (const EntScratch& e : ent_)
+      for (void* p : {(void*)e.skip, (void*)e.midx, (void*)e.base}) (void)hipFree(p);
     (void)hipHostFree(qhost_);
     (void)hipHostFree(quni_);
     for (int k = 0; k < nslots_; ++k) {
@@ -383,7 +388,9 @@ class Core {
     (void)hipEventDestroy(iev_[0]);
     (void)hipEventDestroy(iev_[1]);
     (void)hipStreamDestroy(istream_);
-    if (estream_) (void)hipStreamDestroy(estream_);
+    for (hipStream_t es : estream_)
+      if (es) (void)hipStreamDestroy(es);
+    if (dstream_) (void)hipStreamDestroy(dstream_);
     if (eev_) (void)hipEventDestroy(eev_);
   }
 
@@ -663,7 +670,8 @@ class Core {
     const int nal = write_slice_header(seq_, h.qp[b], seq_.mgop > 1 ? &refs_[f] : nullptr, pic.disp, pic.type == 2, hdr);
     finish_wpp_slice(hdr, ptrs.data(), sizes.data(), g_.hc, nal, slices_[b][f]);
   }
-  EntropyArgs entropy_args(const Slot& s, const DecisionSet& dec, const CodedPic& pic) const {
+  EntropyArgs entropy_args(const Slot& s, const DecisionSet& dec, const CodedPic& pic, int lane) const {
+    const EntScratch& ent = ent_[lane];
     EntropyArgs a{};
     a.g = g_;
     a.pic.type = pic.type;
@@ -678,18 +686,18 @@ class Core {
     a.cs = slot_compact(s);
     const Parts d = carve(s.dev);
     a.sao = seq_.sao ? d.sao : nullptr;
-    a.skip = ent_.skip;
-    a.midx = ent_.midx;
-    a.ctb_cnt = ent_.ctb_cnt;
-    a.regions = ent_.regions;
-    a.ctb_off = ent_.ctb_off;
-    a.seg_tok = ent_.seg_tok;
-    a.tokens = ent_.tokens;
+    a.skip = ent.skip;
+    a.midx = ent.midx;
+    a.ctb_cnt = ent.ctb_cnt;
+    a.regions = ent.regions;
+    a.ctb_off = ent.ctb_off;
+    a.seg_tok = ent.seg_tok;
+    a.tokens = ent.tokens;
     a.tok_cap = tok_cap_;
-    a.stage = ent_.stage;
-    a.wflag = ent_.wflag;
-    a.wctx = ent_.wctx;
-    a.tab = ent_.tab;
+    a.stage = ent.stage;
+    a.wflag = ent.wflag;
+    a.wctx = ent.wctx;
+    a.tab = ent.tab;
     a.status = d.ent_head;
     a.seg_bytes = d.ent_head + 4;
     a.row_bytes = d.ent_head + 4 + cfg_.batch;
@@ -703,8 +711,10 @@ class Core {
   }
 
   void fetch_slot(Slot& s, int B, int ptype) {
-    thread_local hipStream_t ws = nullptr;
-    if (!ws) HIP_OK(hipStreamCreateWithFlags(&ws, hipStreamNonBlocking));
+    // the core's D2H stream: used by its one fetch thread only, destroyed with the core (a
+    // thread_local stream outlived the engine and kept a hardware queue referenced)
+    if (!dstream_) HIP_OK(hipStreamCreateWithFlags(&dstream_, hipStreamNonBlocking));
+    hipStream_t ws = dstream_;
     wait_event(s.ev);
     const Parts d = carve(s.dev), h = carve(s.host);
     const long U = g_.usz;
@@ -873,17 +883,18 @@ class Core {
     }
     const bool use_gpu = gpu_ent_ && !on_host;
     if (use_gpu) {  // entropy coding on its own stream: the next picture's kernels run meanwhile
+      const int lane = f % ent_lanes();
       HIP_OK(hipEventRecord(eev_, stream_));
-      HIP_OK(hipStreamWaitEvent(estream_, eev_, 0));
+      HIP_OK(hipStreamWaitEvent(estream_[lane], eev_, 0));
       // binarisation on the core's entropy stream (one picture at a time: its scratch is per
       // core), the serial arithmetic coder on the slot's own stream, so the coders of the
       // pictures in flight overlap (each is a handful of latency-bound waves)
-      const EntropyArgs ea = entropy_args(s, dec, pic);
+      const EntropyArgs ea = entropy_args(s, dec, pic, lane);
       static const bool serial = [] {  // TV_ENT_SERIAL=1: entropy on the main stream (diagnostics)
         const char* e = getenv("TV_ENT_SERIAL");
         return e && *e == '1';
       }();
-      hipStream_t es = serial ? stream_ : estream_;
+      hipStream_t es = serial ? stream_ : estream_[lane];
       launch_entropy_bin(ea, B, es);
       launch_entropy_ac(ea, B, es);
       stage("entropy");
@@ -988,7 +999,18 @@ class Core {
   RcTables* rc_ = nullptr;
   // GPU entropy coding (k_entropy.hip): its own stream per core, per-core scratch
   bool gpu_ent_ = false;
-  hipStream_t estream_ = nullptr;
+  // entropy lanes: pictures alternate between lanes (own scratch + stream), so the coders of
+  // two pictures overlap (TV_ENT_LANES, default 2; textured content needed more than one)
+  static constexpr int kMaxEntLanes = 2;
+  static int env_lanes() {
+    const char* e = getenv("TV_ENT_LANES");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : (v > kMaxEntLanes ? kMaxEntLanes : v);
+  }
+  int ent_lanes_ = env_lanes();
+  int ent_lanes() const { return ent_lanes_; }
+  hipStream_t estream_[kMaxEntLanes] = {};
+  hipStream_t dstream_ = nullptr;  // D2H copies of host-coded slots (the fetch thread's)
   hipEvent_t eev_ = nullptr;
   struct EntScratch {
     uint8_t* skip = nullptr;
@@ -999,7 +1021,7 @@ class Core {
     int *ctb_cnt = nullptr, *ctb_off = nullptr, *seg_tok = nullptr, *wflag = nullptr;
     uint8_t* wctx = nullptr;
     EntropyTables* tab = nullptr;
-  } ent_;
+  } ent_[kMaxEntLanes];
   long tok_cap_ = 0, slot_host_bytes_ = 0;
   unsigned long long* ent_dbg_ = nullptr;  // TV_ENT_DEBUG=1: coder counters (EntropyArgs::dbg)
   std::atomic<long> ent_fallbacks_{0};
