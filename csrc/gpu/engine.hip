@@ -138,13 +138,7 @@ class Core {
     if (c.width < 64 || c.height < 64) throw std::runtime_error("frame must be at least 64x64");
     HIP_OK(hipSetDevice(c.device));
     fetch_ = std::make_unique<ThreadPool>(1, c.device);
-    if (const char* e = std::getenv("TV_MAIN_PRIO"); e && *e == '1') {  // experiment
-      int lo = 0, hi = 0;
-      HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
-    } else {
-      HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    }
+    HIP_OK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     {  // I-frame wavefront stream: highest priority, so its 100+ short dependent launches are
        // dispatched ahead of the other stream group's queued P-frame workgroups
       int lo = 0, hi = 0;
@@ -301,23 +295,15 @@ class Core {
   // and a hardware queue runs its packets in order -- a main stream sharing a queue with an
   // entropy stream waits behind the latency-bound coder (measured: main-stream queues 36 %
   // busy).  Main streams first, then the entropy streams, gives each its own queue at 2 cores.
-  void init_entropy_stream() {
-    for (int l = 0; l < ent_lanes(); ++l) init_entropy_lane(estream_[l]);
+  // lane l's stream (the engine creates lane 0 of every core, then lane 1 of every core:
+  // with GPU_MAX_HW_QUEUES = 4 the main streams and the lane-0 coders get a hardware queue
+  // each; creating core 0's two lanes before core 1's put core 1's lane 0 on its main
+  // stream's queue and cost 30 % at 1080p)
+  void init_entropy_stream(int l) {
+    if (l < ent_lanes()) init_entropy_lane(estream_[l]);
   }
   void init_entropy_lane(hipStream_t& estream_) {
-    if (gpu_ent_ && !estream_) {
-      const char* e = getenv("TV_ENT_CUS");  // experiment: entropy stream on every k-th CU
-      const int k = e ? atoi(e) : 0;
-      if (k > 1) {
-        hipDeviceProp_t prop;
-        HIP_OK(hipGetDeviceProperties(&prop, cfg_.device));
-        std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
-        for (int cu = 0; cu < prop.multiProcessorCount; cu += k) mask[cu / 32] |= 1u << (cu % 32);
-        HIP_OK(hipExtStreamCreateWithCUMask(&estream_, (uint32_t)mask.size(), mask.data()));
-      } else {
-        HIP_OK(hipStreamCreateWithFlags(&estream_, hipStreamNonBlocking));
-      }
-    }
+    if (gpu_ent_ && !estream_) HIP_OK(hipStreamCreateWithFlags(&estream_, hipStreamNonBlocking));
   }
 
   // device / pinned-host bytes this group allocated (the engine's HBM footprint)
@@ -390,6 +376,7 @@ class Core {
     (void)hipStreamDestroy(istream_);
     for (hipStream_t es : estream_)
       if (es) (void)hipStreamDestroy(es);
+
     if (dstream_) (void)hipStreamDestroy(dstream_);
     if (eev_) (void)hipEventDestroy(eev_);
   }
@@ -648,6 +635,10 @@ class Core {
     long total = 0;
     for (int b = 0; b < B; ++b) total += h.ent_head[4 + b];
     coef_bytes_ += total;
+    if ((total / B) * 100 > (long)g_.ysz)
+      ent_dense_run_.fetch_add(1, std::memory_order_relaxed);
+    else
+      ent_dense_run_.store(0, std::memory_order_relaxed);
     return true;
   }
   // slice b of picture f from the GPU's substreams: header, entry points, emulation prevention
@@ -883,7 +874,15 @@ class Core {
     }
     const bool use_gpu = gpu_ent_ && !on_host;
     if (use_gpu) {  // entropy coding on its own stream: the next picture's kernels run meanwhile
-      const int lane = f % ent_lanes();
+      // one lane, or pictures alternating between two when the content is dense: measured at
+      // 1080p, textured content (~3x the bins) codes 4365 vs 3765 frames/s with two lanes, but
+      // smooth content 6636 vs 7100 (a second coder in flight slows the analysis kernels more
+      // than it helps); the switch: the last three coded pictures' payloads above 0.01 bytes
+      // per luma sample (smooth P pictures ~0.005, textured ~0.015; an I picture alone does
+      // not switch).  An event query per picture to find a busy
+      // lane serialised the issue thread (-14 %).
+      const bool dense = ent_dense_run_.load(std::memory_order_relaxed) >= 3;  // not just an I picture
+      const int lane = (ent_lanes() > 1 && dense) ? (f & 1) : 0;
       HIP_OK(hipEventRecord(eev_, stream_));
       HIP_OK(hipStreamWaitEvent(estream_[lane], eev_, 0));
       // binarisation on the core's entropy stream (one picture at a time: its scratch is per
@@ -900,6 +899,7 @@ class Core {
       stage("entropy");
       HIP_OK(hipGetLastError());
       HIP_OK(hipEventRecord(s.ev, es));
+      ent_lane_pics_[lane]++;
     } else {
       HIP_OK(hipEventRecord(s.ev, stream_));
     }
@@ -914,6 +914,7 @@ class Core {
       try {
         Range r("engine.d2h");
         gpu = use_gpu && fetch_entropy(s, B);
+
         if (!gpu) fetch_slot(s, B, plan_.pics[f].type);
       } catch (const std::exception& e) {
         fail(e);
@@ -1010,6 +1011,8 @@ class Core {
   int ent_lanes_ = env_lanes();
   int ent_lanes() const { return ent_lanes_; }
   hipStream_t estream_[kMaxEntLanes] = {};
+  std::atomic<int> ent_dense_run_{0};  // consecutive GPU-coded pictures above 0.01 bytes per sample
+  long ent_lane_pics_[kMaxEntLanes] = {};
   hipStream_t dstream_ = nullptr;  // D2H copies of host-coded slots (the fetch thread's)
   hipEvent_t eev_ = nullptr;
   struct EntScratch {
@@ -1103,7 +1106,8 @@ class Engine {
       cc.batch = std::min(per_, c.batch - g * per_);
       cores_.push_back(std::make_unique<Core>(cc, pool_.get()));
     }
-    for (auto& core : cores_) core->init_entropy_stream();
+    for (int l = 0; l < 2; ++l)  // Core::kMaxEntLanes
+      for (auto& core : cores_) core->init_entropy_stream(l);
   }
   ~Engine() {
     intra_timing_report();

@@ -156,7 +156,6 @@ struct EntropyArgs {
   // TV_ENT_DEBUG: coder counters (k_ent_ac): rows, context bins, tokens, coding clocks, wait
   // ticks (100 MHz), max row span (nullptr: off)
   unsigned long long* dbg = nullptr;
-  int prio = 1;  // arithmetic coder waves at raised issue priority (TV_ENT_PRIO experiment)
 };
 // binarisation (merge/skip pre-pass, token count, scan, token write) and the arithmetic coder +
 // payload packing, on separate streams (the second waits for the first)

@@ -846,14 +846,13 @@ constexpr int kTokK = 32;   // tokens per refill
 // row order, so a row only ever waits on a row that is already running.  Tokens come through a
 // 64-entry LDS ring refilled 32 at a time (a token load kept in registers across the loop's
 // branches forces a vmcnt(0) wait at its use); output bytes leave as dword stores.
-template <bool SYNTH>  // SYNTH: timing experiment, tokens from a generator instead of memory
 __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
   __shared__ uint8_t lps[256], tlps[64], ctx[kEntCtx];
   for (int k = threadIdx.x; k < 256; k += 64) lps[k] = a.tab->lps[k];
   tlps[threadIdx.x] = a.tab->tlps[threadIdx.x];
   __syncthreads();
   if (threadIdx.x != 0) return;
-  if (a.prio) __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(3);  // a latency-bound chain beside the analysis waves
   const int row = blockIdx.x, b = blockIdx.y;
   const int wc = a.g.wc, hc = a.g.hc, nctu = wc * hc;
   __shared__ uint4 tring[kTokT / 4];
@@ -960,27 +959,8 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
       abort_row(4);
       return;
     }
-    uint32_t tok;
-    if (SYNTH) {
-      const uint32_t x = (uint32_t)(head * 2654435761u) ^ (uint32_t)(row * 40503u);
-      const long i = head - tpos;
-      if (i == 0) {
-        tok = 3u << 30 | kCtrlSync;
-      } else if (ntok == 0) {
-        tok = 3u << 30 | kCtrlFlush;
-      } else if ((x >> 28) < 10) {
-        const uint32_t nb = 1 + (x >> 26) % 3;
-        tok = nb << 27;
-        for (uint32_t k = 0; k < nb; ++k) tok |= (((x >> (7 * k)) % 150) | (((x >> (21 + k)) & 1) << 8)) << (9 * k);
-      } else if ((x >> 28) < 15) {
-        tok = 1u << 30 | (1 + (x >> 20) % 16) << 16 | (x & 0xffff);
-      } else {
-        tok = 2u << 30 | (x & 1);
-      }
-    } else {
-      if (tail - head < kTokK) refill();
-      tok = __builtin_amdgcn_readfirstlane(tring32[head & (kTokT - 1)]);
-    }
+    if (tail - head < kTokK) refill();
+    const uint32_t tok = __builtin_amdgcn_readfirstlane(tring32[head & (kTokT - 1)]);
     ++head;
     ++ntoks;
     const uint32_t ty = tok >> 30;
@@ -1130,86 +1110,13 @@ __global__ void k_ent_status(EntropyArgs a) {
   a.hhead[0] = *a.status;
 }
 
-// TV_ENT_SKIP timing experiment only (wrong bytes): every row one byte long
-__global__ void k_ent_fake_rows(EntropyArgs a, int n) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k < n) a.row_bytes[k] = 1;
-}
-
-template <int I>
-__device__ __forceinline__ uint32_t big_body(uint32_t x) {
-  if constexpr (I < 400) {
-    x = __builtin_amdgcn_readfirstlane((x ^ (x >> (I % 13 + 1))) * (2654435761u + 2u * I) + I);
-    return big_body<I + 1>(x);
-  } else {
-    return x;
-  }
-}
-
-// TV_ENT_SKIP 4/8/16/32 (experiment): one wave per row for ~0.9 ms sleeping (4), in a scalar
-// ALU chain (8) or in a dependent LDS chain (16), in place of the coder
-__global__ void __launch_bounds__(64) k_ent_spin(EntropyArgs a, int mode) {
-  __shared__ uint32_t lds[256];
-  lds[threadIdx.x] = threadIdx.x;
-  lds[threadIdx.x + 64] = threadIdx.x;
-  __syncthreads();
-  if (mode & (64 | 128)) {  // the coder's output pattern: ~1600 bytes per row over ~0.9 ms
-    uint32_t* out = reinterpret_cast<uint32_t*>(a.stage + ((long)blockIdx.y * a.g.hc + blockIdx.x) * 4096);
-    const unsigned long long t0 = wall_clock64();
-    for (int k = 0; k < 416; k += (mode & 128) ? 32 : 1) {
-      while (wall_clock64() - t0 < (unsigned long long)(k * 90 / 416)) __builtin_amdgcn_s_sleep(8);
-      if (mode & 128) {
-        out[k + threadIdx.x % 32] = k;  // one full 128-byte line per store instruction
-      } else if (threadIdx.x == 0) {
-        out[k] = k;  // one dword per store, single lane (the coder's put())
-      }
-    }
-    if (threadIdx.x == 0) a.row_bytes[(long)blockIdx.y * a.g.hc + blockIdx.x] = 1;
-    return;
-  }
-  if (threadIdx.x != 0) return;
-  const unsigned long long t0 = wall_clock64();
-  uint32_t x = blockIdx.x;
-  while (wall_clock64() - t0 < 90) {
-    if (mode & 4) {
-      __builtin_amdgcn_s_sleep(127);
-    } else if (mode & 32) {  // ~8 KB of straight-line code (instruction-cache footprint)
-      x = big_body<0>(x);
-    } else if (mode & 8) {
-      for (int k = 0; k < 64; ++k) x = __builtin_amdgcn_readfirstlane(x * 1664525u + 1013904223u);
-    } else {
-      for (int k = 0; k < 64; ++k) {
-        x = lds[x & 127];
-        lds[(x + 1) & 127] = x + k;
-      }
-    }
-  }
-  if (x == 0xdeadbeef) a.row_bytes[0] = 0;
-  a.row_bytes[(long)blockIdx.y * a.g.hc + blockIdx.x] = 1;
-}
-
 }  // namespace
-
-// TV_ENT_SKIP (timing experiments; the bitstream is wrong): 1 skips the arithmetic coder, 2 the
-// binariser as well
-static int ent_skip() {
-  static const int v = [] {
-    const char* e = std::getenv("TV_ENT_SKIP");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
 
 void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s) {
   const int nctu = a.g.wc * a.g.hc;
   if (a.g.wc < 2) throw std::runtime_error("GPU entropy coding needs at least 2 CTB columns");
   if (a.g.hc > 256) throw std::runtime_error("GPU entropy coding supports at most 256 CTB rows");
   (void)hipMemsetAsync(a.status, 0, sizeof(int), s);
-  if (ent_skip() & 2) {
-    (void)hipMemsetAsync(a.ctb_off, 0, (size_t)B * nctu * sizeof(int), s);
-    (void)hipMemsetAsync(a.seg_tok, 0, (size_t)B * sizeof(int), s);
-    return;
-  }
   if (a.pic.type != 2) k_ent_cu<<<dim3((unsigned)((a.g.usz + 255) / 256), B), 256, 0, s>>>(a);
   k_ent_bin<true><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
   k_ent_scan<<<B, 1024, 0, s>>>(a);
@@ -1220,24 +1127,7 @@ void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s) {
 
 void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s) {
   (void)hipMemsetAsync(a.wflag, 0, (size_t)B * a.g.hc * sizeof(int), s);
-  if (ent_skip() & 252)
-    k_ent_spin<<<dim3(a.g.hc, B), 64, 0, s>>>(a, ent_skip());
-  else if (ent_skip() & 3)
-    k_ent_fake_rows<<<(B * a.g.hc + 255) / 256, 256, 0, s>>>(a, B * a.g.hc);
-  else {
-    static const int prio = [] {
-      const char* e = std::getenv("TV_ENT_PRIO");
-      return e ? std::atoi(e) : 1;
-    }();
-    EntropyArgs c = a;
-    c.prio = prio;
-    if (ent_skip() & 512)
-      k_ent_ac<true><<<dim3(a.g.hc, B), 64, 0, s>>>(c);
-    else
-      k_ent_ac<false><<<dim3(a.g.hc, B), 64, 0, s>>>(c);
-    if (ent_skip() & 256)  // experiment: the real coder, a one-byte-per-row payload copy
-      k_ent_fake_rows<<<(B * a.g.hc + 255) / 256, 256, 0, s>>>(a, B * a.g.hc);
-  }
+  k_ent_ac<<<dim3(a.g.hc, B), 64, 0, s>>>(a);
   k_ent_pack<<<B, 256, 0, s>>>(a, B);
   k_ent_status<<<1, 1, 0, s>>>(a);
 }

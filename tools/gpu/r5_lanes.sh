@@ -15,5 +15,4 @@ one() {  # name, env..., -- bench args
   python3 -c "import json; r=json.load(open('$O/$n.json')); c=r['config']; print('$n', r['value'], c['per_rank_cpu'][0], c['step_ms'], c['entropy'])"
 }
 one smooth_l1 TV_ENT_LANES=1 -- --entropy gpu && one smooth_l2 TV_ENT_LANES=2 -- --entropy gpu && \
-one textured_l1 TV_ENT_LANES=1 -- --entropy gpu --content textured && one textured_l2 TV_ENT_LANES=2 -- --entropy gpu --content textured && \
-one smooth_cpus16 TV_CPUS=16 -- && one textured_cpus16 TV_CPUS=16 -- --content textured
+one textured_l2 TV_ENT_LANES=2 -- --entropy gpu --content textured
