@@ -647,6 +647,8 @@ void CpuEncoder::encode_frame(const uint8_t* const planes[3], const int strides[
         sum += idr ? rc_block_activity(qcur_.data() + (size_t)(8 * cy) * qw + 8 * cx, qw)
                    : (uint64_t)ccost[(size_t)cy * wc + cx];
     fc.qp = rc_crf_qp(cfg_.crf, idr, sum, wc * hc);
+  } else if (cfg_.cascade) {
+    fc.qp = clip3(0, 51, cfg_.qp + ippp_qp_offset(idr ? 0 : poc));
   }
   if (idr) {
     write_parameter_sets(cfg_, out);

@@ -281,6 +281,7 @@ class Core {
     seq_.wpp = (c.deblock & 4) != 0;
     seq_.rqt = !(c.deblock & 8);
     seq_.pintra = !(c.deblock & 16);
+    seq_.cascade = (c.deblock & 64) != 0;
     seq_.mgop = c.mgop;
     if (c.mgop > 1) {
       const GopPlan gp = plan_gop(2 * c.mgop + 1, c.mgop);
@@ -412,12 +413,12 @@ class Core {
   static long align(long n) { return (n + 255) & ~255L; }
   // WPP streams are entropy-coded on the GPU (k_entropy.hip) unless bit 5 asks for the host
   static bool gpu_entropy(const EngineCfg& c) { return (c.deblock & 4) && !(c.deblock & 32); }
-  // token capacity of the per-core entropy scratch: one token per luma sample of every
+  // token capacity of the per-core entropy scratch: half a token per luma sample of every
   // segment (the bench's textured I pictures use about a third of that); a picture that
   // needs more is coded by the host writer instead (status != 0)
   static long tok_capacity(long B, const Geo& g) {
     const char* e = getenv("TV_ENT_TOKENS_PER_PX");  // read per engine (tests shrink it)
-    const double per = e ? atof(e) : 1.0;
+    const double per = e ? atof(e) : 0.5;  // textured I pictures at QP 27 use ~0.33
     return (long)(per * B * g.ysz) + 1024;
   }
   static constexpr long kTokPad = 64;
@@ -754,11 +755,13 @@ class Core {
     for (size_t k = 0; k < plan_.pics.size(); ++k) refs_[k] = slice_refs(plan_.pics[k]);
     for (auto& e : dpb_) e.disp = -1;
     // per-picture QPs in coding order: the caller's base (display order) + the layer offset
-    qmap_given_ = qmap != nullptr || cfg_.mgop > 1;
+    // constant QP, I P P P, cascade on: per-picture QPs like an explicit map (CRF keeps its own)
+    const bool cascade = !qmap && seq_.cascade && cfg_.mgop <= 1 && cfg_.crf <= 0;
+    qmap_given_ = qmap != nullptr || cfg_.mgop > 1 || cascade;
     for (int k = 0; k < nframes; ++k)
       for (int b = 0; b < nseg; ++b) {
         const CodedPic& p = plan_.pics[k];
-        const int base = qmap ? qmap[b * nframes + p.disp] : cfg_.qp;
+        const int base = qmap ? qmap[b * nframes + p.disp] : cfg_.qp + (cascade ? ippp_qp_offset(p.disp) : 0);
         if (base < 0 || base > 51) throw std::runtime_error("slice QP out of range");
         qhost_[k * nseg + b] = (int8_t)clip3(0, 51, base + gop_layer_qp_offset(p.type, p.layer, cfg_.mgop));
       }

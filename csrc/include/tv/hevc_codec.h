@@ -46,17 +46,20 @@ struct SeqConfig {
   // residual quadtree: inter 32x32 CUs of P pictures may code four 16x16 TBs
   // (max_transform_hierarchy_depth_inter 1; hevc_defs.h rqt_split)
   bool rqt = true;
-  // Both change the bitstream: they are explicit configuration (the C API's flag bits 3 / 4,
+  // constant-QP I P P P: the low-delay QP cascade of tv/gop.h ippp_qp_offset
+  bool cascade = false;
+  // All three change the bitstream: they are explicit configuration (the C API's flag bits 3 / 4,
   // EncodeSpec.rqt / .pintra, part of the engine key and the checkpoint fingerprint), never
   // read from the environment here.
   // Flag bits of the C API's `deblock` argument: 1 deblocking, 2 SAO, 4 WPP, 8 no RQT,
-  // 16 no intra-in-P (32: GPU engine only, CABAC on the host)
+  // 16 no intra-in-P (32: GPU engine only, CABAC on the host), 64 I P P P QP cascade
   void set_flags(int f) {
     deblock = (f & 1) != 0;
     sao = (f & 2) != 0;
     wpp = (f & 4) != 0;
     rqt = !(f & 8);
     pintra = !(f & 16);
+    cascade = (f & 64) != 0;
   }
   int fps_num = 30, fps_den = 1;
   void finalize() {

@@ -60,7 +60,8 @@ def test_mp4_roundtrip():
 
 def test_write_frame_from_decisions_matches_encoder():
     frames = _frames(4, 2, 96, 64)
-    enc = hevc.CpuEncoder(96, 64, qp=27, search_range=16, wpp=False)  # write_frame: one substream
+    # write_frame: one substream, the frame at the sequence QP (no I P P P cascade)
+    enc = hevc.CpuEncoder(96, 64, qp=27, search_range=16, wpp=False, cascade=False)
     out = enc.encode(frames[0], True, 0)
     dec = enc.decisions()
     # re-run golden pass B from the decisions and entropy-code it separately

@@ -15,14 +15,16 @@ def _frames(n=4, w=128, h=96, seed=3):
 def test_engine_keys_differ_by_tool():
     base = EncodeSpec(640, 360)
     keys = {base.engine_key(), EncodeSpec(640, 360, rqt=False).engine_key(),
-            EncodeSpec(640, 360, pintra=False).engine_key(), EncodeSpec(640, 360, wpp=False).engine_key()}
-    assert len(keys) == 4
-    assert base.tools() == {"wpp": True, "rqt": True, "pintra": True}
+            EncodeSpec(640, 360, pintra=False).engine_key(), EncodeSpec(640, 360, wpp=False).engine_key(),
+            EncodeSpec(640, 360, cascade=False).engine_key()}
+    assert len(keys) == 5
+    assert base.tools() == {"wpp": True, "rqt": True, "pintra": True, "cascade": True}
 
 
 def test_codec_flags_bits():
     assert hevc.codec_flags() == 1 | 4
     assert hevc.codec_flags(deblock=False, sao=True, wpp=False, rqt=False, pintra=False) == 2 | 8 | 16
+    assert hevc.codec_flags(cascade=True) == 1 | 4 | 64
 
 
 def test_tools_change_the_stream_and_env_does_not(monkeypatch):
@@ -51,3 +53,21 @@ def test_wpp_default_keeps_reconstruction():
     for x, y in zip(ra, rb):
         np.testing.assert_array_equal(x[0], y[0])
     assert a != b
+
+
+def test_ippp_qp_cascade():
+    """Constant QP, I P P P: the IDR at QP - 5 and the P pictures +1 0 +1 -1 +1 0 +1 -3
+    (tv/gop.h); explicit per-frame QPs are not cascaded; the flat stream is the cascade off."""
+    fr = _frames(10)
+    kw = dict(qp=30, search_range=16)
+    casc, rc = hevc.encode_sequence_cpu(fr, **kw)
+    flat, rf = hevc.encode_sequence_cpu(fr, cascade=False, **kw)
+    assert casc != flat
+    offs = [-5] + [[1, 0, 1, -1, 1, 0, 1, -3][(i - 1) % 8] for i in range(1, 10)]
+    explicit, re_ = hevc.encode_sequence_cpu(fr, frame_qps=[30 + o for o in offs], cascade=False, **kw)
+    assert explicit == casc  # the cascade is exactly these slice QPs
+    mapped, _ = hevc.encode_sequence_cpu(fr, frame_qps=[30 + o for o in offs], **kw)
+    assert mapped == casc  # an explicit map is not cascaded a second time
+    for s in (casc, flat):
+        d = hevc.decode(s, coded=False)
+        assert len(d.frames) == len(fr)

@@ -35,6 +35,7 @@ class _FakeEngine:
 
 
 def test_engine_cache_evicts_by_bytes(monkeypatch):
+    monkeypatch.setenv("TV_ENTROPY", "host")  # footprints without the GPU coder's scratch
     cache = EngineCache(batch=0, max_engines=16, budget=64 * GiB)
     monkeypatch.setattr(cache, "_build", lambda spec, batch: _FakeEngine(spec, batch))
     hd = [EncodeSpec(1920, 1080, qp=q) for q in (22, 25, 27, 30, 32)]

@@ -39,10 +39,13 @@ def psnr_yuv(ref: Frame, dec: Frame) -> dict:
     return {"y": py, "u": pu, "v": pv, "yuv": (6 * py + pu + pv) / 8}
 
 
-def codec_flags(deblock: bool = True, sao: bool = False, wpp: bool = True, rqt: bool = True, pintra: bool = True) -> int:
+def codec_flags(deblock: bool = True, sao: bool = False, wpp: bool = True, rqt: bool = True, pintra: bool = True,
+                cascade: bool = False) -> int:
     """The native APIs' configuration bits (tv::SeqConfig::set_flags): 1 deblocking, 2 SAO,
-    4 WPP substreams, 8 no residual quadtree, 16 no intra CUs in P pictures."""
-    return int(bool(deblock)) | (2 if sao else 0) | (4 if wpp else 0) | (0 if rqt else 8) | (0 if pintra else 16)
+    4 WPP substreams, 8 no residual quadtree, 16 no intra CUs in P pictures, 64 the constant-QP
+    I P P P QP cascade (tv/gop.h ippp_qp_offset)."""
+    return (int(bool(deblock)) | (2 if sao else 0) | (4 if wpp else 0) | (0 if rqt else 8) | (0 if pintra else 16)
+            | (64 if cascade else 0))
 
 
 class CpuEncoder:
@@ -50,7 +53,7 @@ class CpuEncoder:
 
     def __init__(self, width: int, height: int, qp: int = 27, deblock: bool = True,
                  search_range: int = 64, max_merge: int = 5, sao: bool = False, crf: int = 0, wpp: bool = True,
-                 bframes: int = 1, rqt: bool = True, pintra: bool = True):
+                 bframes: int = 1, rqt: bool = True, pintra: bool = True, cascade: bool = True):
         """`wpp`: one CABAC substream per CTB row (entropy_coding_sync; the GPU engine's
         default, it codes them on the device); `rqt` / `pintra`: residual quadtree for inter
         CUs and intra 16x16 CUs in P pictures (coding tools; part of the bitstream identity)."""
@@ -66,16 +69,16 @@ class CpuEncoder:
             f = self.lib.tv_cpu_encoder_new_b
             f.restype = C.c_void_p
             f.argtypes = [C.c_int] * 7
-            self.h = f(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra), search_range, max_merge,
+            self.h = f(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade), search_range, max_merge,
                        self.bframes)
         elif crf:
             f = self.lib.tv_cpu_encoder_new_crf
             f.restype = C.c_void_p
             f.argtypes = [C.c_int] * 7
-            self.h = f(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra), search_range, max_merge,
+            self.h = f(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade), search_range, max_merge,
                        int(crf))
         else:
-            self.h = self.lib.tv_cpu_encoder_new(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra),
+            self.h = self.lib.tv_cpu_encoder_new(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade),
                                                  search_range, max_merge)
         if not self.h:
             raise ValueError(self.lib.tv_last_error().decode())
