@@ -413,12 +413,12 @@ class Core {
   static long align(long n) { return (n + 255) & ~255L; }
   // WPP streams are entropy-coded on the GPU (k_entropy.hip) unless bit 5 asks for the host
   static bool gpu_entropy(const EngineCfg& c) { return (c.deblock & 4) && !(c.deblock & 32); }
-  // token capacity of the per-core entropy scratch: half a token per luma sample of every
+  // token capacity of the per-core entropy scratch: one token per luma sample of every
   // segment (the bench's textured I pictures use about a third of that); a picture that
   // needs more is coded by the host writer instead (status != 0)
   static long tok_capacity(long B, const Geo& g) {
     const char* e = getenv("TV_ENT_TOKENS_PER_PX");  // read per engine (tests shrink it)
-    const double per = e ? atof(e) : 0.5;  // textured I pictures at QP 27 use ~0.33
+    const double per = e ? atof(e) : 1.0;  // textured I pictures at QP 22 use more than 0.5
     return (long)(per * B * g.ysz) + 1024;
   }
   static constexpr long kTokPad = 64;
