@@ -449,7 +449,7 @@ def av1_main(args) -> None:
     batch, sizing = _batch_for(args, local, "av1", w, h)
     if args.cpu:
         from thinvids_amd.models.cpu_engines import CpuAv1Engine as Av1GpuEngine  # noqa: F811
-    eng = Av1GpuEngine(w, h, batch=batch, qindex=q, device=local, threads=args.threads or None,
+    eng = Av1GpuEngine(w, h, batch=batch, qindex=q, device=local, threads=args.threads or None, cascade=args.cascade,
                        **({"seed": args.seed} if args.cpu else {}))
     post = _PostQueue(local, args.cpu)
     W, H = eng.W, eng.H

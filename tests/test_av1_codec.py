@@ -24,7 +24,7 @@ def _psnr_y(res, frames, w, h):
 @pytest.mark.parametrize("w,h,q", [(72, 40, 100), (128, 96, 60), (160, 90, 160)])
 def test_golden_stream_decodes_to_golden_recon(w, h, q):
     frames = _frames(3, w, h, 4)
-    res = av1.golden_encode(frames, w, h, q)
+    res = av1.golden_encode(frames, w, h, q, cascade=False)  # constant q: the PSNR floors below
     dec = av1.decode(res.stream)
     assert (dec.width, dec.height) == (w, h)
     assert dec.frames.shape[0] == 4
@@ -53,7 +53,7 @@ def test_skip_block_merging_on_static_content():
     w, h = 200, 136
     f0 = _frames(5, w, h, 1)[0]
     frames = [f0] * 4
-    res = av1.golden_encode(frames, w, h, 120)
+    res = av1.golden_encode(frames, w, h, 120, cascade=False)
     bsz = (res.mode[1:] >> 13) & 3
     assert (bsz == 2).any() and (bsz == 1).any()
     np.testing.assert_array_equal(av1.decode(res.stream).frames, res.recon)
@@ -312,3 +312,16 @@ def test_av1_two_pass_rate_control_gpu_engine(tmp_path, monkeypatch):
     r2 = run_job(src, str(tmp_path / "b.mp4"), gop=16, segment_frames=16, bitrate_kbps=target, codec="av1")
     assert r2["passes"] in (2, 3) and abs(r2["outputs"][0]["kbps"] / target - 1) < 0.05, (r2["outputs"], target)
     assert media.probe(str(tmp_path / "b.mp4"))["codec"] == "av1"
+
+
+def test_constant_q_cascade():
+    """Without a rate-control plan the key frame and the inter frames follow the low-delay
+    q cascade (the HEVC engine's, tv/gop.h), exactly an explicit per-frame q-index map."""
+    w, h, q = 96, 64, 100
+    frames = _frames(2, w, h, 9)
+    qm = av1.cascade_qmap(q, 9)
+    assert qm[0] < q and len(set(qm[1:])) > 1
+    casc = av1.golden_encode(frames, w, h, q)
+    assert casc.stream == av1.golden_encode(frames, w, h, q, qmap=qm).stream
+    assert casc.stream != av1.golden_encode(frames, w, h, q, cascade=False).stream
+    np.testing.assert_array_equal(av1.decode(casc.stream).frames, casc.recon)

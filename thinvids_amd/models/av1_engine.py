@@ -101,9 +101,10 @@ class Av1GpuEngine:
     """B segments x one GOP per call on one GPU; see module docstring."""
 
     def __init__(self, width: int, height: int, batch: int, qindex: int = 100, device: int = 0,
-                 threads: int | None = None):
+                 threads: int | None = None, cascade: bool = True):
         import torch
 
+        self.cascade = bool(cascade)  # constant q: the low-delay q cascade (av1.cascade_qmap)
         self.torch = torch
         self.w, self.h, self.B, self.q = width, height, batch, int(qindex)
         self.W, self.H = av1m.coded_size(width, height)
@@ -272,8 +273,11 @@ class Av1GpuEngine:
             raise ValueError(f"nseg {nseg} outside 1..{self.B}")
         self._alloc_gop(nframes)
         slot = self._use_slot()
-        qm = np.full((nframes, nseg), self.q, np.int32) if qmap is None else \
-            np.clip(np.asarray(qmap, np.int32).reshape(nframes, nseg), 1, 255)
+        if qmap is None:
+            col = av1m.cascade_qmap(self.q, nframes) if self.cascade else [self.q] * nframes
+            qm = np.repeat(np.asarray(col, np.int32)[:, None], nseg, axis=1)
+        else:
+            qm = np.clip(np.asarray(qmap, np.int32).reshape(nframes, nseg), 1, 255)
         lv = np.array([[[lf_level(int(x))] * 4 for x in row] for row in qm], np.int32)
         # pinned + non_blocking: a pageable upload would block the host on the previous
         # GOP's kernels (the stream drains before this GOP's first launch)

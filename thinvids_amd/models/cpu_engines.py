@@ -96,15 +96,16 @@ class CpuAv1Engine:
     loader callback instead)."""
 
     def __init__(self, width: int, height: int, batch: int, qindex: int = 100, threads: int | None = None, seed: int = 1,
-                 **_):
+                 cascade: bool = True, **_):
         self.w, self.h, self.B, self.q, self.seed = width, height, batch, int(qindex), seed
+        self.cascade = cascade
         self.W, self.H = av1m.coded_size(width, height)
         self.pool = cf.ThreadPoolExecutor(threads or 2)
         self.lr_enabled = True
 
     def _one(self, start: int, n: int, qm):
         frames = [hevc.synth_frame(self.seed, start + t, self.w, self.h) for t in range(n)]
-        r = av1m.golden_encode(frames, self.w, self.h, self.q, qmap=qm)
+        r = av1m.golden_encode(frames, self.w, self.h, self.q, qmap=qm, cascade=self.cascade)
         tus = av1m.split_temporal_units(r.stream, r.tu_sizes)
         W, H = self.W, self.H
         sse = []

@@ -59,7 +59,7 @@ class EncodeSpec:
 
     def engine_key(self):
         if self.codec == "av1":
-            return ("av1", self.width, self.height, self.av1_qindex())
+            return ("av1", self.width, self.height, self.av1_qindex(), self.cascade)
         return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed,
                 self.crf, self.hevc_bframes(), self.wpp, self.rqt, self.pintra, self.cascade, self.entropy)
 
@@ -198,7 +198,8 @@ class EngineCache:
         if spec.codec == "av1":
             from ..models.av1_engine import Av1GpuEngine
 
-            eng = Av1GpuEngine(spec.width, spec.height, batch=batch, qindex=spec.av1_qindex(), device=self.device)
+            eng = Av1GpuEngine(spec.width, spec.height, batch=batch, qindex=spec.av1_qindex(), device=self.device,
+                               cascade=spec.cascade)
             eng.batch = eng.B
             return eng
         return GpuEngine(spec.width, spec.height, qp=spec.qp, batch=batch, gop=spec.gop, search_range=spec.search_range,
@@ -368,7 +369,8 @@ def _encode_cpu(frames, spec: EncodeSpec, st: PartStats | None, fq=None) -> byte
         W, H = av1.coded_size(spec.width, spec.height)
         for a in range(0, len(frames), spec.gop):
             qm = None if fq is None else [av1.qindex_for_hevc_qp(int(x)) for x in fq[a:a + spec.gop]]
-            r = av1.golden_encode(frames[a:a + spec.gop], spec.width, spec.height, spec.av1_qindex(), qmap=qm)
+            r = av1.golden_encode(frames[a:a + spec.gop], spec.width, spec.height, spec.av1_qindex(), qmap=qm,
+                                  cascade=spec.cascade)
             bs += r.stream
             for f in r.recon:
                 recons.append((f[:W * H].reshape(H, W), f[W * H:W * H * 5 // 4].reshape(H // 2, W // 2),

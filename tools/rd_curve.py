@@ -40,7 +40,11 @@ def run_point(args):
         W, H = av1.coded_size(w, h)
         stream, ys = b"", []
         for s0 in range(0, len(frames), a["gop"]):
-            r = av1.golden_encode(frames[s0:s0 + a["gop"]], w, h, q)
+            n = min(a["gop"], len(frames) - s0)
+            qm = None
+            if fq is not None:  # a QP cascade in HEVC QP units, mapped to q-indices
+                qm = [av1.qindex_for_hevc_qp(x) for x in fq[s0:s0 + n]]
+            r = av1.golden_encode(frames[s0:s0 + a["gop"]], w, h, q, qmap=qm)
             stream += r.stream
             ys += [hevc.psnr(f[0], rec[:W * H].reshape(H, W)[:h, :w]) for f, rec in zip(frames[s0:], r.recon)]
     else:
