@@ -64,6 +64,7 @@ def test_ippp_qp_cascade():
     flat, rf = hevc.encode_sequence_cpu(fr, cascade=False, **kw)
     assert casc != flat
     offs = [-5] + [[1, 0, 1, -1, 1, 0, 1, -3][(i - 1) % 8] for i in range(1, 10)]
+    assert hevc.ippp_cascade_qps(30, 10) == [30 + o for o in offs]  # the Python mirror
     explicit, re_ = hevc.encode_sequence_cpu(fr, frame_qps=[30 + o for o in offs], cascade=False, **kw)
     assert explicit == casc  # the cascade is exactly these slice QPs
     mapped, _ = hevc.encode_sequence_cpu(fr, frame_qps=[30 + o for o in offs], **kw)

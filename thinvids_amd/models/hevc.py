@@ -48,6 +48,16 @@ def codec_flags(deblock: bool = True, sao: bool = False, wpp: bool = True, rqt: 
             | (64 if cascade else 0))
 
 
+IPPP_CASCADE_IDR = -5
+IPPP_CASCADE_P = (1, 0, 1, -1, 1, 0, 1, -3)
+
+
+def ippp_cascade_qps(qp: int, nframes: int) -> list[int]:
+    """Per-frame slice QPs of one constant-QP I P P P GOP under the cascade (mirror of tv/gop.h
+    ippp_qp_offset): what the engines code when no explicit map is given."""
+    return [max(0, min(51, qp + (IPPP_CASCADE_IDR if i == 0 else IPPP_CASCADE_P[(i - 1) % 8]))) for i in range(nframes)]
+
+
 class CpuEncoder:
     """Scalar C++ HEVC encoder (software path; reference `software_encode`)."""
 

@@ -417,8 +417,11 @@ def _encode_gpu(parts, spec: EncodeSpec, cache: EngineCache, stats, qps) -> list
             for i in range(0, len(items), eng.batch):
                 grp = items[i:i + eng.batch]
                 srcs = [x[2] for x in grp]
+                # segments without a plan keep the engine's constant-QP default (its I P P P cascade)
+                dflt = (np.asarray(hevc.ippp_cascade_qps(spec.qp, n)) if spec.cascade and spec.hevc_bframes() == 1
+                        and not spec.crf else np.full(n, spec.qp))
                 qmap = None if all(x[3] is None for x in grp) else \
-                    np.stack([x[3] if x[3] is not None else np.full(n, spec.qp) for x in grp])
+                    np.stack([x[3] if x[3] is not None else dflt for x in grp])
                 if all(isinstance(s, SynthRange) and s.seed == spec.seed and (s.width, s.height) == own_size
                        for s in srcs):
                     bits = eng.encode_synthetic([s.t0 for s in srcs], nframes=n, qp=qmap)
@@ -494,8 +497,10 @@ def _encode_gpu_av1(eng, chunks: dict, out: list, spec: EncodeSpec, dev, stats) 
 
             qmap = None
             if any(x[3] is not None for x in grp):  # rate-control plan: per-frame HEVC QP -> q-index
+                # segments without a plan keep the engine's constant-q default (its cascade)
+                base = (av1.cascade_qmap(spec.av1_qindex(), n) if spec.cascade else [spec.av1_qindex()] * n)
                 qmap = np.array([[av1.qindex_for_hevc_qp(int(x[3][t])) if x[3] is not None
-                                  else spec.av1_qindex() for x in grp] for t in range(n)], np.int32)
+                                  else base[t] for x in grp] for t in range(n)], np.int32)
             fut = eng.encode_gop(n, load, nseg=len(grp), qmap=qmap, async_host=True)
             if pending is not None:
                 to_writers(*pending)
