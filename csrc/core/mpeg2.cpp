@@ -11,7 +11,8 @@
 namespace tv::mpeg2 {
 const char* const kStatNames[kNumStats] = {
     "intra", "p_mc", "p_no_mc", "b_fwd", "b_bwd", "b_bi", "p_skipped", "b_skipped", "frame_mc", "field_mc_frame_pic",
-    "field_mc_field_pic", "mc_16x8", "field_dct", "escapes", "quant_changes", "intra_blocks", "inter_blocks"};
+    "field_mc_field_pic", "mc_16x8", "field_dct", "escapes", "quant_changes", "intra_blocks", "inter_blocks",
+    "concealed_slices"};
 
 namespace {
 
@@ -482,6 +483,7 @@ void predict(const PicInfo& pi, const Refs& rf, const Motion& m, int mbx, int mb
                     int cdy0) {
       // luma w x h at picture position (lx, ly) + mv, into rows dy0, dy0 + dstep, ...
       if (!im) fail("missing reference picture");
+      if (im->w < 16 || im->h < 32) fail("reference picture too small");
       uint8_t blk[256], cb[64], cr[64];
       mc(plane_view(*im, 0, parity), lx + (mvx >> 1), ly + (mvy >> 1), mvx & 1, mvy & 1, w, h, blk, w);
       const int cx = mvx / 2, cy = mvy / 2;
@@ -723,7 +725,11 @@ StreamIndex index_stream(const uint8_t* d, size_t n) {
       first_seq_open = false;
       PicInfo pi;
       Reader r(d, n, p + 4);
-      parse_picture_header(r, pi);
+      try {
+        parse_picture_header(r, pi);
+      } catch (const std::runtime_error&) {
+        continue;  // a damaged picture header: the decoder skips that picture too
+      }
       // the coding extension (before the first slice)
       for (size_t q = next_start_code(d, n, p + 4); q < n; q = next_start_code(d, n, q + 4)) {
         const uint8_t e = d[q + 3];
@@ -809,6 +815,13 @@ struct Decoder::Impl {
     if (!second) {
       if (cur_fields == 1) finish_frame();  // a lone field: finish what there is
       cur = new_image();
+      // concealment base: a slice lost to a bitstream error leaves the latest reference's
+      // samples there instead of grey
+      if (bwd && bwd->w == cur->w && bwd->h == cur->h) {
+        cur->y = bwd->y;
+        cur->u = bwd->u;
+        cur->v = bwd->v;
+      }
       cur_type = pi.type;
       cur_first_structure = pi.structure;
       cur_fields = 0;
@@ -990,6 +1003,7 @@ struct Decoder::Impl {
         inc += 33;
       }
       inc += r.vlc(tabs().mba);
+      if (addr + inc >= nmb) fail("macroblock address past the picture");
       if (!first && inc > 1) {
         for (int k = 1; k < inc; ++k) skipped_mb(addr + k, mbw);
       }
@@ -1002,6 +1016,8 @@ struct Decoder::Impl {
   }
 
   void put_mb(const uint8_t* py, const uint8_t* pu, const uint8_t* pv, int mbx, int mby) {
+    const int rows = pi.structure == 3 ? cur->h / 16 : cur->h / 32;
+    if (mbx >= cur->w / 16 || mby >= rows) fail("macroblock outside the picture buffer");
     Dest dd = mb_dest(*cur, pi, mbx, mby);
     for (int j = 0; j < 16; ++j) std::memcpy(dd.y + (size_t)j * dd.ys, py + j * 16, 16);
     for (int j = 0; j < 8; ++j) {
@@ -1163,27 +1179,44 @@ struct Decoder::Impl {
       if (c >= 0x01 && c <= 0xAF) {
         if (!in_picture) continue;
         if (!pic_started) begin_picture();
-        decode_slice(d, n, p);
+        try {
+          decode_slice(d, n, p);
+        } catch (const std::runtime_error&) {  // a damaged slice: conceal it, keep decoding
+          ++st[17];
+          if (!cur) throw;
+        }
         continue;
       }
       end_picture();
-      if (c == 0xB3) {
-        Reader r(d, n, p + 4);
-        parse_seq_header(r, seq);
-        have_seq = true;
-      } else if (c == 0xB5) {
-        Reader r(d, n, p + 4);
-        parse_extension(r, seq, in_picture ? &pi : nullptr);
-      } else if (c == 0xB8) {
+      try {
+        if (c == 0xB3) {
+          Reader r(d, n, p + 4);
+          SeqHeader sh = seq;
+          parse_seq_header(r, sh);
+          seq = sh;
+          have_seq = true;
+        } else if (c == 0xB5) {
+          Reader r(d, n, p + 4);
+          SeqHeader sh = seq;
+          PicInfo pc = pi;
+          parse_extension(r, sh, in_picture ? &pc : nullptr);
+          seq = sh;
+          pi = pc;
+        } else if (c == 0x00 && have_seq) {
+          Reader r(d, n, p + 4);
+          parse_picture_header(r, pi);
+          in_picture = true;
+        }
+      } catch (const std::runtime_error&) {  // a damaged header: skip it (and a picture's slices)
+        ++st[17];
+        if (c == 0x00) in_picture = false;
+        continue;
+      }
+      if (c == 0xB8) {
         Reader r(d, n, p + 4);
         r.skip(25);
         gop_closed = r.get(1);
         broken_link = r.get(1);
-      } else if (c == 0x00) {
-        if (!have_seq) continue;  // pictures before the first sequence header
-        Reader r(d, n, p + 4);
-        parse_picture_header(r, pi);
-        in_picture = true;
       } else if (c == 0xB7) {
         in_picture = false;
       }

@@ -61,7 +61,7 @@ struct StreamIndex {
 
 StreamIndex index_stream(const uint8_t* d, size_t n);
 
-constexpr int kNumStats = 17;
+constexpr int kNumStats = 18;
 extern const char* const kStatNames[kNumStats];
 
 class Decoder {

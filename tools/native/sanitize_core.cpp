@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "tv/container.h"
+#include "tv/mpeg2.h"
 
 extern "C" {
 const char* tv_last_error();
@@ -161,6 +162,51 @@ int main() {
     tv_av1_cdef_find_dirs(Y.data(), w, h, dir.data(), var.data());
     for (uint8_t d : dir)
       if (d > 7) return fail("cdef direction out of range");
+  }
+  // 5) MPEG-2: writer -> decoder round trip (frame and field pictures, open GOP), then
+  //    randomly damaged copies of the streams (bit flips, truncation) must decode or fail
+  //    cleanly -- a DVD source is untrusted input
+  {
+    const int W = 96, H = 64, N = 8;
+    std::vector<std::vector<uint8_t>> frames(N, std::vector<uint8_t>(W * H * 3 / 2));
+    for (int t = 0; t < N; ++t) {
+      uint8_t* f = frames[t].data();
+      tv_synth_frame(11, t, W, H, f, f + W * H, f + W * H * 5 / 4);
+    }
+    std::vector<const uint8_t*> ptrs;
+    for (auto& f : frames) ptrs.push_back(f.data());
+    for (int cfgi = 0; cfgi < 3; ++cfgi) {
+      tv::mpeg2::EncConfig c;
+      c.width = W;
+      c.height = H;
+      c.gop = 5;
+      c.interlaced = cfgi > 0;
+      c.field_pictures = cfgi == 2;
+      c.closed_gop = cfgi != 1;
+      c.vary_quant = true;
+      std::vector<tv::mpeg2::Image> rec;
+      const std::vector<uint8_t> es = tv::mpeg2::encode(c, ptrs, nullptr, nullptr, &rec);
+      int got = 0;
+      tv::mpeg2::Decoder dec;
+      dec.decode(es.data(), es.size(), 0, 0, 0, [&](int k, const tv::mpeg2::Image& im) {
+        if (std::memcmp(im.y.data(), rec[k].y.data(), (size_t)W * H) != 0) got = -1000;
+        ++got;
+        return true;
+      });
+      if (got != N) return fail("mpeg2 round trip");
+      for (int it = 0; it < 150; ++it) {
+        std::vector<uint8_t> d = es;
+        const int nflip = 1 + (int)(rnd() % 16);
+        for (int k = 0; k < nflip; ++k) d[rnd() % d.size()] ^= (uint8_t)(1 + rnd() % 255);
+        if (rnd() % 4 == 0) d.resize(rnd() % d.size());
+        try {
+          tv::mpeg2::index_stream(d.data(), d.size());
+          tv::mpeg2::Decoder dd;
+          dd.decode(d.data(), d.size(), 0, 0, 0, [](int, const tv::mpeg2::Image&) { return true; });
+        } catch (const std::exception&) {
+        }
+      }
+    }
   }
   std::puts("sanitize_core: ok");
   return 0;
