@@ -853,12 +853,17 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
   __syncthreads();
   if (threadIdx.x != 0) return;
   __builtin_amdgcn_s_setprio(3);  // a latency-bound chain beside the analysis waves
-  const int row = blockIdx.x, b = blockIdx.y;
+  const int b = blockIdx.y;
   const int wc = a.g.wc, hc = a.g.hc, nctu = wc * hc;
   __shared__ uint4 tring[kTokT / 4];
   const uint32_t* tring32 = reinterpret_cast<const uint32_t*>(tring);
   int* wflag = a.wflag + (long)b * hc;
   uint32_t* wctx = reinterpret_cast<uint32_t*>(a.wctx + (long)b * hc * kEntCtx);
+  // rows blockIdx.x, + gridDim.x, ...: fewer waves per picture than rows, so fewer of them sit
+  // resident waiting for the WPP diagonal.  With more than one row per wave, wave 0's second
+  // row waits on the last wave (dispatched after it): a picture's <= 256 waves are co-resident
+  // on 256 CUs as long as the analysis waves drain, and the wait times out into the host path.
+  auto code_row = [&](const int row) {
   if (*a.status) {  // the binariser gave up on this picture: the host codes it
     __hip_atomic_store(&wflag[row], 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -1061,8 +1066,9 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
       break;
     }
   }
+  };
+  for (int row = blockIdx.x; row < hc; row += gridDim.x) code_row(row);
 }
-
 // Slice b's rows back to back after slices 0..b-1, written straight into the pinned host slot
 // (device-visible): the head (sizes), the slice QP and the payload -- the host needs no copy.
 __global__ void __launch_bounds__(256) k_ent_pack(EntropyArgs a, int B) {
@@ -1126,8 +1132,14 @@ void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s) {
 }
 
 void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s) {
+  // TV_ENT_ROWS_PER_WAVE (1..8, default 1): substream rows coded by one wave, strided
+  static const int rpw = [] {
+    const char* e = std::getenv("TV_ENT_ROWS_PER_WAVE");
+    const int v = e ? std::atoi(e) : 1;
+    return v < 1 ? 1 : v > 8 ? 8 : v;
+  }();
   (void)hipMemsetAsync(a.wflag, 0, (size_t)B * a.g.hc * sizeof(int), s);
-  k_ent_ac<<<dim3(a.g.hc, B), 64, 0, s>>>(a);
+  k_ent_ac<<<dim3((a.g.hc + rpw - 1) / rpw, B), 64, 0, s>>>(a);
   k_ent_pack<<<B, 256, 0, s>>>(a, B);
   k_ent_status<<<1, 1, 0, s>>>(a);
 }
