@@ -1138,7 +1138,16 @@ class Engine {
   // device-to-device copies into each group's source planes, no PCIe crossing.  The
   // caller must have finished writing them (its stream synchronised) before the call.
   void encode_device(const uint8_t* frames, int nseg, int nframes, const int8_t* qmap) {
-    encode_mem(frames, nseg, nframes, qmap);
+    if (reinterpret_cast<uintptr_t>(frames) % 16) {  // the gather kernel reads uint4s
+      encode_mem(frames, nseg, nframes, qmap);
+      return;
+    }
+    run(nseg, nframes, qmap, [&](Core& core, int b0, int f, int B) {
+      const Geo& g = core.geo();
+      const long fsz = g.ysz + 2 * g.csz;
+      launch_gather_frames(frames + ((long)b0 * nframes + f) * fsz, (long)nframes * fsz, core.src(), g, B,
+                           core.stream());
+    });
   }
 
  private:

@@ -13,6 +13,10 @@
 //   and records the slot's event on the caller's stream.  With S = 2T slots every thread
 //   always has a free slot while its previous DMA is in flight, so the SDMA engine streams
 //   chunks back to back while the threads keep reading.
+//   Copies go to D = TV_INGEST_STREAMS (default 4) copy streams of their own, thread t on
+//   stream t % D, ordered after the caller's stream: one DMA queue moved ~23-25 GB/s, four
+//   ~28-31 GB/s (round 5, 1080p y4m job 4942 -> 5192-5282 frames/s).  D = 1 copies on the
+//   caller's stream.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <unistd.h>
@@ -22,6 +26,7 @@
 #include <cerrno>
 #include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -30,6 +35,32 @@
 
 namespace {
 thread_local std::string g_ingest_err;
+
+// per-device copy streams for TV_INGEST_STREAMS > 1 (created once, kept for the process)
+std::vector<hipStream_t>& copy_streams(int want) {
+  static std::mutex mu;
+  static std::vector<std::vector<hipStream_t>> per_dev;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(mu);
+  if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1);
+  auto& v = per_dev[dev];
+  while ((int)v.size() < want) {
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) break;
+    v.push_back(s);
+  }
+  return v;
+}
+
+int ingest_streams() {
+  static const int n = [] {
+    const char* e = std::getenv("TV_INGEST_STREAMS");
+    const int v = e ? std::atoi(e) : 4;
+    return std::max(1, std::min(8, v));
+  }();
+  return n;
+}
 
 int64_t pread_all(int fd, uint8_t* dst, int64_t n, int64_t off) {
   int64_t done = 0;
@@ -74,6 +105,18 @@ int tv_ingest_h2d(const char* path, long long offset, long long nbytes, void* ds
   }
   const int64_t nchunks = (nbytes + chunk - 1) / chunk;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<hipStream_t> cs(1, st);
+  if (ingest_streams() > 1) {  // copy streams start after the caller's stream (dst allocation)
+    const auto& v = copy_streams(ingest_streams());
+    if (!v.empty()) {
+      cs.assign(v.begin(), v.end());
+      hipEvent_t start;
+      (void)hipEventCreateWithFlags(&start, hipEventDisableTiming);
+      (void)hipEventRecord(start, st);
+      for (hipStream_t c : cs) (void)hipStreamWaitEvent(c, start, 0);
+      (void)hipEventDestroy(start);
+    }
+  }
   std::vector<hipEvent_t> ev(S);
   std::vector<char> used(S, 0);
   for (auto& e : ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -97,8 +140,9 @@ int tv_ingest_h2d(const char* path, long long offset, long long nbytes, void* ds
       if (got != n)
         return fail(std::string("pread ") + path + (got < 0 ? std::string(": ") + std::strerror((int)-got)
                                                              : std::string(": short read (file ends)")));
-      if (hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, slot, (size_t)n, hipMemcpyHostToDevice, st) != hipSuccess ||
-          hipEventRecord(ev[s], st) != hipSuccess)
+      hipStream_t q = cs[t % cs.size()];
+      if (hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, slot, (size_t)n, hipMemcpyHostToDevice, q) != hipSuccess ||
+          hipEventRecord(ev[s], q) != hipSuccess)
         return fail("hipMemcpyAsync / hipEventRecord failed");
       used[s] = 1;
     }
@@ -107,7 +151,11 @@ int tv_ingest_h2d(const char* path, long long offset, long long nbytes, void* ds
   for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
   work(0);
   for (auto& th : pool) th.join();
-  const hipError_t se = hipStreamSynchronize(st);  // the ring is reused by the next call
+  hipError_t se = hipSuccess;  // the ring is reused by the next call
+  for (hipStream_t c : cs) {
+    const hipError_t e = hipStreamSynchronize(c);
+    if (se == hipSuccess) se = e;
+  }
   for (auto& e : ev) (void)hipEventDestroy(e);
   ::close(fd);
   if (se != hipSuccess && !failed.load()) fail(std::string("hipStreamSynchronize: ") + hipGetErrorString(se));

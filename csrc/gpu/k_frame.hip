@@ -372,6 +372,26 @@ void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi,
   else
     k_synth<false><<<grid, 256, 0, s>>>(src, g, seed, fi);
 }
+// One picture of B device-resident segments ([segment][frame][Y | U | V] at the coded size,
+// segment stride seg_stride bytes) into the B source planes: one launch instead of 3 B
+// copyBuffer blits in front of every picture's analysis (the node job's file sources).
+__global__ void __launch_bounds__(256) k_gather_frames(const uint8_t* frames, long seg_stride, FrameSet src, Geo g,
+                                                       int B) {
+  const long f16 = (g.ysz + 2 * g.csz) / 16, y16 = g.ysz / 16, c16 = g.csz / 16;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < B * f16; i += (long)gridDim.x * 256) {
+    const int b = (int)(i / f16);
+    const long r = i - b * f16;
+    const uint4 v = reinterpret_cast<const uint4*>(frames + b * seg_stride)[r];
+    uint4* d = r < y16 ? reinterpret_cast<uint4*>(src.y + b * g.ysz) + r
+               : r < y16 + c16 ? reinterpret_cast<uint4*>(src.u + b * g.csz) + (r - y16)
+                               : reinterpret_cast<uint4*>(src.v + b * g.csz) + (r - y16 - c16);
+    *d = v;
+  }
+}
+void launch_gather_frames(const uint8_t* frames, long seg_stride, FrameSet src, const Geo& g, int B, hipStream_t s) {
+  const long n = B * (g.ysz + 2 * g.csz) / 16;
+  k_gather_frames<<<(unsigned)tv_min(4096L, (n + 255) / 256), 256, 0, s>>>(frames, seg_stride, src, g, B);
+}
 void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s) {
   dim3 grid((unsigned)tv_min(256, (int)((g.ysz / 4 + 4095) / 4096)), 3, B);
   k_sse<<<grid, 256, 0, s>>>(a, r, g, sse);
