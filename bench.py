@@ -384,7 +384,7 @@ def job_main(args) -> None:
                                   f"{dvd_info['kbps']} kbps ({dvd_info['unique']} unique frames repeated; written before the "
                                   "timed region); decoded on host threads, bwdif (k_bwdif) + HEVC on the GPU",
                    "source_gen_s": round(gen_s, 2), "job_mode": args.job_mode,
-                   "decode_threads_per_rank": os.environ.get("TV_DECODE_THREADS") or "auto (min(8, cpus))"}
+                   "decode_threads_per_rank": os.environ.get("TV_DECODE_THREADS") or "auto (min(16, cpus))"}
     if y4m:
         fb = w * h * 3 // 2
         cfg_src = {"source_file": f"y4m {w}x{h} 8-bit 4:2:0, {frames} frames, {round(frames * (fb + 6) / 1e9, 2)} GB "

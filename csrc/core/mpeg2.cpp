@@ -203,6 +203,7 @@ struct Tables {
   Lut mba, type[4], cbp, motion, dcl, dcc;
   CoefLut coef[2];
   double cosx[8][8];  // C(u)/2 cos((2x+1) u pi / 16)
+  float cosf[8][8];   // the same in single precision (inverse DCT)
   Tables() {
     mba.init(11);
     for (int i = 1; i <= 33; ++i) mba.add(kMba[i], i);
@@ -224,8 +225,10 @@ struct Tables {
     coef[0].build(false);
     coef[1].build(true);
     for (int u = 0; u < 8; ++u)
-      for (int x = 0; x < 8; ++x)
+      for (int x = 0; x < 8; ++x) {
         cosx[u][x] = (u == 0 ? std::sqrt(0.125) : 0.5) * std::cos((2 * x + 1) * u * M_PI / 16.0);
+        cosf[u][x] = (float)cosx[u][x];
+      }
   }
 };
 const Tables& tabs() {
@@ -313,9 +316,13 @@ size_t next_start_code(const uint8_t* d, size_t n, size_t p) {
 }
 
 // ---------------------------------------------------------------- pixel kernels --------
+// Separable inverse DCT in single precision (|coefficient| <= 2048: the float sums stay within
+// ~1e-3 of the exact transform, far inside the IEEE 1180 accuracy 13818-2 Annex A asks for),
+// all-zero rows skipped.  The writer's reconstruction uses this same function, so decoder
+// and writer agree sample for sample.
 void idct(const int32_t* F, int16_t* out) {
-  const auto& c = tabs().cosx;
-  double t[64];
+  const auto& c = tabs().cosf;
+  float t[64];
   int rows[8], nr = 0;  // rows with a coefficient (all-zero rows add exact zeros: skipped)
   for (int v = 0; v < 8; ++v) {
     const int32_t* r = F + v * 8;
@@ -323,22 +330,26 @@ void idct(const int32_t* F, int16_t* out) {
     for (int u = 0; u < 8; ++u) any |= r[u] != 0;
     if (!any) continue;
     rows[nr++] = v;
-    double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int u = 0; u < 8; ++u) {
       if (!r[u]) continue;  // exact: a zero coefficient adds zeros
-      const double f = r[u];
+      const float f = (float)r[u];
       for (int x = 0; x < 8; ++x) s[x] += c[u][x] * f;
     }
     for (int x = 0; x < 8; ++x) t[v * 8 + x] = s[x];
   }
+  if (nr == 0) {
+    std::memset(out, 0, 64 * sizeof(int16_t));
+    return;
+  }
   for (int y = 0; y < 8; ++y) {
-    double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // x innermost (vectorised); per element the
-    for (int k = 0; k < nr; ++k) {           // same ascending-row order of additions
-      const double cv = c[rows[k]][y];
-      const double* tr = t + rows[k] * 8;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // x innermost (vectorised); per element the
+    for (int k = 0; k < nr; ++k) {          // same ascending-row order of additions
+      const float cv = c[rows[k]][y];
+      const float* tr = t + rows[k] * 8;
       for (int x = 0; x < 8; ++x) s[x] += cv * tr[x];
     }
-    for (int x = 0; x < 8; ++x) out[y * 8 + x] = int16_t(std::clamp((int)std::floor(s[x] + 0.5), -256, 255));
+    for (int x = 0; x < 8; ++x) out[y * 8 + x] = int16_t(std::clamp((int)std::floor(s[x] + 0.5f), -256, 255));
   }
 }
 

@@ -478,11 +478,13 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     software = software or not gpu_available()
     synthetic = isinstance(src, media.SynthSource)
     deinterlace = bool(deinterlace) and not synthetic
-    # decoded sources (MPEG-2 / HEVC / AV1 files) spend the host on decoding: their WPP
-    # substreams are coded on the GPU; synthetic and y4m sources follow the CPU budget ("auto":
-    # a y4m job with the GPU coder measured 4559 vs 4949 frames/s with the host writer)
-    entropy = os.environ.get("TV_ENTROPY") or ("gpu" if not synthetic and not isinstance(src, media.Y4MSource)
-                                               else "auto")
+    # decoded sources (MPEG-2 / HEVC / AV1 files) spend the host on decoding: from 720p up
+    # their WPP substreams are coded on the GPU; smaller pictures (DVD 480i / 576i), synthetic
+    # and y4m sources follow the CPU budget ("auto").  A y4m job with the GPU coder measured
+    # 4559 vs 4949 frames/s with the host writer; at 480p the GPU coder's per-picture row
+    # chain (15 rows, ~3.4 ms per picture batch) bounded the DVD job (profiles/README.md).
+    decoded_src = not synthetic and not isinstance(src, media.Y4MSource)
+    entropy = os.environ.get("TV_ENTROPY") or ("gpu" if decoded_src and w0 * h0 >= 1280 * 720 else "auto")
     tff = bool(getattr(src, "top_field_first", True))
     fps = src.fps_num / src.fps_den
     abr = rc_mode == "abr" and bitrate_kbps > 0
@@ -595,7 +597,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     # decoded sources (MPEG-2 / HEVC / AV1 files): a claim's segments are decoded on parallel
     # host threads (each decode is one GOP range; the native decoders release the GIL)
     decoded = not synthetic and not isinstance(src, media.Y4MSource)
-    ndec = int(os.environ.get("TV_DECODE_THREADS", "0") or 0) or min(8, len(os.sched_getaffinity(0)))
+    ndec = int(os.environ.get("TV_DECODE_THREADS", "0") or 0) or min(16, len(os.sched_getaffinity(0)))
     dec_pool = cf.ThreadPoolExecutor(ndec) if decoded and ndec > 1 else None
 
     def preload(ids):
