@@ -168,3 +168,25 @@ def test_corrupt_streams_fail_cleanly():
     got = mpeg2.decode_es(bytes(bad), stats=st)
     assert len(got) == 6 and st["concealed_slices"] >= 1
     assert sum(np.array_equal(a[0], b[0]) for a, b in zip(rec, got)) >= 4
+
+
+def test_job_entropy_placement(tmp_path, monkeypatch):
+    """Node-job CABAC placement: decoded sources from 720p up on the GPU coder, DVD-size
+    decoded sources and y4m / synthetic sources by CPU budget (node_job.job_entropy)."""
+    from thinvids_amd.parallel.node_job import job_entropy
+
+    monkeypatch.delenv("TV_ENTROPY", raising=False)
+    es, _, _, _ = mpeg2.encode(_frames(4), bframes=0)
+    path = tmp_path / "clip.m2v"
+    path.write_bytes(es)
+    src = media.open_source(str(path))
+    assert job_entropy(src, 720, 480) == "auto"
+    assert job_entropy(src, 1920, 1080) == "gpu"
+    y4m = tmp_path / "clip.y4m"
+    with open(y4m, "wb") as f:
+        f.write(b"YUV4MPEG2 W96 H64 F30:1 Ip A1:1 C420jpeg\n")
+        for y, u, v in _frames(2):
+            f.write(b"FRAME\n" + y.tobytes() + u.tobytes() + v.tobytes())
+    assert job_entropy(media.open_source(str(y4m)), 1920, 1080) == "auto"
+    monkeypatch.setenv("TV_ENTROPY", "host")
+    assert job_entropy(src, 1920, 1080) == "host"

@@ -434,6 +434,23 @@ def _side_plan(input_path: str, audio_stream: int = 0):
         return None
 
 
+def job_entropy(src, width: int, height: int) -> str:
+    """Where a node job's WPP substreams are CABAC-coded (TV_ENTROPY overrides).  Decoded
+    sources (MPEG-2 / HEVC / AV1 files) spend the host on decoding: from 720p up they use the
+    GPU coder; smaller pictures (DVD 480i / 576i), synthetic and y4m sources follow the CPU
+    budget ("auto").  A y4m job with the GPU coder measured 4559 vs 4949 frames/s with the
+    host writer; at 480p the GPU coder's short per-picture row chain (15 rows, ~3.4 ms per
+    picture batch) bounded the DVD job at 955 frames/s against 1633 with the host writer
+    (profiles/README.md, round 5)."""
+    from ..models import media
+
+    env = os.environ.get("TV_ENTROPY")
+    if env:
+        return env
+    decoded = not isinstance(src, (media.SynthSource, media.Y4MSource))
+    return "gpu" if decoded and width * height >= 1280 * 720 else "auto"
+
+
 def run_job(input_path: str, output: str, height: int | None = None, qp: int = 27, gop: int = 64,
             segment_frames: int = 256, mode: str = "direct", bitrate_kbps: float = 0.0, ladder=None,
             search_range: int = 64, software: bool = False, batch_segments: int = 8,
@@ -478,13 +495,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
     software = software or not gpu_available()
     synthetic = isinstance(src, media.SynthSource)
     deinterlace = bool(deinterlace) and not synthetic
-    # decoded sources (MPEG-2 / HEVC / AV1 files) spend the host on decoding: from 720p up
-    # their WPP substreams are coded on the GPU; smaller pictures (DVD 480i / 576i), synthetic
-    # and y4m sources follow the CPU budget ("auto").  A y4m job with the GPU coder measured
-    # 4559 vs 4949 frames/s with the host writer; at 480p the GPU coder's per-picture row
-    # chain (15 rows, ~3.4 ms per picture batch) bounded the DVD job (profiles/README.md).
-    decoded_src = not synthetic and not isinstance(src, media.Y4MSource)
-    entropy = os.environ.get("TV_ENTROPY") or ("gpu" if decoded_src and w0 * h0 >= 1280 * 720 else "auto")
+    entropy = job_entropy(src, w0, h0)
     tff = bool(getattr(src, "top_field_first", True))
     fps = src.fps_num / src.fps_den
     abr = rc_mode == "abr" and bitrate_kbps > 0
