@@ -33,6 +33,22 @@ __global__ void __launch_bounds__(256) k_pad_plane(const uint8_t* __restrict__ s
     if (x0 + k < pw) D[x0 + k] = S[tv_min(x0 + k, sw - 1)];
 }
 
+// 8x8 block means of n luma planes (scene-cut thumbnails, models/scenecut.py): one thread per
+// block, straight from the 8- or 16-bit samples (the sum of 64 samples and the / 64 are exact
+// in float, so any summation order gives the same value; 10-bit samples are scaled by 1/4).
+template <typename T>
+__global__ void __launch_bounds__(256) k_thumbs8(const T* __restrict__ y, int tw, int stride, long fs, float* out,
+                                                 float scale) {
+  const int x = blockIdx.x * 256 + threadIdx.x, r = blockIdx.y, f = blockIdx.z;
+  if (x >= tw) return;
+  const T* p = y + (long)f * fs + (long)(8 * r) * stride + 8 * x;
+  unsigned s = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += p[(long)j * stride + i];
+  out[((long)f * gridDim.y + r) * tw + x] = (float)s * scale / 64.0f;
+}
 }  // namespace gpu
 }  // namespace tv
 
@@ -48,6 +64,23 @@ int stage_status() {
 
 extern "C" {
 const char* tv_stage_last_error() { return g_stage_err.c_str(); }
+
+// 8x8 block means of n luma planes (element offsets / strides; bits 8 or 10) -> out
+// [n][h / 8][w / 8] float
+int tv_thumbs8_batch(const void* y, int bits, int w, int h, int stride, long fs, int n, float* out, void* stream) {
+  const int tw = w / 8, th = h / 8;
+  if (tw <= 0 || th <= 0 || th > 65535 || n <= 0 || n > 65535 || stride < w) {
+    g_stage_err = "tv_thumbs8_batch: bad geometry";
+    return -1;
+  }
+  const dim3 grid((unsigned)((tw + 255) / 256), (unsigned)th, (unsigned)n);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (bits > 8)
+    tv::gpu::k_thumbs8<uint16_t><<<grid, 256, 0, st>>>(static_cast<const uint16_t*>(y), tw, stride, fs, out, 0.25f);
+  else
+    tv::gpu::k_thumbs8<uint8_t><<<grid, 256, 0, st>>>(static_cast<const uint8_t*>(y), tw, stride, fs, out, 1.0f);
+  return stage_status();
+}
 
 // n frames of one plane: display (sw x sh, row stride sstride, frame stride sfs) -> coded
 // (pw x ph, row stride dstride, frame stride dfs) with edge replication

@@ -60,3 +60,28 @@ def test_scenecut_idr_gpu_matches_cpu():
     g = encode_parts([frames], EncodeSpec(192, 128, **spec))[0]
     c = encode_parts([frames], EncodeSpec(192, 128, software=True, **spec))[0]
     assert g == c
+
+
+@pytest.mark.gpu
+def test_device_thumbnails_equal_host():
+    """k_thumbs8 (csrc/gpu/k_stage.hip) against the numpy 8x8 means (exact), 8-bit and
+    10-bit, whole buffers and a view at an offset; d(t) equal to the host's up to the order
+    of the final mean."""
+    import torch
+
+    from thinvids_amd.ops import stage
+
+    frames = _clip(n=6, cut=3, w=136, h=72)
+    dev = stage.upload_frames(frames, torch.device("cuda", 0))
+    close = lambda a, b: np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5)  # noqa: E731 (mean order)
+    close(scenecut.diffs_device(dev), scenecut.diffs_host(frames))
+    f10 = [tuple((p.astype(np.uint16) * 4 + (p & 3)) for p in f) for f in frames]
+    d10 = stage.upload_frames(f10, torch.device("cuda", 0))
+    close(scenecut.diffs_device(d10), scenecut.diffs_host(f10))
+    # planes at an offset into the buffer: a view one frame in
+    close(scenecut.diffs_device(dev.select(1, 5)), scenecut.diffs_host(frames[1:]))
+    # the thumbnails themselves
+    t = torch.empty((6, 9, 17), dtype=torch.float32, device="cuda")
+    off, w, h, stride, fs = dev.planes[0]
+    stage.thumbs8(dev.ptr(0), 8, w, h, stride, fs, 6, t)
+    np.testing.assert_array_equal(t.cpu().numpy(), scenecut.thumbs_host(frames))

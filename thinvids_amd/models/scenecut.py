@@ -38,19 +38,20 @@ def thumbs_host(frames) -> np.ndarray:
 
 def diffs_device(dev_frames) -> np.ndarray:
     """d(t) for t = 1..n-1 of a :class:`~thinvids_amd.ops.stage.DevFrames`, computed on its
-    device: only n - 1 floats come back."""
+    device: the 8x8 thumbnails come from one HIP kernel straight from the samples
+    (csrc/gpu/k_stage.hip k_thumbs8; a float copy of every luma plane + avg_pool2d cost ~5 %
+    of a y4m job's GPU time), only n - 1 floats come back."""
     import torch
-    import torch.nn.functional as F
+
+    from ..ops import stage
 
     off, w, h, stride, fs = dev_frames.planes[0]
     n = dev_frames.n
     if n < 2:
         return np.zeros(0, np.float32)
-    flat = dev_frames.buf.reshape(-1)
-    y = torch.as_strided(flat, (n, h // 8 * 8, w // 8 * 8), (fs, stride, 1), off).float()
-    if dev_frames.bits == 10:
-        y = y / 4.0
-    t = F.avg_pool2d(y.unsqueeze(1), 8).squeeze(1)
+    tw, th = w // 8, h // 8
+    t = torch.empty((n, th, tw), dtype=torch.float32, device=dev_frames.buf.device)
+    stage.thumbs8(dev_frames.ptr(0), dev_frames.bits, w, h, stride, fs, n, t)
     return (t[1:] - t[:-1]).abs().mean(dim=(1, 2)).cpu().numpy()
 
 

@@ -37,6 +37,7 @@ def _lib():
                                         vp, vp, ci, vp, vp, ci, vp, ci, ci, ci, vp]
         lib.tv_tonemap_pq_batch.argtypes = [vp, vp, ci, ci, ci, vp, C.c_float, C.c_float, vp]
         lib.tv_ops_last_error.restype = C.c_char_p
+        lib.tv_thumbs8_batch.argtypes = [vp, ci, ci, ci, ci, cl, ci, vp, vp]
         lib._stage_sigs = True
     return lib
 
@@ -101,6 +102,15 @@ def from_flat(t, w: int, h: int, n: int | None = None, bits: int = 8) -> DevFram
     segment) — no copy."""
     n = n if n is not None else t.shape[0]
     return DevFrames(t, n, w, h, flat_layout(w, h), bits)
+
+
+def thumbs8(ptr: int, bits: int, w: int, h: int, stride: int, fs: int, n: int, out) -> None:
+    """8x8 block means of n luma planes at device address `ptr` (element strides) into the
+    float32 CUDA tensor `out` [n][h // 8][w // 8], on the current stream."""
+    import torch
+
+    st = C.c_void_p(torch.cuda.current_stream(out.device).cuda_stream)
+    _ok(_lib().tv_thumbs8_batch(C.c_void_p(ptr), bits, w, h, stride, fs, n, C.c_void_p(out.data_ptr()), st))
 
 
 def upload_frames(frames, device) -> DevFrames:
