@@ -118,3 +118,27 @@ def test_write_synth_y4m_matches_host_generator(tmp_path):
     for t, f in enumerate(src.read(0, 5)):
         want = hevc.synth_frame(3, t, 160, 90)
         assert all(np.array_equal(a, b) for a, b in zip(f, want)), t
+
+
+@pytest.mark.gpu
+def test_read_y4m_device_many_chunks_over_copy_streams(tmp_path):
+    """A range of several 32 MiB ring chunks: each reader thread's chunks go to its own DMA
+    stream (TV_INGEST_STREAMS, default 4), all ordered after the caller's stream."""
+    import torch
+
+    from thinvids_amd.models import media
+    from thinvids_amd.ops import stage
+
+    rng = np.random.default_rng(9)
+    w, h, n = 1920, 1080, 44  # ~137 MB: 5 chunks
+    frames = [tuple(rng.integers(0, 256, s, dtype=np.uint8) for s in ((h, w), (h // 2, w // 2), (h // 2, w // 2)))
+              for _ in range(n)]
+    p = str(tmp_path / "big.y4m")
+    media.write_y4m(p, frames, 30, 1)
+    src = media.Y4MSource(p)
+    d = stage.read_y4m_device(src, 2, n - 3, torch.device("cuda", 0), threads=4)
+    flat = d.buf.reshape(-1)
+    for c in range(3):
+        off, pw, ph, stride, fs = d.planes[c]
+        got = torch.as_strided(flat, (n - 3, ph, pw), (fs, stride, 1), off).cpu().numpy()
+        assert np.array_equal(got, np.stack([f[c] for f in frames[2:n - 1]])), c
