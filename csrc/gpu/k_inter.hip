@@ -42,7 +42,11 @@ namespace gpu {
 //                the phase planes and the bottom-up CU split decision.  Rate = MVD bits
 //                against the CTB predictor.
 // ---------------------------------------------------------------------------------------
-constexpr int kMeThreads = 256;
+#ifndef TV_ME_THREADS
+#define TV_ME_THREADS 256
+#endif
+constexpr int kMeThreads = TV_ME_THREADS;  // a multiple of 64 (the DPP group sums assume it)
+static_assert(kMeThreads % 64 == 0 && kMeThreads >= 256, "k_inter_me block size");
 constexpr int kFRows = kCtb + kMeWinH - 1;  // 38 window rows per candidate
 constexpr int kFWords = 12;                 // 48 bytes staged (40 used: 32 + 7 offsets + 1)
 constexpr int kFChunks = kFWords / 4;       // 16-byte chunks per staged row
