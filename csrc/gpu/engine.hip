@@ -387,6 +387,7 @@ class Core {
   long coef_bytes() const { return coef_bytes_; }
   long ent_fallbacks() const { return ent_fallbacks_; }
   long ent_host_pictures() const { return ent_host_pics_; }
+  long ent_lane_pictures(int l) const { return (l >= 0 && l < kMaxEntLanes) ? ent_lane_pics_[l] : 0; }
   int host_share() const { return host_share_; }
   static std::atomic<int>& host_inflight() {  // pictures in the (process-wide) host writer pool
     static std::atomic<int> n{0};
@@ -412,7 +413,13 @@ class Core {
   }
   static long align(long n) { return (n + 255) & ~255L; }
   // WPP streams are entropy-coded on the GPU (k_entropy.hip) unless bit 5 asks for the host
-  static bool gpu_entropy(const EngineCfg& c) { return (c.deblock & 4) && !(c.deblock & 32); }
+  // WPP on, not forced to the host, and a geometry the coder handles (>= 2 CTB columns for the
+  // 9.3.2.4 storage after CTB 1, <= 256 rows): anything else uses the host writer from the start
+  static bool gpu_entropy(const EngineCfg& c) {
+    if (!((c.deblock & 4) && !(c.deblock & 32))) return false;
+    const Geo g = make_geo(c.width, c.height);
+    return g.wc >= 2 && g.hc <= 256;
+  }
   // token capacity of the per-core entropy scratch: one token per luma sample of every
   // segment (the bench's textured I pictures use about a third of that); a picture that
   // needs more is coded by the host writer instead (status != 0)
@@ -761,8 +768,11 @@ class Core {
     for (int k = 0; k < nframes; ++k)
       for (int b = 0; b < nseg; ++b) {
         const CodedPic& p = plan_.pics[k];
-        const int base = qmap ? qmap[b * nframes + p.disp] : cfg_.qp + (cascade ? ippp_qp_offset(p.disp) : 0);
-        if (base < 0 || base > 51) throw std::runtime_error("slice QP out of range");
+        // only the caller's QP is range-checked; the cascade / layer offsets clip (as the golden
+        // encoder does, cpu_encoder.cpp), so QP 0..4 and 51 keep working with the cascade on
+        const int q0 = qmap ? qmap[b * nframes + p.disp] : cfg_.qp;
+        if (q0 < 0 || q0 > 51) throw std::runtime_error("slice QP out of range");
+        const int base = q0 + (cascade ? ippp_qp_offset(p.disp) : 0);
         qhost_[k * nseg + b] = (int8_t)clip3(0, 51, base + gop_layer_qp_offset(p.type, p.layer, cfg_.mgop));
       }
     last_frames_ = nframes;
@@ -884,7 +894,7 @@ class Core {
       // per luma sample (smooth P pictures ~0.005, textured ~0.015; an I picture alone does
       // not switch).  An event query per picture to find a busy
       // lane serialised the issue thread (-14 %).
-      const bool dense = ent_dense_run_.load(std::memory_order_relaxed) >= 3;  // not just an I picture
+      const bool dense = ent_dense_run_.load(std::memory_order_relaxed) >= dense_after();  // not just an I picture
       const int lane = (ent_lanes() > 1 && dense) ? (f & 1) : 0;
       HIP_OK(hipEventRecord(eev_, stream_));
       HIP_OK(hipStreamWaitEvent(estream_[lane], eev_, 0));
@@ -921,6 +931,8 @@ class Core {
         if (!gpu) fetch_slot(s, B, plan_.pics[f].type);
       } catch (const std::exception& e) {
         fail(e);
+        if (s.host_coded.exchange(0, std::memory_order_relaxed))  // hand back its host-writer share
+          host_inflight().fetch_sub(1, std::memory_order_relaxed);
         release(s, B + 1);
         return;
       }
@@ -1012,6 +1024,13 @@ class Core {
     return v < 1 ? 1 : (v > kMaxEntLanes ? kMaxEntLanes : v);
   }
   int ent_lanes_ = env_lanes();
+  // TV_ENT_DENSE_AFTER (default 3): consecutive dense pictures before the second lane is used
+  // (0: alternate lanes from the first picture -- the tests' way into the two-lane path)
+  int dense_after_ = [] {  // read per engine (tests set it)
+    const char* e = getenv("TV_ENT_DENSE_AFTER");
+    return e ? std::max(0, atoi(e)) : 3;
+  }();
+  int dense_after() const { return dense_after_; }
   int ent_lanes() const { return ent_lanes_; }
   hipStream_t estream_[kMaxEntLanes] = {};
   std::atomic<int> ent_dense_run_{0};  // consecutive GPU-coded pictures above 0.01 bytes per sample
@@ -1198,6 +1217,11 @@ class Engine {
     for (const auto& c : cores_) n += c->ent_host_pictures();
     return n;
   }
+  long entropy_lane_pictures(int l) const {
+    long n = 0;
+    for (const auto& c : cores_) n += c->ent_lane_pictures(l);
+    return n;
+  }
   const Geo& geo() const { return cores_[0]->geo(); }
   size_t dev_bytes() const {
     size_t n = 0;
@@ -1357,6 +1381,10 @@ void tv_engine_entropy_stats(void* e, int* on, long long* fallbacks, int* status
 // pictures the hybrid policy (TV_ENT_HOST) sent to the host writer since construction
 long long tv_engine_entropy_host_pictures(void* e) {
   return static_cast<tv::gpu::Engine*>(e)->entropy_host_pictures();
+}
+// pictures GPU coder lane l coded since construction (lane 1 only on dense content)
+long long tv_engine_entropy_lane_pictures(void* e, int lane) {
+  return static_cast<tv::gpu::Engine*>(e)->entropy_lane_pictures(lane);
 }
 // The same for an engine not built yet (same arguments as tv_engine_new_b's geometry part)
 int tv_engine_estimate(int width, int height, int batch, int gop, int deblock, int mgop, unsigned long long* dev,

@@ -48,6 +48,18 @@ def test_gpu_entropy_equals_host_writer(w, h, qp, sao, extra):
     eng.close()
 
 
+@pytest.mark.parametrize("qp", [0, 3, 51])
+def test_cascade_edge_qps_clip_like_the_golden_encoder(qp):
+    """Constant QP with the I P P P cascade at the ends of the range: the IDR's -5 and the
+    P pictures' +1 clip to 0..51 (as cpu_encoder.cpp does) instead of failing the encode."""
+    w, h, gop, rng, seed = 128, 96, 9, 16, 5
+    for ent in ("gpu", "host"):
+        eng = _engine(width=w, height=h, qp=qp, batch=2, gop=gop, search_range=rng, seed=seed, entropy=ent)
+        segs = eng.encode_synthetic([0, 10])
+        eng.close()
+        assert segs == _golden(seed, [0, 10], w, h, gop, qp=qp, search_range=rng), ent
+
+
 def test_gpu_entropy_equals_host_entropy_same_engine_config():
     """entropy="host" (the C++ writer on the engine's thread pool, WPP) and "gpu" give the
     same bytes at the bench geometry's width (60 CTB columns) on textured content."""
@@ -108,6 +120,26 @@ def test_gpu_entropy_capacity_fallback(monkeypatch):
     assert segs == gold
     eng.close()
     assert st["gpu"] and st["fallbacks"] > 0 and st["status"] & 1, st
+
+
+def test_two_coder_lanes_dense_routing_is_byte_identical(monkeypatch):
+    """The second coder lane (pictures alternate between two entropy streams and their
+    scratch once the content is dense): forced from the first picture with
+    TV_ENT_DENSE_AFTER=0 on textured content, the stream equals the host writer's and the
+    golden encoder's, and both lanes coded pictures."""
+    monkeypatch.setenv("TV_ENT_LANES", "2")
+    monkeypatch.setenv("TV_ENT_DENSE_AFTER", "0")
+    w, h, gop, rng = 256, 160, 8, 16
+    seed = 11 | 0x80000000
+    eng = _engine(width=w, height=h, qp=22, batch=3, gop=gop, search_range=rng, seed=seed, sao=True)
+    segs = eng.encode_synthetic([0, 9, 30])
+    st = eng.entropy_stats()
+    eng.close()
+    assert st["fallbacks"] == 0 and min(st["lane_pictures"]) > 0, st
+    host = _engine(width=w, height=h, qp=22, batch=3, gop=gop, search_range=rng, seed=seed, sao=True, entropy="host")
+    assert segs == host.encode_synthetic([0, 9, 30])
+    host.close()
+    assert segs == _golden(seed, [0, 9, 30], w, h, gop, qp=22, search_range=rng, sao=True)
 
 
 def test_hybrid_entropy_routes_pictures_to_the_host(monkeypatch):

@@ -226,8 +226,10 @@ class GpuEngine:
         f(self.h, C.byref(on), C.byref(fb), C.byref(st))
         hp = self.lib.tv_engine_entropy_host_pictures
         hp.argtypes, hp.restype = [C.c_void_p], C.c_longlong
+        lp = self.lib.tv_engine_entropy_lane_pictures
+        lp.argtypes, lp.restype = [C.c_void_p, C.c_int], C.c_longlong
         return {"gpu": bool(on.value), "fallbacks": int(fb.value), "status": int(st.value),
-                "host_pictures": int(hp(self.h))}
+                "host_pictures": int(hp(self.h)), "lane_pictures": [int(lp(self.h, l)) for l in range(2)]}
 
     def last_recon(self, b: int):
         y = np.empty((self.ch, self.cw), np.uint8)

@@ -571,6 +571,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
         return q, "p" + hashlib.sha1(q.astype(np.int8).tobytes()).hexdigest()[:12]
 
     prefetched: dict = {}  # segment -> device frames loaded ahead by the prefetch thread
+    stats_lock = threading.Lock()  # stats["reads"]: main thread and prefetch thread
 
     def load(i):
         """Segment i's source: a synthetic range (generated where it is encoded), a Y4M byte
@@ -583,7 +584,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 buf.record_stream(torch.cuda.current_stream(buf.device))
             return fr
         s, n = segs[i]
-        stats["reads"] += 1
+        with stats_lock:  # load() also runs on the prefetch thread
+            stats["reads"] += 1
         if synthetic:
             return SynthRange(src.seed, w0, h0, src.start + s, n)
         if isinstance(src, media.Y4MSource) and not software:
@@ -617,15 +619,17 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             return {}
         with trace.span("node_job.decode", segments=len(ids)):
             hosts = list(dec_pool.map(lambda i: src.read(*segs[i]), ids))
-        stats["reads"] += len(ids)
+        with stats_lock:
+            stats["reads"] += len(ids)
         return {i: finish(fr) for i, fr in zip(ids, hosts)}
 
     # file sources on the GPU: the next claim is read + uploaded on a side thread / HIP
     # stream while this claim encodes (the reference overlaps GET part with the previous
     # encode only across nodes; here ingest hides behind the engine on every rank)
-    # Only Y4M sources: their reads are pread threads + DMA, so the side thread costs the
-    # engine nothing; a decoded source (HEVC / AV1 / MPEG-2) would run a whole CPU decode there
-    # (ADVICE r4), unmeasured -- those load on demand.
+    # Y4M sources: their reads are pread threads + DMA, so the side thread costs the engine
+    # nothing.  Decoded sources (HEVC / AV1 / MPEG-2) prefetch too when the decode pool exists:
+    # the next claim's segments decode on the pool's threads (the native decoders release the
+    # GIL) and upload on the prefetch stream while this claim encodes.
     prefetch = (not synthetic and not software and dev.type == "cuda"
                 and (isinstance(src, media.Y4MSource) or dec_pool is not None)
                 and os.environ.get("TV_PREFETCH", "1") != "0")
