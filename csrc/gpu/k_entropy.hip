@@ -18,6 +18,7 @@
 // Reference: the reference entropy-codes in VA-API fixed function (worker/tasks.py:1573-1586).
 #include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "gpu_common.h"
 #include "k_encode.h"
@@ -1069,6 +1070,283 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
   };
   for (int row = blockIdx.x; row < hc; row += gridDim.x) code_row(row);
 }
+
+// ---- lane-per-substream coder --------------------------------------------------------------
+// One WAVE per CTB row index r, one LANE per segment: lane b codes substream (b, r).  Rows of
+// different segments are independent, so every lane of the wave is busy (the single-lane
+// coder above keeps 816 mostly idle waves resident at the 1080p bench shape; this one 34).
+// The WPP storage after CTB 1 (9.3.2.4) goes from lane b of wave r - 1 to lane b of wave r
+// through global memory (agent-scope stores / loads + flag, as above).
+//
+// Every lane executes one coder OPERATION per iteration -- a context-coded bin, a bypass run
+// of up to 16 bins, or a terminating bin -- in one branch-free form:
+//   low = ((low << pre) + add) << post,  range = nr << post,  bits_left -= pre + post,
+//   post = clz(nr) - 23
+// (bypass: pre = n, add = range * bins, nr = range; context bin: pre = 0, add = LPS ? range -
+// rLPS : 0, nr = LPS ? rLPS : range - rLPS; terminate: pre = 0, add = bin ? range - 2 : 0, nr =
+// bin ? 2 : range - 2).  `low` is 64-bit so a whole 16-bin bypass run fits before the byte
+// output (CabacEncoder::write_out, at most twice per operation).  Bytes depend only on the
+// sequence of interval updates, not on when they are written out, so the output is the host
+// writer's byte for byte.
+//
+// LDS, per wave: the context states as [ctx][lane] dwords (a lane's reads hit bank lane % 32
+// whatever the context: conflict-free), a per-lane token ring [slot][lane] refilled 16 tokens
+// at a time one block of iterations ahead (the dwordx4 loads of block k are stored into the
+// ring at block k + 1, so their latency hides behind 8 iterations), and the rLPS / transIdxLps
+// tables (rLPS of the four range quarters packed in one dword per state).
+constexpr int kLnRing = 64;  // token slots per lane
+constexpr int kLnRefill = 16;
+constexpr int kLnBlock = 8;  // iterations between refills (<= kLnRefill / tokens per iteration)
+
+__global__ void __launch_bounds__(64) k_ent_ac_lanes(EntropyArgs a, int B) {
+  __shared__ uint32_t ctxL[kEntCtx * 64];
+  __shared__ uint32_t ring[kLnRing * 64];
+  __shared__ uint32_t lps4[64], tl[64];
+  const int lane = threadIdx.x, row = blockIdx.x;
+  const int b = blockIdx.y * 64 + lane;
+  {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v |= (uint32_t)a.tab->lps[lane * 4 + q] << (8 * q);
+    lps4[lane] = v;
+    tl[lane] = a.tab->tlps[lane];
+  }
+  const int wc = a.g.wc, hc = a.g.hc, nctu = wc * hc;
+  bool active = b < B;
+  int* flag = a.wflag + (long)b * hc + row;
+  auto abort_lane = [&](int code) {
+    atomicOr(a.status, code);
+    __hip_atomic_store(flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    active = false;
+  };
+  if (*a.status) {  // the binariser gave up on this picture: the host codes it
+    if (active) __hip_atomic_store(flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // the lane's token range: segments back to back (exclusive prefix of seg_tok over the wave)
+  const int stok = active ? a.seg_tok[b] : 0;
+  int pre_tok = stok;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(pre_tok, o, 64);
+    if (lane >= o) pre_tok += t;
+  }
+  long tbase = pre_tok - stok;
+  for (int k = 0; k < blockIdx.y * 64; ++k) tbase += a.seg_tok[k];  // lane groups before this one
+  const int* off = a.ctb_off + (long)(active ? b : 0) * nctu;
+  const long tpos = tbase + off[row * wc];
+  const long tend = row + 1 < hc ? tbase + off[(row + 1) * wc] : tbase + stok;
+  uint32_t* out = reinterpret_cast<uint32_t*>(a.stage + stage_off(tpos, (long)(active ? b : 0) * hc + row));
+  const unsigned long long w0 = wall_clock64();
+  // WPP: wait for the row above of every lane's segment (rows of a picture progress together)
+  if (row > 0) {
+    const int* up = flag - 1;
+    for (int spin = 0;; ++spin) {
+      const int f = active ? __hip_atomic_load(up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1;
+      if (f == 2 && active) {  // the row above aborted: so does this one
+        __hip_atomic_store(flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        active = false;
+      }
+      if (__all(f != 0)) break;
+      if (spin > (1 << 23)) {  // ~25 s: the row above never came (never expected)
+        if (active && f == 0) abort_lane(32);
+        break;
+      }
+      if (spin < 8)
+        __builtin_amdgcn_s_sleep(4);
+      else
+        __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  // contexts: row 0 from the init table, else the row above's after its CTB 1
+  if (active) {
+    if (row == 0) {
+      const uint8_t* src = a.tab->init[a.pic.init_type][clip3(0, 51, (int)a.dec.qp[b])];
+      for (int c = 0; c < kEntCtx; c += 4) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(src + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ctxL[(c + q) * 64 + lane] = (w >> (8 * q)) & 255;
+      }
+    } else {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wctx + ((long)b * hc + row - 1) * kEntCtx);
+      uint32_t t[kEntCtx / 4];
+#pragma unroll
+      for (int i = 0; i < kEntCtx / 4; ++i) t[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < kEntCtx / 4; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ctxL[(4 * i + q) * 64 + lane] = (t[i] >> (8 * q)) & 255;
+    }
+  }
+  // token ring: 32 tokens now, then 16 per block one block ahead
+  const uint4* gtok = reinterpret_cast<const uint4*>(a.tokens);
+  long head = tpos, tail = tpos & ~3L;
+  if (active) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = gtok[(tail >> 2) + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int s0 = (int)((tail + 4 * k) & (kLnRing - 1));
+      ring[(s0 + 0) * 64 + lane] = v[k].x;
+      ring[(s0 + 1) * 64 + lane] = v[k].y;
+      ring[(s0 + 2) * 64 + lane] = v[k].z;
+      ring[(s0 + 3) * 64 + lane] = v[k].w;
+    }
+    tail += 32;
+  }
+  __syncthreads();  // tables (every lane wrote one entry)
+  // coder state (CabacEncoder), low widened to 64 bits
+  unsigned long long low = 0;
+  uint32_t range = 510, buffered = 0xff, ow = 0;
+  int bl = 23, nbuf = 0, pos = 0;
+  int sub = 0;  // next bin of a context token
+  long left = tend - tpos;  // tokens this substream may still consume
+  bool synced = false;
+  uint32_t tok = active ? ring[(head & (kLnRing - 1)) * 64 + lane] : 0;
+  long nctxbins = 0, ntoks = 0;
+  const unsigned long long w1 = wall_clock64(), c1 = clock64();
+  auto put = [&](uint32_t byte) {
+    ow |= (byte & 255) << (8 * (pos & 3));
+    if ((++pos & 3) == 0) {
+      out[(pos >> 2) - 1] = ow;
+      ow = 0;
+    }
+  };
+  uint4 pend[kLnRefill / 4];
+  bool pending = false;
+  while (__any(active)) {
+    if (active && pending) {  // the block-ahead refill lands in the ring
+#pragma unroll
+      for (int k = 0; k < kLnRefill / 4; ++k) {
+        const int s0 = (int)((tail + 4 * k) & (kLnRing - 1));
+        ring[(s0 + 0) * 64 + lane] = pend[k].x;
+        ring[(s0 + 1) * 64 + lane] = pend[k].y;
+        ring[(s0 + 2) * 64 + lane] = pend[k].z;
+        ring[(s0 + 3) * 64 + lane] = pend[k].w;
+      }
+      tail += kLnRefill;
+    }
+    pending = active && tail - head <= kLnRing - 2 * kLnRefill && tail < tend;
+    if (pending) {
+#pragma unroll
+      for (int k = 0; k < kLnRefill / 4; ++k) pend[k] = gtok[(tail >> 2) + k];
+    }
+    for (int it = 0; it < kLnBlock; ++it) {
+      if (!active) break;
+      const uint32_t ty = tok >> 30;
+      const bool isC = ty == 0, isB = ty == 1, isT = ty == 2;
+      const int nbins = (tok >> 27) & 3;
+      const bool more = isC && sub + 1 < nbins;  // the token has another bin after this one
+      // the next token, read while this operation runs
+      const uint32_t ntok = ring[((head + 1) & (kLnRing - 1)) * 64 + lane];
+      const uint32_t f = (tok >> (9 * sub)) & 511;
+      const int c = isC ? (int)(f & 255) : 0;
+      const uint32_t sv = ctxL[c * 64 + lane];
+      const uint32_t st = sv & 63, mps = (sv >> 6) & 1;
+      const uint32_t lp = (lps4[st] >> (8 * ((range >> 6) & 3))) & 255;
+      const uint32_t tlp = tl[st];
+      const uint32_t rmps = range - lp;
+      const bool lpsb = isC && (f >> 8) != mps;
+      const uint32_t tb = tok & 1;
+      const int bn = (tok >> 16) & 31;
+      const uint32_t nr = isC ? (lpsb ? lp : rmps) : isT ? (tb ? 2u : range - 2) : range;
+      const unsigned long long add = isC ? (lpsb ? rmps : 0u) : isT ? (tb ? range - 2 : 0u)
+                                   : isB ? (unsigned long long)range * (tok & 0xffffu) : 0ull;
+      const int prs = isB ? bn : 0;
+      const int post = __clz(nr) - 23;
+      low = ((low << prs) + add) << post;
+      range = nr << post;
+      bl -= prs + post;
+      if (isC) {
+        const uint32_t nsv = lpsb ? (tlp | ((mps ^ (st == 0 ? 1u : 0u)) << 6)) : ((st < 62 ? st + 1 : st) | (mps << 6));
+        ctxL[c * 64 + lane] = nsv;
+        ++nctxbins;
+      }
+      while (bl < 12) {  // CabacEncoder::write_out (bl >= -4 here: <= 16 bits per operation)
+        const uint32_t lead = (uint32_t)(low >> (24 - bl));
+        bl += 8;
+        low &= (1ull << (32 - bl)) - 1;
+        if (lead == 0xff) {
+          nbuf++;
+        } else if (nbuf > 0) {
+          const uint32_t carry = lead >> 8;
+          put(buffered + carry);
+          buffered = lead & 0xff;
+          const uint32_t byte = (0xff + carry) & 0xff;
+          for (; nbuf > 1; --nbuf) put(byte);
+        } else {
+          nbuf = 1;
+          buffered = lead;
+        }
+      }
+      if (ty == 3) {
+        if ((tok & 0xff) == kCtrlSync) {  // 9.3.2.4 storage for the row below
+          uint32_t* dst = reinterpret_cast<uint32_t*>(a.wctx + ((long)b * hc + row) * kEntCtx);
+          uint32_t t[kEntCtx / 4];
+#pragma unroll
+          for (int i = 0; i < kEntCtx / 4; ++i)
+            t[i] = ctxL[(4 * i) * 64 + lane] | ctxL[(4 * i + 1) * 64 + lane] << 8 | ctxL[(4 * i + 2) * 64 + lane] << 16 |
+                   ctxL[(4 * i + 3) * 64 + lane] << 24;
+#pragma unroll
+          for (int i = 0; i < kEntCtx / 4; ++i) __hip_atomic_store(dst + i, t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          synced = true;
+        } else {  // finish() + '1' + byte alignment (end_of_subset_one_bit / slice trailing bits)
+          const unsigned long long top = 1ull << (32 - bl);
+          if (low >= top) {
+            put(buffered + 1);
+            for (; nbuf > 1; --nbuf) put(0x00);
+            low -= top;
+          } else {
+            if (nbuf > 0) put(buffered);
+            for (; nbuf > 1; --nbuf) put(0xff);
+          }
+          const int nb = 24 - bl;  // 1..12 bits of low >> 8, then the '1', then zeros
+          uint32_t v = ((((uint32_t)low >> 8) & ((1u << nb) - 1)) << 1) | 1u;
+          int t = nb + 1;
+          const int pad = (8 - (t & 7)) & 7;
+          v <<= pad;
+          t += pad;
+          while (t > 0) {
+            t -= 8;
+            put((v >> t) & 0xff);
+          }
+          uint8_t* o8 = reinterpret_cast<uint8_t*>(out);
+          for (int k = pos & ~3; k < pos; ++k) o8[k] = (uint8_t)(ow >> (8 * (k & 3)));
+          a.row_bytes[(long)b * hc + row] = pos;
+          if (!synced) {
+            abort_lane(4);  // a substream that never stored its contexts (corrupt stream)
+          } else {
+            active = false;
+          }
+          if (a.dbg) {  // TV_ENT_DEBUG: rows, context bins, tokens, coding clocks, wait ticks, max row span
+            atomicAdd(&a.dbg[0], 1ull);
+            atomicAdd(&a.dbg[1], (unsigned long long)nctxbins);
+            atomicAdd(&a.dbg[2], (unsigned long long)ntoks);
+            atomicAdd(&a.dbg[3], clock64() - c1);
+            atomicAdd(&a.dbg[4], w1 - w0);
+            atomicMax(&a.dbg[5], wall_clock64() - w0);
+          }
+          break;
+        }
+      }
+      if (more) {
+        ++sub;
+      } else {
+        sub = 0;
+        ++head;
+        ++ntoks;
+        tok = ntok;
+        if (--left <= 0) {  // no FLUSH before the row's tokens ran out
+          abort_lane(4);
+          break;
+        }
+      }
+    }
+  }
+}
 // Slice b's rows back to back after slices 0..b-1, written straight into the pinned host slot
 // (device-visible): the head (sizes), the slice QP and the payload -- the host needs no copy.
 __global__ void __launch_bounds__(256) k_ent_pack(EntropyArgs a, int B) {
@@ -1138,8 +1416,16 @@ void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s) {
     const int v = e ? std::atoi(e) : 1;
     return v < 1 ? 1 : v > 8 ? 8 : v;
   }();
+  // TV_ENT_CODER=wave: the single-lane coder (one wave per substream), for A/B measurements
+  static const bool wave_coder = [] {
+    const char* e = std::getenv("TV_ENT_CODER");
+    return e && std::string(e) == "wave";
+  }();
   (void)hipMemsetAsync(a.wflag, 0, (size_t)B * a.g.hc * sizeof(int), s);
-  k_ent_ac<<<dim3((a.g.hc + rpw - 1) / rpw, B), 64, 0, s>>>(a);
+  if (wave_coder)
+    k_ent_ac<<<dim3((a.g.hc + rpw - 1) / rpw, B), 64, 0, s>>>(a);
+  else
+    k_ent_ac_lanes<<<dim3(a.g.hc, (B + 63) / 64), 64, 0, s>>>(a, B);
   k_ent_pack<<<B, 256, 0, s>>>(a, B);
   k_ent_status<<<1, 1, 0, s>>>(a);
 }

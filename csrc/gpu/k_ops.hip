@@ -342,10 +342,9 @@ __global__ void k_overlay_mask(uint8_t* __restrict__ frames, int w, int h, const
 // it (prev2/next2), refined by an edge-aware spatial interpolator (4-tap, or a 5-line
 // low/high-frequency blend when the vertical edge is strong) and clamped to the temporal
 // uncertainty `diff` widened by the spatial check.
-__global__ void k_bwdif(const uint8_t* __restrict__ prev, const uint8_t* __restrict__ cur,
-                        const uint8_t* __restrict__ next, uint8_t* __restrict__ out, int w, int h, int keep) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-  if (x >= w || y >= h) return;
+__device__ __forceinline__ void bwdif_px(const uint8_t* __restrict__ prev, const uint8_t* __restrict__ cur,
+                                         const uint8_t* __restrict__ next, uint8_t* __restrict__ out, int w, int h,
+                                         int keep, int x, int y) {
   const long o = (long)y * w + x;
   if ((y & 1) == keep || y < 2 || y >= h - 2) {  // kept field (and border lines: bob)
     if ((y & 1) == keep) {
@@ -388,6 +387,31 @@ __global__ void k_bwdif(const uint8_t* __restrict__ prev, const uint8_t* __restr
     v = clampi(interp, d - diff, d + diff);
   }
   out[o] = sat8(v);
+}
+__global__ void k_bwdif(const uint8_t* __restrict__ prev, const uint8_t* __restrict__ cur,
+                        const uint8_t* __restrict__ next, uint8_t* __restrict__ out, int w, int h, int keep) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  bwdif_px(prev, cur, next, out, w, h, keep, x, y);
+}
+// A whole segment in one launch: z = frame * nplanes + plane; frame i from (i-1, i, i+1) with
+// the segment's edges repeated (send_frame per part).  Planes are packed (pitch = width).
+struct BwdifPlanes {
+  long off[3];
+  int w[3], h[3];
+  int n;
+};
+__global__ void k_bwdif_seg(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, long fs, int nframes,
+                            BwdifPlanes pl, int keep) {
+  const int i = blockIdx.z / pl.n, p = blockIdx.z - i * pl.n;
+  const int w = pl.w[p], h = pl.h[p];
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  const long o = pl.off[p];
+  const uint8_t* cur = src + (long)i * fs + o;
+  const uint8_t* prev = src + (long)(i > 0 ? i - 1 : 0) * fs + o;
+  const uint8_t* next = src + (long)(i + 1 < nframes ? i + 1 : nframes - 1) * fs + o;
+  bwdif_px(prev, cur, next, dst + (long)i * fs + o, w, h, keep, x, y);
 }
 
 // ------------------------------------------------------------------------ SSIM
@@ -555,6 +579,32 @@ int tv_overlay_mask(uint8_t* frames, int n, int w, int h, const uint8_t* masks, 
   }
   tv::ops::k_overlay_mask<<<dim3(cdiv(mw, 128), mh, n), 128, 0, static_cast<hipStream_t>(stream)>>>(
       frames, w, h, masks, mw, mh, x0, y0);
+  return ops_status();
+}
+// bwdif over a segment of n packed frames (frame stride fs bytes; np planes at byte offsets
+// off[] of sizes w[] x h[]), one launch for every frame and plane
+int tv_bwdif_segment(const uint8_t* src, uint8_t* dst, long fs, int n, int np, const long* off, const int* w,
+                     const int* h, int tff, void* stream) {
+  if (n <= 0 || np < 1 || np > 3 || n * np > 65535) {
+    g_ops_err = "tv_bwdif_segment: bad arguments";
+    return -1;
+  }
+  tv::ops::BwdifPlanes pl{};
+  int mw = 0, mh = 0;
+  for (int p = 0; p < np; ++p) {
+    if (w[p] <= 0 || h[p] < 4 || off[p] < 0 || off[p] + (long)w[p] * h[p] > fs) {
+      g_ops_err = "tv_bwdif_segment: bad plane geometry";
+      return -1;
+    }
+    pl.off[p] = off[p];
+    pl.w[p] = w[p];
+    pl.h[p] = h[p];
+    mw = w[p] > mw ? w[p] : mw;
+    mh = h[p] > mh ? h[p] : mh;
+  }
+  pl.n = np;
+  tv::ops::k_bwdif_seg<<<dim3(cdiv(mw, 256), mh, n * np), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      src, dst, fs, n, pl, tff ? 0 : 1);
   return ops_status();
 }
 int tv_bwdif_plane(const uint8_t* prev, const uint8_t* cur, const uint8_t* next, uint8_t* out, int w, int h,

@@ -194,6 +194,22 @@ def test_watcher_config_validation(mgr):
     s = c.get("/watcher/status").json
     assert s["config"]["STABLE_CHECKS"] == "3" and s["env_file"]["exists"]
     assert c.post("/watcher/control", json={"action": "explode"}).status_code == 400
+    # the page's typed form is driven by these: every int field carries its server-side range
+    t = s["field_types"]
+    assert t["int"]["STABLE_CHECKS"] == [1, 60] and "USE_SCANNER" in t["bool"] and "PROCESSED_PATH_ALIASES" in t["text"]
+    assert {"free_bytes", "total_bytes"} <= set(s["watch_root"]) and s["watch_root"]["exists"]
+
+
+def test_ui_pages_carry_their_controls(mgr):
+    """Watcher page: typed config form with range checks, service / root / env panels;
+    browse page: both roots, sortable size / modified columns, persistent selection."""
+    c = mgr["c"]
+    w = c.get("/watcher").get_data(as_text=True)
+    for needle in ('type="number"', "p-root", "p-svc", "p-env", "collect()", "field_types"):
+        assert needle in w, needle
+    b = c.get("/browse").get_data(as_text=True)
+    for needle in ("source_media", "sortBy('size')", "sortBy('mtime')", "selectAll", "mark_watcher_processed"):
+        assert needle in b, needle
 
 
 def test_watchdog_fails_stalled_jobs(mgr, monkeypatch):

@@ -143,6 +143,32 @@ def test_bwdif_hip_matches_reference():
     assert (got == deint.bwdif_plane_ref(*fr)).all()
 
 
+@pytest.mark.gpu
+def test_bwdif_segment_one_launch_matches_reference():
+    """deinterlace_device: every frame and plane of a segment in one k_bwdif_seg launch, on a
+    view that starts mid-buffer (DevFrames.select), equals the per-frame numpy reference with
+    the segment's edges repeated."""
+    import torch
+
+    from thinvids_amd.ops import deint
+    from thinvids_amd.ops.stage import DevFrames, flat_layout
+
+    w, h, n = 96, 72, 5
+    frames = [tuple(_img(hh, ww, seed=10 * k + c) for c, (hh, ww) in enumerate(((h, w), (h // 2, w // 2), (h // 2, w // 2))))
+              for k in range(n + 1)]
+    flat = np.stack([np.concatenate([p.ravel() for p in f]) for f in frames])
+    df = DevFrames(torch.from_numpy(flat.ravel().copy()).cuda(), n + 1, w, h, flat_layout(w, h)).select(1, n)
+    out = deint.deinterlace_device(df, tff=True)
+    host = out.buf.cpu().numpy().reshape(n + 1, -1)
+    ref = deint.deinterlace_frames(frames[1:], tff=True)
+    for k in range(n):
+        got = host[k + 1]
+        ysz, csz = w * h, (w // 2) * (h // 2)
+        assert (got[:ysz].reshape(h, w) == ref[k][0]).all(), k
+        assert (got[ysz:ysz + csz].reshape(h // 2, w // 2) == ref[k][1]).all(), k
+        assert (got[ysz + csz:].reshape(h // 2, w // 2) == ref[k][2]).all(), k
+
+
 def test_ssim_ref():
     from thinvids_amd.ops import quality
 

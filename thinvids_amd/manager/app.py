@@ -237,6 +237,9 @@ def watcher_status_payload(limit=80) -> dict:
     config.update({k: v for k, v in svc.get("environment", {}).items() if k in WATCHER_FIELDS})
     config.update({k: v for k, v in envf.items() if k in WATCHER_FIELDS})
     return {"service": svc, "config": config, "config_fields": sorted(WATCHER_FIELDS),
+            "field_types": {"bool": sorted(WATCHER_BOOL_FIELDS),
+                            "int": {k: list(v) for k, v in WATCHER_INT_FIELDS.items()},
+                            "text": dict(WATCHER_TEXT_FIELDS)},
             "known_roots": [{"label": "Watch folder", "path": core.CFG.watch_root},
                             {"label": "Source media", "path": core.CFG.source_media_root}],
             "env_file": {"path": core.CFG.watcher_env_file, "exists": os.path.exists(core.CFG.watcher_env_file),

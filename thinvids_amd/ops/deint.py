@@ -78,8 +78,9 @@ def bwdif_plane(prev, cur, nxt, tff: bool = True):
 
 def deinterlace_device(df, tff: bool = True):
     """bwdif (send_frame) over a segment of 8-bit device frames (ops.stage.DevFrames) with
-    ``k_bwdif``: frame i from (i-1, i, i+1), the segment's edges repeat (the split pipeline's
-    per-part rule).  Returns new DevFrames in the same layout."""
+    ``k_bwdif_seg``: one launch for every frame and plane, frame i from (i-1, i, i+1), the
+    segment's edges repeat (the split pipeline's per-part rule).  Returns new DevFrames in the
+    same layout."""
     import torch
 
     from .._native import gpu_lib
@@ -91,17 +92,23 @@ def deinterlace_device(df, tff: bool = True):
     lib = gpu_lib()
     stream = C.c_void_p(torch.cuda.current_stream(df.buf.device).cuda_stream)
     esz = df.buf.element_size()
-    src, dst = df.buf.data_ptr(), out.data_ptr()
-    for i in range(df.n):
-        for off, pw, ph, st, fs in df.planes:
-            if st != pw:
-                raise ValueError("bwdif: planes must be packed")
-            at = lambda base, k: C.c_void_p(base + (off + k * fs) * esz)  # noqa: E731
-            rc = lib.tv_bwdif_plane(at(src, max(0, i - 1)), at(src, i), at(src, min(df.n - 1, i + 1)), at(dst, i),
-                                    pw, ph, int(tff), stream)
-            if rc != 0:
-                lib.tv_ops_last_error.restype = C.c_char_p
-                raise RuntimeError(lib.tv_ops_last_error().decode())
+    if any(st != pw for _, pw, _, st, _ in df.planes):
+        raise ValueError("bwdif: planes must be packed")
+    fs = df.planes[0][4]
+    base = min(off for off, *_ in df.planes)
+    rel = [off - base for off, *_ in df.planes]
+    if any(p[4] != fs for p in df.planes) or any(r + pw * ph > fs for r, (_, pw, ph, _, _) in zip(rel, df.planes)):
+        raise ValueError("bwdif: planes of one frame must share the frame stride")
+    npl = len(df.planes)
+    f = lib.tv_bwdif_segment
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_long), C.POINTER(C.c_int),
+                  C.POINTER(C.c_int), C.c_int, C.c_void_p]
+    rc = f(C.c_void_p(df.buf.data_ptr() + base * esz), C.c_void_p(out.data_ptr() + base * esz), fs * esz, df.n, npl,
+           (C.c_long * npl)(*[r * esz for r in rel]), (C.c_int * npl)(*[p[1] for p in df.planes]),
+           (C.c_int * npl)(*[p[2] for p in df.planes]), int(tff), stream)
+    if rc != 0:
+        lib.tv_ops_last_error.restype = C.c_char_p
+        raise RuntimeError(lib.tv_ops_last_error().decode())
     return DevFrames(out, df.n, df.w, df.h, df.planes, df.bits, [df.buf, *df.keep])
 
 
