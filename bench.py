@@ -172,7 +172,8 @@ def _timed(args, step, dev, world, post, extra_ranks=None):
     el_t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     cores = meter.cores()
     dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    ranks = _per_rank([cores] + list(extra_ranks or []), dev)
+    # extra per-rank values; callables are read after the timed region (e.g. byte counters)
+    ranks = _per_rank([cores] + [v() if callable(v) else v for v in (extra_ranks or [])], dev)
     return float(el_t.item()), step_ms, res, ranks
 
 
@@ -582,7 +583,10 @@ def av1_main(args) -> None:
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",
-                "comm": f"rccl world={world}: stats all_reduce + bitstream gather to rank 0 (overlapped)",
+                "comm": f"{dist.get_backend()} world={world}: stats all_reduce + bitstream gather to rank 0 (overlapped)",
+                "per_rank_comm": [{"transport": "rccl p2p" if dist.get_backend() == "nccl" else dist.get_backend(),
+                                   "p2p_sent_mb_incl_warmup": round(r[3] / 1e6, 3), "p2p_recv_mb_incl_warmup": round(r[4] / 1e6, 3)}
+                                  for r in ranks],
                 "resolution": f"{w}x{h}",
                 "segments_per_gpu": batch,
                 "batch_sizing": sizing,
@@ -803,7 +807,12 @@ def hevc_pass(args, world, rank, local, dev, cpus):
         segs = eng.encode_synthetic(starts_of(s))
         post.submit(comm, segs, np.array([eng.sse(b) for b in range(batch)]).sum(0))
 
-    el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), eng.threads])
+    from thinvids_amd.parallel.comm import COMM_STATS
+
+    c0 = dict(COMM_STATS)
+    el, step_ms, res, ranks = _timed(args, step, dev, world, post,
+                                     [len(cpus), eng.threads, lambda: COMM_STATS["p2p_sent_bytes"] - c0["p2p_sent_bytes"],
+                                      lambda: COMM_STATS["p2p_recv_bytes"] - c0["p2p_recv_bytes"]])
     for f in first.values():  # the look-ahead pass 1 of the step after the last one
         f.result()
     tot = np.sum([r[0] for r in res], axis=0)
@@ -846,7 +855,10 @@ def hevc_pass(args, world, rank, local, dev, cpus):
                 "global_batch": world * batch,
                 "seq_len": args.gop,
                 "parallelism": f"dp{world}",
-                "comm": f"rccl world={world}: stats all_reduce + bitstream gather to rank 0 (overlapped)",
+                "comm": f"{dist.get_backend()} world={world}: stats all_reduce + bitstream gather to rank 0 (overlapped)",
+                "per_rank_comm": [{"transport": "rccl p2p" if dist.get_backend() == "nccl" else dist.get_backend(),
+                                   "p2p_sent_mb_incl_warmup": round(r[3] / 1e6, 3), "p2p_recv_mb_incl_warmup": round(r[4] / 1e6, 3)}
+                                  for r in ranks],
                 "resolution": f"{w}x{h}",
                 "segments_per_gpu": batch,
                 "batch_sizing": dict(sizing, **({"engine_hbm_gib": round(eng.footprint()["dev"] / 2**30, 2)}

@@ -32,9 +32,73 @@ def _live() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+# Per-process P2P counters of the byte gathers (bench.py reports them per rank).
+COMM_STATS = {"p2p_sent_bytes": 0, "p2p_recv_bytes": 0, "p2p_ops": 0}
+
+
+class _PinnedStage:
+    """A reusable pinned host buffer per direction and device: a payload is copied into it
+    once and moved with one asynchronous copy (no per-call ``bytearray`` + ``pin_memory``
+    allocation, which is a page-locking ``hipHostMalloc`` every time).  An event guards reuse:
+    the next call waits until the previous copy out of / into the buffer has completed."""
+
+    def __init__(self):
+        self.buf = None
+        self.ev = None
+
+    def get(self, n: int, device) -> "torch.Tensor":
+        if self.ev is not None:
+            self.ev.synchronize()
+        if self.buf is None or self.buf.numel() < n:
+            self.buf = torch.empty(max(n, 1 << 20, 2 * (self.buf.numel() if self.buf is not None else 0)),
+                                   dtype=torch.uint8, pin_memory=True)
+        return self.buf[:n]
+
+    def mark(self, device) -> None:
+        self.ev = torch.cuda.Event()
+        self.ev.record(torch.cuda.current_stream(device))
+
+
+_STAGES: dict = {}
+
+
+def _stage(kind: str, device) -> _PinnedStage:
+    key = (kind, str(device))
+    if key not in _STAGES:
+        _STAGES[key] = _PinnedStage()
+    return _STAGES[key]
+
+
+def to_device_bytes(payload: bytes, device: torch.device) -> torch.Tensor:
+    """Host bytes -> a uint8 tensor on `device` (CPU: a view of the bytes, no copy)."""
+    src = torch.frombuffer(memoryview(payload), dtype=torch.uint8) if len(payload) else torch.empty(0, dtype=torch.uint8)
+    if device.type != "cuda":
+        return src
+    st = _stage("h2d", device)
+    pin = st.get(len(payload), device)
+    pin.copy_(src)
+    out = pin.to(device, non_blocking=True)
+    st.mark(device)
+    return out
+
+
+def from_device_bytes(t: torch.Tensor, n: int) -> bytes:
+    """The first n bytes of a device (or host) uint8 tensor as bytes, through the reusable
+    pinned receive buffer."""
+    if t.device.type != "cuda":
+        return t[:n].numpy().tobytes()
+    st = _stage("d2h", t.device)
+    pin = st.get(n, t.device)
+    pin.copy_(t[:n], non_blocking=True)
+    st.mark(t.device)
+    st.ev.synchronize()
+    return pin.numpy().tobytes()
+
+
 def gather_bytes_to_root(payload: bytes, device: torch.device, root: int = 0):
     """Gather one byte string from every rank to `root`.  Returns list[bytes] on root, None
-    elsewhere."""
+    elsewhere.  Sizes travel in one all_gather; payloads as one grouped isend/irecv (one
+    xGMI hop per peer), staged through reusable pinned buffers."""
     world, rank = _world()
     if not _live():
         return [payload]
@@ -43,24 +107,28 @@ def gather_bytes_to_root(payload: bytes, device: torch.device, root: int = 0):
     dist.all_gather(sizes, n)
     sizes = [int(s.item()) for s in sizes]
     if rank == root:
-        bufs = [torch.empty(max(1, sizes[r]), dtype=torch.uint8, device=device) for r in range(world)]
-        ops = [dist.P2POp(dist.irecv, bufs[r], r) for r in range(world) if r != root and sizes[r] > 0]
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
+        bufs = {r: torch.empty(sizes[r], dtype=torch.uint8, device=device)
+                for r in range(world) if r != root and sizes[r] > 0}
+        if bufs:
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.irecv, b, r) for r, b in bufs.items()]):
                 req.wait()
+            COMM_STATS["p2p_ops"] += len(bufs)
         out = []
         for r in range(world):
             if r == root:
                 out.append(payload)
+            elif r in bufs:
+                out.append(from_device_bytes(bufs[r], sizes[r]))
+                COMM_STATS["p2p_recv_bytes"] += sizes[r]
             else:
-                out.append(bytes(bufs[r][: sizes[r]].cpu().numpy().tobytes()) if sizes[r] else b"")
+                out.append(b"")
         return out
     if len(payload):
-        t = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
-        if device.type == "cuda":
-            t = t.pin_memory().to(device, non_blocking=True)
+        t = to_device_bytes(payload, device)
         for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, root)]):
             req.wait()
+        COMM_STATS["p2p_sent_bytes"] += len(payload)
+        COMM_STATS["p2p_ops"] += 1
     return None
 
 
@@ -247,7 +315,7 @@ class SegmentStream:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
             for r in sorted(bufs):
-                raw = bufs[r].cpu().numpy().tobytes()
+                raw = from_device_bytes(bufs[r], sizes[r])
                 hl = int.from_bytes(raw[:8], "little")
                 off = 8 + hl
                 for k, n in json.loads(raw[8:off]):
@@ -256,9 +324,7 @@ class SegmentStream:
                     self.stats["segments"] += 1
                 self.stats["bytes"] += len(raw)
         elif blob:
-            t = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
-            if self.dev.type == "cuda":
-                t = t.pin_memory().to(self.dev, non_blocking=True)
+            t = to_device_bytes(blob, self.dev)
             for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, self.root, group=self.data)]):
                 req.wait()
             self.stats["bytes"] += len(blob)
