@@ -548,7 +548,13 @@ def av1_main(args) -> None:
         else:
             post.submit(comm, eng.encode_gop(args.gop, loader(i), async_host=True))
 
-    el, step_ms, res, ranks = _timed(args, step, dev, world, post, [len(cpus), eng.pool._max_workers])
+    from thinvids_amd.parallel.comm import COMM_STATS
+
+    c0 = dict(COMM_STATS)
+    el, step_ms, res, ranks = _timed(args, step, dev, world, post,
+                                     [len(cpus), eng.pool._max_workers,
+                                      lambda: COMM_STATS["p2p_sent_bytes"] - c0["p2p_sent_bytes"],
+                                      lambda: COMM_STATS["p2p_recv_bytes"] - c0["p2p_recv_bytes"]])
     for f in plans.values():  # the look-ahead pass 1 of the step after the last one
         f.result()
     tot = np.sum([r[0] for r in res], axis=0)
