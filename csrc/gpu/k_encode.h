@@ -110,7 +110,7 @@ void launch_pack_flags(DecisionSet dec, uint8_t* flags, const Geo& g, int B, hip
 constexpr int kEntCtx = 160;  // >= tv::CTX_COUNT (static_assert in k_entropy.hip)
 // tokens per CTB region of the single binarisation pass (a CTB that needs more is binarised
 // again straight into the picture's token list)
-constexpr int kEntRegionTokens = 2048;  // one token per coder operation (bin / bypass run)
+constexpr int kEntRegionTokens = 1024;
 struct EntropyPic {
   int type;        // 2 I, 1 P, 0 B
   int init_type;   // cabac initType: 0 I, 1 P, 2 B

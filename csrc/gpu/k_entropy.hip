@@ -30,62 +30,62 @@ namespace gpu {
 
 namespace {
 
-// ---- token format (32 bits, type in bits 30..31): one arithmetic-coder OPERATION each ----
-//   CTX : one context-coded bin: bits 0..13 = the context's byte offset in the lane coder's
-//         LDS image ((ctx / 4) * 256 + ctx % 4: ctx_off), bit 14 = the bin.  A terminating
-//         bin is a CTX bin on kTermCtx, a context pinned at pStateIdx 63 (rLPS 2, transIdx 63:
-//         exactly encode_terminate, 9.3.4.3.5)
-//   BYP : bits 8..11 = count n (1..kBypRun), bits 0..7 = the bins, MSB first
-//   CTRL: bits 16..17: 0 = SYNC (store the row's contexts for the row below), 1 = FLUSH (end
-//         of substream: flush the coder, '1' bit, byte alignment); bits 0..15 zero, so the
-//         coder's bypass arithmetic (n = 0, bins = 0) leaves the interval untouched
-constexpr uint32_t kTkCtx = 0u << 30, kTkByp = 1u << 30, kTkCtrl = 3u << 30;
+// ---- token format (32 bits, type in bits 30..31) ----------------------------------------
+//   CTX : bits 27..28 = number of bins n (1..3); bin i at bits 9i..9i+8 = ctx | bin << 8
+//   BYP : bits 16..20 = count (1..16), bits 0..15 = the bins, MSB first
+//   TERM: bit 0 = the terminating bin
+//   CTRL: 0 = SYNC (store the row's contexts for the row below), 1 = FLUSH (end of substream:
+//         flush the coder, '1' bit, byte alignment)
+constexpr uint32_t kTkCtx = 0u << 30, kTkByp = 1u << 30, kTkTerm = 2u << 30, kTkCtrl = 3u << 30;
 constexpr uint32_t kCtrlSync = 0, kCtrlFlush = 1;
-constexpr int kBypRun = 8;             // bypass bins per BYP token
-constexpr int kTermCtx = kEntCtx;      // the terminate context (state 63, never stored for WPP)
-constexpr int kDummyCtx = kEntCtx + 1; // written by non-context operations of the lane coder
-constexpr int kCtxSlots = kEntCtx + 4; // contexts + terminate + dummy, a multiple of 4
-static_assert(CTX_COUNT <= kEntCtx && kEntCtx % 4 == 0 && kEntCtx <= 252, "context layout");
-__host__ __device__ constexpr uint32_t ctx_off(int c) { return (uint32_t)(((c >> 2) << 8) | (c & 3)); }
-__device__ __forceinline__ int ctx_of_off(uint32_t off) { return (int)(((off >> 8) << 2) | (off & 3)); }
+static_assert(CTX_COUNT <= kEntCtx && kEntCtx <= 256, "context index must fit 8 bits");
 
 struct TokSink {
   uint32_t* out;  // nullptr: count only
   int cap;        // tokens past `cap` are counted, not written
   int n = 0;
-  uint32_t pb = 0;  // pending bypass bins
-  int npb = 0;
+  uint32_t pc = 0, pb = 0;  // pending context bins / bypass bins
+  int npc = 0, npb = 0;
   __device__ __forceinline__ void put(uint32_t t) {
     if (out && n < cap) out[n] = t;
     ++n;
   }
-  __device__ __forceinline__ void flush_c() {}
+  __device__ __forceinline__ void flush_c() {
+    if (npc) put(kTkCtx | ((uint32_t)npc << 27) | pc);
+    npc = 0;
+    pc = 0;
+  }
   __device__ __forceinline__ void flush_b() {
-    if (npb) put(kTkByp | ((uint32_t)npb << 8) | pb);
+    if (npb) put(kTkByp | ((uint32_t)npb << 16) | pb);
     npb = 0;
     pb = 0;
   }
   __device__ __forceinline__ void bin(int b, int ctx) {
     flush_b();
-    put(kTkCtx | ((uint32_t)b << 14) | ctx_off(ctx));
+    pc |= (uint32_t)(ctx | (b << 8)) << (9 * npc);
+    if (++npc == 3) flush_c();
   }
   // consecutive bypass bins are one run: equiprobable bins, so splitting or merging a run
-  // never changes the arithmetic code.  Runs are cut at kBypRun (8) bins: one coder operation
-  // then adds at most 8 bits to `low`, so a coder keeps a 32-bit low and needs at most one
-  // byte output per operation.
+  // never changes the arithmetic code
   __device__ __forceinline__ void bypass(uint32_t v, int nb) {
+    flush_c();
     while (nb > 0) {
-      const int take = tv_min(nb, kBypRun - npb);
+      const int take = tv_min(nb, 16 - npb);
       nb -= take;
       pb = (pb << take) | ((v >> nb) & ((1u << take) - 1));
       npb += take;
-      if (npb == kBypRun) flush_b();
+      if (npb == 16) flush_b();
     }
   }
-  __device__ __forceinline__ void term(int b) { bin(b, kTermCtx); }
-  __device__ __forceinline__ void ctrl(uint32_t c) {
+  __device__ __forceinline__ void term(int b) {
+    flush_c();
     flush_b();
-    put(kTkCtrl | (c << 16));
+    put(kTkTerm | (uint32_t)b);
+  }
+  __device__ __forceinline__ void ctrl(uint32_t c) {
+    flush_c();
+    flush_b();
+    put(kTkCtrl | c);
   }
 };
 
@@ -848,7 +848,7 @@ constexpr int kTokK = 32;   // tokens per refill
 // 64-entry LDS ring refilled 32 at a time (a token load kept in registers across the loop's
 // branches forces a vmcnt(0) wait at its use); output bytes leave as dword stores.
 __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
-  __shared__ uint8_t lps[256], tlps[64], ctx[kCtxSlots];
+  __shared__ uint8_t lps[256], tlps[64], ctx[kEntCtx];
   for (int k = threadIdx.x; k < 256; k += 64) lps[k] = a.tab->lps[k];
   tlps[threadIdx.x] = a.tab->tlps[threadIdx.x];
   __syncthreads();
@@ -918,7 +918,6 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
     src = wctx + (long)(row - 1) * (kEntCtx / 4);
   }
   uint32_t* ctx32 = reinterpret_cast<uint32_t*>(ctx);
-  ctx[kTermCtx] = 63;  // the terminate context (pStateIdx 63, valMps 0)
   if (row == 0) {
 #pragma unroll
     for (int i = 0; i < kEntCtx / 4; ++i) ctx32[i] = src[i];
@@ -971,38 +970,57 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
     ++head;
     ++ntoks;
     const uint32_t ty = tok >> 30;
-    if (ty == 0) {  // one context-coded bin (CabacEncoder::bin_step); kTermCtx = terminate
-      ++nctxbins;
-      const int c = ctx_of_off(tok & 0x3fff);
-      const int sv = ctx[c];
-      const int st = sv & 63, mps = sv >> 6;
-      const uint32_t lp = lps[st * 4 + ((range >> 6) & 3)];
-      int nsv;
-      const uint32_t rmps = range - lp;
-      if ((int)((tok >> 14) & 1) != mps) {  // LPS
-        const int nb = __clz(lp) - 23;
-        low = (low + rmps) << nb;
-        range = lp << nb;
-        bl -= nb;
-        nsv = tlps[st] | ((mps ^ (st == 0 ? 1 : 0)) << 6);
-      } else {
-        const int nb = __clz(rmps) - 23;  // 0 or 1
-        low <<= nb;
-        range = rmps << nb;
-        bl -= nb;
-        nsv = (st < 62 ? st + 1 : st) | (mps << 6);
+    if (ty == 0) {  // 1..3 context-coded bins (CabacEncoder::bin_step)
+      const int nbins = (tok >> 27) & 3;
+      nctxbins += nbins;
+      for (int k = 0; k < nbins; ++k) {
+        const uint32_t f = (tok >> (9 * k)) & 511;
+        const int c = (int)(f & 255);
+        const int sv = ctx[c];
+        const int st = sv & 63, mps = sv >> 6;
+        const uint32_t lp = lps[st * 4 + ((range >> 6) & 3)];
+        int nsv;
+        const uint32_t rmps = range - lp;
+        if ((int)(f >> 8) != mps) {  // LPS
+          const int nb = __clz(lp) - 23;
+          low = (low + rmps) << nb;
+          range = lp << nb;
+          bl -= nb;
+          nsv = tlps[st] | ((mps ^ (st == 0 ? 1 : 0)) << 6);
+        } else {
+          const int nb = __clz(rmps) - 23;  // 0 or 1
+          low <<= nb;
+          range = rmps << nb;
+          bl -= nb;
+          nsv = (st < 62 ? st + 1 : st) | (mps << 6);
+        }
+        ctx[c] = (uint8_t)nsv;
+        if (bl < 12) write_out();
       }
-      ctx[c] = (uint8_t)nsv;
-      if (bl < 12) write_out();
-    } else if (ty == 1) {  // bypass bins, MSB first, <= 8 (encode_bypass_bins)
-      const int m = (tok >> 8) & 15;
-      low = (low << m) + range * (tok & 255);
-      bl -= m;
-      if (bl < 12) write_out();
-    } else if (ty == 2) {  // not produced
-      abort_row(4);
-      return;
-    } else if (((tok >> 16) & 3) == kCtrlSync) {  // 9.3.2.4 storage for the row below
+    } else if (ty == 1) {  // bypass bins, MSB first, <= 8 per step (encode_bypass_bins)
+      int n = (tok >> 16) & 31;
+      while (n > 0) {
+        const int m = n > 8 ? 8 : n;
+        n -= m;
+        low = (low << m) + range * ((tok >> n) & ((1u << m) - 1));
+        bl -= m;
+        if (bl < 12) write_out();
+      }
+    } else if (ty == 2) {  // terminating bin (encode_terminate)
+      range -= 2;
+      if (tok & 1) {
+        low += range;
+        low <<= 7;
+        range = 2 << 7;
+        bl -= 7;
+        if (bl < 12) write_out();
+      } else if (range < 256) {
+        low <<= 1;
+        range <<= 1;
+        bl--;
+        if (bl < 12) write_out();
+      }
+    } else if ((tok & 0xff) == kCtrlSync) {  // 9.3.2.4 storage for the row below
       uint32_t* dst = wctx + (long)row * (kEntCtx / 4);
       // agent-scope stores (sc1, written through to the fabric), completed before the flag:
       // an agent release fence here wrote back the whole L2 of the XCD for every row, which
@@ -1060,45 +1078,38 @@ __global__ void __launch_bounds__(64) k_ent_ac(EntropyArgs a) {
 // The WPP storage after CTB 1 (9.3.2.4) goes from lane b of wave r - 1 to lane b of wave r
 // through global memory (agent-scope stores / loads + flag, as above).
 //
-// Every lane executes one coder OPERATION (one token) per iteration -- a context-coded bin
-// (terminating bins are context bins on kTermCtx) or a bypass run of up to kBypRun (8) bins --
-// in one branch-free form:
+// Every lane executes one coder OPERATION per iteration -- a context-coded bin, a bypass run
+// of up to 16 bins, or a terminating bin -- in one branch-free form:
 //   low = ((low << pre) + add) << post,  range = nr << post,  bits_left -= pre + post,
 //   post = clz(nr) - 23
 // (bypass: pre = n, add = range * bins, nr = range; context bin: pre = 0, add = LPS ? range -
-// rLPS : 0, nr = LPS ? rLPS : range - rLPS).  An operation adds at most 8 bits, so after it
-// bits_left >= 4 and one CabacEncoder::write_out restores >= 12; bytes depend only on the
-// sequence of interval updates, so the output is the host writer's byte for byte.
+// rLPS : 0, nr = LPS ? rLPS : range - rLPS; terminate: pre = 0, add = bin ? range - 2 : 0, nr =
+// bin ? 2 : range - 2).  `low` is 64-bit so a whole 16-bin bypass run fits before the byte
+// output (CabacEncoder::write_out, at most twice per operation).  Bytes depend only on the
+// sequence of interval updates, not on when they are written out, so the output is the host
+// writer's byte for byte.
 //
-// Inside a block of kLnBlock iterations a lane touches no global memory: contexts, tokens and
-// output bytes all live in LDS.  At a block boundary the wave waits for the loads / stores it
-// issued at the previous boundary (long since complete), moves the prefetched tokens into the
-// ring, issues the next prefetch and stores the block's output bytes.  (On CDNA a vmcnt wait
-// also waits for stores, so a global access inside the loop would serialise on store latency.)
-// LDS per wave ~21 KB: contexts as bytes [ctx / 4][lane][ctx % 4] (the token carries the
-// context's byte offset; a lane's reads land in bank lane % 32 whatever the context:
-// conflict-free), the token ring [slot][lane], the output staging [dword][lane], the
-// rLPS / transIdxLps table {rLPS of the 4 range quarters, transIdx} per state.
-constexpr int kLnRing = 32;  // token slots per lane
-constexpr int kLnRefill = 8;
-constexpr int kLnBlock = 8;   // iterations per block (<= kLnRefill: one token each)
-constexpr int kLnOut = 16;    // staged output dwords per lane (<= 1 byte per op + rare runs)
-constexpr int kLnCtxW = kCtxSlots / 4;  // context dwords per lane
+// LDS, per wave: the context states as [ctx][lane] dwords (a lane's reads hit bank lane % 32
+// whatever the context: conflict-free), a per-lane token ring [slot][lane] refilled 16 tokens
+// at a time one block of iterations ahead (the dwordx4 loads of block k are stored into the
+// ring at block k + 1, so their latency hides behind 8 iterations), and the rLPS / transIdxLps
+// tables (rLPS of the four range quarters packed in one dword per state).
+constexpr int kLnRing = 64;  // token slots per lane
+constexpr int kLnRefill = 16;
+constexpr int kLnBlock = 8;  // iterations between refills (<= kLnRefill / tokens per iteration)
 
 __global__ void __launch_bounds__(64) k_ent_ac_lanes(EntropyArgs a, int B) {
-  __shared__ uint32_t ctxL[kLnCtxW * 64];
+  __shared__ uint32_t ctxL[kEntCtx * 64];
   __shared__ uint32_t ring[kLnRing * 64];
-  __shared__ uint32_t outL[kLnOut * 64];
-  __shared__ uint2 tab[64];
-  uint8_t* ctx8 = reinterpret_cast<uint8_t*>(ctxL);
-  uint8_t* out8 = reinterpret_cast<uint8_t*>(outL);
+  __shared__ uint32_t lps4[64], tl[64];
   const int lane = threadIdx.x, row = blockIdx.x;
   const int b = blockIdx.y * 64 + lane;
   {
     uint32_t v = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) v |= (uint32_t)a.tab->lps[lane * 4 + q] << (8 * q);
-    tab[lane] = make_uint2(v, a.tab->tlps[lane]);
+    lps4[lane] = v;
+    tl[lane] = a.tab->tlps[lane];
   }
   const int wc = a.g.wc, hc = a.g.hc, nctu = wc * hc;
   bool active = b < B;
@@ -1125,7 +1136,7 @@ __global__ void __launch_bounds__(64) k_ent_ac_lanes(EntropyArgs a, int B) {
   const int* off = a.ctb_off + (long)(active ? b : 0) * nctu;
   const long tpos = tbase + off[row * wc];
   const long tend = row + 1 < hc ? tbase + off[(row + 1) * wc] : tbase + stok;
-  uint8_t* gout = a.stage + stage_off(tpos, (long)(active ? b : 0) * hc + row);  // 4-aligned
+  uint32_t* out = reinterpret_cast<uint32_t*>(a.stage + stage_off(tpos, (long)(active ? b : 0) * hc + row));
   const unsigned long long w0 = wall_clock64();
   // WPP: wait for the row above of every lane's segment (rows of a picture progress together)
   if (row > 0) {
@@ -1147,160 +1158,153 @@ __global__ void __launch_bounds__(64) k_ent_ac_lanes(EntropyArgs a, int B) {
         __builtin_amdgcn_s_sleep(127);
     }
   }
-  // contexts: row 0 from the init table, else the row above's after its CTB 1; then the
-  // terminate context (state 63, MPS 0) and the dummy
+  // contexts: row 0 from the init table, else the row above's after its CTB 1
   if (active) {
-    const uint32_t* src = row == 0
-                              ? reinterpret_cast<const uint32_t*>(a.tab->init[a.pic.init_type][clip3(0, 51, (int)a.dec.qp[b])])
-                              : reinterpret_cast<const uint32_t*>(a.wctx + ((long)b * hc + row - 1) * kEntCtx);
-    uint32_t t[kEntCtx / 4];
+    if (row == 0) {
+      const uint8_t* src = a.tab->init[a.pic.init_type][clip3(0, 51, (int)a.dec.qp[b])];
+      for (int c = 0; c < kEntCtx; c += 4) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(src + c);
 #pragma unroll
-    for (int i = 0; i < kEntCtx / 4; ++i)
-      t[i] = row == 0 ? src[i] : __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int q = 0; q < 4; ++q) ctxL[(c + q) * 64 + lane] = (w >> (8 * q)) & 255;
+      }
+    } else {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wctx + ((long)b * hc + row - 1) * kEntCtx);
+      uint32_t t[kEntCtx / 4];
 #pragma unroll
-    for (int i = 0; i < kEntCtx / 4; ++i) ctxL[i * 64 + lane] = t[i];
-    ctxL[(kEntCtx / 4) * 64 + lane] = 63u;
+      for (int i = 0; i < kEntCtx / 4; ++i) t[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < kEntCtx / 4; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ctxL[(4 * i + q) * 64 + lane] = (t[i] >> (8 * q)) & 255;
+    }
   }
-  // token ring: 2 x kLnRefill tokens now, then kLnRefill per block, one block ahead
+  // token ring: 32 tokens now, then 16 per block one block ahead
   const uint4* gtok = reinterpret_cast<const uint4*>(a.tokens);
-  int head = (int)(tpos & 3);  // ring positions relative to tpos & ~3 (32-bit arithmetic)
-  int tail = 0;
-  const int tlim = (int)(tend - (tpos & ~3L));  // one past the row's last token
-  const uint4* gt = gtok + (tpos >> 2);
-  auto ring_put = [&](int at, const uint4& v) {
-    const int s0 = at & (kLnRing - 1);
-    ring[(s0 + 0) * 64 + lane] = v.x;
-    ring[(s0 + 1) * 64 + lane] = v.y;
-    ring[(s0 + 2) * 64 + lane] = v.z;
-    ring[(s0 + 3) * 64 + lane] = v.w;
-  };
+  long head = tpos, tail = tpos & ~3L;
   if (active) {
-    uint4 v[2 * kLnRefill / 4];
+    uint4 v[8];
 #pragma unroll
-    for (int k = 0; k < 2 * kLnRefill / 4; ++k) v[k] = gt[k];
+    for (int k = 0; k < 8; ++k) v[k] = gtok[(tail >> 2) + k];
 #pragma unroll
-    for (int k = 0; k < 2 * kLnRefill / 4; ++k) ring_put(4 * k, v[k]);
-    tail = 2 * kLnRefill;
+    for (int k = 0; k < 8; ++k) {
+      const int s0 = (int)((tail + 4 * k) & (kLnRing - 1));
+      ring[(s0 + 0) * 64 + lane] = v[k].x;
+      ring[(s0 + 1) * 64 + lane] = v[k].y;
+      ring[(s0 + 2) * 64 + lane] = v[k].z;
+      ring[(s0 + 3) * 64 + lane] = v[k].w;
+    }
+    tail += 32;
   }
   __syncthreads();  // tables (every lane wrote one entry)
-  __builtin_amdgcn_s_setprio(3);  // a latency-bound chain beside the analysis waves on its SIMD
-  // coder state (CabacEncoder)
-  uint32_t low = 0, range = 510, buffered = 0xff;
-  int bl = 23, nbuf = 0;
-  int opos = 0;   // output bytes staged in outL (global position gpos + opos)
-  int gpos = 0;   // output bytes stored to global memory (a multiple of 4)
+  // coder state (CabacEncoder), low widened to 64 bits
+  unsigned long long low = 0;
+  uint32_t range = 510, buffered = 0xff, ow = 0;
+  int bl = 23, nbuf = 0, pos = 0;
+  int sub = 0;  // next bin of a context token
+  long left = tend - tpos;  // tokens this substream may still consume
   bool synced = false;
   uint32_t tok = active ? ring[(head & (kLnRing - 1)) * 64 + lane] : 0;
-  int nctx = 0, ntoks = 0;
+  long nctxbins = 0, ntoks = 0;
   const unsigned long long w1 = wall_clock64(), c1 = clock64();
-  const int lane4 = lane * 4;
-  auto put = [&](uint32_t byte) {  // conflict-free staging: byte k at [k / 4][lane][k % 4]
-    out8[(opos >> 2) * 256 + lane4 + (opos & 3)] = (uint8_t)byte;
-    ++opos;
-  };
-  // staged whole dwords -> global; a partial last dword moves to the front of the staging
-  auto flush_out = [&](bool all) {
-    const int nd = all ? (opos + 3) >> 2 : opos >> 2;
-    uint32_t* g32 = reinterpret_cast<uint32_t*>(gout + gpos);
-    for (int k = 0; k < nd; ++k) g32[k] = outL[k * 64 + lane];
-    if (!all && nd) {
-      outL[lane] = outL[nd * 64 + lane];
-      gpos += 4 * nd;
-      opos -= 4 * nd;
+  auto put = [&](uint32_t byte) {
+    ow |= (byte & 255) << (8 * (pos & 3));
+    if ((++pos & 3) == 0) {
+      out[(pos >> 2) - 1] = ow;
+      ow = 0;
     }
   };
   uint4 pend[kLnRefill / 4];
   bool pending = false;
   while (__any(active)) {
-    // ---- block boundary: everything issued at the previous boundary has landed ----
-    if (active) {
-      if (pending) {
+    if (active && pending) {  // the block-ahead refill lands in the ring
 #pragma unroll
-        for (int k = 0; k < kLnRefill / 4; ++k) ring_put(tail + 4 * k, pend[k]);
-        tail += kLnRefill;
+      for (int k = 0; k < kLnRefill / 4; ++k) {
+        const int s0 = (int)((tail + 4 * k) & (kLnRing - 1));
+        ring[(s0 + 0) * 64 + lane] = pend[k].x;
+        ring[(s0 + 1) * 64 + lane] = pend[k].y;
+        ring[(s0 + 2) * 64 + lane] = pend[k].z;
+        ring[(s0 + 3) * 64 + lane] = pend[k].w;
       }
-      pending = tail - head <= kLnRing - 2 * kLnRefill && tail < tlim;
-      if (pending) {
-#pragma unroll
-        for (int k = 0; k < kLnRefill / 4; ++k) pend[k] = gt[(tail >> 2) + k];
-      }
-      if (opos >= 4) flush_out(false);
+      tail += kLnRefill;
     }
-    for (int it = 0; it < kLnBlock && active; ++it) {
-      if (head >= tlim) {  // the row's tokens ran out without a FLUSH (corrupt token stream)
-        abort_lane(4);
-        break;
-      }
-      const uint32_t ntok = ring[((head + 1) & (kLnRing - 1)) * 64 + lane];  // read while this op runs
-      const bool isB = (tok >> 30) != 0;  // bypass, or a control token (n = 0, bins = 0)
-      const int ca = (isB ? (int)ctx_off(kDummyCtx) : (int)(tok & 0x3fffu)) + lane4;
-      const uint32_t sv = ctx8[ca];
+    pending = active && tail - head <= kLnRing - 2 * kLnRefill && tail < tend;
+    if (pending) {
+#pragma unroll
+      for (int k = 0; k < kLnRefill / 4; ++k) pend[k] = gtok[(tail >> 2) + k];
+    }
+    for (int it = 0; it < kLnBlock; ++it) {
+      if (!active) break;
+      const uint32_t ty = tok >> 30;
+      const bool isC = ty == 0, isB = ty == 1, isT = ty == 2;
+      const int nbins = (tok >> 27) & 3;
+      const bool more = isC && sub + 1 < nbins;  // the token has another bin after this one
+      // the next token, read while this operation runs
+      const uint32_t ntok = ring[((head + 1) & (kLnRing - 1)) * 64 + lane];
+      const uint32_t f = (tok >> (9 * sub)) & 511;
+      const int c = isC ? (int)(f & 255) : 0;
+      const uint32_t sv = ctxL[c * 64 + lane];
       const uint32_t st = sv & 63, mps = (sv >> 6) & 1;
-      const uint2 tb2 = tab[st];
-      const uint32_t lp = (tb2.x >> ((range >> 3) & 24)) & 255;
+      const uint32_t lp = (lps4[st] >> (8 * ((range >> 6) & 3))) & 255;
+      const uint32_t tlp = tl[st];
       const uint32_t rmps = range - lp;
-      const bool lpsb = ((tok >> 14) & 1) != mps;
-      const uint32_t nr = isB ? range : (lpsb ? lp : rmps);
-      const uint32_t add = isB ? __umul24(range, tok & 255u) : (lpsb ? rmps : 0u);
-      const uint32_t prs = isB ? (tok >> 8) & 15 : 0u;
-      const uint32_t post = (uint32_t)__clz(nr) - 23;
+      const bool lpsb = isC && (f >> 8) != mps;
+      const uint32_t tb = tok & 1;
+      const int bn = (tok >> 16) & 31;
+      const uint32_t nr = isC ? (lpsb ? lp : rmps) : isT ? (tb ? 2u : range - 2) : range;
+      const unsigned long long add = isC ? (lpsb ? rmps : 0u) : isT ? (tb ? range - 2 : 0u)
+                                   : isB ? (unsigned long long)range * (tok & 0xffffu) : 0ull;
+      const int prs = isB ? bn : 0;
+      const int post = __clz(nr) - 23;
       low = ((low << prs) + add) << post;
       range = nr << post;
-      bl -= (int)(prs + post);
-      // context update (non-context operations write the dummy slot)
-      const uint32_t nst = lpsb ? tb2.y : (st < 62 ? st + 1 : st);
-      ctx8[ca] = (uint8_t)(nst | ((mps ^ (lpsb && st == 0 ? 1u : 0u)) << 6));
-      if (bl < 12) {  // CabacEncoder::write_out (once: an operation adds <= 8 bits)
-        const uint32_t lead = low >> (24 - bl);
+      bl -= prs + post;
+      if (isC) {
+        const uint32_t nsv = lpsb ? (tlp | ((mps ^ (st == 0 ? 1u : 0u)) << 6)) : ((st < 62 ? st + 1 : st) | (mps << 6));
+        ctxL[c * 64 + lane] = nsv;
+        ++nctxbins;
+      }
+      while (bl < 12) {  // CabacEncoder::write_out (bl >= -4 here: <= 16 bits per operation)
+        const uint32_t lead = (uint32_t)(low >> (24 - bl));
         bl += 8;
-        low &= 0xffffffffu >> bl;
-        if (lead != 0xff) {
-          if (nbuf > 0) {
-            const uint32_t carry = lead >> 8;
-            put(buffered + carry);
-            if (nbuf > 1) {  // a run of outstanding 0xff bytes (rare)
-              const uint32_t byte = (0xff + carry) & 0xff;
-              for (; nbuf > 1; --nbuf) {
-                put(byte);
-                if (opos >= 4 * kLnOut - 4) flush_out(false);
-              }
-            }
-          }
-          nbuf = 1;
-          buffered = lead & 0xff;
-        } else {
+        low &= (1ull << (32 - bl)) - 1;
+        if (lead == 0xff) {
           nbuf++;
+        } else if (nbuf > 0) {
+          const uint32_t carry = lead >> 8;
+          put(buffered + carry);
+          buffered = lead & 0xff;
+          const uint32_t byte = (0xff + carry) & 0xff;
+          for (; nbuf > 1; --nbuf) put(byte);
+        } else {
+          nbuf = 1;
+          buffered = lead;
         }
       }
-      if ((tok >> 30) == 3) {
-        if (((tok >> 16) & 3) == kCtrlSync) {  // 9.3.2.4 storage for the row below
+      if (ty == 3) {
+        if ((tok & 0xff) == kCtrlSync) {  // 9.3.2.4 storage for the row below
           uint32_t* dst = reinterpret_cast<uint32_t*>(a.wctx + ((long)b * hc + row) * kEntCtx);
           uint32_t t[kEntCtx / 4];
 #pragma unroll
-          for (int i = 0; i < kEntCtx / 4; ++i) t[i] = ctxL[i * 64 + lane];
+          for (int i = 0; i < kEntCtx / 4; ++i)
+            t[i] = ctxL[(4 * i) * 64 + lane] | ctxL[(4 * i + 1) * 64 + lane] << 8 | ctxL[(4 * i + 2) * 64 + lane] << 16 |
+                   ctxL[(4 * i + 3) * 64 + lane] << 24;
 #pragma unroll
           for (int i = 0; i < kEntCtx / 4; ++i) __hip_atomic_store(dst + i, t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           synced = true;
         } else {  // finish() + '1' + byte alignment (end_of_subset_one_bit / slice trailing bits)
-          if ((low >> (32 - bl)) != 0) {
+          const unsigned long long top = 1ull << (32 - bl);
+          if (low >= top) {
             put(buffered + 1);
-            for (; nbuf > 1; --nbuf) {
-              put(0x00);
-              if (opos >= 4 * kLnOut - 4) flush_out(false);
-            }
-            low -= 1u << (32 - bl);
+            for (; nbuf > 1; --nbuf) put(0x00);
+            low -= top;
           } else {
             if (nbuf > 0) put(buffered);
-            for (; nbuf > 1; --nbuf) {
-              put(0xff);
-              if (opos >= 4 * kLnOut - 4) flush_out(false);
-            }
+            for (; nbuf > 1; --nbuf) put(0xff);
           }
-          if (opos >= 4 * kLnOut - 4) flush_out(false);
           const int nb = 24 - bl;  // 1..12 bits of low >> 8, then the '1', then zeros
-          uint32_t v = (((low >> 8) & ((1u << nb) - 1)) << 1) | 1u;
+          uint32_t v = ((((uint32_t)low >> 8) & ((1u << nb) - 1)) << 1) | 1u;
           int t = nb + 1;
           const int pad = (8 - (t & 7)) & 7;
           v <<= pad;
@@ -1309,9 +1313,9 @@ __global__ void __launch_bounds__(64) k_ent_ac_lanes(EntropyArgs a, int B) {
             t -= 8;
             put((v >> t) & 0xff);
           }
-          const int total = gpos + opos;
-          flush_out(true);  // the slack after the last byte is never read (row_bytes)
-          a.row_bytes[(long)b * hc + row] = total;
+          uint8_t* o8 = reinterpret_cast<uint8_t*>(out);
+          for (int k = pos & ~3; k < pos; ++k) o8[k] = (uint8_t)(ow >> (8 * (k & 3)));
+          a.row_bytes[(long)b * hc + row] = pos;
           if (!synced) {
             abort_lane(4);  // a substream that never stored its contexts (corrupt stream)
           } else {
@@ -1319,8 +1323,8 @@ __global__ void __launch_bounds__(64) k_ent_ac_lanes(EntropyArgs a, int B) {
           }
           if (a.dbg) {  // TV_ENT_DEBUG: rows, context bins, tokens, coding clocks, wait ticks, max row span
             atomicAdd(&a.dbg[0], 1ull);
-            atomicAdd(&a.dbg[1], (unsigned long long)nctx);
-            atomicAdd(&a.dbg[2], (unsigned long long)(ntoks + 1));
+            atomicAdd(&a.dbg[1], (unsigned long long)nctxbins);
+            atomicAdd(&a.dbg[2], (unsigned long long)ntoks);
             atomicAdd(&a.dbg[3], clock64() - c1);
             atomicAdd(&a.dbg[4], w1 - w0);
             atomicMax(&a.dbg[5], wall_clock64() - w0);
@@ -1328,10 +1332,18 @@ __global__ void __launch_bounds__(64) k_ent_ac_lanes(EntropyArgs a, int B) {
           break;
         }
       }
-      nctx += isB ? 0 : 1;
-      ++ntoks;
-      ++head;
-      tok = ntok;
+      if (more) {
+        ++sub;
+      } else {
+        sub = 0;
+        ++head;
+        ++ntoks;
+        tok = ntok;
+        if (--left <= 0) {  // no FLUSH before the row's tokens ran out
+          abort_lane(4);
+          break;
+        }
+      }
     }
   }
 }
