@@ -1416,13 +1416,14 @@ void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s) {
     const int v = e ? std::atoi(e) : 1;
     return v < 1 ? 1 : v > 8 ? 8 : v;
   }();
-  // TV_ENT_CODER=wave: the single-lane coder (one wave per substream), for A/B measurements
-  static const bool wave_coder = [] {
-    const char* e = std::getenv("TV_ENT_CODER");
-    return e && std::string(e) == "wave";
-  }();
+  // TV_ENT_CODER=lanes: the lane-per-substream coder (one wave per CTB row index, one lane per
+  // segment) -- byte-exact, 24x fewer waves, but ~1300 clocks per operation against ~610 per
+  // bin here, so a picture's substreams take ~2x longer and the slot pipeline stalls
+  // (profiles/README.md, round 6).  The single-lane wave coder stays the default.
+  const char* ce = std::getenv("TV_ENT_CODER");  // per launch (tests switch it)
+  const bool lane_coder = ce && std::string(ce) == "lanes";
   (void)hipMemsetAsync(a.wflag, 0, (size_t)B * a.g.hc * sizeof(int), s);
-  if (wave_coder)
+  if (!lane_coder)
     k_ent_ac<<<dim3((a.g.hc + rpw - 1) / rpw, B), 64, 0, s>>>(a);
   else
     k_ent_ac_lanes<<<dim3(a.g.hc, (B + 63) / 64), 64, 0, s>>>(a, B);

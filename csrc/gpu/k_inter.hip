@@ -46,7 +46,7 @@ namespace gpu {
 #define TV_ME_THREADS 256
 #endif
 constexpr int kMeThreads = TV_ME_THREADS;  // a multiple of 64 (the DPP group sums assume it)
-static_assert(kMeThreads % 64 == 0 && kMeThreads >= 256, "k_inter_me block size");
+static_assert(kMeThreads % 64 == 0 && kMeThreads >= 256 && 768 % kMeThreads == 0, "k_inter_me block size (the sub-pel passes need a uniform trip count)");
 constexpr int kFRows = kCtb + kMeWinH - 1;  // 38 window rows per candidate
 constexpr int kFWords = 12;                 // 48 bytes staged (40 used: 32 + 7 offsets + 1)
 constexpr int kFChunks = kFWords / 4;       // 16-byte chunks per staged row
@@ -324,24 +324,27 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   const int last_step = skip_sub ? 4 : (diag_stop == 3 ? 2 : 1);
   for (int step = 2; step >= last_step; step >>= 1) {
     __syncthreads();  // bmv of the previous step / the integer search
-    // A thread owns a group of 8 rows x 8 pixels of one (block, candidate): per row it loads
+    // A thread owns a group of 4 rows x 8 pixels of one (block, candidate): per row it loads
     // 3 aligned dwords of the phase plane, forms the 2 shifted dwords with v_alignbyte and
-    // accumulates with v_sad_u8.  Groups per candidate: 16 (8x8) + 16 (16x16) + 16 (32x32).
-    for (int grp = tid; grp < 8 * 48; grp += kMeThreads) {
-      const int k = grp / 48, r = grp - k * 48;
+    // accumulates with v_sad_u8.  Groups per candidate: 32 (8x8) + 32 (16x16) + 32 (32x32),
+    // 768 in all = exactly 3 per thread (8-row groups were 384 = 1.5 per thread: half the
+    // threads ran a second pass of 8 rows while the others idled at the barrier).
+    for (int grp = tid; grp < 8 * 96; grp += kMeThreads) {
+      const int k = grp / 96, r = grp - k * 96;
       int bi, row0, col0;
-      if (r < 16) {
-        bi = r;
-        row0 = col0 = 0;
-      } else if (r < 32) {
-        const int q = (r - 16) & 3;
-        bi = 16 + ((r - 16) >> 2);
-        row0 = 8 * (q >> 1);
+      if (r < 32) {
+        bi = r >> 1;
+        row0 = 4 * (r & 1);
+        col0 = 0;
+      } else if (r < 64) {
+        const int q = (r - 32) & 7;
+        bi = 16 + ((r - 32) >> 3);
+        row0 = 4 * (q >> 1);
         col0 = 8 * (q & 1);
       } else {
-        const int q = r - 32;
+        const int q = r - 64;
         bi = 20;
-        row0 = 8 * (q >> 2);
+        row0 = 4 * (q >> 2);
         col0 = 8 * (q & 3);
       }
       int bx, by, l2b;
@@ -354,11 +357,11 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       const int gy0 = cy + by + row0 + (my >> 2);
       const int sr0 = by + row0, sw0 = (bx + col0) >> 2;  // source row / word of row 0
       unsigned sad = 0;
-      if (gx0 >= -8 && gx0 + 11 <= g.W + 7 && gy0 >= -8 && gy0 + 7 <= g.H + 7) {
+      if (gx0 >= -8 && gx0 + 11 <= g.W + 7 && gy0 >= -8 && gy0 + 3 <= g.H + 7) {
         const int a = gx0 & ~3, sh = gx0 & 3;
         const uint8_t* rowp = P + (long)(gy0 + 8) * g.pw16 + a + 8;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4; ++j) {
           const uint32_t* wp = reinterpret_cast<const uint32_t*>(rowp + (long)j * g.pw16);
           const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
           const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
@@ -367,7 +370,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
           sad = __builtin_amdgcn_sad_u8(hi, s32[sw + 1], __builtin_amdgcn_sad_u8(lo, s32[sw], sad));
         }
       } else {  // touches the clamped border: per-pixel path
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4; ++j) {
           const int gy = clip3(-8, g.H + 7, gy0 + j);
           for (int i = 0; i < 8; ++i) {
             const int gx = clip3(-8, g.W + 7, gx0 + i);
@@ -375,19 +378,20 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
           }
         }
       }
-      // group sums on the VALU instead of LDS atomics (r < 16: one 8x8 group per block;
-      // 16..31: 4 aligned lanes per 16x16 block; 32..47: one aligned 16-lane row per 32x32)
-      // -- every (block, candidate) cell is written exactly once, by a plain store
-      int q4 = (int)sad;
-      q4 += dpp::mov<dpp::kQuadXor1>(q4);
-      q4 += dpp::mov<dpp::kQuadXor2>(q4);
-      int s16 = q4 + dpp::mov<dpp::kRowHalfMirror>(q4);
-      s16 += dpp::mov<dpp::kRowMirror>(s16);
-      if (r < 16) subsad[bi][k] = (int)sad;
-      else if (r < 32) {
-        if (((r - 16) & 3) == 0) subsad[bi][k] = q4;
-      } else if (r == 32) {
-        subsad[bi][k] = s16;
+      // group sums on the VALU (every lane runs all three passes, so the wave is full):
+      // pairs = an 8x8 block, aligned 8-lane groups = a 16x16 block, aligned 32-lane groups =
+      // the 32x32 block -- every (block, candidate) cell is written exactly once, by a store
+      int s2 = (int)sad + dpp::mov<dpp::kQuadXor1>((int)sad);
+      int s8 = s2 + dpp::mov<dpp::kQuadXor2>(s2);
+      s8 += dpp::mov<dpp::kRowHalfMirror>(s8);
+      int s32v = s8 + dpp::mov<dpp::kRowMirror>(s8);
+      s32v += __shfl_xor(s32v, 16, 64);
+      if (r < 32) {
+        if (!(r & 1)) subsad[bi][k] = s2;
+      } else if (r < 64) {
+        if (((r - 32) & 7) == 0) subsad[bi][k] = s8;
+      } else if (r == 64) {
+        subsad[bi][k] = s32v;
       }
     }
     __syncthreads();

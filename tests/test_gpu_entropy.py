@@ -142,6 +142,21 @@ def test_two_coder_lanes_dense_routing_is_byte_identical(monkeypatch):
     assert segs == _golden(seed, [0, 9, 30], w, h, gop, qp=22, search_range=rng, sao=True)
 
 
+def test_lane_coder_is_byte_identical(monkeypatch):
+    """TV_ENT_CODER=lanes (one wave per CTB row index, one lane per segment, the WPP hand-off
+    between waves) codes the same bytes as the host writer on I / P pictures with SAO and on
+    textured content."""
+    monkeypatch.setenv("TV_ENT_CODER", "lanes")
+    for seed, qp in ((5, 27), (3 | 0x80000000, 22)):
+        w, h, gop, rng = 256, 160, 5, 16
+        eng = _engine(width=w, height=h, qp=qp, batch=3, gop=gop, search_range=rng, seed=seed, sao=True)
+        segs = eng.encode_synthetic([0, 7, 20])
+        st = eng.entropy_stats()
+        eng.close()
+        assert st["fallbacks"] == 0, st
+        assert segs == _golden(seed, [0, 7, 20], w, h, gop, qp=qp, search_range=rng, sao=True)
+
+
 def test_hybrid_entropy_routes_pictures_to_the_host(monkeypatch):
     """TV_ENT_HOST=n: while fewer than n pictures sit in the host writer pool the next one is
     coded there instead of on the GPU; the stream is the same either way."""
