@@ -14,6 +14,7 @@
 //  k_inter_recon  pass B per CTB: luma prediction = phase-plane loads, chroma 4-tap MC,
 //                 residual, MFMA transform/quant, exact inverse, reconstruction.
 #include <cstdlib>
+#include <string>
 
 #include "gpu_common.h"
 #include "k_encode.h"
@@ -46,7 +47,7 @@ namespace gpu {
 #define TV_ME_THREADS 256
 #endif
 constexpr int kMeThreads = TV_ME_THREADS;  // a multiple of 64 (the DPP group sums assume it)
-static_assert(kMeThreads % 64 == 0 && kMeThreads >= 256 && 768 % kMeThreads == 0, "k_inter_me block size (the sub-pel passes need a uniform trip count)");
+static_assert(kMeThreads % 64 == 0 && kMeThreads >= 256, "k_inter_me block size");
 constexpr int kFRows = kCtb + kMeWinH - 1;  // 38 window rows per candidate
 constexpr int kFWords = 12;                 // 48 bytes staged (40 used: 32 + 7 offsets + 1)
 constexpr int kFChunks = kFWords / 4;       // 16-byte chunks per staged row
@@ -173,7 +174,14 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
   }
 }
 
-__global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
+// ROWS: rows per sub-pel SAD group, 8 (384 groups) or 4 (768 groups, 3 per thread: measured
+// 10 % slower -- a third pass exposes its load latency once more).  PEN_LDS: the MV-rate table
+// (Penalties::mv, 64 ints) staged in LDS -- the integer search and the sub-pel argmin read it
+// per candidate, which from global memory put a dependent load chain between the barriers.
+// WPE: waves per SIMD the register allocation must allow (8: <= 64 VGPRs, 8 CTBs per CU --
+// with the 7.8 KB quadrant table gone the LDS fits 8 as well; 7 = the compiler's own 70 VGPRs).
+template <int ROWS, bool PEN_LDS, int WPE>
+__global__ void __launch_bounds__(kMeThreads) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_inter_me(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                          DecisionSet dec, const int16_t* prev_mv, const int16_t* cmv,
                                                          Geo g, const RcTables* rc, int range, int diag_stop,
                                                          CtbMeOut* bout, PIntraBuffers pi) {
@@ -181,6 +189,9 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   int ctu, b;
   xcd_ctb(ctu, b);
   const Penalties& pen = rc->pen[dec.qp[b]];
+  __shared__ int penL[64];
+  if (PEN_LDS && tid < 64) penL[tid] = pen.mv[tid];
+  const int* penmv = PEN_LDS ? penL : pen.mv;  // visible after the first barrier below
   const int cxi = ctu % g.wc, cyi = ctu / g.wc, cx = cxi * 32, cy = cyi * 32;
   const uint8_t* S = src.plane(0, b, g);
   const uint8_t* R = ref.plane(0, b, g);
@@ -191,9 +202,6 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   __shared__ unsigned best[21];
   __shared__ int bcost[21], bmv[21][2];
   __shared__ int subsad[21][8];
-  // per position: the 4 quadrant 16x16 SADs, row stride 5 (odd): the quadrant lanes of 8
-  // items write 32 distinct banks (stride 4 put them on 8 banks: 4-way conflicts)
-  __shared__ int sad16[kMeMaxCand * kMePosPerCand][5];
   for (int t = tid; t < 256; t += kMeThreads)
     s32[src_word(t >> 3, t & 7)] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (t >> 3)) * g.W + cx + 4 * (t & 7));
   if (tid == 0) {
@@ -233,11 +241,14 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   // ------------------------------- integer refinement -----------------------------------
   // item = (candidate, window row, 4-position group, 16x16 quadrant): a lane accumulates
   // the 4 8x8 SADs of its quadrant for 4 adjacent positions (their sum is the quadrant's
-  // 16x16 SAD); the 32x32 SADs are the sums of the 4 quadrants, formed after a barrier.
+  // 16x16 SAD); the 32x32 SADs are the sums of the 4 quadrants, which are the 4 lanes of a
+  // quad (items 4j..4j+3): a DPP quad sum, no LDS round trip (a [position][quadrant] LDS
+  // table cost 7.8 KB -- a CTB per CU of occupancy -- and a barrier).
   // Splitting by quadrant keeps every lane busy when few distinct candidates remain.
   unsigned lb[5];  // 4 8x8 blocks of my quadrant, then its 16x16
 #pragma unroll
   for (int k = 0; k < 5; ++k) lb[k] = 0xffffffffu;
+  unsigned lb32 = 0xffffffffu;  // the 32x32 minimum (quadrant-0 lanes)
   int qd = 0;
   for (int item = skip_int ? kMeThreads * 64 : tid; item < nc * kMeWinH * 2 * 4; item += kMeThreads) {
     qd = item & 3;
@@ -250,7 +261,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
 #pragma unroll
     for (int sft = 0; sft < 4; ++sft) {
       const int mx = cand[k][0] + kMeWinX0 + 4 * gs + sft;
-      mvc[sft] = (unsigned)pen.mv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])];
+      mvc[sft] = (unsigned)penmv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])];
     }
     const int qx = (qd & 1) * 16, qy = (qd >> 1) * 16;
 
@@ -285,7 +296,12 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
     for (int sft = 0; sft < 4; ++sft) {
       const unsigned v = ((q16[sft] + mvc[sft]) << 11) | (unsigned)(pos0 + sft);
       lb[4] = v < lb[4] ? v : lb[4];
-      sad16[pos0 + sft][qd] = (int)q16[sft];
+      // the quad's lanes are one position's 4 quadrants (a quad is always wholly in range)
+      int t = (int)q16[sft];
+      t += dpp::mov<dpp::kQuadXor1>(t);
+      t += dpp::mov<dpp::kQuadXor2>(t);
+      const unsigned v32 = ((unsigned)(t + (int)mvc[sft]) << 11) | (unsigned)(pos0 + sft);
+      lb32 = (qd == 0 && v32 < lb32) ? v32 : lb32;
     }
   }
   // a lane's quadrant is fixed (item stride is a multiple of 4), so lb[] maps to static slots
@@ -296,17 +312,8 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
     const unsigned m = wave_min_u32(qd == kq ? lb[kj] : 0xffffffffu);
     if ((tid & 63) == 0) atomicMin(&best[k], m);
   }
-  __syncthreads();
-  {  // 32x32 = the 4 quadrant SADs of a position
-    unsigned b32 = 0xffffffffu;
-    for (int p = skip_int ? kMeThreads * 64 : tid; p < nc * kMePosPerCand; p += kMeThreads) {
-      const int k = p / kMePosPerCand, r = p - k * kMePosPerCand;
-      const int mx = cand[k][0] + kMeWinX0 + (r % kMeWinW), my = cand[k][1] + kMeWinY0 + r / kMeWinW;
-      const unsigned t = (unsigned)(sad16[p][0] + sad16[p][1] + sad16[p][2] + sad16[p][3]);
-      const unsigned v = ((t + (unsigned)pen.mv[me_pen_index(4 * mx - pmv[0], 4 * my - pmv[1])]) << 11) | (unsigned)p;
-      b32 = v < b32 ? v : b32;
-    }
-    const unsigned m = wave_min_u32(b32);
+  {
+    const unsigned m = wave_min_u32(lb32);
     if ((tid & 63) == 0) atomicMin(&best[20], m);
   }
   __syncthreads();
@@ -324,27 +331,28 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
   const int last_step = skip_sub ? 4 : (diag_stop == 3 ? 2 : 1);
   for (int step = 2; step >= last_step; step >>= 1) {
     __syncthreads();  // bmv of the previous step / the integer search
-    // A thread owns a group of 4 rows x 8 pixels of one (block, candidate): per row it loads
-    // 3 aligned dwords of the phase plane, forms the 2 shifted dwords with v_alignbyte and
-    // accumulates with v_sad_u8.  Groups per candidate: 32 (8x8) + 32 (16x16) + 32 (32x32),
-    // 768 in all = exactly 3 per thread (8-row groups were 384 = 1.5 per thread: half the
-    // threads ran a second pass of 8 rows while the others idled at the barrier).
-    for (int grp = tid; grp < 8 * 96; grp += kMeThreads) {
-      const int k = grp / 96, r = grp - k * 96;
+    // A thread owns a group of ROWS rows x 8 pixels of one (block, candidate): per row it
+    // loads 3 aligned dwords of the phase plane, forms the 2 shifted dwords with v_alignbyte
+    // and accumulates with v_sad_u8.  ROWS = 4: 32 (8x8) + 32 (16x16) + 32 (32x32) groups per
+    // candidate, 768 in all = exactly 3 per thread; ROWS = 8: 384 = 1.5 per thread (half the
+    // threads run a second pass while the others wait at the barrier).
+    constexpr int G8 = 8 / ROWS, N8 = 16 * G8, NC = 3 * N8;  // groups per 8x8 block / class / candidate
+    for (int grp = tid; grp < 8 * NC; grp += kMeThreads) {
+      const int k = grp / NC, r = grp - k * NC;
       int bi, row0, col0;
-      if (r < 32) {
-        bi = r >> 1;
-        row0 = 4 * (r & 1);
+      if (r < N8) {
+        bi = r / G8;
+        row0 = ROWS * (r % G8);
         col0 = 0;
-      } else if (r < 64) {
-        const int q = (r - 32) & 7;
-        bi = 16 + ((r - 32) >> 3);
-        row0 = 4 * (q >> 1);
+      } else if (r < 2 * N8) {
+        const int q = (r - N8) % (4 * G8);
+        bi = 16 + (r - N8) / (4 * G8);
+        row0 = ROWS * (q >> 1);
         col0 = 8 * (q & 1);
       } else {
-        const int q = r - 64;
+        const int q = r - 2 * N8;
         bi = 20;
-        row0 = 4 * (q >> 2);
+        row0 = ROWS * (q >> 2);
         col0 = 8 * (q & 3);
       }
       int bx, by, l2b;
@@ -357,11 +365,11 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       const int gy0 = cy + by + row0 + (my >> 2);
       const int sr0 = by + row0, sw0 = (bx + col0) >> 2;  // source row / word of row 0
       unsigned sad = 0;
-      if (gx0 >= -8 && gx0 + 11 <= g.W + 7 && gy0 >= -8 && gy0 + 3 <= g.H + 7) {
+      if (gx0 >= -8 && gx0 + 11 <= g.W + 7 && gy0 >= -8 && gy0 + ROWS - 1 <= g.H + 7) {
         const int a = gx0 & ~3, sh = gx0 & 3;
         const uint8_t* rowp = P + (long)(gy0 + 8) * g.pw16 + a + 8;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < ROWS; ++j) {
           const uint32_t* wp = reinterpret_cast<const uint32_t*>(rowp + (long)j * g.pw16);
           const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
           const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
@@ -370,7 +378,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
           sad = __builtin_amdgcn_sad_u8(hi, s32[sw + 1], __builtin_amdgcn_sad_u8(lo, s32[sw], sad));
         }
       } else {  // touches the clamped border: per-pixel path
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < ROWS; ++j) {
           const int gy = clip3(-8, g.H + 7, gy0 + j);
           for (int i = 0; i < 8; ++i) {
             const int gx = clip3(-8, g.W + 7, gx0 + i);
@@ -378,20 +386,24 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
           }
         }
       }
-      // group sums on the VALU (every lane runs all three passes, so the wave is full):
-      // pairs = an 8x8 block, aligned 8-lane groups = a 16x16 block, aligned 32-lane groups =
-      // the 32x32 block -- every (block, candidate) cell is written exactly once, by a store
-      int s2 = (int)sad + dpp::mov<dpp::kQuadXor1>((int)sad);
-      int s8 = s2 + dpp::mov<dpp::kQuadXor2>(s2);
-      s8 += dpp::mov<dpp::kRowHalfMirror>(s8);
-      int s32v = s8 + dpp::mov<dpp::kRowMirror>(s8);
-      s32v += __shfl_xor(s32v, 16, 64);
-      if (r < 32) {
-        if (!(r & 1)) subsad[bi][k] = s2;
-      } else if (r < 64) {
-        if (((r - 32) & 7) == 0) subsad[bi][k] = s8;
-      } else if (r == 64) {
-        subsad[bi][k] = s32v;
+      // group sums on the VALU (a wave's lanes all run the same passes): aligned groups of G8
+      // lanes = an 8x8 block, 4 G8 = a 16x16 block, 16 G8 = the 32x32 block -- every
+      // (block, candidate) cell is written exactly once, by a plain store
+      int s1 = (int)sad;
+      if (G8 == 2) s1 += dpp::mov<dpp::kQuadXor1>(s1);
+      int s4 = s1 + dpp::mov<G8 == 2 ? dpp::kQuadXor2 : dpp::kQuadXor1>(s1);
+      if (G8 == 1) s4 += dpp::mov<dpp::kQuadXor2>(s4);
+      else s4 += dpp::mov<dpp::kRowHalfMirror>(s4);  // G8 = 2: 8 lanes
+      int s16 = s4;
+      if (G8 == 1) s16 += dpp::mov<dpp::kRowHalfMirror>(s16);
+      s16 += dpp::mov<dpp::kRowMirror>(s16);
+      if (G8 == 2) s16 += __shfl_xor(s16, 16, 64);
+      if (r < N8) {
+        if (r % G8 == 0) subsad[bi][k] = s1;
+      } else if (r < 2 * N8) {
+        if ((r - N8) % (4 * G8) == 0) subsad[bi][k] = s4;
+      } else if (r == 2 * N8) {
+        subsad[bi][k] = s16;
       }
     }
     __syncthreads();
@@ -402,7 +414,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
         me_cand_offset(k, ox, oy);
         const int mx = bmv[tid][0] + ox * step, my = bmv[tid][1] + oy * step;
         const unsigned v =
-            ((unsigned)(subsad[tid][k] + pen.mv[me_pen_index(mx - pmv[0], my - pmv[1])]) << 4) | (unsigned)(k + 1);
+            ((unsigned)(subsad[tid][k] + penmv[me_pen_index(mx - pmv[0], my - pmv[1])]) << 4) | (unsigned)(k + 1);
         bestv = v < bestv ? v : bestv;
       }
       const int kk = (int)(bestv & 15);
@@ -424,7 +436,7 @@ __global__ void __launch_bounds__(kMeThreads) k_inter_me(FrameSet src, FrameSet 
       o.cost[tid] = bcost[tid];
       o.mv[tid][0] = bmv[tid][0];
       o.mv[tid][1] = bmv[tid][1];
-      o.pen[tid] = pen.mv[me_pen_index(bmv[tid][0] - pmv[0], bmv[tid][1] - pmv[1])];
+      o.pen[tid] = penmv[me_pen_index(bmv[tid][0] - pmv[0], bmv[tid][1] - pmv[1])];
     }
     return;
   }
@@ -1071,6 +1083,23 @@ static int recon_tile_skip() {
   return v;
 }
 
+// Variants for same-box A/B measurements (same decisions): TV_ME_SUBPEL_ROWS=4 (768 sub-pel
+// groups), TV_ME_PEN=global (MV-rate table read from global memory), TV_ME_WPE=7 (the
+// compiler's register allocation: 7 CTBs per CU).
+using MeKernel = decltype(&k_inter_me<8, true, 8>);
+static MeKernel me_kernel() {
+  static const MeKernel k = [] {
+    const char* r = std::getenv("TV_ME_SUBPEL_ROWS");
+    const char* p = std::getenv("TV_ME_PEN");
+    const char* w = std::getenv("TV_ME_WPE");
+    const bool rows4 = r && std::atoi(r) == 4, glob = p && std::string(p) == "global", w7 = w && std::atoi(w) == 7;
+    if (rows4) return glob ? &k_inter_me<4, false, 8> : &k_inter_me<4, true, 8>;
+    if (w7) return glob ? &k_inter_me<8, false, 7> : &k_inter_me<8, true, 7>;
+    return glob ? &k_inter_me<8, false, 8> : &k_inter_me<8, true, 8>;
+  }();
+  return k;
+}
+
 void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameSet rec, DecisionSet dec,
                         const Geo& g, const RcTables* rc, int range, const MeBuffers& me, int B, hipStream_t s,
                         const PIntraBuffers* pi) {
@@ -1080,7 +1109,7 @@ void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameS
   }();
   const PIntraBuffers none{};
   if (pi && hipMemsetAsync(pi->count, 0, 6 * sizeof(int), s) != hipSuccess) return;
-  k_inter_me<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range,
+  me_kernel()<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range,
                                                          diag_stop, nullptr, pi ? *pi : none);
   if (pi) launch_pintra_decide(src, dec, g, rc, *pi, B, s);
   k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, recon_tile_skip(), FrameSet{},
@@ -1094,8 +1123,8 @@ void launch_inter_frame_b(FrameSet src, FrameSet ref0, const uint8_t* phase0, Fr
   const dim3 grid(g.wc * g.hc, B);
   CtbMeOut* o1 = meout + (long)B * g.wc * g.hc;
   const PIntraBuffers none{};
-  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref0, phase0, dec, me0.prev_mv, me0.cmv, g, rc, range[0], 0, meout, none);
-  k_inter_me<<<grid, kMeThreads, 0, s>>>(src, ref1, phase1, dec, me1.prev_mv, me1.cmv, g, rc, range[1], 0, o1, none);
+  me_kernel()<<<grid, kMeThreads, 0, s>>>(src, ref0, phase0, dec, me0.prev_mv, me0.cmv, g, rc, range[0], 0, meout, none);
+  me_kernel()<<<grid, kMeThreads, 0, s>>>(src, ref1, phase1, dec, me1.prev_mv, me1.cmv, g, rc, range[1], 0, o1, none);
   k_bi_decide<<<grid, 256, 0, s>>>(src, phase0, phase1, meout, o1, dec, g, rc);
   k_inter_recon<<<grid, 256, 0, s>>>(src, ref0, phase0, rec, dec, g, recon_tile_skip(), ref1, phase1);
 }
