@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(256) k_phase_planes(FrameSet ref, uint8_t* pha
 }
 
 // ------------------------------------ deblocking ----------------------------------------
-__global__ void __launch_bounds__(256) k_deblock(FrameSet rec, DecisionSet dec, Geo g, int horizontal) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_deblock(FrameSet rec, DecisionSet dec, Geo g, int horizontal) {
   const int b = blockIdx.y;
   const int qp = dec.qp[b];
   const long ub = b * g.usz;

@@ -204,13 +204,35 @@ __global__ void __launch_bounds__(kMeThreads) __attribute__((amdgpu_waves_per_eu
   __shared__ int subsad[21][8];
   for (int t = tid; t < 256; t += kMeThreads)
     s32[src_word(t >> 3, t & 7)] = *reinterpret_cast<const uint32_t*>(S + (long)(cy + (t >> 3)) * g.W + cx + 4 * (t & 7));
-  if (tid == 0) {
+  // candidate sources: the coarse vectors of the CTB's 3x3 neighbourhood (clipped to the
+  // picture) and the co-located previous vector, gathered by 10 lanes at once into LDS; thread
+  // 0 then runs me_candidates on that local window (same bounds, so the same candidates)
+  // instead of a chain of dependent global loads ahead of the window staging
+  __shared__ int16_t nbmv[18], tmv[2];
+  const int lx0 = cxi > 0 ? cxi - 1 : 0, ly0 = cyi > 0 ? cyi - 1 : 0;
+  const int lw = (cxi + 1 < g.wc ? cxi + 1 : g.wc - 1) - lx0 + 1, lh = (cyi + 1 < g.hc ? cyi + 1 : g.hc - 1) - ly0 + 1;
+  if (tid < 9) {
+    const int i = tid % 3, j = tid / 3;
+    if (i < lw && j < lh) {
+      const int16_t* c = cmv + (long)b * g.wc * g.hc * 2 + 2 * ((long)(ly0 + j) * g.wc + lx0 + i);
+      nbmv[2 * (j * lw + i)] = c[0];
+      nbmv[2 * (j * lw + i) + 1] = c[1];
+    }
+  } else if (tid == 9) {
     const long u0 = b * g.usz + (long)(cy >> 3) * g.w8 + (cx >> 3);
-    ncand = me_candidates(cmv + (long)b * g.wc * g.hc * 2, g.wc, g.hc, cxi, cyi, prev_mv[2 * u0], prev_mv[2 * u0 + 1],
-                          range - 4, cand, pmv);
+    tmv[0] = prev_mv[2 * u0];
+    tmv[1] = prev_mv[2 * u0 + 1];
   }
   if (tid < 21) best[tid] = 0xffffffffu;
   __syncthreads();
+  if (tid == 0) {
+    if (diag_stop & 16)  // TV_ME_CAND=global (A/B reference): the former global-memory path
+      ncand = me_candidates(cmv + (long)b * g.wc * g.hc * 2, g.wc, g.hc, cxi, cyi, tmv[0], tmv[1], range - 4, cand, pmv);
+    else
+      ncand = me_candidates(nbmv, lw, lh, cxi - lx0, cyi - ly0, tmv[0], tmv[1], range - 4, cand, pmv);
+  }
+  __syncthreads();
+  diag_stop &= 15;
   const int nc = ncand;
   // candidate windows, each pre-aligned so byte 0 of a row is x = cx + cand_x + kMeWinX0
   // one lane per 16-byte chunk: a dwordx4 + dword load from the dword-aligned address, then
@@ -655,7 +677,10 @@ __device__ __forceinline__ bool pr_zeroed(const PReconLds& L, int id) {
   return L.nz[id] == 0 || (L.nz[id] == 1 && L.sa[id] == 1 && L.dc[id] == 0);
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
+// WPE: waves per SIMD the register allocation must allow (6: 79 VGPRs; 7: 72, no scratch;
+// 8: 64 + a 12-byte spill, measured +2.3 % at 1080p) -- TV_RECON_WPE for same-box A/B, default 8.
+template <int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                      FrameSet rec, DecisionSet dec, Geo g, int tile_skip,
                                                      FrameSet ref1, const uint8_t* phase1) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1083,6 +1108,16 @@ static int recon_tile_skip() {
   return v;
 }
 
+using ReconKernel = decltype(&k_inter_recon<7>);
+static ReconKernel recon_kernel() {
+  static const ReconKernel k = [] {
+    const char* e = std::getenv("TV_RECON_WPE");
+    const int w = e ? std::atoi(e) : 8;
+    return w == 6 ? &k_inter_recon<6> : (w == 8 ? &k_inter_recon<8> : &k_inter_recon<7>);
+  }();
+  return k;
+}
+
 // Variants for same-box A/B measurements (same decisions): TV_ME_SUBPEL_ROWS=4 (768 sub-pel
 // groups), TV_ME_PEN=global (MV-rate table read from global memory), TV_ME_WPE=7 (the
 // compiler's register allocation: 7 CTBs per CU).
@@ -1105,14 +1140,15 @@ void launch_inter_frame(FrameSet src, FrameSet ref, const uint8_t* phase, FrameS
                         const PIntraBuffers* pi) {
   static const int diag_stop = [] {
     const char* e = std::getenv("TV_DIAG_ME_STOP");
-    return e ? std::atoi(e) : 0;
+    const char* c = std::getenv("TV_ME_CAND");
+    return (e ? std::atoi(e) : 0) | (c && std::string(c) == "global" ? 16 : 0);
   }();
   const PIntraBuffers none{};
   if (pi && hipMemsetAsync(pi->count, 0, 6 * sizeof(int), s) != hipSuccess) return;
   me_kernel()<<<dim3(g.wc * g.hc, B), kMeThreads, 0, s>>>(src, ref, phase, dec, me.prev_mv, me.cmv, g, rc, range,
                                                          diag_stop, nullptr, pi ? *pi : none);
   if (pi) launch_pintra_decide(src, dec, g, rc, *pi, B, s);
-  k_inter_recon<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, recon_tile_skip(), FrameSet{},
+  recon_kernel()<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, ref, phase, rec, dec, g, recon_tile_skip(), FrameSet{},
                                                      nullptr);
   if (pi) launch_pintra_recon(src, rec, dec, g, *pi, B, s);
 }
@@ -1126,7 +1162,7 @@ void launch_inter_frame_b(FrameSet src, FrameSet ref0, const uint8_t* phase0, Fr
   me_kernel()<<<grid, kMeThreads, 0, s>>>(src, ref0, phase0, dec, me0.prev_mv, me0.cmv, g, rc, range[0], 0, meout, none);
   me_kernel()<<<grid, kMeThreads, 0, s>>>(src, ref1, phase1, dec, me1.prev_mv, me1.cmv, g, rc, range[1], 0, o1, none);
   k_bi_decide<<<grid, 256, 0, s>>>(src, phase0, phase1, meout, o1, dec, g, rc);
-  k_inter_recon<<<grid, 256, 0, s>>>(src, ref0, phase0, rec, dec, g, recon_tile_skip(), ref1, phase1);
+  recon_kernel()<<<grid, 256, 0, s>>>(src, ref0, phase0, rec, dec, g, recon_tile_skip(), ref1, phase1);
 }
 
 }  // namespace gpu
