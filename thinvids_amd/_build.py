@@ -34,7 +34,7 @@ ARCH = os.environ.get("TV_OFFLOAD_ARCH", "gfx950")
 CXXFLAGS = ["-O2", "-std=c++17", "-fPIC", "-pthread", "-Wall", "-Wno-unused-function", f"-I{INC}"]
 HIPFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INC}",
             "-Wno-unused-result", "-munsafe-fp-atomics", *os.environ.get("TV_HIPFLAGS_EXTRA", "").split()]
-GPU_LINK = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
+GPU_LINK = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lhsa-runtime64", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
 
 
 def _hipcc() -> str:
