@@ -415,8 +415,26 @@ void launch_phase_planes(FrameSet ref, uint8_t* phase, const Geo& g, int B, hipS
 // to the CPU golden model), the band-position argmin of the 3 components on 3 waves.
 constexpr int kSaoT = 34;   // luma tile side with border
 constexpr int kSaoTc = 18;  // chroma
-constexpr int kSaoTile = kSaoT * kSaoT + 2 * kSaoTc * kSaoTc;
+// Tile rows are stored with pitch T + 2 and one column of offset, so a sample pair (even x,
+// x + 1) of the CTB is one aligned dword: the packed statistics read pairs as ds_read_b32.
+constexpr int kSaoP = kSaoT + 2, kSaoPc = kSaoTc + 2;
+constexpr int kSaoTile = kSaoT * kSaoP + 2 * kSaoTc * kSaoPc;
 constexpr int kSaoStage = (kSaoTile + 255) / 256;
+// tile index of (row, col) of component c (row / col 0 = the one-sample border)
+__device__ __forceinline__ int sao_tix(int c, int row, int col) {
+  return c == 0 ? row * kSaoP + col + 1 : kSaoT * kSaoP + (c - 1) * kSaoTc * kSaoPc + row * kSaoPc + col + 1;
+}
+typedef short sao_s2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ sao_s2 sao_pair(uint32_t w) { return __builtin_bit_cast(sao_s2, w); }
+typedef unsigned short sao_u2 __attribute__((ext_vector_type(2)));
+// per half: -1, 0, 1 for |d| < 2^15 -- shifts and an OR (v_pk_ashrrev / v_pk_lshrrev), no
+// compares: (d >> 15) is -1 for d < 0, ((-d) >>> 15) is 1 for d > 0
+__device__ __forceinline__ sao_s2 sao_sign2(sao_s2 d) {
+  const sao_s2 z = {0, 0};
+  const sao_u2 f = {15, 15};
+  return (d >> 15) | __builtin_bit_cast(sao_s2, __builtin_bit_cast(sao_u2, z - d) >> f);
+}
+__device__ __forceinline__ sao_s2 sao_relu2(sao_s2 e) { return e & ~(e >> 15); }  // max(e, 0)
 
 __device__ __forceinline__ void sao_tile_pos(int i, int& c, int& j) {
   c = i < kSaoT * kSaoT ? 0 : (i < kSaoT * kSaoT + kSaoTc * kSaoTc ? 1 : 2);
@@ -432,7 +450,7 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   const long long lam16 = rc->sao_lam16[qp[b]];
   const int cx = ctu % g.wc, cy = ctu / g.wc;
   __shared__ SaoStats st[3];
-  __shared__ int16_t tile[kSaoTile];  // luma 34 x 34, then Cb, Cr 18 x 18
+  __shared__ __align__(16) int16_t tile[kSaoTile];  // luma 34 x 34, then Cb, Cr 18 x 18 (sao_tix)
   __shared__ int bpos[3];
   // band statistics: a packed (sum * 2048 + count) histogram per component with 16 copies
   // (lane & 15), so same-band lanes of a wave rarely hit one LDS address
@@ -465,72 +483,141 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       if (i >= kItems) continue;
       const int c = i < kL ? 0 : (i < kL + kC ? 1 : 2), j = c == 0 ? i : i - kL - (c - 1) * kC;
       const int nd = c ? 6 : 10, T = c ? kSaoTc : kSaoT;
-      int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
       const int row = j / nd, col0 = 4 * (j % nd) - 3;  // tile column of the dword's first byte
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int col = col0 + q;
-        if (col >= 0 && col < T) t[row * T + col] = (inside >> k) & 1 ? (int16_t)((v[k] >> (8 * q)) & 255) : (int16_t)-1;
+        if (col >= 0 && col < T) tile[sao_tix(c, row, col)] = (inside >> k) & 1 ? (int16_t)((v[k] >> (8 * q)) & 255) : (int16_t)-1;
       }
     }
   }
-  // one region per wave: waves 0/1 = luma rows 0-15 / 16-31 (8 samples per lane), wave 2 =
-  // Cb, wave 3 = Cr (4 per lane).  Counts and sums travel packed as sum * 2048 + count
-  // (count <= 1024, |sum| <= 255 * 1024): one wave reduction per EO counter, not two.
+  // one region per wave: waves 0/1 = luma rows 0-15 / 16-31, wave 2 = Cb, wave 3 = Cr.
+  // Counts and sums travel packed as sum * 2048 + count (count <= 1024, |sum| <= 255 * 1024):
+  // one wave reduction per EO counter, not two.
   const int wave = tid >> 6;
   const int c = wave < 2 ? 0 : wave - 1;
-  const int n = c ? 16 : 32, T = c ? kSaoTc : kSaoT, w = c ? g.W / 2 : g.W;
+  const int n = c ? 16 : 32, w = c ? g.W / 2 : g.W;
   const int nsh = c ? 4 : 5;  // log2 n: the sample index splits with shifts, not a runtime division
-  const int16_t* t = tile + (c == 0 ? 0 : kSaoT * kSaoT + (c - 1) * kSaoTc * kSaoTc);
   const int iters = c ? 4 : 8;
   const uint8_t* S = src.plane(c, b, g) + (long)(cy * n) * w + cx * n;
-  int sv[8];
+  // A CTB away from the picture edge has no outside (-1) neighbours: its statistics run on
+  // sample PAIRS in packed 16-bit arithmetic (v_pk_*: two samples per instruction, the 9
+  // neighbour dwords of a pair read once for all 4 classes).  Edge CTBs take the per-sample
+  // path with the validity checks.  Both give the same counters.
+  static_assert(!kSaoBandOffsets, "the packed statistics carry no band histogram");
+  const bool interior = cx > 0 && cy > 0 && cx < g.wc - 1 && cy < g.hc - 1 && !(diag & 16);  // 16: TV_SAO_PACKED=0 (A/B)
+  diag &= 15;
+  const int piters = c ? 2 : 4;  // pairs per lane: luma 16 rows x 16 pairs, chroma 16 x 8
+  int sv[8] = {};
+  uint32_t sp[4] = {};
+  if (interior) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {  // source samples of this lane, loads in flight together
-    const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
-    sv[k] = k < iters ? S[(i >> nsh) * w + (i & (n - 1))] : 0;
+    for (int k = 0; k < 4; ++k) {  // source pairs of this lane, loads in flight together
+      const int pidx = lane + 64 * k;
+      const int ly = (c == 0 ? wave * 16 : 0) + (pidx >> (nsh - 1)), lx = 2 * (pidx & ((n >> 1) - 1));
+      sp[k] = k < piters ? *reinterpret_cast<const uint16_t*>(S + ly * w + lx) : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // source samples of this lane, loads in flight together
+      const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
+      sv[k] = k < iters ? S[(i >> nsh) * w + (i & (n - 1))] : 0;
+    }
   }
   __syncthreads();
   // timing diagnostics only (TV_DIAG_SAO_STOP=1/2/3: stop after staging / statistics /
   // decision; the output is then incomplete) -- never set in production
   if (diag == 1) {
-    if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)(sv[0] + sv[7] + tile[tid]);
+    if (tid == 0) sao[3 * ((long)b * g.wc * g.hc + ctu)] = (uint32_t)(sv[0] + sp[0] + tile[tid]);
     return;
   }
-  // EO statistics per lane in one 64-bit register per class: four signed 16-bit fields
-  // (category 1..4) of sum(orig - deb) * 16 + count over the lane's <= 8 samples (|field| <=
-  // 255 * 8 * 16 + 8 < 2^15), added as one shifted 64-bit value per (sample, class) instead
-  // of four compare/select/adds; unpacked into the wave-sum format afterwards.
-  unsigned long long eo64[4] = {0, 0, 0, 0};
+  int eo[4][4];
+  if (interior) {
+    const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile);
+    sao_s2 cnt[4][4], sum[4][4];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (k >= iters) break;
-    const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
-    const int lx = i & (n - 1), ly = i >> nsh;
-    const int v = t[(ly + 1) * T + lx + 1];
-    const int d16 = (sv[k] - v) * 16 + 1;
-    const unsigned long long p64 = (unsigned long long)(long long)d16;
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cnt[d][q] = sum[d][q] = sao_s2{0, 0};
+    const sao_s2 zero = {0, 0}, one = {1, 1};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= piters) break;
+      const int pidx = lane + 64 * k;
+      const int ly = (c == 0 ? wave * 16 : 0) + (pidx >> (nsh - 1)), lx = 2 * (pidx & ((n >> 1) - 1));
+      uint32_t Pv[3], Cv[3], Nv[3];  // rows ly - 1, ly, ly + 1: dwords at lx - 2, lx, lx + 2
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int i0 = sao_tix(c, ly + r, lx + 1) >> 1;  // tile column lx + 1 = sample lx (even index)
+        Pv[r] = tile32[i0 - 1];
+        Cv[r] = tile32[i0];
+        Nv[r] = tile32[i0 + 1];
+      }
+      sao_s2 L[3], R[3], Cc[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        L[r] = sao_pair(__builtin_amdgcn_alignbyte(Cv[r], Pv[r], 2));  // samples (lx - 1, lx)
+        R[r] = sao_pair(__builtin_amdgcn_alignbyte(Nv[r], Cv[r], 2));  // samples (lx + 1, lx + 2)
+        Cc[r] = sao_pair(Cv[r]);
+      }
+      const sao_s2 v = Cc[1];
+      const uint32_t o = sp[k];
+      const sao_s2 orig = {(short)(o & 255), (short)(o >> 8)};
+      const sao_s2 dlt = orig - v;
+      // classes (sao_eo_dir): 0 horizontal, 1 vertical, 2 135 degrees, 3 45 degrees
+      const sao_s2 A[4] = {L[1], Cc[0], L[0], R[0]}, Bn[4] = {R[1], Cc[2], R[2], L[2]};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const sao_s2 e = sao_sign2(v - A[d]) + sao_sign2(v - Bn[d]);  // -2..2
+        const sao_s2 pos = sao_relu2(e), neg = sao_relu2(zero - e);
+        const sao_s2 is[4] = {neg >> one, neg & one, pos & one, pos >> one};  // categories 1..4
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          cnt[d][q] += is[q];
+          sum[d][q] += dlt * is[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        eo[d][q] = ((int)sum[d][q].x + (int)sum[d][q].y) * 2048 + (int)cnt[d][q].x + (int)cnt[d][q].y;
+  } else {
+    // EO statistics per lane in one 64-bit register per class: four signed 16-bit fields
+    // (category 1..4) of sum(orig - deb) * 16 + count over the lane's <= 8 samples (|field| <=
+    // 255 * 8 * 16 + 8 < 2^15), added as one shifted 64-bit value per (sample, class) instead
+    // of four compare/select/adds; unpacked into the wave-sum format afterwards.
+    unsigned long long eo64[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= iters) break;
+      const int i = (c == 0 ? wave * 512 : 0) + lane + 64 * k;
+      const int lx = i & (n - 1), ly = i >> nsh;
+      const int v = tile[sao_tix(c, ly + 1, lx + 1)];
+      const int d16 = (sv[k] - v) * 16 + 1;
+      const unsigned long long p64 = (unsigned long long)(long long)d16;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        int dx, dy;
+        sao_eo_dir(d, dx, dy);
+        const int a = tile[sao_tix(c, ly + 1 + dy, lx + 1 + dx)], bb = tile[sao_tix(c, ly + 1 - dy, lx + 1 - dx)];
+        const int e = tv_min(tv_max(v - a, -1), 1) + tv_min(tv_max(v - bb, -1), 1);  // -2..2, 0 = none
+        const int f = e + 2 - (e > 0);  // category 1..4 -> field 0..3 (e = 0 is masked below)
+        eo64[d] += (a >= 0 && bb >= 0 && e != 0) ? p64 << (16 * f) : 0ull;
+      }
+      if (kSaoBandOffsets) atomicAdd(&bh[c][v >> 3][lane & 15], (sv[k] - v) * 2048 + 1);  // band statistics
+    }
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      int dx, dy;
-      sao_eo_dir(d, dx, dy);
-      const int a = t[(ly + 1 + dy) * T + lx + 1 + dx], bb = t[(ly + 1 - dy) * T + lx + 1 - dx];
-      const int e = tv_min(tv_max(v - a, -1), 1) + tv_min(tv_max(v - bb, -1), 1);  // -2..2, 0 = none
-      const int f = e + 2 - (e > 0);  // category 1..4 -> field 0..3 (e = 0 is masked below)
-      eo64[d] += (a >= 0 && bb >= 0 && e != 0) ? p64 << (16 * f) : 0ull;
-    }
-    if (kSaoBandOffsets) atomicAdd(&bh[c][v >> 3][lane & 15], (sv[k] - v) * 2048 + 1);  // band statistics
-  }
-  int eo[4][4];
+      unsigned long long acc = eo64[d];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    unsigned long long acc = eo64[d];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int fv = (int)(int16_t)(acc & 0xffffu);  // 16 * sum + count
-      acc = (acc - (unsigned long long)(long long)fv) >> 16;
-      const int cnt = fv & 15;
-      eo[d][q] = ((fv - cnt) >> 4) * 2048 + cnt;  // sum * 2048 + count, as before
+      for (int q = 0; q < 4; ++q) {
+        const int fv = (int)(int16_t)(acc & 0xffffu);  // 16 * sum + count
+        acc = (acc - (unsigned long long)(long long)fv) >> 16;
+        const int cnt = fv & 15;
+        eo[d][q] = ((fv - cnt) >> 4) * 2048 + cnt;  // sum * 2048 + count, as before
+      }
     }
   }
 #pragma unroll
@@ -596,9 +683,8 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   for (int i = tid; i < 256 + 128; i += 256) {
     const int cc = i < 256 ? 0 : (i < 320 ? 1 : 2);
     const int j = cc == 0 ? i : i - 256 - (cc - 1) * 64;
-    const int nd = cc ? 4 : 8, nn = cc ? 16 : 32, TT = cc ? kSaoTc : kSaoT, ww = cc ? g.W / 2 : g.W;
+    const int nd = cc ? 4 : 8, nn = cc ? 16 : 32, ww = cc ? g.W / 2 : g.W;
     const int ly = j >> (cc ? 2 : 3), lx0 = 4 * (j & (nd - 1));  // nd = 4 / 8 dwords per row
-    const int16_t* tt = tile + (cc == 0 ? 0 : kSaoT * kSaoT + (cc - 1) * kSaoTc * kSaoTc);
     const uint32_t p = prm[cc];
     int dx = 0, dy = 0;
     if (sao_type(p) == 2) sao_eo_dir(sao_class(p), dx, dy);
@@ -606,9 +692,9 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int lx = lx0 + q;
-      const int v = tt[(ly + 1) * TT + lx + 1];
-      const int r = sao_type(p) ? sao_sample_nb(v, tt[(ly + 1 + dy) * TT + lx + 1 + dx],
-                                                tt[(ly + 1 - dy) * TT + lx + 1 - dx], p)
+      const int v = tile[sao_tix(cc, ly + 1, lx + 1)];
+      const int r = sao_type(p) ? sao_sample_nb(v, tile[sao_tix(cc, ly + 1 + dy, lx + 1 + dx)],
+                                                tile[sao_tix(cc, ly + 1 - dy, lx + 1 - dx)], p)
                                 : v;
       word |= (uint32_t)r << (8 * q);
     }
@@ -642,7 +728,8 @@ void launch_sao(FrameSet src, FrameSet deb, FrameSet out, uint32_t* sao, const i
                 const Geo& g, int B, hipStream_t s, unsigned long long* sse) {
   static const int diag = [] {
     const char* e = std::getenv("TV_DIAG_SAO_STOP");
-    return e ? std::atoi(e) : 0;
+    const char* pk = std::getenv("TV_SAO_PACKED");
+    return (e ? std::atoi(e) : 0) | (pk && std::atoi(pk) == 0 ? 16 : 0);
   }();
   k_sao_decide<<<dim3(g.wc * g.hc, B), 256, 0, s>>>(src, deb, out, sao, g, qp, rc, diag, sse);
 }
