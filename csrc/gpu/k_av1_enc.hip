@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <string>
 
+#include <cstdlib>
+
 #include "gpu_common.h"
 #include "mfma_exact.h"
 #include "tv/av1_defs.h"
@@ -180,8 +182,10 @@ struct Planes3W {
 // ================================================================= inter ================
 // STAGE 0: the motion search only (mvout = the block's MV).  STAGE 1: prediction at mvin
 // (the refined field) + residual coding + reconstruction (mvout = mvin).
-template <int STAGE>
-__global__ void __launch_bounds__(64) k_av1e_inter(Planes3 src, Planes3 ref, Planes3W rec, uint32_t* __restrict__ mode,
+// WPE: minimum waves per SIMD for the register allocation (stage 0: 6 -> <= 80 VGPRs, no
+// scratch, against the compiler's 84 / 5 waves; stage 1 is LDS-limited, left alone)
+template <int STAGE, int WPE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) k_av1e_inter(Planes3 src, Planes3 ref, Planes3W rec, uint32_t* __restrict__ mode,
                                                    const uint32_t* __restrict__ mvin, uint32_t* __restrict__ mvout,
                                                    int16_t* __restrict__ ly, int16_t* __restrict__ lu,
                                                    int16_t* __restrict__ lv, int W, int H, const int* __restrict__ qarr,
@@ -1080,6 +1084,16 @@ __global__ void __launch_bounds__(256) k_av1e_tb_pack(const int16_t* __restrict_
   }
 }
 
+// TV_AV1_INTER_WPE=5: the stage-0 search at the compiler's own allocation (same-box A/B)
+using Av1InterKernel = decltype(&k_av1e_inter<0, 6>);
+static Av1InterKernel av1_inter0_kernel() {
+  static const Av1InterKernel k = [] {
+    const char* e = std::getenv("TV_AV1_INTER_WPE");
+    return (e && std::atoi(e) == 5) ? &k_av1e_inter<0, 1> : &k_av1e_inter<0, 6>;
+  }();
+  return k;
+}
+
 }  // namespace
 }  // namespace gpu
 }  // namespace tv
@@ -1101,7 +1115,7 @@ int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const
   static_assert(kMvRefineRounds % 2 == 1, "an odd round count ends the field in `mv`");
   const int nb = (W >> 4) * (H >> 4), nsb = ((W + 63) >> 6) * ((H + 63) >> 6);
   hipStream_t st = (hipStream_t)stream;
-  k_av1e_inter<0><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
+  av1_inter0_kernel()<<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
                                                nullptr, tmp, ly, lu, lv, W, H, qarr, satd_acc);
   // memo: two [B][nb] record sets (mv words, SATDs, counts), ping-ponged across the rounds
   const long nrec = (long)B * nb;
@@ -1120,7 +1134,7 @@ int tv_av1e_inter(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const
   }
   if (hipMemsetAsync(satd_acc, 0, (size_t)B * sizeof(unsigned long long), st) != hipSuccess) return status("av1e_inter");
   k_av1e_mv_unify<<<dim3(nsb, B), 256, 0, st>>>(sy, ry, mv, W, H, qarr, satd_acc);
-  k_av1e_inter<1><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
+  k_av1e_inter<1, 1><<<dim3(nb, B), 64, 0, st>>>(Planes3{sy, su, sv}, Planes3{ry, ru, rv}, Planes3W{oy, ou, ov}, mode,
                                                mv, mv, ly, lu, lv, W, H, qarr, satd_acc);
   return status("av1e_inter");
 }
@@ -1224,3 +1238,4 @@ int tv_av1e_cdef_choose(const unsigned long long* sy, const unsigned long long* 
   return status("av1e_cdef_choose");
 }
 }
+
