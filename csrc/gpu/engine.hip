@@ -481,11 +481,11 @@ class Core {
   static long align(long n) { return (n + 255) & ~255L; }
   // WPP streams are entropy-coded on the GPU (k_entropy.hip) unless bit 5 asks for the host
   // WPP on, not forced to the host, and a geometry the coder handles (>= 2 CTB columns for the
-  // 9.3.2.4 storage after CTB 1, <= 256 rows): anything else uses the host writer from the start
+  // 9.3.2.4 storage after CTB 1, <= 256 rows and columns): anything else uses the host writer from the start
   static bool gpu_entropy(const EngineCfg& c) {
     if (!((c.deblock & 4) && !(c.deblock & 32))) return false;
     const Geo g = make_geo(c.width, c.height);
-    return g.wc >= 2 && g.hc <= 256;
+    return g.wc >= 2 && g.wc <= 256 && g.hc <= 256;
   }
   // token capacity of the per-core entropy scratch: one token per luma sample of every
   // segment (the bench's textured I pictures use about a third of that); a picture that

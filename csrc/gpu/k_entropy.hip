@@ -737,22 +737,89 @@ __global__ void __launch_bounds__(256) k_ent_cu(EntropyArgs a) {
 // (kEntRegionTokens) and its exact count.  !REGION (after the scan): only CTBs whose tokens
 // did not fit binarise again, straight into the picture's token list; the others were moved by
 // k_ent_place.  (A count pass + write pass binarised every CTB twice.)
+// One workgroup per CTB row (one thread per CTB, 64 * ceil(wc / 64) threads).  The row's
+// decision planes -- the 4 unit rows of the CTB row and the one above (left / upper / upper-
+// right neighbours), all columns, a contiguous range of every plane -- are staged in LDS by
+// the whole workgroup first, so the per-CTB syntax walk reads LDS instead of issuing chains
+// of dependent global loads (one thread per CTB left every neighbour check a ~1 us round
+// trip).  REGION (the single full pass): the CTB's tokens into its fixed region
+// (kEntRegionTokens) and its exact count.  !REGION (after the scan): only rows with a CTB whose
+// tokens did not fit binarise again, straight into the picture's token list; the others were
+// moved by k_ent_place.  (A count pass + write pass binarised every CTB twice.)
+struct BinStage {  // byte offsets of the staged planes in dynamic LDS (nu units each)
+  int nu, cu, in, ipm, cbf, tu, sk, mi, dir, mv, mv1, bytes;
+};
+__host__ __device__ inline BinStage bin_stage(int w8, bool tu, bool bpic) {
+  BinStage t;
+  t.nu = 5 * w8;
+  int o = 0;
+  t.cu = o; o += t.nu;
+  t.in = o; o += t.nu;
+  t.ipm = o; o += t.nu;
+  t.cbf = o; o += t.nu;
+  t.sk = o; o += t.nu;
+  t.mi = o; o += t.nu;
+  t.tu = tu ? o : -1; o += tu ? t.nu : 0;
+  t.dir = bpic ? o : -1; o += bpic ? t.nu : 0;
+  o = (o + 15) & ~15;
+  t.mv = o; o += 4 * t.nu;
+  t.mv1 = bpic ? o : -1; o += bpic ? 4 * t.nu : 0;
+  t.bytes = o;
+  return t;
+}
 template <bool REGION>
-__global__ void __launch_bounds__(64) k_ent_bin(EntropyArgs a) {
+__global__ void __launch_bounds__(256) k_ent_bin(EntropyArgs a) {
   __shared__ BinTables T;
-  const int b = blockIdx.y, nctu = a.g.wc * a.g.hc;
-  const int ctu = blockIdx.x * 64 + threadIdx.x;
+  extern __shared__ __align__(16) uint8_t dyn[];
+  const int b = blockIdx.y, nctu = a.g.wc * a.g.hc, wc = a.g.wc, w8 = a.g.w8;
+  const int cy = blockIdx.x, cx = threadIdx.x;
+  const int ctu = cy * wc + cx;
   const long i = (long)b * nctu + ctu;
-  bool work = ctu < nctu;
+  bool work = cx < wc;
   if (!REGION) {  // the whole workgroup leaves unless one of its CTBs overflowed
     work = work && !*a.status && a.ctb_cnt[i] > kEntRegionTokens;
     if (__syncthreads_or(work) == 0) return;
   }
+  const int nt = blockDim.x;
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&c_tab);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
-    for (int k = threadIdx.x; k < (int)(sizeof(BinTables) / 4); k += 64) dst[k] = src[k];
+    for (int k = threadIdx.x; k < (int)(sizeof(BinTables) / 4); k += nt) dst[k] = src[k];
   }
+  SegView v = seg_view(a, b);
+  const bool bpic = v.dir != nullptr;
+  const BinStage L = bin_stage(w8, v.tu != nullptr, bpic);
+  const int uy0 = cy > 0 ? 4 * cy - 1 : 0, nrows = 4 * cy + 4 - uy0;
+  const long u0 = (long)uy0 * w8;  // first staged unit
+  const int nw = nrows * w8 / 4;   // dwords of a byte plane's window (w8 is a multiple of 4)
+  auto stage8 = [&](int off, const uint8_t*& p) {
+    if (off < 0) return;
+    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(p + u0);
+    uint32_t* l32 = reinterpret_cast<uint32_t*>(dyn + off);
+    for (int k = threadIdx.x; k < nw; k += nt) l32[k] = g32[k];
+    p = dyn + off - u0;  // unit(x, y) indexes the LDS window directly (rows uy0 .. uy0 + nrows)
+  };
+  auto stage16 = [&](int off, const int16_t*& p) {
+    if (off < 0) return;
+    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(p + 2 * u0);
+    uint32_t* l32 = reinterpret_cast<uint32_t*>(dyn + off);
+    for (int k = threadIdx.x; k < nrows * w8; k += nt) l32[k] = g32[k];
+    p = reinterpret_cast<const int16_t*>(dyn + off) - 2 * u0;
+  };
+  stage8(L.cu, v.cu_log2);
+  stage8(L.in, v.intra);
+  stage8(L.ipm, v.ipm);
+  stage8(L.cbf, v.cbf);
+  stage8(L.sk, v.skip);
+  {
+    const uint8_t* mi = reinterpret_cast<const uint8_t*>(v.midx);
+    stage8(L.mi, mi);
+    v.midx = reinterpret_cast<const int8_t*>(mi);
+  }
+  stage8(L.tu, v.tu);
+  stage8(L.dir, v.dir);
+  stage16(L.mv, v.mv);
+  stage16(L.mv1, v.mv1);
   __syncthreads();
   if (!work) return;
   uint32_t* out;
@@ -766,10 +833,9 @@ __global__ void __launch_bounds__(64) k_ent_bin(EntropyArgs a) {
     out = a.tokens + base + a.ctb_off[i];
     cap = 1 << 30;
   }
-  const SegView v = seg_view(a, b);
   TokSink s{out, cap};
   CtbBinariser z{v, a.pic, s, T};
-  z.ctb(ctu % v.wc, ctu / v.wc, a.pic.sao != 0);
+  z.ctb(cx, cy, a.pic.sao != 0);
   s.flush_c();
   s.flush_b();
   if (z.err) atomicOr(a.status, 2);
@@ -1402,11 +1468,15 @@ void launch_entropy_bin(const EntropyArgs& a, int B, hipStream_t s) {
   if (a.g.hc > 256) throw std::runtime_error("GPU entropy coding supports at most 256 CTB rows");
   (void)hipMemsetAsync(a.status, 0, sizeof(int), s);
   if (a.pic.type != 2) k_ent_cu<<<dim3((unsigned)((a.g.usz + 255) / 256), B), 256, 0, s>>>(a);
-  k_ent_bin<true><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
+  if (a.g.wc > 256) throw std::runtime_error("GPU entropy coding supports at most 256 CTB columns");
+  const BinStage L = bin_stage(a.g.w8, a.dec.tu != nullptr, a.dec.dir != nullptr);
+  const dim3 rows(a.g.hc, B);
+  const int nthr = 64 * ((a.g.wc + 63) / 64);
+  k_ent_bin<true><<<rows, nthr, L.bytes, s>>>(a);
   k_ent_scan<<<B, 1024, 0, s>>>(a);
   k_ent_check<<<1, 1, 0, s>>>(a, B);
   k_ent_place<<<dim3((nctu + 3) / 4, B), 256, 0, s>>>(a);
-  k_ent_bin<false><<<dim3((nctu + 63) / 64, B), 64, 0, s>>>(a);
+  k_ent_bin<false><<<rows, nthr, L.bytes, s>>>(a);
 }
 
 void launch_entropy_ac(const EntropyArgs& a, int B, hipStream_t s) {
