@@ -168,6 +168,7 @@ struct SegView {
   const int16_t* packed;
   const uint32_t* sao;
   int w8, wc, hc, W, H;
+  long ubase = 0;  // first unit of the planes' window (k_ent_bin stages a window in LDS)
 };
 
 __device__ __forceinline__ SegView seg_view(const EntropyArgs& a, int b) {
@@ -198,7 +199,7 @@ __device__ __forceinline__ SegView seg_view(const EntropyArgs& a, int b) {
   return v;
 }
 
-__device__ __forceinline__ int unit_of(const SegView& v, int x, int y) { return (y >> 3) * v.w8 + (x >> 3); }
+__device__ __forceinline__ int unit_of(const SegView& v, int x, int y) { return (int)((y >> 3) * v.w8 + (x >> 3) - v.ubase); }
 __device__ __forceinline__ Motion motion_of(const SegView& v, int u) {
   Motion m;
   m.dir = v.dir ? v.dir[u] : 1;
@@ -797,14 +798,14 @@ __global__ void __launch_bounds__(256) k_ent_bin(EntropyArgs a) {
     const uint32_t* g32 = reinterpret_cast<const uint32_t*>(p + u0);
     uint32_t* l32 = reinterpret_cast<uint32_t*>(dyn + off);
     for (int k = threadIdx.x; k < nw; k += nt) l32[k] = g32[k];
-    p = dyn + off - u0;  // unit(x, y) indexes the LDS window directly (rows uy0 .. uy0 + nrows)
+    p = dyn + off;  // unit_of subtracts v.ubase: unit(x, y) indexes the window (no pointer below dyn)
   };
   auto stage16 = [&](int off, const int16_t*& p) {
     if (off < 0) return;
     const uint32_t* g32 = reinterpret_cast<const uint32_t*>(p + 2 * u0);
     uint32_t* l32 = reinterpret_cast<uint32_t*>(dyn + off);
     for (int k = threadIdx.x; k < nrows * w8; k += nt) l32[k] = g32[k];
-    p = reinterpret_cast<const int16_t*>(dyn + off) - 2 * u0;
+    p = reinterpret_cast<const int16_t*>(dyn + off);
   };
   stage8(L.cu, v.cu_log2);
   stage8(L.in, v.intra);
@@ -820,6 +821,7 @@ __global__ void __launch_bounds__(256) k_ent_bin(EntropyArgs a) {
   stage8(L.dir, v.dir);
   stage16(L.mv, v.mv);
   stage16(L.mv1, v.mv1);
+  v.ubase = u0;
   __syncthreads();
   if (!work) return;
   uint32_t* out;
