@@ -976,7 +976,7 @@ class Core {
       // not switch).  An event query per picture to find a busy
       // lane serialised the issue thread (-14 %).
       const bool dense = ent_dense_run_.load(std::memory_order_relaxed) >= dense_after();  // not just an I picture
-      const int lane = (ent_lanes() > 1 && dense) ? (f & 1) : 0;
+      const int lane = (ent_lanes() > 1 && dense) ? f % ent_lanes() : 0;
       HIP_OK(hipEventRecord(eev_, stream_));
       HIP_OK(hipStreamWaitEvent(estream_[lane], eev_, 0));
       // binarisation on the core's entropy stream (one picture at a time: its scratch is per
@@ -1098,7 +1098,7 @@ class Core {
   bool gpu_ent_ = false;
   // entropy lanes: pictures alternate between lanes (own scratch + stream), so the coders of
   // two pictures overlap (TV_ENT_LANES, default 2; textured content needed more than one)
-  static constexpr int kMaxEntLanes = 2;
+  static constexpr int kMaxEntLanes = 4;
   static int env_lanes() {
     const char* e = getenv("TV_ENT_LANES");
     const int v = e ? atoi(e) : 2;
@@ -1209,7 +1209,7 @@ class Engine {
       cc.batch = std::min(per_, c.batch - g * per_);
       cores_.push_back(std::make_unique<Core>(cc, pool_.get()));
     }
-    for (int l = 0; l < 2; ++l)  // Core::kMaxEntLanes
+    for (int l = 0; l < 4; ++l)  // Core::kMaxEntLanes
       for (auto& core : cores_) core->init_entropy_stream(l);
   }
   ~Engine() {
