@@ -59,11 +59,13 @@ constexpr int kFChunks = kFWords / 4;       // 16-byte chunks per staged row
 constexpr int kFPitch = kFWords, kWinSkew = 2, kWinCand = kFRows * kFPitch + kWinSkew;
 __device__ __forceinline__ int win_word(int k, int r, int w) { return k * kWinCand + r * kFPitch + (r >= 16 ? kWinSkew : 0) + w; }
 // LDS pitch (words) of a source-CTB row (uniform s0/s1 reads stay one aligned 8-byte read).
-// The bottom 16 rows sit kSrcSkew words further: the four quadrant lanes of an integer-
-// search item read rows r and r + 16 at the same time, which with a flat 8-word pitch are
-// 128 words apart -- the same LDS bank (a 2-way conflict on every source read).
-constexpr int kSrcP = 8, kSrcSkew = 2;
-__device__ __forceinline__ int src_word(int row, int w) { return row * kSrcP + w + ((row >> 4) & 1) * kSrcSkew; }
+// Every 8-row band sits kSrcSkew (8) words further, so rows 8 apart land 8 banks apart: the
+// sub-pel SAD lanes of one candidate read rows by + j of blocks 8 / 16 rows apart at the same
+// time (with a flat 8-word pitch 64 words apart -- one bank, 4-way conflicts: 18.6 % of the
+// kernel's LDS cycles, r6_prof), and the four quadrant lanes of an integer-search item read
+// rows r and r + 16 (16 banks apart) at word offsets 0 / 4: 32 distinct banks either way.
+constexpr int kSrcP = 8, kSrcSkew = 8;
+__device__ __forceinline__ int src_word(int row, int w) { return row * kSrcP + w + (row >> 3) * kSrcSkew; }
 
 __device__ __forceinline__ void me_blk_geom(int bi, int& bx, int& by, int& l2) {
   if (bi < 16) {
@@ -195,7 +197,7 @@ __global__ void __launch_bounds__(kMeThreads) __attribute__((amdgpu_waves_per_eu
   const int cxi = ctu % g.wc, cyi = ctu / g.wc, cx = cxi * 32, cy = cyi * 32;
   const uint8_t* S = src.plane(0, b, g);
   const uint8_t* R = ref.plane(0, b, g);
-  __shared__ uint32_t s32[32 * kSrcP + kSrcSkew];
+  __shared__ uint32_t s32[32 * kSrcP + 3 * kSrcSkew];
   __shared__ uint32_t win[kMeMaxCand * kWinCand];
   __shared__ int cand[kMeMaxCand][2];
   __shared__ int pmv[2], ncand;
