@@ -239,22 +239,47 @@ __global__ void __launch_bounds__(kMeThreads) __attribute__((amdgpu_waves_per_eu
   // candidate windows, each pre-aligned so byte 0 of a row is x = cx + cand_x + kMeWinX0
   // one lane per 16-byte chunk: a dwordx4 + dword load from the dword-aligned address, then
   // v_alignbyte to the candidate's byte offset (the clamped per-byte path only at the edges)
-  for (int e = tid; e < nc * kFRows * kFChunks; e += kMeThreads) {
-    const int k = e / (kFRows * kFChunks), rem = e - k * (kFRows * kFChunks);
-    const int r = rem / kFChunks, ch = rem - r * kFChunks;
-    const uint8_t* row = R + (long)clip3(0, g.H - 1, cy + cand[k][1] + kMeWinY0 + r) * g.W;
-    const int x = cx + cand[k][0] + kMeWinX0 + 16 * ch, a = x & ~3, sh = x & 3;
-    uint32_t* dst = win + win_word(k, r, 4 * ch);
-    if (x >= 0 && a + 20 <= g.W) {
-      const uint4 u = *reinterpret_cast<const uint4*>(row + a);
-      const uint32_t u4 = *reinterpret_cast<const uint32_t*>(row + a + 16);
-      dst[0] = __builtin_amdgcn_alignbyte(u.y, u.x, sh);
-      dst[1] = __builtin_amdgcn_alignbyte(u.z, u.y, sh);
-      dst[2] = __builtin_amdgcn_alignbyte(u.w, u.z, sh);
-      dst[3] = __builtin_amdgcn_alignbyte(u4, u.w, sh);
-    } else {
+  // All of a thread's chunks (<= 4) are loaded before any is stored, so their global
+  // latencies overlap instead of one round trip per loop pass.
+  constexpr int kWinPer = (kMeMaxCand * kFRows * kFChunks + kMeThreads - 1) / kMeThreads;
+  {
+    const int ntot = nc * kFRows * kFChunks;
+    uint4 u[kWinPer];
+    uint32_t u4[kWinPer];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dst[j] = load4_clamped(row, x + 4 * j, g.W);
+    for (int n = 0; n < kWinPer; ++n) {
+      const int e = tid + n * kMeThreads;
+      u[n] = make_uint4(0, 0, 0, 0);
+      u4[n] = 0;
+      if (e < ntot) {
+        const int k = e / (kFRows * kFChunks), rem = e - k * (kFRows * kFChunks);
+        const int r = rem / kFChunks, ch = rem - r * kFChunks;
+        const uint8_t* row = R + (long)clip3(0, g.H - 1, cy + cand[k][1] + kMeWinY0 + r) * g.W;
+        const int x = cx + cand[k][0] + kMeWinX0 + 16 * ch, a = x & ~3;
+        if (x >= 0 && a + 20 <= g.W) {
+          u[n] = *reinterpret_cast<const uint4*>(row + a);
+          u4[n] = *reinterpret_cast<const uint32_t*>(row + a + 16);
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < kWinPer; ++n) {
+      const int e = tid + n * kMeThreads;
+      if (e >= ntot) break;
+      const int k = e / (kFRows * kFChunks), rem = e - k * (kFRows * kFChunks);
+      const int r = rem / kFChunks, ch = rem - r * kFChunks;
+      const int x = cx + cand[k][0] + kMeWinX0 + 16 * ch, a = x & ~3, sh = x & 3;
+      uint32_t* dst = win + win_word(k, r, 4 * ch);
+      if (x >= 0 && a + 20 <= g.W) {
+        dst[0] = __builtin_amdgcn_alignbyte(u[n].y, u[n].x, sh);
+        dst[1] = __builtin_amdgcn_alignbyte(u[n].z, u[n].y, sh);
+        dst[2] = __builtin_amdgcn_alignbyte(u[n].w, u[n].z, sh);
+        dst[3] = __builtin_amdgcn_alignbyte(u4[n], u[n].w, sh);
+      } else {  // the clamped per-byte path at the picture edges
+        const uint8_t* row = R + (long)clip3(0, g.H - 1, cy + cand[k][1] + kMeWinY0 + r) * g.W;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[j] = load4_clamped(row, x + 4 * j, g.W);
+      }
     }
   }
   __syncthreads();
