@@ -17,8 +17,14 @@
 //   stream t % D, ordered after the caller's stream: one DMA queue moved ~23-25 GB/s, four
 //   ~28-31 GB/s (round 5, 1080p y4m job 4942 -> 5192-5282 frames/s).  D = 1 copies on the
 //   caller's stream.
+//   Round 6: hipMemcpyAsync moves a pinned-host -> device chunk with a blit kernel on this
+//   runtime (`__amd_rocclr_copyBuffer`), CU time taken from the encoder running beside the
+//   next claim's ingest; the chunks now go to the SDMA engines (hsa_amd_memory_async_copy,
+//   one completion signal per ring slot).  TV_INGEST_DMA=hip keeps the HIP copies.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -60,6 +66,33 @@ int ingest_streams() {
     return std::max(1, std::min(8, v));
   }();
   return n;
+}
+
+// the CPU agent (source of host -> device SDMA copies), found once; handle 0: none
+hsa_agent_t cpu_agent() {
+  static const hsa_agent_t a = [] {
+    hsa_agent_t r{0};
+    hsa_iterate_agents(
+        [](hsa_agent_t x, void* data) {
+          hsa_device_type_t t;
+          if (hsa_agent_get_info(x, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+            *static_cast<hsa_agent_t*>(data) = x;
+            return HSA_STATUS_INFO_BREAK;
+          }
+          return HSA_STATUS_SUCCESS;
+        },
+        &r);
+    return r;
+  }();
+  return a;
+}
+
+bool use_sdma() {
+  static const bool on = [] {
+    const char* e = std::getenv("TV_INGEST_DMA");
+    return !(e && std::string(e) == "hip");
+  }();
+  return on;
 }
 
 int64_t pread_all(int fd, uint8_t* dst, int64_t n, int64_t off) {
@@ -120,6 +153,25 @@ int tv_ingest_h2d(const char* path, long long offset, long long nbytes, void* ds
   std::vector<hipEvent_t> ev(S);
   std::vector<char> used(S, 0);
   for (auto& e : ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  // SDMA mode: the destination was allocated on the caller's stream, so that stream drains
+  // first (the prefetch stream is idle; the first claim's load runs before its encode)
+  hsa_agent_t cpu = cpu_agent(), gpu{0};
+  bool sdma = use_sdma() && cpu.handle != 0;
+  if (sdma) {
+    hsa_amd_pointer_info_t info{};
+    info.size = sizeof(info);
+    sdma = hsa_amd_pointer_info(dst, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+           info.type == HSA_EXT_POINTER_TYPE_HSA;
+    gpu = info.agentOwner;
+  }
+  std::vector<hsa_signal_t> sig(sdma ? S : 0);
+  for (auto& g : sig)
+    if (hsa_signal_create(0, 0, nullptr, &g) != HSA_STATUS_SUCCESS) sdma = false;
+  if (sdma && hipStreamSynchronize(st) != hipSuccess) sdma = false;
+  auto wait_sig = [&](hsa_signal_t g) {
+    while (hsa_signal_wait_scacquire(g, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
+    }
+  };
   std::atomic<bool> failed{false};
   std::mutex err_mu;
   std::string err;  // set by the first failing thread; g_ingest_err is the caller's thread-local
@@ -131,7 +183,10 @@ int tv_ingest_h2d(const char* path, long long offset, long long nbytes, void* ds
   auto work = [&](int t) {
     for (int64_t k = t; k < nchunks && !failed.load(); k += T) {
       const int s = (int)(k % S);  // slots k % S with k = t (mod T) are touched by thread t only
-      if (used[s] && hipEventSynchronize(ev[s]) != hipSuccess) return fail("hipEventSynchronize failed");
+      if (used[s]) {
+        if (sdma) wait_sig(sig[s]);
+        else if (hipEventSynchronize(ev[s]) != hipSuccess) return fail("hipEventSynchronize failed");
+      }
       const int64_t off = k * chunk, n = std::min<int64_t>(chunk, nbytes - off);
       uint8_t* slot = static_cast<uint8_t*>(ring) + (int64_t)s * chunk;
       const auto r0 = clk::now();
@@ -140,10 +195,19 @@ int tv_ingest_h2d(const char* path, long long offset, long long nbytes, void* ds
       if (got != n)
         return fail(std::string("pread ") + path + (got < 0 ? std::string(": ") + std::strerror((int)-got)
                                                              : std::string(": short read (file ends)")));
-      hipStream_t q = cs[t % cs.size()];
-      if (hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, slot, (size_t)n, hipMemcpyHostToDevice, q) != hipSuccess ||
-          hipEventRecord(ev[s], q) != hipSuccess)
-        return fail("hipMemcpyAsync / hipEventRecord failed");
+      if (sdma) {
+        hsa_signal_store_relaxed(sig[s], 1);
+        if (hsa_amd_memory_async_copy(static_cast<uint8_t*>(dst) + off, gpu, slot, cpu, (size_t)n, 0, nullptr, sig[s]) !=
+            HSA_STATUS_SUCCESS) {
+          hsa_signal_store_relaxed(sig[s], 0);
+          return fail("hsa_amd_memory_async_copy failed");
+        }
+      } else {
+        hipStream_t q = cs[t % cs.size()];
+        if (hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, slot, (size_t)n, hipMemcpyHostToDevice, q) != hipSuccess ||
+            hipEventRecord(ev[s], q) != hipSuccess)
+          return fail("hipMemcpyAsync / hipEventRecord failed");
+      }
       used[s] = 1;
     }
   };
@@ -155,6 +219,10 @@ int tv_ingest_h2d(const char* path, long long offset, long long nbytes, void* ds
   for (hipStream_t c : cs) {
     const hipError_t e = hipStreamSynchronize(c);
     if (se == hipSuccess) se = e;
+  }
+  for (auto& g : sig) {
+    wait_sig(g);
+    hsa_signal_destroy(g);
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
   ::close(fd);
