@@ -299,7 +299,10 @@ def job_main(args) -> None:
     dvd = args.source == "mpeg2"
     seg_frames = args.gop * 16
     frames = args.job_frames or (args.gop * 16 * 3 * 4 * args.gpus if y4m else args.gop * 16 * 2 * 48 * args.gpus)
-    warm_frames = args.gop * 16 * (3 if y4m else 1) * args.gpus
+    # y4m: two claims per rank, so the warm-up also runs the next-claim prefetch (its thread,
+    # stream and that stream's device buffers) -- a resident executor's steady state; with one
+    # claim the timed job's first prefetch allocated ~10 GB beside the first encode (+250 ms)
+    warm_frames = args.gop * 16 * (6 if y4m else 1) * args.gpus
     if dvd:  # DVD-native: 720x480 kept (never upscaled), bwdif, segments of 2 GOPs
         w, h = 720, 480
         seg_frames = args.gop * 2
