@@ -646,7 +646,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                 got = preload(ids)
                 return {i: got[i] if i in got else load(i) for i in ids}
 
-    def encode_segments(seg_ids, source_of) -> dict:
+    def encode_segments(seg_ids, source_of, on_loaded=None) -> dict:
         """Work item = one segment with ALL its rungs: the source range is read (or received)
         once, every rung is staged from it on the device, and each rung engine then encodes
         the claimed segments in one batched launch.  In pass 2 the per-frame QP plan of
@@ -675,6 +675,8 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     part = source_of(i)
                 todo.extend(((r, i), part, spec(r), plans[(r, i)][0]) for r in need)
                 keep.append(part)
+        if on_loaded is not None:
+            on_loaded()
         if todo:
             with trace.span("node_job.encode", segments=len(todo)):
                 got, qual = _encode_many(todo, cache)
@@ -788,7 +790,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
             wq = WorkQueue(f"{job_tag}_pass{encode_pass.calls}", list(range(len(segs))), world, max_retries)
             fault.check("rank", rank)  # TV_FAULT=rank:<r>:hang|die|fail (tests)
 
-            def run(batch):
+            def run(batch, on_loaded=None):
                 todo = []
                 for i in batch:
                     try:
@@ -800,7 +802,7 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                     return
                 try:
                     prefetched.update(preload(todo))
-                    mine.update(encode_segments(todo, load))
+                    mine.update(encode_segments(todo, load, on_loaded))
                 except Exception as e:  # a real engine/IO failure: every item goes back
                     for i in todo:
                         wq.fail((i,), repr(e))
@@ -829,13 +831,28 @@ def run_job(input_path: str, output: str, height: int | None = None, qp: int = 2
                         break
                     # claim ahead only while enough work remains for every rank: at the tail of a
                     # job a prefetched batch would sit idle on this rank while others starve
+                    pend = None  # [next claim, its prefetch future once submitted]
                     if (prefetcher is not None and len(claimed) == batch_segments
                             and wq.unclaimed() >= world * batch_segments):
                         with trace.span("node_job.claim"):
                             nxt = wq.claim(batch_segments)
                         if nxt:
-                            ahead = (nxt, prefetcher.submit(load_ahead, nxt))
-                    run(claimed)
+                            pend = [nxt, None]
+                    cold = pend is not None and not all(i in prefetched for i in claimed)
+
+                    def start_ahead(p=pend):
+                        if p is not None and p[1] is None:
+                            p[1] = prefetcher.submit(load_ahead, p[0])
+
+                    if not cold:
+                        start_ahead()
+                    # a claim not prefetched (a job's first) loads on this thread first: its
+                    # successor's prefetch starts once those reads are done instead of halving
+                    # their host-memory / DMA bandwidth while the engine waits on them
+                    run(claimed, start_ahead if cold else None)
+                    start_ahead()  # run() failed before its loads finished
+                    if pend is not None:
+                        ahead = (pend[0], pend[1])
                     if len(claimed) < batch_segments and ahead is None:
                         break
             finally:
