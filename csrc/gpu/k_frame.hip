@@ -435,6 +435,18 @@ __device__ __forceinline__ sao_s2 sao_sign2(sao_s2 d) {
   return (d >> 15) | __builtin_bit_cast(sao_s2, __builtin_bit_cast(sao_u2, z - d) >> f);
 }
 __device__ __forceinline__ sao_s2 sao_relu2(sao_s2 e) { return e & ~(e >> 15); }  // max(e, 0)
+// v_pk_max_i16 / v_pk_min_i16 (clang lowers a packed clamp to -1..1 as a sign idiom of
+// per-half compares and selects, so these are spelled out)
+__device__ __forceinline__ sao_s2 sao_pkmax(sao_s2 a, sao_s2 b) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, %2" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, a)), "v"(__builtin_bit_cast(uint32_t, b)));
+  return sao_pair(r);
+}
+__device__ __forceinline__ sao_s2 sao_pkmin(sao_s2 a, sao_s2 b) {
+  uint32_t r;
+  asm("v_pk_min_i16 %0, %1, %2" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, a)), "v"(__builtin_bit_cast(uint32_t, b)));
+  return sao_pair(r);
+}
 
 __device__ __forceinline__ void sao_tile_pos(int i, int& c, int& j) {
   c = i < kSaoT * kSaoT ? 0 : (i < kSaoT * kSaoT + kSaoTc * kSaoTc ? 1 : 2);
@@ -459,42 +471,53 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   if (kSaoBandOffsets)
     for (int i = tid; i < 3 * 32 * 16; i += 256) (&bh[0][0][0])[i] = 0;
   {  // deblocked CTB + 1-sample ring as aligned dwords (a CTB edge is a multiple of 4, so a
-     // dword is wholly inside or wholly outside the plane): luma 34 rows x 10 dwords, chroma
-     // 18 x 6 each; every load is issued before the first LDS store
-    constexpr int kL = 34 * 10, kC = 18 * 6, kItems = kL + 2 * kC, kPer = (kItems + 255) / 256;
-    uint32_t v[kPer], inside = 0;
+     // dword is wholly inside or wholly outside the plane): luma 34 rows x 10 dwords (items
+     // tid, tid + 256), chroma 2 x 18 rows x 6 dwords (item tid); each slot has one component,
+     // so the row / dword split is a division by a constant.  Every load is issued before the
+     // first LDS store.  The 4 bytes land as two int16 pairs (v_perm), each one aligned
+     // dword store: dword d of a row covers tile columns 4d - 3 .. 4d, so pair 0 is stored
+     // for d >= 1 and pair 1 for d < last (column -1 / T are the pitch padding, never read).
+    uint32_t* tile32 = reinterpret_cast<uint32_t*>(tile);
+    uint32_t v[3];
+    int at[3], dw[3], nd[3];
+    bool act[3], in[3];
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int i = tid + 256 * k;
-      v[k] = 0;
-      if (i < kItems) {
-        const int c = i < kL ? 0 : (i < kL + kC ? 1 : 2), j = c == 0 ? i : i - kL - (c - 1) * kC;
-        const int nd = c ? 6 : 10, n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
-        const int x = cx * n - 4 + 4 * (j % nd), y = cy * n - 1 + j / nd;
-        if (x >= 0 && x < w && y >= 0 && y < h) {
-          v[k] = *reinterpret_cast<const uint32_t*>(deb.plane(c, b, g) + (long)y * w + x);
-          inside |= 1u << k;
-        }
+    for (int k = 0; k < 3; ++k) {
+      int c, row, d;
+      if (k < 2) {
+        const int i = tid + 256 * k;
+        c = 0;
+        row = i / 10;
+        d = i - 10 * row;
+        act[k] = i < 34 * 10;
+      } else {
+        const int pl = tid >= 108 ? 1 : 0, j = tid - 108 * pl;
+        c = 1 + pl;
+        row = j / 6;
+        d = j - 6 * row;
+        act[k] = tid < 2 * 108;
       }
+      const int n = c ? 16 : 32, w = c ? g.W / 2 : g.W, h = c ? g.H / 2 : g.H;
+      const int x = cx * n - 4 + 4 * d, y = cy * n - 1 + row;
+      in[k] = act[k] && x >= 0 && x < w && y >= 0 && y < h;
+      v[k] = in[k] ? *reinterpret_cast<const uint32_t*>(deb.plane(c, b, g) + (long)y * w + x) : 0u;
+      at[k] = (sao_tix(c, row, -1) >> 1) + 2 * d - 1;  // dword of tile columns 4d - 3, 4d - 2
+      dw[k] = d;
+      nd[k] = c ? 6 : 10;
     }
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int i = tid + 256 * k;
-      if (i >= kItems) continue;
-      const int c = i < kL ? 0 : (i < kL + kC ? 1 : 2), j = c == 0 ? i : i - kL - (c - 1) * kC;
-      const int nd = c ? 6 : 10, T = c ? kSaoTc : kSaoT;
-      const int row = j / nd, col0 = 4 * (j % nd) - 3;  // tile column of the dword's first byte
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int col = col0 + q;
-        if (col >= 0 && col < T) tile[sao_tix(c, row, col)] = (inside >> k) & 1 ? (int16_t)((v[k] >> (8 * q)) & 255) : (int16_t)-1;
-      }
+    for (int k = 0; k < 3; ++k) {
+      if (!act[k]) continue;
+      const uint32_t lo = in[k] ? __builtin_amdgcn_perm(0u, v[k], 0x0c010c00u) : 0xFFFFFFFFu;  // outside: -1 pairs
+      const uint32_t hi = in[k] ? __builtin_amdgcn_perm(0u, v[k], 0x0c030c02u) : 0xFFFFFFFFu;
+      if (dw[k] >= 1) tile32[at[k]] = lo;
+      if (dw[k] < nd[k] - 1) tile32[at[k] + 1] = hi;
     }
   }
   // one region per wave: waves 0/1 = luma rows 0-15 / 16-31, wave 2 = Cb, wave 3 = Cr.
   // Counts and sums travel packed as sum * 2048 + count (count <= 1024, |sum| <= 255 * 1024):
   // one wave reduction per EO counter, not two.
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar component logic
   const int c = wave < 2 ? 0 : wave - 1;
   const int n = c ? 16 : 32, w = c ? g.W / 2 : g.W;
   const int nsh = c ? 4 : 5;  // log2 n: the sample index splits with shifts, not a runtime division
@@ -505,7 +528,8 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   // neighbour dwords of a pair read once for all 4 classes).  Edge CTBs take the per-sample
   // path with the validity checks.  Both give the same counters.
   static_assert(!kSaoBandOffsets, "the packed statistics carry no band histogram");
-  const bool interior = cx > 0 && cy > 0 && cx < g.wc - 1 && cy < g.hc - 1 && !(diag & 16);  // 16: TV_SAO_PACKED=0 (A/B)
+  const bool packed = !(diag & 16);  // 16: TV_SAO_PACKED=0 (A/B: per-sample statistics and filter)
+  const bool interior = cx > 0 && cy > 0 && cx < g.wc - 1 && cy < g.hc - 1 && packed;
   diag &= 15;
   const int piters = c ? 2 : 4;  // pairs per lane: luma 16 rows x 16 pairs, chroma 16 x 8
   int sv[8] = {};
@@ -534,12 +558,14 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   int eo[4][4];
   if (interior) {
     const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile);
-    sao_s2 cnt[4][4], sum[4][4];
+    // per half and (class, category): sum(orig - deb) * 16 + count, one v_pk_mad per bin
+    // (count <= 4 samples per half, |sum| <= 4 * 255: |acc| < 2^14)
+    sao_s2 acc[4][4];
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) cnt[d][q] = sum[d][q] = sao_s2{0, 0};
-    const sao_s2 zero = {0, 0}, one = {1, 1};
+      for (int q = 0; q < 4; ++q) acc[d][q] = sao_s2{0, 0};
+    const sao_s2 zero = {0, 0}, one = {1, 1}, mone = {-1, -1}, sixteen = {16, 16};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (k >= piters) break;
@@ -563,26 +589,25 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       const sao_s2 v = Cc[1];
       const uint32_t o = sp[k];
       const sao_s2 orig = {(short)(o & 255), (short)(o >> 8)};
-      const sao_s2 dlt = orig - v;
+      const sao_s2 w = (orig - v) * sixteen + one;
       // classes (sao_eo_dir): 0 horizontal, 1 vertical, 2 135 degrees, 3 45 degrees
       const sao_s2 A[4] = {L[1], Cc[0], L[0], R[0]}, Bn[4] = {R[1], Cc[2], R[2], L[2]};
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const sao_s2 e = sao_sign2(v - A[d]) + sao_sign2(v - Bn[d]);  // -2..2
-        const sao_s2 pos = sao_relu2(e), neg = sao_relu2(zero - e);
+        const sao_s2 e = sao_pkmin(sao_pkmax(v - A[d], mone), one) + sao_pkmin(sao_pkmax(v - Bn[d], mone), one);
+        const sao_s2 pos = sao_pkmax(e, zero), neg = sao_pkmax(zero - e, zero);
         const sao_s2 is[4] = {neg >> one, neg & one, pos & one, pos >> one};  // categories 1..4
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          cnt[d][q] += is[q];
-          sum[d][q] += dlt * is[q];
-        }
+        for (int q = 0; q < 4; ++q) acc[d][q] += w * is[q];
       }
     }
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        eo[d][q] = ((int)sum[d][q].x + (int)sum[d][q].y) * 2048 + (int)cnt[d][q].x + (int)cnt[d][q].y;
+      for (int q = 0; q < 4; ++q) {  // both halves: F = 16 * sum + count (count <= 8)
+        const int F = __builtin_amdgcn_sdot2(acc[d][q], one, 0, false), C = F & 15;
+        eo[d][q] = (F - C) * 128 + C;  // sum * 2048 + count
+      }
   } else {
     // EO statistics per lane in one 64-bit register per class: four signed 16-bit fields
     // (category 1..4) of sum(orig - deb) * 16 + count over the lane's <= 8 samples (|field| <=
@@ -620,16 +645,45 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
       }
     }
   }
+  {  // the 16 counters of the wave in one transpose-reduce: each exchange step (lanes 32,
+     // 16, 8, 4 apart) halves the values a lane holds -- it keeps one half and adds the
+     // partner's copy of it -- so lane L ends with counter (L >> 2) summed over 16 lanes; two
+     // quad DPP adds finish the sum (~40 VALU instead of 16 full wave reductions).  Lanes 32
+     // / 16 apart swap with v_permlane32_swap / v_permlane16_swap (gfx950), lanes 8 apart
+     // with a DPP row rotate; the halves are chosen with xor masks, not selects (a select
+     // of two array elements became a dynamically indexed array)
+    int t[16];
 #pragma unroll
-  for (int d = 0; d < 4; ++d)
+    for (int k = 0; k < 16; ++k) t[k] = eo[k >> 2][k & 3];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int tot = wave_sum(eo[d][q]);
-      if (lane == 0 && (tot & 2047)) {
-        atomicAdd(&st[c].eo_n[d][q + 1], tot & 2047);
-        atomicAdd(&st[c].eo_s[d][q + 1], (tot - (tot & 2047)) / 2048);
-      }
+    for (int j = 0; j < 8; ++j) {  // lanes 0-31 keep t[j], lanes 32-63 t[j + 8]
+      const auto r = __builtin_amdgcn_permlane32_swap((unsigned)t[j], (unsigned)t[j + 8], false, false);
+      t[j] = (int)(r[0] + r[1]);
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // even 16-lane rows keep t[j], odd rows t[j + 4]
+      const auto r = __builtin_amdgcn_permlane16_swap((unsigned)t[j], (unsigned)t[j + 4], false, false);
+      t[j] = (int)(r[0] + r[1]);
+    }
+    const int m8 = -((lane >> 3) & 1), m4 = -((lane >> 2) & 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int x = (t[j] ^ t[j + 2]) & m8;
+      t[j] = (t[j] ^ x) + dpp::mov<dpp::kRowRor8>(t[j + 2] ^ x);
+    }
+    {
+      const int x = (t[0] ^ t[1]) & m4;
+      t[0] = (t[0] ^ x) + __shfl_xor(t[1] ^ x, 4, 64);
+    }
+    int tot = t[0];
+    tot += dpp::mov<dpp::kQuadXor1>(tot);
+    tot += dpp::mov<dpp::kQuadXor2>(tot);
+    const int k = lane >> 2;  // class k >> 2, category (k & 3) + 1
+    if ((lane & 3) == 0 && (tot & 2047)) {
+      atomicAdd(&st[c].eo_n[k >> 2][(k & 3) + 1], tot & 2047);
+      atomicAdd(&st[c].eo_s[k >> 2][(k & 3) + 1], (tot - (tot & 2047)) / 2048);
+    }
+  }
   __shared__ SaoTables tab;
   __shared__ uint32_t prm[3];
   __syncthreads();
@@ -678,35 +732,92 @@ __global__ void __launch_bounds__(256) k_sao_decide(FrameSet src, FrameSet deb, 
   if (diag == 3) return;
   __syncthreads();
   // the SAO'd CTB from the tile, 4 samples per dword store: luma 32 rows x 8, chroma 16 x 4;
-  // the squared error against the source (display area) is summed on the way (no k_sse)
+  // the squared error against the source (display area) is summed on the way (no k_sse).
+  // Packed: the dword's samples are two int16 pairs of the tile (aligned dwords; the EO
+  // neighbours of a +-1 column shift are v_alignbyte of two), the category index e + 2 of
+  // both halves selects the biased offsets with one v_perm, and the squared error is a
+  // v_dot2 of the differences.  Neighbours outside the picture (-1) leave the sample as is.
+  static_assert(!kSaoBandOffsets, "the SAO filter has no band-offset path");
   unsigned e2[3] = {0, 0, 0};
+  const uint32_t* tile32 = reinterpret_cast<const uint32_t*>(tile);
   for (int i = tid; i < 256 + 128; i += 256) {
     const int cc = i < 256 ? 0 : (i < 320 ? 1 : 2);
     const int j = cc == 0 ? i : i - 256 - (cc - 1) * 64;
     const int nd = cc ? 4 : 8, nn = cc ? 16 : 32, ww = cc ? g.W / 2 : g.W;
     const int ly = j >> (cc ? 2 : 3), lx0 = 4 * (j & (nd - 1));  // nd = 4 / 8 dwords per row
     const uint32_t p = prm[cc];
-    int dx = 0, dy = 0;
-    if (sao_type(p) == 2) sao_eo_dir(sao_class(p), dx, dy);
-    uint32_t word = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int lx = lx0 + q;
-      const int v = tile[sao_tix(cc, ly + 1, lx + 1)];
-      const int r = sao_type(p) ? sao_sample_nb(v, tile[sao_tix(cc, ly + 1 + dy, lx + 1 + dx)],
-                                                tile[sao_tix(cc, ly + 1 - dy, lx + 1 - dx)], p)
-                                : v;
-      word |= (uint32_t)r << (8 * q);
-    }
     const long at = (long)(cy * nn + ly) * ww + cx * nn + lx0;
-    *reinterpret_cast<uint32_t*>(out.plane(cc, b, g) + at) = word;
     const int dwc = cc ? g.dw / 2 : g.dw, dhc = cc ? g.dh / 2 : g.dh;
-    if (sse && cy * nn + ly < dhc) {
-      const uint32_t sw = *reinterpret_cast<const uint32_t*>(src.plane(cc, b, g) + at);
+    const bool want_sse = sse && cy * nn + ly < dhc;
+    const uint32_t sw = want_sse ? *reinterpret_cast<const uint32_t*>(src.plane(cc, b, g) + at) : 0u;
+    uint32_t word = 0;
+    if (packed) {
+      const int i0 = sao_tix(cc, ly + 1, lx0 + 1) >> 1;  // pairs (lx0, lx0 + 1), (lx0 + 2, lx0 + 3)
+      const uint32_t C0 = tile32[i0], C1 = tile32[i0 + 1];
+      if (sao_type(p) == 2) {
+        int dx, dy;
+        sao_eo_dir(sao_class(p), dx, dy);
+        const int pd = (cc ? kSaoPc : kSaoP) >> 1;  // dwords per tile row
+        const int ra = i0 + dy * pd, rb = i0 - dy * pd;
+        const uint32_t Wa[4] = {tile32[ra - 1], tile32[ra], tile32[ra + 1], tile32[ra + 2]};
+        const uint32_t Wb[4] = {tile32[rb - 1], tile32[rb], tile32[rb + 1], tile32[rb + 2]};
+        // pair k of a row shifted by s columns (s = -1, 0, 1): dwords W[k .. k + 2] = columns
+        // lx0 + 2k - 2 .. lx0 + 2k + 3
+        auto shifted = [](const uint32_t* W, int k, int s) -> uint32_t {
+          return s == 0 ? W[k + 1] : s < 0 ? __builtin_amdgcn_alignbyte(W[k + 1], W[k], 2)
+                                           : __builtin_amdgcn_alignbyte(W[k + 2], W[k + 1], 2);
+        };
+        // biased offsets (o + 8) by category index e + 2: bytes {o0, o1, 8 (none), o2 | o3}
+        const uint32_t t0 = ((p >> 7) & 15) | ((p >> 11) & 15) << 8 | 8u << 16 | ((p >> 15) & 15) << 24;
+        const uint32_t t1 = (p >> 19) & 15;
+        const sao_s2 two = {2, 2}, eight = {8, 8};
+        const sao_u2 u8s = {8, 8};
+        uint32_t r2[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const sao_s2 v = sao_pair(k ? C1 : C0);
+          const sao_s2 A = sao_pair(shifted(Wa, k, dx)), B = sao_pair(shifted(Wb, k, -dx));
+          const sao_s2 inv = (A | B) >> 15;  // -1 where a neighbour is outside the picture
+          const sao_s2 e = (sao_sign2(v - A) + sao_sign2(v - B)) & ~inv;
+          const uint32_t sel = __builtin_bit_cast(uint32_t, e + two) | 0x0c000c00u;
+          const sao_s2 off = sao_pair(__builtin_amdgcn_perm(t1, t0, sel));
+          const sao_s2 r = sao_relu2(v + off - eight);  // -7 .. 262 -> 0 .. 262
+          // >= 256 -> low byte 0xFF (only the low byte of each half is kept)
+          r2[k] = __builtin_bit_cast(uint32_t, r | (sao_s2{0, 0} - __builtin_bit_cast(sao_s2, __builtin_bit_cast(sao_u2, r) >> u8s)));
+        }
+        word = __builtin_amdgcn_perm(r2[1], r2[0], 0x06040200u);
+      } else {
+        word = __builtin_amdgcn_perm(C1, C0, 0x06040200u);
+      }
+    } else {
+      int dx = 0, dy = 0;
+      if (sao_type(p) == 2) sao_eo_dir(sao_class(p), dx, dy);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int d = (int)((sw >> (8 * q)) & 255) - (int)((word >> (8 * q)) & 255);
-        e2[cc] += cx * nn + lx0 + q < dwc ? (unsigned)(d * d) : 0u;
+        const int lx = lx0 + q;
+        const int v = tile[sao_tix(cc, ly + 1, lx + 1)];
+        const int r = sao_type(p) ? sao_sample_nb(v, tile[sao_tix(cc, ly + 1 + dy, lx + 1 + dx)],
+                                                  tile[sao_tix(cc, ly + 1 - dy, lx + 1 - dx)], p)
+                                  : v;
+        word |= (uint32_t)r << (8 * q);
+      }
+    }
+    *reinterpret_cast<uint32_t*>(out.plane(cc, b, g) + at) = word;
+    if (want_sse) {
+      if (cx * nn + lx0 + 4 <= dwc) {  // the whole dword is in the display area
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t sel = h ? 0x0c030c02u : 0x0c010c00u;
+          const sao_s2 d = sao_pair(__builtin_amdgcn_perm(0u, sw, sel)) - sao_pair(__builtin_amdgcn_perm(0u, word, sel));
+          const sao_u2 dd = __builtin_bit_cast(sao_u2, d * d);  // <= 65025 per half
+          e2[cc] = __builtin_amdgcn_udot2(dd, sao_u2{1, 1}, e2[cc], false);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = (int)((sw >> (8 * q)) & 255) - (int)((word >> (8 * q)) & 255);
+          e2[cc] += cx * nn + lx0 + q < dwc ? (unsigned)(d * d) : 0u;
+        }
       }
     }
   }
