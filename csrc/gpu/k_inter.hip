@@ -84,6 +84,15 @@ __device__ __forceinline__ void me_blk_geom(int bi, int& bx, int& by, int& l2) {
 __device__ __forceinline__ int me_blk8_of(int q, int r) {
   return (((q >> 1) * 2 + (r >> 1)) << 2) + (q & 1) * 2 + (r & 1);
 }
+// the 4 byte differences a - b as two dwords of int16 pairs (residual = source - prediction)
+__device__ __forceinline__ uint2 bytes_minus(uint32_t a, uint32_t b) {
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  const s2 lo = __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, a, 0x0c010c00u)) -
+                __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, b, 0x0c010c00u));
+  const s2 hi = __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, a, 0x0c030c02u)) -
+                __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, b, 0x0c030c02u));
+  return make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+}
 __device__ __forceinline__ int phase_at(const uint8_t* P, const Geo& g, int x, int y) {
   x = clip3(-8, g.W + 7, x);
   y = clip3(-8, g.H + 7, y);
@@ -679,6 +688,7 @@ struct PReconLds {
   int qsad[4], split;         // RQT: luma residual SAD per quadrant of a 32x32 CU, the decision
   int qsplit[4];              // RQT of the 16x16 CU in quadrant q (four 8x8 TBs)
   int qintra[4];              // quadrant q is an intra CU of a P picture (k_pintra_recon codes it)
+  uint32_t ctap[8];           // chroma filter of fraction f as 4 signed bytes
 };
 
 // block size (log2) of the TB owning luma sample (x, y) / chroma sample (x, y) of the CTB
@@ -704,13 +714,16 @@ __device__ __forceinline__ bool pr_zeroed(const PReconLds& L, int id) {
   return L.nz[id] == 0 || (L.nz[id] == 1 && L.sa[id] == 1 && L.dc[id] == 0);
 }
 
-// WPE: waves per SIMD the register allocation must allow (6: 79 VGPRs; 7: 72, no scratch;
-// 8: 64 + a 12-byte spill, measured +2.3 % at 1080p) -- TV_RECON_WPE for same-box A/B, default 8.
+// WPE: waves per SIMD the register allocation must allow (6: 80 VGPRs; 7: 72, no scratch;
+// 8: 64 + a 36-byte spill since the packed prediction) -- TV_RECON_WPE for same-box A/B,
+// default 7 (+1.9 % over 8 at 1080p, profiles/r6_recon/).
 template <int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) k_inter_recon(FrameSet src, FrameSet ref, const uint8_t* phase,
                                                      FrameSet rec, DecisionSet dec, Geo g, int tile_skip,
                                                      FrameSet ref1, const uint8_t* phase1) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int diag = tile_skip >> 8;  // TV_DIAG_RECON_STOP (timing only)
+  tile_skip &= 255;
   int ctu, b;
   xcd_ctb(ctu, b);
   const int qp = dec.qp[b];
@@ -728,6 +741,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     L.mv1[tid][1] = dec.mv1 ? dec.mv1[2 * u + 1] : 0;
   }
   if (tid < 48) L.nz[tid] = L.sa[tid] = L.dc[tid] = 0;
+  if (tid < 8)
+    L.ctap[tid] = (uint32_t)(uint8_t)kChromaFilter[tid][0] | (uint32_t)(uint8_t)kChromaFilter[tid][1] << 8 |
+                  (uint32_t)(uint8_t)kChromaFilter[tid][2] << 16 | (uint32_t)(uint8_t)kChromaFilter[tid][3] << 24;
   if (tid == 0) L.split = 0;
   if (tid < 4) {
     L.qsplit[tid] = 0;
@@ -743,19 +759,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     const uint8_t* S = src.plane(0, b, g);
     const uint8_t* ph = phase + (long)b * 16 * g.psz;
     const uint8_t* ph1 = phase1 ? phase1 + (long)b * 16 * g.psz : nullptr;
-    for (int i = tid; i < 1024; i += 256) {
-      const int x = i & 31, y = i >> 5, un = (y >> 3) * 4 + (x >> 3);
+    {  // uni-prediction: the reference's phase plane holds the final samples; one item = 4
+       // samples of a row of one 8x8 unit (a dword of prediction, two int16 residual pairs)
+      const int x = (tid & 7) * 4, y = tid >> 3, un = (y >> 3) * 4 + (x >> 3);
       const int d = L.dir[un];
-      int p;
-      if (d != 3) {  // uni-prediction: the reference's phase plane holds the final samples
+      if (d != 3) {  // bi units: below, one wave per unit
         const int mvx = d == 1 ? L.mv[un][0] : L.mv1[un][0], mvy = d == 1 ? L.mv[un][1] : L.mv1[un][1];
         const uint8_t* P = (d == 1 ? ph : ph1) + (long)((mvx & 3) + 4 * (mvy & 3)) * g.psz;
-        p = phase_at(P, g, cx + x + (mvx >> 2), cy + y + (mvy >> 2));
-      } else {
-        continue;  // bi units: below, one wave per unit
+        const int px = cx + x + (mvx >> 2), py = clip3(-8, g.H + 7, cy + y + (mvy >> 2));
+        const uint8_t* row = P + (long)(py + 8) * g.pw16;
+        const int bx = px + 8, a4 = bx & ~3;
+        uint32_t pw;
+        if (bx >= 0 && a4 + 7 < g.pw16) {  // in the padded row: two aligned dwords
+          const uint32_t d0 = *reinterpret_cast<const uint32_t*>(row + a4);
+          const uint32_t d1 = *reinterpret_cast<const uint32_t*>(row + a4 + 4);
+          pw = __builtin_amdgcn_alignbyte(d1, d0, bx & 3);
+        } else {
+          pw = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) pw |= (uint32_t)phase_at(P, g, px + k, cy + y + (mvy >> 2)) << (8 * k);
+        }
+        const uint32_t sw = *reinterpret_cast<const uint32_t*>(S + (long)(cy + y) * g.W + cx + x);
+        *reinterpret_cast<uint32_t*>(&L.predY[y * 32 + x]) = pw;
+        *reinterpret_cast<uint2*>(&L.resY[y * 32 + x]) = bytes_minus(sw, pw);
       }
-      L.predY[i] = (uint8_t)p;
-      L.resY[i] = (int16_t)((int)S[(long)(cy + y) * g.W + cx + x] - p);
     }
     // bi-predicted 8x8 units (8.5.3.3.4.2): per list the 15x15 reference window is staged
     // in this wave's LDS, the 8-tap horizontal pass gives 15 x 8 intermediates, the vertical
@@ -808,25 +835,67 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       L.predY[y * 32 + x] = (uint8_t)p;
       L.resY[y * 32 + x] = (int16_t)((int)S[(long)(cy + y) * g.W + cx + x] - p);
     }
-    for (int i = tid; i < 512; i += 256) {
-      const int pl = i >> 8, x = i & 15, y = (i >> 4) & 15, un = (y >> 2) * 4 + (x >> 2);
+    // chroma: one item = 4 samples of a row of one 4x4 unit (128 items), the separable 4-tap
+    // filter on packed bytes: per reference row the 7 samples are two dwords, each output a
+    // v_dot4 of a v_alignbyte window against the biased taps (samples ^ 0x80 as int8: the
+    // bias is 128 * 64 = 8192), then the vertical taps.  The 0-fraction filter {0, 64, 0, 0}
+    // makes the one 2-D formula exact for every fraction (8.5.3.3.3.2, as mc_chroma_inter).
+    if (tid < 128) {
+      const int pl = tid >> 6, y = (tid >> 2) & 15, x = (tid & 3) * 4, un = (y >> 2) * 4 + (x >> 2);
       const int d = L.dir[un];
       const int gx = (cx >> 1) + x, gy = (cy >> 1) + y;
-      int p;
-      if (d != 3) {
-        const int mvx = d == 1 ? L.mv[un][0] : L.mv1[un][0], mvy = d == 1 ? L.mv[un][1] : L.mv1[un][1];
-        const uint8_t* Rf = (d == 1 ? ref : ref1).plane(1 + pl, b, g);
-        p = mc_chroma_sample(Rf, Wc, Wc, Hc, gx + (mvx >> 3), gy + (mvy >> 3), mvx & 7, mvy & 7);
-      } else {
-        const int m0x = L.mv[un][0], m0y = L.mv[un][1], m1x = L.mv1[un][0], m1y = L.mv1[un][1];
-        const int a = mc_chroma_inter(ref.plane(1 + pl, b, g), Wc, Wc, Hc, gx + (m0x >> 3), gy + (m0y >> 3), m0x & 7,
-                                      m0y & 7);
-        const int c = mc_chroma_inter(ref1.plane(1 + pl, b, g), Wc, Wc, Hc, gx + (m1x >> 3), gy + (m1y >> 3), m1x & 7,
-                                      m1y & 7);
-        p = bipred_sample(a, c);
+      int prev[4] = {0, 0, 0, 0};  // bi: the list-0 intermediates
+      uint32_t pw = 0;
+#pragma unroll 1
+      for (int l = 0; l < 2; ++l) {
+        if (!(d & (1 << l))) continue;
+        const int mvx = l ? L.mv1[un][0] : L.mv[un][0], mvy = l ? L.mv1[un][1] : L.mv[un][1];
+        const uint8_t* Rf = (l ? ref1 : ref).plane(1 + pl, b, g);
+        const uint32_t tx = L.ctap[mvx & 7], ty = L.ctap[mvy & 7];
+        const int x0 = gx + (mvx >> 3) - 1, y0 = gy + (mvy >> 3) - 1;
+        int acc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint8_t* row = Rf + (long)clip3(0, Hc - 1, y0 + j) * Wc;
+          const int a4 = x0 & ~3;
+          uint32_t w0, w1;
+          if (x0 >= 0 && a4 + 11 < Wc) {
+            const uint32_t d0 = *reinterpret_cast<const uint32_t*>(row + a4);
+            const uint32_t d1 = *reinterpret_cast<const uint32_t*>(row + a4 + 4);
+            const uint32_t d2 = *reinterpret_cast<const uint32_t*>(row + a4 + 8);
+            w0 = __builtin_amdgcn_alignbyte(d1, d0, x0 & 3);
+            w1 = __builtin_amdgcn_alignbyte(d2, d1, x0 & 3);
+          } else {
+            w0 = w1 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              w0 |= (uint32_t)row[clip3(0, Wc - 1, x0 + k)] << (8 * k);
+              w1 |= (uint32_t)row[clip3(0, Wc - 1, x0 + 4 + k)] << (8 * k);
+            }
+          }
+          w0 ^= 0x80808080u;
+          w1 ^= 0x80808080u;
+          const int fyj = (int)(int8_t)(ty >> (8 * j));
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t win = k == 0 ? w0 : __builtin_amdgcn_alignbyte(w1, w0, k);
+            acc[k] += fyj * __builtin_amdgcn_sdot4((int)win, (int)tx, 8192, false);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int v = acc[k] >> 6;  // the 14-bit intermediate
+          if (d == 3 && l == 0) {
+            prev[k] = v;
+          } else {
+            const int p = d == 3 ? bipred_sample(prev[k], v) : clip_pixel((v + 32) >> 6);
+            pw |= (uint32_t)p << (8 * k);
+          }
+        }
       }
-      L.predC[pl][y * 16 + x] = (uint8_t)p;
-      L.resC[pl][y * 16 + x] = (int16_t)((int)src.plane(1 + pl, b, g)[(long)gy * Wc + gx] - p);
+      const uint32_t sw = *reinterpret_cast<const uint32_t*>(src.plane(1 + pl, b, g) + (long)gy * Wc + gx);
+      *reinterpret_cast<uint32_t*>(&L.predC[pl][y * 16 + x]) = pw;
+      *reinterpret_cast<uint2*>(&L.resC[pl][y * 16 + x]) = bytes_minus(sw, pw);
     }
   }
   __syncthreads();
@@ -865,7 +934,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   // tile t: luma (whole: 32x32 tile ti,tj = t>>1, t&1; else quadrant t) for t < 4, chroma
   // (whole: plane t-4 as one 16x16 TB; else the Cb|Cr pair of quadrant t-4) for t >= 4.
   // ---------------------------------------------------------------- stage 1: T * R
-  for (int t = wave; t < ntiles; t += 4) {
+  // (diag 1: no forward transform -- every TB counts as empty, the stream stays consistent)
+  for (int t = wave; t < (diag == 1 ? 0 : ntiles); t += 4) {
     int o[4];
     if (t < 4) {
       if (whole) {
@@ -919,7 +989,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
     if (origin) L.dc[id] = lev;
   };
-  for (int t = wave; t < ntiles; t += 4) {
+  for (int t = wave; t < (diag == 1 ? 0 : ntiles); t += 4) {
     int o[4];
     if (t < 4) {
       if (whole) {
@@ -964,16 +1034,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   __syncthreads();
   // ---- final levels (dropped TBs zeroed) -> the level planes; cbf per CU
   {
+    // 4 levels (one TB: TBs are >= 4 wide and 4-aligned) per item, one 8-byte store
     int16_t* LY = dec.coef_y + b * g.ysz + (long)cy * g.W + cx;
-    for (int i = tid; i < 1024; i += 256) {
-      const int x = i & 31, y = i >> 5;
-      if (pr_zeroed(L, pr_tb_luma(L, x, y))) L.resY[i] = 0;
-      LY[(long)y * g.W + x] = L.resY[i];
+    {
+      const int x = (tid & 7) * 4, y = tid >> 3;
+      uint2* r = reinterpret_cast<uint2*>(&L.resY[y * 32 + x]);
+      if (pr_zeroed(L, pr_tb_luma(L, x, y))) *r = make_uint2(0u, 0u);
+      *reinterpret_cast<uint2*>(LY + (long)y * g.W + x) = *r;
     }
-    for (int i = tid; i < 512; i += 256) {
-      const int pl = i >> 8, x = i & 15, y = (i >> 4) & 15;
-      if (pr_zeroed(L, pr_tb_chroma(L, pl, x, y))) L.resC[pl][y * 16 + x] = 0;
-      (pl ? dec.coef_v : dec.coef_u)[b * g.csz + (long)((cy >> 1) + y) * Wc + (cx >> 1) + x] = L.resC[pl][y * 16 + x];
+    if (tid < 128) {
+      const int pl = tid >> 6, y = (tid >> 2) & 15, x = (tid & 3) * 4;
+      uint2* r = reinterpret_cast<uint2*>(&L.resC[pl][y * 16 + x]);
+      if (pr_zeroed(L, pr_tb_chroma(L, pl, x, y))) *r = make_uint2(0u, 0u);
+      *reinterpret_cast<uint2*>((pl ? dec.coef_v : dec.coef_u) + b * g.csz + (long)((cy >> 1) + y) * Wc + (cx >> 1) + x) = *r;
     }
     if (tid < 8) {  // tiles whose TBs all dropped out skip the inverse transform
       bool z = true;
@@ -997,6 +1070,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
   }
   __syncthreads();
+  if (diag == 3) return;
   // --------------------------------------- stage 3: T^T * dequant(levels)  (split d)
   for (int t = wave; t < ntiles; t += 4) {
     if (L.tzero[t]) continue;  // wave-uniform: an all-zero tile reconstructs to the prediction
@@ -1038,6 +1112,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
   }
   __syncthreads();
+  if (diag == 4) return;
   // ------------------------------------- stage 4: G * T + prediction -> reconstruction
   for (int t = wave; t < ntiles; t += 4) {
     int o[4];
@@ -1130,7 +1205,11 @@ void launch_rc_crf(const uint8_t* q, const int* ccost, int8_t* qp, const Geo& g,
 static int recon_tile_skip() {
   static const int v = [] {
     const char* e = std::getenv("TV_RECON_TILE_SKIP");
-    return e ? std::atoi(e) : 1;
+    // timing diagnostics only (TV_DIAG_RECON_STOP=1: no forward transform (all TBs empty), 3:
+    // stop after the level write, 4: after inverse stage 1; the reconstruction is then
+    // incomplete) -- never in production
+    const char* d = std::getenv("TV_DIAG_RECON_STOP");
+    return (e ? std::atoi(e) : 1) | (d ? (std::atoi(d) & 15) << 8 : 0);
   }();
   return v;
 }
@@ -1139,7 +1218,7 @@ using ReconKernel = decltype(&k_inter_recon<7>);
 static ReconKernel recon_kernel() {
   static const ReconKernel k = [] {
     const char* e = std::getenv("TV_RECON_WPE");
-    const int w = e ? std::atoi(e) : 8;
+    const int w = e ? std::atoi(e) : 7;
     return w == 6 ? &k_inter_recon<6> : (w == 8 ? &k_inter_recon<8> : &k_inter_recon<7>);
   }();
   return k;

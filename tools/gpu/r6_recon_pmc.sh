@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 6: k_inter_recon phase costs -- TV_DIAG_RECON_STOP=1 (no forward transform), 3, 4 (stop after
+# the level write / inverse stage 1; timing and counting only), instruction
+# counters per stop and a single-group kernel trace per stop.  Usage: r6_recon_pmc.sh <tag>
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export PYTHONPATH=$PWD TMPDIR=/tmp TV_NO_AUTOBUILD=1
+O=gpurun_out/${1:-r6recon}; mkdir -p $O
+for st in 1 3 4 0; do
+  TV_DIAG_RECON_STOP=$st timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_MFMA SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --output-format csv -d $O/p$st -o run -- python3 bench.py --no-4k --steps 1 --warmup 1 --batch 16 --gop 8 > $O/p$st.log 2>&1 || { echo "stop $st failed"; tail -n 5 $O/p$st.log; exit 1; }
+  echo "== stop $st"; python3 tools/pmcsum.py $(find $O/p$st -name "*counter_collection.csv" | head -1) k_inter_recon
+  TV_ENGINE_GROUPS=1 TV_DIAG_RECON_STOP=$st timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/s$st -o run -- python3 bench.py --no-4k --steps 2 --warmup 1 > $O/s$st.log 2>&1 || { echo "trace $st failed"; exit 1; }
+  python3 tools/profsum.py $(find $O/s$st -name "*kernel_trace.csv" | head -1) --skip 0.3 2>&1 | grep -E "inter_recon"
+done 2>&1 | tee $O/summary.txt
