@@ -1,5 +1,6 @@
 // mpeg2.cpp — MPEG-2 video decoder + fixture writer (see tv/mpeg2.h).
 #include "tv/mpeg2.h"
+#include "mpeg2_wtab.h"
 
 #include <algorithm>
 #include <array>
@@ -286,6 +287,7 @@ class Writer {
     }
   }
   void put(Vc c) { put(c.code, c.len); }
+  void put(wtab::Code c) { put(c.code, c.len); }
   void align() {
     if (nacc_) put(0, 8 - nacc_);
   }
@@ -1256,6 +1258,9 @@ struct Lcg {
   int below(int n) { return int(next() % uint32_t(n)); }
 };
 
+// quantiser_scale from quantiser_scale_code with the writer's copy of Table 7-6
+inline int w_quant_scale(int code, int qst) { return qst ? wtab::get().nonlinear_q[code] : 2 * code; }
+
 class Encoder {
  public:
   Encoder(const EncConfig& c, std::vector<uint8_t>& es) : c_(c), w_(es), es_(es), rng_{c.seed * 2654435761u + 7} {
@@ -1266,7 +1271,7 @@ class Encoder {
     seq_.progressive_seq = c.interlaced ? 0 : 1;
     if (c.custom_matrices) {
       for (int i = 0; i < 64; ++i) {
-        seq_.intra_q[i] = uint8_t(std::min(255, kDefaultIntra[i] + (i % 5)));
+        seq_.intra_q[i] = uint8_t(std::min(255, 8 + 2 * ((i >> 3) + (i & 7)) + (i % 5)));  // any custom matrix
         seq_.inter_q[i] = uint8_t(14 + (i * 7) % 9);
       }
       seq_.intra_q[0] = 8;
@@ -1287,10 +1292,10 @@ class Encoder {
     w_.put(0, 1);
     w_.put(c_.custom_matrices, 1);
     if (c_.custom_matrices)
-      for (int i = 0; i < 64; ++i) w_.put(seq_.intra_q[kScan[0][i]], 8);
+      for (int i = 0; i < 64; ++i) w_.put(seq_.intra_q[wt_.scan[0][i]], 8);
     w_.put(c_.custom_matrices, 1);
     if (c_.custom_matrices)
-      for (int i = 0; i < 64; ++i) w_.put(seq_.inter_q[kScan[0][i]], 8);
+      for (int i = 0; i < 64; ++i) w_.put(seq_.inter_q[wt_.scan[0][i]], 8);
     w_.start_code(0xB5);  // sequence_extension
     w_.put(1, 4);
     w_.put(0x48, 8);  // Main Profile @ Main Level
@@ -1547,28 +1552,31 @@ class Encoder {
   // ---------------------------------------------------------------- syntax writing ---
   void put_mba(int inc) {
     while (inc > 33) {
-      w_.put(kMbaEscape);
+      w_.put(wt_.mba_escape);
       inc -= 33;
     }
-    w_.put(kMba[inc]);
+    w_.put(wt_.mba[inc]);
   }
 
   void put_type(int flags) {
-    const TypeCode* t;
+    const wtab::TypeEntry* t;
     int n;
     if (pi_.type == 1) {
-      t = kTypeI;
+      t = wt_.type_i;
       n = 2;
     } else if (pi_.type == 2) {
-      t = kTypeP;
+      t = wt_.type_p;
       n = 7;
     } else {
-      t = kTypeB;
+      t = wt_.type_b;
       n = 11;
     }
+    // the writer's flag bits are its own (wtab) and mean the same columns of B.2-B.4
+    const int wf = (flags & MQ ? wtab::kQuant : 0) | (flags & MF ? wtab::kFwd : 0) | (flags & MB ? wtab::kBwd : 0) |
+                   (flags & MP ? wtab::kPattern : 0) | (flags & MI ? wtab::kIntra : 0);
     for (int i = 0; i < n; ++i)
-      if (t[i].flags == flags) {
-        w_.put(t[i].c);
+      if (t[i].flags == wf) {
+        w_.put(wtab::detail::bits(t[i].bits));
         return;
       }
     fail("writer: no macroblock_type for these flags");
@@ -1586,7 +1594,7 @@ class Encoder {
       if (delta < 0) mc = -mc;
     }
     if (std::abs(mc) > 16) fail("writer: motion vector out of the f_code range");
-    w_.put(kMotion[std::abs(mc)]);
+    w_.put(wt_.motion[std::abs(mc)]);
     if (mc) w_.put(mc < 0, 1);
     if (f != 1 && mc) w_.put(resid, rsize);
   }
@@ -1623,9 +1631,9 @@ class Encoder {
   }
 
   void put_block(const int32_t* qf, bool intra, int b) {
-    const uint8_t* scan = kScan[pi_.alt];
+    const uint8_t* scan = wt_.scan[pi_.alt];
     int start = 0;
-    const CoefLut& lut = tabs().coef[intra && pi_.ivlc ? 1 : 0];
+    const int vlc = intra && pi_.ivlc ? 1 : 0;
     if (intra) {
       const int cc = b < 4 ? 0 : b - 3;
       const int diff = qf[0] - dc_pred_[cc];
@@ -1633,7 +1641,7 @@ class Encoder {
       const int a = std::abs(diff);
       int size = 0;
       while ((1 << size) <= a) ++size;
-      w_.put(cc == 0 ? kDcLuma[size] : kDcChroma[size]);
+      w_.put(cc == 0 ? wt_.dc_luma[size] : wt_.dc_chroma[size]);
       if (size) w_.put(diff > 0 ? diff : diff + (1 << size) - 1, size);
       start = 1;
     }
@@ -1649,18 +1657,18 @@ class Encoder {
       if (first && run == 0 && a == 1) {
         w_.put(1, 1);
         w_.put(v < 0, 1);
-      } else if (run < 32 && a <= 40 && lut.enc[run][a].len) {
-        w_.put(lut.enc[run][a]);
+      } else if (run < 32 && a <= 40 && wt_.coef[vlc][run][a].len) {
+        w_.put(wt_.coef[vlc][run][a]);
         w_.put(v < 0, 1);
       } else {
-        w_.put(kEsc);
+        w_.put(wt_.escape);
         w_.put(run, 6);
         w_.put(v & 0xfff, 12);
       }
       first = false;
       run = 0;
     }
-    w_.put(lut.eob);
+    w_.put(wt_.eob[vlc]);
   }
 
   // ---------------------------------------------------------------- residual ---------
@@ -1776,11 +1784,11 @@ class Encoder {
           const int dct_type = (frame_pic && !pi_.fpfd) ? rng_.below(2) : 0;
           int32_t qf[6][64];
           uint8_t ry[256], ru[64], rv[64];
-          int cbp = code_mb(sy, su, sv, k, dct_type, quant_scale(qc, pi_.qst), qf, ry, ru, rv);
+          int cbp = code_mb(sy, su, sv, k, dct_type, w_quant_scale(qc, pi_.qst), qf, ry, ru, rv);
           if ((flags & MQ) && cbp == 0 && !k.intra) {
             flags &= ~MQ;
             qc = qcode_;
-            cbp = code_mb(sy, su, sv, k, dct_type, quant_scale(qc, pi_.qst), qf, ry, ru, rv);
+            cbp = code_mb(sy, su, sv, k, dct_type, w_quant_scale(qc, pi_.qst), qf, ry, ru, rv);
           }
           qcode_ = qc;
           const bool edge = mbx == x0 || mbx == x1 - 1;
@@ -1813,7 +1821,7 @@ class Encoder {
           if (flags & MQ) w_.put(qcode_, 5);
           if (flags & MF) put_vectors(k.m, 0);
           if (flags & MB) put_vectors(k.m, 1);
-          if (flags & MP) w_.put(kCbp[cbp]);
+          if (flags & MP) w_.put(wt_.cbp[cbp]);
           for (int b = 0; b < 6; ++b)
             if (cbp & (32 >> b)) put_block(qf[b], k.intra, b);
           if (k.intra) {
@@ -1946,6 +1954,7 @@ class Encoder {
   EncConfig c_;
   Writer w_;
   std::vector<uint8_t>& es_;
+  const wtab::Tables& wt_ = wtab::get();  // the writer's own Annex B transcription
   SeqHeader seq_;
   PicInfo pi_;
   Lcg rng_;
@@ -2101,26 +2110,59 @@ int tv_mpeg2_decode(const uint8_t* d, size_t n, int64_t seq_off, int64_t start, 
   });
 }
 
-// the decoder's VLC tables (see models/mpeg2.py table())
+// the decoder's VLC tables (see models/mpeg2.py table()); which + 100: the fixture writer's
+// own transcription (mpeg2_wtab.h) in the same layout, so the two can be compared entry by
+// entry.  7 / 8 / 9: macroblock_type of I / P / B pictures (value = the flag bits MQ 1, MF 2,
+// MB 4, MP 8, MI 16).
 int tv_mpeg2_table(int which, int32_t* code, int32_t* len, int32_t* value, int cap) {
   std::vector<std::array<int32_t, 3>> t;
   auto add = [&](Vc c, int v) { t.push_back({c.code, c.len, v}); };
+  auto addw = [&](wtab::Code c, int v) { t.push_back({c.code, c.len, v}); };
+  const bool wr = which >= 100;
+  which %= 100;
+  const wtab::Tables& W = wtab::get();
   if (which == 0 || which == 1) {
     const CoefLut& l = tabs().coef[which];
     for (int r = 0; r < 32; ++r)
-      for (int lv = 1; lv <= 40; ++lv)
-        if (l.enc[r][lv].len) add(l.enc[r][lv], r << 8 | lv);
-    add(l.eob, -1);
-    add(kEsc, -2);
+      for (int lv = 1; lv <= 40; ++lv) {
+        if (wr && W.coef[which][r][lv].len) addw(W.coef[which][r][lv], r << 8 | lv);
+        if (!wr && l.enc[r][lv].len) add(l.enc[r][lv], r << 8 | lv);
+      }
+    if (wr) {
+      addw(W.eob[which], -1);
+      addw(W.escape, -2);
+    } else {
+      add(l.eob, -1);
+      add(kEsc, -2);
+    }
   } else if (which == 2) {
-    for (int i = 0; i < 64; ++i) add(kCbp[i], i);
+    for (int i = 0; i < 64; ++i) wr ? addw(W.cbp[i], i) : add(kCbp[i], i);
   } else if (which == 3) {
-    for (int i = 0; i <= 16; ++i) add(kMotion[i], i);
+    for (int i = 0; i <= 16; ++i) wr ? addw(W.motion[i], i) : add(kMotion[i], i);
   } else if (which == 4 || which == 5) {
-    for (int i = 0; i < 12; ++i) add(which == 4 ? kDcLuma[i] : kDcChroma[i], i);
+    for (int i = 0; i < 12; ++i)
+      wr ? addw(which == 4 ? W.dc_luma[i] : W.dc_chroma[i], i) : add(which == 4 ? kDcLuma[i] : kDcChroma[i], i);
   } else if (which == 6) {
-    for (int i = 1; i <= 33; ++i) add(kMba[i], i);
-    add(kMbaEscape, 0);
+    for (int i = 1; i <= 33; ++i) wr ? addw(W.mba[i], i) : add(kMba[i], i);
+    wr ? addw(W.mba_escape, 0) : add(kMbaEscape, 0);
+  } else if (which >= 7 && which <= 9) {
+    const int n = which == 7 ? 2 : (which == 8 ? 7 : 11);
+    for (int i = 0; i < n; ++i) {
+      if (wr) {
+        const wtab::TypeEntry& e = (which == 7 ? W.type_i : which == 8 ? W.type_p : W.type_b)[i];
+        const int f = (e.flags & wtab::kQuant ? MQ : 0) | (e.flags & wtab::kFwd ? MF : 0) |
+                      (e.flags & wtab::kBwd ? MB : 0) | (e.flags & wtab::kPattern ? MP : 0) |
+                      (e.flags & wtab::kIntra ? MI : 0);
+        addw(wtab::detail::bits(e.bits), f);
+      } else {
+        const TypeCode& e = (which == 7 ? kTypeI : which == 8 ? kTypeP : kTypeB)[i];
+        add(e.c, e.flags);
+      }
+    }
+  } else if (which == 10 || which == 11) {  // scans (code = position, len 0)
+    for (int i = 0; i < 64; ++i) t.push_back({wr ? W.scan[which - 10][i] : kScan[which - 10][i], 0, i});
+  } else if (which == 12) {  // non-linear quantiser_scale
+    for (int i = 0; i < 32; ++i) t.push_back({wr ? W.nonlinear_q[i] : kNonLinearQ[i], 0, i});
   }
   for (int i = 0; i < (int)t.size() && i < cap; ++i) {
     code[i] = t[i][0];

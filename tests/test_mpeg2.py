@@ -75,6 +75,22 @@ def test_vlc_tables_are_the_standard_ones():
     assert mba[1] == "1" and mba[8] == "0000111" and mba[33] == "00000011000" and mba[0] == "00000001000"
 
 
+def test_writer_tables_are_an_independent_transcription():
+    """The fixture writer codes with its own Annex B transcription (csrc/core/mpeg2_wtab.h:
+    spec bit strings, zig-zag generated from the anti-diagonals), not the decoder's numeric
+    tables: the two must agree entry by entry for every table the writer uses, so a typo in
+    either shows up here (and as a mis-decoded round trip below) instead of cancelling out."""
+    for t in range(13):
+        dec, wr = mpeg2.table(t), mpeg2.table(t, writer=True)
+        assert sorted(dec) == sorted(wr), t
+    # structure of the writer's copy on its own: the same Kraft sums as the decoder's
+    kraft = lambda t: sum(2.0 ** -len(c) for c, _ in t)  # noqa: E731
+    assert kraft(mpeg2.table(0, writer=True)) == 1 - 2 ** -12
+    assert kraft(mpeg2.table(1, writer=True)) == 1 - 9 * 2 ** -12
+    zz = [int(c) for c, _ in mpeg2.table(10, writer=True)]
+    assert zz[:10] == [0, 1, 8, 16, 9, 2, 3, 10, 17, 24] and sorted(zz) == list(range(64))
+
+
 @pytest.mark.parametrize("name", sorted(CONFIGS))
 def test_decoder_reproduces_the_writer(name):
     cfg = CONFIGS[name]

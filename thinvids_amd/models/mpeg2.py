@@ -155,13 +155,20 @@ def decode_es(data, first: int = 0, count: int | None = None, stats: dict | None
     return _decode(a, n, so, off, fb, first, count, info["width"], info["height"], stats)
 
 
-def table(which: int) -> list[tuple[str, int]]:
-    """A VLC table of the decoder as (code bits, value): 0 B.14 and 1 B.15 (value run << 8 |
-    level; EOB -1, escape -2), 2 B.9 coded_block_pattern, 3 B.10 motion_code magnitude, 4 / 5
-    B.12 / B.13 dct_dc_size, 6 B.1 macroblock_address_increment (escape 0)."""
-    n = _lib().tv_mpeg2_table(which, None, None, None, 0)
+def table(which: int, writer: bool = False) -> list[tuple[str, int]]:
+    """A VLC table of the decoder (or, writer=True, of the fixture writer's independent
+    transcription, csrc/core/mpeg2_wtab.h) as (code bits, value): 0 B.14 and 1 B.15 (value
+    run << 8 | level; EOB -1, escape -2), 2 B.9 coded_block_pattern, 3 B.10 motion_code
+    magnitude, 4 / 5 B.12 / B.13 dct_dc_size, 6 B.1 macroblock_address_increment (escape 0),
+    7 / 8 / 9 macroblock_type of I / P / B (value = flags MQ 1, MF 2, MB 4, MP 8, MI 16);
+    10 / 11 the zig-zag / alternate scans and 12 the non-linear quantiser_scale as
+    (str(entry), index)."""
+    w = which + (100 if writer else 0)
+    n = _lib().tv_mpeg2_table(w, None, None, None, 0)
     code, ln, val = np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.int32)
-    _lib().tv_mpeg2_table(which, ptr(code, i32p), ptr(ln, i32p), ptr(val, i32p), n)
+    _lib().tv_mpeg2_table(w, ptr(code, i32p), ptr(ln, i32p), ptr(val, i32p), n)
+    if which >= 10:
+        return [(str(int(c)), int(v)) for c, v in zip(code, val)]
     return [(format(int(c), f"0{int(l)}b"), int(v)) for c, l, v in zip(code, ln, val)]
 
 
