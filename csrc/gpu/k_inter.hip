@@ -14,6 +14,7 @@
 //  k_inter_recon  pass B per CTB: luma prediction = phase-plane loads, chroma 4-tap MC,
 //                 residual, MFMA transform/quant, exact inverse, reconstruction.
 #include <cstdlib>
+#include <stdexcept>
 #include <string>
 
 #include "gpu_common.h"
@@ -140,8 +141,10 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
   const uint8_t* C = qcur + (long)b * qw * qh;
   const uint8_t* P = qprev + (long)b * qw * qh;
   __shared__ uint32_t s32[16];
-  __shared__ uint32_t win[kCoarseRows * (kCoarseWords | 1)];
+  extern __shared__ uint32_t win[];  // (8 + 2 rq) rows x ((rq / 2 + 3) | 1) words: sized per launch
+  __shared__ int penL[64];  // the MV-rate table: read per candidate (a global load chain before)
   const int side = 2 * rq + 1, rows = 8 + 2 * rq, wpr = rq / 2 + 3, pitch = wpr | 1;
+  penL[lane] = pen.mv[lane];
   if (lane < 16) s32[lane] = *reinterpret_cast<const uint32_t*>(C + (long)(y0 + (lane >> 1)) * qw + x0 + 4 * (lane & 1));
   for (int w = lane; w < rows * wpr; w += 64) {
     const int r = w / wpr, c = w - r * wpr;
@@ -151,13 +154,18 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
   __syncthreads();
   unsigned best = 0xffffffffu;
   const int groups = rq / 2 + 1;
+  uint32_t sv[16];  // the source block in registers (loop-invariant)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) sv[k] = s32[k];
+  // item = gi * side + dyi, advanced by 64 per pass without a division
+  const int step_g = 64 / side, step_d = 64 - step_g * side;
+  int gi = lane / side, dyi = lane - gi * side;
   for (int item = lane; item < groups * side; item += 64) {
-    const int gi = item / side, dyi = item - gi * side;
     const int dy = dyi - rq, dx0 = 4 * gi - rq;
     unsigned acc[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint32_t s0 = s32[2 * j], s1 = s32[2 * j + 1];
+      const uint32_t s0 = sv[2 * j], s1 = sv[2 * j + 1];
       const int wr = (dyi + j) * pitch + gi;
       const uint32_t w0 = win[wr], w1 = win[wr + 1], w2 = win[wr + 2];
       acc[0] = __builtin_amdgcn_sad_u8(w1, s1, __builtin_amdgcn_sad_u8(w0, s0, acc[0]));
@@ -172,8 +180,14 @@ __global__ void __launch_bounds__(64) k_coarse_me(const uint8_t* qcur, const uin
     for (int sft = 0; sft < 4; ++sft) {
       const int dx = dx0 + sft;
       if (dx > rq) continue;
-      const unsigned v = ((acc[sft] + (unsigned)me_coarse_pen(pen.mv, dx, dy)) << 13) | (unsigned)(dyi * side + dx + rq);
+      const unsigned v = ((acc[sft] + (unsigned)me_coarse_pen(penL, dx, dy)) << 13) | (unsigned)(dyi * side + dx + rq);
       best = v < best ? v : best;
+    }
+    gi += step_g;
+    dyi += step_d;
+    if (dyi >= side) {
+      dyi -= side;
+      ++gi;
     }
   }
   best = wave_min_u32(best);
@@ -1170,7 +1184,10 @@ void launch_quarter(FrameSet src, uint8_t* q, const Geo& g, int B, hipStream_t s
 
 void launch_coarse_me(const MeBuffers& me, const Geo& g, const RcTables* rc, int seq_qp, int range, int B,
                       hipStream_t s) {
-  k_coarse_me<<<dim3(g.wc * g.hc, B), 64, 0, s>>>(me.qcur, me.qprev, g, rc, seq_qp, range / 4, me.cmv, me.ccost);
+  const int rq = range / 4;
+  if (rq > kCoarseMaxRq) throw std::runtime_error("coarse search range too large");
+  const size_t lds = sizeof(uint32_t) * (size_t)(8 + 2 * rq) * (size_t)((rq / 2 + 3) | 1);  // the window only
+  k_coarse_me<<<dim3(g.wc * g.hc, B), 64, lds, s>>>(me.qcur, me.qprev, g, rc, seq_qp, rq, me.cmv, me.ccost);
 }
 
 // CRF (tv/rc_model.h): the frame QP of every segment from its lookahead complexity — the
