@@ -78,6 +78,7 @@ constexpr int kQuadXor1 = 0xB1;       // quad_perm [1,0,3,2]
 constexpr int kQuadXor2 = 0x4E;       // quad_perm [2,3,0,1]
 constexpr int kRowShl4 = 0x104, kRowShr4 = 0x114, kRowShl8 = 0x108, kRowShr8 = 0x118;
 constexpr int kRowRor8 = 0x128;      // lane i <- i ^ 8 within 16 (rotate by 8)
+constexpr int kRowRor4 = 0x124;      // lane i <- (i - 4) mod 16 within the row
 constexpr int kRowHalfMirror = 0x141;  // lane i <- 7 - i within 8
 constexpr int kRowMirror = 0x140;      // lane i <- 15 - i within 16
 template <int CTRL> __device__ __forceinline__ int mov(int v) {

@@ -376,13 +376,28 @@ __global__ void __launch_bounds__(kMeThreads) __attribute__((amdgpu_waves_per_eu
       lb32 = (qd == 0 && v32 < lb32) ? v32 : lb32;
     }
   }
-  // a lane's quadrant is fixed (item stride is a multiple of 4), so lb[] maps to static slots
+  // a lane's quadrant is fixed (item stride is a multiple of 4: quadrant = lane & 3), so lb[]
+  // maps to static slots.  Each slot is reduced over the 16 lanes of its quadrant class:
+  // rotations by 4 and 8 inside a DPP row, then the row pairs and halves exchanged with
+  // v_permlane16_swap / v_permlane32_swap (gfx950) -- lanes 0..3 end with quadrant 0..3's
+  // minima and post them (5 x ~6 VALU instead of 20 full wave reductions)
+  {
+    auto umin = [](unsigned x, unsigned y) { return x < y ? x : y; };
+    const int lane = tid & 63;
 #pragma unroll
-  for (int k = 0; k < 20; ++k) {
-    const int kq = k < 16 ? ((k >> 3) << 1) | ((k >> 1) & 1) : k - 16;  // quadrant of 8x8 raster block k
-    const int kj = k < 16 ? ((k >> 2) & 1) * 2 + (k & 1) : 4;           // its slot in lb[]
-    const unsigned m = wave_min_u32(qd == kq ? lb[kj] : 0xffffffffu);
-    if ((tid & 63) == 0) atomicMin(&best[k], m);
+    for (int j = 0; j < 5; ++j) {
+      unsigned v = lb[j];
+      v = umin(v, (unsigned)dpp::mov<dpp::kRowRor4>((int)v));
+      v = umin(v, (unsigned)dpp::mov<dpp::kRowRor8>((int)v));
+      const auto r16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+      v = umin(r16[0], r16[1]);
+      const auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+      v = umin(r32[0], r32[1]);
+      if (lane < 4) {  // quadrant q = lane: 8x8 block (q, j) in raster order, or its 16x16
+        const int k = j < 4 ? ((lane >> 1) << 3) | ((j >> 1) << 2) | ((lane & 1) << 1) | (j & 1) : 16 + lane;
+        atomicMin(&best[k], v);
+      }
+    }
   }
   {
     const unsigned m = wave_min_u32(lb32);
@@ -513,40 +528,35 @@ __global__ void __launch_bounds__(kMeThreads) __attribute__((amdgpu_waves_per_eu
     return;
   }
   // ------------------------------- CU split decision ------------------------------------
-  if (tid == 0) {
-    const int ps = pen.split_inter;
-    int sum16 = 0;
-    uint8_t l2u[16];
-    int mvu[16][2];
+  // one lane per 8x8 unit k (raster): every lane forms the same quadrant / CTB sums from the
+  // 21 block costs (the same order of additions as the serial form), then writes its unit
+  if (tid < 16) {
+    const int ps = pen.split_inter, k = tid, ux = k & 3, uy = k >> 2;
+    int sum16 = 0, qsplit = 0;
+#pragma unroll
     for (int q = 0; q < 4; ++q) {
       int sum8 = 0;
+#pragma unroll
       for (int r = 0; r < 4; ++r) sum8 += bcost[me_blk8_of(q, r)] + ps;
       const bool split = sum8 < bcost[16 + q] + ps;
       sum16 += split ? sum8 : bcost[16 + q] + ps;
-      for (int r = 0; r < 4; ++r) {
-        const int ux = (q & 1) * 2 + (r & 1), uy = (q >> 1) * 2 + (r >> 1);
-        const int sbi = split ? me_blk8_of(q, r) : 16 + q;
-        l2u[uy * 4 + ux] = split ? 3 : 4;
-        mvu[uy * 4 + ux][0] = bmv[sbi][0];
-        mvu[uy * 4 + ux][1] = bmv[sbi][1];
-      }
+      qsplit |= split ? 1 << q : 0;
     }
     const bool whole = bcost[20] + ps <= sum16;
-    for (int k = 0; k < 16; ++k) {
-      const long u = b * g.usz + (long)((cy >> 3) + (k >> 2)) * g.w8 + (cx >> 3) + (k & 3);
-      dec.cu_log2[u] = whole ? 5 : l2u[k];
-      dec.mv[2 * u] = (int16_t)(whole ? bmv[20][0] : mvu[k][0]);
-      dec.mv[2 * u + 1] = (int16_t)(whole ? bmv[20][1] : mvu[k][1]);
-      dec.intra[u] = 0;
-      dec.ipm[u] = 1;
-    }
-    if (pi.qcost) {  // intra-in-P: quadrants past the gate go on k_pintra_analysis' list
-      for (int q = 0; q < 4; ++q) {
-        const long qi = ((long)b * g.wc * g.hc + ctu) * 4 + q;
-        pi.qcost[qi] = bcost[16 + q];
-        pi.cand[qi] = 0;
-        if (bcost[16 + q] > kPIntraGate * 256) pi.gate[atomicAdd(&pi.count[0], 1)] = (int)qi;
-      }
+    const int q = (uy >> 1) * 2 + (ux >> 1), r = (uy & 1) * 2 + (ux & 1);
+    const bool split = (qsplit >> q) & 1;
+    const int sbi = whole ? 20 : (split ? me_blk8_of(q, r) : 16 + q);
+    const long u = b * g.usz + (long)((cy >> 3) + uy) * g.w8 + (cx >> 3) + ux;
+    dec.cu_log2[u] = whole ? 5 : (split ? 3 : 4);
+    dec.mv[2 * u] = (int16_t)bmv[sbi][0];
+    dec.mv[2 * u + 1] = (int16_t)bmv[sbi][1];
+    dec.intra[u] = 0;
+    dec.ipm[u] = 1;
+    if (pi.qcost && k < 4) {  // intra-in-P: quadrants past the gate go on k_pintra_analysis' list
+      const long qi = ((long)b * g.wc * g.hc + ctu) * 4 + k;
+      pi.qcost[qi] = bcost[16 + k];
+      pi.cand[qi] = 0;
+      if (bcost[16 + k] > kPIntraGate * 256) pi.gate[atomicAdd(&pi.count[0], 1)] = (int)qi;
     }
   }
 }
