@@ -332,16 +332,43 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   const int qpc = chroma_qp(qp, 0);
   const int nl = horizontal ? (H / 8 - 1) * (W / 4) : (W / 8 - 1) * (H / 4);
   const int nc = horizontal ? (H / 16 - 1) * (Wc / 4) : (W / 16 - 1) * (H / 8);
+  // Each item's samples are moved as aligned dwords into registers (a vertical edge: the
+  // 8 bytes x-4..x+3 of each of its 4 lines; a horizontal edge: 8 rows x the segment's 4
+  // columns), filtered there by the shared tv::deblock_* functions and written back the same
+  // way: 8 dword loads per luma segment instead of 32 byte loads.  Items of a pass never
+  // share a dword (edges are 8 samples apart), so the write-back of unchanged bytes is safe.
+  auto ld = [](const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); };
+  auto st = [](uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; };
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nl + nc; i += gridDim.x * blockDim.x) {
     if (i < nl) {
       if (!horizontal) {
         const int x = 8 * (1 + i % (W / 8 - 1)), y = 4 * (i / (W / 8 - 1));
         const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, x - 1, y, x, y, dir, mv1, tu);
-        if (bs) deblock_luma_edge4(Y + (long)y * W + x, 1, W, bs, qp);
+        if (bs) {
+          uint32_t v[4][2];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[k][0] = ld(Y + (long)(y + k) * W + x - 4);
+            v[k][1] = ld(Y + (long)(y + k) * W + x);
+          }
+          deblock_luma_edge4(reinterpret_cast<uint8_t*>(&v[0][1]), 1, 8, bs, qp);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            st(Y + (long)(y + k) * W + x - 4, v[k][0]);
+            st(Y + (long)(y + k) * W + x, v[k][1]);
+          }
+        }
       } else {
         const int y = 8 * (1 + i % (H / 8 - 1)), x = 4 * (i / (H / 8 - 1));
         const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, x, y - 1, x, y, dir, mv1, tu);
-        if (bs) deblock_luma_edge4(Y + (long)y * W + x, W, 1, bs, qp);
+        if (bs) {
+          uint32_t v[8];  // rows y-4 .. y+3, columns x .. x+3
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = ld(Y + (long)(y - 4 + r) * W + x);
+          deblock_luma_edge4(reinterpret_cast<uint8_t*>(&v[4]), 4, 1, bs, qp);
+#pragma unroll
+          for (int r = 1; r < 7; ++r) st(Y + (long)(y - 4 + r) * W + x, v[r]);  // rows p2..q2
+        }
       }
     } else {
       const int j = i - nl;
@@ -349,15 +376,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         const int xc = 8 * (1 + j % (W / 16 - 1)), yc = 4 * (j / (W / 16 - 1));
         const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, 2 * xc - 1, 2 * yc, 2 * xc, 2 * yc, dir, mv1, tu);
         if (bs == 2) {
-          deblock_chroma_edge(U + (long)yc * Wc + xc, 1, Wc, 4, qpc);
-          deblock_chroma_edge(V + (long)yc * Wc + xc, 1, Wc, 4, qpc);
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl) {
+            uint8_t* P = pl ? V : U;
+            uint32_t v[4][2];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              v[k][0] = ld(P + (long)(yc + k) * Wc + xc - 4);
+              v[k][1] = ld(P + (long)(yc + k) * Wc + xc);
+            }
+            deblock_chroma_edge(reinterpret_cast<uint8_t*>(&v[0][1]), 1, 8, 4, qpc);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              st(P + (long)(yc + k) * Wc + xc - 4, v[k][0]);
+              st(P + (long)(yc + k) * Wc + xc, v[k][1]);
+            }
+          }
         }
       } else {
         const int yc = 8 * (1 + j % (H / 16 - 1)), xc = 4 * (j / (H / 16 - 1));
         const int bs = deblock_edge_bs(cl, in, cb, mv, g.w8, 2 * xc, 2 * yc - 1, 2 * xc, 2 * yc, dir, mv1, tu);
         if (bs == 2) {
-          deblock_chroma_edge(U + (long)yc * Wc + xc, Wc, 1, 4, qpc);
-          deblock_chroma_edge(V + (long)yc * Wc + xc, Wc, 1, 4, qpc);
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl) {
+            uint8_t* P = pl ? V : U;
+            uint32_t v[4];  // rows yc-2 .. yc+1
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = ld(P + (long)(yc - 2 + r) * Wc + xc);
+            deblock_chroma_edge(reinterpret_cast<uint8_t*>(&v[2]), 4, 1, 4, qpc);
+            st(P + (long)(yc - 1) * Wc + xc, v[1]);
+            st(P + (long)yc * Wc + xc, v[2]);
+          }
         }
       }
     }
