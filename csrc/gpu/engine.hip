@@ -878,10 +878,10 @@ class Core {
     // this frame's QPs: copied only when they differ from what the slot already holds (a
     // constant-QP stream pays nothing per frame; a QP map or CRF rewrites them every frame)
     if (qmap_given_) {
-      HIP_OK(hipMemcpyAsync(dec0.qp, qhost_ + f * B, B, hipMemcpyHostToDevice, stream_));
+      launch_set_qp(dec0.qp, qhost_ + f * B, B, stream_);
       s.qp_dirty = true;
     } else if (s.qp_dirty) {  // back to the sequence QP for every segment slot
-      HIP_OK(hipMemcpyAsync(dec0.qp, quni_, cfg_.batch, hipMemcpyHostToDevice, stream_));
+      launch_set_qp(dec0.qp, quni_, cfg_.batch, stream_);
       s.qp_dirty = false;
     }
     if (cfg_.crf > 0 && !qmap_given_) s.qp_dirty = true;  // k_rc_crf overwrites them

@@ -28,6 +28,8 @@ struct RcTables {
 
 void launch_synth(FrameSet src, const Geo& g, uint32_t seed, const FrameIdx& fi, int B, hipStream_t s);
 void launch_gather_frames(const uint8_t* frames, long seg_stride, FrameSet src, const Geo& g, int B, hipStream_t s);
+// n slice QPs from host memory into device memory as kernel arguments (no blit copy)
+void launch_set_qp(int8_t* dst, const int8_t* host, int n, hipStream_t s);
 void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s);
 bool intra_timing();
 void intra_timing_report();

@@ -1,6 +1,7 @@
 // k_frame.hip — frame-level kernels: synthetic source, PSNR SSE, quarter-pel phase planes,
 // in-loop deblocking.  Batched: blockIdx.z (or .y) selects the segment.
 #include <cstdlib>
+#include <cstring>
 
 #include "gpu_common.h"
 #include "k_encode.h"
@@ -441,6 +442,24 @@ void launch_gather_frames(const uint8_t* frames, long seg_stride, FrameSet src, 
   const long n = B * (g.ysz + 2 * g.csz) / 16;
   k_gather_frames<<<(unsigned)tv_min(4096L, (n + 255) / 256), 256, 0, s>>>(frames, seg_stride, src, g, B);
 }
+// Per-frame slice QPs into the device slot: the values travel as kernel arguments (64 per
+// launch) instead of a pinned-host -> device hipMemcpyAsync, which this runtime runs as a
+// blit kernel that reads host memory over PCIe (~77 us per picture in the kernel trace).
+struct QpArgs {
+  int8_t q[64];
+};
+__global__ void __launch_bounds__(64) k_set_qp(int8_t* dst, QpArgs a, int n) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = a.q[threadIdx.x];
+}
+void launch_set_qp(int8_t* dst, const int8_t* host, int n, hipStream_t s) {
+  for (int o = 0; o < n; o += 64) {
+    QpArgs a;
+    const int m = n - o < 64 ? n - o : 64;
+    std::memcpy(a.q, host + o, (size_t)m);
+    k_set_qp<<<1, 64, 0, s>>>(dst + o, a, m);
+  }
+}
+
 void launch_sse(FrameSet a, FrameSet r, const Geo& g, unsigned long long* sse, int B, hipStream_t s) {
   dim3 grid((unsigned)tv_min(256, (int)((g.ysz / 4 + 4095) / 4096)), 3, B);
   k_sse<<<grid, 256, 0, s>>>(a, r, g, sse);
