@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) k_phase_planes(FrameSet ref, uint8_t* pha
       int v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        v[j] = (dot4(C[0][j], pack_taps4(fy, 0), dot4(C[1][j], pack_taps4(fy, 4), 8192)) + 32) >> 6;
+        v[j] = dot4(C[0][j], pack_taps4(fy, 0), dot4(C[1][j], pack_taps4(fy, 4), 8192 + 32)) >> 6;  // rounding folded in
       store(4 * fy, pack4_pixels(v[0], v[1], v[2], v[3]));
     }
   }
