@@ -84,7 +84,9 @@ __global__ void __launch_bounds__(1024) k_sb_scan(Geo g, CompactSet cs) {
   if (tid == 1023) cs.total[b] = part[1023];
 }
 
-// pack the non-zero groups: one wave per CTB, 4 lanes per group (one row of 4 each)
+// pack the non-zero groups: one wave per CTB, lane = group bit (luma 0..63, then chroma
+// 0..31): a set bit's output slot is the popcount of the bits below it, and its lane copies
+// the group's 4 rows (no per-lane walk over the mask)
 __global__ void __launch_bounds__(256) k_sb_pack(DecisionSet dec, Geo g, CompactSet cs) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ctu = blockIdx.x * 4 + wave, b = blockIdx.y;
@@ -95,29 +97,26 @@ __global__ void __launch_bounds__(256) k_sb_pack(DecisionSet dec, Geo g, Compact
   const unsigned long long my = cs.mask_y[i];
   const unsigned mc = cs.mask_c[i];
   const int ny = __popcll(my);
-  const int n = ny + __popc(mc);
-  // segments are packed back to back (one device->host copy per frame for all of them)
-  long base = 0;
-  for (int k = 0; k < b; ++k) base += cs.total[k];
+  // segments are packed back to back (one device->host copy per frame for all of them): the
+  // groups of the segments before b, summed across the wave
+  int pre = 0;
+  for (int k = lane; k < b; k += 64) pre += cs.total[k];
+  const long base = wave_sum(pre);
   int16_t* out = cs.packed + (base + cs.offset[i]) * 16;
-  for (int t = lane; t < n * 4; t += 64) {
-    const int gidx = t >> 2, row = t & 3;
-    const int16_t* src;
-    long stride;
-    if (gidx < ny) {  // gidx-th set bit of my
-      unsigned long long m = my;
-      for (int k = 0; k < gidx; ++k) m &= m - 1;
-      const int bit = __ffsll(m) - 1, sx = bit & 7, sy = bit >> 3;
-      stride = g.W;
-      src = dec.coef_y + b * g.ysz + (long)(cy + 4 * sy) * g.W + cx + 4 * sx;
-    } else {
-      unsigned m = mc;
-      for (int k = 0; k < gidx - ny; ++k) m &= m - 1;
-      const int bit = __ffs(m) - 1, l = bit & 15, sx = l & 3, sy = l >> 2;
-      stride = g.W / 2;
-      src = (bit < 16 ? dec.coef_u : dec.coef_v) + b * g.csz + (long)(cy / 2 + 4 * sy) * stride + cx / 2 + 4 * sx;
-    }
-    *reinterpret_cast<uint2*>(out + gidx * 16 + row * 4) = *reinterpret_cast<const uint2*>(src + row * stride);
+  if ((my >> lane) & 1) {
+    const int gi = __popcll(my & ((1ull << lane) - 1)), sx = lane & 7, sy = lane >> 3;
+    const int16_t* src = dec.coef_y + b * g.ysz + (long)(cy + 4 * sy) * g.W + cx + 4 * sx;
+#pragma unroll
+    for (int row = 0; row < 4; ++row)
+      *reinterpret_cast<uint2*>(out + gi * 16 + row * 4) = *reinterpret_cast<const uint2*>(src + (long)row * g.W);
+  }
+  if (lane < 32 && ((mc >> lane) & 1)) {
+    const int gi = ny + __popc(mc & ((1u << lane) - 1)), l = lane & 15, sx = l & 3, sy = l >> 2;
+    const long stride = g.W / 2;
+    const int16_t* src = (lane < 16 ? dec.coef_u : dec.coef_v) + b * g.csz + (long)(cy / 2 + 4 * sy) * stride + cx / 2 + 4 * sx;
+#pragma unroll
+    for (int row = 0; row < 4; ++row)
+      *reinterpret_cast<uint2*>(out + gi * 16 + row * 4) = *reinterpret_cast<const uint2*>(src + row * stride);
   }
 }
 
