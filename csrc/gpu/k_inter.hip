@@ -85,6 +85,26 @@ __device__ __forceinline__ void me_blk_geom(int bi, int& bx, int& by, int& l2) {
 __device__ __forceinline__ int me_blk8_of(int q, int r) {
   return (((q >> 1) * 2 + (r >> 1)) << 2) + (q & 1) * 2 + (r & 1);
 }
+// tv::dequant_level in 32-bit arithmetic: with m = 16 * levelScale << (qp / 6) and the level
+// clamped to +-thr, where thr * m just exceeds (32768 + 1) << bdShift, a clamped level still
+// saturates to the same int16 bound and every unclamped product fits in 32 bits -- the same
+// result as the 64-bit golden form, with a med3 + mad + shift + med3 per level.
+struct DeqParams {
+  int m, thr, sh, rnd;
+};
+__device__ __forceinline__ DeqParams deq_params(int qp, int log2N) {
+  DeqParams d;
+  d.sh = 8 + log2N - 5;
+  d.rnd = 1 << (d.sh - 1);
+  d.m = (16 * level_scale(qp)) << (qp / 6);
+  d.thr = (((32768 + 1) << d.sh) + d.m - 1) / d.m;
+  return d;
+}
+__device__ __forceinline__ int deq_fast(int level, const DeqParams& d) {
+  const int t = clip3(-d.thr, d.thr, level);
+  return clip3(-32768, 32767, (t * d.m + d.rnd) >> d.sh);
+}
+
 // the 4 byte differences a - b as two dwords of int16 pairs (residual = source - prediction)
 __device__ __forceinline__ uint2 bytes_minus(uint32_t a, uint32_t b) {
   typedef short s2 __attribute__((ext_vector_type(2)));
@@ -1096,17 +1116,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   __syncthreads();
   if (diag == 3) return;
   // --------------------------------------- stage 3: T^T * dequant(levels)  (split d)
+  const DeqParams dq5 = deq_params(qp, 5), dqc4 = deq_params(qpc, 4);
   for (int t = wave; t < ntiles; t += 4) {
     if (L.tzero[t]) continue;  // wave-uniform: an all-zero tile reconstructs to the prediction
     int o[4];
     if (t < 4) {
       if (whole) {
         mfma_tile([&](int r, int k) { return (int)L.T[k][r]; },
-                  [&](int k, int c) { return dequant_level(L.resY[k * 32 + c], qp, 5); }, t >> 1, t & 1, 32, true, false, o);
+                  [&](int k, int c) { return deq_fast(L.resY[k * 32 + c], dq5); }, t >> 1, t & 1, 32, true, false, o);
       } else {
         const int ox = (t & 1) * 16, oy = (t >> 1) * 16, l2 = L.qtype[t] == 1 ? 4 : 3;
+        const DeqParams dql = deq_params(qp, l2);
         mfma_tile([&](int r, int k) { return pr_comp(L, l2, k, r); },
-                  [&](int k, int c) { return dequant_level(L.resY[(oy + k) * 32 + ox + c], qp, l2); }, 0, 0, 16, true, false, o);
+                  [&](int k, int c) { return deq_fast(L.resY[(oy + k) * 32 + ox + c], dql); }, 0, 0, 16, true, false, o);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1116,15 +1138,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     } else if (whole) {
       const int pl = t - 4;
       mfma_tile([&](int r, int k) { return pr_comp(L, 4, k, r); },
-                [&](int k, int c) { return dequant_level(L.resC[pl][k * 16 + c], qpc, 4); }, 0, 0, 16, true, false, o);
+                [&](int k, int c) { return deq_fast(L.resC[pl][k * 16 + c], dqc4); }, 0, 0, 16, true, false, o);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         L.tmpC[pl][((lane >> 4) * 4 + r) * 16 + (lane & 15)] = clip3(-32768, 32767, (o[r] + 64) >> 7);
     } else {
       const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
+      const DeqParams dqcl = deq_params(qpc, l2);
       mfma_tile([&](int r, int k) { return pr_comp(L, l2, k, r); },
                 [&](int k, int c) {
-                  return (k >> 3) == (c >> 3) ? dequant_level(L.resC[k >> 3][(oy + (k & 7)) * 16 + ox + (c & 7)], qpc, l2) : 0;
+                  return (k >> 3) == (c >> 3) ? deq_fast(L.resC[k >> 3][(oy + (k & 7)) * 16 + ox + (c & 7)], dqcl) : 0;
                 },
                 0, 0, 16, true, false, o);
 #pragma unroll
