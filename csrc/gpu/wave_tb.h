@@ -50,7 +50,7 @@ __device__ __forceinline__ void wave_stage(int log2N, FX X, FY Y, bool split, bo
 // resid/pred: LDS N*N (pred may be uint8).  Levels -> `lev` (global, stride ls);
 // reconstruction -> `rec` (LDS or global, stride rs).  Returns cbf (wave-uniform).
 template <class PredT, class RecT>
-__device__ int wave_code_tb(const int16_t* resid, const PredT* pred, int log2N, int qp, bool intra,
+__device__ __forceinline__ int wave_code_tb(const int16_t* resid, const PredT* pred, int log2N, int qp, bool intra,
                             int16_t* lev, int ls, RecT* rec, int rs, const int (*tbm)[33], WaveTbScratch& s) {
   const int N = 1 << log2N, n2 = N * N, lane = threadIdx.x & 63;
   const int sh1 = log2N - 1, sh2 = log2N + 6;
