@@ -131,9 +131,10 @@ __device__ void wave_txfm(const int16_t* in, int16_t* tmp, int16_t* out, int tco
 // reconstruction added onto pred (int, LDS) -> returns 1 if any level is nonzero.
 // Scratch a/b: LDS int16 [N*N] each; ti: LDS int32 [N*N].  Forward: the basis-matrix
 // transform (MFMA for 16x16); inverse: the specification's 2-D process (tv/av1_itx.h), one
-// lane per row, then one lane per column.
+// lane per row, then one lane per column.  Force-inlined: called, its LDS pointers were flat
+// (generic) accesses.
 template <int LG>
-__device__ int code_tb(int16_t* res, int16_t* a, int16_t* b, int32_t* ti, int tcol, int trow, int qidx, int rnd,
+__device__ __forceinline__ int code_tb(int16_t* res, int16_t* a, int16_t* b, int32_t* ti, int tcol, int trow, int qidx, int rnd,
                        int16_t* __restrict__ lev_out) {
   constexpr int N = 1 << LG;
   const int lane = threadIdx.x & 63;
