@@ -185,17 +185,22 @@ __global__ void __launch_bounds__(256) k_intra_analysis(FrameSet src, DecisionSe
 // source, own reconstruction and the reconstructed borders of the left / above /
 // above-right neighbours are staged in LDS once; each TB is then predicted, transformed and
 // reconstructed wave-synchronously from LDS (no workgroup barrier per TB).
-struct CompLds {
-  uint8_t src[1024];
-  uint8_t rec[1024];
-  uint8_t top[72];   // row y = cy-1, x = cx-1 .. cx+2S-1  (index 0 = corner)
-  uint8_t left[32];  // column x = cx-1, y = cy .. cy+S-1
-  uint8_t pred[1024];
-  int16_t resid[1024];
-  int V[132];
-  int L[65], T[65], FL[65], FT[65];
-  WaveTbScratch tb;
+// one component's CTB state; S = 32 (luma) or 16 (chroma): the chroma waves' copies are a
+// third of the luma one, so the workgroup's LDS (50 KB with three luma-sized copies) allows 5
+// CTBs per CU instead of 3 on the short wavefront launches
+template <int S>
+struct CompLdsT {
+  uint8_t src[S * S];
+  uint8_t rec[S * S];
+  uint8_t top[2 * S + 8];  // row y = cy-1, x = cx-1 .. cx+2S-1  (index 0 = corner)
+  uint8_t left[S];         // column x = cx-1, y = cy .. cy+S-1
+  uint8_t pred[S * S];
+  int16_t resid[S * S];
+  int V[4 * S + 4];
+  int L[2 * S + 1], T[2 * S + 1], FL[2 * S + 1], FT[2 * S + 1];
+  WaveTbScratchT<S> tb;
 };
+using CompLds = CompLdsT<32>;
 
 // TV_DIAG_INTRA=1: lane 0 of every wave adds the clock cycles of each phase to
 // g_intra_phase[c][phase] (c = component wave): timing only, printed at engine teardown.
@@ -206,7 +211,8 @@ __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec,
   const int b = blockIdx.y, c = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qp = dec.qp[b];
   __shared__ int Tm[32][33];
-  __shared__ CompLds W[3];
+  __shared__ CompLdsT<32> WY;    // luma
+  __shared__ CompLdsT<16> WC[2];  // Cb, Cr
   __shared__ int cus[16][4];
   __shared__ AngleLds ang;
   ang.load(threadIdx.x, 192);
@@ -256,7 +262,9 @@ __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec,
     ncu = n;
   }
   if (threadIdx.x < 16) cbfs[threadIdx.x] = 0;
-  CompLds& L = W[c];
+  // the component's work, instantiated for the luma- and the chroma-sized state (each wave
+  // runs one: the branch on c is wave-uniform; both run the same two barriers)
+  auto comp = [&](auto& L) {
   const int sh = c ? 1 : 0, S = c ? 16 : 32;
   const int pw = g.W >> sh, ph = g.H >> sh, bx = cx >> sh, by = cy >> sh;
   {  // stage source + neighbour borders of this component
@@ -362,6 +370,9 @@ __global__ void __launch_bounds__(192) k_intra_recon(FrameSet src, FrameSet rec,
   // write the CTB reconstruction and the per-CU cbf flags back
   uint8_t* Rp = rec.plane(c, b, g) + (long)by * pw + bx;
   for (int i = lane; i < S * S; i += 64) Rp[(long)(i / S) * pw + i % S] = L.rec[i];
+  };
+  if (c == 0) comp(WY);
+  else comp(WC[c - 1]);
   for (int k = threadIdx.x; k < ncu * 16; k += blockDim.x) {
     const int cu = k >> 4, j = k & 15, log2 = cus[cu][2], n8 = 1 << (log2 - 3);
     if (j < n8 * n8)

@@ -20,10 +20,13 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-struct WaveTbScratch {
-  int tmp[32 * 33];
-  int coef[1024];
+// scratch of TBs up to N_MAX x N_MAX (stage outputs at pitch 33, coefficients at pitch N)
+template <int N_MAX>
+struct WaveTbScratchT {
+  int tmp[N_MAX * 33];
+  int coef[N_MAX * N_MAX];
 };
+using WaveTbScratch = WaveTbScratchT<32>;
 
 template <class FX, class FY, class EMIT>
 __device__ __forceinline__ void wave_stage(int log2N, FX X, FY Y, bool split, bool split_x, EMIT emit) {
@@ -49,9 +52,9 @@ __device__ __forceinline__ void wave_stage(int log2N, FX X, FY Y, bool split, bo
 
 // resid/pred: LDS N*N (pred may be uint8).  Levels -> `lev` (global, stride ls);
 // reconstruction -> `rec` (LDS or global, stride rs).  Returns cbf (wave-uniform).
-template <class PredT, class RecT>
+template <class PredT, class RecT, class Scratch>
 __device__ __forceinline__ int wave_code_tb(const int16_t* resid, const PredT* pred, int log2N, int qp, bool intra,
-                            int16_t* lev, int ls, RecT* rec, int rs, const int (*tbm)[33], WaveTbScratch& s) {
+                            int16_t* lev, int ls, RecT* rec, int rs, const int (*tbm)[33], Scratch& s) {
   const int N = 1 << log2N, n2 = N * N, lane = threadIdx.x & 63;
   const int sh1 = log2N - 1, sh2 = log2N + 6;
   wave_stage(
