@@ -273,7 +273,8 @@ __device__ __forceinline__ int mvd_cost(int d) {
 
 // ------------------------------------------------------------------ binariser (one CTB)
 struct CtbBinariser {
-  const SegView& v;
+  const SegView v;  // by value: a reference put the view in scratch and its plane pointers
+                    // (LDS in k_ent_bin) became flat accesses
   const EntropyPic& p;
   TokSink& s;
   const BinTables& T;  // LDS
@@ -793,34 +794,34 @@ __global__ void __launch_bounds__(256) k_ent_bin(EntropyArgs a) {
   const int uy0 = cy > 0 ? 4 * cy - 1 : 0, nrows = 4 * cy + 4 - uy0;
   const long u0 = (long)uy0 * w8;  // first staged unit
   const int nw = nrows * w8 / 4;   // dwords of a byte plane's window (w8 is a multiple of 4)
-  auto stage8 = [&](int off, const uint8_t*& p) {
-    if (off < 0) return;
+  // the staging helpers return the window pointer (no reference into v: taking a field's
+  // address put the whole view in scratch and every plane access became a flat one)
+  auto stage8 = [&](int off, const uint8_t* p) -> const uint8_t* {
+    if (off < 0) return p;  // only tu / dir are optional (bin_stage): the rest are always staged
     const uint32_t* g32 = reinterpret_cast<const uint32_t*>(p + u0);
     uint32_t* l32 = reinterpret_cast<uint32_t*>(dyn + off);
     for (int k = threadIdx.x; k < nw; k += nt) l32[k] = g32[k];
-    p = dyn + off;  // unit_of subtracts v.ubase: unit(x, y) indexes the window (no pointer below dyn)
+    return dyn + off;  // unit_of subtracts v.ubase: unit(x, y) indexes the window (no pointer below dyn)
   };
-  auto stage16 = [&](int off, const int16_t*& p) {
-    if (off < 0) return;
+  auto stage16 = [&](int off, const int16_t* p) -> const int16_t* {
+    if (off < 0) return p;
     const uint32_t* g32 = reinterpret_cast<const uint32_t*>(p + 2 * u0);
     uint32_t* l32 = reinterpret_cast<uint32_t*>(dyn + off);
     for (int k = threadIdx.x; k < nrows * w8; k += nt) l32[k] = g32[k];
-    p = reinterpret_cast<const int16_t*>(dyn + off);
+    return reinterpret_cast<const int16_t*>(dyn + off);
   };
-  stage8(L.cu, v.cu_log2);
-  stage8(L.in, v.intra);
-  stage8(L.ipm, v.ipm);
-  stage8(L.cbf, v.cbf);
-  stage8(L.sk, v.skip);
-  {
-    const uint8_t* mi = reinterpret_cast<const uint8_t*>(v.midx);
-    stage8(L.mi, mi);
-    v.midx = reinterpret_cast<const int8_t*>(mi);
-  }
-  stage8(L.tu, v.tu);
-  stage8(L.dir, v.dir);
-  stage16(L.mv, v.mv);
-  stage16(L.mv1, v.mv1);
+  // planes that are always staged take the offset unconditionally (max(off, 0) is off), so
+  // the compiler sees LDS pointers (ds_* instead of flat_* accesses in the binariser)
+  v.cu_log2 = stage8(tv_max(L.cu, 0), v.cu_log2);
+  v.intra = stage8(tv_max(L.in, 0), v.intra);
+  v.ipm = stage8(tv_max(L.ipm, 0), v.ipm);
+  v.cbf = stage8(tv_max(L.cbf, 0), v.cbf);
+  v.skip = stage8(tv_max(L.sk, 0), v.skip);
+  v.midx = reinterpret_cast<const int8_t*>(stage8(tv_max(L.mi, 0), reinterpret_cast<const uint8_t*>(v.midx)));
+  v.tu = stage8(L.tu, v.tu);
+  v.dir = stage8(L.dir, v.dir);
+  v.mv = stage16(tv_max(L.mv, 0), v.mv);
+  v.mv1 = stage16(L.mv1, v.mv1);
   v.ubase = u0;
   __syncthreads();
   if (!work) return;
