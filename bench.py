@@ -75,7 +75,7 @@ def _batch_for(args, local: int, codec: str, w: int, h: int):
 
     spec = EncodeSpec(w, h, qp=args.qp, gop=args.gop, sao=args.sao, codec=codec,
                       bframes=args.bframes if codec == "hevc" else 1, wpp=args.wpp, rqt=args.rqt, pintra=args.pintra,
-                      cascade=args.cascade)
+                      cascade=args.cascade, rdoq=args.rdoq)
     if args.batch:
         return args.batch, {"batch": args.batch, "source": "--batch"}
     if args.cpu:
@@ -665,6 +665,7 @@ def main() -> None:
     ap.add_argument("--no-cascade", dest="cascade", action="store_false",
                     help="HEVC: flat QP (no constant-QP I P P P QP cascade)")
     ap.add_argument("--no-pintra", dest="pintra", action="store_false", help="HEVC: no intra CUs in P pictures")
+    ap.add_argument("--no-rdoq", dest="rdoq", action="store_false", help="HEVC: no RDOQ-lite coefficient-group trimming")
     ap.add_argument("--entropy", choices=("gpu", "host", "auto"), default=None,
                     help="where WPP substreams are CABAC-coded (default auto: the host writer with >= 12 CPUs "
                          "per rank, else the GPU; TV_ENTROPY); same bytes either way")
@@ -739,7 +740,7 @@ def hevc_pass(args, world, rank, local, dev, cpus):
     batch, sizing = _batch_for(args, local, "hevc", w, h)
     if args.cpu:
         from thinvids_amd.models.cpu_engines import CpuHevcEngine as GpuEngine  # noqa: F811
-    tools = dict(wpp=args.wpp, rqt=args.rqt, pintra=args.pintra, entropy=args.entropy, cascade=args.cascade)
+    tools = dict(wpp=args.wpp, rqt=args.rqt, pintra=args.pintra, entropy=args.entropy, cascade=args.cascade, rdoq=args.rdoq)
     eng = GpuEngine(width=w, height=h, qp=args.qp, batch=batch, gop=args.gop, search_range=args.range, sao=args.sao,
                     seed=args.seed, threads=args.threads or None, device=local, bframes=args.bframes, **tools)
     post = _PostQueue(local, args.cpu)
@@ -884,7 +885,7 @@ def hevc_pass(args, world, rank, local, dev, cpus):
                 "last_step_coef_mb_d2h": round(tm["coef_mb"], 2),
                 "entropy": (dict(eng.entropy_stats(), wpp=args.wpp, where=getattr(eng, "entropy", "host"))
                             if hasattr(eng, "entropy_stats") else {"wpp": args.wpp, "where": "cpu rehearsal"}),
-                "coding_tools": {"wpp": args.wpp, "rqt": args.rqt, "pintra": args.pintra, "cascade": args.cascade},
+                "coding_tools": {"wpp": args.wpp, "rqt": args.rqt, "pintra": args.pintra, "cascade": args.cascade, "rdoq": args.rdoq},
                 "per_rank_cpu": [{"busy_cores": r[0], "pinned_cpus": int(r[1]), "cabac_threads": int(r[2])}
                                  for r in ranks],
                 "step_ms": step_ms,

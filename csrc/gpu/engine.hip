@@ -349,6 +349,8 @@ class Core {
     seq_.rqt = !(c.deblock & 8);
     seq_.pintra = !(c.deblock & 16);
     seq_.cascade = (c.deblock & 64) != 0;
+    seq_.rdoq = !(c.deblock & 128);
+    g_.rdoq = seq_.rdoq ? kRdoqMode : 0;
     seq_.mgop = c.mgop;
     if (c.mgop > 1) {
       const GopPlan gp = plan_gop(2 * c.mgop + 1, c.mgop);

@@ -21,6 +21,7 @@ struct Geo {
   long usz;        // units
   int pw16;        // phase-plane pitch (W + 16: 8-sample pad each side)
   long psz;        // phase-plane size ((W + 16) * (H + 16))
+  int rdoq = 0;    // k_inter_recon RDOQ-lite mode (hevc_defs.h kRdoqMode; 0 off): SeqConfig::rdoq
 };
 
 inline Geo make_geo(int dw, int dh) {

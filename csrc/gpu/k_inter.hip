@@ -733,6 +733,7 @@ struct PReconLds {
   int qsplit[4];              // RQT of the 16x16 CU in quadrant q (four 8x8 TBs)
   int qintra[4];              // quadrant q is an intra CU of a P picture (k_pintra_recon codes it)
   uint32_t ctap[8];           // chroma filter of fraction f as 4 signed bytes
+  int cgmax[48];              // RDOQ-lite: highest scan key of a TB's groups that are kept
 };
 
 // block size (log2) of the TB owning luma sample (x, y) / chroma sample (x, y) of the CTB
@@ -766,7 +767,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
                                                      FrameSet rec, DecisionSet dec, Geo g, int tile_skip,
                                                      FrameSet ref1, const uint8_t* phase1) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int diag = tile_skip >> 8;  // TV_DIAG_RECON_STOP (timing only)
+  const int diag = (tile_skip >> 8) & 255;  // TV_DIAG_RECON_STOP (timing only)
+  const int rdoq = g.rdoq;                  // RDOQ-lite mode (tv code_tb), 0 off
   tile_skip &= 255;
   int ctu, b;
   xcd_ctb(ctu, b);
@@ -784,7 +786,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     L.mv1[tid][0] = dec.mv1 ? dec.mv1[2 * u] : 0;
     L.mv1[tid][1] = dec.mv1 ? dec.mv1[2 * u + 1] : 0;
   }
-  if (tid < 48) L.nz[tid] = L.sa[tid] = L.dc[tid] = 0;
+  if (tid < 48) {
+    L.nz[tid] = L.sa[tid] = L.dc[tid] = 0;
+    L.cgmax[tid] = -1;
+  }
   if (tid < 8)
     L.ctap[tid] = (uint32_t)(uint8_t)kChromaFilter[tid][0] | (uint32_t)(uint8_t)kChromaFilter[tid][1] << 8 |
                   (uint32_t)(uint8_t)kChromaFilter[tid][2] << 16 | (uint32_t)(uint8_t)kChromaFilter[tid][3] << 24;
@@ -1076,6 +1081,55 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
   }
   __syncthreads();
+  // ---- RDOQ-lite (tv code_tb, inter TBs of 8x8 and up): trailing coefficient groups whose
+  // only level is a lone +-1 are dropped -- tv walks the TB's groups in reverse up-right
+  // diagonal scan to the first group holding anything else, down to diagonal rdoq_dmin.  In
+  // parallel that is: a lone group is dropped iff its scan key (diagonal major, then rows
+  // from the bottom) is above every other non-empty-non-lone group's of its TB (one LDS max
+  // per TB) and its diagonal is >= rdoq_dmin.  One thread per 4x4 group (luma 64, Cb / Cr 16).
+  if (diag != 1 && rdoq) {
+    int code = 0, key = 0, id = 0, dmin = 1 << 20;
+    int16_t* p = nullptr;
+    int st = 32;
+    if (tid < 96) {
+      int x, y, l2, pl = -1;
+      if (tid < 64) {
+        x = (tid & 7) * 4, y = (tid >> 3) * 4;
+        l2 = pr_l2_luma(L, x, y);
+        id = pr_tb_luma(L, x, y);
+        p = &L.resY[y * 32 + x];
+      } else {
+        const int c = tid - 64;
+        pl = c >> 4, x = (c & 3) * 4, y = ((c & 15) >> 2) * 4;
+        l2 = pr_l2_luma(L, 2 * x, 2 * y) - 1;
+        id = pr_tb_chroma(L, pl, x, y);
+        p = &L.resC[pl][y * 16 + x];
+        st = 16;
+      }
+      int t = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint2 w = *reinterpret_cast<const uint2*>(p + j * st);
+        t += tv_abs((int)(int16_t)(w.x & 0xffff)) + tv_abs((int)(int16_t)(w.x >> 16)) + tv_abs((int)(int16_t)(w.y & 0xffff)) +
+             tv_abs((int)(int16_t)(w.y >> 16));
+      }
+      const int m = (1 << l2) - 1, gx = (x & m) >> 2, gy = (y & m) >> 2;
+      code = tv_min(t, 2);
+      key = (gx + gy) * 16 + 15 - gy;
+      const int q = pl < 0 ? (y >> 4) * 2 + (x >> 4) : (y >> 3) * 2 + (x >> 3);
+      if (l2 >= 3 && !L.qintra[L.qtype[0] == 0 ? 0 : q]) dmin = rdoq_dmin(rdoq, 1 << (l2 - 2));
+      if (code == 2) atomicMax(&L.cgmax[id], key);
+      if (gx + gy < dmin) code = 0;  // groups this TB keeps whatever they hold
+    }
+    __syncthreads();
+    if (code == 1 && key > L.cgmax[id]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<uint2*>(p + j * st) = make_uint2(0u, 0u);
+      atomicSub(&L.nz[id], 1);
+      atomicSub(&L.sa[id], 1);
+    }
+    __syncthreads();
+  }
   // ---- final levels (dropped TBs zeroed) -> the level planes; cbf per CU
   {
     // 4 levels (one TB: TBs are >= 4 wide and 4-aligned) per item, one 8-byte store

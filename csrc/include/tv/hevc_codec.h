@@ -48,11 +48,14 @@ struct SeqConfig {
   bool rqt = true;
   // constant-QP I P P P: the low-delay QP cascade of tv/gop.h ippp_qp_offset
   bool cascade = false;
-  // All three change the bitstream: they are explicit configuration (the C API's flag bits 3 / 4,
+  // RDOQ-lite: inter TBs drop trailing lone-+-1 coefficient groups (hevc_defs.h kRdoqMode)
+  bool rdoq = true;
+  // All of these change the bitstream: they are explicit configuration (the C API's flag bits 3 / 4,
   // EncodeSpec.rqt / .pintra, part of the engine key and the checkpoint fingerprint), never
   // read from the environment here.
   // Flag bits of the C API's `deblock` argument: 1 deblocking, 2 SAO, 4 WPP, 8 no RQT,
-  // 16 no intra-in-P (32: GPU engine only, CABAC on the host), 64 I P P P QP cascade
+  // 16 no intra-in-P (32: GPU engine only, CABAC on the host), 64 I P P P QP cascade,
+  // 128 no RDOQ-lite
   void set_flags(int f) {
     deblock = (f & 1) != 0;
     sao = (f & 2) != 0;
@@ -60,6 +63,7 @@ struct SeqConfig {
     rqt = !(f & 8);
     pintra = !(f & 16);
     cascade = (f & 64) != 0;
+    rdoq = !(f & 128);
   }
   int fps_num = 30, fps_den = 1;
   void finalize() {

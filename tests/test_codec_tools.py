@@ -16,15 +16,16 @@ def test_engine_keys_differ_by_tool():
     base = EncodeSpec(640, 360)
     keys = {base.engine_key(), EncodeSpec(640, 360, rqt=False).engine_key(),
             EncodeSpec(640, 360, pintra=False).engine_key(), EncodeSpec(640, 360, wpp=False).engine_key(),
-            EncodeSpec(640, 360, cascade=False).engine_key()}
-    assert len(keys) == 5
-    assert base.tools() == {"wpp": True, "rqt": True, "pintra": True, "cascade": True}
+            EncodeSpec(640, 360, cascade=False).engine_key(), EncodeSpec(640, 360, rdoq=False).engine_key()}
+    assert len(keys) == 6
+    assert base.tools() == {"wpp": True, "rqt": True, "pintra": True, "cascade": True, "rdoq": True}
 
 
 def test_codec_flags_bits():
     assert hevc.codec_flags() == 1 | 4
     assert hevc.codec_flags(deblock=False, sao=True, wpp=False, rqt=False, pintra=False) == 2 | 8 | 16
     assert hevc.codec_flags(cascade=True) == 1 | 4 | 64
+    assert hevc.codec_flags(rdoq=False) == 1 | 4 | 128
 
 
 def test_tools_change_the_stream_and_env_does_not(monkeypatch):
@@ -72,3 +73,21 @@ def test_ippp_qp_cascade():
     for s in (casc, flat):
         d = hevc.decode(s, coded=False)
         assert len(d.frames) == len(fr)
+
+
+def test_rdoq_lite_trims_trailing_lone_groups():
+    """RDOQ-lite (tv/hevc_defs.h kRdoqMode, tv code_tb): inter TBs drop trailing coefficient
+    groups whose only level is a lone +-1.  Same decisions otherwise, so the stream with the
+    tool is smaller, both decode to their encoder's reconstruction, and the I picture (intra
+    TBs are never trimmed) is identical."""
+    fr = [hevc.synth_frame(1 | (1 << 31), t, 192, 128) for t in range(4)]  # textured
+    kw = dict(qp=27, search_range=16, sao=False)
+    on, r_on = hevc.encode_sequence_cpu(fr, **kw)
+    off, r_off = hevc.encode_sequence_cpu(fr, rdoq=False, **kw)
+    assert len(on) < len(off)
+    np.testing.assert_array_equal(r_on[0][0], r_off[0][0])
+    for s, rec in ((on, r_on), (off, r_off)):
+        d = hevc.decode(s, coded=False)
+        assert len(d.frames) == len(fr)
+        for a, b in zip(d.frames, rec):
+            np.testing.assert_array_equal(a[0], b[0][:128, :192])

@@ -37,9 +37,9 @@ class CpuHevcEngine:
 
     def __init__(self, width: int, height: int, qp: int = 27, batch: int = 2, gop: int = 8, search_range: int = 16,
                  sao: bool = False, seed: int = 1, threads: int | None = None, bframes: int = 1, wpp: bool = True,
-                 rqt: bool = True, pintra: bool = True, cascade: bool = True, **_):
+                 rqt: bool = True, pintra: bool = True, cascade: bool = True, rdoq: bool = True, **_):
         self.width, self.height, self.qp, self.batch, self.gop = width, height, qp, batch, gop
-        self.tools = {"wpp": wpp, "rqt": rqt, "pintra": pintra, "cascade": cascade}
+        self.tools = {"wpp": wpp, "rqt": rqt, "pintra": pintra, "cascade": cascade, "rdoq": rdoq}
         self.search_range, self.sao, self.seed, self.bframes = search_range, sao, seed, int(bframes)
         self.threads = threads or 2
         self.pool = cf.ThreadPoolExecutor(self.threads)

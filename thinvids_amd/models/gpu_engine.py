@@ -87,7 +87,8 @@ class GpuEngine:
                  search_range: int = 64, deblock: bool = True, sao: bool = False, seed: int = 1,
                  threads: int | None = None,
                  device: int = 0, max_merge: int = 5, crf: int = 0, bframes: int = 1, wpp: bool = True,
-                 rqt: bool = True, pintra: bool = True, entropy: str | None = None, cascade: bool = True):
+                 rqt: bool = True, pintra: bool = True, entropy: str | None = None, cascade: bool = True,
+                 rdoq: bool = True):
         """`bframes` > 1: hierarchical-B mini-GOPs of that size (power of 2, tv/gop.h); the
         segments' streams are then in coding order (the decoder reorders by POC) and
         :meth:`last_recon` returns the last DISPLAY frame.
@@ -108,7 +109,7 @@ class GpuEngine:
         from .hevc import codec_flags
 
         self.entropy = resolve_entropy(entropy) if wpp else "host"
-        self.flags = codec_flags(deblock, sao, wpp, rqt, pintra, cascade) | (32 if self.entropy == "host" else 0)
+        self.flags = codec_flags(deblock, sao, wpp, rqt, pintra, cascade, rdoq) | (32 if self.entropy == "host" else 0)
         self.h = self.lib.tv_engine_new_b(width, height, qp, batch, gop, search_range, self.flags,
                                           seed & 0xFFFFFFFF, self.threads, device, max_merge, int(crf), self.bframes)
         if not self.h:
@@ -270,14 +271,14 @@ def resolve_entropy(entropy: str | None = None) -> str:
 
 def estimate_footprint(width: int, height: int, batch: int, gop: int, sao: bool = False, bframes: int = 1,
                        wpp: bool = True, rqt: bool = True, pintra: bool = True, entropy: str | None = None,
-                       cascade: bool = True) -> dict:
+                       cascade: bool = True, rdoq: bool = True) -> dict:
     """HBM / pinned-host bytes an engine of this geometry would allocate, computed by the
     native constructor's own size formulas without allocating (tv_engine_estimate)."""
     from .hevc import codec_flags
 
     lib = _lib()
     ent = resolve_entropy(entropy) if wpp else "host"
-    flags = codec_flags(True, sao, wpp, rqt, pintra, cascade) | (32 if ent == "host" else 0)
+    flags = codec_flags(True, sao, wpp, rqt, pintra, cascade, rdoq) | (32 if ent == "host" else 0)
     d, h = C.c_ulonglong(), C.c_ulonglong()
     f = lib.tv_engine_estimate
     f.argtypes = [C.c_int] * 6 + [C.POINTER(C.c_ulonglong)] * 2

@@ -40,12 +40,13 @@ def psnr_yuv(ref: Frame, dec: Frame) -> dict:
 
 
 def codec_flags(deblock: bool = True, sao: bool = False, wpp: bool = True, rqt: bool = True, pintra: bool = True,
-                cascade: bool = False) -> int:
+                cascade: bool = False, rdoq: bool = True) -> int:
     """The native APIs' configuration bits (tv::SeqConfig::set_flags): 1 deblocking, 2 SAO,
     4 WPP substreams, 8 no residual quadtree, 16 no intra CUs in P pictures, 64 the constant-QP
-    I P P P QP cascade (tv/gop.h ippp_qp_offset)."""
+    I P P P QP cascade (tv/gop.h ippp_qp_offset), 128 no RDOQ-lite coefficient-group trimming
+    (tv/hevc_defs.h kRdoqMode)."""
     return (int(bool(deblock)) | (2 if sao else 0) | (4 if wpp else 0) | (0 if rqt else 8) | (0 if pintra else 16)
-            | (64 if cascade else 0))
+            | (64 if cascade else 0) | (0 if rdoq else 128))
 
 
 IPPP_CASCADE_IDR = -5
@@ -63,10 +64,11 @@ class CpuEncoder:
 
     def __init__(self, width: int, height: int, qp: int = 27, deblock: bool = True,
                  search_range: int = 64, max_merge: int = 5, sao: bool = False, crf: int = 0, wpp: bool = True,
-                 bframes: int = 1, rqt: bool = True, pintra: bool = True, cascade: bool = True):
+                 bframes: int = 1, rqt: bool = True, pintra: bool = True, cascade: bool = True, rdoq: bool = True):
         """`wpp`: one CABAC substream per CTB row (entropy_coding_sync; the GPU engine's
-        default, it codes them on the device); `rqt` / `pintra`: residual quadtree for inter
-        CUs and intra 16x16 CUs in P pictures (coding tools; part of the bitstream identity)."""
+        default, it codes them on the device); `rqt` / `pintra` / `rdoq`: residual quadtree for
+        inter CUs, intra 16x16 CUs in P pictures, trailing lone-level coefficient groups of inter
+        TBs dropped (coding tools; part of the bitstream identity)."""
         if width % 2 or height % 2:
             raise ValueError("width/height must be even")
         self.lib = core_lib()
@@ -79,16 +81,16 @@ class CpuEncoder:
             f = self.lib.tv_cpu_encoder_new_b
             f.restype = C.c_void_p
             f.argtypes = [C.c_int] * 7
-            self.h = f(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade), search_range, max_merge,
+            self.h = f(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade, rdoq), search_range, max_merge,
                        self.bframes)
         elif crf:
             f = self.lib.tv_cpu_encoder_new_crf
             f.restype = C.c_void_p
             f.argtypes = [C.c_int] * 7
-            self.h = f(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade), search_range, max_merge,
+            self.h = f(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade, rdoq), search_range, max_merge,
                        int(crf))
         else:
-            self.h = self.lib.tv_cpu_encoder_new(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade),
+            self.h = self.lib.tv_cpu_encoder_new(width, height, qp, codec_flags(deblock, sao, wpp, rqt, pintra, cascade, rdoq),
                                                  search_range, max_merge)
         if not self.h:
             raise ValueError(self.lib.tv_last_error().decode())

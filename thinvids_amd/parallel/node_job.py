@@ -215,7 +215,7 @@ class WorkQueue:
 
 # bumped whenever the encoders' output for identical settings changes (a checkpoint written
 # by an older build must not be mixed into a newer job's output)
-BITSTREAM_VERSION = 10  # 10: the constant-QP I P P P QP cascade by default (9: WPP substreams)
+BITSTREAM_VERSION = 11  # 11: RDOQ-lite trailing coefficient-group trimming (inter); 10: the constant-QP I P P P QP cascade by default (9: WPP substreams)
 
 
 class Checkpoint:
@@ -1074,6 +1074,7 @@ def main(argv=None) -> int:
     ap.add_argument("--no-rqt", dest="rqt", action="store_false", help="HEVC: no residual quadtree")
     ap.add_argument("--no-cascade", dest="cascade", action="store_false", help="HEVC: flat QP (no I P P P QP cascade)")
     ap.add_argument("--no-pintra", dest="pintra", action="store_false", help="HEVC: no intra CUs in P pictures")
+    ap.add_argument("--no-rdoq", dest="rdoq", action="store_false", help="HEVC: no RDOQ-lite coefficient-group trimming")
     ap.add_argument("--deinterlace", action="store_true", help="bwdif every segment (DVD-native interlaced sources)")
     a = ap.parse_args(argv)
     import torch
@@ -1092,7 +1093,7 @@ def main(argv=None) -> int:
     ladder = [int(x) for x in a.ladder.split(",") if x.strip()] or None
     res = run_job(a.input, a.output, a.height, a.qp, a.gop, a.segment_frames, a.mode, a.bitrate_kbps, ladder,
                   software=a.software, resume_dir=a.resume_dir, max_retries=a.max_retries, bframes=a.bframes,
-                  tools={"wpp": a.wpp, "rqt": a.rqt, "pintra": a.pintra, "cascade": a.cascade},
+                  tools={"wpp": a.wpp, "rqt": a.rqt, "pintra": a.pintra, "cascade": a.cascade, "rdoq": a.rdoq},
                   deinterlace=a.deinterlace)
     if int(os.environ.get("RANK", "0")) == 0:
         print(json.dumps(res), flush=True)

@@ -53,6 +53,7 @@ class EncodeSpec:
     rqt: bool = True
     pintra: bool = True
     cascade: bool = True  # constant-QP I P P P: the low-delay QP cascade (tv/gop.h)
+    rdoq: bool = True  # inter TBs drop trailing lone-+-1 coefficient groups (tv/hevc_defs.h)
     # where the WPP substreams are CABAC-coded ("auto" / "gpu" / "host"): the same bytes, so
     # not a coding tool (not in tools() / the checkpoint fingerprint), but its own engine
     entropy: str = "auto"
@@ -61,11 +62,11 @@ class EncodeSpec:
         if self.codec == "av1":
             return ("av1", self.width, self.height, self.av1_qindex(), self.cascade)
         return (self.width, self.height, self.qp, self.gop, self.search_range, self.deblock, self.sao, self.seed,
-                self.crf, self.hevc_bframes(), self.wpp, self.rqt, self.pintra, self.cascade, self.entropy)
+                self.crf, self.hevc_bframes(), self.wpp, self.rqt, self.pintra, self.cascade, self.rdoq, self.entropy)
 
     def tools(self) -> dict:
         """The coding-tool switches as GpuEngine / CpuEncoder keyword arguments."""
-        return {"wpp": self.wpp, "rqt": self.rqt, "pintra": self.pintra, "cascade": self.cascade}
+        return {"wpp": self.wpp, "rqt": self.rqt, "pintra": self.pintra, "cascade": self.cascade, "rdoq": self.rdoq}
 
     def hevc_bframes(self) -> int:
         """Mini-GOP actually used: in-engine CRF keeps I P P P (its lookahead QP is per

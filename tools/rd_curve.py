@@ -48,7 +48,7 @@ def run_point(args):
             stream += r.stream
             ys += [hevc.psnr(f[0], rec[:W * H].reshape(H, W)[:h, :w]) for f, rec in zip(frames[s0:], r.recon)]
     else:
-        kw = dict(sao=a["sao"], rqt=a["rqt"], pintra=a["pintra"], wpp=a["wpp"], cascade=a["ippp_cascade"])
+        kw = dict(sao=a["sao"], rqt=a["rqt"], pintra=a["pintra"], wpp=a["wpp"], cascade=a["ippp_cascade"], rdoq=a["rdoq"])
         stream, recons = hevc.encode_sequence_cpu(frames, qp=qp, gop=a["gop"], frame_qps=fq, bframes=a["bframes"], **kw)
         ys = [hevc.psnr(f[0], r[0][:h, :w]) for f, r in zip(frames, recons)]
 
@@ -79,13 +79,14 @@ def main():
     ap.add_argument("--ippp-cascade", type=int, default=1, help="built-in constant-QP I P P P QP cascade (tv/gop.h)")
     ap.add_argument("--pintra", type=int, default=int(env_on("TV_PINTRA")))
     ap.add_argument("--wpp", type=int, default=int(env_on("TV_WPP")))
+    ap.add_argument("--rdoq", type=int, default=1, help="RDOQ-lite coefficient-group trimming")
     ap.add_argument("--anchor", default="")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     cfg = dict(res=a.res, frames=a.frames, gop=a.gop, sao=bool(a.sao), seed=a.seed, textured=a.textured,
                cascade=[int(x) for x in a.cascade.split(",")] if a.cascade else [], iqp=a.iqp,
                bframes=a.bframes, codec=a.codec, rqt=bool(a.rqt), pintra=bool(a.pintra), wpp=bool(a.wpp),
-               ippp_cascade=bool(a.ippp_cascade))
+               ippp_cascade=bool(a.ippp_cascade), rdoq=bool(a.rdoq))
     qps = [int(q) for q in a.qps.split(",")]
     with ProcessPoolExecutor(len(qps)) as ex:
         pts = list(ex.map(run_point, [(q, cfg) for q in qps]))
