@@ -734,6 +734,7 @@ struct PReconLds {
   int qintra[4];              // quadrant q is an intra CU of a P picture (k_pintra_recon codes it)
   uint32_t ctap[8];           // chroma filter of fraction f as 4 signed bytes
   int cgmax[48];              // RDOQ-lite: highest scan key of a TB's groups that are kept
+  int multi;                  // some TB has >= 2 non-zero levels (else RDOQ-lite changes nothing)
 };
 
 // block size (log2) of the TB owning luma sample (x, y) / chroma sample (x, y) of the CTB
@@ -793,7 +794,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   if (tid < 8)
     L.ctap[tid] = (uint32_t)(uint8_t)kChromaFilter[tid][0] | (uint32_t)(uint8_t)kChromaFilter[tid][1] << 8 |
                   (uint32_t)(uint8_t)kChromaFilter[tid][2] << 16 | (uint32_t)(uint8_t)kChromaFilter[tid][3] << 24;
-  if (tid == 0) L.split = 0;
+  if (tid == 0) L.split = 0, L.multi = 0;
   if (tid < 4) {
     L.qsplit[tid] = 0;
     L.qintra[tid] = dec.intra[ub + (long)((cy >> 3) + (tid >> 1) * 2) * g.w8 + (cx >> 3) + (tid & 1) * 2];
@@ -1033,7 +1034,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     const int lev = quant_level((v + (1 << (sh2 - 1))) >> sh2, q, l2, false);
     *dst = (int16_t)lev;
     if (lev) {
-      atomicAdd(&L.nz[id], 1);
+      if (atomicAdd(&L.nz[id], 1)) L.multi = 1;
       atomicAdd(&L.sa[id], tv_abs(lev));
     }
     if (origin) L.dc[id] = lev;
@@ -1087,7 +1088,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   // parallel that is: a lone group is dropped iff its scan key (diagonal major, then rows
   // from the bottom) is above every other non-empty-non-lone group's of its TB (one LDS max
   // per TB) and its diagonal is >= rdoq_dmin.  One thread per 4x4 group (luma 64, Cb / Cr 16).
-  if (diag != 1 && rdoq) {
+  // A CTB whose TBs hold at most one level each skips it (workgroup-uniform): a lone level
+  // the pass could drop is dropped by the whole-TB rule (pr_zeroed) anyway.
+  if (diag != 1 && rdoq && L.multi) {
     int code = 0, key = 0, id = 0, dmin = 1 << 20;
     int16_t* p = nullptr;
     int st = 32;
@@ -1121,7 +1124,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       if (code == 2) atomicMax(&L.cgmax[id], key);
       if (gx + gy < dmin) code = 0;  // groups this TB keeps whatever they hold
     }
-    __syncthreads();
+    // all groups of a TB are in one wave (luma wave 0, chroma wave 1) and one wave's LDS
+    // operations execute in order: the max needs no workgroup barrier before it is read
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (code == 1 && key > L.cgmax[id]) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) *reinterpret_cast<uint2*>(p + j * st) = make_uint2(0u, 0u);

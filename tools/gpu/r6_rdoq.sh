@@ -14,4 +14,5 @@ for i in 1 2; do
     grep '^{' $O/ab_${m}_$i.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); c=r['config']; print('ab $m', r['value'], c['last_step_gpu_ms'], c['psnr_y_db'], c['kbps_per_30fps_stream'], c['coding_tools'])"
   done
 done
+[ "${RD:-1}" = 0 ] && exit 0
 bash tools/gpu/rd_vs.sh ${1:-r6_rdoq4}/rd_on && bash tools/gpu/rd_vs.sh ${1:-r6_rdoq4}/rd_off profiles/r5_rd_cascade_1080p --no-rdoq
