@@ -714,7 +714,8 @@ __global__ void __launch_bounds__(256) k_bi_decide(FrameSet src, const uint8_t* 
 // bit-identical to tv::forward_transform / tv::inverse_transform (see tb_coder.h).
 // ---------------------------------------------------------------------------------------
 struct PReconLds {
-  int16_t T[32][32];          // DCT-32 (every smaller DCT is a row subsample)
+  int16_t T[32][34];          // DCT-32 (every smaller DCT is a row subsample); rows padded to
+                              // 17 dwords: column reads across lanes hit distinct banks
   int tmpY[32 * 33];          // stage 1 / stage 3 outputs (luma)
   int tmpC[2][16 * 16];       // stage 1 / stage 3 outputs (Cb, Cr)
   int16_t resY[32 * 32];      // residual, later levels (luma)
