@@ -717,7 +717,7 @@ struct PReconLds {
   int16_t T[32][34];          // DCT-32 (every smaller DCT is a row subsample); rows padded to
                               // 17 dwords: column reads across lanes hit distinct banks
   int tmpY[32 * 33];          // stage 1 / stage 3 outputs (luma)
-  int tmpC[2][16 * 16];       // stage 1 / stage 3 outputs (Cb, Cr)
+  int tmpC[2][16 * 17];       // stage 1 / stage 3 outputs (Cb, Cr), rows of 17 (bank spread)
   int16_t resY[32 * 32];      // residual, later levels (luma)
   int16_t resC[2][16 * 16];   // residual, later levels (chroma)
   uint8_t predY[32 * 32];
@@ -1011,7 +1011,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
-        L.tmpC[pl][rr * 16 + cc] = (o[r] + 4) >> 3;  // 16-point: sh1 = 3
+        L.tmpC[pl][rr * 17 + cc] = (o[r] + 4) >> 3;  // 16-point: sh1 = 3
       }
     } else {
       const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
@@ -1024,7 +1024,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
-        if ((rr >> 3) == (cc >> 3)) L.tmpC[rr >> 3][(oy + (rr & 7)) * 16 + ox + (cc & 7)] = (o[r] + (1 << (sh1 - 1))) >> sh1;
+        if ((rr >> 3) == (cc >> 3)) L.tmpC[rr >> 3][(oy + (rr & 7)) * 17 + ox + (cc & 7)] = (o[r] + (1 << (sh1 - 1))) >> sh1;
       }
     }
   }
@@ -1060,7 +1060,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       }
     } else if (whole) {
       const int pl = t - 4;
-      mfma_tile([&](int r, int k) { return L.tmpC[pl][r * 16 + k]; }, [&](int k, int c) { return pr_comp(L, 4, c, k); },
+      mfma_tile([&](int r, int k) { return L.tmpC[pl][r * 17 + k]; }, [&](int k, int c) { return pr_comp(L, 4, c, k); },
                 0, 0, 16, true, true, o);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1070,7 +1070,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     } else {
       const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
       mfma_tile([&](int r, int k) {
-                  return (r >> 3) == (k >> 3) ? L.tmpC[r >> 3][(oy + (r & 7)) * 16 + ox + (k & 7)] : 0;
+                  return (r >> 3) == (k >> 3) ? L.tmpC[r >> 3][(oy + (r & 7)) * 17 + ox + (k & 7)] : 0;
                 },
                 [&](int k, int c) { return pr_comp(L, l2, c, k); }, 0, 0, 16, true, true, o);
 #pragma unroll
@@ -1203,7 +1203,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
                 [&](int k, int c) { return deq_fast(L.resC[pl][k * 16 + c], dqc4); }, 0, 0, 16, true, false, o);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        L.tmpC[pl][((lane >> 4) * 4 + r) * 16 + (lane & 15)] = clip3(-32768, 32767, (o[r] + 64) >> 7);
+        L.tmpC[pl][((lane >> 4) * 4 + r) * 17 + (lane & 15)] = clip3(-32768, 32767, (o[r] + 64) >> 7);
     } else {
       const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
       const DeqParams dqcl = deq_params(qpc, l2);
@@ -1216,7 +1216,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       for (int r = 0; r < 4; ++r) {
         const int rr = (lane >> 4) * 4 + r, cc = lane & 15;
         if ((rr >> 3) == (cc >> 3))
-          L.tmpC[rr >> 3][(oy + (rr & 7)) * 16 + ox + (cc & 7)] = clip3(-32768, 32767, (o[r] + 64) >> 7);
+          L.tmpC[rr >> 3][(oy + (rr & 7)) * 17 + ox + (cc & 7)] = clip3(-32768, 32767, (o[r] + 64) >> 7);
       }
     }
   }
@@ -1246,7 +1246,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       }
     } else if (whole) {
       const int pl = t - 4;
-      if (!tz) mfma_tile([&](int r, int k) { return L.tmpC[pl][r * 16 + k]; }, [&](int k, int c) { return pr_comp(L, 4, k, c); },
+      if (!tz) mfma_tile([&](int r, int k) { return L.tmpC[pl][r * 17 + k]; }, [&](int k, int c) { return pr_comp(L, 4, k, c); },
                 0, 0, 16, true, true, o);
       uint8_t* R = rec.plane(1 + pl, b, g) + (long)(cy >> 1) * Wc + (cx >> 1);
 #pragma unroll
@@ -1257,7 +1257,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     } else {
       const int q = t - 4, ox = (q & 1) * 8, oy = (q >> 1) * 8, l2 = L.qtype[q] == 1 ? 3 : 2;
       if (!tz) mfma_tile([&](int r, int k) {
-                  return (r >> 3) == (k >> 3) ? L.tmpC[r >> 3][(oy + (r & 7)) * 16 + ox + (k & 7)] : 0;
+                  return (r >> 3) == (k >> 3) ? L.tmpC[r >> 3][(oy + (r & 7)) * 17 + ox + (k & 7)] : 0;
                 },
                 [&](int k, int c) { return pr_comp(L, l2, k, c); }, 0, 0, 16, true, true, o);
 #pragma unroll
